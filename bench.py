@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: BASELINE.json metric — Msamples/s (+ Mrays/s) of the Cornell-box path tracer,
+PathIntegrator depth 8, 1920x1080 x 64 spp (BASELINE config C2; C3 when launched on N GPUs).
+
+One "step" = one full frame (132.7 M camera samples) rendered through the C API
+(yafaray_amd_renderQuiet = yafaray_render without the per-pixel callbacks), inputs resident on
+the GPU.  On N GPUs (torch.distributed.run, one process per GPU, backend nccl = RCCL) the frame's
+32-pixel tile rows are dealt round-robin to the ranks and the finished tile rows are all-gathered
+over RCCL into the full film every step (strong scaling: total work fixed).
+
+Prints ONE JSON line (rank 0).  Extra keys: mrays_per_s, roofline (k_trace vs HBM), cpu_baseline
+(the CPU oracle restatement on the host cores, bounded sample of the same frame).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "Mrays/sec + Msamples/sec, 1920×1080×64spp path-trace at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--no-rr", action="store_true", help="Russian roulette off (bit-parity variant)")
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere"])
+    ap.add_argument("--chunk", type=int, default=1 << 20)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import libyafaray_amd as Y
+    from libyafaray_amd import scenes
+    if a.scene == "sphere":
+        spec = scenes.cornell_sphere(width=a.width, height=a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
+    else:
+        spec = scenes.cornell(a.width, a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
+    # the reference's PathIntegrator default caustic_type is "path" (integrator_path_tracer.cc:43);
+    # a diffuse-only scene never takes a caustic branch either way.
+    yi = Y.Interface()
+    scenes.apply(spec, yi)
+    yi.L.yafaray_amd_setChunkSlots(yi.h, a.chunk)
+    yi.L.yafaray_amd_setTileRowShard(yi.h, rank, world)
+    if not yi.L.yafaray_amd_buildAccelerator(yi.h):
+        raise RuntimeError(yi.last_error())
+
+    W, H, ts = a.width, a.height, spec.render.tile_size
+    tile_rows = (H + ts - 1) // ts
+    my_rows = [r for r in range(tile_rows) if r % world == rank]
+    max_rows = (tile_rows + world - 1) // world
+    band = torch.zeros((max_rows * ts, W, 4), dtype=torch.float32, device=dev)
+    gathered = torch.zeros((world * max_rows * ts, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
+
+    def step():
+        yi.render_quiet()
+        for k, r in enumerate(my_rows):
+            y0, y1 = r * ts, min(H, r * ts + ts)
+            ptr = band.data_ptr() + k * ts * W * 16
+            if not yi.L.yafaray_amd_getFilmDevice(yi.h, ptr, y0, y1):
+                raise RuntimeError(yi.last_error())
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, band)
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    # timed region: k_trace launches bracketed by HIP events on the render stream (profile mode)
+    yi.L.yafaray_amd_setProfileKernels(yi.h, 1)
+    sync()
+    t0 = time.perf_counter()
+    stats_acc = []
+    for _ in range(a.steps):
+        step()
+        stats_acc.append(yi.stats())
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([sum(s["closest_rays"] + s["shadow_rays"] for s in stats_acc),
+                            sum(s["node_visits"] for s in stats_acc), sum(s["tri_tests"] for s in stats_acc)],
+                           device=dev, dtype=torch.float64)
+        dist.all_reduce(tot)
+        rays_total = float(tot[0].item())
+    else:
+        rays_total = float(sum(s["closest_rays"] + s["shadow_rays"] for s in stats_acc))
+
+    samples_total = float(W * H * a.spp * a.steps)     # whole job: every rank's tile rows together
+    msps = samples_total / elapsed / 1e6
+    mrays = rays_total / elapsed / 1e6
+
+    # roofline of the dominant kernel (k_trace) on this rank: algorithmic bytes per launch over the
+    # average launch duration from the HIP events.  Bytes per traced ray:
+    # 64 B per BVH node fetched + 48 B per triangle tested + ray I/O (closest: 32 in + 8 out,
+    # shadow: 32 in + 1 out + 4 index).
+    s = stats_acc[-1]
+    algo_bytes = (64.0 * s["node_visits"] + 48.0 * s["tri_tests"] + 40.0 * s["closest_rays"] + 37.0 * s["shadow_rays"])
+    launches = max(1, s["trace_launches"])
+    avg_ms = s["trace_kernel_ms"] / launches
+    per_launch = algo_bytes / launches
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "trace_hbm_bytes_per_launch.json")
+    if os.path.exists(tfile):
+        try:
+            with open(tfile) as f:
+                tj = json.load(f)
+            if tj.get("config") == f"{a.scene}-{W}x{H}x{a.spp}-b{a.bounces}-rr{int(not a.no_rr)}-chunk{a.chunk}":
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(spec, a)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(msps, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (Cornell box scene generated in-repo, SURVEY.md §8d)",
+            "config": {"workload": f"C2 Cornell PathIntegrator depth {a.bounces}, {W}x{H}x{a.spp}spp"
+                                   + (", RR off" if a.no_rr else ", RR on (reference default)")
+                                   + ("" if a.scene == "cornell" else " + 1M-triangle sphere (C4)"),
+                       "width": W, "height": H, "spp": a.spp, "bounces": a.bounces,
+                       "samples_per_step": W * H * a.spp, "parallelism": f"tile-rows x{world}",
+                       "chunk_slots": a.chunk},
+            "mrays_per_s": round(mrays, 2),
+            "rays_per_sample": round(rays_total / samples_total, 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_trace", "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
+                         "algo_bytes_per_launch": round(per_launch)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    yi.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(spec, a):
+    """The CPU oracle (C++ restatement of the reference loop) on the host cores, on a bounded
+    band of rows of the same frame, scaled to Msamples/s."""
+    try:
+        from oracle import oracle as O
+    except Exception as e:  # pragma: no cover
+        return {"error": str(e)}
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cores = max(1, min(cores, os.cpu_count() or 1))
+    osc = O.OracleScene(spec, threads=cores)
+    # probe one 32-row tile band, then size the sample to ~cpu_seconds
+    ts = spec.render.tile_size
+    y0 = (spec.render.height // 2 // ts) * ts
+    t0 = time.perf_counter()
+    osc.render(y0, y0 + 4)
+    probe = time.perf_counter() - t0
+    per_row = probe / 4
+    rows = int(max(4, min(spec.render.height - y0, a.cpu_seconds / max(per_row, 1e-6))))
+    t0 = time.perf_counter()
+    _, _, ctr = osc.render(y0, y0 + rows)
+    dt = time.perf_counter() - t0
+    n = rows * spec.render.width * spec.render.aa_samples
+    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "mrays_per_s": round((ctr[0] + ctr[1]) / dt / 1e6, 3),
+            "sample": f"rows {y0}..{y0 + rows} of the same {spec.render.width}x{spec.render.height}x"
+                      f"{spec.render.aa_samples}spp frame ({n} samples, {dt:.1f} s, {cores} threads)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+/*
+ * yafaray_amd.h — MI355X extensions next to the drop-in ABI (yafaray_c_api.h).
+ *
+ * These entry points are additive (version node LIBYAFARAY_AMD_1.0): a reference client never
+ * needs them.  They expose what a GPU host wants beyond the reference's per-pixel callbacks:
+ *
+ *  - bulk geometry upload (one call per object instead of one per vertex / triangle);
+ *  - the batched ray-level seam that replaces the reference's per-ray const virtuals
+ *    Accelerator::intersect / Accelerator::isShadowed (reference include/accelerator/accelerator.h:53-69,
+ *    src/accelerator/accelerator.cc:55-78): SoA rays in, hits out, on the GPU BVH;
+ *  - the rendered film (normalised RGBA + weights) as arrays, the in-kernel ray / node / triangle
+ *    counters and per-phase timings the bench reports;
+ *  - multi-GPU: render only a subset of tile rows (one process per GPU; the tile results are then
+ *    all-gathered over RCCL by the caller).
+ *
+ * All pointers are plain host pointers unless a name says `_dev` (HIP device pointers, e.g. from
+ * torch tensors on the same device).  Errors are reported the reference's way (logger + return 0).
+ */
+#ifndef YAFARAY_AMD_H
+#define YAFARAY_AMD_H
+
+#include "yafaray_c_api.h"
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct
+{
+	uint64_t closest_rays;      /* closest-hit queries issued to the BVH */
+	uint64_t shadow_rays;       /* any-hit (shadow) queries */
+	uint64_t node_visits;       /* BVH nodes fetched (64 B each) */
+	uint64_t tri_tests;         /* triangles tested (48 B each) */
+	uint64_t samples;           /* camera samples rendered */
+	double build_seconds;       /* BVH build + upload (host) */
+	double render_seconds;      /* GPU wall time of the sample loop + film (hipEvent) */
+	double trace_kernel_ms;     /* summed k_trace time (hipEvent pairs), 0 if not profiled */
+	uint64_t trace_launches;
+	uint32_t bvh_nodes, bvh_depth, scene_in_lds, pad;
+} yafaray_amd_stats_t;
+
+/* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */
+YAFARAY_C_API_EXPORT int yafaray_amd_addVertices(yafaray_Interface_t *interface, const double *xyz, int n);
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_addTriangles(yafaray_Interface_t *interface, const int *abc, int n);
+
+/* Build (or rebuild) the GPU acceleration structure for the current scene. */
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_buildAccelerator(yafaray_Interface_t *interface);
+
+/* Batched ray queries.  rays: n x 8 floats (from xyz, dir xyz, tmin, tmax; tmax < 0 = infinite).
+ * closest: hits n x 1 float t (-1 = miss), prims n ints (global triangle index in creation order).
+ * shadow : occluded n ints (Accelerator::isShadowed semantics: origin moved by tmin, t_max = tmax - 2 tmin). */
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_traceClosest(yafaray_Interface_t *interface, const float *rays, int n, float *t, int *prims);
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_traceShadow(yafaray_Interface_t *interface, const float *rays, int n, int *occluded);
+
+/* Film of the last render: rgba width*height*4 floats (normalised, = put-pixel values), weights width*height. */
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_getFilm(const yafaray_Interface_t *interface, float *rgba, float *weights);
+/* Film straight into device memory (rows [y0, y1) of a width*height*4 float buffer on the render device). */
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_getFilmDevice(const yafaray_Interface_t *interface, void *rgba_dev, int y0, int y1);
+
+/* Restrict the next render to tile rows r with r % world == rank (one process per GPU).  world = 1 renders all. */
+YAFARAY_C_API_EXPORT void yafaray_amd_setTileRowShard(yafaray_Interface_t *interface, int rank, int world);
+
+/* Render without callbacks / console output (bench loop); same work as yafaray_render. */
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t *interface);
+
+/* Counters and timings of the last render. */
+YAFARAY_C_API_EXPORT void yafaray_amd_getStats(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats);
+
+/* Tuning: samples in flight per wavefront chunk (default 1 << 20) and whether to time k_trace with events. */
+YAFARAY_C_API_EXPORT void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots);
+YAFARAY_C_API_EXPORT void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_t enable);
+
+/* Last error message (empty if none); owned by the interface. */
+YAFARAY_C_API_EXPORT const char *yafaray_amd_lastError(const yafaray_Interface_t *interface);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* YAFARAY_AMD_H */

@@ -1,0 +1,267 @@
+"""libyafaray_amd — Python host mirror of libYafaRay's C API over the MI355X core (libyafaray4.so).
+
+The shared library is the product: every call below is a thin ctypes forward to an extern "C"
+symbol of include/yafaray_c_api.h (reference include/public_api/yafaray_c_api.h:53-130) or of the
+MI355X extensions in include/yafaray_amd.h.  There is no Python or CPU fallback: importing works
+without a GPU (so the C ABI can be inspected), but rendering / tracing raise if the HIP path
+fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libyafaray4.so")
+
+# enums (yafaray_c_api.h)
+LOG_MUTE, LOG_ERROR, LOG_WARNING, LOG_PARAMS, LOG_INFO, LOG_VERBOSE, LOG_DEBUG = range(7)
+CONSOLE_HIDDEN, CONSOLE_NORMAL = 0, 1
+
+PutPixelCb = C.CFUNCTYPE(None, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float,
+                         C.c_void_p)
+FlushAreaCb = C.CFUNCTYPE(None, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p)
+FlushCb = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
+NotifyViewCb = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
+NotifyLayerCb = C.CFUNCTYPE(None, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_void_p)
+ProgressCb = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_char_p, C.c_void_p)
+LoggerCb = C.CFUNCTYPE(None, C.c_int, C.c_long, C.c_char_p, C.c_char_p, C.c_void_p)
+
+
+class Stats(C.Structure):
+    _fields_ = [("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
+                ("tri_tests", C.c_uint64), ("samples", C.c_uint64), ("build_seconds", C.c_double),
+                ("render_seconds", C.c_double), ("trace_kernel_ms", C.c_double), ("trace_launches", C.c_uint64),
+                ("bvh_nodes", C.c_uint32), ("bvh_depth", C.c_uint32), ("scene_in_lds", C.c_uint32),
+                ("pad", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+_lib = None
+
+
+def build(quiet: bool = True) -> str:
+    """Compile libyafaray4.so for gfx950 in-tree (libyafaray_amd/csrc/Makefile)."""
+    import subprocess
+    out = subprocess.run(["make", "-C", os.path.join(HERE, "csrc"), "-j8"], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("libyafaray4.so build failed:\n" + out.stdout[-4000:] + out.stderr[-4000:])
+    if not quiet:
+        print(out.stdout)
+    return LIB_PATH
+
+
+def lib():
+    """Load libyafaray4.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run libyafaray_amd.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        vp, cp, i, d, f, b = C.c_void_p, C.c_char_p, C.c_int, C.c_double, C.c_float, C.c_int
+        sig = {
+            "yafaray_createInterface": (vp, [i, cp, C.c_void_p, vp, i]),
+            "yafaray_destroyInterface": (None, [vp]),
+            "yafaray_createScene": (None, [vp]),
+            "yafaray_getSceneFilmWidth": (i, [vp]),
+            "yafaray_getSceneFilmHeight": (i, [vp]),
+            "yafaray_startGeometry": (b, [vp]),
+            "yafaray_endGeometry": (b, [vp]),
+            "yafaray_endObject": (b, [vp]),
+            "yafaray_addVertex": (i, [vp, d, d, d]),
+            "yafaray_addVertexWithOrco": (i, [vp, d, d, d, d, d, d]),
+            "yafaray_addTriangle": (b, [vp, i, i, i]),
+            "yafaray_paramsSetVector": (None, [vp, cp, d, d, d]),
+            "yafaray_paramsSetString": (None, [vp, cp, cp]),
+            "yafaray_paramsSetBool": (None, [vp, cp, b]),
+            "yafaray_paramsSetInt": (None, [vp, cp, i]),
+            "yafaray_paramsSetFloat": (None, [vp, cp, d]),
+            "yafaray_paramsSetColor": (None, [vp, cp, f, f, f, f]),
+            "yafaray_paramsClearAll": (None, [vp]),
+            "yafaray_paramsPushList": (None, [vp]),
+            "yafaray_paramsEndList": (None, [vp]),
+            "yafaray_setCurrentMaterial": (None, [vp, cp]),
+            "yafaray_createObject": (b, [vp, cp]),
+            "yafaray_createLight": (b, [vp, cp]),
+            "yafaray_createTexture": (b, [vp, cp]),
+            "yafaray_createMaterial": (b, [vp, cp]),
+            "yafaray_createCamera": (b, [vp, cp]),
+            "yafaray_createBackground": (b, [vp, cp]),
+            "yafaray_createIntegrator": (b, [vp, cp]),
+            "yafaray_createRenderView": (b, [vp, cp]),
+            "yafaray_createOutput": (b, [vp, cp]),
+            "yafaray_setRenderPutPixelCallback": (None, [vp, PutPixelCb, vp]),
+            "yafaray_setRenderFlushAreaCallback": (None, [vp, FlushAreaCb, vp]),
+            "yafaray_setRenderFlushCallback": (None, [vp, FlushCb, vp]),
+            "yafaray_setRenderNotifyViewCallback": (None, [vp, NotifyViewCb, vp]),
+            "yafaray_setRenderNotifyLayerCallback": (None, [vp, NotifyLayerCb, vp]),
+            "yafaray_setupRender": (None, [vp]),
+            "yafaray_render": (None, [vp, ProgressCb, vp, i]),
+            "yafaray_defineLayer": (None, [vp]),
+            "yafaray_setConsoleVerbosityLevel": (None, [vp, i]),
+            "yafaray_setLogVerbosityLevel": (None, [vp, i]),
+            "yafaray_cancelRendering": (None, [vp]),
+            "yafaray_setInputColorSpace": (None, [vp, cp, f]),
+            "yafaray_getVersionString": (vp, []),
+            "yafaray_deallocateCharPointer": (None, [vp]),
+            "yafaray_amd_addVertices": (i, [vp, C.POINTER(C.c_double), i]),
+            "yafaray_amd_addTriangles": (b, [vp, C.POINTER(C.c_int), i]),
+            "yafaray_amd_buildAccelerator": (b, [vp]),
+            "yafaray_amd_traceClosest": (b, [vp, C.POINTER(C.c_float), i, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
+            "yafaray_amd_traceShadow": (b, [vp, C.POINTER(C.c_float), i, C.POINTER(C.c_int)]),
+            "yafaray_amd_getFilm": (b, [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+            "yafaray_amd_getFilmDevice": (b, [vp, vp, i, i]),
+            "yafaray_amd_setTileRowShard": (None, [vp, i, i]),
+            "yafaray_amd_renderQuiet": (b, [vp]),
+            "yafaray_amd_getStats": (None, [vp, C.POINTER(Stats)]),
+            "yafaray_amd_setChunkSlots": (None, [vp, i]),
+            "yafaray_amd_setProfileKernels": (None, [vp, b]),
+            "yafaray_amd_lastError": (cp, [vp]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def version() -> str:
+    L = lib()
+    p = L.yafaray_getVersionString()
+    s = C.cast(p, C.c_char_p).value.decode()
+    L.yafaray_deallocateCharPointer(p)
+    return s
+
+
+def _b(s):
+    return s.encode() if isinstance(s, str) else s
+
+
+class Interface:
+    """One yafaray_Interface_t.  Method names are the C API's without the `yafaray_` prefix."""
+
+    def __init__(self, console=CONSOLE_HIDDEN, verbosity=LOG_WARNING):
+        self.L = lib()
+        self.h = self.L.yafaray_createInterface(0, None, None, None, console)
+        self.L.yafaray_setConsoleVerbosityLevel(self.h, verbosity)
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            self.L.yafaray_destroyInterface(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- generic forwarding for simple calls ---
+    def __getattr__(self, name):
+        fn = getattr(lib(), "yafaray_" + name, None)
+        if fn is None:
+            raise AttributeError(name)
+
+        def call(*args):
+            return fn(self.h, *[_b(a) for a in args])
+        return call
+
+    # --- bulk geometry (extensions) ---
+    def addVertices(self, xyz):
+        a = np.ascontiguousarray(xyz, np.float64).reshape(-1)
+        return self.L.yafaray_amd_addVertices(self.h, a.ctypes.data_as(C.POINTER(C.c_double)), len(a) // 3)
+
+    def addTriangles(self, abc):
+        a = np.ascontiguousarray(abc, np.int32).reshape(-1)
+        if not self.L.yafaray_amd_addTriangles(self.h, a.ctypes.data_as(C.POINTER(C.c_int)), len(a) // 3):
+            raise RuntimeError(self.last_error())
+
+    def last_error(self) -> str:
+        e = self.L.yafaray_amd_lastError(self.h)
+        return e.decode() if e else ""
+
+    # --- render ---
+    def render(self, progress=None, put_pixel=None, flush_area=None, flush=None):
+        cbs = []
+        if put_pixel is not None:
+            cb = PutPixelCb(lambda v, l, x, y, r, g, b, a, d: put_pixel(x, y, r, g, b, a))
+            self.L.yafaray_setRenderPutPixelCallback(self.h, cb, None)
+            cbs.append(cb)
+        if flush_area is not None:
+            cb = FlushAreaCb(lambda v, aid, x0, y0, x1, y1, d: flush_area(aid, x0, y0, x1, y1))
+            self.L.yafaray_setRenderFlushAreaCallback(self.h, cb, None)
+            cbs.append(cb)
+        if flush is not None:
+            cb = FlushCb(lambda v, d: flush())
+            self.L.yafaray_setRenderFlushCallback(self.h, cb, None)
+            cbs.append(cb)
+        pcb = ProgressCb(lambda t, dn, tag, d: progress(t, dn) if progress else None)
+        cbs.append(pcb)
+        self._keep = cbs
+        before = self.last_error()
+        self.L.yafaray_render(self.h, pcb, None, CONSOLE_HIDDEN)
+        err = self.last_error()
+        if err and err != before:
+            raise RuntimeError("yafaray_render failed: " + err)
+
+    def render_quiet(self):
+        if not self.L.yafaray_amd_renderQuiet(self.h):
+            raise RuntimeError("render failed: " + self.last_error())
+
+    def film(self):
+        w, h = self.L.yafaray_getSceneFilmWidth(self.h), self.L.yafaray_getSceneFilmHeight(self.h)
+        rgba = np.empty((h, w, 4), np.float32)
+        wt = np.empty((h, w), np.float32)
+        if not self.L.yafaray_amd_getFilm(self.h, rgba.ctypes.data_as(C.POINTER(C.c_float)),
+                                          wt.ctypes.data_as(C.POINTER(C.c_float))):
+            raise RuntimeError("no film: " + self.last_error())
+        return rgba, wt
+
+    def stats(self) -> dict:
+        s = Stats()
+        self.L.yafaray_amd_getStats(self.h, C.byref(s))
+        return s.as_dict()
+
+    def trace_closest(self, rays):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1)
+        n = len(r) // 8
+        t = np.empty(n, np.float32)
+        p = np.empty(n, np.int32)
+        if not self.L.yafaray_amd_traceClosest(self.h, r.ctypes.data_as(C.POINTER(C.c_float)), n,
+                                               t.ctypes.data_as(C.POINTER(C.c_float)),
+                                               p.ctypes.data_as(C.POINTER(C.c_int))):
+            raise RuntimeError("traceClosest failed: " + self.last_error())
+        return t, p
+
+    def trace_shadow(self, rays):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1)
+        n = len(r) // 8
+        o = np.empty(n, np.int32)
+        if not self.L.yafaray_amd_traceShadow(self.h, r.ctypes.data_as(C.POINTER(C.c_float)), n,
+                                              o.ctypes.data_as(C.POINTER(C.c_int))):
+            raise RuntimeError("traceShadow failed: " + self.last_error())
+        return o
+
+
+def render_spec(spec, chunk_slots=None, profile=False, shard=None):
+    """Replay a scenes.SceneSpec through the C API and render it; returns (rgba, weights, stats)."""
+    from . import scenes
+    yi = Interface()
+    scenes.apply(spec, yi)
+    if chunk_slots:
+        yi.L.yafaray_amd_setChunkSlots(yi.h, int(chunk_slots))
+    if profile:
+        yi.L.yafaray_amd_setProfileKernels(yi.h, 1)
+    if shard is not None:
+        yi.L.yafaray_amd_setTileRowShard(yi.h, int(shard[0]), int(shard[1]))
+    yi.render()
+    rgba, w = yi.film()
+    st = yi.stats()
+    yi.close()
+    return rgba, w, st

@@ -1,0 +1,544 @@
+// extern "C" entry points of libyafaray4.so — the drop-in boundary (include/yafaray_c_api.h) and
+// the MI355X extensions (include/yafaray_amd.h).  Reference counterpart:
+// src/public_api/yafaray_c_api.cc:32-433 + src/interface/interface.cc:34-357.
+#include "../../include/yafaray_amd.h"
+#include "../../include/yafaray_c_api.h"
+#include "host.h"
+#include "hostmath.h"
+#include "render.h"
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+using namespace yafamd;
+
+static Interface *I(yafaray_Interface_t *p) { return reinterpret_cast<Interface *>(p); }
+static const Interface *I(const yafaray_Interface_t *p) { return reinterpret_cast<const Interface *>(p); }
+
+static char *dupString(const std::string &s)
+{
+	char *c = static_cast<char *>(std::malloc(s.size() + 1));
+	std::memcpy(c, s.c_str(), s.size() + 1);
+	return c;
+}
+
+extern "C" {
+
+yafaray_Interface_t *yafaray_createInterface(yafaray_Interface_Type_t interface_type, const char *exported_file_path, yafaray_LoggerCallback_t logger_callback, void *callback_data, yafaray_DisplayConsole_t display_console)
+{
+	auto *it = new Interface(logger_callback, callback_data, display_console);
+	if(interface_type != YAFARAY_INTERFACE_FOR_RENDERING)
+		it->logger.warning("Interface: scene exporters (XML/C/Python) are not part of the GPU core; creating a rendering interface");
+	(void)exported_file_path;
+	return reinterpret_cast<yafaray_Interface_t *>(it);
+}
+
+void yafaray_destroyInterface(yafaray_Interface_t *interface) { delete I(interface); }
+
+void yafaray_setLoggingCallback(yafaray_Interface_t *interface, yafaray_LoggerCallback_t cb, void *data) { I(interface)->logger.setCallback(cb, data); }
+
+void yafaray_createScene(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	it->scene.reset(new Scene(it->logger));
+	it->params.clear();
+}
+
+int yafaray_getSceneFilmWidth(const yafaray_Interface_t *interface)
+{
+	const Interface *it = I(interface);
+	return it->scene ? it->scene->setup.width : 0;
+}
+
+int yafaray_getSceneFilmHeight(const yafaray_Interface_t *interface)
+{
+	const Interface *it = I(interface);
+	return it->scene ? it->scene->setup.height : 0;
+}
+
+yafaray_bool_t yafaray_startGeometry(yafaray_Interface_t *interface) { return I(interface)->sc() ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE; }
+yafaray_bool_t yafaray_endGeometry(yafaray_Interface_t *interface) { return I(interface)->sc() ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE; }
+
+unsigned int yafaray_getNextFreeId(yafaray_Interface_t *interface)
+{
+	Scene *s = I(interface)->sc();
+	return s ? (unsigned int)s->objects.size() + 1 : 0;
+}
+
+yafaray_bool_t yafaray_endObject(yafaray_Interface_t *interface)
+{
+	Scene *s = I(interface)->sc();
+	return (s && s->endObject()) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+int yafaray_addVertex(yafaray_Interface_t *interface, double x, double y, double z)
+{
+	Scene *s = I(interface)->sc();
+	return s ? s->addVertex((float)x, (float)y, (float)z) : -1;
+}
+
+int yafaray_addVertexWithOrco(yafaray_Interface_t *interface, double x, double y, double z, double ox, double oy, double oz)
+{
+	(void)ox; (void)oy; (void)oz;   // orco coordinates only feed texture mapping (not in the GPU core yet)
+	return yafaray_addVertex(interface, x, y, z);
+}
+
+void yafaray_addNormal(yafaray_Interface_t *interface, double nx, double ny, double nz)
+{
+	(void)nx; (void)ny; (void)nz;
+	I(interface)->logger.warning("Scene: per-vertex normals (smooth shading) are not supported by the GPU core yet; ignored");
+}
+
+yafaray_bool_t yafaray_addTriangle(yafaray_Interface_t *interface, int a, int b, int c)
+{
+	Scene *s = I(interface)->sc();
+	return (s && s->addTriangle(a, b, c)) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+yafaray_bool_t yafaray_addTriangleWithUv(yafaray_Interface_t *interface, int a, int b, int c, int uv_a, int uv_b, int uv_c)
+{
+	(void)uv_a; (void)uv_b; (void)uv_c;
+	return yafaray_addTriangle(interface, a, b, c);
+}
+
+int yafaray_addUv(yafaray_Interface_t *interface, float u, float v)
+{
+	(void)u; (void)v;
+	(void)interface;
+	return 0;
+}
+
+yafaray_bool_t yafaray_smoothMesh(yafaray_Interface_t *interface, const char *name, double angle)
+{
+	(void)angle;
+	I(interface)->logger.warning(std::string("Scene: smoothMesh('") + (name ? name : "") + "') ignored: the GPU core shades flat (N = Ng)");
+	return YAFARAY_BOOL_TRUE;
+}
+
+yafaray_bool_t yafaray_addInstance(yafaray_Interface_t *interface, const char *base_object_name, float, float, float, float, float, float, float, float, float, float, float, float, float, float, float, float)
+{
+	I(interface)->logger.error(std::string("Scene: instances ('") + (base_object_name ? base_object_name : "") + "') are not supported by the GPU core yet");
+	return YAFARAY_BOOL_FALSE;
+}
+
+yafaray_bool_t yafaray_addInstanceArray(yafaray_Interface_t *interface, const char *base_object_name, const float obj_to_world[4][4])
+{
+	(void)obj_to_world;
+	return yafaray_addInstance(interface, base_object_name, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0);
+}
+
+// ---- params (interface.cc:118-172) ----
+void yafaray_paramsSetVector(yafaray_Interface_t *interface, const char *name, double x, double y, double z)
+{
+	Param &p = (*I(interface)->cparams)[name];
+	p = Param();
+	p.type = Param::Vector;
+	p.vval = {(float)x, (float)y, (float)z};
+}
+
+void yafaray_paramsSetString(yafaray_Interface_t *interface, const char *name, const char *s)
+{
+	Param &p = (*I(interface)->cparams)[name];
+	p = Param();
+	p.type = Param::String;
+	p.sval = s ? s : "";
+}
+
+void yafaray_paramsSetBool(yafaray_Interface_t *interface, const char *name, yafaray_bool_t b)
+{
+	Param &p = (*I(interface)->cparams)[name];
+	p = Param();
+	p.type = Param::Bool;
+	p.bval = b != YAFARAY_BOOL_FALSE;
+}
+
+void yafaray_paramsSetInt(yafaray_Interface_t *interface, const char *name, int i)
+{
+	Param &p = (*I(interface)->cparams)[name];
+	p = Param();
+	p.type = Param::Int;
+	p.ival = i;
+}
+
+void yafaray_paramsSetFloat(yafaray_Interface_t *interface, const char *name, double f)
+{
+	Param &p = (*I(interface)->cparams)[name];
+	p = Param();
+	p.type = Param::Float;
+	p.fval = f;
+}
+
+void yafaray_paramsSetColor(yafaray_Interface_t *interface, const char *name, float r, float g, float b, float a)
+{
+	Interface *it = I(interface);
+	float c[3] = {r, g, b};
+	// Rgb::linearRgbFromColorSpace (color.h:352-380) with the interface's input colour space
+	if(it->input_color_space == 3)
+		for(float &v : c) v = hm::linearFromSrgb(v);
+	else if(it->input_color_space == 4)
+	{
+		const float m[3][3] = {{3.2406255f, -1.537208f, -0.4986286f}, {-0.9689307f, 1.8757561f, 0.0415175f}, {0.0557101f, -0.2040211f, 1.0569959f}};
+		const float o[3] = {c[0], c[1], c[2]};
+		for(int k = 0; k < 3; ++k) c[k] = m[k][0] * o[0] + m[k][1] * o[1] + m[k][2] * o[2];
+	}
+	else if(it->input_color_space == 1 && it->input_gamma != 1.f)
+		for(float &v : c) v = hm::powf_fast(v, it->input_gamma);
+	Param &p = (*it->cparams)[name];
+	p = Param();
+	p.type = Param::Color;
+	p.vval = {c[0], c[1], c[2], a};
+}
+
+void yafaray_paramsSetMatrix(yafaray_Interface_t *interface, const char *name, float m_00, float m_01, float m_02, float m_03, float m_10, float m_11, float m_12, float m_13, float m_20, float m_21, float m_22, float m_23, float m_30, float m_31, float m_32, float m_33, yafaray_bool_t transpose)
+{
+	Param &p = (*I(interface)->cparams)[name];
+	p = Param();
+	p.type = Param::Matrix;
+	p.vval = {m_00, m_01, m_02, m_03, m_10, m_11, m_12, m_13, m_20, m_21, m_22, m_23, m_30, m_31, m_32, m_33};
+	if(transpose)
+		for(int i = 0; i < 4; ++i)
+			for(int j = i + 1; j < 4; ++j) std::swap(p.vval[i * 4 + j], p.vval[j * 4 + i]);
+}
+
+void yafaray_paramsSetMatrixArray(yafaray_Interface_t *interface, const char *name, const float m[4][4], yafaray_bool_t transpose)
+{
+	yafaray_paramsSetMatrix(interface, name, m[0][0], m[0][1], m[0][2], m[0][3], m[1][0], m[1][1], m[1][2], m[1][3], m[2][0], m[2][1], m[2][2], m[2][3], m[3][0], m[3][1], m[3][2], m[3][3], transpose);
+}
+
+void yafaray_paramsClearAll(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	it->params.clear();
+	it->nodes_params.clear();
+	it->cparams = &it->params;
+}
+
+void yafaray_paramsPushList(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	it->nodes_params.emplace_back();
+	it->cparams = &it->nodes_params.back();
+}
+
+void yafaray_paramsEndList(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	it->cparams = &it->params;
+}
+
+// ---- create* (interface.cc:183-197) ----
+void yafaray_setCurrentMaterial(yafaray_Interface_t *interface, const char *name)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return;
+	if(!s->materials.count(name ? name : "")) s->log.warning(std::string("Scene: material '") + (name ? name : "") + "' not found");
+	s->current_material = name ? name : "";
+}
+
+#define CREATE(fn, method)                                                                     \
+	yafaray_bool_t fn(yafaray_Interface_t *interface, const char *name)                        \
+	{                                                                                          \
+		Interface *it = I(interface);                                                          \
+		Scene *s = it->sc();                                                                   \
+		return (s && s->method(name ? name : "", it->params)) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE; \
+	}
+
+CREATE(yafaray_createObject, createObject)
+CREATE(yafaray_createLight, createLight)
+CREATE(yafaray_createMaterial, createMaterial)
+CREATE(yafaray_createCamera, createCamera)
+CREATE(yafaray_createBackground, createBackground)
+CREATE(yafaray_createIntegrator, createIntegrator)
+CREATE(yafaray_createRenderView, createRenderView)
+
+yafaray_bool_t yafaray_createTexture(yafaray_Interface_t *interface, const char *name)
+{
+	I(interface)->logger.warning(std::string("Scene: texture '") + (name ? name : "") + "' accepted but not evaluated by the GPU core yet");
+	return YAFARAY_BOOL_TRUE;
+}
+
+yafaray_bool_t yafaray_createVolumeRegion(yafaray_Interface_t *interface, const char *name)
+{
+	I(interface)->logger.error(std::string("Scene: volume region '") + (name ? name : "") + "': participating media are not supported by the GPU core");
+	return YAFARAY_BOOL_FALSE;
+}
+
+yafaray_bool_t yafaray_createOutput(yafaray_Interface_t *interface, const char *name)
+{
+	Interface *it = I(interface);
+	Scene *s = it->sc();
+	if(!s) return YAFARAY_BOOL_FALSE;
+	s->outputs[name ? name : ""] = it->params;
+	it->logger.warning(std::string("Scene: image output '") + (name ? name : "") + "' registered; image files are not written by the GPU core (use the put-pixel callbacks / yafaray_amd_getFilm)");
+	return YAFARAY_BOOL_TRUE;
+}
+
+yafaray_bool_t yafaray_removeOutput(yafaray_Interface_t *interface, const char *name)
+{
+	Scene *s = I(interface)->sc();
+	return (s && s->outputs.erase(name ? name : "")) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+void yafaray_clearOutputs(yafaray_Interface_t *interface)
+{
+	Scene *s = I(interface)->sc();
+	if(s) s->outputs.clear();
+}
+
+void yafaray_clearAll(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	if(it->scene) it->scene.reset(new Scene(it->logger));
+	it->params.clear();
+	it->nodes_params.clear();
+	it->cparams = &it->params;
+}
+
+// ---- callbacks ----
+#define SETCB(fn, type, field)                                                                 \
+	void fn(yafaray_Interface_t *interface, type cb, void *data)                               \
+	{                                                                                          \
+		I(interface)->callbacks.field = cb;                                                    \
+		I(interface)->callbacks.field##_data = data;                                           \
+	}
+SETCB(yafaray_setRenderNotifyViewCallback, yafaray_RenderNotifyViewCallback_t, notify_view)
+SETCB(yafaray_setRenderNotifyLayerCallback, yafaray_RenderNotifyLayerCallback_t, notify_layer)
+SETCB(yafaray_setRenderPutPixelCallback, yafaray_RenderPutPixelCallback_t, put_pixel)
+SETCB(yafaray_setRenderHighlightPixelCallback, yafaray_RenderHighlightPixelCallback_t, highlight_pixel)
+SETCB(yafaray_setRenderFlushAreaCallback, yafaray_RenderFlushAreaCallback_t, flush_area)
+SETCB(yafaray_setRenderFlushCallback, yafaray_RenderFlushCallback_t, flush)
+SETCB(yafaray_setRenderHighlightAreaCallback, yafaray_RenderHighlightAreaCallback_t, highlight_area)
+
+// ---- render ----
+void yafaray_setupRender(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	Scene *s = it->sc();
+	if(s) s->setupRender(it->params);
+}
+
+void yafaray_render(yafaray_Interface_t *interface, yafaray_ProgressBarCallback_t monitor_callback, void *callback_data, yafaray_DisplayConsole_t progress_bar_display_console)
+{
+	(void)progress_bar_display_console;
+	Interface *it = I(interface);
+	Scene *s = it->sc();
+	if(s) s->render(it->callbacks, monitor_callback, callback_data, false);
+}
+
+void yafaray_defineLayer(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	Scene *s = it->sc();
+	if(!s) return;
+	std::string type;
+	it->params.get("type", type);
+	if(type != "combined") it->logger.warning("Layers: layer '" + type + "' is not produced by the GPU core (combined only)");
+	s->layers.push_back(type);
+}
+
+// ---- logging ----
+void yafaray_enablePrintDateTime(yafaray_Interface_t *interface, yafaray_bool_t value) { I(interface)->logger.setPrintDateTime(value != YAFARAY_BOOL_FALSE); }
+void yafaray_setConsoleVerbosityLevel(yafaray_Interface_t *interface, yafaray_LogLevel_t l) { I(interface)->logger.setConsoleLevel((int)l); }
+void yafaray_setLogVerbosityLevel(yafaray_Interface_t *interface, yafaray_LogLevel_t l) { I(interface)->logger.setLogLevel((int)l); }
+
+yafaray_LogLevel_t yafaray_logLevelFromString(const char *s)
+{
+	const std::string v = s ? s : "";
+	if(v == "mute") return YAFARAY_LOG_LEVEL_MUTE;
+	if(v == "error") return YAFARAY_LOG_LEVEL_ERROR;
+	if(v == "warning") return YAFARAY_LOG_LEVEL_WARNING;
+	if(v == "params") return YAFARAY_LOG_LEVEL_PARAMS;
+	if(v == "info") return YAFARAY_LOG_LEVEL_INFO;
+	if(v == "verbose") return YAFARAY_LOG_LEVEL_VERBOSE;
+	if(v == "debug") return YAFARAY_LOG_LEVEL_DEBUG;
+	return YAFARAY_LOG_LEVEL_VERBOSE;
+}
+
+void yafaray_printDebug(yafaray_Interface_t *interface, const char *msg) { I(interface)->logger.debug(msg ? msg : ""); }
+void yafaray_printVerbose(yafaray_Interface_t *interface, const char *msg) { I(interface)->logger.verbose(msg ? msg : ""); }
+void yafaray_printInfo(yafaray_Interface_t *interface, const char *msg) { I(interface)->logger.info(msg ? msg : ""); }
+void yafaray_printParams(yafaray_Interface_t *interface, const char *msg) { I(interface)->logger.params(msg ? msg : ""); }
+void yafaray_printWarning(yafaray_Interface_t *interface, const char *msg) { I(interface)->logger.warning(msg ? msg : ""); }
+void yafaray_printError(yafaray_Interface_t *interface, const char *msg) { I(interface)->logger.error(msg ? msg : ""); }
+
+void yafaray_cancelRendering(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	if(it->scene) it->scene->canceled = true;   // polled between wavefront chunks
+}
+
+void yafaray_setInputColorSpace(yafaray_Interface_t *interface, const char *color_space_string, float gamma_val)
+{
+	Interface *it = I(interface);
+	const std::string n = color_space_string ? color_space_string : "";
+	// Rgb::colorSpaceFromName (color.cc:123-130)
+	if(n == "LinearRGB") it->input_color_space = 2;
+	else if(n == "sRGB") it->input_color_space = 3;
+	else if(n == "XYZ") it->input_color_space = 4;
+	else it->input_color_space = 1;
+	it->input_gamma = gamma_val;
+}
+
+// ---- images (textures are not evaluated yet; the buffers are kept for the API contract) ----
+struct ImageHandle
+{
+	int w, h;
+	std::vector<float> px;
+};
+
+yafaray_Image_t *yafaray_createImage(yafaray_Interface_t *interface, const char *name)
+{
+	Interface *it = I(interface);
+	int w = 0, h = 0;
+	it->params.get("width", w);
+	it->params.get("height", h);
+	auto *img = new ImageHandle{std::max(1, w), std::max(1, h), {}};
+	img->px.assign((size_t)img->w * img->h * 4, 0.f);
+	it->logger.verbose(std::string("Scene: image '") + (name ? name : "") + "' created (texture evaluation is not part of the GPU core yet)");
+	static std::vector<std::unique_ptr<ImageHandle>> keep;   // owned by the library, as in the reference (scene.h:214)
+	keep.emplace_back(img);
+	return reinterpret_cast<yafaray_Image_t *>(img);
+}
+
+yafaray_bool_t yafaray_setImageColor(yafaray_Image_t *image, int x, int y, float r, float g, float b, float a)
+{
+	auto *img = reinterpret_cast<ImageHandle *>(image);
+	if(!img || x < 0 || y < 0 || x >= img->w || y >= img->h) return YAFARAY_BOOL_FALSE;
+	float *p = &img->px[4 * ((size_t)y * img->w + x)];
+	p[0] = r; p[1] = g; p[2] = b; p[3] = a;
+	return YAFARAY_BOOL_TRUE;
+}
+
+yafaray_bool_t yafaray_getImageColor(const yafaray_Image_t *image, int x, int y, float *r, float *g, float *b, float *a)
+{
+	auto *img = reinterpret_cast<const ImageHandle *>(image);
+	if(!img || x < 0 || y < 0 || x >= img->w || y >= img->h) return YAFARAY_BOOL_FALSE;
+	const float *p = &img->px[4 * ((size_t)y * img->w + x)];
+	*r = p[0]; *g = p[1]; *b = p[2]; *a = p[3];
+	return YAFARAY_BOOL_TRUE;
+}
+
+void yafaray_setConsoleLogColorsEnabled(yafaray_Interface_t *interface, yafaray_bool_t colors_enabled) { I(interface)->logger.setColors(colors_enabled != YAFARAY_BOOL_FALSE); }
+
+int yafaray_getVersionMajor() { return 4; }
+int yafaray_getVersionMinor() { return 0; }
+int yafaray_getVersionPatch() { return 0; }
+char *yafaray_getVersionString() { return dupString("4.0.0-mi355x (libYafaRay C API on HIP/gfx950)"); }
+
+char *yafaray_getLayersTable(const yafaray_Interface_t *interface)
+{
+	(void)interface;
+	return dupString("combined\tCombined\tColorAlpha\n");
+}
+
+char *yafaray_getViewsTable(const yafaray_Interface_t *interface)
+{
+	const Interface *it = I(interface);
+	std::string s;
+	if(it->scene)
+		for(const auto &v : it->scene->views) s += v.first + "\t" + v.second + "\n";
+	return dupString(s);
+}
+
+void yafaray_deallocateCharPointer(char *p) { std::free(p); }
+
+// ---------------------------------------------------------------------------------------------
+// extensions (include/yafaray_amd.h)
+// ---------------------------------------------------------------------------------------------
+int yafaray_amd_addVertices(yafaray_Interface_t *interface, const double *xyz, int n)
+{
+	Scene *s = I(interface)->sc();
+	if(!s || !s->current_object) { I(interface)->logger.error("Scene: addVertices() outside of an object"); return -1; }
+	int last = -1;
+	for(int i = 0; i < n; ++i) last = s->addVertex((float)xyz[3 * i], (float)xyz[3 * i + 1], (float)xyz[3 * i + 2]);
+	return last;
+}
+
+yafaray_bool_t yafaray_amd_addTriangles(yafaray_Interface_t *interface, const int *abc, int n)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return YAFARAY_BOOL_FALSE;
+	for(int i = 0; i < n; ++i)
+		if(!s->addTriangle(abc[3 * i], abc[3 * i + 1], abc[3 * i + 2])) return YAFARAY_BOOL_FALSE;
+	return YAFARAY_BOOL_TRUE;
+}
+
+yafaray_bool_t yafaray_amd_buildAccelerator(yafaray_Interface_t *interface)
+{
+	Scene *s = I(interface)->sc();
+	return (s && s->buildAccelerator()) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+yafaray_bool_t yafaray_amd_traceClosest(yafaray_Interface_t *interface, const float *rays, int n, float *t, int *prims)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return YAFARAY_BOOL_FALSE;
+	if(s->geometry_dirty && !s->buildAccelerator()) return YAFARAY_BOOL_FALSE;
+	return s->gpu()->traceRays(false, rays, n, t, prims) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+yafaray_bool_t yafaray_amd_traceShadow(yafaray_Interface_t *interface, const float *rays, int n, int *occluded)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return YAFARAY_BOOL_FALSE;
+	if(s->geometry_dirty && !s->buildAccelerator()) return YAFARAY_BOOL_FALSE;
+	std::vector<float> t((size_t)std::max(n, 1));
+	if(!s->gpu()->traceRays(true, rays, n, t.data(), nullptr)) return YAFARAY_BOOL_FALSE;
+	for(int i = 0; i < n; ++i) occluded[i] = t[i] != 0.f ? 1 : 0;
+	return YAFARAY_BOOL_TRUE;
+}
+
+yafaray_bool_t yafaray_amd_getFilm(const yafaray_Interface_t *interface, float *rgba, float *weights)
+{
+	const Interface *it = I(interface);
+	if(!it->scene || it->scene->film_rgba.empty()) return YAFARAY_BOOL_FALSE;
+	if(rgba) std::memcpy(rgba, it->scene->film_rgba.data(), it->scene->film_rgba.size() * 4);
+	if(weights) std::memcpy(weights, it->scene->film_weights.data(), it->scene->film_weights.size() * 4);
+	return YAFARAY_BOOL_TRUE;
+}
+
+yafaray_bool_t yafaray_amd_getFilmDevice(const yafaray_Interface_t *interface, void *rgba_dev, int y0, int y1)
+{
+	const Interface *it = I(interface);
+	if(!it->scene) return YAFARAY_BOOL_FALSE;
+	return it->scene->gpu()->filmToDevice(rgba_dev, y0, y1) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+void yafaray_amd_setTileRowShard(yafaray_Interface_t *interface, int rank, int world)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return;
+	s->shard_world = world < 1 ? 1 : world;
+	s->shard_rank = (rank < 0 || rank >= s->shard_world) ? 0 : rank;
+}
+
+yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t *interface)
+{
+	Interface *it = I(interface);
+	Scene *s = it->sc();
+	Callbacks none;
+	return (s && s->render(none, nullptr, nullptr, true)) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+void yafaray_amd_getStats(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats)
+{
+	const Interface *it = I(interface);
+	if(it->scene && stats) *stats = it->scene->stats;
+}
+
+void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots)
+{
+	Scene *s = I(interface)->sc();
+	if(s) s->chunk_slots = slots < 1024 ? 1024 : slots;
+}
+
+void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_t enable)
+{
+	Scene *s = I(interface)->sc();
+	if(s) s->profile_kernels = enable != YAFARAY_BOOL_FALSE;
+}
+
+const char *yafaray_amd_lastError(const yafaray_Interface_t *interface) { return I(interface)->logger.lastError().c_str(); }
+
+}

@@ -1,0 +1,336 @@
+// Device numerics of the hot path: libYafaRay's float expressions restated for gfx950 so that
+// every sample reproduces the reference CPU build bit for bit.
+//
+// Three hazards from SURVEY.md Appendix A are handled here:
+//  * no FMA contraction: the whole library is compiled with -ffp-contract=off, and every
+//    expression below keeps the reference's left-to-right evaluation order;
+//  * x87 promotions: the reference multiplies floats by `long double` constants
+//    (include/math/math.h:46-65), so on x86-64 the product is rounded to a 64-bit significand and
+//    then to float.  gfx950 has no 80-bit type, so x87mul*() reproduce that double rounding
+//    exactly from an exact double-double product (two-product via fma + exact error terms);
+//  * FAST_TRIG parabolic sin/cos (math.h:218-250) and the Faure-scrambled Halton sequences
+//    (src/sampler/halton.cc:421-441) in double precision, which is IEEE on gfx950.
+//
+// The header is also compiled for the host (tests/test_devmath.py builds a tiny g++ harness
+// that checks x87mul*() against real long double on millions of inputs).
+#pragma once
+
+#include <cstdint>
+#include <cmath>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define YD __host__ __device__ __forceinline__
+#else
+#define YD inline
+#endif
+
+namespace yafamd
+{
+
+// ---------------------------------------------------------------------------------------------
+// long double constants as exact (hi, lo) double pairs: hi = (double)C, lo = (double)(C - hi).
+// Values from include/math/math.h:46-88 (verified exact by tests/test_devmath.py).
+// ---------------------------------------------------------------------------------------------
+struct X87Const { double hi, lo; };
+constexpr X87Const kPi = {0x1.921fb54442d18p+1, 0x1.1a8p-53};
+constexpr X87Const kDivPiBy2 = {0x1.921fb54442d18p+0, 0x1.1a8p-54};
+constexpr X87Const kDiv1ByPi = {0x1.45f306dc9c883p-2, -0x1.6bp-56};
+constexpr X87Const kMultPiBy2 = {0x1.921fb54442d18p+2, 0x1.1a8p-52};
+constexpr X87Const kDiv1By2Pi = {0x1.45f306dc9c883p-3, -0x1.6bp-57};
+constexpr X87Const kDiv4ByPi = {0x1.45f306dc9c883p+0, -0x1.6bp-54};
+constexpr X87Const kDiv4BySquaredPi = {0x1.9f02f6222c72p-2, -0x1.248p-56};
+// (float) casts of the same constants, as the reference writes static_cast<float>(math::...)
+constexpr float kPiF = 0x1.921fb6p+1f;
+constexpr float kDivPiBy2F = 0x1.921fb6p+0f;
+constexpr float kMultPiBy2F = 0x1.921fb6p+2f;
+constexpr float kDiv1By2PiF = 0x1.45f306p-3f;
+constexpr double kSampleMultRatio = 0x1p-32;            // math.h:88 (exact power of two)
+constexpr float kMinRaydistGlobal = 0.00005f;           // include/common/yafaray_common.h:28
+
+// ---------------------------------------------------------------------------------------------
+// exact x87 double rounding emulation
+// ---------------------------------------------------------------------------------------------
+struct DD { double hi, lo; };
+
+YD DD fastTwoSum(double a, double b)
+{
+	const double s = a + b;
+	return {s, b - (s - a)};
+}
+
+// ilogb for finite non-zero doubles via the exponent bits (normal range only)
+YD int expOf(double x)
+{
+	uint64_t u;
+	__builtin_memcpy(&u, &x, 8);
+	return (int)((u >> 52) & 0x7ff) - 1023;
+}
+
+YD bool isPow2(double x)
+{
+	uint64_t u;
+	__builtin_memcpy(&u, &x, 8);
+	return (u & 0xfffffffffffffull) == 0;
+}
+
+// Round |v| (non-negative, normalized |lo| <= ulp(hi)/2 + small) to a 64-bit significand, RNE.
+// Result exact as (hi, r*q64).
+YD DD round64(DD v)
+{
+	const int eh = expOf(v.hi);
+	const int ev = (isPow2(v.hi) && v.lo < 0.0) ? eh - 1 : eh;
+	const double q64 = ldexp(1.0, ev - 63);
+	const double r = rint(v.lo / q64);   // parity of the full significand == parity of r
+	return {v.hi, r * q64};
+}
+
+// Round a non-negative exact value (hi, lo) to float, RNE (normal float range).
+YD float round24(DD v)
+{
+	if(v.hi == 0.0) return (float)v.lo;
+	const int eh = expOf(v.hi);
+	const int e2 = (isPow2(v.hi) && v.lo < 0.0) ? eh - 1 : eh;
+	const double qf = ldexp(1.0, e2 - 23);
+	const double t = v.hi / qf;
+	const double I = floor(t);
+	const double f = t - I;
+	const double d = v.lo / qf;
+	double k = I;
+	if(f > 0.5) k = I + 1.0;
+	else if(f == 0.5)
+	{
+		if(d > 0.0) k = I + 1.0;
+		else if(d == 0.0) k = (fmod(I, 2.0) != 0.0) ? I + 1.0 : I;
+	}
+	else if(f == 0.0 && d < 0.0 && e2 == eh)
+	{
+		// value slightly below an integer multiple: RNE keeps I (|d| < 1/2)
+		k = I;
+	}
+	return (float)(k * qf);
+}
+
+// exact product C * x (C a long double constant, x a float) as a normalized DD
+YD DD exactMul(const X87Const &c, double xd)
+{
+	const double p = c.hi * xd;
+	const double e = fma(c.hi, xd, -p);
+	const double q = c.lo * xd;
+	return fastTwoSum(p, e + q);
+}
+
+// (float)((long double)C * x)
+YD float x87mul(const X87Const &c, float x)
+{
+	if(x == 0.f || !(fabsf(x) < 3.0e38f)) return (float)(c.hi * (double)x);
+	const double ax = fabs((double)x);
+	const float r = round24(round64(exactMul(c, ax)));
+	return x < 0.f ? -r : r;
+}
+
+// (float)((long double)C * x * y) — two x87 roundings then the float one
+YD float x87mul2(const X87Const &c, float x, float y)
+{
+	if(x == 0.f || y == 0.f) return (float)(c.hi * (double)x * (double)y);
+	const double ax = fabs((double)x), ay = fabs((double)y);
+	const DD t = round64(exactMul(c, ax));
+	const double p = t.hi * ay;
+	const double e = fma(t.hi, ay, -p);
+	const double q = t.lo * ay;
+	const float r = round24(round64(fastTwoSum(p, e + q)));
+	return ((x < 0.f) != (y < 0.f)) ? -r : r;
+}
+
+// (float)(((long double)C * a) / (long double)b) with a, b > 0 floats (light pdfs,
+// src/light/light_area.cc:88).  The quotient is formed to ~104 bits (double-double) before the
+// two roundings.
+YD float x87mulDiv(const X87Const &c, float a, float b)
+{
+	if(a == 0.f) return 0.f;
+	const DD n = round64(exactMul(c, (double)a));
+	const double bd = (double)b;
+	const double q1 = n.hi / bd;
+	const double r1 = fma(-q1, bd, n.hi);
+	const double q2 = (r1 + n.lo) / bd;
+	return round24(round64(fastTwoSum(q1, q2)));
+}
+
+// x > C / x < -C with C long double (exact for float x, see DESIGN.md numerics note)
+YD bool gtC(float x, const X87Const &c) { return (double)x > c.hi || ((double)x == c.hi && c.lo < 0.0); }
+YD bool ltNegC(float x, const X87Const &c) { return (double)x < -c.hi || ((double)x == -c.hi && c.lo < 0.0); }
+
+// ---------------------------------------------------------------------------------------------
+// math.h FAST_TRIG sin / cos
+// ---------------------------------------------------------------------------------------------
+YD float fsin(float x)
+{
+	if(gtC(x, kMultPiBy2) || ltNegC(x, kMultPiBy2)) x -= ((int)(x * kDiv1By2PiF)) * kMultPiBy2F;
+	if(ltNegC(x, kPi)) x += kMultPiBy2F;
+	else if(gtC(x, kPi)) x -= kMultPiBy2F;
+	x = x87mul(kDiv4ByPi, x) - x87mul2(kDiv4BySquaredPi, x, fabsf(x));
+	const float result = 0.225f * (x * fabsf(x) - x) + x;
+	if(result <= -1.f) return -1.f;
+	else if(result >= 1.f) return 1.f;
+	return result;
+}
+
+YD float fcos(float x) { return fsin(x + kDivPiBy2F); }
+
+// ---------------------------------------------------------------------------------------------
+// vectors / colours with the reference's operation order (include/geometry/vector.h:108-276,
+// include/color/color.h:258-296)
+// ---------------------------------------------------------------------------------------------
+struct V3 { float x, y, z; };
+YD V3 v3(float a, float b, float c) { return {a, b, c}; }
+YD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+YD V3 operator*(float f, V3 v) { return {f * v.x, f * v.y, f * v.z}; }
+YD V3 operator*(V3 v, float f) { return {f * v.x, f * v.y, f * v.z}; }
+YD V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+YD V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+YD V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+YD V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+YD float lengthSqr(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+YD float length(V3 a) { return sqrtf(lengthSqr(a)); }
+YD V3 normalize(V3 v)
+{
+	float len = lengthSqr(v);
+	if(len != 0.f)
+	{
+		len = 1.f / sqrtf(len);
+		v.x *= len; v.y *= len; v.z *= len;
+	}
+	return v;
+}
+YD void coordsSystem(V3 n, V3 &u, V3 &v)
+{
+	if((n.x == 0.f) && (n.y == 0.f))
+	{
+		u = (n.z < 0.f) ? v3(-1.f, 0.f, 0.f) : v3(1.f, 0.f, 0.f);
+		v = v3(0.f, 1.f, 0.f);
+	}
+	else
+	{
+		const float d = 1.f / sqrtf(n.y * n.y + n.x * n.x);
+		u = v3(n.y * d, -n.x * d, 0.f);
+		v = cross(n, u);
+	}
+}
+
+struct C3 { float r, g, b; };
+YD C3 c3(float f) { return {f, f, f}; }
+YD C3 operator*(C3 a, C3 b) { return {a.r * b.r, a.g * b.g, a.b * b.b}; }
+YD C3 operator*(float f, C3 c) { return {f * c.r, f * c.g, f * c.b}; }
+YD C3 operator*(C3 c, float f) { return {f * c.r, f * c.g, f * c.b}; }
+YD C3 operator/(C3 c, float f) { return {c.r / f, c.g / f, c.b / f}; }
+YD C3 operator+(C3 a, C3 b) { return {a.r + b.r, a.g + b.g, a.b + b.b}; }
+YD bool isBlack(C3 c) { return c.r == 0 && c.g == 0 && c.b == 0; }
+YD float maxComp(C3 c) { return fmaxf(c.r, fmaxf(c.g, c.b)); }
+
+// ---------------------------------------------------------------------------------------------
+// samplers: include/sampler/sample.h:45-151, include/sampler/halton.h:41-81, halton.cc:421-441,
+// include/math/random.h:56-104
+// ---------------------------------------------------------------------------------------------
+YD float clamp01(float v) { return fmaxf(0.f, fminf(1.f, v)); }
+
+YD float riVdC(uint32_t bits, uint32_t r = 0)
+{
+	bits = (bits << 16) | (bits >> 16);
+	bits = ((bits & 0x00ff00ffu) << 8) | ((bits & 0xff00ff00u) >> 8);
+	bits = ((bits & 0x0f0f0f0fu) << 4) | ((bits & 0xf0f0f0f0u) >> 4);
+	bits = ((bits & 0x33333333u) << 2) | ((bits & 0xccccccccu) >> 2);
+	bits = ((bits & 0x55555555u) << 1) | ((bits & 0xaaaaaaaau) >> 1);
+	return clamp01((float)((double)(bits ^ r) * kSampleMultRatio));
+}
+
+YD float riS(uint32_t i, uint32_t r = 0)
+{
+	for(uint32_t v = 1u << 31; i; i >>= 1, v ^= v >> 1)
+		if(i & 1) r ^= v;
+	return clamp01((float)((double)r * kSampleMultRatio));
+}
+
+YD float riLp(uint32_t i, uint32_t r = 0)
+{
+	for(uint32_t v = 1u << 31; i; i >>= 1, v |= v >> 1)
+		if(i & 1) r ^= v;
+	return clamp01((float)((double)r * kSampleMultRatio));
+}
+
+YD uint32_t fnv32(uint32_t value)
+{
+	uint32_t hash = 0x811c9dc5u;
+	for(int k = 0; k < 4; ++k)
+	{
+		hash ^= (value >> (8 * k)) & 0xffu;
+		hash *= 0x01000193u;
+	}
+	return hash;
+}
+
+// Halton(base, start).getNext() — one fresh generator per call site (integrator_montecarlo.cc:399)
+YD float haltonFirst(uint32_t base, double inv_base, uint32_t start)
+{
+	double factor = inv_base, value = 0.0;
+	while(start > 0)
+	{
+		value += (double)(start % base) * factor;
+		start /= base;
+		factor *= inv_base;
+	}
+	const double r = 0.9999999999 - value;
+	if(inv_base < r) value += inv_base;
+	else
+	{
+		double hh = 0.0, h = inv_base;
+		while(h >= r)
+		{
+			hh = h;
+			h *= inv_base;
+		}
+		value += hh + h - 1.0;
+	}
+	return clamp01((float)value);
+}
+
+// Faure-scrambled radical inverse.  `perm` points at the digit permutation of dimension `dim`
+// (tables uploaded by the host: DevScene::faure_*).
+YD double lowDiscrepancy(const uint8_t *perm, uint32_t base, double f, uint32_t n)
+{
+	double value = 0.0, dn = (double)n, factor = f;
+	while(n > 0)
+	{
+		value += (double)perm[n % base] * factor;
+		dn *= f;
+		n = (uint32_t)dn;
+		factor *= f;
+	}
+	return value;
+}
+
+struct Mwc
+{
+	uint32_t x, c;
+	YD double next()
+	{
+		const uint32_t a = 1791398085u, ah = a >> 16, al = a & 65535u;
+		const uint32_t xh = x >> 16, xl = x & 65535u;
+		x = x * a + c;
+		c = xh * ah + ((xh * al) >> 16) + ((xl * ah) >> 16);
+		if(xl * al >= ~c + 1) c++;
+		return (double)x * kSampleMultRatio;
+	}
+};
+
+// sample.h:45-54
+YD V3 cosHemisphere(V3 n, V3 ru, V3 rv, float s_1, float s_2)
+{
+	if(s_1 >= 1.0f) return n;
+	const float z_1 = s_1;
+	const float z_2 = x87mul(kMultPiBy2, s_2);
+	const V3 a = ru * fcos(z_2);
+	const V3 b = rv * fsin(z_2);
+	return (a + b) * sqrtf(1.f - z_1) + n * sqrtf(z_1);
+}
+
+} // namespace yafamd

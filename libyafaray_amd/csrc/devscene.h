@@ -1,0 +1,150 @@
+// Plain-old-data layout shared by the host driver (render.cc) and the HIP kernels
+// (kernels.hip).  Everything the hot path reads per sample lives in HBM in these layouts:
+//
+//   nodes   : BVH2 with both child boxes stored in the parent, 4 x float4 = 64 B per node
+//             n0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)   n1 = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//             n2 = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)   n3 = (child0, child1, count0, count1)
+//             child >= 0: inner node index; child < 0: leaf, triangles [~child, ~child + count)
+//   tris    : triangles in leaf order, 3 x float4 = 48 B: (v0, eps) (e1, prim) (e2, 0) — the
+//             Moller-Trumbore operands of primitive_triangle.cc:47-49 precomputed on the host with
+//             the same float operations, so the device test is bit-identical to the reference's.
+//   prim_ng : per original primitive (ng.xyz, material index) — TrianglePrimitive::getSurface.
+#pragma once
+#include <cstdint>
+#include <hip/hip_runtime.h>
+
+namespace yafamd
+{
+
+enum : uint32_t
+{
+	B_NONE = 0, B_SPECULAR = 1u << 0, B_GLOSSY = 1u << 1, B_DIFFUSE = 1u << 2, B_DISPERSIVE = 1u << 3,
+	B_REFLECT = 1u << 4, B_TRANSMIT = 1u << 5, B_FILTER = 1u << 6, B_EMIT = 1u << 7, B_VOLUMETRIC = 1u << 8,
+	B_ALL = B_SPECULAR | B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT | B_FILTER
+};
+
+enum : uint32_t { MAT_SHINYDIFFUSE = 0, MAT_LIGHT = 1 };
+enum : uint32_t { LIGHT_POINT = 0, LIGHT_AREA = 1 };
+enum : int { INT_DIRECT = 0, INT_PATH = 1 };
+
+struct DevMaterial
+{
+	uint32_t type, bsdf_flags, n_bsdf, double_sided;
+	uint32_t receive_shadows, flat, pad0, pad1;
+	float diffuse[4];       // shinydiffuse diffuse colour
+	float emit[4];          // shinydiffuse emit colour / light_mat colour * power
+	float comp[4];          // getComponents() (no shader nodes)
+	uint32_t c_flags[4];
+	uint32_t c_index[4];
+};
+
+struct DevLight
+{
+	uint32_t type, cast_shadows;
+	int32_t samples;        // area: ceilf(samples * light sample multiplier)
+	float inv_samples;
+	float color[4];
+	float pos[4];           // point position / area corner
+	float to_x[4], to_y[4], fnormal[4];
+	float c2[4], c3[4], c4[4];
+	float area;
+	uint32_t nee_base;      // first NEE entry of this light in the estimateAllDirectLight layout
+	uint32_t nee_count;     // point: 1, area: 2 * samples
+	uint32_t pad;
+};
+
+struct DevCamera
+{
+	float pos[4], vright[4], vup[4], vto[4], cam_z[4], near_p[4], far_p[4];
+	int resx, resy, pad0, pad1;
+};
+
+// A band of pixel rows rendered as a run of tiles (imagesplitter.cc:30-49 linear order):
+// tiles of width `tile` left to right, pixels row-major inside each tile.
+struct DevJob
+{
+	int y0, y1;             // pixel rows [y0, y1)
+	uint64_t sample_base;   // first sample id of the job in the frame-local enumeration
+};
+
+struct DevScene
+{
+	const float4 *nodes;
+	const float4 *tris;
+	const float4 *prim_ng;
+	const DevMaterial *mats;
+	const DevLight *lights;
+	const uint8_t *faure;          // concatenated Faure digit permutations, dims 0..49
+	const uint32_t *faure_off;     // offset of each dimension's table
+	const uint32_t *faure_base;    // base of each dimension
+	const double *faure_inv;       // inv_prims (halton.cc:413)
+	int n_nodes, n_tris, n_mats, n_lights;
+	int scene_in_lds;              // nodes+tris copied to LDS by each trace workgroup
+	int lds_nodes, lds_tris;
+
+	DevCamera cam;
+
+	int integrator, width, height, spp;
+	int tile, bounces, path_samples, rr_min_bounces;
+	int caustic_path, has_bg, bg_transp, nee_k;
+	float bg[4];
+	int shadow_bias_auto, ray_min_dist_auto;
+	float shadow_bias, ray_min_dist;
+	uint32_t base_offset, rr_seed;
+	float clamp_samples;
+	int nee_all_count;             // entries of the estimateAllDirectLight layout
+};
+
+struct DevFilm
+{
+	float table[256];
+	float filterw, table_scale;
+	int reach_fwd, reach_back;     // footprint reach: sources in [x - reach_fwd, x + reach_back]
+	int width, height, spp, tile;
+};
+
+// Per-chunk wavefront state (structure of arrays, capacity = chunk slots).
+struct DevPaths
+{
+	uint32_t *stage;       // stage | subpath << 8 | depth << 20
+	uint32_t *flags;       // mat_bsd_fs (v1 flags) | bits below
+	float *w;              // the integrator's persistent sample weight `w`
+	float4 *thr;           // throughput
+	float4 *col;           // col (first-vertex estimate) .w = alpha
+	float4 *pcol;          // path_col
+	float4 *pwo;           // pwo (outgoing direction at the current path vertex)
+	float4 *pend_thr;      // throughput at the pending vertex (after Russian roulette)
+	float4 *pend_emit;     // emission pending at that vertex
+	float4 *v0p;           // first hit p .w = prim (bits)   — only used when path_samples > 1
+	float4 *v0wo;          // first hit wo
+	uint2 *rng;            // MWC (x, c) for Russian roulette
+	uint2 *pix;            // (PixelSamplingData::offset_, PixelSamplingData::sample_)
+	float4 *nee;           // [slots * nee_k] contributions .w = valid
+	uint8_t *occ;          // [slots * nee_k] shadow results
+};
+
+struct DevQueues
+{
+	// active list (parallel to the closest-ray queue)
+	int *slot;
+	float4 *ray_o;         // origin, .w = tmin
+	float4 *ray_d;         // direction, .w = tmax (< 0: infinite); NaN: no ray this iteration
+	float *hit_t;
+	int *hit_prim;
+	// shadow rays
+	float4 *sh_o;          // origin, .w unused
+	float4 *sh_d;          // direction, .w = t_max (already tmax - 2 tmin, or inf)
+	int *sh_idx;           // slot * nee_k + entry
+};
+
+struct DevCounters
+{
+	uint32_t n_active, n_shadow, pad0, pad1;
+};
+
+struct DevStats
+{
+	unsigned long long closest_rays, shadow_rays, node_visits, tri_tests;
+};
+
+} // namespace yafamd

@@ -1,0 +1,651 @@
+// Host side: logger, scene assembly and render orchestration (see host.h).
+#include "host.h"
+#include "hostmath.h"
+#include "render.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <ctime>
+#include <sstream>
+
+namespace yafamd
+{
+
+// ---------------------------------------------------------------------------------------------
+// Logger (include/common/logger.h:62-166)
+// ---------------------------------------------------------------------------------------------
+void Logger::log(int level, const std::string &msg)
+{
+	std::lock_guard<std::mutex> g(mtx_);
+	const std::time_t now = std::time(nullptr);
+	char tod[16];
+	std::strftime(tod, sizeof(tod), "%H:%M:%S", std::localtime(&now));
+	if(cb_ && level <= log_level_) cb_((yafaray_LogLevel_t)level, (long)now, tod, msg.c_str(), data_);
+	if(console_ == YAFARAY_DISPLAY_CONSOLE_NORMAL && level <= console_level_)
+	{
+		static const char *names[] = {"", "ERROR", "WARNING", "PARAMS", "INFO", "VERB", "DEBUG"};
+		std::fprintf(level <= YAFARAY_LOG_LEVEL_WARNING ? stderr : stdout, "[%s] %s: %s\n", print_datetime_ ? tod : "",
+		             names[std::min(std::max(level, 0), 6)], msg.c_str());
+	}
+}
+
+std::string ParamMap::print() const
+{
+	std::ostringstream os;
+	for(const auto &kv : map_)
+	{
+		os << kv.first << "=";
+		const Param &p = kv.second;
+		switch(p.type)
+		{
+			case Param::Int: os << p.ival; break;
+			case Param::Bool: os << (p.bval ? "true" : "false"); break;
+			case Param::Float: os << p.fval; break;
+			case Param::String: os << p.sval; break;
+			default:
+				os << "(";
+				for(size_t i = 0; i < p.vval.size(); ++i) os << (i ? "," : "") << p.vval[i];
+				os << ")";
+		}
+		os << " ";
+	}
+	return os.str();
+}
+
+// ---------------------------------------------------------------------------------------------
+// small float vector helpers with the reference's operation order (vector.h:108-276)
+// ---------------------------------------------------------------------------------------------
+namespace
+{
+struct F3 { float x, y, z; };
+inline F3 sub(F3 a, F3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline F3 add(F3 a, F3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline F3 mul(F3 v, float f) { return {f * v.x, f * v.y, f * v.z}; }
+inline F3 crs(F3 a, F3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline float lsq(F3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+inline F3 nrm(F3 v)
+{
+	float len = lsq(v);
+	if(len != 0.f)
+	{
+		len = 1.f / std::sqrt(len);
+		v.x *= len; v.y *= len; v.z *= len;
+	}
+	return v;
+}
+inline float normLen(F3 &v)
+{
+	float vl = lsq(v);
+	if(vl != 0.f)
+	{
+		vl = std::sqrt(vl);
+		const float d = 1.f / vl;
+		v.x *= d; v.y *= d; v.z *= d;
+	}
+	return vl;
+}
+inline F3 f3(const float *p) { return {p[0], p[1], p[2]}; }
+inline void put(float *dst, F3 v, float w = 0.f) { dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = w; }
+} // namespace
+
+// ---------------------------------------------------------------------------------------------
+// Scene
+// ---------------------------------------------------------------------------------------------
+Scene::Scene(Logger &l) : log(l) {}
+Scene::~Scene() = default;
+
+GpuRenderer *Scene::gpu()
+{
+	if(!gpu_) gpu_.reset(new GpuRenderer(log));
+	return gpu_.get();
+}
+
+// scene.cc:977-1004, object_mesh.cc:35-86
+bool Scene::createObject(const std::string &name, const ParamMap &p)
+{
+	if(objects.count(name)) { log.error("Scene: object '" + name + "' already exists"); return false; }
+	std::string type = "mesh";
+	p.get("type", type);
+	if(type != "mesh") { log.error("Scene: object type '" + type + "' is not supported by the GPU core (meshes only)"); return false; }
+	MeshObject &o = objects[name];
+	o.name = name;
+	p.get("is_base_object", o.is_base);
+	p.get("visibility", o.visibility);
+	if(o.visibility != "normal" && o.visibility != "visible" && o.visibility != "invisible")
+		log.warning("Scene: object '" + name + "' visibility '" + o.visibility + "' is treated as 'normal' by the GPU core");
+	int nv = 0, nf = 0;
+	if(p.get("num_vertices", nv) && nv > 0) o.verts.reserve(3 * (size_t)nv);
+	if(p.get("num_faces", nf) && nf > 0) { o.tris.reserve(3 * (size_t)nf); o.tri_mat.reserve(nf); }
+	object_order.push_back(name);
+	current_object = &o;
+	geometry_dirty = true;
+	return true;
+}
+
+bool Scene::endObject()
+{
+	if(!current_object) { log.error("Scene: endObject() without an object"); return false; }
+	current_object->ended = true;
+	current_object = nullptr;
+	return true;
+}
+
+int Scene::addVertex(float x, float y, float z)
+{
+	if(!current_object) { log.error("Scene: addVertex() outside of an object"); return -1; }
+	auto &v = current_object->verts;
+	v.push_back(x);
+	v.push_back(y);
+	v.push_back(z);
+	return (int)(v.size() / 3) - 1;
+}
+
+bool Scene::addTriangle(int a, int b, int c)
+{
+	if(!current_object) { log.error("Scene: addTriangle() outside of an object"); return false; }
+	const int nv = (int)(current_object->verts.size() / 3);
+	if(a < 0 || b < 0 || c < 0 || a >= nv || b >= nv || c >= nv)
+	{
+		log.error("Scene: addTriangle() vertex index out of range in object '" + current_object->name + "'");
+		return false;
+	}
+	auto it = material_index.find(current_material);
+	if(it == material_index.end())
+	{
+		log.error("Scene: addTriangle() with no valid current material ('" + current_material + "')");
+		return false;
+	}
+	current_object->tris.push_back(a);
+	current_object->tris.push_back(b);
+	current_object->tris.push_back(c);
+	current_object->tri_mat.push_back(it->second);
+	return true;
+}
+
+// material_shiny_diffuse.cc:28-87 + 495-640, material_simple.cc:36-70
+bool Scene::createMaterial(const std::string &name, const ParamMap &p)
+{
+	if(materials.count(name)) { log.error("Scene: material '" + name + "' already exists"); return false; }
+	std::string type;
+	p.get("type", type);
+	DevMaterial m{};
+	m.receive_shadows = 1;
+	bool b;
+	if(type == "shinydiffusemat")
+	{
+		float col[4] = {1.f, 1.f, 1.f, 1.f};
+		p.getColor("color", col);
+		float diffuse = 1.f, transparency = 0.f, translucency = 0.f, mirror = 0.f, emit = 0.f;
+		p.get("diffuse_reflect", diffuse);
+		p.get("transparency", transparency);
+		p.get("translucency", translucency);
+		p.get("specular_reflect", mirror);
+		p.get("emit", emit);
+		bool fresnel = false;
+		p.get("fresnel_effect", fresnel);
+		std::string brdf;
+		if(mirror > 0.00001f || transparency > 0.00001f || translucency > 0.00001f || fresnel)
+		{
+			log.error("Material '" + name + "': specular / transparent / translucent / Fresnel shinydiffuse components are not supported by the GPU core yet");
+			return false;
+		}
+		if(p.get("diffuse_brdf", brdf) && brdf == "oren_nayar")
+		{
+			log.error("Material '" + name + "': Oren-Nayar diffuse BRDF is not supported by the GPU core yet");
+			return false;
+		}
+		std::string shader;
+		if(p.get("diffuse_shader", shader) || p.get("mirror_color_shader", shader) || p.get("bump_shader", shader))
+			log.warning("Material '" + name + "': shader nodes / textures are not evaluated by the GPU core yet; using the plain diffuse colour");
+		m.type = MAT_SHINYDIFFUSE;
+		for(int k = 0; k < 3; ++k) m.diffuse[k] = col[k];
+		for(int k = 0; k < 3; ++k) m.emit[k] = emit * col[k];     // emit_color_(emit_strength * diffuse_color)
+		if(emit > 0.f) m.bsdf_flags |= B_EMIT;
+		const float acc = 1.f;
+		if(diffuse * acc > 0.00001f)
+		{
+			m.bsdf_flags |= B_DIFFUSE | B_REFLECT;
+			m.c_flags[m.n_bsdf] = B_DIFFUSE | B_REFLECT;
+			m.c_index[m.n_bsdf] = 3;
+			++m.n_bsdf;
+			m.comp[3] = diffuse;
+		}
+		if(p.get("receive_shadows", b)) m.receive_shadows = b ? 1 : 0;
+		if(p.get("flat_material", b)) m.flat = b ? 1 : 0;
+	}
+	else if(type == "light_mat")
+	{
+		float col[4] = {1.f, 1.f, 1.f, 1.f};
+		double power = 1.0;
+		bool ds = false;
+		p.getColor("color", col);
+		p.get("power", power);
+		p.get("double_sided", ds);
+		m.type = MAT_LIGHT;
+		m.bsdf_flags = B_EMIT;
+		for(int k = 0; k < 3; ++k) m.emit[k] = static_cast<float>(power) * col[k];
+		m.double_sided = ds ? 1 : 0;
+	}
+	else
+	{
+		log.error("Scene: material type '" + type + "' is not supported by the GPU core");
+		return false;
+	}
+	materials[name] = m;
+	material_index[name] = (int)material_order.size();
+	material_order.push_back(name);
+	return true;
+}
+
+// light_point.cc:28-35 + 104-132, light_area.cc:33-53 + 168-204
+bool Scene::createLight(const std::string &name, const ParamMap &p)
+{
+	std::string type;
+	p.get("type", type);
+	DevLight L{};
+	float col[4] = {1.f, 1.f, 1.f, 1.f};
+	float power = 1.f;
+	bool enabled = true, cast = true, photon_only = false;
+	p.getColor("color", col);
+	p.get("power", power);
+	p.get("light_enabled", enabled);
+	p.get("cast_shadows", cast);
+	p.get("photon_only", photon_only);
+	L.cast_shadows = cast ? 1 : 0;
+	if(type == "pointlight")
+	{
+		float from[3] = {0.f, 0.f, 0.f};
+		p.getVec("from", from);
+		L.type = LIGHT_POINT;
+		for(int k = 0; k < 3; ++k) { L.pos[k] = from[k]; L.color[k] = power * col[k]; }
+		L.samples = 1;
+		L.inv_samples = 1.f;
+		L.nee_count = 1;
+	}
+	else if(type == "arealight")
+	{
+		float corner[3] = {0, 0, 0}, p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+		int samples = 4;
+		p.getVec("corner", corner);
+		p.getVec("point1", p1);
+		p.getVec("point2", p2);
+		p.get("samples", samples);
+		std::string object_name;
+		if(p.get("object_name", object_name) && !object_name.empty())
+			log.warning("Light '" + name + "': area light geometry objects are rendered as ordinary meshes by the GPU core");
+		L.type = LIGHT_AREA;
+		const F3 c = f3(corner), tx = sub(f3(p1), c), ty = sub(f3(p2), c);
+		F3 fn = crs(ty, tx);
+		const float pi_f = static_cast<float>(hm::num_pi);
+		for(int k = 0; k < 3; ++k) L.color[k] = pi_f * (power * col[k]);
+		L.area = normLen(fn);
+		const F3 c2 = add(c, tx), c3 = add(c, add(tx, ty)), c4 = add(c, ty);
+		put(L.pos, c);
+		put(L.to_x, tx);
+		put(L.to_y, ty);
+		put(L.fnormal, fn);
+		put(L.c2, c2);
+		put(L.c3, c3);
+		put(L.c4, c4);
+		// integrator_montecarlo.cc:396: ceilf(nSamples * aa_light_sample_multiplier(1))
+		L.samples = (int)std::ceil((float)samples * 1.f);
+		if(L.samples < 1) L.samples = 1;
+		L.inv_samples = 1.f / (float)L.samples;
+		L.nee_count = 2 * (uint32_t)L.samples;
+	}
+	else
+	{
+		log.error("Scene: light type '" + type + "' is not supported by the GPU core");
+		return false;
+	}
+	if(!enabled || photon_only) { log.verbose("Light '" + name + "' disabled / photon-only: not used by the integrators"); return true; }
+	lights[name] = L;
+	return true;
+}
+
+bool Scene::createCamera(const std::string &name, const ParamMap &p)
+{
+	std::string type;
+	p.get("type", type);
+	if(type != "perspective") { log.error("Scene: camera type '" + type + "' is not supported by the GPU core"); return false; }
+	CameraDesc c;
+	p.getVec("from", c.from);
+	p.getVec("to", c.to);
+	p.getVec("up", c.up);
+	p.get("resx", c.resx);
+	p.get("resy", c.resy);
+	p.get("focal", c.focal);
+	p.get("aperture", c.aperture);
+	p.get("aspect_ratio", c.aspect);
+	p.get("nearClip", c.near_clip);
+	p.get("farClip", c.far_clip);
+	if(c.aperture != 0.f) { log.error("Camera '" + name + "': depth of field (aperture != 0) is not supported by the GPU core yet"); return false; }
+	cameras[name] = c;
+	return true;
+}
+
+bool Scene::createBackground(const std::string &name, const ParamMap &p)
+{
+	std::string type;
+	p.get("type", type);
+	if(type != "constant") { log.error("Scene: background type '" + type + "' is not supported by the GPU core"); return false; }
+	float col[4] = {0.f, 0.f, 0.f, 1.f};
+	float power = 1.f;
+	bool ibl = false;
+	p.getColor("color", col);
+	p.get("power", power);
+	p.get("ibl", ibl);
+	if(ibl) log.warning("Background '" + name + "': image-based lighting is not supported by the GPU core; ignored");
+	backgrounds[name] = {power * col[0], power * col[1], power * col[2]};   // background_constant.cc:56
+	return true;
+}
+
+bool Scene::createIntegrator(const std::string &name, const ParamMap &p)
+{
+	std::string type;
+	p.get("type", type);
+	if(type != "directlighting" && type != "pathtracing")
+	{
+		log.error("Scene: integrator type '" + type + "' is not supported by the GPU core (directlighting, pathtracing)");
+		return false;
+	}
+	integrators[name] = p;
+	return true;
+}
+
+bool Scene::createRenderView(const std::string &name, const ParamMap &p)
+{
+	std::string cam;
+	p.get("camera_name", cam);
+	views[name] = cam;
+	return true;
+}
+
+// scene.cc:528-644 + imagefilm.cc:48-127
+bool Scene::setupRender(const ParamMap &p)
+{
+	RenderSetup s;
+	if(!p.get("integrator_name", s.integrator_name)) { log.error("Scene: Specify an Integrator!!"); return false; }
+	if(!integrators.count(s.integrator_name)) { log.error("Scene: Specify an _existing_ Integrator!!"); return false; }
+	std::string vol;
+	if(p.get("volintegrator_name", vol)) log.warning("Scene: volume integrators are not supported by the GPU core; ignored");
+	if(p.get("background_name", s.background_name) && !backgrounds.count(s.background_name))
+		log.error("Scene: please specify an _existing_ Background!!");
+	p.get("AA_passes", s.aa_passes);
+	p.get("AA_minsamples", s.aa_samples);
+	p.get("AA_clamp_samples", s.clamp_samples);
+	p.get("threads", s.threads);
+	p.get("adv_auto_shadow_bias_enabled", s.shadow_bias_auto);
+	p.get("adv_shadow_bias_value", s.shadow_bias);
+	p.get("adv_auto_min_raydist_enabled", s.ray_min_dist_auto);
+	p.get("adv_min_raydist_value", s.ray_min_dist);
+	p.get("adv_base_sampling_offset", s.base_sampling_offset);
+	p.get("adv_computer_node", s.computer_node);
+	p.get("scene_accelerator", s.accelerator);
+	p.get("AA_pixelwidth", s.aa_pixelwidth);
+	p.get("width", s.width);
+	p.get("height", s.height);
+	p.get("xstart", s.xstart);
+	p.get("ystart", s.ystart);
+	p.get("filter_type", s.filter);
+	p.get("tile_size", s.tile_size);
+	p.get("tiles_order", s.tiles_order);
+	if(s.accelerator != "yafaray-kdtree-original" && s.accelerator != "yafaray-kdtree-multi-thread" && s.accelerator != "yafaray-simpletest")
+		log.warning("Accelerator type '" + s.accelerator + "' could not be created, using the GPU BVH instead.");  // accelerator.cc:47-51
+	if(s.aa_passes > 1) log.error("Scene: AA_passes > 1 (adaptive anti-aliasing) is not supported by the GPU core yet; rendering the first pass only");
+	if(s.xstart != 0 || s.ystart != 0) { log.error("Scene: cropped films (xstart/ystart != 0) are not supported by the GPU core yet"); return false; }
+	if(s.filter != "box" && s.filter != "gauss" && s.filter != "mitchell" && s.filter != "lanczos")
+	{
+		log.warning("ImageFilm: No AA filter defined defaulting to Box!");
+		s.filter = "box";
+	}
+	if(s.tile_size < 1) s.tile_size = 32;
+	s.aa_samples = std::max(1, s.aa_samples);
+	s.valid = true;
+	setup = s;
+	return true;
+}
+
+bool Scene::buildAccelerator()
+{
+	// scene.cc:1032-1060 updateObjects: gather visible, non-base mesh primitives
+	std::vector<float> verts;
+	std::vector<int> tris, tri_mat;
+	for(const std::string &name : object_order)
+	{
+		const MeshObject &o = objects[name];
+		if(o.is_base || o.visibility == "invisible") continue;
+		const int v0 = (int)(verts.size() / 3);
+		verts.insert(verts.end(), o.verts.begin(), o.verts.end());
+		for(size_t t = 0; t < o.tri_mat.size(); ++t)
+		{
+			tris.push_back(o.tris[3 * t] + v0);
+			tris.push_back(o.tris[3 * t + 1] + v0);
+			tris.push_back(o.tris[3 * t + 2] + v0);
+			tri_mat.push_back(o.tri_mat[t]);
+		}
+	}
+	const auto t0 = std::chrono::steady_clock::now();
+	HostScene hs;
+	hs.n_prims = (int)tri_mat.size();
+	BvhInput in{verts.data(), tris.data(), hs.n_prims};
+	hs.bvh = buildBvh(in, 4, 8);
+	// primitive_triangle.cc:87-95 geometric normal; material index per primitive
+	hs.prim_ng.resize(4 * (size_t)hs.n_prims);
+	for(int t = 0; t < hs.n_prims; ++t)
+	{
+		const F3 a = f3(&verts[3 * (size_t)tris[3 * t]]), b = f3(&verts[3 * (size_t)tris[3 * t + 1]]), c = f3(&verts[3 * (size_t)tris[3 * t + 2]]);
+		const F3 n = nrm(crs(sub(b, a), sub(c, a)));
+		float matf;
+		std::memcpy(&matf, &tri_mat[t], 4);
+		put(&hs.prim_ng[4 * (size_t)t], n, matf);
+	}
+	for(const std::string &mn : material_order) hs.mats.push_back(materials[mn]);
+	if(hs.mats.empty()) hs.mats.push_back(DevMaterial{});
+	for(auto &kv : lights) hs.lights.push_back(kv.second);
+	uint32_t base = 0;
+	for(DevLight &L : hs.lights) { L.nee_base = base; base += L.nee_count; }
+	if(!gpu()->upload(hs)) return false;
+	const auto t1 = std::chrono::steady_clock::now();
+	stats.build_seconds = std::chrono::duration<double>(t1 - t0).count();
+	std::ostringstream os;
+	os << "Accelerator: GPU BVH2 built over " << hs.n_prims << " triangles: " << hs.bvh.n_nodes << " nodes, depth " << hs.bvh.depth
+	   << ", max leaf " << hs.bvh.max_leaf << " (" << stats.build_seconds << " s)";
+	log.info(os.str());
+	geometry_dirty = false;
+	return true;
+}
+
+// scene.cc:203-263 Scene::render + integrator_tiled.cc:97-233 (single AA pass)
+bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, void *progress_data, bool quiet)
+{
+	if(!setup.valid) { log.error("Scene: No ImageFilm present, bailing out..."); return false; }
+	if(views.empty()) { log.error("Scene: no render view defined"); return false; }
+	canceled = false;
+	if(geometry_dirty && !buildAccelerator()) return false;
+	const RenderSetup &s = setup;
+	const ParamMap &ip = integrators[s.integrator_name];
+	std::string itype;
+	ip.get("type", itype);
+	for(const auto &view : views)
+	{
+		auto cit = cameras.find(view.second);
+		if(cit == cameras.end()) { log.error("RenderView '" + view.first + "': Camera not found in the scene."); return false; }
+		const CameraDesc &c = cit->second;
+		RenderParams rp{};
+		DevScene &S = rp.scene;
+		// camera.cc:51-71 + camera_perspective.cc:28-69
+		const F3 pos = f3(c.from), look = f3(c.to), up = f3(c.up);
+		const float aspect_ratio = c.aspect * (float)c.resy / (float)c.resx;
+		F3 cam_y = sub(up, pos), cam_z = sub(look, pos);
+		F3 cam_x = crs(cam_z, cam_y);
+		cam_y = crs(cam_z, cam_x);
+		cam_x = nrm(cam_x);
+		cam_y = nrm(cam_y);
+		cam_z = nrm(cam_z);
+		F3 vright = cam_x, vup = mul(cam_y, aspect_ratio);
+		const F3 vto = sub(mul(cam_z, c.focal), mul(add(vup, vright), static_cast<float>(0.5)));
+		vup = {vup.x / (float)c.resy, vup.y / (float)c.resy, vup.z / (float)c.resy};
+		vright = {vright.x / (float)c.resx, vright.y / (float)c.resx, vright.z / (float)c.resx};
+		put(S.cam.pos, pos);
+		put(S.cam.vright, vright);
+		put(S.cam.vup, vup);
+		put(S.cam.vto, vto);
+		put(S.cam.cam_z, cam_z);
+		put(S.cam.near_p, add(pos, mul(cam_z, c.near_clip)));
+		put(S.cam.far_p, add(pos, mul(cam_z, c.far_clip)));
+		S.cam.resx = c.resx;
+		S.cam.resy = c.resy;
+		// integrator + render parameters
+		S.integrator = (itype == "pathtracing") ? INT_PATH : INT_DIRECT;
+		S.width = s.width;
+		S.height = s.height;
+		S.spp = s.aa_samples;
+		S.tile = s.tile_size;
+		int bounces = 3, path_samples = 32, rr_min = 0;
+		std::string caustic_type;
+		ip.get("bounces", bounces);
+		ip.get("path_samples", path_samples);
+		ip.get("russian_roulette_min_bounces", rr_min);
+		S.caustic_path = 1;   // PathIntegrator ctor: CausticType::Path (integrator_path_tracer.cc:43)
+		if(ip.get("caustic_type", caustic_type))
+		{
+			if(caustic_type == "none") S.caustic_path = 0;
+			else if(caustic_type == "photon" || caustic_type == "both")
+			{
+				if(caustic_type == "photon") S.caustic_path = 0;
+				log.warning("PathIntegrator: photon caustics are not supported by the GPU core yet; ignored");
+			}
+		}
+		if(S.integrator == INT_DIRECT)
+		{
+			bool caus = false, ao = false;
+			ip.get("caustics", caus);
+			ip.get("do_AO", ao);
+			if(caus || ao) log.warning("DirectLight: caustic photons / ambient occlusion are not supported by the GPU core yet; ignored");
+		}
+		S.bounces = bounces;
+		S.path_samples = std::max(1, path_samples);
+		S.rr_min_bounces = rr_min;
+		bool bg_transp = false;
+		ip.get("bg_transp", bg_transp);
+		S.bg_transp = bg_transp ? 1 : 0;
+		S.has_bg = 0;
+		if(!s.background_name.empty() && backgrounds.count(s.background_name))
+		{
+			const auto &bgc = backgrounds[s.background_name];
+			S.has_bg = 1;
+			for(int k = 0; k < 3; ++k) S.bg[k] = bgc[k];
+		}
+		S.shadow_bias_auto = s.shadow_bias_auto ? 1 : 0;
+		S.shadow_bias = s.shadow_bias;
+		S.ray_min_dist_auto = s.ray_min_dist_auto ? 1 : 0;
+		S.ray_min_dist = s.ray_min_dist;
+		S.base_offset = (uint32_t)s.base_sampling_offset;
+		S.clamp_samples = s.clamp_samples;
+		S.rr_seed = 0;
+		uint32_t nee_all = 0, nee_max_one = 1;
+		for(auto &kv : lights)
+		{
+			nee_all += kv.second.nee_count;
+			nee_max_one = std::max(nee_max_one, kv.second.nee_count);
+		}
+		S.nee_all_count = (int)nee_all;
+		S.nee_k = (int)std::max(nee_all, nee_max_one);
+		if(S.integrator == INT_PATH && S.path_samples > 4095) { log.error("PathIntegrator: path_samples > 4095 unsupported"); return false; }
+		if(S.integrator == INT_PATH && 4 * S.bounces + 4 >= 50)
+			log.warning("PathIntegrator: bounces > 11 use Halton dimensions >= 50 (reference: racy FastRandom); those dimensions return 0 here");
+		// film (imagefilm.cc:129-173)
+		DevFilm &F = rp.film;
+		float filterw = static_cast<float>(s.aa_pixelwidth * 0.5);
+		float (*ff)(float, float) = hm::filterBox;
+		if(s.filter == "mitchell") { ff = hm::filterMitchell; filterw *= 2.6f; }
+		else if(s.filter == "lanczos") ff = hm::filterLanczos;
+		else if(s.filter == "gauss") { ff = hm::filterGauss; filterw *= 2.f; }
+		filterw = std::min(std::max(0.501f, filterw), 0.5f * 8);
+		const float scale = 1.f / 16.f;
+		for(int y = 0; y < 16; ++y)
+			for(int x = 0; x < 16; ++x) F.table[y * 16 + x] = ff((x + .5f) * scale, (y + .5f) * scale);
+		F.filterw = filterw;
+		F.table_scale = static_cast<float>(0.9999 * 16 / filterw);
+		F.reach_fwd = std::max(0, (int)((double)filterw + (.5 - 1.4e-11)));
+		F.reach_back = std::max(0, -(int)(-(double)filterw + (.5 - 1.4e-11)));
+		F.width = s.width;
+		F.height = s.height;
+		F.spp = s.aa_samples;
+		F.tile = s.tile_size;
+		rp.shard_rank = shard_rank;
+		rp.shard_world = std::max(1, shard_world);
+		rp.chunk_slots = chunk_slots;
+		rp.profile = profile_kernels;
+		film_w = s.width;
+		film_h = s.height;
+		if(!quiet)
+		{
+			std::ostringstream os;
+			os << itype << ": " << s.width << "x" << s.height << " x " << s.aa_samples << " spp, filter " << s.filter << " " << s.aa_pixelwidth
+			   << ", tile " << s.tile_size;
+			if(S.integrator == INT_PATH) os << ", bounces " << S.bounces << ", path_samples " << S.path_samples << ", rr_min " << S.rr_min_bounces;
+			log.params(os.str());
+			if(cb.notify_view) cb.notify_view(view.first.c_str(), cb.notify_view_data);
+			if(cb.notify_layer) cb.notify_layer("combined", "Combined", s.width, s.height, 4, cb.notify_layer_data);
+			if(progress) progress(s.width * s.height, 0, "Rendering...", progress_data);
+		}
+		if(!gpu()->render(rp, &canceled)) return false;
+		const double build = stats.build_seconds;
+		stats = gpu()->stats();
+		stats.build_seconds = build;
+		if(quiet) continue;
+		if(!gpu()->download(film_rgba, film_weights, s.width, s.height)) return false;
+		{
+			std::ostringstream os;
+			os << "Render: " << stats.samples << " samples, " << stats.closest_rays << " closest + " << stats.shadow_rays
+			   << " shadow rays in " << stats.render_seconds << " s";
+			log.info(os.str());
+		}
+		// imagefilm.cc:489-568 finishArea per tile (linear order) then :570-670 flush
+		const auto owned = gpu()->ownedRows();
+		auto ownedRow = [&](int y) {
+			for(const auto &r : owned) if(y >= r.first && y < r.second) return true;
+			return false;
+		};
+		if(cb.put_pixel || cb.flush_area)
+		{
+			int area_id = 0;
+			const int ts = s.tile_size;
+			for(int ty = 0; ty < s.height; ty += ts)
+			{
+				for(int tx = 0; tx < s.width; tx += ts, ++area_id)
+				{
+					const int x1 = std::min(s.width, tx + ts), y1 = std::min(s.height, ty + ts);
+					if(!ownedRow(ty)) continue;
+					if(cb.put_pixel)
+						for(int y = ty; y < y1; ++y)
+							for(int x = tx; x < x1; ++x)
+							{
+								const float *px = &film_rgba[4 * ((size_t)y * s.width + x)];
+								cb.put_pixel(view.first.c_str(), "combined", x, y, px[0], px[1], px[2], px[3], cb.put_pixel_data);
+							}
+					if(cb.flush_area) cb.flush_area(view.first.c_str(), area_id, tx, ty, x1, y1, cb.flush_area_data);
+				}
+			}
+		}
+		if(cb.put_pixel)
+			for(int y = 0; y < s.height; ++y)
+			{
+				if(!ownedRow(y)) continue;
+				for(int x = 0; x < s.width; ++x)
+				{
+					const float *px = &film_rgba[4 * ((size_t)y * s.width + x)];
+					cb.put_pixel(view.first.c_str(), "combined", x, y, px[0], px[1], px[2], px[3], cb.put_pixel_data);
+				}
+			}
+		if(cb.flush) cb.flush(view.first.c_str(), cb.flush_data);
+		if(progress) progress(s.width * s.height, s.width * s.height, "Rendering finished", progress_data);
+	}
+	return true;
+}
+
+} // namespace yafamd

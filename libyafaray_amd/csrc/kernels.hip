@@ -1,0 +1,1254 @@
+// HIP kernels of the MI355X path-tracing core (gfx950, wave64).
+//
+// Wavefront pipeline for one chunk of camera samples (render.cc drives it):
+//
+//   k_camera  -> [ k_trace -> k_shade ] x iterations -> (all chunks) -> k_film
+//
+//   k_camera : one camera sample per slot — TiledIntegrator::renderTile sample loop
+//              (integrator_tiled.cc:288-361) + PerspectiveCamera::shootRay
+//              (camera_perspective.cc:128-146).
+//   k_trace  : closest-hit rays of the active list + any-hit shadow rays in one launch —
+//              Accelerator::intersect / isShadowed (accelerator.cc:55-78) over a BVH2;
+//              AcceleratorKdTree::intersect / intersectS semantics (accelerator_kdtree.cc:726-746,
+//              851-873) and TrianglePrimitive::intersect (primitive_triangle.cc:44-71).
+//              Small scenes are staged into LDS per workgroup; the per-lane traversal stack
+//              lives in LDS ([level][lane] layout: conflict-free).
+//   k_shade  : connects the previous vertex's next-event estimate with the shadow results, then
+//              shades the new hit: emission, MC light estimation (integrator_montecarlo.cc:54-408),
+//              BSDF sampling (material_shiny_diffuse.cc:244-327), Russian roulette, and appends
+//              the next extension ray / shadow rays with wave-ballot compaction
+//              (PathIntegrator::integrate integrator_path_tracer.cc:120-290,
+//               DirectLightIntegrator::integrate integrator_direct_light.cc:97-144).
+//   k_film   : ImageFilm::addSample (imagefilm.cc:680-733) as a per-destination-pixel gather
+//              that replays the reference's single-thread linear-tile splat order, so every film
+//              sum is bit-identical without a mutex or atomics; then flush normalisation
+//              (imagefilm.cc:590-617, color.h:554-558).
+//
+// Compiled with -ffp-contract=off: every float expression keeps the reference's order.
+
+#include <hip/hip_runtime.h>
+#include "devmath.h"
+#include "devscene.h"
+
+namespace yafamd
+{
+
+constexpr int kTraceBlock = 128;
+constexpr int kShadeBlock = 256;
+
+enum : uint32_t
+{
+	ST_CAMERA = 0,       // closest ray = camera ray; hit is v0
+	ST_FIRST = 1,        // ray = first path segment of the current subpath; hit is v1
+	ST_BOUNCE = 2,       // ray = bounce `depth`; hit is v_{depth+1}
+	ST_NORAY = 3         // no ray this iteration (only a pending connect, then an action)
+};
+// flags word
+enum : uint32_t
+{
+	F_MATFLAGS = 0xffffu,        // mat_bsd_fs captured at the first path vertex
+	F_SAMPLED = 1u << 16,        // s.sampled_flags_ != None at the first segment
+	F_CAUSTIC = 1u << 17,
+	F_PEND_V0 = 1u << 18,        // pending: estimateAllDirectLight at v0
+	F_PEND_ONE = 1u << 19,       // pending: estimateOneDirectLight at v_k
+	F_PEND_EMIT = 1u << 20,      // pending emission add
+	F_V0_DIFFUSE = 1u << 21,     // v0 had the Diffuse flag (NEE estimated there)
+	F_END_SUBPATH = 1u << 22,    // after the connect: the current subpath ends
+	F_LNUM_SHIFT = 24            // light picked by estimateOneDirectLight (8 bits)
+};
+
+__device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ V3 xyz(const float4 &a) { return v3(a.x, a.y, a.z); }
+__device__ __forceinline__ C3 rgb(const float4 &a) { return C3{a.x, a.y, a.z}; }
+__device__ __forceinline__ float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
+__device__ __forceinline__ float4 f4(C3 c, float w) { return make_float4(c.r, c.g, c.b, w); }
+
+__device__ __forceinline__ int laneId() { return __lane_id(); }
+
+// Wave-level append: returns this lane's index in the queue (valid only where `want`).
+__device__ __forceinline__ uint32_t waveAppend(bool want, uint32_t *counter)
+{
+	const uint64_t mask = __ballot(want);
+	if(mask == 0) return 0;
+	const int leader = __ffsll((unsigned long long)mask) - 1;
+	uint32_t base = 0;
+	if(laneId() == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+	base = __shfl(base, leader);
+	const uint64_t below = mask & ((1ull << laneId()) - 1ull);
+	return base + (uint32_t)__popcll(below);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_camera
+// ---------------------------------------------------------------------------------------------
+struct SampleCoord { int x, y, s; };
+
+// sample id (frame-local enumeration over jobs) -> pixel + sample index
+__device__ SampleCoord sampleCoord(const DevJob *jobs, int n_jobs, int width, int tile, int spp, uint64_t sid)
+{
+	int j = 0;
+	while(j + 1 < n_jobs && jobs[j + 1].sample_base <= sid) ++j;
+	const DevJob job = jobs[j];
+	const uint64_t local = sid - job.sample_base;
+	const uint32_t pix = (uint32_t)(local / (uint64_t)spp);
+	const int s = (int)(local % (uint64_t)spp);
+	const int bh = job.y1 - job.y0;
+	const uint32_t per_tile = (uint32_t)(tile * bh);
+	const int tx = (int)(pix / per_tile);
+	const int tw = min(tile, width - tx * tile);
+	const uint32_t l = pix - (uint32_t)tx * per_tile;
+	SampleCoord c;
+	c.x = tx * tile + (int)(l % (uint32_t)tw);
+	c.y = job.y0 + (int)(l / (uint32_t)tw);
+	c.s = s;
+	return c;
+}
+
+__global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueues Q, DevCounters *cnt,
+                                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n)
+{
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const SampleCoord sc = sampleCoord(jobs, n_jobs, S.width, S.tile, S.spp, chunk_base + (uint64_t)i);
+	// integrator_tiled.cc:313-335
+	const uint32_t offset = fnv32((uint32_t)sc.y * fnv32((uint32_t)sc.x));
+	float dx = 0.5f, dy = 0.5f;
+	if(S.spp > 1)
+	{
+		const float d_1 = 1.f / (float)S.spp;
+		dx = (0.5f + (float)sc.s) * d_1;
+		dy = riLp((uint32_t)sc.s + offset);
+	}
+	const float px = (float)sc.x + dx, py = (float)sc.y + dy;
+	// camera_perspective.cc:128-146, plane.h:37-40
+	const DevCamera &c = S.cam;
+	const V3 pos = v3(c.pos[0], c.pos[1], c.pos[2]);
+	V3 dir = v3(c.vright[0], c.vright[1], c.vright[2]) * px + v3(c.vup[0], c.vup[1], c.vup[2]) * py + v3(c.vto[0], c.vto[1], c.vto[2]);
+	dir = normalize(dir);
+	const V3 cz = v3(c.cam_z[0], c.cam_z[1], c.cam_z[2]);
+	const float tmin = dot(cz, v3(c.near_p[0], c.near_p[1], c.near_p[2]) - pos) / dot(dir, cz);
+	const float tmax = dot(cz, v3(c.far_p[0], c.far_p[1], c.far_p[2]) - pos) / dot(dir, cz);
+	Q.slot[i] = i;
+	Q.ray_o[i] = f4(pos, tmin);
+	Q.ray_d[i] = f4(dir, tmax);
+	P.stage[i] = ST_CAMERA;
+	P.flags[i] = 0;
+	P.w[i] = 0.f;
+	P.col[i] = make_float4(0.f, 0.f, 0.f, 1.f);
+	P.pcol[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+	P.pix[i] = make_uint2(offset, S.base_offset + (uint32_t)sc.s);
+	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
+	// output is matched statistically — integrator_tiled.cc:272)
+	const uint32_t seed = fnv32((uint32_t)(chunk_base + (uint64_t)i) ^ S.rr_seed) + 123u;
+	P.rng[i] = make_uint2(30903u, seed);
+	if(i == 0) { cnt->n_active = (uint32_t)n; cnt->n_shadow = 0; }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_trace: BVH2 traversal
+// ---------------------------------------------------------------------------------------------
+struct TraceCtx
+{
+	const float4 *nodes;
+	const float4 *tris;
+	int *stack;     // LDS, [level * kTraceBlock + lane]
+};
+
+__device__ __forceinline__ void boxPair(const float4 &n0, const float4 &n1, const float4 &n2, V3 o, V3 id,
+                                        float t0, float t1, bool &h0, bool &h1, float &tn0, float &tn1)
+{
+	// child 0
+	float ax = (n0.x - o.x) * id.x, bx = (n0.y - o.x) * id.x;
+	float ay = (n0.z - o.y) * id.y, by = (n0.w - o.y) * id.y;
+	float az = (n2.x - o.z) * id.z, bz = (n2.y - o.z) * id.z;
+	float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), t0));
+	float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), t1));
+	h0 = lo <= hi;
+	tn0 = lo;
+	ax = (n1.x - o.x) * id.x; bx = (n1.y - o.x) * id.x;
+	ay = (n1.z - o.y) * id.y; by = (n1.w - o.y) * id.y;
+	az = (n2.z - o.z) * id.z; bz = (n2.w - o.z) * id.z;
+	lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), t0));
+	hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), t1));
+	h1 = lo <= hi;
+	tn1 = lo;
+}
+
+// primitive_triangle.cc:44-71.  Returns t or -1.
+__device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const float4 &c, V3 o, V3 d)
+{
+	const V3 v0 = xyz(a), e1 = xyz(b), e2 = xyz(c);
+	const float eps = a.w;
+	const V3 pvec = cross(d, e2);
+	const float det = dot(e1, pvec);
+	if(det > -eps && det < eps) return -1.f;
+	const float inv_det = 1.f / det;
+	const V3 tvec = o - v0;
+	const float u = dot(tvec, pvec) * inv_det;
+	if(u < 0.f || u > 1.f) return -1.f;
+	const V3 qvec = cross(tvec, e1);
+	const float v = dot(d, qvec) * inv_det;
+	if((v < 0.f) || ((u + v) > 1.f)) return -1.f;
+	const float t = dot(e2, qvec) * inv_det;
+	if(t < eps) return -1.f;
+	return t;
+}
+
+// Closest hit with t in [tmin, tmax) (ties -> lower primitive index), or any hit with t in
+// [0, tmax).  Box tests are conservative (boxes padded at build time + a relative slack), so
+// culling never drops a hit the exhaustive reference semantics would return.
+template<bool ANY>
+__device__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
+                         uint32_t &visits, uint32_t &tests)
+{
+	const int lane = threadIdx.x;
+	V3 dd = d;
+	if(fabsf(dd.x) < 1e-20f) dd.x = copysignf(1e-20f, dd.x);
+	if(fabsf(dd.y) < 1e-20f) dd.y = copysignf(1e-20f, dd.y);
+	if(fabsf(dd.z) < 1e-20f) dd.z = copysignf(1e-20f, dd.z);
+	const V3 id = v3(1.f / dd.x, 1.f / dd.y, 1.f / dd.z);
+	const float box_t0 = ANY ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
+	t_best = tmax;
+	prim_best = -1;
+	int sp = 0;
+	int node = 0;
+	for(;;)
+	{
+		++visits;
+		const float4 *np = C.nodes + 4 * node;
+		const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
+		bool h0, h1;
+		float tn0, tn1;
+		boxPair(n0, n1, n2, o, id, box_t0, slack_t, h0, h1, tn0, tn1);
+		const int c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
+		const int k0 = __float_as_int(n3.z), k1 = __float_as_int(n3.w);
+		int next = -1;
+		// leaves are tested right away; inner children are descended nearest-first
+#pragma unroll
+		for(int side = 0; side < 2; ++side)
+		{
+			const bool h = side ? h1 : h0;
+			const int c = side ? c1 : c0;
+			const int k = side ? k1 : k0;
+			if(!h || c >= 0 || k == 0) continue;
+			const int start = ~c;
+			for(int q = start; q < start + k; ++q)
+			{
+				++tests;
+				const float4 *tp = C.tris + 3 * q;
+				const float4 ta = tp[0], tb = tp[1], tc = tp[2];
+				const float t = triTest(ta, tb, tc, o, d);
+				if(t == -1.f) continue;
+				const int prim = __float_as_int(tb.w);
+				if(ANY)
+				{
+					if(t < tmax && t >= 0.f) { t_best = t; prim_best = prim; return true; }
+				}
+				else if(t >= tmin && (t < t_best || (t == t_best && prim_best >= 0 && prim < prim_best)))
+				{
+					t_best = t;
+					prim_best = prim;
+				}
+			}
+		}
+		const bool i0 = h0 && c0 >= 0, i1 = h1 && c1 >= 0;
+		if(i0 && i1)
+		{
+			const bool first0 = tn0 <= tn1;
+			next = first0 ? c0 : c1;
+			C.stack[sp * kTraceBlock + lane] = first0 ? c1 : c0;
+			++sp;
+		}
+		else if(i0) next = c0;
+		else if(i1) next = c1;
+		if(next < 0)
+		{
+			if(sp == 0) break;
+			--sp;
+			next = C.stack[sp * kTraceBlock + lane];
+		}
+		node = next;
+	}
+	return prim_best >= 0;
+}
+
+template<bool LDS_SCENE>
+__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, const DevCounters *cnt,
+                                                      DevCounters *cnt_next, DevPaths P, DevStats *stats, int stack_depth)
+{
+	// the next shade appends into cnt_next: reset it here (it was consumed by the previous shade)
+	if(blockIdx.x == 0 && threadIdx.x == 0) { cnt_next->n_active = 0; cnt_next->n_shadow = 0; }
+	extern __shared__ float4 smem[];
+	int *stack = reinterpret_cast<int *>(smem);
+	TraceCtx C;
+	C.stack = stack;
+	if(LDS_SCENE)
+	{
+		float4 *lds_nodes = smem + (stack_depth * kTraceBlock) / 4;
+		float4 *lds_tris = lds_nodes + 4 * S.n_nodes;
+		for(int k = threadIdx.x; k < 4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = S.nodes[k];
+		for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = S.tris[k];
+		__syncthreads();
+		C.nodes = lds_nodes;
+		C.tris = lds_tris;
+	}
+	else
+	{
+		C.nodes = S.nodes;
+		C.tris = S.tris;
+	}
+	const uint32_t n_a = cnt->n_active, n_s = cnt->n_shadow;
+	const uint32_t total = n_a + n_s;
+	uint32_t visits = 0, tests = 0, n_closest = 0, n_shadow = 0;
+	const uint32_t stride = gridDim.x * blockDim.x;
+	// one uniform trip count per workgroup so every lane reaches the same exits
+	for(uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride)
+	{
+		const uint32_t i = base + threadIdx.x;
+		if(i < n_a)
+		{
+			const float4 od = Q.ray_o[i], dd = Q.ray_d[i];
+			if(!(dd.w != dd.w))   // NaN marks "no ray this iteration"
+			{
+				float t;
+				int prim;
+				const float tmax = (dd.w >= 0.f) ? dd.w : __builtin_huge_valf();
+				traverse<false>(C, xyz(od), xyz(dd), od.w, tmax, t, prim, visits, tests);
+				Q.hit_t[i] = t;
+				Q.hit_prim[i] = prim;
+				++n_closest;
+			}
+		}
+		else if(i < total)
+		{
+			const uint32_t k = i - n_a;
+			const float4 od = Q.sh_o[k], dd = Q.sh_d[k];
+			float t;
+			int prim;
+			const bool occ = traverse<true>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
+			P.occ[Q.sh_idx[k]] = occ ? 1 : 0;
+			++n_shadow;
+		}
+	}
+	// wave-reduced statistics (rays issued, nodes visited, triangles tested)
+	for(int off = 32; off > 0; off >>= 1)
+	{
+		visits += __shfl_down(visits, off);
+		tests += __shfl_down(tests, off);
+		n_closest += __shfl_down(n_closest, off);
+		n_shadow += __shfl_down(n_shadow, off);
+	}
+	if(laneId() == 0 && (visits | tests | n_closest | n_shadow))
+	{
+		atomicAdd(&stats->node_visits, (unsigned long long)visits);
+		atomicAdd(&stats->tri_tests, (unsigned long long)tests);
+		atomicAdd(&stats->closest_rays, (unsigned long long)n_closest);
+		atomicAdd(&stats->shadow_rays, (unsigned long long)n_shadow);
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_shade
+// ---------------------------------------------------------------------------------------------
+struct Surf
+{
+	V3 p, n, ng, nu, nv;
+	int mat;
+	uint32_t flags;
+};
+
+__device__ __forceinline__ Surf makeSurf(const DevScene &S, V3 o, V3 d, float t, int prim)
+{
+	// accelerator.cc:61 hit point + primitive_triangle.cc:97-176 (flat shading: N = Ng)
+	Surf s;
+	s.p = o + t * d;
+	const float4 g = S.prim_ng[prim];
+	s.ng = xyz(g);
+	s.n = s.ng;
+	coordsSystem(s.n, s.nu, s.nv);
+	s.mat = __float_as_int(g.w);
+	s.flags = S.mats[s.mat].bsdf_flags;
+	return s;
+}
+
+__device__ __forceinline__ V3 faceForward(V3 ng, V3 n, V3 wo) { return (dot(ng, wo) < 0) ? -n : n; }
+
+// material_shiny_diffuse.cc:190-228, material_simple.cc (light_mat evaluates to black)
+__device__ C3 matEval(const DevMaterial &m, const Surf &sp, V3 wo, V3 wl, uint32_t bsdfs)
+{
+	if(m.type == MAT_LIGHT) return c3(0.f);
+	const V3 n = faceForward(sp.ng, sp.n, wo);
+	if(!(bsdfs & (m.bsdf_flags & B_DIFFUSE))) return c3(0.f);
+	const float m_t = (1.f - 1.f * m.comp[0]) * (1.f - m.comp[1]);
+	if((double)dot(n, wl) < 0.0 && !m.flat) return c3(0.f);
+	const float m_d = m_t * (1.f - m.comp[2]) * m.comp[3];
+	return m_d * C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+}
+
+// material_shiny_diffuse.cc:237-242, material_simple.cc:50-55
+__device__ C3 matEmit(const DevMaterial &m, const Surf &sp, V3 wo)
+{
+	if(m.type == MAT_LIGHT)
+	{
+		if(m.double_sided) return C3{m.emit[0], m.emit[1], m.emit[2]};
+		return dot(wo, sp.n) > 0 ? C3{m.emit[0], m.emit[1], m.emit[2]} : c3(0.f);
+	}
+	return C3{m.emit[0], m.emit[1], m.emit[2]};
+}
+
+// material_shiny_diffuse.cc:107-119 (Kr = 1)
+__device__ __forceinline__ void accumulateComp(const float *c, float *a)
+{
+	a[0] = c[0] * 1.f;
+	float acc = 1.f - a[0];
+	a[1] = c[1] * acc;
+	acc *= 1.f - c[1];
+	a[2] = c[2] * acc;
+	acc *= 1.f - c[2];
+	a[3] = c[3] * acc;
+}
+
+struct BsdfSample
+{
+	float s_1, s_2, pdf;
+	uint32_t flags, sampled;
+};
+
+// material_shiny_diffuse.cc:244-327 (diffuse reflect component), material_simple.cc:42-48
+__device__ C3 matSample(const DevMaterial &m, const Surf &sp, V3 wo, V3 &wi, BsdfSample &s, float &w)
+{
+	if(m.type == MAT_LIGHT)
+	{
+		s.pdf = 0.f;
+		w = 0.f;
+		return c3(0.f);
+	}
+	const float cos_ng_wo = dot(sp.ng, wo);
+	const V3 n = faceForward(sp.ng, sp.n, wo);
+	float accum_c[4];
+	accumulateComp(m.comp, accum_c);
+	float sum = 0.f, val[4], width[4];
+	uint32_t choice[4];
+	int n_match = 0, pick = -1;
+	for(int i = 0; i < (int)m.n_bsdf; ++i)
+	{
+		if((s.flags & m.c_flags[i]) == m.c_flags[i])
+		{
+			width[n_match] = accum_c[m.c_index[i]];
+			sum += width[n_match];
+			choice[n_match] = m.c_flags[i];
+			val[n_match] = sum;
+			++n_match;
+		}
+	}
+	if(!n_match || (double)sum < 0.00001) { s.sampled = B_NONE; s.pdf = 0.f; return c3(1.f); }
+	const float inv_sum = 1.f / sum;
+	for(int i = 0; i < n_match; ++i)
+	{
+		val[i] *= inv_sum;
+		width[i] *= inv_sum;
+		if((s.s_1 <= val[i]) && (pick < 0)) pick = i;
+	}
+	if(pick < 0) pick = n_match - 1;
+	float s_1;
+	if(pick > 0) s_1 = (s.s_1 - val[pick - 1]) / width[pick];
+	else s_1 = s.s_1 / width[pick];
+	C3 scolor = c3(0.f);
+	wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
+	if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+	s.pdf = fabsf(dot(wi, n)) * width[pick];
+	s.sampled = choice[pick];
+	w = fabsf(dot(wi, sp.n)) / (s.pdf * 0.99f + 0.01f);
+	const float alpha = 1.f;
+	w = w * (alpha) + 1.f * (1.f - alpha);
+	return scolor;
+}
+
+// material_shiny_diffuse.cc:329-366
+__device__ float matPdf(const DevMaterial &m, const Surf &sp, V3 wo, V3 wi, uint32_t bsdfs)
+{
+	if(m.type == MAT_LIGHT) return 0.f;
+	if(!(bsdfs & B_DIFFUSE)) return 0.f;
+	float pdf = 0.f;
+	const V3 n = faceForward(sp.ng, sp.n, wo);
+	float accum_c[4];
+	accumulateComp(m.comp, accum_c);
+	float sum = 0.f;
+	int n_match = 0;
+	for(int i = 0; i < (int)m.n_bsdf; ++i)
+	{
+		if(bsdfs & m.c_flags[i])
+		{
+			const float width = accum_c[m.c_index[i]];
+			sum += width;
+			if(m.c_flags[i] == (B_DIFFUSE | B_REFLECT)) pdf += fabsf(dot(wi, n)) * width;
+			++n_match;
+		}
+	}
+	if(!n_match || (double)sum < 0.00001) return 0.f;
+	return pdf / sum;
+}
+
+__device__ __forceinline__ V3 lv(const float *a) { return v3(a[0], a[1], a[2]); }
+
+// light_area.cc:116-135
+__device__ __forceinline__ bool areaTri(V3 a, V3 b, V3 c, V3 o, V3 d, float &t)
+{
+	const V3 edge_1 = b - a;
+	const V3 edge_2 = c - a;
+	const V3 pvec = cross(d, edge_2);
+	const float det = dot(edge_1, pvec);
+	if(det == 0.f) return false;
+	const float inv_det = 1.f / det;
+	const V3 tvec = o - a;
+	const float u = dot(tvec, pvec) * inv_det;
+	if(u < 0.f || u > 1.f) return false;
+	const V3 qvec = cross(tvec, edge_1);
+	const float v = dot(d, qvec) * inv_det;
+	if((v < 0.f) || ((u + v) > 1.f)) return false;
+	t = dot(edge_2, qvec) * inv_det;
+	return true;
+}
+
+struct ShadeOut
+{
+	uint32_t *sh_count;
+	DevQueues Qn;
+};
+
+// Appends (or not) one shadow ray per lane — all lanes of the wave must call.
+__device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, int idx, const ShadeOut &out)
+{
+	const uint32_t k = waveAppend(want, out.sh_count);
+	if(want)
+	{
+		out.Qn.sh_o[k] = f4(o, 0.f);
+		out.Qn.sh_d[k] = f4(d, t_max);
+		out.Qn.sh_idx[k] = idx;
+	}
+}
+
+// accelerator.cc:69-78: origin moved by tmin, t_max = tmax - 2 tmin (tmax >= 0) else inf
+__device__ __forceinline__ void shadowRayOf(V3 from, V3 dir, float tmin, float tmax, V3 &o, float &t_max)
+{
+	o = from + dir * tmin;
+	t_max = (tmax >= 0.f) ? tmax - 2 * tmin : __builtin_huge_valf();
+}
+
+// Next-event estimation for one light: writes the contributions of every sample into
+// nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
+// Wave-uniform structure: `active` lanes do the work, every lane walks the same loop bounds.
+__device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
+                         uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int slot, int base,
+                         float4 *nee, uint8_t *occ, const ShadeOut &out)
+{
+	const bool cast_shadows = L.cast_shadows && m.receive_shadows;
+	const float p_len = length(sp.p);
+	const float sh_tmin = S.shadow_bias_auto ? S.shadow_bias * fmaxf(1.f, p_len) : S.shadow_bias;
+	if(L.type == LIGHT_POINT)
+	{
+		// light_point.cc:38-57 + montecarlo.cc:80-154
+		bool ok = active;
+		C3 contrib = c3(0.f);
+		V3 ldir = lv(L.pos) - sp.p;
+		const float dist_sqr = ldir.x * ldir.x + ldir.y * ldir.y + ldir.z * ldir.z;
+		const float dist = sqrtf(dist_sqr);
+		if((double)dist == 0.0) ok = false;
+		V3 so = sp.p;
+		float st = 0.f;
+		if(ok)
+		{
+			const float idist_sqr = 1.f / (dist_sqr);
+			ldir = ldir * (1.f / dist);
+			const C3 lcol = C3{L.color[0], L.color[1], L.color[2]} * idist_sqr;
+			const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
+			const C3 surf_col = matEval(m, sp, wo, ldir, B_ALL);
+			const C3 transmit = c3(1.f);
+			contrib = surf_col * lcol * angle * transmit;
+			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
+			nee[slot * S.nee_k + base] = f4(contrib, 1.f);
+		}
+		else if(active) nee[slot * S.nee_k + base] = make_float4(0.f, 0.f, 0.f, 0.f);
+		if(active) occ[slot * S.nee_k + base] = 0;
+		emitShadow(ok && cast_shadows, so, ldir, st, slot * S.nee_k + base, out);
+		return;
+	}
+	// area light: montecarlo.cc:393-405
+	const uint32_t l_offs = loffs * 4567u;
+	const int num_samples = L.samples;
+	const uint32_t offs = (uint32_t)num_samples * sample_idx + offset + l_offs;
+	const V3 corner = lv(L.pos), to_x = lv(L.to_x), to_y = lv(L.to_y), fn = lv(L.fnormal);
+	const C3 lcolor = C3{L.color[0], L.color[1], L.color[2]};
+	for(int i = 0; i < num_samples; ++i)
+	{
+		// areaLightSampleLight (montecarlo.cc:156-282) with Halton(2/3, offs - 1) getNext() i+1 times
+		bool ok = active;
+		C3 contrib = c3(0.f);
+		V3 so = sp.p, ldir = v3(0.f, 0.f, 1.f);
+		float st = 0.f;
+		if(ok)
+		{
+			const float s_1 = haltonFirst(2u, 0.5, offs - 1u + (uint32_t)i);
+			const float s_2 = haltonFirst(3u, 1.0 / 3.0, offs - 1u + (uint32_t)i);
+			// light_area.cc:66-96
+			const V3 p = corner + s_1 * to_x + s_2 * to_y;
+			ldir = p - sp.p;
+			const float dist_sqr = lengthSqr(ldir);
+			const float dist = sqrtf(dist_sqr);
+			if((double)dist <= 0.0) ok = false;
+			float cos_angle = 0.f;
+			if(ok)
+			{
+				ldir = ldir * (1.f / dist);
+				cos_angle = dot(ldir, fn);
+				if(cos_angle <= 0) ok = false;
+			}
+			if(ok)
+			{
+				const float pdf = x87mulDiv(kPi, dist_sqr, L.area * cos_angle);
+				if(pdf > 1e-6f)
+				{
+					const C3 surf_col = matEval(m, sp, wo, ldir, B_ALL);
+					const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
+					float w = 1.f;
+					const float m_pdf = matPdf(m, sp, wo, ldir, B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT);
+					if(m_pdf > 1e-6f)
+					{
+						const float l_2 = pdf * pdf;
+						const float m_2 = m_pdf * m_pdf;
+						w = l_2 / (l_2 + m_2);
+					}
+					contrib = surf_col * lcolor * angle * w / pdf;
+					shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
+				}
+				else ok = false;
+			}
+		}
+		if(active)
+		{
+			nee[slot * S.nee_k + base + i] = f4(contrib, ok ? 1.f : 0.f);
+			occ[slot * S.nee_k + base + i] = 0;
+		}
+		emitShadow(ok && cast_shadows, so, ldir, st, slot * S.nee_k + base + i, out);
+	}
+	for(int i = 0; i < num_samples; ++i)
+	{
+		// areaLightSampleMaterial (montecarlo.cc:284-383)
+		bool ok = active;
+		C3 contrib = c3(0.f);
+		V3 so = sp.p, dir = v3(0.f, 0.f, 1.f);
+		float st = 0.f;
+		if(ok)
+		{
+			const float b_tmin = S.ray_min_dist_auto ? S.ray_min_dist * fmaxf(1.f, p_len) : S.ray_min_dist;
+			BsdfSample s;
+			s.s_1 = haltonFirst(2u, 0.5, offs - 1u + (uint32_t)i);
+			s.s_2 = haltonFirst(3u, 1.0 / 3.0, offs - 1u + (uint32_t)i);
+			s.flags = B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT;
+			s.pdf = 0.f;
+			s.sampled = B_NONE;
+			float W = 0.f;
+			const C3 surf_col = matSample(m, sp, wo, dir, s, W);
+			ok = s.pdf > 1e-6f;
+			float t = 0.f, cos_angle = 0.f;
+			if(ok)
+			{
+				// light_area.cc:137-151
+				cos_angle = dot(dir, fn);
+				if(cos_angle <= 0) ok = false;
+				else if(!areaTri(corner, lv(L.c2), lv(L.c3), sp.p, dir, t))
+				{
+					if(!areaTri(corner, lv(L.c3), lv(L.c4), sp.p, dir, t)) ok = false;
+				}
+				if(ok && !(t > 1.0e-10f)) ok = false;
+			}
+			if(ok)
+			{
+				const float light_pdf = x87mul(kDiv1ByPi, 1.f / (t * t) * L.area * cos_angle);
+				if(light_pdf > 1e-6f)
+				{
+					const float l_pdf = 1.f / light_pdf;
+					const float l_2 = l_pdf * l_pdf;
+					const float m_2 = s.pdf * s.pdf;
+					const float w = m_2 / (l_2 + m_2);
+					contrib = surf_col * lcolor * w * W;
+					shadowRayOf(sp.p, dir, b_tmin, t, so, st);
+				}
+				else ok = false;
+			}
+		}
+		if(active)
+		{
+			nee[slot * S.nee_k + base + num_samples + i] = f4(contrib, ok ? 1.f : 0.f);
+			occ[slot * S.nee_k + base + num_samples + i] = 0;
+		}
+		emitShadow(ok && cast_shadows, so, dir, st, slot * S.nee_k + base + num_samples + i, out);
+	}
+}
+
+// Sum of one light's entries with the reference's addition order (montecarlo.cc:385-408).
+__device__ C3 neeSum(const DevScene &S, const DevLight &L, const float4 *nee, const uint8_t *occ, int slot, int base)
+{
+	const int k0 = slot * S.nee_k + base;
+	if(L.type == LIGHT_POINT)
+	{
+		const float4 e = nee[k0];
+		C3 c = c3(0.f);
+		if(e.w != 0.f && !occ[k0]) c = c + rgb(e);
+		return c3(0.f) + c;
+	}
+	C3 acc_l = c3(0.f), acc_m = c3(0.f);
+	for(int i = 0; i < L.samples; ++i)
+	{
+		const float4 e = nee[k0 + i];
+		if(e.w != 0.f && !occ[k0 + i]) acc_l = acc_l + rgb(e);
+	}
+	for(int i = 0; i < L.samples; ++i)
+	{
+		const float4 e = nee[k0 + L.samples + i];
+		if(e.w != 0.f && !occ[k0 + L.samples + i]) acc_m = acc_m + rgb(e);
+	}
+	const C3 col_l = acc_l * L.inv_samples;
+	const C3 col_m = acc_m * L.inv_samples;
+	return (c3(0.f) + col_l) + col_m;
+}
+
+__device__ __forceinline__ float ldsDim(const DevScene &S, int dim, uint32_t n)
+{
+	return (float)lowDiscrepancy(S.faure + S.faure_off[dim], S.faure_base[dim], S.faure_inv[dim], n);
+}
+
+struct ShadeArgs
+{
+	DevScene S;
+	DevPaths P;
+	DevQueues Q;         // current (active list + hits)
+	DevQueues Qn;        // next
+	const DevCounters *cnt;
+	DevCounters *cnt_next;
+	float4 *samples;     // frame sample buffer [(y * W + x) * spp + s]
+	const DevJob *jobs;
+	int n_jobs;
+	uint64_t chunk_base;
+};
+
+__device__ __forceinline__ void writeSample(const ShadeArgs &A, int slot, C3 col, float alpha)
+{
+	const SampleCoord sc = sampleCoord(A.jobs, A.n_jobs, A.S.width, A.S.tile, A.S.spp, A.chunk_base + (uint64_t)slot);
+	if(alpha > 1.f) alpha = 1.f;   // integrator_tiled.cc:399
+	A.samples[((size_t)sc.y * A.S.width + sc.x) * A.S.spp + sc.s] = f4(col, alpha);
+}
+
+// First hit v0 of a later subpath, rebuilt from the primitive stored with the camera hit.
+__device__ __forceinline__ Surf surfFromPrim(const DevScene &S, V3 p, int prim)
+{
+	Surf s;
+	s.p = p;
+	const float4 g = S.prim_ng[prim];
+	s.ng = xyz(g);
+	s.n = s.ng;
+	coordsSystem(s.n, s.nu, s.nv);
+	s.mat = __float_as_int(g.w);
+	s.flags = S.mats[s.mat].bsdf_flags;
+	return s;
+}
+
+// One path vertex per active slot.  Control flow restates PathIntegrator::integrate
+// (integrator_path_tracer.cc:120-290) / DirectLightIntegrator::integrate (:97-144) as a state
+// machine whose vertices are processed one iteration at a time:
+//   1. connect the estimate left pending by the previous vertex (its shadow rays were traced
+//      by this iteration's k_trace) — additions happen in the reference's order;
+//   2. shade the new hit (camera hit v0, first segment hit v1, or bounce hit);
+//   3. next-event estimation: contributions + shadow rays (wave-uniform loops);
+//   4. sample the next segment, or end the subpath (next subpath / finalize);
+//   5. wave-ballot compaction of the slots that continue.
+__global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
+{
+	const DevScene &S = A.S;
+	const DevPaths &P = A.P;
+	const uint32_t n_a = A.cnt->n_active;
+	ShadeOut out;
+	out.sh_count = &A.cnt_next->n_shadow;
+	out.Qn = A.Qn;
+	const bool is_path = S.integrator == INT_PATH;
+	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
+	const uint32_t stride = gridDim.x * blockDim.x;
+	for(uint32_t base_i = blockIdx.x * blockDim.x; base_i < n_a; base_i += stride)
+	{
+		const uint32_t i = base_i + threadIdx.x;
+		const bool live = i < n_a;
+		int slot = 0;
+		uint32_t stage = ST_NORAY, flags = 0;
+		uint2 pix = make_uint2(0u, 0u);
+		if(live)
+		{
+			slot = A.Q.slot[i];
+			stage = P.stage[slot];
+			flags = P.flags[slot];
+			pix = P.pix[slot];
+		}
+		const uint32_t st = stage & 0xffu;
+		uint32_t subpath = (stage >> 8) & 0xfffu;
+		int depth = (int)(stage >> 20);
+		const uint32_t offset = pix.x, sample_idx = pix.y;
+
+		// ---- 1. connect the pending next-event estimate ----
+		if(live && (flags & F_PEND_V0))
+		{
+			// estimateAllDirectLight (montecarlo.cc:54-68): col += sum over lights in name order
+			C3 total = c3(0.f);
+			for(int l = 0; l < S.n_lights; ++l) total = total + neeSum(S, S.lights[l], P.nee, P.occ, slot, (int)S.lights[l].nee_base);
+			const float4 c = P.col[slot];
+			P.col[slot] = f4(rgb(c) + total, c.w);
+		}
+		if(live && (flags & F_PEND_ONE))
+		{
+			// path_tracer.cc:201-207 / :244-266: lcol = estimateOne * nlights (+ emit); path_col += lcol * thr
+			const int lnum = (int)(flags >> F_LNUM_SHIFT);
+			C3 lcol = neeSum(S, S.lights[lnum], P.nee, P.occ, slot, 0) * (float)S.n_lights;
+			if(flags & F_PEND_EMIT) lcol = lcol + rgb(P.pend_emit[slot]);
+			P.pcol[slot] = f4(rgb(P.pcol[slot]) + lcol * rgb(P.pend_thr[slot]), 0.f);
+		}
+		flags &= ~(F_PEND_V0 | F_PEND_ONE | F_PEND_EMIT);
+
+		// ---- 2. the new hit ----
+		Surf sp;
+		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
+		V3 wo = v3(0.f, 0.f, 1.f);
+		bool have_hit = false;
+		if(live && st != ST_NORAY)
+		{
+			const int prim = A.Q.hit_prim[i];
+			if(prim >= 0)
+			{
+				const float4 ro = A.Q.ray_o[i], rd = A.Q.ray_d[i];
+				have_hit = true;
+				sp = makeSurf(S, xyz(ro), xyz(rd), A.Q.hit_t[i], prim);
+				wo = -xyz(rd);
+			}
+		}
+		bool nee_v0 = false, nee_one = false, sample_next = false, end_sub = false, finalize = false, start_sub = false;
+		C3 emit_pend = c3(0.f);
+		C3 thr = c3(0.f);
+		if(live)
+		{
+			if(st == ST_NORAY) end_sub = true;   // a finished subpath whose estimate just got connected
+			else if(st == ST_CAMERA)
+			{
+				if(!have_hit)
+				{
+					// integrator_tiled.cc:707-720 background
+					C3 col = c3(0.f);
+					float alpha = 1.f;
+					if(S.bg_transp) alpha = 0.f;
+					else if(S.has_bg) col = C3{S.bg[0], S.bg[1], S.bg[2]};
+					writeSample(A, slot, col, alpha);
+				}
+				else
+				{
+					const DevMaterial &m = S.mats[sp.mat];
+					C3 col = c3(0.f);
+					if(sp.flags & B_EMIT) col = col + matEmit(m, sp, wo);
+					P.col[slot] = f4(col, 1.f);
+					if(sp.flags & B_DIFFUSE) { nee_v0 = true; flags |= F_V0_DIFFUSE; }
+					if(is_path && (sp.flags & B_DIFFUSE))
+					{
+						P.v0p[slot] = f4(sp.p, __int_as_float(A.Q.hit_prim[i]));
+						P.v0wo[slot] = f4(wo, 0.f);
+						start_sub = true;
+						subpath = 0;
+					}
+					else end_sub = true;
+				}
+			}
+			else if(st == ST_FIRST)
+			{
+				if(!have_hit) end_sub = true;     // path_tracer.cc:192 `continue`
+				else
+				{
+					// path_tracer.cc:193-207
+					if(flags & F_SAMPLED) P.pwo[slot] = f4(wo, 0.f);
+					else wo = xyz(P.pwo[slot]);
+					nee_one = true;
+					flags = (flags & ~F_MATFLAGS) | (sp.flags & F_MATFLAGS);
+					if(sp.flags & B_EMIT) { emit_pend = matEmit(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
+					thr = rgb(P.thr[slot]);
+					depth = 1;
+					sample_next = true;
+				}
+			}
+			else   // ST_BOUNCE, ray of loop iteration `depth`
+			{
+				if(!have_hit) end_sub = true;     // path_tracer.cc:235
+				else
+				{
+					const uint32_t mfl = flags & F_MATFLAGS;
+					P.pwo[slot] = f4(wo, 0.f);
+					thr = rgb(P.thr[slot]);
+					bool killed = false;
+					if(depth > S.rr_min_bounces)
+					{
+						// path_tracer.cc:249-255 (the draw does not depend on the light estimate)
+						const uint2 r = P.rng[slot];
+						Mwc g{r.x, r.y};
+						const float random_value = (float)g.next();
+						P.rng[slot] = make_uint2(g.x, g.c);
+						const float probability = maxComp(thr);
+						if(probability <= 0.f || probability < random_value) killed = true;
+						else thr = thr * (1.f / probability);
+					}
+					if(killed) end_sub = true;
+					else
+					{
+						P.thr[slot] = f4(thr, 0.f);
+						if((mfl & B_EMIT) && (flags & F_CAUSTIC)) { emit_pend = matEmit(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
+						if(mfl & B_DIFFUSE) nee_one = true;
+						else
+						{
+							// lcol = 0 (+ emission): nothing to trace, connect now
+							C3 lcol = c3(0.f);
+							if(flags & F_PEND_EMIT) lcol = lcol + emit_pend;
+							P.pcol[slot] = f4(rgb(P.pcol[slot]) + lcol * thr, 0.f);
+							flags &= ~F_PEND_EMIT;
+						}
+						++depth;
+						sample_next = true;
+					}
+				}
+			}
+		}
+		uint32_t lnum = 0;
+		if(nee_one)
+		{
+			// integrator_montecarlo.cc:70-78 light pick.  The reference draws from a running
+			// per-thread counter; a per-sample counter keeps the GPU deterministic (multi-light
+			// PT is therefore matched statistically; one light is exact).
+			if(S.n_lights > 1)
+			{
+				const uint32_t corr = (uint32_t)depth + subpath * (uint32_t)S.bounces;
+				const float hv = haltonFirst(2u, 0.5, S.base_offset + corr - 1u);
+				lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
+			}
+			flags = (flags & ((1u << F_LNUM_SHIFT) - 1u)) | (lnum << F_LNUM_SHIFT) | F_PEND_ONE;
+			P.pend_thr[slot] = f4(thr, 0.f);
+			if(flags & F_PEND_EMIT) P.pend_emit[slot] = f4(emit_pend, 0.f);
+		}
+		if(nee_v0) flags |= F_PEND_V0;
+
+		// ---- 3. next-event estimation ----
+		if(__any(nee_v0))
+		{
+			for(int l = 0; l < S.n_lights; ++l)
+				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, nee_v0, slot,
+				         (int)S.lights[l].nee_base, P.nee, P.occ, out);
+		}
+		if(__any(nee_one))
+		{
+			for(int l = 0; l < S.n_lights; ++l)
+			{
+				const bool mine = nee_one && (int)lnum == l;
+				if(!__any(mine)) continue;
+				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, mine, slot, 0, P.nee, P.occ, out);
+			}
+		}
+
+		// ---- 4. next segment ----
+		V3 ray_o = v3(0.f, 0.f, 0.f), ray_d = v3(0.f, 0.f, 1.f);
+		bool want_ray = false;
+		if(live && sample_next)
+		{
+			if(depth < S.bounces)
+			{
+				// path_tracer.cc:211-234, loop iteration `depth`
+				const uint32_t offs = n_paths * sample_idx + offset + subpath;
+				const int d_4 = 4 * depth;
+				BsdfSample s;
+				s.s_1 = ldsDim(S, d_4 + 3, offs);
+				s.s_2 = ldsDim(S, d_4 + 4, offs);
+				s.flags = B_ALL;
+				s.pdf = 0.f;
+				s.sampled = B_NONE;
+				float w = P.w[slot];
+				V3 dir = v3(0.f, 0.f, 0.f);
+				C3 scol = matSample(S.mats[sp.mat], sp, wo, dir, s, w);
+				P.w[slot] = w;
+				scol = scol * w;
+				if(isBlack(scol)) end_sub = true;
+				else
+				{
+					P.thr[slot] = f4(thr * scol, 0.f);
+					if(S.caustic_path && (s.sampled & (B_SPECULAR | B_GLOSSY | B_FILTER))) flags |= F_CAUSTIC;
+					else flags &= ~F_CAUSTIC;
+					ray_o = sp.p;
+					ray_d = dir;
+					want_ray = true;
+					stage = ST_BOUNCE | (subpath << 8) | ((uint32_t)depth << 20);
+				}
+			}
+			else end_sub = true;
+		}
+		const bool pending = (flags & (F_PEND_V0 | F_PEND_ONE)) != 0;
+		if(live && end_sub && !pending)
+		{
+			// end of the subpath: next subpath (path_tracer.cc:166) or the end of integrate()
+			if(is_path && (flags & F_V0_DIFFUSE) && subpath + 1 < n_paths) { start_sub = true; ++subpath; }
+			else finalize = true;
+		}
+		if(live && start_sub)
+		{
+			// path_tracer.cc:168-191: first segment of subpath `subpath` from v0
+			const float4 v0p = P.v0p[slot];
+			const Surf s0 = (st == ST_CAMERA) ? sp : surfFromPrim(S, xyz(v0p), __float_as_int(v0p.w));
+			const V3 wo0 = (st == ST_CAMERA) ? wo : xyz(P.v0wo[slot]);
+			const uint32_t offs = n_paths * sample_idx + offset + subpath;
+			BsdfSample s;
+			s.s_1 = riVdC(offs);
+			s.s_2 = ldsDim(S, 2, offs);
+			s.flags = B_DIFFUSE | B_REFLECT | B_TRANSMIT;
+			s.pdf = 0.f;
+			s.sampled = B_NONE;
+			float w = P.w[slot];
+			V3 dir = v3(0.f, 0.f, 0.f);
+			C3 scol = matSample(S.mats[s0.mat], s0, wo0, dir, s, w);
+			P.w[slot] = w;
+			scol = scol * w;
+			P.thr[slot] = f4(scol, 0.f);
+			P.pwo[slot] = f4(wo0, 0.f);
+			if(s.sampled != B_NONE) flags |= F_SAMPLED;
+			else flags &= ~F_SAMPLED;
+			flags &= ~F_CAUSTIC;
+			ray_o = s0.p;
+			ray_d = dir;
+			want_ray = true;
+			stage = ST_FIRST | (subpath << 8);
+		}
+		if(live && finalize)
+		{
+			// path_tracer.cc:274-278 / direct_light.cc:129-131
+			const float4 c = P.col[slot];
+			C3 col = rgb(c);
+			if(is_path && (flags & F_V0_DIFFUSE)) col = col + rgb(P.pcol[slot]) / (float)n_paths;
+			col = col + c3(0.f);   // recursiveRaytrace: no specular/glossy component
+			writeSample(A, slot, col, c.w);
+		}
+
+		// ---- 5. compaction ----
+		const bool keep = live && (want_ray || (end_sub && pending));
+		const uint32_t k = waveAppend(keep, &A.cnt_next->n_active);
+		if(keep)
+		{
+			A.Qn.slot[k] = slot;
+			if(want_ray)
+			{
+				A.Qn.ray_o[k] = f4(ray_o, S.ray_min_dist);
+				A.Qn.ray_d[k] = f4(ray_d, -1.f);
+			}
+			else
+			{
+				A.Qn.ray_o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+				A.Qn.ray_d[k] = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));
+				stage = ST_NORAY | (subpath << 8);
+			}
+			P.stage[slot] = stage;
+			P.flags[slot] = flags;
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_film: deterministic gather splat + flush normalisation
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int roundToInt(double v) { return (int)(v + (.5 - 1.4e-11)); }
+__device__ __forceinline__ int floorToInt(double v) { return (int)floor(v); }
+
+// rank of a pixel in the single-thread linear tile order (imagesplitter.cc:30-49)
+__device__ __forceinline__ uint64_t pixelRank(int x, int y, int W, int H, int ts)
+{
+	const int ty = y / ts, tx = x / ts;
+	const int th = min(ts, H - ty * ts), tw = min(ts, W - tx * ts);
+	return (uint64_t)ty * ts * W + (uint64_t)tx * ts * th + (uint64_t)(y - ty * ts) * tw + (x - tx * ts);
+}
+
+__global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, float4 *out, float *weights,
+                                              int y0, int y1, float clamp_samples)
+{
+	const int x = blockIdx.x * blockDim.x + threadIdx.x;
+	const int y = y0 + blockIdx.y;
+	if(x >= F.width || y >= y1) return;
+	const int W = F.width, H = F.height, spp = F.spp;
+	// candidate sources, sorted by their rank in the reference's splat order
+	int sx[81], sy[81];
+	uint64_t rk[81];
+	int n = 0;
+	for(int yy = y - F.reach_fwd; yy <= y + F.reach_back; ++yy)
+	{
+		if(yy < 0 || yy >= H) continue;
+		for(int xx = x - F.reach_fwd; xx <= x + F.reach_back; ++xx)
+		{
+			if(xx < 0 || xx >= W) continue;
+			const uint64_t r = pixelRank(xx, yy, W, H, F.tile);
+			int p = n++;
+			while(p > 0 && rk[p - 1] > r) { rk[p] = rk[p - 1]; sx[p] = sx[p - 1]; sy[p] = sy[p - 1]; --p; }
+			rk[p] = r; sx[p] = xx; sy[p] = yy;
+		}
+	}
+	float wsum = 0.f;
+	float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+	const float d_1 = 1.f / (float)spp;
+	for(int c = 0; c < n; ++c)
+	{
+		const int px = sx[c], py = sy[c];
+		const uint32_t offset = fnv32((uint32_t)py * fnv32((uint32_t)px));
+		for(int s = 0; s < spp; ++s)
+		{
+			float dx = 0.5f, dy = 0.5f;
+			if(spp > 1)
+			{
+				dx = (0.5f + (float)s) * d_1;
+				dy = riLp((uint32_t)s + offset);
+			}
+			// imagefilm.cc:684-707 footprint of this sample, then the table weight at (x, y)
+			const int dx_0 = max(0 - px, roundToInt((double)dx - F.filterw));
+			const int dx_1 = min(W - px - 1, roundToInt((double)dx + F.filterw - 1.0));
+			const int dy_0 = max(0 - py, roundToInt((double)dy - F.filterw));
+			const int dy_1 = min(H - py - 1, roundToInt((double)dy + F.filterw - 1.0));
+			const int ox = x - px, oy = y - py;
+			if(ox < dx_0 || ox > dx_1 || oy < dy_0 || oy > dy_1) continue;
+			const int xi = floorToInt(fabs(((double)ox - (dx - 0.5)) * F.table_scale));
+			const int yi = floorToInt(fabs(((double)oy - (dy - 0.5)) * F.table_scale));
+			const float wt = F.table[yi * 16 + xi];
+			wsum = wsum + wt;
+			const float4 col = samples[((size_t)py * W + px) * spp + s];
+			float r = col.x, g = col.y, b = col.z;
+			if(clamp_samples > 0.f)
+			{
+				// color.h:415-440 clampProportionalRgb
+				const float max_rgb = fmaxf(r, fmaxf(g, b));
+				const float adj = clamp_samples / max_rgb;
+				if(max_rgb > clamp_samples)
+				{
+					if(r >= max_rgb) { r = clamp_samples; g *= adj; b *= adj; }
+					else if(g >= max_rgb) { g = clamp_samples; r *= adj; b *= adj; }
+					else { b = clamp_samples; r *= adj; g *= adj; }
+				}
+			}
+			acc.x = acc.x + r * wt;
+			acc.y = acc.y + g * wt;
+			acc.z = acc.z + b * wt;
+			acc.w = acc.w + col.w * wt;
+		}
+	}
+	const size_t p = (size_t)y * W + x;
+	if(weights) weights[p] = wsum;
+	if(wsum != 0.f) out[p] = make_float4(acc.x / wsum, acc.y / wsum, acc.z / wsum, acc.w / wsum);
+	else out[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// ---------------------------------------------------------------------------------------------
+// ray-level entry (batched Accelerator::intersect / isShadowed for parity tests and hosts)
+// ---------------------------------------------------------------------------------------------
+template<bool ANY>
+__global__ void __launch_bounds__(kTraceBlock) k_trace_rays(DevScene S, const float4 *ro, const float4 *rd, int n,
+                                                           float *t_out, int *prim_out, int stack_depth)
+{
+	extern __shared__ float4 smem[];
+	TraceCtx C;
+	C.stack = reinterpret_cast<int *>(smem);
+	C.nodes = S.nodes;
+	C.tris = S.tris;
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const float4 o = ro[i], d = rd[i];
+	uint32_t v = 0, t = 0;
+	float tb;
+	int pb;
+	if(ANY)
+	{
+		// accelerator.cc:69-78
+		V3 so;
+		float tm;
+		shadowRayOf(xyz(o), xyz(d), o.w, d.w, so, tm);
+		const bool occ = traverse<true>(C, so, xyz(d), 0.f, tm, tb, pb, v, t);
+		t_out[i] = occ ? 1.f : 0.f;
+		prim_out[i] = occ ? pb : -1;
+	}
+	else
+	{
+		const float tmax = (d.w >= 0.f) ? d.w : __builtin_huge_valf();
+		const bool hit = traverse<false>(C, xyz(o), xyz(d), o.w, tmax, tb, pb, v, t);
+		t_out[i] = hit ? tb : -1.f;
+		prim_out[i] = hit ? pb : -1;
+	}
+}
+
+} // namespace yafamd
+
+// ---------------------------------------------------------------------------------------------
+// launch wrappers used by render.cc (C++ host code, no HIP language there)
+// ---------------------------------------------------------------------------------------------
+using namespace yafamd;
+
+extern "C" {
+
+hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, DevCounters *cnt,
+                                const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st)
+{
+	if(n <= 0) return hipSuccess;
+	hipLaunchKernelGGL(k_camera, dim3((n + 255) / 256), dim3(256), 0, st, *S, *P, *Q, cnt, jobs, n_jobs, chunk_base, n);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, DevCounters *cnt_next,
+                               const DevPaths *P, DevStats *stats, int stack_depth, int grid, hipStream_t st)
+{
+	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
+	if(S->scene_in_lds)
+	{
+		const size_t bytes = stack_bytes + (size_t)(4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
+		hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, cnt, cnt_next, *P, stats, stack_depth);
+	}
+	else hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kTraceBlock), stack_bytes, st, *S, *Q, cnt, cnt_next, *P, stats, stack_depth);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevQueues *Qn,
+                               const DevCounters *cnt, DevCounters *cnt_next, float4 *samples, const DevJob *jobs,
+                               int n_jobs, uint64_t chunk_base, int grid, hipStream_t st)
+{
+	ShadeArgs A;
+	A.S = *S;
+	A.P = *P;
+	A.Q = *Q;
+	A.Qn = *Qn;
+	A.cnt = cnt;
+	A.cnt_next = cnt_next;
+	A.samples = samples;
+	A.jobs = jobs;
+	A.n_jobs = n_jobs;
+	A.chunk_base = chunk_base;
+	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, st, A);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
+                              float clamp_samples, hipStream_t st)
+{
+	if(y1 <= y0) return hipSuccess;
+	hipLaunchKernelGGL(k_film, dim3((F->width + 255) / 256, y1 - y0), dim3(256), 0, st, *F, samples, out, weights, y0,
+	                   y1, clamp_samples);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_trace_rays(const DevScene *S, int any, const float4 *ro, const float4 *rd, int n, float *t_out,
+                                    int *prim_out, int stack_depth, hipStream_t st)
+{
+	if(n <= 0) return hipSuccess;
+	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
+	if(any) hipLaunchKernelGGL(k_trace_rays<true>, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), stack_bytes, st, *S, ro, rd, n, t_out, prim_out, stack_depth);
+	else hipLaunchKernelGGL(k_trace_rays<false>, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), stack_bytes, st, *S, ro, rd, n, t_out, prim_out, stack_depth);
+	return hipGetLastError();
+}
+
+}

@@ -1,0 +1,435 @@
+// GPU driver (see render.h).  Plain C++ against the HIP runtime API; kernels are launched
+// through the extern "C" wrappers at the end of kernels.hip.
+#include "render.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <sstream>
+
+using namespace yafamd;
+
+extern "C" {
+hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, DevCounters *cnt,
+                                const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st);
+hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, DevCounters *cnt_next,
+                               const DevPaths *P, DevStats *stats, int stack_depth, int grid, hipStream_t st);
+hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevQueues *Qn,
+                               const DevCounters *cnt, DevCounters *cnt_next, float4 *samples, const DevJob *jobs,
+                               int n_jobs, uint64_t chunk_base, int grid, hipStream_t st);
+hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
+                              float clamp_samples, hipStream_t st);
+hipError_t yafamd_launch_trace_rays(const DevScene *S, int any, const float4 *ro, const float4 *rd, int n, float *t_out,
+                                    int *prim_out, int stack_depth, hipStream_t st);
+}
+
+namespace
+{
+
+struct Buf
+{
+	void *p = nullptr;
+	size_t bytes = 0;
+	void release()
+	{
+		if(p) hipFree(p);
+		p = nullptr;
+		bytes = 0;
+	}
+};
+
+// Faure digit permutations (Faure 1992 construction; the reference holds them as literal tables,
+// src/sampler/halton.cc:26-401) and the 9-decimal inverse primes of halton.cc:413.
+std::vector<int> faurePerm(int b)
+{
+	if(b <= 2) return {0, 1};
+	if((b & 1) == 0)
+	{
+		const std::vector<int> h = faurePerm(b / 2);
+		std::vector<int> out;
+		for(int v : h) out.push_back(2 * v);
+		for(int v : h) out.push_back(2 * v + 1);
+		return out;
+	}
+	const std::vector<int> p = faurePerm(b - 1);
+	const int c = (b - 1) / 2;
+	std::vector<int> out;
+	for(int i = 0; i < (int)p.size(); ++i)
+	{
+		if(i == c) out.push_back(c);
+		out.push_back(p[i] + (p[i] >= c ? 1 : 0));
+	}
+	return out;
+}
+
+} // namespace
+
+struct GpuRenderer::Impl
+{
+	bool ok = false, init_done = false;
+	hipStream_t stream = nullptr;
+	Buf nodes, tris, prim_ng, mats, lights, faure, faure_off, faure_base, faure_inv;
+	int n_nodes = 0, n_tris = 0, n_mats = 0, n_lights = 0, depth = 0, stack_depth = 32;
+	bool scene_in_lds = false;
+	// frame buffers
+	Buf samples, film, weights, jobs;
+	int film_w = 0, film_h = 0;
+	// chunk buffers
+	size_t slots_cap = 0;
+	int nee_cap = 0;
+	std::vector<Buf> chunk_bufs;
+	DevPaths P{};
+	DevQueues Q[2]{};
+	Buf counters, stats;
+	std::vector<hipEvent_t> ev_pool;
+	int trace_grid = 2048, shade_grid = 1024;
+
+	~Impl()
+	{
+		for(Buf *b : {&nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_off, &faure_base, &faure_inv, &samples, &film,
+		              &weights, &jobs, &counters, &stats})
+			b->release();
+		for(Buf &b : chunk_bufs) b.release();
+		for(hipEvent_t e : ev_pool) hipEventDestroy(e);
+		if(stream) hipStreamDestroy(stream);
+	}
+};
+
+#define HIPCHECK(expr)                                                                                         \
+	do                                                                                                         \
+	{                                                                                                          \
+		const hipError_t e_ = (expr);                                                                          \
+		if(e_ != hipSuccess)                                                                                   \
+		{                                                                                                      \
+			std::ostringstream os_;                                                                            \
+			os_ << "GPU: " << #expr << " failed: " << hipGetErrorString(e_) << " (" << __FILE__ << ":" << __LINE__ << ")"; \
+			log_.error(os_.str());                                                                             \
+			return false;                                                                                      \
+		}                                                                                                      \
+	} while(0)
+
+GpuRenderer::GpuRenderer(Logger &log) : d_(new Impl), log_(log) {}
+GpuRenderer::~GpuRenderer() { delete d_; }
+
+bool GpuRenderer::ready()
+{
+	if(d_->init_done) return d_->ok;
+	d_->init_done = true;
+	int n = 0;
+	if(hipGetDeviceCount(&n) != hipSuccess || n == 0)
+	{
+		log_.error("GPU: no HIP device available — the MI355X core has no CPU fallback");
+		return false;
+	}
+	HIPCHECK(hipStreamCreateWithFlags(&d_->stream, hipStreamNonBlocking));
+	int dev = 0;
+	HIPCHECK(hipGetDevice(&dev));
+	hipDeviceProp_t prop;
+	HIPCHECK(hipGetDeviceProperties(&prop, dev));
+	d_->trace_grid = std::max(256, prop.multiProcessorCount * 8);
+	d_->shade_grid = std::max(256, prop.multiProcessorCount * 4);
+	std::ostringstream os;
+	os << "GPU: device " << dev << " " << prop.name << " (" << prop.gcnArchName << ", " << prop.multiProcessorCount << " CUs, "
+	   << (prop.totalGlobalMem >> 30) << " GiB)";
+	log_.info(os.str());
+	d_->ok = true;
+	return true;
+}
+
+template<class T>
+static bool allocCopy(Logger &log_, Buf &b, const T *src, size_t count)
+{
+	b.release();
+	const size_t bytes = std::max<size_t>(16, count * sizeof(T));
+	HIPCHECK(hipMalloc(&b.p, bytes));
+	b.bytes = bytes;
+	if(count) HIPCHECK(hipMemcpy(b.p, src, count * sizeof(T), hipMemcpyHostToDevice));
+	return true;
+}
+
+static bool ensure(Logger &log_, Buf &b, size_t bytes)
+{
+	if(b.bytes >= bytes && b.p) return true;
+	b.release();
+	HIPCHECK(hipMalloc(&b.p, std::max<size_t>(bytes, 16)));
+	b.bytes = std::max<size_t>(bytes, 16);
+	return true;
+}
+
+bool GpuRenderer::upload(const HostScene &hs)
+{
+	if(!ready()) return false;
+	Impl &d = *d_;
+	if(!allocCopy(log_, d.nodes, hs.bvh.nodes.data(), hs.bvh.nodes.size())) return false;
+	if(!allocCopy(log_, d.tris, hs.bvh.tris.data(), hs.bvh.tris.size())) return false;
+	if(!allocCopy(log_, d.prim_ng, hs.prim_ng.data(), hs.prim_ng.size())) return false;
+	if(!allocCopy(log_, d.mats, hs.mats.data(), hs.mats.size())) return false;
+	if(!allocCopy(log_, d.lights, hs.lights.data(), hs.lights.size())) return false;
+	d.n_nodes = hs.bvh.n_nodes;
+	d.n_tris = (int)(hs.bvh.tris.size() / 12);
+	d.n_mats = (int)hs.mats.size();
+	d.n_lights = (int)hs.lights.size();
+	d.depth = hs.bvh.depth;
+	d.stack_depth = std::max(8, ((hs.bvh.depth + 2 + 7) / 8) * 8);
+	const size_t scene_bytes = (size_t)(4 * d.n_nodes + 3 * d.n_tris) * 16;
+	d.scene_in_lds = scene_bytes + (size_t)d.stack_depth * 128 * 4 <= 48 * 1024;
+	// Faure tables, dims 0..49 (halton.cc:403-414: dims 0-2 share the base-3 table)
+	std::vector<uint8_t> perm;
+	std::vector<uint32_t> off(50), base(50);
+	std::vector<double> inv(50);
+	int primes[50];
+	primes[0] = 1;
+	for(int k = 1, c = 2; k < 50; ++c)
+	{
+		bool pr = true;
+		for(int q = 2; q * q <= c; ++q) if(c % q == 0) { pr = false; break; }
+		if(pr) primes[k++] = c;
+	}
+	for(int dim = 0; dim < 50; ++dim)
+	{
+		const std::vector<int> p = faurePerm(dim <= 2 ? 3 : primes[dim]);
+		off[dim] = (uint32_t)perm.size();
+		for(int v : p) perm.push_back((uint8_t)v);
+		base[dim] = (uint32_t)primes[dim];
+		inv[dim] = (double)std::llround(1e9 / primes[dim]) / 1e9;
+	}
+	if(!allocCopy(log_, d.faure, perm.data(), perm.size())) return false;
+	if(!allocCopy(log_, d.faure_off, off.data(), off.size())) return false;
+	if(!allocCopy(log_, d.faure_base, base.data(), base.size())) return false;
+	if(!allocCopy(log_, d.faure_inv, inv.data(), inv.size())) return false;
+	stats_.bvh_nodes = (uint32_t)d.n_nodes;
+	stats_.bvh_depth = (uint32_t)d.depth;
+	stats_.scene_in_lds = d.scene_in_lds ? 1u : 0u;
+	return true;
+}
+
+static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
+{
+	S.nodes = (const float4 *)d.nodes.p;
+	S.tris = (const float4 *)d.tris.p;
+	S.prim_ng = (const float4 *)d.prim_ng.p;
+	S.mats = (const DevMaterial *)d.mats.p;
+	S.lights = (const DevLight *)d.lights.p;
+	S.faure = (const uint8_t *)d.faure.p;
+	S.faure_off = (const uint32_t *)d.faure_off.p;
+	S.faure_base = (const uint32_t *)d.faure_base.p;
+	S.faure_inv = (const double *)d.faure_inv.p;
+	S.n_nodes = d.n_nodes;
+	S.n_tris = d.n_tris;
+	S.n_mats = d.n_mats;
+	S.n_lights = d.n_lights;
+	S.scene_in_lds = d.scene_in_lds ? 1 : 0;
+}
+
+bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
+{
+	if(!ready()) return false;
+	Impl &d = *d_;
+	DevScene &S = rp.scene;
+	fillScenePointers(d, S);
+	const int W = S.width, H = S.height, spp = S.spp, ts = S.tile;
+	// ---- jobs: owned tile rows (+ halo rows for the film gather when sharded) ----
+	const int tile_rows = (H + ts - 1) / ts;
+	std::vector<DevJob> jobs;
+	owned_rows_.clear();
+	uint64_t total = 0;
+	auto owns = [&](int r) { return r >= 0 && r < tile_rows && (r % rp.shard_world) == rp.shard_rank; };
+	for(int r = 0; r < tile_rows; ++r)
+	{
+		if(!owns(r)) continue;
+		const int y0 = r * ts, y1 = std::min(H, y0 + ts);
+		if(rp.shard_world > 1 && rp.film.reach_fwd > 0 && y0 > 0 && !owns(r - 1))
+		{
+			const int hy0 = std::max(0, y0 - rp.film.reach_fwd);
+			jobs.push_back({hy0, y0, total});
+			total += (uint64_t)W * (y0 - hy0) * spp;
+		}
+		jobs.push_back({y0, y1, total});
+		total += (uint64_t)W * (y1 - y0) * spp;
+		owned_rows_.push_back({y0, y1});
+		if(rp.shard_world > 1 && rp.film.reach_back > 0 && y1 < H && !owns(r + 1))
+		{
+			const int hy1 = std::min(H, y1 + rp.film.reach_back);
+			jobs.push_back({y1, hy1, total});
+			total += (uint64_t)W * (hy1 - y1) * spp;
+		}
+	}
+	if(!allocCopy(log_, d.jobs, jobs.data(), jobs.size())) return false;
+	const int n_jobs = (int)jobs.size();
+	// ---- frame buffers ----
+	if(!ensure(log_, d.samples, (size_t)W * H * spp * sizeof(float4))) return false;
+	if(!ensure(log_, d.film, (size_t)W * H * sizeof(float4))) return false;
+	if(!ensure(log_, d.weights, (size_t)W * H * sizeof(float))) return false;
+	d.film_w = W;
+	d.film_h = H;
+	HIPCHECK(hipMemsetAsync(d.film.p, 0, (size_t)W * H * sizeof(float4), d.stream));
+	HIPCHECK(hipMemsetAsync(d.weights.p, 0, (size_t)W * H * sizeof(float), d.stream));
+	// ---- chunk buffers ----
+	const size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
+	const int K = std::max(1, S.nee_k);
+	if(M > d.slots_cap || K > d.nee_cap)
+	{
+		for(Buf &b : d.chunk_bufs) b.release();
+		d.chunk_bufs.clear();
+		auto A = [&](size_t bytes) -> void * {
+			d.chunk_bufs.emplace_back();
+			Buf &b = d.chunk_bufs.back();
+			if(hipMalloc(&b.p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+			b.bytes = bytes;
+			return b.p;
+		};
+		DevPaths &P = d.P;
+		P.stage = (uint32_t *)A(M * 4);
+		P.flags = (uint32_t *)A(M * 4);
+		P.w = (float *)A(M * 4);
+		P.thr = (float4 *)A(M * 16);
+		P.col = (float4 *)A(M * 16);
+		P.pcol = (float4 *)A(M * 16);
+		P.pwo = (float4 *)A(M * 16);
+		P.pend_thr = (float4 *)A(M * 16);
+		P.pend_emit = (float4 *)A(M * 16);
+		P.v0p = (float4 *)A(M * 16);
+		P.v0wo = (float4 *)A(M * 16);
+		P.rng = (uint2 *)A(M * 8);
+		P.pix = (uint2 *)A(M * 8);
+		P.nee = (float4 *)A(M * K * 16);
+		P.occ = (uint8_t *)A(M * K);
+		for(int q = 0; q < 2; ++q)
+		{
+			DevQueues &Q = d.Q[q];
+			Q.slot = (int *)A(M * 4);
+			Q.ray_o = (float4 *)A(M * 16);
+			Q.ray_d = (float4 *)A(M * 16);
+			Q.hit_t = (float *)A(M * 4);
+			Q.hit_prim = (int *)A(M * 4);
+			Q.sh_o = (float4 *)A(M * K * 16);
+			Q.sh_d = (float4 *)A(M * K * 16);
+			Q.sh_idx = (int *)A(M * K * 4);
+		}
+		for(const Buf &b : d.chunk_bufs)
+			if(!b.p) { log_.error("GPU: out of device memory for the wavefront buffers"); return false; }
+		d.slots_cap = M;
+		d.nee_cap = K;
+	}
+	if(!ensure(log_, d.counters, 2 * sizeof(DevCounters))) return false;
+	if(!ensure(log_, d.stats, sizeof(DevStats))) return false;
+	HIPCHECK(hipMemsetAsync(d.counters.p, 0, 2 * sizeof(DevCounters), d.stream));
+	HIPCHECK(hipMemsetAsync(d.stats.p, 0, sizeof(DevStats), d.stream));
+	DevCounters *cnt = (DevCounters *)d.counters.p;
+	DevStats *dstats = (DevStats *)d.stats.p;
+	const int n_paths = std::max(1, S.path_samples);
+	const int iters = (S.integrator == INT_PATH) ? 2 + n_paths * (S.bounces + 2) : 3;
+
+	// ---- events ----
+	const size_t n_chunks = (size_t)((total + M - 1) / M);
+	const size_t ev_needed = 2 + (rp.profile ? 2 * n_chunks * (size_t)iters : 0);
+	while(d.ev_pool.size() < ev_needed)
+	{
+		hipEvent_t e;
+		HIPCHECK(hipEventCreate(&e));
+		d.ev_pool.push_back(e);
+	}
+	size_t ev_i = 2;
+	HIPCHECK(hipEventRecord(d.ev_pool[0], d.stream));
+	for(uint64_t base = 0; base < total; base += M)
+	{
+		if(canceled && *canceled) break;
+		const int n = (int)std::min<uint64_t>(M, total - base);
+		HIPCHECK(yafamd_launch_camera(&S, &d.P, &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
+		int cur = 0;
+		for(int it = 0; it < iters; ++it)
+		{
+			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i], d.stream));
+			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &cnt[cur ^ 1], &d.P, dstats, d.stack_depth, d.trace_grid, d.stream));
+			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 1], d.stream));
+			if(rp.profile) ev_i += 2;
+			HIPCHECK(yafamd_launch_shade(&S, &d.P, &d.Q[cur], &d.Q[cur ^ 1], &cnt[cur], &cnt[cur ^ 1], (float4 *)d.samples.p,
+			                             (const DevJob *)d.jobs.p, n_jobs, base, d.shade_grid, d.stream));
+			cur ^= 1;
+		}
+	}
+	for(const auto &r : owned_rows_)
+		HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (float4 *)d.film.p, (float *)d.weights.p, r.first,
+		                            r.second, S.clamp_samples, d.stream));
+	HIPCHECK(hipEventRecord(d.ev_pool[1], d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	float ms = 0.f;
+	HIPCHECK(hipEventElapsedTime(&ms, d.ev_pool[0], d.ev_pool[1]));
+	DevStats hs{};
+	HIPCHECK(hipMemcpy(&hs, d.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+	stats_.closest_rays = hs.closest_rays;
+	stats_.shadow_rays = hs.shadow_rays;
+	stats_.node_visits = hs.node_visits;
+	stats_.tri_tests = hs.tri_tests;
+	stats_.samples = total;
+	stats_.render_seconds = ms * 1e-3;
+	stats_.trace_kernel_ms = 0.0;
+	stats_.trace_launches = 0;
+	if(rp.profile)
+	{
+		for(size_t e = 2; e + 1 < ev_i; e += 2)
+		{
+			float t = 0.f;
+			HIPCHECK(hipEventElapsedTime(&t, d.ev_pool[e], d.ev_pool[e + 1]));
+			stats_.trace_kernel_ms += t;
+			++stats_.trace_launches;
+		}
+	}
+	return true;
+}
+
+bool GpuRenderer::download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h)
+{
+	Impl &d = *d_;
+	if(!d.film.p || w != d.film_w || h != d.film_h) { log_.error("GPU: no film to download"); return false; }
+	rgba.resize((size_t)w * h * 4);
+	weights.resize((size_t)w * h);
+	HIPCHECK(hipMemcpy(rgba.data(), d.film.p, rgba.size() * 4, hipMemcpyDeviceToHost));
+	HIPCHECK(hipMemcpy(weights.data(), d.weights.p, weights.size() * 4, hipMemcpyDeviceToHost));
+	return true;
+}
+
+bool GpuRenderer::filmToDevice(void *dst, int y0, int y1)
+{
+	Impl &d = *d_;
+	if(!d.film.p || y0 < 0 || y1 > d.film_h || y1 < y0) { log_.error("GPU: bad film row range"); return false; }
+	const size_t row = (size_t)d.film_w * sizeof(float4);
+	HIPCHECK(hipMemcpy(dst, (char *)d.film.p + row * y0, row * (y1 - y0), hipMemcpyDeviceToDevice));
+	return true;
+}
+
+bool GpuRenderer::traceRays(bool any, const float *rays, int n, float *t, int *prim)
+{
+	if(!ready()) return false;
+	Impl &d = *d_;
+	if(!d.nodes.p) { log_.error("GPU: no acceleration structure built"); return false; }
+	std::vector<float> o((size_t)n * 4), dd((size_t)n * 4);
+	for(int i = 0; i < n; ++i)
+	{
+		const float *r = rays + 8 * (size_t)i;
+		o[4 * i] = r[0]; o[4 * i + 1] = r[1]; o[4 * i + 2] = r[2]; o[4 * i + 3] = r[6];
+		dd[4 * i] = r[3]; dd[4 * i + 1] = r[4]; dd[4 * i + 2] = r[5]; dd[4 * i + 3] = r[7];
+	}
+	Buf bo, bd, bt, bp;
+	bool ok = allocCopy(log_, bo, o.data(), o.size()) && allocCopy(log_, bd, dd.data(), dd.size()) &&
+	          ensure(log_, bt, (size_t)n * 4) && ensure(log_, bp, (size_t)n * 4);
+	if(ok)
+	{
+		DevScene S{};
+		fillScenePointers(d, S);
+		ok = yafamd_launch_trace_rays(&S, any ? 1 : 0, (const float4 *)bo.p, (const float4 *)bd.p, n, (float *)bt.p, (int *)bp.p,
+		                              d.stack_depth, d.stream) == hipSuccess &&
+		     hipStreamSynchronize(d.stream) == hipSuccess;
+		if(!ok) log_.error("GPU: trace launch failed");
+		if(ok && t) ok = hipMemcpy(t, bt.p, (size_t)n * 4, hipMemcpyDeviceToHost) == hipSuccess;
+		if(ok && prim) ok = hipMemcpy(prim, bp.p, (size_t)n * 4, hipMemcpyDeviceToHost) == hipSuccess;
+	}
+	bo.release();
+	bd.release();
+	bt.release();
+	bp.release();
+	return ok;
+}

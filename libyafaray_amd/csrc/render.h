@@ -1,0 +1,62 @@
+// GPU driver of the hot path: uploads the scene in the devscene.h layouts, runs the wavefront
+// pipeline of kernels.hip chunk by chunk on one HIP stream, and gathers the film.
+//
+// Replaces TiledIntegrator::render / renderPass / renderWorker / renderTile
+// (src/integrator/surface/integrator_tiled.cc:50-408): instead of `threads` CPU workers pulling
+// 32x32 tiles from an atomic counter, the whole tile list is one enumeration of camera samples
+// (tile order preserved) processed `chunk_slots` samples at a time by the GPU.
+#pragma once
+
+#include "bvh.h"
+#include "devscene.h"
+#include "host.h"
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace yafamd
+{
+
+struct HostScene
+{
+	BvhOutput bvh;
+	std::vector<float> prim_ng;          // 4 floats per primitive
+	std::vector<DevMaterial> mats;
+	std::vector<DevLight> lights;        // render order (by name)
+	int n_prims = 0;
+};
+
+struct RenderParams
+{
+	DevScene scene;                      // pointers filled by the renderer
+	DevFilm film;
+	int shard_rank = 0, shard_world = 1;
+	int chunk_slots = 1 << 20;
+	bool profile = false;
+};
+
+class GpuRenderer
+{
+	public:
+		explicit GpuRenderer(Logger &log);
+		~GpuRenderer();
+		bool ready();
+		bool upload(const HostScene &hs);
+		bool render(RenderParams &rp, volatile bool *canceled);
+		bool download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h);
+		bool filmToDevice(void *dst, int y0, int y1);
+		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
+		const yafaray_amd_stats_t &stats() const { return stats_; }
+		std::vector<std::pair<int, int>> ownedRows() const { return owned_rows_; }
+
+		struct Impl;
+
+	private:
+		Impl *d_;
+		Logger &log_;
+		yafaray_amd_stats_t stats_{};
+		std::vector<std::pair<int, int>> owned_rows_;
+};
+
+} // namespace yafamd

@@ -1,0 +1,364 @@
+"""Scene descriptions used by the tests, the bench and the smoke check.
+
+A `SceneSpec` is plain data (numpy geometry + small dataclasses).  `apply(spec, yi)` replays it
+through the C API exactly the way the reference's C clients do (tests/test01/test01.c:27-1018:
+paramsSet* -> create* -> addVertex/addTriangle -> setupRender -> render), so every product
+render in this repository goes through the drop-in boundary.
+
+Builders:
+  * `cornell(...)`       — BASELINE config C2/C3: 5 walls + 2 boxes (34 triangles), 0.5 x 0.5 area
+                           light at z = 1.98, camera from (0, -3.9, 1), focal 1.4.
+  * `cornell_sphere(...)`— config C4: C2 + a UV sphere of 707 x 707 x 2 = 999,698 triangles.
+  * `test01(...)`        — config C1: the reference's tests/test01 scene (six cubes + plane, point
+                           light, direct lighting, gauss 1.5) with textures stripped; its geometry is
+                           read from tests/golden/test01_scene.json (made by make_test01_scene.py).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+
+@dataclass
+class Material:
+    name: str
+    type: str = "shinydiffusemat"          # or "light_mat"
+    color: tuple = (0.8, 0.8, 0.8)
+    diffuse_reflect: float = 1.0
+    emit: float = 0.0
+    power: float = 1.0                     # light_mat
+    double_sided: bool = False             # light_mat
+    receive_shadows: bool = True
+    flat_material: bool = False
+
+
+@dataclass
+class Light:
+    name: str
+    type: str = "pointlight"               # or "arealight"
+    color: tuple = (1.0, 1.0, 1.0)
+    power: float = 1.0
+    from_: tuple = (0.0, 0.0, 0.0)         # pointlight
+    corner: tuple = (0.0, 0.0, 0.0)        # arealight
+    point1: tuple = (0.0, 0.0, 0.0)
+    point2: tuple = (0.0, 0.0, 0.0)
+    samples: int = 1
+    cast_shadows: bool = True
+
+
+@dataclass
+class Camera:
+    from_: tuple
+    to: tuple
+    up: tuple
+    resx: int
+    resy: int
+    focal: float = 1.0
+    aspect_ratio: float = 1.0
+    near_clip: float = 0.0
+    far_clip: float = -1.0
+
+
+@dataclass
+class Background:
+    color: tuple = (0.0, 0.0, 0.0)
+    power: float = 1.0
+
+
+@dataclass
+class Render:
+    integrator: str = "pathtracing"        # or "directlighting"
+    width: int = 64
+    height: int = 64
+    aa_samples: int = 1
+    filter_type: str = "box"
+    aa_pixelwidth: float = 1.0
+    tile_size: int = 32
+    bounces: int = 8
+    path_samples: int = 1
+    rr_min_bounces: int = 0
+    caustic_type: str = "path"
+    raydepth: int = 5
+    bg_transp: bool = False
+    shadow_bias_auto: bool = True
+    shadow_bias: float = 0.0005
+    ray_min_dist_auto: bool = True
+    ray_min_dist: float = 0.00005
+    base_sampling_offset: int = 0
+    clamp_samples: float = 0.0
+    accelerator: str = "yafaray-kdtree-original"
+
+
+@dataclass
+class Object:
+    name: str
+    v0: int            # first vertex (global index)
+    nv: int
+    t0: int            # first triangle (global index)
+    nt: int
+
+
+@dataclass
+class SceneSpec:
+    verts: np.ndarray                       # (N, 3) float32
+    tris: np.ndarray                        # (M, 3) int32 — global vertex indices
+    tri_mat: np.ndarray                     # (M,) int32 — index into materials
+    materials: List[Material]
+    lights: List[Light]
+    camera: Camera
+    render: Render
+    background: Optional[Background] = None
+    objects: List[Object] = field(default_factory=list)
+
+    def render_lights(self):
+        """Lights in the order the integrators see them: by name (render_view.cc:61, std::map)."""
+        return sorted(self.lights, key=lambda l: l.name)
+
+    def with_render(self, **kw):
+        import dataclasses
+        return dataclasses.replace(self, render=dataclasses.replace(self.render, **kw))
+
+    def with_camera(self, **kw):
+        import dataclasses
+        return dataclasses.replace(self, camera=dataclasses.replace(self.camera, **kw))
+
+
+# ---------------------------------------------------------------------------------------------
+# geometry helpers
+# ---------------------------------------------------------------------------------------------
+
+class _Builder:
+    def __init__(self):
+        self.verts, self.tris, self.tri_mat, self.objects = [], [], [], []
+
+    def add_object(self, name, verts, tris, mat):
+        v0, t0 = len(self.verts), len(self.tris)
+        self.verts.extend([tuple(map(float, v)) for v in verts])
+        self.tris.extend([(a + v0, b + v0, c + v0) for (a, b, c) in tris])
+        self.tri_mat.extend([mat] * len(tris))
+        self.objects.append(Object(name, v0, len(verts), t0, len(tris)))
+
+    def arrays(self):
+        return (np.asarray(self.verts, np.float32).reshape(-1, 3), np.asarray(self.tris, np.int32).reshape(-1, 3),
+                np.asarray(self.tri_mat, np.int32))
+
+
+def _quad(p0, p1, p2, p3):
+    return [p0, p1, p2, p3], [(0, 1, 2), (0, 2, 3)]
+
+
+def _box(cx, cy, sx, sy, h, angle_deg):
+    a = math.radians(angle_deg)
+    ca, sa = math.cos(a), math.sin(a)
+    corners = []
+    for dz in (0.0, h):
+        for (ux, uy) in ((-sx, -sy), (sx, -sy), (sx, sy), (-sx, sy)):
+            corners.append((cx + ux * ca - uy * sa, cy + ux * sa + uy * ca, dz))
+    tris = [(0, 2, 1), (0, 3, 2),            # bottom
+            (4, 5, 6), (4, 6, 7),            # top
+            (0, 1, 5), (0, 5, 4), (1, 2, 6), (1, 6, 5), (2, 3, 7), (2, 7, 6), (3, 0, 4), (3, 4, 7)]
+    return corners, tris
+
+
+def cornell(width=1920, height=1080, spp=64, bounces=8, rr=False, integrator="pathtracing",
+            filter_type="box", pixelwidth=1.0, light_samples=1, tile_size=32) -> SceneSpec:
+    """BASELINE C2: Cornell box, area light 0.5 x 0.5 at z = 1.98 facing down, power 6."""
+    b = _Builder()
+    mats = [Material("white", color=(0.75, 0.75, 0.75)), Material("red", color=(0.75, 0.1, 0.1)),
+            Material("green", color=(0.1, 0.75, 0.1))]
+    W, R, G = 0, 1, 2
+    b.add_object("floor", *_quad((-1, -1, 0), (1, -1, 0), (1, 1, 0), (-1, 1, 0)), W)
+    b.add_object("ceiling", *_quad((-1, -1, 2), (-1, 1, 2), (1, 1, 2), (1, -1, 2)), W)
+    b.add_object("back", *_quad((-1, 1, 0), (1, 1, 0), (1, 1, 2), (-1, 1, 2)), W)
+    b.add_object("left", *_quad((-1, -1, 0), (-1, 1, 0), (-1, 1, 2), (-1, -1, 2)), R)
+    b.add_object("right", *_quad((1, -1, 0), (1, -1, 2), (1, 1, 2), (1, 1, 0)), G)
+    b.add_object("short_box", *_box(0.35, -0.25, 0.3, 0.3, 0.6, -17.0), W)
+    b.add_object("tall_box", *_box(-0.35, 0.35, 0.3, 0.3, 1.2, 17.0), W)
+    verts, tris, tri_mat = b.arrays()
+    light = Light("area", type="arealight", color=(1.0, 1.0, 1.0), power=6.0, corner=(-0.25, -0.25, 1.98),
+                  point1=(-0.25, 0.25, 1.98), point2=(0.25, -0.25, 1.98), samples=light_samples)
+    cam = Camera(from_=(0.0, -3.9, 1.0), to=(0.0, 0.0, 1.0), up=(0.0, -3.9, 2.0), resx=width, resy=height,
+                 focal=1.4)
+    rend = Render(integrator=integrator, width=width, height=height, aa_samples=spp, filter_type=filter_type,
+                  aa_pixelwidth=pixelwidth, tile_size=tile_size, bounces=bounces, path_samples=1,
+                  rr_min_bounces=(0 if rr else bounces), caustic_type="none")
+    return SceneSpec(verts, tris, tri_mat, mats, [light], cam, rend, Background((0.0, 0.0, 0.0), 1.0), b.objects)
+
+
+def uv_sphere(n=707, center=(0.0, 0.0, 1.0), r=0.5):
+    """SURVEY.md §8d C4 generator: vertex (i, j) = r(sin t cos p, sin t sin p, cos t) + c,
+    t = pi i / n, p = 2 pi j / n; faces (a, c, b), (b, c, d) per quad -> n * n * 2 triangles."""
+    i = np.arange(n + 1, dtype=np.float64)[:, None]
+    j = np.arange(n, dtype=np.float64)[None, :]
+    th, ph = math.pi * i / n, 2.0 * math.pi * j / n
+    x = r * np.sin(th) * np.cos(ph) + center[0]
+    y = r * np.sin(th) * np.sin(ph) + center[1]
+    z = r * np.cos(th) * np.ones_like(ph) + center[2]
+    verts = np.stack([x, y, z], -1).reshape(-1, 3).astype(np.float32)
+    ii, jj = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    a = ii * n + jj
+    bb = ii * n + (jj + 1) % n
+    c = (ii + 1) * n + jj
+    d = (ii + 1) * n + (jj + 1) % n
+    tris = np.stack([np.stack([a, c, bb], -1), np.stack([bb, c, d], -1)], 2).reshape(-1, 3).astype(np.int32)
+    return verts, tris
+
+
+def cornell_sphere(n=707, **kw) -> SceneSpec:
+    """BASELINE C4: the C2 Cornell box plus a UV sphere (centre (0,0,1), r 0.5, white)."""
+    s = cornell(**kw)
+    sv, st = uv_sphere(n)
+    v0 = len(s.verts)
+    verts = np.concatenate([s.verts, sv])
+    tris = np.concatenate([s.tris, st + v0])
+    tri_mat = np.concatenate([s.tri_mat, np.zeros(len(st), np.int32)])
+    objs = list(s.objects) + [Object("sphere", v0, len(sv), len(s.tris), len(st))]
+    import dataclasses
+    return dataclasses.replace(s, verts=verts, tris=tris, tri_mat=tri_mat, objects=objs)
+
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+
+
+def test01(width=256, height=256, spp=4, filter_type="gauss", pixelwidth=1.5, tile_size=32) -> SceneSpec:
+    """BASELINE C1: the reference's test01 scene, textures stripped (diffuse colour only)."""
+    with open(os.path.join(GOLDEN_DIR, "test01_scene.json")) as f:
+        d = json.load(f)
+    b = _Builder()
+    mat_names = [m["name"] for m in d["materials"]]
+    mats = [Material(m["name"], color=tuple(m["color"]), diffuse_reflect=m["diffuse_reflect"], emit=m["emit"])
+            for m in d["materials"]]
+    for o in d["objects"]:
+        b.add_object(o["name"], o["verts"], o["tris"], mat_names.index(o["material"]))
+    verts, tris, tri_mat = b.arrays()
+    lights = [Light(l["name"], type="pointlight", color=tuple(l["color"]), power=l["power"], from_=tuple(l["from"]))
+              for l in d["lights"]]
+    c = d["camera"]
+    cam = Camera(from_=tuple(c["from"]), to=tuple(c["to"]), up=tuple(c["up"]), resx=width, resy=height,
+                 focal=c["focal"])
+    bg = Background(tuple(d["background"]["color"]), d["background"]["power"])
+    rend = Render(integrator="directlighting", width=width, height=height, aa_samples=spp,
+                  filter_type=filter_type, aa_pixelwidth=pixelwidth, tile_size=tile_size, raydepth=2)
+    return SceneSpec(verts, tris, tri_mat, mats, lights, cam, rend, bg, b.objects)
+
+
+# ---------------------------------------------------------------------------------------------
+# replay through the C API (the drop-in boundary)
+# ---------------------------------------------------------------------------------------------
+
+def apply(spec: SceneSpec, api) -> None:
+    """Issue the reference C-API call sequence for `spec` on `api` (a libyafaray_amd.Interface)."""
+    api.createScene()
+    for m in spec.materials:
+        api.paramsClearAll()
+        api.paramsSetString("type", m.type)
+        api.paramsSetColor("color", *m.color, 1.0)
+        if m.type == "light_mat":
+            api.paramsSetFloat("power", m.power)
+            api.paramsSetBool("double_sided", m.double_sided)
+        else:
+            api.paramsSetFloat("diffuse_reflect", m.diffuse_reflect)
+            api.paramsSetFloat("emit", m.emit)
+            api.paramsSetBool("receive_shadows", m.receive_shadows)
+            api.paramsSetBool("flat_material", m.flat_material)
+        api.createMaterial(m.name)
+    api.paramsClearAll()
+    for l in spec.lights:
+        api.paramsClearAll()
+        api.paramsSetString("type", l.type)
+        api.paramsSetColor("color", *l.color, 1.0)
+        api.paramsSetFloat("power", l.power)
+        api.paramsSetBool("cast_shadows", l.cast_shadows)
+        if l.type == "pointlight":
+            api.paramsSetVector("from", *l.from_)
+        else:
+            api.paramsSetVector("corner", *l.corner)
+            api.paramsSetVector("point1", *l.point1)
+            api.paramsSetVector("point2", *l.point2)
+            api.paramsSetInt("samples", l.samples)
+        api.createLight(l.name)
+    for o in spec.objects:
+        api.paramsClearAll()
+        api.paramsSetString("type", "mesh")
+        api.paramsSetInt("num_vertices", o.nv)
+        api.paramsSetInt("num_faces", o.nt)
+        api.paramsSetBool("has_orco", False)
+        api.paramsSetBool("has_uv", False)
+        api.createObject(o.name)
+        api.addVertices(spec.verts[o.v0:o.v0 + o.nv])
+        tri = spec.tris[o.t0:o.t0 + o.nt] - o.v0
+        mats = spec.tri_mat[o.t0:o.t0 + o.nt]
+        # setCurrentMaterial + addTriangle runs (object_mesh.cc:78-86)
+        start = 0
+        while start < len(tri):
+            end = start
+            while end < len(tri) and mats[end] == mats[start]:
+                end += 1
+            api.setCurrentMaterial(spec.materials[int(mats[start])].name)
+            api.addTriangles(tri[start:end])
+            start = end
+        api.endObject()
+    cam = spec.camera
+    api.paramsClearAll()
+    api.paramsSetString("type", "perspective")
+    api.paramsSetVector("from", *cam.from_)
+    api.paramsSetVector("to", *cam.to)
+    api.paramsSetVector("up", *cam.up)
+    api.paramsSetInt("resx", cam.resx)
+    api.paramsSetInt("resy", cam.resy)
+    api.paramsSetFloat("focal", cam.focal)
+    api.paramsSetFloat("aspect_ratio", cam.aspect_ratio)
+    api.paramsSetFloat("nearClip", cam.near_clip)
+    api.paramsSetFloat("farClip", cam.far_clip)
+    api.createCamera("cam")
+    api.paramsClearAll()
+    api.paramsSetString("camera_name", "cam")
+    api.createRenderView("")
+    if spec.background is not None:
+        api.paramsClearAll()
+        api.paramsSetString("type", "constant")
+        api.paramsSetColor("color", *spec.background.color, 1.0)
+        api.paramsSetFloat("power", spec.background.power)
+        api.createBackground("world_background")
+    r = spec.render
+    api.paramsClearAll()
+    api.paramsSetString("type", r.integrator)
+    api.paramsSetInt("raydepth", r.raydepth)
+    api.paramsSetBool("bg_transp", r.bg_transp)
+    if r.integrator == "pathtracing":
+        api.paramsSetInt("bounces", r.bounces)
+        api.paramsSetInt("path_samples", r.path_samples)
+        api.paramsSetInt("russian_roulette_min_bounces", r.rr_min_bounces)
+        api.paramsSetString("caustic_type", r.caustic_type)
+    api.createIntegrator("default")
+    api.paramsClearAll()
+    api.paramsSetString("type", "combined")
+    api.paramsSetString("image_type", "ColorAlpha")
+    api.defineLayer()
+    api.paramsClearAll()
+    api.paramsSetString("integrator_name", "default")
+    if spec.background is not None:
+        api.paramsSetString("background_name", "world_background")
+    api.paramsSetInt("width", r.width)
+    api.paramsSetInt("height", r.height)
+    api.paramsSetInt("AA_minsamples", r.aa_samples)
+    api.paramsSetInt("AA_passes", 1)
+    api.paramsSetString("filter_type", r.filter_type)
+    api.paramsSetFloat("AA_pixelwidth", r.aa_pixelwidth)
+    api.paramsSetFloat("AA_clamp_samples", r.clamp_samples)
+    api.paramsSetInt("tile_size", r.tile_size)
+    api.paramsSetString("tiles_order", "linear")
+    api.paramsSetBool("adv_auto_shadow_bias_enabled", r.shadow_bias_auto)
+    api.paramsSetFloat("adv_shadow_bias_value", r.shadow_bias)
+    api.paramsSetBool("adv_auto_min_raydist_enabled", r.ray_min_dist_auto)
+    api.paramsSetFloat("adv_min_raydist_value", r.ray_min_dist)
+    api.paramsSetInt("adv_base_sampling_offset", r.base_sampling_offset)
+    api.paramsSetString("scene_accelerator", r.accelerator)
+    api.paramsSetInt("threads", -1)
+    api.setupRender()
+    api.paramsClearAll()

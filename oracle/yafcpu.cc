@@ -1,0 +1,1615 @@
+// TEST INFRASTRUCTURE ONLY — CPU oracle (restatement) of libYafaRay's path-tracing hot path.
+// See yafcpu.h for scope and parity status.  Every function cites the reference file:line it
+// restates (paths relative to the reference repository root).  Built by oracle/Makefile with
+// -ffp-contract=off so that no FMA contraction happens (the reference Release build is plain
+// x86-64 SSE2, Appendix A.1 of SURVEY.md).
+
+#include "yafcpu.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <thread>
+#include <vector>
+
+namespace yc
+{
+using LD = long double;
+
+// include/math/math.h:46-88 — x87 long double constants (the promotions matter for parity).
+constexpr LD num_pi = 3.1415926535897932384626433832795L;
+constexpr LD div_pi_by_2 = 1.5707963267948966192313216916398L;
+constexpr LD div_1_by_pi = 0.31830988618379067153776752674503L;
+constexpr LD mult_pi_by_2 = 6.283185307179586476925286766559L;
+constexpr LD div_1_by_2pi = 0.15915494309189533576888376337251L;
+constexpr LD div_4_by_pi = 1.2732395447351626861510701069801L;
+constexpr LD div_4_by_squared_pi = 0.40528473456935108577551785283891L;
+constexpr LD log2e = 1.4426950408889634073599246810019L;
+constexpr LD ln2 = 0.69314718055994530941723212145818L;
+constexpr LD sample_mult_ratio = 0.00000000023283064365386962890625L;
+constexpr float min_raydist_global = 0.00005f;   // include/common/yafaray_common.h:28
+
+// ---------------------------------------------------------------------------------------------
+// math (include/math/math.h)
+// ---------------------------------------------------------------------------------------------
+
+// math.h:218-245 (FAST_TRIG parabolic sine)
+static inline float fsin(float x)
+{
+	if(x > mult_pi_by_2 || x < -mult_pi_by_2) x -= ((int)(x * static_cast<float>(div_1_by_2pi))) * static_cast<float>(mult_pi_by_2);
+	if(x < -num_pi) x += static_cast<float>(mult_pi_by_2);
+	else if(x > num_pi) x -= static_cast<float>(mult_pi_by_2);
+	x = (static_cast<float>(div_4_by_pi * x)) - (static_cast<float>(div_4_by_squared_pi * x * std::abs(x)));
+	const float result = 0.225f * (x * std::abs(x) - x) + x;
+	if(result <= -1.f) return -1.f;
+	else if(result >= 1.f) return 1.f;
+	return result;
+}
+
+// math.h:247-254
+static inline float fcos(float x) { return fsin(x + static_cast<float>(div_pi_by_2)); }
+
+// math.h:144-169 + 199-206: FAST_MATH sqrt is std::sqrt on x86-64.
+static inline float fsqrt(float x) { return std::sqrt(x); }
+
+union BitTw { int i; float f; };
+
+// math.h:96-125
+static inline float polyexp(float x)
+{
+	return x * (x * (x * (x * (x * 1.8775767e-3f + 8.9893397e-3f) + 5.5826318e-2f) + 2.4015361e-1f) + 6.9315308e-1f) + 9.9999994e-1f;
+}
+static inline float fexp2(float x)
+{
+	BitTw ip, fp, ep;
+	x = std::min(x, 129.00000f);
+	x = std::max(x, -126.99999f);
+	ip.i = static_cast<int>(x - 0.5f);
+	fp.f = (x - static_cast<float>(ip.i));
+	ep.i = ((ip.i + 127) << 23);
+	return ep.f * polyexp(fp.f);
+}
+// math.h:183-188 (FAST_MATH exp)
+static inline float fexp(float a) { return fexp2(static_cast<float>(log2e * a)); }
+
+// math.h:268-296 (FAST_INT disabled)
+static inline int roundToInt(double v) { return static_cast<int>(v + (.5 - 1.4e-11)); }
+static inline int floorToInt(double v) { return static_cast<int>(std::floor(v)); }
+
+// ---------------------------------------------------------------------------------------------
+// geometry (include/geometry/vector.h)
+// ---------------------------------------------------------------------------------------------
+struct V3
+{
+	float x = 0.f, y = 0.f, z = 0.f;
+	V3() = default;
+	V3(float a, float b, float c) : x(a), y(b), z(c) {}
+	float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+	float &operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+	float lengthSqr() const { return x * x + y * y + z * z; }
+	float length() const { return fsqrt(lengthSqr()); }
+	// vector.h:201-210
+	V3 &normalize()
+	{
+		float len = lengthSqr();
+		if(len != 0.f)
+		{
+			len = 1.f / fsqrt(len);
+			x *= len; y *= len; z *= len;
+		}
+		return *this;
+	}
+	// vector.h:234-243
+	float normLen()
+	{
+		float vl = lengthSqr();
+		if(vl != 0.f)
+		{
+			vl = fsqrt(vl);
+			const float d = 1.f / vl;
+			x *= d; y *= d; z *= d;
+		}
+		return vl;
+	}
+	V3 &operator+=(const V3 &s) { x += s.x; y += s.y; z += s.z; return *this; }
+	V3 &operator*=(float s) { x *= s; y *= s; z *= s; return *this; }
+};
+// vector.h:108-186
+static inline float dot(const V3 &a, const V3 &b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline V3 operator*(float f, const V3 &v) { return {f * v.x, f * v.y, f * v.z}; }
+static inline V3 operator*(const V3 &v, float f) { return {f * v.x, f * v.y, f * v.z}; }
+static inline V3 operator^(const V3 &a, const V3 &b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+static inline V3 operator-(const V3 &a, const V3 &b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline V3 operator+(const V3 &a, const V3 &b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static inline V3 operator-(const V3 &v) { return {-v.x, -v.y, -v.z}; }
+
+// vector.h:262-276
+static inline void createCoordsSystem(const V3 &n, V3 &u, V3 &v)
+{
+	if((n.x == 0.f) && (n.y == 0.f))
+	{
+		u = (n.z < 0.f ? V3{-1.f, 0.f, 0.f} : V3{1.f, 0.f, 0.f});
+		v = V3{0.f, 1.f, 0.f};
+	}
+	else
+	{
+		const float d = 1.f / fsqrt(n.y * n.y + n.x * n.x);
+		u = V3{n.y * d, -n.x * d, 0.f};
+		v = n ^ u;
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// colour (include/color/color.h)
+// ---------------------------------------------------------------------------------------------
+struct C3
+{
+	float r = 0.f, g = 0.f, b = 0.f;
+	C3() = default;
+	explicit C3(float f) : r(f), g(f), b(f) {}
+	C3(float a, float bb, float c) : r(a), g(bb), b(c) {}
+	bool isBlack() const { return r == 0 && g == 0 && b == 0; }
+	float maximum() const { return std::max(r, std::max(g, b)); }
+	C3 &operator+=(const C3 &c) { r += c.r; g += c.g; b += c.b; return *this; }
+	C3 &operator*=(const C3 &c) { r *= c.r; g *= c.g; b *= c.b; return *this; }
+	C3 &operator*=(float f) { r *= f; g *= f; b *= f; return *this; }
+	// color.h:415-440
+	void clampProportional(float max_value)
+	{
+		if(max_value > 0.f)
+		{
+			const float max_rgb = std::max(r, std::max(g, b));
+			const float adj = max_value / max_rgb;
+			if(max_rgb > max_value)
+			{
+				if(r >= max_rgb) { r = max_value; g *= adj; b *= adj; }
+				else if(g >= max_rgb) { g = max_value; r *= adj; b *= adj; }
+				else { b = max_value; r *= adj; g *= adj; }
+			}
+		}
+	}
+};
+static inline C3 operator*(const C3 &a, const C3 &b) { return {a.r * b.r, a.g * b.g, a.b * b.b}; }
+static inline C3 operator*(float f, const C3 &c) { return {f * c.r, f * c.g, f * c.b}; }
+static inline C3 operator*(const C3 &c, float f) { return {f * c.r, f * c.g, f * c.b}; }
+static inline C3 operator/(const C3 &c, float f) { return {c.r / f, c.g / f, c.b / f}; }
+static inline C3 operator+(const C3 &a, const C3 &b) { return {a.r + b.r, a.g + b.g, a.b + b.b}; }
+
+// ---------------------------------------------------------------------------------------------
+// samplers (include/sampler/sample.h, include/sampler/halton.h, src/sampler/halton.cc,
+// include/math/random.h)
+// ---------------------------------------------------------------------------------------------
+// sample.h:102-110
+static inline float riVdC(uint32_t bits, uint32_t r = 0)
+{
+	bits = (bits << 16) | (bits >> 16);
+	bits = ((bits & 0x00ff00ff) << 8) | ((bits & 0xff00ff00) >> 8);
+	bits = ((bits & 0x0f0f0f0f) << 4) | ((bits & 0xf0f0f0f0) >> 4);
+	bits = ((bits & 0x33333333) << 2) | ((bits & 0xcccccccc) >> 2);
+	bits = ((bits & 0x55555555) << 1) | ((bits & 0xaaaaaaaa) >> 1);
+	return std::max(0.f, std::min(1.f, static_cast<float>(static_cast<double>(bits ^ r) * sample_mult_ratio)));
+}
+// sample.h:112-117 (Sobol generator matrix: v ^= v >> 1)
+static inline float riS(uint32_t i, uint32_t r = 0)
+{
+	for(uint32_t v = 1u << 31; i; i >>= 1, v ^= v >> 1)
+		if(i & 1) r ^= v;
+	return std::max(0.f, std::min(1.f, static_cast<float>(static_cast<double>(r) * sample_mult_ratio)));
+}
+// sample.h:119-124 (Larcher-Pillichshammer: v |= v >> 1)
+static inline float riLp(uint32_t i, uint32_t r = 0)
+{
+	for(uint32_t v = 1u << 31; i; i >>= 1, v |= v >> 1)
+		if(i & 1) r ^= v;
+	return std::max(0.f, std::min(1.f, static_cast<float>(static_cast<double>(r) * sample_mult_ratio)));
+}
+// sample.h:132-149 (FNV-1a over the 4 little-endian bytes)
+static inline uint32_t fnv32(uint32_t value)
+{
+	uint32_t hash = 0x811c9dc5u;
+	for(int k = 0; k < 4; ++k)
+	{
+		hash ^= (value >> (8 * k)) & 0xffu;
+		hash *= 0x01000193u;
+	}
+	return hash;
+}
+
+// sample.h:45-54 — note the long double product s_2 * 2pi before the float conversion.
+static inline V3 cosHemisphere(const V3 &n, const V3 &ru, const V3 &rv, float s_1, float s_2)
+{
+	if(s_1 >= 1.0f) return n;
+	const float z_1 = s_1;
+	const float z_2 = static_cast<float>(s_2 * mult_pi_by_2);
+	const V3 a = ru * fcos(z_2);
+	const V3 b = rv * fsin(z_2);
+	return (a + b) * fsqrt(1.f - z_1) + n * fsqrt(z_1);
+}
+
+// halton.h:41-81
+struct Halton
+{
+	uint32_t base;
+	double inv_base, value;
+	explicit Halton(int b) : base(b), inv_base(1.0 / static_cast<double>(b)), value(0.0) {}
+	Halton(int b, uint32_t start) : Halton(b) { setStart(start); }
+	void setStart(uint32_t start)
+	{
+		double factor = inv_base;
+		value = 0.0;
+		while(start > 0)
+		{
+			value += static_cast<double>(start % base) * factor;
+			start /= base;
+			factor *= inv_base;
+		}
+	}
+	float getNext()
+	{
+		const double r = 0.9999999999 - value;
+		if(inv_base < r) value += inv_base;
+		else
+		{
+			double hh = 0.0, h = inv_base;
+			while(h >= r)
+			{
+				hh = h;
+				h *= inv_base;
+			}
+			value += hh + h - 1.0;
+		}
+		return std::max(0.f, std::min(1.f, static_cast<float>(value)));
+	}
+};
+
+// Faure digit permutations (halton.cc:26-401 holds them as literal tables; here they are
+// generated by Faure's recursive construction and checked against the reference tables
+// through oracle/_ref).  sigma_2 = identity; sigma_2b = (2*sigma_b, 2*sigma_b + 1);
+// sigma_{2b+1} = sigma_2b with entries >= b shifted up by one and b inserted in the middle.
+static std::vector<int> faurePerm(int b)
+{
+	if(b <= 2) return {0, 1};
+	if((b & 1) == 0)
+	{
+		const std::vector<int> h = faurePerm(b / 2);
+		std::vector<int> out;
+		for(int v : h) out.push_back(2 * v);
+		for(int v : h) out.push_back(2 * v + 1);
+		return out;
+	}
+	const std::vector<int> p = faurePerm(b - 1);
+	const int c = (b - 1) / 2;
+	std::vector<int> out;
+	for(int i = 0; i < static_cast<int>(p.size()); ++i)
+	{
+		if(i == c) out.push_back(c);
+		out.push_back(p[i] + (p[i] >= c ? 1 : 0));
+	}
+	return out;
+}
+
+struct FaureTables
+{
+	int prims[50];
+	double inv_prims[50];
+	std::vector<int> sigma[50];
+	FaureTables()
+	{
+		// halton.cc:409-414: prims[0] = 1, then the first 49 primes; inv_prims are 1/p rounded to
+		// 9 decimals (literal decimal constants in the reference, reproduced exactly as n / 1e9).
+		int p = 1, k = 0;
+		prims[k++] = 1;
+		for(int c = 2; k < 50; ++c)
+		{
+			bool pr = true;
+			for(int d = 2; d * d <= c; ++d) if(c % d == 0) { pr = false; break; }
+			if(pr) prims[k++] = c;
+		}
+		(void)p;
+		for(int i = 0; i < 50; ++i)
+		{
+			inv_prims[i] = static_cast<double>(std::llround(1e9 / prims[i])) / 1e9;
+			// halton.cc:403-407: dims 0..2 share the base-3 table
+			sigma[i] = faurePerm(i <= 2 ? 3 : prims[i]);
+		}
+	}
+};
+static const FaureTables &faure()
+{
+	static const FaureTables t;
+	return t;
+}
+
+// halton.cc:421-441
+static double lowDiscrepancySampling(int dim, uint32_t n)
+{
+	double value = 0.0;
+	if(dim == 0) return 0.0;  // base 1: the reference loops forever for n > 0; never used
+	if(dim < 50)
+	{
+		const FaureTables &t = faure();
+		const std::vector<int> &sigma = t.sigma[dim];
+		const uint32_t base = t.prims[dim];
+		const double f = t.inv_prims[dim];
+		double dn = static_cast<double>(n);
+		double factor = f;
+		while(n > 0)
+		{
+			value += static_cast<double>(sigma[n % base]) * factor;
+			dn *= f;
+			n = static_cast<uint32_t>(dn);
+			factor *= f;
+		}
+	}
+	return value;
+}
+
+// random.h:56-104 (MWC)
+struct Mwc
+{
+	uint32_t x = 30903, c = 0;
+	explicit Mwc(uint32_t seed) : c(seed) {}
+	double operator()()
+	{
+		const uint32_t a = 1791398085u, ah = a >> 16, al = a & 65535u;
+		const uint32_t xh = x >> 16, xl = x & 65535u;
+		x = x * a + c;
+		c = xh * ah + ((xh * al) >> 16) + ((xl * ah) >> 16);
+		if(xl * al >= ~c + 1) c++;
+		return static_cast<double>(static_cast<LD>(x) * sample_mult_ratio);
+	}
+};
+
+// ---------------------------------------------------------------------------------------------
+// film filter (include/math/filter.h:34-90, src/render/imagefilm.cc:129-162)
+// ---------------------------------------------------------------------------------------------
+static float filterBox(float, float) { return 1.f; }
+static float filterGauss(float dx, float dy)
+{
+	const float r_2 = dx * dx + dy * dy;
+	return std::max(0.f, fexp(-6 * r_2) - 0.00247875f);
+}
+static float filterMitchell(float dx, float dy)
+{
+	const float x = 2.f * fsqrt(dx * dx + dy * dy);
+	if(x >= 2.f) return 0.f;
+	if(x >= 1.f) return x * (x * (x * -0.38888889f + 2.0f) - 3.33333333f) + 1.77777778f;
+	return x * x * (1.16666666f * x - 2.0f) + 0.88888889f;
+}
+static float filterLanczos(float dx, float dy)
+{
+	const float x = fsqrt(dx * dx + dy * dy);
+	if(x == 0.f) return 1.f;
+	if(-2 < x && x < 2)
+	{
+		const float a = static_cast<float>(num_pi * x);
+		const float b = static_cast<float>(div_pi_by_2 * x);
+		return (fsin(a) * fsin(b)) / (a * b);
+	}
+	return 0.f;
+}
+
+struct FilmTable
+{
+	float table[256];
+	float filterw, table_scale;
+	FilmTable(int filter, float filter_size)
+	{
+		// imagefilm.cc:129 filterw_(filter_size * 0.5), 144-151, 153-162
+		filterw = static_cast<float>(filter_size * 0.5);
+		float (*ff)(float, float) = filterBox;
+		switch(filter)
+		{
+			case YC_FILTER_MITCHELL: ff = filterMitchell; filterw *= 2.6f; break;
+			case YC_FILTER_LANCZOS: ff = filterLanczos; break;
+			case YC_FILTER_GAUSS: ff = filterGauss; filterw *= 2.f; break;
+			default: ff = filterBox; break;
+		}
+		filterw = std::min(std::max(0.501f, filterw), 0.5f * 8);
+		const float scale = 1.f / 16.f;
+		for(int y = 0; y < 16; ++y)
+			for(int x = 0; x < 16; ++x) table[y * 16 + x] = ff((x + .5f) * scale, (y + .5f) * scale);
+		table_scale = static_cast<float>(0.9999 * 16 / filterw);
+	}
+};
+
+// ---------------------------------------------------------------------------------------------
+// scene restatement
+// ---------------------------------------------------------------------------------------------
+enum BsdfFlags : unsigned
+{
+	BNone = 0, BSpecular = 1 << 0, BGlossy = 1 << 1, BDiffuse = 1 << 2, BDispersive = 1 << 3,
+	BReflect = 1 << 4, BTransmit = 1 << 5, BFilter = 1 << 6, BEmit = 1 << 7, BVolumetric = 1 << 8,
+	BAll = BSpecular | BGlossy | BDiffuse | BDispersive | BReflect | BTransmit | BFilter
+};
+
+struct Material
+{
+	int type = YC_MAT_SHINYDIFFUSE;
+	unsigned bsdf_flags = BNone;
+	C3 diffuse_color, emit_color, light_col;
+	float components[4] = {0.f, 0.f, 0.f, 0.f};
+	bool is_diffuse = false, double_sided = false, receive_shadows = true, flat = false;
+	int n_bsdf = 0;
+	unsigned c_flags[4];
+	int c_index[4];
+};
+
+struct Light
+{
+	int type = YC_LIGHT_POINT;
+	bool cast_shadows = true;
+	C3 color;
+	V3 position;
+	// area light (light_area.cc:33-53)
+	V3 corner, to_x, to_y, fnormal, normal, du, dv, c2, c3, c4;
+	float area = 0.f, inv_area = 0.f;
+	int samples = 1;
+};
+
+struct Tri
+{
+	V3 v0, v1, v2, ng;
+	int mat;
+};
+
+struct Camera
+{
+	V3 position, vright, vup, vto, cam_z;
+	V3 near_p, far_p;
+	int resx, resy;
+};
+
+struct Ray
+{
+	V3 from, dir;
+	float tmin = 0.f, tmax = -1.f;
+};
+
+struct SurfacePoint
+{
+	V3 p, n, ng, nu, nv;
+	const Material *mat = nullptr;
+	int prim = -1;
+	unsigned bsdf_flags = 0;
+};
+
+struct IsectData
+{
+	bool hit = false;
+	float t = 0.f, bu = 0.f, bv = 0.f, bw = 0.f;
+	int prim = -1;
+};
+
+// primitive_triangle.cc:44-71 (Moller-Trumbore with the reference's edge-scaled epsilon)
+static inline IsectData triIntersect(const Tri &tr, const Ray &ray)
+{
+	IsectData d;
+	const V3 edge_1 = tr.v1 - tr.v0;
+	const V3 edge_2 = tr.v2 - tr.v0;
+	const float epsilon = 0.1f * min_raydist_global * std::max(edge_1.length(), edge_2.length());
+	const V3 pvec = ray.dir ^ edge_2;
+	const float det = dot(edge_1, pvec);
+	if(det > -epsilon && det < epsilon) return d;
+	const float inv_det = 1.f / det;
+	const V3 tvec = ray.from - tr.v0;
+	const float u = dot(tvec, pvec) * inv_det;
+	if(u < 0.f || u > 1.f) return d;
+	const V3 qvec = tvec ^ edge_1;
+	const float v = dot(ray.dir, qvec) * inv_det;
+	if((v < 0.f) || ((u + v) > 1.f)) return d;
+	const float t = dot(edge_2, qvec) * inv_det;
+	if(t < epsilon) return d;
+	d.hit = true;
+	d.t = t;
+	d.bu = 1.f - u - v;
+	d.bv = u;
+	d.bw = v;
+	return d;
+}
+
+// Plain binary BVH used only to make the oracle fast enough on big meshes.  Boxes are padded
+// so that culling is conservative: the closest / any hit returned is the one the reference's
+// exhaustive semantics define (accelerator_kdtree.cc:726-746, 851-873); only exact-t ties
+// between different primitives may resolve differently.
+struct BvhNode
+{
+	double lo[3], hi[3];
+	int left = -1, right = -1, start = 0, count = 0;
+};
+
+class Scene
+{
+	public:
+		std::vector<Tri> tris;
+		std::vector<Material> mats;
+		std::vector<Light> lights;
+		Camera cam;
+		yc_render rp;
+		std::unique_ptr<FilmTable> film;
+		std::vector<BvhNode> nodes;
+		std::vector<int> order;
+
+		explicit Scene(const yc_scene &s);
+		IsectData intersect(const Ray &ray, float t_max, bool any, uint64_t *ctr) const;
+		void buildBvh();
+		int buildRec(int start, int end, std::vector<V3> &cent);
+};
+
+Scene::Scene(const yc_scene &s)
+{
+	rp = s.rp;
+	// materials: material_shiny_diffuse.cc:28-87 (ctor + config), material_simple.cc:36-70
+	for(int i = 0; i < s.n_mats; ++i)
+	{
+		const yc_material &m = s.mats[i];
+		Material mm;
+		mm.type = m.type;
+		mm.receive_shadows = m.receive_shadows != 0;
+		mm.flat = m.flat_material != 0;
+		if(m.type == YC_MAT_LIGHT)
+		{
+			mm.bsdf_flags = BEmit;
+			mm.light_col = C3(m.color[0], m.color[1], m.color[2]);
+			mm.double_sided = m.double_sided != 0;
+		}
+		else
+		{
+			mm.diffuse_color = C3(m.color[0], m.color[1], m.color[2]);
+			mm.emit_color = m.emit_strength * mm.diffuse_color;
+			if(m.emit_strength > 0.f) mm.bsdf_flags |= BEmit;
+			float acc = 1.f;
+			if(m.diffuse_strength * acc > 0.00001f)
+			{
+				mm.is_diffuse = true;
+				mm.bsdf_flags |= BDiffuse | BReflect;
+				mm.c_flags[mm.n_bsdf] = BDiffuse | BReflect;
+				mm.c_index[mm.n_bsdf] = 3;
+				++mm.n_bsdf;
+			}
+			// material_shiny_diffuse.cc:92-105 getComponents (no shader nodes)
+			mm.components[3] = mm.is_diffuse ? m.diffuse_strength : 0.f;
+		}
+		mats.push_back(mm);
+	}
+	// lights: light_point.cc:28-35, light_area.cc:33-53
+	for(int i = 0; i < s.n_lights; ++i)
+	{
+		const yc_light &l = s.lights[i];
+		Light L;
+		L.type = l.type;
+		L.cast_shadows = l.cast_shadows != 0;
+		const C3 col(l.color[0], l.color[1], l.color[2]);
+		if(l.type == YC_LIGHT_POINT)
+		{
+			L.position = V3(l.from[0], l.from[1], l.from[2]);
+			L.color = col * l.power;
+		}
+		else
+		{
+			L.corner = V3(l.from[0], l.from[1], l.from[2]);
+			const V3 p1(l.point1[0], l.point1[1], l.point1[2]), p2(l.point2[0], l.point2[1], l.point2[2]);
+			L.to_x = p1 - L.corner;
+			L.to_y = p2 - L.corner;
+			L.samples = l.samples;
+			L.fnormal = L.to_y ^ L.to_x;
+			L.color = col * l.power * static_cast<float>(num_pi);
+			L.area = L.fnormal.normLen();
+			L.inv_area = static_cast<float>(1.0 / L.area);
+			L.normal = -L.fnormal;
+			L.du = L.to_x;
+			L.du.normalize();
+			L.dv = L.normal ^ L.du;
+			L.c2 = L.corner + L.to_x;
+			L.c3 = L.corner + (L.to_x + L.to_y);
+			L.c4 = L.corner + L.to_y;
+		}
+		lights.push_back(L);
+	}
+	// geometry: primitive_triangle.cc:34-37 + 87-95 (geometric normal), object_mesh.cc:78-86
+	for(int i = 0; i < s.n_tris; ++i)
+	{
+		Tri t;
+		const int *idx = s.tris + 3 * i;
+		t.v0 = V3(s.verts[3 * idx[0]], s.verts[3 * idx[0] + 1], s.verts[3 * idx[0] + 2]);
+		t.v1 = V3(s.verts[3 * idx[1]], s.verts[3 * idx[1] + 1], s.verts[3 * idx[1] + 2]);
+		t.v2 = V3(s.verts[3 * idx[2]], s.verts[3 * idx[2] + 1], s.verts[3 * idx[2] + 2]);
+		t.ng = ((t.v1 - t.v0) ^ (t.v2 - t.v0)).normalize();
+		t.mat = s.tri_mat[i];
+		tris.push_back(t);
+	}
+	// camera: camera.cc:51-71, camera_perspective.cc:28-69 (no depth of field)
+	const yc_camera &c = s.cam;
+	const V3 pos(c.from[0], c.from[1], c.from[2]), look(c.to[0], c.to[1], c.to[2]), up(c.up[0], c.up[1], c.up[2]);
+	cam.resx = c.resx;
+	cam.resy = c.resy;
+	const float aspect_ratio = c.aspect * (float)c.resy / (float)c.resx;
+	V3 cam_y = up - pos;
+	V3 cam_z = look - pos;
+	V3 cam_x = cam_z ^ cam_y;
+	cam_y = cam_z ^ cam_x;
+	cam_x.normalize();
+	cam_y.normalize();
+	cam_z.normalize();
+	cam.position = pos;
+	cam.cam_z = cam_z;
+	cam.near_p = pos + cam_z * c.near_clip;
+	cam.far_p = pos + cam_z * c.far_clip;
+	cam.vright = cam_x;
+	cam.vup = aspect_ratio * cam_y;
+	cam.vto = (cam_z * c.focal) - V3(static_cast<float>(0.5) * (cam.vup + cam.vright));
+	cam.vup = V3(cam.vup.x / (float)c.resy, cam.vup.y / (float)c.resy, cam.vup.z / (float)c.resy);
+	cam.vright = V3(cam.vright.x / (float)c.resx, cam.vright.y / (float)c.resx, cam.vright.z / (float)c.resx);
+	film.reset(new FilmTable(rp.filter, rp.filter_size));
+	buildBvh();
+}
+
+int Scene::buildRec(int start, int end, std::vector<V3> &cent)
+{
+	BvhNode n;
+	for(int k = 0; k < 3; ++k) { n.lo[k] = 1e300; n.hi[k] = -1e300; }
+	for(int i = start; i < end; ++i)
+	{
+		const Tri &t = tris[order[i]];
+		for(int k = 0; k < 3; ++k)
+		{
+			n.lo[k] = std::min(n.lo[k], (double)std::min(t.v0[k], std::min(t.v1[k], t.v2[k])));
+			n.hi[k] = std::max(n.hi[k], (double)std::max(t.v0[k], std::max(t.v1[k], t.v2[k])));
+		}
+	}
+	for(int k = 0; k < 3; ++k)
+	{
+		const double pad = 1e-5 * (std::fabs(n.lo[k]) + std::fabs(n.hi[k]) + (n.hi[k] - n.lo[k])) + 1e-9;
+		n.lo[k] -= pad;
+		n.hi[k] += pad;
+	}
+	const int id = (int)nodes.size();
+	nodes.push_back(n);
+	if(end - start <= 4)
+	{
+		nodes[id].start = start;
+		nodes[id].count = end - start;
+		return id;
+	}
+	int axis = 0;
+	double ext = -1;
+	for(int k = 0; k < 3; ++k)
+		if(nodes[id].hi[k] - nodes[id].lo[k] > ext) { ext = nodes[id].hi[k] - nodes[id].lo[k]; axis = k; }
+	const int mid = (start + end) / 2;
+	std::nth_element(order.begin() + start, order.begin() + mid, order.begin() + end,
+					 [&](int a, int b) { return cent[a][axis] < cent[b][axis] || (cent[a][axis] == cent[b][axis] && a < b); });
+	const int l = buildRec(start, mid, cent);
+	const int r = buildRec(mid, end, cent);
+	nodes[id].left = l;
+	nodes[id].right = r;
+	return id;
+}
+
+void Scene::buildBvh()
+{
+	order.resize(tris.size());
+	std::vector<V3> cent(tris.size());
+	for(size_t i = 0; i < tris.size(); ++i)
+	{
+		order[i] = (int)i;
+		for(int k = 0; k < 3; ++k) cent[i][k] = (tris[i].v0[k] + tris[i].v1[k] + tris[i].v2[k]) / 3.f;
+	}
+	nodes.clear();
+	if(!tris.empty()) buildRec(0, (int)tris.size(), cent);
+}
+
+static inline bool boxHit(const BvhNode &n, const Ray &ray, double t0, double t1)
+{
+	double tn = t0, tf = t1;
+	for(int k = 0; k < 3; ++k)
+	{
+		const double o = ray.from[k], d = ray.dir[k];
+		if(d == 0.0)
+		{
+			if(o < n.lo[k] || o > n.hi[k]) return false;
+			continue;
+		}
+		double a = (n.lo[k] - o) / d, b = (n.hi[k] - o) / d;
+		if(a > b) std::swap(a, b);
+		tn = std::max(tn, a);
+		tf = std::min(tf, b);
+		if(tn > tf) return false;
+	}
+	return true;
+}
+
+// closest: accelerator_kdtree.cc:726-746 (t < t_max && t >= ray.tmin); any: :851-873
+// (t < t_max && t >= 0).  All primitives are "normal" visibility here.
+IsectData Scene::intersect(const Ray &ray, float t_max, bool any, uint64_t *ctr) const
+{
+	if(ctr) ++*ctr;
+	IsectData best;
+	float best_t = t_max;
+	if(nodes.empty()) return best;
+	int stack[128];
+	int sp = 0;
+	stack[sp++] = 0;
+	const double lo_t = -1e-3 * (1.0 + std::fabs(ray.tmin));
+	while(sp)
+	{
+		const BvhNode &n = nodes[stack[--sp]];
+		const double hi_t = std::isinf(best_t) ? 1e300 : (double)best_t * (1.0 + 1e-5) + 1e-6;
+		if(!boxHit(n, ray, lo_t, hi_t)) continue;
+		if(n.count)
+		{
+			for(int i = n.start; i < n.start + n.count; ++i)
+			{
+				const int pi = order[i];
+				IsectData d = triIntersect(tris[pi], ray);
+				if(!d.hit) continue;
+				if(any)
+				{
+					if(d.t < t_max && d.t >= 0.f) { d.prim = pi; return d; }
+				}
+				else if(d.t < best_t && d.t >= ray.tmin)
+				{
+					// keep the lower primitive index on exact ties so the result is order-free
+					d.prim = pi;
+					best = d;
+					best_t = d.t;
+				}
+				else if(d.t == best_t && best.hit && pi < best.prim && d.t >= ray.tmin)
+				{
+					d.prim = pi;
+					best = d;
+				}
+			}
+		}
+		else
+		{
+			stack[sp++] = n.left;
+			stack[sp++] = n.right;
+		}
+	}
+	return best;
+}
+
+// ---------------------------------------------------------------------------------------------
+// render-side restatement
+// ---------------------------------------------------------------------------------------------
+struct Sample
+{
+	float s_1, s_2, pdf = 0.f;
+	unsigned flags, sampled_flags = BNone;
+	Sample(float a, float b, unsigned f) : s_1(a), s_2(b), flags(f) {}
+};
+
+struct LSample
+{
+	float s_1, s_2;
+	C3 col;
+	float pdf;
+};
+
+class Renderer
+{
+	public:
+		Renderer(const Scene &s) : sc_(s) {}
+		const Scene &sc_;
+		std::atomic<uint64_t> n_closest{0}, n_shadow{0};
+
+		// per-thread state
+		struct Thread
+		{
+			uint64_t closest = 0, shadow = 0;
+			uint32_t correlative = 0;
+		};
+
+		// accelerator.cc:55-67 + primitive_triangle.cc:97-176 (flat-shaded, no UV/orco use)
+		bool intersect(Thread &th, Ray &ray, SurfacePoint &sp) const
+		{
+			const float t_max = (ray.tmax >= 0.f) ? ray.tmax : std::numeric_limits<float>::infinity();
+			const IsectData d = sc_.intersect(ray, t_max, false, &th.closest);
+			if(!d.hit) return false;
+			const Tri &tr = sc_.tris[d.prim];
+			sp.p = ray.from + d.t * ray.dir;
+			sp.ng = tr.ng;
+			sp.n = tr.ng;
+			createCoordsSystem(sp.n, sp.nu, sp.nv);
+			sp.mat = &sc_.mats[tr.mat];
+			sp.bsdf_flags = sp.mat->bsdf_flags;
+			sp.prim = d.prim;
+			ray.tmax = d.t;
+			return true;
+		}
+		// accelerator.cc:69-78
+		bool isShadowed(Thread &th, const Ray &ray) const
+		{
+			Ray sray = ray;
+			sray.from += sray.dir * sray.tmin;
+			const float t_max = (ray.tmax >= 0.f) ? sray.tmax - 2 * sray.tmin : std::numeric_limits<float>::infinity();
+			return sc_.intersect(sray, t_max, true, &th.shadow).hit;
+		}
+
+		// surface.h:62-65
+		static V3 faceForward(const V3 &ng, const V3 &n, const V3 &wo) { return (dot(ng, wo) < 0) ? -n : n; }
+
+		// material_shiny_diffuse.cc:107-119 accumulate (Kr = 1: no Fresnel)
+		static void accumulate(const float *c, float kr, float *a)
+		{
+			a[0] = c[0] * kr;
+			float acc = 1.f - a[0];
+			a[1] = c[1] * acc;
+			acc *= 1.f - c[1];
+			a[2] = c[2] * acc;
+			acc *= 1.f - c[2];
+			a[3] = c[3] * acc;
+		}
+
+		// material_shiny_diffuse.cc:190-228
+		C3 eval(const SurfacePoint &sp, const V3 &wo, const V3 &wl, unsigned bsdfs) const
+		{
+			const Material &m = *sp.mat;
+			if(m.type == YC_MAT_LIGHT) return C3(0.f);
+			const V3 n = faceForward(sp.ng, sp.n, wo);
+			if(!(bsdfs & (m.bsdf_flags & BDiffuse))) return C3(0.f);
+			const float m_t = (1.f - 1.f * m.components[0]) * (1.f - m.components[1]);
+			if(dot(n, wl) < 0.0 && !m.flat) return C3(0.f);
+			const float m_d = m_t * (1.f - m.components[2]) * m.components[3];
+			return m_d * m.diffuse_color;
+		}
+
+		// material_shiny_diffuse.cc:237-242, material_simple.cc:50-55
+		C3 emit(const SurfacePoint &sp, const V3 &wo) const
+		{
+			const Material &m = *sp.mat;
+			if(m.type == YC_MAT_LIGHT)
+			{
+				if(m.double_sided) return m.light_col;
+				const float angle = dot(wo, sp.n);
+				return angle > 0 ? m.light_col : C3(0.f);
+			}
+			return m.emit_color;
+		}
+
+		// material_shiny_diffuse.cc:244-327 (diffuse-reflect branch), material_simple.cc:42-48
+		C3 sample(const SurfacePoint &sp, const V3 &wo, V3 &wi, Sample &s, float &w) const
+		{
+			const Material &m = *sp.mat;
+			if(m.type == YC_MAT_LIGHT)
+			{
+				s.pdf = 0.f;
+				w = 0.f;
+				return C3(0.f);
+			}
+			const float cos_ng_wo = dot(sp.ng, wo);
+			const V3 n = faceForward(sp.ng, sp.n, wo);
+			float accum_c[4];
+			accumulate(m.components, 1.f, accum_c);
+			float sum = 0.f, val[4], width[4];
+			unsigned choice[4];
+			int n_match = 0, pick = -1;
+			for(int i = 0; i < m.n_bsdf; ++i)
+			{
+				if((s.flags & m.c_flags[i]) == m.c_flags[i])
+				{
+					width[n_match] = accum_c[m.c_index[i]];
+					sum += width[n_match];
+					choice[n_match] = m.c_flags[i];
+					val[n_match] = sum;
+					++n_match;
+				}
+			}
+			if(!n_match || sum < 0.00001) { s.sampled_flags = BNone; s.pdf = 0.f; return C3(1.f); }
+			const float inv_sum = 1.f / sum;
+			for(int i = 0; i < n_match; ++i)
+			{
+				val[i] *= inv_sum;
+				width[i] *= inv_sum;
+				if((s.s_1 <= val[i]) && (pick < 0)) pick = i;
+			}
+			if(pick < 0) pick = n_match - 1;
+			float s_1;
+			if(pick > 0) s_1 = (s.s_1 - val[pick - 1]) / width[pick];
+			else s_1 = s.s_1 / width[pick];
+			C3 scolor(0.f);
+			// DiffuseReflect (the only component a plain shinydiffuse configures here)
+			wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
+			if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * m.diffuse_color;
+			s.pdf = std::abs(dot(wi, n)) * width[pick];
+			s.sampled_flags = choice[pick];
+			w = std::abs(dot(wi, sp.n)) / (s.pdf * 0.99f + 0.01f);
+			const float alpha = 1.f;
+			w = w * (alpha) + 1.f * (1.f - alpha);
+			return scolor;
+		}
+
+		// material_shiny_diffuse.cc:329-366
+		float pdf(const SurfacePoint &sp, const V3 &wo, const V3 &wi, unsigned bsdfs) const
+		{
+			const Material &m = *sp.mat;
+			if(m.type == YC_MAT_LIGHT) return 0.f;
+			if(!(bsdfs & BDiffuse)) return 0.f;
+			float pdf = 0.f;
+			const V3 n = faceForward(sp.ng, sp.n, wo);
+			float accum_c[4];
+			accumulate(m.components, 1.f, accum_c);
+			float sum = 0.f, width;
+			int n_match = 0;
+			for(int i = 0; i < m.n_bsdf; ++i)
+			{
+				if(bsdfs & m.c_flags[i])
+				{
+					width = accum_c[m.c_index[i]];
+					sum += width;
+					if(m.c_flags[i] == (BDiffuse | BReflect)) pdf += std::abs(dot(wi, n)) * width;
+					++n_match;
+				}
+			}
+			if(!n_match || sum < 0.00001) return 0.f;
+			return pdf / sum;
+		}
+
+		float shadowTmin(const SurfacePoint &sp) const
+		{
+			return sc_.rp.shadow_bias_auto ? sc_.rp.shadow_bias * std::max(1.f, sp.p.length()) : sc_.rp.shadow_bias;
+		}
+
+		// light_area.cc:66-96
+		static bool areaIllumSample(const Light &L, const SurfacePoint &sp, LSample &s, Ray &wi)
+		{
+			const V3 p = L.corner + s.s_1 * L.to_x + s.s_2 * L.to_y;
+			V3 ldir = p - sp.p;
+			const float dist_sqr = ldir.lengthSqr();
+			const float dist = fsqrt(dist_sqr);
+			if(dist <= 0.0) return false;
+			ldir *= 1.f / dist;
+			const float cos_angle = dot(ldir, L.fnormal);
+			if(cos_angle <= 0) return false;
+			wi.tmax = dist;
+			wi.dir = ldir;
+			s.col = L.color;
+			s.pdf = static_cast<float>(dist_sqr * num_pi / (L.area * cos_angle));
+			return true;
+		}
+		// light_area.cc:116-135
+		static bool areaTri(const V3 &a, const V3 &b, const V3 &c, const Ray &ray, float &t)
+		{
+			const V3 edge_1 = b - a;
+			const V3 edge_2 = c - a;
+			const V3 pvec = ray.dir ^ edge_2;
+			const float det = dot(edge_1, pvec);
+			if(det == 0.f) return false;
+			const float inv_det = 1.f / det;
+			const V3 tvec = ray.from - a;
+			const float u = dot(tvec, pvec) * inv_det;
+			if(u < 0.f || u > 1.f) return false;
+			const V3 qvec = tvec ^ edge_1;
+			const float v = dot(ray.dir, qvec) * inv_det;
+			if((v < 0.f) || ((u + v) > 1.f)) return false;
+			t = dot(edge_2, qvec) * inv_det;
+			return true;
+		}
+		// light_area.cc:137-151
+		static bool areaIntersect(const Light &L, const Ray &ray, float &t, C3 &col, float &ipdf)
+		{
+			const float cos_angle = dot(ray.dir, L.fnormal);
+			if(cos_angle <= 0) return false;
+			if(!areaTri(L.corner, L.c2, L.c3, ray, t))
+			{
+				if(!areaTri(L.corner, L.c3, L.c4, ray, t)) return false;
+			}
+			if(!(t > 1.0e-10f)) return false;
+			col = L.color;
+			ipdf = static_cast<float>(1.f / (t * t) * L.area * cos_angle * div_1_by_pi);
+			return true;
+		}
+
+		// integrator_montecarlo.cc:80-154 (point light)
+		C3 diracLight(Thread &th, const Light &L, const V3 &wo, const SurfacePoint &sp, bool cast_shadows) const
+		{
+			// light_point.cc:38-57
+			V3 ldir = L.position - sp.p;
+			const float dist_sqr = ldir.x * ldir.x + ldir.y * ldir.y + ldir.z * ldir.z;
+			const float dist = fsqrt(dist_sqr);
+			if(dist == 0.0) return C3(0.f);
+			const float idist_sqr = 1.f / (dist_sqr);
+			ldir *= 1.f / dist;
+			Ray light_ray;
+			light_ray.tmax = dist;
+			light_ray.dir = ldir;
+			const C3 lcol = L.color * idist_sqr;
+			C3 col(0.f);
+			light_ray.from = sp.p;
+			light_ray.tmin = shadowTmin(sp);
+			bool shadowed = false;
+			if(cast_shadows) shadowed = isShadowed(th, light_ray);
+			const float angle_light_normal = sp.mat->flat ? 1.f : std::abs(dot(sp.n, light_ray.dir));
+			if(!shadowed)
+			{
+				const C3 surf_col = eval(sp, wo, light_ray.dir, BAll);
+				const C3 transmit_col(1.f);
+				col += surf_col * lcol * angle_light_normal * transmit_col;
+			}
+			return col;
+		}
+
+		// integrator_montecarlo.cc:156-282
+		C3 areaLightSampleLight(Thread &th, Halton &hal_2, Halton &hal_3, const Light &L, const V3 &wo, const SurfacePoint &sp, bool cast_shadows, unsigned num_samples, float inv_num_samples) const
+		{
+			Ray light_ray;
+			light_ray.from = sp.p;
+			C3 col(0.f);
+			LSample ls;
+			for(unsigned i = 0; i < num_samples; ++i)
+			{
+				ls.s_1 = hal_2.getNext();
+				ls.s_2 = hal_3.getNext();
+				if(areaIllumSample(L, sp, ls, light_ray))
+				{
+					light_ray.tmin = shadowTmin(sp);
+					bool shadowed = false;
+					if(cast_shadows) shadowed = isShadowed(th, light_ray);
+					if(!shadowed && ls.pdf > 1e-6f)
+					{
+						const C3 surf_col = eval(sp, wo, light_ray.dir, BAll);
+						const float angle_light_normal = sp.mat->flat ? 1.f : std::abs(dot(sp.n, light_ray.dir));
+						float w = 1.f;
+						const float m_pdf = pdf(sp, wo, light_ray.dir, BGlossy | BDiffuse | BDispersive | BReflect | BTransmit);
+						if(m_pdf > 1e-6f)
+						{
+							const float l_2 = ls.pdf * ls.pdf;
+							const float m_2 = m_pdf * m_pdf;
+							w = l_2 / (l_2 + m_2);
+						}
+						col += surf_col * ls.col * angle_light_normal * w / ls.pdf;
+					}
+				}
+			}
+			return col * inv_num_samples;
+		}
+
+		// integrator_montecarlo.cc:284-383
+		C3 areaLightSampleMaterial(Thread &th, Halton &hal_2, Halton &hal_3, const Light &L, const V3 &wo, const SurfacePoint &sp, bool cast_shadows, unsigned num_samples, float inv_num_samples) const
+		{
+			Ray b_ray;
+			C3 col(0.f), lcol;
+			for(unsigned i = 0; i < num_samples; ++i)
+			{
+				if(sc_.rp.ray_min_dist_auto) b_ray.tmin = sc_.rp.ray_min_dist * std::max(1.f, sp.p.length());
+				else b_ray.tmin = sc_.rp.ray_min_dist;
+				b_ray.from = sp.p;
+				const float s_1 = hal_2.getNext();
+				const float s_2 = hal_3.getNext();
+				float W = 0.f;
+				Sample s(s_1, s_2, BGlossy | BDiffuse | BDispersive | BReflect | BTransmit);
+				const C3 surf_col = sample(sp, wo, b_ray.dir, s, W);
+				float light_pdf;
+				if(s.pdf > 1e-6f && areaIntersect(L, b_ray, b_ray.tmax, lcol, light_pdf))
+				{
+					bool shadowed = false;
+					if(cast_shadows) shadowed = isShadowed(th, b_ray);
+					if(!shadowed && light_pdf > 1e-6f)
+					{
+						const float l_pdf = 1.f / light_pdf;
+						const float l_2 = l_pdf * l_pdf;
+						const float m_2 = s.pdf * s.pdf;
+						const float w = m_2 / (l_2 + m_2);
+						col += surf_col * lcol * w * W;
+					}
+				}
+			}
+			return col * inv_num_samples;
+		}
+
+		// integrator_montecarlo.cc:385-408
+		C3 doLightEstimation(Thread &th, const Light &L, const SurfacePoint &sp, const V3 &wo, unsigned loffs, uint32_t sample_idx, uint32_t offset) const
+		{
+			C3 col(0.f);
+			const bool cast_shadows = L.cast_shadows && sp.mat->receive_shadows;
+			if(L.type == YC_LIGHT_POINT) col += diracLight(th, L, wo, sp, cast_shadows);
+			else
+			{
+				const unsigned l_offs = loffs * 4567;
+				const int num_samples = static_cast<int>(std::ceil(static_cast<float>(L.samples) * 1.f));
+				const float inv_num_samples = 1.f / static_cast<float>(num_samples);
+				const unsigned offs = num_samples * sample_idx + offset + l_offs;
+				Halton hal_2(2, offs - 1);
+				Halton hal_3(3, offs - 1);
+				col += areaLightSampleLight(th, hal_2, hal_3, L, wo, sp, cast_shadows, num_samples, inv_num_samples);
+				hal_2.setStart(offs - 1);
+				hal_3.setStart(offs - 1);
+				col += areaLightSampleMaterial(th, hal_2, hal_3, L, wo, sp, cast_shadows, num_samples, inv_num_samples);
+			}
+			return col;
+		}
+
+		// integrator_montecarlo.cc:54-68
+		C3 estimateAllDirectLight(Thread &th, const SurfacePoint &sp, const V3 &wo, uint32_t sample_idx, uint32_t offset) const
+		{
+			C3 col(0.f);
+			unsigned loffs = 0;
+			for(const Light &L : sc_.lights)
+			{
+				col += doLightEstimation(th, L, sp, wo, loffs, sample_idx, offset);
+				++loffs;
+			}
+			return col;
+		}
+
+		// integrator_montecarlo.cc:70-78 (the light pick uses a per-thread running counter)
+		C3 estimateOneDirectLight(Thread &th, const SurfacePoint &sp, const V3 &wo, uint32_t sample_idx, uint32_t offset) const
+		{
+			const int num_lights = (int)sc_.lights.size();
+			if(num_lights == 0) return C3(0.f);
+			Halton hal_2(2, sc_.rp.base_sampling_offset + th.correlative - 1);
+			const int lnum = std::min(static_cast<int>(hal_2.getNext() * static_cast<float>(num_lights)), num_lights - 1);
+			++th.correlative;
+			return doLightEstimation(th, sc_.lights[lnum], sp, wo, lnum, sample_idx, offset) * static_cast<float>(num_lights);
+		}
+
+		// integrator_tiled.cc:707-720
+		void background(const Ray &, C3 &col, float &alpha) const
+		{
+			if(sc_.rp.bg_transp) { col = C3(0.f); alpha = 0.f; }
+			else if(sc_.rp.has_background) { col = C3(sc_.rp.bg_color[0], sc_.rp.bg_color[1], sc_.rp.bg_color[2]); alpha = 1.f; }
+			else { col = C3(0.f); alpha = 1.f; }
+		}
+
+		// integrator_direct_light.cc:97-144
+		void integrateDirect(Thread &th, Ray &ray, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha) const
+		{
+			col = C3(0.f);
+			alpha = 1.f;
+			SurfacePoint sp;
+			if(intersect(th, ray, sp))
+			{
+				const unsigned mat_bsdfs = sp.bsdf_flags;
+				const V3 wo = -ray.dir;
+				if(mat_bsdfs & BEmit) col += emit(sp, wo);
+				if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+				col += C3(0.f);  // recursiveRaytrace: no specular/glossy components here (montecarlo.cc:918-968)
+				alpha = 1.f;
+			}
+			else background(ray, col, alpha);
+		}
+
+		// integrator_path_tracer.cc:120-290
+		void integratePath(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha) const
+		{
+			const yc_render &rp = sc_.rp;
+			col = C3(0.f);
+			alpha = 1.f;
+			float w = 0.f;
+			SurfacePoint sp;
+			if(!intersect(th, ray, sp)) { background(ray, col, alpha); return; }
+			const unsigned mat_bsdfs = sp.bsdf_flags;
+			const V3 wo = -ray.dir;
+			if(mat_bsdfs & BEmit) col += emit(sp, wo);
+			if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+			unsigned path_flags = BDiffuse;
+			if(mat_bsdfs & path_flags)
+			{
+				C3 path_col(0.f);
+				path_flags |= (BDiffuse | BReflect | BTransmit);
+				const int n_samples = std::max(1, rp.path_samples);
+				for(int i = 0; i < n_samples; ++i)
+				{
+					const unsigned offs = rp.path_samples * sample_idx + offset + i;
+					C3 throughput(1.f), lcol, scol;
+					SurfacePoint hit = sp;
+					V3 pwo = wo;
+					Ray p_ray;
+					const float s_1 = riVdC(offs);
+					const float s_2 = static_cast<float>(lowDiscrepancySampling(2, offs));
+					Sample s(s_1, s_2, path_flags);
+					scol = sample(sp, pwo, p_ray.dir, s, w);
+					scol *= w;
+					throughput = scol;
+					p_ray.tmin = rp.ray_min_dist;
+					p_ray.tmax = -1.f;
+					p_ray.from = sp.p;
+					SurfacePoint nh;
+					if(!intersect(th, p_ray, nh)) continue;
+					hit = nh;
+					if(s.sampled_flags != BNone) pwo = -p_ray.dir;
+					lcol = estimateOneDirectLight(th, hit, pwo, sample_idx, offset);
+					const unsigned mat_bsd_fs = hit.bsdf_flags;
+					if(mat_bsd_fs & BEmit) lcol += emit(hit, pwo);
+					path_col += lcol * throughput;
+					bool caustic = false;
+					for(int depth = 1; depth < rp.bounces; ++depth)
+					{
+						const int d_4 = 4 * depth;
+						s.s_1 = static_cast<float>(lowDiscrepancySampling(d_4 + 3, offs));
+						s.s_2 = static_cast<float>(lowDiscrepancySampling(d_4 + 4, offs));
+						s.flags = BAll;
+						scol = sample(hit, pwo, p_ray.dir, s, w);
+						scol *= w;
+						if(scol.isBlack()) break;
+						throughput *= scol;
+						caustic = rp.caustic_path && (s.sampled_flags & (BSpecular | BGlossy | BFilter));
+						p_ray.tmin = rp.ray_min_dist;
+						p_ray.tmax = -1.f;
+						p_ray.from = hit.p;
+						SurfacePoint nh2;
+						if(!intersect(th, p_ray, nh2)) break;
+						hit = nh2;
+						pwo = -p_ray.dir;
+						if(mat_bsd_fs & BDiffuse) lcol = estimateOneDirectLight(th, hit, pwo, sample_idx, offset);
+						else lcol = C3(0.f);
+						if(depth > rp.rr_min_bounces)
+						{
+							const float random_value = static_cast<float>(rng());
+							const float probability = throughput.maximum();
+							if(probability <= 0.f || probability < random_value) break;
+							throughput *= 1.f / probability;
+						}
+						if((mat_bsd_fs & BEmit) && caustic) lcol += emit(hit, pwo);
+						path_col += lcol * throughput;
+					}
+				}
+				col += path_col / static_cast<float>(n_samples);
+			}
+			col += C3(0.f);  // recursiveRaytrace (no specular/glossy here)
+			alpha = 1.f;
+		}
+
+		// camera_perspective.cc:128-146 + plane.h:37-40
+		Ray shootRay(float px, float py) const
+		{
+			const Camera &c = sc_.cam;
+			Ray ray;
+			ray.from = c.position;
+			ray.dir = c.vright * px + c.vup * py + c.vto;
+			ray.dir.normalize();
+			ray.tmin = dot(c.cam_z, (c.near_p - ray.from)) / dot(ray.dir, c.cam_z);
+			ray.tmax = dot(c.cam_z, (c.far_p - ray.from)) / dot(ray.dir, c.cam_z);
+			return ray;
+		}
+
+		// integrator_tiled.cc:288-405 for one pixel: writes n_samples RGBA
+		void renderPixel(Thread &th, Mwc &rng, int i, int j, float *out) const
+		{
+			const yc_render &rp = sc_.rp;
+			const int n_samples = rp.aa_samples;
+			const int pass_offs = rp.base_sampling_offset;
+			const float d_1 = 1.f / static_cast<float>(n_samples);
+			const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
+			for(int sample = 0; sample < n_samples; ++sample)
+			{
+				const uint32_t sample_idx = pass_offs + sample;
+				float dx = 0.5f, dy = 0.5f;
+				if(n_samples > 1)
+				{
+					dx = (0.5f + static_cast<float>(sample)) * d_1;
+					dy = riLp(sample + offset);
+				}
+				Ray ray = shootRay(j + dx, i + dy);
+				C3 col;
+				float alpha;
+				if(rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha);
+				else integrateDirect(th, ray, sample_idx, offset, col, alpha);
+				if(alpha > 1.f) alpha = 1.f;
+				out[4 * sample] = col.r;
+				out[4 * sample + 1] = col.g;
+				out[4 * sample + 2] = col.b;
+				out[4 * sample + 3] = alpha;
+			}
+		}
+};
+
+// integrator_tiled.cc:56-67 + imagefilm.cc:447-487 + imagesplitter.cc:30-107 (linear order,
+// one thread: no tail subdivision)
+struct Tile { int x, y, w, h; };
+
+static std::vector<Tile> tilesLinear(int w, int h, int bs)
+{
+	std::vector<Tile> t;
+	const int nx = (w + bs - 1) / bs, ny = (h + bs - 1) / bs;
+	for(int j = 0; j < ny; ++j)
+		for(int i = 0; i < nx; ++i)
+		{
+			Tile r{i * bs, j * bs, 0, 0};
+			r.w = std::min(bs, w - r.x);
+			r.h = std::min(bs, h - r.y);
+			t.push_back(r);
+		}
+	return t;
+}
+
+struct Film
+{
+	int w, h;
+	std::vector<float> rgba, weight;
+	const FilmTable &tab;
+	float clamp_samples;
+	Film(int ww, int hh, const FilmTable &t, float cs) : w(ww), h(hh), rgba(4 * (size_t)ww * hh, 0.f), weight((size_t)ww * hh, 0.f), tab(t), clamp_samples(cs) {}
+	// imagefilm.cc:680-733
+	void addSample(int x, int y, float dx, float dy, const float *col_in)
+	{
+		const int dx_0 = std::max(0 - x, roundToInt(static_cast<double>(dx) - tab.filterw));
+		const int dx_1 = std::min(w - x - 1, roundToInt(static_cast<double>(dx) + tab.filterw - 1.0));
+		const int dy_0 = std::max(0 - y, roundToInt(static_cast<double>(dy) - tab.filterw));
+		const int dy_1 = std::min(h - y - 1, roundToInt(static_cast<double>(dy) + tab.filterw - 1.0));
+		int x_index[9], y_index[9];
+		const double x_offs = dx - 0.5;
+		for(int i = dx_0, n = 0; i <= dx_1; ++i, ++n) x_index[n] = floorToInt(std::abs((static_cast<double>(i) - x_offs) * tab.table_scale));
+		const double y_offs = dy - 0.5;
+		for(int i = dy_0, n = 0; i <= dy_1; ++i, ++n) y_index[n] = floorToInt(std::abs((static_cast<double>(i) - y_offs) * tab.table_scale));
+		const int x_0 = x + dx_0, x_1 = x + dx_1, y_0 = y + dy_0, y_1 = y + dy_1;
+		for(int j = y_0; j <= y_1; ++j)
+			for(int i = x_0; i <= x_1; ++i)
+			{
+				const float wt = tab.table[y_index[j - y_0] * 16 + x_index[i - x_0]];
+				const size_t p = (size_t)j * w + i;
+				weight[p] = weight[p] + wt;
+				C3 c(col_in[0], col_in[1], col_in[2]);
+				c.clampProportional(clamp_samples);
+				rgba[4 * p] = rgba[4 * p] + c.r * wt;
+				rgba[4 * p + 1] = rgba[4 * p + 1] + c.g * wt;
+				rgba[4 * p + 2] = rgba[4 * p + 2] + c.b * wt;
+				rgba[4 * p + 3] = rgba[4 * p + 3] + col_in[3] * wt;
+			}
+	}
+};
+
+static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float *out_w, yc_counters *ctr)
+{
+	Scene sc(*s);
+	Renderer R(sc);
+	const yc_render &rp = sc.rp;
+	const int W = rp.width, H = rp.height;
+	if(y1 <= y0) { y0 = 0; y1 = H; }
+	Film film(W, H, *sc.film, rp.clamp_samples);
+	const int spp = rp.aa_samples;
+	std::vector<Tile> all = tilesLinear(W, H, rp.tile_size);
+	std::vector<Tile> tiles;
+	for(const Tile &t : all)
+	{
+		const int ya = std::max(t.y, y0), yb = std::min(t.y + t.h, y1);
+		if(ya < yb) tiles.push_back({t.x, ya, t.w, yb - ya});
+	}
+	const int nthreads = std::max(1, rp.threads);
+	std::vector<Renderer::Thread> th(nthreads);
+	// sample loop: tiles in parallel, each tile sequential (reference renderWorker), then the film
+	// pass in linear tile order (reference single-thread order), so output is thread-count free.
+	const size_t band = 256;
+	for(size_t t0 = 0; t0 < tiles.size(); t0 += band)
+	{
+		const size_t t1 = std::min(tiles.size(), t0 + band);
+		std::vector<std::vector<float>> buf(t1 - t0);
+		std::atomic<size_t> next{t0};
+		auto worker = [&](int tid) {
+			for(;;)
+			{
+				const size_t k = next++;
+				if(k >= t1) break;
+				const Tile &a = tiles[k];
+				std::vector<float> &b = buf[k - t0];
+				b.resize((size_t)a.w * a.h * spp * 4);
+				// integrator_tiled.cc:272 — RandomGenerator(rand() + offset*(resx*y0+x0) + 123)
+				Mwc rng(rp.rr_seed + rp.base_sampling_offset * (sc.cam.resx * a.y + a.x) + 123);
+				for(int i = a.y; i < a.y + a.h; ++i)
+					for(int j = a.x; j < a.x + a.w; ++j)
+						R.renderPixel(th[tid], rng, i, j, &b[(((size_t)(i - a.y) * a.w + (j - a.x)) * spp) * 4]);
+			}
+		};
+		if(nthreads == 1) worker(0);
+		else
+		{
+			std::vector<std::thread> pool;
+			for(int tt = 0; tt < nthreads; ++tt) pool.emplace_back(worker, tt);
+			for(auto &p : pool) p.join();
+		}
+		for(size_t k = t0; k < t1; ++k)
+		{
+			const Tile &a = tiles[k];
+			const std::vector<float> &b = buf[k - t0];
+			const float d_1 = 1.f / static_cast<float>(spp);
+			for(int i = a.y; i < a.y + a.h; ++i)
+				for(int j = a.x; j < a.x + a.w; ++j)
+				{
+					const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
+					for(int sample = 0; sample < spp; ++sample)
+					{
+						float dx = 0.5f, dy = 0.5f;
+						if(spp > 1)
+						{
+							dx = (0.5f + static_cast<float>(sample)) * d_1;
+							dy = riLp(sample + offset);
+						}
+						film.addSample(j, i, dx, dy, &b[((((size_t)(i - a.y) * a.w + (j - a.x)) * spp) + sample) * 4]);
+					}
+				}
+		}
+	}
+	// imagefilm.cc:590-617 flush: colour / weight (Rgba::normalized, color.h:554-558)
+	for(size_t p = 0; p < (size_t)W * H; ++p)
+	{
+		const float wt = film.weight[p];
+		for(int k = 0; k < 4; ++k) out_rgba[4 * p + k] = (wt != 0.f) ? film.rgba[4 * p + k] / wt : 0.f;
+		if(out_w) out_w[p] = wt;
+	}
+	if(ctr)
+	{
+		ctr->closest_rays = 0;
+		ctr->shadow_rays = 0;
+		for(const auto &t : th) { ctr->closest_rays += t.closest; ctr->shadow_rays += t.shadow; }
+	}
+	return 0;
+}
+
+} // namespace yc
+
+using namespace yc;
+
+extern "C" {
+
+int yc_render_image(const yc_scene *scene, int y0, int y1, float *rgba, float *weights, yc_counters *counters)
+{
+	return renderImage(scene, y0, y1, rgba, weights, counters);
+}
+
+int yc_render_samples(const yc_scene *s, int n, const int *xys, float *rgba)
+{
+	Scene sc(*s);
+	Renderer R(sc);
+	Renderer::Thread th;
+	const yc_render &rp = sc.rp;
+	const int spp = rp.aa_samples;
+	const float d_1 = 1.f / static_cast<float>(spp);
+	for(int k = 0; k < n; ++k)
+	{
+		const int j = xys[3 * k], i = xys[3 * k + 1], sample = xys[3 * k + 2];
+		const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
+		float dx = 0.5f, dy = 0.5f;
+		if(spp > 1)
+		{
+			dx = (0.5f + static_cast<float>(sample)) * d_1;
+			dy = riLp(sample + offset);
+		}
+		Ray ray = R.shootRay(j + dx, i + dy);
+		Mwc rng(rp.rr_seed + 123);
+		C3 col;
+		float alpha;
+		const uint32_t sample_idx = rp.base_sampling_offset + sample;
+		if(rp.integrator == YC_INT_PATH) R.integratePath(th, ray, rng, sample_idx, offset, col, alpha);
+		else R.integrateDirect(th, ray, sample_idx, offset, col, alpha);
+		rgba[4 * k] = col.r; rgba[4 * k + 1] = col.g; rgba[4 * k + 2] = col.b; rgba[4 * k + 3] = std::min(alpha, 1.f);
+	}
+	return 0;
+}
+
+int yc_trace_closest(const yc_scene *s, int n, const float *rays, float *hit, int *prim)
+{
+	Scene sc(*s);
+	for(int k = 0; k < n; ++k)
+	{
+		const float *r = rays + 8 * k;
+		Ray ray;
+		ray.from = V3(r[0], r[1], r[2]);
+		ray.dir = V3(r[3], r[4], r[5]);
+		ray.tmin = r[6];
+		ray.tmax = r[7];
+		const float t_max = (ray.tmax >= 0.f) ? ray.tmax : std::numeric_limits<float>::infinity();
+		const IsectData d = sc.intersect(ray, t_max, false, nullptr);
+		hit[4 * k] = d.hit ? d.t : -1.f;
+		hit[4 * k + 1] = d.bu;
+		hit[4 * k + 2] = d.bv;
+		hit[4 * k + 3] = d.bw;
+		prim[k] = d.hit ? d.prim : -1;
+	}
+	return 0;
+}
+
+int yc_trace_shadow(const yc_scene *s, int n, const float *rays, int *occluded)
+{
+	Scene sc(*s);
+	for(int k = 0; k < n; ++k)
+	{
+		const float *r = rays + 8 * k;
+		Ray ray;
+		ray.from = V3(r[0], r[1], r[2]);
+		ray.dir = V3(r[3], r[4], r[5]);
+		ray.tmin = r[6];
+		ray.tmax = r[7];
+		const float t_max = (ray.tmax >= 0.f) ? ray.tmax : std::numeric_limits<float>::infinity();
+		occluded[k] = sc.intersect(ray, t_max, true, nullptr).hit ? 1 : 0;
+	}
+	return 0;
+}
+
+void yc_riVdC(const uint32_t *bits, const uint32_t *r, float *out, int n) { for(int i = 0; i < n; ++i) out[i] = riVdC(bits[i], r[i]); }
+void yc_riS(const uint32_t *bits, const uint32_t *r, float *out, int n) { for(int i = 0; i < n; ++i) out[i] = riS(bits[i], r[i]); }
+void yc_riLp(const uint32_t *bits, const uint32_t *r, float *out, int n) { for(int i = 0; i < n; ++i) out[i] = riLp(bits[i], r[i]); }
+void yc_fnv32(const uint32_t *in, uint32_t *out, int n) { for(int i = 0; i < n; ++i) out[i] = fnv32(in[i]); }
+void yc_lds(const int *dim, const uint32_t *idx, double *out, int n) { for(int i = 0; i < n; ++i) out[i] = lowDiscrepancySampling(dim[i], idx[i]); }
+void yc_halton_seq(int base, uint32_t start, int steps, float *out)
+{
+	Halton h(base, start);
+	for(int i = 0; i < steps; ++i) out[i] = h.getNext();
+}
+void yc_sin(const float *x, float *out, int n) { for(int i = 0; i < n; ++i) out[i] = fsin(x[i]); }
+void yc_cos(const float *x, float *out, int n) { for(int i = 0; i < n; ++i) out[i] = fcos(x[i]); }
+void yc_exp(const float *x, float *out, int n) { for(int i = 0; i < n; ++i) out[i] = fexp(x[i]); }
+void yc_cos_hemisphere(const float *p9, const float *s, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const float *p = p9 + 9 * i;
+		const V3 r = cosHemisphere(V3(p[0], p[1], p[2]), V3(p[3], p[4], p[5]), V3(p[6], p[7], p[8]), s[2 * i], s[2 * i + 1]);
+		out[3 * i] = r.x; out[3 * i + 1] = r.y; out[3 * i + 2] = r.z;
+	}
+}
+void yc_coords_system(const float *in, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		V3 u, v;
+		createCoordsSystem(V3(in[3 * i], in[3 * i + 1], in[3 * i + 2]), u, v);
+		out[6 * i] = u.x; out[6 * i + 1] = u.y; out[6 * i + 2] = u.z;
+		out[6 * i + 3] = v.x; out[6 * i + 4] = v.y; out[6 * i + 5] = v.z;
+	}
+}
+void yc_normalize(const float *in, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		V3 v(in[3 * i], in[3 * i + 1], in[3 * i + 2]);
+		v.normalize();
+		out[3 * i] = v.x; out[3 * i + 1] = v.y; out[3 * i + 2] = v.z;
+	}
+}
+// bound.h:141-211 (Smits)
+void yc_bound_cross(const float *box, const float *ray, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const float *b = box + 6 * i, *r = ray + 7 * i;
+		const V3 a0(b[0], b[1], b[2]), a1(b[3], b[4], b[5]);
+		const V3 from(r[0], r[1], r[2]), dir(r[3], r[4], r[5]);
+		const float t_max = r[6];
+		const V3 p = from - a0;
+		float lmin = -1e38f, lmax = 1e38f, ltmin, ltmax;
+		bool ok = true;
+		for(int k = 0; k < 3 && ok; ++k)
+		{
+			if(dir[k] != 0)
+			{
+				const float inv = 1.f / dir[k];
+				if(inv > 0) { ltmin = -p[k] * inv; ltmax = ((a1[k] - a0[k]) - p[k]) * inv; }
+				else { ltmin = ((a1[k] - a0[k]) - p[k]) * inv; ltmax = -p[k] * inv; }
+				if(k == 0) { lmin = ltmin; lmax = ltmax; }
+				else { lmin = std::max(ltmin, lmin); lmax = std::min(ltmax, lmax); }
+				if((lmax < 0) || (lmin > t_max)) ok = false;
+			}
+		}
+		if(ok && (lmin <= lmax) && (lmax >= 0) && (lmin <= t_max)) { out[3 * i] = 1.f; out[3 * i + 1] = lmin; out[3 * i + 2] = lmax; }
+		else { out[3 * i] = 0.f; out[3 * i + 1] = 0.f; out[3 * i + 2] = 0.f; }
+	}
+}
+void yc_mwc(uint32_t seed, int steps, double *out)
+{
+	Mwc m(seed);
+	for(int i = 0; i < steps; ++i) out[i] = m();
+}
+void yc_filter_gauss(const float *dxdy, float *out, int n) { for(int i = 0; i < n; ++i) out[i] = filterGauss(dxdy[2 * i], dxdy[2 * i + 1]); }
+void yc_round_to_int(const double *v, int *out, int n) { for(int i = 0; i < n; ++i) out[i] = roundToInt(v[i]); }
+void yc_floor_to_int(const double *v, int *out, int n) { for(int i = 0; i < n; ++i) out[i] = floorToInt(v[i]); }
+void yc_clamp_proportional(const float *rgb, float max_value, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		C3 c(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2]);
+		c.clampProportional(max_value);
+		out[3 * i] = c.r; out[3 * i + 1] = c.g; out[3 * i + 2] = c.b;
+	}
+}
+void yc_film_table(int filter, float filter_size, float *table, float *filterw, float *table_scale)
+{
+	FilmTable t(filter, filter_size);
+	std::memcpy(table, t.table, sizeof(t.table));
+	*filterw = t.filterw;
+	*table_scale = t.table_scale;
+}
+
+}

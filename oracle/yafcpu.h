@@ -1,0 +1,121 @@
+// TEST INFRASTRUCTURE ONLY — the CPU oracle for the path-tracing hot path.
+//
+// A plain C++ restatement of libYafaRay's per-sample Monte Carlo loop (tiled sample loop,
+// DirectLight and Path integrators, MC light estimation, shinydiffuse/light_mat materials,
+// point/area lights, perspective camera, film splatting) written scalar and close to the
+// reference's own code structure, with `long double` wherever the reference's expressions
+// promote to x87 80-bit.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+// may load it; the product path (libyafaray_amd) never does.
+//
+// Parity status: the numeric building blocks (samplers, Halton/Faure, FAST_TRIG sin/cos,
+// cosHemisphere, Vec3, Bound::cross, MWC, gauss filter, rounding helpers) are PINNED against the
+// reference's own code compiled in oracle/_ref (tests/golden/prims.npz).  The integrator
+// composition is a restatement (reference library unbuildable here).
+
+#pragma once
+#include <cstdint>
+
+extern "C" {
+
+enum { YC_MAT_SHINYDIFFUSE = 0, YC_MAT_LIGHT = 1 };
+enum { YC_LIGHT_POINT = 0, YC_LIGHT_AREA = 1 };
+enum { YC_INT_DIRECT = 0, YC_INT_PATH = 1 };
+enum { YC_FILTER_BOX = 0, YC_FILTER_GAUSS = 1, YC_FILTER_MITCHELL = 2, YC_FILTER_LANCZOS = 3 };
+
+typedef struct {
+	int type;                 // YC_MAT_*
+	float color[3];           // shinydiffuse diffuse colour / light_mat colour (already * power)
+	float diffuse_strength;   // shinydiffuse "diffuse_reflect"
+	float emit_strength;      // shinydiffuse "emit"
+	int double_sided;         // light_mat
+	int receive_shadows;
+	int flat_material;
+} yc_material;
+
+typedef struct {
+	int type;                 // YC_LIGHT_*
+	float color[3];           // raw colour param
+	float power;
+	float from[3];            // point light position / area light corner
+	float point1[3];          // area light
+	float point2[3];          // area light
+	int samples;              // area light
+	int cast_shadows;
+} yc_light;
+
+typedef struct {
+	float from[3], to[3], up[3];
+	int resx, resy;
+	float focal, aspect;
+	float near_clip, far_clip;
+} yc_camera;
+
+typedef struct {
+	int integrator;           // YC_INT_*
+	int width, height;        // film
+	int aa_samples;           // AA_minsamples (single pass)
+	int filter;               // YC_FILTER_*
+	float filter_size;        // AA_pixelwidth
+	int tile_size;
+	int bounces, path_samples, rr_min_bounces;
+	int caustic_path;         // PathIntegrator caustic_type != none && != photon
+	int has_background;
+	float bg_color[3];        // constant background colour * power
+	int bg_transp;
+	int shadow_bias_auto; float shadow_bias;
+	int ray_min_dist_auto; float ray_min_dist;
+	int base_sampling_offset;
+	float clamp_samples;
+	int threads;              // oracle worker threads for the sample loop (film order is fixed)
+	uint32_t rr_seed;         // stand-in for the reference's glibc rand() per-tile seed term
+} yc_render;
+
+typedef struct {
+	int n_verts; const float *verts;
+	int n_tris; const int *tris; const int *tri_mat;
+	int n_mats; const yc_material *mats;
+	int n_lights; const yc_light *lights;   // already in render order (alphabetical by name)
+	yc_camera cam;
+	yc_render rp;
+} yc_scene;
+
+typedef struct {
+	uint64_t closest_rays, shadow_rays;
+} yc_counters;
+
+// Renders rows [y0, y1) of the film (all rows if y1 <= y0).  rgba: width*height*4 floats
+// (normalized, the put-pixel/flush values), weights: width*height (may be NULL).  The film pass
+// walks the reference's linear tile order, so results do not depend on `threads`.
+int yc_render_image(const yc_scene *scene, int y0, int y1, float *rgba, float *weights, yc_counters *counters);
+
+// Per-sample radiance for a list of (x, y, s) camera samples (RGBA per sample).
+int yc_render_samples(const yc_scene *scene, int n, const int *xys, float *rgba);
+
+// Ray-level oracle: closest hit / any hit against the scene triangles.
+// rays: 8 floats each (from xyz, dir xyz, tmin, tmax(<0 = inf)).
+// hit out: 4 floats (t, bary_u, bary_v, bary_w) + prim index (-1 = miss).
+int yc_trace_closest(const yc_scene *scene, int n, const float *rays, float *hit, int *prim);
+int yc_trace_shadow(const yc_scene *scene, int n, const float *rays, int *occluded);
+
+// Numeric building blocks (pinned against oracle/_ref).
+void yc_riVdC(const uint32_t *bits, const uint32_t *r, float *out, int n);
+void yc_riS(const uint32_t *bits, const uint32_t *r, float *out, int n);
+void yc_riLp(const uint32_t *bits, const uint32_t *r, float *out, int n);
+void yc_fnv32(const uint32_t *in, uint32_t *out, int n);
+void yc_lds(const int *dim, const uint32_t *idx, double *out, int n);
+void yc_halton_seq(int base, uint32_t start, int steps, float *out);
+void yc_sin(const float *x, float *out, int n);
+void yc_cos(const float *x, float *out, int n);
+void yc_exp(const float *x, float *out, int n);
+void yc_cos_hemisphere(const float *n_ru_rv, const float *s, float *out, int n);
+void yc_coords_system(const float *in, float *out, int n);
+void yc_normalize(const float *in, float *out, int n);
+void yc_bound_cross(const float *box, const float *ray, float *out, int n);
+void yc_mwc(uint32_t seed, int steps, double *out);
+void yc_filter_gauss(const float *dxdy, float *out, int n);
+void yc_round_to_int(const double *v, int *out, int n);
+void yc_floor_to_int(const double *v, int *out, int n);
+void yc_clamp_proportional(const float *rgb, float max_value, float *out, int n);
+void yc_film_table(int filter, float filter_size, float *table16x16, float *filterw, float *table_scale);
+
+}
