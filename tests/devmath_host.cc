@@ -1,0 +1,53 @@
+// Host build of the device numerics (libyafaray_amd/csrc/devmath.h) with extern "C" wrappers, so
+// tests/test_devmath.py can pin the exact code the kernels run against the reference's golden
+// vectors (tests/golden/prims.npz).  Compiled with g++ -ffp-contract=off at test time.
+#include "../libyafaray_amd/csrc/devmath.h"
+using namespace yafamd;
+extern "C" {
+void dm_ri(int which, const uint32_t *b, const uint32_t *r, float *o, int n)
+{
+	for(int i = 0; i < n; ++i) o[i] = which == 0 ? riVdC(b[i], r[i]) : which == 1 ? riS(b[i], r[i]) : riLp(b[i], r[i]);
+}
+void dm_fnv(const uint32_t *in, uint32_t *o, int n) { for(int i = 0; i < n; ++i) o[i] = fnv32(in[i]); }
+void dm_lds(const uint8_t *perm, uint32_t base, double f, const uint32_t *idx, double *o, int n)
+{
+	for(int i = 0; i < n; ++i) o[i] = lowDiscrepancy(perm, base, f, idx[i]);
+}
+void dm_halton_first(uint32_t base, const uint32_t *start, float *o, int n)
+{
+	for(int i = 0; i < n; ++i) o[i] = haltonFirst(base, 1.0 / (double)base, start[i]);
+}
+void dm_sin(const float *x, float *o, int n) { for(int i = 0; i < n; ++i) o[i] = fsin(x[i]); }
+void dm_cos(const float *x, float *o, int n) { for(int i = 0; i < n; ++i) o[i] = fcos(x[i]); }
+void dm_hemi(const float *p, const float *s, float *o, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const float *q = p + 9 * i;
+		const V3 r = cosHemisphere(v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), v3(q[6], q[7], q[8]), s[2 * i], s[2 * i + 1]);
+		o[3 * i] = r.x; o[3 * i + 1] = r.y; o[3 * i + 2] = r.z;
+	}
+}
+void dm_coords(const float *in, float *o, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		V3 u, v;
+		coordsSystem(v3(in[3 * i], in[3 * i + 1], in[3 * i + 2]), u, v);
+		o[6 * i] = u.x; o[6 * i + 1] = u.y; o[6 * i + 2] = u.z; o[6 * i + 3] = v.x; o[6 * i + 4] = v.y; o[6 * i + 5] = v.z;
+	}
+}
+void dm_normalize(const float *in, float *o, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const V3 r = normalize(v3(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+		o[3 * i] = r.x; o[3 * i + 1] = r.y; o[3 * i + 2] = r.z;
+	}
+}
+void dm_mwc(uint32_t seed, int steps, double *o)
+{
+	Mwc m{30903u, seed};
+	for(int i = 0; i < steps; ++i) o[i] = m.next();
+}
+}

@@ -1,0 +1,118 @@
+"""The exact code the kernels run (libyafaray_amd/csrc/devmath.h), built for the host, against
+(a) the reference's golden vectors and (b) real x87 long double arithmetic."""
+import ctypes as C
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = np.load(os.path.join(HERE, "golden", "prims.npz"))
+
+
+@pytest.fixture(scope="module")
+def dm():
+    out = os.path.join(tempfile.gettempdir(), "yaf_devmath_host.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", "-o", out,
+                    os.path.join(HERE, "devmath_host.cc")], check=True)
+    return C.CDLL(out)
+
+
+def P(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def test_x87_emulation_vs_long_double():
+    exe = os.path.join(tempfile.gettempdir(), "yaf_devmath_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", exe, os.path.join(HERE, "devmath_check.cc")],
+                   check=True)
+    r = subprocess.run([exe, "400000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("which,name", [(0, "riVdC"), (1, "riS"), (2, "riLp")])
+def test_radical_inverses(dm, which, name):
+    b, r = GOLD["ri_bits"], GOLD["ri_r"]
+    o = np.empty(len(b), np.float32)
+    dm.dm_ri(which, P(b, C.c_uint32), P(r, C.c_uint32), P(o, C.c_float), len(b))
+    assert np.array_equal(o.view(np.uint32), GOLD[name].view(np.uint32))
+
+
+def test_fnv(dm):
+    b = GOLD["fnv_in"]
+    o = np.empty(len(b), np.uint32)
+    dm.dm_fnv(P(b, C.c_uint32), P(o, C.c_uint32), len(b))
+    assert np.array_equal(o, GOLD["fnv"])
+
+
+def test_trig_and_hemisphere(dm):
+    x = GOLD["trig_x"]
+    for fn, key in (("dm_sin", "sin"), ("dm_cos", "cos")):
+        o = np.empty(len(x), np.float32)
+        getattr(dm, fn)(P(x, C.c_float), P(o, C.c_float), len(x))
+        assert np.array_equal(o.view(np.uint32), GOLD[key].view(np.uint32)), key
+    nrv, s = np.ascontiguousarray(GOLD["hemi_nrv"]), np.ascontiguousarray(GOLD["hemi_s"])
+    o = np.empty((len(s), 3), np.float32)
+    dm.dm_hemi(P(nrv, C.c_float), P(s, C.c_float), P(o, C.c_float), len(s))
+    assert np.array_equal(o.view(np.uint32), GOLD["hemi"].view(np.uint32))
+
+
+def test_vectors(dm):
+    cin = np.ascontiguousarray(GOLD["coords_in"])
+    o = np.empty((len(cin), 6), np.float32)
+    dm.dm_coords(P(cin, C.c_float), P(o, C.c_float), len(cin))
+    assert np.array_equal(o.view(np.uint32), GOLD["coords"].view(np.uint32))
+    v = np.ascontiguousarray(GOLD["norm_in"])
+    o = np.empty_like(v)
+    dm.dm_normalize(P(v, C.c_float), P(o, C.c_float), len(v))
+    assert np.array_equal(o.view(np.uint32), GOLD["norm"].view(np.uint32))
+
+
+def test_mwc(dm):
+    for seed, ref in zip(GOLD["mwc_seeds"], GOLD["mwc"]):
+        o = np.empty(len(ref), np.float64)
+        dm.dm_mwc(C.c_uint32(int(seed)), len(ref), P(o, C.c_double))
+        assert np.array_equal(o, ref)
+
+
+def test_halton_first_matches_sequence_start(dm):
+    # Halton(base, start).getNext() == first element of the reference sequence from `start`
+    for base, start, seq in zip(GOLD["halton_bases"], GOLD["halton_starts"], GOLD["halton_seq"]):
+        st = np.array([start], np.uint32)
+        o = np.empty(1, np.float32)
+        dm.dm_halton_first(C.c_uint32(int(base)), P(st, C.c_uint32), P(o, C.c_float), 1)
+        assert o[0] == seq[0]
+
+
+def test_low_discrepancy_faure(dm):
+    # the device uses the Faure tables the host uploads (render.cc faurePerm); rebuild them here
+    def perm(b):
+        if b <= 2:
+            return [0, 1]
+        if b % 2 == 0:
+            h = perm(b // 2)
+            return [2 * v for v in h] + [2 * v + 1 for v in h]
+        p, c = perm(b - 1), (b - 1) // 2
+        out = []
+        for i, v in enumerate(p):
+            if i == c:
+                out.append(c)
+            out.append(v + (v >= c))
+        return out
+    primes = [1]
+    c = 2
+    while len(primes) < 50:
+        if all(c % q for q in range(2, int(c ** 0.5) + 1)):
+            primes.append(c)
+        c += 1
+    dims, idx, ref = GOLD["lds_dim"], GOLD["lds_idx"], GOLD["lds"]
+    for d in np.unique(dims):
+        m = dims == d
+        pt = np.array(perm(3 if d <= 2 else primes[d]), np.uint8)
+        ii = np.ascontiguousarray(idx[m])
+        o = np.empty(len(ii), np.float64)
+        dm.dm_lds(P(pt, C.c_uint8), C.c_uint32(primes[d]), C.c_double(round(1e9 / primes[d]) / 1e9), P(ii, C.c_uint32),
+                  P(o, C.c_double), len(ii))
+        assert np.array_equal(o, ref[m]), d

@@ -1,0 +1,88 @@
+"""Pin the CPU oracle (oracle/yafcpu.cc) against the reference's own code:
+(1) the committed golden vectors of tests/golden/prims.npz (made by make_golden_prims.py from
+    oracle/_ref, i.e. the reference sources compiled here), always;
+(2) the live reference building blocks on fresh random inputs, when oracle/_ref is built."""
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+G = np.load(os.path.join(HERE, "golden", "prims.npz"))
+
+
+@pytest.fixture(scope="module")
+def o(oracle_built):
+    return oracle_built.oracle_prims()
+
+
+def same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    if a.dtype.kind == "f":
+        return np.array_equal(a.view(np.uint32 if a.dtype == np.float32 else np.uint64),
+                              b.astype(a.dtype).view(np.uint32 if a.dtype == np.float32 else np.uint64))
+    return np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("w", ["riVdC", "riS", "riLp"])
+def test_radical_inverse(o, w):
+    assert same(o.ri(w, G["ri_bits"], G["ri_r"]), G[w])
+
+
+def test_fnv(o):
+    assert same(o.fnv32(G["fnv_in"]), G["fnv"])
+
+
+def test_low_discrepancy_faure(o):
+    assert same(o.lds(G["lds_dim"], G["lds_idx"]), G["lds"])
+
+
+def test_halton_incremental(o):
+    for base, start, seq in zip(G["halton_bases"], G["halton_starts"], G["halton_seq"]):
+        assert same(o.halton_seq(int(base), int(start), len(seq)), seq), (base, start)
+
+
+def test_fast_trig_and_exp(o):
+    assert same(o.unary("sin", G["trig_x"]), G["sin"])
+    assert same(o.unary("cos", G["trig_x"]), G["cos"])
+    assert same(o.unary("exp", G["exp_x"]), G["exp"])
+
+
+def test_vectors_and_hemisphere(o):
+    assert same(o.unary("coords_system", G["coords_in"].reshape(-1), 6, 3).reshape(-1, 6), G["coords"])
+    assert same(o.unary("normalize", G["norm_in"].reshape(-1), 3, 3).reshape(-1, 3), G["norm"])
+    assert same(o.cos_hemisphere(G["hemi_nrv"], G["hemi_s"]), G["hemi"])
+
+
+def test_bound_cross(o):
+    assert same(o.bound_cross(G["bound_box"], G["bound_ray"]), G["bound"])
+
+
+def test_mwc(o):
+    for seed, ref in zip(G["mwc_seeds"], G["mwc"]):
+        assert same(o.mwc(int(seed), len(ref)), ref)
+
+
+def test_film_filter_and_rounding(o):
+    assert same(o.unary("filter_gauss", G["gauss_in"].reshape(-1), 1, 2), G["gauss"])
+    assert same(o.int_of_double("round_to_int", G["int_in"]), G["round_to_int"])
+    assert same(o.int_of_double("floor_to_int", G["int_in"]), G["floor_to_int"])
+    assert same(o.clamp_proportional(G["clamp_in"], 1.5), G["clamp_1_5"])
+    assert same(o.clamp_proportional(G["clamp_in"], 0.0), G["clamp_0"])
+
+
+def test_live_reference_random_inputs(o, oracle_built):
+    r = oracle_built.ref_prims()
+    if r is None:
+        pytest.skip("oracle/_ref not built (reference tree absent): golden vectors above still pin the oracle")
+    rng = np.random.default_rng(99)
+    n = 100000
+    b = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    rr = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    for w in ("riVdC", "riS", "riLp"):
+        assert same(o.ri(w, b, rr), r.ri(w, b, rr))
+    dims = rng.integers(1, 50, n).astype(np.int32)
+    assert same(o.lds(dims, b), r.lds(dims, b))
+    x = rng.uniform(-50, 50, n).astype(np.float32)
+    assert same(o.unary("sin", x), r.unary("sin", x))
+    assert same(o.unary("cos", x), r.unary("cos", x))

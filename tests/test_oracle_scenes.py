@@ -1,0 +1,94 @@
+"""Scene-level properties of the CPU oracle: film order independent of thread count, BVH culling
+never changes a hit (vs an exhaustive numpy Moller-Trumbore), scene generators match SURVEY §8d."""
+import numpy as np
+import pytest
+
+from libyafaray_amd import scenes
+
+
+def brute_closest(spec, rays):
+    """Exhaustive primitive_triangle.cc:44-71 in float32 numpy (same operation order)."""
+    v = spec.verts[spec.tris]                     # (M, 3, 3)
+    v0, e1, e2 = v[:, 0], v[:, 1] - v[:, 0], v[:, 2] - v[:, 0]
+    f = np.float32
+    l1 = np.sqrt(((e1[:, 0] * e1[:, 0]) + (e1[:, 1] * e1[:, 1])) + (e1[:, 2] * e1[:, 2]))
+    l2 = np.sqrt(((e2[:, 0] * e2[:, 0]) + (e2[:, 1] * e2[:, 1])) + (e2[:, 2] * e2[:, 2]))
+    eps = (f(0.1) * f(0.00005)) * np.maximum(l1, l2)
+
+    def cross(a, b):
+        return np.stack([a[..., 1] * b[..., 2] - a[..., 2] * b[..., 1], a[..., 2] * b[..., 0] - a[..., 0] * b[..., 2],
+                         a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]], -1)
+
+    def dot(a, b):
+        return (a[..., 0] * b[..., 0] + a[..., 1] * b[..., 1]) + a[..., 2] * b[..., 2]
+
+    out_t = np.full(len(rays), -1.0, np.float32)
+    out_p = np.full(len(rays), -1, np.int32)
+    for i, r in enumerate(rays):
+        o, d, tmin, tmax = r[:3], r[3:6], r[6], r[7]
+        pvec = cross(d[None], e2)
+        det = dot(e1, pvec)
+        ok = ~((det > -eps) & (det < eps))
+        with np.errstate(all="ignore"):
+            inv = f(1) / det
+            tvec = o[None] - v0
+            u = dot(tvec, pvec) * inv
+            ok &= ~((u < 0) | (u > 1))
+            q = cross(tvec, e1)
+            vv = dot(d[None], q) * inv
+            ok &= ~((vv < 0) | ((u + vv) > 1))
+            t = dot(e2, q) * inv
+        ok &= ~(t < eps)
+        ok &= t >= tmin
+        if tmax >= 0:
+            ok &= t < tmax
+        if ok.any():
+            tt = np.where(ok, t, np.inf)
+            m = tt.min()
+            out_t[i] = m
+            out_p[i] = np.nonzero(tt == m)[0].min()
+    return out_t, out_p
+
+
+@pytest.mark.parametrize("which", ["cornell", "test01"])
+def test_oracle_bvh_equals_exhaustive(oracle_built, which):
+    spec = scenes.cornell(16, 16) if which == "cornell" else scenes.test01(16, 16)
+    rng = np.random.default_rng(3)
+    n = 3000
+    lo, hi = spec.verts.min(0), spec.verts.max(0)
+    o = lo + rng.random((n, 3)) * (hi - lo)
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d, np.zeros((n, 1)), np.full((n, 1), -1.0)], 1).astype(np.float32)
+    hit, prim = oracle_built.OracleScene(spec).trace_closest(rays)
+    bt, bp = brute_closest(spec, rays)
+    assert np.array_equal(prim, bp)
+    assert np.array_equal(hit[:, 0][prim >= 0], bt[bp >= 0])
+
+
+@pytest.mark.parametrize("integrator", ["directlighting", "pathtracing"])
+def test_film_independent_of_thread_count(oracle_built, integrator):
+    spec = scenes.cornell(48, 40, spp=4, bounces=4, rr=False, integrator=integrator, filter_type="gauss",
+                          pixelwidth=1.5, tile_size=16)
+    a, wa, _ = oracle_built.OracleScene(spec, threads=1).render()
+    b, wb, _ = oracle_built.OracleScene(spec, threads=6).render()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(wa, wb)
+
+
+def test_row_band_render_matches_full_render(oracle_built):
+    spec = scenes.test01(40, 40, spp=2)
+    osc = oracle_built.OracleScene(spec, threads=2)
+    full, _, _ = osc.render()
+    # rows [0, 16) rendered alone: rows 0..14 only receive splats from rows <= 15
+    part, _, _ = osc.render(0, 16)
+    assert np.array_equal(part[:15].view(np.uint32), full[:15].view(np.uint32))
+
+
+def test_generators():
+    c = scenes.cornell(8, 8)
+    assert len(c.tris) == 34 and len(c.materials) == 3
+    s = scenes.cornell_sphere(n=707, width=8, height=8)
+    assert len(s.tris) == 34 + 707 * 707 * 2 == 999732
+    t = scenes.test01(8, 8)
+    assert len(t.tris) == 74
