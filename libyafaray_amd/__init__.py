@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libyafaray4.so")
+LIB_PATH = os.environ.get("YAFARAY_AMD_LIB") or os.path.join(HERE, "libyafaray4.so")
 
 # enums (yafaray_c_api.h)
 LOG_MUTE, LOG_ERROR, LOG_WARNING, LOG_PARAMS, LOG_INFO, LOG_VERBOSE, LOG_DEBUG = range(7)

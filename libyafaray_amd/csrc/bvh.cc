@@ -245,7 +245,7 @@ BvhOutput buildBvh(const BvhInput &in, int leaf_size, int threads)
 		             &out.tris[12 * (size_t)i]);
 	}
 	auto writeChild = [&](const BuildNode &c, int ci, float *lo, float *hi, int &child, int &count) {
-		if(ci < 0 || c.count == 0 && c.left < 0)
+		if(ci < 0 || (c.count == 0 && c.left < 0))
 		{
 			lo[0] = lo[1] = lo[2] = 1.f;
 			hi[0] = hi[1] = hi[2] = -1.f;

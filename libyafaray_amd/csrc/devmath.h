@@ -120,10 +120,30 @@ YD DD exactMul(const X87Const &c, double xd)
 	return fastTwoSum(p, e + q);
 }
 
+// Fast path of the emulation: a double-precision approximation D of the exact value E is within
+// 2^-50 |E| of it.  When D is farther than 1e-6 float-ulp from every float rounding midpoint, E
+// and its x87 64-bit rounding lie on the same side of that midpoint as D, so (float)D is the
+// reference's result; only the ~1e-6 of cases near a midpoint take the exact path.
+YD bool safeToRound(double d, float &f)
+{
+	f = (float)d;
+	uint32_t b;
+	__builtin_memcpy(&b, &f, 4);
+	const int ef = (int)((b >> 23) & 0xffu);
+	if(ef == 0 || ef >= 254) return false;      // zero / subnormal / huge: take the exact path
+	const double ulp = ldexp(1.0, ef - 127 - 23);
+	const double df = (double)f;
+	const double t = fabs(d - df) / ulp;         // in [0, 0.5]
+	const bool low_binade = ((b & 0x7fffffu) == 0) && (fabs(d) < fabs(df));
+	return (low_binade ? 0.25 : 0.5) - t > 1e-6;
+}
+
 // (float)((long double)C * x)
 YD float x87mul(const X87Const &c, float x)
 {
 	if(x == 0.f || !(fabsf(x) < 3.0e38f)) return (float)(c.hi * (double)x);
+	float f;
+	if(safeToRound(c.hi * (double)x, f)) return f;
 	const double ax = fabs((double)x);
 	const float r = round24(round64(exactMul(c, ax)));
 	return x < 0.f ? -r : r;
@@ -133,6 +153,8 @@ YD float x87mul(const X87Const &c, float x)
 YD float x87mul2(const X87Const &c, float x, float y)
 {
 	if(x == 0.f || y == 0.f) return (float)(c.hi * (double)x * (double)y);
+	float f;
+	if(safeToRound(c.hi * (double)x * (double)y, f)) return f;
 	const double ax = fabs((double)x), ay = fabs((double)y);
 	const DD t = round64(exactMul(c, ax));
 	const double p = t.hi * ay;
@@ -148,6 +170,8 @@ YD float x87mul2(const X87Const &c, float x, float y)
 YD float x87mulDiv(const X87Const &c, float a, float b)
 {
 	if(a == 0.f) return 0.f;
+	float f;
+	if(safeToRound(c.hi * (double)a / (double)b, f)) return f;
 	const DD n = round64(exactMul(c, (double)a));
 	const double bd = (double)b;
 	const double q1 = n.hi / bd;
@@ -233,6 +257,19 @@ YD float maxComp(C3 c) { return fmaxf(c.r, fmaxf(c.g, c.b)); }
 // ---------------------------------------------------------------------------------------------
 YD float clamp01(float v) { return fmaxf(0.f, fminf(1.f, v)); }
 
+YD uint32_t bitReverse32(uint32_t v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_bitreverse32(v);
+#else
+	v = (v << 16) | (v >> 16);
+	v = ((v & 0x00ff00ffu) << 8) | ((v & 0xff00ff00u) >> 8);
+	v = ((v & 0x0f0f0f0fu) << 4) | ((v & 0xf0f0f0f0u) >> 4);
+	v = ((v & 0x33333333u) << 2) | ((v & 0xccccccccu) >> 2);
+	return ((v & 0x55555555u) << 1) | ((v & 0xaaaaaaaau) >> 1);
+#endif
+}
+
 YD float riVdC(uint32_t bits, uint32_t r = 0)
 {
 	bits = (bits << 16) | (bits >> 16);
@@ -250,10 +287,17 @@ YD float riS(uint32_t i, uint32_t r = 0)
 	return clamp01((float)((double)r * kSampleMultRatio));
 }
 
+// Larcher-Pillichshammer: bit k of i toggles bits [31-k, 31] of r, so bit (31-t) of r is the
+// parity of i >> t — a suffix-XOR scan plus a bit reversal instead of the 32-step loop.
 YD float riLp(uint32_t i, uint32_t r = 0)
 {
-	for(uint32_t v = 1u << 31; i; i >>= 1, v |= v >> 1)
-		if(i & 1) r ^= v;
+	uint32_t y = i;
+	y ^= y >> 1;
+	y ^= y >> 2;
+	y ^= y >> 4;
+	y ^= y >> 8;
+	y ^= y >> 16;
+	r ^= bitReverse32(y);
 	return clamp01((float)((double)r * kSampleMultRatio));
 }
 
@@ -271,12 +315,21 @@ YD uint32_t fnv32(uint32_t value)
 // Halton(base, start).getNext() — one fresh generator per call site (integrator_montecarlo.cc:399)
 YD float haltonFirst(uint32_t base, double inv_base, uint32_t start)
 {
-	double factor = inv_base, value = 0.0;
-	while(start > 0)
+	double value = 0.0;
+	if(base == 2)
 	{
-		value += (double)(start % base) * factor;
-		start /= base;
-		factor *= inv_base;
+		// halton.h:53-63 in base 2 sums distinct powers of two: exactly bitreverse(start) * 2^-32
+		value = (double)bitReverse32(start) * kSampleMultRatio;
+	}
+	else
+	{
+		double factor = inv_base;
+		while(start > 0)
+		{
+			value += (double)(start % base) * factor;
+			start /= base;
+			factor *= inv_base;
+		}
 	}
 	const double r = 0.9999999999 - value;
 	if(inv_base < r) value += inv_base;

@@ -33,7 +33,13 @@
 namespace yafamd
 {
 
-constexpr int kTraceBlock = 128;
+#ifndef YAF_TRACE_BLOCK
+#define YAF_TRACE_BLOCK 128
+#endif
+#ifndef YAF_SHADE_MIN_WAVES
+#define YAF_SHADE_MIN_WAVES 1
+#endif
+constexpr int kTraceBlock = YAF_TRACE_BLOCK;
 constexpr int kShadeBlock = 256;
 
 enum : uint32_t
@@ -129,7 +135,7 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	const V3 cz = v3(c.cam_z[0], c.cam_z[1], c.cam_z[2]);
 	const float tmin = dot(cz, v3(c.near_p[0], c.near_p[1], c.near_p[2]) - pos) / dot(dir, cz);
 	const float tmax = dot(cz, v3(c.far_p[0], c.far_p[1], c.far_p[2]) - pos) / dot(dir, cz);
-	Q.slot[i] = i;
+	Q.slot[i] = i;          // sample id within the chunk travels with the queue entry
 	Q.ray_o[i] = f4(pos, tmin);
 	Q.ray_d[i] = f4(dir, tmax);
 	P.stage[i] = ST_CAMERA;
@@ -328,7 +334,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, 
 			float t;
 			int prim;
 			const bool occ = traverse<true>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
-			P.occ[Q.sh_idx[k]] = occ ? 1 : 0;
+			P.occ[Q.sh_idx[k]] = occ ? 1 : 0;   // P = state set of the consumer shade
 			++n_shadow;
 		}
 	}
@@ -541,7 +547,7 @@ __device__ __forceinline__ void shadowRayOf(V3 from, V3 dir, float tmin, float t
 // nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
 // Wave-uniform structure: `active` lanes do the work, every lane walks the same loop bounds.
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
-                         uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int slot, int base,
+                         uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
                          float4 *nee, uint8_t *occ, const ShadeOut &out)
 {
 	const bool cast_shadows = L.cast_shadows && m.receive_shadows;
@@ -568,11 +574,11 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			const C3 transmit = c3(1.f);
 			contrib = surf_col * lcol * angle * transmit;
 			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
-			nee[slot * S.nee_k + base] = f4(contrib, 1.f);
+			nee[e0] = f4(contrib, 1.f);
 		}
-		else if(active) nee[slot * S.nee_k + base] = make_float4(0.f, 0.f, 0.f, 0.f);
-		if(active) occ[slot * S.nee_k + base] = 0;
-		emitShadow(ok && cast_shadows, so, ldir, st, slot * S.nee_k + base, out);
+		else if(active) nee[e0] = make_float4(0.f, 0.f, 0.f, 0.f);
+		if(active) occ[e0] = 0;
+		emitShadow(ok && cast_shadows, so, ldir, st, e0, out);
 		return;
 	}
 	// area light: montecarlo.cc:393-405
@@ -628,10 +634,10 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 		}
 		if(active)
 		{
-			nee[slot * S.nee_k + base + i] = f4(contrib, ok ? 1.f : 0.f);
-			occ[slot * S.nee_k + base + i] = 0;
+			nee[e0 + i] = f4(contrib, ok ? 1.f : 0.f);
+			occ[e0 + i] = 0;
 		}
-		emitShadow(ok && cast_shadows, so, ldir, st, slot * S.nee_k + base + i, out);
+		emitShadow(ok && cast_shadows, so, ldir, st, e0 + i, out);
 	}
 	for(int i = 0; i < num_samples; ++i)
 	{
@@ -681,17 +687,16 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 		}
 		if(active)
 		{
-			nee[slot * S.nee_k + base + num_samples + i] = f4(contrib, ok ? 1.f : 0.f);
-			occ[slot * S.nee_k + base + num_samples + i] = 0;
+			nee[e0 + num_samples + i] = f4(contrib, ok ? 1.f : 0.f);
+			occ[e0 + num_samples + i] = 0;
 		}
-		emitShadow(ok && cast_shadows, so, dir, st, slot * S.nee_k + base + num_samples + i, out);
+		emitShadow(ok && cast_shadows, so, dir, st, e0 + num_samples + i, out);
 	}
 }
 
 // Sum of one light's entries with the reference's addition order (montecarlo.cc:385-408).
-__device__ C3 neeSum(const DevScene &S, const DevLight &L, const float4 *nee, const uint8_t *occ, int slot, int base)
+__device__ C3 neeSum(const DevScene &S, const DevLight &L, const float4 *nee, const uint8_t *occ, int k0)
 {
-	const int k0 = slot * S.nee_k + base;
 	if(L.type == LIGHT_POINT)
 	{
 		const float4 e = nee[k0];
@@ -723,7 +728,8 @@ __device__ __forceinline__ float ldsDim(const DevScene &S, int dim, uint32_t n)
 struct ShadeArgs
 {
 	DevScene S;
-	DevPaths P;
+	DevPaths Pc;         // state of the current active list (indexed by queue position)
+	DevPaths Pn;         // state of the next active list (written at the compacted position)
 	DevQueues Q;         // current (active list + hits)
 	DevQueues Qn;        // next
 	const DevCounters *cnt;
@@ -734,9 +740,9 @@ struct ShadeArgs
 	uint64_t chunk_base;
 };
 
-__device__ __forceinline__ void writeSample(const ShadeArgs &A, int slot, C3 col, float alpha)
+__device__ __forceinline__ void writeSample(const ShadeArgs &A, uint32_t sid, C3 col, float alpha)
 {
-	const SampleCoord sc = sampleCoord(A.jobs, A.n_jobs, A.S.width, A.S.tile, A.S.spp, A.chunk_base + (uint64_t)slot);
+	const SampleCoord sc = sampleCoord(A.jobs, A.n_jobs, A.S.width, A.S.tile, A.S.spp, A.chunk_base + (uint64_t)sid);
 	if(alpha > 1.f) alpha = 1.f;   // integrator_tiled.cc:399
 	A.samples[((size_t)sc.y * A.S.width + sc.x) * A.S.spp + sc.s] = f4(col, alpha);
 }
@@ -755,40 +761,58 @@ __device__ __forceinline__ Surf surfFromPrim(const DevScene &S, V3 p, int prim)
 	return s;
 }
 
-// One path vertex per active slot.  Control flow restates PathIntegrator::integrate
+// One path vertex per active queue entry.  Control flow restates PathIntegrator::integrate
 // (integrator_path_tracer.cc:120-290) / DirectLightIntegrator::integrate (:97-144) as a state
 // machine whose vertices are processed one iteration at a time:
 //   1. connect the estimate left pending by the previous vertex (its shadow rays were traced
 //      by this iteration's k_trace) — additions happen in the reference's order;
 //   2. shade the new hit (camera hit v0, first segment hit v1, or bounce hit);
-//   3. next-event estimation: contributions + shadow rays (wave-uniform loops);
-//   4. sample the next segment, or end the subpath (next subpath / finalize);
-//   5. wave-ballot compaction of the slots that continue.
-__global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
+//   3. sample the next segment, or end the subpath (next subpath / finalize);
+//   4. wave-ballot compaction: the entry's state moves to its position in the next queue
+//      (coalesced SoA reads and writes, no indirection);
+//   5. next-event estimation into the next state: contributions + shadow rays.
+__global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(ShadeArgs A)
 {
 	const DevScene &S = A.S;
-	const DevPaths &P = A.P;
+	const DevPaths &Pc = A.Pc;
+	const DevPaths &Pn = A.Pn;
 	const uint32_t n_a = A.cnt->n_active;
 	ShadeOut out;
 	out.sh_count = &A.cnt_next->n_shadow;
 	out.Qn = A.Qn;
 	const bool is_path = S.integrator == INT_PATH;
 	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
+	const int K = S.nee_k;
 	const uint32_t stride = gridDim.x * blockDim.x;
 	for(uint32_t base_i = blockIdx.x * blockDim.x; base_i < n_a; base_i += stride)
 	{
 		const uint32_t i = base_i + threadIdx.x;
 		const bool live = i < n_a;
-		int slot = 0;
-		uint32_t stage = ST_NORAY, flags = 0;
-		uint2 pix = make_uint2(0u, 0u);
+		// ---- 0. load the entry (independent coalesced loads) ----
+		uint32_t sid = 0, stage = ST_NORAY, flags = 0;
+		uint2 pix = make_uint2(0u, 0u), rng = make_uint2(0u, 0u);
+		float w = 0.f;
+		float4 thr4 = make_float4(0.f, 0.f, 0.f, 0.f), col4 = thr4, pcol4 = thr4, pwo4 = thr4, pthr4 = thr4, pem4 = thr4;
+		float4 v0p4 = thr4, v0wo4 = thr4;
 		if(live)
 		{
-			slot = A.Q.slot[i];
-			stage = P.stage[slot];
-			flags = P.flags[slot];
-			pix = P.pix[slot];
+			sid = (uint32_t)A.Q.slot[i];
+			stage = Pc.stage[i];
+			flags = Pc.flags[i];
+			pix = Pc.pix[i];
+			rng = Pc.rng[i];
+			w = Pc.w[i];
+			thr4 = Pc.thr[i];
+			col4 = Pc.col[i];
+			pcol4 = Pc.pcol[i];
+			pwo4 = Pc.pwo[i];
+			pthr4 = Pc.pend_thr[i];
+			if(flags & F_PEND_EMIT) pem4 = Pc.pend_emit[i];
+			if(n_paths > 1) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
 		}
+		C3 thr = rgb(thr4), col = rgb(col4), pcol = rgb(pcol4);
+		const float alpha = col4.w;
+		V3 pwo = xyz(pwo4);
 		const uint32_t st = stage & 0xffu;
 		uint32_t subpath = (stage >> 8) & 0xfffu;
 		int depth = (int)(stage >> 20);
@@ -799,17 +823,16 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 		{
 			// estimateAllDirectLight (montecarlo.cc:54-68): col += sum over lights in name order
 			C3 total = c3(0.f);
-			for(int l = 0; l < S.n_lights; ++l) total = total + neeSum(S, S.lights[l], P.nee, P.occ, slot, (int)S.lights[l].nee_base);
-			const float4 c = P.col[slot];
-			P.col[slot] = f4(rgb(c) + total, c.w);
+			for(int l = 0; l < S.n_lights; ++l) total = total + neeSum(S, S.lights[l], Pc.nee, Pc.occ, (int)i * K + (int)S.lights[l].nee_base);
+			col = col + total;
 		}
 		if(live && (flags & F_PEND_ONE))
 		{
 			// path_tracer.cc:201-207 / :244-266: lcol = estimateOne * nlights (+ emit); path_col += lcol * thr
 			const int lnum = (int)(flags >> F_LNUM_SHIFT);
-			C3 lcol = neeSum(S, S.lights[lnum], P.nee, P.occ, slot, 0) * (float)S.n_lights;
-			if(flags & F_PEND_EMIT) lcol = lcol + rgb(P.pend_emit[slot]);
-			P.pcol[slot] = f4(rgb(P.pcol[slot]) + lcol * rgb(P.pend_thr[slot]), 0.f);
+			C3 lcol = neeSum(S, S.lights[lnum], Pc.nee, Pc.occ, (int)i * K) * (float)S.n_lights;
+			if(flags & F_PEND_EMIT) lcol = lcol + rgb(pem4);
+			pcol = pcol + lcol * rgb(pthr4);
 		}
 		flags &= ~(F_PEND_V0 | F_PEND_ONE | F_PEND_EMIT);
 
@@ -818,20 +841,21 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
 		V3 wo = v3(0.f, 0.f, 1.f);
 		bool have_hit = false;
+		int hit_prim = -1;
 		if(live && st != ST_NORAY)
 		{
-			const int prim = A.Q.hit_prim[i];
-			if(prim >= 0)
+			hit_prim = A.Q.hit_prim[i];
+			if(hit_prim >= 0)
 			{
 				const float4 ro = A.Q.ray_o[i], rd = A.Q.ray_d[i];
 				have_hit = true;
-				sp = makeSurf(S, xyz(ro), xyz(rd), A.Q.hit_t[i], prim);
+				sp = makeSurf(S, xyz(ro), xyz(rd), A.Q.hit_t[i], hit_prim);
 				wo = -xyz(rd);
 			}
 		}
 		bool nee_v0 = false, nee_one = false, sample_next = false, end_sub = false, finalize = false, start_sub = false;
 		C3 emit_pend = c3(0.f);
-		C3 thr = c3(0.f);
+		C3 pend_thr = c3(0.f);
 		if(live)
 		{
 			if(st == ST_NORAY) end_sub = true;   // a finished subpath whose estimate just got connected
@@ -840,23 +864,22 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 				if(!have_hit)
 				{
 					// integrator_tiled.cc:707-720 background
-					C3 col = c3(0.f);
-					float alpha = 1.f;
-					if(S.bg_transp) alpha = 0.f;
-					else if(S.has_bg) col = C3{S.bg[0], S.bg[1], S.bg[2]};
-					writeSample(A, slot, col, alpha);
+					C3 bg = c3(0.f);
+					float a = 1.f;
+					if(S.bg_transp) a = 0.f;
+					else if(S.has_bg) bg = C3{S.bg[0], S.bg[1], S.bg[2]};
+					writeSample(A, sid, bg, a);
 				}
 				else
 				{
 					const DevMaterial &m = S.mats[sp.mat];
-					C3 col = c3(0.f);
+					col = c3(0.f);
 					if(sp.flags & B_EMIT) col = col + matEmit(m, sp, wo);
-					P.col[slot] = f4(col, 1.f);
 					if(sp.flags & B_DIFFUSE) { nee_v0 = true; flags |= F_V0_DIFFUSE; }
 					if(is_path && (sp.flags & B_DIFFUSE))
 					{
-						P.v0p[slot] = f4(sp.p, __int_as_float(A.Q.hit_prim[i]));
-						P.v0wo[slot] = f4(wo, 0.f);
+						v0p4 = f4(sp.p, __int_as_float(hit_prim));
+						v0wo4 = f4(wo, 0.f);
 						start_sub = true;
 						subpath = 0;
 					}
@@ -869,12 +892,12 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 				else
 				{
 					// path_tracer.cc:193-207
-					if(flags & F_SAMPLED) P.pwo[slot] = f4(wo, 0.f);
-					else wo = xyz(P.pwo[slot]);
+					if(flags & F_SAMPLED) pwo = wo;
+					else wo = pwo;
 					nee_one = true;
 					flags = (flags & ~F_MATFLAGS) | (sp.flags & F_MATFLAGS);
 					if(sp.flags & B_EMIT) { emit_pend = matEmit(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
-					thr = rgb(P.thr[slot]);
+					pend_thr = thr;
 					depth = 1;
 					sample_next = true;
 				}
@@ -885,16 +908,14 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 				else
 				{
 					const uint32_t mfl = flags & F_MATFLAGS;
-					P.pwo[slot] = f4(wo, 0.f);
-					thr = rgb(P.thr[slot]);
+					pwo = wo;
 					bool killed = false;
 					if(depth > S.rr_min_bounces)
 					{
 						// path_tracer.cc:249-255 (the draw does not depend on the light estimate)
-						const uint2 r = P.rng[slot];
-						Mwc g{r.x, r.y};
+						Mwc g{rng.x, rng.y};
 						const float random_value = (float)g.next();
-						P.rng[slot] = make_uint2(g.x, g.c);
+						rng = make_uint2(g.x, g.c);
 						const float probability = maxComp(thr);
 						if(probability <= 0.f || probability < random_value) killed = true;
 						else thr = thr * (1.f / probability);
@@ -902,15 +923,14 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 					if(killed) end_sub = true;
 					else
 					{
-						P.thr[slot] = f4(thr, 0.f);
 						if((mfl & B_EMIT) && (flags & F_CAUSTIC)) { emit_pend = matEmit(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
-						if(mfl & B_DIFFUSE) nee_one = true;
+						if(mfl & B_DIFFUSE) { nee_one = true; pend_thr = thr; }
 						else
 						{
 							// lcol = 0 (+ emission): nothing to trace, connect now
 							C3 lcol = c3(0.f);
 							if(flags & F_PEND_EMIT) lcol = lcol + emit_pend;
-							P.pcol[slot] = f4(rgb(P.pcol[slot]) + lcol * thr, 0.f);
+							pcol = pcol + lcol * thr;
 							flags &= ~F_PEND_EMIT;
 						}
 						++depth;
@@ -932,29 +952,11 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 				lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
 			}
 			flags = (flags & ((1u << F_LNUM_SHIFT) - 1u)) | (lnum << F_LNUM_SHIFT) | F_PEND_ONE;
-			P.pend_thr[slot] = f4(thr, 0.f);
-			if(flags & F_PEND_EMIT) P.pend_emit[slot] = f4(emit_pend, 0.f);
 		}
 		if(nee_v0) flags |= F_PEND_V0;
+		const bool pending = (flags & (F_PEND_V0 | F_PEND_ONE)) != 0;
 
-		// ---- 3. next-event estimation ----
-		if(__any(nee_v0))
-		{
-			for(int l = 0; l < S.n_lights; ++l)
-				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, nee_v0, slot,
-				         (int)S.lights[l].nee_base, P.nee, P.occ, out);
-		}
-		if(__any(nee_one))
-		{
-			for(int l = 0; l < S.n_lights; ++l)
-			{
-				const bool mine = nee_one && (int)lnum == l;
-				if(!__any(mine)) continue;
-				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, mine, slot, 0, P.nee, P.occ, out);
-			}
-		}
-
-		// ---- 4. next segment ----
+		// ---- 3. next segment ----
 		V3 ray_o = v3(0.f, 0.f, 0.f), ray_d = v3(0.f, 0.f, 1.f);
 		bool want_ray = false;
 		if(live && sample_next)
@@ -970,15 +972,13 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 				s.flags = B_ALL;
 				s.pdf = 0.f;
 				s.sampled = B_NONE;
-				float w = P.w[slot];
 				V3 dir = v3(0.f, 0.f, 0.f);
 				C3 scol = matSample(S.mats[sp.mat], sp, wo, dir, s, w);
-				P.w[slot] = w;
 				scol = scol * w;
 				if(isBlack(scol)) end_sub = true;
 				else
 				{
-					P.thr[slot] = f4(thr * scol, 0.f);
+					thr = thr * scol;
 					if(S.caustic_path && (s.sampled & (B_SPECULAR | B_GLOSSY | B_FILTER))) flags |= F_CAUSTIC;
 					else flags &= ~F_CAUSTIC;
 					ray_o = sp.p;
@@ -989,7 +989,6 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 			}
 			else end_sub = true;
 		}
-		const bool pending = (flags & (F_PEND_V0 | F_PEND_ONE)) != 0;
 		if(live && end_sub && !pending)
 		{
 			// end of the subpath: next subpath (path_tracer.cc:166) or the end of integrate()
@@ -999,9 +998,8 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 		if(live && start_sub)
 		{
 			// path_tracer.cc:168-191: first segment of subpath `subpath` from v0
-			const float4 v0p = P.v0p[slot];
-			const Surf s0 = (st == ST_CAMERA) ? sp : surfFromPrim(S, xyz(v0p), __float_as_int(v0p.w));
-			const V3 wo0 = (st == ST_CAMERA) ? wo : xyz(P.v0wo[slot]);
+			const Surf s0 = (st == ST_CAMERA) ? sp : surfFromPrim(S, xyz(v0p4), __float_as_int(v0p4.w));
+			const V3 wo0 = (st == ST_CAMERA) ? wo : xyz(v0wo4);
 			const uint32_t offs = n_paths * sample_idx + offset + subpath;
 			BsdfSample s;
 			s.s_1 = riVdC(offs);
@@ -1009,13 +1007,10 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 			s.flags = B_DIFFUSE | B_REFLECT | B_TRANSMIT;
 			s.pdf = 0.f;
 			s.sampled = B_NONE;
-			float w = P.w[slot];
 			V3 dir = v3(0.f, 0.f, 0.f);
 			C3 scol = matSample(S.mats[s0.mat], s0, wo0, dir, s, w);
-			P.w[slot] = w;
-			scol = scol * w;
-			P.thr[slot] = f4(scol, 0.f);
-			P.pwo[slot] = f4(wo0, 0.f);
+			thr = scol * w;
+			pwo = wo0;
 			if(s.sampled != B_NONE) flags |= F_SAMPLED;
 			else flags &= ~F_SAMPLED;
 			flags &= ~F_CAUSTIC;
@@ -1027,19 +1022,17 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 		if(live && finalize)
 		{
 			// path_tracer.cc:274-278 / direct_light.cc:129-131
-			const float4 c = P.col[slot];
-			C3 col = rgb(c);
-			if(is_path && (flags & F_V0_DIFFUSE)) col = col + rgb(P.pcol[slot]) / (float)n_paths;
+			if(is_path && (flags & F_V0_DIFFUSE)) col = col + pcol / (float)n_paths;
 			col = col + c3(0.f);   // recursiveRaytrace: no specular/glossy component
-			writeSample(A, slot, col, c.w);
+			writeSample(A, sid, col, alpha);
 		}
 
-		// ---- 5. compaction ----
-		const bool keep = live && (want_ray || (end_sub && pending));
+		// ---- 4. compaction: the entry moves to position k of the next queue ----
+		const bool keep = live && (want_ray || pending);   // pending => never finalized this iteration
 		const uint32_t k = waveAppend(keep, &A.cnt_next->n_active);
 		if(keep)
 		{
-			A.Qn.slot[k] = slot;
+			A.Qn.slot[k] = (int)sid;
 			if(want_ray)
 			{
 				A.Qn.ray_o[k] = f4(ray_o, S.ray_min_dist);
@@ -1049,10 +1042,38 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(ShadeArgs A)
 			{
 				A.Qn.ray_o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
 				A.Qn.ray_d[k] = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));
-				stage = ST_NORAY | (subpath << 8);
+				stage = ST_NORAY | (subpath << 8) | ((uint32_t)depth << 20);
 			}
-			P.stage[slot] = stage;
-			P.flags[slot] = flags;
+			Pn.stage[k] = stage;
+			Pn.flags[k] = flags;
+			Pn.pix[k] = pix;
+			Pn.rng[k] = rng;
+			Pn.w[k] = w;
+			Pn.thr[k] = f4(thr, 0.f);
+			Pn.col[k] = f4(col, alpha);
+			Pn.pcol[k] = f4(pcol, 0.f);
+			Pn.pwo[k] = f4(pwo, 0.f);
+			if(nee_one) Pn.pend_thr[k] = f4(pend_thr, 0.f);
+			if(flags & F_PEND_EMIT) Pn.pend_emit[k] = f4(emit_pend, 0.f);
+			if(n_paths > 1) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }
+		}
+
+		// ---- 5. next-event estimation into the next state (wave-uniform loops, masked lanes) ----
+		const int e0 = (int)k * K;
+		if(__any(nee_v0))
+		{
+			for(int l = 0; l < S.n_lights; ++l)
+				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, nee_v0,
+				         e0 + (int)S.lights[l].nee_base, Pn.nee, Pn.occ, out);
+		}
+		if(__any(nee_one))
+		{
+			for(int l = 0; l < S.n_lights; ++l)
+			{
+				const bool mine = nee_one && (int)lnum == l;
+				if(!__any(mine)) continue;
+				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, mine, e0, Pn.nee, Pn.occ, out);
+			}
 		}
 	}
 }
@@ -1071,23 +1092,32 @@ __device__ __forceinline__ uint64_t pixelRank(int x, int y, int W, int H, int ts
 	return (uint64_t)ty * ts * W + (uint64_t)tx * ts * th + (uint64_t)(y - ty * ts) * tw + (x - tx * ts);
 }
 
+// RF / RB: compile-time footprint reach (box and gauss filters: RF = 1, RB = 0 -> a 2x2 window
+// kept in registers); RF = RB = -1 selects the generic runtime window (<= 9x9).
+template<int RF, int RB>
 __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, float4 *out, float *weights,
                                               int y0, int y1, float clamp_samples)
 {
+	constexpr bool kStatic = RF >= 0;
+	constexpr int kWin = kStatic ? (RF + RB + 1) * (RF + RB + 1) : 81;
 	const int x = blockIdx.x * blockDim.x + threadIdx.x;
 	const int y = y0 + blockIdx.y;
 	if(x >= F.width || y >= y1) return;
 	const int W = F.width, H = F.height, spp = F.spp;
+	const int rf = kStatic ? RF : F.reach_fwd, rb = kStatic ? RB : F.reach_back;
 	// candidate sources, sorted by their rank in the reference's splat order
-	int sx[81], sy[81];
-	uint64_t rk[81];
+	int sx[kWin], sy[kWin];
+	uint64_t rk[kWin];
 	int n = 0;
-	for(int yy = y - F.reach_fwd; yy <= y + F.reach_back; ++yy)
+#pragma unroll
+	for(int dyy = 0; dyy < (kStatic ? RF + RB + 1 : 9); ++dyy)
 	{
-		if(yy < 0 || yy >= H) continue;
-		for(int xx = x - F.reach_fwd; xx <= x + F.reach_back; ++xx)
+#pragma unroll
+		for(int dxx = 0; dxx < (kStatic ? RF + RB + 1 : 9); ++dxx)
 		{
-			if(xx < 0 || xx >= W) continue;
+			if(!kStatic && (dyy > rf + rb || dxx > rf + rb)) continue;
+			const int yy = y - rf + dyy, xx = x - rf + dxx;
+			if(yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
 			const uint64_t r = pixelRank(xx, yy, W, H, F.tile);
 			int p = n++;
 			while(p > 0 && rk[p - 1] > r) { rk[p] = rk[p - 1]; sx[p] = sx[p - 1]; sy[p] = sy[p - 1]; --p; }
@@ -1101,6 +1131,7 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 	{
 		const int px = sx[c], py = sy[c];
 		const uint32_t offset = fnv32((uint32_t)py * fnv32((uint32_t)px));
+		const int ox = x - px, oy = y - py;
 		for(int s = 0; s < spp; ++s)
 		{
 			float dx = 0.5f, dy = 0.5f;
@@ -1114,7 +1145,6 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 			const int dx_1 = min(W - px - 1, roundToInt((double)dx + F.filterw - 1.0));
 			const int dy_0 = max(0 - py, roundToInt((double)dy - F.filterw));
 			const int dy_1 = min(H - py - 1, roundToInt((double)dy + F.filterw - 1.0));
-			const int ox = x - px, oy = y - py;
 			if(ox < dx_0 || ox > dx_1 || oy < dy_0 || oy > dy_1) continue;
 			const int xi = floorToInt(fabs(((double)ox - (dx - 0.5)) * F.table_scale));
 			const int yi = floorToInt(fabs(((double)oy - (dy - 0.5)) * F.table_scale));
@@ -1192,6 +1222,8 @@ using namespace yafamd;
 
 extern "C" {
 
+int yafamd_trace_block() { return kTraceBlock; }
+
 hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, DevCounters *cnt,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st)
 {
@@ -1213,13 +1245,14 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 	return hipGetLastError();
 }
 
-hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevQueues *Qn,
-                               const DevCounters *cnt, DevCounters *cnt_next, float4 *samples, const DevJob *jobs,
-                               int n_jobs, uint64_t chunk_base, int grid, hipStream_t st)
+hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
+                               const DevQueues *Qn, const DevCounters *cnt, DevCounters *cnt_next, float4 *samples,
+                               const DevJob *jobs, int n_jobs, uint64_t chunk_base, int grid, hipStream_t st)
 {
 	ShadeArgs A;
 	A.S = *S;
-	A.P = *P;
+	A.Pc = *Pc;
+	A.Pn = *Pn;
 	A.Q = *Q;
 	A.Qn = *Qn;
 	A.cnt = cnt;
@@ -1236,8 +1269,11 @@ hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *o
                               float clamp_samples, hipStream_t st)
 {
 	if(y1 <= y0) return hipSuccess;
-	hipLaunchKernelGGL(k_film, dim3((F->width + 255) / 256, y1 - y0), dim3(256), 0, st, *F, samples, out, weights, y0,
-	                   y1, clamp_samples);
+	const dim3 grid((F->width + 255) / 256, y1 - y0);
+	if(F->reach_fwd == 1 && F->reach_back == 0)
+		hipLaunchKernelGGL((k_film<1, 0>), grid, dim3(256), 0, st, *F, samples, out, weights, y0, y1, clamp_samples);
+	else
+		hipLaunchKernelGGL((k_film<-1, -1>), grid, dim3(256), 0, st, *F, samples, out, weights, y0, y1, clamp_samples);
 	return hipGetLastError();
 }
 

@@ -17,7 +17,8 @@ hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQ
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st);
 hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, DevCounters *cnt_next,
                                const DevPaths *P, DevStats *stats, int stack_depth, int grid, hipStream_t st);
-hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevQueues *Qn,
+int yafamd_trace_block();
+hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q, const DevQueues *Qn,
                                const DevCounters *cnt, DevCounters *cnt_next, float4 *samples, const DevJob *jobs,
                                int n_jobs, uint64_t chunk_base, int grid, hipStream_t st);
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
@@ -35,7 +36,7 @@ struct Buf
 	size_t bytes = 0;
 	void release()
 	{
-		if(p) hipFree(p);
+		if(p) (void)hipFree(p);
 		p = nullptr;
 		bytes = 0;
 	}
@@ -81,7 +82,7 @@ struct GpuRenderer::Impl
 	size_t slots_cap = 0;
 	int nee_cap = 0;
 	std::vector<Buf> chunk_bufs;
-	DevPaths P{};
+	DevPaths P[2]{};       // path state, parallel to Q[q] (indexed by queue position)
 	DevQueues Q[2]{};
 	Buf counters, stats;
 	std::vector<hipEvent_t> ev_pool;
@@ -93,8 +94,8 @@ struct GpuRenderer::Impl
 		              &weights, &jobs, &counters, &stats})
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
-		for(hipEvent_t e : ev_pool) hipEventDestroy(e);
-		if(stream) hipStreamDestroy(stream);
+		for(hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+		if(stream) (void)hipStreamDestroy(stream);
 	}
 };
 
@@ -175,7 +176,7 @@ bool GpuRenderer::upload(const HostScene &hs)
 	d.depth = hs.bvh.depth;
 	d.stack_depth = std::max(8, ((hs.bvh.depth + 2 + 7) / 8) * 8);
 	const size_t scene_bytes = (size_t)(4 * d.n_nodes + 3 * d.n_tris) * 16;
-	d.scene_in_lds = scene_bytes + (size_t)d.stack_depth * 128 * 4 <= 48 * 1024;
+	d.scene_in_lds = scene_bytes + (size_t)d.stack_depth * yafamd_trace_block() * 4 <= 48 * 1024;
 	// Faure tables, dims 0..49 (halton.cc:403-414: dims 0-2 share the base-3 table)
 	std::vector<uint8_t> perm;
 	std::vector<uint32_t> off(50), base(50);
@@ -281,22 +282,25 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			b.bytes = bytes;
 			return b.p;
 		};
-		DevPaths &P = d.P;
-		P.stage = (uint32_t *)A(M * 4);
-		P.flags = (uint32_t *)A(M * 4);
-		P.w = (float *)A(M * 4);
-		P.thr = (float4 *)A(M * 16);
-		P.col = (float4 *)A(M * 16);
-		P.pcol = (float4 *)A(M * 16);
-		P.pwo = (float4 *)A(M * 16);
-		P.pend_thr = (float4 *)A(M * 16);
-		P.pend_emit = (float4 *)A(M * 16);
-		P.v0p = (float4 *)A(M * 16);
-		P.v0wo = (float4 *)A(M * 16);
-		P.rng = (uint2 *)A(M * 8);
-		P.pix = (uint2 *)A(M * 8);
-		P.nee = (float4 *)A(M * K * 16);
-		P.occ = (uint8_t *)A(M * K);
+		for(int q = 0; q < 2; ++q)
+		{
+			DevPaths &P = d.P[q];
+			P.stage = (uint32_t *)A(M * 4);
+			P.flags = (uint32_t *)A(M * 4);
+			P.w = (float *)A(M * 4);
+			P.thr = (float4 *)A(M * 16);
+			P.col = (float4 *)A(M * 16);
+			P.pcol = (float4 *)A(M * 16);
+			P.pwo = (float4 *)A(M * 16);
+			P.pend_thr = (float4 *)A(M * 16);
+			P.pend_emit = (float4 *)A(M * 16);
+			P.v0p = (float4 *)A(M * 16);
+			P.v0wo = (float4 *)A(M * 16);
+			P.rng = (uint2 *)A(M * 8);
+			P.pix = (uint2 *)A(M * 8);
+			P.nee = (float4 *)A(M * K * 16);
+			P.occ = (uint8_t *)A(M * K);
+		}
 		for(int q = 0; q < 2; ++q)
 		{
 			DevQueues &Q = d.Q[q];
@@ -338,15 +342,15 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	{
 		if(canceled && *canceled) break;
 		const int n = (int)std::min<uint64_t>(M, total - base);
-		HIPCHECK(yafamd_launch_camera(&S, &d.P, &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
+		HIPCHECK(yafamd_launch_camera(&S, &d.P[0], &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
 		int cur = 0;
 		for(int it = 0; it < iters; ++it)
 		{
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i], d.stream));
-			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &cnt[cur ^ 1], &d.P, dstats, d.stack_depth, d.trace_grid, d.stream));
+			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &cnt[cur ^ 1], &d.P[cur], dstats, d.stack_depth, d.trace_grid, d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 1], d.stream));
 			if(rp.profile) ev_i += 2;
-			HIPCHECK(yafamd_launch_shade(&S, &d.P, &d.Q[cur], &d.Q[cur ^ 1], &cnt[cur], &cnt[cur ^ 1], (float4 *)d.samples.p,
+			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &cnt[cur], &cnt[cur ^ 1], (float4 *)d.samples.p,
 			                             (const DevJob *)d.jobs.p, n_jobs, base, d.shade_grid, d.stream));
 			cur ^= 1;
 		}
