@@ -43,6 +43,10 @@ def parse():
     return ap.parse_args()
 
 
+def traffic_config(a, W, H):
+    return f"{a.scene}-{W}x{H}x{a.spp}-b{a.bounces}-rr{int(not a.no_rr)}-chunk{a.chunk}"
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,7 +144,11 @@ def main():
         try:
             with open(tfile) as f:
                 tj = json.load(f)
-            if tj.get("config") == f"{a.scene}-{W}x{H}x{a.spp}-b{a.bounces}-rr{int(not a.no_rr)}-chunk{a.chunk}":
+            import hashlib
+            with open(os.path.join(ROOT, "libyafaray_amd", "csrc", "kernels.hip"), "rb") as f:
+                sha = hashlib.sha1(f.read()).hexdigest()
+            # only a measurement of this exact kernel source on this exact workload counts
+            if tj.get("config") == traffic_config(a, W, H) and tj.get("kernels_hip_sha1") == sha:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None

@@ -96,3 +96,19 @@ def test_params_are_strictly_typed(product):
     yi.paramsSetVector("point2", 0, 1, 0)
     assert yi.createLight("l") == 1
     yi.close()
+
+
+CLIENTS = os.path.join(ROOT, "oracle", "_ref", "clients")
+
+
+@pytest.mark.skipif(not os.path.isdir(CLIENTS), reason="reference clients not built (needs /root/reference at build time)")
+@pytest.mark.parametrize("t", ["00", "01", "02", "03", "04"])
+def test_reference_clients_link_and_run(product, tmp_path, t):
+    """The reference's own C clients (tests/test0N/test0N.c), compiled against include/ and linked
+    against libyafaray4.so.4, resolve every symbol and run to completion.  Without a GPU the render
+    step logs the no-fallback error; unsupported plugin types are logged, never fatal."""
+    exe = os.path.join(CLIENTS, f"test{t}")
+    r = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-2000:]
+    assert "symbol lookup error" not in out and "error while loading" not in out

@@ -103,3 +103,19 @@ def test_path_RR_statistical(product, oracle_built):
     z = np.abs(a - b) / s
     assert z.max() < 5.0, z.max()
     assert abs(a.mean() - b.mean()) / b.mean() < 0.02
+
+
+def test_reference_client_test01_renders(tmp_path):
+    """The reference's tests/test01/test01.c client (built by `make -C oracle clients`) renders its
+    scene on the GPU through the drop-in library without any error (textures are accepted and
+    reported as not evaluated yet: warnings only)."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "clients", "test01")
+    if not os.path.exists(exe):
+        pytest.skip("reference clients not built")
+    r = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-2000:]
+    errors = [ln for ln in out.splitlines() if "ERROR" in ln]
+    assert not errors, errors[:5]
