@@ -183,6 +183,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_trace", "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
                          "algo_bytes_per_launch": round(per_launch)},
+            "launch": {k: s[k] for k in ("trace_grid", "shade_grid", "trace_block", "stack_depth", "scene_in_lds")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

@@ -38,6 +38,8 @@ typedef struct
 	double trace_kernel_ms;     /* summed k_trace time (hipEvent pairs), 0 if not profiled */
 	uint64_t trace_launches;
 	uint32_t bvh_nodes, bvh_depth, scene_in_lds, pad;
+	uint32_t trace_grid, shade_grid;   /* persistent grids (workgroups) of k_trace / k_shade */
+	uint32_t trace_block, stack_depth;
 } yafaray_amd_stats_t;
 
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */

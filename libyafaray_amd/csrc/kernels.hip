@@ -85,6 +85,29 @@ __device__ __forceinline__ uint32_t waveAppend(bool want, uint32_t *counter)
 	return base + (uint32_t)__popcll(below);
 }
 
+// Workgroup-level append (one atomic per workgroup): every thread of the block must call it.
+// `scratch` is LDS of at least blockDim/64 + 1 words.
+template<int BLOCK>
+__device__ __forceinline__ uint32_t blockAppend(bool want, uint32_t *counter, uint32_t *scratch)
+{
+	const uint64_t mask = __ballot(want);
+	const int wid = threadIdx.x >> 6;
+	if(laneId() == 0) scratch[wid] = (uint32_t)__popcll(mask);
+	__syncthreads();
+	if(threadIdx.x == 0)
+	{
+		uint32_t tot = 0;
+		for(int w = 0; w < BLOCK / 64; ++w) tot += scratch[w];
+		scratch[BLOCK / 64] = tot ? atomicAdd(counter, tot) : 0u;
+	}
+	__syncthreads();
+	uint32_t base = scratch[BLOCK / 64];
+	for(int w = 0; w < wid; ++w) base += scratch[w];
+	__syncthreads();   // scratch is reused by the next call
+	const uint64_t below = mask & ((1ull << laneId()) - 1ull);
+	return base + (uint32_t)__popcll(below);
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_camera
 // ---------------------------------------------------------------------------------------------
@@ -93,8 +116,14 @@ struct SampleCoord { int x, y, s; };
 // sample id (frame-local enumeration over jobs) -> pixel + sample index
 __device__ SampleCoord sampleCoord(const DevJob *jobs, int n_jobs, int width, int tile, int spp, uint64_t sid)
 {
-	int j = 0;
-	while(j + 1 < n_jobs && jobs[j + 1].sample_base <= sid) ++j;
+	// last job whose first sample is <= sid (jobs are in ascending sample_base order)
+	int j = 0, hi = n_jobs - 1;
+	while(j < hi)
+	{
+		const int mid = (j + hi + 1) >> 1;
+		if(jobs[mid].sample_base <= sid) j = mid;
+		else hi = mid - 1;
+	}
 	const DevJob job = jobs[j];
 	const uint64_t local = sid - job.sample_base;
 	const uint32_t pix = (uint32_t)(local / (uint64_t)spp);
@@ -338,7 +367,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, 
 			++n_shadow;
 		}
 	}
-	// wave-reduced statistics (rays issued, nodes visited, triangles tested)
+	// statistics (rays issued, nodes visited, triangles tested): wave reduce, then one plain
+	// read-modify-write per workgroup into its own record (no atomics: the same block index owns
+	// the same record in every launch of the stream; summed on the host after the render)
 	for(int off = 32; off > 0; off >>= 1)
 	{
 		visits += __shfl_down(visits, off);
@@ -346,12 +377,17 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, 
 		n_closest += __shfl_down(n_closest, off);
 		n_shadow += __shfl_down(n_shadow, off);
 	}
-	if(laneId() == 0 && (visits | tests | n_closest | n_shadow))
+	__shared__ uint32_t red[kTraceBlock / 64][4];
+	const int wid = threadIdx.x >> 6;
+	if(laneId() == 0) { red[wid][0] = visits; red[wid][1] = tests; red[wid][2] = n_closest; red[wid][3] = n_shadow; }
+	__syncthreads();
+	if(threadIdx.x < 4)
 	{
-		atomicAdd(&stats->node_visits, (unsigned long long)visits);
-		atomicAdd(&stats->tri_tests, (unsigned long long)tests);
-		atomicAdd(&stats->closest_rays, (unsigned long long)n_closest);
-		atomicAdd(&stats->shadow_rays, (unsigned long long)n_shadow);
+		unsigned long long v = 0;
+		for(int w = 0; w < kTraceBlock / 64; ++w) v += red[w][threadIdx.x];
+		unsigned long long *rec = &stats[blockIdx.x].closest_rays;
+		const int slot = (threadIdx.x == 0) ? 2 : (threadIdx.x == 1) ? 3 : (threadIdx.x == 2) ? 0 : 1;
+		if(v) rec[slot] += v;
 	}
 }
 
@@ -1029,7 +1065,8 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 
 		// ---- 4. compaction: the entry moves to position k of the next queue ----
 		const bool keep = live && (want_ray || pending);   // pending => never finalized this iteration
-		const uint32_t k = waveAppend(keep, &A.cnt_next->n_active);
+		__shared__ uint32_t append_scratch[kShadeBlock / 64 + 1];
+		const uint32_t k = blockAppend<kShadeBlock>(keep, &A.cnt_next->n_active, append_scratch);
 		if(keep)
 		{
 			A.Qn.slot[k] = (int)sid;
@@ -1223,6 +1260,22 @@ using namespace yafamd;
 extern "C" {
 
 int yafamd_trace_block() { return kTraceBlock; }
+
+// Resident workgroups per CU of the persistent kernels (their grids fill the chip exactly once).
+int yafamd_trace_blocks_per_cu(int lds_scene, size_t dyn_lds)
+{
+	int nb = 0;
+	if(lds_scene) { if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true>, kTraceBlock, dyn_lds) != hipSuccess) nb = 0; }
+	else if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false>, kTraceBlock, dyn_lds) != hipSuccess) nb = 0;
+	return nb;
+}
+
+int yafamd_shade_blocks_per_cu()
+{
+	int nb = 0;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade, kShadeBlock, 0) != hipSuccess) nb = 0;
+	return nb;
+}
 
 hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, DevCounters *cnt,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st)

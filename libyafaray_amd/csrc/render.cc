@@ -18,6 +18,8 @@ hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQ
 hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, DevCounters *cnt_next,
                                const DevPaths *P, DevStats *stats, int stack_depth, int grid, hipStream_t st);
 int yafamd_trace_block();
+int yafamd_trace_blocks_per_cu(int lds_scene, size_t dyn_lds);
+int yafamd_shade_blocks_per_cu();
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q, const DevQueues *Qn,
                                const DevCounters *cnt, DevCounters *cnt_next, float4 *samples, const DevJob *jobs,
                                int n_jobs, uint64_t chunk_base, int grid, hipStream_t st);
@@ -86,7 +88,7 @@ struct GpuRenderer::Impl
 	DevQueues Q[2]{};
 	Buf counters, stats;
 	std::vector<hipEvent_t> ev_pool;
-	int trace_grid = 2048, shade_grid = 1024;
+	int trace_grid = 2048, shade_grid = 1024, n_cu = 256;
 
 	~Impl()
 	{
@@ -130,8 +132,9 @@ bool GpuRenderer::ready()
 	HIPCHECK(hipGetDevice(&dev));
 	hipDeviceProp_t prop;
 	HIPCHECK(hipGetDeviceProperties(&prop, dev));
-	d_->trace_grid = std::max(256, prop.multiProcessorCount * 8);
-	d_->shade_grid = std::max(256, prop.multiProcessorCount * 4);
+	d_->n_cu = prop.multiProcessorCount;
+	d_->shade_grid = d_->n_cu * std::max(1, yafamd_shade_blocks_per_cu());
+	if(const char *e = getenv("YAFARAY_AMD_SHADE_GRID")) d_->shade_grid = std::max(1, atoi(e));   // tuning sweeps
 	std::ostringstream os;
 	os << "GPU: device " << dev << " " << prop.name << " (" << prop.gcnArchName << ", " << prop.multiProcessorCount << " CUs, "
 	   << (prop.totalGlobalMem >> 30) << " GiB)";
@@ -177,6 +180,12 @@ bool GpuRenderer::upload(const HostScene &hs)
 	d.stack_depth = std::max(8, ((hs.bvh.depth + 2 + 7) / 8) * 8);
 	const size_t scene_bytes = (size_t)(4 * d.n_nodes + 3 * d.n_tris) * 16;
 	d.scene_in_lds = scene_bytes + (size_t)d.stack_depth * yafamd_trace_block() * 4 <= 48 * 1024;
+	{
+		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy))
+		const size_t dyn = (size_t)d.stack_depth * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : 0);
+		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, dyn));
+		if(const char *e = getenv("YAFARAY_AMD_TRACE_GRID")) d.trace_grid = std::max(1, atoi(e));
+	}
 	// Faure tables, dims 0..49 (halton.cc:403-414: dims 0-2 share the base-3 table)
 	std::vector<uint8_t> perm;
 	std::vector<uint32_t> off(50), base(50);
@@ -204,6 +213,10 @@ bool GpuRenderer::upload(const HostScene &hs)
 	stats_.bvh_nodes = (uint32_t)d.n_nodes;
 	stats_.bvh_depth = (uint32_t)d.depth;
 	stats_.scene_in_lds = d.scene_in_lds ? 1u : 0u;
+	stats_.trace_grid = (uint32_t)d.trace_grid;
+	stats_.shade_grid = (uint32_t)d.shade_grid;
+	stats_.trace_block = (uint32_t)yafamd_trace_block();
+	stats_.stack_depth = (uint32_t)d.stack_depth;
 	return true;
 }
 
@@ -319,9 +332,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		d.nee_cap = K;
 	}
 	if(!ensure(log_, d.counters, 2 * sizeof(DevCounters))) return false;
-	if(!ensure(log_, d.stats, sizeof(DevStats))) return false;
+	if(!ensure(log_, d.stats, sizeof(DevStats) * (size_t)d.trace_grid)) return false;
 	HIPCHECK(hipMemsetAsync(d.counters.p, 0, 2 * sizeof(DevCounters), d.stream));
-	HIPCHECK(hipMemsetAsync(d.stats.p, 0, sizeof(DevStats), d.stream));
+	HIPCHECK(hipMemsetAsync(d.stats.p, 0, sizeof(DevStats) * (size_t)d.trace_grid, d.stream));
 	DevCounters *cnt = (DevCounters *)d.counters.p;
 	DevStats *dstats = (DevStats *)d.stats.p;
 	const int n_paths = std::max(1, S.path_samples);
@@ -363,7 +376,17 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	float ms = 0.f;
 	HIPCHECK(hipEventElapsedTime(&ms, d.ev_pool[0], d.ev_pool[1]));
 	DevStats hs{};
-	HIPCHECK(hipMemcpy(&hs, d.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+	{
+		std::vector<DevStats> per_block((size_t)d.trace_grid);
+		HIPCHECK(hipMemcpy(per_block.data(), d.stats.p, sizeof(DevStats) * per_block.size(), hipMemcpyDeviceToHost));
+		for(const DevStats &b : per_block)
+		{
+			hs.closest_rays += b.closest_rays;
+			hs.shadow_rays += b.shadow_rays;
+			hs.node_visits += b.node_visits;
+			hs.tri_tests += b.tri_tests;
+		}
+	}
 	stats_.closest_rays = hs.closest_rays;
 	stats_.shadow_rays = hs.shadow_rays;
 	stats_.node_visits = hs.node_visits;
