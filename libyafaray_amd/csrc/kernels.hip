@@ -557,13 +557,14 @@ __device__ __forceinline__ bool areaTri(V3 a, V3 b, V3 c, V3 o, V3 d, float &t)
 struct ShadeOut
 {
 	uint32_t *sh_count;
+	uint32_t *scratch;     // LDS for blockAppend
 	DevQueues Qn;
 };
 
-// Appends (or not) one shadow ray per lane — all lanes of the wave must call.
+// Appends (or not) one shadow ray per lane — every thread of the workgroup must call.
 __device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, int idx, const ShadeOut &out)
 {
-	const uint32_t k = waveAppend(want, out.sh_count);
+	const uint32_t k = blockAppend<kShadeBlock>(want, out.sh_count, out.scratch);
 	if(want)
 	{
 		out.Qn.sh_o[k] = f4(o, 0.f);
@@ -581,7 +582,8 @@ __device__ __forceinline__ void shadowRayOf(V3 from, V3 dir, float tmin, float t
 
 // Next-event estimation for one light: writes the contributions of every sample into
 // nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
-// Wave-uniform structure: `active` lanes do the work, every lane walks the same loop bounds.
+// Workgroup-uniform structure: `active` lanes do the work, every thread of the workgroup walks
+// the same loop bounds (the shadow-ray appends are workgroup-level).
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
                          float4 *nee, uint8_t *occ, const ShadeOut &out)
@@ -813,8 +815,10 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 	const DevPaths &Pc = A.Pc;
 	const DevPaths &Pn = A.Pn;
 	const uint32_t n_a = A.cnt->n_active;
+	__shared__ uint32_t append_scratch[kShadeBlock / 64 + 1];
 	ShadeOut out;
 	out.sh_count = &A.cnt_next->n_shadow;
+	out.scratch = append_scratch;
 	out.Qn = A.Qn;
 	const bool is_path = S.integrator == INT_PATH;
 	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
@@ -1065,7 +1069,6 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 
 		// ---- 4. compaction: the entry moves to position k of the next queue ----
 		const bool keep = live && (want_ray || pending);   // pending => never finalized this iteration
-		__shared__ uint32_t append_scratch[kShadeBlock / 64 + 1];
 		const uint32_t k = blockAppend<kShadeBlock>(keep, &A.cnt_next->n_active, append_scratch);
 		if(keep)
 		{
@@ -1095,20 +1098,20 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			if(n_paths > 1) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }
 		}
 
-		// ---- 5. next-event estimation into the next state (wave-uniform loops, masked lanes) ----
+		// ---- 5. next-event estimation into the next state (workgroup-uniform loops, masked lanes) ----
 		const int e0 = (int)k * K;
-		if(__any(nee_v0))
+		if(__syncthreads_or(nee_v0))
 		{
 			for(int l = 0; l < S.n_lights; ++l)
 				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, nee_v0,
 				         e0 + (int)S.lights[l].nee_base, Pn.nee, Pn.occ, out);
 		}
-		if(__any(nee_one))
+		if(__syncthreads_or(nee_one))
 		{
 			for(int l = 0; l < S.n_lights; ++l)
 			{
 				const bool mine = nee_one && (int)lnum == l;
-				if(!__any(mine)) continue;
+				if(!__syncthreads_or(mine)) continue;
 				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, mine, e0, Pn.nee, Pn.occ, out);
 			}
 		}
