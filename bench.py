@@ -24,6 +24,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "Mrays/sec + Msamples/sec, 1920×1080×64spp path-trace at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+LDS_PEAK_GBS = 256 * 256 * 2.4   # 256 CUs x 256 B/clk (ds_read_b128, MI355X_MICROARCH.md §LDS) x 2.4 GHz
 
 
 def parse():
@@ -37,7 +38,7 @@ def parse():
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--no-rr", action="store_true", help="Russian roulette off (bit-parity variant)")
     ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere"])
-    ap.add_argument("--chunk", type=int, default=1 << 20)
+    ap.add_argument("--chunk", type=int, default=1 << 25)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -128,16 +129,22 @@ def main():
     msps = samples_total / elapsed / 1e6
     mrays = rays_total / elapsed / 1e6
 
-    # roofline of the dominant kernel (k_trace) on this rank: algorithmic bytes per launch over the
-    # average launch duration from the HIP events.  Bytes per traced ray:
-    # 64 B per BVH node fetched + 48 B per triangle tested + ray I/O (closest: 32 in + 8 out,
-    # shadow: 32 in + 1 out + 4 index).
+    # roofline of the dominant kernel (k_trace) on this rank, per launch, with the average launch
+    # duration from HIP events on the render stream.  Algorithmic bytes:
+    #   ray I/O      closest 32 B in + 8 B out, shadow 32 B in + 4 B index + 1 B out  (always HBM)
+    #   traversal    64 B per BVH node visited + 48 B per triangle tested
+    # The traversal bytes count against HBM only when the scene is not LDS-resident; for the
+    # Cornell box (3 KB) they are served by LDS and reported separately against the LDS peak.
     s = stats_acc[-1]
-    algo_bytes = (64.0 * s["node_visits"] + 48.0 * s["tri_tests"] + 40.0 * s["closest_rays"] + 37.0 * s["shadow_rays"])
     launches = max(1, s["trace_launches"])
     avg_ms = s["trace_kernel_ms"] / launches
+    ray_io = 40.0 * s["closest_rays"] + 37.0 * s["shadow_rays"]
+    trav = 64.0 * s["node_visits"] + 48.0 * s["tri_tests"]
+    in_lds = bool(s["scene_in_lds"])
+    algo_bytes = ray_io + (0.0 if in_lds else trav)
     per_launch = algo_bytes / launches
     achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    trav_rate = trav / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "trace_hbm_bytes_per_launch.json")
     if os.path.exists(tfile):
@@ -182,7 +189,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_trace", "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
-                         "algo_bytes_per_launch": round(per_launch)},
+                         "algo_bytes_per_launch": round(per_launch),
+                         "traversal": {"bytes_per_launch": round(trav / launches), "served_from": "LDS" if in_lds else "L2/MALL/HBM",
+                                       "achieved": round(trav_rate, 1), "unit": "GB/s",
+                                       "lds_peak": LDS_PEAK_GBS, "frac_of_lds_peak": round(trav_rate / LDS_PEAK_GBS, 4)}},
+            "shade": {"avg_launch_ms": round(s["shade_kernel_ms"] / launches, 4),
+                      "ms_per_step": round(s["shade_kernel_ms"], 2), "trace_ms_per_step": round(s["trace_kernel_ms"], 2),
+                      "nee_ms_per_step": round(s["nee_kernel_ms"], 2)},
             "launch": {k: s[k] for k in ("trace_grid", "shade_grid", "trace_block", "stack_depth", "scene_in_lds")},
             "cpu_baseline": cpu,
         }

@@ -40,6 +40,8 @@ typedef struct
 	uint32_t bvh_nodes, bvh_depth, scene_in_lds, pad;
 	uint32_t trace_grid, shade_grid;   /* persistent grids (workgroups) of k_trace / k_shade */
 	uint32_t trace_block, stack_depth;
+	double shade_kernel_ms;     /* summed k_shade time (hipEvent pairs), 0 if not profiled */
+	double nee_kernel_ms;       /* summed k_nee time */
 } yafaray_amd_stats_t;
 
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */
@@ -69,9 +71,14 @@ YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t 
 /* Counters and timings of the last render. */
 YAFARAY_C_API_EXPORT void yafaray_amd_getStats(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats);
 
-/* Tuning: samples in flight per wavefront chunk (default 1 << 20) and whether to time k_trace with events. */
+/* Tuning: samples in flight per wavefront chunk (default 1 << 25, halved automatically if it does not fit) and whether to time k_trace with events. */
 YAFARAY_C_API_EXPORT void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots);
 YAFARAY_C_API_EXPORT void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_t enable);
+
+/* Diagnostic: summed wave cycles of the k_shade phases (load, connect, hit, next segment, compaction,
+ * NEE) since the last reset; returns the number of counters, 0 unless the library was built with
+ * -DYAF_PHASE_TIMING (never in the product build). */
+YAFARAY_C_API_EXPORT int yafaray_amd_getPhaseCycles(unsigned long long *cycles, int n, yafaray_bool_t reset);
 
 /* Last error message (empty if none); owned by the interface. */
 YAFARAY_C_API_EXPORT const char *yafaray_amd_lastError(const yafaray_Interface_t *interface);

@@ -53,6 +53,7 @@ struct Builder
 	std::vector<BuildNode> nodes;
 	std::mutex mtx;
 
+	float node_cost = 0.5f;   // SAH: cost of one node visit (two box tests) relative to one triangle test
 	explicit Builder(const BvhInput &i, int ls) : in(i), leaf_size(ls) {}
 
 	int newNode()
@@ -119,7 +120,7 @@ struct Builder
 				acc.grow(bb[b]);
 				cnt += bc[b];
 				if(cnt == 0 || rc[b + 1] == 0) continue;
-				const float cost = 0.5f + (acc.area() * cnt + ra[b + 1] * rc[b + 1]) * inv_area;
+				const float cost = node_cost + (acc.area() * cnt + ra[b + 1] * rc[b + 1]) * inv_area;
 				if(cost < best_cost) { best_cost = cost; best_axis = axis; best_split = b; }
 			}
 		}
@@ -199,6 +200,7 @@ BvhOutput buildBvh(const BvhInput &in, int leaf_size, int threads)
 {
 	BvhOutput out;
 	Builder b(in, leaf_size);
+	if(in.node_cost > 0.f) b.node_cost = in.node_cost;
 	const int n = in.n_tris;
 	b.tri_box.resize(n);
 	b.cent.resize(3 * (size_t)n);

@@ -18,6 +18,7 @@ struct BvhInput
 	const float *verts;     // xyz per vertex
 	const int *tris;        // 3 vertex indices per triangle
 	int n_tris;
+	float node_cost = 0.f;   // SAH node cost (<= 0: default 0.5)
 };
 
 struct BvhOutput

@@ -23,6 +23,8 @@ static char *dupString(const std::string &s)
 	return c;
 }
 
+extern "C" int yafamd_phase_cycles(unsigned long long *out, int n, int reset);
+
 extern "C" {
 
 yafaray_Interface_t *yafaray_createInterface(yafaray_Interface_Type_t interface_type, const char *exported_file_path, yafaray_LoggerCallback_t logger_callback, void *callback_data, yafaray_DisplayConsole_t display_console)
@@ -540,5 +542,10 @@ void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_
 }
 
 const char *yafaray_amd_lastError(const yafaray_Interface_t *interface) { return I(interface)->logger.lastError().c_str(); }
+
+int yafaray_amd_getPhaseCycles(unsigned long long *cycles, int n, yafaray_bool_t reset)
+{
+	return yafamd_phase_cycles(cycles, n, reset != YAFARAY_BOOL_FALSE ? 1 : 0);
+}
 
 }

@@ -21,8 +21,14 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define YD __host__ __device__ __forceinline__
+#ifdef YAF_INLINE_COLD
+#define YD_COLD YD
+#else
+#define YD_COLD inline __host__ __device__ __attribute__((noinline, cold))
+#endif
 #else
 #define YD inline
+#define YD_COLD inline __attribute__((noinline, cold))
 #endif
 
 namespace yafamd
@@ -138,15 +144,46 @@ YD bool safeToRound(double d, float &f)
 	return (low_binade ? 0.25 : 0.5) - t > 1e-6;
 }
 
+// Exact (slow) paths, taken only within 1e-6 float-ulp of a rounding midpoint: kept out of line so
+// their code and registers do not weigh on the callers.
+YD_COLD float x87mulExact(double chi, double clo, float x)
+{
+	const X87Const c = {chi, clo};
+	const double ax = fabs((double)x);
+	const float r = round24(round64(exactMul(c, ax)));
+	return x < 0.f ? -r : r;
+}
+
+YD_COLD float x87mul2Exact(double chi, double clo, float x, float y)
+{
+	const X87Const c = {chi, clo};
+	const double ax = fabs((double)x), ay = fabs((double)y);
+	const DD t = round64(exactMul(c, ax));
+	const double p = t.hi * ay;
+	const double e = fma(t.hi, ay, -p);
+	const double q = t.lo * ay;
+	const float r = round24(round64(fastTwoSum(p, e + q)));
+	return ((x < 0.f) != (y < 0.f)) ? -r : r;
+}
+
+YD_COLD float x87mulDivExact(double chi, double clo, float a, float b)
+{
+	const X87Const c = {chi, clo};
+	const DD n = round64(exactMul(c, (double)a));
+	const double bd = (double)b;
+	const double q1 = n.hi / bd;
+	const double r1 = fma(-q1, bd, n.hi);
+	const double q2 = (r1 + n.lo) / bd;
+	return round24(round64(fastTwoSum(q1, q2)));
+}
+
 // (float)((long double)C * x)
 YD float x87mul(const X87Const &c, float x)
 {
 	if(x == 0.f || !(fabsf(x) < 3.0e38f)) return (float)(c.hi * (double)x);
 	float f;
 	if(safeToRound(c.hi * (double)x, f)) return f;
-	const double ax = fabs((double)x);
-	const float r = round24(round64(exactMul(c, ax)));
-	return x < 0.f ? -r : r;
+	return x87mulExact(c.hi, c.lo, x);
 }
 
 // (float)((long double)C * x * y) — two x87 roundings then the float one
@@ -155,13 +192,7 @@ YD float x87mul2(const X87Const &c, float x, float y)
 	if(x == 0.f || y == 0.f) return (float)(c.hi * (double)x * (double)y);
 	float f;
 	if(safeToRound(c.hi * (double)x * (double)y, f)) return f;
-	const double ax = fabs((double)x), ay = fabs((double)y);
-	const DD t = round64(exactMul(c, ax));
-	const double p = t.hi * ay;
-	const double e = fma(t.hi, ay, -p);
-	const double q = t.lo * ay;
-	const float r = round24(round64(fastTwoSum(p, e + q)));
-	return ((x < 0.f) != (y < 0.f)) ? -r : r;
+	return x87mul2Exact(c.hi, c.lo, x, y);
 }
 
 // (float)(((long double)C * a) / (long double)b) with a, b > 0 floats (light pdfs,
@@ -172,12 +203,7 @@ YD float x87mulDiv(const X87Const &c, float a, float b)
 	if(a == 0.f) return 0.f;
 	float f;
 	if(safeToRound(c.hi * (double)a / (double)b, f)) return f;
-	const DD n = round64(exactMul(c, (double)a));
-	const double bd = (double)b;
-	const double q1 = n.hi / bd;
-	const double r1 = fma(-q1, bd, n.hi);
-	const double q2 = (r1 + n.lo) / bd;
-	return round24(round64(fastTwoSum(q1, q2)));
+	return x87mulDivExact(c.hi, c.lo, a, b);
 }
 
 // x > C / x < -C with C long double (exact for float x, see DESIGN.md numerics note)
@@ -346,14 +372,37 @@ YD float haltonFirst(uint32_t base, double inv_base, uint32_t start)
 	return clamp01((float)value);
 }
 
-// Faure-scrambled radical inverse.  `perm` points at the digit permutation of dimension `dim`
-// (tables uploaded by the host: DevScene::faure_*).
-YD double lowDiscrepancy(const uint8_t *perm, uint32_t base, double f, uint32_t n)
+// Exact unsigned division by a divisor d in [2, 2^31] known only at run time, from a
+// precomputed magic number (Granlund–Montgomery "round-up" form): q = (t + ((n - t) >> 1)) >> sh
+// with t = mulhi(n, m).  Replaces the ~20-instruction generic u32 division in the digit loops.
+struct UDiv { uint32_t m, sh; };
+YD UDiv udivMake(uint32_t d)
+{
+	uint32_t l = 0;
+	while((1ull << l) < (uint64_t)d) ++l;                       // ceil(log2 d)
+	UDiv q;
+	q.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+	q.sh = l - 1;
+	return q;
+}
+YD uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+YD uint32_t udiv(uint32_t n, UDiv q)
+{
+	const uint32_t t = mulhi32(n, q.m);
+	return (t + ((n - t) >> 1)) >> q.sh;
+}
+
+// Faure-scrambled radical inverse (halton.cc:421-441).  `perm` points at the digit permutation
+// of the dimension, `base` its prime, `dv` the magic of `base`, `f` the reference's inv_prims
+// entry (llround(1e9 / p) / 1e9, NOT 1/p: the digit sequence comes from truncating dn * f, exactly
+// as the reference does).
+YD double lowDiscrepancy(const uint8_t *perm, uint32_t base, UDiv dv, double f, uint32_t n)
 {
 	double value = 0.0, dn = (double)n, factor = f;
 	while(n > 0)
 	{
-		value += (double)perm[n % base] * factor;
+		const uint32_t digit = n - udiv(n, dv) * base;   // n % base
+		value += (double)perm[digit] * factor;
 		dn *= f;
 		n = (uint32_t)dn;
 		factor *= f;

@@ -75,8 +75,7 @@ struct DevScene
 	const DevMaterial *mats;
 	const DevLight *lights;
 	const uint8_t *faure;          // concatenated Faure digit permutations, dims 0..49
-	const uint32_t *faure_off;     // offset of each dimension's table
-	const uint32_t *faure_base;    // base of each dimension
+	const uint4 *faure_dim;        // per dimension: (base, table offset, division magic m, shift)
 	const double *faure_inv;       // inv_prims (halton.cc:413)
 	int n_nodes, n_tris, n_mats, n_lights;
 	int scene_in_lds;              // nodes+tris copied to LDS by each trace workgroup
@@ -137,9 +136,17 @@ struct DevQueues
 	int *sh_idx;           // slot * nee_k + entry
 };
 
+// Next-event-estimation requests written by k_shade, consumed by k_nee in the same iteration.
+struct DevNeeQueue
+{
+	float4 *p_prim;        // hit point, .w = primitive (bits)
+	float4 *wo_k;          // outgoing direction, .w = index k of the path in the next active list (bits)
+	uint4 *pix_mode;       // (PixelSamplingData offset, sample index, mode | light << 8, 0)
+};
+
 struct DevCounters
 {
-	uint32_t n_active, n_shadow, pad0, pad1;
+	uint32_t n_active, n_shadow, n_nee, pad1;
 };
 
 struct DevStats

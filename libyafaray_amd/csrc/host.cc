@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <ctime>
 #include <sstream>
 
@@ -431,7 +432,10 @@ bool Scene::buildAccelerator()
 	HostScene hs;
 	hs.n_prims = (int)tri_mat.size();
 	BvhInput in{verts.data(), tris.data(), hs.n_prims};
-	hs.bvh = buildBvh(in, 4, 8);
+	int leaf = 4;
+	if(const char *e = getenv("YAFARAY_AMD_BVH_LEAF")) leaf = std::max(1, atoi(e));          // tuning sweeps
+	if(const char *e = getenv("YAFARAY_AMD_BVH_NODE_COST")) in.node_cost = (float)atof(e);
+	hs.bvh = buildBvh(in, leaf, 8);
 	// primitive_triangle.cc:87-95 geometric normal; material index per primitive
 	hs.prim_ng.resize(4 * (size_t)hs.n_prims);
 	for(int t = 0; t < hs.n_prims; ++t)

@@ -171,7 +171,7 @@ class Scene
 		std::string current_material;
 		bool geometry_dirty = true;
 		int shard_rank = 0, shard_world = 1;
-		int chunk_slots = 1 << 20;
+		int chunk_slots = 1 << 25;   // samples in flight per wavefront chunk
 		bool profile_kernels = false;
 		volatile bool canceled = false;
 

@@ -85,6 +85,19 @@ __device__ __forceinline__ uint32_t waveAppend(bool want, uint32_t *counter)
 	return base + (uint32_t)__popcll(below);
 }
 
+// Diagnostic build (-DYAF_PHASE_TIMING): per-phase wave cycles of k_shade (clock64 deltas summed
+// by lane 0 of each wave), read with yafaray_amd_getPhaseCycles.  Off in the product build.
+#ifdef YAF_PHASE_TIMING
+__device__ unsigned long long g_phase[16];
+#define PHASE_DECL uint64_t ph_t = clock64(); uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PHASE(k) do { const uint64_t t_ = clock64(); ph_acc[k] += t_ - ph_t; ph_t = t_; } while(0)
+#define PHASE_FLUSH do { if(laneId() == 0) for(int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_phase[k_], (unsigned long long)ph_acc[k_]); } while(0)
+#else
+#define PHASE_DECL
+#define PHASE(k)
+#define PHASE_FLUSH
+#endif
+
 // Workgroup-level append (one atomic per workgroup): every thread of the block must call it.
 // `scratch` is LDS of at least blockDim/64 + 1 words.
 template<int BLOCK>
@@ -106,6 +119,30 @@ __device__ __forceinline__ uint32_t blockAppend(bool want, uint32_t *counter, ui
 	__syncthreads();   // scratch is reused by the next call
 	const uint64_t below = mask & ((1ull << laneId()) - 1ull);
 	return base + (uint32_t)__popcll(below);
+}
+
+// Two independent appends in one workgroup-level round (one barrier sequence, two atomics).
+template<int BLOCK>
+__device__ __forceinline__ uint2 blockAppend2(bool want_a, bool want_b, uint32_t *counter_a, uint32_t *counter_b,
+                                              uint32_t *scratch)
+{
+	constexpr int NW = BLOCK / 64;
+	const uint64_t ma = __ballot(want_a), mb = __ballot(want_b);
+	const int wid = threadIdx.x >> 6;
+	if(laneId() == 0) { scratch[wid] = (uint32_t)__popcll(ma); scratch[NW + wid] = (uint32_t)__popcll(mb); }
+	__syncthreads();
+	if(threadIdx.x < 2)
+	{
+		uint32_t tot = 0;
+		for(int w = 0; w < NW; ++w) tot += scratch[threadIdx.x * NW + w];
+		scratch[2 * NW + threadIdx.x] = tot ? atomicAdd(threadIdx.x ? counter_b : counter_a, tot) : 0u;
+	}
+	__syncthreads();
+	uint32_t ba = scratch[2 * NW], bb = scratch[2 * NW + 1];
+	for(int w = 0; w < wid; ++w) { ba += scratch[w]; bb += scratch[NW + w]; }
+	__syncthreads();
+	const uint64_t below = (1ull << laneId()) - 1ull;
+	return make_uint2(ba + (uint32_t)__popcll(ma & below), bb + (uint32_t)__popcll(mb & below));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -314,7 +351,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, 
                                                       DevCounters *cnt_next, DevPaths P, DevStats *stats, int stack_depth)
 {
 	// the next shade appends into cnt_next: reset it here (it was consumed by the previous shade)
-	if(blockIdx.x == 0 && threadIdx.x == 0) { cnt_next->n_active = 0; cnt_next->n_shadow = 0; }
+	if(blockIdx.x == 0 && threadIdx.x == 0) { cnt_next->n_active = 0; cnt_next->n_shadow = 0; cnt_next->n_nee = 0; }
 	extern __shared__ float4 smem[];
 	int *stack = reinterpret_cast<int *>(smem);
 	TraceCtx C;
@@ -564,6 +601,10 @@ struct ShadeOut
 // Appends (or not) one shadow ray per lane — every thread of the workgroup must call.
 __device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, int idx, const ShadeOut &out)
 {
+#ifdef YAF_EXP_NO_EMIT
+	if(want) out.Qn.sh_idx[idx] = idx;   // timing experiment only: no append (wrong images)
+	return;
+#endif
 	const uint32_t k = blockAppend<kShadeBlock>(want, out.sh_count, out.scratch);
 	if(want)
 	{
@@ -627,15 +668,20 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 	const C3 lcolor = C3{L.color[0], L.color[1], L.color[2]};
 	for(int i = 0; i < num_samples; ++i)
 	{
-		// areaLightSampleLight (montecarlo.cc:156-282) with Halton(2/3, offs - 1) getNext() i+1 times
+		// areaLightSampleLight (montecarlo.cc:156-282) and areaLightSampleMaterial (:284-383) draw
+		// the same Halton(2/3, offs - 1 + i) pair: computed once for both.
+		float s_1 = 0.f, s_2 = 0.f;
+		if(active)
+		{
+			s_1 = haltonFirst(2u, 0.5, offs - 1u + (uint32_t)i);
+			s_2 = haltonFirst(3u, 1.0 / 3.0, offs - 1u + (uint32_t)i);
+		}
 		bool ok = active;
 		C3 contrib = c3(0.f);
 		V3 so = sp.p, ldir = v3(0.f, 0.f, 1.f);
 		float st = 0.f;
 		if(ok)
 		{
-			const float s_1 = haltonFirst(2u, 0.5, offs - 1u + (uint32_t)i);
-			const float s_2 = haltonFirst(3u, 1.0 / 3.0, offs - 1u + (uint32_t)i);
 			// light_area.cc:66-96
 			const V3 p = corner + s_1 * to_x + s_2 * to_y;
 			ldir = p - sp.p;
@@ -676,20 +722,19 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			occ[e0 + i] = 0;
 		}
 		emitShadow(ok && cast_shadows, so, ldir, st, e0 + i, out);
-	}
-	for(int i = 0; i < num_samples; ++i)
-	{
+
 		// areaLightSampleMaterial (montecarlo.cc:284-383)
-		bool ok = active;
-		C3 contrib = c3(0.f);
-		V3 so = sp.p, dir = v3(0.f, 0.f, 1.f);
-		float st = 0.f;
+		ok = active;
+		contrib = c3(0.f);
+		so = sp.p;
+		V3 dir = v3(0.f, 0.f, 1.f);
+		st = 0.f;
 		if(ok)
 		{
 			const float b_tmin = S.ray_min_dist_auto ? S.ray_min_dist * fmaxf(1.f, p_len) : S.ray_min_dist;
 			BsdfSample s;
-			s.s_1 = haltonFirst(2u, 0.5, offs - 1u + (uint32_t)i);
-			s.s_2 = haltonFirst(3u, 1.0 / 3.0, offs - 1u + (uint32_t)i);
+			s.s_1 = s_1;
+			s.s_2 = s_2;
 			s.flags = B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT;
 			s.pdf = 0.f;
 			s.sampled = B_NONE;
@@ -760,7 +805,14 @@ __device__ C3 neeSum(const DevScene &S, const DevLight &L, const float4 *nee, co
 
 __device__ __forceinline__ float ldsDim(const DevScene &S, int dim, uint32_t n)
 {
-	return (float)lowDiscrepancy(S.faure + S.faure_off[dim], S.faure_base[dim], S.faure_inv[dim], n);
+#ifdef YAF_EXP_CHEAP_LDS
+	return riVdC(n * (uint32_t)(dim + 1));   // timing experiment only (wrong images)
+#endif
+	const uint4 fd = S.faure_dim[dim];
+	UDiv dv;
+	dv.m = fd.z;
+	dv.sh = fd.w;
+	return (float)lowDiscrepancy(S.faure + fd.y, fd.x, dv, S.faure_inv[dim], n);
 }
 
 struct ShadeArgs
@@ -770,6 +822,7 @@ struct ShadeArgs
 	DevPaths Pn;         // state of the next active list (written at the compacted position)
 	DevQueues Q;         // current (active list + hits)
 	DevQueues Qn;        // next
+	DevNeeQueue N;       // NEE requests for k_nee
 	const DevCounters *cnt;
 	DevCounters *cnt_next;
 	float4 *samples;     // frame sample buffer [(y * W + x) * spp + s]
@@ -815,15 +868,12 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 	const DevPaths &Pc = A.Pc;
 	const DevPaths &Pn = A.Pn;
 	const uint32_t n_a = A.cnt->n_active;
-	__shared__ uint32_t append_scratch[kShadeBlock / 64 + 1];
-	ShadeOut out;
-	out.sh_count = &A.cnt_next->n_shadow;
-	out.scratch = append_scratch;
-	out.Qn = A.Qn;
+	__shared__ uint32_t append_scratch[2 * (kShadeBlock / 64) + 2];
 	const bool is_path = S.integrator == INT_PATH;
 	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
 	const int K = S.nee_k;
 	const uint32_t stride = gridDim.x * blockDim.x;
+	PHASE_DECL
 	for(uint32_t base_i = blockIdx.x * blockDim.x; base_i < n_a; base_i += stride)
 	{
 		const uint32_t i = base_i + threadIdx.x;
@@ -858,6 +908,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		int depth = (int)(stage >> 20);
 		const uint32_t offset = pix.x, sample_idx = pix.y;
 
+		PHASE(0);
 		// ---- 1. connect the pending next-event estimate ----
 		if(live && (flags & F_PEND_V0))
 		{
@@ -876,6 +927,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		}
 		flags &= ~(F_PEND_V0 | F_PEND_ONE | F_PEND_EMIT);
 
+		PHASE(1);
 		// ---- 2. the new hit ----
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
@@ -979,6 +1031,10 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 				}
 			}
 		}
+#ifdef YAF_EXP_NO_NEE
+		nee_one = false;   // timing experiment only (wrong images)
+		nee_v0 = false;
+#endif
 		uint32_t lnum = 0;
 		if(nee_one)
 		{
@@ -996,6 +1052,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		if(nee_v0) flags |= F_PEND_V0;
 		const bool pending = (flags & (F_PEND_V0 | F_PEND_ONE)) != 0;
 
+		PHASE(2);
 		// ---- 3. next segment ----
 		V3 ray_o = v3(0.f, 0.f, 0.f), ray_d = v3(0.f, 0.f, 1.f);
 		bool want_ray = false;
@@ -1067,9 +1124,12 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			writeSample(A, sid, col, alpha);
 		}
 
+		PHASE(3);
 		// ---- 4. compaction: the entry moves to position k of the next queue ----
 		const bool keep = live && (want_ray || pending);   // pending => never finalized this iteration
-		const uint32_t k = blockAppend<kShadeBlock>(keep, &A.cnt_next->n_active, append_scratch);
+		const bool want_nee = live && (nee_v0 || nee_one);
+		const uint2 kj = blockAppend2<kShadeBlock>(keep, want_nee, &A.cnt_next->n_active, &A.cnt_next->n_nee, append_scratch);
+		const uint32_t k = kj.x;
 		if(keep)
 		{
 			A.Qn.slot[k] = (int)sid;
@@ -1098,21 +1158,84 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			if(n_paths > 1) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }
 		}
 
-		// ---- 5. next-event estimation into the next state (workgroup-uniform loops, masked lanes) ----
-		const int e0 = (int)k * K;
-		if(__syncthreads_or(nee_v0))
+		PHASE(4);
+		// ---- 5. next-event estimation request (served by k_nee; wants -> keep, so k is valid) ----
+		if(want_nee)
 		{
-			for(int l = 0; l < S.n_lights; ++l)
-				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, nee_v0,
-				         e0 + (int)S.lights[l].nee_base, Pn.nee, Pn.occ, out);
+			const uint32_t j = kj.y;
+			A.N.p_prim[j] = f4(sp.p, __int_as_float(hit_prim));
+			A.N.wo_k[j] = f4(wo, __uint_as_float(k));
+			A.N.pix_mode[j] = make_uint4(offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8), 0u);
 		}
-		if(__syncthreads_or(nee_one))
+		PHASE(5);
+	}
+	PHASE_FLUSH;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_nee: next-event estimation for the vertices k_shade queued (integrator_montecarlo.cc:54-408).
+// Dense (every lane has a request), so the light-sampling arithmetic runs at full SIMD width and
+// k_shade keeps fewer registers live.  Contributions go to the next state set at k * nee_k,
+// shadow rays to the next queue (workgroup-level appends).
+// ---------------------------------------------------------------------------------------------
+struct NeeArgs
+{
+	DevScene S;
+	DevNeeQueue N;
+	DevPaths Pn;
+	DevQueues Qn;
+	DevCounters *cnt_next;
+};
+
+#ifndef YAF_NEE_MIN_WAVES
+#define YAF_NEE_MIN_WAVES 1
+#endif
+__global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
+{
+	const DevScene &S = A.S;
+	__shared__ uint32_t append_scratch[kShadeBlock / 64 + 1];
+	ShadeOut out;
+	out.sh_count = &A.cnt_next->n_shadow;
+	out.scratch = append_scratch;
+	out.Qn = A.Qn;
+	const uint32_t n_req = A.cnt_next->n_nee;
+	const int K = S.nee_k;
+	const uint32_t stride = gridDim.x * blockDim.x;
+	for(uint32_t base_j = blockIdx.x * blockDim.x; base_j < n_req; base_j += stride)
+	{
+		const uint32_t j = base_j + threadIdx.x;
+		const bool live = j < n_req;
+		float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), wk = pp;
+		uint4 pm = make_uint4(0u, 0u, 0u, 0u);
+		if(live)
 		{
+			pp = A.N.p_prim[j];
+			wk = A.N.wo_k[j];
+			pm = A.N.pix_mode[j];
+		}
+		Surf sp;
+		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
+		if(live) sp = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
+		const V3 wo = xyz(wk);
+		const int e0 = (int)__float_as_uint(wk.w) * K;
+		const bool all = live && (pm.z & 1u);
+		const bool one = live && !(pm.z & 1u);
+		const uint32_t lnum = pm.z >> 8;
+		if(__syncthreads_or(all))
+		{
+			// estimateAllDirectLight (montecarlo.cc:54-68)
+			for(int l = 0; l < S.n_lights; ++l)
+				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
+				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out);
+		}
+		if(__syncthreads_or(one))
+		{
+			// estimateOneDirectLight (montecarlo.cc:70-78), light `lnum`
 			for(int l = 0; l < S.n_lights; ++l)
 			{
-				const bool mine = nee_one && (int)lnum == l;
+				const bool mine = one && lnum == (uint32_t)l;
 				if(!__syncthreads_or(mine)) continue;
-				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, sample_idx, offset, mine, e0, Pn.nee, Pn.occ, out);
+				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out);
 			}
 		}
 	}
@@ -1264,12 +1387,38 @@ extern "C" {
 
 int yafamd_trace_block() { return kTraceBlock; }
 
+// Diagnostic: k_shade phase cycles (only a -DYAF_PHASE_TIMING build records them).
+int yafamd_phase_cycles(unsigned long long *out, int n, int reset)
+{
+#ifdef YAF_PHASE_TIMING
+	unsigned long long h[16];
+	if(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)) != hipSuccess) return 0;
+	for(int k = 0; k < n && k < 16; ++k) out[k] = h[k];
+	if(reset)
+	{
+		const unsigned long long z[16] = {};
+		if(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return 0;
+	}
+	return 16;
+#else
+	(void)out; (void)n; (void)reset;
+	return 0;
+#endif
+}
+
 // Resident workgroups per CU of the persistent kernels (their grids fill the chip exactly once).
 int yafamd_trace_blocks_per_cu(int lds_scene, size_t dyn_lds)
 {
 	int nb = 0;
 	if(lds_scene) { if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true>, kTraceBlock, dyn_lds) != hipSuccess) nb = 0; }
 	else if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false>, kTraceBlock, dyn_lds) != hipSuccess) nb = 0;
+	return nb;
+}
+
+int yafamd_nee_blocks_per_cu()
+{
+	int nb = 0;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_nee, kShadeBlock, 0) != hipSuccess) nb = 0;
 	return nb;
 }
 
@@ -1302,8 +1451,8 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 }
 
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
-                               const DevQueues *Qn, const DevCounters *cnt, DevCounters *cnt_next, float4 *samples,
-                               const DevJob *jobs, int n_jobs, uint64_t chunk_base, int grid, hipStream_t st)
+                               const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, DevCounters *cnt_next,
+                               float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, int grid, hipStream_t st)
 {
 	ShadeArgs A;
 	A.S = *S;
@@ -1311,6 +1460,7 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	A.Pn = *Pn;
 	A.Q = *Q;
 	A.Qn = *Qn;
+	A.N = *N;
 	A.cnt = cnt;
 	A.cnt_next = cnt_next;
 	A.samples = samples;
@@ -1318,6 +1468,19 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
 	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, st, A);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
+                             DevCounters *cnt_next, int grid, hipStream_t st)
+{
+	NeeArgs A;
+	A.S = *S;
+	A.N = *N;
+	A.Pn = *Pn;
+	A.Qn = *Qn;
+	A.cnt_next = cnt_next;
+	hipLaunchKernelGGL(k_nee, dim3(grid), dim3(kShadeBlock), 0, st, A);
 	return hipGetLastError();
 }
 

@@ -1,6 +1,7 @@
 // GPU driver (see render.h).  Plain C++ against the HIP runtime API; kernels are launched
 // through the extern "C" wrappers at the end of kernels.hip.
 #include "render.h"
+#include "devmath.h"
 
 #include <hip/hip_runtime.h>
 
@@ -20,9 +21,12 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 int yafamd_trace_block();
 int yafamd_trace_blocks_per_cu(int lds_scene, size_t dyn_lds);
 int yafamd_shade_blocks_per_cu();
-hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q, const DevQueues *Qn,
-                               const DevCounters *cnt, DevCounters *cnt_next, float4 *samples, const DevJob *jobs,
-                               int n_jobs, uint64_t chunk_base, int grid, hipStream_t st);
+hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
+                               const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, DevCounters *cnt_next,
+                               float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, int grid, hipStream_t st);
+hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
+                             DevCounters *cnt_next, int grid, hipStream_t st);
+int yafamd_nee_blocks_per_cu();
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
                               float clamp_samples, hipStream_t st);
 hipError_t yafamd_launch_trace_rays(const DevScene *S, int any, const float4 *ro, const float4 *rd, int n, float *t_out,
@@ -74,7 +78,7 @@ struct GpuRenderer::Impl
 {
 	bool ok = false, init_done = false;
 	hipStream_t stream = nullptr;
-	Buf nodes, tris, prim_ng, mats, lights, faure, faure_off, faure_base, faure_inv;
+	Buf nodes, tris, prim_ng, mats, lights, faure, faure_dim, faure_inv;
 	int n_nodes = 0, n_tris = 0, n_mats = 0, n_lights = 0, depth = 0, stack_depth = 32;
 	bool scene_in_lds = false;
 	// frame buffers
@@ -82,17 +86,19 @@ struct GpuRenderer::Impl
 	int film_w = 0, film_h = 0;
 	// chunk buffers
 	size_t slots_cap = 0;
+	bool v0_alloc = false;
 	int nee_cap = 0;
 	std::vector<Buf> chunk_bufs;
 	DevPaths P[2]{};       // path state, parallel to Q[q] (indexed by queue position)
 	DevQueues Q[2]{};
 	Buf counters, stats;
 	std::vector<hipEvent_t> ev_pool;
-	int trace_grid = 2048, shade_grid = 1024, n_cu = 256;
+	int trace_grid = 2048, shade_grid = 1024, nee_grid = 1024, n_cu = 256;
+	DevNeeQueue N{};
 
 	~Impl()
 	{
-		for(Buf *b : {&nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_off, &faure_base, &faure_inv, &samples, &film,
+		for(Buf *b : {&nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_dim, &faure_inv, &samples, &film,
 		              &weights, &jobs, &counters, &stats})
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
@@ -135,6 +141,8 @@ bool GpuRenderer::ready()
 	d_->n_cu = prop.multiProcessorCount;
 	d_->shade_grid = d_->n_cu * std::max(1, yafamd_shade_blocks_per_cu());
 	if(const char *e = getenv("YAFARAY_AMD_SHADE_GRID")) d_->shade_grid = std::max(1, atoi(e));   // tuning sweeps
+	d_->nee_grid = d_->n_cu * std::max(1, yafamd_nee_blocks_per_cu());
+	if(const char *e = getenv("YAFARAY_AMD_NEE_GRID")) d_->nee_grid = std::max(1, atoi(e));
 	std::ostringstream os;
 	os << "GPU: device " << dev << " " << prop.name << " (" << prop.gcnArchName << ", " << prop.multiProcessorCount << " CUs, "
 	   << (prop.totalGlobalMem >> 30) << " GiB)";
@@ -207,8 +215,13 @@ bool GpuRenderer::upload(const HostScene &hs)
 		inv[dim] = (double)std::llround(1e9 / primes[dim]) / 1e9;
 	}
 	if(!allocCopy(log_, d.faure, perm.data(), perm.size())) return false;
-	if(!allocCopy(log_, d.faure_off, off.data(), off.size())) return false;
-	if(!allocCopy(log_, d.faure_base, base.data(), base.size())) return false;
+	std::vector<uint4> fdim(50);
+	for(int dim = 0; dim < 50; ++dim)
+	{
+		const UDiv dv = udivMake(base[dim]);
+		fdim[dim] = make_uint4(base[dim], off[dim], dv.m, dv.sh);
+	}
+	if(!allocCopy(log_, d.faure_dim, fdim.data(), fdim.size())) return false;
 	if(!allocCopy(log_, d.faure_inv, inv.data(), inv.size())) return false;
 	stats_.bvh_nodes = (uint32_t)d.n_nodes;
 	stats_.bvh_depth = (uint32_t)d.depth;
@@ -228,8 +241,7 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.mats = (const DevMaterial *)d.mats.p;
 	S.lights = (const DevLight *)d.lights.p;
 	S.faure = (const uint8_t *)d.faure.p;
-	S.faure_off = (const uint32_t *)d.faure_off.p;
-	S.faure_base = (const uint32_t *)d.faure_base.p;
+	S.faure_dim = (const uint4 *)d.faure_dim.p;
 	S.faure_inv = (const double *)d.faure_inv.p;
 	S.n_nodes = d.n_nodes;
 	S.n_tris = d.n_tris;
@@ -282,52 +294,71 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	HIPCHECK(hipMemsetAsync(d.film.p, 0, (size_t)W * H * sizeof(float4), d.stream));
 	HIPCHECK(hipMemsetAsync(d.weights.p, 0, (size_t)W * H * sizeof(float), d.stream));
 	// ---- chunk buffers ----
-	const size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
+	size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
 	const int K = std::max(1, S.nee_k);
-	if(M > d.slots_cap || K > d.nee_cap)
+	const bool need_v0 = S.path_samples > 1;
+	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc)
 	{
-		for(Buf &b : d.chunk_bufs) b.release();
-		d.chunk_bufs.clear();
-		auto A = [&](size_t bytes) -> void * {
-			d.chunk_bufs.emplace_back();
-			Buf &b = d.chunk_bufs.back();
-			if(hipMalloc(&b.p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
-			b.bytes = bytes;
-			return b.p;
-		};
-		for(int q = 0; q < 2; ++q)
+		// Wavefront buffers for M samples in flight (~0.7 KB each: 288 GB of HBM holds tens of millions,
+		// and big chunks amortise the per-launch cost).  On allocation failure the chunk is halved.
+		for(;;)
 		{
-			DevPaths &P = d.P[q];
-			P.stage = (uint32_t *)A(M * 4);
-			P.flags = (uint32_t *)A(M * 4);
-			P.w = (float *)A(M * 4);
-			P.thr = (float4 *)A(M * 16);
-			P.col = (float4 *)A(M * 16);
-			P.pcol = (float4 *)A(M * 16);
-			P.pwo = (float4 *)A(M * 16);
-			P.pend_thr = (float4 *)A(M * 16);
-			P.pend_emit = (float4 *)A(M * 16);
-			P.v0p = (float4 *)A(M * 16);
-			P.v0wo = (float4 *)A(M * 16);
-			P.rng = (uint2 *)A(M * 8);
-			P.pix = (uint2 *)A(M * 8);
-			P.nee = (float4 *)A(M * K * 16);
-			P.occ = (uint8_t *)A(M * K);
+			for(Buf &b : d.chunk_bufs) b.release();
+			d.chunk_bufs.clear();
+			auto A = [&](size_t bytes) -> void * {
+				d.chunk_bufs.emplace_back();
+				Buf &b = d.chunk_bufs.back();
+				if(hipMalloc(&b.p, std::max<size_t>(bytes, 16)) != hipSuccess)
+				{
+					b.p = nullptr;
+					(void)hipGetLastError();
+					return nullptr;
+				}
+				b.bytes = bytes;
+				return b.p;
+			};
+			for(int q = 0; q < 2; ++q)
+			{
+				DevPaths &P = d.P[q];
+				P.stage = (uint32_t *)A(M * 4);
+				P.flags = (uint32_t *)A(M * 4);
+				P.w = (float *)A(M * 4);
+				P.thr = (float4 *)A(M * 16);
+				P.col = (float4 *)A(M * 16);
+				P.pcol = (float4 *)A(M * 16);
+				P.pwo = (float4 *)A(M * 16);
+				P.pend_thr = (float4 *)A(M * 16);
+				P.pend_emit = (float4 *)A(M * 16);
+				P.v0p = (float4 *)A(need_v0 ? M * 16 : 16);      // first-hit data: path_samples > 1 only
+				P.v0wo = (float4 *)A(need_v0 ? M * 16 : 16);
+				P.rng = (uint2 *)A(M * 8);
+				P.pix = (uint2 *)A(M * 8);
+				P.nee = (float4 *)A(M * K * 16);
+				P.occ = (uint8_t *)A(M * K);
+			}
+			for(int q = 0; q < 2; ++q)
+			{
+				DevQueues &Q = d.Q[q];
+				Q.slot = (int *)A(M * 4);
+				Q.ray_o = (float4 *)A(M * 16);
+				Q.ray_d = (float4 *)A(M * 16);
+				Q.hit_t = (float *)A(M * 4);
+				Q.hit_prim = (int *)A(M * 4);
+				Q.sh_o = (float4 *)A(M * K * 16);
+				Q.sh_d = (float4 *)A(M * K * 16);
+				Q.sh_idx = (int *)A(M * K * 4);
+			}
+			d.N.p_prim = (float4 *)A(M * 16);
+			d.N.wo_k = (float4 *)A(M * 16);
+			d.N.pix_mode = (uint4 *)A(M * 16);
+			bool ok = true;
+			for(const Buf &b : d.chunk_bufs) ok = ok && b.p;
+			if(ok) break;
+			if(M <= 65536) { log_.error("GPU: out of device memory for the wavefront buffers"); return false; }
+			M /= 2;
+			log_.warning("GPU: wavefront buffers do not fit, retrying with " + std::to_string(M) + " samples in flight");
 		}
-		for(int q = 0; q < 2; ++q)
-		{
-			DevQueues &Q = d.Q[q];
-			Q.slot = (int *)A(M * 4);
-			Q.ray_o = (float4 *)A(M * 16);
-			Q.ray_d = (float4 *)A(M * 16);
-			Q.hit_t = (float *)A(M * 4);
-			Q.hit_prim = (int *)A(M * 4);
-			Q.sh_o = (float4 *)A(M * K * 16);
-			Q.sh_d = (float4 *)A(M * K * 16);
-			Q.sh_idx = (int *)A(M * K * 4);
-		}
-		for(const Buf &b : d.chunk_bufs)
-			if(!b.p) { log_.error("GPU: out of device memory for the wavefront buffers"); return false; }
+		d.v0_alloc = need_v0;
 		d.slots_cap = M;
 		d.nee_cap = K;
 	}
@@ -342,7 +373,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 
 	// ---- events ----
 	const size_t n_chunks = (size_t)((total + M - 1) / M);
-	const size_t ev_needed = 2 + (rp.profile ? 2 * n_chunks * (size_t)iters : 0);
+	const size_t ev_needed = 2 + (rp.profile ? 4 * n_chunks * (size_t)iters : 0);
 	while(d.ev_pool.size() < ev_needed)
 	{
 		hipEvent_t e;
@@ -362,9 +393,12 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i], d.stream));
 			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &cnt[cur ^ 1], &d.P[cur], dstats, d.stack_depth, d.trace_grid, d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 1], d.stream));
-			if(rp.profile) ev_i += 2;
-			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &cnt[cur], &cnt[cur ^ 1], (float4 *)d.samples.p,
-			                             (const DevJob *)d.jobs.p, n_jobs, base, d.shade_grid, d.stream));
+			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
+			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.shade_grid, d.stream));
+			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 2], d.stream));
+			HIPCHECK(yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.nee_grid, d.stream));
+			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 3], d.stream));
+			if(rp.profile) ev_i += 4;
 			cur ^= 1;
 		}
 	}
@@ -394,14 +428,20 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	stats_.samples = total;
 	stats_.render_seconds = ms * 1e-3;
 	stats_.trace_kernel_ms = 0.0;
+	stats_.shade_kernel_ms = 0.0;
+	stats_.nee_kernel_ms = 0.0;
 	stats_.trace_launches = 0;
 	if(rp.profile)
 	{
-		for(size_t e = 2; e + 1 < ev_i; e += 2)
+		for(size_t e = 2; e + 3 < ev_i + 1; e += 4)
 		{
-			float t = 0.f;
+			float t = 0.f, u = 0.f, v = 0.f;
 			HIPCHECK(hipEventElapsedTime(&t, d.ev_pool[e], d.ev_pool[e + 1]));
+			HIPCHECK(hipEventElapsedTime(&u, d.ev_pool[e + 1], d.ev_pool[e + 2]));
+			HIPCHECK(hipEventElapsedTime(&v, d.ev_pool[e + 2], d.ev_pool[e + 3]));
 			stats_.trace_kernel_ms += t;
+			stats_.shade_kernel_ms += u;
+			stats_.nee_kernel_ms += v;
 			++stats_.trace_launches;
 		}
 	}

@@ -32,7 +32,7 @@ struct RenderParams
 	DevScene scene;                      // pointers filled by the renderer
 	DevFilm film;
 	int shard_rank = 0, shard_world = 1;
-	int chunk_slots = 1 << 20;
+	int chunk_slots = 1 << 25;   // samples in flight per wavefront chunk
 	bool profile = false;
 };
 

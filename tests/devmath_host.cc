@@ -8,10 +8,17 @@ void dm_ri(int which, const uint32_t *b, const uint32_t *r, float *o, int n)
 {
 	for(int i = 0; i < n; ++i) o[i] = which == 0 ? riVdC(b[i], r[i]) : which == 1 ? riS(b[i], r[i]) : riLp(b[i], r[i]);
 }
+int dm_udiv_check(uint32_t d, const uint32_t *n, int cnt)
+{
+	const UDiv q = udivMake(d);
+	for(int i = 0; i < cnt; ++i) if(udiv(n[i], q) != n[i] / d) return i;
+	return -1;
+}
 void dm_fnv(const uint32_t *in, uint32_t *o, int n) { for(int i = 0; i < n; ++i) o[i] = fnv32(in[i]); }
 void dm_lds(const uint8_t *perm, uint32_t base, double f, const uint32_t *idx, double *o, int n)
 {
-	for(int i = 0; i < n; ++i) o[i] = lowDiscrepancy(perm, base, f, idx[i]);
+	const UDiv dv = udivMake(base);
+	for(int i = 0; i < n; ++i) o[i] = lowDiscrepancy(perm, base, dv, f, idx[i]);
 }
 void dm_halton_first(uint32_t base, const uint32_t *start, float *o, int n)
 {

@@ -116,3 +116,16 @@ def test_low_discrepancy_faure(dm):
         dm.dm_lds(P(pt, C.c_uint8), C.c_uint32(primes[d]), C.c_double(round(1e9 / primes[d]) / 1e9), P(ii, C.c_uint32),
                   P(o, C.c_double), len(ii))
         assert np.array_equal(o, ref[m]), d
+
+
+def test_magic_division_exact(dm):
+    """udiv() (the digit loops' division by a run-time prime) equals n / d for every prime base the
+    samplers use, on edge values and random 32-bit numerators."""
+    rng = np.random.default_rng(7)
+    n = np.concatenate([np.arange(0, 5000), 2**32 - 1 - np.arange(0, 5000), rng.integers(0, 2**32, 200000)]).astype(np.uint32)
+    primes = [p for p in range(2, 260) if all(p % q for q in range(2, int(p**0.5) + 1))]
+    for d in primes + [2**31, 2**31 - 1, 1000003]:
+        nn = np.concatenate([n, (np.arange(1, 4000, dtype=np.uint64) * d % 2**32).astype(np.uint32)])
+        nn = np.concatenate([nn, nn - 1, nn + 1]).astype(np.uint32)
+        bad = dm.dm_udiv_check(d, P(nn, C.c_uint32), len(nn))
+        assert bad == -1, (d, int(nn[bad]))
