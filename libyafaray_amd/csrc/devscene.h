@@ -86,6 +86,7 @@ struct DevScene
 	int integrator, width, height, spp;
 	int tile, bounces, path_samples, rr_min_bounces;
 	int caustic_path, has_bg, bg_transp, nee_k;
+	uint32_t n_seg, cap_a, cap_s;   // queue segments; capacities: active list / NEE requests, shadow rays (= nee_k * cap_a)
 	float bg[4];
 	int shadow_bias_auto, ray_min_dist_auto;
 	float shadow_bias, ray_min_dist;
@@ -144,9 +145,17 @@ struct DevNeeQueue
 	uint4 *pix_mode;       // (PixelSamplingData offset, sample index, mode | light << 8, 0)
 };
 
+// Queues are segmented: segment b (capacity cap_a entries / cap_s shadow rays) belongs to workgroup
+// b of k_shade and k_nee, whose grids are the n_seg segments.  A workgroup consumes its segment and
+// appends its outputs to the same segment of the next queue through an LDS counter (one LDS atomic
+// per wave, no global atomics, no workgroup barriers), then publishes the count with a plain store.
+// An entry yields at most one next entry (and at most nee_k shadow rays), so a segment never
+// outgrows the camera's share.  k_trace runs n_seg * m workgroups, m per segment.
 struct DevCounters
 {
-	uint32_t n_active, n_shadow, n_nee, pad1;
+	uint32_t *n_active;   // [n_seg] active-list entries (closest rays + paths) per segment
+	uint32_t *n_shadow;   // [n_seg] shadow rays per segment
+	uint32_t *n_nee;      // [n_seg] NEE requests per segment
 };
 
 struct DevStats

@@ -85,6 +85,21 @@ __device__ __forceinline__ uint32_t waveAppend(bool want, uint32_t *counter)
 	return base + (uint32_t)__popcll(below);
 }
 
+// Segment worked on by this k_trace workgroup, its rank among the segment's workgroups and their
+// number (the trace grid is a multiple of n_seg).
+struct SegLoop
+{
+	uint32_t s, r, nb;
+};
+__device__ __forceinline__ SegLoop segLoop(uint32_t n_seg)
+{
+	SegLoop L;
+	L.s = blockIdx.x % n_seg;
+	L.r = blockIdx.x / n_seg;
+	L.nb = (gridDim.x - L.s + n_seg - 1) / n_seg;
+	return L;
+}
+
 // Diagnostic build (-DYAF_PHASE_TIMING): per-phase wave cycles of k_shade (clock64 deltas summed
 // by lane 0 of each wave), read with yafaray_amd_getPhaseCycles.  Off in the product build.
 #ifdef YAF_PHASE_TIMING
@@ -97,53 +112,6 @@ __device__ unsigned long long g_phase[16];
 #define PHASE(k)
 #define PHASE_FLUSH
 #endif
-
-// Workgroup-level append (one atomic per workgroup): every thread of the block must call it.
-// `scratch` is LDS of at least blockDim/64 + 1 words.
-template<int BLOCK>
-__device__ __forceinline__ uint32_t blockAppend(bool want, uint32_t *counter, uint32_t *scratch)
-{
-	const uint64_t mask = __ballot(want);
-	const int wid = threadIdx.x >> 6;
-	if(laneId() == 0) scratch[wid] = (uint32_t)__popcll(mask);
-	__syncthreads();
-	if(threadIdx.x == 0)
-	{
-		uint32_t tot = 0;
-		for(int w = 0; w < BLOCK / 64; ++w) tot += scratch[w];
-		scratch[BLOCK / 64] = tot ? atomicAdd(counter, tot) : 0u;
-	}
-	__syncthreads();
-	uint32_t base = scratch[BLOCK / 64];
-	for(int w = 0; w < wid; ++w) base += scratch[w];
-	__syncthreads();   // scratch is reused by the next call
-	const uint64_t below = mask & ((1ull << laneId()) - 1ull);
-	return base + (uint32_t)__popcll(below);
-}
-
-// Two independent appends in one workgroup-level round (one barrier sequence, two atomics).
-template<int BLOCK>
-__device__ __forceinline__ uint2 blockAppend2(bool want_a, bool want_b, uint32_t *counter_a, uint32_t *counter_b,
-                                              uint32_t *scratch)
-{
-	constexpr int NW = BLOCK / 64;
-	const uint64_t ma = __ballot(want_a), mb = __ballot(want_b);
-	const int wid = threadIdx.x >> 6;
-	if(laneId() == 0) { scratch[wid] = (uint32_t)__popcll(ma); scratch[NW + wid] = (uint32_t)__popcll(mb); }
-	__syncthreads();
-	if(threadIdx.x < 2)
-	{
-		uint32_t tot = 0;
-		for(int w = 0; w < NW; ++w) tot += scratch[threadIdx.x * NW + w];
-		scratch[2 * NW + threadIdx.x] = tot ? atomicAdd(threadIdx.x ? counter_b : counter_a, tot) : 0u;
-	}
-	__syncthreads();
-	uint32_t ba = scratch[2 * NW], bb = scratch[2 * NW + 1];
-	for(int w = 0; w < wid; ++w) { ba += scratch[w]; bb += scratch[NW + w]; }
-	__syncthreads();
-	const uint64_t below = (1ull << laneId()) - 1ull;
-	return make_uint2(ba + (uint32_t)__popcll(ma & below), bb + (uint32_t)__popcll(mb & below));
-}
 
 // ---------------------------------------------------------------------------------------------
 // k_camera
@@ -177,11 +145,20 @@ __device__ SampleCoord sampleCoord(const DevJob *jobs, int n_jobs, int width, in
 	return c;
 }
 
-__global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueues Q, DevCounters *cnt,
+__global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueues Q, DevCounters cnt,
                                                  const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n)
 {
+	// sample i of the chunk -> segment (i / 256) % n_seg, groups of 256 dense within the segment
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if((uint32_t)i < S.n_seg)
+	{
+		const uint32_t groups = (uint32_t)n / 256u, rem = (uint32_t)n % 256u, sg = (uint32_t)i, R = S.n_seg;
+		cnt.n_active[sg] = (groups / R) * 256u + (sg < groups % R ? 256u : 0u) + (sg == groups % R ? rem : 0u);
+		cnt.n_shadow[sg] = 0;
+	}
 	if(i >= n) return;
+	const uint32_t g = (uint32_t)i / 256u;
+	const uint32_t a = (g % S.n_seg) * S.cap_a + (g / S.n_seg) * 256u + (uint32_t)i % 256u;
 	const SampleCoord sc = sampleCoord(jobs, n_jobs, S.width, S.tile, S.spp, chunk_base + (uint64_t)i);
 	// integrator_tiled.cc:313-335
 	const uint32_t offset = fnv32((uint32_t)sc.y * fnv32((uint32_t)sc.x));
@@ -201,20 +178,19 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	const V3 cz = v3(c.cam_z[0], c.cam_z[1], c.cam_z[2]);
 	const float tmin = dot(cz, v3(c.near_p[0], c.near_p[1], c.near_p[2]) - pos) / dot(dir, cz);
 	const float tmax = dot(cz, v3(c.far_p[0], c.far_p[1], c.far_p[2]) - pos) / dot(dir, cz);
-	Q.slot[i] = i;          // sample id within the chunk travels with the queue entry
-	Q.ray_o[i] = f4(pos, tmin);
-	Q.ray_d[i] = f4(dir, tmax);
-	P.stage[i] = ST_CAMERA;
-	P.flags[i] = 0;
-	P.w[i] = 0.f;
-	P.col[i] = make_float4(0.f, 0.f, 0.f, 1.f);
-	P.pcol[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-	P.pix[i] = make_uint2(offset, S.base_offset + (uint32_t)sc.s);
+	Q.slot[a] = i;          // sample id within the chunk travels with the queue entry
+	Q.ray_o[a] = f4(pos, tmin);
+	Q.ray_d[a] = f4(dir, tmax);
+	P.stage[a] = ST_CAMERA;
+	P.flags[a] = 0;
+	P.w[a] = 0.f;
+	P.col[a] = make_float4(0.f, 0.f, 0.f, 1.f);
+	P.pcol[a] = make_float4(0.f, 0.f, 0.f, 0.f);
+	P.pix[a] = make_uint2(offset, S.base_offset + (uint32_t)sc.s);
 	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
 	// output is matched statistically — integrator_tiled.cc:272)
 	const uint32_t seed = fnv32((uint32_t)(chunk_base + (uint64_t)i) ^ S.rr_seed) + 123u;
-	P.rng[i] = make_uint2(30903u, seed);
-	if(i == 0) { cnt->n_active = (uint32_t)n; cnt->n_shadow = 0; }
+	P.rng[a] = make_uint2(30903u, seed);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -347,11 +323,9 @@ __device__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, 
 }
 
 template<bool LDS_SCENE>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, const DevCounters *cnt,
-                                                      DevCounters *cnt_next, DevPaths P, DevStats *stats, int stack_depth)
+__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P,
+                                                      DevStats *stats, int stack_depth)
 {
-	// the next shade appends into cnt_next: reset it here (it was consumed by the previous shade)
-	if(blockIdx.x == 0 && threadIdx.x == 0) { cnt_next->n_active = 0; cnt_next->n_shadow = 0; cnt_next->n_nee = 0; }
 	extern __shared__ float4 smem[];
 	int *stack = reinterpret_cast<int *>(smem);
 	TraceCtx C;
@@ -371,16 +345,19 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, 
 		C.nodes = S.nodes;
 		C.tris = S.tris;
 	}
-	const uint32_t n_a = cnt->n_active, n_s = cnt->n_shadow;
+	const SegLoop L = segLoop(S.n_seg);
+	const uint32_t n_a = cnt.n_active[L.s], n_s = cnt.n_shadow[L.s];
 	const uint32_t total = n_a + n_s;
+	const uint32_t a0 = L.s * S.cap_a, s0 = L.s * S.cap_s;
 	uint32_t visits = 0, tests = 0, n_closest = 0, n_shadow = 0;
-	const uint32_t stride = gridDim.x * blockDim.x;
+	const uint32_t stride = L.nb * blockDim.x;
 	// one uniform trip count per workgroup so every lane reaches the same exits
-	for(uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride)
+	for(uint32_t base = L.r * blockDim.x; base < total; base += stride)
 	{
-		const uint32_t i = base + threadIdx.x;
-		if(i < n_a)
+		const uint32_t j = base + threadIdx.x;
+		if(j < n_a)
 		{
+			const uint32_t i = a0 + j;
 			const float4 od = Q.ray_o[i], dd = Q.ray_d[i];
 			if(!(dd.w != dd.w))   // NaN marks "no ray this iteration"
 			{
@@ -393,9 +370,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, 
 				++n_closest;
 			}
 		}
-		else if(i < total)
+		else if(j < total)
 		{
-			const uint32_t k = i - n_a;
+			const uint32_t k = s0 + (j - n_a);
 			const float4 od = Q.sh_o[k], dd = Q.sh_d[k];
 			float t;
 			int prim;
@@ -593,19 +570,19 @@ __device__ __forceinline__ bool areaTri(V3 a, V3 b, V3 c, V3 o, V3 d, float &t)
 
 struct ShadeOut
 {
-	uint32_t *sh_count;
-	uint32_t *scratch;     // LDS for blockAppend
+	uint32_t *sh_count;    // shadow-ray counter of the shard
+	uint32_t sh_base;      // first address of the shard's shadow queue
 	DevQueues Qn;
 };
 
-// Appends (or not) one shadow ray per lane — every thread of the workgroup must call.
+// Appends (or not) one shadow ray per lane — every lane of the wave must call.
 __device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, int idx, const ShadeOut &out)
 {
 #ifdef YAF_EXP_NO_EMIT
 	if(want) out.Qn.sh_idx[idx] = idx;   // timing experiment only: no append (wrong images)
 	return;
 #endif
-	const uint32_t k = blockAppend<kShadeBlock>(want, out.sh_count, out.scratch);
+	const uint32_t k = out.sh_base + waveAppend(want, out.sh_count);
 	if(want)
 	{
 		out.Qn.sh_o[k] = f4(o, 0.f);
@@ -623,8 +600,8 @@ __device__ __forceinline__ void shadowRayOf(V3 from, V3 dir, float tmin, float t
 
 // Next-event estimation for one light: writes the contributions of every sample into
 // nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
-// Workgroup-uniform structure: `active` lanes do the work, every thread of the workgroup walks
-// the same loop bounds (the shadow-ray appends are workgroup-level).
+// Wave-uniform structure: `active` lanes do the work, every lane of the wave walks the same loop
+// bounds (the shadow-ray appends are wave-level).
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
                          float4 *nee, uint8_t *occ, const ShadeOut &out)
@@ -823,8 +800,8 @@ struct ShadeArgs
 	DevQueues Q;         // current (active list + hits)
 	DevQueues Qn;        // next
 	DevNeeQueue N;       // NEE requests for k_nee
-	const DevCounters *cnt;
-	DevCounters *cnt_next;
+	DevCounters cnt;     // counts of the current queue
+	DevCounters cnt_next;
 	float4 *samples;     // frame sample buffer [(y * W + x) * spp + s]
 	const DevJob *jobs;
 	int n_jobs;
@@ -867,17 +844,22 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 	const DevScene &S = A.S;
 	const DevPaths &Pc = A.Pc;
 	const DevPaths &Pn = A.Pn;
-	const uint32_t n_a = A.cnt->n_active;
-	__shared__ uint32_t append_scratch[2 * (kShadeBlock / 64) + 2];
+	// workgroup b works on segment b and appends to segment b of the next queue
+	const uint32_t seg = blockIdx.x;
+	const uint32_t n_a = A.cnt.n_active[seg];
+	const uint32_t a0 = seg * S.cap_a;
+	__shared__ uint32_t s_count[2];   // next active entries, NEE requests
+	if(threadIdx.x < 2) s_count[threadIdx.x] = 0;
+	__syncthreads();
 	const bool is_path = S.integrator == INT_PATH;
 	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
 	const int K = S.nee_k;
-	const uint32_t stride = gridDim.x * blockDim.x;
+	const uint32_t stride = blockDim.x;
 	PHASE_DECL
-	for(uint32_t base_i = blockIdx.x * blockDim.x; base_i < n_a; base_i += stride)
+	for(uint32_t base_j = 0; base_j < n_a; base_j += stride)
 	{
-		const uint32_t i = base_i + threadIdx.x;
-		const bool live = i < n_a;
+		const bool live = base_j + threadIdx.x < n_a;
+		const uint32_t i = a0 + base_j + threadIdx.x;   // address of the entry (shard base + position)
 		// ---- 0. load the entry (independent coalesced loads) ----
 		uint32_t sid = 0, stage = ST_NORAY, flags = 0;
 		uint2 pix = make_uint2(0u, 0u), rng = make_uint2(0u, 0u);
@@ -1128,8 +1110,8 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		// ---- 4. compaction: the entry moves to position k of the next queue ----
 		const bool keep = live && (want_ray || pending);   // pending => never finalized this iteration
 		const bool want_nee = live && (nee_v0 || nee_one);
-		const uint2 kj = blockAppend2<kShadeBlock>(keep, want_nee, &A.cnt_next->n_active, &A.cnt_next->n_nee, append_scratch);
-		const uint32_t k = kj.x;
+		// the entry stays in its shard: at most one next entry per entry, so the shard never overflows
+		const uint32_t k = a0 + waveAppend(keep, &s_count[0]);
 		if(keep)
 		{
 			A.Qn.slot[k] = (int)sid;
@@ -1160,9 +1142,10 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 
 		PHASE(4);
 		// ---- 5. next-event estimation request (served by k_nee; wants -> keep, so k is valid) ----
+		const uint32_t jn = waveAppend(want_nee, &s_count[1]);
 		if(want_nee)
 		{
-			const uint32_t j = kj.y;
+			const uint32_t j = a0 + jn;
 			A.N.p_prim[j] = f4(sp.p, __int_as_float(hit_prim));
 			A.N.wo_k[j] = f4(wo, __uint_as_float(k));
 			A.N.pix_mode[j] = make_uint4(offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8), 0u);
@@ -1170,6 +1153,12 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		PHASE(5);
 	}
 	PHASE_FLUSH;
+	__syncthreads();
+	if(threadIdx.x == 0)
+	{
+		A.cnt_next.n_active[seg] = s_count[0];
+		A.cnt_next.n_nee[seg] = s_count[1];
+	}
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1184,7 +1173,7 @@ struct NeeArgs
 	DevNeeQueue N;
 	DevPaths Pn;
 	DevQueues Qn;
-	DevCounters *cnt_next;
+	DevCounters cnt_next;
 };
 
 #ifndef YAF_NEE_MIN_WAVES
@@ -1193,18 +1182,23 @@ struct NeeArgs
 __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
 {
 	const DevScene &S = A.S;
-	__shared__ uint32_t append_scratch[kShadeBlock / 64 + 1];
+	// workgroup b serves the NEE requests of segment b, shadow rays go to segment b
+	const uint32_t seg = blockIdx.x;
+	__shared__ uint32_t s_count;
+	if(threadIdx.x == 0) s_count = 0;
+	__syncthreads();
 	ShadeOut out;
-	out.sh_count = &A.cnt_next->n_shadow;
-	out.scratch = append_scratch;
+	out.sh_count = &s_count;
+	out.sh_base = seg * S.cap_s;
 	out.Qn = A.Qn;
-	const uint32_t n_req = A.cnt_next->n_nee;
+	const uint32_t n_req = A.cnt_next.n_nee[seg];
+	const uint32_t a0 = seg * S.cap_a;
 	const int K = S.nee_k;
-	const uint32_t stride = gridDim.x * blockDim.x;
-	for(uint32_t base_j = blockIdx.x * blockDim.x; base_j < n_req; base_j += stride)
+	const uint32_t stride = blockDim.x;
+	for(uint32_t base_j = 0; base_j < n_req; base_j += stride)
 	{
-		const uint32_t j = base_j + threadIdx.x;
-		const bool live = j < n_req;
+		const bool live = base_j + threadIdx.x < n_req;
+		const uint32_t j = a0 + base_j + threadIdx.x;
 		float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), wk = pp;
 		uint4 pm = make_uint4(0u, 0u, 0u, 0u);
 		if(live)
@@ -1221,24 +1215,26 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs 
 		const bool all = live && (pm.z & 1u);
 		const bool one = live && !(pm.z & 1u);
 		const uint32_t lnum = pm.z >> 8;
-		if(__syncthreads_or(all))
+		if(__any(all))
 		{
 			// estimateAllDirectLight (montecarlo.cc:54-68)
 			for(int l = 0; l < S.n_lights; ++l)
 				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
 				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out);
 		}
-		if(__syncthreads_or(one))
+		if(__any(one))
 		{
 			// estimateOneDirectLight (montecarlo.cc:70-78), light `lnum`
 			for(int l = 0; l < S.n_lights; ++l)
 			{
 				const bool mine = one && lnum == (uint32_t)l;
-				if(!__syncthreads_or(mine)) continue;
+				if(!__any(mine)) continue;
 				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out);
 			}
 		}
 	}
+	__syncthreads();
+	if(threadIdx.x == 0) A.cnt_next.n_shadow[seg] = s_count;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1429,30 +1425,31 @@ int yafamd_shade_blocks_per_cu()
 	return nb;
 }
 
-hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, DevCounters *cnt,
+hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st)
 {
 	if(n <= 0) return hipSuccess;
-	hipLaunchKernelGGL(k_camera, dim3((n + 255) / 256), dim3(256), 0, st, *S, *P, *Q, cnt, jobs, n_jobs, chunk_base, n);
+	const int threads = max(n, (int)S->n_seg);   // the first n_seg threads also write the segment counts
+	hipLaunchKernelGGL(k_camera, dim3((threads + 255) / 256), dim3(256), 0, st, *S, *P, *Q, *cnt, jobs, n_jobs, chunk_base, n);
 	return hipGetLastError();
 }
 
-hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, DevCounters *cnt_next,
-                               const DevPaths *P, DevStats *stats, int stack_depth, int grid, hipStream_t st)
+hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P,
+                               DevStats *stats, int stack_depth, int grid, hipStream_t st)
 {
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	if(S->scene_in_lds)
 	{
 		const size_t bytes = stack_bytes + (size_t)(4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
-		hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, cnt, cnt_next, *P, stats, stack_depth);
+		hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth);
 	}
-	else hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kTraceBlock), stack_bytes, st, *S, *Q, cnt, cnt_next, *P, stats, stack_depth);
+	else hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kTraceBlock), stack_bytes, st, *S, *Q, *cnt, *P, stats, stack_depth);
 	return hipGetLastError();
 }
 
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
-                               const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, DevCounters *cnt_next,
-                               float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, int grid, hipStream_t st)
+                               const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, const DevCounters *cnt_next,
+                               float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st)
 {
 	ShadeArgs A;
 	A.S = *S;
@@ -1461,26 +1458,26 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	A.Q = *Q;
 	A.Qn = *Qn;
 	A.N = *N;
-	A.cnt = cnt;
-	A.cnt_next = cnt_next;
+	A.cnt = *cnt;
+	A.cnt_next = *cnt_next;
 	A.samples = samples;
 	A.jobs = jobs;
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
-	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, st, A);
+	hipLaunchKernelGGL(k_shade, dim3(S->n_seg), dim3(kShadeBlock), 0, st, A);
 	return hipGetLastError();
 }
 
 hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
-                             DevCounters *cnt_next, int grid, hipStream_t st)
+                             const DevCounters *cnt_next, hipStream_t st)
 {
 	NeeArgs A;
 	A.S = *S;
 	A.N = *N;
 	A.Pn = *Pn;
 	A.Qn = *Qn;
-	A.cnt_next = cnt_next;
-	hipLaunchKernelGGL(k_nee, dim3(grid), dim3(kShadeBlock), 0, st, A);
+	A.cnt_next = *cnt_next;
+	hipLaunchKernelGGL(k_nee, dim3(S->n_seg), dim3(kShadeBlock), 0, st, A);
 	return hipGetLastError();
 }
 

@@ -14,18 +14,18 @@
 using namespace yafamd;
 
 extern "C" {
-hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, DevCounters *cnt,
+hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st);
-hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, DevCounters *cnt_next,
-                               const DevPaths *P, DevStats *stats, int stack_depth, int grid, hipStream_t st);
+hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P,
+                               DevStats *stats, int stack_depth, int grid, hipStream_t st);
 int yafamd_trace_block();
 int yafamd_trace_blocks_per_cu(int lds_scene, size_t dyn_lds);
 int yafamd_shade_blocks_per_cu();
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
-                               const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, DevCounters *cnt_next,
-                               float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, int grid, hipStream_t st);
+                               const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, const DevCounters *cnt_next,
+                               float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
 hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
-                             DevCounters *cnt_next, int grid, hipStream_t st);
+                             const DevCounters *cnt_next, hipStream_t st);
 int yafamd_nee_blocks_per_cu();
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
                               float clamp_samples, hipStream_t st);
@@ -143,6 +143,8 @@ bool GpuRenderer::ready()
 	if(const char *e = getenv("YAFARAY_AMD_SHADE_GRID")) d_->shade_grid = std::max(1, atoi(e));   // tuning sweeps
 	d_->nee_grid = d_->n_cu * std::max(1, yafamd_nee_blocks_per_cu());
 	if(const char *e = getenv("YAFARAY_AMD_NEE_GRID")) d_->nee_grid = std::max(1, atoi(e));
+	// queue segments = k_shade / k_nee workgroups (devscene.h DevCounters)
+	d_->nee_grid = d_->shade_grid;
 	std::ostringstream os;
 	os << "GPU: device " << dev << " " << prop.name << " (" << prop.gcnArchName << ", " << prop.multiProcessorCount << " CUs, "
 	   << (prop.totalGlobalMem >> 30) << " GiB)";
@@ -193,6 +195,8 @@ bool GpuRenderer::upload(const HostScene &hs)
 		const size_t dyn = (size_t)d.stack_depth * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : 0);
 		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, dyn));
 		if(const char *e = getenv("YAFARAY_AMD_TRACE_GRID")) d.trace_grid = std::max(1, atoi(e));
+		// a whole number of workgroups per queue segment
+		d.trace_grid = std::max(1, d.trace_grid / d.shade_grid) * d.shade_grid;
 	}
 	// Faure tables, dims 0..49 (halton.cc:403-414: dims 0-2 share the base-3 table)
 	std::vector<uint8_t> perm;
@@ -297,12 +301,16 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
 	const int K = std::max(1, S.nee_k);
 	const bool need_v0 = S.path_samples > 1;
+	// segment capacity: the camera deals groups of 256 samples round-robin over the segments
+	const size_t R = (size_t)d.shade_grid;
+	auto shardCap = [R](size_t m) { return (((m + 255) / 256 + R - 1) / R) * 256; };
 	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc)
 	{
 		// Wavefront buffers for M samples in flight (~0.7 KB each: 288 GB of HBM holds tens of millions,
 		// and big chunks amortise the per-launch cost).  On allocation failure the chunk is halved.
 		for(;;)
 		{
+			const size_t MA = R * shardCap(M);   // addresses of the segmented arrays
 			for(Buf &b : d.chunk_bufs) b.release();
 			d.chunk_bufs.clear();
 			auto A = [&](size_t bytes) -> void * {
@@ -320,37 +328,37 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			for(int q = 0; q < 2; ++q)
 			{
 				DevPaths &P = d.P[q];
-				P.stage = (uint32_t *)A(M * 4);
-				P.flags = (uint32_t *)A(M * 4);
-				P.w = (float *)A(M * 4);
-				P.thr = (float4 *)A(M * 16);
-				P.col = (float4 *)A(M * 16);
-				P.pcol = (float4 *)A(M * 16);
-				P.pwo = (float4 *)A(M * 16);
-				P.pend_thr = (float4 *)A(M * 16);
-				P.pend_emit = (float4 *)A(M * 16);
-				P.v0p = (float4 *)A(need_v0 ? M * 16 : 16);      // first-hit data: path_samples > 1 only
-				P.v0wo = (float4 *)A(need_v0 ? M * 16 : 16);
-				P.rng = (uint2 *)A(M * 8);
-				P.pix = (uint2 *)A(M * 8);
-				P.nee = (float4 *)A(M * K * 16);
-				P.occ = (uint8_t *)A(M * K);
+				P.stage = (uint32_t *)A(MA * 4);
+				P.flags = (uint32_t *)A(MA * 4);
+				P.w = (float *)A(MA * 4);
+				P.thr = (float4 *)A(MA * 16);
+				P.col = (float4 *)A(MA * 16);
+				P.pcol = (float4 *)A(MA * 16);
+				P.pwo = (float4 *)A(MA * 16);
+				P.pend_thr = (float4 *)A(MA * 16);
+				P.pend_emit = (float4 *)A(MA * 16);
+				P.v0p = (float4 *)A(need_v0 ? MA * 16 : 16);      // first-hit data: path_samples > 1 only
+				P.v0wo = (float4 *)A(need_v0 ? MA * 16 : 16);
+				P.rng = (uint2 *)A(MA * 8);
+				P.pix = (uint2 *)A(MA * 8);
+				P.nee = (float4 *)A(MA * K * 16);
+				P.occ = (uint8_t *)A(MA * K);
 			}
 			for(int q = 0; q < 2; ++q)
 			{
 				DevQueues &Q = d.Q[q];
-				Q.slot = (int *)A(M * 4);
-				Q.ray_o = (float4 *)A(M * 16);
-				Q.ray_d = (float4 *)A(M * 16);
-				Q.hit_t = (float *)A(M * 4);
-				Q.hit_prim = (int *)A(M * 4);
-				Q.sh_o = (float4 *)A(M * K * 16);
-				Q.sh_d = (float4 *)A(M * K * 16);
-				Q.sh_idx = (int *)A(M * K * 4);
+				Q.slot = (int *)A(MA * 4);
+				Q.ray_o = (float4 *)A(MA * 16);
+				Q.ray_d = (float4 *)A(MA * 16);
+				Q.hit_t = (float *)A(MA * 4);
+				Q.hit_prim = (int *)A(MA * 4);
+				Q.sh_o = (float4 *)A(MA * K * 16);
+				Q.sh_d = (float4 *)A(MA * K * 16);
+				Q.sh_idx = (int *)A(MA * K * 4);
 			}
-			d.N.p_prim = (float4 *)A(M * 16);
-			d.N.wo_k = (float4 *)A(M * 16);
-			d.N.pix_mode = (uint4 *)A(M * 16);
+			d.N.p_prim = (float4 *)A(MA * 16);
+			d.N.wo_k = (float4 *)A(MA * 16);
+			d.N.pix_mode = (uint4 *)A(MA * 16);
 			bool ok = true;
 			for(const Buf &b : d.chunk_bufs) ok = ok && b.p;
 			if(ok) break;
@@ -362,11 +370,21 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		d.slots_cap = M;
 		d.nee_cap = K;
 	}
-	if(!ensure(log_, d.counters, 2 * sizeof(DevCounters))) return false;
+	S.n_seg = (uint32_t)R;
+	S.cap_a = (uint32_t)shardCap(d.slots_cap);
+	S.cap_s = S.cap_a * (uint32_t)K;
+	if(!ensure(log_, d.counters, 2 * 3 * R * sizeof(uint32_t))) return false;
 	if(!ensure(log_, d.stats, sizeof(DevStats) * (size_t)d.trace_grid)) return false;
-	HIPCHECK(hipMemsetAsync(d.counters.p, 0, 2 * sizeof(DevCounters), d.stream));
+	HIPCHECK(hipMemsetAsync(d.counters.p, 0, 2 * 3 * R * sizeof(uint32_t), d.stream));
 	HIPCHECK(hipMemsetAsync(d.stats.p, 0, sizeof(DevStats) * (size_t)d.trace_grid, d.stream));
-	DevCounters *cnt = (DevCounters *)d.counters.p;
+	DevCounters cnt[2];
+	for(int q = 0; q < 2; ++q)
+	{
+		uint32_t *base_q = (uint32_t *)d.counters.p + (size_t)q * 3 * R;
+		cnt[q].n_active = base_q;
+		cnt[q].n_shadow = base_q + R;
+		cnt[q].n_nee = base_q + 2 * R;
+	}
 	DevStats *dstats = (DevStats *)d.stats.p;
 	const int n_paths = std::max(1, S.path_samples);
 	const int iters = (S.integrator == INT_PATH) ? 2 + n_paths * (S.bounces + 2) : 3;
@@ -391,12 +409,12 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		for(int it = 0; it < iters; ++it)
 		{
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i], d.stream));
-			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &cnt[cur ^ 1], &d.P[cur], dstats, d.stack_depth, d.trace_grid, d.stream));
+			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], dstats, d.stack_depth, d.trace_grid, d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 1], d.stream));
 			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
-			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.shade_grid, d.stream));
+			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 2], d.stream));
-			HIPCHECK(yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.nee_grid, d.stream));
+			HIPCHECK(yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 3], d.stream));
 			if(rp.profile) ev_i += 4;
 			cur ^= 1;
