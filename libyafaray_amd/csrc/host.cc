@@ -432,7 +432,7 @@ bool Scene::buildAccelerator()
 	HostScene hs;
 	hs.n_prims = (int)tri_mat.size();
 	BvhInput in{verts.data(), tris.data(), hs.n_prims};
-	int leaf = 4;
+	int leaf = 1;   // pure SAH leaves (measured best on the Cornell box)
 	if(const char *e = getenv("YAFARAY_AMD_BVH_LEAF")) leaf = std::max(1, atoi(e));          // tuning sweeps
 	if(const char *e = getenv("YAFARAY_AMD_BVH_NODE_COST")) in.node_cost = (float)atof(e);
 	hs.bvh = buildBvh(in, leaf, 8);

@@ -223,24 +223,25 @@ __device__ __forceinline__ void boxPair(const float4 &n0, const float4 &n1, cons
 	tn1 = lo;
 }
 
-// primitive_triangle.cc:44-71.  Returns t or -1.
-__device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const float4 &c, V3 o, V3 d)
+// primitive_triangle.cc:44-71.  Returns t or -1.  The reference's arithmetic (correctly rounded
+// 1/det, then products) evaluated branch-free: every lane computes the same instruction stream
+// and the reference's early returns become one combined predicate (NaN comparisons keep their
+// reference outcome).  `t_cut` is unused by the exact test.
+__device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const float4 &c, V3 o, V3 d, float t_cut)
 {
+	(void)t_cut;
 	const V3 v0 = xyz(a), e1 = xyz(b), e2 = xyz(c);
 	const float eps = a.w;
 	const V3 pvec = cross(d, e2);
 	const float det = dot(e1, pvec);
-	if(det > -eps && det < eps) return -1.f;
 	const float inv_det = 1.f / det;
 	const V3 tvec = o - v0;
 	const float u = dot(tvec, pvec) * inv_det;
-	if(u < 0.f || u > 1.f) return -1.f;
 	const V3 qvec = cross(tvec, e1);
 	const float v = dot(d, qvec) * inv_det;
-	if((v < 0.f) || ((u + v) > 1.f)) return -1.f;
 	const float t = dot(e2, qvec) * inv_det;
-	if(t < eps) return -1.f;
-	return t;
+	const bool miss = (det > -eps && det < eps) || (u < 0.f || u > 1.f) || (v < 0.f) || ((u + v) > 1.f) || (t < eps);
+	return miss ? -1.f : t;
 }
 
 // Closest hit with t in [tmin, tmax) (ties -> lower primitive index), or any hit with t in
@@ -287,7 +288,7 @@ __device__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, 
 				++tests;
 				const float4 *tp = C.tris + 3 * q;
 				const float4 ta = tp[0], tb = tp[1], tc = tp[2];
-				const float t = triTest(ta, tb, tc, o, d);
+				const float t = triTest(ta, tb, tc, o, d, ANY ? tmax : t_best);
 				if(t == -1.f) continue;
 				const int prim = __float_as_int(tb.w);
 				if(ANY)
