@@ -93,6 +93,8 @@ struct DevScene
 	uint32_t base_offset, rr_seed;
 	float clamp_samples;
 	int nee_all_count;             // entries of the estimateAllDirectLight layout
+	int faure_bytes;               // size of the permutation table (padded to 16 B)
+	int small_tables;              // materials + per-primitive normals fit k_shade / k_nee LDS
 };
 
 struct DevFilm

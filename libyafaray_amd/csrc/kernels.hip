@@ -793,6 +793,50 @@ __device__ __forceinline__ float ldsDim(const DevScene &S, int dim, uint32_t n)
 	return (float)lowDiscrepancy(S.faure + fd.y, fd.x, dv, S.faure_inv[dim], n);
 }
 
+// k_shade / k_nee stage their per-sample lookup tables in LDS once per workgroup: the Faure
+// permutations and dimension descriptors (every Halton draw of the path sampler), and for small
+// scenes the materials and per-primitive normals (every hit).  The returned scene copy points at
+// the LDS copies, so the shading code reads them at LDS latency instead of L2 latency.
+__device__ __forceinline__ void copy16(uint4 *dst, const void *src, int n)
+{
+	const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+	for(int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = s4[k];
+}
+
+__host__ __device__ inline size_t shadeLdsBytes(const DevScene &S, bool small)
+{
+	size_t b = 50 * 16 + 25 * 16 + (size_t)S.faure_bytes;
+	if(small) b += (size_t)S.n_mats * sizeof(DevMaterial) + (size_t)S.n_tris * 16;
+	return b;
+}
+
+template<bool SMALL>
+__device__ __forceinline__ DevScene stageTables(const DevScene &G, uint4 *smem)
+{
+	DevScene S = G;
+	uint4 *p = smem;
+	copy16(p, G.faure_dim, 50);
+	S.faure_dim = p;
+	p += 50;
+	copy16(p, G.faure_inv, 25);
+	S.faure_inv = reinterpret_cast<const double *>(p);
+	p += 25;
+	if(SMALL)
+	{
+		const int nm = G.n_mats * (int)(sizeof(DevMaterial) / 16);
+		copy16(p, G.mats, nm);
+		S.mats = reinterpret_cast<const DevMaterial *>(p);
+		p += nm;
+		copy16(p, G.prim_ng, G.n_tris);
+		S.prim_ng = reinterpret_cast<const float4 *>(p);
+		p += G.n_tris;
+	}
+	copy16(p, G.faure, G.faure_bytes / 16);
+	S.faure = reinterpret_cast<const uint8_t *>(p);
+	__syncthreads();
+	return S;
+}
+
 struct ShadeArgs
 {
 	DevScene S;
@@ -840,9 +884,11 @@ __device__ __forceinline__ Surf surfFromPrim(const DevScene &S, V3 p, int prim)
 //   4. wave-ballot compaction: the entry's state moves to its position in the next queue
 //      (coalesced SoA reads and writes, no indirection);
 //   5. next-event estimation into the next state: contributions + shadow rays.
+template<bool SMALL>
 __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(ShadeArgs A)
 {
-	const DevScene &S = A.S;
+	extern __shared__ uint4 shade_smem[];
+	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
 	const DevPaths &Pc = A.Pc;
 	const DevPaths &Pn = A.Pn;
 	// workgroup b works on segment b and appends to segment b of the next queue
@@ -1180,9 +1226,11 @@ struct NeeArgs
 #ifndef YAF_NEE_MIN_WAVES
 #define YAF_NEE_MIN_WAVES 1
 #endif
+template<bool SMALL>
 __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
 {
-	const DevScene &S = A.S;
+	extern __shared__ uint4 shade_smem[];
+	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
 	// workgroup b serves the NEE requests of segment b, shadow rays go to segment b
 	const uint32_t seg = blockIdx.x;
 	__shared__ uint32_t s_count;
@@ -1415,14 +1463,14 @@ int yafamd_trace_blocks_per_cu(int lds_scene, size_t dyn_lds)
 int yafamd_nee_blocks_per_cu()
 {
 	int nb = 0;
-	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_nee, kShadeBlock, 0) != hipSuccess) nb = 0;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_nee<true>, kShadeBlock, 8192) != hipSuccess) nb = 0;
 	return nb;
 }
 
 int yafamd_shade_blocks_per_cu()
 {
 	int nb = 0;
-	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade, kShadeBlock, 0) != hipSuccess) nb = 0;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<true>, kShadeBlock, 8192) != hipSuccess) nb = 0;
 	return nb;
 }
 
@@ -1465,7 +1513,9 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	A.jobs = jobs;
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
-	hipLaunchKernelGGL(k_shade, dim3(S->n_seg), dim3(kShadeBlock), 0, st, A);
+	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
+	if(S->small_tables) hipLaunchKernelGGL(k_shade<true>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	else hipLaunchKernelGGL(k_shade<false>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	return hipGetLastError();
 }
 
@@ -1478,7 +1528,9 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	A.Pn = *Pn;
 	A.Qn = *Qn;
 	A.cnt_next = *cnt_next;
-	hipLaunchKernelGGL(k_nee, dim3(S->n_seg), dim3(kShadeBlock), 0, st, A);
+	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
+	if(S->small_tables) hipLaunchKernelGGL(k_nee<true>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	else hipLaunchKernelGGL(k_nee<false>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	return hipGetLastError();
 }
 

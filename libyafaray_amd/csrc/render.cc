@@ -81,6 +81,7 @@ struct GpuRenderer::Impl
 	Buf nodes, tris, prim_ng, mats, lights, faure, faure_dim, faure_inv;
 	int n_nodes = 0, n_tris = 0, n_mats = 0, n_lights = 0, depth = 0, stack_depth = 32;
 	bool scene_in_lds = false;
+	int faure_bytes = 0;
 	// frame buffers
 	Buf samples, film, weights, jobs;
 	int film_w = 0, film_h = 0;
@@ -218,6 +219,8 @@ bool GpuRenderer::upload(const HostScene &hs)
 		base[dim] = (uint32_t)primes[dim];
 		inv[dim] = (double)std::llround(1e9 / primes[dim]) / 1e9;
 	}
+	while(perm.size() % 16) perm.push_back(0);   // staged to LDS as 16-B words
+	d.faure_bytes = (int)perm.size();
 	if(!allocCopy(log_, d.faure, perm.data(), perm.size())) return false;
 	std::vector<uint4> fdim(50);
 	for(int dim = 0; dim < 50; ++dim)
@@ -245,6 +248,9 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.mats = (const DevMaterial *)d.mats.p;
 	S.lights = (const DevLight *)d.lights.p;
 	S.faure = (const uint8_t *)d.faure.p;
+	S.faure_bytes = d.faure_bytes;
+	// materials + per-primitive normals staged in LDS by k_shade / k_nee when they are small
+	S.small_tables = ((size_t)d.n_mats * sizeof(DevMaterial) + (size_t)d.n_tris * 16 <= 24 * 1024) ? 1 : 0;
 	S.faure_dim = (const uint4 *)d.faure_dim.p;
 	S.faure_inv = (const double *)d.faure_inv.p;
 	S.n_nodes = d.n_nodes;
