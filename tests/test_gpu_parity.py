@@ -45,9 +45,11 @@ def product_scene(product, spec):
     return yi
 
 
-@pytest.mark.parametrize("which", ["cornell", "test01"])
+@pytest.mark.parametrize("which", ["cornell", "test01", "sphere"])
 def test_trace_closest_and_shadow_bitexact(product, oracle_built, which):
-    spec = scenes.cornell(32, 32, spp=1) if which == "cornell" else scenes.test01(32, 32, spp=1)
+    """Ray level on all three scenes; "sphere" is BASELINE C4 (1M triangles, BVH in HBM/L2)."""
+    spec = {"cornell": lambda: scenes.cornell(32, 32, spp=1), "test01": lambda: scenes.test01(32, 32, spp=1),
+            "sphere": lambda: scenes.cornell_sphere(width=32, height=32, spp=1)}[which]()
     rays = random_rays(spec, 20000, 7)
     yi = product_scene(product, spec)
     t, prim = yi.trace_closest(rays)
@@ -82,6 +84,19 @@ def test_path_noRR_cornell_matches_oracle(product, oracle_built):
     # ray accounting: same queries as the reference loop (no RR)
     assert st["closest_rays"] == octr[0]
     assert st["shadow_rays"] <= octr[1]
+
+
+def test_path_noRR_sphere_matches_oracle(product, oracle_built):
+    """BASELINE C4 scene (Cornell box + 999,698-triangle sphere): the BVH does not fit LDS, so this
+    exercises the global-memory traversal (k_trace<false>) end to end."""
+    spec = scenes.cornell_sphere(width=64, height=48, spp=4, bounces=8, rr=False)
+    rgba, w, st = product.render_spec(spec)
+    assert st["scene_in_lds"] == 0
+    orgba, ow, octr = oracle_built.OracleScene(spec, threads=8).render()
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    d = ulp_diff(rgba, orgba)
+    assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
+    assert st["closest_rays"] == octr[0]
 
 
 def test_path_gauss_filter_and_multichunk(product, oracle_built):
