@@ -177,6 +177,26 @@ YD_COLD float x87mulDivExact(double chi, double clo, float a, float b)
 	return round24(round64(fastTwoSum(q1, q2)));
 }
 
+// (float)(1.0L / ((long double)C * a)) with a > 0 (photon density scale,
+// integrator_photon_mapping.cc:963: 1.f / ((float)paths * radius * num_pi)): the product is
+// rounded to 64 bits, the quotient formed to ~104 bits, then rounded to 64 bits and to float.
+YD_COLD float x87recipMulExact(double chi, double clo, float a)
+{
+	const X87Const c = {chi, clo};
+	const DD t = round64(exactMul(c, (double)a));
+	const double q1 = 1.0 / t.hi;
+	const double r1 = fma(-q1, t.hi, 1.0) - q1 * t.lo;   // 1 - q1 * (t.hi + t.lo), exact to ~2^-104
+	const double q2 = r1 / t.hi;
+	return round24(round64(fastTwoSum(q1, q2)));
+}
+
+YD float x87recipMul(const X87Const &c, float a)
+{
+	float f;
+	if(safeToRound(1.0 / (c.hi * (double)a), f)) return f;
+	return x87recipMulExact(c.hi, c.lo, a);
+}
+
 // (float)((long double)C * x)
 YD float x87mul(const X87Const &c, float x)
 {

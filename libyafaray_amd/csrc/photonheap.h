@@ -1,0 +1,101 @@
+// k-nearest-photon max-heap with exactly the element moves of libstdc++'s std::make_heap /
+// std::pop_heap / std::push_heap (bits/stl_heap.h: __adjust_heap, __push_heap), which the
+// reference's PhotonGather uses on FoundPhoton (operator< on the squared distance;
+// src/photon/photon.cc:31-52).  The density estimate sums the found photons in heap-array order
+// (integrator_photon_mapping.cc:964-975), so reproducing the array order bit for bit requires the
+// same algorithm, not just any heap.  Compiled for the device (kernels.hip) and for the host
+// (tests/photon_check.cc pins it against std:: on random inputs with ties).
+#pragma once
+
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define YPH __host__ __device__ __forceinline__
+#else
+#define YPH inline
+#endif
+
+namespace yafamd
+{
+
+// Heap storage accessor: entries are (photon index, squared distance), possibly strided in LDS.
+struct HeapRef
+{
+	uint32_t *idx;
+	float *dist;
+	int stride;   // distance in elements between consecutive heap slots (lanes interleaved in LDS)
+	YPH uint32_t &i(int k) const { return idx[k * stride]; }
+	YPH float &d(int k) const { return dist[k * stride]; }
+};
+
+// __push_heap(first, holeIndex, topIndex, value)
+YPH void heapPushUp(const HeapRef &h, int hole, int top, uint32_t vi, float vd)
+{
+	int parent = (hole - 1) / 2;
+	while(hole > top && h.d(parent) < vd)
+	{
+		h.i(hole) = h.i(parent);
+		h.d(hole) = h.d(parent);
+		hole = parent;
+		parent = (hole - 1) / 2;
+	}
+	h.i(hole) = vi;
+	h.d(hole) = vd;
+}
+
+// __adjust_heap(first, holeIndex, len, value)
+YPH void heapAdjust(const HeapRef &h, int hole, int len, uint32_t vi, float vd)
+{
+	const int top = hole;
+	int second = hole;
+	while(second < (len - 1) / 2)
+	{
+		second = 2 * (second + 1);
+		if(h.d(second) < h.d(second - 1)) --second;
+		h.i(hole) = h.i(second);
+		h.d(hole) = h.d(second);
+		hole = second;
+	}
+	if((len & 1) == 0 && second == (len - 2) / 2)
+	{
+		second = 2 * (second + 1);
+		h.i(hole) = h.i(second - 1);
+		h.d(hole) = h.d(second - 1);
+		hole = second - 1;
+	}
+	heapPushUp(h, hole, top, vi, vd);
+}
+
+// std::make_heap(first, first + len)
+YPH void heapMake(const HeapRef &h, int len)
+{
+	if(len < 2) return;
+	for(int parent = (len - 2) / 2;; --parent)
+	{
+		const uint32_t vi = h.i(parent);
+		const float vd = h.d(parent);
+		heapAdjust(h, parent, len, vi, vd);
+		if(parent == 0) return;
+	}
+}
+
+// std::pop_heap(first, first + len) followed by first[len - 1] = new value and
+// std::push_heap(first, first + len): PhotonGather's "replace the farthest" step.
+YPH void heapReplaceTop(const HeapRef &h, int len, uint32_t ni, float nd)
+{
+	if(len > 1)
+	{
+		// __pop_heap: value = *(last - 1); *(last - 1) = *first; __adjust_heap(first, 0, len - 1, value)
+		const uint32_t vi = h.i(len - 1);
+		const float vd = h.d(len - 1);
+		h.i(len - 1) = h.i(0);
+		h.d(len - 1) = h.d(0);
+		heapAdjust(h, 0, len - 1, vi, vd);
+	}
+	h.i(len - 1) = ni;
+	h.d(len - 1) = nd;
+	// __push_heap(first, len - 1, 0, value)
+	heapPushUp(h, len - 1, 0, ni, nd);
+}
+
+} // namespace yafamd

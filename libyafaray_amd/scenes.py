@@ -92,6 +92,14 @@ class Render:
     base_sampling_offset: int = 0
     clamp_samples: float = 0.0
     accelerator: str = "yafaray-kdtree-original"
+    # photonmapping (integrator_photon_mapping.cc:765-850); final gathering is not supported
+    pm_photons: int = 100000
+    pm_search: int = 50
+    pm_diffuse_radius: float = 0.1
+    pm_bounces: int = 5
+    pm_caustics: bool = False
+    pm_caustic_photons: int = 500000
+    threads_photons: int = 1
 
 
 @dataclass
@@ -188,6 +196,17 @@ def cornell(width=1920, height=1080, spp=64, bounces=8, rr=False, integrator="pa
                   aa_pixelwidth=pixelwidth, tile_size=tile_size, bounces=bounces, path_samples=1,
                   rr_min_bounces=(0 if rr else bounces), caustic_type="none")
     return SceneSpec(verts, tris, tri_mat, mats, [light], cam, rend, Background((0.0, 0.0, 0.0), 1.0), b.objects)
+
+
+def cornell_photon(width=1920, height=1080, spp=1, photons=10_000_000, search=50, radius=0.1, bounces=5,
+                   caustics=False, **kw) -> SceneSpec:
+    """BASELINE C5: the C2 Cornell box rendered by the PhotonIntegrator (diffuse photon map,
+    k-NN density estimate, finalGather off — SURVEY.md §8d)."""
+    import dataclasses
+    s = cornell(width, height, spp=spp, integrator="photonmapping", **kw)
+    r = dataclasses.replace(s.render, pm_photons=photons, pm_search=search, pm_diffuse_radius=radius,
+                            pm_bounces=bounces, pm_caustics=caustics)
+    return dataclasses.replace(s, render=r)
 
 
 def uv_sphere(n=707, center=(0.0, 0.0, 1.0), r=0.5):
@@ -335,6 +354,14 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetInt("path_samples", r.path_samples)
         api.paramsSetInt("russian_roulette_min_bounces", r.rr_min_bounces)
         api.paramsSetString("caustic_type", r.caustic_type)
+    if r.integrator == "photonmapping":
+        api.paramsSetInt("photons", r.pm_photons)
+        api.paramsSetInt("cPhotons", r.pm_caustic_photons)
+        api.paramsSetInt("search", r.pm_search)
+        api.paramsSetFloat("diffuseRadius", r.pm_diffuse_radius)
+        api.paramsSetInt("bounces", r.pm_bounces)
+        api.paramsSetBool("caustics", r.pm_caustics)
+        api.paramsSetBool("finalGather", False)
     api.createIntegrator("default")
     api.paramsClearAll()
     api.paramsSetString("type", "combined")
@@ -360,5 +387,6 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetInt("adv_base_sampling_offset", r.base_sampling_offset)
     api.paramsSetString("scene_accelerator", r.accelerator)
     api.paramsSetInt("threads", -1)
+    api.paramsSetInt("threads_photons", r.threads_photons)
     api.setupRender()
     api.paramsClearAll()

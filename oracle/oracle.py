@@ -18,7 +18,7 @@ REF_SO = os.path.join(HERE, "_ref", "libyafref_prims.so")
 
 YC_MAT_SHINYDIFFUSE, YC_MAT_LIGHT = 0, 1
 YC_LIGHT_POINT, YC_LIGHT_AREA = 0, 1
-YC_INT_DIRECT, YC_INT_PATH = 0, 1
+YC_INT_DIRECT, YC_INT_PATH, YC_INT_PHOTON = 0, 1, 2
 FILTERS = {"box": 0, "gauss": 1, "mitchell": 2, "lanczos": 3}
 
 
@@ -47,7 +47,9 @@ class yc_render(C.Structure):
                 ("has_background", C.c_int), ("bg_color", C.c_float * 3), ("bg_transp", C.c_int),
                 ("shadow_bias_auto", C.c_int), ("shadow_bias", C.c_float), ("ray_min_dist_auto", C.c_int),
                 ("ray_min_dist", C.c_float), ("base_sampling_offset", C.c_int), ("clamp_samples", C.c_float),
-                ("threads", C.c_int), ("rr_seed", C.c_uint32)]
+                ("threads", C.c_int), ("rr_seed", C.c_uint32), ("pm_photons", C.c_int), ("pm_search", C.c_int),
+                ("pm_diffuse_radius", C.c_float), ("pm_bounces", C.c_int), ("pm_caustics", C.c_int),
+                ("pm_threads", C.c_int)]
 
 
 class yc_scene(C.Structure):
@@ -247,7 +249,7 @@ class OracleScene:
         sc.cam.near_clip, sc.cam.far_clip = cam.near_clip, cam.far_clip
         r = s.render
         rp = sc.rp
-        rp.integrator = YC_INT_PATH if r.integrator == "pathtracing" else YC_INT_DIRECT
+        rp.integrator = {"pathtracing": YC_INT_PATH, "photonmapping": YC_INT_PHOTON}.get(r.integrator, YC_INT_DIRECT)
         rp.width, rp.height = r.width, r.height
         rp.aa_samples = r.aa_samples
         rp.filter = FILTERS[r.filter_type]
@@ -265,6 +267,8 @@ class OracleScene:
         rp.clamp_samples = r.clamp_samples
         rp.threads = threads
         rp.rr_seed = rr_seed
+        rp.pm_photons, rp.pm_search, rp.pm_diffuse_radius = r.pm_photons, r.pm_search, r.pm_diffuse_radius
+        rp.pm_bounces, rp.pm_caustics, rp.pm_threads = r.pm_bounces, int(r.pm_caustics), r.threads_photons
         self.sc = sc
         self.spec = spec
 
@@ -276,6 +280,19 @@ class OracleScene:
         oracle_lib().yc_render_image(C.byref(self.sc), C.c_int(y0), C.c_int(y1), _p(rgba, C.c_float),
                                      _p(w, C.c_float), C.byref(ctr))
         return rgba.reshape(r.height, r.width, 4), w.reshape(r.height, r.width), (ctr.closest_rays, ctr.shadow_rays)
+
+    def photon_map(self):
+        """(pos, dir, col [n x 3 each], kd nodes [m x 2 uint32], n_paths) of the diffuse photon map."""
+        L = oracle_lib()
+        n_paths = C.c_int(0)
+        n = L.yc_photon_map(C.byref(self.sc), None, None, None, None, C.byref(n_paths))
+        if n < 0:
+            raise RuntimeError("photon map failed (too few photons)")
+        pos, d, col = (np.empty(3 * n, np.float32) for _ in range(3))
+        nodes = np.empty(2 * max(1, 2 * n - 1), np.uint32)
+        L.yc_photon_map(C.byref(self.sc), _p(pos, C.c_float), _p(d, C.c_float), _p(col, C.c_float),
+                        _p(nodes, C.c_uint32), C.byref(n_paths))
+        return pos.reshape(n, 3), d.reshape(n, 3), col.reshape(n, 3), nodes.reshape(-1, 2)[:max(0, 2 * n - 1)], n_paths.value
 
     def render_samples(self, xys):
         xys = np.ascontiguousarray(xys, np.int32).reshape(-1)

@@ -1253,6 +1253,347 @@ class Renderer
 			alpha = 1.f;
 		}
 
+		// ------------------------------------------------------------------------------------
+		// Photon mapping (integrator_photon_mapping.cc, finalGather = false)
+		// ------------------------------------------------------------------------------------
+		// include/photon/photon.h:30-78 (no SMALL_PHOTONS)
+		struct Photon { V3 pos, dir; C3 col; };
+		// include/photon/pkdtree.h:41-64: leaf -> photon index, interior -> split + right child
+		struct PkNode
+		{
+			uint32_t data = 0;    // split position bits (interior) or photon index (leaf)
+			uint32_t flags = 0;   // bits 0-1 axis (3 = leaf), bits 2.. right child
+			bool isLeaf() const { return (flags & 3u) == 3u; }
+			int axis() const { return (int)(flags & 3u); }
+			float split() const { float f; std::memcpy(&f, &data, 4); return f; }
+			uint32_t right() const { return flags >> 2; }
+		};
+		std::vector<Photon> photons;
+		std::vector<PkNode> pk_nodes;
+		int n_paths = 0;
+
+		// include/sampler/sample_pdf1d.h:52-93 (cumulateStep1DDf + dSample)
+		struct Pdf1D
+		{
+			std::vector<float> func, cdf;
+			float integral = 0.f, inv_integral = 0.f;
+			explicit Pdf1D(const std::vector<float> &f) : func(f), cdf(f.size())
+			{
+				const double delta = 1.0 / static_cast<double>(f.size());
+				double c = 0.0;
+				for(size_t i = 0; i < f.size(); ++i)
+				{
+					c += static_cast<double>(f[i]) * delta;
+					cdf[i] = static_cast<float>(c);
+				}
+				integral = static_cast<float>(c);
+				for(float &e : cdf) e /= integral;
+				inv_integral = 1.f / integral;
+			}
+			int dSample(float u, float &pdf) const
+			{
+				int index;
+				if(u <= 0.f) index = 0;
+				else if(u >= 1.f) index = (int)cdf.size() - 1;
+				else index = (int)(std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin());
+				pdf = func[index] * inv_integral;
+				return index;
+			}
+		};
+
+		// sample.h:58-75
+		static V3 sphereDir(float s_1, float s_2)
+		{
+			V3 dir;
+			dir.z = 1.0f - 2.0f * s_1;
+			float r = 1.0f - dir.z * dir.z;
+			if(r > 0.0f)
+			{
+				r = fsqrt(r);
+				const float a = static_cast<float>(mult_pi_by_2 * s_2);
+				dir.x = fcos(a) * r;
+				dir.y = fsin(a) * r;
+			}
+			else { dir.x = 0.0f; dir.y = 0.0f; }
+			return dir;
+		}
+
+		// light_area.cc:98-104, light_point.cc:79-85
+		static C3 emitPhoton(const Light &L, float s_1, float s_2, float s_3, float s_4, Ray &ray, float &ipdf)
+		{
+			if(L.type == YC_LIGHT_POINT)
+			{
+				ray.from = L.position;
+				ray.dir = sphereDir(s_1, s_2);
+				ipdf = static_cast<float>(4.0f * num_pi);
+				return L.color;
+			}
+			ipdf = L.area;
+			ray.from = L.corner + s_3 * L.to_x + s_4 * L.to_y;
+			ray.dir = cosHemisphere(L.normal, L.du, L.dv, s_1, s_2);
+			return L.color;
+		}
+
+		// light_area.cc:64, light_point.h:41 (Rgb::energy, color.h:59)
+		static float lightEnergy(const Light &L)
+		{
+			const C3 e = (L.type == YC_LIGHT_POINT) ? (L.color * 4.0f) * static_cast<float>(num_pi) : L.color * L.area;
+			return (e.r + e.g + e.b) * 0.333333f;
+		}
+
+		// material.cc:137-153 (Material::scatterPhoton) with PSample (material.h:260-268)
+		bool scatterPhoton(const SurfacePoint &sp, const V3 &wi, V3 &wo, float s_1, float s_2, float s_3, const C3 &lcol,
+		                   C3 &color_out, unsigned &sampled) const
+		{
+			float w = 0.f;
+			Sample s(s_1, s_2, BAll);
+			const C3 scol = sample(sp, wi, wo, s, w);
+			sampled = s.sampled_flags;
+			if(s.pdf > 1.0e-6f)
+			{
+				const C3 alpha(1.f);
+				const C3 cnew = lcol * alpha * scol * w;
+				const float new_max = std::max(cnew.r, std::max(cnew.g, cnew.b));
+				const float old_max = std::max(lcol.r, std::max(lcol.g, lcol.b));
+				const float prob = std::min(1.f, new_max / old_max);
+				if(s_3 <= prob && prob > 1e-4f)
+				{
+					color_out = cnew / prob;
+					return true;
+				}
+			}
+			return false;
+		}
+
+		// integrator_photon_mapping.cc:110-235 (diffuseWorker), photons in photon-id order
+		void shootDiffusePhotons(Thread &th)
+		{
+			const yc_render &rp = sc_.rp;
+			photons.clear();
+			const int num_lights = (int)sc_.lights.size();
+			if(num_lights == 0 || rp.pm_photons <= 0) { n_paths = 0; return; }
+			std::vector<float> energies(num_lights);
+			for(int i = 0; i < num_lights; ++i) energies[i] = lightEnergy(sc_.lights[i]);
+			const Pdf1D light_power(energies);
+			const int T = std::max(1, rp.pm_threads);
+			const unsigned n_photons = std::max((unsigned)T, ((unsigned)rp.pm_photons / T) * T);   // :437
+			const float f_num_lights = static_cast<float>(num_lights);
+			const float inv_diff_photons = 1.f / static_cast<float>(n_photons);
+			for(unsigned h = 0; h < n_photons; ++h)
+			{
+				const float s_1 = riVdC(h);
+				const float s_2 = static_cast<float>(lowDiscrepancySampling(2, h));
+				const float s_3 = static_cast<float>(lowDiscrepancySampling(3, h));
+				const float s_4 = static_cast<float>(lowDiscrepancySampling(4, h));
+				const float s_l = float(h) * inv_diff_photons;
+				float light_num_pdf;
+				const int light_num = light_power.dSample(s_l, light_num_pdf);
+				Ray ray;
+				float light_pdf;
+				C3 pcol = emitPhoton(sc_.lights[light_num], s_1, s_2, s_3, s_4, ray, light_pdf);
+				ray.tmin = rp.ray_min_dist;
+				ray.tmax = -1.f;
+				pcol = pcol * (f_num_lights * light_pdf / light_num_pdf);
+				if(pcol.r == 0.f && pcol.g == 0.f && pcol.b == 0.f) continue;
+				int n_bounces = 0;
+				bool caustic_photon = false, direct_photon = true;
+				for(;;)
+				{
+					SurfacePoint sp;
+					if(!intersect(th, ray, sp)) break;
+					const V3 wi = -ray.dir;
+					if(sp.bsdf_flags & BDiffuse)
+					{
+						if(!caustic_photon) photons.push_back({sp.p, wi, pcol});
+					}
+					if(n_bounces == rp.pm_bounces) break;
+					const int d_5 = 3 * n_bounces + 5;
+					const float s_5 = static_cast<float>(lowDiscrepancySampling(d_5, h));
+					const float s_6 = static_cast<float>(lowDiscrepancySampling(d_5 + 1, h));
+					const float s_7 = static_cast<float>(lowDiscrepancySampling(d_5 + 2, h));
+					V3 wo;
+					C3 ncol;
+					unsigned sampled = BNone;
+					if(!scatterPhoton(sp, wi, wo, s_5, s_6, s_7, pcol, ncol, sampled)) break;
+					pcol = ncol;
+					caustic_photon = ((sampled & (BGlossy | BSpecular | BDispersive)) && direct_photon) ||
+					                 ((sampled & (BGlossy | BSpecular | BFilter | BDispersive)) && caustic_photon);
+					direct_photon = (sampled & BFilter) && direct_photon;
+					ray.from = sp.p;
+					ray.dir = wo;
+					ray.tmin = rp.ray_min_dist;
+					ray.tmax = -1.f;
+					++n_bounces;
+				}
+			}
+			n_paths = (int)n_photons;
+		}
+
+		// pkdtree.h:115-222 (the threaded and sequential builds produce the same DFS layout)
+		void buildPhotonTree()
+		{
+			const uint32_t n = (uint32_t)photons.size();
+			pk_nodes.assign(n ? 2 * (size_t)n - 1 : 0, PkNode());
+			if(!n) return;
+			std::vector<uint32_t> el(n);
+			for(uint32_t i = 0; i < n; ++i) el[i] = i;
+			V3 lo = photons[0].pos, hi = photons[0].pos;
+			for(uint32_t i = 1; i < n; ++i)
+				for(int a = 0; a < 3; ++a)
+				{
+					lo[a] = std::min(lo[a], photons[i].pos[a]);
+					hi[a] = std::max(hi[a], photons[i].pos[a]);
+				}
+			uint32_t next = 0;
+			buildRec(0, n, lo, hi, el.data(), next);
+		}
+		void buildRec(uint32_t start, uint32_t end, V3 lo, V3 hi, uint32_t *el, uint32_t &next)
+		{
+			if(end - start == 1)
+			{
+				pk_nodes[next].flags = 3;
+				pk_nodes[next].data = el[start];
+				++next;
+				return;
+			}
+			// bound.h:111-115 largestAxis
+			const V3 d = hi - lo;
+			const int axis = (d.x > d.y) ? ((d.x > d.z) ? 0 : 2) : ((d.y > d.z) ? 1 : 2);
+			const uint32_t split_el = (start + end) / 2;
+			// pkdtree.h:66-74 CompareNode: by coordinate, ties by element address (= index)
+			std::nth_element(el + start, el + split_el, el + end, [&](uint32_t a, uint32_t b) {
+				const float pa = photons[a].pos[axis], pb = photons[b].pos[axis];
+				return pa == pb ? (a < b) : pa < pb;
+			});
+			const uint32_t cur = next;
+			const float split_pos = photons[el[split_el]].pos[axis];
+			std::memcpy(&pk_nodes[cur].data, &split_pos, 4);
+			pk_nodes[cur].flags = (uint32_t)axis;
+			++next;
+			V3 hi_l = hi, lo_r = lo;
+			hi_l[axis] = split_pos;
+			lo_r[axis] = split_pos;
+			buildRec(start, split_el, lo, hi_l, el, next);
+			pk_nodes[cur].flags = (pk_nodes[cur].flags & 3u) | (next << 2);
+			buildRec(split_el, end, lo_r, hi, el, next);
+		}
+
+		// photon.h:93-100 FoundPhoton (operator< on the squared distance)
+		struct Found
+		{
+			uint32_t photon;
+			float dist_square;
+			bool operator<(const Found &o) const { return dist_square < o.dist_square; }
+		};
+
+		// pkdtree.h:225-292 (non-recursive lookup) + photon.cc:31-52 (PhotonGather heap management)
+		int gather(const V3 &p, Found *found, uint32_t k, float &max_dist_squared) const
+		{
+			struct Stack { int node; float s; int axis; };
+			Stack stack[64];
+			uint32_t n_found = 0;
+			int curr = 0;
+			int sp = 1;
+			stack[sp].node = -1;
+			for(;;)
+			{
+				while(!pk_nodes[curr].isLeaf())
+				{
+					const int axis = pk_nodes[curr].axis();
+					const float split_val = pk_nodes[curr].split();
+					int far_child;
+					if(p[axis] <= split_val) { far_child = (int)pk_nodes[curr].right(); curr = curr + 1; }
+					else { far_child = curr + 1; curr = (int)pk_nodes[curr].right(); }
+					++sp;
+					stack[sp].node = far_child;
+					stack[sp].axis = axis;
+					stack[sp].s = split_val;
+				}
+				const Photon &ph = photons[pk_nodes[curr].data];
+				const V3 v = ph.pos - p;
+				float dist_2 = v.lengthSqr();
+				if(dist_2 < max_dist_squared)
+				{
+					if(n_found < k)
+					{
+						found[n_found++] = {pk_nodes[curr].data, dist_2};
+						if(n_found == k)
+						{
+							std::make_heap(found, found + k);
+							max_dist_squared = found[0].dist_square;
+						}
+					}
+					else
+					{
+						std::pop_heap(found, found + k);
+						found[k - 1] = {pk_nodes[curr].data, dist_2};
+						std::push_heap(found, found + k);
+						max_dist_squared = found[0].dist_square;
+					}
+				}
+				if(stack[sp].node < 0) return (int)n_found;
+				int axis = stack[sp].axis;
+				dist_2 = p[axis] - stack[sp].s;
+				dist_2 *= dist_2;
+				while(dist_2 > max_dist_squared)
+				{
+					--sp;
+					if(stack[sp].node < 0) return (int)n_found;
+					axis = stack[sp].axis;
+					dist_2 = p[axis] - stack[sp].s;
+					dist_2 *= dist_2;
+				}
+				curr = stack[sp].node;
+				--sp;
+			}
+		}
+
+		// integrator_photon_mapping.cc:852-1004 with finalGather = false, show_map = false
+		void integratePhoton(Thread &th, Ray &ray, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha) const
+		{
+			const yc_render &rp = sc_.rp;
+			col = C3(0.f);
+			alpha = 1.f;
+			SurfacePoint sp;
+			if(intersect(th, ray, sp))
+			{
+				const V3 wo = -ray.dir;
+				const unsigned mat_bsdfs = sp.bsdf_flags;
+				col += emit(sp, wo);                                   // :868-869
+				if(mat_bsdfs & BEmit) col += emit(sp, wo);             // :938-946 (added a second time)
+				if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+				std::vector<Found> gathered((size_t)std::max(1, rp.pm_search));
+				float radius = rp.pm_diffuse_radius;                   // "actually the square radius"
+				int n_gathered = 0;
+				if(!photons.empty()) n_gathered = gather(sp.p, gathered.data(), (uint32_t)rp.pm_search, radius);
+				if(n_gathered > 0)
+				{
+					const float scale = 1.f / ((float)n_paths * radius * num_pi);
+					for(int i = 0; i < n_gathered; ++i)
+					{
+						const Photon &ph = photons[gathered[i].photon];
+						const C3 surf_col = eval(sp, wo, ph.dir, BDiffuse);
+						const C3 col_tmp = surf_col * scale * ph.col;
+						col += col_tmp;
+					}
+				}
+				if(rp.pm_caustics && (mat_bsdfs & BDiffuse)) col += C3(0.f);   // empty caustic map (:981-984, montecarlo.cc:644)
+				col += C3(0.f);   // recursiveRaytrace: no specular/glossy components
+				alpha = 1.f;
+			}
+			else background(ray, col, alpha);
+		}
+
+		bool preprocessPhotons()
+		{
+			if(sc_.rp.integrator != YC_INT_PHOTON) return true;
+			Thread th;
+			shootDiffusePhotons(th);
+			if(photons.size() < 50) return false;   // :448-452 "Too few diffuse photons"
+			buildPhotonTree();
+			return true;
+		}
+
 		// camera_perspective.cc:128-146 + plane.h:37-40
 		Ray shootRay(float px, float py) const
 		{
@@ -1287,6 +1628,7 @@ class Renderer
 				C3 col;
 				float alpha;
 				if(rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha);
+				else if(rp.integrator == YC_INT_PHOTON) integratePhoton(th, ray, sample_idx, offset, col, alpha);
 				else integrateDirect(th, ray, sample_idx, offset, col, alpha);
 				if(alpha > 1.f) alpha = 1.f;
 				out[4 * sample] = col.r;
@@ -1356,6 +1698,7 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 {
 	Scene sc(*s);
 	Renderer R(sc);
+	if(!R.preprocessPhotons()) return -1;
 	const yc_render &rp = sc.rp;
 	const int W = rp.width, H = rp.height;
 	if(y1 <= y0) { y0 = 0; y1 = H; }
@@ -1453,6 +1796,7 @@ int yc_render_samples(const yc_scene *s, int n, const int *xys, float *rgba)
 {
 	Scene sc(*s);
 	Renderer R(sc);
+	if(!R.preprocessPhotons()) return -1;
 	Renderer::Thread th;
 	const yc_render &rp = sc.rp;
 	const int spp = rp.aa_samples;
@@ -1473,6 +1817,7 @@ int yc_render_samples(const yc_scene *s, int n, const int *xys, float *rgba)
 		float alpha;
 		const uint32_t sample_idx = rp.base_sampling_offset + sample;
 		if(rp.integrator == YC_INT_PATH) R.integratePath(th, ray, rng, sample_idx, offset, col, alpha);
+		else if(rp.integrator == YC_INT_PHOTON) R.integratePhoton(th, ray, sample_idx, offset, col, alpha);
 		else R.integrateDirect(th, ray, sample_idx, offset, col, alpha);
 		rgba[4 * k] = col.r; rgba[4 * k + 1] = col.g; rgba[4 * k + 2] = col.b; rgba[4 * k + 3] = std::min(alpha, 1.f);
 	}
@@ -1610,6 +1955,26 @@ void yc_film_table(int filter, float filter_size, float *table, float *filterw, 
 	std::memcpy(table, t.table, sizeof(t.table));
 	*filterw = t.filterw;
 	*table_scale = t.table_scale;
+}
+
+
+int yc_photon_map(const yc_scene *s, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths)
+{
+	Scene sc(*s);
+	Renderer R(sc);
+	if(!R.preprocessPhotons()) return -1;
+	const size_t n = R.photons.size();
+	if(n_paths) *n_paths = R.n_paths;
+	for(size_t i = 0; i < n; ++i)
+	{
+		const auto &p = R.photons[i];
+		if(pos) { pos[3 * i] = p.pos.x; pos[3 * i + 1] = p.pos.y; pos[3 * i + 2] = p.pos.z; }
+		if(dir) { dir[3 * i] = p.dir.x; dir[3 * i + 1] = p.dir.y; dir[3 * i + 2] = p.dir.z; }
+		if(col) { col[3 * i] = p.col.r; col[3 * i + 1] = p.col.g; col[3 * i + 2] = p.col.b; }
+	}
+	if(nodes)
+		for(size_t i = 0; i < R.pk_nodes.size(); ++i) { nodes[2 * i] = R.pk_nodes[i].data; nodes[2 * i + 1] = R.pk_nodes[i].flags; }
+	return (int)n;
 }
 
 }

@@ -19,7 +19,7 @@ extern "C" {
 
 enum { YC_MAT_SHINYDIFFUSE = 0, YC_MAT_LIGHT = 1 };
 enum { YC_LIGHT_POINT = 0, YC_LIGHT_AREA = 1 };
-enum { YC_INT_DIRECT = 0, YC_INT_PATH = 1 };
+enum { YC_INT_DIRECT = 0, YC_INT_PATH = 1, YC_INT_PHOTON = 2 };
 enum { YC_FILTER_BOX = 0, YC_FILTER_GAUSS = 1, YC_FILTER_MITCHELL = 2, YC_FILTER_LANCZOS = 3 };
 
 typedef struct {
@@ -68,6 +68,14 @@ typedef struct {
 	float clamp_samples;
 	int threads;              // oracle worker threads for the sample loop (film order is fixed)
 	uint32_t rr_seed;         // stand-in for the reference's glibc rand() per-tile seed term
+	// photon mapping (integrator_photon_mapping.cc factory :765-850; finalGather = false only)
+	int pm_photons;           // "photons" (diffuse map)
+	int pm_search;            // "search" (k of the k-NN gather)
+	float pm_diffuse_radius;  // "diffuseRadius" — used as the SQUARED gather radius (:954)
+	int pm_bounces;           // "bounces"
+	int pm_caustics;          // "caustics": caustic photons are shot but only stored after specular
+	                          // bounces, which the supported materials never produce
+	int pm_threads;           // threads_photons: the photon count is rounded to a multiple (:437)
 } yc_render;
 
 typedef struct {
@@ -87,6 +95,12 @@ typedef struct {
 // (normalized, the put-pixel/flush values), weights: width*height (may be NULL).  The film pass
 // walks the reference's linear tile order, so results do not depend on `threads`.
 int yc_render_image(const yc_scene *scene, int y0, int y1, float *rgba, float *weights, yc_counters *counters);
+
+// Photon map of a PhotonIntegrator scene (shot in photon-id order, the reference's one-thread
+// order): positions/directions/colours (3 floats each) and the point kd-tree (2 uint32 per node:
+// split-position bits or photon index, flags).  Returns the photon count (n_paths in *n_paths),
+// or -1.  Pass NULL buffers to query the count.
+int yc_photon_map(const yc_scene *scene, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths);
 
 // Per-sample radiance for a list of (x, y, s) camera samples (RGBA per sample).
 int yc_render_samples(const yc_scene *scene, int n, const int *xys, float *rgba);

@@ -54,6 +54,16 @@ int main(int argc, char **argv)
 		if(!same(x87mul2(kDiv4BySquaredPi, x, std::abs(x)), (float)(div_4_by_squared_pi * x * std::abs(x)))) ++bad_mul2;
 		const float a = pos(rng), b = pos(rng);
 		if(!same(x87mulDiv(kPi, a, b), (float)(a * pi / b))) ++bad_div;
+		{
+			// integrator_photon_mapping.cc:963 — 1.f / ((float)paths * radius * num_pi)
+			const float pr = (float)(1 + (rng() % 20000000)) * (a * 1e-3f);
+			if(!same(x87recipMul(kPi, pr), (float)(1.f / (pr * pi)))) ++bad_div;
+			// the exact (slow) paths on every input, not only near rounding midpoints
+			if(!same(x87recipMulExact(kPi.hi, kPi.lo, pr), (float)(1.f / (pr * pi)))) ++bad_div;
+			if(!same(x87mulDivExact(kPi.hi, kPi.lo, a, b), (float)(a * pi / b))) ++bad_div;
+			if(x != 0.f && !same(x87mulExact(kDiv4ByPi.hi, kDiv4ByPi.lo, x), (float)(div_4_by_pi * x))) ++bad_mul;
+			if(x != 0.f && !same(x87mul2Exact(kDiv4BySquaredPi.hi, kDiv4BySquaredPi.lo, x, std::abs(x)), (float)(div_4_by_squared_pi * x * std::abs(x)))) ++bad_mul2;
+		}
 		if(!same(fsin(x), refSin(x))) ++bad_sin;
 		if(!same(fcos(x), refSin(x + static_cast<float>(div_pi_by_2)))) ++bad_cos;
 		const float s2 = s(rng);
