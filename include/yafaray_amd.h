@@ -42,6 +42,8 @@ typedef struct
 	uint32_t trace_block, stack_depth;
 	double shade_kernel_ms;     /* summed k_shade time (hipEvent pairs), 0 if not profiled */
 	double nee_kernel_ms;       /* summed k_nee time */
+	uint64_t photons;           /* photons stored in the diffuse photon map (photon mapping) */
+	double photon_seconds;      /* photon shooting + kd-tree build + upload */
 } yafaray_amd_stats_t;
 
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */

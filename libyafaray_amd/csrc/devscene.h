@@ -25,7 +25,7 @@ enum : uint32_t
 
 enum : uint32_t { MAT_SHINYDIFFUSE = 0, MAT_LIGHT = 1 };
 enum : uint32_t { LIGHT_POINT = 0, LIGHT_AREA = 1 };
-enum : int { INT_DIRECT = 0, INT_PATH = 1 };
+enum : int { INT_DIRECT = 0, INT_PATH = 1, INT_PHOTON = 2 };
 
 struct DevMaterial
 {
@@ -47,10 +47,11 @@ struct DevLight
 	float pos[4];           // point position / area corner
 	float to_x[4], to_y[4], fnormal[4];
 	float c2[4], c3[4], c4[4];
+	float du[4], dv[4];     // area: emission frame (light_area.cc:47-51), photon emission
 	float area;
 	uint32_t nee_base;      // first NEE entry of this light in the estimateAllDirectLight layout
 	uint32_t nee_count;     // point: 1, area: 2 * samples
-	uint32_t pad;
+	uint32_t shoot;         // bit 0: diffuse photons, bit 1: caustic photons
 };
 
 struct DevCamera
@@ -95,6 +96,21 @@ struct DevScene
 	int nee_all_count;             // entries of the estimateAllDirectLight layout
 	int faure_bytes;               // size of the permutation table (padded to 16 B)
 	int small_tables;              // materials + per-primitive normals fit k_shade / k_nee LDS
+
+	// photon mapping (integrator_photon_mapping.cc): diffuse photon map + point kd-tree
+	const float4 *ph_pos;          // (position, colour.r) per photon, kd-tree order of the map
+	const float4 *ph_dir;          // (direction, colour.g)
+	const float *ph_colb;          // colour.b
+	const uint2 *pk_nodes;         // point kd-tree (pkdtree.h:41-64): (split bits | photon, flags)
+	int n_photons, pm_paths, pm_search, pm_stack;
+	float pm_radius2;              // "diffuseRadius", used as the squared gather radius (:954)
+	// light selection for photon emission (sample_pdf1d.h: Pdf1D over the total energy of the
+	// lights that shoot diffuse photons, render_view.cc:103-110)
+	const int *ph_lights;          // photon light k -> index into lights
+	const float *light_cdf;
+	const float *light_func;
+	float light_inv_integral;
+	int n_ph_lights;
 };
 
 struct DevFilm
@@ -153,6 +169,20 @@ struct DevNeeQueue
 // per wave, no global atomics, no workgroup barriers), then publishes the count with a plain store.
 // An entry yields at most one next entry (and at most nee_k shadow rays), so a segment never
 // outgrows the camera's share.  k_trace runs n_seg * m workgroups, m per segment.
+// Photon paths in flight while the photon map is shot (render.cc / k_photon_*).
+struct PhotonState
+{
+	float4 *ray_o;       // origin, tmin
+	float4 *ray_d;       // direction
+	float4 *pcol;        // photon colour, .w = flags (bit 0 caustic, bit 1 direct)
+	uint32_t *alive[2];  // photon ids of the current / next bounce
+	uint32_t *n_alive;   // [2]
+	float4 *dep_a;       // deposit slots: (position, colour.r)
+	float4 *dep_b;       // (direction, colour.g)
+	float *dep_c;        // colour.b
+	uint8_t *dep_flag;   // 1 = a photon was stored in this slot
+};
+
 struct DevCounters
 {
 	uint32_t *n_active;   // [n_seg] active-list entries (closest rays + paths) per segment

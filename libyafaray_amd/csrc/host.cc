@@ -255,6 +255,10 @@ bool Scene::createLight(const std::string &name, const ParamMap &p)
 	p.get("cast_shadows", cast);
 	p.get("photon_only", photon_only);
 	L.cast_shadows = cast ? 1 : 0;
+	bool shoot_d = true, shoot_c = true;   // light_area.cc:179-200, light_point.cc:111-128
+	p.get("with_diffuse", shoot_d);
+	p.get("with_caustic", shoot_c);
+	L.shoot = (shoot_d ? 1u : 0u) | (shoot_c ? 2u : 0u);
 	if(type == "pointlight")
 	{
 		float from[3] = {0.f, 0.f, 0.f};
@@ -290,6 +294,19 @@ bool Scene::createLight(const std::string &name, const ParamMap &p)
 		put(L.c2, c2);
 		put(L.c3, c3);
 		put(L.c4, c4);
+		// light_area.cc:47-51: normal = -fnormal, du = normalize(to_x), dv = normal ^ du
+		const F3 nrml = {-fn.x, -fn.y, -fn.z};
+		F3 du = tx;
+		{
+			float len = du.x * du.x + du.y * du.y + du.z * du.z;
+			if(len != 0.f)
+			{
+				len = 1.f / std::sqrt(len);
+				du = {du.x * len, du.y * len, du.z * len};
+			}
+		}
+		put(L.du, du);
+		put(L.dv, crs(nrml, du));
 		// integrator_montecarlo.cc:396: ceilf(nSamples * aa_light_sample_multiplier(1))
 		L.samples = (int)std::ceil((float)samples * 1.f);
 		if(L.samples < 1) L.samples = 1;
@@ -347,10 +364,25 @@ bool Scene::createIntegrator(const std::string &name, const ParamMap &p)
 {
 	std::string type;
 	p.get("type", type);
-	if(type != "directlighting" && type != "pathtracing")
+	if(type != "directlighting" && type != "pathtracing" && type != "photonmapping")
 	{
-		log.error("Scene: integrator type '" + type + "' is not supported by the GPU core (directlighting, pathtracing)");
+		log.error("Scene: integrator type '" + type + "' is not supported by the GPU core (directlighting, pathtracing, photonmapping)");
 		return false;
+	}
+	if(type == "photonmapping")
+	{
+		// integrator_photon_mapping.cc:765-850.  The GPU core serves the diffuse photon map with the
+		// k-NN density estimate (finalGather = false); final gathering, map display, ambient
+		// occlusion and photon-map files are not part of it yet.
+		bool fg = true, show_map = false, ao = false;
+		std::string processing = "generate";
+		p.get("finalGather", fg);
+		p.get("show_map", show_map);
+		p.get("do_AO", ao);
+		p.get("photon_maps_processing", processing);
+		if(fg) { log.error("PhotonIntegrator: finalGather = true is not supported by the GPU core yet (set finalGather false)"); return false; }
+		if(show_map || ao) { log.error("PhotonIntegrator: show_map / do_AO are not supported by the GPU core yet"); return false; }
+		if(processing != "generate") { log.error("PhotonIntegrator: photon_maps_processing '" + processing + "' is not supported (generate only)"); return false; }
 	}
 	integrators[name] = p;
 	return true;
@@ -378,6 +410,7 @@ bool Scene::setupRender(const ParamMap &p)
 	p.get("AA_minsamples", s.aa_samples);
 	p.get("AA_clamp_samples", s.clamp_samples);
 	p.get("threads", s.threads);
+	p.get("threads_photons", s.threads_photons);
 	p.get("adv_auto_shadow_bias_enabled", s.shadow_bias_auto);
 	p.get("adv_shadow_bias_value", s.shadow_bias);
 	p.get("adv_auto_min_raydist_enabled", s.ray_min_dist_auto);
@@ -503,7 +536,27 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		S.cam.resx = c.resx;
 		S.cam.resy = c.resy;
 		// integrator + render parameters
-		S.integrator = (itype == "pathtracing") ? INT_PATH : INT_DIRECT;
+		S.integrator = (itype == "pathtracing") ? INT_PATH : (itype == "photonmapping") ? INT_PHOTON : INT_DIRECT;
+		if(S.integrator == INT_PHOTON)
+		{
+			// integrator_photon_mapping.cc:765-850 defaults
+			int photons = 100000, cphotons = 500000, search = 50, pbounces = 5;
+			float ds_rad = 0.1f;
+			bool caustics = true, diffuse = true;
+			ip.get("photons", photons);
+			ip.get("cPhotons", cphotons);
+			ip.get("search", search);
+			ip.get("diffuseRadius", ds_rad);
+			ip.get("bounces", pbounces);
+			ip.get("caustics", caustics);
+			ip.get("diffuse", diffuse);
+			rp.pm.photons = diffuse ? std::max(0, photons) : 0;
+			rp.pm.caustic_photons = caustics ? std::max(0, cphotons) : 0;
+			rp.pm.search = std::max(1, search);
+			rp.pm.radius2 = ds_rad;
+			rp.pm.bounces = std::max(0, pbounces);
+			rp.pm.threads = s.threads_photons;
+		}
 		S.width = s.width;
 		S.height = s.height;
 		S.spp = s.aa_samples;
@@ -531,7 +584,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			if(caus || ao) log.warning("DirectLight: caustic photons / ambient occlusion are not supported by the GPU core yet; ignored");
 		}
 		S.bounces = bounces;
-		S.path_samples = std::max(1, path_samples);
+		S.path_samples = (S.integrator == INT_PATH) ? std::max(1, path_samples) : 1;
 		S.rr_min_bounces = rr_min;
 		bool bg_transp = false;
 		ip.get("bg_transp", bg_transp);

@@ -125,7 +125,7 @@ struct RenderSetup
 	std::string filter = "box";
 	int tile_size = 32;
 	std::string tiles_order = "centre";
-	int threads = -1;
+	int threads = -1, threads_photons = -1;
 	bool shadow_bias_auto = true, ray_min_dist_auto = true;
 	float shadow_bias = 0.0005f, ray_min_dist = 0.00005f;
 	int base_sampling_offset = 0, computer_node = 0;

@@ -28,6 +28,7 @@
 
 #include <hip/hip_runtime.h>
 #include "devmath.h"
+#include "photonheap.h"
 #include "devscene.h"
 
 namespace yafamd
@@ -899,6 +900,8 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 	if(threadIdx.x < 2) s_count[threadIdx.x] = 0;
 	__syncthreads();
 	const bool is_path = S.integrator == INT_PATH;
+	const bool is_photon = S.integrator == INT_PHOTON;
+	const bool keep_v0 = S.path_samples > 1 || is_photon;   // first-hit data carried to the end
 	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
 	const int K = S.nee_k;
 	const uint32_t stride = blockDim.x;
@@ -927,7 +930,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			pwo4 = Pc.pwo[i];
 			pthr4 = Pc.pend_thr[i];
 			if(flags & F_PEND_EMIT) pem4 = Pc.pend_emit[i];
-			if(n_paths > 1) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
+			if(keep_v0) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
 		}
 		C3 thr = rgb(thr4), col = rgb(col4), pcol = rgb(pcol4);
 		const float alpha = col4.w;
@@ -995,8 +998,16 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 				{
 					const DevMaterial &m = S.mats[sp.mat];
 					col = c3(0.f);
+					// photon_mapping.cc:868-869 adds emit(wo) unconditionally and :938-946 adds it again
+					// for emitting materials; the other integrators add it once (direct_light.cc:120)
+					if(is_photon) col = col + matEmit(m, sp, wo);
 					if(sp.flags & B_EMIT) col = col + matEmit(m, sp, wo);
 					if(sp.flags & B_DIFFUSE) { nee_v0 = true; flags |= F_V0_DIFFUSE; }
+					if(is_photon)
+					{
+						v0p4 = f4(sp.p, __int_as_float(hit_prim));
+						v0wo4 = f4(wo, 0.f);
+					}
 					if(is_path && (sp.flags & B_DIFFUSE))
 					{
 						v0p4 = f4(sp.p, __int_as_float(hit_prim));
@@ -1145,7 +1156,9 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			want_ray = true;
 			stage = ST_FIRST | (subpath << 8);
 		}
-		if(live && finalize)
+		// photon mapping: a diffuse camera hit still owes the photon density estimate (k_gather)
+		const bool want_gather = live && finalize && is_photon && (flags & F_V0_DIFFUSE) && S.n_photons > 0;
+		if(live && finalize && !want_gather)
 		{
 			// path_tracer.cc:274-278 / direct_light.cc:129-131
 			if(is_path && (flags & F_V0_DIFFUSE)) col = col + pcol / (float)n_paths;
@@ -1184,18 +1197,28 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			Pn.pwo[k] = f4(pwo, 0.f);
 			if(nee_one) Pn.pend_thr[k] = f4(pend_thr, 0.f);
 			if(flags & F_PEND_EMIT) Pn.pend_emit[k] = f4(emit_pend, 0.f);
-			if(n_paths > 1) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }
+			if(keep_v0) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }
 		}
 
 		PHASE(4);
 		// ---- 5. next-event estimation request (served by k_nee; wants -> keep, so k is valid) ----
-		const uint32_t jn = waveAppend(want_nee, &s_count[1]);
+		// (photon mapping: the gather requests of the last iteration use the same queue — a path
+		// never asks for NEE and a gather in the same iteration, and the DL-style pipeline of the
+		// photon integrator serves NEE in iteration 0 and gathers in iteration 1)
+		const uint32_t jn = waveAppend(want_nee || want_gather, &s_count[1]);
 		if(want_nee)
 		{
 			const uint32_t j = a0 + jn;
 			A.N.p_prim[j] = f4(sp.p, __int_as_float(hit_prim));
 			A.N.wo_k[j] = f4(wo, __uint_as_float(k));
 			A.N.pix_mode[j] = make_uint4(offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8), 0u);
+		}
+		else if(want_gather)
+		{
+			const uint32_t j = a0 + jn;
+			A.N.p_prim[j] = v0p4;
+			A.N.wo_k[j] = f4(xyz(v0wo4), __uint_as_float(sid));
+			A.N.pix_mode[j] = make_uint4(__float_as_uint(col.r), __float_as_uint(col.g), __float_as_uint(col.b), __float_as_uint(alpha));
 		}
 		PHASE(5);
 	}
@@ -1421,6 +1444,405 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_rays(DevScene S, const fl
 	}
 }
 
+// =============================================================================================
+// Photon mapping (integrator_photon_mapping.cc, BASELINE C5)
+// =============================================================================================
+// Photon paths are shot as a wavefront of their own: k_photon_emit starts every photon id h
+// (integrator_photon_mapping.cc:127-156), then one k_photon_bounce launch per bounce traces the
+// rays, deposits on diffuse hits and scatters (:162-219).  Deposits land in slot
+// h * (bounces + 1) + bounce, so a stable compaction of the slots yields the photon map in
+// exactly the order one reference thread would append it (photon id, then bounce).
+
+// sample.h:58-75 (uniform sphere; the angle is a long double product)
+__device__ __forceinline__ V3 sphereDir(float s_1, float s_2)
+{
+	V3 dir;
+	dir.z = 1.0f - 2.0f * s_1;
+	float r = 1.0f - dir.z * dir.z;
+	if(r > 0.0f)
+	{
+		r = sqrtf(r);
+		const float a = x87mul(kMultPiBy2, s_2);
+		dir.x = fcos(a) * r;
+		dir.y = fsin(a) * r;
+	}
+	else
+	{
+		dir.x = 0.0f;
+		dir.y = 0.0f;
+	}
+	return dir;
+}
+
+
+struct PhotonArgs
+{
+	DevScene S;
+	PhotonState P;
+	uint32_t n_photons;  // photon paths (rounded like the reference, :437)
+	int max_bounces;
+	int bounce;          // k_photon_bounce: the bounce this launch traces
+	int cur;             // alive list read by this launch
+	int stack_depth;
+};
+
+// :127-156 — photon id h: light pick by Pdf1D::dSample over the lights' energies, emitPhoton
+__global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
+{
+	const DevScene &S = A.S;
+	const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+	bool ok = h < A.n_photons;
+	V3 o = v3(0.f, 0.f, 0.f), d = o;
+	C3 pcol = c3(0.f);
+	if(ok)
+	{
+		const float s_1 = riVdC(h);
+		const float s_2 = ldsDim(S, 2, h);
+		const float s_3 = ldsDim(S, 3, h);
+		const float s_4 = ldsDim(S, 4, h);
+		const float s_l = float(h) * (1.f / static_cast<float>(A.n_photons));
+		// sample_pdf1d.h:77-93 dSample (lower_bound over the cdf)
+		const int nl = S.n_ph_lights;
+		int light_num;
+		if(s_l <= 0.f) light_num = 0;
+		else if(s_l >= 1.f) light_num = nl - 1;
+		else
+		{
+			light_num = 0;
+			while(light_num < nl && S.light_cdf[light_num] < s_l) ++light_num;
+			if(light_num >= nl) light_num = nl - 1;
+		}
+		const float light_num_pdf = S.light_func[light_num] * S.light_inv_integral;
+		const DevLight &L = S.lights[S.ph_lights[light_num]];
+		float light_pdf;
+		// light_area.cc:98-104, light_point.cc:79-85
+		if(L.type == LIGHT_POINT)
+		{
+			o = lv(L.pos);
+			d = sphereDir(s_1, s_2);
+			light_pdf = x87mul(kPi, 4.0f);
+		}
+		else
+		{
+			light_pdf = L.area;
+			o = lv(L.pos) + s_3 * lv(L.to_x) + s_4 * lv(L.to_y);
+			d = cosHemisphere(-lv(L.fnormal), lv(L.du), lv(L.dv), s_1, s_2);
+		}
+		const float f_num_lights = static_cast<float>(nl);
+		pcol = C3{L.color[0], L.color[1], L.color[2]} * (f_num_lights * light_pdf / light_num_pdf);
+		ok = !isBlack(pcol);
+	}
+	const uint32_t j = waveAppend(ok, &A.P.n_alive[A.cur]);
+	if(ok)
+	{
+		A.P.alive[A.cur][j] = h;
+		A.P.ray_o[h] = f4(o, S.ray_min_dist);
+		A.P.ray_d[h] = f4(d, -1.f);
+		A.P.pcol[h] = f4(pcol, __uint_as_float(2u));   // caustic = false, direct = true
+	}
+}
+
+// :162-219 — one bounce of every live photon path: intersect, deposit, scatter (material.cc:137-153)
+template<bool LDS_SCENE>
+__global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
+{
+	const DevScene &S = A.S;
+	extern __shared__ float4 smem[];
+	TraceCtx C;
+	C.stack = reinterpret_cast<int *>(smem);
+	if(LDS_SCENE)
+	{
+		float4 *lds_nodes = smem + (A.stack_depth * kTraceBlock) / 4;
+		float4 *lds_tris = lds_nodes + 4 * S.n_nodes;
+		for(int k = threadIdx.x; k < 4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = S.nodes[k];
+		for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = S.tris[k];
+		__syncthreads();
+		C.nodes = lds_nodes;
+		C.tris = lds_tris;
+	}
+	else
+	{
+		C.nodes = S.nodes;
+		C.tris = S.tris;
+	}
+	const uint32_t n = A.P.n_alive[A.cur];
+	const int nxt = A.cur ^ 1;
+	const uint32_t slots = (uint32_t)A.max_bounces + 1u;
+	uint32_t visits = 0, tests = 0;
+	for(uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x)
+	{
+		const uint32_t j = base + threadIdx.x;
+		bool cont = false;
+		uint32_t h = 0;
+		V3 new_o = v3(0.f, 0.f, 0.f), new_d = new_o;
+		C3 new_col = c3(0.f);
+		uint32_t new_flags = 0;
+		if(j < n)
+		{
+			h = A.P.alive[A.cur][j];
+			const float4 ro = A.P.ray_o[h], rd = A.P.ray_d[h], pc = A.P.pcol[h];
+			float t;
+			int prim;
+			if(traverse<false>(C, xyz(ro), xyz(rd), ro.w, __builtin_huge_valf(), t, prim, visits, tests))
+			{
+				const Surf sp = makeSurf(S, xyz(ro), xyz(rd), t, prim);
+				const V3 wi = -xyz(rd);
+				const C3 lcol = rgb(pc);
+				uint32_t flags = __float_as_uint(pc.w);
+				const bool caustic = flags & 1u, direct = flags & 2u;
+				if((sp.flags & B_DIFFUSE) && !caustic)
+				{
+					const uint32_t slot = h * slots + (uint32_t)A.bounce;
+					A.P.dep_a[slot] = f4(sp.p, lcol.r);
+					A.P.dep_b[slot] = f4(wi, lcol.g);
+					A.P.dep_c[slot] = lcol.b;
+					A.P.dep_flag[slot] = 1;
+				}
+				if(A.bounce < A.max_bounces)
+				{
+					const int d_5 = 3 * A.bounce + 5;
+					BsdfSample s;
+					s.s_1 = ldsDim(S, d_5, h);
+					s.s_2 = ldsDim(S, d_5 + 1, h);
+					const float s_3 = ldsDim(S, d_5 + 2, h);
+					s.flags = B_ALL;
+					s.pdf = 0.f;
+					s.sampled = B_NONE;
+					float w = 0.f;
+					V3 wo = v3(0.f, 0.f, 0.f);
+					const C3 scol = matSample(S.mats[sp.mat], sp, wi, wo, s, w);
+					if(s.pdf > 1.0e-6f)
+					{
+						const C3 cnew = lcol * c3(1.f) * scol * w;
+						const float new_max = fmaxf(cnew.r, fmaxf(cnew.g, cnew.b));
+						const float old_max = fmaxf(lcol.r, fmaxf(lcol.g, lcol.b));
+						const float prob = fminf(1.f, new_max / old_max);
+						if(s_3 <= prob && prob > 1e-4f)
+						{
+							new_col = cnew / prob;
+							const uint32_t sf = s.sampled;
+							const bool nc = ((sf & (B_GLOSSY | B_SPECULAR | B_DISPERSIVE)) && direct) ||
+							                ((sf & (B_GLOSSY | B_SPECULAR | B_FILTER | B_DISPERSIVE)) && caustic);
+							const bool nd = (sf & B_FILTER) && direct;
+							new_flags = (nc ? 1u : 0u) | (nd ? 2u : 0u);
+							new_o = sp.p;
+							new_d = wo;
+							cont = true;
+						}
+					}
+				}
+			}
+		}
+		const uint32_t k = waveAppend(cont, &A.P.n_alive[nxt]);
+		if(cont)
+		{
+			A.P.alive[nxt][k] = h;
+			A.P.ray_o[h] = f4(new_o, S.ray_min_dist);
+			A.P.ray_d[h] = f4(new_d, -1.f);
+			A.P.pcol[h] = f4(new_col, __uint_as_float(new_flags));
+		}
+	}
+}
+
+// Stable compaction of the deposit slots (photon-id order): per-1024-slot counts, an exclusive
+// scan of the counts in one workgroup, then each workgroup writes its photons in slot order.
+__global__ void __launch_bounds__(256) k_photon_count(const uint8_t *flag, uint32_t n_slots, uint32_t *counts)
+{
+	const uint32_t b0 = blockIdx.x * 1024u;
+	uint32_t c = 0;
+	for(uint32_t k = threadIdx.x; k < 1024u; k += 256u)
+		if(b0 + k < n_slots) c += flag[b0 + k];
+	for(int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
+	__shared__ uint32_t red[4];
+	if(laneId() == 0) red[threadIdx.x >> 6] = c;
+	__syncthreads();
+	if(threadIdx.x == 0) counts[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(1024) k_photon_scan(uint32_t *counts, uint32_t n, uint32_t *total)
+{
+	// exclusive scan of n counts by one workgroup: each thread scans a contiguous run
+	__shared__ uint32_t part[1024];
+	const uint32_t per = (n + 1023u) / 1024u;
+	const uint32_t a = threadIdx.x * per, b = min(n, a + per);
+	uint32_t sum = 0;
+	for(uint32_t k = a; k < b; ++k) sum += counts[k];
+	part[threadIdx.x] = sum;
+	__syncthreads();
+	if(threadIdx.x == 0)
+	{
+		uint32_t run = 0;
+		for(int k = 0; k < 1024; ++k) { const uint32_t v = part[k]; part[k] = run; run += v; }
+		*total = run;
+	}
+	__syncthreads();
+	uint32_t run = part[threadIdx.x];
+	for(uint32_t k = a; k < b; ++k) { const uint32_t v = counts[k]; counts[k] = run; run += v; }
+}
+
+__global__ void __launch_bounds__(1024) k_photon_scatter(PhotonState P, uint32_t n_slots, const uint32_t *offsets,
+                                                         float4 *pos, float4 *dir, float *colb)
+{
+	__shared__ uint32_t wsum[16];
+	const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+	const bool f = k < n_slots && P.dep_flag[k];
+	const uint64_t m = __ballot(f);
+	const int wid = threadIdx.x >> 6;
+	if(laneId() == 0) wsum[wid] = (uint32_t)__popcll(m);
+	__syncthreads();
+	uint32_t base = offsets[blockIdx.x];
+	for(int w = 0; w < wid; ++w) base += wsum[w];
+	if(f)
+	{
+		const uint32_t o = base + (uint32_t)__popcll(m & ((1ull << laneId()) - 1ull));
+		pos[o] = P.dep_a[k];
+		dir[o] = P.dep_b[k];
+		colb[o] = P.dep_c[k];
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_gather: the photon density estimate of PhotonIntegrator::integrate (:953-976) for every
+// diffuse camera hit, after its direct light has been connected: k-NN lookup in the point
+// kd-tree (pkdtree.h:225-292) with PhotonGather's heap (photon.cc:31-52, photonheap.h), then the
+// contributions are added to the sample's colour in heap-array order and the sample is written.
+// ---------------------------------------------------------------------------------------------
+constexpr int kGatherBlock = 64;
+
+struct GatherArgs
+{
+	DevScene S;
+	DevNeeQueue N;           // gather requests: (p, prim), (wo, sample id), (colour, alpha) bits
+	DevCounters cnt_next;    // n_nee = requests per segment
+	float4 *samples;
+	const DevJob *jobs;
+	int n_jobs;
+	uint64_t chunk_base;
+};
+
+template<bool SMALL>
+__global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
+{
+	extern __shared__ uint4 shade_smem[];
+	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
+	// per-lane heap and lookup stack, lane-interleaved after the staged tables
+	uint32_t *lds_words = reinterpret_cast<uint32_t *>(shade_smem) + shadeLdsBytes(A.S, SMALL) / 4;
+	const int k = S.pm_search;
+	const int lane = threadIdx.x;
+	HeapRef heap;
+	heap.idx = lds_words + lane;
+	heap.dist = reinterpret_cast<float *>(lds_words + (size_t)k * kGatherBlock) + lane;
+	heap.stride = kGatherBlock;
+	uint32_t *st_node = lds_words + (size_t)2 * k * kGatherBlock + lane;
+	float *st_s = reinterpret_cast<float *>(st_node + (size_t)S.pm_stack * kGatherBlock);
+	const uint32_t seg = blockIdx.x;
+	const uint32_t n_req = A.cnt_next.n_nee[seg];
+	const uint32_t a0 = seg * S.cap_a;
+	for(uint32_t base_j = 0; base_j < n_req; base_j += blockDim.x)
+	{
+		if(base_j + threadIdx.x >= n_req) continue;
+		const uint32_t j = a0 + base_j + threadIdx.x;
+		const float4 pp = A.N.p_prim[j], wk = A.N.wo_k[j];
+		const uint4 cb = A.N.pix_mode[j];
+		const V3 p = xyz(pp);
+		const Surf sp = surfFromPrim(S, p, __float_as_int(pp.w));
+		const V3 wo = xyz(wk);
+		const uint32_t sid = __float_as_uint(wk.w);
+		C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)};
+		const float alpha = __uint_as_float(cb.w);
+		// ---- k-NN lookup (pkdtree.h:225-292, NON_REC_LOOKUP) ----
+		float max_d2 = S.pm_radius2;
+		int found = 0;
+		uint32_t curr = 0;
+		int sp_top = 0;   // entries above the reference's "nowhere" sentinel
+		for(;;)
+		{
+			uint2 nd = S.pk_nodes[curr];
+			while((nd.y & 3u) != 3u)
+			{
+				const int axis = (int)(nd.y & 3u);
+				const float split_val = __uint_as_float(nd.x);
+				const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+				uint32_t far_child;
+				if(pa <= split_val) { far_child = nd.y >> 2; curr = curr + 1; }
+				else { far_child = curr + 1; curr = nd.y >> 2; }
+				st_node[sp_top * kGatherBlock] = far_child | ((uint32_t)axis << 30);
+				st_s[sp_top * kGatherBlock] = split_val;
+				++sp_top;
+				nd = S.pk_nodes[curr];
+			}
+			const uint32_t ph = nd.x;
+			const float4 q = S.ph_pos[ph];
+			const V3 v = xyz(q) - p;
+			float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
+			if(dist_2 < max_d2)
+			{
+				// photon.cc:31-52
+				if(found < k)
+				{
+					heap.i(found) = ph;
+					heap.d(found) = dist_2;
+					++found;
+					if(found == k)
+					{
+						heapMake(heap, k);
+						max_d2 = heap.d(0);
+					}
+				}
+				else
+				{
+					heapReplaceTop(heap, k, ph, dist_2);
+					max_d2 = heap.d(0);
+				}
+			}
+			if(sp_top == 0) break;
+			uint32_t top = st_node[(sp_top - 1) * kGatherBlock];
+			int axis = (int)(top >> 30);
+			float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+			dist_2 = pa - st_s[(sp_top - 1) * kGatherBlock];
+			dist_2 *= dist_2;
+			bool done = false;
+			while(dist_2 > max_d2)
+			{
+				--sp_top;
+				if(sp_top == 0) { done = true; break; }
+				top = st_node[(sp_top - 1) * kGatherBlock];
+				axis = (int)(top >> 30);
+				pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+				dist_2 = pa - st_s[(sp_top - 1) * kGatherBlock];
+				dist_2 *= dist_2;
+			}
+			if(done) break;
+			curr = top & 0x3fffffffu;
+			--sp_top;
+		}
+		// ---- density estimate (:959-976) ----
+		if(found > 0)
+		{
+			const float scale = x87recipMul(kPi, (float)S.pm_paths * max_d2);
+			const DevMaterial &m = S.mats[sp.mat];
+			for(int i = 0; i < found; ++i)
+			{
+				const uint32_t ph = heap.i(i);
+				const float4 a = S.ph_pos[ph], b = S.ph_dir[ph];
+				const C3 pc = C3{a.w, b.w, S.ph_colb[ph]};
+				const C3 surf_col = matEval(m, sp, wo, xyz(b), B_DIFFUSE);
+				const C3 col_tmp = surf_col * scale * pc;
+				col = col + col_tmp;
+			}
+		}
+		col = col + c3(0.f);   // caustic map empty for the supported materials (montecarlo.cc:644)
+		col = col + c3(0.f);   // recursiveRaytrace: no specular/glossy components
+		const SampleCoord sc = sampleCoord(A.jobs, A.n_jobs, S.width, S.tile, S.spp, A.chunk_base + (uint64_t)sid);
+		A.samples[((size_t)sc.y * S.width + sc.x) * S.spp + sc.s] = f4(col, alpha > 1.f ? 1.f : alpha);
+	}
+}
+
+__host__ __device__ inline size_t gatherLdsBytes(const DevScene &S, bool small)
+{
+	return shadeLdsBytes(S, small) + (size_t)kGatherBlock * (8u * (size_t)S.pm_search + 8u * (size_t)S.pm_stack);
+}
+
 } // namespace yafamd
 
 // ---------------------------------------------------------------------------------------------
@@ -1533,6 +1955,73 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	else hipLaunchKernelGGL(k_nee<false>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	return hipGetLastError();
 }
+
+hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, hipStream_t st)
+{
+	PhotonArgs A;
+	A.S = *S;
+	A.P = *P;
+	A.n_photons = n_photons;
+	A.max_bounces = max_bounces;
+	A.bounce = 0;
+	A.cur = 0;
+	A.stack_depth = 0;
+	if(n_photons == 0) return hipSuccess;
+	hipLaunchKernelGGL(k_photon_emit, dim3((n_photons + 255) / 256), dim3(256), 0, st, A);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, int bounce,
+                                int cur, int stack_depth, int grid, hipStream_t st)
+{
+	PhotonArgs A;
+	A.S = *S;
+	A.P = *P;
+	A.n_photons = n_photons;
+	A.max_bounces = max_bounces;
+	A.bounce = bounce;
+	A.cur = cur;
+	A.stack_depth = stack_depth;
+	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
+	if(S->scene_in_lds)
+	{
+		const size_t bytes = stack_bytes + (size_t)(4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
+		hipLaunchKernelGGL(k_photon_bounce<true>, dim3(grid), dim3(kTraceBlock), bytes, st, A);
+	}
+	else hipLaunchKernelGGL(k_photon_bounce<false>, dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
+	return hipGetLastError();
+}
+
+// Stable compaction of the deposit slots into the photon map; *total_dev receives the count.
+hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev,
+                                 float4 *pos, float4 *dir, float *colb, hipStream_t st)
+{
+	const uint32_t nb = (n_slots + 1023u) / 1024u;
+	if(nb == 0) return hipSuccess;
+	hipLaunchKernelGGL(k_photon_count, dim3(nb), dim3(256), 0, st, P->dep_flag, n_slots, scratch_counts);
+	hipLaunchKernelGGL(k_photon_scan, dim3(1), dim3(1024), 0, st, scratch_counts, nb, total_dev);
+	hipLaunchKernelGGL(k_photon_scatter, dim3(nb), dim3(1024), 0, st, *P, n_slots, (const uint32_t *)scratch_counts, pos, dir, colb);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const DevCounters *cnt_next, float4 *samples,
+                                const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st)
+{
+	GatherArgs A;
+	A.S = *S;
+	A.N = *N;
+	A.cnt_next = *cnt_next;
+	A.samples = samples;
+	A.jobs = jobs;
+	A.n_jobs = n_jobs;
+	A.chunk_base = chunk_base;
+	const size_t lds = gatherLdsBytes(*S, S->small_tables != 0);
+	if(S->small_tables) hipLaunchKernelGGL(k_gather<true>, dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
+	else hipLaunchKernelGGL(k_gather<false>, dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
+	return hipGetLastError();
+}
+
+size_t yafamd_gather_lds_bytes(const DevScene *S) { return gatherLdsBytes(*S, S->small_tables != 0); }
 
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
                               float clamp_samples, hipStream_t st)

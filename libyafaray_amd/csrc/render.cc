@@ -9,6 +9,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <future>
+#include <mutex>
 #include <sstream>
 
 using namespace yafamd;
@@ -27,6 +29,14 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
                              const DevCounters *cnt_next, hipStream_t st);
 int yafamd_nee_blocks_per_cu();
+hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, hipStream_t st);
+hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, int bounce,
+                                int cur, int stack_depth, int grid, hipStream_t st);
+hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev,
+                                 float4 *pos, float4 *dir, float *colb, hipStream_t st);
+hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const DevCounters *cnt_next, float4 *samples,
+                                const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
+size_t yafamd_gather_lds_bytes(const DevScene *S);
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
                               float clamp_samples, hipStream_t st);
 hipError_t yafamd_launch_trace_rays(const DevScene *S, int any, const float4 *ro, const float4 *rd, int n, float *t_out,
@@ -79,6 +89,13 @@ struct GpuRenderer::Impl
 	bool ok = false, init_done = false;
 	hipStream_t stream = nullptr;
 	Buf nodes, tris, prim_ng, mats, lights, faure, faure_dim, faure_inv;
+	// photon mapping: light selection Pdf1D, photon paths in flight, the map and its kd-tree
+	Buf ph_lights, light_cdf, light_func;
+	float light_inv_integral = 0.f;
+	int n_ph_lights = 0;
+	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
+	Buf ph_pos, ph_dir, ph_colb, pk_nodes;
+	int n_photons = 0, pm_paths = 0, pm_stack = 0;
 	int n_nodes = 0, n_tris = 0, n_mats = 0, n_lights = 0, depth = 0, stack_depth = 32;
 	bool scene_in_lds = false;
 	int faure_bytes = 0;
@@ -99,6 +116,9 @@ struct GpuRenderer::Impl
 
 	~Impl()
 	{
+		for(Buf *b : {&ph_lights, &light_cdf, &light_func, &ph_ray_o, &ph_ray_d, &ph_pcol, &ph_alive0, &ph_alive1, &ph_n_alive,
+		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes})
+			b->release();
 		for(Buf *b : {&nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_dim, &faure_inv, &samples, &film,
 		              &weights, &jobs, &counters, &stats})
 			b->release();
@@ -187,6 +207,40 @@ bool GpuRenderer::upload(const HostScene &hs)
 	d.n_tris = (int)(hs.bvh.tris.size() / 12);
 	d.n_mats = (int)hs.mats.size();
 	d.n_lights = (int)hs.lights.size();
+	{
+		// sample_pdf1d.h:52-66 over the lights shooting diffuse photons (render_view.cc:103-110),
+		// energies = totalEnergy().energy() (light_area.cc:64, light_point.h:41, color.h:59)
+		std::vector<int> idx;
+		std::vector<float> func;
+		for(int i = 0; i < d.n_lights; ++i)
+		{
+			const DevLight &L = hs.lights[i];
+			if(!(L.shoot & 1u)) continue;
+			float e[3];
+			for(int k = 0; k < 3; ++k)
+				e[k] = (L.type == LIGHT_POINT) ? static_cast<float>(3.14159265358979323846264338327950288L) * (4.0f * L.color[k]) : L.area * L.color[k];
+			func.push_back((e[0] + e[1] + e[2]) * 0.333333f);
+			idx.push_back(i);
+		}
+		d.n_ph_lights = (int)idx.size();
+		if(!idx.empty())
+		{
+			std::vector<float> cdf(func.size());
+			const double delta = 1.0 / static_cast<double>(func.size());
+			double c = 0.0;
+			for(size_t i = 0; i < func.size(); ++i)
+			{
+				c += static_cast<double>(func[i]) * delta;
+				cdf[i] = static_cast<float>(c);
+			}
+			const float integral = static_cast<float>(c);
+			for(float &e : cdf) e /= integral;
+			d.light_inv_integral = 1.f / integral;
+			if(!allocCopy(log_, d.ph_lights, idx.data(), idx.size())) return false;
+			if(!allocCopy(log_, d.light_cdf, cdf.data(), cdf.size())) return false;
+			if(!allocCopy(log_, d.light_func, func.data(), func.size())) return false;
+		}
+	}
 	d.depth = hs.bvh.depth;
 	d.stack_depth = std::max(8, ((hs.bvh.depth + 2 + 7) / 8) * 8);
 	const size_t scene_bytes = (size_t)(4 * d.n_nodes + 3 * d.n_tris) * 16;
@@ -258,6 +312,162 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.n_mats = d.n_mats;
 	S.n_lights = d.n_lights;
 	S.scene_in_lds = d.scene_in_lds ? 1 : 0;
+	S.ph_lights = (const int *)d.ph_lights.p;
+	S.light_cdf = (const float *)d.light_cdf.p;
+	S.light_func = (const float *)d.light_func.p;
+	S.light_inv_integral = d.light_inv_integral;
+	S.n_ph_lights = d.n_ph_lights;
+}
+
+// Point kd-tree of the photon map (pkdtree.h:115-222): median split on the largest axis of the
+// node bound by std::nth_element with the reference's comparator (coordinate, ties by element
+// address = photon index).  Node indices follow the reference's depth-first layout: a subtree of
+// m photons holds 2m - 1 nodes, so the right child of node i with a left subtree of nl photons is
+// i + 2 nl — which lets the top levels build in parallel into disjoint ranges with the exact same
+// result as the sequential build.
+namespace
+{
+struct F3b { float v[3]; };
+
+struct PkBuild
+{
+	const float4 *pos;
+	uint32_t *el;
+	uint2 *nodes;
+	int max_depth = 0;
+	std::mutex mtx;
+	void build(uint32_t start, uint32_t end, F3b lo, F3b hi, uint32_t node, int level)
+	{
+		if(end - start == 1)
+		{
+			nodes[node] = make_uint2(el[start], 3u);
+			std::lock_guard<std::mutex> g(mtx);
+			max_depth = std::max(max_depth, level);
+			return;
+		}
+		const float dx = hi.v[0] - lo.v[0], dy = hi.v[1] - lo.v[1], dz = hi.v[2] - lo.v[2];
+		const int axis = (dx > dy) ? ((dx > dz) ? 0 : 2) : ((dy > dz) ? 1 : 2);
+		const uint32_t split_el = (start + end) / 2;
+		auto coord = [&](uint32_t a) { const float4 &q = pos[a]; return axis == 0 ? q.x : (axis == 1 ? q.y : q.z); };
+		std::nth_element(el + start, el + split_el, el + end, [&](uint32_t a, uint32_t b) {
+			const float pa = coord(a), pb = coord(b);
+			return pa == pb ? (a < b) : pa < pb;
+		});
+		const float split_pos = coord(el[split_el]);
+		const uint32_t nl = split_el - start;
+		const uint32_t right = node + 2 * nl;
+		uint32_t bits;
+		std::memcpy(&bits, &split_pos, 4);
+		nodes[node] = make_uint2(bits, (uint32_t)axis | (right << 2));
+		F3b hi_l = hi, lo_r = lo;
+		hi_l.v[axis] = split_pos;
+		lo_r.v[axis] = split_pos;
+		if(level < 4 && end - start > 65536)
+		{
+			auto f = std::async(std::launch::async, [&, start, split_el, lo, hi_l, node, level]() { build(start, split_el, lo, hi_l, node + 1, level + 1); });
+			build(split_el, end, lo_r, hi, right, level + 1);
+			f.get();
+		}
+		else
+		{
+			build(start, split_el, lo, hi_l, node + 1, level + 1);
+			build(split_el, end, lo_r, hi, right, level + 1);
+		}
+	}
+};
+} // namespace
+
+bool GpuRenderer::buildPhotonMap(RenderParams &rp)
+{
+	Impl &d = *d_;
+	DevScene &S = rp.scene;
+	const PhotonParams &pm = rp.pm;
+	S.n_photons = 0;
+	S.pm_paths = 0;
+	S.pm_search = pm.search;
+	S.pm_radius2 = pm.radius2;
+	S.pm_stack = 8;
+	if(pm.photons <= 0 || d.n_ph_lights == 0)
+	{
+		if(pm.photons > 0) log_.warning("PhotonIntegrator: no lights shoot diffuse photons; diffuse photon map disabled");
+		return true;
+	}
+	const auto t0 = std::chrono::steady_clock::now();
+	// integrator_photon_mapping.cc:437 (threads_photons <= 0 counts as one thread here)
+	const uint32_t T = (uint32_t)std::max(1, pm.threads);
+	const uint32_t N = std::max(T, ((uint32_t)pm.photons / T) * T);
+	const uint32_t slots = (uint32_t)pm.bounces + 1u;
+	const size_t n_slots = (size_t)N * slots;
+	if(n_slots > 0xffffffffull) { log_.error("PhotonIntegrator: photons x (bounces + 1) exceeds 2^32 deposit slots"); return false; }
+	if(!ensure(log_, d.ph_ray_o, (size_t)N * 16) || !ensure(log_, d.ph_ray_d, (size_t)N * 16) || !ensure(log_, d.ph_pcol, (size_t)N * 16) ||
+	   !ensure(log_, d.ph_alive0, (size_t)N * 4) || !ensure(log_, d.ph_alive1, (size_t)N * 4) || !ensure(log_, d.ph_n_alive, 16) ||
+	   !ensure(log_, d.dep_a, n_slots * 16) || !ensure(log_, d.dep_b, n_slots * 16) || !ensure(log_, d.dep_c, n_slots * 4) ||
+	   !ensure(log_, d.dep_flag, n_slots) || !ensure(log_, d.ph_scan, ((n_slots + 1023) / 1024) * 4 + 16) || !ensure(log_, d.ph_total, 16))
+		return false;
+	PhotonState P{};
+	P.ray_o = (float4 *)d.ph_ray_o.p;
+	P.ray_d = (float4 *)d.ph_ray_d.p;
+	P.pcol = (float4 *)d.ph_pcol.p;
+	P.alive[0] = (uint32_t *)d.ph_alive0.p;
+	P.alive[1] = (uint32_t *)d.ph_alive1.p;
+	P.n_alive = (uint32_t *)d.ph_n_alive.p;
+	P.dep_a = (float4 *)d.dep_a.p;
+	P.dep_b = (float4 *)d.dep_b.p;
+	P.dep_c = (float *)d.dep_c.p;
+	P.dep_flag = (uint8_t *)d.dep_flag.p;
+	HIPCHECK(hipMemsetAsync(d.dep_flag.p, 0, n_slots, d.stream));
+	HIPCHECK(hipMemsetAsync(d.ph_n_alive.p, 0, 16, d.stream));
+	HIPCHECK(yafamd_photon_emit(&S, &P, N, pm.bounces, d.stream));
+	int cur = 0;
+	for(int b = 0; b <= pm.bounces; ++b)
+	{
+		HIPCHECK(hipMemsetAsync((uint32_t *)d.ph_n_alive.p + (cur ^ 1), 0, 4, d.stream));
+		HIPCHECK(yafamd_photon_bounce(&S, &P, N, pm.bounces, b, cur, d.stack_depth, d.trace_grid, d.stream));
+		cur ^= 1;
+	}
+	// the photon map in photon-id order (one reference thread's append order); outputs sized for
+	// the worst case (every slot stored), the count comes back from the scan
+	uint32_t n = 0;
+	if(!ensure(log_, d.ph_pos, n_slots * 16) || !ensure(log_, d.ph_dir, n_slots * 16) || !ensure(log_, d.ph_colb, n_slots * 4)) return false;
+	HIPCHECK(yafamd_photon_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)d.ph_pos.p,
+	                               (float4 *)d.ph_dir.p, (float *)d.ph_colb.p, d.stream));
+	HIPCHECK(hipMemcpyAsync(&n, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	if(n < 50) { log_.error("PhotonIntegrator: Too few diffuse photons, stopping now."); return false; }   // :448-452
+	// point kd-tree on the host (exactly the reference's element order), then upload
+	std::vector<float4> hpos(n);
+	HIPCHECK(hipMemcpy(hpos.data(), d.ph_pos.p, (size_t)n * 16, hipMemcpyDeviceToHost));
+	std::vector<uint32_t> el(n);
+	for(uint32_t i = 0; i < n; ++i) el[i] = i;
+	F3b lo{{hpos[0].x, hpos[0].y, hpos[0].z}}, hi = lo;
+	for(uint32_t i = 1; i < n; ++i)
+	{
+		const float q[3] = {hpos[i].x, hpos[i].y, hpos[i].z};
+		for(int k = 0; k < 3; ++k) { lo.v[k] = std::min(lo.v[k], q[k]); hi.v[k] = std::max(hi.v[k], q[k]); }
+	}
+	std::vector<uint2> nodes(2 * (size_t)n - 1);
+	PkBuild pb;
+	pb.pos = hpos.data();
+	pb.el = el.data();
+	pb.nodes = nodes.data();
+	pb.build(0, n, lo, hi, 0, 0);
+	if(!allocCopy(log_, d.pk_nodes, nodes.data(), nodes.size())) return false;
+	d.n_photons = (int)n;
+	d.pm_paths = (int)N;
+	d.pm_stack = pb.max_depth + 1;
+	S.ph_pos = (const float4 *)d.ph_pos.p;
+	S.ph_dir = (const float4 *)d.ph_dir.p;
+	S.ph_colb = (const float *)d.ph_colb.p;
+	S.pk_nodes = (const uint2 *)d.pk_nodes.p;
+	S.n_photons = (int)n;
+	S.pm_paths = (int)N;
+	S.pm_stack = d.pm_stack;
+	stats_.photons = n;
+	stats_.photon_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+	std::ostringstream os;
+	os << "PhotonIntegrator: shot " << N << " photons, stored " << n << " (kd-tree depth " << pb.max_depth << ") in " << stats_.photon_seconds << " s";
+	log_.info(os.str());
+	return true;
 }
 
 bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
@@ -266,6 +476,19 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	Impl &d = *d_;
 	DevScene &S = rp.scene;
 	fillScenePointers(d, S);
+	stats_.photons = 0;
+	stats_.photon_seconds = 0.0;
+	if(S.integrator == INT_PHOTON)
+	{
+		// PhotonIntegrator::preprocess (integrator_photon_mapping.cc:242-638): the photon map is
+		// rebuilt for every render, as the reference's "generate" mode does
+		if(!buildPhotonMap(rp)) return false;
+		if(yafamd_gather_lds_bytes(&S) > 64 * 1024)
+		{
+			log_.error("PhotonIntegrator: search " + std::to_string(S.pm_search) + " needs more LDS than the gather kernel has");
+			return false;
+		}
+	}
 	const int W = S.width, H = S.height, spp = S.spp, ts = S.tile;
 	// ---- jobs: owned tile rows (+ halo rows for the film gather when sharded) ----
 	const int tile_rows = (H + ts - 1) / ts;
@@ -306,7 +529,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	// ---- chunk buffers ----
 	size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
 	const int K = std::max(1, S.nee_k);
-	const bool need_v0 = S.path_samples > 1;
+	const bool need_v0 = S.path_samples > 1 || S.integrator == INT_PHOTON;
 	// segment capacity: the camera deals groups of 256 samples round-robin over the segments
 	const size_t R = (size_t)d.shade_grid;
 	auto shardCap = [R](size_t m) { return (((m + 255) / 256 + R - 1) / R) * 256; };
@@ -420,7 +643,11 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 2], d.stream));
-			HIPCHECK(yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));
+			// photon mapping follows the direct-lighting pipeline: NEE requests in iteration 0, the
+			// photon density estimates of the connected camera hits in iteration 1
+			if(S.integrator == INT_PHOTON && it == 1)
+				HIPCHECK(yafamd_launch_gather(&S, &d.N, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
+			else HIPCHECK(yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 3], d.stream));
 			if(rp.profile) ev_i += 4;
 			cur ^= 1;

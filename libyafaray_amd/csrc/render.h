@@ -27,9 +27,20 @@ struct HostScene
 	int n_prims = 0;
 };
 
+struct PhotonParams
+{
+	int photons = 0;           // diffuse photons to shoot (0: no diffuse map)
+	int caustic_photons = 0;   // caustic photons (shot; stored only after specular bounces)
+	int search = 50;           // k of the k-NN gather
+	float radius2 = 0.1f;      // "diffuseRadius" (squared radius of the gather)
+	int bounces = 5;
+	int threads = -1;          // threads_photons: photon count rounded to a multiple (:437); <= 0 -> 1
+};
+
 struct RenderParams
 {
 	DevScene scene;                      // pointers filled by the renderer
+	PhotonParams pm;
 	DevFilm film;
 	int shard_rank = 0, shard_world = 1;
 	int chunk_slots = 1 << 25;   // samples in flight per wavefront chunk
@@ -47,6 +58,7 @@ class GpuRenderer
 		bool download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h);
 		bool filmToDevice(void *dst, int y0, int y1);
 		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
+		bool buildPhotonMap(RenderParams &rp);
 		const yafaray_amd_stats_t &stats() const { return stats_; }
 		std::vector<std::pair<int, int>> ownedRows() const { return owned_rows_; }
 

@@ -134,3 +134,17 @@ def test_reference_client_test01_renders(tmp_path):
     assert r.returncode == 0, out[-2000:]
     errors = [ln for ln in out.splitlines() if "ERROR" in ln]
     assert not errors, errors[:5]
+
+
+def test_photon_mapping_matches_oracle(product, oracle_built):
+    """BASELINE C5 pipeline at a small size: photon shooting (GPU wavefront), point kd-tree,
+    k-NN gather with the reference's heap order, PM integrate (emission twice, direct light,
+    density estimate) — per pixel <= 4 ULP of the oracle."""
+    spec = scenes.cornell_photon(64, 48, spp=2, photons=30000, search=50, radius=0.1)
+    rgba, w, st = product.render_spec(spec)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
+    opos, _, _, _, npaths = oracle_built.OracleScene(spec, threads=8).photon_map()
+    assert st["photons"] == len(opos)
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    d = ulp_diff(rgba, orgba)
+    assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
