@@ -34,14 +34,24 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--spp", type=int, default=None, help="default 64 (C2/C4), 1 (C5 photon)")
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--no-rr", action="store_true", help="Russian roulette off (bit-parity variant)")
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere"])
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere", "photon"])
+    ap.add_argument("--photons", type=int, default=10_000_000, help="C5: diffuse photons")
     ap.add_argument("--chunk", type=int, default=1 << 25)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
+
+
+def workload_name(a, W, H):
+    if a.scene == "photon":
+        return (f"C5 Cornell PhotonIntegrator, {a.photons} diffuse photons, k=50 gather r^2=0.1, finalGather off, "
+                f"{W}x{H}x{a.spp}spp (photon map rebuilt every step)")
+    return (f"C2 Cornell PathIntegrator depth {a.bounces}, {W}x{H}x{a.spp}spp"
+            + (", RR off" if a.no_rr else ", RR on (reference default)")
+            + ("" if a.scene == "cornell" else " + 1M-triangle sphere (C4)"))
 
 
 def traffic_config(a, W, H):
@@ -50,6 +60,8 @@ def traffic_config(a, W, H):
 
 def main():
     a = parse()
+    if a.spp is None:
+        a.spp = 1 if a.scene == "photon" else 64
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -67,6 +79,8 @@ def main():
     from libyafaray_amd import scenes
     if a.scene == "sphere":
         spec = scenes.cornell_sphere(width=a.width, height=a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
+    elif a.scene == "photon":
+        spec = scenes.cornell_photon(a.width, a.height, spp=a.spp, photons=a.photons)
     else:
         spec = scenes.cornell(a.width, a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
     # the reference's PathIntegrator default caustic_type is "path" (integrator_path_tracer.cc:43);
@@ -178,9 +192,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (Cornell box scene generated in-repo, SURVEY.md §8d)",
-            "config": {"workload": f"C2 Cornell PathIntegrator depth {a.bounces}, {W}x{H}x{a.spp}spp"
-                                   + (", RR off" if a.no_rr else ", RR on (reference default)")
-                                   + ("" if a.scene == "cornell" else " + 1M-triangle sphere (C4)"),
+            "config": {"workload": workload_name(a, W, H),
                        "width": W, "height": H, "spp": a.spp, "bounces": a.bounces,
                        "samples_per_step": W * H * a.spp, "parallelism": f"tile-rows x{world}",
                        "chunk_slots": a.chunk},
@@ -196,6 +208,9 @@ def main():
             "shade": {"avg_launch_ms": round(s["shade_kernel_ms"] / launches, 4),
                       "ms_per_step": round(s["shade_kernel_ms"], 2), "trace_ms_per_step": round(s["trace_kernel_ms"], 2),
                       "nee_ms_per_step": round(s["nee_kernel_ms"], 2)},
+            "photon_map": ({"photons_stored": s["photons"], "seconds_per_step": round(s["photon_seconds"], 4),
+                            "shoot_seconds": round(s["photon_shoot_seconds"], 4), "tree_seconds": round(s["photon_tree_seconds"], 4)}
+                           if a.scene == "photon" else None),
             "launch": {k: s[k] for k in ("trace_grid", "shade_grid", "trace_block", "stack_depth", "scene_in_lds")},
             "cpu_baseline": cpu,
         }

@@ -37,6 +37,7 @@ hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const DevCounters *cnt_next, float4 *samples,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
 size_t yafamd_gather_lds_bytes(const DevScene *S);
+hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint2 *nodes_dev, int *depth_out, hipStream_t st);
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
                               float clamp_samples, hipStream_t st);
 hipError_t yafamd_launch_trace_rays(const DevScene *S, int any, const float4 *ro, const float4 *rd, int n, float *t_out,
@@ -319,64 +320,6 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.n_ph_lights = d.n_ph_lights;
 }
 
-// Point kd-tree of the photon map (pkdtree.h:115-222): median split on the largest axis of the
-// node bound by std::nth_element with the reference's comparator (coordinate, ties by element
-// address = photon index).  Node indices follow the reference's depth-first layout: a subtree of
-// m photons holds 2m - 1 nodes, so the right child of node i with a left subtree of nl photons is
-// i + 2 nl — which lets the top levels build in parallel into disjoint ranges with the exact same
-// result as the sequential build.
-namespace
-{
-struct F3b { float v[3]; };
-
-struct PkBuild
-{
-	const float4 *pos;
-	uint32_t *el;
-	uint2 *nodes;
-	int max_depth = 0;
-	std::mutex mtx;
-	void build(uint32_t start, uint32_t end, F3b lo, F3b hi, uint32_t node, int level)
-	{
-		if(end - start == 1)
-		{
-			nodes[node] = make_uint2(el[start], 3u);
-			std::lock_guard<std::mutex> g(mtx);
-			max_depth = std::max(max_depth, level);
-			return;
-		}
-		const float dx = hi.v[0] - lo.v[0], dy = hi.v[1] - lo.v[1], dz = hi.v[2] - lo.v[2];
-		const int axis = (dx > dy) ? ((dx > dz) ? 0 : 2) : ((dy > dz) ? 1 : 2);
-		const uint32_t split_el = (start + end) / 2;
-		auto coord = [&](uint32_t a) { const float4 &q = pos[a]; return axis == 0 ? q.x : (axis == 1 ? q.y : q.z); };
-		std::nth_element(el + start, el + split_el, el + end, [&](uint32_t a, uint32_t b) {
-			const float pa = coord(a), pb = coord(b);
-			return pa == pb ? (a < b) : pa < pb;
-		});
-		const float split_pos = coord(el[split_el]);
-		const uint32_t nl = split_el - start;
-		const uint32_t right = node + 2 * nl;
-		uint32_t bits;
-		std::memcpy(&bits, &split_pos, 4);
-		nodes[node] = make_uint2(bits, (uint32_t)axis | (right << 2));
-		F3b hi_l = hi, lo_r = lo;
-		hi_l.v[axis] = split_pos;
-		lo_r.v[axis] = split_pos;
-		if(level < 4 && end - start > 65536)
-		{
-			auto f = std::async(std::launch::async, [&, start, split_el, lo, hi_l, node, level]() { build(start, split_el, lo, hi_l, node + 1, level + 1); });
-			build(split_el, end, lo_r, hi, right, level + 1);
-			f.get();
-		}
-		else
-		{
-			build(start, split_el, lo, hi_l, node + 1, level + 1);
-			build(split_el, end, lo_r, hi, right, level + 1);
-		}
-	}
-};
-} // namespace
-
 bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 {
 	Impl &d = *d_;
@@ -434,24 +377,13 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	HIPCHECK(hipMemcpyAsync(&n, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	if(n < 50) { log_.error("PhotonIntegrator: Too few diffuse photons, stopping now."); return false; }   // :448-452
-	// point kd-tree on the host (exactly the reference's element order), then upload
-	std::vector<float4> hpos(n);
-	HIPCHECK(hipMemcpy(hpos.data(), d.ph_pos.p, (size_t)n * 16, hipMemcpyDeviceToHost));
-	std::vector<uint32_t> el(n);
-	for(uint32_t i = 0; i < n; ++i) el[i] = i;
-	F3b lo{{hpos[0].x, hpos[0].y, hpos[0].z}}, hi = lo;
-	for(uint32_t i = 1; i < n; ++i)
-	{
-		const float q[3] = {hpos[i].x, hpos[i].y, hpos[i].z};
-		for(int k = 0; k < 3; ++k) { lo.v[k] = std::min(lo.v[k], q[k]); hi.v[k] = std::max(hi.v[k], q[k]); }
-	}
-	std::vector<uint2> nodes(2 * (size_t)n - 1);
-	PkBuild pb;
-	pb.pos = hpos.data();
-	pb.el = el.data();
-	pb.nodes = nodes.data();
-	pb.build(0, n, lo, hi, 0, 0);
-	if(!allocCopy(log_, d.pk_nodes, nodes.data(), nodes.size())) return false;
+	const auto t1 = std::chrono::steady_clock::now();
+	// point kd-tree of the map, built on the GPU node for node like the reference's (pkd.hip)
+	if(!ensure(log_, d.pk_nodes, (2 * (size_t)n - 1) * sizeof(uint2))) return false;
+	int depth = 0;
+	HIPCHECK(yafamd_build_pkd((const float4 *)d.ph_pos.p, n, (uint2 *)d.pk_nodes.p, &depth, d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	struct { int max_depth; } pb{depth};
 	d.n_photons = (int)n;
 	d.pm_paths = (int)N;
 	d.pm_stack = pb.max_depth + 1;
@@ -463,7 +395,10 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	S.pm_paths = (int)N;
 	S.pm_stack = d.pm_stack;
 	stats_.photons = n;
-	stats_.photon_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+	const auto t2 = std::chrono::steady_clock::now();
+	stats_.photon_seconds = std::chrono::duration<double>(t2 - t0).count();
+	stats_.photon_shoot_seconds = std::chrono::duration<double>(t1 - t0).count();
+	stats_.photon_tree_seconds = std::chrono::duration<double>(t2 - t1).count();
 	std::ostringstream os;
 	os << "PhotonIntegrator: shot " << N << " photons, stored " << n << " (kd-tree depth " << pb.max_depth << ") in " << stats_.photon_seconds << " s";
 	log_.info(os.str());
