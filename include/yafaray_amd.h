@@ -44,6 +44,7 @@ typedef struct
 	double nee_kernel_ms;       /* summed k_nee time */
 	uint64_t photons;           /* photons stored in the diffuse photon map (photon mapping) */
 	double photon_seconds;      /* photon shooting + kd-tree build + upload */
+	double photon_shoot_seconds, photon_tree_seconds;
 } yafaray_amd_stats_t;
 
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */

@@ -2,6 +2,7 @@
 #include "bvh.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstring>
@@ -264,6 +265,103 @@ BvhOutput buildBvh(const BvhInput &in, int leaf_size, int threads)
 			out.max_leaf = std::max(out.max_leaf, c.count);
 		}
 	};
+	if(in.width == 4)
+	{
+		// BVH4: collapse the binary tree — each wide node takes the two children of a binary node
+		// and keeps opening its inner child of largest surface area until it holds four children.
+		// Layout per node (8 float4): lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4],
+		// child[4] (inner: node index >= 0; leaf: ~first triangle; empty: -1), count[4] (0 inner/empty, n leaf).
+		out.width = 4;
+		std::vector<int> wide_of;   // BuildNode index of each wide node's binary source
+		std::vector<std::array<int, 4>> kids;
+		std::vector<int> wdepth;
+		std::vector<int> index_of(b.nodes.size(), -1);
+		wide_of.push_back(root);
+		kids.push_back({-1, -1, -1, -1});
+		wdepth.push_back(1);
+		for(size_t w = 0; w < wide_of.size(); ++w)
+		{
+			// a leaf (or empty) root becomes the single child of a synthetic wide root
+			std::vector<int> list;
+			if(wide_of[w] < 0) {}
+			else if(b.nodes[wide_of[w]].left < 0) list.push_back(wide_of[w]);
+			else list = {b.nodes[wide_of[w]].left, b.nodes[wide_of[w]].right};
+			while(list.size() < 4)
+			{
+				int best = -1;
+				float best_area = -1.f;
+				for(size_t k = 0; k < list.size(); ++k)
+				{
+					const BuildNode &c = b.nodes[list[k]];
+					if(c.left >= 0 && c.box.area() > best_area) { best_area = c.box.area(); best = (int)k; }
+				}
+				if(best < 0) break;
+				const BuildNode &c = b.nodes[list[best]];
+				list[best] = c.left;
+				list.insert(list.begin() + best + 1, c.right);
+			}
+			for(size_t k = 0; k < list.size(); ++k)
+			{
+				kids[w][k] = list[k];
+				if(b.nodes[list[k]].left >= 0)
+				{
+					index_of[list[k]] = (int)wide_of.size();
+					wide_of.push_back(list[k]);
+					kids.push_back({-1, -1, -1, -1});
+					wdepth.push_back(wdepth[w] + 1);
+				}
+			}
+		}
+		out.n_nodes = (int)wide_of.size();
+		out.depth = 0;
+		for(int dd : wdepth) out.depth = std::max(out.depth, dd);
+		out.nodes.assign(32 * (size_t)out.n_nodes, 0.f);
+		for(int w = 0; w < out.n_nodes; ++w)
+		{
+			float *o = &out.nodes[32 * (size_t)w];
+			for(int k = 0; k < 4; ++k)
+			{
+				const int ci = kids[w][k];
+				float lo[3] = {1.f, 1.f, 1.f}, hi[3] = {-1.f, -1.f, -1.f};
+				int child = -1, count = 0;
+				if(ci >= 0)
+				{
+					const BuildNode &c = b.nodes[ci];
+					if(c.left >= 0 || c.count > 0)
+					{
+						padBox(c.box, lo, hi);
+						if(c.left >= 0) { child = index_of[ci]; count = 0; }
+						else
+						{
+							child = ~c.start;
+							count = c.count;
+							out.max_leaf = std::max(out.max_leaf, c.count);
+						}
+					}
+				}
+				o[0 + k] = lo[0]; o[4 + k] = hi[0];
+				o[8 + k] = lo[1]; o[12 + k] = hi[1];
+				o[16 + k] = lo[2]; o[20 + k] = hi[2];
+				intAsFloatBits(child, o[24 + k]);
+				intAsFloatBits(count, o[28 + k]);
+			}
+		}
+		// children are numbered after their parent, so one reverse sweep sees every subtree first
+		std::vector<int> need(out.n_nodes, 0);
+		for(int w = out.n_nodes - 1; w >= 0; --w)
+		{
+			int inner = 0, deepest = 0;
+			for(int k = 0; k < 4; ++k)
+				if(kids[w][k] >= 0 && b.nodes[kids[w][k]].left >= 0)
+				{
+					++inner;
+					deepest = std::max(deepest, need[index_of[kids[w][k]]]);
+				}
+			need[w] = std::max(0, inner - 1) + deepest;
+		}
+		out.stack_need = need[0];
+		return out;
+	}
 	if(inner_order.empty())
 	{
 		// a single leaf (or an empty scene): synthesise an inner root with one leaf child

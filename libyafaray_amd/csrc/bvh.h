@@ -19,15 +19,18 @@ struct BvhInput
 	const int *tris;        // 3 vertex indices per triangle
 	int n_tris;
 	float node_cost = 0.f;   // SAH node cost (<= 0: default 0.5)
+	int width = 4;           // 2: BVH2 (4 float4 per node), 4: BVH4 (8 float4 per node)
 };
 
 struct BvhOutput
 {
-	std::vector<float> nodes;   // 16 floats per node (devscene.h layout)
+	std::vector<float> nodes;   // 16 (BVH2) or 32 (BVH4) floats per node (devscene.h layout)
+	int width = 2;
 	std::vector<float> tris;    // 12 floats per triangle, leaf order (devscene.h layout)
 	int n_nodes = 0;
 	int depth = 0;              // inner-node depth (bounds the traversal stack)
 	int max_leaf = 0;
+	int stack_need = 0;         // worst-case traversal stack entries (BVH4: sum of deferred siblings along a path)
 };
 
 // Builds the tree.  `threads` > 1 builds independent subtrees concurrently.

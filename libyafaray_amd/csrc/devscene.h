@@ -79,6 +79,7 @@ struct DevScene
 	const uint4 *faure_dim;        // per dimension: (base, table offset, division magic m, shift)
 	const double *faure_inv;       // inv_prims (halton.cc:413)
 	int n_nodes, n_tris, n_mats, n_lights;
+	int node_f4;                   // float4 per BVH node: 4 (BVH2) or 8 (BVH4)
 	int scene_in_lds;              // nodes+tris copied to LDS by each trace workgroup
 	int lds_nodes, lds_tris;
 

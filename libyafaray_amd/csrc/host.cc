@@ -468,6 +468,7 @@ bool Scene::buildAccelerator()
 	int leaf = 1;   // pure SAH leaves (measured best on the Cornell box)
 	if(const char *e = getenv("YAFARAY_AMD_BVH_LEAF")) leaf = std::max(1, atoi(e));          // tuning sweeps
 	if(const char *e = getenv("YAFARAY_AMD_BVH_NODE_COST")) in.node_cost = (float)atof(e);
+	if(const char *e = getenv("YAFARAY_AMD_BVH_WIDTH")) in.width = atoi(e) == 2 ? 2 : 4;
 	hs.bvh = buildBvh(in, leaf, 8);
 	// primitive_triangle.cc:87-95 geometric normal; material index per primitive
 	hs.prim_ng.resize(4 * (size_t)hs.n_prims);
@@ -488,7 +489,7 @@ bool Scene::buildAccelerator()
 	const auto t1 = std::chrono::steady_clock::now();
 	stats.build_seconds = std::chrono::duration<double>(t1 - t0).count();
 	std::ostringstream os;
-	os << "Accelerator: GPU BVH2 built over " << hs.n_prims << " triangles: " << hs.bvh.n_nodes << " nodes, depth " << hs.bvh.depth
+	os << "Accelerator: GPU BVH" << hs.bvh.width << " built over " << hs.n_prims << " triangles: " << hs.bvh.n_nodes << " nodes, depth " << hs.bvh.depth
 	   << ", max leaf " << hs.bvh.max_leaf << " (" << stats.build_seconds << " s)";
 	log.info(os.str());
 	geometry_dirty = false;

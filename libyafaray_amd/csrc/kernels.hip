@@ -195,13 +195,16 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_trace: BVH2 traversal
+// k_trace: BVH2 / BVH4 traversal
 // ---------------------------------------------------------------------------------------------
 struct TraceCtx
 {
 	const float4 *nodes;
 	const float4 *tris;
-	int *stack;     // LDS, [level * kTraceBlock + lane]
+	int *stack;     // LDS, [level * kTraceBlock + lane], levels [0, lds_depth)
+	int lds_depth;
+	int *spill;     // HBM, [(level - lds_depth) * spill_stride + global lane] (BVH4 deep levels)
+	uint32_t spill_stride;
 };
 
 __device__ __forceinline__ void boxPair(const float4 &n0, const float4 &n1, const float4 &n2, V3 o, V3 id,
@@ -249,8 +252,8 @@ __device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const
 // [0, tmax).  Box tests are conservative (boxes padded at build time + a relative slack), so
 // culling never drops a hit the exhaustive reference semantics would return.
 template<bool ANY>
-__device__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
-                         uint32_t &visits, uint32_t &tests)
+__device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
+                          uint32_t &visits, uint32_t &tests)
 {
 	const int lane = threadIdx.x;
 	V3 dd = d;
@@ -324,19 +327,131 @@ __device__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, 
 	return prim_best >= 0;
 }
 
-template<bool LDS_SCENE>
+__device__ __forceinline__ float lane4(const float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
+__device__ __forceinline__ void cswap(float &ka, int &va, float &kb, int &vb)
+{
+	const bool sw = kb < ka;
+	const float k = sw ? kb : ka;
+	kb = sw ? ka : kb;
+	ka = k;
+	const int v = sw ? vb : va;
+	vb = sw ? va : vb;
+	va = v;
+}
+
+// BVH4 (bvh.cc: collapsed binary SAH tree, 128 B nodes with the four child boxes in SoA form).
+// Same hit semantics as traverse2: leaf children are tested as soon as their box is hit, inner
+// children are sorted by entry distance (5-exchange network) and descended nearest-first.
+template<bool ANY, bool SPILL>
+__device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
+                          uint32_t &visits, uint32_t &tests)
+{
+	const int lane = threadIdx.x;
+	V3 dd = d;
+	if(fabsf(dd.x) < 1e-20f) dd.x = copysignf(1e-20f, dd.x);
+	if(fabsf(dd.y) < 1e-20f) dd.y = copysignf(1e-20f, dd.y);
+	if(fabsf(dd.z) < 1e-20f) dd.z = copysignf(1e-20f, dd.z);
+	const V3 id = v3(1.f / dd.x, 1.f / dd.y, 1.f / dd.z);
+	const float box_t0 = ANY ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
+	const float inf = __builtin_huge_valf();
+	const uint32_t glane = blockIdx.x * blockDim.x + threadIdx.x;
+	t_best = tmax;
+	prim_best = -1;
+	int sp = 0;
+	int node = 0;
+	// the first lds_depth levels live in LDS; deeper ones (rare) spill to this lane's HBM column
+	auto push = [&](int v) {
+		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + lane] = v;
+		else if(SPILL) C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane] = v;
+	};
+	for(;;)
+	{
+		++visits;
+		const float4 *np = C.nodes + 8 * node;
+		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
+		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
+		float key[4];
+		int child[4];
+#pragma unroll
+		for(int k = 0; k < 4; ++k)
+		{
+			const float ax = (lane4(lx, k) - o.x) * id.x, bx = (lane4(hx, k) - o.x) * id.x;
+			const float ay = (lane4(ly, k) - o.y) * id.y, by = (lane4(hy, k) - o.y) * id.y;
+			const float az = (lane4(lz, k) - o.z) * id.z, bz = (lane4(hz, k) - o.z) * id.z;
+			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
+			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
+			const bool h = lo <= hi;
+			const int c = __float_as_int(lane4(cf, k));
+			const int cnt = __float_as_int(lane4(kf, k));
+			child[k] = c;
+			key[k] = (h && c >= 0) ? lo : inf;
+			if(!h || c >= 0 || cnt == 0) continue;
+			const int start = ~c;
+			for(int q = start; q < start + cnt; ++q)
+			{
+				++tests;
+				const float4 *tp = C.tris + 3 * q;
+				const float4 ta = tp[0], tb = tp[1], tc = tp[2];
+				const float t = triTest(ta, tb, tc, o, d, ANY ? tmax : t_best);
+				if(t == -1.f) continue;
+				const int prim = __float_as_int(tb.w);
+				if(ANY)
+				{
+					if(t < tmax && t >= 0.f) { t_best = t; prim_best = prim; return true; }
+				}
+				else if(t >= tmin && (t < t_best || (t == t_best && prim_best >= 0 && prim < prim_best)))
+				{
+					t_best = t;
+					prim_best = prim;
+				}
+			}
+		}
+		cswap(key[0], child[0], key[1], child[1]);
+		cswap(key[2], child[2], key[3], child[3]);
+		cswap(key[0], child[0], key[2], child[2]);
+		cswap(key[1], child[1], key[3], child[3]);
+		cswap(key[1], child[1], key[2], child[2]);
+		if(key[3] < inf) { push(child[3]); ++sp; }
+		if(key[2] < inf) { push(child[2]); ++sp; }
+		if(key[1] < inf) { push(child[1]); ++sp; }
+		int next = key[0] < inf ? child[0] : -1;
+		if(next < 0)
+		{
+			if(sp == 0) break;
+			--sp;
+			next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + lane]
+			                                    : C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane];
+		}
+		node = next;
+	}
+	return prim_best >= 0;
+}
+
+template<bool ANY, bool WIDE, bool SPILL = true>
+__device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best,
+                                         int &prim_best, uint32_t &visits, uint32_t &tests)
+{
+	if(WIDE) return traverse4<ANY, SPILL>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests);
+	return traverse2<ANY>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests);
+}
+
+template<bool LDS_SCENE, bool WIDE>
 __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P,
-                                                      DevStats *stats, int stack_depth)
+                                                      DevStats *stats, int stack_depth, int *spill)
 {
 	extern __shared__ float4 smem[];
 	int *stack = reinterpret_cast<int *>(smem);
 	TraceCtx C;
 	C.stack = stack;
+	C.lds_depth = stack_depth;
+	C.spill = spill;
+	C.spill_stride = gridDim.x * blockDim.x;
 	if(LDS_SCENE)
 	{
 		float4 *lds_nodes = smem + (stack_depth * kTraceBlock) / 4;
-		float4 *lds_tris = lds_nodes + 4 * S.n_nodes;
-		for(int k = threadIdx.x; k < 4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = S.nodes[k];
+		float4 *lds_tris = lds_nodes + S.node_f4 * S.n_nodes;
+		for(int k = threadIdx.x; k < S.node_f4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = S.nodes[k];
 		for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = S.tris[k];
 		__syncthreads();
 		C.nodes = lds_nodes;
@@ -366,7 +481,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, 
 				float t;
 				int prim;
 				const float tmax = (dd.w >= 0.f) ? dd.w : __builtin_huge_valf();
-				traverse<false>(C, xyz(od), xyz(dd), od.w, tmax, t, prim, visits, tests);
+				traverse<false, WIDE>(C, xyz(od), xyz(dd), od.w, tmax, t, prim, visits, tests);
 				Q.hit_t[i] = t;
 				Q.hit_prim[i] = prim;
 				++n_closest;
@@ -378,7 +493,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, DevQueues Q, 
 			const float4 od = Q.sh_o[k], dd = Q.sh_d[k];
 			float t;
 			int prim;
-			const bool occ = traverse<true>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
+			const bool occ = traverse<true, WIDE>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
 			P.occ[Q.sh_idx[k]] = occ ? 1 : 0;   // P = state set of the consumer shade
 			++n_shadow;
 		}
@@ -1410,13 +1525,16 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 // ---------------------------------------------------------------------------------------------
 // ray-level entry (batched Accelerator::intersect / isShadowed for parity tests and hosts)
 // ---------------------------------------------------------------------------------------------
-template<bool ANY>
+template<bool ANY, bool WIDE>
 __global__ void __launch_bounds__(kTraceBlock) k_trace_rays(DevScene S, const float4 *ro, const float4 *rd, int n,
                                                            float *t_out, int *prim_out, int stack_depth)
 {
 	extern __shared__ float4 smem[];
 	TraceCtx C;
 	C.stack = reinterpret_cast<int *>(smem);
+	C.lds_depth = stack_depth;   // the full bound: no spill (traverse<..., SPILL = false>)
+	C.spill = nullptr;
+	C.spill_stride = 0;
 	C.nodes = S.nodes;
 	C.tris = S.tris;
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1431,14 +1549,14 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_rays(DevScene S, const fl
 		V3 so;
 		float tm;
 		shadowRayOf(xyz(o), xyz(d), o.w, d.w, so, tm);
-		const bool occ = traverse<true>(C, so, xyz(d), 0.f, tm, tb, pb, v, t);
+		const bool occ = traverse<true, WIDE, false>(C, so, xyz(d), 0.f, tm, tb, pb, v, t);
 		t_out[i] = occ ? 1.f : 0.f;
 		prim_out[i] = occ ? pb : -1;
 	}
 	else
 	{
 		const float tmax = (d.w >= 0.f) ? d.w : __builtin_huge_valf();
-		const bool hit = traverse<false>(C, xyz(o), xyz(d), o.w, tmax, tb, pb, v, t);
+		const bool hit = traverse<false, WIDE, false>(C, xyz(o), xyz(d), o.w, tmax, tb, pb, v, t);
 		t_out[i] = hit ? tb : -1.f;
 		prim_out[i] = hit ? pb : -1;
 	}
@@ -1483,7 +1601,8 @@ struct PhotonArgs
 	int max_bounces;
 	int bounce;          // k_photon_bounce: the bounce this launch traces
 	int cur;             // alive list read by this launch
-	int stack_depth;
+	int stack_depth;   // LDS stack levels (deeper levels spill, BVH4)
+	int *spill;
 };
 
 // :127-156 — photon id h: light pick by Pdf1D::dSample over the lights' energies, emitPhoton
@@ -1543,18 +1662,21 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 }
 
 // :162-219 — one bounce of every live photon path: intersect, deposit, scatter (material.cc:137-153)
-template<bool LDS_SCENE>
+template<bool LDS_SCENE, bool WIDE>
 __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 {
 	const DevScene &S = A.S;
 	extern __shared__ float4 smem[];
 	TraceCtx C;
 	C.stack = reinterpret_cast<int *>(smem);
+	C.lds_depth = A.stack_depth;
+	C.spill = A.spill;
+	C.spill_stride = gridDim.x * blockDim.x;
 	if(LDS_SCENE)
 	{
 		float4 *lds_nodes = smem + (A.stack_depth * kTraceBlock) / 4;
-		float4 *lds_tris = lds_nodes + 4 * S.n_nodes;
-		for(int k = threadIdx.x; k < 4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = S.nodes[k];
+		float4 *lds_tris = lds_nodes + S.node_f4 * S.n_nodes;
+		for(int k = threadIdx.x; k < S.node_f4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = S.nodes[k];
 		for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = S.tris[k];
 		__syncthreads();
 		C.nodes = lds_nodes;
@@ -1583,7 +1705,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 			const float4 ro = A.P.ray_o[h], rd = A.P.ray_d[h], pc = A.P.pcol[h];
 			float t;
 			int prim;
-			if(traverse<false>(C, xyz(ro), xyz(rd), ro.w, __builtin_huge_valf(), t, prim, visits, tests))
+			if(traverse<false, WIDE>(C, xyz(ro), xyz(rd), ro.w, __builtin_huge_valf(), t, prim, visits, tests))
 			{
 				const Surf sp = makeSurf(S, xyz(ro), xyz(rd), t, prim);
 				const V3 wi = -xyz(rd);
@@ -1874,12 +1996,15 @@ int yafamd_phase_cycles(unsigned long long *out, int n, int reset)
 }
 
 // Resident workgroups per CU of the persistent kernels (their grids fill the chip exactly once).
-int yafamd_trace_blocks_per_cu(int lds_scene, size_t dyn_lds)
+int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds)
 {
 	int nb = 0;
-	if(lds_scene) { if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true>, kTraceBlock, dyn_lds) != hipSuccess) nb = 0; }
-	else if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false>, kTraceBlock, dyn_lds) != hipSuccess) nb = 0;
-	return nb;
+	hipError_t e;
+	if(lds_scene) e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, true>, kTraceBlock, dyn_lds)
+	                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, false>, kTraceBlock, dyn_lds);
+	else e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, true>, kTraceBlock, dyn_lds)
+	              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, false>, kTraceBlock, dyn_lds);
+	return e == hipSuccess ? nb : 0;
 }
 
 int yafamd_nee_blocks_per_cu()
@@ -1906,15 +2031,18 @@ hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQ
 }
 
 hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P,
-                               DevStats *stats, int stack_depth, int grid, hipStream_t st)
+                               DevStats *stats, int stack_depth, int *spill, int grid, hipStream_t st)
 {
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
+	const bool wide = S->node_f4 == 8;
 	if(S->scene_in_lds)
 	{
-		const size_t bytes = stack_bytes + (size_t)(4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
-		hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth);
+		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
+		if(wide) hipLaunchKernelGGL((k_trace<true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill);
+		else hipLaunchKernelGGL((k_trace<true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill);
 	}
-	else hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kTraceBlock), stack_bytes, st, *S, *Q, *cnt, *P, stats, stack_depth);
+	else if(wide) hipLaunchKernelGGL((k_trace<false, true>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill);
+	else hipLaunchKernelGGL((k_trace<false, false>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill);
 	return hipGetLastError();
 }
 
@@ -1966,13 +2094,14 @@ hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, uint32_t 
 	A.bounce = 0;
 	A.cur = 0;
 	A.stack_depth = 0;
+	A.spill = nullptr;
 	if(n_photons == 0) return hipSuccess;
 	hipLaunchKernelGGL(k_photon_emit, dim3((n_photons + 255) / 256), dim3(256), 0, st, A);
 	return hipGetLastError();
 }
 
 hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, int bounce,
-                                int cur, int stack_depth, int grid, hipStream_t st)
+                                int cur, int stack_depth, int *spill, int grid, hipStream_t st)
 {
 	PhotonArgs A;
 	A.S = *S;
@@ -1982,13 +2111,16 @@ hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_
 	A.bounce = bounce;
 	A.cur = cur;
 	A.stack_depth = stack_depth;
+	A.spill = spill;
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	if(S->scene_in_lds)
 	{
-		const size_t bytes = stack_bytes + (size_t)(4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
-		hipLaunchKernelGGL(k_photon_bounce<true>, dim3(grid), dim3(kTraceBlock), bytes, st, A);
+		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
+		if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+		else hipLaunchKernelGGL((k_photon_bounce<true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
 	}
-	else hipLaunchKernelGGL(k_photon_bounce<false>, dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
+	else if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<false, true>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
+	else hipLaunchKernelGGL((k_photon_bounce<false, false>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
 	return hipGetLastError();
 }
 
@@ -2040,8 +2172,12 @@ hipError_t yafamd_launch_trace_rays(const DevScene *S, int any, const float4 *ro
 {
 	if(n <= 0) return hipSuccess;
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
-	if(any) hipLaunchKernelGGL(k_trace_rays<true>, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), stack_bytes, st, *S, ro, rd, n, t_out, prim_out, stack_depth);
-	else hipLaunchKernelGGL(k_trace_rays<false>, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), stack_bytes, st, *S, ro, rd, n, t_out, prim_out, stack_depth);
+	const dim3 grid((n + kTraceBlock - 1) / kTraceBlock);
+	const bool wide = S->node_f4 == 8;
+	if(any && wide) hipLaunchKernelGGL((k_trace_rays<true, true>), grid, dim3(kTraceBlock), stack_bytes, st, *S, ro, rd, n, t_out, prim_out, stack_depth);
+	else if(any) hipLaunchKernelGGL((k_trace_rays<true, false>), grid, dim3(kTraceBlock), stack_bytes, st, *S, ro, rd, n, t_out, prim_out, stack_depth);
+	else if(wide) hipLaunchKernelGGL((k_trace_rays<false, true>), grid, dim3(kTraceBlock), stack_bytes, st, *S, ro, rd, n, t_out, prim_out, stack_depth);
+	else hipLaunchKernelGGL((k_trace_rays<false, false>), grid, dim3(kTraceBlock), stack_bytes, st, *S, ro, rd, n, t_out, prim_out, stack_depth);
 	return hipGetLastError();
 }
 

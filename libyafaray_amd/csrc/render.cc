@@ -19,9 +19,9 @@ extern "C" {
 hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st);
 hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P,
-                               DevStats *stats, int stack_depth, int grid, hipStream_t st);
+                               DevStats *stats, int stack_depth, int *spill, int grid, hipStream_t st);
 int yafamd_trace_block();
-int yafamd_trace_blocks_per_cu(int lds_scene, size_t dyn_lds);
+int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds);
 int yafamd_shade_blocks_per_cu();
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
                                const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, const DevCounters *cnt_next,
@@ -31,7 +31,7 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 int yafamd_nee_blocks_per_cu();
 hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, hipStream_t st);
 hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, int bounce,
-                                int cur, int stack_depth, int grid, hipStream_t st);
+                                int cur, int stack_depth, int *spill, int grid, hipStream_t st);
 hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev,
                                  float4 *pos, float4 *dir, float *colb, hipStream_t st);
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const DevCounters *cnt_next, float4 *samples,
@@ -97,7 +97,9 @@ struct GpuRenderer::Impl
 	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
 	Buf ph_pos, ph_dir, ph_colb, pk_nodes;
 	int n_photons = 0, pm_paths = 0, pm_stack = 0;
-	int n_nodes = 0, n_tris = 0, n_mats = 0, n_lights = 0, depth = 0, stack_depth = 32;
+	int n_nodes = 0, n_tris = 0, n_mats = 0, n_lights = 0, depth = 0, stack_depth = 32, node_f4 = 4;
+	int lds_stack = 32;    // k_trace stack levels held in LDS; levels [lds_stack, stack_depth) spill to `spill`
+	Buf spill;
 	bool scene_in_lds = false;
 	int faure_bytes = 0;
 	// frame buffers
@@ -120,7 +122,7 @@ struct GpuRenderer::Impl
 		for(Buf *b : {&ph_lights, &light_cdf, &light_func, &ph_ray_o, &ph_ray_d, &ph_pcol, &ph_alive0, &ph_alive1, &ph_n_alive,
 		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes})
 			b->release();
-		for(Buf *b : {&nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_dim, &faure_inv, &samples, &film,
+		for(Buf *b : {&spill, &nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_dim, &faure_inv, &samples, &film,
 		              &weights, &jobs, &counters, &stats})
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
@@ -243,17 +245,28 @@ bool GpuRenderer::upload(const HostScene &hs)
 		}
 	}
 	d.depth = hs.bvh.depth;
-	d.stack_depth = std::max(8, ((hs.bvh.depth + 2 + 7) / 8) * 8);
-	const size_t scene_bytes = (size_t)(4 * d.n_nodes + 3 * d.n_tris) * 16;
-	d.scene_in_lds = scene_bytes + (size_t)d.stack_depth * yafamd_trace_block() * 4 <= 48 * 1024;
+	d.node_f4 = hs.bvh.width == 4 ? 8 : 4;
+	const int need = hs.bvh.width == 4 ? hs.bvh.stack_need : hs.bvh.depth;
+	d.stack_depth = std::max(8, ((need + 2 + 7) / 8) * 8);
+	// BVH4's worst-case bound (3 deferred siblings per level) is far above what rays use: k_trace
+	// keeps the first levels in LDS (occupancy) and spills deeper ones to HBM
+	d.lds_stack = d.stack_depth;
+	if(d.node_f4 == 8) d.lds_stack = std::min(d.stack_depth, 24);
+	if(const char *e = getenv("YAFARAY_AMD_LDS_STACK"); e && *e) d.lds_stack = std::min(d.stack_depth, std::max(4, atoi(e)));
+	const size_t scene_bytes = (size_t)(d.node_f4 * d.n_nodes + 3 * d.n_tris) * 16;
+	d.scene_in_lds = scene_bytes + (size_t)d.lds_stack * yafamd_trace_block() * 4 <= 48 * 1024;
 	{
 		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy))
-		const size_t dyn = (size_t)d.stack_depth * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : 0);
-		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, dyn));
+		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : 0);
+		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, d.node_f4 == 8 ? 1 : 0, dyn));
 		if(const char *e = getenv("YAFARAY_AMD_TRACE_GRID")) d.trace_grid = std::max(1, atoi(e));
 		// a whole number of workgroups per queue segment
 		d.trace_grid = std::max(1, d.trace_grid / d.shade_grid) * d.shade_grid;
 	}
+	d.spill.release();
+	if(d.lds_stack < d.stack_depth &&
+	   !ensure(log_, d.spill, (size_t)(d.stack_depth - d.lds_stack) * d.trace_grid * yafamd_trace_block() * sizeof(int)))
+		return false;
 	// Faure tables, dims 0..49 (halton.cc:403-414: dims 0-2 share the base-3 table)
 	std::vector<uint8_t> perm;
 	std::vector<uint32_t> off(50), base(50);
@@ -309,6 +322,7 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.faure_dim = (const uint4 *)d.faure_dim.p;
 	S.faure_inv = (const double *)d.faure_inv.p;
 	S.n_nodes = d.n_nodes;
+	S.node_f4 = d.node_f4;
 	S.n_tris = d.n_tris;
 	S.n_mats = d.n_mats;
 	S.n_lights = d.n_lights;
@@ -365,7 +379,7 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	for(int b = 0; b <= pm.bounces; ++b)
 	{
 		HIPCHECK(hipMemsetAsync((uint32_t *)d.ph_n_alive.p + (cur ^ 1), 0, 4, d.stream));
-		HIPCHECK(yafamd_photon_bounce(&S, &P, N, pm.bounces, b, cur, d.stack_depth, d.trace_grid, d.stream));
+		HIPCHECK(yafamd_photon_bounce(&S, &P, N, pm.bounces, b, cur, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 		cur ^= 1;
 	}
 	// the photon map in photon-id order (one reference thread's append order); outputs sized for
@@ -573,7 +587,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		for(int it = 0; it < iters; ++it)
 		{
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i], d.stream));
-			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], dstats, d.stack_depth, d.trace_grid, d.stream));
+			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], dstats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 1], d.stream));
 			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));

@@ -45,9 +45,21 @@ def product_scene(product, spec):
     return yi
 
 
+# BVH layouts under test: BVH4 (default), BVH4 with a 4-level LDS stack (exercises the HBM spill
+# levels of k_trace / k_photon_bounce), and the binary BVH2
+BVH_VARIANTS = {"bvh4": {}, "bvh4-spill": {"YAFARAY_AMD_LDS_STACK": "4"}, "bvh2": {"YAFARAY_AMD_BVH_WIDTH": "2"}}
+
+
+def use_bvh(monkeypatch, variant):
+    for k, v in BVH_VARIANTS[variant].items():
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("bvh", ["bvh4", "bvh2"])
 @pytest.mark.parametrize("which", ["cornell", "test01", "sphere"])
-def test_trace_closest_and_shadow_bitexact(product, oracle_built, which):
+def test_trace_closest_and_shadow_bitexact(product, oracle_built, which, bvh, monkeypatch):
     """Ray level on all three scenes; "sphere" is BASELINE C4 (1M triangles, BVH in HBM/L2)."""
+    use_bvh(monkeypatch, bvh)
     spec = {"cornell": lambda: scenes.cornell(32, 32, spp=1), "test01": lambda: scenes.test01(32, 32, spp=1),
             "sphere": lambda: scenes.cornell_sphere(width=32, height=32, spp=1)}[which]()
     rays = random_rays(spec, 20000, 7)
@@ -73,7 +85,9 @@ def test_direct_light_test01_matches_oracle(product, oracle_built):
     assert st["samples"] == 96 * 96 * 4
 
 
-def test_path_noRR_cornell_matches_oracle(product, oracle_built):
+@pytest.mark.parametrize("bvh", list(BVH_VARIANTS))
+def test_path_noRR_cornell_matches_oracle(product, oracle_built, bvh, monkeypatch):
+    use_bvh(monkeypatch, bvh)
     spec = scenes.cornell(80, 60, spp=8, bounces=8, rr=False)
     rgba, w, st = product.render_spec(spec, chunk_slots=8192)
     orgba, ow, octr = oracle_built.OracleScene(spec, threads=8).render()
@@ -86,13 +100,20 @@ def test_path_noRR_cornell_matches_oracle(product, oracle_built):
     assert st["shadow_rays"] <= octr[1]
 
 
-def test_path_noRR_sphere_matches_oracle(product, oracle_built):
+_sphere_oracle = {}
+
+
+@pytest.mark.parametrize("bvh", list(BVH_VARIANTS))
+def test_path_noRR_sphere_matches_oracle(product, oracle_built, bvh, monkeypatch):
     """BASELINE C4 scene (Cornell box + 999,698-triangle sphere): the BVH does not fit LDS, so this
-    exercises the global-memory traversal (k_trace<false>) end to end."""
+    exercises the global-memory traversal (k_trace<false, *>) end to end."""
+    use_bvh(monkeypatch, bvh)
     spec = scenes.cornell_sphere(width=64, height=48, spp=4, bounces=8, rr=False)
     rgba, w, st = product.render_spec(spec)
     assert st["scene_in_lds"] == 0
-    orgba, ow, octr = oracle_built.OracleScene(spec, threads=8).render()
+    if "ref" not in _sphere_oracle:
+        _sphere_oracle["ref"] = oracle_built.OracleScene(spec, threads=8).render()
+    orgba, ow, octr = _sphere_oracle["ref"]
     assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
     d = ulp_diff(rgba, orgba)
     assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
@@ -136,10 +157,12 @@ def test_reference_client_test01_renders(tmp_path):
     assert not errors, errors[:5]
 
 
-def test_photon_mapping_matches_oracle(product, oracle_built):
+@pytest.mark.parametrize("bvh", list(BVH_VARIANTS))
+def test_photon_mapping_matches_oracle(product, oracle_built, bvh, monkeypatch):
     """BASELINE C5 pipeline at a small size: photon shooting (GPU wavefront), point kd-tree,
     k-NN gather with the reference's heap order, PM integrate (emission twice, direct light,
     density estimate) — per pixel <= 4 ULP of the oracle."""
+    use_bvh(monkeypatch, bvh)
     spec = scenes.cornell_photon(64, 48, spp=2, photons=30000, search=50, radius=0.1)
     rgba, w, st = product.render_spec(spec)
     orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
