@@ -146,14 +146,15 @@ def main():
     # roofline of the dominant kernel (k_trace) on this rank, per launch, with the average launch
     # duration from HIP events on the render stream.  Algorithmic bytes:
     #   ray I/O      closest 32 B in + 8 B out, shadow 32 B in + 4 B index + 1 B out  (always HBM)
-    #   traversal    64 B per BVH node visited + 48 B per triangle tested
+    #   traversal    64 B (BVH2) / 128 B (BVH4) per BVH node visited + 48 B per triangle tested
     # The traversal bytes count against HBM only when the scene is not LDS-resident; for the
     # Cornell box (3 KB) they are served by LDS and reported separately against the LDS peak.
     s = stats_acc[-1]
     launches = max(1, s["trace_launches"])
     avg_ms = s["trace_kernel_ms"] / launches
     ray_io = 40.0 * s["closest_rays"] + 37.0 * s["shadow_rays"]
-    trav = 64.0 * s["node_visits"] + 48.0 * s["tri_tests"]
+    node_bytes = 128.0 if s["bvh_width"] == 4 else 64.0
+    trav = node_bytes * s["node_visits"] + 48.0 * s["tri_tests"]
     in_lds = bool(s["scene_in_lds"])
     algo_bytes = ray_io + (0.0 if in_lds else trav)
     per_launch = algo_bytes / launches
@@ -204,7 +205,10 @@ def main():
                          "algo_bytes_per_launch": round(per_launch),
                          "traversal": {"bytes_per_launch": round(trav / launches), "served_from": "LDS" if in_lds else "L2/MALL/HBM",
                                        "achieved": round(trav_rate, 1), "unit": "GB/s",
-                                       "lds_peak": LDS_PEAK_GBS, "frac_of_lds_peak": round(trav_rate / LDS_PEAK_GBS, 4)}},
+                                       "lds_peak": LDS_PEAK_GBS, "frac_of_lds_peak": round(trav_rate / LDS_PEAK_GBS, 4),
+                                       "bvh_width": s["bvh_width"],
+                                       "node_visits_per_ray": round(s["node_visits"] / max(1, s["closest_rays"] + s["shadow_rays"]), 2),
+                                       "tri_tests_per_ray": round(s["tri_tests"] / max(1, s["closest_rays"] + s["shadow_rays"]), 2)}},
             "shade": {"avg_launch_ms": round(s["shade_kernel_ms"] / launches, 4),
                       "ms_per_step": round(s["shade_kernel_ms"], 2), "trace_ms_per_step": round(s["trace_kernel_ms"], 2),
                       "nee_ms_per_step": round(s["nee_kernel_ms"], 2)},

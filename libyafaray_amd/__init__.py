@@ -35,13 +35,13 @@ class Stats(C.Structure):
                 ("tri_tests", C.c_uint64), ("samples", C.c_uint64), ("build_seconds", C.c_double),
                 ("render_seconds", C.c_double), ("trace_kernel_ms", C.c_double), ("trace_launches", C.c_uint64),
                 ("bvh_nodes", C.c_uint32), ("bvh_depth", C.c_uint32), ("scene_in_lds", C.c_uint32),
-                ("pad", C.c_uint32), ("trace_grid", C.c_uint32), ("shade_grid", C.c_uint32),
+                ("bvh_width", C.c_uint32), ("trace_grid", C.c_uint32), ("shade_grid", C.c_uint32),
                 ("trace_block", C.c_uint32), ("stack_depth", C.c_uint32), ("shade_kernel_ms", C.c_double),
                 ("nee_kernel_ms", C.c_double), ("photons", C.c_uint64), ("photon_seconds", C.c_double),
                 ("photon_shoot_seconds", C.c_double), ("photon_tree_seconds", C.c_double)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _lib = None

@@ -251,7 +251,7 @@ bool GpuRenderer::upload(const HostScene &hs)
 	// BVH4's worst-case bound (3 deferred siblings per level) is far above what rays use: k_trace
 	// keeps the first levels in LDS (occupancy) and spills deeper ones to HBM
 	d.lds_stack = d.stack_depth;
-	if(d.node_f4 == 8) d.lds_stack = std::min(d.stack_depth, 24);
+	if(d.node_f4 == 8) d.lds_stack = std::min(d.stack_depth, 16);
 	if(const char *e = getenv("YAFARAY_AMD_LDS_STACK"); e && *e) d.lds_stack = std::min(d.stack_depth, std::max(4, atoi(e)));
 	const size_t scene_bytes = (size_t)(d.node_f4 * d.n_nodes + 3 * d.n_tris) * 16;
 	d.scene_in_lds = scene_bytes + (size_t)d.lds_stack * yafamd_trace_block() * 4 <= 48 * 1024;
@@ -300,6 +300,7 @@ bool GpuRenderer::upload(const HostScene &hs)
 	if(!allocCopy(log_, d.faure_inv, inv.data(), inv.size())) return false;
 	stats_.bvh_nodes = (uint32_t)d.n_nodes;
 	stats_.bvh_depth = (uint32_t)d.depth;
+	stats_.bvh_width = d.node_f4 == 8 ? 4u : 2u;
 	stats_.scene_in_lds = d.scene_in_lds ? 1u : 0u;
 	stats_.trace_grid = (uint32_t)d.trace_grid;
 	stats_.shade_grid = (uint32_t)d.shade_grid;
