@@ -125,19 +125,15 @@ struct DevFilm
 // Per-chunk wavefront state (structure of arrays, capacity = chunk slots).
 struct DevPaths
 {
-	uint32_t *stage;       // stage | subpath << 8 | depth << 20
-	uint32_t *flags;       // mat_bsd_fs (v1 flags) | bits below
-	float *w;              // the integrator's persistent sample weight `w`
-	float4 *thr;           // throughput
-	float4 *col;           // col (first-vertex estimate) .w = alpha
-	float4 *pcol;          // path_col
-	float4 *pwo;           // pwo (outgoing direction at the current path vertex)
+	float4 *thr;           // throughput, .w = the integrator's persistent sample weight `w`
+	float4 *col;           // col (first-vertex estimate), .w = stage | subpath << 8 | depth << 20 (bits)
+	float4 *pcol;          // path_col, .w = flags: mat_bsd_fs (v1 flags) | bits below (bits)
+	float4 *pwo;           // pwo (outgoing direction at the current path vertex): ST_FIRST entries only
 	float4 *pend_thr;      // throughput at the pending vertex (after Russian roulette)
 	float4 *pend_emit;     // emission pending at that vertex
 	float4 *v0p;           // first hit p .w = prim (bits)   — only used when path_samples > 1
 	float4 *v0wo;          // first hit wo
-	uint2 *rng;            // MWC (x, c) for Russian roulette
-	uint2 *pix;            // (PixelSamplingData::offset_, PixelSamplingData::sample_)
+	uint4 *pr;             // (PixelSamplingData::offset_, PixelSamplingData::sample_, MWC x, MWC c)
 	float4 *nee;           // [slots * nee_k] contributions .w = valid
 	uint8_t *occ;          // [slots * nee_k] shadow results
 };

@@ -182,16 +182,13 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	Q.slot[a] = i;          // sample id within the chunk travels with the queue entry
 	Q.ray_o[a] = f4(pos, tmin);
 	Q.ray_d[a] = f4(dir, tmax);
-	P.stage[a] = ST_CAMERA;
-	P.flags[a] = 0;
-	P.w[a] = 0.f;
-	P.col[a] = make_float4(0.f, 0.f, 0.f, 1.f);
-	P.pcol[a] = make_float4(0.f, 0.f, 0.f, 0.f);
-	P.pix[a] = make_uint2(offset, S.base_offset + (uint32_t)sc.s);
+	P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
+	P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));   // stage
+	P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
 	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
 	// output is matched statistically — integrator_tiled.cc:272)
 	const uint32_t seed = fnv32((uint32_t)(chunk_base + (uint64_t)i) ^ S.rr_seed) + 123u;
-	P.rng[a] = make_uint2(30903u, seed);
+	P.pr[a] = make_uint4(offset, S.base_offset + (uint32_t)sc.s, 30903u, seed);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1042,7 +1039,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 	{
 		const bool live = base_j + threadIdx.x < n_a;
 		const uint32_t i = a0 + base_j + threadIdx.x;   // address of the entry (shard base + position)
-		// ---- 0. load the entry (independent coalesced loads) ----
+		// ---- 0. load the entry (coalesced loads; stage, flags and w ride in the .w lanes) ----
 		uint32_t sid = 0, stage = ST_NORAY, flags = 0;
 		uint2 pix = make_uint2(0u, 0u), rng = make_uint2(0u, 0u);
 		float w = 0.f;
@@ -1051,21 +1048,23 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		if(live)
 		{
 			sid = (uint32_t)A.Q.slot[i];
-			stage = Pc.stage[i];
-			flags = Pc.flags[i];
-			pix = Pc.pix[i];
-			rng = Pc.rng[i];
-			w = Pc.w[i];
+			const uint4 pr = Pc.pr[i];
+			pix = make_uint2(pr.x, pr.y);
+			rng = make_uint2(pr.z, pr.w);
 			thr4 = Pc.thr[i];
 			col4 = Pc.col[i];
 			pcol4 = Pc.pcol[i];
-			pwo4 = Pc.pwo[i];
-			pthr4 = Pc.pend_thr[i];
-			if(flags & F_PEND_EMIT) pem4 = Pc.pend_emit[i];
 			if(keep_v0) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
+			w = thr4.w;
+			stage = __float_as_uint(col4.w);
+			flags = __float_as_uint(pcol4.w);
+			// only the first segment of a subpath reads the previous wo (path_tracer.cc:193-197)
+			if((stage & 0xffu) == ST_FIRST) pwo4 = Pc.pwo[i];
+			if(flags & F_PEND_ONE) pthr4 = Pc.pend_thr[i];
+			if(flags & F_PEND_EMIT) pem4 = Pc.pend_emit[i];
 		}
 		C3 thr = rgb(thr4), col = rgb(col4), pcol = rgb(pcol4);
-		const float alpha = col4.w;
+		const float alpha = 1.f;   // live entries are opaque (transparent background is written at ST_CAMERA)
 		V3 pwo = xyz(pwo4);
 		const uint32_t st = stage & 0xffu;
 		uint32_t subpath = (stage >> 8) & 0xfffu;
@@ -1318,15 +1317,11 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 				A.Qn.ray_d[k] = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));
 				stage = ST_NORAY | (subpath << 8) | ((uint32_t)depth << 20);
 			}
-			Pn.stage[k] = stage;
-			Pn.flags[k] = flags;
-			Pn.pix[k] = pix;
-			Pn.rng[k] = rng;
-			Pn.w[k] = w;
-			Pn.thr[k] = f4(thr, 0.f);
-			Pn.col[k] = f4(col, alpha);
-			Pn.pcol[k] = f4(pcol, 0.f);
-			Pn.pwo[k] = f4(pwo, 0.f);
+			Pn.pr[k] = make_uint4(pix.x, pix.y, rng.x, rng.y);
+			Pn.thr[k] = f4(thr, w);
+			Pn.col[k] = f4(col, __uint_as_float(stage));
+			Pn.pcol[k] = f4(pcol, __uint_as_float(flags));
+			if((stage & 0xffu) == ST_FIRST) Pn.pwo[k] = f4(pwo, 0.f);
 			if(nee_one) Pn.pend_thr[k] = f4(pend_thr, 0.f);
 			if(flags & F_PEND_EMIT) Pn.pend_emit[k] = f4(emit_pend, 0.f);
 			if(keep_v0) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }

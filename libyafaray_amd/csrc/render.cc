@@ -507,9 +507,6 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			for(int q = 0; q < 2; ++q)
 			{
 				DevPaths &P = d.P[q];
-				P.stage = (uint32_t *)A(MA * 4);
-				P.flags = (uint32_t *)A(MA * 4);
-				P.w = (float *)A(MA * 4);
 				P.thr = (float4 *)A(MA * 16);
 				P.col = (float4 *)A(MA * 16);
 				P.pcol = (float4 *)A(MA * 16);
@@ -518,8 +515,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				P.pend_emit = (float4 *)A(MA * 16);
 				P.v0p = (float4 *)A(need_v0 ? MA * 16 : 16);      // first-hit data: path_samples > 1 only
 				P.v0wo = (float4 *)A(need_v0 ? MA * 16 : 16);
-				P.rng = (uint2 *)A(MA * 8);
-				P.pix = (uint2 *)A(MA * 8);
+				P.pr = (uint4 *)A(MA * 16);
 				P.nee = (float4 *)A(MA * K * 16);
 				P.occ = (uint8_t *)A(MA * K);
 			}
