@@ -215,7 +215,10 @@ def main():
             "photon_map": ({"photons_stored": s["photons"], "seconds_per_step": round(s["photon_seconds"], 4),
                             "shoot_seconds": round(s["photon_shoot_seconds"], 4), "tree_seconds": round(s["photon_tree_seconds"], 4)}
                            if a.scene == "photon" else None),
-            "launch": {k: s[k] for k in ("trace_grid", "shade_grid", "trace_block", "stack_depth", "scene_in_lds")},
+            "launch": {k: s[k] for k in ("trace_grid", "shade_grid", "trace_block", "stack_depth", "scene_in_lds", "bvh_nodes")},
+            # accelerator build + scene upload, once before the timed region (the reference builds
+            # its kd-tree inside render(), scene.cc:218)
+            "scene_build_seconds": round(s["build_seconds"], 4),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

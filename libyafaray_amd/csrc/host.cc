@@ -469,7 +469,16 @@ bool Scene::buildAccelerator()
 	if(const char *e = getenv("YAFARAY_AMD_BVH_LEAF")) leaf = std::max(1, atoi(e));          // tuning sweeps
 	if(const char *e = getenv("YAFARAY_AMD_BVH_NODE_COST")) in.node_cost = (float)atof(e);
 	if(const char *e = getenv("YAFARAY_AMD_BVH_WIDTH")) in.width = atoi(e) == 2 ? 2 : 4;
-	hs.bvh = buildBvh(in, leaf, 8);
+	// large meshes are built on the device (bvhgpu.hip), small ones (LDS-resident scenes, where the
+	// binned-SAH tree's quality matters most) on the host; YAFARAY_AMD_BVH_BUILD=gpu|host overrides
+	hs.gpu_build = in.width == 4 && hs.n_prims >= 65536;
+	if(const char *e = getenv("YAFARAY_AMD_BVH_BUILD"); e && *e) hs.gpu_build = in.width == 4 && std::string(e) == "gpu";
+	if(hs.gpu_build)
+	{
+		hs.verts = verts;
+		hs.tris = tris;
+	}
+	else hs.bvh = buildBvh(in, leaf, 8);
 	// primitive_triangle.cc:87-95 geometric normal; material index per primitive
 	hs.prim_ng.resize(4 * (size_t)hs.n_prims);
 	for(int t = 0; t < hs.n_prims; ++t)
@@ -489,7 +498,7 @@ bool Scene::buildAccelerator()
 	const auto t1 = std::chrono::steady_clock::now();
 	stats.build_seconds = std::chrono::duration<double>(t1 - t0).count();
 	std::ostringstream os;
-	os << "Accelerator: GPU BVH" << hs.bvh.width << " built over " << hs.n_prims << " triangles: " << hs.bvh.n_nodes << " nodes, depth " << hs.bvh.depth
+	os << "Accelerator: BVH" << hs.bvh.width << (hs.gpu_build ? " (built on the GPU: PLOC + collapse)" : " (binned SAH on the host)") << " over " << hs.n_prims << " triangles: " << hs.bvh.n_nodes << " nodes, depth " << hs.bvh.depth
 	   << ", max leaf " << hs.bvh.max_leaf << " (" << stats.build_seconds << " s)";
 	log.info(os.str());
 	geometry_dirty = false;

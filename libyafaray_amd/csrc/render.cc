@@ -37,6 +37,8 @@ hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const DevCounters *cnt_next, float4 *samples,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
 size_t yafamd_gather_lds_bytes(const DevScene *S);
+hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
+                                int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st);
 hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint2 *nodes_dev, int *depth_out, hipStream_t st);
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
                               float clamp_samples, hipStream_t st);
@@ -197,17 +199,45 @@ static bool ensure(Logger &log_, Buf &b, size_t bytes)
 	return true;
 }
 
-bool GpuRenderer::upload(const HostScene &hs)
+bool GpuRenderer::upload(HostScene &hs)
 {
 	if(!ready()) return false;
 	Impl &d = *d_;
-	if(!allocCopy(log_, d.nodes, hs.bvh.nodes.data(), hs.bvh.nodes.size())) return false;
-	if(!allocCopy(log_, d.tris, hs.bvh.tris.data(), hs.bvh.tris.size())) return false;
+	if(hs.gpu_build)
+	{
+		// device build: PLOC + BVH4 collapse (bvhgpu.hip); only the mesh crosses PCIe
+		Buf v, t;
+		if(!allocCopy(log_, v, hs.verts.data(), hs.verts.size())) return false;
+		if(!allocCopy(log_, t, hs.tris.data(), hs.tris.size())) return false;
+		d.nodes.release();
+		d.tris.release();
+		void *np = nullptr, *tp = nullptr;
+		int nn = 0, depth = 0, need = 0, iters = 0;
+		const hipError_t e = yafamd_build_bvh_gpu((const float *)v.p, (const int *)t.p, hs.n_prims, &np, &tp, &nn, &depth, &need, &iters, d.stream);
+		v.release();
+		t.release();
+		HIPCHECK(e);
+		d.nodes.p = np;
+		d.nodes.bytes = (size_t)std::max(1, nn) * 128;
+		d.tris.p = tp;
+		d.tris.bytes = (size_t)std::max(1, hs.n_prims) * 48;
+		hs.bvh.width = 4;
+		hs.bvh.n_nodes = nn;
+		hs.bvh.depth = depth;
+		hs.bvh.stack_need = need;
+		hs.bvh.max_leaf = hs.n_prims > 0 ? 1 : 0;
+		hs.ploc_iters = iters;
+	}
+	else
+	{
+		if(!allocCopy(log_, d.nodes, hs.bvh.nodes.data(), hs.bvh.nodes.size())) return false;
+		if(!allocCopy(log_, d.tris, hs.bvh.tris.data(), hs.bvh.tris.size())) return false;
+	}
 	if(!allocCopy(log_, d.prim_ng, hs.prim_ng.data(), hs.prim_ng.size())) return false;
 	if(!allocCopy(log_, d.mats, hs.mats.data(), hs.mats.size())) return false;
 	if(!allocCopy(log_, d.lights, hs.lights.data(), hs.lights.size())) return false;
 	d.n_nodes = hs.bvh.n_nodes;
-	d.n_tris = (int)(hs.bvh.tris.size() / 12);
+	d.n_tris = hs.n_prims;
 	d.n_mats = (int)hs.mats.size();
 	d.n_lights = (int)hs.lights.size();
 	{

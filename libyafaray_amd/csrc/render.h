@@ -20,7 +20,11 @@ namespace yafamd
 
 struct HostScene
 {
-	BvhOutput bvh;
+	BvhOutput bvh;                       // host build (nodes + triangle records), or metadata of the GPU build
+	bool gpu_build = false;              // build the BVH4 on the device from verts / tris (bvhgpu.hip)
+	std::vector<float> verts;            // xyz per vertex   (gpu_build only)
+	std::vector<int> tris;               // 3 indices per triangle (gpu_build only)
+	int ploc_iters = 0;                  // PLOC iterations of the GPU build
 	std::vector<float> prim_ng;          // 4 floats per primitive
 	std::vector<DevMaterial> mats;
 	std::vector<DevLight> lights;        // render order (by name)
@@ -53,7 +57,7 @@ class GpuRenderer
 		explicit GpuRenderer(Logger &log);
 		~GpuRenderer();
 		bool ready();
-		bool upload(const HostScene &hs);
+		bool upload(HostScene &hs);   // fills hs.bvh's metadata when the BVH is built on the device
 		bool render(RenderParams &rp, volatile bool *canceled);
 		bool download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h);
 		bool filmToDevice(void *dst, int y0, int y1);

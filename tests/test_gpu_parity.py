@@ -47,7 +47,9 @@ def product_scene(product, spec):
 
 # BVH layouts under test: BVH4 (default), BVH4 with a 4-level LDS stack (exercises the HBM spill
 # levels of k_trace / k_photon_bounce), and the binary BVH2
-BVH_VARIANTS = {"bvh4": {}, "bvh4-spill": {"YAFARAY_AMD_LDS_STACK": "4"}, "bvh2": {"YAFARAY_AMD_BVH_WIDTH": "2"}}
+# and the device-built BVH4 (bvhgpu.hip: PLOC + collapse; the default for >= 64 K triangles)
+BVH_VARIANTS = {"bvh4": {"YAFARAY_AMD_BVH_BUILD": "host"}, "bvh4-spill": {"YAFARAY_AMD_LDS_STACK": "4"},
+                "bvh2": {"YAFARAY_AMD_BVH_WIDTH": "2"}, "gpu-build": {"YAFARAY_AMD_BVH_BUILD": "gpu"}}
 
 
 def use_bvh(monkeypatch, variant):
@@ -55,7 +57,7 @@ def use_bvh(monkeypatch, variant):
         monkeypatch.setenv(k, v)
 
 
-@pytest.mark.parametrize("bvh", ["bvh4", "bvh2"])
+@pytest.mark.parametrize("bvh", ["bvh4", "bvh2", "gpu-build"])
 @pytest.mark.parametrize("which", ["cornell", "test01", "sphere"])
 def test_trace_closest_and_shadow_bitexact(product, oracle_built, which, bvh, monkeypatch):
     """Ray level on all three scenes; "sphere" is BASELINE C4 (1M triangles, BVH in HBM/L2)."""
@@ -72,6 +74,39 @@ def test_trace_closest_and_shadow_bitexact(product, oracle_built, which, bvh, mo
     assert np.array_equal(t[hit].view(np.uint32), ohit[hit, 0].view(np.uint32))
     occ = yi.trace_shadow(rays)
     assert np.array_equal(occ, osc.trace_shadow(rays))
+    yi.close()
+
+
+def _subset(spec, n_tris):
+    """The first n_tris triangles of a scene as one object (edge cases of the BVH builders)."""
+    import dataclasses
+    tris = spec.tris[:n_tris]
+    used = np.unique(tris)
+    remap = np.full(len(spec.verts), -1, np.int32)
+    remap[used] = np.arange(len(used), dtype=np.int32)
+    return dataclasses.replace(spec, verts=spec.verts[used], tris=remap[tris], tri_mat=spec.tri_mat[:n_tris],
+                               objects=[scenes.Object("subset", 0, len(used), 0, n_tris)])
+
+
+@pytest.mark.parametrize("n_tris", [1, 2, 3, 5, 34, 3200])
+def test_gpu_bvh_build_small_and_ragged(product, oracle_built, n_tris, monkeypatch):
+    """Device BVH build on 1, 2, 3, 5 triangles, the Cornell box and a 3,200-triangle sphere: rays
+    bit-exact with the oracle (a wrong box or a lost triangle changes hits)."""
+    use_bvh(monkeypatch, "gpu-build")
+    if n_tris == 3200:
+        spec = scenes.cornell_sphere(n=40, width=32, height=32, spp=1)
+    else:
+        spec = _subset(scenes.cornell(32, 32, spp=1), n_tris)
+    rays = random_rays(spec, 8000, 11)
+    yi = product_scene(product, spec)
+    t, prim = yi.trace_closest(rays)
+    osc = oracle_built.OracleScene(spec)
+    ohit, oprim = osc.trace_closest(rays)
+    assert np.array_equal(prim, oprim), f"{(prim != oprim).sum()} primitive mismatches"
+    hit = oprim >= 0
+    assert hit.any() or n_tris < 3
+    assert np.array_equal(t[hit].view(np.uint32), ohit[hit, 0].view(np.uint32))
+    assert np.array_equal(yi.trace_shadow(rays), osc.trace_shadow(rays))
     yi.close()
 
 
