@@ -25,6 +25,7 @@ import numpy as np  # noqa: E402
 METRIC = "Mrays/sec + Msamples/sec, 1920×1080×64spp path-trace at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 LDS_PEAK_GBS = 256 * 256 * 2.4   # 256 CUs x 256 B/clk (ds_read_b128, MI355X_MICROARCH.md §LDS) x 2.4 GHz
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instructions: 4 SIMD-32 per CU, 2 cycles each (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -161,6 +162,7 @@ def main():
     achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     trav_rate = trav / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
+    valu_insts = None
     tfile = os.path.join(ROOT, "profiles", "trace_hbm_bytes_per_launch.json")
     if os.path.exists(tfile):
         try:
@@ -172,6 +174,7 @@ def main():
             # only a measurement of this exact kernel source on this exact workload counts
             if tj.get("config") == traffic_config(a, W, H) and tj.get("kernels_hip_sha1") == sha:
                 traffic = tj.get("hbm_bytes_per_launch")
+                valu_insts = tj.get("valu_insts_per_launch")
         except Exception:
             traffic = None
 
@@ -203,6 +206,14 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_trace", "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
                          "algo_bytes_per_launch": round(per_launch),
+                         # VALU issue (the bound of an LDS-resident traversal): PMC SQ_INSTS_VALU per launch
+                         # (same kernels.hip + workload only) / the live launch time, against 256 CUs x 4 SIMDs
+                         # x 2.4 GHz / 2 cycles per wave64 VALU instruction
+                         "valu": ({"insts_per_launch": valu_insts,
+                                   "achieved_g_per_s": round(valu_insts / (avg_ms * 1e-3) / 1e9, 1),
+                                   "peak_g_per_s": VALU_PEAK_GIPS,
+                                   "frac": round(valu_insts / (avg_ms * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4)}
+                                  if valu_insts and avg_ms > 0 else None),
                          "traversal": {"bytes_per_launch": round(trav / launches), "served_from": "LDS" if in_lds else "L2/MALL/HBM",
                                        "achieved": round(trav_rate, 1), "unit": "GB/s",
                                        "lds_peak": LDS_PEAK_GBS, "frac_of_lds_peak": round(trav_rate / LDS_PEAK_GBS, 4),
