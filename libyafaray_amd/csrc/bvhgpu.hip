@@ -25,7 +25,10 @@ namespace
 {
 
 constexpr int kB = 256;
-constexpr int kRadius = 16;
+#ifndef YAF_PLOC_RADIUS
+#define YAF_PLOC_RADIUS 16
+#endif
+constexpr int kRadius = YAF_PLOC_RADIUS;   // PLOC search window (+-positions in Morton order)
 constexpr int kEmpty = INT_MIN;   // empty child slot in the collapse lists (~p for leaves, p >= 0 never hits it)
 
 struct DevBuf

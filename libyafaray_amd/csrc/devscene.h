@@ -94,6 +94,13 @@ struct DevScene
 	float shadow_bias, ray_min_dist;
 	uint32_t base_offset, rr_seed;
 	float clamp_samples;
+	// adaptive anti-aliasing (integrator_tiled.cc:172-231): passes > 1 switch the sub-pixel
+	// positions to riVdC / riS of the global sample index; pass_offset = samples of earlier passes;
+	// plist = the pixels this pass resamples, in the reference's visiting order (null: every pixel,
+	// enumerated by the jobs)
+	int aa_multipass;
+	uint32_t pass_offset;
+	const uint32_t *plist;
 	int nee_all_count;             // entries of the estimateAllDirectLight layout
 	int faure_bytes;               // size of the permutation table (padded to 16 B)
 	int small_tables;              // materials + per-primitive normals fit k_shade / k_nee LDS
@@ -120,6 +127,8 @@ struct DevFilm
 	float filterw, table_scale;
 	int reach_fwd, reach_back;     // footprint reach: sources in [x - reach_fwd, x + reach_back]
 	int width, height, spp, tile;
+	int multipass;                 // AA_passes > 1: riVdC / riS sub-pixel positions
+	uint32_t sample_offset;        // base sampling offset + this pass's offset
 };
 
 // Per-chunk wavefront state (structure of arrays, capacity = chunk slots).
@@ -178,6 +187,16 @@ struct PhotonState
 	float4 *dep_b;       // (direction, colour.g)
 	float *dep_c;        // colour.b
 	uint8_t *dep_flag;   // 1 = a photon was stored in this slot
+};
+
+// ImageFilm::nextPass inputs (imagefilm.cc:259-420; aa_noise_params.h:27-46)
+struct DevAaParams
+{
+	int detect_color_noise;        // colorDifference over r, g, b, a as well as brightness
+	int dark_type;                 // 0 none, 1 linear, 2 curve
+	float dark_factor;             // AA_dark_threshold_factor
+	int variance_edge;             // AA_variance_edge_size
+	int variance_pixels;           // AA_variance_pixels (0: off)
 };
 
 struct DevCounters

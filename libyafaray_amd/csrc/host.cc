@@ -408,6 +408,18 @@ bool Scene::setupRender(const ParamMap &p)
 		log.error("Scene: please specify an _existing_ Background!!");
 	p.get("AA_passes", s.aa_passes);
 	p.get("AA_minsamples", s.aa_samples);
+	s.aa_inc_samples = s.aa_samples;   // scene.cc:584
+	p.get("AA_inc_samples", s.aa_inc_samples);
+	p.get("AA_threshold", s.aa_threshold);
+	p.get("AA_resampled_floor", s.aa_resampled_floor);
+	p.get("AA_sample_multiplier_factor", s.aa_sample_multiplier_factor);
+	p.get("AA_light_sample_multiplier_factor", s.aa_light_sample_multiplier_factor);
+	p.get("AA_indirect_sample_multiplier_factor", s.aa_indirect_sample_multiplier_factor);
+	p.get("AA_detect_color_noise", s.aa_detect_color_noise);
+	p.get("AA_dark_detection_type", s.aa_dark_detection_type);
+	p.get("AA_dark_threshold_factor", s.aa_dark_threshold_factor);
+	p.get("AA_variance_edge_size", s.aa_variance_edge_size);
+	p.get("AA_variance_pixels", s.aa_variance_pixels);
 	p.get("AA_clamp_samples", s.clamp_samples);
 	p.get("threads", s.threads);
 	p.get("threads_photons", s.threads_photons);
@@ -428,7 +440,8 @@ bool Scene::setupRender(const ParamMap &p)
 	p.get("tiles_order", s.tiles_order);
 	if(s.accelerator != "yafaray-kdtree-original" && s.accelerator != "yafaray-kdtree-multi-thread" && s.accelerator != "yafaray-simpletest")
 		log.warning("Accelerator type '" + s.accelerator + "' could not be created, using the GPU BVH instead.");  // accelerator.cc:47-51
-	if(s.aa_passes > 1) log.error("Scene: AA_passes > 1 (adaptive anti-aliasing) is not supported by the GPU core yet; rendering the first pass only");
+	if(s.aa_passes > 1 && s.aa_light_sample_multiplier_factor != 1.f)
+		log.warning("Scene: AA_light_sample_multiplier_factor != 1 is not supported by the GPU core; light samples stay constant over the passes");
 	if(s.xstart != 0 || s.ystart != 0) { log.error("Scene: cropped films (xstart/ystart != 0) are not supported by the GPU core yet"); return false; }
 	if(s.filter != "box" && s.filter != "gauss" && s.filter != "mitchell" && s.filter != "lanczos")
 	{
@@ -645,6 +658,23 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		F.tile = s.tile_size;
 		rp.shard_rank = shard_rank;
 		rp.shard_world = std::max(1, shard_world);
+		rp.aa.passes = std::max(1, s.aa_passes);
+		if(rp.aa.passes > 1 && rp.shard_world > 1)
+		{
+			// nextPass compares neighbouring pixels across the whole film; the tile-row shards only
+			// hold their own rows
+			log.error("Scene: AA_passes > 1 with tile-row sharding over several GPUs is not supported; rendering the first pass only");
+			rp.aa.passes = 1;
+		}
+		rp.aa.inc_samples = s.aa_inc_samples;
+		rp.aa.threshold = s.aa_threshold;
+		rp.aa.resampled_floor = s.aa_resampled_floor;
+		rp.aa.sample_multiplier_factor = s.aa_sample_multiplier_factor;
+		rp.aa.dev.detect_color_noise = s.aa_detect_color_noise ? 1 : 0;
+		rp.aa.dev.dark_type = s.aa_dark_detection_type == "linear" ? 1 : (s.aa_dark_detection_type == "curve" ? 2 : 0);   // scene.cc:624-626
+		rp.aa.dev.dark_factor = s.aa_dark_threshold_factor;
+		rp.aa.dev.variance_edge = s.aa_variance_edge_size;
+		rp.aa.dev.variance_pixels = s.aa_variance_pixels;
 		rp.chunk_slots = chunk_slots;
 		rp.profile = profile_kernels;
 		film_w = s.width;

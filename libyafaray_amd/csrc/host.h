@@ -121,6 +121,14 @@ struct RenderSetup
 	std::string integrator_name, background_name;
 	int width = 320, height = 240, xstart = 0, ystart = 0;
 	int aa_passes = 1, aa_samples = 1;
+	// adaptive AA (scene.cc:582-595; defaults of aa_noise_params.h:27-46)
+	int aa_inc_samples = 1;
+	float aa_threshold = 0.05f, aa_resampled_floor = 0.f, aa_sample_multiplier_factor = 1.f;
+	float aa_light_sample_multiplier_factor = 1.f, aa_indirect_sample_multiplier_factor = 1.f;
+	bool aa_detect_color_noise = false;
+	std::string aa_dark_detection_type = "none";
+	float aa_dark_threshold_factor = 0.f;
+	int aa_variance_edge_size = 10, aa_variance_pixels = 0;
 	float aa_pixelwidth = 1.5f, clamp_samples = 0.f;
 	std::string filter = "box";
 	int tile_size = 32;

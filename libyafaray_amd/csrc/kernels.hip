@@ -146,6 +146,21 @@ __device__ SampleCoord sampleCoord(const DevJob *jobs, int n_jobs, int width, in
 	return c;
 }
 
+// sample id -> pixel + sample index: the jobs' enumeration, or an adaptive pass's pixel list
+__device__ __forceinline__ SampleCoord sampleAt(const DevScene &S, const DevJob *jobs, int n_jobs, uint64_t sid)
+{
+	if(S.plist)
+	{
+		const uint32_t pix = S.plist[sid / (uint64_t)S.spp];
+		SampleCoord c;
+		c.x = (int)(pix % (uint32_t)S.width);
+		c.y = (int)(pix / (uint32_t)S.width);
+		c.s = (int)(sid % (uint64_t)S.spp);
+		return c;
+	}
+	return sampleCoord(jobs, n_jobs, S.width, S.tile, S.spp, sid);
+}
+
 __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueues Q, DevCounters cnt,
                                                  const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n)
 {
@@ -160,11 +175,17 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	if(i >= n) return;
 	const uint32_t g = (uint32_t)i / 256u;
 	const uint32_t a = (g % S.n_seg) * S.cap_a + (g / S.n_seg) * 256u + (uint32_t)i % 256u;
-	const SampleCoord sc = sampleCoord(jobs, n_jobs, S.width, S.tile, S.spp, chunk_base + (uint64_t)i);
+	const SampleCoord sc = sampleAt(S, jobs, n_jobs, chunk_base + (uint64_t)i);
 	// integrator_tiled.cc:313-335
 	const uint32_t offset = fnv32((uint32_t)sc.y * fnv32((uint32_t)sc.x));
+	const uint32_t sample_idx = S.base_offset + S.pass_offset + (uint32_t)sc.s;   // PixelSamplingData::sample_
 	float dx = 0.5f, dy = 0.5f;
-	if(S.spp > 1)
+	if(S.aa_multipass)
+	{
+		dx = riVdC(sample_idx, offset);
+		dy = riS(sample_idx, offset);
+	}
+	else if(S.spp > 1)
 	{
 		const float d_1 = 1.f / (float)S.spp;
 		dx = (0.5f + (float)sc.s) * d_1;
@@ -187,8 +208,8 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
 	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
 	// output is matched statistically — integrator_tiled.cc:272)
-	const uint32_t seed = fnv32((uint32_t)(chunk_base + (uint64_t)i) ^ S.rr_seed) + 123u;
-	P.pr[a] = make_uint4(offset, S.base_offset + (uint32_t)sc.s, 30903u, seed);
+	const uint32_t seed = fnv32((uint32_t)(chunk_base + (uint64_t)i) ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)) + 123u;
+	P.pr[a] = make_uint4(offset, sample_idx, 30903u, seed);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -985,7 +1006,7 @@ struct ShadeArgs
 
 __device__ __forceinline__ void writeSample(const ShadeArgs &A, uint32_t sid, C3 col, float alpha)
 {
-	const SampleCoord sc = sampleCoord(A.jobs, A.n_jobs, A.S.width, A.S.tile, A.S.spp, A.chunk_base + (uint64_t)sid);
+	const SampleCoord sc = sampleAt(A.S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
 	if(alpha > 1.f) alpha = 1.f;   // integrator_tiled.cc:399
 	A.samples[((size_t)sc.y * A.S.width + sc.x) * A.S.spp + sc.s] = f4(col, alpha);
 }
@@ -1453,8 +1474,8 @@ __device__ __forceinline__ uint64_t pixelRank(int x, int y, int W, int H, int ts
 // RF / RB: compile-time footprint reach (box and gauss filters: RF = 1, RB = 0 -> a 2x2 window
 // kept in registers); RF = RB = -1 selects the generic runtime window (<= 9x9).
 template<int RF, int RB>
-__global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, float4 *out, float *weights,
-                                              int y0, int y1, float clamp_samples)
+__global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, const uint8_t *flags, float4 *accum,
+                                              float4 *out, float *weights, int y0, int y1, float clamp_samples, int accumulate)
 {
 	constexpr bool kStatic = RF >= 0;
 	constexpr int kWin = kStatic ? (RF + RB + 1) * (RF + RB + 1) : 81;
@@ -1482,18 +1503,28 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 			rk[p] = r; sx[p] = xx; sy[p] = yy;
 		}
 	}
-	float wsum = 0.f;
-	float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+	const size_t p = (size_t)y * W + x;
+	// adaptive passes add to the film of the earlier passes (imagefilm.cc addSample: += per sample)
+	float wsum = accumulate ? weights[p] : 0.f;
+	float4 acc = accumulate ? accum[p] : make_float4(0.f, 0.f, 0.f, 0.f);
 	const float d_1 = 1.f / (float)spp;
 	for(int c = 0; c < n; ++c)
 	{
 		const int px = sx[c], py = sy[c];
 		const uint32_t offset = fnv32((uint32_t)py * fnv32((uint32_t)px));
 		const int ox = x - px, oy = y - py;
-		for(int s = 0; s < spp; ++s)
+		// adaptive pass: only resampled pixels splat.  (Skipping them while building the candidate list
+		// instead lost diagonal candidates in the unrolled k_film<1, 0> — tools/film_probe.hip.)
+		const int ns = (flags && !flags[(size_t)py * W + px]) ? 0 : spp;
+		for(int s = 0; s < ns; ++s)
 		{
 			float dx = 0.5f, dy = 0.5f;
-			if(spp > 1)
+			if(F.multipass)
+			{
+				dx = riVdC(F.sample_offset + (uint32_t)s, offset);
+				dy = riS(F.sample_offset + (uint32_t)s, offset);
+			}
+			else if(spp > 1)
 			{
 				dx = (0.5f + (float)s) * d_1;
 				dy = riLp((uint32_t)s + offset);
@@ -1528,9 +1559,14 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 			acc.w = acc.w + col.w * wt;
 		}
 	}
-	const size_t p = (size_t)y * W + x;
-	if(weights) weights[p] = wsum;
-	if(wsum != 0.f) out[p] = make_float4(acc.x / wsum, acc.y / wsum, acc.z / wsum, acc.w / wsum);
+	weights[p] = wsum;
+	accum[p] = acc;
+	// Rgba::normalized (color.h:554-558): colour * (1 / weight) — operator/ takes the reciprocal first
+	if(wsum != 0.f)
+	{
+		const float inv = 1.f / wsum;
+		out[p] = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+	}
 	else out[p] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
@@ -1967,7 +2003,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		}
 		col = col + c3(0.f);   // caustic map empty for the supported materials (montecarlo.cc:644)
 		col = col + c3(0.f);   // recursiveRaytrace: no specular/glossy components
-		const SampleCoord sc = sampleCoord(A.jobs, A.n_jobs, S.width, S.tile, S.spp, A.chunk_base + (uint64_t)sid);
+		const SampleCoord sc = sampleAt(S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
 		A.samples[((size_t)sc.y * S.width + sc.x) * S.spp + sc.s] = f4(col, alpha > 1.f ? 1.f : alpha);
 	}
 }
@@ -2167,15 +2203,16 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const D
 
 size_t yafamd_gather_lds_bytes(const DevScene *S) { return gatherLdsBytes(*S, S->small_tables != 0); }
 
-hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
-                              float clamp_samples, hipStream_t st)
+hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, const uint8_t *flags, float4 *accum, float4 *out,
+                              float *weights, int y0, int y1, float clamp_samples, int accumulate, hipStream_t st)
 {
 	if(y1 <= y0) return hipSuccess;
 	const dim3 grid((F->width + 255) / 256, y1 - y0);
 	if(F->reach_fwd == 1 && F->reach_back == 0)
-		hipLaunchKernelGGL((k_film<1, 0>), grid, dim3(256), 0, st, *F, samples, out, weights, y0, y1, clamp_samples);
+		hipLaunchKernelGGL((k_film<1, 0>), grid, dim3(256), 0, st, *F, samples, flags, accum, out, weights, y0, y1, clamp_samples, accumulate);
 	else
-		hipLaunchKernelGGL((k_film<-1, -1>), grid, dim3(256), 0, st, *F, samples, out, weights, y0, y1, clamp_samples);
+		hipLaunchKernelGGL((k_film<-1, -1>), grid, dim3(256), 0, st, *F, samples, flags, accum, out, weights, y0, y1, clamp_samples,
+		                   accumulate);
 	return hipGetLastError();
 }
 

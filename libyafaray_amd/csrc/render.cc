@@ -40,8 +40,10 @@ size_t yafamd_gather_lds_bytes(const DevScene *S);
 hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
                                 int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st);
 hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint2 *nodes_dev, int *depth_out, hipStream_t st);
-hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, float4 *out, float *weights, int y0, int y1,
-                              float clamp_samples, hipStream_t st);
+hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, const uint8_t *flags, float4 *accum, float4 *out,
+                              float *weights, int y0, int y1, float clamp_samples, int accumulate, hipStream_t st);
+hipError_t yafamd_aa_next_pass(const float4 *accum, const float *weights, int W, int H, int tile, const DevAaParams *prm,
+                               float threshold, uint8_t *flags, uint32_t *plist, uint32_t *count, hipStream_t st);
 hipError_t yafamd_launch_trace_rays(const DevScene *S, int any, const float4 *ro, const float4 *rd, int n, float *t_out,
                                     int *prim_out, int stack_depth, hipStream_t st);
 }
@@ -106,6 +108,7 @@ struct GpuRenderer::Impl
 	int faure_bytes = 0;
 	// frame buffers
 	Buf samples, film, weights, jobs;
+	Buf accum, aa_flags, aa_plist;   // unnormalised film (adaptive passes add to it), nextPass flags, resampled pixels
 	int film_w = 0, film_h = 0;
 	// chunk buffers
 	size_t slots_cap = 0;
@@ -125,7 +128,7 @@ struct GpuRenderer::Impl
 		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes})
 			b->release();
 		for(Buf *b : {&spill, &nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_dim, &faure_inv, &samples, &film,
-		              &weights, &jobs, &counters, &stats})
+		              &weights, &jobs, &counters, &stats, &accum, &aa_flags, &aa_plist})
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
 		for(hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
@@ -501,11 +504,13 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	// ---- frame buffers ----
 	if(!ensure(log_, d.samples, (size_t)W * H * spp * sizeof(float4))) return false;
 	if(!ensure(log_, d.film, (size_t)W * H * sizeof(float4))) return false;
+	if(!ensure(log_, d.accum, (size_t)W * H * sizeof(float4))) return false;
 	if(!ensure(log_, d.weights, (size_t)W * H * sizeof(float))) return false;
 	d.film_w = W;
 	d.film_h = H;
 	HIPCHECK(hipMemsetAsync(d.film.p, 0, (size_t)W * H * sizeof(float4), d.stream));
 	HIPCHECK(hipMemsetAsync(d.weights.p, 0, (size_t)W * H * sizeof(float), d.stream));
+	HIPCHECK(hipMemsetAsync(d.accum.p, 0, (size_t)W * H * sizeof(float4), d.stream));
 	// ---- chunk buffers ----
 	size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
 	const int K = std::max(1, S.nee_k);
@@ -595,20 +600,25 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	const int iters = (S.integrator == INT_PATH) ? 2 + n_paths * (S.bounces + 2) : 3;
 
 	// ---- events ----
-	const size_t n_chunks = (size_t)((total + M - 1) / M);
-	const size_t ev_needed = 2 + (rp.profile ? 4 * n_chunks * (size_t)iters : 0);
-	while(d.ev_pool.size() < ev_needed)
-	{
-		hipEvent_t e;
-		HIPCHECK(hipEventCreate(&e));
-		d.ev_pool.push_back(e);
-	}
+	auto ensureEvents = [&](size_t need) -> bool {
+		while(d.ev_pool.size() < need)
+		{
+			hipEvent_t e;
+			HIPCHECK(hipEventCreate(&e));
+			d.ev_pool.push_back(e);
+		}
+		return true;
+	};
+	if(!ensureEvents(2)) return false;
 	size_t ev_i = 2;
 	HIPCHECK(hipEventRecord(d.ev_pool[0], d.stream));
-	for(uint64_t base = 0; base < total; base += M)
+	// one pass: `n_total` camera samples (the jobs' enumeration, or S.plist x S.spp) through the wavefront
+	auto runSamples = [&](uint64_t n_total) -> bool {
+	if(rp.profile && !ensureEvents(ev_i + 4 * (size_t)((n_total + M - 1) / M) * (size_t)iters)) return false;
+	for(uint64_t base = 0; base < n_total; base += M)
 	{
 		if(canceled && *canceled) break;
-		const int n = (int)std::min<uint64_t>(M, total - base);
+		const int n = (int)std::min<uint64_t>(M, n_total - base);
 		HIPCHECK(yafamd_launch_camera(&S, &d.P[0], &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
 		int cur = 0;
 		for(int it = 0; it < iters; ++it)
@@ -629,9 +639,87 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			cur ^= 1;
 		}
 	}
+	return true;
+	};
+
+	// ---- pass 0 (every pixel), then the adaptive passes (TiledIntegrator::render, integrator_tiled.cc:172-231) ----
+	const int passes = std::max(1, rp.aa.passes);
+	S.aa_multipass = passes > 1 ? 1 : 0;
+	S.pass_offset = 0;
+	S.plist = nullptr;
+	rp.film.multipass = S.aa_multipass;
+	rp.film.sample_offset = S.base_offset;
+	if(!runSamples(total)) return false;
 	for(const auto &r : owned_rows_)
-		HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (float4 *)d.film.p, (float *)d.weights.p, r.first,
-		                            r.second, S.clamp_samples, d.stream));
+		HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, nullptr, (float4 *)d.accum.p, (float4 *)d.film.p,
+		                            (float *)d.weights.p, r.first, r.second, S.clamp_samples, 0, d.stream));
+	passes_done_ = 1;
+	uint64_t samples_total = total;
+	if(passes > 1)
+	{
+		if(!ensure(log_, d.aa_flags, (size_t)W * H) || !ensure(log_, d.aa_plist, (size_t)W * H * 4)) return false;
+		float threshold = rp.aa.threshold, sample_multiplier = 1.f;
+		bool threshold_changed = true;
+		int acum = spp, resampled = 0;
+		const int floor_pixels = (int)floorf(rp.aa.resampled_floor * (float)(W * H) / 100.f);
+		for(int pass = 1; pass < passes; ++pass)
+		{
+			if(canceled && *canceled) break;
+			sample_multiplier *= rp.aa.sample_multiplier_factor;
+			if(resampled <= 0.f && !threshold_changed) {}   // nextPass(..., skipNextPass = true)
+			else
+			{
+				uint32_t count = 0;
+				HIPCHECK(yafamd_aa_next_pass((const float4 *)d.accum.p, (const float *)d.weights.p, W, H, ts, &rp.aa.dev, threshold,
+				                             (uint8_t *)d.aa_flags.p, (uint32_t *)d.aa_plist.p, &count, d.stream));
+				resampled = (int)count;
+				threshold_changed = false;
+				if(const char *dump = getenv("YAFARAY_AMD_AA_DUMP"); dump && *dump)
+				{
+					// diagnostics: the pass's flags as W*H bytes
+					std::vector<uint8_t> hf((size_t)W * H);
+					HIPCHECK(hipMemcpy(hf.data(), d.aa_flags.p, hf.size(), hipMemcpyDeviceToHost));
+					if(FILE *f = fopen((std::string(dump) + "_pass" + std::to_string(pass) + ".bin").c_str(), "wb"))
+					{
+						fwrite(hf.data(), 1, hf.size(), f);
+						fclose(f);
+					}
+				}
+			}
+			const int n_pass = (int)ceilf(rp.aa.inc_samples * sample_multiplier);
+			{
+				std::ostringstream os;
+				os << "Rendering pass " << pass + 1 << " of " << passes << ", resampling " << resampled << " pixels x " << n_pass << " samples.";
+				log_.info(os.str());
+			}
+			if(resampled > 0 && n_pass > 0)
+			{
+				if(!ensure(log_, d.samples, (size_t)W * H * n_pass * sizeof(float4))) return false;
+				S.spp = n_pass;
+				S.pass_offset = (uint32_t)acum;
+				S.plist = (const uint32_t *)d.aa_plist.p;
+				rp.film.spp = n_pass;
+				rp.film.sample_offset = S.base_offset + (uint32_t)acum;
+				const uint64_t n_total = (uint64_t)resampled * (uint64_t)n_pass;
+				if(!runSamples(n_total)) return false;
+				HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (const uint8_t *)d.aa_flags.p, (float4 *)d.accum.p,
+				                            (float4 *)d.film.p, (float *)d.weights.p, 0, H, S.clamp_samples, 1, d.stream));
+				samples_total += n_total;
+				++passes_done_;
+			}
+			acum += n_pass;
+			if(resampled < floor_pixels)
+			{
+				const float ratio = std::min(8.f, ((float)floor_pixels / resampled));
+				threshold *= (1.f - 0.1f * ratio);
+				if(threshold > 0.f) threshold_changed = true;
+			}
+		}
+		S.spp = spp;
+		S.pass_offset = 0;
+		S.plist = nullptr;
+		rp.film.spp = spp;
+	}
 	HIPCHECK(hipEventRecord(d.ev_pool[1], d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	float ms = 0.f;
@@ -652,7 +740,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	stats_.shadow_rays = hs.shadow_rays;
 	stats_.node_visits = hs.node_visits;
 	stats_.tri_tests = hs.tri_tests;
-	stats_.samples = total;
+	stats_.samples = samples_total;
 	stats_.render_seconds = ms * 1e-3;
 	stats_.trace_kernel_ms = 0.0;
 	stats_.shade_kernel_ms = 0.0;

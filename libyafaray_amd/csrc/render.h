@@ -41,10 +41,23 @@ struct PhotonParams
 	int threads = -1;          // threads_photons: photon count rounded to a multiple (:437); <= 0 -> 1
 };
 
+// adaptive anti-aliasing (scene.cc:582-595, aa_noise_params.h:27-46; TiledIntegrator::render,
+// integrator_tiled.cc:172-231)
+struct AaParams
+{
+	int passes = 1;
+	int inc_samples = 1;               // AA_inc_samples (defaults to AA_minsamples)
+	float threshold = 0.05f;
+	float resampled_floor = 0.f;       // % of the pixels
+	float sample_multiplier_factor = 1.f;
+	DevAaParams dev{0, 0, 0.f, 10, 0};
+};
+
 struct RenderParams
 {
 	DevScene scene;                      // pointers filled by the renderer
 	PhotonParams pm;
+	AaParams aa;
 	DevFilm film;
 	int shard_rank = 0, shard_world = 1;
 	int chunk_slots = 1 << 25;   // samples in flight per wavefront chunk
@@ -59,6 +72,7 @@ class GpuRenderer
 		bool ready();
 		bool upload(HostScene &hs);   // fills hs.bvh's metadata when the BVH is built on the device
 		bool render(RenderParams &rp, volatile bool *canceled);
+		int lastPassCount() const { return passes_done_; }   // AA passes rendered by the last render()
 		bool download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h);
 		bool filmToDevice(void *dst, int y0, int y1);
 		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
@@ -73,6 +87,7 @@ class GpuRenderer
 		Logger &log_;
 		yafaray_amd_stats_t stats_{};
 		std::vector<std::pair<int, int>> owned_rows_;
+		int passes_done_ = 0;
 };
 
 } // namespace yafamd

@@ -92,6 +92,17 @@ class Render:
     base_sampling_offset: int = 0
     clamp_samples: float = 0.0
     accelerator: str = "yafaray-kdtree-original"
+    # adaptive anti-aliasing (scene.cc:582-595; defaults of aa_noise_params.h:27-46)
+    aa_passes: int = 1
+    aa_inc_samples: int = 0                 # 0: AA_minsamples (scene.cc:584)
+    aa_threshold: float = 0.05
+    aa_resampled_floor: float = 0.0
+    aa_sample_multiplier_factor: float = 1.0
+    aa_detect_color_noise: bool = False
+    aa_dark_detection_type: str = "none"    # none | linear | curve
+    aa_dark_threshold_factor: float = 0.0
+    aa_variance_edge_size: int = 10
+    aa_variance_pixels: int = 0
     # photonmapping (integrator_photon_mapping.cc:765-850); final gathering is not supported
     pm_photons: int = 100000
     pm_search: int = 50
@@ -374,7 +385,17 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetInt("width", r.width)
     api.paramsSetInt("height", r.height)
     api.paramsSetInt("AA_minsamples", r.aa_samples)
-    api.paramsSetInt("AA_passes", 1)
+    api.paramsSetInt("AA_passes", r.aa_passes)
+    if r.aa_inc_samples > 0:
+        api.paramsSetInt("AA_inc_samples", r.aa_inc_samples)
+    api.paramsSetFloat("AA_threshold", r.aa_threshold)
+    api.paramsSetFloat("AA_resampled_floor", r.aa_resampled_floor)
+    api.paramsSetFloat("AA_sample_multiplier_factor", r.aa_sample_multiplier_factor)
+    api.paramsSetBool("AA_detect_color_noise", r.aa_detect_color_noise)
+    api.paramsSetString("AA_dark_detection_type", r.aa_dark_detection_type)
+    api.paramsSetFloat("AA_dark_threshold_factor", r.aa_dark_threshold_factor)
+    api.paramsSetInt("AA_variance_edge_size", r.aa_variance_edge_size)
+    api.paramsSetInt("AA_variance_pixels", r.aa_variance_pixels)
     api.paramsSetString("filter_type", r.filter_type)
     api.paramsSetFloat("AA_pixelwidth", r.aa_pixelwidth)
     api.paramsSetFloat("AA_clamp_samples", r.clamp_samples)

@@ -49,7 +49,10 @@ class yc_render(C.Structure):
                 ("ray_min_dist", C.c_float), ("base_sampling_offset", C.c_int), ("clamp_samples", C.c_float),
                 ("threads", C.c_int), ("rr_seed", C.c_uint32), ("pm_photons", C.c_int), ("pm_search", C.c_int),
                 ("pm_diffuse_radius", C.c_float), ("pm_bounces", C.c_int), ("pm_caustics", C.c_int),
-                ("pm_threads", C.c_int)]
+                ("pm_threads", C.c_int), ("aa_passes", C.c_int), ("aa_inc_samples", C.c_int), ("aa_threshold", C.c_float),
+                ("aa_resampled_floor", C.c_float), ("aa_sample_multiplier_factor", C.c_float),
+                ("aa_detect_color_noise", C.c_int), ("aa_dark_detection_type", C.c_int),
+                ("aa_dark_threshold_factor", C.c_float), ("aa_variance_edge_size", C.c_int), ("aa_variance_pixels", C.c_int)]
 
 
 class yc_scene(C.Structure):
@@ -269,6 +272,14 @@ class OracleScene:
         rp.rr_seed = rr_seed
         rp.pm_photons, rp.pm_search, rp.pm_diffuse_radius = r.pm_photons, r.pm_search, r.pm_diffuse_radius
         rp.pm_bounces, rp.pm_caustics, rp.pm_threads = r.pm_bounces, int(r.pm_caustics), r.threads_photons
+        rp.aa_passes = max(1, r.aa_passes)
+        rp.aa_inc_samples = r.aa_inc_samples if r.aa_inc_samples > 0 else r.aa_samples
+        rp.aa_threshold, rp.aa_resampled_floor = r.aa_threshold, r.aa_resampled_floor
+        rp.aa_sample_multiplier_factor = r.aa_sample_multiplier_factor
+        rp.aa_detect_color_noise = int(r.aa_detect_color_noise)
+        rp.aa_dark_detection_type = {"linear": 1, "curve": 2}.get(r.aa_dark_detection_type, 0)
+        rp.aa_dark_threshold_factor = r.aa_dark_threshold_factor
+        rp.aa_variance_edge_size, rp.aa_variance_pixels = r.aa_variance_edge_size, r.aa_variance_pixels
         self.sc = sc
         self.spec = spec
 

@@ -9,6 +9,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
+#include <string>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -206,6 +208,24 @@ static inline float riLp(uint32_t i, uint32_t r = 0)
 		if(i & 1) r ^= v;
 	return std::max(0.f, std::min(1.f, static_cast<float>(static_cast<double>(r) * sample_mult_ratio)));
 }
+
+// integrator_tiled.cc:319-335: sub-pixel position of sample `sample` (sample_idx = pass offset + sample)
+static inline void sampleOffsets(int passes, int n_samples, int sample, uint32_t sample_idx, uint32_t offset, float &dx, float &dy)
+{
+	dx = 0.5f;
+	dy = 0.5f;
+	if(passes > 1)
+	{
+		dx = riVdC(sample_idx, offset);
+		dy = riS(sample_idx, offset);
+	}
+	else if(n_samples > 1)
+	{
+		dx = (0.5f + static_cast<float>(sample)) * (1.f / static_cast<float>(n_samples));
+		dy = riLp(sample + offset);
+	}
+}
+
 // sample.h:132-149 (FNV-1a over the 4 little-endian bytes)
 static inline uint32_t fnv32(uint32_t value)
 {
@@ -1608,22 +1628,17 @@ class Renderer
 		}
 
 		// integrator_tiled.cc:288-405 for one pixel: writes n_samples RGBA
-		void renderPixel(Thread &th, Mwc &rng, int i, int j, float *out) const
+		// integrator_tiled.cc:303-345: n_samples camera samples of pixel (j, i); pass_offs = the
+		// pass offset plus the film's base sampling offset (renderPass, :240-250)
+		void renderPixel(Thread &th, Mwc &rng, int i, int j, float *out, int n_samples, int pass_offs) const
 		{
 			const yc_render &rp = sc_.rp;
-			const int n_samples = rp.aa_samples;
-			const int pass_offs = rp.base_sampling_offset;
-			const float d_1 = 1.f / static_cast<float>(n_samples);
 			const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
 			for(int sample = 0; sample < n_samples; ++sample)
 			{
 				const uint32_t sample_idx = pass_offs + sample;
-				float dx = 0.5f, dy = 0.5f;
-				if(n_samples > 1)
-				{
-					dx = (0.5f + static_cast<float>(sample)) * d_1;
-					dy = riLp(sample + offset);
-				}
+				float dx, dy;
+				sampleOffsets(rp.aa_passes, n_samples, sample, sample_idx, offset, dx, dy);
 				Ray ray = shootRay(j + dx, i + dy);
 				C3 col;
 				float alpha;
@@ -1694,6 +1709,114 @@ struct Film
 	}
 };
 
+// imagefilm.cc:799-815
+static float darkThresholdCurve(float b)
+{
+	if(b <= 0.10f) return 0.0001f;
+	else if(b <= 0.20f) return (0.0001f + (b - 0.10f) * (0.0010f - 0.0001f) / 0.10f);
+	else if(b <= 0.30f) return (0.0010f + (b - 0.20f) * (0.0020f - 0.0010f) / 0.10f);
+	else if(b <= 0.40f) return (0.0020f + (b - 0.30f) * (0.0035f - 0.0020f) / 0.10f);
+	else if(b <= 0.50f) return (0.0035f + (b - 0.40f) * (0.0055f - 0.0035f) / 0.10f);
+	else if(b <= 0.60f) return (0.0055f + (b - 0.50f) * (0.0075f - 0.0055f) / 0.10f);
+	else if(b <= 0.70f) return (0.0075f + (b - 0.60f) * (0.0100f - 0.0075f) / 0.10f);
+	else if(b <= 0.80f) return (0.0100f + (b - 0.70f) * (0.0150f - 0.0100f) / 0.10f);
+	else if(b <= 0.90f) return (0.0150f + (b - 0.80f) * (0.0250f - 0.0150f) / 0.10f);
+	else if(b <= 1.00f) return (0.0250f + (b - 0.90f) * (0.0400f - 0.0250f) / 0.10f);
+	else if(b <= 1.20f) return (0.0400f + (b - 1.00f) * (0.0800f - 0.0400f) / 0.20f);
+	else if(b <= 1.40f) return (0.0800f + (b - 1.20f) * (0.0950f - 0.0800f) / 0.20f);
+	else if(b <= 1.80f) return (0.0950f + (b - 1.40f) * (0.1000f - 0.0950f) / 0.40f);
+	else return 0.1000f;
+}
+
+struct Rgba4 { float r, g, b, a; };
+
+// Rgba::normalized (color.h:554-558, operator/ :312-316)
+static Rgba4 filmColor(const Film &film, int W, int x, int y)
+{
+	const size_t p = (size_t)y * W + x;
+	const float w = film.weight[p];
+	if(w == 0.f) return {0.f, 0.f, 0.f, 0.f};
+	const float f = 1.f / w;
+	return {film.rgba[4 * p] * f, film.rgba[4 * p + 1] * f, film.rgba[4 * p + 2] * f, film.rgba[4 * p + 3] * f};
+}
+
+// Rgba::colorDifference (color.h:450-467), col2Bri (color.h:61)
+static float colorDifference(const Rgba4 &a, const Rgba4 &c2, bool rgb)
+{
+	const float bri_a = 0.2126f * a.r + 0.7152f * a.g + 0.0722f * a.b;
+	const float bri_c = 0.2126f * c2.r + 0.7152f * c2.g + 0.0722f * c2.b;
+	float d = std::abs(bri_c - bri_a);
+	if(rgb)
+	{
+		const float rd = std::abs(c2.r - a.r), gd = std::abs(c2.g - a.g), bd = std::abs(c2.b - a.b), ad = std::abs(c2.a - a.a);
+		if(d < rd) d = rd;
+		if(d < gd) d = gd;
+		if(d < bd) d = bd;
+		if(d < ad) d = ad;
+	}
+	return d;
+}
+
+// ImageFilm::nextPass (imagefilm.cc:259-420) with adaptive_aa = true and no DebugSamplingFactor
+// layer: flags the pixels the next pass resamples; returns their count.  doMoreSamples
+// (:672-675) resamples every pixel when the threshold is <= 0.
+static int aaNextPass(const Film &film, int W, int H, const yc_render &rp, float threshold, std::vector<uint8_t> &flags)
+{
+	flags.assign((size_t)W * H, 0);
+	if(!(threshold > 0.f))
+	{
+		flags.assign((size_t)W * H, 1);
+		return W * H;
+	}
+	const bool rgb = rp.aa_detect_color_noise != 0;
+	const int half = rp.aa_variance_edge_size / 2;
+	auto set = [&](int x, int y) { flags[(size_t)y * W + x] = 1; };
+	for(int y = 0; y < H; ++y)
+		for(int x = 0; x < W; ++x) flags[(size_t)y * W + x] = (film.weight[(size_t)y * W + x] > 0.f) ? 0 : 1;
+	float th = threshold;
+	for(int y = 0; y < H - 1; ++y)
+		for(int x = 0; x < W - 1; ++x)
+		{
+			const Rgba4 pc = filmColor(film, W, x, y);
+			const float bri = 0.2126f * std::abs(pc.r) + 0.7152f * std::abs(pc.g) + 0.0722f * std::abs(pc.b);   // abscol2Bri
+			if(rp.aa_dark_detection_type == 1 && rp.aa_dark_threshold_factor > 0.f)
+				th = threshold * ((1.f - rp.aa_dark_threshold_factor) + (bri * rp.aa_dark_threshold_factor));
+			else if(rp.aa_dark_detection_type == 2) th = darkThresholdCurve(bri);
+			if(colorDifference(pc, filmColor(film, W, x + 1, y), rgb) >= th) { set(x, y); set(x + 1, y); }
+			if(colorDifference(pc, filmColor(film, W, x, y + 1), rgb) >= th) { set(x, y); set(x, y + 1); }
+			if(colorDifference(pc, filmColor(film, W, x + 1, y + 1), rgb) >= th) { set(x, y); set(x + 1, y + 1); }
+			if(x > 0 && colorDifference(pc, filmColor(film, W, x - 1, y + 1), rgb) >= th) { set(x, y); set(x - 1, y + 1); }
+			if(rp.aa_variance_pixels > 0)
+			{
+				int vx = 0, vy = 0;
+				for(int xd = -half; xd < half - 1; ++xd)
+				{
+					int xi = x + xd;
+					if(xi < 0) xi = 0;
+					else if(xi >= W - 1) xi = W - 2;
+					if(colorDifference(filmColor(film, W, xi, y), filmColor(film, W, xi + 1, y), rgb) >= th) ++vx;
+				}
+				for(int yd = -half; yd < half - 1; ++yd)
+				{
+					int yi = y + yd;
+					if(yi < 0) yi = 0;
+					else if(yi >= H - 1) yi = H - 2;
+					if(colorDifference(filmColor(film, W, x, yi), filmColor(film, W, x, yi + 1), rgb) >= th) ++vy;
+				}
+				if(vx + vy >= rp.aa_variance_pixels)
+					for(int xd = -half; xd < half; ++xd)
+						for(int yd = -half; yd < half; ++yd)
+						{
+							const int xi = std::min(std::max(x + xd, 0), W - 1), yi = std::min(std::max(y + yd, 0), H - 1);
+							set(xi, yi);
+						}
+			}
+		}
+	int n = 0;
+	for(uint8_t f : flags) n += f;
+	return n;
+}
+
 static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float *out_w, yc_counters *ctr)
 {
 	Scene sc(*s);
@@ -1703,7 +1826,8 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 	const int W = rp.width, H = rp.height;
 	if(y1 <= y0) { y0 = 0; y1 = H; }
 	Film film(W, H, *sc.film, rp.clamp_samples);
-	const int spp = rp.aa_samples;
+	const int passes = std::max(1, rp.aa_passes);
+	if(passes > 1 && (y0 != 0 || y1 != H)) return -2;   // adaptive passes need the whole film
 	std::vector<Tile> all = tilesLinear(W, H, rp.tile_size);
 	std::vector<Tile> tiles;
 	for(const Tile &t : all)
@@ -1713,63 +1837,102 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 	}
 	const int nthreads = std::max(1, rp.threads);
 	std::vector<Renderer::Thread> th(nthreads);
-	// sample loop: tiles in parallel, each tile sequential (reference renderWorker), then the film
-	// pass in linear tile order (reference single-thread order), so output is thread-count free.
-	const size_t band = 256;
-	for(size_t t0 = 0; t0 < tiles.size(); t0 += band)
-	{
-		const size_t t1 = std::min(tiles.size(), t0 + band);
-		std::vector<std::vector<float>> buf(t1 - t0);
-		std::atomic<size_t> next{t0};
-		auto worker = [&](int tid) {
-			for(;;)
+	std::vector<uint8_t> flags;   // imagefilm flags_ (adaptive passes)
+	// renderPass (integrator_tiled.cc:236-267 / renderTile :269-345): tiles in parallel, each tile
+	// sequential (reference renderWorker), then the film pass in linear tile order (reference
+	// single-thread order), so the output is thread-count free.  `adaptive`: only flagged pixels.
+	auto renderPass = [&](int n_samples, int pass_offs, bool adaptive) {
+		const size_t band = 256;
+		for(size_t t0 = 0; t0 < tiles.size(); t0 += band)
+		{
+			const size_t t1 = std::min(tiles.size(), t0 + band);
+			std::vector<std::vector<float>> buf(t1 - t0);
+			std::atomic<size_t> next{t0};
+			auto worker = [&](int tid) {
+				for(;;)
+				{
+					const size_t k = next++;
+					if(k >= t1) break;
+					const Tile &a = tiles[k];
+					std::vector<float> &b = buf[k - t0];
+					b.resize((size_t)a.w * a.h * n_samples * 4);
+					// integrator_tiled.cc:272 — RandomGenerator(rand() + offset*(resx*y0+x0) + 123)
+					Mwc rng(rp.rr_seed + pass_offs * (sc.cam.resx * a.y + a.x) + 123);
+					for(int i = a.y; i < a.y + a.h; ++i)
+						for(int j = a.x; j < a.x + a.w; ++j)
+						{
+							if(adaptive && !flags[(size_t)i * W + j]) continue;   // doMoreSamples (:290)
+							R.renderPixel(th[tid], rng, i, j, &b[(((size_t)(i - a.y) * a.w + (j - a.x)) * n_samples) * 4], n_samples,
+							              pass_offs);
+						}
+				}
+			};
+			if(nthreads == 1) worker(0);
+			else
 			{
-				const size_t k = next++;
-				if(k >= t1) break;
+				std::vector<std::thread> pool;
+				for(int tt = 0; tt < nthreads; ++tt) pool.emplace_back(worker, tt);
+				for(auto &p : pool) p.join();
+			}
+			for(size_t k = t0; k < t1; ++k)
+			{
 				const Tile &a = tiles[k];
-				std::vector<float> &b = buf[k - t0];
-				b.resize((size_t)a.w * a.h * spp * 4);
-				// integrator_tiled.cc:272 — RandomGenerator(rand() + offset*(resx*y0+x0) + 123)
-				Mwc rng(rp.rr_seed + rp.base_sampling_offset * (sc.cam.resx * a.y + a.x) + 123);
+				const std::vector<float> &b = buf[k - t0];
 				for(int i = a.y; i < a.y + a.h; ++i)
 					for(int j = a.x; j < a.x + a.w; ++j)
-						R.renderPixel(th[tid], rng, i, j, &b[(((size_t)(i - a.y) * a.w + (j - a.x)) * spp) * 4]);
+					{
+						if(adaptive && !flags[(size_t)i * W + j]) continue;
+						const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
+						for(int sample = 0; sample < n_samples; ++sample)
+						{
+							float dx, dy;
+							sampleOffsets(passes, n_samples, sample, pass_offs + sample, offset, dx, dy);
+							film.addSample(j, i, dx, dy, &b[((((size_t)(i - a.y) * a.w + (j - a.x)) * n_samples) + sample) * 4]);
+						}
+					}
 			}
-		};
-		if(nthreads == 1) worker(0);
+		}
+	};
+	// TiledIntegrator::render (integrator_tiled.cc:172-231)
+	const int base = rp.base_sampling_offset;
+	renderPass(rp.aa_samples, base, false);
+	float threshold = rp.aa_threshold;
+	float sample_multiplier = 1.f;
+	bool threshold_changed = true;
+	int acum = rp.aa_samples, resampled = 0;
+	const int floor_pixels = (int)floorf(rp.aa_resampled_floor * (float)(W * H) / 100.f);
+	for(int pass = 1; pass < passes; ++pass)
+	{
+		sample_multiplier *= rp.aa_sample_multiplier_factor;
+		if(resampled <= 0.f && !threshold_changed) {}   // nextPass(..., skipNextPass = true): flags untouched
 		else
 		{
-			std::vector<std::thread> pool;
-			for(int tt = 0; tt < nthreads; ++tt) pool.emplace_back(worker, tt);
-			for(auto &p : pool) p.join();
-		}
-		for(size_t k = t0; k < t1; ++k)
-		{
-			const Tile &a = tiles[k];
-			const std::vector<float> &b = buf[k - t0];
-			const float d_1 = 1.f / static_cast<float>(spp);
-			for(int i = a.y; i < a.y + a.h; ++i)
-				for(int j = a.x; j < a.x + a.w; ++j)
+			resampled = aaNextPass(film, W, H, rp, threshold, flags);
+			threshold_changed = false;
+			if(const char *dump = getenv("YC_AA_DUMP"); dump && *dump)
+				if(FILE *f = fopen((std::string(dump) + "_pass" + std::to_string(pass) + ".bin").c_str(), "wb"))
 				{
-					const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
-					for(int sample = 0; sample < spp; ++sample)
-					{
-						float dx = 0.5f, dy = 0.5f;
-						if(spp > 1)
-						{
-							dx = (0.5f + static_cast<float>(sample)) * d_1;
-							dy = riLp(sample + offset);
-						}
-						film.addSample(j, i, dx, dy, &b[((((size_t)(i - a.y) * a.w + (j - a.x)) * spp) + sample) * 4]);
-					}
+					fwrite(flags.data(), 1, flags.size(), f);
+					fclose(f);
 				}
 		}
+		const int n_pass = (int)ceilf(rp.aa_inc_samples * sample_multiplier);
+		if(resampled > 0) renderPass(n_pass, base + acum, true);
+		acum += n_pass;
+		if(resampled < floor_pixels)
+		{
+			const float ratio = std::min(8.f, ((float)floor_pixels / resampled));
+			threshold *= (1.f - 0.1f * ratio);
+			if(threshold > 0.f) threshold_changed = true;
+		}
 	}
-	// imagefilm.cc:590-617 flush: colour / weight (Rgba::normalized, color.h:554-558)
+	// imagefilm.cc:590-617 flush: Rgba::normalized (color.h:554-558) = colour * (1 / weight)
+	// (operator/ takes the reciprocal first, color.h:312-316)
 	for(size_t p = 0; p < (size_t)W * H; ++p)
 	{
 		const float wt = film.weight[p];
-		for(int k = 0; k < 4; ++k) out_rgba[4 * p + k] = (wt != 0.f) ? film.rgba[4 * p + k] / wt : 0.f;
+		const float inv = (wt != 0.f) ? 1.f / wt : 0.f;
+		for(int k = 0; k < 4; ++k) out_rgba[4 * p + k] = (wt != 0.f) ? film.rgba[4 * p + k] * inv : 0.f;
 		if(out_w) out_w[p] = wt;
 	}
 	if(ctr)

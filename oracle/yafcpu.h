@@ -76,6 +76,17 @@ typedef struct {
 	int pm_caustics;          // "caustics": caustic photons are shot but only stored after specular
 	                          // bounces, which the supported materials never produce
 	int pm_threads;           // threads_photons: the photon count is rounded to a multiple (:437)
+	// adaptive anti-aliasing (scene.cc:582-595, aa_noise_params.h:27-46; integrator_tiled.cc:172-231)
+	int aa_passes;
+	int aa_inc_samples;
+	float aa_threshold;
+	float aa_resampled_floor;            // % of the pixels
+	float aa_sample_multiplier_factor;
+	int aa_detect_color_noise;
+	int aa_dark_detection_type;          // 0 none, 1 linear, 2 curve
+	float aa_dark_threshold_factor;
+	int aa_variance_edge_size;
+	int aa_variance_pixels;
 } yc_render;
 
 typedef struct {

@@ -155,6 +155,34 @@ def test_path_noRR_sphere_matches_oracle(product, oracle_built, bvh, monkeypatch
     assert st["closest_rays"] == octr[0]
 
 
+ADAPTIVE_AA = {
+    # DirectLight on test01, 3 passes of 2 extra samples
+    "dl-3pass": lambda: scenes.test01(64, 64, spp=2).with_render(aa_passes=3, aa_inc_samples=2, aa_threshold=0.02),
+    # every nextPass option: dark-curve thresholds, colour-noise detection, variance windows, the
+    # resampled-floor threshold decay and a growing sample multiplier
+    "pt-all-options": lambda: scenes.cornell(48, 40, spp=2, bounces=4, rr=False).with_render(
+        aa_passes=4, aa_inc_samples=1, aa_threshold=0.01, aa_dark_detection_type="curve", aa_detect_color_noise=True,
+        aa_variance_pixels=3, aa_variance_edge_size=6, aa_resampled_floor=60.0, aa_sample_multiplier_factor=1.5),
+    "pt-linear-dark": lambda: scenes.cornell(40, 32, spp=1, bounces=3, rr=False).with_render(
+        aa_passes=3, aa_inc_samples=3, aa_threshold=0.03, aa_dark_detection_type="linear", aa_dark_threshold_factor=0.7),
+    # threshold 0: every pixel is resampled in every pass (doMoreSamples)
+    "threshold-0": lambda: scenes.test01(40, 40, spp=1).with_render(aa_passes=2, aa_inc_samples=2, aa_threshold=0.0),
+}
+
+
+@pytest.mark.parametrize("case", list(ADAPTIVE_AA))
+def test_adaptive_aa_matches_oracle(product, oracle_built, case):
+    """Adaptive anti-aliasing passes (integrator_tiled.cc:172-231, imagefilm.cc:259-420): the GPU's
+    nextPass flags, resampled pixel lists and accumulated film against the oracle's restatement."""
+    spec = ADAPTIVE_AA[case]()
+    rgba, w, st = product.render_spec(spec, chunk_slots=4096)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32)), f"{(w != ow).sum()} weight mismatches"
+    d = ulp_diff(rgba, orgba)
+    assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
+    assert st["samples"] > spec.render.width * spec.render.height * spec.render.aa_samples   # later passes ran
+
+
 def test_path_gauss_filter_and_multichunk(product, oracle_built):
     spec = scenes.cornell(72, 40, spp=3, bounces=4, rr=False, filter_type="gauss", pixelwidth=1.5, tile_size=16)
     rgba, w, _ = product.render_spec(spec, chunk_slots=1024)

@@ -92,3 +92,18 @@ def test_generators():
     assert len(s.tris) == 34 + 707 * 707 * 2 == 999732
     t = scenes.test01(8, 8)
     assert len(t.tris) == 74
+
+
+def test_oracle_adaptive_passes_add_samples():
+    """The oracle's adaptive AA restatement (integrator_tiled.cc:172-231): with threshold 0 every
+    pixel is resampled, so a second pass adds weight everywhere; with an unreachable threshold
+    only the never-rendered pixels (none) would be, so the film equals pass 0 alone."""
+    import numpy as np
+    from libyafaray_amd import scenes
+    from oracle import oracle
+    base = scenes.test01(24, 24, spp=2)
+    _, w1, _ = oracle.OracleScene(base.with_render(aa_passes=2, aa_threshold=1e9), threads=4).render()
+    _, w2, _ = oracle.OracleScene(base.with_render(aa_passes=2, aa_threshold=0.0, aa_inc_samples=2), threads=4).render()
+    assert (w2 > w1).all()
+    _, w3, _ = oracle.OracleScene(base.with_render(aa_passes=1), threads=4).render()
+    assert not np.array_equal(w1, w3)   # multipass sub-pixel positions (riVdC / riS) differ from pass-1 ones
