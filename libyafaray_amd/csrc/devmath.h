@@ -41,6 +41,7 @@ namespace yafamd
 struct X87Const { double hi, lo; };
 constexpr X87Const kPi = {0x1.921fb54442d18p+1, 0x1.1a8p-53};
 constexpr X87Const kDivPiBy2 = {0x1.921fb54442d18p+0, 0x1.1a8p-54};
+constexpr X87Const kDivPiBy4 = {0x1.921fb54442d18p-1, 0x1.1a8p-55};
 constexpr X87Const kDiv1ByPi = {0x1.45f306dc9c883p-2, -0x1.6bp-56};
 constexpr X87Const kMultPiBy2 = {0x1.921fb54442d18p+2, 0x1.1a8p-52};
 constexpr X87Const kDiv1By2Pi = {0x1.45f306dc9c883p-3, -0x1.6bp-57};
@@ -302,6 +303,36 @@ YD float maxComp(C3 c) { return fmaxf(c.r, fmaxf(c.g, c.b)); }
 // include/math/random.h:56-104
 // ---------------------------------------------------------------------------------------------
 YD float clamp01(float v) { return fmaxf(0.f, fminf(1.f, v)); }
+
+// Halton(base) of the camera lens (halton.h:47-81): setStart(start), then k getNext() calls; the
+// value after the k-th call (incremental radical inverse in double, as the reference)
+YD float haltonNext(uint32_t base, uint32_t start, int k)
+{
+	const double inv_base = 1.0 / static_cast<double>(base);
+	double factor = inv_base, value = 0.0;
+	while(start > 0)
+	{
+		value += static_cast<double>(start % base) * factor;
+		start /= base;
+		factor *= inv_base;
+	}
+	for(int i = 0; i < k; ++i)
+	{
+		const double r = 0.9999999999 - value;
+		if(inv_base < r) value += inv_base;
+		else
+		{
+			double hh = 0.0, h = inv_base;
+			while(h >= r)
+			{
+				hh = h;
+				h *= inv_base;
+			}
+			value += hh + h - 1.0;
+		}
+	}
+	return clamp01(static_cast<float>(value));
+}
 
 YD uint32_t bitReverse32(uint32_t v)
 {

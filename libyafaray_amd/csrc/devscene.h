@@ -58,6 +58,11 @@ struct DevCamera
 {
 	float pos[4], vright[4], vup[4], vto[4], cam_z[4], near_p[4], far_p[4];
 	int resx, resy, pad0, pad1;
+	// depth of field (camera_perspective.cc:28-52, 71-146): aperture * camera axes, bokeh polygon
+	float dof_rt[4], dof_up[4];
+	float aperture, dof_distance;
+	int bokeh_type, bokeh_bias;    // BokehType (0 disk1, 1 disk2, 3..6 polygon, 7 ring), BkhBiasType
+	float ls[16];                  // polygon vertices (cos, sin) pairs
 };
 
 // A band of pixel rows rendered as a run of tiles (imagesplitter.cc:30-49 linear order):

@@ -339,7 +339,10 @@ bool Scene::createCamera(const std::string &name, const ParamMap &p)
 	p.get("aspect_ratio", c.aspect);
 	p.get("nearClip", c.near_clip);
 	p.get("farClip", c.far_clip);
-	if(c.aperture != 0.f) { log.error("Camera '" + name + "': depth of field (aperture != 0) is not supported by the GPU core yet"); return false; }
+	p.get("dof_distance", c.dof_distance);
+	p.get("bokeh_type", c.bokeh_type);
+	p.get("bokeh_bias", c.bokeh_bias);
+	p.get("bokeh_rotation", c.bokeh_rotation);
 	cameras[name] = c;
 	return true;
 }
@@ -558,6 +561,35 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		put(S.cam.far_p, add(pos, mul(cam_z, c.far_clip)));
 		S.cam.resx = c.resx;
 		S.cam.resy = c.resy;
+		// depth of field (camera_perspective.cc:28-52, 59-62, 212-224)
+		S.cam.aperture = c.aperture;
+		S.cam.dof_distance = c.dof_distance;
+		put(S.cam.dof_rt, mul(cam_x, c.aperture));
+		put(S.cam.dof_up, mul(cam_y, c.aperture));
+		{
+			int bt = 0;
+			if(c.bokeh_type == "disk2") bt = 1;
+			else if(c.bokeh_type == "triangle") bt = 3;
+			else if(c.bokeh_type == "square") bt = 4;
+			else if(c.bokeh_type == "pentagon") bt = 5;
+			else if(c.bokeh_type == "hexagon") bt = 6;
+			else if(c.bokeh_type == "ring") bt = 7;
+			S.cam.bokeh_type = bt;
+			S.cam.bokeh_bias = c.bokeh_bias == "center" ? 1 : (c.bokeh_bias == "edge" ? 2 : 0);
+			for(float &v : S.cam.ls) v = 0.f;
+			if(bt >= 3 && bt <= 6)
+			{
+				// math::degToRad and mult_pi_by_2 / ns are long double expressions rounded to float
+				float w = static_cast<float>(c.bokeh_rotation * hm::div_pi_by_180);
+				const float wi = static_cast<float>(hm::mult_pi_by_2 / static_cast<float>(bt));
+				for(int i = 0; i < (bt + 2) * 2; i += 2)
+				{
+					S.cam.ls[i] = hm::sinf_fast(w + static_cast<float>(hm::div_pi_by_2));   // math::cos (FAST_TRIG)
+					S.cam.ls[i + 1] = hm::sinf_fast(w);
+					w += wi;
+				}
+			}
+		}
 		// integrator + render parameters
 		S.integrator = (itype == "pathtracing") ? INT_PATH : (itype == "photonmapping") ? INT_PHOTON : INT_DIRECT;
 		if(S.integrator == INT_PHOTON)

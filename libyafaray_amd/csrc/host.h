@@ -114,6 +114,8 @@ struct CameraDesc
 	int resx = 320, resy = 200;
 	float aspect = 1.f, focal = 1.f, aperture = 0.f;
 	float near_clip = 0.f, far_clip = -1.f;
+	float dof_distance = 0.f, bokeh_rotation = 0.f;
+	std::string bokeh_type = "disk1", bokeh_bias = "uniform";
 };
 
 struct RenderSetup

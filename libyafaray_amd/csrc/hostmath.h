@@ -15,6 +15,7 @@ using LD = long double;
 constexpr LD num_pi = 3.1415926535897932384626433832795L;
 constexpr LD div_pi_by_2 = 1.5707963267948966192313216916398L;
 constexpr LD mult_pi_by_2 = 6.283185307179586476925286766559L;
+constexpr LD div_pi_by_180 = 0.01745329251994329576923690768489L;
 constexpr LD div_1_by_2pi = 0.15915494309189533576888376337251L;
 constexpr LD div_4_by_pi = 1.2732395447351626861510701069801L;
 constexpr LD div_4_by_squared_pi = 0.40528473456935108577551785283891L;

@@ -146,6 +146,64 @@ __device__ SampleCoord sampleCoord(const DevJob *jobs, int n_jobs, int width, in
 	return c;
 }
 
+// camera_perspective.cc:71-85
+__device__ __forceinline__ float biasDist(int bias, float r)
+{
+	if(bias == 1) return sqrtf(sqrtf(r) * r);           // BbCenter
+	if(bias == 2) return sqrtf(1.f - r * r);            // BbEdge
+	return sqrtf(r);                                    // BbNone
+}
+
+// vector.cc:128-163 (the long double pi/4 products round like x87)
+__device__ __forceinline__ void shirleyDisk(float r_1, float r_2, float &u, float &v)
+{
+	float phi = 0.f, r = 0.f;
+	const float a = 2.f * r_1 - 1.f, b = 2.f * r_2 - 1.f;
+	if(a > -b)
+	{
+		if(a > b) { r = a; phi = x87mul(kDivPiBy4, b / a); }
+		else { r = b; phi = x87mul(kDivPiBy4, 2.f - a / b); }
+	}
+	else
+	{
+		if(a < b) { r = -a; phi = x87mul(kDivPiBy4, 4.f + b / a); }
+		else
+		{
+			r = -b;
+			phi = (b != 0) ? x87mul(kDivPiBy4, 6.f - a / b) : 0.f;
+		}
+	}
+	u = r * fcos(phi);
+	v = r * fsin(phi);
+}
+
+// camera_perspective.cc:87-124 getLensUv (sampleTsd for the polygon bokehs)
+__device__ void lensUv(const DevCamera &c, float r_1, float r_2, float &u, float &v)
+{
+	const int t = c.bokeh_type;
+	if(t >= 3 && t <= 6)
+	{
+		const float fn = static_cast<float>(t);
+		int idx = int(r_1 * fn);
+		r_1 = (r_1 - ((float)idx) / fn) * fn;
+		r_1 = biasDist(c.bokeh_bias, r_1);
+		const float b_1 = r_1 * r_2;
+		const float b_0 = r_1 - b_1;
+		idx <<= 1;
+		u = c.ls[idx] * b_0 + c.ls[idx + 2] * b_1;
+		v = c.ls[idx + 1] * b_0 + c.ls[idx + 3] * b_1;
+	}
+	else if(t == 1 || t == 7)
+	{
+		const float w = 6.28318548f * r_2;   // (float)math::mult_pi_by_2 * r_2
+		if(t == 7) r_1 = sqrtf((float)0.707106781 + (float)0.292893218);
+		else r_1 = biasDist(c.bokeh_bias, r_1);
+		u = r_1 * fcos(w);
+		v = r_1 * fsin(w);
+	}
+	else shirleyDisk(r_1, r_2, u, v);
+}
+
 // sample id -> pixel + sample index: the jobs' enumeration, or an adaptive pass's pixel list
 __device__ __forceinline__ SampleCoord sampleAt(const DevScene &S, const DevJob *jobs, int n_jobs, uint64_t sid)
 {
@@ -200,8 +258,21 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	const V3 cz = v3(c.cam_z[0], c.cam_z[1], c.cam_z[2]);
 	const float tmin = dot(cz, v3(c.near_p[0], c.near_p[1], c.near_p[2]) - pos) / dot(dir, cz);
 	const float tmax = dot(cz, v3(c.far_p[0], c.far_p[1], c.far_p[2]) - pos) / dot(dir, cz);
+	V3 from = pos;
+	if(c.aperture != 0.f)
+	{
+		// integrator_tiled.cc:314-316, 336-340: Halton(3) / Halton(5) lens streams started at the
+		// pass offset + pixel offset, one getNext() per sample; camera_perspective.cc:137-144
+		const uint32_t hstart = S.base_offset + S.pass_offset + offset;
+		const float lu = haltonNext(3u, hstart, sc.s + 1), lv = haltonNext(5u, hstart, sc.s + 1);
+		float u, v;
+		lensUv(c, lu, lv, u, v);
+		const V3 li = v3(c.dof_rt[0], c.dof_rt[1], c.dof_rt[2]) * u + v3(c.dof_up[0], c.dof_up[1], c.dof_up[2]) * v;
+		from = from + li;
+		dir = normalize(dir * c.dof_distance - li);
+	}
 	Q.slot[a] = i;          // sample id within the chunk travels with the queue entry
-	Q.ray_o[a] = f4(pos, tmin);
+	Q.ray_o[a] = f4(from, tmin);
 	Q.ray_d[a] = f4(dir, tmax);
 	P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
 	P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));   // stage

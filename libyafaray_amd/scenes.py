@@ -62,6 +62,12 @@ class Camera:
     aspect_ratio: float = 1.0
     near_clip: float = 0.0
     far_clip: float = -1.0
+    # depth of field (camera_perspective.cc:190-224)
+    aperture: float = 0.0
+    dof_distance: float = 0.0
+    bokeh_type: str = "disk1"       # disk1 disk2 triangle square pentagon hexagon ring
+    bokeh_bias: str = "uniform"     # uniform center edge
+    bokeh_rotation: float = 0.0
 
 
 @dataclass
@@ -345,6 +351,12 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetFloat("aspect_ratio", cam.aspect_ratio)
     api.paramsSetFloat("nearClip", cam.near_clip)
     api.paramsSetFloat("farClip", cam.far_clip)
+    if cam.aperture != 0.0:
+        api.paramsSetFloat("aperture", cam.aperture)
+        api.paramsSetFloat("dof_distance", cam.dof_distance)
+        api.paramsSetString("bokeh_type", cam.bokeh_type)
+        api.paramsSetString("bokeh_bias", cam.bokeh_bias)
+        api.paramsSetFloat("bokeh_rotation", cam.bokeh_rotation)
     api.createCamera("cam")
     api.paramsClearAll()
     api.paramsSetString("camera_name", "cam")

@@ -37,7 +37,8 @@ class yc_light(C.Structure):
 class yc_camera(C.Structure):
     _fields_ = [("from_", C.c_float * 3), ("to", C.c_float * 3), ("up", C.c_float * 3), ("resx", C.c_int),
                 ("resy", C.c_int), ("focal", C.c_float), ("aspect", C.c_float), ("near_clip", C.c_float),
-                ("far_clip", C.c_float)]
+                ("far_clip", C.c_float), ("aperture", C.c_float), ("dof_distance", C.c_float),
+                ("bokeh_rotation", C.c_float), ("bokeh_type", C.c_int), ("bokeh_bias", C.c_int)]
 
 
 class yc_render(C.Structure):
@@ -250,6 +251,9 @@ class OracleScene:
         sc.cam.resx, sc.cam.resy = cam.resx, cam.resy
         sc.cam.focal, sc.cam.aspect = cam.focal, cam.aspect_ratio
         sc.cam.near_clip, sc.cam.far_clip = cam.near_clip, cam.far_clip
+        sc.cam.aperture, sc.cam.dof_distance, sc.cam.bokeh_rotation = cam.aperture, cam.dof_distance, cam.bokeh_rotation
+        sc.cam.bokeh_type = {"disk2": 1, "triangle": 3, "square": 4, "pentagon": 5, "hexagon": 6, "ring": 7}.get(cam.bokeh_type, 0)
+        sc.cam.bokeh_bias = {"center": 1, "edge": 2}.get(cam.bokeh_bias, 0)
         r = s.render
         rp = sc.rp
         rp.integrator = {"pathtracing": YC_INT_PATH, "photonmapping": YC_INT_PHOTON}.get(r.integrator, YC_INT_DIRECT)

@@ -32,6 +32,8 @@ constexpr LD div_4_by_squared_pi = 0.40528473456935108577551785283891L;
 constexpr LD log2e = 1.4426950408889634073599246810019L;
 constexpr LD ln2 = 0.69314718055994530941723212145818L;
 constexpr LD sample_mult_ratio = 0.00000000023283064365386962890625L;
+constexpr LD div_pi_by_4 = 0.78539816339744830961566084581988L;
+constexpr LD div_pi_by_180 = 0.01745329251994329576923690768489L;
 constexpr float min_raydist_global = 0.00005f;   // include/common/yafaray_common.h:28
 
 // ---------------------------------------------------------------------------------------------
@@ -481,7 +483,114 @@ struct Camera
 	V3 position, vright, vup, vto, cam_z;
 	V3 near_p, far_p;
 	int resx, resy;
+	// camera_perspective.cc:28-52, 59-62: depth of field
+	float aperture = 0.f, dof_distance = 0.f;
+	V3 dof_rt, dof_up;
+	int bokeh_type = 0, bokeh_bias = 0;
+	std::vector<float> ls;
 };
+
+// halton.h:30-81 (the camera's lens streams)
+struct HaltonSeq
+{
+	unsigned int base;
+	double inv_base, value = 0.0;
+	explicit HaltonSeq(int b) : base(b), inv_base(1.0 / static_cast<double>(b)) {}
+	void setStart(unsigned int start)
+	{
+		double factor = inv_base;
+		value = 0.0;
+		while(start > 0)
+		{
+			value += static_cast<double>(start % base) * factor;
+			start /= base;
+			factor *= inv_base;
+		}
+	}
+	float getNext()
+	{
+		const double r = 0.9999999999 - value;
+		if(inv_base < r) value += inv_base;
+		else
+		{
+			double hh = 0.0, h = inv_base;
+			while(h >= r)
+			{
+				hh = h;
+				h *= inv_base;
+			}
+			value += hh + h - 1.0;
+		}
+		return std::max(0.f, std::min(1.f, static_cast<float>(value)));
+	}
+};
+
+// camera_perspective.cc:71-85
+static float biasDist(int bias, float r)
+{
+	switch(bias)
+	{
+		case 1: return std::sqrt(std::sqrt(r) * r);
+		case 2: return std::sqrt(1.f - r * r);
+		default: return std::sqrt(r);
+	}
+}
+
+// vector.cc:128-163
+static void shirleyDisk(float r_1, float r_2, float &u, float &v)
+{
+	float phi = 0.f, r = 0.f;
+	const float a = 2.f * r_1 - 1.f;
+	const float b = 2.f * r_2 - 1.f;
+	if(a > -b)
+	{
+		if(a > b) { r = a; phi = div_pi_by_4 * (b / a); }
+		else { r = b; phi = div_pi_by_4 * (2.f - a / b); }
+	}
+	else
+	{
+		if(a < b) { r = -a; phi = div_pi_by_4 * (4.f + b / a); }
+		else
+		{
+			r = -b;
+			if(b != 0) phi = div_pi_by_4 * (6.f - a / b);
+			else phi = 0.f;
+		}
+	}
+	u = r * fcos(phi);
+	v = r * fsin(phi);
+}
+
+// camera_perspective.cc:87-124
+static void lensUv(const Camera &c, float r_1, float r_2, float &u, float &v)
+{
+	switch(c.bokeh_type)
+	{
+		case 3: case 4: case 5: case 6:
+		{
+			const auto fn = static_cast<float>(c.bokeh_type);
+			int idx = int(r_1 * fn);
+			r_1 = (r_1 - ((float)idx) / fn) * fn;
+			r_1 = biasDist(c.bokeh_bias, r_1);
+			const float b_1 = r_1 * r_2;
+			const float b_0 = r_1 - b_1;
+			idx <<= 1;
+			u = c.ls[idx] * b_0 + c.ls[idx + 2] * b_1;
+			v = c.ls[idx + 1] * b_0 + c.ls[idx + 3] * b_1;
+			break;
+		}
+		case 1: case 7:
+		{
+			const float w = (float)mult_pi_by_2 * r_2;
+			if(c.bokeh_type == 7) r_1 = std::sqrt((float)0.707106781 + (float)0.292893218);
+			else r_1 = biasDist(c.bokeh_bias, r_1);
+			u = r_1 * fcos(w);
+			v = r_1 * fsin(w);
+			break;
+		}
+		default: shirleyDisk(r_1, r_2, u, v);
+	}
+}
 
 struct Ray
 {
@@ -663,6 +772,24 @@ Scene::Scene(const yc_scene &s)
 	cam.vto = (cam_z * c.focal) - V3(static_cast<float>(0.5) * (cam.vup + cam.vright));
 	cam.vup = V3(cam.vup.x / (float)c.resy, cam.vup.y / (float)c.resy, cam.vup.z / (float)c.resy);
 	cam.vright = V3(cam.vright.x / (float)c.resx, cam.vright.y / (float)c.resx, cam.vright.z / (float)c.resx);
+	cam.aperture = c.aperture;
+	cam.dof_distance = c.dof_distance;
+	cam.dof_rt = c.aperture * cam_x;
+	cam.dof_up = c.aperture * cam_y;
+	cam.bokeh_type = c.bokeh_type;
+	cam.bokeh_bias = c.bokeh_bias;
+	if(c.bokeh_type >= 3 && c.bokeh_type <= 6)
+	{
+		float w = c.bokeh_rotation * div_pi_by_180, wi = mult_pi_by_2 / (float)c.bokeh_type;   // degToRad
+		const int ns = (c.bokeh_type + 2) * 2;
+		cam.ls.resize(ns);
+		for(int i = 0; i < ns; i += 2)
+		{
+			cam.ls[i] = fcos(w);
+			cam.ls[i + 1] = fsin(w);
+			w += wi;
+		}
+	}
 	film.reset(new FilmTable(rp.filter, rp.filter_size));
 	buildBvh();
 }
@@ -1615,7 +1742,8 @@ class Renderer
 		}
 
 		// camera_perspective.cc:128-146 + plane.h:37-40
-		Ray shootRay(float px, float py) const
+		// camera_perspective.cc:128-146
+		Ray shootRay(float px, float py, float lu = 0.5f, float lv = 0.5f) const
 		{
 			const Camera &c = sc_.cam;
 			Ray ray;
@@ -1624,6 +1752,15 @@ class Renderer
 			ray.dir.normalize();
 			ray.tmin = dot(c.cam_z, (c.near_p - ray.from)) / dot(ray.dir, c.cam_z);
 			ray.tmax = dot(c.cam_z, (c.far_p - ray.from)) / dot(ray.dir, c.cam_z);
+			if(c.aperture != 0.f)
+			{
+				float u, v;
+				lensUv(c, lu, lv, u, v);
+				const V3 li = c.dof_rt * u + c.dof_up * v;
+				ray.from = ray.from + li;
+				ray.dir = (ray.dir * c.dof_distance) - li;
+				ray.dir.normalize();
+			}
 			return ray;
 		}
 
@@ -1634,12 +1771,22 @@ class Renderer
 		{
 			const yc_render &rp = sc_.rp;
 			const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
+			// :284-285, 315-316: lens streams Halton(3) / Halton(5) started at pass offset + pixel offset
+			HaltonSeq hal_u(3), hal_v(5);
+			hal_u.setStart(pass_offs + offset);
+			hal_v.setStart(pass_offs + offset);
 			for(int sample = 0; sample < n_samples; ++sample)
 			{
 				const uint32_t sample_idx = pass_offs + sample;
 				float dx, dy;
 				sampleOffsets(rp.aa_passes, n_samples, sample, sample_idx, offset, dx, dy);
-				Ray ray = shootRay(j + dx, i + dy);
+				float lens_u = 0.5f, lens_v = 0.5f;
+				if(sc_.cam.aperture != 0.f)
+				{
+					lens_u = hal_u.getNext();
+					lens_v = hal_v.getNext();
+				}
+				Ray ray = shootRay(j + dx, i + dy, lens_u, lens_v);
 				C3 col;
 				float alpha;
 				if(rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha);

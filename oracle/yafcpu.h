@@ -48,6 +48,9 @@ typedef struct {
 	int resx, resy;
 	float focal, aspect;
 	float near_clip, far_clip;
+	float aperture, dof_distance, bokeh_rotation;   // depth of field (camera_perspective.cc:28-52)
+	int bokeh_type;                                 // BokehType: 0 disk1, 1 disk2, 3..6 polygons, 7 ring
+	int bokeh_bias;                                 // 0 uniform, 1 center, 2 edge
 } yc_camera;
 
 typedef struct {

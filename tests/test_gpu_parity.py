@@ -183,6 +183,39 @@ def test_adaptive_aa_matches_oracle(product, oracle_built, case):
     assert st["samples"] > spec.render.width * spec.render.height * spec.render.aa_samples   # later passes ran
 
 
+DOF_CASES = {
+    "disk1": dict(aperture=0.15, dof_distance=3.5),
+    "disk2-center": dict(aperture=0.2, dof_distance=3.0, bokeh_type="disk2", bokeh_bias="center"),
+    "triangle-edge-rot": dict(aperture=0.1, dof_distance=4.0, bokeh_type="triangle", bokeh_bias="edge", bokeh_rotation=30.0),
+    "square": dict(aperture=0.12, dof_distance=3.8, bokeh_type="square"),
+    "pentagon": dict(aperture=0.12, dof_distance=3.8, bokeh_type="pentagon", bokeh_rotation=7.0),
+    "hexagon-rot": dict(aperture=0.1, dof_distance=4.0, bokeh_type="hexagon", bokeh_rotation=-12.5),
+    "ring": dict(aperture=0.1, dof_distance=4.0, bokeh_type="ring"),
+}
+
+
+@pytest.mark.parametrize("case", list(DOF_CASES))
+def test_depth_of_field_matches_oracle(product, oracle_built, case):
+    """Perspective camera with aperture (camera_perspective.cc:71-146): Halton(3)/(5) lens streams,
+    every bokeh shape and bias, against the oracle — PT without RR, <= 4 ULP."""
+    spec = scenes.cornell(48, 36, spp=4, bounces=3, rr=False).with_camera(**DOF_CASES[case])
+    rgba, w, _ = product.render_spec(spec, chunk_slots=2048)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    d = ulp_diff(rgba, orgba)
+    assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
+
+
+def test_depth_of_field_with_adaptive_passes(product, oracle_built):
+    """DOF lens streams restart at every pass's offset (integrator_tiled.cc:314-316)."""
+    spec = scenes.test01(40, 40, spp=2).with_camera(aperture=0.3, dof_distance=8.0, bokeh_type="pentagon").with_render(
+        aa_passes=3, aa_inc_samples=2, aa_threshold=0.02)
+    rgba, w, _ = product.render_spec(spec)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    assert ulp_diff(rgba, orgba).max() <= 4
+
+
 def test_path_gauss_filter_and_multichunk(product, oracle_built):
     spec = scenes.cornell(72, 40, spp=3, bounces=4, rr=False, filter_type="gauss", pixelwidth=1.5, tile_size=16)
     rgba, w, _ = product.render_spec(spec, chunk_slots=1024)
