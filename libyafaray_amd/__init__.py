@@ -78,6 +78,14 @@ def lib():
             "yafaray_addVertex": (i, [vp, d, d, d]),
             "yafaray_addVertexWithOrco": (i, [vp, d, d, d, d, d, d]),
             "yafaray_addTriangle": (b, [vp, i, i, i]),
+            "yafaray_addTriangleWithUv": (b, [vp, i, i, i, i, i, i]),
+            "yafaray_addUv": (i, [vp, f, f]),
+            "yafaray_addNormal": (None, [vp, d, d, d]),
+            "yafaray_smoothMesh": (b, [vp, cp, d]),
+            "yafaray_createImage": (vp, [vp, cp]),
+            "yafaray_setImageColor": (b, [vp, i, i, f, f, f, f]),
+            "yafaray_getImageColor": (b, [vp, i, i, C.POINTER(f), C.POINTER(f), C.POINTER(f), C.POINTER(f)]),
+            "yafaray_paramsSetMatrix": (None, [vp, cp] + [f] * 16 + [b]),
             "yafaray_paramsSetVector": (None, [vp, cp, d, d, d]),
             "yafaray_paramsSetString": (None, [vp, cp, cp]),
             "yafaray_paramsSetBool": (None, [vp, cp, b]),
@@ -174,6 +182,15 @@ class Interface:
         def call(*args):
             return fn(self.h, *[_b(a) for a in args])
         return call
+
+    # --- images (the handle is the first argument, not the interface) ---
+    def setImageColor(self, image, x, y, r, g, b, a):
+        return self.L.yafaray_setImageColor(image, x, y, r, g, b, a)
+
+    def getImageColor(self, image, x, y):
+        c = [C.c_float() for _ in range(4)]
+        ok = self.L.yafaray_getImageColor(image, x, y, *[C.byref(v) for v in c])
+        return tuple(v.value for v in c) if ok else None
 
     # --- bulk geometry (extensions) ---
     def addVertices(self, xyz):

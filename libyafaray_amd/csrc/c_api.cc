@@ -4,6 +4,7 @@
 #include "../../include/yafaray_amd.h"
 #include "../../include/yafaray_c_api.h"
 #include "host.h"
+#include "texture.h"
 #include "hostmath.h"
 #include "render.h"
 
@@ -82,14 +83,14 @@ int yafaray_addVertex(yafaray_Interface_t *interface, double x, double y, double
 
 int yafaray_addVertexWithOrco(yafaray_Interface_t *interface, double x, double y, double z, double ox, double oy, double oz)
 {
-	(void)ox; (void)oy; (void)oz;   // orco coordinates only feed texture mapping (not in the GPU core yet)
-	return yafaray_addVertex(interface, x, y, z);
+	Scene *s = I(interface)->sc();
+	return s ? s->addVertexWithOrco((float)x, (float)y, (float)z, (float)ox, (float)oy, (float)oz) : -1;
 }
 
 void yafaray_addNormal(yafaray_Interface_t *interface, double nx, double ny, double nz)
 {
-	(void)nx; (void)ny; (void)nz;
-	I(interface)->logger.warning("Scene: per-vertex normals (smooth shading) are not supported by the GPU core yet; ignored");
+	Scene *s = I(interface)->sc();
+	if(s) s->addNormal((float)nx, (float)ny, (float)nz);
 }
 
 yafaray_bool_t yafaray_addTriangle(yafaray_Interface_t *interface, int a, int b, int c)
@@ -100,22 +101,20 @@ yafaray_bool_t yafaray_addTriangle(yafaray_Interface_t *interface, int a, int b,
 
 yafaray_bool_t yafaray_addTriangleWithUv(yafaray_Interface_t *interface, int a, int b, int c, int uv_a, int uv_b, int uv_c)
 {
-	(void)uv_a; (void)uv_b; (void)uv_c;
-	return yafaray_addTriangle(interface, a, b, c);
+	Scene *s = I(interface)->sc();
+	return (s && s->addTriangle(a, b, c, uv_a, uv_b, uv_c)) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
 }
 
 int yafaray_addUv(yafaray_Interface_t *interface, float u, float v)
 {
-	(void)u; (void)v;
-	(void)interface;
-	return 0;
+	Scene *s = I(interface)->sc();
+	return s ? s->addUv(u, v) : 0;
 }
 
 yafaray_bool_t yafaray_smoothMesh(yafaray_Interface_t *interface, const char *name, double angle)
 {
-	(void)angle;
-	I(interface)->logger.warning(std::string("Scene: smoothMesh('") + (name ? name : "") + "') ignored: the GPU core shades flat (N = Ng)");
-	return YAFARAY_BOOL_TRUE;
+	Scene *s = I(interface)->sc();
+	return (s && s->smoothMesh(name ? name : "", (float)angle)) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
 }
 
 yafaray_bool_t yafaray_addInstance(yafaray_Interface_t *interface, const char *base_object_name, float, float, float, float, float, float, float, float, float, float, float, float, float, float, float, float)
@@ -248,7 +247,13 @@ void yafaray_setCurrentMaterial(yafaray_Interface_t *interface, const char *name
 
 CREATE(yafaray_createObject, createObject)
 CREATE(yafaray_createLight, createLight)
-CREATE(yafaray_createMaterial, createMaterial)
+yafaray_bool_t yafaray_createMaterial(yafaray_Interface_t *interface, const char *name)
+{
+	// interface.cc:183-186: the material factory also receives the pushed node lists
+	Interface *it = I(interface);
+	Scene *s = it->sc();
+	return (s && s->createMaterial(name ? name : "", it->params, it->nodes_params)) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
 CREATE(yafaray_createCamera, createCamera)
 CREATE(yafaray_createBackground, createBackground)
 CREATE(yafaray_createIntegrator, createIntegrator)
@@ -256,8 +261,9 @@ CREATE(yafaray_createRenderView, createRenderView)
 
 yafaray_bool_t yafaray_createTexture(yafaray_Interface_t *interface, const char *name)
 {
-	I(interface)->logger.warning(std::string("Scene: texture '") + (name ? name : "") + "' accepted but not evaluated by the GPU core yet");
-	return YAFARAY_BOOL_TRUE;
+	Interface *it = I(interface);
+	Scene *s = it->sc();
+	return (s && s->createTexture(name ? name : "", it->params)) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
 }
 
 yafaray_bool_t yafaray_createVolumeRegion(yafaray_Interface_t *interface, const char *name)
@@ -382,42 +388,31 @@ void yafaray_setInputColorSpace(yafaray_Interface_t *interface, const char *colo
 	it->input_gamma = gamma_val;
 }
 
-// ---- images (textures are not evaluated yet; the buffers are kept for the API contract) ----
-struct ImageHandle
-{
-	int w, h;
-	std::vector<float> px;
-};
-
+// ---- images (scene.cc:518-521, image.cc:38-137): owned by the scene, as in the reference (scene.h:214) ----
 yafaray_Image_t *yafaray_createImage(yafaray_Interface_t *interface, const char *name)
 {
 	Interface *it = I(interface);
-	int w = 0, h = 0;
-	it->params.get("width", w);
-	it->params.get("height", h);
-	auto *img = new ImageHandle{std::max(1, w), std::max(1, h), {}};
-	img->px.assign((size_t)img->w * img->h * 4, 0.f);
-	it->logger.verbose(std::string("Scene: image '") + (name ? name : "") + "' created (texture evaluation is not part of the GPU core yet)");
-	static std::vector<std::unique_ptr<ImageHandle>> keep;   // owned by the library, as in the reference (scene.h:214)
-	keep.emplace_back(img);
-	return reinterpret_cast<yafaray_Image_t *>(img);
+	Scene *s = it->sc();
+	return s ? reinterpret_cast<yafaray_Image_t *>(s->createImage(name ? name : "", it->params)) : nullptr;
 }
 
+// Image::setColor through the image's buffer type (quantised as the reference stores it)
 yafaray_bool_t yafaray_setImageColor(yafaray_Image_t *image, int x, int y, float r, float g, float b, float a)
 {
-	auto *img = reinterpret_cast<ImageHandle *>(image);
+	auto *img = reinterpret_cast<HostImage *>(image);
 	if(!img || x < 0 || y < 0 || x >= img->w || y >= img->h) return YAFARAY_BOOL_FALSE;
-	float *p = &img->px[4 * ((size_t)y * img->w + x)];
-	p[0] = r; p[1] = g; p[2] = b; p[3] = a;
+	const float c[4] = {r, g, b, a};
+	img->setColor(x, y, c);
 	return YAFARAY_BOOL_TRUE;
 }
 
 yafaray_bool_t yafaray_getImageColor(const yafaray_Image_t *image, int x, int y, float *r, float *g, float *b, float *a)
 {
-	auto *img = reinterpret_cast<const ImageHandle *>(image);
+	auto *img = reinterpret_cast<const HostImage *>(image);
 	if(!img || x < 0 || y < 0 || x >= img->w || y >= img->h) return YAFARAY_BOOL_FALSE;
-	const float *p = &img->px[4 * ((size_t)y * img->w + x)];
-	*r = p[0]; *g = p[1]; *b = p[2]; *a = p[3];
+	float c[4];
+	img->getColor(x, y, c);
+	*r = c[0]; *g = c[1]; *b = c[2]; *a = c[3];
 	return YAFARAY_BOOL_TRUE;
 }
 

@@ -36,7 +36,78 @@ struct DevMaterial
 	float comp[4];          // getComponents() (no shader nodes)
 	uint32_t c_flags[4];
 	uint32_t c_index[4];
+	// shader-node program (material_node.cc:60-100: the nodes the roots depend on, in evaluation
+	// order): nodes [node0, node0 + n_nodes) of DevScene::shader_nodes; roots are program-local
+	// indices (-1: none).  emit_strength multiplies the diffuse shader's colour in emit()
+	// (material_shiny_diffuse.cc:242-247).
+	int node0, n_nodes, diffuse_root, drefl_root;
+	float emit_strength;
+	int pad2, pad3, pad4;
 };
+
+// ---- textures and shader nodes (src/texture/texture_image.cc, src/shader/shader_node_*.cc) ----
+enum : int { INTERP_NONE = 0, INTERP_BILINEAR = 1, INTERP_BICUBIC = 2 };
+// ImageTexture::ClipMode (include/texture/texture_image.h:62), same numbering
+enum : int { CLIP_EXTEND = 0, CLIP_CLIP = 1, CLIP_CLIPCUBE = 2, CLIP_REPEAT = 3, CLIP_CHECKER = 4 };
+enum : uint32_t
+{
+	TEXF_MIRROR_X = 1u, TEXF_MIRROR_Y = 2u, TEXF_ROT90 = 4u, TEXF_CROPX = 8u, TEXF_CROPY = 16u,
+	TEXF_CHECK_ODD = 32u, TEXF_CHECK_EVEN = 64u, TEXF_ADJ = 128u, TEXF_CLAMP = 256u
+};
+// ColorSpace (include/color/color.h:36)
+enum : int { CS_RAW_MANUAL_GAMMA = 1, CS_LINEAR_RGB = 2, CS_SRGB = 3, CS_XYZ_D65 = 4 };
+
+// An image texture: its texels are the image buffer's getColor() values (already quantised the
+// way the reference's optimized/compressed buffers store them), row-major in DevScene::texels.
+struct DevTexture
+{
+	uint32_t texel0;
+	int w, h, interp;
+	int clip, xrep, yrep;
+	uint32_t flags;
+	float cropminx, cropmaxx, cropminy, cropmaxy;
+	float checker_dist, intensity, contrast, saturation;
+	float hue, fr, fg, fb;      // hue already / 60 (texture.cc:139)
+	int raw_cs;                 // original colour space of the image file (getRawColor)
+	float raw_gamma;
+	int pad0, pad1;
+};
+
+enum : int { NODE_VALUE = 0, NODE_MIX = 1, NODE_LAYER = 2, NODE_TEXMAP = 3 };
+// MixNode variants (shader_node_basic.cc:656-672) and LayerNode blend modes (shader_node_layer.cc:320-330)
+enum : int { BLEND_MIX = 0, BLEND_ADD, BLEND_MULT, BLEND_SUB, BLEND_SCREEN, BLEND_DIV, BLEND_DIFF, BLEND_DARK, BLEND_LIGHT, BLEND_OVERLAY };
+// LayerNode flags (shader_node_layer.h) + the booleans of the node
+enum : uint32_t
+{
+	LAYER_RGB_TO_INT = 1u, LAYER_STENCIL = 2u, LAYER_NEGATIVE = 4u, LAYER_DO_COLOR = 8u, LAYER_DO_SCALAR = 16u,
+	LAYER_COLOR_INPUT = 32u, LAYER_USE_ALPHA = 64u
+};
+// TextureMapperNode::Coords / Projection (shader_node_basic.h)
+enum : int { TC_UV = 0, TC_GLOBAL, TC_ORCO, TC_TRANSFORMED, TC_NORMAL, TC_WINDOW };
+enum : int { PROJ_PLAIN = 0, PROJ_CUBE, PROJ_TUBE, PROJ_SPHERE };
+
+struct DevNode
+{
+	int type, mode;            // NODE_*, BLEND_* (mix / layer)
+	int in[3];                 // program-local inputs (-1: constant).  mix: input1, input2, factor;
+	                           // layer: input, upper_layer
+	uint32_t flags;            // layer: LAYER_*; mapper: bit 0 = do_scalar
+	int tex;                   // mapper: texture index
+	int coords, proj, map_x, map_y, map_z;
+	int pad0, pad1, pad2, pad3;
+	float c0[4], c1[4];        // value: colour+alpha; mix: color1, color2; layer: def_col, upper_col
+	float f[4];                // value: scalar; mix: cfactor, val1, val2; layer: colfac, valfac, def_val, upper_val
+	float scale[4], offset[4]; // mapper (offset already doubled, shader_node_basic.cc:372)
+	float mtx[16];             // mapper "transform" (row-major Matrix4)
+};
+
+// Per-primitive surface attributes (primitive_triangle.cc:97-176), kAttrF4 float4 per primitive:
+//   [0] v0 (.w = flags ATTR_*)  [1] e1  [2] e2          Moller-Trumbore operands (barycentrics)
+//   [3..5] orco vertices        [6] (u0, v0, u1, v1)  [7] (u2, v2, -, -)
+//   [8..10] vertex normals (smooth / exported normals; face normal where a vertex has none)
+constexpr int kAttrF4 = 11;
+constexpr int kMaxNodes = 16;   // shader nodes per material program
+enum : uint32_t { ATTR_ORCO = 1u, ATTR_UV = 2u, ATTR_SMOOTH = 4u };
 
 struct DevLight
 {
@@ -124,6 +195,14 @@ struct DevScene
 	const float *light_func;
 	float light_inv_integral;
 	int n_ph_lights;
+
+	// surface attributes and shader nodes: only when some material has nodes or some mesh has
+	// orco / uv / smooth normals (has_attr); k_surface then fills DevQueues::sattr per hit
+	int has_attr, n_textures;
+	const float4 *prim_attr;       // kAttrF4 per primitive
+	const float4 *texels;
+	const DevTexture *textures;
+	const DevNode *shader_nodes;
 };
 
 struct DevFilm
@@ -150,6 +229,7 @@ struct DevPaths
 	uint4 *pr;             // (PixelSamplingData::offset_, PixelSamplingData::sample_, MWC x, MWC c)
 	float4 *nee;           // [slots * nee_k] contributions .w = valid
 	uint8_t *occ;          // [slots * nee_k] shadow results
+	float4 *v0attr;        // [2 * slots] first-hit surface attributes (has_attr && path_samples > 1)
 };
 
 struct DevQueues
@@ -164,6 +244,7 @@ struct DevQueues
 	float4 *sh_o;          // origin, .w unused
 	float4 *sh_d;          // direction, .w = t_max (already tmax - 2 tmin, or inf)
 	int *sh_idx;           // slot * nee_k + entry
+	float4 *sattr;         // [2 * entries] k_surface output for the hit: (N, diffuse_refl), (diffuse colour, -)
 };
 
 // Next-event-estimation requests written by k_shade, consumed by k_nee in the same iteration.
@@ -172,6 +253,7 @@ struct DevNeeQueue
 	float4 *p_prim;        // hit point, .w = primitive (bits)
 	float4 *wo_k;          // outgoing direction, .w = index k of the path in the next active list (bits)
 	uint4 *pix_mode;       // (PixelSamplingData offset, sample index, mode | light << 8, 0)
+	float4 *attr;          // [2 * requests] surface attributes of the vertex (has_attr only)
 };
 
 // Queues are segmented: segment b (capacity cap_a entries / cap_s shadow rays) belongs to workgroup

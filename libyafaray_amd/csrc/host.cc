@@ -2,6 +2,7 @@
 #include "host.h"
 #include "hostmath.h"
 #include "render.h"
+#include "texture.h"
 
 #include <algorithm>
 #include <chrono>
@@ -143,7 +144,38 @@ int Scene::addVertex(float x, float y, float z)
 	return (int)(v.size() / 3) - 1;
 }
 
-bool Scene::addTriangle(int a, int b, int c)
+int Scene::addVertexWithOrco(float x, float y, float z, float ox, float oy, float oz)
+{
+	const int id = addVertex(x, y, z);
+	if(id < 0) return id;
+	// scene.cc:948-956: addPoint + addOrcoPoint (hasOrco() = orco list non-empty)
+	auto &o = current_object->orco;
+	o.push_back(ox);
+	o.push_back(oy);
+	o.push_back(oz);
+	return id;
+}
+
+void Scene::addNormal(float x, float y, float z)
+{
+	// object_mesh.cc:111-116 (normals exported: faces added afterwards index them by vertex)
+	if(!current_object) { log.error("Scene: addNormal() outside of an object"); return; }
+	auto &n = current_object->normals;
+	n.push_back(x);
+	n.push_back(y);
+	n.push_back(z);
+}
+
+int Scene::addUv(float u, float v)
+{
+	if(!current_object) { log.error("Scene: addUv() outside of an object"); return 0; }
+	auto &uv = current_object->uvs;
+	uv.push_back(u);
+	uv.push_back(v);
+	return (int)(uv.size() / 2) - 1;
+}
+
+bool Scene::addTriangle(int a, int b, int c, int uv_a, int uv_b, int uv_c)
 {
 	if(!current_object) { log.error("Scene: addTriangle() outside of an object"); return false; }
 	const int nv = (int)(current_object->verts.size() / 3);
@@ -158,21 +190,176 @@ bool Scene::addTriangle(int a, int b, int c)
 		log.error("Scene: addTriangle() with no valid current material ('" + current_material + "')");
 		return false;
 	}
+	const int nuv = (int)(current_object->uvs.size() / 2);
+	if(uv_a >= nuv || uv_b >= nuv || uv_c >= nuv)
+	{
+		log.error("Scene: addTriangleWithUv() uv index out of range in object '" + current_object->name + "'");
+		return false;
+	}
 	current_object->tris.push_back(a);
 	current_object->tris.push_back(b);
 	current_object->tris.push_back(c);
 	current_object->tri_mat.push_back(it->second);
+	current_object->tri_uv.push_back(uv_a);
+	current_object->tri_uv.push_back(uv_b);
+	current_object->tri_uv.push_back(uv_c);
+	// object_mesh.cc:84: faces added after normals were exported use the vertex normals
+	const bool exported = !current_object->normals.empty();
+	current_object->tri_nidx.push_back(exported ? a : -1);
+	current_object->tri_nidx.push_back(exported ? b : -1);
+	current_object->tri_nidx.push_back(exported ? c : -1);
+	return true;
+}
+
+HostImage *Scene::createImage(const std::string &name, const ParamMap &p)
+{
+	// scene.cc:518-521 createMapItem: an existing name is a warning, a missing type an error
+	if(images.count(name)) { log.warning("Scene: Image '" + name + "' already exists!"); return nullptr; }
+	std::string type;
+	if(!p.get("type", type)) { log.error("Scene: Image '" + name + "': type not specified"); return nullptr; }
+	std::shared_ptr<HostImage> img = yafamd::createImage(log, name, p);
+	if(!img) { log.error("Scene: Image '" + name + "' could not be created"); return nullptr; }
+	images[name] = img;
+	return img.get();
+}
+
+bool Scene::createTexture(const std::string &name, const ParamMap &p)
+{
+	if(texture_index.count(name)) { log.warning("Scene: Texture '" + name + "' already exists!"); return false; }
+	HostTexture t;
+	if(!yafamd::createTexture(log, images, name, p, t)) return false;
+	texture_index[name] = (int)textures.size();
+	textures.push_back(t);
+	return true;
+}
+
+// scene.cc:909-932 + object_mesh.cc:118-240 (MeshObject::smoothNormals)
+bool Scene::smoothMesh(const std::string &name, float angle)
+{
+	MeshObject *o = nullptr;
+	if(!name.empty())
+	{
+		auto it = objects.find(name);
+		if(it == objects.end()) { log.error("Scene: smoothMesh(): object '" + name + "' not found"); return false; }
+		o = &it->second;
+	}
+	else o = current_object;
+	if(!o) return false;
+	const size_t nv = o->verts.size() / 3, nt = o->tri_mat.size();
+	if(!o->normals.empty() && o->normals.size() / 3 == nv) { o->smooth = true; return true; }
+	struct V { float x, y, z; };
+	auto P = [&](int i) { return V{o->verts[3 * (size_t)i], o->verts[3 * (size_t)i + 1], o->verts[3 * (size_t)i + 2]}; };
+	auto sub3 = [](V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; };
+	auto crs3 = [](V a, V b) { return V{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; };
+	auto len3 = [](V a) { return std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z); };
+	auto nrm3 = [](V v) {
+		float l = v.x * v.x + v.y * v.y + v.z * v.z;
+		if(l != 0.f) { l = 1.f / std::sqrt(l); v.x *= l; v.y *= l; v.z *= l; }
+		return v;
+	};
+	auto dot3 = [](V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; };
+	// Vec3::sinFromVectors (vector.h:212-219) with math::asin's domain clamp (math.h:260-266)
+	auto angleSine = [&](int a, int b, int c) {
+		const V e1 = sub3(P(b), P(a)), e2 = sub3(P(c), P(a));
+		const float div = (len3(e1) * len3(e2)) * 0.99999f + 0.00001f;
+		float arg = (len3(crs3(e1, e2)) / div) * 0.99999f;
+		if(arg > 1.f) arg = 1.f;
+		if(arg <= -1.f) return static_cast<float>(-hm::div_pi_by_2);
+		if(arg >= 1.f) return static_cast<float>(hm::div_pi_by_2);
+		return std::asin(arg);
+	};
+	auto faceN = [&](size_t t) { return nrm3(crs3(sub3(P(o->tris[3 * t + 1]), P(o->tris[3 * t])), sub3(P(o->tris[3 * t + 2]), P(o->tris[3 * t])))); };
+	std::vector<V> normals(nv, V{0.f, 0.f, 0.f});
+	for(size_t i = 0; i < std::min(nv, o->normals.size() / 3); ++i) normals[i] = V{o->normals[3 * i], o->normals[3 * i + 1], o->normals[3 * i + 2]};
+	if(o->tri_nidx.size() < 3 * nt) o->tri_nidx.resize(3 * nt, -1);
+	if(angle >= 180)
+	{
+		for(size_t t = 0; t < nt; ++t)
+		{
+			const V n = faceN(t);
+			const int *vi = &o->tris[3 * t];
+			for(int r = 0; r < 3; ++r)
+			{
+				const float sn = angleSine(vi[r], vi[(r + 1) % 3], vi[(r + 2) % 3]);
+				V &acc = normals[vi[r]];
+				acc.x += n.x * sn; acc.y += n.y * sn; acc.z += n.z * sn;
+				o->tri_nidx[3 * t + r] = vi[r];
+			}
+		}
+		for(V &n : normals) n = nrm3(n);
+	}
+	else if(angle > 0.1f)
+	{
+		const float threshold = hm::cosf_fast(static_cast<float>(angle * hm::div_pi_by_180));
+		std::vector<std::vector<size_t>> pfaces(nv);
+		std::vector<std::vector<float>> psines(nv);
+		for(size_t t = 0; t < nt; ++t)
+		{
+			const int *vi = &o->tris[3 * t];
+			for(int r = 0; r < 3; ++r)
+			{
+				psines[vi[r]].push_back(angleSine(vi[r], vi[(r + 1) % 3], vi[(r + 2) % 3]));
+				pfaces[vi[r]].push_back(t);
+			}
+		}
+		for(size_t pid = 0; pid < nv; ++pid)
+		{
+			int j = 0;
+			std::vector<V> vn;
+			std::vector<int> vn_idx;
+			for(size_t f : pfaces[pid])
+			{
+				bool smooth = false;
+				const V fn = faceN(f);
+				V vnorm{fn.x * psines[pid][j], fn.y * psines[pid][j], fn.z * psines[pid][j]};
+				int k = 0;
+				for(size_t f2 : pfaces[pid])
+				{
+					if(f == f2) { k++; continue; }
+					const V fn2 = faceN(f2);
+					if(dot3(fn, fn2) > threshold)
+					{
+						smooth = true;
+						vnorm.x += fn2.x * psines[pid][k]; vnorm.y += fn2.y * psines[pid][k]; vnorm.z += fn2.z * psines[pid][k];
+					}
+					k++;
+				}
+				int nidx = -1;
+				if(smooth)
+				{
+					vnorm = nrm3(vnorm);
+					for(size_t q = 0; q < vn.size(); ++q)
+						if(dot3(vnorm, vn[q]) > 0.999f) { nidx = vn_idx[q]; break; }
+					if(nidx == -1)
+					{
+						nidx = (int)normals.size();
+						vn.push_back(vnorm);
+						vn_idx.push_back(nidx);
+						normals.push_back(vnorm);
+					}
+				}
+				for(int r = 0; r < 3; ++r)
+					if(o->tris[3 * f + r] == (int)pid) { o->tri_nidx[3 * f + r] = nidx; break; }
+				j++;
+			}
+		}
+	}
+	o->normals.clear();
+	for(const V &n : normals) { o->normals.push_back(n.x); o->normals.push_back(n.y); o->normals.push_back(n.z); }
+	o->smooth = true;
+	geometry_dirty = true;
 	return true;
 }
 
 // material_shiny_diffuse.cc:28-87 + 495-640, material_simple.cc:36-70
-bool Scene::createMaterial(const std::string &name, const ParamMap &p)
+bool Scene::createMaterial(const std::string &name, const ParamMap &p, const std::list<ParamMap> &nodes)
 {
 	if(materials.count(name)) { log.error("Scene: material '" + name + "' already exists"); return false; }
 	std::string type;
 	p.get("type", type);
 	DevMaterial m{};
 	m.receive_shadows = 1;
+	m.diffuse_root = m.drefl_root = -1;
 	bool b;
 	if(type == "shinydiffusemat")
 	{
@@ -197,9 +384,15 @@ bool Scene::createMaterial(const std::string &name, const ParamMap &p)
 			log.error("Material '" + name + "': Oren-Nayar diffuse BRDF is not supported by the GPU core yet");
 			return false;
 		}
-		std::string shader;
-		if(p.get("diffuse_shader", shader) || p.get("mirror_color_shader", shader) || p.get("bump_shader", shader))
-			log.warning("Material '" + name + "': shader nodes / textures are not evaluated by the GPU core yet; using the plain diffuse colour");
+		// shader nodes (material_shiny_diffuse.cc:579-660)
+		std::vector<DevNode> prog;
+		int droot = -1, rroot = -1;
+		if(!buildNodeProgram(log, texture_index, textures, name, p, nodes, prog, droot, rroot)) return false;
+		m.n_nodes = (int)prog.size();
+		m.diffuse_root = droot;
+		m.drefl_root = rroot;
+		m.emit_strength = emit;
+		if(!prog.empty()) mat_nodes[name] = prog;
 		m.type = MAT_SHINYDIFFUSE;
 		for(int k = 0; k < 3; ++k) m.diffuse[k] = col[k];
 		for(int k = 0; k < 3; ++k) m.emit[k] = emit * col[k];     // emit_color_(emit_strength * diffuse_color)
@@ -505,8 +698,91 @@ bool Scene::buildAccelerator()
 		std::memcpy(&matf, &tri_mat[t], 4);
 		put(&hs.prim_ng[4 * (size_t)t], n, matf);
 	}
-	for(const std::string &mn : material_order) hs.mats.push_back(materials[mn]);
+	for(const std::string &mn : material_order)
+	{
+		DevMaterial m = materials[mn];
+		auto nit = mat_nodes.find(mn);
+		m.node0 = (int)hs.shader_nodes.size();
+		if(nit != mat_nodes.end()) hs.shader_nodes.insert(hs.shader_nodes.end(), nit->second.begin(), nit->second.end());
+		else m.n_nodes = 0;
+		if(m.n_nodes > 0) hs.has_attr = true;
+		hs.mats.push_back(m);
+	}
 	if(hs.mats.empty()) hs.mats.push_back(DevMaterial{});
+	// image textures: texels = the image buffers' getColor() values (one copy per image)
+	{
+		std::map<const HostImage *, uint32_t> placed;
+		for(const HostTexture &ht : textures)
+		{
+			DevTexture t = ht.t;
+			auto pit = placed.find(ht.img.get());
+			if(pit == placed.end())
+			{
+				const uint32_t off = (uint32_t)(hs.texels.size() / 4);
+				hs.texels.insert(hs.texels.end(), ht.img->px.begin(), ht.img->px.end());
+				pit = placed.emplace(ht.img.get(), off).first;
+			}
+			t.texel0 = pit->second;
+			hs.textures.push_back(t);
+		}
+	}
+	for(const std::string &name : object_order)
+	{
+		const MeshObject &o = objects[name];
+		if(o.is_base || o.visibility == "invisible") continue;
+		if(o.smooth || !o.normals.empty()) hs.has_attr = true;
+	}
+	if(hs.has_attr)
+	{
+		// per-primitive surface attributes (texeval.h surfAttr; primitive_triangle.cc:97-176)
+		hs.prim_attr.assign((size_t)hs.n_prims * kAttrF4 * 4, 0.f);
+		int t = 0;
+		for(const std::string &name : object_order)
+		{
+			const MeshObject &o = objects[name];
+			if(o.is_base || o.visibility == "invisible") continue;
+			const bool has_orco = !o.orco.empty(), has_uv = !o.uvs.empty(), smooth = o.smooth || !o.normals.empty();
+			const size_t nn = o.normals.size() / 3;
+			for(size_t k = 0; k < o.tri_mat.size(); ++k, ++t)
+			{
+				float *a = &hs.prim_attr[(size_t)t * kAttrF4 * 4];
+				const int *vi = &o.tris[3 * k];
+				const F3 p0 = f3(&o.verts[3 * (size_t)vi[0]]), p1 = f3(&o.verts[3 * (size_t)vi[1]]), p2 = f3(&o.verts[3 * (size_t)vi[2]]);
+				uint32_t fl = 0;
+				put(a + 4, sub(p1, p0));
+				put(a + 8, sub(p2, p0));
+				if(has_orco && o.orco.size() >= 3 * (o.verts.size() / 3))
+				{
+					fl |= ATTR_ORCO;
+					for(int r = 0; r < 3; ++r) put(a + 12 + 4 * r, f3(&o.orco[3 * (size_t)vi[r]]));
+				}
+				const int *ui = o.tri_uv.size() >= 3 * (k + 1) ? &o.tri_uv[3 * k] : nullptr;
+				if(has_uv && ui && ui[0] >= 0 && ui[1] >= 0 && ui[2] >= 0)
+				{
+					const float *u0 = &o.uvs[2 * (size_t)ui[0]], *u1 = &o.uvs[2 * (size_t)ui[1]], *u2 = &o.uvs[2 * (size_t)ui[2]];
+					const float du_1 = u1[0] - u0[0], du_2 = u2[0] - u0[0], dv_1 = u1[1] - u0[1], dv_2 = u2[1] - u0[1];
+					const float det = du_1 * dv_2 - dv_1 * du_2;
+					if(std::abs(det) > 1e-30f) fl |= ATTR_UV;   // else implicit uv (:144-152)
+					a[24] = u0[0]; a[25] = u0[1]; a[26] = u1[0]; a[27] = u1[1];
+					a[28] = u2[0]; a[29] = u2[1];
+				}
+				if(smooth)
+				{
+					fl |= ATTR_SMOOTH;
+					const float *ng = &hs.prim_ng[4 * (size_t)t];
+					for(int r = 0; r < 3; ++r)
+					{
+						const int ni = o.tri_nidx.size() >= 3 * (k + 1) ? o.tri_nidx[3 * k + r] : -1;
+						if(ni >= 0 && (size_t)ni < nn) put(a + 32 + 4 * r, f3(&o.normals[3 * (size_t)ni]));
+						else put(a + 32 + 4 * r, F3{ng[0], ng[1], ng[2]});   // getVertexNormal: face normal
+					}
+				}
+				float flf;
+				std::memcpy(&flf, &fl, 4);
+				put(a, p0, flf);
+			}
+		}
+	}
 	for(auto &kv : lights) hs.lights.push_back(kv.second);
 	uint32_t base = 0;
 	for(DevLight &L : hs.lights) { L.nee_base = base; base += L.nee_count; }

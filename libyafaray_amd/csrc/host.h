@@ -103,6 +103,14 @@ struct MeshObject
 	std::vector<float> verts;            // xyz (addVertex casts the doubles to float, interface.cc:88)
 	std::vector<int> tris;               // abc (object-local vertex indices)
 	std::vector<int> tri_mat;            // material index per triangle
+	// surface attributes (object_mesh.h:48-76): orco per vertex, uv values + per-triangle uv
+	// indices, exported / smoothed vertex normals
+	std::vector<float> orco;             // xyz per vertex (addVertexWithOrco)
+	std::vector<float> uvs;              // (u, v) per addUv
+	std::vector<int> tri_uv;             // 3 per triangle (-1: addTriangle without uv)
+	std::vector<float> normals;          // xyz per addNormal / smoothMesh
+	std::vector<int> tri_nidx;           // 3 normal indices per triangle (-1: face normal)
+	bool smooth = false;
 	bool is_base = false;
 	std::string visibility = "normal";
 	bool ended = false;
@@ -155,6 +163,8 @@ struct Callbacks
 };
 
 class GpuRenderer;
+struct HostImage;
+struct HostTexture;
 
 class Scene
 {
@@ -174,8 +184,10 @@ class Scene
 		std::map<std::string, ParamMap> integrators;
 		std::vector<std::string> layers;
 		std::map<std::string, ParamMap> outputs;
-		std::map<std::string, std::vector<float>> images;
-		std::map<std::string, std::pair<int, int>> image_size;
+		std::map<std::string, std::shared_ptr<HostImage>> images;
+		std::map<std::string, int> texture_index;                 // name -> textures[]
+		std::vector<HostTexture> textures;
+		std::map<std::string, std::vector<DevNode>> mat_nodes;    // material -> node program
 		RenderSetup setup;
 		MeshObject *current_object = nullptr;
 		std::string current_material;
@@ -188,8 +200,14 @@ class Scene
 		bool createObject(const std::string &name, const ParamMap &p);
 		bool endObject();
 		int addVertex(float x, float y, float z);
-		bool addTriangle(int a, int b, int c);
-		bool createMaterial(const std::string &name, const ParamMap &p);
+		int addVertexWithOrco(float x, float y, float z, float ox, float oy, float oz);
+		void addNormal(float x, float y, float z);
+		int addUv(float u, float v);
+		bool addTriangle(int a, int b, int c, int uv_a = -1, int uv_b = -1, int uv_c = -1);
+		bool smoothMesh(const std::string &name, float angle);
+		bool createMaterial(const std::string &name, const ParamMap &p, const std::list<ParamMap> &nodes);
+		HostImage *createImage(const std::string &name, const ParamMap &p);
+		bool createTexture(const std::string &name, const ParamMap &p);
 		bool createLight(const std::string &name, const ParamMap &p);
 		bool createCamera(const std::string &name, const ParamMap &p);
 		bool createBackground(const std::string &name, const ParamMap &p);

@@ -63,6 +63,7 @@ inline float sinf_fast(float x)
 	else if(result >= 1.f) return 1.f;
 	return result;
 }
+inline float cosf_fast(float x) { return sinf_fast(x + static_cast<float>(div_pi_by_2)); }   // math.h:247-254
 
 // include/math/filter.h:34-90
 inline float filterBox(float, float) { return 1.f; }

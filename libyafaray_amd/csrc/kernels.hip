@@ -30,6 +30,7 @@
 #include "devmath.h"
 #include "photonheap.h"
 #include "devscene.h"
+#include "texeval.h"
 
 namespace yafamd
 {
@@ -636,7 +637,19 @@ struct Surf
 	V3 p, n, ng, nu, nv;
 	int mat;
 	uint32_t flags;
+	C3 dcol;          // diffuse shader colour (ATTR kernels only; else the material's colour is read)
+	float drefl;      // diffuse_refl_shader scalar
 };
+
+// Surface attributes computed by k_surface for the hit (texeval.h): shading normal + frame,
+// diffuse shader colour and diffuse_refl scalar
+__device__ __forceinline__ void applyAttr(Surf &s, const float4 &a0, const float4 &a1)
+{
+	s.n = v3(a0.x, a0.y, a0.z);
+	coordsSystem(s.n, s.nu, s.nv);
+	s.drefl = a0.w;
+	s.dcol = C3{a1.x, a1.y, a1.z};
+}
 
 __device__ __forceinline__ Surf makeSurf(const DevScene &S, V3 o, V3 d, float t, int prim)
 {
@@ -655,6 +668,7 @@ __device__ __forceinline__ Surf makeSurf(const DevScene &S, V3 o, V3 d, float t,
 __device__ __forceinline__ V3 faceForward(V3 ng, V3 n, V3 wo) { return (dot(ng, wo) < 0) ? -n : n; }
 
 // material_shiny_diffuse.cc:190-228, material_simple.cc (light_mat evaluates to black)
+template<bool ATTR = false>
 __device__ C3 matEval(const DevMaterial &m, const Surf &sp, V3 wo, V3 wl, uint32_t bsdfs)
 {
 	if(m.type == MAT_LIGHT) return c3(0.f);
@@ -662,11 +676,13 @@ __device__ C3 matEval(const DevMaterial &m, const Surf &sp, V3 wo, V3 wl, uint32
 	if(!(bsdfs & (m.bsdf_flags & B_DIFFUSE))) return c3(0.f);
 	const float m_t = (1.f - 1.f * m.comp[0]) * (1.f - m.comp[1]);
 	if((double)dot(n, wl) < 0.0 && !m.flat) return c3(0.f);
-	const float m_d = m_t * (1.f - m.comp[2]) * m.comp[3];
-	return m_d * C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+	float m_d = m_t * (1.f - m.comp[2]) * m.comp[3];
+	if(ATTR && m.drefl_root >= 0) m_d *= sp.drefl;   // :235
+	return m_d * (ATTR ? sp.dcol : C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]});
 }
 
-// material_shiny_diffuse.cc:237-242, material_simple.cc:50-55
+// material_shiny_diffuse.cc:242-247, material_simple.cc:50-55
+template<bool ATTR = false>
 __device__ C3 matEmit(const DevMaterial &m, const Surf &sp, V3 wo)
 {
 	if(m.type == MAT_LIGHT)
@@ -674,6 +690,7 @@ __device__ C3 matEmit(const DevMaterial &m, const Surf &sp, V3 wo)
 		if(m.double_sided) return C3{m.emit[0], m.emit[1], m.emit[2]};
 		return dot(wo, sp.n) > 0 ? C3{m.emit[0], m.emit[1], m.emit[2]} : c3(0.f);
 	}
+	if(ATTR && m.diffuse_root >= 0) return sp.dcol * m.emit_strength;
 	return C3{m.emit[0], m.emit[1], m.emit[2]};
 }
 
@@ -696,6 +713,7 @@ struct BsdfSample
 };
 
 // material_shiny_diffuse.cc:244-327 (diffuse reflect component), material_simple.cc:42-48
+template<bool ATTR = false>
 __device__ C3 matSample(const DevMaterial &m, const Surf &sp, V3 wo, V3 &wi, BsdfSample &s, float &w)
 {
 	if(m.type == MAT_LIGHT)
@@ -736,7 +754,7 @@ __device__ C3 matSample(const DevMaterial &m, const Surf &sp, V3 wo, V3 &wi, Bsd
 	else s_1 = s.s_1 / width[pick];
 	C3 scolor = c3(0.f);
 	wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
-	if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+	if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * (ATTR ? sp.dcol : C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]});
 	s.pdf = fabsf(dot(wi, n)) * width[pick];
 	s.sampled = choice[pick];
 	w = fabsf(dot(wi, sp.n)) / (s.pdf * 0.99f + 0.01f);
@@ -825,6 +843,7 @@ __device__ __forceinline__ void shadowRayOf(V3 from, V3 dir, float tmin, float t
 // nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
 // Wave-uniform structure: `active` lanes do the work, every lane of the wave walks the same loop
 // bounds (the shadow-ray appends are wave-level).
+template<bool ATTR>
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
                          float4 *nee, uint8_t *occ, const ShadeOut &out)
@@ -849,7 +868,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			ldir = ldir * (1.f / dist);
 			const C3 lcol = C3{L.color[0], L.color[1], L.color[2]} * idist_sqr;
 			const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
-			const C3 surf_col = matEval(m, sp, wo, ldir, B_ALL);
+			const C3 surf_col = matEval<ATTR>(m, sp, wo, ldir, B_ALL);
 			const C3 transmit = c3(1.f);
 			contrib = surf_col * lcol * angle * transmit;
 			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
@@ -900,7 +919,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 				const float pdf = x87mulDiv(kPi, dist_sqr, L.area * cos_angle);
 				if(pdf > 1e-6f)
 				{
-					const C3 surf_col = matEval(m, sp, wo, ldir, B_ALL);
+					const C3 surf_col = matEval<ATTR>(m, sp, wo, ldir, B_ALL);
 					const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
 					float w = 1.f;
 					const float m_pdf = matPdf(m, sp, wo, ldir, B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT);
@@ -939,7 +958,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			s.pdf = 0.f;
 			s.sampled = B_NONE;
 			float W = 0.f;
-			const C3 surf_col = matSample(m, sp, wo, dir, s, W);
+			const C3 surf_col = matSample<ATTR>(m, sp, wo, dir, s, W);
 			ok = s.pdf > 1e-6f;
 			float t = 0.f, cos_angle = 0.f;
 			if(ok)
@@ -1106,7 +1125,7 @@ __device__ __forceinline__ Surf surfFromPrim(const DevScene &S, V3 p, int prim)
 //   4. wave-ballot compaction: the entry's state moves to its position in the next queue
 //      (coalesced SoA reads and writes, no indirection);
 //   5. next-event estimation into the next state: contributions + shadow rays.
-template<bool SMALL>
+template<bool SMALL, bool ATTR>
 __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(ShadeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
@@ -1137,6 +1156,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		float w = 0.f;
 		float4 thr4 = make_float4(0.f, 0.f, 0.f, 0.f), col4 = thr4, pcol4 = thr4, pwo4 = thr4, pthr4 = thr4, pem4 = thr4;
 		float4 v0p4 = thr4, v0wo4 = thr4;
+		float4 v0a0 = thr4, v0a1 = thr4;   // first-hit surface attributes (ATTR && keep_v0)
 		if(live)
 		{
 			sid = (uint32_t)A.Q.slot[i];
@@ -1147,6 +1167,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			col4 = Pc.col[i];
 			pcol4 = Pc.pcol[i];
 			if(keep_v0) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
+			if(ATTR && keep_v0) { v0a0 = Pc.v0attr[2 * (size_t)i]; v0a1 = Pc.v0attr[2 * (size_t)i + 1]; }
 			w = thr4.w;
 			stage = __float_as_uint(col4.w);
 			flags = __float_as_uint(pcol4.w);
@@ -1186,6 +1207,8 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		// ---- 2. the new hit ----
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
+		sp.dcol = c3(0.f); sp.drefl = 1.f;
+		float4 sa0 = make_float4(0.f, 0.f, 0.f, 0.f), sa1 = sa0;
 		V3 wo = v3(0.f, 0.f, 1.f);
 		bool have_hit = false;
 		int hit_prim = -1;
@@ -1197,6 +1220,12 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 				const float4 ro = A.Q.ray_o[i], rd = A.Q.ray_d[i];
 				have_hit = true;
 				sp = makeSurf(S, xyz(ro), xyz(rd), A.Q.hit_t[i], hit_prim);
+				if(ATTR)
+				{
+					sa0 = A.Q.sattr[2 * (size_t)i];
+					sa1 = A.Q.sattr[2 * (size_t)i + 1];
+					applyAttr(sp, sa0, sa1);
+				}
 				wo = -xyz(rd);
 			}
 		}
@@ -1223,8 +1252,8 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 					col = c3(0.f);
 					// photon_mapping.cc:868-869 adds emit(wo) unconditionally and :938-946 adds it again
 					// for emitting materials; the other integrators add it once (direct_light.cc:120)
-					if(is_photon) col = col + matEmit(m, sp, wo);
-					if(sp.flags & B_EMIT) col = col + matEmit(m, sp, wo);
+					if(is_photon) col = col + matEmit<ATTR>(m, sp, wo);
+					if(sp.flags & B_EMIT) col = col + matEmit<ATTR>(m, sp, wo);
 					if(sp.flags & B_DIFFUSE) { nee_v0 = true; flags |= F_V0_DIFFUSE; }
 					if(is_photon)
 					{
@@ -1235,6 +1264,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 					{
 						v0p4 = f4(sp.p, __int_as_float(hit_prim));
 						v0wo4 = f4(wo, 0.f);
+						if(ATTR) { v0a0 = sa0; v0a1 = sa1; }
 						start_sub = true;
 						subpath = 0;
 					}
@@ -1251,7 +1281,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 					else wo = pwo;
 					nee_one = true;
 					flags = (flags & ~F_MATFLAGS) | (sp.flags & F_MATFLAGS);
-					if(sp.flags & B_EMIT) { emit_pend = matEmit(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
+					if(sp.flags & B_EMIT) { emit_pend = matEmit<ATTR>(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
 					pend_thr = thr;
 					depth = 1;
 					sample_next = true;
@@ -1278,7 +1308,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 					if(killed) end_sub = true;
 					else
 					{
-						if((mfl & B_EMIT) && (flags & F_CAUSTIC)) { emit_pend = matEmit(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
+						if((mfl & B_EMIT) && (flags & F_CAUSTIC)) { emit_pend = matEmit<ATTR>(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
 						if(mfl & B_DIFFUSE) { nee_one = true; pend_thr = thr; }
 						else
 						{
@@ -1333,7 +1363,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 				s.pdf = 0.f;
 				s.sampled = B_NONE;
 				V3 dir = v3(0.f, 0.f, 0.f);
-				C3 scol = matSample(S.mats[sp.mat], sp, wo, dir, s, w);
+				C3 scol = matSample<ATTR>(S.mats[sp.mat], sp, wo, dir, s, w);
 				scol = scol * w;
 				if(isBlack(scol)) end_sub = true;
 				else
@@ -1358,7 +1388,8 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 		if(live && start_sub)
 		{
 			// path_tracer.cc:168-191: first segment of subpath `subpath` from v0
-			const Surf s0 = (st == ST_CAMERA) ? sp : surfFromPrim(S, xyz(v0p4), __float_as_int(v0p4.w));
+			Surf s0 = (st == ST_CAMERA) ? sp : surfFromPrim(S, xyz(v0p4), __float_as_int(v0p4.w));
+			if(ATTR && st != ST_CAMERA) applyAttr(s0, v0a0, v0a1);
 			const V3 wo0 = (st == ST_CAMERA) ? wo : xyz(v0wo4);
 			const uint32_t offs = n_paths * sample_idx + offset + subpath;
 			BsdfSample s;
@@ -1368,7 +1399,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			s.pdf = 0.f;
 			s.sampled = B_NONE;
 			V3 dir = v3(0.f, 0.f, 0.f);
-			C3 scol = matSample(S.mats[s0.mat], s0, wo0, dir, s, w);
+			C3 scol = matSample<ATTR>(S.mats[s0.mat], s0, wo0, dir, s, w);
 			thr = scol * w;
 			pwo = wo0;
 			if(s.sampled != B_NONE) flags |= F_SAMPLED;
@@ -1417,6 +1448,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			if(nee_one) Pn.pend_thr[k] = f4(pend_thr, 0.f);
 			if(flags & F_PEND_EMIT) Pn.pend_emit[k] = f4(emit_pend, 0.f);
 			if(keep_v0) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }
+			if(ATTR && keep_v0) { Pn.v0attr[2 * (size_t)k] = v0a0; Pn.v0attr[2 * (size_t)k + 1] = v0a1; }
 		}
 
 		PHASE(4);
@@ -1431,6 +1463,11 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			A.N.p_prim[j] = f4(sp.p, __int_as_float(hit_prim));
 			A.N.wo_k[j] = f4(wo, __uint_as_float(k));
 			A.N.pix_mode[j] = make_uint4(offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8), 0u);
+			if(ATTR)
+			{
+				A.N.attr[2 * (size_t)j] = f4(sp.n, sp.drefl);
+				A.N.attr[2 * (size_t)j + 1] = f4(sp.dcol, 0.f);
+			}
 		}
 		else if(want_gather)
 		{
@@ -1456,6 +1493,39 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 // k_shade keeps fewer registers live.  Contributions go to the next state set at k * nee_k,
 // shadow rays to the next queue (workgroup-level appends).
 // ---------------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------------
+// k_surface: material-shade dispatch for scenes with textures / shader nodes / smooth normals.
+// For every hit of the active queue: barycentrics -> shading normal, orco, uv
+// (TrianglePrimitive::getSurface, primitive_triangle.cc:97-176), then the material's shader-node
+// program (Material::initBsdf, material_shiny_diffuse.cc:133-141) -> diffuse colour + diffuse_refl.
+// Written per queue entry for k_shade (and from there into the NEE requests for k_nee).  Kept out
+// of k_shade so the untextured hot path carries none of its registers.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kShadeBlock) k_surface(DevScene S, DevQueues Q, DevCounters cnt)
+{
+	const uint32_t seg = blockIdx.x;
+	const uint32_t n_a = cnt.n_active[seg];
+	const uint32_t a0 = seg * S.cap_a;
+	for(uint32_t j = threadIdx.x; j < n_a; j += blockDim.x)
+	{
+		const uint32_t i = a0 + j;
+		const float4 rd = Q.ray_d[i];
+		if(rd.w != rd.w) continue;   // no ray this iteration (NaN marker)
+		const int prim = Q.hit_prim[i];
+		if(prim < 0) continue;
+		const float4 ro = Q.ray_o[i];
+		const V3 o = xyz(ro), d = xyz(rd);
+		const V3 p = o + Q.hit_t[i] * d;   // accelerator.cc:61
+		const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, o, d, p);
+		const DevMaterial &m = S.mats[__float_as_int(S.prim_ng[prim].w)];
+		C3 dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+		float drefl = 1.f;
+		if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl);
+		Q.sattr[2 * (size_t)i] = f4(sa.n, drefl);
+		Q.sattr[2 * (size_t)i + 1] = f4(dcol, 0.f);
+	}
+}
+
 struct NeeArgs
 {
 	DevScene S;
@@ -1468,7 +1538,7 @@ struct NeeArgs
 #ifndef YAF_NEE_MIN_WAVES
 #define YAF_NEE_MIN_WAVES 1
 #endif
-template<bool SMALL>
+template<bool SMALL, bool ATTR>
 __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
@@ -1500,7 +1570,9 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs 
 		}
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
+		sp.dcol = c3(0.f); sp.drefl = 1.f;
 		if(live) sp = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
+		if(ATTR && live) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
 		const V3 wo = xyz(wk);
 		const int e0 = (int)__float_as_uint(wk.w) * K;
 		const bool all = live && (pm.z & 1u);
@@ -1510,7 +1582,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs 
 		{
 			// estimateAllDirectLight (montecarlo.cc:54-68)
 			for(int l = 0; l < S.n_lights; ++l)
-				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
+				neeLight<ATTR>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
 				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out);
 		}
 		if(__any(one))
@@ -1520,7 +1592,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs 
 			{
 				const bool mine = one && lnum == (uint32_t)l;
 				if(!__any(mine)) continue;
-				neeLight(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out);
+				neeLight<ATTR>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out);
 			}
 		}
 	}
@@ -2129,14 +2201,14 @@ int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds)
 int yafamd_nee_blocks_per_cu()
 {
 	int nb = 0;
-	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_nee<true>, kShadeBlock, 8192) != hipSuccess) nb = 0;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_nee<true, false>), kShadeBlock, 8192) != hipSuccess) nb = 0;
 	return nb;
 }
 
 int yafamd_shade_blocks_per_cu()
 {
 	int nb = 0;
-	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<true>, kShadeBlock, 8192) != hipSuccess) nb = 0;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (k_shade<true, false>), kShadeBlock, 8192) != hipSuccess) nb = 0;
 	return nb;
 }
 
@@ -2183,8 +2255,19 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
 	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
-	if(S->small_tables) hipLaunchKernelGGL(k_shade<true>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
-	else hipLaunchKernelGGL(k_shade<false>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	if(S->has_attr)
+	{
+		if(S->small_tables) hipLaunchKernelGGL((k_shade<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		else hipLaunchKernelGGL((k_shade<false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	}
+	else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	else hipLaunchKernelGGL((k_shade<false, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_surface(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, hipStream_t st)
+{
+	hipLaunchKernelGGL(k_surface, dim3(S->n_seg), dim3(kShadeBlock), 0, st, *S, *Q, *cnt);
 	return hipGetLastError();
 }
 
@@ -2198,8 +2281,13 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	A.Qn = *Qn;
 	A.cnt_next = *cnt_next;
 	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
-	if(S->small_tables) hipLaunchKernelGGL(k_nee<true>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
-	else hipLaunchKernelGGL(k_nee<false>, dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	if(S->has_attr)
+	{
+		if(S->small_tables) hipLaunchKernelGGL((k_nee<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		else hipLaunchKernelGGL((k_nee<false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	}
+	else if(S->small_tables) hipLaunchKernelGGL((k_nee<true, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	else hipLaunchKernelGGL((k_nee<false, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	return hipGetLastError();
 }
 

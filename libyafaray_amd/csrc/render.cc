@@ -18,6 +18,7 @@ using namespace yafamd;
 extern "C" {
 hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st);
+hipError_t yafamd_launch_surface(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, hipStream_t st);
 hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P,
                                DevStats *stats, int stack_depth, int *spill, int grid, hipStream_t st);
 int yafamd_trace_block();
@@ -94,6 +95,10 @@ struct GpuRenderer::Impl
 	bool ok = false, init_done = false;
 	hipStream_t stream = nullptr;
 	Buf nodes, tris, prim_ng, mats, lights, faure, faure_dim, faure_inv;
+	// surface attributes, textures and shader-node programs (texeval.h)
+	Buf prim_attr, shader_nodes, textures, texels;
+	bool has_attr = false, attr_alloc = false;
+	int n_textures = 0;
 	// photon mapping: light selection Pdf1D, photon paths in flight, the map and its kd-tree
 	Buf ph_lights, light_cdf, light_func;
 	float light_inv_integral = 0.f;
@@ -126,6 +131,8 @@ struct GpuRenderer::Impl
 	{
 		for(Buf *b : {&ph_lights, &light_cdf, &light_func, &ph_ray_o, &ph_ray_d, &ph_pcol, &ph_alive0, &ph_alive1, &ph_n_alive,
 		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes})
+			b->release();
+		for(Buf *b : {&prim_attr, &shader_nodes, &textures, &texels})
 			b->release();
 		for(Buf *b : {&spill, &nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_dim, &faure_inv, &samples, &film,
 		              &weights, &jobs, &counters, &stats, &accum, &aa_flags, &aa_plist})
@@ -239,6 +246,16 @@ bool GpuRenderer::upload(HostScene &hs)
 	if(!allocCopy(log_, d.prim_ng, hs.prim_ng.data(), hs.prim_ng.size())) return false;
 	if(!allocCopy(log_, d.mats, hs.mats.data(), hs.mats.size())) return false;
 	if(!allocCopy(log_, d.lights, hs.lights.data(), hs.lights.size())) return false;
+	d.has_attr = hs.has_attr;
+	d.n_textures = (int)hs.textures.size();
+	if(hs.has_attr)
+	{
+		if(!allocCopy(log_, d.prim_attr, hs.prim_attr.data(), hs.prim_attr.size())) return false;
+		if(!allocCopy(log_, d.shader_nodes, hs.shader_nodes.data(), hs.shader_nodes.size())) return false;
+		if(!allocCopy(log_, d.textures, hs.textures.data(), hs.textures.size())) return false;
+		if(!allocCopy(log_, d.texels, hs.texels.data(), hs.texels.size())) return false;
+	}
+	else for(Buf *b : {&d.prim_attr, &d.shader_nodes, &d.textures, &d.texels}) b->release();
 	d.n_nodes = hs.bvh.n_nodes;
 	d.n_tris = hs.n_prims;
 	d.n_mats = (int)hs.mats.size();
@@ -366,6 +383,12 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.light_func = (const float *)d.light_func.p;
 	S.light_inv_integral = d.light_inv_integral;
 	S.n_ph_lights = d.n_ph_lights;
+	S.has_attr = d.has_attr ? 1 : 0;
+	S.n_textures = d.n_textures;
+	S.prim_attr = (const float4 *)d.prim_attr.p;
+	S.shader_nodes = (const DevNode *)d.shader_nodes.p;
+	S.textures = (const DevTexture *)d.textures.p;
+	S.texels = (const float4 *)d.texels.p;
 }
 
 bool GpuRenderer::buildPhotonMap(RenderParams &rp)
@@ -461,6 +484,11 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	fillScenePointers(d, S);
 	stats_.photons = 0;
 	stats_.photon_seconds = 0.0;
+	if(S.integrator == INT_PHOTON && S.has_attr)
+	{
+		log_.error("PhotonIntegrator: textures / shader nodes / smooth normals are not evaluated by the GPU photon mapping path yet");
+		return false;
+	}
 	if(S.integrator == INT_PHOTON)
 	{
 		// PhotonIntegrator::preprocess (integrator_photon_mapping.cc:242-638): the photon map is
@@ -518,7 +546,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	// segment capacity: the camera deals groups of 256 samples round-robin over the segments
 	const size_t R = (size_t)d.shade_grid;
 	auto shardCap = [R](size_t m) { return (((m + 255) / 256 + R - 1) / R) * 256; };
-	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc)
+	const bool need_attr = S.has_attr != 0;
+	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc)
 	{
 		// Wavefront buffers for M samples in flight (~0.7 KB each: 288 GB of HBM holds tens of millions,
 		// and big chunks amortise the per-launch cost).  On allocation failure the chunk is halved.
@@ -553,6 +582,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				P.pr = (uint4 *)A(MA * 16);
 				P.nee = (float4 *)A(MA * K * 16);
 				P.occ = (uint8_t *)A(MA * K);
+				P.v0attr = (float4 *)A(need_v0 && need_attr ? MA * 32 : 16);
 			}
 			for(int q = 0; q < 2; ++q)
 			{
@@ -565,10 +595,12 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				Q.sh_o = (float4 *)A(MA * K * 16);
 				Q.sh_d = (float4 *)A(MA * K * 16);
 				Q.sh_idx = (int *)A(MA * K * 4);
+				Q.sattr = (float4 *)A(need_attr ? MA * 32 : 16);
 			}
 			d.N.p_prim = (float4 *)A(MA * 16);
 			d.N.wo_k = (float4 *)A(MA * 16);
 			d.N.pix_mode = (uint4 *)A(MA * 16);
+			d.N.attr = (float4 *)A(need_attr ? MA * 32 : 16);
 			bool ok = true;
 			for(const Buf &b : d.chunk_bufs) ok = ok && b.p;
 			if(ok) break;
@@ -577,6 +609,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			log_.warning("GPU: wavefront buffers do not fit, retrying with " + std::to_string(M) + " samples in flight");
 		}
 		d.v0_alloc = need_v0;
+		d.attr_alloc = need_attr;
 		d.slots_cap = M;
 		d.nee_cap = K;
 	}
@@ -626,6 +659,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i], d.stream));
 			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], dstats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 1], d.stream));
+			// material-shade dispatch for textured / smooth scenes: surface attributes + shader nodes
+			// of every hit, before k_shade reads them
+			if(S.has_attr) HIPCHECK(yafamd_launch_surface(&S, &d.Q[cur], &cnt[cur], d.stream));
 			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 2], d.stream));

@@ -29,6 +29,12 @@ struct HostScene
 	std::vector<DevMaterial> mats;
 	std::vector<DevLight> lights;        // render order (by name)
 	int n_prims = 0;
+	// surface attributes / textures / shader nodes (texeval.h), only when has_attr
+	bool has_attr = false;
+	std::vector<float> prim_attr;        // kAttrF4 float4 per primitive
+	std::vector<DevNode> shader_nodes;
+	std::vector<DevTexture> textures;
+	std::vector<float> texels;           // RGBA per texel
 };
 
 struct PhotonParams

@@ -35,6 +35,27 @@ class Material:
     double_sided: bool = False             # light_mat
     receive_shadows: bool = True
     flat_material: bool = False
+    # full typed parameter map {key: (kind, value)} (kinds s f i b v c m) and the pushed shader-node
+    # lists, as a reference client passes them (tests/test01/test01.c:268-650); when set, apply()
+    # issues exactly these instead of the fields above
+    params: Optional[dict] = None
+    nodes: List[dict] = field(default_factory=list)
+
+
+@dataclass
+class ImageSpec:
+    """yafaray_createImage: typed params; a relative "filename" is resolved against base_dir.
+    set_pixels: yafaray_setImageColor calls [(x, y, (r, g, b, a))] issued after creation."""
+    name: str
+    params: dict
+    base_dir: str = ""
+    set_pixels: List[tuple] = field(default_factory=list)
+
+
+@dataclass
+class TextureSpec:
+    name: str
+    params: dict
 
 
 @dataclass
@@ -126,6 +147,10 @@ class Object:
     nv: int
     t0: int            # first triangle (global index)
     nt: int
+    uv0: int = 0       # first uv value (global index into SceneSpec.uvs)
+    nuv: int = 0
+    smooth_angle: Optional[float] = None   # yafaray_smoothMesh(name, angle) after endObject
+    has_orco: bool = True                  # with SceneSpec.orco: addVertexWithOrco (else addVertex)
 
 
 @dataclass
@@ -139,6 +164,13 @@ class SceneSpec:
     render: Render
     background: Optional[Background] = None
     objects: List[Object] = field(default_factory=list)
+    # surface attributes and textures (optional)
+    orco: Optional[np.ndarray] = None       # (N, 3) per vertex: addVertexWithOrco
+    normals: Optional[np.ndarray] = None    # (N, 3) per vertex: addNormal after the vertices
+    uvs: Optional[np.ndarray] = None        # (U, 2) addUv values
+    tri_uv: Optional[np.ndarray] = None     # (M, 3) global uv indices (-1: addTriangle)
+    images: List[ImageSpec] = field(default_factory=list)
+    textures: List[TextureSpec] = field(default_factory=list)
 
     def render_lights(self):
         """Lights in the order the integrators see them: by name (render_view.cc:61, std::map)."""
@@ -283,15 +315,89 @@ def test01(width=256, height=256, spp=4, filter_type="gauss", pixelwidth=1.5, ti
     return SceneSpec(verts, tris, tri_mat, mats, lights, cam, rend, bg, b.objects)
 
 
+TEX01_DIR = os.path.join(GOLDEN_DIR, "tex01")
+
+
+def test01_textured(width=256, height=256, spp=4, filter_type="gauss", pixelwidth=1.5, tile_size=32) -> SceneSpec:
+    """BASELINE C1 with the reference's own texturing: every createImage / createTexture /
+    createMaterial call of tests/test01/test01.c (typed parameter maps + shader-node lists) and the
+    cubes' orco coordinates.  Images resolve against tests/golden/tex01 (tex.tga, tex.hdr); the
+    PNG / JPG / TIFF / EXR images fail to load exactly as in the reference built without those
+    libraries (src/format/format.cc:40-66), which drops their textures and nodes."""
+    import dataclasses
+    s = test01(width, height, spp, filter_type, pixelwidth, tile_size)
+    with open(os.path.join(GOLDEN_DIR, "test01_scene.json")) as f:
+        d = json.load(f)
+    mats = []
+    for m, mf in zip(s.materials, d["materials_full"]):
+        assert m.name == mf["name"]
+        mats.append(dataclasses.replace(m, params={k: tuple(v) for k, v in mf["params"].items()},
+                                        nodes=[{k: tuple(v) for k, v in nd.items()} for nd in mf["nodes"]]))
+    images = [ImageSpec(im["name"], {k: tuple(v) for k, v in im["params"].items()}, TEX01_DIR) for im in d["images"]]
+    textures = [TextureSpec(t["name"], {k: tuple(v) for k, v in t["params"].items()}) for t in d["textures"]]
+    orco = np.asarray([oc for o in d["objects"] for oc in (o["orco"] if o["orco"] else o["verts"])], np.float32)
+    has_orco = all(len(o["orco"]) == len(o["verts"]) for o in d["objects"] if o["orco"])
+    assert has_orco
+    # objects without orco (the plane) replay addVertex: their orco rows are placeholders
+    objs = [dataclasses.replace(o, has_orco=bool(od["orco"])) for o, od in zip(s.objects, d["objects"])]
+    return dataclasses.replace(s, materials=mats, images=images, textures=textures, orco=orco, objects=objs)
+
+
 # ---------------------------------------------------------------------------------------------
 # replay through the C API (the drop-in boundary)
 # ---------------------------------------------------------------------------------------------
 
+def set_typed(api, k, tv):
+    """paramsSet* for one typed value (kind, value): s f i b v c m."""
+    kind, v = tv
+    if kind == "s":
+        api.paramsSetString(k, v)
+    elif kind == "f":
+        api.paramsSetFloat(k, float(v))
+    elif kind == "i":
+        api.paramsSetInt(k, int(v))
+    elif kind == "b":
+        api.paramsSetBool(k, bool(v))
+    elif kind == "v":
+        api.paramsSetVector(k, *map(float, v))
+    elif kind == "c":
+        api.paramsSetColor(k, *map(float, v))
+    elif kind == "m":
+        api.paramsSetMatrix(k, *map(float, v), False)
+    else:
+        raise ValueError(f"unknown parameter kind {kind!r}")
+
+
 def apply(spec: SceneSpec, api) -> None:
     """Issue the reference C-API call sequence for `spec` on `api` (a libyafaray_amd.Interface)."""
     api.createScene()
+    for im in spec.images:
+        api.paramsClearAll()
+        for k, tv in im.params.items():
+            if k == "filename" and tv[1] and not os.path.isabs(tv[1]) and im.base_dir:
+                tv = ("s", os.path.join(im.base_dir, tv[1]))
+            set_typed(api, k, tv)
+        h = api.createImage(im.name)
+        for (x, y, c) in im.set_pixels:
+            if h:
+                api.setImageColor(h, x, y, *c)
+    for t in spec.textures:
+        api.paramsClearAll()
+        for k, tv in t.params.items():
+            set_typed(api, k, tv)
+        api.createTexture(t.name)
     for m in spec.materials:
         api.paramsClearAll()
+        if m.params is not None:
+            for k, tv in m.params.items():
+                set_typed(api, k, tv)
+            for nd in m.nodes:
+                api.paramsPushList()
+                for k, tv in nd.items():
+                    set_typed(api, k, tv)
+            api.paramsEndList()
+            api.createMaterial(m.name)
+            continue
         api.paramsSetString("type", m.type)
         api.paramsSetColor("color", *m.color, 1.0)
         if m.type == "light_mat":
@@ -323,12 +429,38 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetString("type", "mesh")
         api.paramsSetInt("num_vertices", o.nv)
         api.paramsSetInt("num_faces", o.nt)
-        api.paramsSetBool("has_orco", False)
-        api.paramsSetBool("has_uv", False)
+        use_orco = spec.orco is not None and o.has_orco
+        api.paramsSetBool("has_orco", use_orco)
+        api.paramsSetBool("has_uv", o.nuv > 0)
         api.createObject(o.name)
-        api.addVertices(spec.verts[o.v0:o.v0 + o.nv])
+        if use_orco:
+            for v, oc in zip(spec.verts[o.v0:o.v0 + o.nv], spec.orco[o.v0:o.v0 + o.nv]):
+                api.addVertexWithOrco(*map(float, v), *map(float, oc))
+        else:
+            api.addVertices(spec.verts[o.v0:o.v0 + o.nv])
+        if spec.normals is not None:
+            for n in spec.normals[o.v0:o.v0 + o.nv]:
+                api.addNormal(*map(float, n))
+        for k in range(o.nuv):
+            api.addUv(*map(float, spec.uvs[o.uv0 + k]))
         tri = spec.tris[o.t0:o.t0 + o.nt] - o.v0
         mats = spec.tri_mat[o.t0:o.t0 + o.nt]
+        if spec.tri_uv is not None and o.nuv > 0:
+            tuv = spec.tri_uv[o.t0:o.t0 + o.nt]
+            cur = None
+            for k in range(o.nt):
+                if mats[k] != cur:
+                    cur = mats[k]
+                    api.setCurrentMaterial(spec.materials[int(cur)].name)
+                a, b, c = map(int, tri[k])
+                if tuv[k][0] >= 0:
+                    api.addTriangleWithUv(a, b, c, *(int(u) - o.uv0 for u in tuv[k]))
+                else:
+                    api.addTriangle(a, b, c)
+            api.endObject()
+            if o.smooth_angle is not None:
+                api.smoothMesh(o.name, float(o.smooth_angle))
+            continue
         # setCurrentMaterial + addTriangle runs (object_mesh.cc:78-86)
         start = 0
         while start < len(tri):
@@ -339,6 +471,8 @@ def apply(spec: SceneSpec, api) -> None:
             api.addTriangles(tri[start:end])
             start = end
         api.endObject()
+        if o.smooth_angle is not None:
+            api.smoothMesh(o.name, float(o.smooth_angle))
     cam = spec.camera
     api.paramsClearAll()
     api.paramsSetString("type", "perspective")

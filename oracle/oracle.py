@@ -25,7 +25,35 @@ FILTERS = {"box": 0, "gauss": 1, "mitchell": 2, "lanczos": 3}
 class yc_material(C.Structure):
     _fields_ = [("type", C.c_int), ("color", C.c_float * 3), ("diffuse_strength", C.c_float),
                 ("emit_strength", C.c_float), ("double_sided", C.c_int), ("receive_shadows", C.c_int),
-                ("flat_material", C.c_int)]
+                ("flat_material", C.c_int), ("diffuse_shader", C.c_int), ("diffuse_refl_shader", C.c_int)]
+
+
+class yc_image(C.Structure):
+    _fields_ = [("format", C.c_int), ("data", C.POINTER(C.c_uint8)), ("size", C.c_int), ("type", C.c_int),
+                ("optimization", C.c_int), ("color_space", C.c_int), ("gamma", C.c_float), ("width", C.c_int),
+                ("height", C.c_int), ("n_set", C.c_int), ("set_xy", C.POINTER(C.c_int)), ("set_rgba", C.POINTER(C.c_float))]
+
+
+class yc_texture(C.Structure):
+    _fields_ = [("image", C.c_int), ("interpolation", C.c_int), ("clip", C.c_int), ("xrepeat", C.c_int),
+                ("yrepeat", C.c_int), ("mirror_x", C.c_int), ("mirror_y", C.c_int), ("rot90", C.c_int),
+                ("even_tiles", C.c_int), ("odd_tiles", C.c_int), ("cropmin_x", C.c_float), ("cropmin_y", C.c_float),
+                ("cropmax_x", C.c_float), ("cropmax_y", C.c_float), ("checker_dist", C.c_float), ("intensity", C.c_float),
+                ("contrast", C.c_float), ("saturation", C.c_float), ("hue", C.c_float), ("factor_red", C.c_float),
+                ("factor_green", C.c_float), ("factor_blue", C.c_float), ("clamp", C.c_int)]
+
+
+class yc_node(C.Structure):
+    _fields_ = [("type", C.c_int), ("blend", C.c_int), ("input", C.c_int * 3), ("no_rgb", C.c_int), ("stencil", C.c_int),
+                ("negative", C.c_int), ("do_color", C.c_int), ("do_scalar", C.c_int), ("color_input", C.c_int),
+                ("use_alpha", C.c_int), ("texture", C.c_int), ("coords", C.c_int), ("projection", C.c_int),
+                ("map", C.c_int * 3), ("col1", C.c_float * 4), ("col2", C.c_float * 4), ("val", C.c_float * 4),
+                ("scale", C.c_float * 3), ("offset", C.c_float * 3), ("mtx", C.c_float * 16)]
+
+
+class yc_object(C.Structure):
+    _fields_ = [("v0", C.c_int), ("nv", C.c_int), ("t0", C.c_int), ("nt", C.c_int), ("has_orco", C.c_int),
+                ("has_uv", C.c_int), ("normals_exported", C.c_int), ("smooth", C.c_int), ("smooth_angle", C.c_float)]
 
 
 class yc_light(C.Structure):
@@ -60,7 +88,11 @@ class yc_scene(C.Structure):
     _fields_ = [("n_verts", C.c_int), ("verts", C.POINTER(C.c_float)), ("n_tris", C.c_int),
                 ("tris", C.POINTER(C.c_int)), ("tri_mat", C.POINTER(C.c_int)), ("n_mats", C.c_int),
                 ("mats", C.POINTER(yc_material)), ("n_lights", C.c_int), ("lights", C.POINTER(yc_light)),
-                ("cam", yc_camera), ("rp", yc_render)]
+                ("cam", yc_camera), ("rp", yc_render), ("n_objects", C.c_int), ("objects", C.POINTER(yc_object)),
+                ("orco", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)), ("uvs", C.POINTER(C.c_float)),
+                ("tri_uv", C.POINTER(C.c_int)), ("n_images", C.c_int), ("images", C.POINTER(yc_image)),
+                ("n_textures", C.c_int), ("textures", C.POINTER(yc_texture)), ("n_nodes", C.c_int),
+                ("nodes", C.POINTER(yc_node))]
 
 
 class yc_counters(C.Structure):
@@ -203,6 +235,233 @@ def film_table(filter_name: str, filter_size: float):
 
 # ---- scene-level oracle ------------------------------------------------------------------------
 
+# ---- texturing: the reference's host-side setup, restated (scene.cc createMapItem, image.cc:38-100,
+# format.cc:40-66, texture_image.cc:477-596, material_node.cc:102-187, shader node factories) ----
+_IMG_TYPES = {"ColorAlpha": 4, "Color": 3, "GrayAlpha": 2, "Gray": 1}
+_CS = {"Raw_Manual_Gamma": 1, "LinearRGB": 2, "sRGB": 3, "XYZ": 4}
+_CLIP = {"extend": 0, "clip": 1, "clipcube": 2, "checker": 4}
+_BLEND = {"add": 1, "multiply": 2, "subtract": 3, "screen": 4, "divide": 5, "difference": 6, "darken": 7,
+          "lighten": 8, "overlay": 9}
+_ROOTS = ("diffuse_shader", "mirror_color_shader", "bump_shader", "mirror_shader", "transparency_shader",
+          "translucency_shader", "sigma_oren_shader", "diffuse_refl_shader", "IOR_shader", "wireframe_shader")
+
+
+def _get(pm, key, kind, default=None):
+    """ParamMap::getParam: strictly typed (a value of another kind reads as absent)."""
+    tv = pm.get(key)
+    if tv is None or tv[0] != kind:
+        return default
+    return tv[1]
+
+
+def _texturing(self, spec, mats):
+    """Fill the texturing part of self.sc from spec (images, textures, node programs, surface attributes)."""
+    keep = []
+    sc = self.sc
+    # images (Image::factory)
+    img_index, imgs = {}, []
+    for im in spec.images:
+        pm = im.params
+        if im.name in img_index or _get(pm, "type", "s") is None:
+            continue
+        y = yc_image()
+        itype = _IMG_TYPES.get(_get(pm, "type", "s", "ColorAlpha"), 0)
+        opt = {"none": 0, "compressed": 2}.get(_get(pm, "image_optimization", "s", "optimized"), 1)
+        cs = _CS.get(_get(pm, "color_space", "s", "Raw_Manual_Gamma"), 1)
+        y.type, y.optimization, y.color_space = itype, opt, cs
+        y.gamma = float(_get(pm, "gamma", "f", 1.0))
+        y.width, y.height = int(_get(pm, "width", "i", 100)), int(_get(pm, "height", "i", 100))
+        fn = _get(pm, "filename", "s", "")
+        loaded = False
+        if fn:
+            path = fn if os.path.isabs(fn) or not im.base_dir else os.path.join(im.base_dir, fn)
+            ext = os.path.splitext(fn)[1][1:].lower()
+            fmt = 1 if ext in ("tga", "tpic") else 2 if ext in ("hdr", "pic") else 0
+            if fmt and os.path.exists(path):
+                data = np.frombuffer(open(path, "rb").read(), np.uint8).copy()
+                keep.append(data)
+                y.format, y.data, y.size = fmt, _p(data, C.c_uint8), len(data)
+                if fmt == 2:
+                    y.optimization = 0
+                loaded = True   # the oracle decides decode failures itself (falls back to an empty image)
+        if not loaded and itype == 0:
+            continue            # Image::factory(w, h, Type::None) -> nullptr: the image does not exist
+        if im.set_pixels:
+            xy = np.asarray([(x, yy) for (x, yy, _) in im.set_pixels], np.int32).reshape(-1)
+            rgba = np.asarray([c for (_, _, c) in im.set_pixels], np.float32).reshape(-1)
+            keep += [xy, rgba]
+            y.n_set, y.set_xy, y.set_rgba = len(im.set_pixels), _p(xy, C.c_int), _p(rgba, C.c_float)
+        img_index[im.name] = len(imgs)
+        imgs.append(y)
+    # textures (ImageTexture::factory)
+    tex_index, texs = {}, []
+    for t in spec.textures:
+        pm = t.params
+        if t.name in tex_index or _get(pm, "type", "s") != "image":
+            continue
+        iname = _get(pm, "image_name", "s", "")
+        if iname not in img_index:
+            continue
+        x = yc_texture()
+        x.image = img_index[iname]
+        interp = _get(pm, "interpolate", "s", "")
+        x.interpolation = {"none": 0, "bicubic": 2}.get(interp, 1)
+        x.clip = _CLIP.get(_get(pm, "clipping", "s", ""), 3)
+        x.xrepeat, x.yrepeat = int(_get(pm, "xrepeat", "i", 1)), int(_get(pm, "yrepeat", "i", 1))
+        x.mirror_x, x.mirror_y = int(_get(pm, "mirror_x", "b", False)), int(_get(pm, "mirror_y", "b", False))
+        x.rot90 = int(_get(pm, "rot90", "b", False))
+        x.even_tiles, x.odd_tiles = int(_get(pm, "even_tiles", "b", False)), int(_get(pm, "odd_tiles", "b", True))
+        x.cropmin_x, x.cropmin_y = _get(pm, "cropmin_x", "f", 0.0), _get(pm, "cropmin_y", "f", 0.0)
+        x.cropmax_x, x.cropmax_y = _get(pm, "cropmax_x", "f", 1.0), _get(pm, "cropmax_y", "f", 1.0)
+        x.checker_dist = _get(pm, "checker_dist", "f", 0.0)
+        x.intensity, x.contrast = _get(pm, "adj_intensity", "f", 1.0), _get(pm, "adj_contrast", "f", 1.0)
+        x.saturation, x.hue = _get(pm, "adj_saturation", "f", 1.0), _get(pm, "adj_hue", "f", 0.0)
+        x.factor_red = _get(pm, "adj_mult_factor_red", "f", 1.0)
+        x.factor_green = _get(pm, "adj_mult_factor_green", "f", 1.0)
+        x.factor_blue = _get(pm, "adj_mult_factor_blue", "f", 1.0)
+        x.clamp = int(_get(pm, "adj_clamp", "b", False))
+        tex_index[t.name] = len(texs)
+        texs.append(x)
+    # shader nodes per material (loadNodes / configInputs / parseNodes); nodes are global in yc_scene
+    nodes = []
+    for mi, m in enumerate(spec.materials):
+        if m.params is None or not m.nodes:
+            continue
+        table, order, ok = {}, [], True
+        for nd in m.nodes:
+            el = _get(nd, "element", "s")
+            if el is not None and el != "shader_node":
+                continue
+            name, typ = _get(nd, "name", "s"), _get(nd, "type", "s")
+            if name is None or typ is None or name in table:
+                ok = False
+                break
+            y = yc_node()
+            y.input[:] = [-1, -1, -1]
+            if typ == "texture_mapper":
+                tname = _get(nd, "texture", "s")
+                if tname not in tex_index:
+                    ok = False
+                    break
+                y.type, y.texture = 3, tex_index[tname]
+                y.coords = {"uv": 0, "orco": 2, "transformed": 3}.get(_get(nd, "texco", "s", "global"), 1)
+                y.projection = {"cube": 1, "tube": 2, "sphere": 3}.get(_get(nd, "mapping", "s", "plain"), 0)
+                y.map[:] = [min(3, max(0, int(_get(nd, k, "i", dflt)))) for k, dflt in (("proj_x", 1), ("proj_y", 2), ("proj_z", 3))]
+                y.scale[:] = list(_get(nd, "scale", "v", (1.0, 1.0, 1.0)))
+                y.offset[:] = list(_get(nd, "offset", "v", (0.0, 0.0, 0.0)))
+                y.mtx[:] = list(_get(nd, "transform", "m", (1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1)))
+                y.do_scalar = int(_get(nd, "do_scalar", "b", True))
+            elif typ == "value":
+                y.type = 0
+                c = _get(nd, "color", "c", (1.0, 1.0, 1.0, 1.0))
+                y.col1[:] = [c[0], c[1], c[2], _get(nd, "alpha", "f", 1.0)]
+                y.val[0] = _get(nd, "scalar", "f", 1.0)
+            elif typ == "mix":
+                y.type = 1
+                b = _BLEND.get(_get(nd, "blend_mode", "s", ""), 0)
+                y.blend = 0 if b == 5 else b
+                y.val[0] = _get(nd, "cfactor", "f", 0.5) if y.blend == 0 else 0.0
+            elif typ == "layer":
+                y.type = 2
+                b = _BLEND.get(_get(nd, "blend_mode", "s", ""), 0)
+                y.blend = 0 if b == 9 else b
+                c = _get(nd, "def_col", "c", (1.0, 1.0, 1.0, 1.0))
+                y.col1[:] = [c[0], c[1], c[2], 1.0]
+                y.val[0], y.val[1], y.val[2] = _get(nd, "colfac", "f", 1.0), _get(nd, "valfac", "f", 1.0), _get(nd, "def_val", "f", 1.0)
+                for fld, key, dflt in (("no_rgb", "noRGB", False), ("stencil", "stencil", False), ("negative", "negative", False),
+                                       ("do_color", "do_color", True), ("do_scalar", "do_scalar", False),
+                                       ("color_input", "color_input", True), ("use_alpha", "use_alpha", False)):
+                    setattr(y, fld, int(_get(nd, key, "b", dflt)))
+            else:
+                ok = False
+                break
+            table[name] = (y, nd)
+            order.append(name)
+        if ok:
+            for name in order:
+                y, nd = table[name]
+                if y.type == 2:
+                    inp = _get(nd, "input", "s")
+                    if inp not in table:
+                        ok = False
+                        break
+                    up = _get(nd, "upper_layer", "s")
+                    if up is not None:
+                        if up not in table:
+                            ok = False
+                            break
+                    else:
+                        y.col2[:] = list(_get(nd, "upper_color", "c", (0.0, 0.0, 0.0, 0.0)))
+                        y.val[3] = _get(nd, "upper_value", "f", 0.0)
+                elif y.type == 1:
+                    for k, (ik, ck) in enumerate((("input1", "color1"), ("input2", "color2"))):
+                        inp = _get(nd, ik, "s")
+                        if inp is not None:
+                            if inp not in table:
+                                ok = False
+                        elif _get(nd, ck, "c") is not None:
+                            (y.col1 if k == 0 else y.col2)[:] = list(_get(nd, ck, "c"))
+                        else:
+                            ok = False
+                    if _get(nd, "factor", "s") is not None:
+                        ok = ok and _get(nd, "factor", "s") in table
+                    elif _get(nd, "value", "f") is not None:
+                        y.val[0] = _get(nd, "value", "f")
+                    else:
+                        ok = False
+                    if not ok:
+                        break
+        if not ok:
+            continue   # loadNodes cleared the table: plain colours
+        base = len(nodes)
+        gidx = {name: base + k for k, name in enumerate(order)}
+        for name in order:
+            y, nd = table[name]
+            if y.type == 2:
+                y.input[0] = gidx[_get(nd, "input", "s")]
+                if _get(nd, "upper_layer", "s") is not None:
+                    y.input[1] = gidx[_get(nd, "upper_layer", "s")]
+            elif y.type == 1:
+                for k, key in enumerate(("input1", "input2", "factor")):
+                    if _get(nd, key, "s") is not None:
+                        y.input[k] = gidx[_get(nd, key, "s")]
+            nodes.append(y)
+        for root, fld in (("diffuse_shader", "diffuse_shader"), ("diffuse_refl_shader", "diffuse_refl_shader")):
+            nm = _get(m.params, root, "s")
+            if nm is not None and nm in gidx:
+                setattr(mats[mi], fld, gidx[nm])
+    # surface attributes per object
+    objs = (yc_object * max(1, len(spec.objects)))()
+    for k, o in enumerate(spec.objects):
+        objs[k].v0, objs[k].nv, objs[k].t0, objs[k].nt = o.v0, o.nv, o.t0, o.nt
+        objs[k].has_orco = int(spec.orco is not None and o.has_orco)
+        objs[k].has_uv = int(o.nuv > 0)
+        objs[k].normals_exported = int(spec.normals is not None)
+        objs[k].smooth = int(o.smooth_angle is not None)
+        objs[k].smooth_angle = o.smooth_angle if o.smooth_angle is not None else 0.0
+    sc.n_objects, sc.objects = len(spec.objects), C.cast(objs, C.POINTER(yc_object))
+    keep.append(objs)
+    for fld, arr, ct, dt in (("orco", spec.orco, C.c_float, np.float32), ("normals", spec.normals, C.c_float, np.float32),
+                             ("uvs", spec.uvs, C.c_float, np.float32), ("tri_uv", spec.tri_uv, C.c_int, np.int32)):
+        if arr is not None:
+            a = np.ascontiguousarray(arr, dt).reshape(-1)
+            keep.append(a)
+            setattr(sc, fld, _p(a, ct))
+    if imgs:
+        ia = (yc_image * len(imgs))(*imgs)
+        keep.append(ia)
+        sc.n_images, sc.images = len(imgs), C.cast(ia, C.POINTER(yc_image))
+    if texs:
+        ta = (yc_texture * len(texs))(*texs)
+        keep.append(ta)
+        sc.n_textures, sc.textures = len(texs), C.cast(ta, C.POINTER(yc_texture))
+    if nodes:
+        na = (yc_node * len(nodes))(*nodes)
+        keep.append(na)
+        sc.n_nodes, sc.nodes = len(nodes), C.cast(na, C.POINTER(yc_node))
+    self._tex_keep = keep
+
+
 class OracleScene:
     """Owns the numpy buffers referenced by a yc_scene struct built from a SceneSpec."""
 
@@ -223,6 +482,7 @@ class OracleScene:
             mats[i].double_sided = int(m.double_sided)
             mats[i].receive_shadows = int(m.receive_shadows)
             mats[i].flat_material = int(m.flat_material)
+            mats[i].diffuse_shader = mats[i].diffuse_refl_shader = -1
         lights = (yc_light * max(1, len(s.lights)))()
         for i, l in enumerate(s.render_lights()):
             lights[i].type = YC_LIGHT_POINT if l.type == "pointlight" else YC_LIGHT_AREA
@@ -286,6 +546,7 @@ class OracleScene:
         rp.aa_variance_edge_size, rp.aa_variance_pixels = r.aa_variance_edge_size, r.aa_variance_pixels
         self.sc = sc
         self.spec = spec
+        _texturing(self, spec, mats)
 
     def render(self, y0: int = 0, y1: int = 0):
         r = self.spec.render

@@ -7,6 +7,9 @@
 #include "yafcpu.h"
 
 #include <algorithm>
+#include <array>
+#include <cstdlib>
+#include <sstream>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -438,6 +441,8 @@ struct FilmTable
 	}
 };
 
+#include "yaftex.h"
+
 // ---------------------------------------------------------------------------------------------
 // scene restatement
 // ---------------------------------------------------------------------------------------------
@@ -454,6 +459,8 @@ struct Material
 	unsigned bsdf_flags = BNone;
 	C3 diffuse_color, emit_color, light_col;
 	float components[4] = {0.f, 0.f, 0.f, 0.f};
+	float emit_strength = 0.f;
+	int diffuse_shader = -1, diffuse_refl_shader = -1;   // shader-node roots (yc_scene.nodes)
 	bool is_diffuse = false, double_sided = false, receive_shadows = true, flat = false;
 	int n_bsdf = 0;
 	unsigned c_flags[4];
@@ -476,6 +483,16 @@ struct Tri
 {
 	V3 v0, v1, v2, ng;
 	int mat;
+};
+
+// per-triangle surface attributes (FacePrimitive + MeshObject data read by getSurface)
+struct TriAttr
+{
+	bool has_orco = false, has_uv = false, smooth = false;
+	V3 orco[3];
+	float u[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f};
+	V3 vn[3];
+	int nidx[3] = {-1, -1, -1};
 };
 
 struct Camera
@@ -604,6 +621,8 @@ struct SurfacePoint
 	const Material *mat = nullptr;
 	int prim = -1;
 	unsigned bsdf_flags = 0;
+	C3 dcol;            // getShaderColor(diffuse_shader_, ..., diffuse_color_)
+	float drefl = 1.f;  // diffuse_refl_shader_ scalar
 };
 
 struct IsectData
@@ -661,8 +680,16 @@ class Scene
 		std::unique_ptr<FilmTable> film;
 		std::vector<BvhNode> nodes;
 		std::vector<int> order;
+		// texturing
+		bool has_attr = false;
+		std::vector<TriAttr> tattr;
+		std::vector<std::unique_ptr<OImageBase>> images;
+		std::vector<OTexture> texs;
+		std::vector<yc_node> shader_nodes;
 
 		explicit Scene(const yc_scene &s);
+		void setupTexturing(const yc_scene &s);
+		void surface(const IsectData &d, SurfacePoint &sp) const;
 		IsectData intersect(const Ray &ray, float t_max, bool any, uint64_t *ctr) const;
 		void buildBvh();
 		int buildRec(int start, int end, std::vector<V3> &cent);
@@ -689,6 +716,9 @@ Scene::Scene(const yc_scene &s)
 		{
 			mm.diffuse_color = C3(m.color[0], m.color[1], m.color[2]);
 			mm.emit_color = m.emit_strength * mm.diffuse_color;
+			mm.emit_strength = m.emit_strength;
+			mm.diffuse_shader = m.diffuse_shader;
+			mm.diffuse_refl_shader = m.diffuse_refl_shader;
 			if(m.emit_strength > 0.f) mm.bsdf_flags |= BEmit;
 			float acc = 1.f;
 			if(m.diffuse_strength * acc > 0.00001f)
@@ -792,6 +822,239 @@ Scene::Scene(const yc_scene &s)
 	}
 	film.reset(new FilmTable(rp.filter, rp.filter_size));
 	buildBvh();
+	setupTexturing(s);
+}
+
+// Images (image.cc:38-137 with the TGA / HDR loaders), image textures (texture_image.cc:477-596),
+// shader nodes, and per-triangle surface attributes incl. MeshObject::smoothNormals
+// (object_mesh.cc:125-240).
+void Scene::setupTexturing(const yc_scene &s)
+{
+	for(int i = 0; i < s.n_images; ++i)
+	{
+		const yc_image &im = s.images[i];
+		std::unique_ptr<OImageBase> img;
+		const bool gray = im.type == ImgGray || im.type == ImgGrayAlpha;
+		int cs = im.color_space;
+		if(im.format == 1) img = loadTga(im.data, (size_t)im.size, im.optimization, cs, im.gamma, gray);
+		else if(im.format == 2) { img = loadHdr(im.data, (size_t)im.size, gray); cs = CsLinearRgb; }
+		if(!img) img = makeImage(im.width, im.height, im.type, im.optimization);
+		if(img)
+		{
+			img->color_space = cs;
+			img->gamma = im.gamma;
+			for(int k = 0; k < im.n_set; ++k)
+			{
+				const int x = im.set_xy[2 * k], y = im.set_xy[2 * k + 1];
+				const float *c = im.set_rgba + 4 * k;
+				if(x >= 0 && y >= 0 && x < img->w && y < img->h) img->setColor(x, y, Rgba(c[0], c[1], c[2], c[3]));
+			}
+		}
+		images.push_back(std::move(img));
+	}
+	for(int i = 0; i < s.n_textures; ++i)
+	{
+		const yc_texture &t = s.textures[i];
+		OTexture o;
+		o.img = images[t.image].get();
+		o.interp = t.interpolation;
+		o.clip = t.clip;
+		o.xrepeat = t.xrepeat;
+		o.yrepeat = t.yrepeat;
+		o.mirror_x = t.mirror_x != 0;
+		o.mirror_y = t.mirror_y != 0;
+		o.rot90 = t.rot90 != 0;
+		o.checker_even = t.even_tiles != 0;
+		o.checker_odd = t.odd_tiles != 0;
+		o.checker_dist = t.checker_dist;
+		o.cropminx = t.cropmin_x; o.cropminy = t.cropmin_y; o.cropmaxx = t.cropmax_x; o.cropmaxy = t.cropmax_y;
+		o.cropx = (o.cropminx != 0.0) || (o.cropmaxx != 1.0);
+		o.cropy = (o.cropminy != 0.0) || (o.cropmaxy != 1.0);
+		o.adj_intensity = t.intensity; o.adj_contrast = t.contrast; o.adj_saturation = t.saturation;
+		o.adj_hue = t.hue / 60.f;
+		o.adj_r = t.factor_red; o.adj_g = t.factor_green; o.adj_b = t.factor_blue;
+		o.adj_clamp = t.clamp != 0;
+		o.adjustments_set = t.intensity != 1.f || t.contrast != 1.f || t.saturation != 1.f || t.hue != 0.f || t.factor_red != 1.f ||
+		                    t.factor_green != 1.f || t.factor_blue != 1.f || t.clamp;
+		o.orig_cs = o.img->color_space;
+		o.orig_gamma = o.img->gamma;
+		texs.push_back(o);
+	}
+	shader_nodes.assign(s.nodes, s.nodes + s.n_nodes);
+	for(const Material &m : mats) if(m.diffuse_shader >= 0 || m.diffuse_refl_shader >= 0) has_attr = true;
+	tattr.resize(tris.size());
+	for(int oi = 0; oi < s.n_objects; ++oi)
+	{
+		const yc_object &ob = s.objects[oi];
+		auto P = [&](int v) { return V3(s.verts[3 * v], s.verts[3 * v + 1], s.verts[3 * v + 2]); };
+		std::vector<V3> normals;   // MeshObject::normals_
+		if(ob.normals_exported) for(int v = 0; v < ob.nv; ++v) normals.push_back(V3(s.normals[3 * (ob.v0 + v)], s.normals[3 * (ob.v0 + v) + 1], s.normals[3 * (ob.v0 + v) + 2]));
+		std::vector<std::array<int, 3>> fn(ob.nt, std::array<int, 3>{-1, -1, -1});   // FacePrimitive::vertex_normals_
+		for(int t = 0; t < ob.nt; ++t)
+			if(ob.normals_exported) for(int r = 0; r < 3; ++r) fn[t][r] = s.tris[3 * (ob.t0 + t) + r] - ob.v0;   // object_mesh.cc:84
+		bool smooth = false;
+		if(ob.smooth)
+		{
+			smooth = true;
+			if(!(ob.normals_exported && (int)normals.size() == ob.nv))
+			{
+				// object_mesh.cc:125-240 over object-local vertex indices
+				auto vi = [&](int t, int r) { return s.tris[3 * (ob.t0 + t) + r] - ob.v0; };
+				auto lp = [&](int v) { return P(ob.v0 + v); };
+				auto sine = [&](int a, int b, int c) {
+					const V3 e1 = lp(b) - lp(a), e2 = lp(c) - lp(a);
+					const float div = (e1.length() * e2.length()) * 0.99999f + 0.00001f;
+					float arg = ((e1 ^ e2).length() / div) * 0.99999f;
+					if(arg > 1.f) arg = 1.f;
+					return fasin(arg);
+				};
+				normals.resize(ob.nv, V3(0.f, 0.f, 0.f));
+				if(ob.smooth_angle >= 180)
+				{
+					for(int t = 0; t < ob.nt; ++t)
+					{
+						const V3 n = tris[ob.t0 + t].ng;
+						for(int r = 0; r < 3; ++r) normals[vi(t, r)] += n * sine(vi(t, r), vi(t, (r + 1) % 3), vi(t, (r + 2) % 3));
+						for(int r = 0; r < 3; ++r) fn[t][r] = vi(t, r);
+					}
+					for(V3 &n : normals) n.normalize();
+				}
+				else if(ob.smooth_angle > 0.1f)
+				{
+					const float threshold = fcos(static_cast<float>(ob.smooth_angle * div_pi_by_180));
+					std::vector<std::vector<int>> pf(ob.nv);
+					std::vector<std::vector<float>> ps(ob.nv);
+					for(int t = 0; t < ob.nt; ++t)
+						for(int r = 0; r < 3; ++r)
+						{
+							ps[vi(t, r)].push_back(sine(vi(t, r), vi(t, (r + 1) % 3), vi(t, (r + 2) % 3)));
+							pf[vi(t, r)].push_back(t);
+						}
+					for(int pid = 0; pid < ob.nv; ++pid)
+					{
+						std::vector<V3> vns;
+						std::vector<int> vns_idx;
+						for(size_t j = 0; j < pf[pid].size(); ++j)
+						{
+							const int f = pf[pid][j];
+							const V3 face_n = tris[ob.t0 + f].ng;
+							V3 vn = face_n * ps[pid][j];
+							bool sm = false;
+							for(size_t k = 0; k < pf[pid].size(); ++k)
+							{
+								if(pf[pid][k] == f) continue;
+								const V3 n2 = tris[ob.t0 + pf[pid][k]].ng;
+								if(dot(face_n, n2) > threshold) { sm = true; vn += n2 * ps[pid][k]; }
+							}
+							int idx = -1;
+							if(sm)
+							{
+								vn.normalize();
+								for(size_t q = 0; q < vns.size(); ++q)
+									if(dot(vn, vns[q]) > 0.999f) { idx = vns_idx[q]; break; }
+								if(idx == -1)
+								{
+									idx = (int)normals.size();
+									vns.push_back(vn);
+									vns_idx.push_back(idx);
+									normals.push_back(vn);
+								}
+							}
+							for(int r = 0; r < 3; ++r) if(vi(f, r) == pid) { fn[f][r] = idx; break; }
+						}
+					}
+				}
+			}
+		}
+		const bool use_normals = smooth || ob.normals_exported;
+		if(use_normals) has_attr = true;
+		for(int t = 0; t < ob.nt; ++t)
+		{
+			TriAttr &ta = tattr[ob.t0 + t];
+			const int *idx = s.tris + 3 * (ob.t0 + t);
+			if(ob.has_orco)
+			{
+				ta.has_orco = true;
+				for(int r = 0; r < 3; ++r) ta.orco[r] = V3(s.orco[3 * idx[r]], s.orco[3 * idx[r] + 1], s.orco[3 * idx[r] + 2]);
+			}
+			if(ob.has_uv && s.tri_uv && s.tri_uv[3 * (ob.t0 + t)] >= 0)
+			{
+				ta.has_uv = true;
+				for(int r = 0; r < 3; ++r)
+				{
+					const int ui = s.tri_uv[3 * (ob.t0 + t) + r];
+					ta.u[r] = s.uvs[2 * ui];
+					ta.v[r] = s.uvs[2 * ui + 1];
+				}
+			}
+			if(use_normals)
+			{
+				ta.smooth = true;
+				for(int r = 0; r < 3; ++r)
+				{
+					ta.nidx[r] = fn[t][r];
+					if(fn[t][r] >= 0 && fn[t][r] < (int)normals.size()) ta.vn[r] = normals[fn[t][r]];
+				}
+			}
+		}
+	}
+}
+
+// TrianglePrimitive::getSurface (primitive_triangle.cc:97-176) + ShinyDiffuse::initBsdf's node
+// evaluation (material_shiny_diffuse.cc:133-141) for the surface point of hit `d`
+void Scene::surface(const IsectData &d, SurfacePoint &sp) const
+{
+	const Tri &tr = tris[d.prim];
+	const Material &m = mats[tr.mat];
+	sp.dcol = m.diffuse_color;
+	sp.drefl = 1.f;
+	if(!has_attr) return;
+	const TriAttr &ta = tattr[d.prim];
+	const float bu = d.bu, bv = d.bv, bw = d.bw;
+	if(ta.smooth)
+	{
+		V3 v[3];
+		for(int r = 0; r < 3; ++r) v[r] = ta.nidx[r] >= 0 ? ta.vn[r] : sp.ng;   // getVertexNormal
+		sp.n = bu * v[0] + bv * v[1] + bw * v[2];
+		sp.n.normalize();
+		createCoordsSystem(sp.n, sp.nu, sp.nv);
+	}
+	if(m.diffuse_shader < 0 && m.diffuse_refl_shader < 0) return;
+	TexPoint tp;
+	tp.p = sp.p;
+	tp.ng = sp.ng;
+	if(ta.has_orco)
+	{
+		tp.orco_p = bu * ta.orco[0] + bv * ta.orco[1] + bw * ta.orco[2];
+		tp.orco_ng = ((ta.orco[1] - ta.orco[0]) ^ (ta.orco[2] - ta.orco[0])).normalize();
+	}
+	else
+	{
+		tp.orco_p = sp.p;
+		tp.orco_ng = sp.ng;
+	}
+	bool implicit_uv = true;
+	if(ta.has_uv)
+	{
+		tp.u = bu * ta.u[0] + bv * ta.u[1] + bw * ta.u[2];
+		tp.v = bu * ta.v[0] + bv * ta.v[1] + bw * ta.v[2];
+		const float du_1 = ta.u[1] - ta.u[0], du_2 = ta.u[2] - ta.u[0];
+		const float dv_1 = ta.v[1] - ta.v[0], dv_2 = ta.v[2] - ta.v[0];
+		const float det = du_1 * dv_2 - dv_1 * du_2;
+		if(std::abs(det) > 1e-30f) implicit_uv = false;
+	}
+	if(implicit_uv)
+	{
+		tp.u = bu;
+		tp.v = bv;
+	}
+	NodeEval ev(shader_nodes, texs, tp);
+	if(m.diffuse_shader >= 0)
+	{
+		const Rgba c = ev.get(m.diffuse_shader).col;
+		sp.dcol = C3(c.r, c.g, c.b);
+	}
+	if(m.diffuse_refl_shader >= 0) sp.drefl = ev.get(m.diffuse_refl_shader).val;
 }
 
 int Scene::buildRec(int start, int end, std::vector<V3> &cent)
@@ -964,6 +1227,7 @@ class Renderer
 			sp.mat = &sc_.mats[tr.mat];
 			sp.bsdf_flags = sp.mat->bsdf_flags;
 			sp.prim = d.prim;
+			sc_.surface(d, sp);
 			ray.tmax = d.t;
 			return true;
 		}
@@ -1000,8 +1264,9 @@ class Renderer
 			if(!(bsdfs & (m.bsdf_flags & BDiffuse))) return C3(0.f);
 			const float m_t = (1.f - 1.f * m.components[0]) * (1.f - m.components[1]);
 			if(dot(n, wl) < 0.0 && !m.flat) return C3(0.f);
-			const float m_d = m_t * (1.f - m.components[2]) * m.components[3];
-			return m_d * m.diffuse_color;
+			float m_d = m_t * (1.f - m.components[2]) * m.components[3];
+			if(m.diffuse_refl_shader >= 0) m_d *= sp.drefl;   // :235
+			return m_d * sp.dcol;
 		}
 
 		// material_shiny_diffuse.cc:237-242, material_simple.cc:50-55
@@ -1014,6 +1279,7 @@ class Renderer
 				const float angle = dot(wo, sp.n);
 				return angle > 0 ? m.light_col : C3(0.f);
 			}
+			if(m.diffuse_shader >= 0) return sp.dcol * m.emit_strength;   // :242-247
 			return m.emit_color;
 		}
 
@@ -1060,7 +1326,7 @@ class Renderer
 			C3 scolor(0.f);
 			// DiffuseReflect (the only component a plain shinydiffuse configures here)
 			wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
-			if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * m.diffuse_color;
+			if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * sp.dcol;
 			s.pdf = std::abs(dot(wi, n)) * width[pick];
 			s.sampled_flags = choice[pick];
 			w = std::abs(dot(wi, sp.n)) / (s.pdf * 0.99f + 0.01f);

@@ -30,7 +30,53 @@ typedef struct {
 	int double_sided;         // light_mat
 	int receive_shadows;
 	int flat_material;
+	int diffuse_shader;       // shader-node roots (indices into yc_scene.nodes, -1: none)
+	int diffuse_refl_shader;
 } yc_material;
+
+// ---- texturing (material_node.cc, texture_image.cc, shader_node_*.cc; see yaftex.h) ----
+typedef struct {
+	int format;               // 0: no file (empty image of width x height), 1: TGA bytes, 2: Radiance HDR bytes
+	const uint8_t *data; int size;
+	int type;                 // Image::Type: 0 none, 1 gray, 2 gray+alpha, 3 color, 4 color+alpha
+	int optimization;         // 0 none, 1 optimized, 2 compressed
+	int color_space;          // ColorSpace (color.h:36): 1 raw/gamma, 2 linear, 3 sRGB, 4 XYZ
+	float gamma;
+	int width, height;
+	int n_set; const int *set_xy; const float *set_rgba;   // yafaray_setImageColor calls, in order
+} yc_image;
+
+typedef struct {
+	int image;
+	int interpolation;        // 0 none, 1 bilinear, 2 bicubic
+	int clip;                 // ImageTexture::ClipMode: 0 extend, 1 clip, 2 clipcube, 3 repeat, 4 checker
+	int xrepeat, yrepeat;
+	int mirror_x, mirror_y, rot90, even_tiles, odd_tiles;
+	float cropmin_x, cropmin_y, cropmax_x, cropmax_y, checker_dist;
+	float intensity, contrast, saturation, hue, factor_red, factor_green, factor_blue;   // hue in degrees
+	int clamp;
+} yc_texture;
+
+typedef struct {
+	int type;                 // 0 value, 1 mix, 2 layer, 3 texture_mapper
+	int blend;                // 0 mix 1 add 2 multiply 3 subtract 4 screen 5 divide 6 difference 7 darken 8 lighten 9 overlay
+	int input[3];             // mix: input1, input2, factor; layer: input, upper_layer (node indices, -1 none)
+	int no_rgb, stencil, negative, do_color, do_scalar, color_input, use_alpha;   // layer (do_scalar: also mapper)
+	int texture, coords, projection, map[3];      // mapper: coords 0 uv 1 global 2 orco 3 transformed; proj 0 plain 1 cube 2 tube 3 sphere
+	float col1[4], col2[4];   // value colour+alpha / mix color1, color2 / layer def_col, upper_color
+	float val[4];             // value scalar / mix cfactor, val1, val2 / layer colfac, valfac, def_val, upper_value
+	float scale[3], offset[3];
+	float mtx[16];
+} yc_node;
+
+typedef struct {
+	int v0, nv, t0, nt;       // vertex / triangle ranges of the object
+	int has_orco;             // orco given per vertex (yc_scene.orco rows of this object)
+	int has_uv;               // addUv values exist for this object
+	int normals_exported;     // addNormal per vertex before the faces (yc_scene.normals rows)
+	int smooth;               // smoothMesh called after endObject
+	float smooth_angle;
+} yc_object;
 
 typedef struct {
 	int type;                 // YC_LIGHT_*
@@ -99,6 +145,15 @@ typedef struct {
 	int n_lights; const yc_light *lights;   // already in render order (alphabetical by name)
 	yc_camera cam;
 	yc_render rp;
+	// optional texturing / surface attributes (all NULL / 0 for untextured flat scenes)
+	int n_objects; const yc_object *objects;
+	const float *orco;        // n_verts x 3
+	const float *normals;     // n_verts x 3 (exported normals)
+	const float *uvs;         // uv values, 2 per entry
+	const int *tri_uv;        // n_tris x 3 global uv indices (-1: none)
+	int n_images; const yc_image *images;
+	int n_textures; const yc_texture *textures;
+	int n_nodes; const yc_node *nodes;
 } yc_scene;
 
 typedef struct {
