@@ -14,7 +14,9 @@
 //   include/geometry/vector.h      Vec3 normalize / createCoordsSystem / reflectDir
 //   include/geometry/bound.h       Bound::cross (Smits slab test)
 //   include/math/filter.h          box / gauss filter kernels (film table entries)
-//   include/color/color.h          Rgb::clampProportionalRgb
+//   include/color/color.h          Rgb::clampProportionalRgb, colour-space conversions, HSV
+//   include/image/image_buffers.h  the image buffer pixel types (texture storage quantisation)
+//   include/math/interpolation.h   cubicInterpolate (bicubic texture lookups)
 //
 // oracle/Makefile compiles this file together with the two .cc files above, straight from
 // /root/reference, with the reference's Release flags (-O3 -DNDEBUG -DFAST_MATH -DFAST_TRIG,
@@ -30,6 +32,8 @@
 #include "geometry/bound.h"
 #include "math/filter.h"
 #include "color/color.h"
+#include "image/image_buffers.h"
+#include "math/interpolation.h"
 
 #include <cstdint>
 
@@ -177,6 +181,80 @@ void ref_clamp_proportional(const float *rgb, float max_value, float *out, int n
 		c.clampProportionalRgb(max_value);
 		out[3 * i] = c.r_; out[3 * i + 1] = c.g_; out[3 * i + 2] = c.b_;
 	}
+}
+
+
+// ---- texturing building blocks (image_buffers.h, color.h, interpolation.h) ----
+}
+template<class T> static Rgba roundTrip(const Rgba &c) { T px; px.setColor(c); return px.getColor(); }
+extern "C" {
+
+// kind: 0 Rgba1010108, 1 Rgb101010, 2 Rgba7773, 3 Rgb565, 4 Gray8, 5 Gray, 6 GrayAlpha, 7 RgbAlpha
+void ref_tex_quantize(int kind, const float *in, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const Rgba c{in[4 * i], in[4 * i + 1], in[4 * i + 2], in[4 * i + 3]};
+		Rgba r;
+		switch(kind)
+		{
+			case 0: r = roundTrip<Rgba1010108>(c); break;
+			case 1: r = roundTrip<Rgb101010>(c); break;
+			case 2: r = roundTrip<Rgba7773>(c); break;
+			case 3: r = roundTrip<Rgb565>(c); break;
+			case 4: r = roundTrip<Gray8>(c); break;
+			case 5: r = roundTrip<Gray>(c); break;
+			case 6: r = roundTrip<GrayAlpha>(c); break;
+			default: r = roundTrip<RgbAlpha>(c); break;
+		}
+		out[4 * i] = r.r_; out[4 * i + 1] = r.g_; out[4 * i + 2] = r.b_; out[4 * i + 3] = r.a_;
+	}
+}
+
+// dir 0: linearRgbFromColorSpace, 1: colorSpaceFromLinearRgb (rgb in/out, 3 floats)
+void ref_color_space(int dir, int cs, float gamma, const float *in, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		Rgb c{in[3 * i], in[3 * i + 1], in[3 * i + 2]};
+		if(dir == 0) c.linearRgbFromColorSpace((ColorSpace)cs, gamma);
+		else c.colorSpaceFromLinearRgb((ColorSpace)cs, gamma);
+		out[3 * i] = c.r_; out[3 * i + 1] = c.g_; out[3 * i + 2] = c.b_;
+	}
+}
+
+// rgbToHsv, s *= sat, h += hue (wrapped as texture.cc:230-240), hsvToRgb; sat_hue: 2 floats
+void ref_hsv_adjust(const float *in, const float *sat_hue, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		Rgb c{in[3 * i], in[3 * i + 1], in[3 * i + 2]};
+		float h = 0.f, s = 0.f, v = 0.f;
+		c.rgbToHsv(h, s, v);
+		s *= sat_hue[2 * i];
+		h += sat_hue[2 * i + 1];
+		if(h < 0.f) h += 6.f;
+		else if(h > 6.f) h -= 6.f;
+		c.hsvToRgb(h, s, v);
+		out[3 * i] = c.r_; out[3 * i + 1] = c.g_; out[3 * i + 2] = c.b_;
+	}
+}
+
+// cubicInterpolate over Rgba: in = 4 colours (16 floats) + x per element
+void ref_cubic(const float *in, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const float *p = in + 17 * i;
+		const Rgba y0{p[0], p[1], p[2], p[3]}, y1{p[4], p[5], p[6], p[7]}, y2{p[8], p[9], p[10], p[11]}, y3{p[12], p[13], p[14], p[15]};
+		const Rgba r = math::cubicInterpolate(y0, y1, y2, y3, p[16]);
+		out[4 * i] = r.r_; out[4 * i + 1] = r.g_; out[4 * i + 2] = r.b_; out[4 * i + 3] = r.a_;
+	}
+}
+
+void ref_pow(const float *ab, float *out, int n)
+{
+	for(int i = 0; i < n; ++i) out[i] = math::pow(ab[2 * i], ab[2 * i + 1]);
 }
 
 }

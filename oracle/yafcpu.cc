@@ -2553,4 +2553,69 @@ int yc_photon_map(const yc_scene *s, float *pos, float *dir, float *col, uint32_
 	return (int)n;
 }
 
+// ---- texturing building blocks (yaftex.h), pinned against oracle/_ref ref_tex_* ----
+void yc_tex_quantize(int kind, const float *in, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const yc::Rgba c(in[4 * i], in[4 * i + 1], in[4 * i + 2], in[4 * i + 3]);
+		yc::Rgba r;
+		switch(kind)
+		{
+			case 0: { yc::PxRgba1010108 p; p.set(c); r = p.get(); break; }
+			case 1: { yc::PxRgb101010 p; p.set(c); r = p.get(); break; }
+			case 2: { yc::PxRgba7773 p; p.set(c); r = p.get(); break; }
+			case 3: { yc::PxRgb565 p; p.set(c); r = p.get(); break; }
+			case 4: { yc::PxGray8 p; p.set(c); r = p.get(); break; }
+			case 5: { yc::PxGray p; p.set(c); r = p.get(); break; }
+			case 6: { yc::PxGrayAlpha p; p.set(c); r = p.get(); break; }
+			default: { yc::PxRgbAlpha p; p.set(c); r = p.get(); break; }
+		}
+		out[4 * i] = r.r; out[4 * i + 1] = r.g; out[4 * i + 2] = r.b; out[4 * i + 3] = r.a;
+	}
+}
+
+void yc_color_space(int dir, int cs, float gamma, const float *in, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		yc::Rgba c(in[3 * i], in[3 * i + 1], in[3 * i + 2], 1.f);
+		if(dir == 0) yc::linearRgbFromColorSpace(c, cs, gamma);
+		else yc::colorSpaceFromLinearRgb(c, cs, gamma);
+		out[3 * i] = c.r; out[3 * i + 1] = c.g; out[3 * i + 2] = c.b;
+	}
+}
+
+void yc_hsv_adjust(const float *in, const float *sat_hue, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		yc::Rgba c(in[3 * i], in[3 * i + 1], in[3 * i + 2], 1.f);
+		float h = 0.f, s = 0.f, v = 0.f;
+		yc::rgbToHsv(c, h, s, v);
+		s *= sat_hue[2 * i];
+		h += sat_hue[2 * i + 1];
+		if(h < 0.f) h += 6.f;
+		else if(h > 6.f) h -= 6.f;
+		yc::hsvToRgb(c, h, s, v);
+		out[3 * i] = c.r; out[3 * i + 1] = c.g; out[3 * i + 2] = c.b;
+	}
+}
+
+void yc_cubic(const float *in, float *out, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const float *p = in + 17 * i;
+		const yc::Rgba r = yc::OTexture::cubic(yc::Rgba(p[0], p[1], p[2], p[3]), yc::Rgba(p[4], p[5], p[6], p[7]),
+		                                       yc::Rgba(p[8], p[9], p[10], p[11]), yc::Rgba(p[12], p[13], p[14], p[15]), p[16]);
+		out[4 * i] = r.r; out[4 * i + 1] = r.g; out[4 * i + 2] = r.b; out[4 * i + 3] = r.a;
+	}
+}
+
+void yc_pow(const float *ab, float *out, int n)
+{
+	for(int i = 0; i < n; ++i) out[i] = yc::fpow(ab[2 * i], ab[2 * i + 1]);
+}
+
 }

@@ -3,6 +3,7 @@
     oracle/_ref, i.e. the reference sources compiled here), always;
 (2) the live reference building blocks on fresh random inputs, when oracle/_ref is built."""
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -86,3 +87,48 @@ def test_live_reference_random_inputs(o, oracle_built):
     x = rng.uniform(-50, 50, n).astype(np.float32)
     assert same(o.unary("sin", x), r.unary("sin", x))
     assert same(o.unary("cos", x), r.unary("cos", x))
+
+
+# ---- texturing building blocks (tests/golden/tex_prims.npz, made by make_golden_tex.py from the
+# reference's own image_buffers.h / color.h / interpolation.h / math.h) ----
+TEX_KINDS = {0: "Rgba1010108", 1: "Rgb101010", 2: "Rgba7773", 3: "Rgb565", 4: "Gray8", 5: "Gray", 6: "GrayAlpha", 7: "RgbAlpha"}
+
+
+@pytest.fixture(scope="module")
+def tex_golden():
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tex_prims.npz"))
+
+
+def test_oracle_texturing_primitives_bitexact(oracle_built, tex_golden):
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden_tex as M
+    g = tex_golden
+    got = M.run(oracle_built.oracle_lib(), "yc_", g["rgba"], g["rgb"], g["sat_hue"], g["cub"], g["ab"])
+    for k, v in got.items():
+        assert np.array_equal(v.view(np.uint32), g[k].view(np.uint32)), f"{k}: {(v.view(np.uint32) != g[k].view(np.uint32)).sum()} mismatches"
+
+
+def test_product_image_buffers_quantise_like_the_reference(product, tex_golden):
+    """yafaray_createImage + setImageColor / getImageColor through every buffer type (host code of
+    the drop-in library: no GPU involved) against the reference's own buffer classes."""
+    kinds = {0: ("ColorAlpha", "optimized"), 1: ("Color", "optimized"), 2: ("ColorAlpha", "compressed"),
+             3: ("Color", "compressed"), 4: ("Gray", "optimized"), 5: ("Gray", "none"), 6: ("GrayAlpha", "none"),
+             7: ("ColorAlpha", "none")}
+    rgba = tex_golden["rgba"][:1024]
+    yi = product.Interface()
+    yi.createScene()
+    for kind, (typ, opt) in kinds.items():
+        yi.paramsClearAll()
+        yi.paramsSetString("type", typ)
+        yi.paramsSetString("image_optimization", opt)
+        yi.paramsSetInt("width", 32)
+        yi.paramsSetInt("height", 32)
+        h = yi.createImage(f"img{kind}")
+        assert h, typ + "/" + opt
+        out = np.empty_like(rgba)
+        for i, c in enumerate(rgba):
+            yi.setImageColor(h, i % 32, i // 32, *map(float, c))
+            out[i] = yi.getImageColor(h, i % 32, i // 32)
+        ref = tex_golden[f"quant{kind}"][:1024]
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), f"{TEX_KINDS[kind]}: {(out != ref).sum()} mismatches"
+    yi.close()

@@ -71,9 +71,6 @@ def _compare(product, oracle_built, spec, tol_ulp=ULP_TOL, loose=False):
     return rgba, st
 
 
-pytestmark_gpu = pytest.mark.gpu
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", [c for c in T.CASES if c != "tube_sphere"])
 def test_textures_direct_light_match_oracle(product, oracle_built, case):
@@ -116,28 +113,3 @@ def test_test01_textured_matches_oracle(product, oracle_built):
     rgba, st = _compare(product, oracle_built, scenes.test01_textured(128, 128, spp=4))
     plain, _, _ = product.render_spec(scenes.test01(128, 128, spp=4))
     assert np.abs(rgba - plain).max() > 0.1
-
-
-@pytest.mark.gpu
-def test_image_buffers_quantise_like_the_reference(product):
-    """yafaray_setImageColor / getImageColor through each buffer type (image_buffers.h)."""
-    import ctypes as C
-    yi = product.Interface()
-    yi.createScene()
-    vals = [(0.1234, 0.5, 0.9999, 0.3), (1.7, -0.2, 0.0, 1.0), (0.00049, 0.0015, 0.5005, 0.51)]
-    expect = {
-        ("ColorAlpha", "optimized"): lambda c: [round(min(max(x, 0), 1e9) * 1023) % 1024 / 1023 for x in c[:3]] + [round(c[3] * 255) / 255],
-    }
-    for (typ, opt), fn in expect.items():
-        yi.paramsClearAll()
-        yi.paramsSetString("type", typ)
-        yi.paramsSetString("image_optimization", opt)
-        yi.paramsSetInt("width", 4)
-        yi.paramsSetInt("height", 2)
-        h = yi.createImage(f"{typ}_{opt}")
-        assert h
-        for k, c in enumerate(vals[:1]):
-            yi.setImageColor(h, k, 1, *c)
-            got = yi.getImageColor(h, k, 1)
-            np.testing.assert_allclose(got, np.float32(fn(c)), rtol=0, atol=1e-7)
-    yi.close()
