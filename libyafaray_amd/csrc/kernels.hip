@@ -1259,6 +1259,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 					{
 						v0p4 = f4(sp.p, __int_as_float(hit_prim));
 						v0wo4 = f4(wo, 0.f);
+						if(ATTR) { v0a0 = sa0; v0a1 = sa1; }
 					}
 					if(is_path && (sp.flags & B_DIFFUSE))
 					{
@@ -1475,6 +1476,11 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			A.N.p_prim[j] = v0p4;
 			A.N.wo_k[j] = f4(xyz(v0wo4), __uint_as_float(sid));
 			A.N.pix_mode[j] = make_uint4(__float_as_uint(col.r), __float_as_uint(col.g), __float_as_uint(col.b), __float_as_uint(alpha));
+			if(ATTR)
+			{
+				A.N.attr[2 * (size_t)j] = v0a0;
+				A.N.attr[2 * (size_t)j + 1] = v0a1;
+			}
 		}
 		PHASE(5);
 	}
@@ -1853,7 +1859,7 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 }
 
 // :162-219 — one bounce of every live photon path: intersect, deposit, scatter (material.cc:137-153)
-template<bool LDS_SCENE, bool WIDE>
+template<bool LDS_SCENE, bool WIDE, bool ATTR>
 __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 {
 	const DevScene &S = A.S;
@@ -1898,7 +1904,17 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 			int prim;
 			if(traverse<false, WIDE>(C, xyz(ro), xyz(rd), ro.w, __builtin_huge_valf(), t, prim, visits, tests))
 			{
-				const Surf sp = makeSurf(S, xyz(ro), xyz(rd), t, prim);
+				Surf sp = makeSurf(S, xyz(ro), xyz(rd), t, prim);
+				if(ATTR)
+				{
+					// the photon hit's textured colour / shading normal (initBsdf in diffuseWorker)
+					const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, xyz(ro), xyz(rd), sp.p);
+					const DevMaterial &m = S.mats[sp.mat];
+					C3 dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+					float drefl = 1.f;
+					if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl);
+					applyAttr(sp, f4(sa.n, drefl), f4(dcol, 0.f));
+				}
 				const V3 wi = -xyz(rd);
 				const C3 lcol = rgb(pc);
 				uint32_t flags = __float_as_uint(pc.w);
@@ -1923,7 +1939,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 					s.sampled = B_NONE;
 					float w = 0.f;
 					V3 wo = v3(0.f, 0.f, 0.f);
-					const C3 scol = matSample(S.mats[sp.mat], sp, wi, wo, s, w);
+					const C3 scol = matSample<ATTR>(S.mats[sp.mat], sp, wi, wo, s, w);
 					if(s.pdf > 1.0e-6f)
 					{
 						const C3 cnew = lcol * c3(1.f) * scol * w;
@@ -2033,7 +2049,7 @@ struct GatherArgs
 	uint64_t chunk_base;
 };
 
-template<bool SMALL>
+template<bool SMALL, bool ATTR>
 __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
@@ -2058,7 +2074,8 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		const float4 pp = A.N.p_prim[j], wk = A.N.wo_k[j];
 		const uint4 cb = A.N.pix_mode[j];
 		const V3 p = xyz(pp);
-		const Surf sp = surfFromPrim(S, p, __float_as_int(pp.w));
+		Surf sp = surfFromPrim(S, p, __float_as_int(pp.w));
+		if(ATTR) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
 		const V3 wo = xyz(wk);
 		const uint32_t sid = __float_as_uint(wk.w);
 		C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)};
@@ -2139,7 +2156,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 				const uint32_t ph = heap.i(i);
 				const float4 a = S.ph_pos[ph], b = S.ph_dir[ph];
 				const C3 pc = C3{a.w, b.w, S.ph_colb[ph]};
-				const C3 surf_col = matEval(m, sp, wo, xyz(b), B_DIFFUSE);
+				const C3 surf_col = matEval<ATTR>(m, sp, wo, xyz(b), B_DIFFUSE);
 				const C3 col_tmp = surf_col * scale * pc;
 				col = col + col_tmp;
 			}
@@ -2323,11 +2340,21 @@ hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_
 	if(S->scene_in_lds)
 	{
 		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
-		if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
-		else hipLaunchKernelGGL((k_photon_bounce<true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+		if(S->has_attr)
+		{
+			if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<true, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+			else hipLaunchKernelGGL((k_photon_bounce<true, false, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+		}
+		else if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<true, true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+		else hipLaunchKernelGGL((k_photon_bounce<true, false, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
 	}
-	else if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<false, true>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
-	else hipLaunchKernelGGL((k_photon_bounce<false, false>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
+	else if(S->has_attr)
+	{
+		if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<false, true, true>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
+		else hipLaunchKernelGGL((k_photon_bounce<false, false, true>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
+	}
+	else if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<false, true, false>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
+	else hipLaunchKernelGGL((k_photon_bounce<false, false, false>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
 	return hipGetLastError();
 }
 
@@ -2355,8 +2382,13 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const D
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
 	const size_t lds = gatherLdsBytes(*S, S->small_tables != 0);
-	if(S->small_tables) hipLaunchKernelGGL(k_gather<true>, dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
-	else hipLaunchKernelGGL(k_gather<false>, dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
+	if(S->has_attr)
+	{
+		if(S->small_tables) hipLaunchKernelGGL((k_gather<true, true>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
+		else hipLaunchKernelGGL((k_gather<false, true>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
+	}
+	else if(S->small_tables) hipLaunchKernelGGL((k_gather<true, false>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
+	else hipLaunchKernelGGL((k_gather<false, false>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
 	return hipGetLastError();
 }
 

@@ -484,11 +484,6 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	fillScenePointers(d, S);
 	stats_.photons = 0;
 	stats_.photon_seconds = 0.0;
-	if(S.integrator == INT_PHOTON && S.has_attr)
-	{
-		log_.error("PhotonIntegrator: textures / shader nodes / smooth normals are not evaluated by the GPU photon mapping path yet");
-		return false;
-	}
 	if(S.integrator == INT_PHOTON)
 	{
 		// PhotonIntegrator::preprocess (integrator_photon_mapping.cc:242-638): the photon map is

@@ -113,3 +113,18 @@ def test_test01_textured_matches_oracle(product, oracle_built):
     rgba, st = _compare(product, oracle_built, scenes.test01_textured(128, 128, spp=4))
     plain, _, _ = product.render_spec(scenes.test01(128, 128, spp=4))
     assert np.abs(rgba - plain).max() > 0.1
+
+
+@pytest.mark.gpu
+def test_textures_photon_mapping_match_oracle(product, oracle_built):
+    """PhotonIntegrator over textured / smooth materials: photon scattering uses the hit's shader
+    colour (k_photon_bounce<ATTR>), the density estimate the camera hit's (k_gather<ATTR>)."""
+    spec = build_case("layers", width=48, height=36, spp=1, sphere_smooth=60.0)
+    spec = spec.with_render(integrator="photonmapping", pm_photons=20000, pm_search=30, pm_diffuse_radius=0.4)
+    rgba, w, st = product.render_spec(spec)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
+    opos, _, _, _, _ = oracle_built.OracleScene(spec, threads=8).photon_map()
+    assert st["photons"] == len(opos)
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    u = ulp_diff(rgba, orgba)
+    assert u.max() <= ULP_TOL, f"max {u.max()} ULP"
