@@ -23,7 +23,9 @@ enum : uint32_t
 	B_ALL = B_SPECULAR | B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT | B_FILTER
 };
 
-enum : uint32_t { MAT_SHINYDIFFUSE = 0, MAT_LIGHT = 1 };
+enum : uint32_t { MAT_SHINYDIFFUSE = 0, MAT_LIGHT = 1, MAT_MIRROR = 2, MAT_NULL = 3 };
+// ShinyDiffuseMaterial components and options (material_shiny_diffuse.cc:38-87, 548-566)
+enum : uint32_t { SD_MIRROR = 1u, SD_TRANSPARENT = 2u, SD_TRANSLUCENT = 4u, SD_DIFFUSE = 8u, SD_FRESNEL = 16u, SD_TBIAS_MULT = 32u };
 enum : uint32_t { LIGHT_POINT = 0, LIGHT_AREA = 1 };
 enum : int { INT_DIRECT = 0, INT_PATH = 1, INT_PHOTON = 2 };
 
@@ -42,7 +44,12 @@ struct DevMaterial
 	// (material_shiny_diffuse.cc:242-247).
 	int node0, n_nodes, diffuse_root, drefl_root;
 	float emit_strength;
-	int pad2, pad3, pad4;
+	float tfilter;          // transmit_filter
+	float ior_sq;           // IOR^2 (Fresnel)
+	float tbias;            // transparentbias_factor (specularRefract, integrator_montecarlo.cc:890-898)
+	uint32_t sd_flags;      // SD_*
+	uint32_t pad2, pad3, pad4;
+	float mirror_col[4];    // shinydiffuse mirror_color; mirror material: colour * reflect
 };
 
 // ---- textures and shader nodes (src/texture/texture_image.cc, src/shader/shader_node_*.cc) ----
@@ -203,6 +210,21 @@ struct DevScene
 	const float4 *texels;
 	const DevTexture *textures;
 	const DevNode *shader_nodes;
+
+	// EXT kernels: materials beyond diffuse shinydiffuse / light_mat, shader nodes, or the specular
+	// recursion tree (MonteCarloIntegrator::recursiveRaytrace, integrator_montecarlo.cc:664-968):
+	// every integrate() call is a node; nodes of ray level L + 1 are spawned by the level-L pass
+	// and traced by the next pass; k_combine folds the tree bottom-up in the reference's order.
+	int ext, tree, raydepth, cur_level;
+	int bg_transp_refract;
+	uint32_t node_base;            // node id of spawn slot 0 (= level-0 capacity of the chunk)
+	uint32_t spawn_cap;
+	float4 *node_own;              // per node: colour before recursiveRaytrace's result, alpha
+	int2 *node_child;              // per node: reflect / refract child node ids (-1: none)
+	float4 *node_w;                // per node: the colour the parent multiplies this node's total by
+	float4 *spawn_o, *spawn_d;     // spawned rays (origin, tmin) (direction, tmax)
+	uint4 *spawn_pr;               // (pixel offset, sample index, MWC x, MWC c)
+	uint32_t *spawn_count;         // [0] spawned records, [1] overflow flag
 };
 
 struct DevFilm

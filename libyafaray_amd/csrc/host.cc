@@ -365,25 +365,32 @@ bool Scene::createMaterial(const std::string &name, const ParamMap &p, const std
 	{
 		float col[4] = {1.f, 1.f, 1.f, 1.f};
 		p.getColor("color", col);
-		float diffuse = 1.f, transparency = 0.f, translucency = 0.f, mirror = 0.f, emit = 0.f;
+		float diffuse = 1.f, transparency = 0.f, translucency = 0.f, mirror = 0.f, emit = 0.f, ior = 1.33f, tfilter = 1.f;
+		float tbias = 0.f, wire = 0.f;
+		float mcol[4] = {1.f, 1.f, 1.f, 1.f};
+		int add_depth = 0;
+		bool fresnel = false, tbias_mult = false;
 		p.get("diffuse_reflect", diffuse);
 		p.get("transparency", transparency);
 		p.get("translucency", translucency);
 		p.get("specular_reflect", mirror);
 		p.get("emit", emit);
-		bool fresnel = false;
+		p.get("IOR", ior);
+		p.get("transmit_filter", tfilter);
 		p.get("fresnel_effect", fresnel);
+		p.getColor("mirror_color", mcol);
+		p.get("transparentbias_factor", tbias);
+		p.get("transparentbias_multiply_raydepth", tbias_mult);
+		p.get("wireframe_amount", wire);
+		p.get("additionaldepth", add_depth);
 		std::string brdf;
-		if(mirror > 0.00001f || transparency > 0.00001f || translucency > 0.00001f || fresnel)
-		{
-			log.error("Material '" + name + "': specular / transparent / translucent / Fresnel shinydiffuse components are not supported by the GPU core yet");
-			return false;
-		}
 		if(p.get("diffuse_brdf", brdf) && brdf == "oren_nayar")
 		{
 			log.error("Material '" + name + "': Oren-Nayar diffuse BRDF is not supported by the GPU core yet");
 			return false;
 		}
+		if(wire > 0.f) log.warning("Material '" + name + "': wireframe shading is not evaluated by the GPU core; ignored");
+		if(add_depth > 0) log.warning("Material '" + name + "': additionaldepth is not evaluated by the GPU core (raydepth applies); ignored");
 		// shader nodes (material_shiny_diffuse.cc:579-660)
 		std::vector<DevNode> prog;
 		int droot = -1, rroot = -1;
@@ -396,10 +403,47 @@ bool Scene::createMaterial(const std::string &name, const ParamMap &p, const std
 		m.type = MAT_SHINYDIFFUSE;
 		for(int k = 0; k < 3; ++k) m.diffuse[k] = col[k];
 		for(int k = 0; k < 3; ++k) m.emit[k] = emit * col[k];     // emit_color_(emit_strength * diffuse_color)
+		for(int k = 0; k < 3; ++k) m.mirror_col[k] = mcol[k];
 		if(emit > 0.f) m.bsdf_flags |= B_EMIT;
-		const float acc = 1.f;
+		m.tfilter = tfilter;
+		m.tbias = tbias;
+		if(tbias_mult) m.sd_flags |= SD_TBIAS_MULT;
+		if(fresnel) { m.sd_flags |= SD_FRESNEL; m.ior_sq = ior * ior; }   // :560-565
+		// ShinyDiffuseMaterial::config (material_shiny_diffuse.cc:41-87): component order, flags
+		float acc = 1.f;
+		if(mirror > 0.00001f)
+		{
+			m.sd_flags |= SD_MIRROR;
+			if(!fresnel) acc = 1.f - mirror;
+			m.bsdf_flags |= B_SPECULAR | B_REFLECT;
+			m.c_flags[m.n_bsdf] = B_SPECULAR | B_REFLECT;
+			m.c_index[m.n_bsdf] = 0;
+			++m.n_bsdf;
+			m.comp[0] = mirror;
+		}
+		if(transparency * acc > 0.00001f)
+		{
+			m.sd_flags |= SD_TRANSPARENT;
+			acc *= 1.f - transparency;
+			m.bsdf_flags |= B_TRANSMIT | B_FILTER;
+			m.c_flags[m.n_bsdf] = B_TRANSMIT | B_FILTER;
+			m.c_index[m.n_bsdf] = 1;
+			++m.n_bsdf;
+			m.comp[1] = transparency;
+		}
+		if(translucency * acc > 0.00001f)
+		{
+			m.sd_flags |= SD_TRANSLUCENT;
+			acc *= 1.f - transparency;   // sic (:68): the transparency strength
+			m.bsdf_flags |= B_DIFFUSE | B_TRANSMIT;
+			m.c_flags[m.n_bsdf] = B_DIFFUSE | B_TRANSMIT;
+			m.c_index[m.n_bsdf] = 2;
+			++m.n_bsdf;
+			m.comp[2] = translucency;
+		}
 		if(diffuse * acc > 0.00001f)
 		{
+			m.sd_flags |= SD_DIFFUSE;
 			m.bsdf_flags |= B_DIFFUSE | B_REFLECT;
 			m.c_flags[m.n_bsdf] = B_DIFFUSE | B_REFLECT;
 			m.c_index[m.n_bsdf] = 3;
@@ -421,6 +465,22 @@ bool Scene::createMaterial(const std::string &name, const ParamMap &p, const std
 		m.bsdf_flags = B_EMIT;
 		for(int k = 0; k < 3; ++k) m.emit[k] = static_cast<float>(power) * col[k];
 		m.double_sided = ds ? 1 : 0;
+	}
+	else if(type == "mirror")
+	{
+		// MirrorMaterial (material_glass.cc:453-460, material_glass.h:86-91): ref_col_ = color * reflect
+		float col[4] = {1.f, 1.f, 1.f, 1.f};
+		float refl = 1.f;
+		p.getColor("color", col);
+		p.get("reflect", refl);
+		m.type = MAT_MIRROR;
+		m.bsdf_flags = B_SPECULAR;
+		for(int k = 0; k < 3; ++k) m.mirror_col[k] = col[k] * refl;
+	}
+	else if(type == "null")
+	{
+		m.type = MAT_NULL;   // NullMaterial: no BSDF components (material_glass.cc:463-473)
+		m.bsdf_flags = B_NONE;
 	}
 	else
 	{
@@ -917,9 +977,33 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		S.bounces = bounces;
 		S.path_samples = (S.integrator == INT_PATH) ? std::max(1, path_samples) : 1;
 		S.rr_min_bounces = rr_min;
-		bool bg_transp = false;
+		bool bg_transp = false, bg_transp_refract = false;
 		ip.get("bg_transp", bg_transp);
+		ip.get("bg_transp_refract", bg_transp_refract);
 		S.bg_transp = bg_transp ? 1 : 0;
+		S.bg_transp_refract = bg_transp_refract ? 1 : 0;
+		// specular recursion (integrator_direct_light.cc:152-192, integrator_path_tracer.cc:299-306)
+		int raydepth = 5;
+		ip.get("raydepth", raydepth);
+		S.raydepth = raydepth;
+		bool transp_shad = false;
+		ip.get("transpShad", transp_shad);
+		if(transp_shad) log.warning("Integrator: transparent shadows (transpShad) are not evaluated by the GPU core; opaque shadows are traced");
+		S.tree = 0;
+		S.ext = 0;
+		for(const auto &kv : materials)
+		{
+			const DevMaterial &m = kv.second;
+			if(m.bsdf_flags & (B_SPECULAR | B_FILTER)) S.tree = 1;
+			if(m.type == MAT_MIRROR || m.type == MAT_NULL || m.n_nodes > 0 || (m.sd_flags & (SD_MIRROR | SD_TRANSPARENT | SD_TRANSLUCENT | SD_FRESNEL)))
+				S.ext = 1;
+		}
+		if(S.integrator == INT_PHOTON && S.tree)
+		{
+			log.error("PhotonIntegrator: specular / transparent materials (caustic maps, recursive raytracing) are not supported by the GPU photon mapping path yet");
+			return false;
+		}
+
 		S.has_bg = 0;
 		if(!s.background_name.empty() && backgrounds.count(s.background_name))
 		{

@@ -637,7 +637,7 @@ struct Surf
 	V3 p, n, ng, nu, nv;
 	int mat;
 	uint32_t flags;
-	C3 dcol;          // diffuse shader colour (ATTR kernels only; else the material's colour is read)
+	C3 dcol;          // diffuse shader colour (read by EXT kernels only)
 	float drefl;      // diffuse_refl_shader scalar
 };
 
@@ -662,27 +662,70 @@ __device__ __forceinline__ Surf makeSurf(const DevScene &S, V3 o, V3 d, float t,
 	coordsSystem(s.n, s.nu, s.nv);
 	s.mat = __float_as_int(g.w);
 	s.flags = S.mats[s.mat].bsdf_flags;
+	const DevMaterial &m = S.mats[s.mat];
+	s.dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};   // read only by EXT kernels
+	s.drefl = 1.f;
 	return s;
 }
 
 __device__ __forceinline__ V3 faceForward(V3 ng, V3 n, V3 wo) { return (dot(ng, wo) < 0) ? -n : n; }
 
-// material_shiny_diffuse.cc:190-228, material_simple.cc (light_mat evaluates to black)
-template<bool ATTR = false>
+// ---- materials ----
+// Non-EXT kernels only see diffuse shinydiffuse / light_mat (the configs' materials) and keep the
+// lean arithmetic; EXT kernels run the whole ShinyDiffuseMaterial (mirror / transparent /
+// translucent / diffuse components with Fresnel, shader-node colours) and the mirror / null
+// materials (material_glass.cc:435-475).
+
+// material_shiny_diffuse.cc:102-114
+__device__ __forceinline__ float fresnelKr(const DevMaterial &m, V3 wo, V3 n)
+{
+	if(!(m.sd_flags & SD_FRESNEL)) return 1.f;
+	const V3 N = (dot(wo, n) < 0.f) ? -n : n;
+	const float c = dot(wo, N);
+	float g = m.ior_sq + c * c - 1.f;
+	if(g < 0.f) g = 0.f;
+	else g = sqrtf(g);
+	const float aux = c * (g + c);
+	return ((0.5f * (g - c) * (g - c)) / ((g + c) * (g + c))) * (1.f + ((aux - 1) * (aux - 1)) / ((aux + 1) * (aux + 1)));
+}
+
+// vector.h:255-260
+__device__ __forceinline__ V3 reflectDir(V3 normal, V3 v)
+{
+	const float vn = dot(v, normal);
+	if(vn < 0.f) return -v;
+	return 2.f * vn * normal - v;
+}
+
+// material_shiny_diffuse.cc:190-238 (eval), material_simple.cc / material_glass.cc (black)
+template<bool EXT = false>
 __device__ C3 matEval(const DevMaterial &m, const Surf &sp, V3 wo, V3 wl, uint32_t bsdfs)
 {
-	if(m.type == MAT_LIGHT) return c3(0.f);
+	if(m.type != MAT_SHINYDIFFUSE) return c3(0.f);
 	const V3 n = faceForward(sp.ng, sp.n, wo);
 	if(!(bsdfs & (m.bsdf_flags & B_DIFFUSE))) return c3(0.f);
-	const float m_t = (1.f - 1.f * m.comp[0]) * (1.f - m.comp[1]);
+	const C3 dcol = EXT ? sp.dcol : C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+	if(!EXT)
+	{
+		const float m_t = (1.f - 1.f * m.comp[0]) * (1.f - m.comp[1]);
+		if((double)dot(n, wl) < 0.0 && !m.flat) return c3(0.f);
+		const float m_d = m_t * (1.f - m.comp[2]) * m.comp[3];
+		return m_d * dcol;
+	}
+	const float cos_ng_wo = dot(sp.ng, wo);
+	const float cos_ng_wl = dot(sp.ng, wl);
+	const float kr = fresnelKr(m, wo, n);
+	const float m_t = (1.f - kr * m.comp[0]) * (1.f - m.comp[1]);
+	const bool transmit = (cos_ng_wo * cos_ng_wl) < 0.f;
+	if(transmit && (m.sd_flags & SD_TRANSLUCENT)) return m.comp[2] * m_t * dcol;
 	if((double)dot(n, wl) < 0.0 && !m.flat) return c3(0.f);
 	float m_d = m_t * (1.f - m.comp[2]) * m.comp[3];
-	if(ATTR && m.drefl_root >= 0) m_d *= sp.drefl;   // :235
-	return m_d * (ATTR ? sp.dcol : C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]});
+	if(m.drefl_root >= 0) m_d *= sp.drefl;   // :235
+	return m_d * dcol;
 }
 
 // material_shiny_diffuse.cc:242-247, material_simple.cc:50-55
-template<bool ATTR = false>
+template<bool EXT = false>
 __device__ C3 matEmit(const DevMaterial &m, const Surf &sp, V3 wo)
 {
 	if(m.type == MAT_LIGHT)
@@ -690,14 +733,15 @@ __device__ C3 matEmit(const DevMaterial &m, const Surf &sp, V3 wo)
 		if(m.double_sided) return C3{m.emit[0], m.emit[1], m.emit[2]};
 		return dot(wo, sp.n) > 0 ? C3{m.emit[0], m.emit[1], m.emit[2]} : c3(0.f);
 	}
-	if(ATTR && m.diffuse_root >= 0) return sp.dcol * m.emit_strength;
+	if(EXT && m.type != MAT_SHINYDIFFUSE) return c3(0.f);
+	if(EXT && m.diffuse_root >= 0) return sp.dcol * m.emit_strength;
 	return C3{m.emit[0], m.emit[1], m.emit[2]};
 }
 
-// material_shiny_diffuse.cc:107-119 (Kr = 1)
-__device__ __forceinline__ void accumulateComp(const float *c, float *a)
+// material_shiny_diffuse.cc:107-119 (accumulate with the Fresnel factor kr)
+__device__ __forceinline__ void accumulateComp(const float *c, float kr, float *a)
 {
-	a[0] = c[0] * 1.f;
+	a[0] = c[0] * kr;
 	float acc = 1.f - a[0];
 	a[1] = c[1] * acc;
 	acc *= 1.f - c[1];
@@ -706,26 +750,43 @@ __device__ __forceinline__ void accumulateComp(const float *c, float *a)
 	a[3] = c[3] * acc;
 }
 
+// material_shiny_diffuse.cc:457-475 getAlpha
+__device__ __forceinline__ float matAlpha(const DevMaterial &m, const Surf &sp, V3 wo)
+{
+	if(!(m.sd_flags & SD_TRANSPARENT)) return 1.f;
+	const V3 n = faceForward(sp.ng, sp.n, wo);
+	const float kr = fresnelKr(m, wo, n);
+	const float refl = (1.f - m.comp[0] * kr) * m.comp[1];
+	return 1.f - refl;
+}
+
 struct BsdfSample
 {
 	float s_1, s_2, pdf;
 	uint32_t flags, sampled;
 };
 
-// material_shiny_diffuse.cc:244-327 (diffuse reflect component), material_simple.cc:42-48
-template<bool ATTR = false>
+// material_shiny_diffuse.cc:249-337, material_simple.cc:42-48, material_glass.cc:435-468
+template<bool EXT = false>
 __device__ C3 matSample(const DevMaterial &m, const Surf &sp, V3 wo, V3 &wi, BsdfSample &s, float &w)
 {
-	if(m.type == MAT_LIGHT)
+	if(m.type == MAT_LIGHT || (EXT && m.type == MAT_NULL))
 	{
 		s.pdf = 0.f;
 		w = 0.f;
 		return c3(0.f);
 	}
+	if(EXT && m.type == MAT_MIRROR)
+	{
+		wi = reflectDir(sp.n, wo);
+		s.sampled = B_SPECULAR | B_REFLECT;
+		w = 1.f;
+		return C3{m.mirror_col[0], m.mirror_col[1], m.mirror_col[2]} * (1.f / fabsf(dot(sp.n, wi)));
+	}
 	const float cos_ng_wo = dot(sp.ng, wo);
 	const V3 n = faceForward(sp.ng, sp.n, wo);
 	float accum_c[4];
-	accumulateComp(m.comp, accum_c);
+	accumulateComp(m.comp, EXT ? fresnelKr(m, wo, n) : 1.f, accum_c);
 	float sum = 0.f, val[4], width[4];
 	uint32_t choice[4];
 	int n_match = 0, pick = -1;
@@ -752,26 +813,53 @@ __device__ C3 matSample(const DevMaterial &m, const Surf &sp, V3 wo, V3 &wi, Bsd
 	float s_1;
 	if(pick > 0) s_1 = (s.s_1 - val[pick - 1]) / width[pick];
 	else s_1 = s.s_1 / width[pick];
+	const C3 dcol = EXT ? sp.dcol : C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
 	C3 scolor = c3(0.f);
-	wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
-	if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * (ATTR ? sp.dcol : C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]});
-	s.pdf = fabsf(dot(wi, n)) * width[pick];
-	s.sampled = choice[pick];
+	const uint32_t ch = choice[pick];
+	if(EXT && ch == (B_SPECULAR | B_REFLECT))
+	{
+		wi = reflectDir(n, wo);
+		s.pdf = width[pick];
+		scolor = C3{m.mirror_col[0], m.mirror_col[1], m.mirror_col[2]} * (accum_c[0]);
+		scolor = scolor * (1.f / fmaxf(fabsf(dot(sp.n, wi)), 1.0e-6f));
+	}
+	else if(EXT && ch == (B_TRANSMIT | B_FILTER))
+	{
+		wi = -wo;
+		scolor = accum_c[1] * (m.tfilter * dcol + c3(1.f - m.tfilter));
+		if((double)fabsf(dot(wi, n)) < 1e-6) s.pdf = 0.f;
+		else s.pdf = width[pick];
+	}
+	else if(EXT && ch == (B_DIFFUSE | B_TRANSMIT))
+	{
+		wi = cosHemisphere(-n, sp.nu, sp.nv, s_1, s.s_2);
+		if(cos_ng_wo * dot(sp.ng, wi) < 0) scolor = accum_c[2] * dcol;
+		s.pdf = fabsf(dot(wi, n)) * width[pick];
+	}
+	else
+	{
+		wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
+		if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * dcol;
+		s.pdf = fabsf(dot(wi, n)) * width[pick];
+	}
+	s.sampled = ch;
 	w = fabsf(dot(wi, sp.n)) / (s.pdf * 0.99f + 0.01f);
-	const float alpha = 1.f;
+	const float alpha = EXT ? matAlpha(m, sp, wo) : 1.f;
 	w = w * (alpha) + 1.f * (1.f - alpha);
 	return scolor;
 }
 
-// material_shiny_diffuse.cc:329-366
+// material_shiny_diffuse.cc:339-377
+template<bool EXT = false>
 __device__ float matPdf(const DevMaterial &m, const Surf &sp, V3 wo, V3 wi, uint32_t bsdfs)
 {
-	if(m.type == MAT_LIGHT) return 0.f;
+	if(m.type != MAT_SHINYDIFFUSE) return 0.f;
 	if(!(bsdfs & B_DIFFUSE)) return 0.f;
 	float pdf = 0.f;
+	const float cos_ng_wo = dot(sp.ng, wo);
 	const V3 n = faceForward(sp.ng, sp.n, wo);
 	float accum_c[4];
-	accumulateComp(m.comp, accum_c);
+	accumulateComp(m.comp, EXT ? fresnelKr(m, wo, n) : 1.f, accum_c);
 	float sum = 0.f;
 	int n_match = 0;
 	for(int i = 0; i < (int)m.n_bsdf; ++i)
@@ -781,11 +869,62 @@ __device__ float matPdf(const DevMaterial &m, const Surf &sp, V3 wo, V3 wi, uint
 			const float width = accum_c[m.c_index[i]];
 			sum += width;
 			if(m.c_flags[i] == (B_DIFFUSE | B_REFLECT)) pdf += fabsf(dot(wi, n)) * width;
+			else if(EXT && m.c_flags[i] == (B_DIFFUSE | B_TRANSMIT) && cos_ng_wo * dot(sp.ng, wi) < 0) pdf += fabsf(dot(wi, n)) * width;
 			++n_match;
 		}
 	}
 	if(!n_match || (double)sum < 0.00001) return 0.f;
 	return pdf / sum;
+}
+
+// getSpecular: material_shiny_diffuse.cc:390-433, material_glass.cc:443-451 (mirror)
+struct SpecOut
+{
+	bool refl, refr;
+	V3 rdir, tdir;
+	C3 rcol, tcol;
+};
+__device__ SpecOut matSpecular(const DevMaterial &m, const Surf &sp, V3 wo)
+{
+	SpecOut o;
+	o.refl = o.refr = false;
+	o.rdir = o.tdir = v3(0.f, 0.f, 0.f);
+	o.rcol = o.tcol = c3(0.f);
+	if(m.type == MAT_MIRROR)
+	{
+		o.refl = true;
+		o.rcol = C3{m.mirror_col[0], m.mirror_col[1], m.mirror_col[2]};
+		o.rdir = reflectDir(faceForward(sp.ng, sp.n, wo), wo);
+		return o;
+	}
+	if(m.type != MAT_SHINYDIFFUSE) return o;
+	const bool backface = dot(wo, sp.ng) < 0.f;
+	const V3 n = backface ? -sp.n : sp.n;
+	const V3 ng = backface ? -sp.ng : sp.ng;
+	const float kr = fresnelKr(m, wo, n);
+	if(m.sd_flags & SD_TRANSPARENT)
+	{
+		o.refr = true;
+		o.tdir = -wo;
+		const C3 tcol = m.tfilter * sp.dcol + c3(1.f - m.tfilter);
+		o.tcol = (1.f - m.comp[0] * kr) * m.comp[1] * tcol;
+	}
+	if(m.sd_flags & SD_MIRROR)
+	{
+		o.refl = true;
+		const float vn = 2.f * (wo.x * n.x + wo.y * n.y + wo.z * n.z);   // Vec3::reflect (vector.h:227-232)
+		V3 d = v3(vn * n.x - wo.x, vn * n.y - wo.y, vn * n.z - wo.z);
+		const float cos_wi_ng = dot(d, ng);
+		if((double)cos_wi_ng < 0.01)
+		{
+			const float f = (float)(0.01 - (double)cos_wi_ng);
+			d = v3(d.x + f * ng.x, d.y + f * ng.y, d.z + f * ng.z);
+			d = normalize(d);
+		}
+		o.rdir = d;
+		o.rcol = C3{m.mirror_col[0], m.mirror_col[1], m.mirror_col[2]} * (m.comp[0] * kr);
+	}
+	return o;
 }
 
 __device__ __forceinline__ V3 lv(const float *a) { return v3(a[0], a[1], a[2]); }
@@ -843,7 +982,7 @@ __device__ __forceinline__ void shadowRayOf(V3 from, V3 dir, float tmin, float t
 // nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
 // Wave-uniform structure: `active` lanes do the work, every lane of the wave walks the same loop
 // bounds (the shadow-ray appends are wave-level).
-template<bool ATTR>
+template<bool EXT>
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
                          float4 *nee, uint8_t *occ, const ShadeOut &out)
@@ -868,7 +1007,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			ldir = ldir * (1.f / dist);
 			const C3 lcol = C3{L.color[0], L.color[1], L.color[2]} * idist_sqr;
 			const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
-			const C3 surf_col = matEval<ATTR>(m, sp, wo, ldir, B_ALL);
+			const C3 surf_col = matEval<EXT>(m, sp, wo, ldir, B_ALL);
 			const C3 transmit = c3(1.f);
 			contrib = surf_col * lcol * angle * transmit;
 			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
@@ -919,10 +1058,10 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 				const float pdf = x87mulDiv(kPi, dist_sqr, L.area * cos_angle);
 				if(pdf > 1e-6f)
 				{
-					const C3 surf_col = matEval<ATTR>(m, sp, wo, ldir, B_ALL);
+					const C3 surf_col = matEval<EXT>(m, sp, wo, ldir, B_ALL);
 					const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
 					float w = 1.f;
-					const float m_pdf = matPdf(m, sp, wo, ldir, B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT);
+					const float m_pdf = matPdf<EXT>(m, sp, wo, ldir, B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT);
 					if(m_pdf > 1e-6f)
 					{
 						const float l_2 = pdf * pdf;
@@ -958,7 +1097,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			s.pdf = 0.f;
 			s.sampled = B_NONE;
 			float W = 0.f;
-			const C3 surf_col = matSample<ATTR>(m, sp, wo, dir, s, W);
+			const C3 surf_col = matSample<EXT>(m, sp, wo, dir, s, W);
 			ok = s.pdf > 1e-6f;
 			float t = 0.f, cos_angle = 0.f;
 			if(ok)
@@ -1112,7 +1251,48 @@ __device__ __forceinline__ Surf surfFromPrim(const DevScene &S, V3 p, int prim)
 	coordsSystem(s.n, s.nu, s.nv);
 	s.mat = __float_as_int(g.w);
 	s.flags = S.mats[s.mat].bsdf_flags;
+	const DevMaterial &m = S.mats[s.mat];
+	s.dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+	s.drefl = 1.f;
 	return s;
+}
+
+// MonteCarloIntegrator::recursiveRaytrace (integrator_montecarlo.cc:925-968) for the integrate()
+// node `node` hit at ray level S.cur_level: the specular reflect / refract children of ray level
+// cur_level + 1 are appended to the spawn list (traced by the next pass) and linked to the node;
+// k_combine later adds their totals times the specular colours, reflect first.
+__device__ void spawnSpecular(const DevScene &S, const DevMaterial &m, const Surf &sp, V3 wo, uint32_t node, uint2 pix, uint2 rng)
+{
+	int2 child = make_int2(-1, -1);
+	const int level = S.cur_level + 1;
+	if((sp.flags & (B_SPECULAR | B_FILTER)) && level <= S.raydepth && level < 20)
+	{
+		const SpecOut so = matSpecular(m, sp, wo);
+		for(int k = 0; k < 2; ++k)
+		{
+			const bool want = k == 0 ? so.refl : so.refr;
+			if(!want) continue;
+			const uint32_t idx = atomicAdd(&S.spawn_count[0], 1u);
+			if(idx >= S.spawn_cap) { atomicOr(&S.spawn_count[1], 1u); continue; }
+			V3 from = sp.p;
+			const V3 dir = k == 0 ? so.rdir : so.tdir;
+			if(k == 1 && m.tbias > 0.f)
+			{
+				// specularRefract (:890-898): origin pushed along the refracted direction
+				float f = m.tbias;
+				if(m.sd_flags & SD_TBIAS_MULT) f *= (float)level;
+				from = sp.p + dir * f;
+			}
+			S.spawn_o[idx] = f4(from, S.ray_min_dist);
+			S.spawn_d[idx] = f4(dir, -1.f);
+			// the child's own Russian-roulette stream (statistical parity, as the camera's)
+			S.spawn_pr[idx] = make_uint4(pix.x, pix.y, rng.x ^ (0x9e3779b9u * (uint32_t)(2 * level + k + 1)), rng.y + 1u + (uint32_t)k);
+			S.node_w[S.node_base + idx] = f4(k == 0 ? so.rcol : so.tcol, 0.f);
+			if(k == 0) child.x = (int)(S.node_base + idx);
+			else child.y = (int)(S.node_base + idx);
+		}
+	}
+	S.node_child[node] = child;
 }
 
 // One path vertex per active queue entry.  Control flow restates PathIntegrator::integrate
@@ -1125,11 +1305,12 @@ __device__ __forceinline__ Surf surfFromPrim(const DevScene &S, V3 p, int prim)
 //   4. wave-ballot compaction: the entry's state moves to its position in the next queue
 //      (coalesced SoA reads and writes, no indirection);
 //   5. next-event estimation into the next state: contributions + shadow rays.
-template<bool SMALL, bool ATTR>
+template<bool SMALL, bool EXT>
 __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(ShadeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
 	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
+	const bool ATTR = EXT && S.has_attr != 0;   // k_surface output present
 	const DevPaths &Pc = A.Pc;
 	const DevPaths &Pn = A.Pn;
 	// workgroup b works on segment b and appends to segment b of the next queue
@@ -1242,18 +1423,24 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 					// integrator_tiled.cc:707-720 background
 					C3 bg = c3(0.f);
 					float a = 1.f;
-					if(S.bg_transp) a = 0.f;
+					if(S.bg_transp && (!EXT || S.cur_level == 0 || S.bg_transp_refract)) a = 0.f;
 					else if(S.has_bg) bg = C3{S.bg[0], S.bg[1], S.bg[2]};
-					writeSample(A, sid, bg, a);
+					if(EXT && S.tree)
+					{
+						S.node_own[sid] = f4(bg, a);
+						S.node_child[sid] = make_int2(-1, -1);
+					}
+					else writeSample(A, sid, bg, a);
 				}
 				else
 				{
 					const DevMaterial &m = S.mats[sp.mat];
+					if(EXT && S.tree) spawnSpecular(S, m, sp, wo, sid, make_uint2(offset, sample_idx), rng);
 					col = c3(0.f);
 					// photon_mapping.cc:868-869 adds emit(wo) unconditionally and :938-946 adds it again
 					// for emitting materials; the other integrators add it once (direct_light.cc:120)
-					if(is_photon) col = col + matEmit<ATTR>(m, sp, wo);
-					if(sp.flags & B_EMIT) col = col + matEmit<ATTR>(m, sp, wo);
+					if(is_photon) col = col + matEmit<EXT>(m, sp, wo);
+					if(sp.flags & B_EMIT) col = col + matEmit<EXT>(m, sp, wo);
 					if(sp.flags & B_DIFFUSE) { nee_v0 = true; flags |= F_V0_DIFFUSE; }
 					if(is_photon)
 					{
@@ -1282,7 +1469,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 					else wo = pwo;
 					nee_one = true;
 					flags = (flags & ~F_MATFLAGS) | (sp.flags & F_MATFLAGS);
-					if(sp.flags & B_EMIT) { emit_pend = matEmit<ATTR>(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
+					if(sp.flags & B_EMIT) { emit_pend = matEmit<EXT>(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
 					pend_thr = thr;
 					depth = 1;
 					sample_next = true;
@@ -1309,7 +1496,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 					if(killed) end_sub = true;
 					else
 					{
-						if((mfl & B_EMIT) && (flags & F_CAUSTIC)) { emit_pend = matEmit<ATTR>(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
+						if((mfl & B_EMIT) && (flags & F_CAUSTIC)) { emit_pend = matEmit<EXT>(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
 						if(mfl & B_DIFFUSE) { nee_one = true; pend_thr = thr; }
 						else
 						{
@@ -1364,7 +1551,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 				s.pdf = 0.f;
 				s.sampled = B_NONE;
 				V3 dir = v3(0.f, 0.f, 0.f);
-				C3 scol = matSample<ATTR>(S.mats[sp.mat], sp, wo, dir, s, w);
+				C3 scol = matSample<EXT>(S.mats[sp.mat], sp, wo, dir, s, w);
 				scol = scol * w;
 				if(isBlack(scol)) end_sub = true;
 				else
@@ -1400,7 +1587,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			s.pdf = 0.f;
 			s.sampled = B_NONE;
 			V3 dir = v3(0.f, 0.f, 0.f);
-			C3 scol = matSample<ATTR>(S.mats[s0.mat], s0, wo0, dir, s, w);
+			C3 scol = matSample<EXT>(S.mats[s0.mat], s0, wo0, dir, s, w);
 			thr = scol * w;
 			pwo = wo0;
 			if(s.sampled != B_NONE) flags |= F_SAMPLED;
@@ -1418,7 +1605,8 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 			// path_tracer.cc:274-278 / direct_light.cc:129-131
 			if(is_path && (flags & F_V0_DIFFUSE)) col = col + pcol / (float)n_paths;
 			col = col + c3(0.f);   // recursiveRaytrace: no specular/glossy component
-			writeSample(A, sid, col, alpha);
+			if(EXT && S.tree) S.node_own[sid] = f4(col, alpha);   // recursiveRaytrace's part: k_combine
+			else writeSample(A, sid, col, alpha);
 		}
 
 		PHASE(3);
@@ -1500,6 +1688,70 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 // shadow rays to the next queue (workgroup-level appends).
 // ---------------------------------------------------------------------------------------------
 // ---------------------------------------------------------------------------------------------
+// specular recursion tree: k_spawn starts the traced nodes of one ray level (the camera's role for
+// them), k_combine folds totals bottom-up (integrator_montecarlo.cc:866-968):
+//   total(node) = own + ((0 + total(reflect) * reflect colour) + total(refract) * refract colour)
+//   alpha(node) = children ? (sum of their alphas) / count : own alpha
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_spawn(DevScene S, DevPaths P, DevQueues Q, DevCounters cnt, uint32_t s0, int n)
+{
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if((uint32_t)i < S.n_seg)
+	{
+		const uint32_t groups = (uint32_t)n / 256u, rem = (uint32_t)n % 256u, sg = (uint32_t)i, R = S.n_seg;
+		cnt.n_active[sg] = (groups / R) * 256u + (sg < groups % R ? 256u : 0u) + (sg == groups % R ? rem : 0u);
+		cnt.n_shadow[sg] = 0;
+	}
+	if(i >= n) return;
+	const uint32_t g = (uint32_t)i / 256u;
+	const uint32_t a = (g % S.n_seg) * S.cap_a + (g / S.n_seg) * 256u + (uint32_t)i % 256u;
+	const uint32_t idx = s0 + (uint32_t)i;
+	Q.slot[a] = (int)(S.node_base + idx);
+	Q.ray_o[a] = S.spawn_o[idx];
+	Q.ray_d[a] = S.spawn_d[idx];
+	P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);
+	P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));
+	P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+	P.pr[a] = S.spawn_pr[idx];
+}
+
+// nodes [lo, hi) of one level; final: level 0, write the camera samples (integrator_tiled.cc:399)
+__global__ void __launch_bounds__(256) k_combine(DevScene S, uint32_t lo, uint32_t hi, int final_level, float4 *samples,
+                                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base)
+{
+	const uint32_t n = lo + blockIdx.x * blockDim.x + threadIdx.x;
+	if(n >= hi) return;
+	const float4 own = S.node_own[n];
+	const int2 ch = S.node_child[n];
+	C3 rt = c3(0.f);
+	float asum = 0.f;
+	int count = 0;
+	if(ch.x >= 0)
+	{
+		const float4 t = S.node_own[ch.x], w = S.node_w[ch.x];
+		rt = rt + C3{t.x, t.y, t.z} * C3{w.x, w.y, w.z};
+		asum += t.w;
+		++count;
+	}
+	if(ch.y >= 0)
+	{
+		const float4 t = S.node_own[ch.y], w = S.node_w[ch.y];
+		rt = rt + C3{t.x, t.y, t.z} * C3{w.x, w.y, w.z};
+		asum += t.w;
+		++count;
+	}
+	const C3 col = C3{own.x, own.y, own.z} + rt;
+	float alpha = count > 0 ? asum / (float)count : own.w;
+	if(final_level)
+	{
+		const SampleCoord sc = sampleAt(S, jobs, n_jobs, chunk_base + (uint64_t)n);
+		if(alpha > 1.f) alpha = 1.f;
+		samples[((size_t)sc.y * S.width + sc.x) * S.spp + sc.s] = f4(col, alpha);
+	}
+	else S.node_own[n] = f4(col, alpha);
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_surface: material-shade dispatch for scenes with textures / shader nodes / smooth normals.
 // For every hit of the active queue: barycentrics -> shading normal, orco, uv
 // (TrianglePrimitive::getSurface, primitive_triangle.cc:97-176), then the material's shader-node
@@ -1544,11 +1796,12 @@ struct NeeArgs
 #ifndef YAF_NEE_MIN_WAVES
 #define YAF_NEE_MIN_WAVES 1
 #endif
-template<bool SMALL, bool ATTR>
+template<bool SMALL, bool EXT>
 __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
 	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
+	const bool ATTR = EXT && S.has_attr != 0;
 	// workgroup b serves the NEE requests of segment b, shadow rays go to segment b
 	const uint32_t seg = blockIdx.x;
 	__shared__ uint32_t s_count;
@@ -1588,7 +1841,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs 
 		{
 			// estimateAllDirectLight (montecarlo.cc:54-68)
 			for(int l = 0; l < S.n_lights; ++l)
-				neeLight<ATTR>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
+				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
 				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out);
 		}
 		if(__any(one))
@@ -1598,7 +1851,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs 
 			{
 				const bool mine = one && lnum == (uint32_t)l;
 				if(!__any(mine)) continue;
-				neeLight<ATTR>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out);
+				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out);
 			}
 		}
 	}
@@ -1859,7 +2112,7 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 }
 
 // :162-219 — one bounce of every live photon path: intersect, deposit, scatter (material.cc:137-153)
-template<bool LDS_SCENE, bool WIDE, bool ATTR>
+template<bool LDS_SCENE, bool WIDE, bool EXT>
 __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 {
 	const DevScene &S = A.S;
@@ -1905,7 +2158,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 			if(traverse<false, WIDE>(C, xyz(ro), xyz(rd), ro.w, __builtin_huge_valf(), t, prim, visits, tests))
 			{
 				Surf sp = makeSurf(S, xyz(ro), xyz(rd), t, prim);
-				if(ATTR)
+				if(EXT && S.has_attr)
 				{
 					// the photon hit's textured colour / shading normal (initBsdf in diffuseWorker)
 					const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, xyz(ro), xyz(rd), sp.p);
@@ -1939,7 +2192,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 					s.sampled = B_NONE;
 					float w = 0.f;
 					V3 wo = v3(0.f, 0.f, 0.f);
-					const C3 scol = matSample<ATTR>(S.mats[sp.mat], sp, wi, wo, s, w);
+					const C3 scol = matSample<EXT>(S.mats[sp.mat], sp, wi, wo, s, w);
 					if(s.pdf > 1.0e-6f)
 					{
 						const C3 cnew = lcol * c3(1.f) * scol * w;
@@ -2049,11 +2302,12 @@ struct GatherArgs
 	uint64_t chunk_base;
 };
 
-template<bool SMALL, bool ATTR>
+template<bool SMALL, bool EXT>
 __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
 	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
+	const bool ATTR = EXT && S.has_attr != 0;
 	// per-lane heap and lookup stack, lane-interleaved after the staged tables
 	uint32_t *lds_words = reinterpret_cast<uint32_t *>(shade_smem) + shadeLdsBytes(A.S, SMALL) / 4;
 	const int k = S.pm_search;
@@ -2156,7 +2410,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 				const uint32_t ph = heap.i(i);
 				const float4 a = S.ph_pos[ph], b = S.ph_dir[ph];
 				const C3 pc = C3{a.w, b.w, S.ph_colb[ph]};
-				const C3 surf_col = matEval<ATTR>(m, sp, wo, xyz(b), B_DIFFUSE);
+				const C3 surf_col = matEval<EXT>(m, sp, wo, xyz(b), B_DIFFUSE);
 				const C3 col_tmp = surf_col * scale * pc;
 				col = col + col_tmp;
 			}
@@ -2272,13 +2526,29 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
 	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
-	if(S->has_attr)
+	if(S->ext)
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_shade<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 		else hipLaunchKernelGGL((k_shade<false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	}
 	else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	else hipLaunchKernelGGL((k_shade<false, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_spawn(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt, uint32_t s0, int n,
+                               hipStream_t st)
+{
+	const int grid = ((n > (int)S->n_seg ? n : (int)S->n_seg) + 255) / 256;
+	hipLaunchKernelGGL(k_spawn, dim3(grid), dim3(256), 0, st, *S, *P, *Q, *cnt, s0, n);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_combine(const DevScene *S, uint32_t lo, uint32_t hi, int final_level, float4 *samples, const DevJob *jobs,
+                                 int n_jobs, uint64_t chunk_base, hipStream_t st)
+{
+	if(hi <= lo) return hipSuccess;
+	hipLaunchKernelGGL(k_combine, dim3((hi - lo + 255) / 256), dim3(256), 0, st, *S, lo, hi, final_level, samples, jobs, n_jobs, chunk_base);
 	return hipGetLastError();
 }
 
@@ -2298,7 +2568,7 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	A.Qn = *Qn;
 	A.cnt_next = *cnt_next;
 	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
-	if(S->has_attr)
+	if(S->ext)
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_nee<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 		else hipLaunchKernelGGL((k_nee<false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
@@ -2340,7 +2610,7 @@ hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_
 	if(S->scene_in_lds)
 	{
 		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
-		if(S->has_attr)
+		if(S->ext)
 		{
 			if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<true, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
 			else hipLaunchKernelGGL((k_photon_bounce<true, false, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
@@ -2348,7 +2618,7 @@ hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_
 		else if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<true, true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
 		else hipLaunchKernelGGL((k_photon_bounce<true, false, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
 	}
-	else if(S->has_attr)
+	else if(S->ext)
 	{
 		if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<false, true, true>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
 		else hipLaunchKernelGGL((k_photon_bounce<false, false, true>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, A);
@@ -2382,7 +2652,7 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const D
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
 	const size_t lds = gatherLdsBytes(*S, S->small_tables != 0);
-	if(S->has_attr)
+	if(S->ext)
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_gather<true, true>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
 		else hipLaunchKernelGGL((k_gather<false, true>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);

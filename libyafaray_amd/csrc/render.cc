@@ -19,6 +19,10 @@ extern "C" {
 hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st);
 hipError_t yafamd_launch_surface(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, hipStream_t st);
+hipError_t yafamd_launch_spawn(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt, uint32_t s0, int n,
+                               hipStream_t st);
+hipError_t yafamd_launch_combine(const DevScene *S, uint32_t lo, uint32_t hi, int final_level, float4 *samples, const DevJob *jobs,
+                                 int n_jobs, uint64_t chunk_base, hipStream_t st);
 hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P,
                                DevStats *stats, int stack_depth, int *spill, int grid, hipStream_t st);
 int yafamd_trace_block();
@@ -97,6 +101,8 @@ struct GpuRenderer::Impl
 	Buf nodes, tris, prim_ng, mats, lights, faure, faure_dim, faure_inv;
 	// surface attributes, textures and shader-node programs (texeval.h)
 	Buf prim_attr, shader_nodes, textures, texels;
+	// specular recursion tree (k_spawn / k_combine): spawned rays and per-node records
+	Buf spawn_o, spawn_d, spawn_pr, node_own, node_child, node_w, spawn_count;
 	bool has_attr = false, attr_alloc = false;
 	int n_textures = 0;
 	// photon mapping: light selection Pdf1D, photon paths in flight, the map and its kd-tree
@@ -132,7 +138,8 @@ struct GpuRenderer::Impl
 		for(Buf *b : {&ph_lights, &light_cdf, &light_func, &ph_ray_o, &ph_ray_d, &ph_pcol, &ph_alive0, &ph_alive1, &ph_n_alive,
 		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes})
 			b->release();
-		for(Buf *b : {&prim_attr, &shader_nodes, &textures, &texels})
+		for(Buf *b : {&prim_attr, &shader_nodes, &textures, &texels, &spawn_o, &spawn_d, &spawn_pr, &node_own, &node_child, &node_w,
+		              &spawn_count})
 			b->release();
 		for(Buf *b : {&spill, &nodes, &tris, &prim_ng, &mats, &lights, &faure, &faure_dim, &faure_inv, &samples, &film,
 		              &weights, &jobs, &counters, &stats, &accum, &aa_flags, &aa_plist})
@@ -389,6 +396,7 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.shader_nodes = (const DevNode *)d.shader_nodes.p;
 	S.textures = (const DevTexture *)d.textures.p;
 	S.texels = (const float4 *)d.texels.p;
+	if(S.has_attr) S.ext = 1;
 }
 
 bool GpuRenderer::buildPhotonMap(RenderParams &rp)
@@ -536,6 +544,29 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	HIPCHECK(hipMemsetAsync(d.accum.p, 0, (size_t)W * H * sizeof(float4), d.stream));
 	// ---- chunk buffers ----
 	size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
+	if(S.tree)
+	{
+		// the recursion tree of a chunk holds up to 2^(raydepth + 1) - 2 spawned nodes per sample
+		// (88 B each): cap the level-0 chunk at 2 M samples and the spawn records at 64 per sample
+		M = std::min<size_t>(M, (size_t)1 << 21);
+		const int depth = std::max(0, std::min(S.raydepth, 5));
+		const size_t per = std::max<size_t>(2, ((size_t)1 << (depth + 1)) - 2);
+		const size_t cap = M * per;
+		if(!ensure(log_, d.spawn_o, cap * 16) || !ensure(log_, d.spawn_d, cap * 16) || !ensure(log_, d.spawn_pr, cap * 16) ||
+		   !ensure(log_, d.node_own, (M + cap) * 16) || !ensure(log_, d.node_child, (M + cap) * 8) || !ensure(log_, d.node_w, (M + cap) * 16) ||
+		   !ensure(log_, d.spawn_count, 16))
+			return false;
+		S.node_base = (uint32_t)M;
+		S.spawn_cap = (uint32_t)cap;
+		S.spawn_o = (float4 *)d.spawn_o.p;
+		S.spawn_d = (float4 *)d.spawn_d.p;
+		S.spawn_pr = (uint4 *)d.spawn_pr.p;
+		S.node_own = (float4 *)d.node_own.p;
+		S.node_child = (int2 *)d.node_child.p;
+		S.node_w = (float4 *)d.node_w.p;
+		S.spawn_count = (uint32_t *)d.spawn_count.p;
+	}
+	S.cur_level = 0;
 	const int K = std::max(1, S.nee_k);
 	const bool need_v0 = S.path_samples > 1 || S.integrator == INT_PHOTON;
 	// segment capacity: the camera deals groups of 256 samples round-robin over the segments
@@ -641,13 +672,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	size_t ev_i = 2;
 	HIPCHECK(hipEventRecord(d.ev_pool[0], d.stream));
 	// one pass: `n_total` camera samples (the jobs' enumeration, or S.plist x S.spp) through the wavefront
-	auto runSamples = [&](uint64_t n_total) -> bool {
-	if(rp.profile && !ensureEvents(ev_i + 4 * (size_t)((n_total + M - 1) / M) * (size_t)iters)) return false;
-	for(uint64_t base = 0; base < n_total; base += M)
-	{
-		if(canceled && *canceled) break;
-		const int n = (int)std::min<uint64_t>(M, n_total - base);
-		HIPCHECK(yafamd_launch_camera(&S, &d.P[0], &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
+	// one wavefront pass over the active list started by k_camera / k_spawn
+	auto iterate = [&](uint64_t base) -> bool {
 		int cur = 0;
 		for(int it = 0; it < iters; ++it)
 		{
@@ -669,6 +695,51 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			if(rp.profile) ev_i += 4;
 			cur ^= 1;
 		}
+		return true;
+	};
+	bool tree_overflow_logged = false;
+	// one pass: `n_total` camera samples (the jobs' enumeration, or S.plist x S.spp) through the wavefront
+	auto runSamples = [&](uint64_t n_total) -> bool {
+	if(rp.profile && !ensureEvents(ev_i + 4 * (size_t)((n_total + M - 1) / M) * (size_t)iters)) return false;
+	for(uint64_t base = 0; base < n_total; base += M)
+	{
+		if(canceled && *canceled) break;
+		const int n = (int)std::min<uint64_t>(M, n_total - base);
+		if(S.tree) HIPCHECK(hipMemsetAsync(d.spawn_count.p, 0, 16, d.stream));
+		S.cur_level = 0;
+		HIPCHECK(yafamd_launch_camera(&S, &d.P[0], &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
+		if(!iterate(base)) return false;
+		if(!S.tree) continue;
+		// recursiveRaytrace levels: the nodes the last pass spawned are the next pass's active list
+		std::vector<std::pair<uint32_t, uint32_t>> levels;
+		uint32_t done = 0;
+		for(int level = 1;; ++level)
+		{
+			uint32_t hc[2] = {0, 0};
+			HIPCHECK(hipMemcpyAsync(hc, d.spawn_count.p, 8, hipMemcpyDeviceToHost, d.stream));
+			HIPCHECK(hipStreamSynchronize(d.stream));
+			if(hc[1] && !tree_overflow_logged)
+			{
+				log_.error("Integrator: the specular recursion tree exceeded its " + std::to_string(S.spawn_cap) + " node records; deeper rays dropped");
+				tree_overflow_logged = true;
+			}
+			const uint32_t total_spawned = std::min(hc[0], S.spawn_cap);
+			if(total_spawned <= done) break;
+			S.cur_level = level;
+			if(rp.profile && !ensureEvents(ev_i + 4 * (size_t)((total_spawned - done + M - 1) / M) * (size_t)iters)) return false;
+			for(uint32_t sub = done; sub < total_spawned; sub += (uint32_t)M)
+			{
+				const int nn = (int)std::min<uint64_t>(M, total_spawned - sub);
+				HIPCHECK(yafamd_launch_spawn(&S, &d.P[0], &d.Q[0], &cnt[0], sub, nn, d.stream));
+				if(!iterate(base)) return false;
+			}
+			levels.push_back({done, total_spawned});
+			done = total_spawned;
+		}
+		for(size_t k = levels.size(); k-- > 0;)
+			HIPCHECK(yafamd_launch_combine(&S, S.node_base + levels[k].first, S.node_base + levels[k].second, 0, nullptr, nullptr, 0, 0, d.stream));
+		HIPCHECK(yafamd_launch_combine(&S, 0, (uint32_t)n, 1, (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
+		S.cur_level = 0;
 	}
 	return true;
 	};

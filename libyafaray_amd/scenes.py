@@ -35,6 +35,17 @@ class Material:
     double_sided: bool = False             # light_mat
     receive_shadows: bool = True
     flat_material: bool = False
+    # shinydiffuse specular / transparent / translucent components (material_shiny_diffuse.cc:490-566)
+    specular_reflect: float = 0.0
+    transparency: float = 0.0
+    translucency: float = 0.0
+    transmit_filter: float = 1.0
+    ior: float = 1.33
+    fresnel: bool = False
+    mirror_color: tuple = (1.0, 1.0, 1.0)
+    transparentbias_factor: float = 0.0
+    transparentbias_multiply_raydepth: bool = False
+    reflect: float = 1.0                   # type "mirror": colour * reflect
     # full typed parameter map {key: (kind, value)} (kinds s f i b v c m) and the pushed shader-node
     # lists, as a reference client passes them (tests/test01/test01.c:268-650); when set, apply()
     # issues exactly these instead of the fields above
@@ -112,6 +123,7 @@ class Render:
     caustic_type: str = "path"
     raydepth: int = 5
     bg_transp: bool = False
+    bg_transp_refract: bool = False
     shadow_bias_auto: bool = True
     shadow_bias: float = 0.0005
     ray_min_dist_auto: bool = True
@@ -403,7 +415,20 @@ def apply(spec: SceneSpec, api) -> None:
         if m.type == "light_mat":
             api.paramsSetFloat("power", m.power)
             api.paramsSetBool("double_sided", m.double_sided)
+        elif m.type == "mirror":
+            api.paramsSetFloat("reflect", m.reflect)
+        elif m.type == "null":
+            pass
         else:
+            api.paramsSetFloat("specular_reflect", m.specular_reflect)
+            api.paramsSetFloat("transparency", m.transparency)
+            api.paramsSetFloat("translucency", m.translucency)
+            api.paramsSetFloat("transmit_filter", m.transmit_filter)
+            api.paramsSetFloat("IOR", m.ior)
+            api.paramsSetBool("fresnel_effect", m.fresnel)
+            api.paramsSetColor("mirror_color", *m.mirror_color, 1.0)
+            api.paramsSetFloat("transparentbias_factor", m.transparentbias_factor)
+            api.paramsSetBool("transparentbias_multiply_raydepth", m.transparentbias_multiply_raydepth)
             api.paramsSetFloat("diffuse_reflect", m.diffuse_reflect)
             api.paramsSetFloat("emit", m.emit)
             api.paramsSetBool("receive_shadows", m.receive_shadows)
@@ -506,6 +531,7 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetString("type", r.integrator)
     api.paramsSetInt("raydepth", r.raydepth)
     api.paramsSetBool("bg_transp", r.bg_transp)
+    api.paramsSetBool("bg_transp_refract", r.bg_transp_refract)
     if r.integrator == "pathtracing":
         api.paramsSetInt("bounces", r.bounces)
         api.paramsSetInt("path_samples", r.path_samples)
@@ -557,3 +583,30 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetInt("threads_photons", r.threads_photons)
     api.setupRender()
     api.paramsClearAll()
+
+
+def cornell_specular(width=64, height=48, spp=2, integrator="directlighting", bounces=4, raydepth=5, fresnel=True,
+                     rr=False, **kw) -> SceneSpec:
+    """The C2 Cornell box with the shinydiffuse components the configs leave at zero and the mirror
+    material: tall box mirror + diffuse (Fresnel), short box transparent with a transmit filter
+    and translucency, back wall a `mirror` material (MonteCarloIntegrator::recursiveRaytrace,
+    material_shiny_diffuse.cc:249-433, material_glass.cc:435-460)."""
+    import dataclasses
+    s = cornell(width, height, spp=spp, bounces=bounces, rr=rr, integrator=integrator, **kw)
+    mats = list(s.materials) + [
+        Material("tall_mirror", color=(0.7, 0.7, 0.75), specular_reflect=0.7, fresnel=fresnel, ior=1.6,
+                 mirror_color=(0.9, 0.85, 0.8)),
+        Material("short_glassy", color=(0.3, 0.8, 0.4), transparency=0.7, transmit_filter=0.6, translucency=0.2,
+                 diffuse_reflect=0.5, specular_reflect=0.1, transparentbias_factor=0.001),
+        Material("back_mirror", type="mirror", color=(0.8, 0.9, 1.0), reflect=0.75)]
+    tri_mat = s.tri_mat.copy()
+    names = [o.name for o in s.objects]
+    for o in s.objects:
+        if o.name == "tall_box":
+            tri_mat[o.t0:o.t0 + o.nt] = len(s.materials)
+        elif o.name == "short_box":
+            tri_mat[o.t0:o.t0 + o.nt] = len(s.materials) + 1
+        elif o.name == "back":
+            tri_mat[o.t0:o.t0 + o.nt] = len(s.materials) + 2
+    r = dataclasses.replace(s.render, raydepth=raydepth)
+    return dataclasses.replace(s, materials=mats, tri_mat=tri_mat, render=r)

@@ -25,7 +25,10 @@ FILTERS = {"box": 0, "gauss": 1, "mitchell": 2, "lanczos": 3}
 class yc_material(C.Structure):
     _fields_ = [("type", C.c_int), ("color", C.c_float * 3), ("diffuse_strength", C.c_float),
                 ("emit_strength", C.c_float), ("double_sided", C.c_int), ("receive_shadows", C.c_int),
-                ("flat_material", C.c_int), ("diffuse_shader", C.c_int), ("diffuse_refl_shader", C.c_int)]
+                ("flat_material", C.c_int), ("diffuse_shader", C.c_int), ("diffuse_refl_shader", C.c_int),
+                ("specular_reflect", C.c_float), ("transparency", C.c_float), ("translucency", C.c_float),
+                ("transmit_filter", C.c_float), ("ior", C.c_float), ("fresnel_effect", C.c_int), ("mirror_color", C.c_float * 3),
+                ("transparentbias_factor", C.c_float), ("transparentbias_multiply_raydepth", C.c_int), ("reflect", C.c_float)]
 
 
 class yc_image(C.Structure):
@@ -81,7 +84,8 @@ class yc_render(C.Structure):
                 ("pm_threads", C.c_int), ("aa_passes", C.c_int), ("aa_inc_samples", C.c_int), ("aa_threshold", C.c_float),
                 ("aa_resampled_floor", C.c_float), ("aa_sample_multiplier_factor", C.c_float),
                 ("aa_detect_color_noise", C.c_int), ("aa_dark_detection_type", C.c_int),
-                ("aa_dark_threshold_factor", C.c_float), ("aa_variance_edge_size", C.c_int), ("aa_variance_pixels", C.c_int)]
+                ("aa_dark_threshold_factor", C.c_float), ("aa_variance_edge_size", C.c_int), ("aa_variance_pixels", C.c_int),
+                ("raydepth", C.c_int), ("bg_transp_refract", C.c_int)]
 
 
 class yc_scene(C.Structure):
@@ -472,7 +476,7 @@ class OracleScene:
         self.tri_mat = np.ascontiguousarray(s.tri_mat, np.int32).reshape(-1)
         mats = (yc_material * max(1, len(s.materials)))()
         for i, m in enumerate(s.materials):
-            mats[i].type = YC_MAT_LIGHT if m.type == "light_mat" else YC_MAT_SHINYDIFFUSE
+            mats[i].type = {"light_mat": YC_MAT_LIGHT, "mirror": 2, "null": 3}.get(m.type, YC_MAT_SHINYDIFFUSE)
             if m.type == "light_mat":
                 mats[i].color[:] = [np.float32(c) * np.float32(m.power) for c in m.color]
             else:
@@ -483,6 +487,13 @@ class OracleScene:
             mats[i].receive_shadows = int(m.receive_shadows)
             mats[i].flat_material = int(m.flat_material)
             mats[i].diffuse_shader = mats[i].diffuse_refl_shader = -1
+            mats[i].specular_reflect, mats[i].transparency = m.specular_reflect, m.transparency
+            mats[i].translucency, mats[i].transmit_filter = m.translucency, m.transmit_filter
+            mats[i].ior, mats[i].fresnel_effect = m.ior, int(m.fresnel)
+            mats[i].mirror_color[:] = list(m.mirror_color)
+            mats[i].transparentbias_factor = m.transparentbias_factor
+            mats[i].transparentbias_multiply_raydepth = int(m.transparentbias_multiply_raydepth)
+            mats[i].reflect = m.reflect
         lights = (yc_light * max(1, len(s.lights)))()
         for i, l in enumerate(s.render_lights()):
             lights[i].type = YC_LIGHT_POINT if l.type == "pointlight" else YC_LIGHT_AREA
@@ -544,6 +555,7 @@ class OracleScene:
         rp.aa_dark_detection_type = {"linear": 1, "curve": 2}.get(r.aa_dark_detection_type, 0)
         rp.aa_dark_threshold_factor = r.aa_dark_threshold_factor
         rp.aa_variance_edge_size, rp.aa_variance_pixels = r.aa_variance_edge_size, r.aa_variance_pixels
+        rp.raydepth, rp.bg_transp_refract = r.raydepth, int(r.bg_transp_refract)
         self.sc = sc
         self.spec = spec
         _texturing(self, spec, mats)

@@ -461,6 +461,9 @@ struct Material
 	float components[4] = {0.f, 0.f, 0.f, 0.f};
 	float emit_strength = 0.f;
 	int diffuse_shader = -1, diffuse_refl_shader = -1;   // shader-node roots (yc_scene.nodes)
+	bool is_mirror = false, is_transparent = false, is_translucent = false, fresnel = false, tbias_mult = false;
+	float ior_squared = 1.f, transmit_filter = 1.f, tbias = 0.f;
+	C3 mirror_color;          // shinydiffuse mirror colour / mirror material ref_col_
 	bool is_diffuse = false, double_sided = false, receive_shadows = true, flat = false;
 	int n_bsdf = 0;
 	unsigned c_flags[4];
@@ -712,6 +715,13 @@ Scene::Scene(const yc_scene &s)
 			mm.light_col = C3(m.color[0], m.color[1], m.color[2]);
 			mm.double_sided = m.double_sided != 0;
 		}
+		else if(m.type == YC_MAT_MIRROR)
+		{
+			// MirrorMaterial ctor (material_glass.h:86-91): ref_col_ = r_col * ref_val, flags Specular
+			mm.mirror_color = C3(m.color[0], m.color[1], m.color[2]) * m.reflect;
+			mm.bsdf_flags = BSpecular;
+		}
+		else if(m.type == YC_MAT_NULL) mm.bsdf_flags = BNone;
 		else
 		{
 			mm.diffuse_color = C3(m.color[0], m.color[1], m.color[2]);
@@ -719,8 +729,41 @@ Scene::Scene(const yc_scene &s)
 			mm.emit_strength = m.emit_strength;
 			mm.diffuse_shader = m.diffuse_shader;
 			mm.diffuse_refl_shader = m.diffuse_refl_shader;
+			mm.mirror_color = C3(m.mirror_color[0], m.mirror_color[1], m.mirror_color[2]);
+			mm.transmit_filter = m.transmit_filter;
+			mm.tbias = m.transparentbias_factor;
+			mm.tbias_mult = m.transparentbias_multiply_raydepth != 0;
+			if(m.fresnel_effect) { mm.fresnel = true; mm.ior_squared = m.ior * m.ior; }
 			if(m.emit_strength > 0.f) mm.bsdf_flags |= BEmit;
+			// ShinyDiffuseMaterial::config (material_shiny_diffuse.cc:41-87)
 			float acc = 1.f;
+			if(m.specular_reflect > 0.00001f)
+			{
+				mm.is_mirror = true;
+				if(!mm.fresnel) acc = 1.f - m.specular_reflect;
+				mm.bsdf_flags |= BSpecular | BReflect;
+				mm.c_flags[mm.n_bsdf] = BSpecular | BReflect;
+				mm.c_index[mm.n_bsdf] = 0;
+				++mm.n_bsdf;
+			}
+			if(m.transparency * acc > 0.00001f)
+			{
+				mm.is_transparent = true;
+				acc *= 1.f - m.transparency;
+				mm.bsdf_flags |= BTransmit | BFilter;
+				mm.c_flags[mm.n_bsdf] = BTransmit | BFilter;
+				mm.c_index[mm.n_bsdf] = 1;
+				++mm.n_bsdf;
+			}
+			if(m.translucency * acc > 0.00001f)
+			{
+				mm.is_translucent = true;
+				acc *= 1.f - m.transparency;
+				mm.bsdf_flags |= BDiffuse | BTransmit;
+				mm.c_flags[mm.n_bsdf] = BDiffuse | BTransmit;
+				mm.c_index[mm.n_bsdf] = 2;
+				++mm.n_bsdf;
+			}
 			if(m.diffuse_strength * acc > 0.00001f)
 			{
 				mm.is_diffuse = true;
@@ -729,7 +772,10 @@ Scene::Scene(const yc_scene &s)
 				mm.c_index[mm.n_bsdf] = 3;
 				++mm.n_bsdf;
 			}
-			// material_shiny_diffuse.cc:92-105 getComponents (no shader nodes)
+			// material_shiny_diffuse.cc:88-100 getComponents (no component shader nodes)
+			mm.components[0] = mm.is_mirror ? m.specular_reflect : 0.f;
+			mm.components[1] = mm.is_transparent ? m.transparency : 0.f;
+			mm.components[2] = mm.is_translucent ? m.translucency : 0.f;
 			mm.components[3] = mm.is_diffuse ? m.diffuse_strength : 0.f;
 		}
 		mats.push_back(mm);
@@ -1255,21 +1301,46 @@ class Renderer
 			a[3] = c[3] * acc;
 		}
 
-		// material_shiny_diffuse.cc:190-228
+		// material_shiny_diffuse.cc:102-114
+		static float fresnelKr(const Material &m, const V3 &wo, const V3 &n)
+		{
+			if(!m.fresnel) return 1.f;
+			const V3 N = (dot(wo, n) < 0.f) ? -n : n;
+			const float c = dot(wo, N);
+			float g = m.ior_squared + c * c - 1.f;
+			if(g < 0.f) g = 0.f;
+			else g = fsqrt(g);
+			const float aux = c * (g + c);
+			return ((0.5f * (g - c) * (g - c)) / ((g + c) * (g + c))) * (1.f + ((aux - 1) * (aux - 1)) / ((aux + 1) * (aux + 1)));
+		}
+		// vector.h:255-260
+		static V3 reflectDir(const V3 &normal, const V3 &v)
+		{
+			const float vn = dot(v, normal);
+			if(vn < 0.f) return -v;
+			return 2.f * vn * normal - v;
+		}
+
+		// material_shiny_diffuse.cc:196-238 (mirror / null / light materials evaluate to black)
 		C3 eval(const SurfacePoint &sp, const V3 &wo, const V3 &wl, unsigned bsdfs) const
 		{
 			const Material &m = *sp.mat;
-			if(m.type == YC_MAT_LIGHT) return C3(0.f);
+			if(m.type != YC_MAT_SHINYDIFFUSE) return C3(0.f);
+			const float cos_ng_wo = dot(sp.ng, wo);
+			const float cos_ng_wl = dot(sp.ng, wl);
 			const V3 n = faceForward(sp.ng, sp.n, wo);
 			if(!(bsdfs & (m.bsdf_flags & BDiffuse))) return C3(0.f);
-			const float m_t = (1.f - 1.f * m.components[0]) * (1.f - m.components[1]);
+			const float kr = fresnelKr(m, wo, n);
+			const float m_t = (1.f - kr * m.components[0]) * (1.f - m.components[1]);
+			const bool transmit = (cos_ng_wo * cos_ng_wl) < 0.f;
+			if(transmit && m.is_translucent) return m.components[2] * m_t * sp.dcol;
 			if(dot(n, wl) < 0.0 && !m.flat) return C3(0.f);
 			float m_d = m_t * (1.f - m.components[2]) * m.components[3];
 			if(m.diffuse_refl_shader >= 0) m_d *= sp.drefl;   // :235
 			return m_d * sp.dcol;
 		}
 
-		// material_shiny_diffuse.cc:237-242, material_simple.cc:50-55
+		// material_shiny_diffuse.cc:242-247, material_simple.cc:50-55
 		C3 emit(const SurfacePoint &sp, const V3 &wo) const
 		{
 			const Material &m = *sp.mat;
@@ -1279,24 +1350,44 @@ class Renderer
 				const float angle = dot(wo, sp.n);
 				return angle > 0 ? m.light_col : C3(0.f);
 			}
+			if(m.type != YC_MAT_SHINYDIFFUSE) return C3(0.f);
 			if(m.diffuse_shader >= 0) return sp.dcol * m.emit_strength;   // :242-247
 			return m.emit_color;
 		}
 
-		// material_shiny_diffuse.cc:244-327 (diffuse-reflect branch), material_simple.cc:42-48
+		// material_shiny_diffuse.cc:457-475
+		static float getAlpha(const SurfacePoint &sp, const V3 &wo)
+		{
+			const Material &m = *sp.mat;
+			if(!m.is_transparent) return 1.f;
+			const V3 n = faceForward(sp.ng, sp.n, wo);
+			const float kr = fresnelKr(m, wo, n);
+			const float refl = (1.f - m.components[0] * kr) * m.components[1];
+			return 1.f - refl;
+		}
+
+		// material_shiny_diffuse.cc:249-337, material_simple.cc:42-48, material_glass.cc:435-468
 		C3 sample(const SurfacePoint &sp, const V3 &wo, V3 &wi, Sample &s, float &w) const
 		{
 			const Material &m = *sp.mat;
-			if(m.type == YC_MAT_LIGHT)
+			if(m.type == YC_MAT_LIGHT || m.type == YC_MAT_NULL)
 			{
 				s.pdf = 0.f;
 				w = 0.f;
 				return C3(0.f);
 			}
+			if(m.type == YC_MAT_MIRROR)
+			{
+				wi = reflectDir(sp.n, wo);
+				s.sampled_flags = BSpecular | BReflect;
+				w = 1.f;
+				return m.mirror_color * (1.f / std::abs(dot(sp.n, wi)));
+			}
 			const float cos_ng_wo = dot(sp.ng, wo);
 			const V3 n = faceForward(sp.ng, sp.n, wo);
+			const float kr = fresnelKr(m, wo, n);
 			float accum_c[4];
-			accumulate(m.components, 1.f, accum_c);
+			accumulate(m.components, kr, accum_c);
 			float sum = 0.f, val[4], width[4];
 			unsigned choice[4];
 			int n_match = 0, pick = -1;
@@ -1324,27 +1415,49 @@ class Renderer
 			if(pick > 0) s_1 = (s.s_1 - val[pick - 1]) / width[pick];
 			else s_1 = s.s_1 / width[pick];
 			C3 scolor(0.f);
-			// DiffuseReflect (the only component a plain shinydiffuse configures here)
-			wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
-			if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * sp.dcol;
-			s.pdf = std::abs(dot(wi, n)) * width[pick];
+			switch(choice[pick])
+			{
+				case(BSpecular | BReflect):
+					wi = reflectDir(n, wo);
+					s.pdf = width[pick];
+					scolor = m.mirror_color * (accum_c[0]);
+					scolor *= 1.f / std::max(std::abs(dot(sp.n, wi)), 1.0e-6f);
+					break;
+				case(BTransmit | BFilter):
+					wi = -wo;
+					scolor = accum_c[1] * (m.transmit_filter * sp.dcol + C3(1.f - m.transmit_filter));
+					if(std::abs(dot(wi, n)) < 1e-6) s.pdf = 0.f;
+					else s.pdf = width[pick];
+					break;
+				case(BDiffuse | BTransmit):
+					wi = cosHemisphere(-n, sp.nu, sp.nv, s_1, s.s_2);
+					if(cos_ng_wo * dot(sp.ng, wi) < 0) scolor = accum_c[2] * sp.dcol;
+					s.pdf = std::abs(dot(wi, n)) * width[pick];
+					break;
+				default:
+					wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
+					if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * sp.dcol;
+					s.pdf = std::abs(dot(wi, n)) * width[pick];
+					break;
+			}
 			s.sampled_flags = choice[pick];
 			w = std::abs(dot(wi, sp.n)) / (s.pdf * 0.99f + 0.01f);
-			const float alpha = 1.f;
+			const float alpha = getAlpha(sp, wo);
 			w = w * (alpha) + 1.f * (1.f - alpha);
 			return scolor;
 		}
 
-		// material_shiny_diffuse.cc:329-366
+		// material_shiny_diffuse.cc:339-377
 		float pdf(const SurfacePoint &sp, const V3 &wo, const V3 &wi, unsigned bsdfs) const
 		{
 			const Material &m = *sp.mat;
-			if(m.type == YC_MAT_LIGHT) return 0.f;
+			if(m.type != YC_MAT_SHINYDIFFUSE) return 0.f;
 			if(!(bsdfs & BDiffuse)) return 0.f;
 			float pdf = 0.f;
+			const float cos_ng_wo = dot(sp.ng, wo);
 			const V3 n = faceForward(sp.ng, sp.n, wo);
 			float accum_c[4];
-			accumulate(m.components, 1.f, accum_c);
+			accumulate(m.components, fresnelKr(m, wo, n), accum_c);
 			float sum = 0.f, width;
 			int n_match = 0;
 			for(int i = 0; i < m.n_bsdf; ++i)
@@ -1353,12 +1466,100 @@ class Renderer
 				{
 					width = accum_c[m.c_index[i]];
 					sum += width;
-					if(m.c_flags[i] == (BDiffuse | BReflect)) pdf += std::abs(dot(wi, n)) * width;
+					if(m.c_flags[i] == (BDiffuse | BTransmit)) { if(cos_ng_wo * dot(sp.ng, wi) < 0) pdf += std::abs(dot(wi, n)) * width; }
+					else if(m.c_flags[i] == (BDiffuse | BReflect)) pdf += std::abs(dot(wi, n)) * width;
 					++n_match;
 				}
 			}
 			if(!n_match || sum < 0.00001) return 0.f;
 			return pdf / sum;
+		}
+
+		// getSpecular: material_shiny_diffuse.cc:390-433, material_glass.cc:443-451 (mirror)
+		struct Specular { bool refl = false, refr = false; V3 rdir, tdir; C3 rcol, tcol; };
+		Specular getSpecular(const SurfacePoint &sp, const V3 &wo) const
+		{
+			Specular r;
+			const Material &m = *sp.mat;
+			if(m.type == YC_MAT_MIRROR)
+			{
+				r.refl = true;
+				r.rcol = m.mirror_color;
+				r.rdir = reflectDir(faceForward(sp.ng, sp.n, wo), wo);
+				return r;
+			}
+			if(m.type != YC_MAT_SHINYDIFFUSE) return r;
+			const bool backface = dot(wo, sp.ng) < 0.f;
+			const V3 n = backface ? -sp.n : sp.n;
+			const V3 ng = backface ? -sp.ng : sp.ng;
+			const float kr = fresnelKr(m, wo, n);
+			if(m.is_transparent)
+			{
+				r.refr = true;
+				r.tdir = -wo;
+				const C3 tcol = m.transmit_filter * sp.dcol + C3(1.f - m.transmit_filter);
+				r.tcol = (1.f - m.components[0] * kr) * m.components[1] * tcol;
+			}
+			if(m.is_mirror)
+			{
+				r.refl = true;
+				V3 d = wo;
+				const float vn = 2.f * (d.x * n.x + d.y * n.y + d.z * n.z);   // Vec3::reflect
+				d = V3(vn * n.x - d.x, vn * n.y - d.y, vn * n.z - d.z);
+				const float cos_wi_ng = dot(d, ng);
+				if(cos_wi_ng < 0.01)
+				{
+					d += static_cast<float>(0.01 - cos_wi_ng) * ng;
+					d.normalize();
+				}
+				r.rdir = d;
+				r.rcol = m.mirror_color * (m.components[0] * kr);
+			}
+			return r;
+		}
+
+		// MonteCarloIntegrator::recursiveRaytrace (integrator_montecarlo.cc:925-968) with the
+		// specular reflect / refract branches (:866-923); `ray_level` is the recursion's (caller + 1)
+		void recursiveRaytrace(Thread &th, Mwc &rng, int ray_level, unsigned bsdfs, const SurfacePoint &sp, const V3 &wo,
+		                       uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha) const
+		{
+			col = C3(0.f);
+			float asum = 0.f;
+			int count = 0;
+			if(ray_level <= sc_.rp.raydepth && ray_level < 20 && (bsdfs & (BGlossy | BSpecular | BFilter)) && (bsdfs & (BSpecular | BFilter)))
+			{
+				const Specular spec = getSpecular(sp, wo);
+				const Material &m = *sp.mat;
+				for(int k = 0; k < 2; ++k)
+				{
+					if(!(k == 0 ? spec.refl : spec.refr)) continue;
+					Ray ref_ray;
+					ref_ray.dir = k == 0 ? spec.rdir : spec.tdir;
+					ref_ray.from = sp.p;
+					if(k == 1 && m.tbias > 0.f)
+					{
+						float f = m.tbias;
+						if(m.tbias_mult) f *= ray_level;
+						ref_ray.from = sp.p + ref_ray.dir * f;
+					}
+					ref_ray.tmin = sc_.rp.ray_min_dist;
+					ref_ray.tmax = -1.f;
+					C3 c;
+					float a;
+					integrate(th, ref_ray, rng, sample_idx, offset, c, a, ray_level);
+					c *= (k == 0 ? spec.rcol : spec.tcol);
+					col += c;
+					asum += a;
+					++count;
+				}
+			}
+			alpha = count > 0 ? asum / count : 1.f;
+		}
+
+		void integrate(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level) const
+		{
+			if(sc_.rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha, ray_level);
+			else integrateDirect(th, ray, rng, sample_idx, offset, col, alpha, ray_level);
 		}
 
 		float shadowTmin(const SurfacePoint &sp) const
@@ -1560,15 +1761,15 @@ class Renderer
 		}
 
 		// integrator_tiled.cc:707-720
-		void background(const Ray &, C3 &col, float &alpha) const
+		void background(const Ray &, C3 &col, float &alpha, int ray_level = 0) const
 		{
-			if(sc_.rp.bg_transp) { col = C3(0.f); alpha = 0.f; }
+			if(sc_.rp.bg_transp && (ray_level == 0 || sc_.rp.bg_transp_refract)) { col = C3(0.f); alpha = 0.f; }
 			else if(sc_.rp.has_background) { col = C3(sc_.rp.bg_color[0], sc_.rp.bg_color[1], sc_.rp.bg_color[2]); alpha = 1.f; }
 			else { col = C3(0.f); alpha = 1.f; }
 		}
 
 		// integrator_direct_light.cc:97-144
-		void integrateDirect(Thread &th, Ray &ray, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha) const
+		void integrateDirect(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level = 0) const
 		{
 			col = C3(0.f);
 			alpha = 1.f;
@@ -1579,21 +1780,22 @@ class Renderer
 				const V3 wo = -ray.dir;
 				if(mat_bsdfs & BEmit) col += emit(sp, wo);
 				if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
-				col += C3(0.f);  // recursiveRaytrace: no specular/glossy components here (montecarlo.cc:918-968)
-				alpha = 1.f;
+				C3 rcol;
+				recursiveRaytrace(th, rng, ray_level + 1, mat_bsdfs, sp, wo, sample_idx, offset, rcol, alpha);
+				col += rcol;
 			}
-			else background(ray, col, alpha);
+			else background(ray, col, alpha, ray_level);
 		}
 
 		// integrator_path_tracer.cc:120-290
-		void integratePath(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha) const
+		void integratePath(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level = 0) const
 		{
 			const yc_render &rp = sc_.rp;
 			col = C3(0.f);
 			alpha = 1.f;
 			float w = 0.f;
 			SurfacePoint sp;
-			if(!intersect(th, ray, sp)) { background(ray, col, alpha); return; }
+			if(!intersect(th, ray, sp)) { background(ray, col, alpha, ray_level); return; }
 			const unsigned mat_bsdfs = sp.bsdf_flags;
 			const V3 wo = -ray.dir;
 			if(mat_bsdfs & BEmit) col += emit(sp, wo);
@@ -1662,8 +1864,9 @@ class Renderer
 				}
 				col += path_col / static_cast<float>(n_samples);
 			}
-			col += C3(0.f);  // recursiveRaytrace (no specular/glossy here)
-			alpha = 1.f;
+			C3 rcol;
+			recursiveRaytrace(th, rng, ray_level + 1, mat_bsdfs, sp, wo, sample_idx, offset, rcol, alpha);
+			col += rcol;
 		}
 
 		// ------------------------------------------------------------------------------------
@@ -2057,7 +2260,7 @@ class Renderer
 				float alpha;
 				if(rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha);
 				else if(rp.integrator == YC_INT_PHOTON) integratePhoton(th, ray, sample_idx, offset, col, alpha);
-				else integrateDirect(th, ray, sample_idx, offset, col, alpha);
+				else integrateDirect(th, ray, rng, sample_idx, offset, col, alpha);
 				if(alpha > 1.f) alpha = 1.f;
 				out[4 * sample] = col.r;
 				out[4 * sample + 1] = col.g;
@@ -2394,7 +2597,7 @@ int yc_render_samples(const yc_scene *s, int n, const int *xys, float *rgba)
 		const uint32_t sample_idx = rp.base_sampling_offset + sample;
 		if(rp.integrator == YC_INT_PATH) R.integratePath(th, ray, rng, sample_idx, offset, col, alpha);
 		else if(rp.integrator == YC_INT_PHOTON) R.integratePhoton(th, ray, sample_idx, offset, col, alpha);
-		else R.integrateDirect(th, ray, sample_idx, offset, col, alpha);
+		else R.integrateDirect(th, ray, rng, sample_idx, offset, col, alpha);
 		rgba[4 * k] = col.r; rgba[4 * k + 1] = col.g; rgba[4 * k + 2] = col.b; rgba[4 * k + 3] = std::min(alpha, 1.f);
 	}
 	return 0;

@@ -17,7 +17,7 @@
 
 extern "C" {
 
-enum { YC_MAT_SHINYDIFFUSE = 0, YC_MAT_LIGHT = 1 };
+enum { YC_MAT_SHINYDIFFUSE = 0, YC_MAT_LIGHT = 1, YC_MAT_MIRROR = 2, YC_MAT_NULL = 3 };
 enum { YC_LIGHT_POINT = 0, YC_LIGHT_AREA = 1 };
 enum { YC_INT_DIRECT = 0, YC_INT_PATH = 1, YC_INT_PHOTON = 2 };
 enum { YC_FILTER_BOX = 0, YC_FILTER_GAUSS = 1, YC_FILTER_MITCHELL = 2, YC_FILTER_LANCZOS = 3 };
@@ -32,6 +32,14 @@ typedef struct {
 	int flat_material;
 	int diffuse_shader;       // shader-node roots (indices into yc_scene.nodes, -1: none)
 	int diffuse_refl_shader;
+	// shinydiffuse specular / transparent / translucent components (material_shiny_diffuse.cc:490-566);
+	// mirror material: color * reflect (material_glass.cc:453-460)
+	float specular_reflect, transparency, translucency, transmit_filter, ior;
+	int fresnel_effect;
+	float mirror_color[3];
+	float transparentbias_factor;
+	int transparentbias_multiply_raydepth;
+	float reflect;            // mirror material
 } yc_material;
 
 // ---- texturing (material_node.cc, texture_image.cc, shader_node_*.cc; see yaftex.h) ----
@@ -136,6 +144,8 @@ typedef struct {
 	float aa_dark_threshold_factor;
 	int aa_variance_edge_size;
 	int aa_variance_pixels;
+	int raydepth;             // recursiveRaytrace depth (DirectLight / PathIntegrator "raydepth")
+	int bg_transp_refract;
 } yc_render;
 
 typedef struct {
