@@ -217,6 +217,11 @@ struct DevScene
 	// and traced by the next pass; k_combine folds the tree bottom-up in the reference's order.
 	int ext, tree, raydepth, cur_level;
 	int bg_transp_refract;
+	// transparent shadows (MonteCarloIntegrator tr_shad_ / s_depth_, accelerator_kdtree.cc:916-1061):
+	// shadow rays keep tmin in sh_o.w, k_trace<TS> lists the transparent surfaces each one crosses
+	// (DevQueues::ts_hit, s_depth per ray), k_tshadow multiplies their filter colours into the
+	// NEE contributions whose factors k_nee kept in DevPaths::ts
+	int tr_shad, s_depth;
 	uint32_t node_base;            // node id of spawn slot 0 (= level-0 capacity of the chunk)
 	uint32_t spawn_cap;
 	float4 *node_own;              // per node: colour before recursiveRaytrace's result, alpha
@@ -251,6 +256,8 @@ struct DevPaths
 	uint4 *pr;             // (PixelSamplingData::offset_, PixelSamplingData::sample_, MWC x, MWC c)
 	float4 *nee;           // [slots * nee_k] contributions .w = valid
 	uint8_t *occ;          // [slots * nee_k] shadow results
+	float4 *ts;            // [3 * slots * nee_k] transparent shadows: the contribution's factors
+	                       // (surf colour, a) (light colour, b) (c, c divides) — contrib = ((surf * (L * scol)) * a) * b  (* or /) c
 	float4 *v0attr;        // [2 * slots] first-hit surface attributes (has_attr && path_samples > 1)
 };
 
@@ -263,9 +270,11 @@ struct DevQueues
 	float *hit_t;
 	int *hit_prim;
 	// shadow rays
-	float4 *sh_o;          // origin, .w unused
+	float4 *sh_o;          // origin, .w = tmin of the light ray (read by transparent shadows only)
 	float4 *sh_d;          // direction, .w = t_max (already tmax - 2 tmin, or inf)
 	int *sh_idx;           // slot * nee_k + entry
+	float2 *ts_hit;        // [s_depth * shadow rays] transparent shadows: (t, prim bits) of each transparent surface crossed
+	int *ts_n;             // [shadow rays] number of entries in ts_hit (0 when occluded or clear)
 	float4 *sattr;         // [2 * entries] k_surface output for the hit: (N, diffuse_refl), (diffuse colour, -)
 };
 

@@ -986,9 +986,19 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		int raydepth = 5;
 		ip.get("raydepth", raydepth);
 		S.raydepth = raydepth;
+		// transparent shadows (integrator_path_tracer.cc:294-311, integrator_direct_light.cc:148-164,
+		// integrator_photon_mapping.cc:767-796): "transpShad", "shadowDepth" (default 5)
 		bool transp_shad = false;
+		int shadow_depth = 5;
 		ip.get("transpShad", transp_shad);
-		if(transp_shad) log.warning("Integrator: transparent shadows (transpShad) are not evaluated by the GPU core; opaque shadows are traced");
+		ip.get("shadowDepth", shadow_depth);
+		S.tr_shad = transp_shad ? 1 : 0;
+		S.s_depth = std::max(0, shadow_depth);
+		if(transp_shad && shadow_depth > 64)
+		{
+			log.warning("Integrator: shadowDepth " + std::to_string(shadow_depth) + " clamped to 64 by the GPU core");
+			S.s_depth = 64;
+		}
 		S.tree = 0;
 		S.ext = 0;
 		for(const auto &kv : materials)

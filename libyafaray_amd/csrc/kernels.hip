@@ -297,6 +297,28 @@ struct TraceCtx
 	uint32_t spill_stride;
 };
 
+// Transparent-shadow hit list of one shadow ray (accelerator_kdtree.cc:1001-1023): an opaque
+// surface shadows; each transparent one is recorded until `cap` (= shadowDepth) are recorded, the
+// next one shadows.  A BVH holds every triangle once, so the reference's `filtered` set (one
+// factor per primitive) needs no lookup.
+struct TsList
+{
+	float2 *hit;
+	int n, cap;
+	const float4 *prim_ng;
+	const DevMaterial *mats;
+};
+
+__device__ __forceinline__ bool tsShadows(TsList &L, float t, int prim)
+{
+	const int mat = __float_as_int(L.prim_ng[prim].w);
+	if(!(L.mats[mat].sd_flags & SD_TRANSPARENT)) return true;
+	if(L.n >= L.cap) return true;
+	L.hit[L.n] = make_float2(t, __int_as_float(prim));
+	++L.n;
+	return false;
+}
+
 __device__ __forceinline__ void boxPair(const float4 &n0, const float4 &n1, const float4 &n2, V3 o, V3 id,
                                         float t0, float t1, bool &h0, bool &h1, float &tn0, float &tn1)
 {
@@ -341,9 +363,9 @@ __device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const
 // Closest hit with t in [tmin, tmax) (ties -> lower primitive index), or any hit with t in
 // [0, tmax).  Box tests are conservative (boxes padded at build time + a relative slack), so
 // culling never drops a hit the exhaustive reference semantics would return.
-template<bool ANY>
+template<bool ANY, bool TS = false>
 __device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
-                          uint32_t &visits, uint32_t &tests)
+                          uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
 	const int lane = threadIdx.x;
 	V3 dd = d;
@@ -385,7 +407,12 @@ __device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 				const float t = triTest(ta, tb, tc, o, d, ANY ? tmax : t_best);
 				if(t == -1.f) continue;
 				const int prim = __float_as_int(tb.w);
-				if(ANY)
+				if(ANY && TS)
+				{
+					// intersectTs: t in [tmin, t_max) of the moved ray (tmin kept, accelerator.cc:82-85)
+					if(t < tmax && t >= tmin && tsShadows(*ts, t, prim)) { t_best = t; prim_best = prim; return true; }
+				}
+				else if(ANY)
 				{
 					if(t < tmax && t >= 0.f) { t_best = t; prim_best = prim; return true; }
 				}
@@ -433,9 +460,9 @@ __device__ __forceinline__ void cswap(float &ka, int &va, float &kb, int &vb)
 // BVH4 (bvh.cc: collapsed binary SAH tree, 128 B nodes with the four child boxes in SoA form).
 // Same hit semantics as traverse2: leaf children are tested as soon as their box is hit, inner
 // children are sorted by entry distance (5-exchange network) and descended nearest-first.
-template<bool ANY, bool SPILL>
+template<bool ANY, bool SPILL, bool TS = false>
 __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
-                          uint32_t &visits, uint32_t &tests)
+                          uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
 	const int lane = threadIdx.x;
 	V3 dd = d;
@@ -492,7 +519,12 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 				const float t = triTest(ta, tb, tc, o, d, ANY ? tmax : t_best);
 				if(t == -1.f) continue;
 				const int prim = __float_as_int(tb.w);
-				if(ANY)
+				if(ANY && TS)
+				{
+					// intersectTs: t in [tmin, t_max) of the moved ray (tmin kept, accelerator.cc:82-85)
+					if(t < tmax && t >= tmin && tsShadows(*ts, t, prim)) { t_best = t; prim_best = prim; return true; }
+				}
+				else if(ANY)
 				{
 					if(t < tmax && t >= 0.f) { t_best = t; prim_best = prim; return true; }
 				}
@@ -524,12 +556,12 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	return prim_best >= 0;
 }
 
-template<bool ANY, bool WIDE, bool SPILL = true>
+template<bool ANY, bool WIDE, bool SPILL = true, bool TS = false>
 __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best,
-                                         int &prim_best, uint32_t &visits, uint32_t &tests)
+                                         int &prim_best, uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
-	if(WIDE) return traverse4<ANY, SPILL>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests);
-	return traverse2<ANY>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests);
+	if(WIDE) return traverse4<ANY, SPILL, TS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
+	return traverse2<ANY, TS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
 }
 
 // k_trace asks the register allocator for 8 waves per SIMD (<= 64 VGPRs; measured +3% on C2 over
@@ -543,7 +575,7 @@ __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tm
 #define YAF_TRACE_ATTR
 #endif
 
-template<bool LDS_SCENE, bool WIDE>
+template<bool LDS_SCENE, bool WIDE, bool TS>
 __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P,
                                                       DevStats *stats, int stack_depth, int *spill)
 {
@@ -600,7 +632,19 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 			const float4 od = Q.sh_o[k], dd = Q.sh_d[k];
 			float t;
 			int prim;
-			const bool occ = traverse<true, WIDE>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
+			bool occ;
+			if(TS)
+			{
+				TsList L;
+				L.hit = Q.ts_hit + (size_t)k * (uint32_t)S.s_depth;
+				L.n = 0;
+				L.cap = S.s_depth;
+				L.prim_ng = S.prim_ng;
+				L.mats = S.mats;
+				occ = traverse<true, WIDE, true, true>(C, xyz(od), xyz(dd), od.w, dd.w, t, prim, visits, tests, &L);
+				Q.ts_n[k] = occ ? 0 : L.n;
+			}
+			else occ = traverse<true, WIDE>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
 			P.occ[Q.sh_idx[k]] = occ ? 1 : 0;   // P = state set of the consumer shade
 			++n_shadow;
 		}
@@ -956,7 +1000,7 @@ struct ShadeOut
 };
 
 // Appends (or not) one shadow ray per lane — every lane of the wave must call.
-__device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, int idx, const ShadeOut &out)
+__device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, float tmin, int idx, const ShadeOut &out)
 {
 #ifdef YAF_EXP_NO_EMIT
 	if(want) out.Qn.sh_idx[idx] = idx;   // timing experiment only: no append (wrong images)
@@ -965,7 +1009,7 @@ __device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, i
 	const uint32_t k = out.sh_base + waveAppend(want, out.sh_count);
 	if(want)
 	{
-		out.Qn.sh_o[k] = f4(o, 0.f);
+		out.Qn.sh_o[k] = f4(o, tmin);
 		out.Qn.sh_d[k] = f4(d, t_max);
 		out.Qn.sh_idx[k] = idx;
 	}
@@ -978,6 +1022,15 @@ __device__ __forceinline__ void shadowRayOf(V3 from, V3 dir, float tmin, float t
 	t_max = (tmax >= 0.f) ? tmax - 2 * tmin : __builtin_huge_valf();
 }
 
+// Transparent shadows: the factors of an NEE contribution whose light colour k_tshadow still has
+// to filter (integrator_montecarlo.cc:122, 212, 335: `lcol *= scol` comes before the products)
+__device__ __forceinline__ void tsFactors(float4 *ts, int e, C3 surf, float a, C3 lcol, float b, float c, bool div)
+{
+	ts[3 * (size_t)e] = f4(surf, a);
+	ts[3 * (size_t)e + 1] = f4(lcol, b);
+	ts[3 * (size_t)e + 2] = make_float4(c, div ? 1.f : 0.f, 0.f, 0.f);
+}
+
 // Next-event estimation for one light: writes the contributions of every sample into
 // nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
 // Wave-uniform structure: `active` lanes do the work, every lane of the wave walks the same loop
@@ -985,7 +1038,7 @@ __device__ __forceinline__ void shadowRayOf(V3 from, V3 dir, float tmin, float t
 template<bool EXT>
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
-                         float4 *nee, uint8_t *occ, const ShadeOut &out)
+                         float4 *nee, uint8_t *occ, const ShadeOut &out, float4 *ts = nullptr)
 {
 	const bool cast_shadows = L.cast_shadows && m.receive_shadows;
 	const float p_len = length(sp.p);
@@ -1012,10 +1065,11 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			contrib = surf_col * lcol * angle * transmit;
 			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
 			nee[e0] = f4(contrib, 1.f);
+			if(ts && cast_shadows) tsFactors(ts, e0, surf_col, angle, lcol, 1.f, 1.f, false);
 		}
 		else if(active) nee[e0] = make_float4(0.f, 0.f, 0.f, 0.f);
 		if(active) occ[e0] = 0;
-		emitShadow(ok && cast_shadows, so, ldir, st, e0, out);
+		emitShadow(ok && cast_shadows, so, ldir, st, sh_tmin, e0, out);
 		return;
 	}
 	// area light: montecarlo.cc:393-405
@@ -1070,6 +1124,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 					}
 					contrib = surf_col * lcolor * angle * w / pdf;
 					shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
+					if(ts && cast_shadows) tsFactors(ts, e0 + i, surf_col, angle, lcolor, w, pdf, true);
 				}
 				else ok = false;
 			}
@@ -1079,7 +1134,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			nee[e0 + i] = f4(contrib, ok ? 1.f : 0.f);
 			occ[e0 + i] = 0;
 		}
-		emitShadow(ok && cast_shadows, so, ldir, st, e0 + i, out);
+		emitShadow(ok && cast_shadows, so, ldir, st, sh_tmin, e0 + i, out);
 
 		// areaLightSampleMaterial (montecarlo.cc:284-383)
 		ok = active;
@@ -1087,9 +1142,9 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 		so = sp.p;
 		V3 dir = v3(0.f, 0.f, 1.f);
 		st = 0.f;
+		const float b_tmin = S.ray_min_dist_auto ? S.ray_min_dist * fmaxf(1.f, p_len) : S.ray_min_dist;
 		if(ok)
 		{
-			const float b_tmin = S.ray_min_dist_auto ? S.ray_min_dist * fmaxf(1.f, p_len) : S.ray_min_dist;
 			BsdfSample s;
 			s.s_1 = s_1;
 			s.s_2 = s_2;
@@ -1122,6 +1177,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 					const float w = m_2 / (l_2 + m_2);
 					contrib = surf_col * lcolor * w * W;
 					shadowRayOf(sp.p, dir, b_tmin, t, so, st);
+					if(ts && cast_shadows) tsFactors(ts, e0 + num_samples + i, surf_col, w, lcolor, W, 1.f, false);
 				}
 				else ok = false;
 			}
@@ -1131,7 +1187,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			nee[e0 + num_samples + i] = f4(contrib, ok ? 1.f : 0.f);
 			occ[e0 + num_samples + i] = 0;
 		}
-		emitShadow(ok && cast_shadows, so, dir, st, e0 + num_samples + i, out);
+		emitShadow(ok && cast_shadows, so, dir, st, b_tmin, e0 + num_samples + i, out);
 	}
 }
 
@@ -1784,6 +1840,73 @@ __global__ void __launch_bounds__(kShadeBlock) k_surface(DevScene S, DevQueues Q
 	}
 }
 
+// Transparent shadows, second half (accelerator_kdtree.cc:1011-1018 + accelerator.cc:80-93): for
+// every shadow ray k_trace<TS> left unoccluded with transparent surfaces on it, the filter colour
+// is the product of their ShinyDiffuseMaterial::getTransparency (material_shiny_diffuse.cc:441-465,
+// wo = the ray direction) at the surface point getSurface builds from the moved ray; then the NEE
+// contribution is rebuilt with `lcol *= scol` where the reference applies it.  Factors multiply in
+// ascending (t, primitive) order (the kd-tree's cell order: the same value for up to two surfaces).
+__global__ void __launch_bounds__(kShadeBlock) k_tshadow(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P)
+{
+	const uint32_t seg = blockIdx.x;
+	const uint32_t n_s = cnt.n_shadow[seg];
+	const uint32_t s0 = seg * S.cap_s;
+	const uint32_t cap = (uint32_t)S.s_depth;
+	for(uint32_t j = threadIdx.x; j < n_s; j += blockDim.x)
+	{
+		const uint32_t k = s0 + j;
+		const int n = Q.ts_n[k];
+		if(n <= 0) continue;
+		float2 *h = Q.ts_hit + (size_t)k * cap;
+		// insertion sort by (t, prim)
+		for(int a = 1; a < n; ++a)
+		{
+			const float2 x = h[a];
+			int b = a - 1;
+			while(b >= 0 && (h[b].x > x.x || (h[b].x == x.x && __float_as_int(h[b].y) > __float_as_int(x.y))))
+			{
+				h[b + 1] = h[b];
+				--b;
+			}
+			h[b + 1] = x;
+		}
+		const V3 o = xyz(Q.sh_o[k]), d = xyz(Q.sh_d[k]);
+		C3 scol = c3(1.f);
+		for(int a = 0; a < n; ++a)
+		{
+			const float t = h[a].x;
+			const int prim = __float_as_int(h[a].y);
+			const V3 p = o + t * d;
+			const float4 g = S.prim_ng[prim];
+			const V3 ng = xyz(g);
+			const DevMaterial &m = S.mats[__float_as_int(g.w)];
+			V3 nrm = ng;
+			C3 dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+			if(S.has_attr)
+			{
+				const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, o, d, p);
+				nrm = sa.n;
+				float drefl = 1.f;
+				if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl);
+			}
+			const V3 nf = faceForward(ng, nrm, d);
+			const float kr = fresnelKr(m, d, nf);
+			float accum = 1.f;
+			if(m.sd_flags & SD_MIRROR) accum = 1.f - kr * m.comp[0];
+			accum *= m.comp[1] * accum;
+			const C3 tcol = m.tfilter * dcol + c3(1.f - m.tfilter);
+			scol = scol * (accum * tcol);
+		}
+		const uint32_t e = (uint32_t)Q.sh_idx[k];
+		const float4 f0 = P.ts[3 * (size_t)e], f1 = P.ts[3 * (size_t)e + 1], f2 = P.ts[3 * (size_t)e + 2];
+		C3 x = rgb(f0) * (rgb(f1) * scol);
+		x = x * f0.w;
+		x = x * f1.w;
+		x = (f2.y != 0.f) ? x / f2.x : x * f2.x;
+		P.nee[e] = f4(x, P.nee[e].w);
+	}
+}
+
 struct NeeArgs
 {
 	DevScene S;
@@ -1842,7 +1965,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs 
 			// estimateAllDirectLight (montecarlo.cc:54-68)
 			for(int l = 0; l < S.n_lights; ++l)
 				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
-				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out);
+				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out, S.tr_shad ? A.Pn.ts : nullptr);
 		}
 		if(__any(one))
 		{
@@ -1851,7 +1974,8 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs 
 			{
 				const bool mine = one && lnum == (uint32_t)l;
 				if(!__any(mine)) continue;
-				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out);
+				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out,
+				              S.tr_shad ? A.Pn.ts : nullptr);
 			}
 		}
 	}
@@ -2462,10 +2586,10 @@ int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds)
 {
 	int nb = 0;
 	hipError_t e;
-	if(lds_scene) e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, true>, kTraceBlock, dyn_lds)
-	                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, false>, kTraceBlock, dyn_lds);
-	else e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, true>, kTraceBlock, dyn_lds)
-	              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, false>, kTraceBlock, dyn_lds);
+	if(lds_scene) e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, true, false>, kTraceBlock, dyn_lds)
+	                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, false, false>, kTraceBlock, dyn_lds);
+	else e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, true, false>, kTraceBlock, dyn_lds)
+	              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, false, false>, kTraceBlock, dyn_lds);
 	return e == hipSuccess ? nb : 0;
 }
 
@@ -2497,14 +2621,19 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 {
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	const bool wide = S->node_f4 == 8;
-	if(S->scene_in_lds)
+	const size_t lds_scene = S->scene_in_lds ? (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) : 0;
+	const size_t bytes = stack_bytes + lds_scene;
+#define YAF_TRACE_LAUNCH(L, W, T) hipLaunchKernelGGL((k_trace<L, W, T>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill)
+	if(S->tr_shad)
 	{
-		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
-		if(wide) hipLaunchKernelGGL((k_trace<true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill);
-		else hipLaunchKernelGGL((k_trace<true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill);
+		if(S->scene_in_lds) { if(wide) YAF_TRACE_LAUNCH(true, true, true); else YAF_TRACE_LAUNCH(true, false, true); }
+		else if(wide) YAF_TRACE_LAUNCH(false, true, true);
+		else YAF_TRACE_LAUNCH(false, false, true);
 	}
-	else if(wide) hipLaunchKernelGGL((k_trace<false, true>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill);
-	else hipLaunchKernelGGL((k_trace<false, false>), dim3(grid), dim3(kTraceBlock), stack_bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill);
+	else if(S->scene_in_lds) { if(wide) YAF_TRACE_LAUNCH(true, true, false); else YAF_TRACE_LAUNCH(true, false, false); }
+	else if(wide) YAF_TRACE_LAUNCH(false, true, false);
+	else YAF_TRACE_LAUNCH(false, false, false);
+#undef YAF_TRACE_LAUNCH
 	return hipGetLastError();
 }
 
@@ -2555,6 +2684,12 @@ hipError_t yafamd_launch_combine(const DevScene *S, uint32_t lo, uint32_t hi, in
 hipError_t yafamd_launch_surface(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, hipStream_t st)
 {
 	hipLaunchKernelGGL(k_surface, dim3(S->n_seg), dim3(kShadeBlock), 0, st, *S, *Q, *cnt);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_launch_tshadow(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P, hipStream_t st)
+{
+	hipLaunchKernelGGL(k_tshadow, dim3(S->n_seg), dim3(kShadeBlock), 0, st, *S, *Q, *cnt, *P);
 	return hipGetLastError();
 }
 

@@ -19,6 +19,7 @@ extern "C" {
 hipError_t yafamd_launch_camera(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n, hipStream_t st);
 hipError_t yafamd_launch_surface(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, hipStream_t st);
+hipError_t yafamd_launch_tshadow(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P, hipStream_t st);
 hipError_t yafamd_launch_spawn(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt, uint32_t s0, int n,
                                hipStream_t st);
 hipError_t yafamd_launch_combine(const DevScene *S, uint32_t lo, uint32_t hi, int final_level, float4 *samples, const DevJob *jobs,
@@ -104,6 +105,7 @@ struct GpuRenderer::Impl
 	// specular recursion tree (k_spawn / k_combine): spawned rays and per-node records
 	Buf spawn_o, spawn_d, spawn_pr, node_own, node_child, node_w, spawn_count;
 	bool has_attr = false, attr_alloc = false;
+	int ts_alloc = 0;   // shadowDepth the transparent-shadow buffers were sized for (0: none)
 	int n_textures = 0;
 	// photon mapping: light selection Pdf1D, photon paths in flight, the map and its kd-tree
 	Buf ph_lights, light_cdf, light_func;
@@ -573,7 +575,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	const size_t R = (size_t)d.shade_grid;
 	auto shardCap = [R](size_t m) { return (((m + 255) / 256 + R - 1) / R) * 256; };
 	const bool need_attr = S.has_attr != 0;
-	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc)
+	const int need_ts = S.tr_shad ? std::max(1, S.s_depth) : 0;
+	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc || need_ts != d.ts_alloc)
 	{
 		// Wavefront buffers for M samples in flight (~0.7 KB each: 288 GB of HBM holds tens of millions,
 		// and big chunks amortise the per-launch cost).  On allocation failure the chunk is halved.
@@ -609,6 +612,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				P.nee = (float4 *)A(MA * K * 16);
 				P.occ = (uint8_t *)A(MA * K);
 				P.v0attr = (float4 *)A(need_v0 && need_attr ? MA * 32 : 16);
+				P.ts = (float4 *)A(need_ts ? MA * K * 48 : 16);
 			}
 			for(int q = 0; q < 2; ++q)
 			{
@@ -622,6 +626,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				Q.sh_d = (float4 *)A(MA * K * 16);
 				Q.sh_idx = (int *)A(MA * K * 4);
 				Q.sattr = (float4 *)A(need_attr ? MA * 32 : 16);
+				Q.ts_hit = (float2 *)A(need_ts ? MA * K * 8 * (size_t)need_ts : 16);
+				Q.ts_n = (int *)A(need_ts ? MA * K * 4 : 16);
 			}
 			d.N.p_prim = (float4 *)A(MA * 16);
 			d.N.wo_k = (float4 *)A(MA * 16);
@@ -636,6 +642,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		}
 		d.v0_alloc = need_v0;
 		d.attr_alloc = need_attr;
+		d.ts_alloc = need_ts;
 		d.slots_cap = M;
 		d.nee_cap = K;
 	}
@@ -682,6 +689,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 1], d.stream));
 			// material-shade dispatch for textured / smooth scenes: surface attributes + shader nodes
 			// of every hit, before k_shade reads them
+			// transparent shadows: filter colours of the transparent surfaces the shadow rays crossed
+			if(S.tr_shad) HIPCHECK(yafamd_launch_tshadow(&S, &d.Q[cur], &cnt[cur], &d.P[cur], d.stream));
 			if(S.has_attr) HIPCHECK(yafamd_launch_surface(&S, &d.Q[cur], &cnt[cur], d.stream));
 			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));

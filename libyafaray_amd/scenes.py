@@ -124,6 +124,8 @@ class Render:
     raydepth: int = 5
     bg_transp: bool = False
     bg_transp_refract: bool = False
+    transp_shad: bool = False               # transparent shadows (MonteCarloIntegrator tr_shad_)
+    shadow_depth: int = 5                   # "shadowDepth" (integrator_path_tracer.cc:295)
     shadow_bias_auto: bool = True
     shadow_bias: float = 0.0005
     ray_min_dist_auto: bool = True
@@ -532,6 +534,8 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetInt("raydepth", r.raydepth)
     api.paramsSetBool("bg_transp", r.bg_transp)
     api.paramsSetBool("bg_transp_refract", r.bg_transp_refract)
+    api.paramsSetBool("transpShad", r.transp_shad)
+    api.paramsSetInt("shadowDepth", r.shadow_depth)
     if r.integrator == "pathtracing":
         api.paramsSetInt("bounces", r.bounces)
         api.paramsSetInt("path_samples", r.path_samples)
@@ -610,3 +614,43 @@ def cornell_specular(width=64, height=48, spp=2, integrator="directlighting", bo
             tri_mat[o.t0:o.t0 + o.nt] = len(s.materials) + 2
     r = dataclasses.replace(s.render, raydepth=raydepth)
     return dataclasses.replace(s, materials=mats, tri_mat=tri_mat, render=r)
+
+
+def cornell_transparent_shadows(width=64, height=48, spp=2, integrator="directlighting", panes=2, shadow_depth=5,
+                                point_light=False, bounces=3, **kw) -> SceneSpec:
+    """Transparent shadows (MonteCarloIntegrator tr_shad_, accelerator_kdtree.cc:916-1061): the C2
+    Cornell box with `panes` stacked transparent shinydiffuse panes under the light (tinted, with
+    transmit filters), a transparent Fresnel + mirror tall box and a transparent + translucent short
+    box, so that shadow rays cross 0 .. panes + 2 transparent surfaces; `shadow_depth` is the
+    integrator's shadowDepth.  With point_light a point light replaces the area light (diracLight)."""
+    import dataclasses
+    s = cornell(width, height, spp=spp, bounces=bounces, rr=False, integrator=integrator, **kw)
+    b = _Builder()
+    b.verts = [tuple(v) for v in s.verts.tolist()]
+    b.tris = [tuple(t) for t in s.tris.tolist()]
+    b.tri_mat = [int(m) for m in s.tri_mat]
+    b.objects = list(s.objects)
+    tints = [(0.9, 0.3, 0.3), (0.3, 0.9, 0.4), (0.35, 0.45, 0.95), (0.9, 0.9, 0.3)]
+    mats = list(s.materials)
+    for k in range(panes):
+        z = 1.6 - 0.15 * k
+        h = 0.45 - 0.05 * k
+        mats.append(Material(f"pane{k}", color=tints[k % len(tints)], transparency=0.8 - 0.1 * k,
+                             transmit_filter=0.9 - 0.2 * k, diffuse_reflect=0.6))
+        b.add_object(f"pane{k}", *_quad((-h, -h, z), (h, -h, z), (h, h, z), (-h, h, z)), len(mats) - 1)
+    verts, tris, tri_mat = b.arrays()
+    mats.append(Material("tall_glass", color=(0.6, 0.7, 0.9), transparency=0.6, transmit_filter=0.5,
+                         specular_reflect=0.3, fresnel=True, ior=1.5, diffuse_reflect=0.4))
+    mats.append(Material("short_transl", color=(0.8, 0.6, 0.3), transparency=0.4, translucency=0.3,
+                         transmit_filter=0.7, diffuse_reflect=0.5))
+    for o in b.objects:
+        if o.name == "tall_box":
+            tri_mat[o.t0:o.t0 + o.nt] = len(mats) - 2
+        elif o.name == "short_box":
+            tri_mat[o.t0:o.t0 + o.nt] = len(mats) - 1
+    lights = s.lights
+    if point_light:
+        lights = [Light("point", type="pointlight", color=(1.0, 1.0, 1.0), power=3.0, from_=(0.1, -0.1, 1.9))]
+    r = dataclasses.replace(s.render, transp_shad=True, shadow_depth=shadow_depth, raydepth=2)
+    return dataclasses.replace(s, verts=verts, tris=tris, tri_mat=tri_mat, materials=mats, lights=lights,
+                               objects=b.objects, render=r)

@@ -85,7 +85,8 @@ class yc_render(C.Structure):
                 ("aa_resampled_floor", C.c_float), ("aa_sample_multiplier_factor", C.c_float),
                 ("aa_detect_color_noise", C.c_int), ("aa_dark_detection_type", C.c_int),
                 ("aa_dark_threshold_factor", C.c_float), ("aa_variance_edge_size", C.c_int), ("aa_variance_pixels", C.c_int),
-                ("raydepth", C.c_int), ("bg_transp_refract", C.c_int)]
+                ("raydepth", C.c_int), ("bg_transp_refract", C.c_int),
+                ("transp_shad", C.c_int), ("shadow_depth", C.c_int)]
 
 
 class yc_scene(C.Structure):
@@ -556,6 +557,7 @@ class OracleScene:
         rp.aa_dark_threshold_factor = r.aa_dark_threshold_factor
         rp.aa_variance_edge_size, rp.aa_variance_pixels = r.aa_variance_edge_size, r.aa_variance_pixels
         rp.raydepth, rp.bg_transp_refract = r.raydepth, int(r.bg_transp_refract)
+        rp.transp_shad, rp.shadow_depth = int(r.transp_shad), r.shadow_depth
         self.sc = sc
         self.spec = spec
         _texturing(self, spec, mats)

@@ -694,6 +694,7 @@ class Scene
 		void setupTexturing(const yc_scene &s);
 		void surface(const IsectData &d, SurfacePoint &sp) const;
 		IsectData intersect(const Ray &ray, float t_max, bool any, uint64_t *ctr) const;
+		void allHits(const Ray &ray, float t_max, std::vector<IsectData> &out) const;
 		void buildBvh();
 		int buildRec(int start, int end, std::vector<V3> &cent);
 };
@@ -1228,6 +1229,40 @@ IsectData Scene::intersect(const Ray &ray, float t_max, bool any, uint64_t *ctr)
 	return best;
 }
 
+// Every primitive hit with t in [ray.tmin, t_max) — the candidate set of intersectTs
+// (accelerator_kdtree.cc:1001-1023: '<' t_max, '>=' ray.tmin_, material visibility only).
+void Scene::allHits(const Ray &ray, float t_max, std::vector<IsectData> &out) const
+{
+	out.clear();
+	if(nodes.empty()) return;
+	int stack[128];
+	int sp = 0;
+	stack[sp++] = 0;
+	const double lo_t = -1e-3 * (1.0 + std::fabs(ray.tmin));
+	const double hi_t = std::isinf(t_max) ? 1e300 : (double)t_max * (1.0 + 1e-5) + 1e-6;
+	while(sp)
+	{
+		const BvhNode &n = nodes[stack[--sp]];
+		if(!boxHit(n, ray, lo_t, hi_t)) continue;
+		if(n.count)
+		{
+			for(int i = n.start; i < n.start + n.count; ++i)
+			{
+				const int pi = order[i];
+				IsectData d = triIntersect(tris[pi], ray);
+				if(!d.hit || !(d.t < t_max && d.t >= ray.tmin)) continue;
+				d.prim = pi;
+				out.push_back(d);
+			}
+		}
+		else
+		{
+			stack[sp++] = n.left;
+			stack[sp++] = n.right;
+		}
+	}
+}
+
 // ---------------------------------------------------------------------------------------------
 // render-side restatement
 // ---------------------------------------------------------------------------------------------
@@ -1284,6 +1319,61 @@ class Renderer
 			sray.from += sray.dir * sray.tmin;
 			const float t_max = (ray.tmax >= 0.f) ? sray.tmax - 2 * sray.tmin : std::numeric_limits<float>::infinity();
 			return sc_.intersect(sray, t_max, true, &th.shadow).hit;
+		}
+		// accelerator.cc:80-93 + accelerator_kdtree.cc:916-1061 (transparent shadows).  The origin
+		// moves by tmin but tmin is kept, so hits count from 2 tmin along the original ray.  An opaque
+		// hit, or more than `shadow_depth` distinct transparent ones, shadows; otherwise the filter
+		// colour is the product of the transparent surfaces' getTransparency(ray.dir).  The kd-tree
+		// multiplies in its cell-visiting order; here (and on the GPU) the order is ascending
+		// (t, primitive), identical in value for up to two transparent surfaces (a product of two
+		// rounded factors does not depend on the order).
+		bool isShadowedTs(Thread &th, const Ray &ray, C3 &scol) const
+		{
+			++th.shadow;
+			Ray sray = ray;
+			sray.from += sray.dir * sray.tmin;
+			const float t_max = (ray.tmax >= 0.f) ? sray.tmax - 2 * sray.tmin : std::numeric_limits<float>::infinity();
+			scol = C3(1.f);
+			std::vector<IsectData> hits;
+			sc_.allHits(sray, t_max, hits);
+			int n_transp = 0;
+			for(const IsectData &d : hits)
+			{
+				const Material &m = sc_.mats[sc_.tris[d.prim].mat];
+				if(!m.is_transparent) return true;
+				++n_transp;
+			}
+			if(n_transp > sc_.rp.shadow_depth) return true;
+			std::sort(hits.begin(), hits.end(), [](const IsectData &a, const IsectData &b) {
+				return a.t < b.t || (a.t == b.t && a.prim < b.prim);
+			});
+			for(const IsectData &d : hits)
+			{
+				// getSurface (primitive_triangle.cc:97-176) at the hit of the moved ray, then
+				// ShinyDiffuseMaterial::getTransparency (material_shiny_diffuse.cc:441-465), wo = ray dir
+				SurfacePoint sp;
+				const Tri &tr = sc_.tris[d.prim];
+				sp.p = sray.from + d.t * sray.dir;
+				sp.ng = tr.ng;
+				sp.n = tr.ng;
+				createCoordsSystem(sp.n, sp.nu, sp.nv);
+				sp.mat = &sc_.mats[tr.mat];
+				sp.prim = d.prim;
+				sc_.surface(d, sp);
+				scol = scol * getTransparency(sp, sray.dir);
+			}
+			return false;
+		}
+		static C3 getTransparency(const SurfacePoint &sp, const V3 &wo)
+		{
+			const Material &m = *sp.mat;
+			const V3 n = faceForward(sp.ng, sp.n, wo);
+			const float kr = fresnelKr(m, wo, n);
+			float accum = 1.f;
+			if(m.is_mirror) accum = 1.f - kr * m.components[0];
+			accum *= m.components[1] * accum;
+			const C3 tcol = m.transmit_filter * sp.dcol + C3(1.f - m.transmit_filter);
+			return accum * tcol;
 		}
 
 		// surface.h:62-65
@@ -1635,13 +1725,15 @@ class Renderer
 			light_ray.from = sp.p;
 			light_ray.tmin = shadowTmin(sp);
 			bool shadowed = false;
-			if(cast_shadows) shadowed = isShadowed(th, light_ray);
+			C3 scol(0.f);
+			if(cast_shadows) shadowed = sc_.rp.transp_shad ? isShadowedTs(th, light_ray, scol) : isShadowed(th, light_ray);
 			const float angle_light_normal = sp.mat->flat ? 1.f : std::abs(dot(sp.n, light_ray.dir));
 			if(!shadowed)
 			{
 				const C3 surf_col = eval(sp, wo, light_ray.dir, BAll);
 				const C3 transmit_col(1.f);
-				col += surf_col * lcol * angle_light_normal * transmit_col;
+				const C3 lcol_s = (sc_.rp.transp_shad && cast_shadows) ? lcol * scol : lcol;
+				col += surf_col * lcol_s * angle_light_normal * transmit_col;
 			}
 			return col;
 		}
@@ -1661,9 +1753,11 @@ class Renderer
 				{
 					light_ray.tmin = shadowTmin(sp);
 					bool shadowed = false;
-					if(cast_shadows) shadowed = isShadowed(th, light_ray);
+					C3 scol(0.f);
+					if(cast_shadows) shadowed = sc_.rp.transp_shad ? isShadowedTs(th, light_ray, scol) : isShadowed(th, light_ray);
 					if(!shadowed && ls.pdf > 1e-6f)
 					{
+						if(sc_.rp.transp_shad && cast_shadows) ls.col = ls.col * scol;
 						const C3 surf_col = eval(sp, wo, light_ray.dir, BAll);
 						const float angle_light_normal = sp.mat->flat ? 1.f : std::abs(dot(sp.n, light_ray.dir));
 						float w = 1.f;
@@ -1700,9 +1794,11 @@ class Renderer
 				if(s.pdf > 1e-6f && areaIntersect(L, b_ray, b_ray.tmax, lcol, light_pdf))
 				{
 					bool shadowed = false;
-					if(cast_shadows) shadowed = isShadowed(th, b_ray);
+					C3 scol(0.f);
+					if(cast_shadows) shadowed = sc_.rp.transp_shad ? isShadowedTs(th, b_ray, scol) : isShadowed(th, b_ray);
 					if(!shadowed && light_pdf > 1e-6f)
 					{
+						if(sc_.rp.transp_shad && cast_shadows) lcol = lcol * scol;
 						const float l_pdf = 1.f / light_pdf;
 						const float l_2 = l_pdf * l_pdf;
 						const float m_2 = s.pdf * s.pdf;

@@ -146,6 +146,8 @@ typedef struct {
 	int aa_variance_pixels;
 	int raydepth;             // recursiveRaytrace depth (DirectLight / PathIntegrator "raydepth")
 	int bg_transp_refract;
+	// transparent shadows (integrator "transpShad" / "shadowDepth", MonteCarloIntegrator tr_shad_ / s_depth_)
+	int transp_shad, shadow_depth;
 } yc_render;
 
 typedef struct {
