@@ -38,8 +38,11 @@ namespace yafamd
 #ifndef YAF_TRACE_BLOCK
 #define YAF_TRACE_BLOCK 128
 #endif
+// k_shade / k_nee (non-EXT instantiations): at least 4 waves per SIMD (<= 128 VGPRs; the unconstrained allocation took
+// 132 / 143 and 3 waves).  Measured on C2: 1400 -> 1500 Msamples/s (shade 0.70 -> 0.62 ms per
+// launch, NEE 17.7 -> 15.6 ms per frame), -DYAF_*_MIN_WAVES=n overrides for tuning
 #ifndef YAF_SHADE_MIN_WAVES
-#define YAF_SHADE_MIN_WAVES 1
+#define YAF_SHADE_MIN_WAVES 4
 #endif
 constexpr int kTraceBlock = YAF_TRACE_BLOCK;
 constexpr int kShadeBlock = 256;
@@ -343,6 +346,20 @@ __device__ __forceinline__ void boxPair(const float4 &n0, const float4 &n1, cons
 // 1/det, then products) evaluated branch-free: every lane computes the same instruction stream
 // and the reference's early returns become one combined predicate (NaN comparisons keep their
 // reference outcome).  `t_cut` is unused by the exact test.
+// Correctly rounded 1/x: v_rcp_f32 + one FMA Newton step, which tools/rcp_check.hip
+// verified exhaustively on gfx950 to equal the IEEE quotient for every float with
+// 2^-125 <= |x| <= 2^125 (other magnitudes, zero, inf and NaN take the IEEE division).
+__device__ __forceinline__ float rcpExact(float x)
+{
+	const float ax = fabsf(x);
+	if(ax >= 0x1p-125f && ax <= 0x1p125f)
+	{
+		const float y = __builtin_amdgcn_rcpf(x);
+		return __builtin_fmaf(y, __builtin_fmaf(-x, y, 1.f), y);
+	}
+	return 1.f / x;
+}
+
 __device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const float4 &c, V3 o, V3 d, float t_cut)
 {
 	(void)t_cut;
@@ -350,7 +367,7 @@ __device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const
 	const float eps = a.w;
 	const V3 pvec = cross(d, e2);
 	const float det = dot(e1, pvec);
-	const float inv_det = 1.f / det;
+	const float inv_det = rcpExact(det);
 	const V3 tvec = o - v0;
 	const float u = dot(tvec, pvec) * inv_det;
 	const V3 qvec = cross(tvec, e1);
@@ -372,7 +389,7 @@ __device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	if(fabsf(dd.x) < 1e-20f) dd.x = copysignf(1e-20f, dd.x);
 	if(fabsf(dd.y) < 1e-20f) dd.y = copysignf(1e-20f, dd.y);
 	if(fabsf(dd.z) < 1e-20f) dd.z = copysignf(1e-20f, dd.z);
-	const V3 id = v3(1.f / dd.x, 1.f / dd.y, 1.f / dd.z);
+	const V3 id = v3(rcpExact(dd.x), rcpExact(dd.y), rcpExact(dd.z));
 	const float box_t0 = ANY ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
 	t_best = tmax;
 	prim_best = -1;
@@ -469,7 +486,10 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	if(fabsf(dd.x) < 1e-20f) dd.x = copysignf(1e-20f, dd.x);
 	if(fabsf(dd.y) < 1e-20f) dd.y = copysignf(1e-20f, dd.y);
 	if(fabsf(dd.z) < 1e-20f) dd.z = copysignf(1e-20f, dd.z);
-	const V3 id = v3(1.f / dd.x, 1.f / dd.y, 1.f / dd.z);
+	const V3 id = v3(rcpExact(dd.x), rcpExact(dd.y), rcpExact(dd.z));
+	// slab distances as fma(bound, 1/d, -o/d): the rounding of o/d is covered by the boxes' build-time
+	// padding (mag * 1e-5, bvh.cc padBox) as the rounding of (bound - o) is
+	const V3 oid = v3(o.x * id.x, o.y * id.y, o.z * id.z);
 	const float box_t0 = ANY ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
 	const float inf = __builtin_huge_valf();
 	const uint32_t glane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -495,9 +515,9 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 #pragma unroll
 		for(int k = 0; k < 4; ++k)
 		{
-			const float ax = (lane4(lx, k) - o.x) * id.x, bx = (lane4(hx, k) - o.x) * id.x;
-			const float ay = (lane4(ly, k) - o.y) * id.y, by = (lane4(hy, k) - o.y) * id.y;
-			const float az = (lane4(lz, k) - o.z) * id.z, bz = (lane4(hz, k) - o.z) * id.z;
+			const float ax = __builtin_fmaf(lane4(lx, k), id.x, -oid.x), bx = __builtin_fmaf(lane4(hx, k), id.x, -oid.x);
+			const float ay = __builtin_fmaf(lane4(ly, k), id.y, -oid.y), by = __builtin_fmaf(lane4(hy, k), id.y, -oid.y);
+			const float az = __builtin_fmaf(lane4(lz, k), id.z, -oid.z), bz = __builtin_fmaf(lane4(hz, k), id.z, -oid.z);
 			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
 			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
 			const bool h = lo <= hi;
@@ -825,7 +845,7 @@ __device__ C3 matSample(const DevMaterial &m, const Surf &sp, V3 wo, V3 &wi, Bsd
 		wi = reflectDir(sp.n, wo);
 		s.sampled = B_SPECULAR | B_REFLECT;
 		w = 1.f;
-		return C3{m.mirror_col[0], m.mirror_col[1], m.mirror_col[2]} * (1.f / fabsf(dot(sp.n, wi)));
+		return C3{m.mirror_col[0], m.mirror_col[1], m.mirror_col[2]} * rcpExact(fabsf(dot(sp.n, wi)));
 	}
 	const float cos_ng_wo = dot(sp.ng, wo);
 	const V3 n = faceForward(sp.ng, sp.n, wo);
@@ -865,7 +885,7 @@ __device__ C3 matSample(const DevMaterial &m, const Surf &sp, V3 wo, V3 &wi, Bsd
 		wi = reflectDir(n, wo);
 		s.pdf = width[pick];
 		scolor = C3{m.mirror_col[0], m.mirror_col[1], m.mirror_col[2]} * (accum_c[0]);
-		scolor = scolor * (1.f / fmaxf(fabsf(dot(sp.n, wi)), 1.0e-6f));
+		scolor = scolor * rcpExact(fmaxf(fabsf(dot(sp.n, wi)), 1.0e-6f));
 	}
 	else if(EXT && ch == (B_TRANSMIT | B_FILTER))
 	{
@@ -981,7 +1001,7 @@ __device__ __forceinline__ bool areaTri(V3 a, V3 b, V3 c, V3 o, V3 d, float &t)
 	const V3 pvec = cross(d, edge_2);
 	const float det = dot(edge_1, pvec);
 	if(det == 0.f) return false;
-	const float inv_det = 1.f / det;
+	const float inv_det = rcpExact(det);
 	const V3 tvec = o - a;
 	const float u = dot(tvec, pvec) * inv_det;
 	if(u < 0.f || u > 1.f) return false;
@@ -1056,8 +1076,8 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 		float st = 0.f;
 		if(ok)
 		{
-			const float idist_sqr = 1.f / (dist_sqr);
-			ldir = ldir * (1.f / dist);
+			const float idist_sqr = rcpExact(dist_sqr);
+			ldir = ldir * rcpExact(dist);
 			const C3 lcol = C3{L.color[0], L.color[1], L.color[2]} * idist_sqr;
 			const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
 			const C3 surf_col = matEval<EXT>(m, sp, wo, ldir, B_ALL);
@@ -1103,7 +1123,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			float cos_angle = 0.f;
 			if(ok)
 			{
-				ldir = ldir * (1.f / dist);
+				ldir = ldir * rcpExact(dist);
 				cos_angle = dot(ldir, fn);
 				if(cos_angle <= 0) ok = false;
 			}
@@ -1168,10 +1188,10 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			}
 			if(ok)
 			{
-				const float light_pdf = x87mul(kDiv1ByPi, 1.f / (t * t) * L.area * cos_angle);
+				const float light_pdf = x87mul(kDiv1ByPi, rcpExact(t * t) * L.area * cos_angle);
 				if(light_pdf > 1e-6f)
 				{
-					const float l_pdf = 1.f / light_pdf;
+					const float l_pdf = rcpExact(light_pdf);
 					const float l_2 = l_pdf * l_pdf;
 					const float m_2 = s.pdf * s.pdf;
 					const float w = m_2 / (l_2 + m_2);
@@ -1362,7 +1382,7 @@ __device__ void spawnSpecular(const DevScene &S, const DevMaterial &m, const Sur
 //      (coalesced SoA reads and writes, no indirection);
 //   5. next-event estimation into the next state: contributions + shadow rays.
 template<bool SMALL, bool EXT>
-__global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(ShadeArgs A)
+__global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_shade(ShadeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
 	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
@@ -1547,7 +1567,7 @@ __global__ void __launch_bounds__(kShadeBlock, YAF_SHADE_MIN_WAVES) k_shade(Shad
 						rng = make_uint2(g.x, g.c);
 						const float probability = maxComp(thr);
 						if(probability <= 0.f || probability < random_value) killed = true;
-						else thr = thr * (1.f / probability);
+						else thr = thr * rcpExact(probability);
 					}
 					if(killed) end_sub = true;
 					else
@@ -1917,10 +1937,10 @@ struct NeeArgs
 };
 
 #ifndef YAF_NEE_MIN_WAVES
-#define YAF_NEE_MIN_WAVES 1
+#define YAF_NEE_MIN_WAVES 4
 #endif
 template<bool SMALL, bool EXT>
-__global__ void __launch_bounds__(kShadeBlock, YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
+__global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
 	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
