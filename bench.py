@@ -77,7 +77,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     import libyafaray_amd as Y
-    from libyafaray_amd import scenes
+    from libyafaray_amd import scenes, tiles
     if a.scene == "sphere":
         spec = scenes.cornell_sphere(width=a.width, height=a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
     elif a.scene == "photon":
@@ -89,26 +89,30 @@ def main():
     yi = Y.Interface()
     scenes.apply(spec, yi)
     yi.L.yafaray_amd_setChunkSlots(yi.h, a.chunk)
-    yi.L.yafaray_amd_setTileRowShard(yi.h, rank, world)
+    # one contiguous pixel-row band per rank (+ its halo row): equal rows at first, then the
+    # boundaries follow the ranks' measured render times (tiles.rebalance_bands, every step)
     if not yi.L.yafaray_amd_buildAccelerator(yi.h):
         raise RuntimeError(yi.last_error())
 
-    W, H, ts = a.width, a.height, spec.render.tile_size
-    tile_rows = (H + ts - 1) // ts
-    my_rows = [r for r in range(tile_rows) if r % world == rank]
-    max_rows = (tile_rows + world - 1) // world
-    band = torch.zeros((max_rows * ts, W, 4), dtype=torch.float32, device=dev)
-    gathered = torch.zeros((world * max_rows * ts, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
+    W, H = a.width, a.height
+    bounds = [tiles.band_range(H, r, world)[0] for r in range(world)] + [H]
+    max_rows = min(H, -(-H * 5 // (4 * world)) + 1)    # a band may grow to 1.25x the mean
+    band = torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev)
+    gathered = torch.zeros((world * max_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
+    t_all = torch.zeros(world, dtype=torch.float64, device=dev) if world > 1 else None
 
     def step():
+        y0, y1 = bounds[rank], bounds[rank + 1]
+        yi.L.yafaray_amd_setRowBandRange(yi.h, y0, y1, world)
+        t_r = time.perf_counter()
         yi.render_quiet()
-        for k, r in enumerate(my_rows):
-            y0, y1 = r * ts, min(H, r * ts + ts)
-            ptr = band.data_ptr() + k * ts * W * 16
-            if not yi.L.yafaray_amd_getFilmDevice(yi.h, ptr, y0, y1):
-                raise RuntimeError(yi.last_error())
+        t_r = time.perf_counter() - t_r
+        if y1 > y0 and not yi.L.yafaray_amd_getFilmDevice(yi.h, band.data_ptr(), y0, y1):
+            raise RuntimeError(yi.last_error())
         if world > 1:
             dist.all_gather_into_tensor(gathered, band)
+            dist.all_gather_into_tensor(t_all, torch.tensor([t_r], dtype=torch.float64, device=dev))
+            bounds[:] = tiles.rebalance_bands(bounds, t_all.tolist(), cap_rows=max_rows)
 
     def sync():
         torch.cuda.synchronize()
@@ -198,7 +202,7 @@ def main():
             "data": "synthetic (Cornell box scene generated in-repo, SURVEY.md §8d)",
             "config": {"workload": workload_name(a, W, H),
                        "width": W, "height": H, "spp": a.spp, "bounces": a.bounces,
-                       "samples_per_step": W * H * a.spp, "parallelism": f"tile-rows x{world}",
+                       "samples_per_step": W * H * a.spp, "parallelism": f"row-bands x{world}",
                        "chunk_slots": a.chunk},
             "mrays_per_s": round(mrays, 2),
             "rays_per_sample": round(rays_total / samples_total, 3),

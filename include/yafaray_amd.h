@@ -67,6 +67,15 @@ YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_getFilmDevice(const yafaray_Inte
 
 /* Restrict the next render to tile rows r with r % world == rank (one process per GPU).  world = 1 renders all. */
 YAFARAY_C_API_EXPORT void yafaray_amd_setTileRowShard(yafaray_Interface_t *interface, int rank, int world);
+/* Restrict the next render to the contiguous pixel-row band [height*rank/world, height*(rank+1)/world)
+   (the default split across GPUs: per-row cost is nearly uniform; one halo row is rendered twice). */
+YAFARAY_C_API_EXPORT void yafaray_amd_setRowBandShard(yafaray_Interface_t *interface, int rank, int world);
+/* Restrict the next render to the explicit pixel-row band [y0, y1) of a film split over `world` GPUs
+   (host-side load balancing moves the band boundaries between frames; halo rows are added here). */
+YAFARAY_C_API_EXPORT void yafaray_amd_setRowBandRange(yafaray_Interface_t *interface, int y0, int y1, int world);
+/* Pixel-row ranges [rows[2k], rows[2k+1]) owned by this rank in the last render; returns their count
+   (at most max_ranges are written). */
+YAFARAY_C_API_EXPORT int yafaray_amd_getOwnedRows(const yafaray_Interface_t *interface, int *rows, int max_ranges);
 
 /* Render without callbacks / console output (bench loop); same work as yafaray_render. */
 YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t *interface);

@@ -127,6 +127,9 @@ def lib():
             "yafaray_amd_getFilm": (b, [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
             "yafaray_amd_getFilmDevice": (b, [vp, vp, i, i]),
             "yafaray_amd_setTileRowShard": (None, [vp, i, i]),
+            "yafaray_amd_setRowBandShard": (None, [vp, i, i]),
+            "yafaray_amd_setRowBandRange": (None, [vp, i, i, i]),
+            "yafaray_amd_getOwnedRows": (i, [vp, C.POINTER(C.c_int), i]),
             "yafaray_amd_renderQuiet": (b, [vp]),
             "yafaray_amd_getStats": (None, [vp, C.POINTER(Stats)]),
             "yafaray_amd_setChunkSlots": (None, [vp, i]),
@@ -248,6 +251,13 @@ class Interface:
         self.L.yafaray_amd_getStats(self.h, C.byref(s))
         return s.as_dict()
 
+    def owned_rows(self):
+        """[(y0, y1), ...] pixel rows this rank's last render owns (yafaray_amd_getOwnedRows)."""
+        n = self.L.yafaray_amd_getOwnedRows(self.h, None, 0)
+        buf = (C.c_int * max(2, 2 * n))()
+        self.L.yafaray_amd_getOwnedRows(self.h, buf, n)
+        return [(buf[2 * k], buf[2 * k + 1]) for k in range(n)]
+
     def trace_closest(self, rays):
         r = np.ascontiguousarray(rays, np.float32).reshape(-1)
         n = len(r) // 8
@@ -279,9 +289,12 @@ def render_spec(spec, chunk_slots=None, profile=False, shard=None):
     if profile:
         yi.L.yafaray_amd_setProfileKernels(yi.h, 1)
     if shard is not None:
-        yi.L.yafaray_amd_setTileRowShard(yi.h, int(shard[0]), int(shard[1]))
+        # (rank, world[, mode]): mode "band" (default, contiguous row band) or "tile" (tile rows r % world)
+        fn = yi.L.yafaray_amd_setTileRowShard if (len(shard) > 2 and shard[2] == "tile") else yi.L.yafaray_amd_setRowBandShard
+        fn(yi.h, int(shard[0]), int(shard[1]))
     yi.render()
     rgba, w = yi.film()
     st = yi.stats()
+    st["owned_rows"] = yi.owned_rows()
     yi.close()
     return rgba, w, st

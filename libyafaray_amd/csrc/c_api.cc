@@ -508,6 +508,41 @@ void yafaray_amd_setTileRowShard(yafaray_Interface_t *interface, int rank, int w
 	if(!s) return;
 	s->shard_world = world < 1 ? 1 : world;
 	s->shard_rank = (rank < 0 || rank >= s->shard_world) ? 0 : rank;
+	s->shard_mode = 0;
+}
+
+void yafaray_amd_setRowBandShard(yafaray_Interface_t *interface, int rank, int world)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return;
+	s->shard_world = world < 1 ? 1 : world;
+	s->shard_rank = (rank < 0 || rank >= s->shard_world) ? 0 : rank;
+	s->shard_mode = 1;
+}
+
+void yafaray_amd_setRowBandRange(yafaray_Interface_t *interface, int y0, int y1, int world)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return;
+	s->shard_world = world < 1 ? 1 : world;
+	s->shard_rank = 0;
+	s->shard_mode = 2;
+	s->shard_y0 = y0;
+	s->shard_y1 = y1;
+}
+
+int yafaray_amd_getOwnedRows(const yafaray_Interface_t *interface, int *rows, int max_ranges)
+{
+	const Interface *it = I(interface);
+	if(!it->scene) return 0;
+	const auto owned = it->scene->gpu()->ownedRows();
+	const int n = (int)owned.size();
+	for(int k = 0; k < n && k < max_ranges && rows; ++k)
+	{
+		rows[2 * k] = owned[k].first;
+		rows[2 * k + 1] = owned[k].second;
+	}
+	return n;
 }
 
 yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t *interface)

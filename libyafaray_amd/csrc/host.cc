@@ -1060,12 +1060,15 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		F.tile = s.tile_size;
 		rp.shard_rank = shard_rank;
 		rp.shard_world = std::max(1, shard_world);
+		rp.shard_mode = shard_mode;
+		rp.shard_y0 = shard_y0;
+		rp.shard_y1 = shard_y1;
 		rp.aa.passes = std::max(1, s.aa_passes);
 		if(rp.aa.passes > 1 && rp.shard_world > 1)
 		{
 			// nextPass compares neighbouring pixels across the whole film; the tile-row shards only
 			// hold their own rows
-			log.error("Scene: AA_passes > 1 with tile-row sharding over several GPUs is not supported; rendering the first pass only");
+			log.error("Scene: AA_passes > 1 with the film sharded over several GPUs is not supported; rendering the first pass only");
 			rp.aa.passes = 1;
 		}
 		rp.aa.inc_samples = s.aa_inc_samples;
@@ -1119,9 +1122,12 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 				for(int tx = 0; tx < s.width; tx += ts, ++area_id)
 				{
 					const int x1 = std::min(s.width, tx + ts), y1 = std::min(s.height, ty + ts);
-					if(!ownedRow(ty)) continue;
+					bool any = false;
+					for(int y = ty; y < y1 && !any; ++y) any = ownedRow(y);
+					if(!any) continue;
 					if(cb.put_pixel)
 						for(int y = ty; y < y1; ++y)
+							if(ownedRow(y))
 							for(int x = tx; x < x1; ++x)
 							{
 								const float *px = &film_rgba[4 * ((size_t)y * s.width + x)];

@@ -192,7 +192,8 @@ class Scene
 		MeshObject *current_object = nullptr;
 		std::string current_material;
 		bool geometry_dirty = true;
-		int shard_rank = 0, shard_world = 1;
+		int shard_rank = 0, shard_world = 1, shard_mode = 1;
+		int shard_y0 = 0, shard_y1 = 0;   // shard_mode 2: explicit row band
 		int chunk_slots = 1 << 25;   // samples in flight per wavefront chunk
 		bool profile_kernels = false;
 		volatile bool canceled = false;

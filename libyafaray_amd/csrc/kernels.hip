@@ -282,8 +282,10 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));   // stage
 	P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
 	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
-	// output is matched statistically — integrator_tiled.cc:272)
-	const uint32_t seed = fnv32((uint32_t)(chunk_base + (uint64_t)i) ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)) + 123u;
+	// output is matched statistically — integrator_tiled.cc:272), seeded from the pixel-major sample
+	// id so that the image does not depend on how the film is split over GPUs or chunks
+	const uint32_t gid = ((uint32_t)sc.y * (uint32_t)S.width + (uint32_t)sc.x) * (uint32_t)S.spp + (uint32_t)sc.s;
+	const uint32_t seed = fnv32(gid ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)) + 123u;
 	P.pr[a] = make_uint4(offset, sample_idx, 30903u, seed);
 }
 

@@ -506,17 +506,38 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		}
 	}
 	const int W = S.width, H = S.height, spp = S.spp, ts = S.tile;
-	// ---- jobs: owned tile rows (+ halo rows for the film gather when sharded) ----
+	// ---- jobs: owned rows (+ halo rows for the film gather when sharded) ----
+	// shard_mode 1: one contiguous band of H / world pixel rows per rank (per-row cost is nearly
+	// uniform, so equal bands balance the GPUs and only one halo row is rendered twice);
+	// shard_mode 0: whole tile rows r % world == rank.  Either way every owned pixel gets exactly the
+	// samples, and the film order, of a one-GPU render.
 	const int tile_rows = (H + ts - 1) / ts;
 	std::vector<DevJob> jobs;
 	owned_rows_.clear();
 	uint64_t total = 0;
-	auto owns = [&](int r) { return r >= 0 && r < tile_rows && (r % rp.shard_world) == rp.shard_rank; };
-	for(int r = 0; r < tile_rows; ++r)
+	if(rp.shard_world <= 1) owned_rows_.push_back({0, H});
+	else if(rp.shard_mode == 2)
 	{
-		if(!owns(r)) continue;
-		const int y0 = r * ts, y1 = std::min(H, y0 + ts);
-		if(rp.shard_world > 1 && rp.film.reach_fwd > 0 && y0 > 0 && !owns(r - 1))
+		const int y0 = std::max(0, rp.shard_y0), y1 = std::min(H, rp.shard_y1);
+		if(y1 > y0) owned_rows_.push_back({y0, y1});
+	}
+	else if(rp.shard_mode == 1)
+	{
+		const int y0 = (int)((int64_t)H * rp.shard_rank / rp.shard_world), y1 = (int)((int64_t)H * (rp.shard_rank + 1) / rp.shard_world);
+		if(y1 > y0) owned_rows_.push_back({y0, y1});
+	}
+	else
+		for(int r = 0; r < tile_rows; ++r)
+		{
+			if(r % rp.shard_world != rp.shard_rank) continue;
+			const int y0 = r * ts, y1 = std::min(H, y0 + ts);
+			if(!owned_rows_.empty() && owned_rows_.back().second == y0) owned_rows_.back().second = y1;
+			else owned_rows_.push_back({y0, y1});
+		}
+	for(const auto &o : owned_rows_)
+	{
+		const int y0 = o.first, y1 = o.second;
+		if(rp.shard_world > 1 && rp.film.reach_fwd > 0 && y0 > 0)
 		{
 			const int hy0 = std::max(0, y0 - rp.film.reach_fwd);
 			jobs.push_back({hy0, y0, total});
@@ -524,8 +545,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		}
 		jobs.push_back({y0, y1, total});
 		total += (uint64_t)W * (y1 - y0) * spp;
-		owned_rows_.push_back({y0, y1});
-		if(rp.shard_world > 1 && rp.film.reach_back > 0 && y1 < H && !owns(r + 1))
+		if(rp.shard_world > 1 && rp.film.reach_back > 0 && y1 < H)
 		{
 			const int hy1 = std::min(H, y1 + rp.film.reach_back);
 			jobs.push_back({y1, hy1, total});

@@ -66,6 +66,9 @@ struct RenderParams
 	AaParams aa;
 	DevFilm film;
 	int shard_rank = 0, shard_world = 1;
+	int shard_mode = 1;   // 0: tile rows r % world == rank, 1: contiguous row band [H rank / world, H (rank + 1) / world),
+	                      // 2: the explicit band [shard_y0, shard_y1) (host-side load balancing)
+	int shard_y0 = 0, shard_y1 = 0;
 	int chunk_slots = 1 << 25;   // samples in flight per wavefront chunk
 	bool profile = false;
 };

@@ -60,3 +60,46 @@ def test_sharding_covers_every_row_once():
             for t in tiles.owned_tile_rows(H, ts, r, world):
                 seen[t * ts:min(H, t * ts + ts)] += 1
         assert (seen == 1).all()
+
+
+def _band_worker(rank, world, port, image, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    H = image.shape[0]
+    band = torch.from_numpy(tiles.pack_row_band(image, rank, world))
+    parts = [torch.zeros_like(band) for _ in range(world)]
+    dist.all_gather(parts, band)
+    full = tiles.assemble_row_bands(torch.cat(parts).numpy(), H, world)
+    if rank == 0:
+        q.put(full)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allgather_reassembles_row_bands(world, oracle_built):
+    """The default split (contiguous row bands, bench.py) through gloo all-gather."""
+    from libyafaray_amd import scenes
+    spec = scenes.cornell(96, 70, spp=2, bounces=3, rr=False)
+    image, _, _ = oracle_built.OracleScene(spec, threads=4).render()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, image, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.array_equal(full.view(np.uint32), image.view(np.uint32))
+
+
+def test_row_bands_cover_every_row_once():
+    for H, world in [(1080, 8), (1080, 3), (70, 4), (5, 8), (1, 2)]:
+        seen = np.zeros(H, int)
+        for r in range(world):
+            y0, y1 = tiles.band_range(H, r, world)
+            seen[y0:y1] += 1
+        assert (seen == 1).all()
+        assert tiles.band_rows_max(H, world) <= -(-H // world)
