@@ -1,5 +1,6 @@
 // Host side: logger, scene assembly and render orchestration (see host.h).
 #include "host.h"
+#include "filmio.h"
 #include "hostmath.h"
 #include "render.h"
 #include "texture.h"
@@ -685,6 +686,11 @@ bool Scene::setupRender(const ParamMap &p)
 	p.get("adv_min_raydist_value", s.ray_min_dist);
 	p.get("adv_base_sampling_offset", s.base_sampling_offset);
 	p.get("adv_computer_node", s.computer_node);
+	p.get("film_load_save_mode", s.film_load_save_mode);
+	p.get("film_load_save_path", s.film_load_save_path);
+	p.get("film_autosave_interval_type", s.film_autosave_interval_type);
+	p.get("film_autosave_interval_passes", s.film_autosave_interval_passes);
+	p.get("film_autosave_interval_seconds", s.film_autosave_interval_seconds);
 	p.get("scene_accelerator", s.accelerator);
 	p.get("AA_pixelwidth", s.aa_pixelwidth);
 	p.get("width", s.width);
@@ -1095,7 +1101,67 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			if(cb.notify_layer) cb.notify_layer("combined", "Combined", s.width, s.height, 4, cb.notify_layer_data);
 			if(progress) progress(s.width * s.height, 0, "Rendering...", progress_data);
 		}
+		// ---- film load / save (ImageFilm::init imagefilm.cc:225-241, flush :657-662, nextPass :282-286) ----
+		const filmio::Mode fmode = filmio::parseMode(s.film_load_save_mode);
+		filmio::Film film_io;
+		film_io.computer_node = (uint32_t)s.computer_node;
+		film_io.base_sampling_offset = (uint32_t)s.base_sampling_offset;
+		film_io.width = s.width;
+		film_io.height = s.height;
+		film_io.cx0 = s.xstart;
+		film_io.cx1 = s.xstart + s.width;
+		film_io.cy0 = s.ystart;
+		film_io.cy1 = s.ystart + s.height;
+		const std::string film_file = filmio::filmPath(s.film_load_save_path, s.computer_node);
+		if(fmode != filmio::None && rp.shard_world > 1)
+		{
+			log.error("Scene: film load/save with the film sharded over several GPUs is not supported");
+			return false;
+		}
+		if(fmode == filmio::LoadAndSave)
+		{
+			film_io.weights.assign((size_t)s.width * s.height, 0.f);
+			film_io.rgba.assign((size_t)s.width * s.height * 4, 0.f);
+			if(filmio::loadAllInFolder(log, s.film_load_save_path, film_io))
+			{
+				rp.resumed = true;
+				rp.load_rgba = film_io.rgba.data();
+				rp.load_weights = film_io.weights.data();
+				rp.resume_sampling_offset = film_io.sampling_offset;
+				S.base_offset = film_io.base_sampling_offset;
+				rp.film.sample_offset = S.base_offset;
+				log.info(itype + ": Combining ImageFilm files, skipping pass 1...");
+			}
+		}
+		if(fmode != filmio::None) filmio::backup(log, film_file);
+		auto saveFilm = [&]() {
+			filmio::Film out = film_io;
+			out.sampling_offset = gpu()->samplingOffset();
+			if(gpu()->downloadAccum(out.rgba, out.weights)) filmio::save(log, film_file, out);
+		};
+		int autosave_passes = 0;
+		const auto autosave_t0 = std::chrono::steady_clock::now();
+		auto autosave_last = autosave_t0;
+		if(fmode != filmio::None && s.film_autosave_interval_type != "none")
+			rp.on_next_pass = [&](bool skipped) {
+				++autosave_passes;
+				if(skipped) return;
+				if(s.film_autosave_interval_type == "pass-interval" && autosave_passes >= s.film_autosave_interval_passes)
+				{
+					saveFilm();
+					autosave_passes = 0;
+				}
+				// time-interval autosave: checked at pass boundaries (the reference checks per finished tile)
+				const auto now = std::chrono::steady_clock::now();
+				if(s.film_autosave_interval_type == "time-interval" &&
+				   std::chrono::duration<double>(now - autosave_last).count() > s.film_autosave_interval_seconds)
+				{
+					saveFilm();
+					autosave_last = now;
+				}
+			};
 		if(!gpu()->render(rp, &canceled)) return false;
+		if(fmode != filmio::None) saveFilm();
 		const double build = stats.build_seconds;
 		stats = gpu()->stats();
 		stats.build_seconds = build;

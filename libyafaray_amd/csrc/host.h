@@ -147,6 +147,10 @@ struct RenderSetup
 	bool shadow_bias_auto = true, ray_min_dist_auto = true;
 	float shadow_bias = 0.0005f, ray_min_dist = 0.00005f;
 	int base_sampling_offset = 0, computer_node = 0;
+	// film load/save (imagefilm.cc:55-118)
+	std::string film_load_save_mode = "none", film_load_save_path = "./", film_autosave_interval_type = "none";
+	int film_autosave_interval_passes = 1;
+	double film_autosave_interval_seconds = 300.0;
 	std::string accelerator = "yafaray-kdtree-original";
 	bool valid = false;
 };

@@ -564,6 +564,13 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	HIPCHECK(hipMemsetAsync(d.film.p, 0, (size_t)W * H * sizeof(float4), d.stream));
 	HIPCHECK(hipMemsetAsync(d.weights.p, 0, (size_t)W * H * sizeof(float), d.stream));
 	HIPCHECK(hipMemsetAsync(d.accum.p, 0, (size_t)W * H * sizeof(float4), d.stream));
+	if(rp.load_rgba && rp.load_weights)
+	{
+		// film files loaded and summed on the host (imageFilmLoadAllInFolder) become the accumulators
+		HIPCHECK(hipMemcpyAsync(d.accum.p, rp.load_rgba, (size_t)W * H * sizeof(float4), hipMemcpyHostToDevice, d.stream));
+		HIPCHECK(hipMemcpyAsync(d.weights.p, rp.load_weights, (size_t)W * H * sizeof(float), hipMemcpyHostToDevice, d.stream));
+		HIPCHECK(hipStreamSynchronize(d.stream));
+	}
 	// ---- chunk buffers ----
 	size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
 	if(S.tree)
@@ -780,12 +787,27 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	S.plist = nullptr;
 	rp.film.multipass = S.aa_multipass;
 	rp.film.sample_offset = S.base_offset;
-	if(!runSamples(total)) return false;
-	for(const auto &r : owned_rows_)
-		HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, nullptr, (float4 *)d.accum.p, (float4 *)d.film.p,
-		                            (float *)d.weights.p, r.first, r.second, S.clamp_samples, 0, d.stream));
-	passes_done_ = 1;
 	uint64_t samples_total = total;
+	if(rp.resumed)
+	{
+		// renderPass(0, sampling_offset): no samples; the loaded film is only normalised
+		DevFilm F0 = rp.film;
+		F0.spp = 0;
+		for(const auto &r : owned_rows_)
+			HIPCHECK(yafamd_launch_film(&F0, (const float4 *)d.samples.p, nullptr, (float4 *)d.accum.p, (float4 *)d.film.p,
+			                            (float *)d.weights.p, r.first, r.second, S.clamp_samples, 1, d.stream));
+		samples_total = 0;
+		sampling_offset_ = rp.resume_sampling_offset;
+	}
+	else
+	{
+		if(!runSamples(total)) return false;
+		for(const auto &r : owned_rows_)
+			HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, nullptr, (float4 *)d.accum.p, (float4 *)d.film.p,
+			                            (float *)d.weights.p, r.first, r.second, S.clamp_samples, 0, d.stream));
+		sampling_offset_ = (uint32_t)spp;
+	}
+	passes_done_ = 1;
 	if(passes > 1)
 	{
 		if(!ensure(log_, d.aa_flags, (size_t)W * H) || !ensure(log_, d.aa_plist, (size_t)W * H * 4)) return false;
@@ -797,7 +819,13 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		{
 			if(canceled && *canceled) break;
 			sample_multiplier *= rp.aa.sample_multiplier_factor;
-			if(resampled <= 0.f && !threshold_changed) {}   // nextPass(..., skipNextPass = true)
+			const bool skip = resampled <= 0.f && !threshold_changed;
+			if(rp.on_next_pass)
+			{
+				HIPCHECK(hipStreamSynchronize(d.stream));
+				rp.on_next_pass(skip);
+			}
+			if(skip) {}   // nextPass(..., skipNextPass = true)
 			else
 			{
 				uint32_t count = 0;
@@ -837,6 +865,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				                            (float4 *)d.film.p, (float *)d.weights.p, 0, H, S.clamp_samples, 1, d.stream));
 				samples_total += n_total;
 				++passes_done_;
+				sampling_offset_ = (uint32_t)(acum + n_pass);   // renderPass: setSamplingOffset(offset + samples)
 			}
 			acum += n_pass;
 			if(resampled < floor_pixels)
@@ -901,6 +930,18 @@ bool GpuRenderer::download(std::vector<float> &rgba, std::vector<float> &weights
 	rgba.resize((size_t)w * h * 4);
 	weights.resize((size_t)w * h);
 	HIPCHECK(hipMemcpy(rgba.data(), d.film.p, rgba.size() * 4, hipMemcpyDeviceToHost));
+	HIPCHECK(hipMemcpy(weights.data(), d.weights.p, weights.size() * 4, hipMemcpyDeviceToHost));
+	return true;
+}
+
+bool GpuRenderer::downloadAccum(std::vector<float> &rgba, std::vector<float> &weights)
+{
+	Impl &d = *d_;
+	if(!d.accum.p || !d.weights.p) { log_.error("GPU: no film to download"); return false; }
+	rgba.resize((size_t)d.film_w * d.film_h * 4);
+	weights.resize((size_t)d.film_w * d.film_h);
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	HIPCHECK(hipMemcpy(rgba.data(), d.accum.p, rgba.size() * 4, hipMemcpyDeviceToHost));
 	HIPCHECK(hipMemcpy(weights.data(), d.weights.p, weights.size() * 4, hipMemcpyDeviceToHost));
 	return true;
 }

@@ -13,6 +13,7 @@
 
 #include <cstdint>
 #include <string>
+#include <functional>
 #include <vector>
 
 namespace yafamd
@@ -71,6 +72,14 @@ struct RenderParams
 	int shard_y0 = 0, shard_y1 = 0;
 	int chunk_slots = 1 << 25;   // samples in flight per wavefront chunk
 	bool profile = false;
+	// film load/save (filmio.h): accumulators loaded from film files, uploaded before the first pass;
+	// resumed = the first pass renders no samples (integrator_tiled.cc:174-177)
+	const float *load_rgba = nullptr, *load_weights = nullptr;
+	bool resumed = false;
+	uint32_t resume_sampling_offset = 0;   // the loaded films' sampling offset (max over the files)
+	// ImageFilm::nextPass hook (imagefilm.cc:259-287), called before every adaptive pass with
+	// skipped = the pass's nextPass was skipped; the film autosave lives there
+	std::function<void(bool skipped)> on_next_pass;
 };
 
 class GpuRenderer
@@ -81,7 +90,9 @@ class GpuRenderer
 		bool ready();
 		bool upload(HostScene &hs);   // fills hs.bvh's metadata when the BVH is built on the device
 		bool render(RenderParams &rp, volatile bool *canceled);
-		int lastPassCount() const { return passes_done_; }   // AA passes rendered by the last render()
+		int lastPassCount() const { return passes_done_; }
+		uint32_t samplingOffset() const { return sampling_offset_; }   // ImageFilm::sampling_offset_ after the last pass
+		bool downloadAccum(std::vector<float> &rgba, std::vector<float> &weights);   // unnormalised film (film files)   // AA passes rendered by the last render()
 		bool download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h);
 		bool filmToDevice(void *dst, int y0, int y1);
 		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
@@ -97,6 +108,7 @@ class GpuRenderer
 		yafaray_amd_stats_t stats_{};
 		std::vector<std::pair<int, int>> owned_rows_;
 		int passes_done_ = 0;
+		uint32_t sampling_offset_ = 0;
 };
 
 } // namespace yafamd

@@ -131,6 +131,12 @@ class Render:
     ray_min_dist_auto: bool = True
     ray_min_dist: float = 0.00005
     base_sampling_offset: int = 0
+    computer_node: int = 0
+    # film load/save (imagefilm.cc:55-118)
+    film_load_save_mode: str = "none"       # "save" | "load-save"
+    film_load_save_path: str = "./"
+    film_autosave_interval_type: str = "none"   # "pass-interval" | "time-interval"
+    film_autosave_interval_passes: int = 1
     clamp_samples: float = 0.0
     accelerator: str = "yafaray-kdtree-original"
     # adaptive anti-aliasing (scene.cc:582-595; defaults of aa_noise_params.h:27-46)
@@ -582,6 +588,11 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetBool("adv_auto_min_raydist_enabled", r.ray_min_dist_auto)
     api.paramsSetFloat("adv_min_raydist_value", r.ray_min_dist)
     api.paramsSetInt("adv_base_sampling_offset", r.base_sampling_offset)
+    api.paramsSetInt("adv_computer_node", r.computer_node)
+    api.paramsSetString("film_load_save_mode", r.film_load_save_mode)
+    api.paramsSetString("film_load_save_path", r.film_load_save_path)
+    api.paramsSetString("film_autosave_interval_type", r.film_autosave_interval_type)
+    api.paramsSetInt("film_autosave_interval_passes", r.film_autosave_interval_passes)
     api.paramsSetString("scene_accelerator", r.accelerator)
     api.paramsSetInt("threads", -1)
     api.paramsSetInt("threads_photons", r.threads_photons)
