@@ -103,3 +103,30 @@ def test_row_bands_cover_every_row_once():
             seen[y0:y1] += 1
         assert (seen == 1).all()
         assert tiles.band_rows_max(H, world) <= -(-H // world)
+
+
+def test_rebalance_bands_moves_towards_equal_cost():
+    """bench.py's band load balancing (tiles.rebalance_bands): boundaries stay ordered, every band keeps
+    >= 1 row, the cap is honoured, equal times keep equal bands, and a slow band shrinks."""
+    H, world = 1080, 8
+    bounds = [tiles.band_range(H, r, world)[0] for r in range(world)] + [H]
+    assert tiles.rebalance_bands(bounds, [1.0] * world) == bounds
+    times = [1.0] * world
+    times[3] = 2.0
+    new = tiles.rebalance_bands(bounds, times)
+    assert new[0] == 0 and new[-1] == H and all(new[r] < new[r + 1] for r in range(world))
+    assert new[4] - new[3] < bounds[4] - bounds[3]
+    # iterating with a fixed per-row cost density converges to equal cost per band
+    dens = np.linspace(1.0, 3.0, H)
+    b = list(bounds)
+    for _ in range(30):
+        cost = [dens[b[r]:b[r + 1]].sum() for r in range(world)]
+        b = tiles.rebalance_bands(b, cost)
+    cost = [dens[b[r]:b[r + 1]].sum() for r in range(world)]
+    assert max(cost) / min(cost) < 1.03
+    # a cap that the new split would exceed keeps the old bounds; degenerate sizes are left alone
+    cap = max(bounds[r + 1] - bounds[r] for r in range(world))
+    assert tiles.rebalance_bands(bounds, times, cap_rows=cap) in (bounds, new)
+    assert tiles.rebalance_bands([0, 3], [1.0]) == [0, 3]
+    tiny = tiles.rebalance_bands([0, 1, 2, 3], [5.0, 1.0, 1.0])
+    assert tiny == [0, 1, 2, 3]
