@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--no-rr", action="store_true", help="Russian roulette off (bit-parity variant)")
     ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere", "photon"])
     ap.add_argument("--photons", type=int, default=10_000_000, help="C5: diffuse photons")
-    ap.add_argument("--chunk", type=int, default=1 << 25)
+    ap.add_argument("--chunk", type=int, default=1 << 26)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()

@@ -198,7 +198,7 @@ class Scene
 		bool geometry_dirty = true;
 		int shard_rank = 0, shard_world = 1, shard_mode = 1;
 		int shard_y0 = 0, shard_y1 = 0;   // shard_mode 2: explicit row band
-		int chunk_slots = 1 << 25;   // samples in flight per wavefront chunk
+		int chunk_slots = 1 << 26;   // samples in flight per wavefront chunk (64 M: the C2 frame in two chunks)
 		bool profile_kernels = false;
 		volatile bool canceled = false;
 

@@ -13,6 +13,6 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU --output-format csv -d $R/gpurun_out/pmcV_$TAG -o run -- python3 $P > $R/gpurun_out/pmcV_$TAG.log 2>&1
 cd $R
 python3 tools/pmc_traffic.py gpurun_out/pmcF_$TAG/run_counter_collection.csv gpurun_out/pmcW_$TAG/run_counter_collection.csv \
-	cornell-1920x1080x64-b8-rr1-chunk33554432 gpurun_out/trace_hbm_bytes_per_launch.json gpurun_out/pmcV_$TAG/run_counter_collection.csv
+	cornell-1920x1080x64-b8-rr1-chunk67108864 gpurun_out/trace_hbm_bytes_per_launch.json gpurun_out/pmcV_$TAG/run_counter_collection.csv
 cp gpurun_out/trace_hbm_bytes_per_launch.json profiles/
 timeout -k 10 240 python3 bench.py > gpurun_out/bench_$TAG.log 2>&1
