@@ -389,6 +389,48 @@ YD uint32_t fnv32(uint32_t value)
 	return hash;
 }
 
+// Halton(base, start) as a running generator (halton.h:41-81: setStart, then getNext per draw) —
+// for loops that draw consecutive numbers of one sequence (area-light samples, AO samples)
+template<uint32_t B>
+struct HaltonInc
+{
+	double value;
+	static constexpr double inv_base = 1.0 / static_cast<double>(B);
+	YD void start(uint32_t s)
+	{
+		if(B == 2)
+		{
+			// distinct powers of two: the digit sum is exactly bitreverse(s) * 2^-32
+			value = static_cast<double>(bitReverse32(s)) * 2.3283064365386962890625e-10;
+			return;
+		}
+		double factor = inv_base;
+		value = 0.0;
+		while(s > 0)
+		{
+			value += static_cast<double>(s % B) * factor;
+			s /= B;
+			factor *= inv_base;
+		}
+	}
+	YD float next()
+	{
+		const double r = 0.9999999999 - value;
+		if(inv_base < r) value += inv_base;
+		else
+		{
+			double hh = 0.0, h = inv_base;
+			while(h >= r)
+			{
+				hh = h;
+				h *= inv_base;
+			}
+			value += hh + h - 1.0;
+		}
+		return clamp01(static_cast<float>(value));
+	}
+};
+
 // Halton(base, start).getNext() — one fresh generator per call site (integrator_montecarlo.cc:399)
 YD float haltonFirst(uint32_t base, double inv_base, uint32_t start)
 {

@@ -25,14 +25,17 @@ enum : uint32_t
 
 enum : uint32_t { MAT_SHINYDIFFUSE = 0, MAT_LIGHT = 1, MAT_MIRROR = 2, MAT_NULL = 3 };
 // ShinyDiffuseMaterial components and options (material_shiny_diffuse.cc:38-87, 548-566)
-enum : uint32_t { SD_MIRROR = 1u, SD_TRANSPARENT = 2u, SD_TRANSLUCENT = 4u, SD_DIFFUSE = 8u, SD_FRESNEL = 16u, SD_TBIAS_MULT = 32u };
+enum : uint32_t { SD_MIRROR = 1u, SD_TRANSPARENT = 2u, SD_TRANSLUCENT = 4u, SD_DIFFUSE = 8u, SD_FRESNEL = 16u, SD_TBIAS_MULT = 32u,
+                  SD_OREN_NAYAR = 64u };
 enum : uint32_t { LIGHT_POINT = 0, LIGHT_AREA = 1 };
 enum : int { INT_DIRECT = 0, INT_PATH = 1, INT_PHOTON = 2 };
 
 struct DevMaterial
 {
 	uint32_t type, bsdf_flags, n_bsdf, double_sided;
-	uint32_t receive_shadows, flat, pad0, pad1;
+	uint32_t receive_shadows, flat;
+	int add_depth;          // additionaldepth (Material::additional_depth_, integrator_montecarlo.cc:923)
+	int sigma_root;         // sigma_oren_shader root (program-local, -1: none)
 	float diffuse[4];       // shinydiffuse diffuse colour
 	float emit[4];          // shinydiffuse emit colour / light_mat colour * power
 	float comp[4];          // getComponents() (no shader nodes)
@@ -48,7 +51,8 @@ struct DevMaterial
 	float ior_sq;           // IOR^2 (Fresnel)
 	float tbias;            // transparentbias_factor (specularRefract, integrator_montecarlo.cc:890-898)
 	uint32_t sd_flags;      // SD_*
-	uint32_t pad2, pad3, pad4;
+	float on_a, on_b;       // Oren-Nayar A / B (initOrenNayar, material_shiny_diffuse.cc:146-152), SD_OREN_NAYAR
+	uint32_t pad4;
 	float mirror_col[4];    // shinydiffuse mirror_color; mirror material: colour * reflect
 };
 
@@ -216,12 +220,18 @@ struct DevScene
 	// every integrate() call is a node; nodes of ray level L + 1 are spawned by the level-L pass
 	// and traced by the next pass; k_combine folds the tree bottom-up in the reference's order.
 	int ext, tree, raydepth, cur_level;
+	int max_add_depth;             // largest material additionaldepth (sizes the recursion tree)
 	int bg_transp_refract;
 	// transparent shadows (MonteCarloIntegrator tr_shad_ / s_depth_, accelerator_kdtree.cc:916-1061):
 	// shadow rays keep tmin in sh_o.w, k_trace<TS> lists the transparent surfaces each one crosses
 	// (DevQueues::ts_hit, s_depth per ray), k_tshadow multiplies their filter colours into the
 	// NEE contributions whose factors k_nee kept in DevPaths::ts
 	int tr_shad, s_depth;
+	// DirectLight ambient occlusion (TiledIntegrator::sampleAmbientOcclusion, integrator_tiled.cc:644-691):
+	// ao_samples NEE entries per diffuse camera vertex after the lights' (nee_all_count) entries
+	int do_ao, ao_samples;
+	float ao_dist;
+	float ao_col[3];
 	uint32_t node_base;            // node id of spawn slot 0 (= level-0 capacity of the chunk)
 	uint32_t spawn_cap;
 	float4 *node_own;              // per node: colour before recursiveRaytrace's result, alpha

@@ -116,8 +116,13 @@ bool Scene::createObject(const std::string &name, const ParamMap &p)
 	o.name = name;
 	p.get("is_base_object", o.is_base);
 	p.get("visibility", o.visibility);
-	if(o.visibility != "normal" && o.visibility != "visible" && o.visibility != "invisible")
-		log.warning("Scene: object '" + name + "' visibility '" + o.visibility + "' is treated as 'normal' by the GPU core");
+	// visibility::fromString (include/common/visibility.h:36-43): unknown strings are "normal"
+	if(o.visibility == "shadow_only" || o.visibility == "no_shadows")
+	{
+		log.error("Scene: object '" + name + "' visibility '" + o.visibility + "' is not supported by the GPU core (normal / invisible)");
+		objects.erase(name);
+		return false;
+	}
 	int nv = 0, nf = 0;
 	if(p.get("num_vertices", nv) && nv > 0) o.verts.reserve(3 * (size_t)nv);
 	if(p.get("num_faces", nf) && nf > 0) { o.tris.reserve(3 * (size_t)nf); o.tri_mat.reserve(nf); }
@@ -360,7 +365,7 @@ bool Scene::createMaterial(const std::string &name, const ParamMap &p, const std
 	p.get("type", type);
 	DevMaterial m{};
 	m.receive_shadows = 1;
-	m.diffuse_root = m.drefl_root = -1;
+	m.diffuse_root = m.drefl_root = m.sigma_root = -1;
 	bool b;
 	if(type == "shinydiffusemat")
 	{
@@ -384,21 +389,32 @@ bool Scene::createMaterial(const std::string &name, const ParamMap &p, const std
 		p.get("transparentbias_multiply_raydepth", tbias_mult);
 		p.get("wireframe_amount", wire);
 		p.get("additionaldepth", add_depth);
+		// material_shiny_diffuse.cc:561-571: diffuse_brdf "oren_nayar" -> initOrenNayar(sigma) (:146-152),
+		// double arithmetic stored to the float A / B members
 		std::string brdf;
 		if(p.get("diffuse_brdf", brdf) && brdf == "oren_nayar")
 		{
-			log.error("Material '" + name + "': Oren-Nayar diffuse BRDF is not supported by the GPU core yet");
+			double sigma = 0.1;
+			p.get("sigma", sigma);
+			const double sigma_squared = sigma * sigma;
+			m.on_a = static_cast<float>(1.0 - 0.5 * (sigma_squared / (sigma_squared + 0.33)));
+			m.on_b = static_cast<float>(0.45 * sigma_squared / (sigma_squared + 0.09));
+			m.sd_flags |= SD_OREN_NAYAR;
+		}
+		m.add_depth = add_depth;
+		if(wire > 0.f)
+		{
+			log.error("Material '" + name + "': wireframe shading (wireframe_amount > 0) is not supported by the GPU core");
 			return false;
 		}
-		if(wire > 0.f) log.warning("Material '" + name + "': wireframe shading is not evaluated by the GPU core; ignored");
-		if(add_depth > 0) log.warning("Material '" + name + "': additionaldepth is not evaluated by the GPU core (raydepth applies); ignored");
 		// shader nodes (material_shiny_diffuse.cc:579-660)
 		std::vector<DevNode> prog;
-		int droot = -1, rroot = -1;
-		if(!buildNodeProgram(log, texture_index, textures, name, p, nodes, prog, droot, rroot)) return false;
+		int droot = -1, rroot = -1, sroot = -1;
+		if(!buildNodeProgram(log, texture_index, textures, name, p, nodes, prog, droot, rroot, sroot)) return false;
 		m.n_nodes = (int)prog.size();
 		m.diffuse_root = droot;
 		m.drefl_root = rroot;
+		m.sigma_root = (m.sd_flags & SD_OREN_NAYAR) ? sroot : -1;   // sigma_oren_shader_ is read by orenNayar only
 		m.emit_strength = emit;
 		if(!prog.empty()) mat_nodes[name] = prog;
 		m.type = MAT_SHINYDIFFUSE;
@@ -533,7 +549,7 @@ bool Scene::createLight(const std::string &name, const ParamMap &p)
 		p.get("samples", samples);
 		std::string object_name;
 		if(p.get("object_name", object_name) && !object_name.empty())
-			log.warning("Light '" + name + "': area light geometry objects are rendered as ordinary meshes by the GPU core");
+			object_name.clear();   // AreaLight::init -> Object::setLight: read only by the bidirectional integrator (primitive_triangle.cc:166)
 		L.type = LIGHT_AREA;
 		const F3 c = f3(corner), tx = sub(f3(p1), c), ty = sub(f3(p2), c);
 		F3 fn = crs(ty, tx);
@@ -612,7 +628,12 @@ bool Scene::createBackground(const std::string &name, const ParamMap &p)
 	p.getColor("color", col);
 	p.get("power", power);
 	p.get("ibl", ibl);
-	if(ibl) log.warning("Background '" + name + "': image-based lighting is not supported by the GPU core; ignored");
+	if(ibl)
+	{
+		// background_constant.cc:58-69 would add a "bglight" (BackgroundLight) to the scene
+		log.error("Background '" + name + "': image-based lighting (ibl = true) is not supported by the GPU core");
+		return false;
+	}
 	backgrounds[name] = {power * col[0], power * col[1], power * col[2]};   // background_constant.cc:56
 	return true;
 }
@@ -660,7 +681,14 @@ bool Scene::setupRender(const ParamMap &p)
 	if(!p.get("integrator_name", s.integrator_name)) { log.error("Scene: Specify an Integrator!!"); return false; }
 	if(!integrators.count(s.integrator_name)) { log.error("Scene: Specify an _existing_ Integrator!!"); return false; }
 	std::string vol;
-	if(p.get("volintegrator_name", vol)) log.warning("Scene: volume integrators are not supported by the GPU core; ignored");
+	// scene.cc:564-572: a named integrator that is not a volume integrator is an error; an unknown name
+	// means no volume integrator.  Volume integrator types are not created by the GPU core, so every
+	// existing integrator is a surface one.
+	if(p.get("volintegrator_name", vol) && integrators.count(vol))
+	{
+		log.error("Scene: Integrator '" + vol + "' is not a volume integrator!");
+		return false;
+	}
 	if(p.get("background_name", s.background_name) && !backgrounds.count(s.background_name))
 		log.error("Scene: please specify an _existing_ Background!!");
 	p.get("AA_passes", s.aa_passes);
@@ -702,8 +730,6 @@ bool Scene::setupRender(const ParamMap &p)
 	p.get("tiles_order", s.tiles_order);
 	if(s.accelerator != "yafaray-kdtree-original" && s.accelerator != "yafaray-kdtree-multi-thread" && s.accelerator != "yafaray-simpletest")
 		log.warning("Accelerator type '" + s.accelerator + "' could not be created, using the GPU BVH instead.");  // accelerator.cc:47-51
-	if(s.aa_passes > 1 && s.aa_light_sample_multiplier_factor != 1.f)
-		log.warning("Scene: AA_light_sample_multiplier_factor != 1 is not supported by the GPU core; light samples stay constant over the passes");
 	if(s.xstart != 0 || s.ystart != 0) { log.error("Scene: cropped films (xstart/ystart != 0) are not supported by the GPU core yet"); return false; }
 	if(s.filter != "box" && s.filter != "gauss" && s.filter != "mitchell" && s.filter != "lanczos")
 	{
@@ -969,8 +995,8 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			if(caustic_type == "none") S.caustic_path = 0;
 			else if(caustic_type == "photon" || caustic_type == "both")
 			{
-				if(caustic_type == "photon") S.caustic_path = 0;
-				log.warning("PathIntegrator: photon caustics are not supported by the GPU core yet; ignored");
+				log.error("PathIntegrator: caustic_type '" + caustic_type + "' (photon caustics) is not supported by the GPU core");
+				return false;
 			}
 		}
 		if(S.integrator == INT_DIRECT)
@@ -978,7 +1004,30 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			bool caus = false, ao = false;
 			ip.get("caustics", caus);
 			ip.get("do_AO", ao);
-			if(caus || ao) log.warning("DirectLight: caustic photons / ambient occlusion are not supported by the GPU core yet; ignored");
+			if(caus)
+			{
+				log.error("DirectLight: caustics = true (caustic photon map) is not supported by the GPU core");
+				return false;
+			}
+			// integrator_direct_light.cc:161-186: do_AO, AO_samples (32), AO_distance (1.0, double), AO_color (1)
+			if(ao)
+			{
+				int ao_samples = 32;
+				double ao_dist = 1.0;
+				float ao_col[4] = {1.f, 1.f, 1.f, 1.f};
+				ip.get("AO_samples", ao_samples);
+				ip.get("AO_distance", ao_dist);
+				ip.getColor("AO_color", ao_col);
+				if(ao_samples < 1)
+				{
+					log.error("DirectLight: AO_samples must be >= 1");   // the reference divides by it (integrator_tiled.cc:690)
+					return false;
+				}
+				S.do_ao = 1;
+				S.ao_samples = ao_samples;
+				S.ao_dist = static_cast<float>(ao_dist);
+				for(int k = 0; k < 3; ++k) S.ao_col[k] = ao_col[k];
+			}
 		}
 		S.bounces = bounces;
 		S.path_samples = (S.integrator == INT_PATH) ? std::max(1, path_samples) : 1;
@@ -1007,11 +1056,14 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		}
 		S.tree = 0;
 		S.ext = 0;
+		S.max_add_depth = 0;
 		for(const auto &kv : materials)
 		{
 			const DevMaterial &m = kv.second;
+			S.max_add_depth = std::max(S.max_add_depth, m.add_depth);
 			if(m.bsdf_flags & (B_SPECULAR | B_FILTER)) S.tree = 1;
-			if(m.type == MAT_MIRROR || m.type == MAT_NULL || m.n_nodes > 0 || (m.sd_flags & (SD_MIRROR | SD_TRANSPARENT | SD_TRANSLUCENT | SD_FRESNEL)))
+			if(m.type == MAT_MIRROR || m.type == MAT_NULL || m.n_nodes > 0 ||
+			   (m.sd_flags & (SD_MIRROR | SD_TRANSPARENT | SD_TRANSLUCENT | SD_FRESNEL | SD_OREN_NAYAR)))
 				S.ext = 1;
 		}
 		if(S.integrator == INT_PHOTON && S.tree)
@@ -1041,10 +1093,16 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			nee_max_one = std::max(nee_max_one, kv.second.nee_count);
 		}
 		S.nee_all_count = (int)nee_all;
-		S.nee_k = (int)std::max(nee_all, nee_max_one);
+		// NEE entries per vertex: estimateAllDirectLight's (+ the AO samples), or one light's
+		S.nee_k = (int)std::max(nee_all + (S.do_ao ? (uint32_t)S.ao_samples : 0u), nee_max_one);
 		if(S.integrator == INT_PATH && S.path_samples > 4095) { log.error("PathIntegrator: path_samples > 4095 unsupported"); return false; }
 		if(S.integrator == INT_PATH && 4 * S.bounces + 4 >= 50)
-			log.warning("PathIntegrator: bounces > 11 use Halton dimensions >= 50 (reference: racy FastRandom); those dimensions return 0 here");
+		{
+			// halton.cc:439: dimensions >= 50 draw from the racy global FastRandom (not reproducible)
+			log.error("PathIntegrator: bounces > 11 use Halton dimensions >= 50, which the reference draws from a racy "
+			          "global FastRandom; not supported by the GPU core");
+			return false;
+		}
 		// film (imagefilm.cc:129-173)
 		DevFilm &F = rp.film;
 		float filterw = static_cast<float>(s.aa_pixelwidth * 0.5);
@@ -1074,10 +1132,11 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		{
 			// nextPass compares neighbouring pixels across the whole film; the tile-row shards only
 			// hold their own rows
-			log.error("Scene: AA_passes > 1 with the film sharded over several GPUs is not supported; rendering the first pass only");
-			rp.aa.passes = 1;
+			log.error("Scene: AA_passes > 1 with the film sharded over several GPUs is not supported");
+			return false;
 		}
 		rp.aa.inc_samples = s.aa_inc_samples;
+		rp.aa.light_sample_multiplier_factor = s.aa_light_sample_multiplier_factor;
 		rp.aa.threshold = s.aa_threshold;
 		rp.aa.resampled_floor = s.aa_resampled_floor;
 		rp.aa.sample_multiplier_factor = s.aa_sample_multiplier_factor;
@@ -1160,6 +1219,13 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 					autosave_last = now;
 				}
 			};
+		if(progress && !quiet)
+		{
+			const int n_pix = s.width * s.height;
+			rp.on_chunk = [&, n_pix](uint64_t done, uint64_t total) {
+				progress(n_pix, (int)((double)n_pix * (double)done / (double)std::max<uint64_t>(1, total)), "Rendering...", progress_data);
+			};
+		}
 		if(!gpu()->render(rp, &canceled)) return false;
 		if(fmode != filmio::None) saveFilm();
 		const double build = stats.build_seconds;
@@ -1214,7 +1280,13 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 				}
 			}
 		if(cb.flush) cb.flush(view.first.c_str(), cb.flush_data);
-		if(progress) progress(s.width * s.height, s.width * s.height, "Rendering finished", progress_data);
+		if(progress)
+		{
+			// a canceled render reports the pixels it completed
+			const int done_pix = canceled ? (int)std::min<uint64_t>((uint64_t)s.width * s.height, stats.samples / (uint64_t)std::max(1, s.aa_samples))
+			                              : s.width * s.height;
+			progress(s.width * s.height, done_pix, canceled ? "Rendering canceled" : "Rendering finished", progress_data);
+		}
 	}
 	return true;
 }

@@ -65,6 +65,7 @@ enum : uint32_t
 	F_PEND_EMIT = 1u << 20,      // pending emission add
 	F_V0_DIFFUSE = 1u << 21,     // v0 had the Diffuse flag (NEE estimated there)
 	F_END_SUBPATH = 1u << 22,    // after the connect: the current subpath ends
+	F_AO_EMIT = 1u << 23,        // ambient occlusion at an emitting v0: pend_emit holds emit(wo)
 	F_LNUM_SHIFT = 24            // light picked by estimateOneDirectLight (8 bits)
 };
 
@@ -284,8 +285,10 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
 	// output is matched statistically — integrator_tiled.cc:272), seeded from the pixel-major sample
 	// id so that the image does not depend on how the film is split over GPUs or chunks
-	const uint32_t gid = ((uint32_t)sc.y * (uint32_t)S.width + (uint32_t)sc.x) * (uint32_t)S.spp + (uint32_t)sc.s;
-	const uint32_t seed = fnv32(gid ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)) + 123u;
+	// (64-bit id: W * H * spp passes 2^32 at 4K x 1024 spp; both halves are hashed)
+	const uint64_t gid = ((uint64_t)sc.y * (uint64_t)S.width + (uint64_t)sc.x) * (uint64_t)S.spp + (uint64_t)sc.s;
+	const uint32_t gid32 = (uint32_t)gid ^ fnv32((uint32_t)(gid >> 32));
+	const uint32_t seed = fnv32(gid32 ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)) + 123u;
 	P.pr[a] = make_uint4(offset, sample_idx, 30903u, seed);
 }
 
@@ -705,6 +708,7 @@ struct Surf
 	uint32_t flags;
 	C3 dcol;          // diffuse shader colour (read by EXT kernels only)
 	float drefl;      // diffuse_refl_shader scalar
+	float sigma;      // sigma_oren_shader scalar (Oren-Nayar with a texture sigma)
 };
 
 // Surface attributes computed by k_surface for the hit (texeval.h): shading normal + frame,
@@ -715,6 +719,7 @@ __device__ __forceinline__ void applyAttr(Surf &s, const float4 &a0, const float
 	coordsSystem(s.n, s.nu, s.nv);
 	s.drefl = a0.w;
 	s.dcol = C3{a1.x, a1.y, a1.z};
+	s.sigma = a1.w;
 }
 
 __device__ __forceinline__ Surf makeSurf(const DevScene &S, V3 o, V3 d, float t, int prim)
@@ -731,6 +736,7 @@ __device__ __forceinline__ Surf makeSurf(const DevScene &S, V3 o, V3 d, float t,
 	const DevMaterial &m = S.mats[s.mat];
 	s.dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};   // read only by EXT kernels
 	s.drefl = 1.f;
+	s.sigma = 0.f;
 	return s;
 }
 
@@ -763,6 +769,41 @@ __device__ __forceinline__ V3 reflectDir(V3 normal, V3 v)
 	return 2.f * vn * normal - v;
 }
 
+// material_shiny_diffuse.cc:154-188 ShinyDiffuseMaterial::orenNayar(wi, wo, n, use_texture_sigma,
+// texture_sigma): float arithmetic with the A / B members, or double arithmetic with a texture sigma
+__device__ float orenNayar(V3 wi, V3 wo, V3 n, const DevMaterial &m, const Surf &sp)
+{
+	const float cos_ti = fmaxf(-1.f, fminf(1.f, dot(n, wi)));
+	const float cos_to = fmaxf(-1.f, fminf(1.f, dot(n, wo)));
+	float maxcos_f = 0.f;
+	if(cos_ti < 0.9999f && cos_to < 0.9999f)
+	{
+		const V3 v_1 = normalize(wi - n * cos_ti);
+		const V3 v_2 = normalize(wo - n * cos_to);
+		maxcos_f = fmaxf(0.f, dot(v_1, v_2));
+	}
+	float sin_alpha, tan_beta;
+	if(cos_to >= cos_ti)
+	{
+		sin_alpha = sqrtf(1.f - cos_ti * cos_ti);
+		tan_beta = sqrtf(1.f - cos_to * cos_to) / ((cos_to == 0.f) ? 1e-8f : cos_to);
+	}
+	else
+	{
+		sin_alpha = sqrtf(1.f - cos_to * cos_to);
+		tan_beta = sqrtf(1.f - cos_ti * cos_ti) / ((cos_ti == 0.f) ? 1e-8f : cos_ti);
+	}
+	if(m.sigma_root >= 0)
+	{
+		const double texture_sigma = (double)sp.sigma;
+		const double sigma_squared = texture_sigma * texture_sigma;
+		const double a = 1.0 - 0.5 * (sigma_squared / (sigma_squared + 0.33));
+		const double b = 0.45 * sigma_squared / (sigma_squared + 0.09);
+		return fminf(1.f, fmaxf(0.f, (float)(a + b * (double)maxcos_f * (double)sin_alpha * (double)tan_beta)));
+	}
+	return fminf(1.f, fmaxf(0.f, m.on_a + m.on_b * maxcos_f * sin_alpha * tan_beta));
+}
+
 // material_shiny_diffuse.cc:190-238 (eval), material_simple.cc / material_glass.cc (black)
 template<bool EXT = false>
 __device__ C3 matEval(const DevMaterial &m, const Surf &sp, V3 wo, V3 wl, uint32_t bsdfs)
@@ -786,6 +827,7 @@ __device__ C3 matEval(const DevMaterial &m, const Surf &sp, V3 wo, V3 wl, uint32
 	if(transmit && (m.sd_flags & SD_TRANSLUCENT)) return m.comp[2] * m_t * dcol;
 	if((double)dot(n, wl) < 0.0 && !m.flat) return c3(0.f);
 	float m_d = m_t * (1.f - m.comp[2]) * m.comp[3];
+	if(m.sd_flags & SD_OREN_NAYAR) m_d *= orenNayar(wo, wl, n, m, sp);   // :228-233
 	if(m.drefl_root >= 0) m_d *= sp.drefl;   // :235
 	return m_d * dcol;
 }
@@ -906,6 +948,7 @@ __device__ C3 matSample(const DevMaterial &m, const Surf &sp, V3 wo, V3 &wi, Bsd
 	{
 		wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
 		if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * dcol;
+		if(EXT && (m.sd_flags & SD_OREN_NAYAR)) scolor = scolor * orenNayar(wo, wi, n, m, sp);   // :320-325
 		s.pdf = fabsf(dot(wi, n)) * width[pick];
 	}
 	s.sampled = ch;
@@ -1100,15 +1143,23 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 	const uint32_t offs = (uint32_t)num_samples * sample_idx + offset + l_offs;
 	const V3 corner = lv(L.pos), to_x = lv(L.to_x), to_y = lv(L.to_y), fn = lv(L.fnormal);
 	const C3 lcolor = C3{L.color[0], L.color[1], L.color[2]};
+	// areaLightSampleLight (montecarlo.cc:156-282) and areaLightSampleMaterial (:284-383) draw the
+	// same Halton(2/3) sequences from setStart(offs - 1) (:399-403): computed once for both
+	HaltonInc<2> hal_2;
+	HaltonInc<3> hal_3;
+	hal_2.value = hal_3.value = 0.0;
+	if(active)
+	{
+		hal_2.start(offs - 1u);
+		hal_3.start(offs - 1u);
+	}
 	for(int i = 0; i < num_samples; ++i)
 	{
-		// areaLightSampleLight (montecarlo.cc:156-282) and areaLightSampleMaterial (:284-383) draw
-		// the same Halton(2/3, offs - 1 + i) pair: computed once for both.
 		float s_1 = 0.f, s_2 = 0.f;
 		if(active)
 		{
-			s_1 = haltonFirst(2u, 0.5, offs - 1u + (uint32_t)i);
-			s_2 = haltonFirst(3u, 1.0 / 3.0, offs - 1u + (uint32_t)i);
+			s_1 = hal_2.next();
+			s_2 = hal_3.next();
 		}
 		bool ok = active;
 		C3 contrib = c3(0.f);
@@ -1211,6 +1262,69 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 		}
 		emitShadow(ok && cast_shadows, so, dir, st, b_tmin, e0 + num_samples + i, out);
 	}
+}
+
+// TiledIntegrator::sampleAmbientOcclusion (integrator_tiled.cc:644-691; clay = false, one ray
+// division): one entry per AO sample after the lights' entries — (ao_col * surf_col * cos * w, pdf)
+// — and its shadow ray (tmin = shadow bias, tmax = AO_distance).  The material sample keeps the
+// previous direction when it draws none (light_ray.dir_ persists, :647); such samples weigh 0.
+template<bool EXT>
+__device__ void aoSamples(const DevScene &S, const DevMaterial &m, const Surf &sp, V3 wo, uint32_t sample_idx, uint32_t offset,
+                          bool active, int e0, float4 *nee, uint8_t *occ, const ShadeOut &out, float4 *ts)
+{
+	const int n = S.ao_samples;
+	const uint32_t offs = (uint32_t)n * sample_idx + offset;
+	HaltonInc<2> hal_2;
+	HaltonInc<3> hal_3;
+	hal_2.value = hal_3.value = 0.0;
+	if(active)
+	{
+		hal_2.start(offs - 1u);
+		hal_3.start(offs - 1u);
+	}
+	const float sh_tmin = S.shadow_bias_auto ? S.shadow_bias * fmaxf(1.f, length(sp.p)) : S.shadow_bias;
+	const C3 ao_col = C3{S.ao_col[0], S.ao_col[1], S.ao_col[2]};
+	V3 dir = v3(0.f, 0.f, 0.f);
+	for(int i = 0; i < n; ++i)
+	{
+		bool want = false;
+		V3 so = sp.p;
+		float st = 0.f;
+		if(active)
+		{
+			BsdfSample s;
+			s.s_1 = hal_2.next();
+			s.s_2 = hal_3.next();
+			s.flags = B_GLOSSY | B_DIFFUSE | B_REFLECT;
+			s.pdf = 0.f;
+			s.sampled = B_NONE;
+			float w = 0.f;
+			const C3 surf_col = matSample<EXT>(m, sp, wo, dir, s, w);
+			const float cos = fabsf(dot(sp.n, dir));
+			const C3 contrib = ao_col * surf_col * cos * w;
+			// a zero contribution does not depend on the occlusion: no ray
+			want = !(contrib.r == 0.f && contrib.g == 0.f && contrib.b == 0.f);
+			shadowRayOf(sp.p, dir, sh_tmin, S.ao_dist, so, st);
+			if(ts && want) tsFactors(ts, e0 + i, surf_col, cos, ao_col, w, 1.f, false);
+			nee[e0 + i] = f4(contrib, s.pdf);
+			occ[e0 + i] = 0;
+		}
+		emitShadow(want, so, dir, st, sh_tmin, e0 + i, out);
+	}
+}
+
+// AO result of a vertex: sum in sample order of emit * pdf (emitting materials) and the unoccluded
+// contributions, divided by the sample count (integrator_tiled.cc:672-690)
+__device__ C3 aoSum(const DevScene &S, const float4 *nee, const uint8_t *occ, int k0, bool emitting, C3 emit)
+{
+	C3 col = c3(0.f);
+	for(int i = 0; i < S.ao_samples; ++i)
+	{
+		const float4 e = nee[k0 + i];
+		if(emitting) col = col + emit * e.w;
+		if(!occ[k0 + i]) col = col + rgb(e);
+	}
+	return col / (float)S.ao_samples;
 }
 
 // Sum of one light's entries with the reference's addition order (montecarlo.cc:385-408).
@@ -1332,6 +1446,7 @@ __device__ __forceinline__ Surf surfFromPrim(const DevScene &S, V3 p, int prim)
 	const DevMaterial &m = S.mats[s.mat];
 	s.dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
 	s.drefl = 1.f;
+	s.sigma = 0.f;
 	return s;
 }
 
@@ -1339,11 +1454,16 @@ __device__ __forceinline__ Surf surfFromPrim(const DevScene &S, V3 p, int prim)
 // node `node` hit at ray level S.cur_level: the specular reflect / refract children of ray level
 // cur_level + 1 are appended to the spawn list (traced by the next pass) and linked to the node;
 // k_combine later adds their totals times the specular colours, reflect first.
-__device__ void spawnSpecular(const DevScene &S, const DevMaterial &m, const Surf &sp, V3 wo, uint32_t node, uint2 pix, uint2 rng)
+// additional_depth: the value integrate() received (max over the ancestors' materials, carried in the
+// spawned ray's tmax as -1 - depth); the node's own material raises it (direct_light.cc:107,
+// path_tracer.cc:133) and the children inherit it.
+__device__ void spawnSpecular(const DevScene &S, const DevMaterial &m, const Surf &sp, V3 wo, uint32_t node, uint2 pix, uint2 rng,
+                              int additional_depth)
 {
 	int2 child = make_int2(-1, -1);
 	const int level = S.cur_level + 1;
-	if((sp.flags & (B_SPECULAR | B_FILTER)) && level <= S.raydepth && level < 20)
+	additional_depth = max(additional_depth, m.add_depth);
+	if((sp.flags & (B_SPECULAR | B_FILTER)) && level <= S.raydepth + additional_depth && level < 20)
 	{
 		const SpecOut so = matSpecular(m, sp, wo);
 		for(int k = 0; k < 2; ++k)
@@ -1362,7 +1482,7 @@ __device__ void spawnSpecular(const DevScene &S, const DevMaterial &m, const Sur
 				from = sp.p + dir * f;
 			}
 			S.spawn_o[idx] = f4(from, S.ray_min_dist);
-			S.spawn_d[idx] = f4(dir, -1.f);
+			S.spawn_d[idx] = f4(dir, -1.f - (float)additional_depth);   // tmax < 0: unbounded ray
 			// the child's own Russian-roulette stream (statistical parity, as the camera's)
 			S.spawn_pr[idx] = make_uint4(pix.x, pix.y, rng.x ^ (0x9e3779b9u * (uint32_t)(2 * level + k + 1)), rng.y + 1u + (uint32_t)k);
 			S.node_w[S.node_base + idx] = f4(k == 0 ? so.rcol : so.tcol, 0.f);
@@ -1433,7 +1553,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			// only the first segment of a subpath reads the previous wo (path_tracer.cc:193-197)
 			if((stage & 0xffu) == ST_FIRST) pwo4 = Pc.pwo[i];
 			if(flags & F_PEND_ONE) pthr4 = Pc.pend_thr[i];
-			if(flags & F_PEND_EMIT) pem4 = Pc.pend_emit[i];
+			if(flags & (F_PEND_EMIT | F_AO_EMIT)) pem4 = Pc.pend_emit[i];
 		}
 		C3 thr = rgb(thr4), col = rgb(col4), pcol = rgb(pcol4);
 		const float alpha = 1.f;   // live entries are opaque (transparent background is written at ST_CAMERA)
@@ -1451,6 +1571,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			C3 total = c3(0.f);
 			for(int l = 0; l < S.n_lights; ++l) total = total + neeSum(S, S.lights[l], Pc.nee, Pc.occ, (int)i * K + (int)S.lights[l].nee_base);
 			col = col + total;
+			// DirectLight: col += sampleAmbientOcclusion (integrator_direct_light.cc:124)
+			if(S.do_ao) col = col + aoSum(S, Pc.nee, Pc.occ, (int)i * K + S.nee_all_count, (flags & F_AO_EMIT) != 0, rgb(pem4));
 		}
 		if(live && (flags & F_PEND_ONE))
 		{
@@ -1460,23 +1582,25 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			if(flags & F_PEND_EMIT) lcol = lcol + rgb(pem4);
 			pcol = pcol + lcol * rgb(pthr4);
 		}
-		flags &= ~(F_PEND_V0 | F_PEND_ONE | F_PEND_EMIT);
+		flags &= ~(F_PEND_V0 | F_PEND_ONE | F_PEND_EMIT | F_AO_EMIT);
 
 		PHASE(1);
 		// ---- 2. the new hit ----
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
-		sp.dcol = c3(0.f); sp.drefl = 1.f;
+		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
 		float4 sa0 = make_float4(0.f, 0.f, 0.f, 0.f), sa1 = sa0;
 		V3 wo = v3(0.f, 0.f, 1.f);
 		bool have_hit = false;
 		int hit_prim = -1;
+		int add_depth_in = 0;   // additional_depth of a spawned specular node (spawnSpecular)
 		if(live && st != ST_NORAY)
 		{
 			hit_prim = A.Q.hit_prim[i];
 			if(hit_prim >= 0)
 			{
 				const float4 ro = A.Q.ray_o[i], rd = A.Q.ray_d[i];
+				if(EXT && S.cur_level > 0) add_depth_in = (int)(-rd.w) - 1;
 				have_hit = true;
 				sp = makeSurf(S, xyz(ro), xyz(rd), A.Q.hit_t[i], hit_prim);
 				if(ATTR)
@@ -1513,13 +1637,18 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				else
 				{
 					const DevMaterial &m = S.mats[sp.mat];
-					if(EXT && S.tree) spawnSpecular(S, m, sp, wo, sid, make_uint2(offset, sample_idx), rng);
+					if(EXT && S.tree) spawnSpecular(S, m, sp, wo, sid, make_uint2(offset, sample_idx), rng, add_depth_in);
 					col = c3(0.f);
 					// photon_mapping.cc:868-869 adds emit(wo) unconditionally and :938-946 adds it again
 					// for emitting materials; the other integrators add it once (direct_light.cc:120)
 					if(is_photon) col = col + matEmit<EXT>(m, sp, wo);
 					if(sp.flags & B_EMIT) col = col + matEmit<EXT>(m, sp, wo);
 					if(sp.flags & B_DIFFUSE) { nee_v0 = true; flags |= F_V0_DIFFUSE; }
+					if(S.do_ao && (sp.flags & B_DIFFUSE) && (sp.flags & B_EMIT))
+					{
+						emit_pend = matEmit<EXT>(m, sp, wo);   // sampleAmbientOcclusion adds sp.emit(wo) * pdf per sample
+						flags |= F_AO_EMIT;
+					}
 					if(is_photon)
 					{
 						v0p4 = f4(sp.p, __int_as_float(hit_prim));
@@ -1713,7 +1842,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			Pn.pcol[k] = f4(pcol, __uint_as_float(flags));
 			if((stage & 0xffu) == ST_FIRST) Pn.pwo[k] = f4(pwo, 0.f);
 			if(nee_one) Pn.pend_thr[k] = f4(pend_thr, 0.f);
-			if(flags & F_PEND_EMIT) Pn.pend_emit[k] = f4(emit_pend, 0.f);
+			if(flags & (F_PEND_EMIT | F_AO_EMIT)) Pn.pend_emit[k] = f4(emit_pend, 0.f);
 			if(keep_v0) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }
 			if(ATTR && keep_v0) { Pn.v0attr[2 * (size_t)k] = v0a0; Pn.v0attr[2 * (size_t)k + 1] = v0a1; }
 		}
@@ -1733,7 +1862,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			if(ATTR)
 			{
 				A.N.attr[2 * (size_t)j] = f4(sp.n, sp.drefl);
-				A.N.attr[2 * (size_t)j + 1] = f4(sp.dcol, 0.f);
+				A.N.attr[2 * (size_t)j + 1] = f4(sp.dcol, sp.sigma);
 			}
 		}
 		else if(want_gather)
@@ -1855,10 +1984,10 @@ __global__ void __launch_bounds__(kShadeBlock) k_surface(DevScene S, DevQueues Q
 		const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, o, d, p);
 		const DevMaterial &m = S.mats[__float_as_int(S.prim_ng[prim].w)];
 		C3 dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
-		float drefl = 1.f;
-		if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl);
+		float drefl = 1.f, sigma = 0.f;
+		if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl, sigma);
 		Q.sattr[2 * (size_t)i] = f4(sa.n, drefl);
-		Q.sattr[2 * (size_t)i + 1] = f4(dcol, 0.f);
+		Q.sattr[2 * (size_t)i + 1] = f4(dcol, sigma);
 	}
 }
 
@@ -1908,8 +2037,8 @@ __global__ void __launch_bounds__(kShadeBlock) k_tshadow(DevScene S, DevQueues Q
 			{
 				const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, o, d, p);
 				nrm = sa.n;
-				float drefl = 1.f;
-				if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl);
+				float drefl = 1.f, sigma = 0.f;
+				if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl, sigma);
 			}
 			const V3 nf = faceForward(ng, nrm, d);
 			const float kr = fresnelKr(m, d, nf);
@@ -1974,7 +2103,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 		}
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
-		sp.dcol = c3(0.f); sp.drefl = 1.f;
+		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
 		if(live) sp = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
 		if(ATTR && live) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
 		const V3 wo = xyz(wk);
@@ -1988,6 +2117,9 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 			for(int l = 0; l < S.n_lights; ++l)
 				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
 				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out, S.tr_shad ? A.Pn.ts : nullptr);
+			if(S.do_ao)
+				aoSamples<EXT>(S, S.mats[sp.mat], sp, wo, pm.y, pm.x, all, e0 + S.nee_all_count, A.Pn.nee, A.Pn.occ, out,
+				               S.tr_shad ? A.Pn.ts : nullptr);
 		}
 		if(__any(one))
 		{
@@ -2116,6 +2248,24 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 		out[p] = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
 	}
 	else out[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Canceled render (integrator_tiled.cc:292: a canceled worker stops before its next pixel, so a
+// pixel is either fully sampled or not at all): flags the pixels whose samples the completed
+// chunks rendered, for k_film's `flags` argument.  Pass 0 enumerates the jobs (pixel ranks
+// [0, n_pix)); an adaptive pass (plist) clears the flags of its pixels beyond `done_pix`.
+__global__ void __launch_bounds__(256) k_done_flags(DevScene S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix,
+                                                    uint8_t *flags)
+{
+	const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+	if(p >= n_pix) return;
+	if(S.plist)
+	{
+		if(p >= done_pix) flags[S.plist[p]] = 0;
+		return;
+	}
+	const SampleCoord c = sampleCoord(jobs, n_jobs, S.width, S.tile, S.spp, (uint64_t)p * (uint64_t)S.spp);
+	flags[(size_t)c.y * S.width + c.x] = p < done_pix ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2310,9 +2460,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 					const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, xyz(ro), xyz(rd), sp.p);
 					const DevMaterial &m = S.mats[sp.mat];
 					C3 dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
-					float drefl = 1.f;
-					if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl);
-					applyAttr(sp, f4(sa.n, drefl), f4(dcol, 0.f));
+					float drefl = 1.f, sigma = 0.f;
+					if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl, sigma);
+					applyAttr(sp, f4(sa.n, drefl), f4(dcol, sigma));
 				}
 				const V3 wi = -xyz(rd);
 				const C3 lcol = rgb(pc);
@@ -2820,6 +2970,14 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const D
 }
 
 size_t yafamd_gather_lds_bytes(const DevScene *S) { return gatherLdsBytes(*S, S->small_tables != 0); }
+
+hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix, uint8_t *flags,
+                                    hipStream_t st)
+{
+	if(n_pix == 0) return hipSuccess;
+	hipLaunchKernelGGL(k_done_flags, dim3((n_pix + 255) / 256), dim3(256), 0, st, *S, jobs, n_jobs, n_pix, done_pix, flags);
+	return hipGetLastError();
+}
 
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, const uint8_t *flags, float4 *accum, float4 *out,
                               float *weights, int y0, int y1, float clamp_samples, int accumulate, hipStream_t st)

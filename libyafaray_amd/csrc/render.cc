@@ -46,6 +46,8 @@ size_t yafamd_gather_lds_bytes(const DevScene *S);
 hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
                                 int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st);
 hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint2 *nodes_dev, int *depth_out, hipStream_t st);
+hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix, uint8_t *flags,
+                                    hipStream_t st);
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, const uint8_t *flags, float4 *accum, float4 *out,
                               float *weights, int y0, int y1, float clamp_samples, int accumulate, hipStream_t st);
 hipError_t yafamd_aa_next_pass(const float4 *accum, const float *weights, int W, int H, int tile, const DevAaParams *prm,
@@ -113,6 +115,8 @@ struct GpuRenderer::Impl
 	int n_ph_lights = 0;
 	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
 	Buf ph_pos, ph_dir, ph_colb, pk_nodes;
+	std::vector<DevLight> host_lights;   // as uploaded (light sample multiplier passes rewrite the device copy)
+	std::vector<DevLight> pass_lights;   // staging of the current pass's copy (alive until the stream syncs)
 	int n_photons = 0, pm_paths = 0, pm_stack = 0;
 	int n_nodes = 0, n_tris = 0, n_mats = 0, n_lights = 0, depth = 0, stack_depth = 32, node_f4 = 4;
 	int lds_stack = 32;    // k_trace stack levels held in LDS; levels [lds_stack, stack_depth) spill to `spill`
@@ -255,6 +259,7 @@ bool GpuRenderer::upload(HostScene &hs)
 	if(!allocCopy(log_, d.prim_ng, hs.prim_ng.data(), hs.prim_ng.size())) return false;
 	if(!allocCopy(log_, d.mats, hs.mats.data(), hs.mats.size())) return false;
 	if(!allocCopy(log_, d.lights, hs.lights.data(), hs.lights.size())) return false;
+	d.host_lights = hs.lights;
 	d.has_attr = hs.has_attr;
 	d.n_textures = (int)hs.textures.size();
 	if(hs.has_attr)
@@ -578,7 +583,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		// the recursion tree of a chunk holds up to 2^(raydepth + 1) - 2 spawned nodes per sample
 		// (88 B each): cap the level-0 chunk at 2 M samples and the spawn records at 64 per sample
 		M = std::min<size_t>(M, (size_t)1 << 21);
-		const int depth = std::max(0, std::min(S.raydepth, 5));
+		const int depth = std::max(0, std::min(S.raydepth + S.max_add_depth, 5));
 		const size_t per = std::max<size_t>(2, ((size_t)1 << (depth + 1)) - 2);
 		const size_t cap = M * per;
 		if(!ensure(log_, d.spawn_o, cap * 16) || !ensure(log_, d.spawn_d, cap * 16) || !ensure(log_, d.spawn_pr, cap * 16) ||
@@ -596,6 +601,38 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		S.spawn_count = (uint32_t *)d.spawn_count.p;
 	}
 	S.cur_level = 0;
+	// AA_light_sample_multiplier_factor: pass p draws ceilf(samples * factor^p) samples per area light
+	// (integrator_montecarlo.cc:396), so the NEE layout changes per pass; size it for the largest
+	const bool light_mult = rp.aa.passes > 1 && rp.aa.light_sample_multiplier_factor != 1.f;
+	auto lightLayout = [&](float mult, std::vector<DevLight> &ls) -> int {
+		ls = d.host_lights;
+		uint32_t base = 0, max_one = 1;
+		for(DevLight &L : ls)
+		{
+			if(L.type == LIGHT_AREA)
+			{
+				L.samples = (int)ceilf((float)L.samples * mult);
+				L.inv_samples = 1.f / (float)L.samples;
+				L.nee_count = 2u * (uint32_t)std::max(0, L.samples);
+			}
+			L.nee_base = base;
+			base += L.nee_count;
+			max_one = std::max(max_one, L.nee_count);
+		}
+		S.nee_all_count = (int)base;
+		return (int)std::max(base + (S.do_ao ? (uint32_t)S.ao_samples : 0u), max_one);
+	};
+	if(light_mult)
+	{
+		float mult = 1.f;
+		std::vector<DevLight> tmp;
+		for(int p = 1; p < rp.aa.passes; ++p)
+		{
+			mult *= rp.aa.light_sample_multiplier_factor;
+			S.nee_k = std::max(S.nee_k, lightLayout(mult, tmp));
+		}
+		lightLayout(1.f, tmp);
+	}
 	const int K = std::max(1, S.nee_k);
 	const bool need_v0 = S.path_samples > 1 || S.integrator == INT_PHOTON;
 	// segment capacity: the camera deals groups of 256 samples round-robin over the segments
@@ -734,13 +771,22 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		return true;
 	};
 	bool tree_overflow_logged = false;
-	// one pass: `n_total` camera samples (the jobs' enumeration, or S.plist x S.spp) through the wavefront
+	// one pass: `n_total` camera samples (the jobs' enumeration, or S.plist x S.spp) through the wavefront;
+	// `done` = samples of the chunks that ran (< n_total only when the render was canceled)
+	uint64_t done = 0;
 	auto runSamples = [&](uint64_t n_total) -> bool {
+	done = 0;
 	if(rp.profile && !ensureEvents(ev_i + 4 * (size_t)((n_total + M - 1) / M) * (size_t)iters)) return false;
-	for(uint64_t base = 0; base < n_total; base += M)
+	for(uint64_t base = 0; base < n_total; base += M, done = std::min(base, n_total))
 	{
 		if(canceled && *canceled) break;
 		const int n = (int)std::min<uint64_t>(M, n_total - base);
+		if(rp.on_chunk && base > 0)
+		{
+			HIPCHECK(hipStreamSynchronize(d.stream));
+			rp.on_chunk(base, n_total);
+			if(canceled && *canceled) break;
+		}
 		if(S.tree) HIPCHECK(hipMemsetAsync(d.spawn_count.p, 0, 16, d.stream));
 		S.cur_level = 0;
 		HIPCHECK(yafamd_launch_camera(&S, &d.P[0], &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
@@ -802,16 +848,29 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	else
 	{
 		if(!runSamples(total)) return false;
+		const uint8_t *done_flags = nullptr;
+		if(done < total)
+		{
+			// canceled: only the pixels of the completed chunks splat (the others were never rendered)
+			if(!ensure(log_, d.aa_flags, (size_t)W * H)) return false;
+			HIPCHECK(hipMemsetAsync(d.aa_flags.p, 0, (size_t)W * H, d.stream));
+			HIPCHECK(yafamd_launch_done_flags(&S, (const DevJob *)d.jobs.p, n_jobs, (uint32_t)(total / (uint64_t)spp), (uint32_t)(done / (uint64_t)spp),
+			                                  (uint8_t *)d.aa_flags.p, d.stream));
+			done_flags = (const uint8_t *)d.aa_flags.p;
+			samples_total = done / (uint64_t)spp * (uint64_t)spp;
+		}
 		for(const auto &r : owned_rows_)
-			HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, nullptr, (float4 *)d.accum.p, (float4 *)d.film.p,
+			HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, done_flags, (float4 *)d.accum.p, (float4 *)d.film.p,
 			                            (float *)d.weights.p, r.first, r.second, S.clamp_samples, 0, d.stream));
+		// renderPass sets the sampling offset before its workers start (integrator_tiled.cc:244), so a
+		// canceled pass advances it too
 		sampling_offset_ = (uint32_t)spp;
 	}
 	passes_done_ = 1;
 	if(passes > 1)
 	{
 		if(!ensure(log_, d.aa_flags, (size_t)W * H) || !ensure(log_, d.aa_plist, (size_t)W * H * 4)) return false;
-		float threshold = rp.aa.threshold, sample_multiplier = 1.f;
+		float threshold = rp.aa.threshold, sample_multiplier = 1.f, light_multiplier = 1.f;
 		bool threshold_changed = true;
 		int acum = spp, resampled = 0;
 		const int floor_pixels = (int)floorf(rp.aa.resampled_floor * (float)(W * H) / 100.f);
@@ -819,6 +878,14 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		{
 			if(canceled && *canceled) break;
 			sample_multiplier *= rp.aa.sample_multiplier_factor;
+			light_multiplier *= rp.aa.light_sample_multiplier_factor;
+			if(light_mult)
+			{
+				HIPCHECK(hipStreamSynchronize(d.stream));   // the previous pass's staging copy is consumed
+				lightLayout(light_multiplier, d.pass_lights);
+				HIPCHECK(hipMemcpyAsync(d.lights.p, d.pass_lights.data(), d.pass_lights.size() * sizeof(DevLight), hipMemcpyHostToDevice,
+				                        d.stream));
+			}
 			const bool skip = resampled <= 0.f && !threshold_changed;
 			if(rp.on_next_pass)
 			{
@@ -861,11 +928,15 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				rp.film.sample_offset = S.base_offset + (uint32_t)acum;
 				const uint64_t n_total = (uint64_t)resampled * (uint64_t)n_pass;
 				if(!runSamples(n_total)) return false;
+				if(done < n_total)
+					HIPCHECK(yafamd_launch_done_flags(&S, (const DevJob *)d.jobs.p, n_jobs, (uint32_t)resampled, (uint32_t)(done / (uint64_t)n_pass),
+					                                  (uint8_t *)d.aa_flags.p, d.stream));
 				HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (const uint8_t *)d.aa_flags.p, (float4 *)d.accum.p,
 				                            (float4 *)d.film.p, (float *)d.weights.p, 0, H, S.clamp_samples, 1, d.stream));
-				samples_total += n_total;
+				samples_total += done / (uint64_t)n_pass * (uint64_t)n_pass;
+				sampling_offset_ = (uint32_t)(acum + n_pass);   // renderPass: setSamplingOffset(offset + samples), :244
+				if(done < n_total) break;   // canceled mid-pass
 				++passes_done_;
-				sampling_offset_ = (uint32_t)(acum + n_pass);   // renderPass: setSamplingOffset(offset + samples)
 			}
 			acum += n_pass;
 			if(resampled < floor_pixels)
@@ -879,6 +950,12 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		S.pass_offset = 0;
 		S.plist = nullptr;
 		rp.film.spp = spp;
+		if(light_mult)
+		{
+			HIPCHECK(hipStreamSynchronize(d.stream));
+			lightLayout(1.f, d.pass_lights);
+			HIPCHECK(hipMemcpy(d.lights.p, d.pass_lights.data(), d.pass_lights.size() * sizeof(DevLight), hipMemcpyHostToDevice));
+		}
 	}
 	HIPCHECK(hipEventRecord(d.ev_pool[1], d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));

@@ -54,6 +54,7 @@ struct AaParams
 {
 	int passes = 1;
 	int inc_samples = 1;               // AA_inc_samples (defaults to AA_minsamples)
+	float light_sample_multiplier_factor = 1.f;   // AA_light_sample_multiplier_factor (integrator_tiled.cc:190)
 	float threshold = 0.05f;
 	float resampled_floor = 0.f;       // % of the pixels
 	float sample_multiplier_factor = 1.f;
@@ -80,6 +81,9 @@ struct RenderParams
 	// ImageFilm::nextPass hook (imagefilm.cc:259-287), called before every adaptive pass with
 	// skipped = the pass's nextPass was skipped; the film autosave lives there
 	std::function<void(bool skipped)> on_next_pass;
+	// progress hook after every completed chunk (the reference's per-tile progress updates,
+	// integrator_tiled.cc:258-262): samples done / samples of the pass.  Set -> one stream sync per chunk.
+	std::function<void(uint64_t done, uint64_t total)> on_chunk;
 };
 
 class GpuRenderer

@@ -532,7 +532,7 @@ YD float blendValue(float tex, float out, float fact, float facg, int mode)
 // Evaluates the material's node program at the surface point; returns the diffuse shader colour
 // (Rgb of its getColor) and the diffuse_refl_shader scalar (1 when absent).
 YD void evalNodes(const DevMaterial &m, const DevNode *nodes, const DevTexture *texs, const float4 *px,
-                  const SurfAttr &sa, C3 &dcol, float &drefl)
+                  const SurfAttr &sa, C3 &dcol, float &drefl, float &sigma)
 {
 	C4 rc[kMaxNodes];
 	float rv[kMaxNodes];
@@ -692,6 +692,7 @@ YD void evalNodes(const DevMaterial &m, const DevNode *nodes, const DevTexture *
 	if(m.diffuse_root >= 0) { const C4 c = rc[m.diffuse_root]; dcol = C3{c.r, c.g, c.b}; }
 	else dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
 	drefl = m.drefl_root >= 0 ? rv[m.drefl_root] : 1.f;
+	sigma = m.sigma_root >= 0 ? rv[m.sigma_root] : 0.f;   // getShaderScalar(sigma_oren_shader_, ..., 0.f)
 }
 
 // primitive_triangle.cc:44-71 barycentrics of the (already found) hit + getSurface :97-176

@@ -685,10 +685,10 @@ int blendFromName(const std::string &s, bool layer)
 
 bool buildNodeProgram(Logger &log, const std::map<std::string, int> &texture_index, const std::vector<HostTexture> &textures,
                       const std::string &mat, const ParamMap &mp, const std::list<ParamMap> &nodes, std::vector<DevNode> &prog,
-                      int &diffuse_root, int &drefl_root)
+                      int &diffuse_root, int &drefl_root, int &sigma_root)
 {
 	prog.clear();
-	diffuse_root = drefl_root = -1;
+	diffuse_root = drefl_root = sigma_root = -1;
 	// ---- loadNodes (material_node.cc:102-169) ----
 	std::map<std::string, NodeDesc> table;
 	bool error = false;
@@ -900,9 +900,10 @@ bool buildNodeProgram(Logger &log, const std::map<std::string, int> &texture_ind
 		else log.warning(std::string("Shader node ") + roots[r] + " '" + name + "' does not exist!");
 	}
 	for(int r = 0; r < 10; ++r)
-		if(!root_node[r].empty() && r != 0 && r != 7)
+		if(!root_node[r].empty() && r != 0 && r != 6 && r != 7)
 		{
-			log.error("Material '" + mat + "': shader node root '" + roots[r] + "' is not evaluated by the GPU core (diffuse_shader / diffuse_refl_shader only)");
+			log.error("Material '" + mat + "': shader node root '" + roots[r] +
+			          "' is not evaluated by the GPU core (diffuse_shader / sigma_oren_shader / diffuse_refl_shader only)");
 			return false;
 		}
 	// ---- the nodes the roots depend on, dependencies first (solveNodesOrder :60-100) ----
@@ -920,7 +921,7 @@ bool buildNodeProgram(Logger &log, const std::map<std::string, int> &texture_ind
 		order.push_back(n);
 		return true;
 	};
-	for(int r : {0, 7})
+	for(int r : {0, 6, 7})
 		if(!root_node[r].empty() && !place(root_node[r])) return false;
 	if((int)order.size() > kMaxNodes) { log.error("Material '" + mat + "': more than " + std::to_string(kMaxNodes) + " shader nodes"); return false; }
 	for(const std::string &n : order)
@@ -937,6 +938,7 @@ bool buildNodeProgram(Logger &log, const std::map<std::string, int> &texture_ind
 	}
 	if(!root_node[0].empty()) diffuse_root = placed[root_node[0]];
 	if(!root_node[7].empty()) drefl_root = placed[root_node[7]];
+	if(!root_node[6].empty()) sigma_root = placed[root_node[6]];
 	return true;
 }
 

@@ -60,6 +60,6 @@ bool createTexture(Logger &log, const std::map<std::string, std::shared_ptr<Host
 // unsupported coordinates, mipmap interpolation on uv coordinates).
 bool buildNodeProgram(Logger &log, const std::map<std::string, int> &texture_index, const std::vector<HostTexture> &textures,
                       const std::string &mat, const ParamMap &mp, const std::list<ParamMap> &nodes, std::vector<DevNode> &prog,
-                      int &diffuse_root, int &drefl_root);
+                      int &diffuse_root, int &drefl_root, int &sigma_root);
 
 } // namespace yafamd

@@ -46,6 +46,9 @@ class Material:
     transparentbias_factor: float = 0.0
     transparentbias_multiply_raydepth: bool = False
     reflect: float = 1.0                   # type "mirror": colour * reflect
+    diffuse_brdf: str = "lambert"          # "oren_nayar" (material_shiny_diffuse.cc:561-571)
+    sigma: float = 0.1                     # Oren-Nayar roughness
+    additionaldepth: int = 0               # extra recursiveRaytrace depth (integrator_montecarlo.cc:923)
     # full typed parameter map {key: (kind, value)} (kinds s f i b v c m) and the pushed shader-node
     # lists, as a reference client passes them (tests/test01/test01.c:268-650); when set, apply()
     # issues exactly these instead of the fields above
@@ -158,6 +161,12 @@ class Render:
     pm_caustics: bool = False
     pm_caustic_photons: int = 500000
     threads_photons: int = 1
+    # DirectLight ambient occlusion (integrator_direct_light.cc:161-186)
+    do_ao: bool = False
+    ao_samples: int = 32
+    ao_distance: float = 1.0
+    ao_color: tuple = (1.0, 1.0, 1.0)
+    aa_light_sample_multiplier_factor: float = 1.0
 
 
 @dataclass
@@ -441,6 +450,11 @@ def apply(spec: SceneSpec, api) -> None:
             api.paramsSetFloat("emit", m.emit)
             api.paramsSetBool("receive_shadows", m.receive_shadows)
             api.paramsSetBool("flat_material", m.flat_material)
+            if m.diffuse_brdf != "lambert":
+                api.paramsSetString("diffuse_brdf", m.diffuse_brdf)
+                api.paramsSetFloat("sigma", m.sigma)
+            if m.additionaldepth:
+                api.paramsSetInt("additionaldepth", m.additionaldepth)
         api.createMaterial(m.name)
     api.paramsClearAll()
     for l in spec.lights:
@@ -555,6 +569,13 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetInt("bounces", r.pm_bounces)
         api.paramsSetBool("caustics", r.pm_caustics)
         api.paramsSetBool("finalGather", False)
+    if r.integrator == "directlighting" and r.pm_caustics:
+        api.paramsSetBool("caustics", True)
+    if r.integrator == "directlighting" and r.do_ao:
+        api.paramsSetBool("do_AO", True)
+        api.paramsSetInt("AO_samples", r.ao_samples)
+        api.paramsSetFloat("AO_distance", r.ao_distance)
+        api.paramsSetColor("AO_color", *r.ao_color, 1.0)
     api.createIntegrator("default")
     api.paramsClearAll()
     api.paramsSetString("type", "combined")
@@ -573,6 +594,7 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetFloat("AA_threshold", r.aa_threshold)
     api.paramsSetFloat("AA_resampled_floor", r.aa_resampled_floor)
     api.paramsSetFloat("AA_sample_multiplier_factor", r.aa_sample_multiplier_factor)
+    api.paramsSetFloat("AA_light_sample_multiplier_factor", r.aa_light_sample_multiplier_factor)
     api.paramsSetBool("AA_detect_color_noise", r.aa_detect_color_noise)
     api.paramsSetString("AA_dark_detection_type", r.aa_dark_detection_type)
     api.paramsSetFloat("AA_dark_threshold_factor", r.aa_dark_threshold_factor)

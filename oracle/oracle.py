@@ -28,7 +28,8 @@ class yc_material(C.Structure):
                 ("flat_material", C.c_int), ("diffuse_shader", C.c_int), ("diffuse_refl_shader", C.c_int),
                 ("specular_reflect", C.c_float), ("transparency", C.c_float), ("translucency", C.c_float),
                 ("transmit_filter", C.c_float), ("ior", C.c_float), ("fresnel_effect", C.c_int), ("mirror_color", C.c_float * 3),
-                ("transparentbias_factor", C.c_float), ("transparentbias_multiply_raydepth", C.c_int), ("reflect", C.c_float)]
+                ("transparentbias_factor", C.c_float), ("transparentbias_multiply_raydepth", C.c_int), ("reflect", C.c_float),
+                ("additional_depth", C.c_int), ("oren_nayar", C.c_int), ("sigma", C.c_double), ("sigma_shader", C.c_int)]
 
 
 class yc_image(C.Structure):
@@ -86,7 +87,8 @@ class yc_render(C.Structure):
                 ("aa_detect_color_noise", C.c_int), ("aa_dark_detection_type", C.c_int),
                 ("aa_dark_threshold_factor", C.c_float), ("aa_variance_edge_size", C.c_int), ("aa_variance_pixels", C.c_int),
                 ("raydepth", C.c_int), ("bg_transp_refract", C.c_int),
-                ("transp_shad", C.c_int), ("shadow_depth", C.c_int)]
+                ("transp_shad", C.c_int), ("shadow_depth", C.c_int), ("do_ao", C.c_int), ("ao_samples", C.c_int),
+                ("ao_dist", C.c_float), ("ao_col", C.c_float * 3), ("aa_light_sample_multiplier_factor", C.c_float)]
 
 
 class yc_scene(C.Structure):
@@ -431,7 +433,8 @@ def _texturing(self, spec, mats):
                     if _get(nd, key, "s") is not None:
                         y.input[k] = gidx[_get(nd, key, "s")]
             nodes.append(y)
-        for root, fld in (("diffuse_shader", "diffuse_shader"), ("diffuse_refl_shader", "diffuse_refl_shader")):
+        for root, fld in (("diffuse_shader", "diffuse_shader"), ("diffuse_refl_shader", "diffuse_refl_shader"),
+                          ("sigma_oren_shader", "sigma_shader")):
             nm = _get(m.params, root, "s")
             if nm is not None and nm in gidx:
                 setattr(mats[mi], fld, gidx[nm])
@@ -495,6 +498,10 @@ class OracleScene:
             mats[i].transparentbias_factor = m.transparentbias_factor
             mats[i].transparentbias_multiply_raydepth = int(m.transparentbias_multiply_raydepth)
             mats[i].reflect = m.reflect
+            mats[i].additional_depth = m.additionaldepth
+            mats[i].oren_nayar = int(m.diffuse_brdf == "oren_nayar")
+            mats[i].sigma = m.sigma
+            mats[i].sigma_shader = -1
         lights = (yc_light * max(1, len(s.lights)))()
         for i, l in enumerate(s.render_lights()):
             lights[i].type = YC_LIGHT_POINT if l.type == "pointlight" else YC_LIGHT_AREA
@@ -558,6 +565,9 @@ class OracleScene:
         rp.aa_variance_edge_size, rp.aa_variance_pixels = r.aa_variance_edge_size, r.aa_variance_pixels
         rp.raydepth, rp.bg_transp_refract = r.raydepth, int(r.bg_transp_refract)
         rp.transp_shad, rp.shadow_depth = int(r.transp_shad), r.shadow_depth
+        rp.do_ao, rp.ao_samples, rp.ao_dist = int(r.do_ao), r.ao_samples, r.ao_distance
+        rp.ao_col[:] = list(r.ao_color)
+        rp.aa_light_sample_multiplier_factor = r.aa_light_sample_multiplier_factor
         self.sc = sc
         self.spec = spec
         _texturing(self, spec, mats)

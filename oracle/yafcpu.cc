@@ -465,6 +465,12 @@ struct Material
 	float ior_squared = 1.f, transmit_filter = 1.f, tbias = 0.f;
 	C3 mirror_color;          // shinydiffuse mirror colour / mirror material ref_col_
 	bool is_diffuse = false, double_sided = false, receive_shadows = true, flat = false;
+	int additional_depth = 0;   // Material::additional_depth_ (material_shiny_diffuse.cc:548)
+	// Oren-Nayar (material_shiny_diffuse.cc:146-152): coefficients as the float members the
+	// reference stores them in; sigma_shader: root of sigma_oren_shader (-1: none)
+	bool oren_nayar = false;
+	float on_a = 0.f, on_b = 0.f;
+	int sigma_shader = -1;
 	int n_bsdf = 0;
 	unsigned c_flags[4];
 	int c_index[4];
@@ -626,6 +632,7 @@ struct SurfacePoint
 	unsigned bsdf_flags = 0;
 	C3 dcol;            // getShaderColor(diffuse_shader_, ..., diffuse_color_)
 	float drefl = 1.f;  // diffuse_refl_shader_ scalar
+	float sigma = 0.f;  // sigma_oren_shader_ scalar (getShaderScalar(..., 0.f))
 };
 
 struct IsectData
@@ -778,6 +785,16 @@ Scene::Scene(const yc_scene &s)
 			mm.components[1] = mm.is_transparent ? m.transparency : 0.f;
 			mm.components[2] = mm.is_translucent ? m.translucency : 0.f;
 			mm.components[3] = mm.is_diffuse ? m.diffuse_strength : 0.f;
+			mm.additional_depth = m.additional_depth;
+			if(m.oren_nayar)
+			{
+				// initOrenNayar(double sigma) (:146-152): double arithmetic stored to float members
+				const double sigma_squared = m.sigma * m.sigma;
+				mm.on_a = static_cast<float>(1.0 - 0.5 * (sigma_squared / (sigma_squared + 0.33)));
+				mm.on_b = static_cast<float>(0.45 * sigma_squared / (sigma_squared + 0.09));
+				mm.oren_nayar = true;
+				mm.sigma_shader = m.sigma_shader;
+			}
 		}
 		mats.push_back(mm);
 	}
@@ -928,7 +945,7 @@ void Scene::setupTexturing(const yc_scene &s)
 		texs.push_back(o);
 	}
 	shader_nodes.assign(s.nodes, s.nodes + s.n_nodes);
-	for(const Material &m : mats) if(m.diffuse_shader >= 0 || m.diffuse_refl_shader >= 0) has_attr = true;
+	for(const Material &m : mats) if(m.diffuse_shader >= 0 || m.diffuse_refl_shader >= 0 || m.sigma_shader >= 0) has_attr = true;
 	tattr.resize(tris.size());
 	for(int oi = 0; oi < s.n_objects; ++oi)
 	{
@@ -1066,7 +1083,7 @@ void Scene::surface(const IsectData &d, SurfacePoint &sp) const
 		sp.n.normalize();
 		createCoordsSystem(sp.n, sp.nu, sp.nv);
 	}
-	if(m.diffuse_shader < 0 && m.diffuse_refl_shader < 0) return;
+	if(m.diffuse_shader < 0 && m.diffuse_refl_shader < 0 && m.sigma_shader < 0) return;
 	TexPoint tp;
 	tp.p = sp.p;
 	tp.ng = sp.ng;
@@ -1102,6 +1119,7 @@ void Scene::surface(const IsectData &d, SurfacePoint &sp) const
 		sp.dcol = C3(c.r, c.g, c.b);
 	}
 	if(m.diffuse_refl_shader >= 0) sp.drefl = ev.get(m.diffuse_refl_shader).val;
+	if(m.sigma_shader >= 0) sp.sigma = ev.get(m.sigma_shader).val;
 }
 
 int Scene::buildRec(int start, int end, std::vector<V3> &cent)
@@ -1286,6 +1304,7 @@ class Renderer
 		Renderer(const Scene &s) : sc_(s) {}
 		const Scene &sc_;
 		std::atomic<uint64_t> n_closest{0}, n_shadow{0};
+		float light_mult = 1.f;   // TiledIntegrator::aa_light_sample_multiplier_ of the current pass
 
 		// per-thread state
 		struct Thread
@@ -1411,6 +1430,43 @@ class Renderer
 			return 2.f * vn * normal - v;
 		}
 
+		// material_shiny_diffuse.cc:154-188 ShinyDiffuseMaterial::orenNayar(wi, wo, n, use_texture_sigma,
+		// texture_sigma); math::sqrt is std::sqrt under FAST_MATH
+		static float orenNayar(const V3 &wi, const V3 &wo, const V3 &n, const Material &m, const SurfacePoint &sp)
+		{
+			const float cos_ti = std::max(-1.f, std::min(1.f, dot(n, wi)));
+			const float cos_to = std::max(-1.f, std::min(1.f, dot(n, wo)));
+			float maxcos_f = 0.f;
+			if(cos_ti < 0.9999f && cos_to < 0.9999f)
+			{
+				V3 v_1 = wi - n * cos_ti;
+				v_1.normalize();
+				V3 v_2 = wo - n * cos_to;
+				v_2.normalize();
+				maxcos_f = std::max(0.f, dot(v_1, v_2));
+			}
+			float sin_alpha, tan_beta;
+			if(cos_to >= cos_ti)
+			{
+				sin_alpha = fsqrt(1.f - cos_ti * cos_ti);
+				tan_beta = fsqrt(1.f - cos_to * cos_to) / ((cos_to == 0.f) ? 1e-8f : cos_to);
+			}
+			else
+			{
+				sin_alpha = fsqrt(1.f - cos_to * cos_to);
+				tan_beta = fsqrt(1.f - cos_ti * cos_ti) / ((cos_ti == 0.f) ? 1e-8f : cos_ti);
+			}
+			if(m.sigma_shader >= 0)
+			{
+				const double texture_sigma = sp.sigma;
+				const double sigma_squared = texture_sigma * texture_sigma;
+				const double a = 1.0 - 0.5 * (sigma_squared / (sigma_squared + 0.33));
+				const double b = 0.45 * sigma_squared / (sigma_squared + 0.09);
+				return std::min(1.f, std::max(0.f, (float)(a + b * maxcos_f * sin_alpha * tan_beta)));
+			}
+			return std::min(1.f, std::max(0.f, m.on_a + m.on_b * maxcos_f * sin_alpha * tan_beta));
+		}
+
 		// material_shiny_diffuse.cc:196-238 (mirror / null / light materials evaluate to black)
 		C3 eval(const SurfacePoint &sp, const V3 &wo, const V3 &wl, unsigned bsdfs) const
 		{
@@ -1426,6 +1482,7 @@ class Renderer
 			if(transmit && m.is_translucent) return m.components[2] * m_t * sp.dcol;
 			if(dot(n, wl) < 0.0 && !m.flat) return C3(0.f);
 			float m_d = m_t * (1.f - m.components[2]) * m.components[3];
+			if(m.oren_nayar) m_d *= orenNayar(wo, wl, n, m, sp);   // :228-233
 			if(m.diffuse_refl_shader >= 0) m_d *= sp.drefl;   // :235
 			return m_d * sp.dcol;
 		}
@@ -1527,6 +1584,7 @@ class Renderer
 				default:
 					wi = cosHemisphere(n, sp.nu, sp.nv, s_1, s.s_2);
 					if(cos_ng_wo * dot(sp.ng, wi) > 0) scolor = accum_c[3] * sp.dcol;
+					if(m.oren_nayar) scolor *= orenNayar(wo, wi, n, m, sp);   // :320-325
 					s.pdf = std::abs(dot(wi, n)) * width[pick];
 					break;
 			}
@@ -1611,12 +1669,12 @@ class Renderer
 		// MonteCarloIntegrator::recursiveRaytrace (integrator_montecarlo.cc:925-968) with the
 		// specular reflect / refract branches (:866-923); `ray_level` is the recursion's (caller + 1)
 		void recursiveRaytrace(Thread &th, Mwc &rng, int ray_level, unsigned bsdfs, const SurfacePoint &sp, const V3 &wo,
-		                       uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha) const
+		                       uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int additional_depth) const
 		{
 			col = C3(0.f);
 			float asum = 0.f;
 			int count = 0;
-			if(ray_level <= sc_.rp.raydepth && ray_level < 20 && (bsdfs & (BGlossy | BSpecular | BFilter)) && (bsdfs & (BSpecular | BFilter)))
+			if(ray_level <= sc_.rp.raydepth + additional_depth && ray_level < 20 && (bsdfs & (BGlossy | BSpecular | BFilter)) && (bsdfs & (BSpecular | BFilter)))
 			{
 				const Specular spec = getSpecular(sp, wo);
 				const Material &m = *sp.mat;
@@ -1636,7 +1694,7 @@ class Renderer
 					ref_ray.tmax = -1.f;
 					C3 c;
 					float a;
-					integrate(th, ref_ray, rng, sample_idx, offset, c, a, ray_level);
+					integrate(th, ref_ray, rng, sample_idx, offset, c, a, ray_level, additional_depth);
 					c *= (k == 0 ? spec.rcol : spec.tcol);
 					col += c;
 					asum += a;
@@ -1646,10 +1704,11 @@ class Renderer
 			alpha = count > 0 ? asum / count : 1.f;
 		}
 
-		void integrate(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level) const
+		void integrate(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level,
+		               int additional_depth = 0) const
 		{
-			if(sc_.rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha, ray_level);
-			else integrateDirect(th, ray, rng, sample_idx, offset, col, alpha, ray_level);
+			if(sc_.rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha, ray_level, additional_depth);
+			else integrateDirect(th, ray, rng, sample_idx, offset, col, alpha, ray_level, additional_depth);
 		}
 
 		float shadowTmin(const SurfacePoint &sp) const
@@ -1819,7 +1878,8 @@ class Renderer
 			else
 			{
 				const unsigned l_offs = loffs * 4567;
-				const int num_samples = static_cast<int>(std::ceil(static_cast<float>(L.samples) * 1.f));
+				// integrator_montecarlo.cc:396: ceilf(nSamples() * aa_light_sample_multiplier_)
+				const int num_samples = static_cast<int>(ceilf(static_cast<float>(L.samples) * light_mult));
 				const float inv_num_samples = 1.f / static_cast<float>(num_samples);
 				const unsigned offs = num_samples * sample_idx + offset + l_offs;
 				Halton hal_2(2, offs - 1);
@@ -1865,7 +1925,46 @@ class Renderer
 		}
 
 		// integrator_direct_light.cc:97-144
-		void integrateDirect(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level = 0) const
+		// TiledIntegrator::sampleAmbientOcclusion (integrator_tiled.cc:644-691), clay = false, one ray division
+		C3 sampleAmbientOcclusion(Thread &th, const SurfacePoint &sp, const V3 &wo, uint32_t sample_idx, uint32_t offset) const
+		{
+			const yc_render &rp = sc_.rp;
+			C3 col(0.f);
+			const unsigned mat_bsdfs = sp.bsdf_flags;
+			Ray light_ray;
+			light_ray.from = sp.p;
+			light_ray.dir = V3(0.f, 0.f, 0.f);
+			const int n = rp.ao_samples;
+			const unsigned offs = n * sample_idx + offset;
+			Halton hal_2(2, offs - 1);
+			Halton hal_3(3, offs - 1);
+			const C3 ao_col(rp.ao_col[0], rp.ao_col[1], rp.ao_col[2]);
+			for(int i = 0; i < n; ++i)
+			{
+				const float s_1 = hal_2.getNext();
+				const float s_2 = hal_3.getNext();
+				light_ray.tmin = shadowTmin(sp);
+				light_ray.tmax = rp.ao_dist;
+				float w = 0.f;
+				Sample s(s_1, s_2, BGlossy | BDiffuse | BReflect);
+				const C3 surf_col = sample(sp, wo, light_ray.dir, s, w);
+				if(mat_bsdfs & BEmit) col += emit(sp, wo) * s.pdf;
+				bool shadowed;
+				C3 scol(0.f);
+				if(rp.transp_shad) shadowed = isShadowedTs(th, light_ray, scol);
+				else shadowed = isShadowed(th, light_ray);
+				if(!shadowed)
+				{
+					const float cos = std::abs(dot(sp.n, light_ray.dir));
+					if(rp.transp_shad) col += ao_col * scol * surf_col * cos * w;
+					else col += ao_col * surf_col * cos * w;
+				}
+			}
+			return col / static_cast<float>(n);
+		}
+
+		void integrateDirect(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level = 0,
+		                     int additional_depth = 0) const
 		{
 			col = C3(0.f);
 			alpha = 1.f;
@@ -1874,17 +1973,23 @@ class Renderer
 			{
 				const unsigned mat_bsdfs = sp.bsdf_flags;
 				const V3 wo = -ray.dir;
+				additional_depth = std::max(additional_depth, sp.mat->additional_depth);   // :107
 				if(mat_bsdfs & BEmit) col += emit(sp, wo);
-				if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+				if(mat_bsdfs & BDiffuse)
+				{
+					col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+					if(sc_.rp.do_ao) col += sampleAmbientOcclusion(th, sp, wo, sample_idx, offset);   // :124
+				}
 				C3 rcol;
-				recursiveRaytrace(th, rng, ray_level + 1, mat_bsdfs, sp, wo, sample_idx, offset, rcol, alpha);
+				recursiveRaytrace(th, rng, ray_level + 1, mat_bsdfs, sp, wo, sample_idx, offset, rcol, alpha, additional_depth);
 				col += rcol;
 			}
 			else background(ray, col, alpha, ray_level);
 		}
 
 		// integrator_path_tracer.cc:120-290
-		void integratePath(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level = 0) const
+		void integratePath(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level = 0,
+		                   int additional_depth = 0) const
 		{
 			const yc_render &rp = sc_.rp;
 			col = C3(0.f);
@@ -1894,6 +1999,7 @@ class Renderer
 			if(!intersect(th, ray, sp)) { background(ray, col, alpha, ray_level); return; }
 			const unsigned mat_bsdfs = sp.bsdf_flags;
 			const V3 wo = -ray.dir;
+			additional_depth = std::max(additional_depth, sp.mat->additional_depth);   // path_tracer.cc:133
 			if(mat_bsdfs & BEmit) col += emit(sp, wo);
 			if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
 			unsigned path_flags = BDiffuse;
@@ -1961,7 +2067,7 @@ class Renderer
 				col += path_col / static_cast<float>(n_samples);
 			}
 			C3 rcol;
-			recursiveRaytrace(th, rng, ray_level + 1, mat_bsdfs, sp, wo, sample_idx, offset, rcol, alpha);
+			recursiveRaytrace(th, rng, ray_level + 1, mat_bsdfs, sp, wo, sample_idx, offset, rcol, alpha, additional_depth);
 			col += rcol;
 		}
 
@@ -2616,6 +2722,7 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 	for(int pass = 1; pass < passes; ++pass)
 	{
 		sample_multiplier *= rp.aa_sample_multiplier_factor;
+		R.light_mult *= rp.aa_light_sample_multiplier_factor;   // integrator_tiled.cc:190
 		if(resampled <= 0.f && !threshold_changed) {}   // nextPass(..., skipNextPass = true): flags untouched
 		else
 		{

@@ -40,6 +40,12 @@ typedef struct {
 	float transparentbias_factor;
 	int transparentbias_multiply_raydepth;
 	float reflect;            // mirror material
+	// ShinyDiffuseMaterial::factory (material_shiny_diffuse.cc:507, 561-571): additionaldepth,
+	// diffuse_brdf = "oren_nayar" with "sigma" (double), root "sigma_oren_shader" (yc_scene.nodes, -1: none)
+	int additional_depth;
+	int oren_nayar;
+	double sigma;
+	int sigma_shader;
 } yc_material;
 
 // ---- texturing (material_node.cc, texture_image.cc, shader_node_*.cc; see yaftex.h) ----
@@ -148,6 +154,12 @@ typedef struct {
 	int bg_transp_refract;
 	// transparent shadows (integrator "transpShad" / "shadowDepth", MonteCarloIntegrator tr_shad_ / s_depth_)
 	int transp_shad, shadow_depth;
+	// DirectLight ambient occlusion (integrator_direct_light.cc:161-163, 183-186): do_AO, AO_samples,
+	// AO_distance, AO_color; AA_light_sample_multiplier_factor (scene.cc:589, integrator_tiled.cc:190)
+	int do_ao, ao_samples;
+	float ao_dist;
+	float ao_col[3];
+	float aa_light_sample_multiplier_factor;
 } yc_render;
 
 typedef struct {
