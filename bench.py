@@ -4,16 +4,26 @@ PathIntegrator depth 8, 1920x1080 x 64 spp (BASELINE config C2; C3 when launched
 
 One "step" = one full frame (132.7 M camera samples) rendered through the C API
 (yafaray_amd_renderQuiet = yafaray_render without the per-pixel callbacks), inputs resident on
-the GPU.  On N GPUs (torch.distributed.run, one process per GPU, backend nccl = RCCL) the frame's
-32-pixel tile rows are dealt round-robin to the ranks and the finished tile rows are all-gathered
-over RCCL into the full film every step (strong scaling: total work fixed).
+the GPU.  On N GPUs (torch.distributed.run, one process per GPU) every rank renders one
+contiguous band of pixel rows and the library itself all-gathers the bands over RCCL into every
+rank's film (yafaray_amd_setRenderGroup: the multi-GPU split lives behind the drop-in boundary).
 
-Prints ONE JSON line (rank 0).  Extra keys: mrays_per_s, roofline (k_trace vs HBM), cpu_baseline
-(the CPU oracle restatement on the host cores, bounded sample of the same frame).
+Prints ONE JSON line (rank 0).  Extra keys:
+  * mrays_per_s                       closest + shadow rays per second (in-kernel counters)
+  * roofline                          the dominant kernel against its bound (HIP events live, per launch)
+  * kernels                           every kernel: time share, algorithmic bytes per work item
+                                      (SURVEY §8d model), measured HBM traffic (PMC,
+                                      profiles/pmc_<config>.json), achieved GB/s and fraction of 8 TB/s
+  * parity                            full-size checks of this frame against the CPU oracle:
+                                      the cpu_baseline band block-by-block (RR on: paired z-test of
+                                      8x8 block means) and an RR-off band bit for bit
+  * cpu_baseline                      the oracle restatement on this host's cores, bounded band
 """
 import argparse
 import json
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -43,6 +53,8 @@ def parse():
     ap.add_argument("--chunk", type=int, default=1 << 26)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the full-size parity checks")
+    ap.add_argument("--parity-rows", type=int, default=12, help="rows of the RR-off bit-exact band")
     return ap.parse_args()
 
 
@@ -55,8 +67,63 @@ def workload_name(a, W, H):
             + ("" if a.scene == "cornell" else " + 1M-triangle sphere (C4)"))
 
 
-def traffic_config(a, W, H):
-    return f"{a.scene}-{W}x{H}x{a.spp}-b{a.bounces}-rr{int(not a.no_rr)}-chunk{a.chunk}"
+def pmc_config(a, W, H):
+    """Key of profiles/pmc_<key>.json (tools/pmc_all.sh): one workload, one kernel source."""
+    return f"{a.scene}-{W}x{H}x{a.spp}-b{a.bounces}-rr{int(not a.no_rr)}-chunk{a.chunk}" + (
+        f"-ph{a.photons}" if a.scene == "photon" else "")
+
+
+def kernels_src_sha1():
+    import hashlib
+    h = hashlib.sha1()
+    for f in ("kernels.hip", "pkd.hip", "aa.hip"):
+        with open(os.path.join(ROOT, "libyafaray_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def load_pmc(a, W, H):
+    """Per-kernel PMC traffic of this exact workload and kernel source, or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{pmc_config(a, W, H)}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            pj = json.load(f)
+    except Exception:
+        return None
+    if pj.get("config") != pmc_config(a, W, H) or pj.get("kernels_src_sha1") != kernels_src_sha1():
+        return None
+    return pj
+
+
+# ---------------------------------------------------------------------------------------------
+# algorithmic bytes per work item (SURVEY.md §8d; DESIGN.md §4 restates each with our design's bytes)
+# ---------------------------------------------------------------------------------------------
+def algo_bytes(kind, s, kt, in_lds, a):
+    """Total algorithmic HBM bytes of all launches of one kernel kind in one frame."""
+    it = kt["items"]
+    if kind == "k_trace":
+        # ray I/O: closest 32 B in + 8 B out (t, prim); shadow 32 B in + 4 B index + 1 B out; traversal
+        # bytes (128 B per BVH4 node, 48 B per triangle) only when the scene is not LDS-resident
+        trav = (128.0 if s["bvh_width"] == 4 else 64.0) * s["node_visits"] + 48.0 * s["tri_tests"]
+        return 40.0 * s["closest_rays"] + 37.0 * s["shadow_rays"] + (0.0 if in_lds else trav)
+    if kind == "k_shade":
+        return 64.0 * it          # §8d: path-state read + write per path segment
+    if kind == "k_nee":
+        # per request: the vertex in (p, prim, wo, pixel, sample) 48 B; out: one shadow ray per light
+        # sample (o, d, index 36 B) + contribution (16 B) + occlusion byte
+        return 48.0 * it + 53.0 * (s["shadow_rays"] / max(1, s["closest_rays"])) * it
+    if kind == "k_camera":
+        return 96.0 * it          # camera ray 32 B + initial path state 64 B (§8d)
+    if kind == "k_film":
+        return 16.0 * it + 20.0 * a.width * a.height   # the samples (float4) + RGBA + weight per pixel
+    if kind == "k_gather":
+        # §8d: N_visit * 16 B (kd nodes 8 B + photon position) + k * 36 B photon records per query
+        return 16.0 * s.get("gather_visits", 0) + 36.0 * 50 * it
+    if kind == "k_photon_bounce":
+        return (32.0 + 36.0) * s["photons"] + 32.0 * it   # deposits + one ray per path per bounce
+    return None
 
 
 def main():
@@ -74,45 +141,24 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
 
     import libyafaray_amd as Y
-    from libyafaray_amd import scenes, tiles
+    from libyafaray_amd import scenes
     if a.scene == "sphere":
         spec = scenes.cornell_sphere(width=a.width, height=a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
     elif a.scene == "photon":
         spec = scenes.cornell_photon(a.width, a.height, spp=a.spp, photons=a.photons)
     else:
         spec = scenes.cornell(a.width, a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
-    # the reference's PathIntegrator default caustic_type is "path" (integrator_path_tracer.cc:43);
-    # a diffuse-only scene never takes a caustic branch either way.
     yi = Y.Interface()
     scenes.apply(spec, yi)
     yi.L.yafaray_amd_setChunkSlots(yi.h, a.chunk)
-    # one contiguous pixel-row band per rank (+ its halo row): equal rows at first, then the
-    # boundaries follow the ranks' measured render times (tiles.rebalance_bands, every step)
+    if world > 1:
+        # the library renders this rank's row band and all-gathers the bands over RCCL itself
+        Y.join_render_group(yi, rank, world, dist)
     if not yi.L.yafaray_amd_buildAccelerator(yi.h):
         raise RuntimeError(yi.last_error())
-
     W, H = a.width, a.height
-    bounds = [tiles.band_range(H, r, world)[0] for r in range(world)] + [H]
-    max_rows = min(H, -(-H * 5 // (4 * world)) + 1)    # a band may grow to 1.25x the mean
-    band = torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev)
-    gathered = torch.zeros((world * max_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
-    t_all = torch.zeros(world, dtype=torch.float64, device=dev) if world > 1 else None
-
-    def step():
-        y0, y1 = bounds[rank], bounds[rank + 1]
-        yi.L.yafaray_amd_setRowBandRange(yi.h, y0, y1, world)
-        t_r = time.perf_counter()
-        yi.render_quiet()
-        t_r = time.perf_counter() - t_r
-        if y1 > y0 and not yi.L.yafaray_amd_getFilmDevice(yi.h, band.data_ptr(), y0, y1):
-            raise RuntimeError(yi.last_error())
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, band)
-            dist.all_gather_into_tensor(t_all, torch.tensor([t_r], dtype=torch.float64, device=dev))
-            bounds[:] = tiles.rebalance_bands(bounds, t_all.tolist(), cap_rows=max_rows)
 
     def sync():
         torch.cuda.synchronize()
@@ -121,70 +167,47 @@ def main():
             torch.cuda.synchronize()
 
     for _ in range(a.warmup):
-        step()
-    # timed region: k_trace launches bracketed by HIP events on the render stream (profile mode)
+        yi.render_quiet()
+    # timed region: every launch bracketed by HIP events on the render stream (profile mode)
     yi.L.yafaray_amd_setProfileKernels(yi.h, 1)
     sync()
     t0 = time.perf_counter()
-    stats_acc = []
+    stats_acc, kt_acc = [], []
     for _ in range(a.steps):
-        step()
+        yi.render_quiet()
         stats_acc.append(yi.stats())
+        kt_acc.append(yi.kernel_times())
     sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([sum(s["closest_rays"] + s["shadow_rays"] for s in stats_acc),
-                            sum(s["node_visits"] for s in stats_acc), sum(s["tri_tests"] for s in stats_acc)],
-                           device=dev, dtype=torch.float64)
+        tot = torch.tensor([sum(s["closest_rays"] + s["shadow_rays"] for s in stats_acc)], device="cuda", dtype=torch.float64)
         dist.all_reduce(tot)
         rays_total = float(tot[0].item())
     else:
         rays_total = float(sum(s["closest_rays"] + s["shadow_rays"] for s in stats_acc))
 
-    samples_total = float(W * H * a.spp * a.steps)     # whole job: every rank's tile rows together
+    samples_total = float(W * H * a.spp * a.steps)     # whole job: every rank's band together
     msps = samples_total / elapsed / 1e6
     mrays = rays_total / elapsed / 1e6
 
-    # roofline of the dominant kernel (k_trace) on this rank, per launch, with the average launch
-    # duration from HIP events on the render stream.  Algorithmic bytes:
-    #   ray I/O      closest 32 B in + 8 B out, shadow 32 B in + 4 B index + 1 B out  (always HBM)
-    #   traversal    64 B (BVH2) / 128 B (BVH4) per BVH node visited + 48 B per triangle tested
-    # The traversal bytes count against HBM only when the scene is not LDS-resident; for the
-    # Cornell box (3 KB) they are served by LDS and reported separately against the LDS peak.
-    s = stats_acc[-1]
-    launches = max(1, s["trace_launches"])
-    avg_ms = s["trace_kernel_ms"] / launches
-    ray_io = 40.0 * s["closest_rays"] + 37.0 * s["shadow_rays"]
-    node_bytes = 128.0 if s["bvh_width"] == 4 else 64.0
-    trav = node_bytes * s["node_visits"] + 48.0 * s["tri_tests"]
-    in_lds = bool(s["scene_in_lds"])
-    algo_bytes = ray_io + (0.0 if in_lds else trav)
-    per_launch = algo_bytes / launches
-    achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    trav_rate = trav / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = None
-    valu_insts = None
-    tfile = os.path.join(ROOT, "profiles", "trace_hbm_bytes_per_launch.json")
-    if os.path.exists(tfile):
-        try:
-            with open(tfile) as f:
-                tj = json.load(f)
-            import hashlib
-            with open(os.path.join(ROOT, "libyafaray_amd", "csrc", "kernels.hip"), "rb") as f:
-                sha = hashlib.sha1(f.read()).hexdigest()
-            # only a measurement of this exact kernel source on this exact workload counts
-            if tj.get("config") == traffic_config(a, W, H) and tj.get("kernels_hip_sha1") == sha:
-                traffic = tj.get("hbm_bytes_per_launch")
-                valu_insts = tj.get("valu_insts_per_launch")
-        except Exception:
-            traffic = None
+    s, kt = stats_acc[-1], kt_acc[-1]
+    pmc = load_pmc(a, W, H)
+    kernels, frame_ms = kernel_table(a, s, kt, pmc)
+    roof = dominant_roofline(s, kt, kernels, pmc)
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(spec, a)
+    cpu, parity = None, None
+    if rank == 0 and world == 1:
+        if not a.no_cpu_baseline:
+            cpu, band = cpu_baseline(spec, a)
+            if not a.no_parity and band is not None:
+                rgba, w = yi.film()
+                parity = {"band": band_parity(spec, rgba, w, band)}
+        if not a.no_parity and a.scene == "cornell":
+            parity = parity or {}
+            parity["rr_off_bitexact"] = rr_off_parity(Y, a)
 
     if rank == 0:
         out = {
@@ -202,31 +225,13 @@ def main():
             "data": "synthetic (Cornell box scene generated in-repo, SURVEY.md §8d)",
             "config": {"workload": workload_name(a, W, H),
                        "width": W, "height": H, "spp": a.spp, "bounces": a.bounces,
-                       "samples_per_step": W * H * a.spp, "parallelism": f"row-bands x{world}",
+                       "samples_per_step": W * H * a.spp, "parallelism": f"row-bands x{world} (in-library RCCL all-gather)",
                        "chunk_slots": a.chunk},
             "mrays_per_s": round(mrays, 2),
             "rays_per_sample": round(rays_total / samples_total, 3),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_trace", "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
-                         "algo_bytes_per_launch": round(per_launch),
-                         # VALU issue (the bound of an LDS-resident traversal): PMC SQ_INSTS_VALU per launch
-                         # (same kernels.hip + workload only) / the live launch time, against 256 CUs x 4 SIMDs
-                         # x 2.4 GHz / 2 cycles per wave64 VALU instruction
-                         "valu": ({"insts_per_launch": valu_insts,
-                                   "achieved_g_per_s": round(valu_insts / (avg_ms * 1e-3) / 1e9, 1),
-                                   "peak_g_per_s": VALU_PEAK_GIPS,
-                                   "frac": round(valu_insts / (avg_ms * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4)}
-                                  if valu_insts and avg_ms > 0 else None),
-                         "traversal": {"bytes_per_launch": round(trav / launches), "served_from": "LDS" if in_lds else "L2/MALL/HBM",
-                                       "achieved": round(trav_rate, 1), "unit": "GB/s",
-                                       "lds_peak": LDS_PEAK_GBS, "frac_of_lds_peak": round(trav_rate / LDS_PEAK_GBS, 4),
-                                       "bvh_width": s["bvh_width"],
-                                       "node_visits_per_ray": round(s["node_visits"] / max(1, s["closest_rays"] + s["shadow_rays"]), 2),
-                                       "tri_tests_per_ray": round(s["tri_tests"] / max(1, s["closest_rays"] + s["shadow_rays"]), 2)}},
-            "shade": {"avg_launch_ms": round(s["shade_kernel_ms"] / launches, 4),
-                      "ms_per_step": round(s["shade_kernel_ms"], 2), "trace_ms_per_step": round(s["trace_kernel_ms"], 2),
-                      "nee_ms_per_step": round(s["nee_kernel_ms"], 2)},
+            "roofline": roof,
+            "kernels": kernels,
+            "kernel_ms_per_step": round(frame_ms, 3),
             "photon_map": ({"photons_stored": s["photons"], "seconds_per_step": round(s["photon_seconds"], 4),
                             "shoot_seconds": round(s["photon_shoot_seconds"], 4), "tree_seconds": round(s["photon_tree_seconds"], 4)}
                            if a.scene == "photon" else None),
@@ -234,6 +239,7 @@ def main():
             # accelerator build + scene upload, once before the timed region (the reference builds
             # its kd-tree inside render(), scene.cc:218)
             "scene_build_seconds": round(s["build_seconds"], 4),
+            "parity": parity,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
@@ -242,15 +248,95 @@ def main():
         dist.destroy_process_group()
 
 
+def kernel_table(a, s, kt, pmc):
+    """Per kernel kind: ms per frame, share, launches, algorithmic bytes, measured traffic, fraction."""
+    frame_ms = sum(v["ms"] for v in kt.values())
+    in_lds = bool(s["scene_in_lds"])
+    out = {}
+    for kind, v in sorted(kt.items(), key=lambda kv: -kv[1]["ms"]):
+        e = {"ms": round(v["ms"], 3), "share": round(v["ms"] / frame_ms, 4) if frame_ms else None, "launches": v["launches"],
+             "items": v["items"]}
+        ab = algo_bytes(kind, s, v, in_lds, a)
+        if ab is not None and v["ms"] > 0:
+            e["algo_bytes_per_item"] = round(ab / max(1, v["items"]), 1)
+            e["achieved_gbs"] = round(ab / (v["ms"] * 1e-3) / 1e9, 1)
+            e["frac"] = round(ab / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        p = (pmc or {}).get("kernels", {}).get(kind)
+        if p and "hbm_bytes_total" in p and v["ms"] > 0:
+            e["traffic_bytes"] = p["hbm_bytes_total"]                 # measured, one frame (PMC pass)
+            e["traffic_gbs"] = round(p["hbm_bytes_total"] / (v["ms"] * 1e-3) / 1e9, 1)
+            e["traffic_frac"] = round(e["traffic_gbs"] / HBM_PEAK_GBS, 4)
+            if "valu_lane_util" in p:
+                e["valu_lane_util"] = p["valu_lane_util"]
+            if "sq_insts_valu_per_launch" in p and v["launches"]:
+                e["valu_issue_frac"] = round(p["sq_insts_valu_per_launch"] / (v["ms"] / v["launches"] * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4)
+        out[kind] = e
+    return out, frame_ms
+
+
+def dominant_roofline(s, kt, kernels, pmc):
+    """The contract's roofline object for the kernel with the largest share of the frame."""
+    if not kt:
+        return None
+    kind = max(kt, key=lambda k: kt[k]["ms"])
+    v, e = kt[kind], kernels[kind]
+    launches = max(1, v["launches"])
+    avg_ms = v["ms"] / launches
+    achieved = e.get("achieved_gbs", 0.0)
+    per_launch = achieved * 1e9 * avg_ms * 1e-3
+    p = (pmc or {}).get("kernels", {}).get(kind, {})
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": p.get("hbm_bytes_per_launch"),
+            "kernel": kind, "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
+            "algo_bytes_per_launch": round(per_launch)}
+    if kind == "k_trace":
+        trav = (128.0 if s["bvh_width"] == 4 else 64.0) * s["node_visits"] + 48.0 * s["tri_tests"]
+        rate = trav / launches / (avg_ms * 1e-3) / 1e9
+        rays = max(1, s["closest_rays"] + s["shadow_rays"])
+        roof["traversal"] = {"bytes_per_launch": round(trav / launches), "served_from": "LDS" if s["scene_in_lds"] else "L2/MALL/HBM",
+                             "achieved": round(rate, 1), "unit": "GB/s", "lds_peak": LDS_PEAK_GBS,
+                             "frac_of_lds_peak": round(rate / LDS_PEAK_GBS, 4), "bvh_width": s["bvh_width"],
+                             "node_visits_per_ray": round(s["node_visits"] / rays, 2), "tri_tests_per_ray": round(s["tri_tests"] / rays, 2)}
+        if "valu_issue_frac" in e:
+            roof["valu"] = {"issue_frac": e["valu_issue_frac"], "lane_util": e.get("valu_lane_util")}
+    return roof
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU baseline + parity
+# ---------------------------------------------------------------------------------------------
+def host_cpu():
+    """(threads, nproc, model): the threads the CPU baseline runs = the cores this job may use —
+    the scheduler affinity, capped by the box's CPU share when the pool states one in
+    OMP_NUM_THREADS (the GPU pool gives each one-GPU job 16 of the host's cores and shows the
+    whole machine in nproc; measured: 256 threads on such a box ran slower than 16)."""
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except Exception:
+        n_aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if share > 0:
+        n_aff = min(n_aff, share)
+    model = platform.processor() or ""
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith("Model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return n_aff, os.cpu_count() or 1, model
+
+
 def cpu_baseline(spec, a):
-    """The CPU oracle (C++ restatement of the reference loop) on the host cores, on a bounded
-    band of rows of the same frame, scaled to Msamples/s."""
+    """The CPU oracle (C++ restatement of the reference loop, std::thread per core) on every core this
+    process may run on, over a bounded band of rows of the same frame, scaled to Msamples/s.
+    Returns (cpu_baseline dict, (y0, y1, rgba, weights) of the band or None)."""
     try:
         from oracle import oracle as O
     except Exception as e:  # pragma: no cover
-        return {"error": str(e)}
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    cores = max(1, min(cores, os.cpu_count() or 1))
+        return {"error": str(e)}, None
+    cores, nproc, model = host_cpu()
     photon_note = ""
     t_photons = 0.0
     if spec.render.integrator == "photonmapping":
@@ -265,29 +351,86 @@ def cpu_baseline(spec, a):
         t_photons = (time.perf_counter() - t0) * (n_full / n_cpu)
         photon_note = f"; photon map: {n_cpu} photons shot+built in {t_photons * n_cpu / n_full:.1f} s (1 thread), scaled x{n_full / n_cpu:g}"
     osc = O.OracleScene(spec, threads=cores)
-    # probe one 32-row tile band, then size the sample to ~cpu_seconds
+    # probe 4 rows, then size the band to ~cpu_seconds
     ts = spec.render.tile_size
     y0 = (spec.render.height // 2 // ts) * ts
     t0 = time.perf_counter()
     osc.render(y0, y0 + 4)
-    probe = time.perf_counter() - t0
-    per_row = probe / 4
-    rows = int(max(4, min(spec.render.height - y0, a.cpu_seconds / max(per_row, 1e-6))))
+    per_row = (time.perf_counter() - t0) / 4
+    rows = int(max(8, min(spec.render.height - y0, a.cpu_seconds / max(per_row, 1e-6))))
     t0 = time.perf_counter()
-    _, _, ctr = osc.render(y0, y0 + rows)
+    rgba, w, ctr = osc.render(y0, y0 + rows)
     dt = time.perf_counter() - t0
     n = rows * spec.render.width * spec.render.aa_samples
+    base = {"unit": "Msamples/s", "cores": cores, "kind": "port", "nproc": nproc, "cpu_model": model,
+            "threads": cores, "threads_rule": "sched affinity capped by OMP_NUM_THREADS (the box's CPU share)"}
+    band = None if spec.render.integrator == "photonmapping" else (y0, y0 + rows, rgba, w)
     if t_photons > 0.0:
-        # whole frame = photon map + every row; rate over the frame
         frame = spec.render.width * spec.render.height * spec.render.aa_samples
         t_frame = t_photons + dt * frame / n
-        return {"value": round(frame / t_frame / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
-                "sample": f"rows {y0}..{y0 + rows} of the {spec.render.width}x{spec.render.height} frame "
-                          f"({n} samples, {dt:.1f} s, {cores} threads){photon_note}"}
-    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
-            "mrays_per_s": round((ctr[0] + ctr[1]) / dt / 1e6, 3),
-            "sample": f"rows {y0}..{y0 + rows} of the same {spec.render.width}x{spec.render.height}x"
-                      f"{spec.render.aa_samples}spp frame ({n} samples, {dt:.1f} s, {cores} threads)"}
+        base.update({"value": round(frame / t_frame / 1e6, 4),
+                     "sample": f"rows {y0}..{y0 + rows} of the {spec.render.width}x{spec.render.height} frame "
+                               f"({n} samples, {dt:.1f} s, {cores} threads){photon_note}"})
+        return base, band
+    base.update({"value": round(n / dt / 1e6, 4), "mrays_per_s": round((ctr[0] + ctr[1]) / dt / 1e6, 3),
+                 "sample": f"rows {y0}..{y0 + rows} of the same {spec.render.width}x{spec.render.height}x"
+                           f"{spec.render.aa_samples}spp frame ({n} samples, {dt:.1f} s, {cores} threads)"})
+    return base, band
+
+
+def band_parity(spec, rgba, w, band):
+    """GPU frame vs the oracle's band.  The band's first row lacks the splats of the row above it
+    (forward-only footprint), so rows y0+1..y1-1 are compared.  Russian roulette on: the reference's
+    RR draws are tile-order dependent, so the check is statistical — paired 8x8 block
+    means of the difference image, z = mean / (sd / 8); without RR it is exact."""
+    y0, y1, orgba, ow = band
+    g = rgba[y0 + 1:y1, :, :3].astype(np.float64)
+    o = orgba[y0 + 1:y1, :, :3].astype(np.float64)
+    rr = spec.render.rr_min_bounces < spec.render.bounces
+    res = {"rows": [y0 + 1, y1], "pixels": int(g.shape[0] * g.shape[1]), "rr": rr,
+           "weights_equal": bool(np.array_equal(w[y0 + 1:y1], ow[y0 + 1:y1]))}
+    d = (g - o).mean(-1)
+    hb, wb = d.shape[0] // 8, d.shape[1] // 8
+    blocks = d[:hb * 8, :wb * 8].reshape(hb, 8, wb, 8).transpose(0, 2, 1, 3).reshape(hb * wb, 64)
+    sd = blocks.std(1, ddof=1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        z = np.where(sd > 0, blocks.mean(1) / (sd / 8.0), 0.0)
+    res.update({"blocks": int(hb * wb), "max_abs_z": round(float(np.abs(z).max()), 3),
+                "frac_abs_z_gt_4": round(float((np.abs(z) > 4).mean()), 5),
+                "mean_rel_diff": round(float((g.mean() - o.mean()) / max(1e-12, o.mean())), 6)})
+    if not rr:
+        res["bit_identical"] = bool(np.array_equal(rgba[y0 + 1:y1].view(np.uint32), orgba[y0 + 1:y1].view(np.uint32)))
+    res["pass"] = bool(res["weights_equal"] and (res.get("bit_identical", True)) and res["max_abs_z"] < 5.5
+                       and abs(res["mean_rel_diff"]) < 0.005)
+    return res
+
+
+def rr_off_parity(Y, a):
+    """The same full-size frame with Russian roulette off, rendered on the GPU, against the oracle
+    on a band of rows: bit for bit (the reference's integrator without RR is deterministic)."""
+    from libyafaray_amd import scenes
+    from oracle import oracle as O
+    spec = scenes.cornell(a.width, a.height, spp=a.spp, bounces=a.bounces, rr=False)
+    yi = Y.Interface()
+    scenes.apply(spec, yi)
+    yi.L.yafaray_amd_setChunkSlots(yi.h, a.chunk)
+    t0 = time.perf_counter()
+    yi.render_quiet()
+    t_gpu = time.perf_counter() - t0
+    rgba, w = yi.film()
+    yi.close()
+    cores, _, _ = host_cpu()
+    y0 = a.height // 3
+    y1 = min(a.height, y0 + max(2, a.parity_rows))
+    t0 = time.perf_counter()
+    orgba, ow, _ = O.OracleScene(spec, threads=cores).render(y0, y1)
+    t_cpu = time.perf_counter() - t0
+    a_ = rgba[y0 + 1:y1].view(np.uint32)
+    b_ = orgba[y0 + 1:y1].view(np.uint32)
+    ulp = np.abs(a_.astype(np.int64) - b_.astype(np.int64))
+    return {"rows": [y0 + 1, y1], "pixels": int(a_.shape[0] * a_.shape[1]), "bit_identical": bool(np.array_equal(a_, b_)),
+            "max_ulp": int(ulp.max()), "weights_equal": bool(np.array_equal(w[y0 + 1:y1], ow[y0 + 1:y1])),
+            "gpu_frame_s": round(t_gpu, 3), "cpu_band_s": round(t_cpu, 2)}
 
 
 if __name__ == "__main__":

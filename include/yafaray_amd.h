@@ -45,6 +45,7 @@ typedef struct
 	uint64_t photons;           /* photons stored in the diffuse photon map (photon mapping) */
 	double photon_seconds;      /* photon shooting + kd-tree build + upload */
 	double photon_shoot_seconds, photon_tree_seconds;
+	uint64_t gather_visits;     /* point kd-tree nodes fetched by the photon density estimates */
 } yafaray_amd_stats_t;
 
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */
@@ -82,6 +83,28 @@ YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t 
 
 /* Counters and timings of the last render. */
 YAFARAY_C_API_EXPORT void yafaray_amd_getStats(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats);
+
+/* Per-kernel timing of the last render with setProfileKernels on (HIP events before / after every
+ * launch on the render stream): for each kernel kind k < return value (and < max): its name, summed
+ * launch time in ms, launch count and work items (samples for k_camera / k_film, rays for k_trace,
+ * active entries for k_shade, requests for k_nee, queries for k_gather, photon paths for the photon
+ * shoot, stored photons for the photon map).  Any output pointer may be NULL.  (LIBYAFARAY_AMD_1.1) */
+YAFARAY_C_API_EXPORT int yafaray_amd_getKernelTimes(const yafaray_Interface_t *interface, const char **names, double *ms, uint64_t *launches,
+                                                    uint64_t *items, int max);
+
+/* Render group (LIBYAFARAY_AMD_1.1): several GPUs render one film, one member per GPU (e.g. one
+ * process per GPU).  Member 0 creates the group id (an RCCL unique id, <= 128 bytes) and hands it to
+ * the others by any host means; every member then calls setRenderGroup with its rank on its own
+ * current HIP device.  From then on yafaray_render / renderQuiet on each member renders a contiguous
+ * band of pixel rows (+ the halo rows its splats need) and all-gathers every band over RCCL (xGMI)
+ * into the member's film: each member ends with the whole frame, bit-identical to a one-GPU render.
+ * The bands follow the members' measured render times from frame to frame (rebalanceBands).
+ * world = 1 leaves the group.  getRenderGroupId returns the id size (0 on failure). */
+YAFARAY_C_API_EXPORT int yafaray_amd_getRenderGroupId(void *id, int bytes);
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_setRenderGroup(yafaray_Interface_t *interface, int rank, int world, const void *id, int bytes);
+/* The group's band balancer: world + 1 boundaries and each band's render time -> new boundaries
+ * (out, world + 1 ints); cap_rows > 0 rejects a split with a larger band.  Returns 1. */
+YAFARAY_C_API_EXPORT int yafaray_amd_rebalanceBands(const int *bounds, int world, const double *times, int cap_rows, int *out);
 
 /* Tuning: samples in flight per wavefront chunk (default 1 << 25, halved automatically if it does not fit) and whether to time k_trace with events. */
 YAFARAY_C_API_EXPORT void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots);

@@ -38,7 +38,7 @@ class Stats(C.Structure):
                 ("bvh_width", C.c_uint32), ("trace_grid", C.c_uint32), ("shade_grid", C.c_uint32),
                 ("trace_block", C.c_uint32), ("stack_depth", C.c_uint32), ("shade_kernel_ms", C.c_double),
                 ("nee_kernel_ms", C.c_double), ("photons", C.c_uint64), ("photon_seconds", C.c_double),
-                ("photon_shoot_seconds", C.c_double), ("photon_tree_seconds", C.c_double)]
+                ("photon_shoot_seconds", C.c_double), ("photon_tree_seconds", C.c_double), ("gather_visits", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -135,6 +135,11 @@ def lib():
             "yafaray_amd_setChunkSlots": (None, [vp, i]),
             "yafaray_amd_setProfileKernels": (None, [vp, b]),
             "yafaray_amd_lastError": (cp, [vp]),
+            "yafaray_amd_getRenderGroupId": (i, [vp, i]),
+            "yafaray_amd_setRenderGroup": (b, [vp, i, i, vp, i]),
+            "yafaray_amd_rebalanceBands": (i, [C.POINTER(C.c_int), i, C.POINTER(C.c_double), i, C.POINTER(C.c_int)]),
+            "yafaray_amd_getKernelTimes": (i, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                               C.POINTER(C.c_uint64), i]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -251,6 +256,16 @@ class Interface:
         self.L.yafaray_amd_getStats(self.h, C.byref(s))
         return s.as_dict()
 
+    def kernel_times(self) -> dict:
+        """{kernel: {"ms", "launches", "items"}} of the last render with profiling on (yafaray_amd_getKernelTimes)."""
+        n = 32
+        names = (C.c_char_p * n)()
+        ms = (C.c_double * n)()
+        la = (C.c_uint64 * n)()
+        it = (C.c_uint64 * n)()
+        k = self.L.yafaray_amd_getKernelTimes(self.h, names, ms, la, it, n)
+        return {names[j].decode(): {"ms": ms[j], "launches": la[j], "items": it[j]} for j in range(min(k, n)) if la[j]}
+
     def owned_rows(self):
         """[(y0, y1), ...] pixel rows this rank's last render owns (yafaray_amd_getOwnedRows)."""
         n = self.L.yafaray_amd_getOwnedRows(self.h, None, 0)
@@ -277,6 +292,37 @@ class Interface:
                                               o.ctypes.data_as(C.POINTER(C.c_int))):
             raise RuntimeError("traceShadow failed: " + self.last_error())
         return o
+
+
+def render_group_id() -> bytes:
+    """A fresh render-group id (RCCL unique id) for yafaray_amd_setRenderGroup."""
+    buf = C.create_string_buffer(128)
+    n = lib().yafaray_amd_getRenderGroupId(buf, 128)
+    if n <= 0:
+        raise RuntimeError("yafaray_amd_getRenderGroupId failed")
+    return buf.raw[:n]
+
+
+def join_render_group(yi, rank, world, dist):
+    """Make `yi` member `rank` of a `world`-GPU render group (one process per GPU): rank 0 creates
+    the id, torch.distributed broadcasts it, every member joins on its current HIP device.  The
+    library then splits every render into row bands and all-gathers them over RCCL itself."""
+    obj = [render_group_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(obj, src=0)
+    gid = obj[0]
+    if not yi.L.yafaray_amd_setRenderGroup(yi.h, int(rank), int(world), gid, len(gid)):
+        raise RuntimeError("setRenderGroup failed: " + yi.last_error())
+
+
+def rebalance_bands(bounds, times, cap_rows=0):
+    """The library's band balancer (yafaray_amd_rebalanceBands)."""
+    world = len(bounds) - 1
+    b = (C.c_int * (world + 1))(*bounds)
+    t = (C.c_double * world)(*times)
+    out = (C.c_int * (world + 1))()
+    lib().yafaray_amd_rebalanceBands(b, world, t, int(cap_rows), out)
+    return list(out)
 
 
 def render_spec(spec, chunk_slots=None, profile=False, shard=None):

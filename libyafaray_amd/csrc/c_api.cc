@@ -8,6 +8,8 @@
 #include "hostmath.h"
 #include "render.h"
 
+#include <rccl/rccl.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -489,7 +491,12 @@ yafaray_bool_t yafaray_amd_traceShadow(yafaray_Interface_t *interface, const flo
 yafaray_bool_t yafaray_amd_getFilm(const yafaray_Interface_t *interface, float *rgba, float *weights)
 {
 	const Interface *it = I(interface);
-	if(!it->scene || it->scene->film_rgba.empty()) return YAFARAY_BOOL_FALSE;
+	if(!it->scene) return YAFARAY_BOOL_FALSE;
+	Scene *s = it->scene.get();
+	// a quiet render (renderQuiet) leaves the film on the GPU: fetch it now
+	if(s->film_on_gpu_only && !s->gpu()->download(s->film_rgba, s->film_weights, s->film_w, s->film_h)) return YAFARAY_BOOL_FALSE;
+	s->film_on_gpu_only = false;
+	if(s->film_rgba.empty()) return YAFARAY_BOOL_FALSE;
 	if(rgba) std::memcpy(rgba, it->scene->film_rgba.data(), it->scene->film_rgba.size() * 4);
 	if(weights) std::memcpy(weights, it->scene->film_weights.data(), it->scene->film_weights.size() * 4);
 	return YAFARAY_BOOL_TRUE;
@@ -572,6 +579,48 @@ void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_
 }
 
 const char *yafaray_amd_lastError(const yafaray_Interface_t *interface) { return I(interface)->logger.lastError().c_str(); }
+
+int yafaray_amd_getRenderGroupId(void *id, int bytes)
+{
+	ncclUniqueId uid;
+	if(!id || bytes < (int)sizeof(uid) || ncclGetUniqueId(&uid) != ncclSuccess) return 0;
+	std::memcpy(id, &uid, sizeof(uid));
+	return (int)sizeof(uid);
+}
+
+yafaray_bool_t yafaray_amd_setRenderGroup(yafaray_Interface_t *interface, int rank, int world, const void *id, int bytes)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return YAFARAY_BOOL_FALSE;
+	s->group_bounds.clear();
+	return s->gpu()->joinGroup(rank, world, id, bytes < 0 ? 0 : (size_t)bytes) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+int yafaray_amd_rebalanceBands(const int *bounds, int world, const double *times, int cap_rows, int *out)
+{
+	if(!bounds || !times || !out || world < 1) return 0;
+	const std::vector<int> b(bounds, bounds + world + 1);
+	const std::vector<double> t(times, times + world);
+	const std::vector<int> nb = rebalanceBands(b, t, cap_rows);
+	for(int r = 0; r <= world; ++r) out[r] = nb[r];
+	return 1;
+}
+
+int yafaray_amd_getKernelTimes(const yafaray_Interface_t *interface, const char **names, double *ms, uint64_t *launches, uint64_t *items,
+                               int max)
+{
+	const Interface *it = I(interface);
+	if(!it->scene) return 0;
+	const KernelTimes &kt = it->scene->kernelTimes();
+	for(int k = 0; k < KK_COUNT && k < max; ++k)
+	{
+		if(names) names[k] = kernelKindName(k);
+		if(ms) ms[k] = kt.ms[k];
+		if(launches) launches[k] = kt.launches[k];
+		if(items) items[k] = kt.items[k];
+	}
+	return KK_COUNT;
+}
 
 int yafaray_amd_getPhaseCycles(unsigned long long *cycles, int n, yafaray_bool_t reset)
 {

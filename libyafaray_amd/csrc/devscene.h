@@ -15,6 +15,7 @@
 
 namespace yafamd
 {
+struct DevStats;
 
 enum : uint32_t
 {
@@ -196,7 +197,9 @@ struct DevScene
 	const float4 *ph_pos;          // (position, colour.r) per photon, kd-tree order of the map
 	const float4 *ph_dir;          // (direction, colour.g)
 	const float *ph_colb;          // colour.b
-	const uint2 *pk_nodes;         // point kd-tree (pkdtree.h:41-64): (split bits | photon, flags)
+	const uint4 *pk_nodes;         // point kd-tree (pkdtree.h:41-64): .w flags (axis / leaf, right child or photon << 2),
+	                               // interior .x split position, leaf .xyz the photon's position
+	uint2 *pk_stack;               // k_gather lookup stacks: pm_stack levels x gather lanes (HBM)
 	int n_photons, pm_paths, pm_search, pm_stack;
 	float pm_radius2;              // "diffuseRadius", used as the squared gather radius (:954)
 	// light selection for photon emission (sample_pdf1d.h: Pdf1D over the total energy of the
@@ -232,6 +235,7 @@ struct DevScene
 	int do_ao, ao_samples;
 	float ao_dist;
 	float ao_col[3];
+	struct DevStats *stats;        // per-workgroup counters (null: not counted)
 	uint32_t node_base;            // node id of spawn slot 0 (= level-0 capacity of the chunk)
 	uint32_t spawn_cap;
 	float4 *node_own;              // per node: colour before recursiveRaytrace's result, alpha
@@ -334,9 +338,15 @@ struct DevCounters
 	uint32_t *n_nee;      // [n_seg] NEE requests per segment
 };
 
+// Per-workgroup counters (record b belongs to workgroup b of every launch on the stream: plain
+// read-modify-writes, no atomics; summed on the host after the render)
 struct DevStats
 {
 	unsigned long long closest_rays, shadow_rays, node_visits, tri_tests;
+	unsigned long long shade_entries;    // active-list entries k_shade processed
+	unsigned long long nee_requests;     // NEE requests k_nee served
+	unsigned long long gather_queries;   // photon density estimates k_gather computed
+	unsigned long long gather_visits;    // point kd-tree nodes k_gather fetched
 };
 
 } // namespace yafamd

@@ -105,6 +105,8 @@ GpuRenderer *Scene::gpu()
 	return gpu_.get();
 }
 
+const KernelTimes &Scene::kernelTimes() { return gpu()->kernelTimes(); }
+
 // scene.cc:977-1004, object_mesh.cc:35-86
 bool Scene::createObject(const std::string &name, const ParamMap &p)
 {
@@ -1127,6 +1129,18 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		rp.shard_mode = shard_mode;
 		rp.shard_y0 = shard_y0;
 		rp.shard_y1 = shard_y1;
+		const int group_world = gpu()->groupWorld();
+		if(group_world > 1)
+		{
+			// render group: this member renders its row band (+ halo rows), groupCombine below
+			// all-gathers the bands over RCCL into every member's film
+			if((int)group_bounds.size() != group_world + 1 || group_bounds.back() != s.height) group_bounds = equalBands(s.height, group_world);
+			rp.shard_world = group_world;
+			rp.shard_rank = gpu()->groupRank();
+			rp.shard_mode = 2;
+			rp.shard_y0 = group_bounds[rp.shard_rank];
+			rp.shard_y1 = group_bounds[rp.shard_rank + 1];
+		}
 		rp.aa.passes = std::max(1, s.aa_passes);
 		if(rp.aa.passes > 1 && rp.shard_world > 1)
 		{
@@ -1227,10 +1241,17 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			};
 		}
 		if(!gpu()->render(rp, &canceled)) return false;
+		if(group_world > 1)
+		{
+			std::vector<double> all_ms;
+			if(!gpu()->groupCombine(group_bounds, gpu()->stats().render_seconds * 1e3, all_ms)) return false;
+			group_bounds = rebalanceBands(group_bounds, all_ms, 0);
+		}
 		if(fmode != filmio::None) saveFilm();
 		const double build = stats.build_seconds;
 		stats = gpu()->stats();
 		stats.build_seconds = build;
+		film_on_gpu_only = quiet;
 		if(quiet) continue;
 		if(!gpu()->download(film_rgba, film_weights, s.width, s.height)) return false;
 		{

@@ -167,6 +167,7 @@ struct Callbacks
 };
 
 class GpuRenderer;
+struct KernelTimes;
 struct HostImage;
 struct HostTexture;
 
@@ -198,6 +199,7 @@ class Scene
 		bool geometry_dirty = true;
 		int shard_rank = 0, shard_world = 1, shard_mode = 1;
 		int shard_y0 = 0, shard_y1 = 0;   // shard_mode 2: explicit row band
+		std::vector<int> group_bounds;    // render group: row-band boundaries of the members (rebalanced per frame)
 		int chunk_slots = 1 << 26;   // samples in flight per wavefront chunk (64 M: the C2 frame in two chunks)
 		bool profile_kernels = false;
 		volatile bool canceled = false;
@@ -222,10 +224,12 @@ class Scene
 		bool render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, void *progress_data, bool quiet);
 		bool buildAccelerator();
 		GpuRenderer *gpu();
+		const KernelTimes &kernelTimes();   // per-kernel timing of the last profiled render
 
 		// film of the last render
 		std::vector<float> film_rgba, film_weights;
 		int film_w = 0, film_h = 0;
+		bool film_on_gpu_only = false;   // the last render was quiet: film_rgba / film_weights are stale
 		yafaray_amd_stats_t stats{};
 
 	private:

@@ -45,6 +45,14 @@ namespace yafamd
 #define YAF_SHADE_MIN_WAVES 4
 #endif
 constexpr int kTraceBlock = YAF_TRACE_BLOCK;
+// -DYAF_FUSE: the non-EXT k_shade runs the NEE itself (no k_nee launch).  Measured on C2 (r02):
+// 1591 Msamples/s split vs 1455 fused at 3 waves/SIMD (1347 at 4 with 240 B/lane of scratch, 1154
+// at 2) — the HBM-bound shade loses more occupancy than the request round trip costs.
+#ifdef YAF_FUSE
+constexpr bool kShadeFused = true;
+#else
+constexpr bool kShadeFused = false;
+#endif
 constexpr int kShadeBlock = 256;
 
 enum : uint32_t
@@ -1503,7 +1511,11 @@ __device__ void spawnSpecular(const DevScene &S, const DevMaterial &m, const Sur
 //   4. wave-ballot compaction: the entry's state moves to its position in the next queue
 //      (coalesced SoA reads and writes, no indirection);
 //   5. next-event estimation into the next state: contributions + shadow rays.
-template<bool SMALL, bool EXT>
+// FUSED (the non-EXT instantiations): step 5 runs the next-event estimation in place instead of
+// queueing requests for k_nee — the NEE request round trip through HBM (48 B written + read per
+// vertex) and one launch per iteration disappear; the shade loop is HBM-bound, so the light
+// sampling arithmetic overlaps its memory traffic.
+template<bool SMALL, bool EXT, bool FUSED = false>
 __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_shade(ShadeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
@@ -1515,9 +1527,13 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 	const uint32_t seg = blockIdx.x;
 	const uint32_t n_a = A.cnt.n_active[seg];
 	const uint32_t a0 = seg * S.cap_a;
-	__shared__ uint32_t s_count[2];   // next active entries, NEE requests
-	if(threadIdx.x < 2) s_count[threadIdx.x] = 0;
+	__shared__ uint32_t s_count[3];   // next active entries, NEE / gather requests, shadow rays (FUSED)
+	if(threadIdx.x < 3) s_count[threadIdx.x] = 0;
 	__syncthreads();
+	ShadeOut out;
+	out.sh_count = &s_count[2];
+	out.sh_base = seg * S.cap_s;
+	out.Qn = A.Qn;
 	const bool is_path = S.integrator == INT_PATH;
 	const bool is_photon = S.integrator == INT_PHOTON;
 	const bool keep_v0 = S.path_samples > 1 || is_photon;   // first-hit data carried to the end
@@ -1852,8 +1868,33 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		// (photon mapping: the gather requests of the last iteration use the same queue — a path
 		// never asks for NEE and a gather in the same iteration, and the DL-style pipeline of the
 		// photon integrator serves NEE in iteration 0 and gathers in iteration 1)
-		const uint32_t jn = waveAppend(want_nee || want_gather, &s_count[1]);
-		if(want_nee)
+		if(FUSED)
+		{
+			// k_nee's work in place (integrator_montecarlo.cc:54-408): contributions into the next
+			// state at k * nee_k, shadow rays appended to segment `seg` of the next queue
+			const int e0 = (int)k * K;
+			const bool all = live && nee_v0, one = live && nee_one;
+			const DevMaterial &m = S.mats[sp.mat];
+			float4 *ts = S.tr_shad ? Pn.ts : nullptr;
+			if(__any(all))
+			{
+				for(int l = 0; l < S.n_lights; ++l)
+					neeLight<EXT>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, all, e0 + (int)S.lights[l].nee_base, Pn.nee,
+					              Pn.occ, out, ts);
+				if(S.do_ao) aoSamples<EXT>(S, m, sp, wo, sample_idx, offset, all, e0 + S.nee_all_count, Pn.nee, Pn.occ, out, ts);
+			}
+			if(__any(one))
+			{
+				for(int l = 0; l < S.n_lights; ++l)
+				{
+					const bool mine = one && lnum == (uint32_t)l;
+					if(!__any(mine)) continue;
+					neeLight<EXT>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, mine, e0, Pn.nee, Pn.occ, out, ts);
+				}
+			}
+		}
+		const uint32_t jn = waveAppend((!FUSED && want_nee) || want_gather, &s_count[1]);
+		if(!FUSED && want_nee)
 		{
 			const uint32_t j = a0 + jn;
 			A.N.p_prim[j] = f4(sp.p, __int_as_float(hit_prim));
@@ -1885,6 +1926,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 	{
 		A.cnt_next.n_active[seg] = s_count[0];
 		A.cnt_next.n_nee[seg] = s_count[1];
+		if(FUSED) A.cnt_next.n_shadow[seg] = s_count[2];
+		if(S.stats) S.stats[seg].shade_entries += n_a;
 	}
 }
 
@@ -2134,7 +2177,11 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 		}
 	}
 	__syncthreads();
-	if(threadIdx.x == 0) A.cnt_next.n_shadow[seg] = s_count;
+	if(threadIdx.x == 0)
+	{
+		A.cnt_next.n_shadow[seg] = s_count;
+		if(S.stats) S.stats[seg].nee_requests += n_req;
+	}
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2586,6 +2633,13 @@ __global__ void __launch_bounds__(1024) k_photon_scatter(PhotonState P, uint32_t
 // contributions are added to the sample's colour in heap-array order and the sample is written.
 // ---------------------------------------------------------------------------------------------
 constexpr int kGatherBlock = 64;
+constexpr int kGatherPerSeg = 4;   // workgroups per queue segment (fills the chip: 4 x 1024 x 64 lanes)
+//
+// Occupancy is the lever (a kd walk is a chain of dependent loads): the 50-entry heap stays in LDS
+// (8 B per entry and lane, the only per-lane LDS), the lookup stack lives in a per-lane HBM column
+// (pushes are fire-and-forget stores, pops hit L2: a 64-lane workgroup's stack is <= 14 KB), leaf
+// nodes carry their photon's position (one dependent load per leaf instead of two), and no Faure
+// tables are staged.  Result: ~25 KB LDS per 64 lanes instead of ~45 KB.
 
 struct GatherArgs
 {
@@ -2598,26 +2652,49 @@ struct GatherArgs
 	uint64_t chunk_base;
 };
 
+__host__ __device__ inline size_t gatherTableBytes(const DevScene &S, bool small)
+{
+	return small ? (size_t)S.n_mats * sizeof(DevMaterial) + (size_t)S.n_tris * 16 : 0;
+}
+
+__host__ __device__ inline size_t gatherLdsBytes(const DevScene &S, bool small)
+{
+	return gatherTableBytes(S, small) + (size_t)kGatherBlock * 8u * (size_t)S.pm_search;
+}
+
 template<bool SMALL, bool EXT>
 __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 {
-	extern __shared__ uint4 shade_smem[];
-	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
+	extern __shared__ uint4 gather_smem[];
+	DevScene S = A.S;
+	if(SMALL)
+	{
+		uint4 *p = gather_smem;
+		const int nm = S.n_mats * (int)(sizeof(DevMaterial) / 16);
+		copy16(p, S.mats, nm);
+		S.mats = reinterpret_cast<const DevMaterial *>(p);
+		p += nm;
+		copy16(p, S.prim_ng, S.n_tris);
+		S.prim_ng = reinterpret_cast<const float4 *>(p);
+		__syncthreads();
+	}
 	const bool ATTR = EXT && S.has_attr != 0;
-	// per-lane heap and lookup stack, lane-interleaved after the staged tables
-	uint32_t *lds_words = reinterpret_cast<uint32_t *>(shade_smem) + shadeLdsBytes(A.S, SMALL) / 4;
+	// per-lane heap, lane-interleaved after the staged tables
+	uint32_t *lds_words = reinterpret_cast<uint32_t *>(gather_smem) + gatherTableBytes(A.S, SMALL) / 4;
 	const int k = S.pm_search;
 	const int lane = threadIdx.x;
 	HeapRef heap;
 	heap.idx = lds_words + lane;
 	heap.dist = reinterpret_cast<float *>(lds_words + (size_t)k * kGatherBlock) + lane;
 	heap.stride = kGatherBlock;
-	uint32_t *st_node = lds_words + (size_t)2 * k * kGatherBlock + lane;
-	float *st_s = reinterpret_cast<float *>(st_node + (size_t)S.pm_stack * kGatherBlock);
-	const uint32_t seg = blockIdx.x;
+	// lookup stack: this lane's column of the HBM stack buffer, [level][global lane]
+	const uint32_t gstride = gridDim.x * kGatherBlock;
+	uint2 *stk = S.pk_stack + blockIdx.x * kGatherBlock + threadIdx.x;
+	const uint32_t seg = blockIdx.x % S.n_seg, part = blockIdx.x / S.n_seg, parts = gridDim.x / S.n_seg;
 	const uint32_t n_req = A.cnt_next.n_nee[seg];
 	const uint32_t a0 = seg * S.cap_a;
-	for(uint32_t base_j = 0; base_j < n_req; base_j += blockDim.x)
+	uint32_t visits = 0;
+	for(uint32_t base_j = part * kGatherBlock; base_j < n_req; base_j += parts * kGatherBlock)
 	{
 		if(base_j + threadIdx.x >= n_req) continue;
 		const uint32_t j = a0 + base_j + threadIdx.x;
@@ -2631,29 +2708,31 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)};
 		const float alpha = __uint_as_float(cb.w);
 		// ---- k-NN lookup (pkdtree.h:225-292, NON_REC_LOOKUP) ----
+		// nodes: .w = flags (bits 0-1 axis, 3 = leaf; interior: right child << 2, leaf: photon << 2),
+		// interior .x = split position; leaf .xyz = the photon's position
 		float max_d2 = S.pm_radius2;
 		int found = 0;
 		uint32_t curr = 0;
 		int sp_top = 0;   // entries above the reference's "nowhere" sentinel
 		for(;;)
 		{
-			uint2 nd = S.pk_nodes[curr];
-			while((nd.y & 3u) != 3u)
+			uint4 nd = S.pk_nodes[curr];
+			++visits;
+			while((nd.w & 3u) != 3u)
 			{
-				const int axis = (int)(nd.y & 3u);
+				const int axis = (int)(nd.w & 3u);
 				const float split_val = __uint_as_float(nd.x);
 				const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
 				uint32_t far_child;
-				if(pa <= split_val) { far_child = nd.y >> 2; curr = curr + 1; }
-				else { far_child = curr + 1; curr = nd.y >> 2; }
-				st_node[sp_top * kGatherBlock] = far_child | ((uint32_t)axis << 30);
-				st_s[sp_top * kGatherBlock] = split_val;
+				if(pa <= split_val) { far_child = nd.w >> 2; curr = curr + 1; }
+				else { far_child = curr + 1; curr = nd.w >> 2; }
+				stk[(size_t)sp_top * gstride] = make_uint2(far_child | ((uint32_t)axis << 30), nd.x);
 				++sp_top;
 				nd = S.pk_nodes[curr];
+				++visits;
 			}
-			const uint32_t ph = nd.x;
-			const float4 q = S.ph_pos[ph];
-			const V3 v = xyz(q) - p;
+			const uint32_t ph = nd.w >> 2;
+			const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
 			float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
 			if(dist_2 < max_d2)
 			{
@@ -2676,24 +2755,24 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 				}
 			}
 			if(sp_top == 0) break;
-			uint32_t top = st_node[(sp_top - 1) * kGatherBlock];
-			int axis = (int)(top >> 30);
+			uint2 top = stk[(size_t)(sp_top - 1) * gstride];
+			int axis = (int)(top.x >> 30);
 			float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
-			dist_2 = pa - st_s[(sp_top - 1) * kGatherBlock];
+			dist_2 = pa - __uint_as_float(top.y);
 			dist_2 *= dist_2;
 			bool done = false;
 			while(dist_2 > max_d2)
 			{
 				--sp_top;
 				if(sp_top == 0) { done = true; break; }
-				top = st_node[(sp_top - 1) * kGatherBlock];
-				axis = (int)(top >> 30);
+				top = stk[(size_t)(sp_top - 1) * gstride];
+				axis = (int)(top.x >> 30);
 				pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
-				dist_2 = pa - st_s[(sp_top - 1) * kGatherBlock];
+				dist_2 = pa - __uint_as_float(top.y);
 				dist_2 *= dist_2;
 			}
 			if(done) break;
-			curr = top & 0x3fffffffu;
+			curr = top.x & 0x3fffffffu;
 			--sp_top;
 		}
 		// ---- density estimate (:959-976) ----
@@ -2716,11 +2795,13 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		const SampleCoord sc = sampleAt(S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
 		A.samples[((size_t)sc.y * S.width + sc.x) * S.spp + sc.s] = f4(col, alpha > 1.f ? 1.f : alpha);
 	}
-}
-
-__host__ __device__ inline size_t gatherLdsBytes(const DevScene &S, bool small)
-{
-	return shadeLdsBytes(S, small) + (size_t)kGatherBlock * (8u * (size_t)S.pm_search + 8u * (size_t)S.pm_stack);
+	// counters: wave sums, then one atomic per workgroup (several workgroups share a segment)
+	for(int off = 32; off > 0; off >>= 1) visits += __shfl_down(visits, off);
+	if(threadIdx.x == 0 && S.stats)
+	{
+		atomicAdd(&S.stats[seg].gather_visits, (unsigned long long)visits);
+		if(part == 0) atomicAdd(&S.stats[seg].gather_queries, (unsigned long long)n_req);
+	}
 }
 
 } // namespace yafamd
@@ -2733,6 +2814,10 @@ using namespace yafamd;
 extern "C" {
 
 int yafamd_trace_block() { return kTraceBlock; }
+
+// Whether the non-EXT k_shade runs the next-event estimation itself (then render.cc launches no
+// k_nee for those scenes); -DYAF_FUSE builds that variant (measured slower, see kShadeFused).
+int yafamd_shade_fused() { return kShadeFused ? 1 : 0; }
 
 // Diagnostic: k_shade phase cycles (only a -DYAF_PHASE_TIMING build records them).
 int yafamd_phase_cycles(unsigned long long *out, int n, int reset)
@@ -2832,8 +2917,8 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 		if(S->small_tables) hipLaunchKernelGGL((k_shade<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 		else hipLaunchKernelGGL((k_shade<false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	}
-	else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
-	else hipLaunchKernelGGL((k_shade<false, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, kShadeFused>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	else hipLaunchKernelGGL((k_shade<false, false, kShadeFused>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	return hipGetLastError();
 }
 
@@ -2959,15 +3044,19 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const D
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
 	const size_t lds = gatherLdsBytes(*S, S->small_tables != 0);
+	const dim3 grid(S->n_seg * kGatherPerSeg);
 	if(S->ext)
 	{
-		if(S->small_tables) hipLaunchKernelGGL((k_gather<true, true>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
-		else hipLaunchKernelGGL((k_gather<false, true>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
+		if(S->small_tables) hipLaunchKernelGGL((k_gather<true, true>), grid, dim3(kGatherBlock), lds, st, A);
+		else hipLaunchKernelGGL((k_gather<false, true>), grid, dim3(kGatherBlock), lds, st, A);
 	}
-	else if(S->small_tables) hipLaunchKernelGGL((k_gather<true, false>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
-	else hipLaunchKernelGGL((k_gather<false, false>), dim3(S->n_seg), dim3(kGatherBlock), lds, st, A);
+	else if(S->small_tables) hipLaunchKernelGGL((k_gather<true, false>), grid, dim3(kGatherBlock), lds, st, A);
+	else hipLaunchKernelGGL((k_gather<false, false>), grid, dim3(kGatherBlock), lds, st, A);
 	return hipGetLastError();
 }
+
+// lanes of one gather launch (the HBM lookup stack holds pm_stack levels per lane)
+size_t yafamd_gather_lanes(const DevScene *S) { return (size_t)S->n_seg * kGatherPerSeg * kGatherBlock; }
 
 size_t yafamd_gather_lds_bytes(const DevScene *S) { return gatherLdsBytes(*S, S->small_tables != 0); }
 

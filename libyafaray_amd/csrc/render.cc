@@ -4,6 +4,7 @@
 #include "devmath.h"
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -27,6 +28,7 @@ hipError_t yafamd_launch_combine(const DevScene *S, uint32_t lo, uint32_t hi, in
 hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P,
                                DevStats *stats, int stack_depth, int *spill, int grid, hipStream_t st);
 int yafamd_trace_block();
+int yafamd_shade_fused();
 int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds);
 int yafamd_shade_blocks_per_cu();
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
@@ -43,9 +45,10 @@ hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const DevCounters *cnt_next, float4 *samples,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
 size_t yafamd_gather_lds_bytes(const DevScene *S);
+size_t yafamd_gather_lanes(const DevScene *S);
 hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
                                 int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st);
-hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint2 *nodes_dev, int *depth_out, hipStream_t st);
+hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st);
 hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix, uint8_t *flags,
                                     hipStream_t st);
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, const uint8_t *flags, float4 *accum, float4 *out,
@@ -114,7 +117,10 @@ struct GpuRenderer::Impl
 	float light_inv_integral = 0.f;
 	int n_ph_lights = 0;
 	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
-	Buf ph_pos, ph_dir, ph_colb, pk_nodes;
+	Buf ph_pos, ph_dir, ph_colb, pk_nodes, pk_stack;
+	// render group (RCCL communicator over the group's GPUs) and its exchange buffers
+	ncclComm_t comm = nullptr;
+	Buf g_send, g_recv, g_wsend, g_wrecv, g_times;
 	std::vector<DevLight> host_lights;   // as uploaded (light sample multiplier passes rewrite the device copy)
 	std::vector<DevLight> pass_lights;   // staging of the current pass's copy (alive until the stream syncs)
 	int n_photons = 0, pm_paths = 0, pm_stack = 0;
@@ -135,14 +141,44 @@ struct GpuRenderer::Impl
 	DevPaths P[2]{};       // path state, parallel to Q[q] (indexed by queue position)
 	DevQueues Q[2]{};
 	Buf counters, stats;
-	std::vector<hipEvent_t> ev_pool;
+	std::vector<hipEvent_t> ev_pool;   // [0], [1]: the render's start / end; then the profile events
+	// profile mode: HIP events before / after every launch on the render stream
+	bool prof_on = false;
+	size_t ev_n = 2;
+	struct ProfRec { int kind, e0, e1; };
+	std::vector<ProfRec> prof_recs;
+	hipEvent_t event(size_t i)
+	{
+		while(ev_pool.size() <= i)
+		{
+			hipEvent_t e = nullptr;
+			if(hipEventCreate(&e) != hipSuccess) return nullptr;
+			ev_pool.push_back(e);
+		}
+		return ev_pool[i];
+	}
+	int profBegin()
+	{
+		if(!prof_on) return -1;
+		hipEvent_t e = event(ev_n);
+		if(!e || hipEventRecord(e, stream) != hipSuccess) return -1;
+		return (int)ev_n++;
+	}
+	void profEnd(int kind, int e0)
+	{
+		if(e0 < 0) return;
+		hipEvent_t e = event(ev_n);
+		if(!e || hipEventRecord(e, stream) != hipSuccess) return;
+		prof_recs.push_back({kind, e0, (int)ev_n});
+		++ev_n;
+	}
 	int trace_grid = 2048, shade_grid = 1024, nee_grid = 1024, n_cu = 256;
 	DevNeeQueue N{};
 
 	~Impl()
 	{
 		for(Buf *b : {&ph_lights, &light_cdf, &light_func, &ph_ray_o, &ph_ray_d, &ph_pcol, &ph_alive0, &ph_alive1, &ph_n_alive,
-		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes})
+		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes, &pk_stack})
 			b->release();
 		for(Buf *b : {&prim_attr, &shader_nodes, &textures, &texels, &spawn_o, &spawn_d, &spawn_pr, &node_own, &node_child, &node_w,
 		              &spawn_count})
@@ -151,6 +187,8 @@ struct GpuRenderer::Impl
 		              &weights, &jobs, &counters, &stats, &accum, &aa_flags, &aa_plist})
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
+		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times}) b->release();
+		if(comm) (void)ncclCommDestroy(comm);
 		for(hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
 		if(stream) (void)hipStreamDestroy(stream);
 	}
@@ -167,6 +205,15 @@ struct GpuRenderer::Impl
 			log_.error(os_.str());                                                                             \
 			return false;                                                                                      \
 		}                                                                                                      \
+	} while(0)
+
+// a launch timed in profile mode (kernel kind `kind`)
+#define PROF(kind, expr)                                                                                       \
+	do                                                                                                         \
+	{                                                                                                          \
+		const int e0_ = d_->profBegin();                                                                       \
+		HIPCHECK(expr);                                                                                        \
+		d_->profEnd(kind, e0_);                                                                                \
 	} while(0)
 
 GpuRenderer::GpuRenderer(Logger &log) : d_(new Impl), log_(log) {}
@@ -446,28 +493,28 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	P.dep_flag = (uint8_t *)d.dep_flag.p;
 	HIPCHECK(hipMemsetAsync(d.dep_flag.p, 0, n_slots, d.stream));
 	HIPCHECK(hipMemsetAsync(d.ph_n_alive.p, 0, 16, d.stream));
-	HIPCHECK(yafamd_photon_emit(&S, &P, N, pm.bounces, d.stream));
+	PROF(KK_PHOTON_EMIT, yafamd_photon_emit(&S, &P, N, pm.bounces, d.stream));
 	int cur = 0;
 	for(int b = 0; b <= pm.bounces; ++b)
 	{
 		HIPCHECK(hipMemsetAsync((uint32_t *)d.ph_n_alive.p + (cur ^ 1), 0, 4, d.stream));
-		HIPCHECK(yafamd_photon_bounce(&S, &P, N, pm.bounces, b, cur, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+		PROF(KK_PHOTON_BOUNCE, yafamd_photon_bounce(&S, &P, N, pm.bounces, b, cur, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 		cur ^= 1;
 	}
 	// the photon map in photon-id order (one reference thread's append order); outputs sized for
 	// the worst case (every slot stored), the count comes back from the scan
 	uint32_t n = 0;
 	if(!ensure(log_, d.ph_pos, n_slots * 16) || !ensure(log_, d.ph_dir, n_slots * 16) || !ensure(log_, d.ph_colb, n_slots * 4)) return false;
-	HIPCHECK(yafamd_photon_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)d.ph_pos.p,
+	PROF(KK_PHOTON_COMPACT, yafamd_photon_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)d.ph_pos.p,
 	                               (float4 *)d.ph_dir.p, (float *)d.ph_colb.p, d.stream));
 	HIPCHECK(hipMemcpyAsync(&n, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	if(n < 50) { log_.error("PhotonIntegrator: Too few diffuse photons, stopping now."); return false; }   // :448-452
 	const auto t1 = std::chrono::steady_clock::now();
 	// point kd-tree of the map, built on the GPU node for node like the reference's (pkd.hip)
-	if(!ensure(log_, d.pk_nodes, (2 * (size_t)n - 1) * sizeof(uint2))) return false;
+	if(!ensure(log_, d.pk_nodes, (2 * (size_t)n - 1) * sizeof(uint4))) return false;
 	int depth = 0;
-	HIPCHECK(yafamd_build_pkd((const float4 *)d.ph_pos.p, n, (uint2 *)d.pk_nodes.p, &depth, d.stream));
+	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)d.ph_pos.p, n, (uint4 *)d.pk_nodes.p, &depth, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	struct { int max_depth; } pb{depth};
 	d.n_photons = (int)n;
@@ -476,7 +523,12 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	S.ph_pos = (const float4 *)d.ph_pos.p;
 	S.ph_dir = (const float4 *)d.ph_dir.p;
 	S.ph_colb = (const float *)d.ph_colb.p;
-	S.pk_nodes = (const uint2 *)d.pk_nodes.p;
+	S.pk_nodes = (const uint4 *)d.pk_nodes.p;
+	// k_gather's lookup stacks (pm_stack levels per gather lane, in HBM)
+	DevScene seg_probe = S;
+	seg_probe.n_seg = (uint32_t)d.shade_grid;   // the queue segments of the render that follows
+	if(!ensure(log_, d.pk_stack, (size_t)d.pm_stack * yafamd_gather_lanes(&seg_probe) * sizeof(uint2))) return false;
+	S.pk_stack = (uint2 *)d.pk_stack.p;
 	S.n_photons = (int)n;
 	S.pm_paths = (int)N;
 	S.pm_stack = d.pm_stack;
@@ -499,6 +551,10 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	fillScenePointers(d, S);
 	stats_.photons = 0;
 	stats_.photon_seconds = 0.0;
+	d.prof_on = rp.profile;
+	d.ev_n = 2;
+	d.prof_recs.clear();
+	ktimes_ = KernelTimes{};
 	if(S.integrator == INT_PHOTON)
 	{
 		// PhotonIntegrator::preprocess (integrator_photon_mapping.cc:242-638): the photon map is
@@ -726,6 +782,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		cnt[q].n_nee = base_q + 2 * R;
 	}
 	DevStats *dstats = (DevStats *)d.stats.p;
+	S.stats = dstats;
 	const int n_paths = std::max(1, S.path_samples);
 	const int iters = (S.integrator == INT_PATH) ? 2 + n_paths * (S.bounces + 2) : 3;
 
@@ -740,7 +797,6 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		return true;
 	};
 	if(!ensureEvents(2)) return false;
-	size_t ev_i = 2;
 	HIPCHECK(hipEventRecord(d.ev_pool[0], d.stream));
 	// one pass: `n_total` camera samples (the jobs' enumeration, or S.plist x S.spp) through the wavefront
 	// one wavefront pass over the active list started by k_camera / k_spawn
@@ -748,24 +804,21 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		int cur = 0;
 		for(int it = 0; it < iters; ++it)
 		{
-			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i], d.stream));
-			HIPCHECK(yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], dstats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
-			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 1], d.stream));
+			PROF(KK_TRACE, yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], dstats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 			// material-shade dispatch for textured / smooth scenes: surface attributes + shader nodes
 			// of every hit, before k_shade reads them
 			// transparent shadows: filter colours of the transparent surfaces the shadow rays crossed
-			if(S.tr_shad) HIPCHECK(yafamd_launch_tshadow(&S, &d.Q[cur], &cnt[cur], &d.P[cur], d.stream));
-			if(S.has_attr) HIPCHECK(yafamd_launch_surface(&S, &d.Q[cur], &cnt[cur], d.stream));
-			HIPCHECK(yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
+			if(S.tr_shad) PROF(KK_TSHADOW, yafamd_launch_tshadow(&S, &d.Q[cur], &cnt[cur], &d.P[cur], d.stream));
+			if(S.has_attr) PROF(KK_SURFACE, yafamd_launch_surface(&S, &d.Q[cur], &cnt[cur], d.stream));
+			PROF(KK_SHADE, yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
-			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 2], d.stream));
+
 			// photon mapping follows the direct-lighting pipeline: NEE requests in iteration 0, the
 			// photon density estimates of the connected camera hits in iteration 1
 			if(S.integrator == INT_PHOTON && it == 1)
-				HIPCHECK(yafamd_launch_gather(&S, &d.N, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
-			else HIPCHECK(yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));
-			if(rp.profile) HIPCHECK(hipEventRecord(d.ev_pool[ev_i + 3], d.stream));
-			if(rp.profile) ev_i += 4;
+				PROF(KK_GATHER, yafamd_launch_gather(&S, &d.N, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
+			else if(S.ext || !yafamd_shade_fused()) PROF(KK_NEE, yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));
+			// (non-EXT k_shade runs the NEE itself: FUSED)
 			cur ^= 1;
 		}
 		return true;
@@ -776,7 +829,6 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	uint64_t done = 0;
 	auto runSamples = [&](uint64_t n_total) -> bool {
 	done = 0;
-	if(rp.profile && !ensureEvents(ev_i + 4 * (size_t)((n_total + M - 1) / M) * (size_t)iters)) return false;
 	for(uint64_t base = 0; base < n_total; base += M, done = std::min(base, n_total))
 	{
 		if(canceled && *canceled) break;
@@ -789,7 +841,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		}
 		if(S.tree) HIPCHECK(hipMemsetAsync(d.spawn_count.p, 0, 16, d.stream));
 		S.cur_level = 0;
-		HIPCHECK(yafamd_launch_camera(&S, &d.P[0], &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
+		PROF(KK_CAMERA, yafamd_launch_camera(&S, &d.P[0], &d.Q[0], &cnt[0], (const DevJob *)d.jobs.p, n_jobs, base, n, d.stream));
 		if(!iterate(base)) return false;
 		if(!S.tree) continue;
 		// recursiveRaytrace levels: the nodes the last pass spawned are the next pass's active list
@@ -808,19 +860,18 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			const uint32_t total_spawned = std::min(hc[0], S.spawn_cap);
 			if(total_spawned <= done) break;
 			S.cur_level = level;
-			if(rp.profile && !ensureEvents(ev_i + 4 * (size_t)((total_spawned - done + M - 1) / M) * (size_t)iters)) return false;
 			for(uint32_t sub = done; sub < total_spawned; sub += (uint32_t)M)
 			{
 				const int nn = (int)std::min<uint64_t>(M, total_spawned - sub);
-				HIPCHECK(yafamd_launch_spawn(&S, &d.P[0], &d.Q[0], &cnt[0], sub, nn, d.stream));
+				PROF(KK_SPAWN, yafamd_launch_spawn(&S, &d.P[0], &d.Q[0], &cnt[0], sub, nn, d.stream));
 				if(!iterate(base)) return false;
 			}
 			levels.push_back({done, total_spawned});
 			done = total_spawned;
 		}
 		for(size_t k = levels.size(); k-- > 0;)
-			HIPCHECK(yafamd_launch_combine(&S, S.node_base + levels[k].first, S.node_base + levels[k].second, 0, nullptr, nullptr, 0, 0, d.stream));
-		HIPCHECK(yafamd_launch_combine(&S, 0, (uint32_t)n, 1, (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
+			PROF(KK_COMBINE, yafamd_launch_combine(&S, S.node_base + levels[k].first, S.node_base + levels[k].second, 0, nullptr, nullptr, 0, 0, d.stream));
+		PROF(KK_COMBINE, yafamd_launch_combine(&S, 0, (uint32_t)n, 1, (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 		S.cur_level = 0;
 	}
 	return true;
@@ -840,7 +891,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		DevFilm F0 = rp.film;
 		F0.spp = 0;
 		for(const auto &r : owned_rows_)
-			HIPCHECK(yafamd_launch_film(&F0, (const float4 *)d.samples.p, nullptr, (float4 *)d.accum.p, (float4 *)d.film.p,
+			PROF(KK_FILM, yafamd_launch_film(&F0, (const float4 *)d.samples.p, nullptr, (float4 *)d.accum.p, (float4 *)d.film.p,
 			                            (float *)d.weights.p, r.first, r.second, S.clamp_samples, 1, d.stream));
 		samples_total = 0;
 		sampling_offset_ = rp.resume_sampling_offset;
@@ -860,7 +911,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			samples_total = done / (uint64_t)spp * (uint64_t)spp;
 		}
 		for(const auto &r : owned_rows_)
-			HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, done_flags, (float4 *)d.accum.p, (float4 *)d.film.p,
+			PROF(KK_FILM, yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, done_flags, (float4 *)d.accum.p, (float4 *)d.film.p,
 			                            (float *)d.weights.p, r.first, r.second, S.clamp_samples, 0, d.stream));
 		// renderPass sets the sampling offset before its workers start (integrator_tiled.cc:244), so a
 		// canceled pass advances it too
@@ -896,7 +947,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			else
 			{
 				uint32_t count = 0;
-				HIPCHECK(yafamd_aa_next_pass((const float4 *)d.accum.p, (const float *)d.weights.p, W, H, ts, &rp.aa.dev, threshold,
+				PROF(KK_AA, yafamd_aa_next_pass((const float4 *)d.accum.p, (const float *)d.weights.p, W, H, ts, &rp.aa.dev, threshold,
 				                             (uint8_t *)d.aa_flags.p, (uint32_t *)d.aa_plist.p, &count, d.stream));
 				resampled = (int)count;
 				threshold_changed = false;
@@ -931,7 +982,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				if(done < n_total)
 					HIPCHECK(yafamd_launch_done_flags(&S, (const DevJob *)d.jobs.p, n_jobs, (uint32_t)resampled, (uint32_t)(done / (uint64_t)n_pass),
 					                                  (uint8_t *)d.aa_flags.p, d.stream));
-				HIPCHECK(yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (const uint8_t *)d.aa_flags.p, (float4 *)d.accum.p,
+				PROF(KK_FILM, yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (const uint8_t *)d.aa_flags.p, (float4 *)d.accum.p,
 				                            (float4 *)d.film.p, (float *)d.weights.p, 0, H, S.clamp_samples, 1, d.stream));
 				samples_total += done / (uint64_t)n_pass * (uint64_t)n_pass;
 				sampling_offset_ = (uint32_t)(acum + n_pass);   // renderPass: setSamplingOffset(offset + samples), :244
@@ -971,6 +1022,10 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			hs.shadow_rays += b.shadow_rays;
 			hs.node_visits += b.node_visits;
 			hs.tri_tests += b.tri_tests;
+			hs.shade_entries += b.shade_entries;
+			hs.nee_requests += b.nee_requests;
+			hs.gather_queries += b.gather_queries;
+			hs.gather_visits += b.gather_visits;
 		}
 	}
 	stats_.closest_rays = hs.closest_rays;
@@ -985,18 +1040,28 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	stats_.trace_launches = 0;
 	if(rp.profile)
 	{
-		for(size_t e = 2; e + 3 < ev_i + 1; e += 4)
+		for(const Impl::ProfRec &pr : d.prof_recs)
 		{
-			float t = 0.f, u = 0.f, v = 0.f;
-			HIPCHECK(hipEventElapsedTime(&t, d.ev_pool[e], d.ev_pool[e + 1]));
-			HIPCHECK(hipEventElapsedTime(&u, d.ev_pool[e + 1], d.ev_pool[e + 2]));
-			HIPCHECK(hipEventElapsedTime(&v, d.ev_pool[e + 2], d.ev_pool[e + 3]));
-			stats_.trace_kernel_ms += t;
-			stats_.shade_kernel_ms += u;
-			stats_.nee_kernel_ms += v;
-			++stats_.trace_launches;
+			float t = 0.f;
+			HIPCHECK(hipEventElapsedTime(&t, d.ev_pool[pr.e0], d.ev_pool[pr.e1]));
+			ktimes_.ms[pr.kind] += t;
+			++ktimes_.launches[pr.kind];
 		}
+		ktimes_.items[KK_CAMERA] = samples_total;
+		ktimes_.items[KK_FILM] = samples_total;
+		ktimes_.items[KK_TRACE] = hs.closest_rays + hs.shadow_rays;
+		ktimes_.items[KK_SHADE] = hs.shade_entries;
+		ktimes_.items[KK_NEE] = hs.nee_requests;
+		ktimes_.items[KK_GATHER] = hs.gather_queries;
+		ktimes_.items[KK_PHOTON_EMIT] = ktimes_.items[KK_PHOTON_BOUNCE] = (uint64_t)d.pm_paths;
+		ktimes_.items[KK_PHOTON_COMPACT] = ktimes_.items[KK_PHOTON_TREE] = stats_.photons;
+		stats_.trace_kernel_ms = ktimes_.ms[KK_TRACE];
+		stats_.shade_kernel_ms = ktimes_.ms[KK_SHADE];
+		stats_.nee_kernel_ms = ktimes_.ms[KK_NEE] + ktimes_.ms[KK_GATHER];
+		stats_.trace_launches = ktimes_.launches[KK_TRACE];
 	}
+	stats_.gather_visits = hs.gather_visits;
+	d.prof_on = false;
 	return true;
 }
 
@@ -1064,3 +1129,134 @@ bool GpuRenderer::traceRays(bool any, const float *rays, int n, float *t, int *p
 	bp.release();
 	return ok;
 }
+
+// ---------------------------------------------------------------------------------------------
+// render group
+// ---------------------------------------------------------------------------------------------
+#define NCCLCHECK(expr)                                                                                        \
+	do                                                                                                         \
+	{                                                                                                          \
+		const ncclResult_t r_ = (expr);                                                                        \
+		if(r_ != ncclSuccess)                                                                                  \
+		{                                                                                                      \
+			log_.error(std::string("GPU group: ") + #expr + " failed: " + ncclGetErrorString(r_));            \
+			return false;                                                                                      \
+		}                                                                                                      \
+	} while(0)
+
+bool GpuRenderer::joinGroup(int rank, int world, const void *rccl_id, size_t id_bytes)
+{
+	if(!ready()) return false;
+	Impl &d = *d_;
+	if(d.comm)
+	{
+		(void)ncclCommDestroy(d.comm);
+		d.comm = nullptr;
+	}
+	group_rank_ = 0;
+	group_world_ = 1;
+	if(world <= 1) return true;
+	if(rank < 0 || rank >= world || !rccl_id || id_bytes < sizeof(ncclUniqueId))
+	{
+		log_.error("GPU group: bad rank / world / id");
+		return false;
+	}
+	ncclUniqueId id;
+	std::memcpy(&id, rccl_id, sizeof(id));
+	NCCLCHECK(ncclCommInitRank(&d.comm, world, id, rank));
+	group_rank_ = rank;
+	group_world_ = world;
+	std::ostringstream os;
+	os << "GPU group: member " << rank << " of " << world << " (RCCL)";
+	log_.info(os.str());
+	return true;
+}
+
+bool GpuRenderer::groupCombine(const std::vector<int> &bounds, double render_ms, std::vector<double> &all_ms)
+{
+	Impl &d = *d_;
+	const int world = group_world_;
+	all_ms.assign((size_t)world, render_ms);
+	if(world <= 1 || !d.comm) return true;
+	const int W = d.film_w, H = d.film_h;
+	if((int)bounds.size() != world + 1 || bounds.back() != H) { log_.error("GPU group: band bounds do not cover the film"); return false; }
+	int max_rows = 1;
+	for(int r = 0; r < world; ++r) max_rows = std::max(max_rows, bounds[r + 1] - bounds[r]);
+	const size_t band_px = (size_t)max_rows * W;
+	if(!ensure(log_, d.g_send, band_px * sizeof(float4)) || !ensure(log_, d.g_recv, band_px * world * sizeof(float4)) ||
+	   !ensure(log_, d.g_wsend, band_px * sizeof(float)) || !ensure(log_, d.g_wrecv, band_px * world * sizeof(float)) ||
+	   !ensure(log_, d.g_times, 2 * (size_t)world * sizeof(double)))
+		return false;
+	const int y0 = bounds[group_rank_], y1 = bounds[group_rank_ + 1];
+	const size_t row4 = (size_t)W * sizeof(float4), row1 = (size_t)W * sizeof(float);
+	if(y1 > y0)
+	{
+		HIPCHECK(hipMemcpyAsync(d.g_send.p, (char *)d.film.p + row4 * y0, row4 * (y1 - y0), hipMemcpyDeviceToDevice, d.stream));
+		HIPCHECK(hipMemcpyAsync(d.g_wsend.p, (char *)d.weights.p + row1 * y0, row1 * (y1 - y0), hipMemcpyDeviceToDevice, d.stream));
+	}
+	double *times = (double *)d.g_times.p;
+	HIPCHECK(hipMemcpyAsync(times, &render_ms, sizeof(double), hipMemcpyHostToDevice, d.stream));
+	NCCLCHECK(ncclGroupStart());
+	NCCLCHECK(ncclAllGather(d.g_send.p, d.g_recv.p, band_px * 4, ncclFloat32, d.comm, d.stream));
+	NCCLCHECK(ncclAllGather(d.g_wsend.p, d.g_wrecv.p, band_px, ncclFloat32, d.comm, d.stream));
+	NCCLCHECK(ncclAllGather(times, times + world, 1, ncclFloat64, d.comm, d.stream));
+	NCCLCHECK(ncclGroupEnd());
+	for(int r = 0; r < world; ++r)
+	{
+		const int a = bounds[r], b = bounds[r + 1];
+		if(b <= a || r == group_rank_) continue;
+		HIPCHECK(hipMemcpyAsync((char *)d.film.p + row4 * a, (char *)d.g_recv.p + (size_t)r * band_px * sizeof(float4), row4 * (b - a),
+		                        hipMemcpyDeviceToDevice, d.stream));
+		HIPCHECK(hipMemcpyAsync((char *)d.weights.p + row1 * a, (char *)d.g_wrecv.p + (size_t)r * band_px * sizeof(float), row1 * (b - a),
+		                        hipMemcpyDeviceToDevice, d.stream));
+	}
+	HIPCHECK(hipMemcpyAsync(all_ms.data(), times + world, sizeof(double) * world, hipMemcpyDeviceToHost, d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	owned_rows_.assign(1, {0, H});
+	return true;
+}
+
+namespace yafamd
+{
+
+std::vector<int> equalBands(int height, int world)
+{
+	std::vector<int> b((size_t)world + 1);
+	for(int r = 0; r <= world; ++r) b[r] = (int)((int64_t)height * r / world);
+	return b;
+}
+
+std::vector<int> rebalanceBands(const std::vector<int> &bounds, const std::vector<double> &times, int cap_rows)
+{
+	const int world = (int)bounds.size() - 1;
+	const int H = bounds.back();
+	if(world <= 1 || H < world || (int)times.size() < world) return bounds;
+	std::vector<double> cum((size_t)H + 1, 0.0);
+	{
+		std::vector<double> dens((size_t)H, 0.0);
+		for(int r = 0; r < world; ++r)
+		{
+			const int rows = bounds[r + 1] - bounds[r];
+			if(rows > 0)
+				for(int y = bounds[r]; y < bounds[r + 1]; ++y) dens[y] = std::max(times[r], 1e-9) / rows;
+		}
+		for(int y = 0; y < H; ++y) cum[y + 1] = cum[y] + dens[y];
+	}
+	std::vector<int> nb(1, 0);
+	for(int r = 1; r < world; ++r)
+	{
+		const double target = cum[H] * r / world;
+		int y = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+		if(y > 0 && y <= H && (cum[y] - target) > (target - cum[y - 1])) --y;
+		y = (int)std::nearbyint(0.5 * bounds[r] + 0.5 * y);   // round half to even, as Python's round()
+		nb.push_back(y);
+	}
+	nb.push_back(H);
+	for(int r = 1; r < world; ++r) nb[r] = std::min(std::max(nb[r], nb[r - 1] + 1), H - (world - r));
+	if(cap_rows > 0)
+		for(int r = 0; r < world; ++r)
+			if(nb[r + 1] - nb[r] > cap_rows) return bounds;
+	return nb;
+}
+
+} // namespace yafamd

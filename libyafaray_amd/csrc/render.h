@@ -61,6 +61,27 @@ struct AaParams
 	DevAaParams dev{0, 0, 0.f, 10, 0};
 };
 
+// Kernel kinds timed by the profile mode (HIP events around every launch on the render stream)
+enum KernelKind : int
+{
+	KK_CAMERA = 0, KK_TRACE, KK_SURFACE, KK_TSHADOW, KK_SHADE, KK_NEE, KK_GATHER, KK_SPAWN, KK_COMBINE, KK_FILM, KK_AA,
+	KK_PHOTON_EMIT, KK_PHOTON_BOUNCE, KK_PHOTON_COMPACT, KK_PHOTON_TREE, KK_COUNT
+};
+inline const char *kernelKindName(int k)
+{
+	static const char *n[KK_COUNT] = {"k_camera", "k_trace", "k_surface", "k_tshadow", "k_shade", "k_nee", "k_gather", "k_spawn",
+	                                  "k_combine", "k_film", "aa_next_pass", "k_photon_emit", "k_photon_bounce", "photon_compact",
+	                                  "pkd_build"};
+	return (k >= 0 && k < KK_COUNT) ? n[k] : "";
+}
+struct KernelTimes
+{
+	double ms[KK_COUNT] = {};
+	uint64_t launches[KK_COUNT] = {};
+	uint64_t items[KK_COUNT] = {};   // work units: samples (camera, film), rays (trace), entries (shade),
+	                                 // requests (nee), queries (gather), photon paths (emit, bounce), photons (tree)
+};
+
 struct RenderParams
 {
 	DevScene scene;                      // pointers filled by the renderer
@@ -101,7 +122,20 @@ class GpuRenderer
 		bool filmToDevice(void *dst, int y0, int y1);
 		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
 		bool buildPhotonMap(RenderParams &rp);
+
+		// ---- render group: the film split into contiguous row bands over several GPUs ----
+		// One member per GPU (one process per GPU, each calling joinGroup with the same RCCL id).
+		// After a member rendered its band (RenderParams shard_mode 2), groupCombine all-gathers every
+		// member's band rows (normalised RGBA + weights) and render time over RCCL into this member's
+		// film, so every member ends with the whole frame; the band boundaries for the next frame
+		// come from rebalanceBands over the gathered times.  imagesplitter.cc:30-107 partitions the
+		// reference's film into tiles for threads; imagefilm.cc:997-1008 sums film files of nodes.
+		bool joinGroup(int rank, int world, const void *rccl_id, size_t id_bytes);
+		bool groupCombine(const std::vector<int> &bounds, double render_ms, std::vector<double> &all_ms);
+		int groupRank() const { return group_rank_; }
+		int groupWorld() const { return group_world_; }
 		const yafaray_amd_stats_t &stats() const { return stats_; }
+		const KernelTimes &kernelTimes() const { return ktimes_; }
 		std::vector<std::pair<int, int>> ownedRows() const { return owned_rows_; }
 
 		struct Impl;
@@ -110,9 +144,19 @@ class GpuRenderer
 		Impl *d_;
 		Logger &log_;
 		yafaray_amd_stats_t stats_{};
+		KernelTimes ktimes_{};
 		std::vector<std::pair<int, int>> owned_rows_;
 		int passes_done_ = 0;
+		int group_rank_ = 0, group_world_ = 1;
 		uint32_t sampling_offset_ = 0;
 };
+
+// Band boundaries (world + 1 rows) moved towards equal cost from each band's last render time:
+// each band's time is spread evenly over its rows (piecewise-constant cost density), boundaries
+// move half way to the equal-cost split, every band keeps >= 1 row; a result with a band above
+// cap_rows rows (0: no cap) keeps the old bounds.  Pure and deterministic, so every group member
+// computes the same bounds from the same gathered times (libyafaray_amd/tiles.py mirrors it).
+std::vector<int> rebalanceBands(const std::vector<int> &bounds, const std::vector<double> &times, int cap_rows);
+std::vector<int> equalBands(int height, int world);
 
 } // namespace yafamd

@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(product):
     assert not missing, missing
     # the reference's names carry the reference's version node
     assert all(syms[s] == "LIBYAFARAY_4.0.0" for s in api), {s: syms[s] for s in api if syms[s] != "LIBYAFARAY_4.0.0"}
-    assert all(syms[s] == "LIBYAFARAY_AMD_1.0" for s in ext)
+    assert all(syms[s].startswith("LIBYAFARAY_AMD_1.") for s in ext), {s: syms[s] for s in ext}
     # nothing else leaks out (reference: CXX_VISIBILITY_PRESET hidden, src/CMakeLists.txt:22)
     assert set(syms) == api | ext, sorted(set(syms) - api - ext)[:10]
 

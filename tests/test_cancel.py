@@ -16,13 +16,14 @@ from libyafaray_amd import scenes
 pytestmark = pytest.mark.gpu
 
 
-def pixel_rank(W, H, ts):
-    """Rank of every pixel in the linear tile order (imagesplitter.cc:30-49)."""
+def sample_rank(W, H, ts):
+    """Rank of every pixel in the GPU's sample enumeration of a one-band render (render.cc jobs,
+    kernels.hip sampleCoord): strips of `ts` columns over the band's rows, left to right, pixels
+    row-major inside a strip.  Chunks complete in this order."""
     y, x = np.mgrid[0:H, 0:W]
-    ty, tx = y // ts, x // ts
-    th = np.minimum(ts, H - ty * ts)
+    tx = x // ts
     tw = np.minimum(ts, W - tx * ts)
-    return ty * ts * W + tx * ts * th + (y - ty * ts) * tw + (x - tx * ts)
+    return tx * ts * H + y * tw + (x - tx * ts)
 
 
 def render(product, spec, chunk, cancel_after=None):
@@ -58,7 +59,7 @@ def test_cancel_between_chunks(product, cancel_after):
     # progress reports are monotone and end before the whole frame
     dones = [c[1] for c in calls]
     assert dones == sorted(dones) and max(dones) < W * H
-    rank = pixel_rank(W, H, ts)
+    rank = sample_rank(W, H, ts)
     rendered = rank < done_pix
     # box-1 footprint: a pixel collects samples from itself, its left, upper and upper-left neighbours
     src = np.zeros((H + 1, W + 1, 4), bool)

@@ -277,3 +277,17 @@ def test_photon_mapping_matches_oracle(product, oracle_built, bvh, monkeypatch):
     assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
     d = ulp_diff(rgba, orgba)
     assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
+
+
+@pytest.mark.parametrize("photons", [120, 400000])
+def test_photon_map_sizes_match_oracle(product, oracle_built, photons):
+    """Photon-map sizes on both sides of the GPU kd-tree build's phase switch (pkd.hip: subtrees of
+    <= 256 photons are finished in LDS, larger nodes are split level by level across the chip):
+    ~240 photons (LDS phase only) and ~800 K photons (11 top levels)."""
+    spec = scenes.cornell_photon(48, 36, spp=1, photons=photons, search=50, radius=0.1)
+    rgba, w, st = product.render_spec(spec)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    d = ulp_diff(rgba, orgba)
+    assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
+    assert st["gather_visits"] > 0

@@ -130,3 +130,18 @@ def test_rebalance_bands_moves_towards_equal_cost():
     assert tiles.rebalance_bands([0, 3], [1.0]) == [0, 3]
     tiny = tiles.rebalance_bands([0, 1, 2, 3], [5.0, 1.0, 1.0])
     assert tiny == [0, 1, 2, 3]
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_library_band_balancer_matches_python(product, world):
+    """yafaray_amd_rebalanceBands (the in-library group's balancer, C++) == tiles.rebalance_bands."""
+    rng = np.random.default_rng(world)
+    for H in (70, 1080):
+        bounds = tiles_bounds = [H * r // world for r in range(world + 1)]
+        for _ in range(6):
+            times = list(rng.uniform(0.5, 2.0, world))
+            lib = product.rebalance_bands(bounds, times)
+            py = tiles.rebalance_bands(tiles_bounds, times)
+            assert lib == [int(v) for v in py], (lib, py)
+            assert lib[0] == 0 and lib[-1] == H and all(b > a for a, b in zip(lib, lib[1:]))
+            bounds = tiles_bounds = lib

@@ -9,5 +9,5 @@ for spec in "$@"; do
 	echo "== $spec" >> $R/gpurun_out/sweep_$TAG.log
 	envs=()
 	if [ -n "$rest" ]; then IFS=: read -ra envs <<< "$rest"; fi
-	env "${envs[@]}" YAFARAY_AMD_LIB=$R/libyafaray_amd/variants/$v.so timeout -k 10 ${BENCH_TIMEOUT:-150} python $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 ${BENCH_ARGS} >> $R/gpurun_out/sweep_$TAG.log 2>&1
+	env "${envs[@]}" YAFARAY_AMD_LIB=$R/libyafaray_amd/variants/$v.so timeout -k 10 ${BENCH_TIMEOUT:-150} python $R/bench.py --no-cpu-baseline --no-parity --steps 2 --warmup 1 ${BENCH_ARGS} >> $R/gpurun_out/sweep_$TAG.log 2>&1
 done
