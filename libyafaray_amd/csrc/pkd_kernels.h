@@ -1,0 +1,413 @@
+// Device code of the photon kd-tree build (pkd.hip): node splitting, partitions and the LDS
+// subtree kernel.  Kept apart from the host driver so tools/pkd_emu.cc can run the same kernels
+// on CPU threads (one std::thread per lane, barriers for __syncthreads) under ThreadSanitizer.
+#pragma once
+
+// Checked build (-DPKD_CHECK, tools/pkd_check.py): every computed index is range-checked before
+// use; a failure records the first offending source line and the index is clamped, so a broken
+// invariant shows up as a line number instead of a memory fault.
+#ifdef PKD_CHECK
+__device__ uint32_t g_pkd_err;
+#define PK_GUARD(cond, idx) do { if(!(cond)) { atomicCAS(&g_pkd_err, 0u, (uint32_t)__LINE__); (idx) = 0; } } while(0)
+#else
+#define PK_GUARD(cond, idx) do {} while(0)
+#endif
+
+namespace yafamd_pkd
+{
+
+constexpr int kSub = 256;           // subtree size finished by one workgroup in LDS (~51 KB of LDS)
+constexpr int kSubThreads = 256;
+
+struct Seg
+{
+	uint32_t node, start, end;   // tree node and its photon range in the lists
+	float lo[3], hi[3];          // node bound (pkdtree.h:152-160)
+};
+
+// per node of the current top level: split axis and median element
+struct Split
+{
+	uint32_t axis, split_el, med_key, med_idx;
+};
+
+// Component selects on values already in registers.  Taking the record by reference let the
+// compiler turn the select into a branchy address computation whose lowering dropped the axis-2
+// case in one unrolled copy of the flag loop (the key was then read from LDS address 0); loading
+// the whole record first keeps the selects as v_cndmask.
+__device__ __forceinline__ float coordOf(const float4 p, int a)
+{
+	float c = p.x;
+	c = (a == 1) ? p.y : c;
+	c = (a == 2) ? p.z : c;
+	return c;
+}
+__device__ __forceinline__ uint32_t keyOf(const uint4 r, int a)
+{
+	uint32_t k = r.x;
+	k = (a == 1) ? r.y : k;
+	k = (a == 2) ? r.z : k;
+	return k;
+}
+
+// orderable key of a float coordinate; -0 and +0 compare equal in the reference's comparator
+__device__ __forceinline__ uint32_t orderKey(float f)
+{
+	if(f == 0.f) f = 0.f;
+	const uint32_t u = __float_as_uint(f);
+	return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// "left of the median" in the (coordinate, index) order of `axis`
+__device__ __forceinline__ bool leftOf(const uint4 r, uint32_t axis, uint32_t med_key, uint32_t med_idx)
+{
+	const uint32_t k = keyOf(r, (int)axis);
+	return k < med_key || (k == med_key && r.w < med_idx);
+}
+
+// bound.h:111-115 largestAxis
+__device__ __forceinline__ int largestAxis(const float *lo, const float *hi)
+{
+	const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+	return (dx > dy) ? ((dx > dz) ? 0 : 2) : ((dy > dz) ? 1 : 2);
+}
+
+__global__ void k_keys(const float4 *pos, uint32_t n, uint32_t *kx, uint32_t *ky, uint32_t *kz, uint32_t *iota)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const float4 p = pos[i];
+	kx[i] = orderKey(p.x);
+	ky[i] = orderKey(p.y);
+	kz[i] = orderKey(p.z);
+	iota[i] = i;
+}
+
+__global__ void k_records(const uint32_t *sorted_idx, uint32_t n, const uint32_t *kx, const uint32_t *ky, const uint32_t *kz, uint4 *rec)
+{
+	const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+	if(p >= n) return;
+	const uint32_t i = sorted_idx[p];
+	rec[p] = make_uint4(kx[i], ky[i], kz[i], i);
+}
+
+// root bound (pkdtree.h:98-101): per-workgroup min/max, then one workgroup folds the partials
+__global__ void k_bound(const float4 *pos, uint32_t n, float *partial /* gridDim.x * 6 */)
+{
+	float v[6] = {3.4e38f, 3.4e38f, 3.4e38f, -3.4e38f, -3.4e38f, -3.4e38f};
+	for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+	{
+		const float4 p = pos[i];
+		v[0] = fminf(v[0], p.x); v[1] = fminf(v[1], p.y); v[2] = fminf(v[2], p.z);
+		v[3] = fmaxf(v[3], p.x); v[4] = fmaxf(v[4], p.y); v[5] = fmaxf(v[5], p.z);
+	}
+	__shared__ float red[6][256];
+	for(int k = 0; k < 6; ++k) red[k][threadIdx.x] = v[k];
+	__syncthreads();
+	for(int w = blockDim.x / 2; w > 0; w >>= 1)
+	{
+		if((int)threadIdx.x < w)
+		{
+			for(int k = 0; k < 3; ++k) red[k][threadIdx.x] = fminf(red[k][threadIdx.x], red[k][threadIdx.x + w]);
+			for(int k = 3; k < 6; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + w]);
+		}
+		__syncthreads();
+	}
+	if(threadIdx.x < 6) partial[blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// fold the partials (256 threads) and create the root segment
+__global__ void k_root(const float *partial, uint32_t n_part, uint32_t n, Seg *segs)
+{
+	__shared__ float red[6][256];
+	float v[6] = {3.4e38f, 3.4e38f, 3.4e38f, -3.4e38f, -3.4e38f, -3.4e38f};
+	for(uint32_t b = threadIdx.x; b < n_part; b += blockDim.x)
+	{
+		for(int k = 0; k < 3; ++k) v[k] = fminf(v[k], partial[b * 6 + k]);
+		for(int k = 3; k < 6; ++k) v[k] = fmaxf(v[k], partial[b * 6 + k]);
+	}
+	for(int k = 0; k < 6; ++k) red[k][threadIdx.x] = v[k];
+	__syncthreads();
+	for(int w = blockDim.x / 2; w > 0; w >>= 1)
+	{
+		if((int)threadIdx.x < w)
+		{
+			for(int k = 0; k < 3; ++k) red[k][threadIdx.x] = fminf(red[k][threadIdx.x], red[k][threadIdx.x + w]);
+			for(int k = 3; k < 6; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + w]);
+		}
+		__syncthreads();
+	}
+	if(threadIdx.x == 0)
+	{
+		Seg g;
+		g.node = 0;
+		g.start = 0;
+		g.end = n;
+		for(int k = 0; k < 3; ++k)
+		{
+			g.lo[k] = red[k][0];
+			g.hi[k] = red[3 + k][0];
+		}
+		segs[0] = g;
+	}
+}
+
+// ---- top phase (one level: every node splits in two) ----
+__global__ void k_level_split(const Seg *segs, uint32_t n_seg, uint32_t n, const uint4 *rx, const uint4 *ry, const uint4 *rz, const float4 *pos,
+                              uint4 *nodes, Split *splits, Seg *next)
+{
+	uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+	if(s >= n_seg) return;
+	const Seg g = segs[s];
+	const int axis = largestAxis(g.lo, g.hi);
+	uint32_t se = (g.start + g.end) / 2;
+	PK_GUARD(g.start < se && g.end <= n, se);
+	uint4 med = (axis == 0 ? rx : (axis == 1 ? ry : rz))[se];
+	PK_GUARD(med.w < n, med.w);
+	const float split_pos = coordOf(pos[med.w], axis);
+	const uint32_t nl = se - g.start;
+	uint32_t right = g.node + 2u * nl;
+	uint32_t nd = g.node;
+	PK_GUARD(right < 2 * n - 1 && nd < right, nd);
+	PK_GUARD(2 * s + 1 < n, s);
+	nodes[nd] = make_uint4(__float_as_uint(split_pos), 0u, 0u, (uint32_t)axis | (right << 2));
+	splits[s] = {(uint32_t)axis, se, keyOf(med, axis), med.w};
+	Seg l = g, r = g;
+	l.node = g.node + 1;
+	l.end = se;
+	l.hi[axis] = split_pos;
+	r.node = right;
+	r.start = se;
+	r.lo[axis] = split_pos;
+	next[2 * s] = l;
+	next[2 * s + 1] = r;
+}
+
+// the scan input of the stable partitions: 1 for entries left of their node's median
+struct LeftFlag
+{
+	const uint4 *rec;
+	const uint32_t *seg_of;
+	const Split *splits;
+	uint32_t n;
+	__host__ __device__ uint32_t operator()(const uint32_t &p_in) const
+	{
+		uint32_t p = p_in;
+		PK_GUARD(p < n, p);
+		uint32_t so = seg_of[p];
+		PK_GUARD(so < n, so);
+		const Split sp = splits[so];
+		const uint4 r = rec[p];
+		return leftOf(r, sp.axis, sp.med_key, sp.med_idx) ? 1u : 0u;
+	}
+};
+
+__global__ void k_partition(const uint4 *rec, uint32_t n, const uint32_t *scan, const uint32_t *seg_of, const Seg *segs, const Split *splits,
+                            uint4 *out)
+{
+	const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+	if(p >= n) return;
+	uint32_t s = seg_of[p];
+	PK_GUARD(s < n, s);
+	const Split sp = splits[s];
+	const uint4 r = rec[p];
+	const uint32_t start = segs[s].start;
+	const uint32_t left_before = scan[p] - scan[start];
+	uint32_t np = leftOf(r, sp.axis, sp.med_key, sp.med_idx) ? start + left_before : sp.split_el + ((p - start) - left_before);
+	PK_GUARD(np < n, np);
+	out[np] = r;
+}
+
+__global__ void k_seg_of(uint32_t *seg_of, uint32_t n, const Split *splits)
+{
+	const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+	if(p >= n) return;
+	uint32_t s = seg_of[p];
+	PK_GUARD(s < n, s);
+	seg_of[p] = 2u * s + (p < splits[s].split_el ? 0u : 1u);
+}
+
+// ---- bottom phase: one workgroup per subtree of <= kSub photons ----
+// One lane per list entry and per segment (kSub == kSubThreads): the three lists of the subtree
+// sit in LDS (in / out buffers); per level every segment either becomes a leaf or splits at the
+// median of its largest bound axis; the stable partitions take their offsets from wave ballots
+// (prefix popcounts + four per-wave totals) instead of a shared-memory scan.  Three barriers per
+// level.  The rule and node numbering are the top phase's, restricted to the workgroup's range.
+struct LSeg
+{
+	uint32_t node, start, end;   // start / end relative to the subtree's first element
+	float lo[3], hi[3];
+};
+
+constexpr int kSubWaves = kSubThreads / 64;
+static_assert(kSub == kSubThreads && kSubWaves == 4, "one lane per entry, four waves");
+
+__device__ __forceinline__ uint32_t lanePrefix(uint64_t ballot)
+{
+	return (uint32_t)__popcll(ballot & __lanemask_lt());
+}
+
+__global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const uint4 *gx, const uint4 *gy, const uint4 *gz, const float4 *pos,
+                                                        uint4 *nodes, uint32_t n, int base_level, int *max_level)
+{
+	constexpr uint16_t kNone = 0xffffu;
+	__shared__ uint4 buf[2][3][kSub];
+	__shared__ uint32_t scan[3][kSub];         // exclusive count of left-going entries before e, per list
+	__shared__ LSeg lsegs[2][kSub];
+	__shared__ Split lsplit[kSub];
+	__shared__ uint32_t cb[kSub];              // first child segment of splitting segment s
+	__shared__ uint16_t seg_of[kSub];          // segment of entry position e (kNone once a leaf)
+	__shared__ uint32_t wsum[4][kSubWaves];    // per-wave ballot totals: lists 0-2, splitting segments
+	const Seg g = segs[blockIdx.x];
+	uint32_t m = g.end - g.start;
+	PK_GUARD(m >= 1 && m <= (uint32_t)kSub && g.end <= n, m);
+	const uint32_t t = threadIdx.x, wv = t >> 6;
+	const bool act = t < m;
+	if(act)
+	{
+		buf[0][0][t] = gx[g.start + t];
+		buf[0][1][t] = gy[g.start + t];
+		buf[0][2][t] = gz[g.start + t];
+	}
+	seg_of[t] = act ? 0 : kNone;
+	if(t == 0)
+	{
+		LSeg l;
+		l.node = g.node;
+		l.start = 0;
+		l.end = m;
+		for(int k = 0; k < 3; ++k) { l.lo[k] = g.lo[k]; l.hi[k] = g.hi[k]; }
+		lsegs[0][0] = l;
+	}
+	__syncthreads();
+	int cur = 0, cs = 0, level = base_level;
+	uint32_t ns = 1;
+	for(;;)
+	{
+		// (1) segment t: a leaf (one photon, pkdtree.h:29-33) or a split at the median of its largest axis
+		bool split = false;
+		if(t < ns)
+		{
+			const LSeg l = lsegs[cs][t];
+			if(l.end - l.start == 1)
+			{
+				uint32_t idx = buf[cur][0][l.start].w;
+				PK_GUARD(idx < n, idx);
+				const float4 ph = pos[idx];
+				uint32_t nd = l.node;
+				PK_GUARD(nd < 2 * n - 1, nd);
+				nodes[nd] = make_uint4(__float_as_uint(ph.x), __float_as_uint(ph.y), __float_as_uint(ph.z), 3u | (idx << 2));
+				lsplit[t] = {3u, 0u, 0u, 0u};
+			}
+			else
+			{
+				const int axis = largestAxis(l.lo, l.hi);
+				uint32_t se = (l.start + l.end) / 2;
+				PK_GUARD(se > l.start && l.end <= m, se);
+				uint4 med = buf[cur][axis][se];
+				PK_GUARD(med.w < n, med.w);
+				const float split_pos = coordOf(pos[med.w], axis);
+				const uint32_t right = l.node + 2u * (se - l.start);
+				uint32_t nd = l.node;
+				PK_GUARD(right < 2 * n - 1, nd);
+				nodes[nd] = make_uint4(__float_as_uint(split_pos), 0u, 0u, (uint32_t)axis | (right << 2));
+				lsplit[t] = {(uint32_t)axis, se, keyOf(med, axis), med.w};
+				split = true;
+			}
+		}
+		const uint64_t bs = __ballot(split);
+		if((t & 63) == 0) wsum[3][wv] = (uint32_t)__popcll(bs);
+		__syncthreads();
+		uint32_t n_split = 0, split_before = 0;
+		for(uint32_t w = 0; w < (uint32_t)kSubWaves; ++w)
+		{
+			const uint32_t c = wsum[3][w];
+			split_before += (w < wv) ? c : 0u;
+			n_split += c;
+		}
+		if(n_split == 0)
+		{
+			// every segment of this level was a leaf: the deepest level of this subtree
+			if(t == 0) atomicMax(max_level, level);
+			break;
+		}
+		if(split) cb[t] = 2u * (split_before + lanePrefix(bs));
+		// (2) left-of-median flags of the three lists, prefix counts from ballots
+		uint16_t so = seg_of[t];
+		Split sp = {3u, 0u, 0u, 0u};
+		if(so != kNone)
+		{
+			PK_GUARD(so < ns, so);
+			sp = lsplit[so];
+		}
+		const bool part = sp.axis != 3u;
+		uint4 r[3];
+		uint32_t pre[3];
+		bool f[3];
+		for(int a = 0; a < 3; ++a)
+		{
+			r[a] = act ? buf[cur][a][t] : make_uint4(0u, 0u, 0u, 0u);
+			f[a] = part && leftOf(r[a], sp.axis, sp.med_key, sp.med_idx);
+			const uint64_t b = __ballot(f[a]);
+			pre[a] = lanePrefix(b);
+			if((t & 63) == 0) wsum[a][wv] = (uint32_t)__popcll(b);
+		}
+		__syncthreads();
+		for(int a = 0; a < 3; ++a)
+		{
+			uint32_t off = 0;
+			for(uint32_t w = 0; w < wv; ++w) off += wsum[a][w];
+			pre[a] += off;
+			scan[a][t] = pre[a];
+		}
+		__syncthreads();
+		// (3) scatter (entries of leaves stay put), the next level's segments and entry segments
+		if(act)
+		{
+			uint16_t nso = kNone;
+			if(part)
+			{
+				const uint32_t start = lsegs[cs][so].start;
+				for(int a = 0; a < 3; ++a)
+				{
+					const uint32_t left_before = pre[a] - scan[a][start];
+					uint32_t np = f[a] ? start + left_before : sp.split_el + ((t - start) - left_before);
+					PK_GUARD(np < m, np);
+					buf[cur ^ 1][a][np] = r[a];
+				}
+				nso = (uint16_t)(cb[so] + (t < sp.split_el ? 0u : 1u));
+			}
+			else
+				for(int a = 0; a < 3; ++a) buf[cur ^ 1][a][t] = r[a];
+			seg_of[t] = nso;
+		}
+		if(split)
+		{
+			const LSeg l = lsegs[cs][t];
+			const Split ls = lsplit[t];
+			const float split_pos = coordOf(pos[ls.med_idx], (int)ls.axis);
+			uint32_t c0 = cb[t];
+			PK_GUARD(c0 + 1 < 2 * n_split, c0);
+			LSeg lo = l, hi = l;
+			lo.node = l.node + 1;
+			lo.end = ls.split_el;
+			hi.node = l.node + 2u * (ls.split_el - l.start);
+			hi.start = ls.split_el;
+			// lo.hi[axis] = hi.lo[axis] = split position, written without a dynamic array index
+			for(int k = 0; k < 3; ++k)
+			{
+				lo.hi[k] = (k == (int)ls.axis) ? split_pos : l.hi[k];
+				hi.lo[k] = (k == (int)ls.axis) ? split_pos : l.lo[k];
+			}
+			lsegs[cs ^ 1][c0] = lo;
+			lsegs[cs ^ 1][c0 + 1] = hi;
+		}
+		ns = 2u * n_split;
+		cur ^= 1;
+		cs ^= 1;
+		++level;
+		__syncthreads();
+	}
+}
+
+} // namespace yafamd_pkd
