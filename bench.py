@@ -76,7 +76,7 @@ def pmc_config(a, W, H):
 def kernels_src_sha1():
     import hashlib
     h = hashlib.sha1()
-    for f in ("kernels.hip", "pkd.hip", "aa.hip"):
+    for f in ("kernels.hip", "pkd.hip", "pkd_kernels.h", "aa.hip"):
         with open(os.path.join(ROOT, "libyafaray_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()

@@ -2634,13 +2634,25 @@ __global__ void __launch_bounds__(1024) k_photon_scatter(PhotonState P, uint32_t
 // ---------------------------------------------------------------------------------------------
 constexpr int kGatherBlock = 64;
 constexpr int kGatherPerSeg = 4;   // workgroups per queue segment (fills the chip: 4 x 1024 x 64 lanes)
+#ifndef YAF_GATHER_STACK_LDS
+#define YAF_GATHER_STACK_LDS 0     // 1: lookup stack in LDS (8 B x depth per lane) instead of HBM
+#endif
+#ifndef YAF_GATHER_XCD
+#define YAF_GATHER_XCD 1           // 1: each XCD gathers a contiguous eighth of the segments (L2 locality)
+#endif
 //
-// Occupancy is the lever (a kd walk is a chain of dependent loads): the 50-entry heap stays in LDS
-// (8 B per entry and lane, the only per-lane LDS), the lookup stack lives in a per-lane HBM column
-// (pushes are fire-and-forget stores, pops hit L2: a 64-lane workgroup's stack is <= 14 KB), leaf
-// nodes carry their photon's position (one dependent load per leaf instead of two), and no Faure
-// tables are staged.  Result: ~25 KB LDS per 64 lanes instead of ~45 KB.
-
+// The walk is latency-bound (a chain of dependent loads, 64 lanes on 64 neighbouring pixels), so
+// the levers are occupancy, coherence and L2 locality (C5 measurements):
+//   * the only per-lane LDS is the k-entry heap; one 8-byte slot = index + distance, so a sift step
+//     moves a slot with one 64-bit access.  The lookup stack is a per-lane HBM column (pushes are
+//     fire-and-forget stores, pops hit L2): an LDS stack costs occupancy and measured slower;
+//   * a far child whose plane distance already exceeds the current radius is never pushed (the
+//     reference pushes it and discards it when popped; the radius never grows, so the visit order
+//     and the heap are unchanged) — 53 -> 42 ms;
+//   * workgroups are renumbered so that each XCD walks the photons of a contiguous eighth of the
+//     image (56 -> 53 ms);
+//   * tried and dropped: one node per loop trip (if-if, 67 ms), lanes refilling independently with
+//     the estimate in a second kernel (lanes drift apart and stop sharing cache lines, 59-70 ms).
 struct GatherArgs
 {
 	DevScene S;
@@ -2657,9 +2669,28 @@ __host__ __device__ inline size_t gatherTableBytes(const DevScene &S, bool small
 	return small ? (size_t)S.n_mats * sizeof(DevMaterial) + (size_t)S.n_tris * 16 : 0;
 }
 
-__host__ __device__ inline size_t gatherLdsBytes(const DevScene &S, bool small)
+__host__ __device__ inline size_t gatherLdsBytes(const DevScene &S)
 {
-	return gatherTableBytes(S, small) + (size_t)kGatherBlock * 8u * (size_t)S.pm_search;
+	return (size_t)kGatherBlock * 8u * (size_t)S.pm_search + (YAF_GATHER_STACK_LDS ? (size_t)kGatherBlock * 8u * (size_t)S.pm_stack : 0u);
+}
+
+// workgroups are dealt to the 8 XCDs round-robin: renumber them so that XCD x gets the contiguous
+// run of segments [x, x + 1) * n_seg / 8 (neighbouring pixels -> one L2)
+__device__ __forceinline__ void gatherSegPart(uint32_t n_seg, uint32_t &seg, uint32_t &part, uint32_t &parts)
+{
+	const uint32_t nb = gridDim.x;
+	parts = nb / n_seg;
+	if(YAF_GATHER_XCD && (nb & 7u) == 0)
+	{
+		const uint32_t v = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
+		seg = v / parts;
+		part = v % parts;
+	}
+	else
+	{
+		seg = blockIdx.x % n_seg;
+		part = blockIdx.x / n_seg;
+	}
 }
 
 template<bool SMALL, bool EXT>
@@ -2683,14 +2714,19 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 	uint32_t *lds_words = reinterpret_cast<uint32_t *>(gather_smem) + gatherTableBytes(A.S, SMALL) / 4;
 	const int k = S.pm_search;
 	const int lane = threadIdx.x;
-	HeapRef heap;
-	heap.idx = lds_words + lane;
-	heap.dist = reinterpret_cast<float *>(lds_words + (size_t)k * kGatherBlock) + lane;
+	HeapRefPacked heap;
+	heap.e = lds_words + 2 * lane;
 	heap.stride = kGatherBlock;
-	// lookup stack: this lane's column of the HBM stack buffer, [level][global lane]
+	// lookup stack: this lane's column, [level][lane] (LDS after the heap, or the HBM stack buffer)
+#if YAF_GATHER_STACK_LDS
+	const uint32_t gstride = kGatherBlock;
+	uint2 *stk = reinterpret_cast<uint2 *>(lds_words + (size_t)2 * k * kGatherBlock) + threadIdx.x;
+#else
 	const uint32_t gstride = gridDim.x * kGatherBlock;
 	uint2 *stk = S.pk_stack + blockIdx.x * kGatherBlock + threadIdx.x;
-	const uint32_t seg = blockIdx.x % S.n_seg, part = blockIdx.x / S.n_seg, parts = gridDim.x / S.n_seg;
+#endif
+	uint32_t seg, part, parts;
+	gatherSegPart(S.n_seg, seg, part, parts);
 	const uint32_t n_req = A.cnt_next.n_nee[seg];
 	const uint32_t a0 = seg * S.cap_a;
 	uint32_t visits = 0;
@@ -2698,15 +2734,8 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 	{
 		if(base_j + threadIdx.x >= n_req) continue;
 		const uint32_t j = a0 + base_j + threadIdx.x;
-		const float4 pp = A.N.p_prim[j], wk = A.N.wo_k[j];
-		const uint4 cb = A.N.pix_mode[j];
+		const float4 pp = A.N.p_prim[j];
 		const V3 p = xyz(pp);
-		Surf sp = surfFromPrim(S, p, __float_as_int(pp.w));
-		if(ATTR) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
-		const V3 wo = xyz(wk);
-		const uint32_t sid = __float_as_uint(wk.w);
-		C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)};
-		const float alpha = __uint_as_float(cb.w);
 		// ---- k-NN lookup (pkdtree.h:225-292, NON_REC_LOOKUP) ----
 		// nodes: .w = flags (bits 0-1 axis, 3 = leaf; interior: right child << 2, leaf: photon << 2),
 		// interior .x = split position; leaf .xyz = the photon's position
@@ -2726,14 +2755,21 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 				uint32_t far_child;
 				if(pa <= split_val) { far_child = nd.w >> 2; curr = curr + 1; }
 				else { far_child = curr + 1; curr = nd.w >> 2; }
-				stk[(size_t)sp_top * gstride] = make_uint2(far_child | ((uint32_t)axis << 30), nd.x);
-				++sp_top;
+				// the reference pushes every far child and discards it at pop time when (p - split)^2 >
+				// max_d2; max_d2 never grows, so one that already fails now is never visited
+				float d2 = pa - split_val;
+				d2 *= d2;
+				if(d2 <= max_d2)
+				{
+					stk[(size_t)sp_top * gstride] = make_uint2(far_child, __float_as_uint(d2));
+					++sp_top;
+				}
 				nd = S.pk_nodes[curr];
 				++visits;
 			}
 			const uint32_t ph = nd.w >> 2;
 			const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
-			float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
+			const float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
 			if(dist_2 < max_d2)
 			{
 				// photon.cc:31-52
@@ -2756,26 +2792,26 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 			}
 			if(sp_top == 0) break;
 			uint2 top = stk[(size_t)(sp_top - 1) * gstride];
-			int axis = (int)(top.x >> 30);
-			float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
-			dist_2 = pa - __uint_as_float(top.y);
-			dist_2 *= dist_2;
 			bool done = false;
-			while(dist_2 > max_d2)
+			while(__uint_as_float(top.y) > max_d2)
 			{
 				--sp_top;
 				if(sp_top == 0) { done = true; break; }
 				top = stk[(size_t)(sp_top - 1) * gstride];
-				axis = (int)(top.x >> 30);
-				pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
-				dist_2 = pa - __uint_as_float(top.y);
-				dist_2 *= dist_2;
 			}
 			if(done) break;
-			curr = top.x & 0x3fffffffu;
+			curr = top.x;
 			--sp_top;
 		}
-		// ---- density estimate (:959-976) ----
+		// ---- density estimate (:959-976), in heap-array order ----
+		const float4 wk = A.N.wo_k[j];
+		const uint4 cb = A.N.pix_mode[j];
+		Surf sp = surfFromPrim(S, p, __float_as_int(pp.w));
+		if(ATTR) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
+		const V3 wo = xyz(wk);
+		const uint32_t sid = __float_as_uint(wk.w);
+		C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)};
+		const float alpha = __uint_as_float(cb.w);
 		if(found > 0)
 		{
 			const float scale = x87recipMul(kPi, (float)S.pm_paths * max_d2);
@@ -3043,8 +3079,8 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const D
 	A.jobs = jobs;
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
-	const size_t lds = gatherLdsBytes(*S, S->small_tables != 0);
 	const dim3 grid(S->n_seg * kGatherPerSeg);
+	const size_t lds = gatherTableBytes(*S, S->small_tables != 0) + gatherLdsBytes(*S);
 	if(S->ext)
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_gather<true, true>), grid, dim3(kGatherBlock), lds, st, A);
@@ -3058,7 +3094,7 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const D
 // lanes of one gather launch (the HBM lookup stack holds pm_stack levels per lane)
 size_t yafamd_gather_lanes(const DevScene *S) { return (size_t)S->n_seg * kGatherPerSeg * kGatherBlock; }
 
-size_t yafamd_gather_lds_bytes(const DevScene *S) { return gatherLdsBytes(*S, S->small_tables != 0); }
+size_t yafamd_gather_lds_bytes(const DevScene *S) { return gatherTableBytes(*S, S->small_tables != 0) + gatherLdsBytes(*S); }
 
 hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix, uint8_t *flags,
                                     hipStream_t st)

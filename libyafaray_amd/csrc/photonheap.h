@@ -28,8 +28,18 @@ struct HeapRef
 	YPH float &d(int k) const { return dist[k * stride]; }
 };
 
+// Packed storage: slot k = (index, distance bits) in one 8-byte word, so a slot moves with one
+// 64-bit LDS read / write (k_gather: lanes interleaved, stride = workgroup lanes).
+struct HeapRefPacked
+{
+	uint32_t *e;   // e[2 * k * stride] = index, e[2 * k * stride + 1] = distance bits
+	int stride;
+	YPH uint32_t &i(int k) const { return e[2 * k * stride]; }
+	YPH float &d(int k) const { return reinterpret_cast<float *>(e)[2 * k * stride + 1]; }
+};
+
 // __push_heap(first, holeIndex, topIndex, value)
-YPH void heapPushUp(const HeapRef &h, int hole, int top, uint32_t vi, float vd)
+template<class H> YPH void heapPushUp(const H &h, int hole, int top, uint32_t vi, float vd)
 {
 	int parent = (hole - 1) / 2;
 	while(hole > top && h.d(parent) < vd)
@@ -44,7 +54,7 @@ YPH void heapPushUp(const HeapRef &h, int hole, int top, uint32_t vi, float vd)
 }
 
 // __adjust_heap(first, holeIndex, len, value)
-YPH void heapAdjust(const HeapRef &h, int hole, int len, uint32_t vi, float vd)
+template<class H> YPH void heapAdjust(const H &h, int hole, int len, uint32_t vi, float vd)
 {
 	const int top = hole;
 	int second = hole;
@@ -67,7 +77,7 @@ YPH void heapAdjust(const HeapRef &h, int hole, int len, uint32_t vi, float vd)
 }
 
 // std::make_heap(first, first + len)
-YPH void heapMake(const HeapRef &h, int len)
+template<class H> YPH void heapMake(const H &h, int len)
 {
 	if(len < 2) return;
 	for(int parent = (len - 2) / 2;; --parent)
@@ -81,7 +91,7 @@ YPH void heapMake(const HeapRef &h, int len)
 
 // std::pop_heap(first, first + len) followed by first[len - 1] = new value and
 // std::push_heap(first, first + len): PhotonGather's "replace the farthest" step.
-YPH void heapReplaceTop(const HeapRef &h, int len, uint32_t ni, float nd)
+template<class H> YPH void heapReplaceTop(const H &h, int len, uint32_t ni, float nd)
 {
 	if(len > 1)
 	{

@@ -23,13 +23,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KINDS = ["k_camera", "k_trace", "k_surface", "k_tshadow", "k_shade", "k_nee", "k_gather", "k_spawn", "k_combine", "k_film",
          "k_photon_emit", "k_photon_bounce"]
 COMPACT = ("k_photon_count", "k_photon_scan", "k_photon_scatter")
-PKD = ("k_keys", "k_bound", "k_bound_final", "k_flags", "k_gather_flags", "k_partition", "k_level_nodes", "k_seg_of", "k_children", "k_init_seg",
-       "k_pkd_", "k_sub")
+PKD = ("k_keys", "k_records", "k_bound", "k_root", "k_level_split", "k_partition", "k_seg_of", "k_subtrees")
 
 
 def kernel_src_sha1():
     h = hashlib.sha1()
-    for f in ("kernels.hip", "pkd.hip", "aa.hip"):
+    for f in ("kernels.hip", "pkd.hip", "pkd_kernels.h", "aa.hip"):
         with open(os.path.join(ROOT, "libyafaray_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()
@@ -95,6 +94,9 @@ def main():
                     e[n.lower() + "_frac"] = round(v[n] / wc, 4)
         if v.get("SQ_ACTIVE_INST_VALU") and v.get("SQ_THREAD_CYCLES_VALU"):
             e["valu_lane_util"] = round(v["SQ_THREAD_CYCLES_VALU"] / (64 * v["SQ_ACTIVE_INST_VALU"]), 4)
+        hit, miss = v.get("TCC_HIT_sum"), v.get("TCC_MISS_sum")
+        if hit is not None and miss is not None and hit + miss > 0:
+            e["l2_hit_rate"] = round(hit / (hit + miss), 4)
         for n in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_WAVES",
                   "SQ_LDS_BANK_CONFLICT"):
             if n in v:

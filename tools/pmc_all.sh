@@ -18,5 +18,6 @@ run F FETCH_SIZE
 run W WRITE_SIZE
 run A SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
 run B SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS
+run D TCC_HIT_sum TCC_MISS_sum
 run C SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT
 cd $R && python3 tools/pmc_aggregate.py $CFG gpurun_out/pmc_$CFG.json $dirs > /dev/null && echo "wrote gpurun_out/pmc_$CFG.json"
