@@ -46,6 +46,7 @@ typedef struct
 	double photon_seconds;      /* photon shooting + kd-tree build + upload */
 	double photon_shoot_seconds, photon_tree_seconds;
 	uint64_t gather_visits;     /* point kd-tree nodes fetched by the photon density estimates */
+	uint64_t caustic_photons;   /* photons stored in the caustic photon map (0: none / disabled) */
 } yafaray_amd_stats_t;
 
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */

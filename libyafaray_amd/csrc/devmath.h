@@ -216,6 +216,31 @@ YD float x87mul2(const X87Const &c, float x, float y)
 	return x87mul2Exact(c.hi, c.lo, x, y);
 }
 
+YD_COLD float x87mul3Exact(double chi, double clo, float x, float y, float z)
+{
+	const X87Const c = {chi, clo};
+	DD t = round64(exactMul(c, (double)x));
+	const double f2[2] = {(double)y, (double)z};
+	for(int k = 0; k < 2; ++k)
+	{
+		const double p = t.hi * f2[k];
+		const double e = fma(t.hi, f2[k], -p);
+		const double q = t.lo * f2[k];
+		t = round64(fastTwoSum(p, e + q));
+	}
+	return round24(t);
+}
+
+// (float)((long double)C * x * y * z) for x, y, z >= 0: three x87 roundings then the float one
+// (the photon kernel 3 ir / pi (1 - d^2 ir)^2, sample.h:31-35)
+YD float x87mul3(const X87Const &c, float x, float y, float z)
+{
+	if(x == 0.f || y == 0.f || z == 0.f) return 0.f;
+	float f;
+	if(safeToRound(c.hi * (double)x * (double)y * (double)z, f)) return f;
+	return x87mul3Exact(c.hi, c.lo, x, y, z);
+}
+
 // (float)(((long double)C * a) / (long double)b) with a, b > 0 floats (light pdfs,
 // src/light/light_area.cc:88).  The quotient is formed to ~104 bits (double-double) before the
 // two roundings.

@@ -209,6 +209,17 @@ struct DevScene
 	const float *light_func;
 	float light_inv_integral;
 	int n_ph_lights;
+	// caustic photon map (MonteCarloIntegrator::createCausticMap / causticWorker,
+	// integrator_montecarlo.cc:410-640): same layout as the diffuse map; caus_map = the integrator
+	// adds causticPhotons() at diffuse hits (PhotonIntegrator / DirectLight "caustics",
+	// PathIntegrator caustic_type photon | both) and the map holds photons
+	const float4 *cph_pos;
+	const float4 *cph_dir;
+	const float *cph_colb;
+	const uint4 *cpk_nodes;
+	int caus_map, c_photons, c_paths, c_search;
+	float c_radius2;               // caustic_radius^2 (float product, :629)
+	int gather_on;                 // k_shade queues k_gather requests (diffuse and / or caustic estimates)
 
 	// surface attributes and shader nodes: only when some material has nodes or some mesh has
 	// orco / uv / smooth normals (has_attr); k_surface then fills DevQueues::sattr per hit
@@ -299,6 +310,15 @@ struct DevNeeQueue
 	float4 *wo_k;          // outgoing direction, .w = index k of the path in the next active list (bits)
 	uint4 *pix_mode;       // (PixelSamplingData offset, sample index, mode | light << 8, 0)
 	float4 *attr;          // [2 * requests] surface attributes of the vertex (has_attr only)
+	float4 *extra;         // gather requests only: colour added after the estimates, .w = G_* mode bits
+};
+
+// k_gather request modes (DevNeeQueue::extra.w)
+enum : uint32_t
+{
+	G_DIFFUSE = 1u,   // diffuse-map density estimate (PhotonIntegrator)
+	G_CAUSTIC = 2u,   // causticPhotons()
+	G_EXTRA = 4u,     // then add extra.xyz
 };
 
 // Queues are segmented: segment b (capacity cap_a entries / cap_s shadow rays) belongs to workgroup
@@ -321,6 +341,18 @@ struct PhotonState
 	uint8_t *dep_flag;   // 1 = a photon was stored in this slot
 };
 
+// the lights one photon map is shot from (render_view.cc:103-110: lights emitting diffuse / caustic
+// photons) with their Pdf1D over the total energies (sample_pdf1d.h:52-66), and the map kind
+struct PhotonSet
+{
+	const int *lights;   // k -> index into DevScene::lights
+	const float *cdf;
+	const float *func;
+	float inv_integral;
+	int n_lights;
+	int caustic;         // 0: diffuseWorker rules, 1: causticWorker rules
+};
+
 // ImageFilm::nextPass inputs (imagefilm.cc:259-420; aa_noise_params.h:27-46)
 struct DevAaParams
 {
@@ -336,6 +368,7 @@ struct DevCounters
 	uint32_t *n_active;   // [n_seg] active-list entries (closest rays + paths) per segment
 	uint32_t *n_shadow;   // [n_seg] shadow rays per segment
 	uint32_t *n_nee;      // [n_seg] NEE requests per segment
+	uint32_t *n_gather;   // [n_seg] photon-map estimate requests per segment (k_gather)
 };
 
 // Per-workgroup counters (record b belongs to workgroup b of every launch on the stream: plain

@@ -966,17 +966,25 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		{
 			// integrator_photon_mapping.cc:765-850 defaults
 			int photons = 100000, cphotons = 500000, search = 50, pbounces = 5;
-			float ds_rad = 0.1f;
+			float ds_rad = 0.1f, c_rad = 0.01f;
 			bool caustics = true, diffuse = true;
 			ip.get("photons", photons);
 			ip.get("cPhotons", cphotons);
 			ip.get("search", search);
+			int caustic_mix = search;
+			ip.get("caustic_mix", caustic_mix);
 			ip.get("diffuseRadius", ds_rad);
+			ip.get("causticRadius", c_rad);
 			ip.get("bounces", pbounces);
 			ip.get("caustics", caustics);
 			ip.get("diffuse", diffuse);
 			rp.pm.photons = diffuse ? std::max(0, photons) : 0;
-			rp.pm.caustic_photons = caustics ? std::max(0, cphotons) : 0;
+			// the caustic map: MonteCarloIntegrator::createCausticMap with caus_depth = bounces
+			rp.pm.caustic_map = caustics;
+			rp.pm.caustic_photons = std::max(0, cphotons);
+			rp.pm.caustic_search = std::max(1, caustic_mix);
+			rp.pm.caustic_radius = c_rad;
+			rp.pm.caustic_depth = std::max(0, pbounces);
 			rp.pm.search = std::max(1, search);
 			rp.pm.radius2 = ds_rad;
 			rp.pm.bounces = std::max(0, pbounces);
@@ -992,25 +1000,35 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		ip.get("path_samples", path_samples);
 		ip.get("russian_roulette_min_bounces", rr_min);
 		S.caustic_path = 1;   // PathIntegrator ctor: CausticType::Path (integrator_path_tracer.cc:43)
-		if(ip.get("caustic_type", caustic_type))
+		// DirectLight "caustics" / PathIntegrator caustic_type photon | both: the caustic photon map
+		// (integrator_direct_light.cc:147-190, integrator_path_tracer.cc:325-342; defaults photons
+		// 500000, caustic_mix 100, caustic_depth 10, caustic_radius 0.25 as double)
+		auto causticParams = [&]() {
+			int c_photons = 500000, c_search = 100, c_depth = 10;
+			double c_rad = 0.25;
+			ip.get("photons", c_photons);
+			ip.get("caustic_mix", c_search);
+			ip.get("caustic_depth", c_depth);
+			ip.get("caustic_radius", c_rad);
+			rp.pm.caustic_map = true;
+			rp.pm.caustic_photons = std::max(0, c_photons);
+			rp.pm.caustic_search = std::max(1, c_search);
+			rp.pm.caustic_depth = std::max(0, c_depth);
+			rp.pm.caustic_radius = static_cast<float>(c_rad);
+			rp.pm.threads = s.threads_photons;
+		};
+		if(S.integrator == INT_PATH && ip.get("caustic_type", caustic_type))
 		{
 			if(caustic_type == "none") S.caustic_path = 0;
-			else if(caustic_type == "photon" || caustic_type == "both")
-			{
-				log.error("PathIntegrator: caustic_type '" + caustic_type + "' (photon caustics) is not supported by the GPU core");
-				return false;
-			}
+			else if(caustic_type == "photon") { S.caustic_path = 0; causticParams(); }
+			else if(caustic_type == "both") causticParams();
 		}
 		if(S.integrator == INT_DIRECT)
 		{
 			bool caus = false, ao = false;
 			ip.get("caustics", caus);
 			ip.get("do_AO", ao);
-			if(caus)
-			{
-				log.error("DirectLight: caustics = true (caustic photon map) is not supported by the GPU core");
-				return false;
-			}
+			if(caus) causticParams();
 			// integrator_direct_light.cc:161-186: do_AO, AO_samples (32), AO_distance (1.0, double), AO_color (1)
 			if(ao)
 			{
@@ -1067,11 +1085,6 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			if(m.type == MAT_MIRROR || m.type == MAT_NULL || m.n_nodes > 0 ||
 			   (m.sd_flags & (SD_MIRROR | SD_TRANSPARENT | SD_TRANSLUCENT | SD_FRESNEL | SD_OREN_NAYAR)))
 				S.ext = 1;
-		}
-		if(S.integrator == INT_PHOTON && S.tree)
-		{
-			log.error("PhotonIntegrator: specular / transparent materials (caustic maps, recursive raytracing) are not supported by the GPU photon mapping path yet");
-			return false;
 		}
 
 		S.has_bg = 0;

@@ -1425,6 +1425,7 @@ struct ShadeArgs
 	DevQueues Q;         // current (active list + hits)
 	DevQueues Qn;        // next
 	DevNeeQueue N;       // NEE requests for k_nee
+	DevNeeQueue G;       // photon-map estimate requests for k_gather (gather_on)
 	DevCounters cnt;     // counts of the current queue
 	DevCounters cnt_next;
 	float4 *samples;     // frame sample buffer [(y * W + x) * spp + s]
@@ -1527,8 +1528,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 	const uint32_t seg = blockIdx.x;
 	const uint32_t n_a = A.cnt.n_active[seg];
 	const uint32_t a0 = seg * S.cap_a;
-	__shared__ uint32_t s_count[3];   // next active entries, NEE / gather requests, shadow rays (FUSED)
-	if(threadIdx.x < 3) s_count[threadIdx.x] = 0;
+	__shared__ uint32_t s_count[4];   // next active entries, NEE requests, shadow rays (FUSED), gather requests
+	if(threadIdx.x < 4) s_count[threadIdx.x] = 0;
 	__syncthreads();
 	ShadeOut out;
 	out.sh_count = &s_count[2];
@@ -1536,7 +1537,11 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 	out.Qn = A.Qn;
 	const bool is_path = S.integrator == INT_PATH;
 	const bool is_photon = S.integrator == INT_PHOTON;
-	const bool keep_v0 = S.path_samples > 1 || is_photon;   // first-hit data carried to the end
+	// first-hit data carried to the end (the photon-map estimates of k_gather read it)
+	const bool keep_v0 = S.path_samples > 1 || is_photon || S.caus_map;
+	// DirectLight with a caustic map: causticPhotons() comes between the direct light and the AO
+	// (integrator_direct_light.cc:120-124), so the AO sum rides with the gather request
+	const bool ao_after_caustic = S.caus_map && S.integrator == INT_DIRECT;
 	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
 	const int K = S.nee_k;
 	const uint32_t stride = blockDim.x;
@@ -1578,6 +1583,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		uint32_t subpath = (stage >> 8) & 0xfffu;
 		int depth = (int)(stage >> 20);
 		const uint32_t offset = pix.x, sample_idx = pix.y;
+		C3 ao_extra = c3(0.f);
 
 		PHASE(0);
 		// ---- 1. connect the pending next-event estimate ----
@@ -1588,7 +1594,12 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			for(int l = 0; l < S.n_lights; ++l) total = total + neeSum(S, S.lights[l], Pc.nee, Pc.occ, (int)i * K + (int)S.lights[l].nee_base);
 			col = col + total;
 			// DirectLight: col += sampleAmbientOcclusion (integrator_direct_light.cc:124)
-			if(S.do_ao) col = col + aoSum(S, Pc.nee, Pc.occ, (int)i * K + S.nee_all_count, (flags & F_AO_EMIT) != 0, rgb(pem4));
+			if(S.do_ao)
+			{
+				const C3 ao = aoSum(S, Pc.nee, Pc.occ, (int)i * K + S.nee_all_count, (flags & F_AO_EMIT) != 0, rgb(pem4));
+				if(ao_after_caustic) ao_extra = ao;
+				else col = col + ao;
+			}
 		}
 		if(live && (flags & F_PEND_ONE))
 		{
@@ -1665,7 +1676,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 						emit_pend = matEmit<EXT>(m, sp, wo);   // sampleAmbientOcclusion adds sp.emit(wo) * pdf per sample
 						flags |= F_AO_EMIT;
 					}
-					if(is_photon)
+					if(is_photon || (S.caus_map && (sp.flags & B_DIFFUSE)))
 					{
 						v0p4 = f4(sp.p, __int_as_float(hit_prim));
 						v0wo4 = f4(wo, 0.f);
@@ -1821,8 +1832,18 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			want_ray = true;
 			stage = ST_FIRST | (subpath << 8);
 		}
-		// photon mapping: a diffuse camera hit still owes the photon density estimate (k_gather)
-		const bool want_gather = live && finalize && is_photon && (flags & F_V0_DIFFUSE) && S.n_photons > 0;
+		// a diffuse first hit still owes its photon-map estimates (k_gather): the diffuse map's
+		// density estimate (photon mapping) and / or causticPhotons(); whatever the integrator adds
+		// after them rides along as `extra` (DirectLight: the AO sum; path tracing: the paths)
+		const bool want_gather = live && finalize && (flags & F_V0_DIFFUSE) && ((is_photon && S.n_photons > 0) || S.caus_map);
+		C3 g_extra = c3(0.f);
+		uint32_t g_mode = 0;
+		if(want_gather)
+		{
+			g_mode = ((is_photon && S.n_photons > 0) ? G_DIFFUSE : 0u) | (S.caus_map ? G_CAUSTIC : 0u);
+			if(ao_after_caustic && S.do_ao) { g_extra = ao_extra; g_mode |= G_EXTRA; }
+			if(is_path) { g_extra = pcol / (float)n_paths; g_mode |= G_EXTRA; }   // path_tracer.cc:274-278
+		}
 		if(live && finalize && !want_gather)
 		{
 			// path_tracer.cc:274-278 / direct_light.cc:129-131
@@ -1893,7 +1914,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				}
 			}
 		}
-		const uint32_t jn = waveAppend((!FUSED && want_nee) || want_gather, &s_count[1]);
+		const uint32_t jn = waveAppend(!FUSED && want_nee, &s_count[1]);
+		const uint32_t jg = waveAppend(want_gather, &s_count[3]);
 		if(!FUSED && want_nee)
 		{
 			const uint32_t j = a0 + jn;
@@ -1906,16 +1928,17 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				A.N.attr[2 * (size_t)j + 1] = f4(sp.dcol, sp.sigma);
 			}
 		}
-		else if(want_gather)
+		if(want_gather)
 		{
-			const uint32_t j = a0 + jn;
-			A.N.p_prim[j] = v0p4;
-			A.N.wo_k[j] = f4(xyz(v0wo4), __uint_as_float(sid));
-			A.N.pix_mode[j] = make_uint4(__float_as_uint(col.r), __float_as_uint(col.g), __float_as_uint(col.b), __float_as_uint(alpha));
+			const uint32_t j = a0 + jg;
+			A.G.p_prim[j] = v0p4;
+			A.G.wo_k[j] = f4(xyz(v0wo4), __uint_as_float(sid));
+			A.G.pix_mode[j] = make_uint4(__float_as_uint(col.r), __float_as_uint(col.g), __float_as_uint(col.b), __float_as_uint(alpha));
+			A.G.extra[j] = f4(g_extra, __uint_as_float(g_mode));
 			if(ATTR)
 			{
-				A.N.attr[2 * (size_t)j] = v0a0;
-				A.N.attr[2 * (size_t)j + 1] = v0a1;
+				A.G.attr[2 * (size_t)j] = v0a0;
+				A.G.attr[2 * (size_t)j + 1] = v0a1;
 			}
 		}
 		PHASE(5);
@@ -1927,6 +1950,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		A.cnt_next.n_active[seg] = s_count[0];
 		A.cnt_next.n_nee[seg] = s_count[1];
 		if(FUSED) A.cnt_next.n_shadow[seg] = s_count[2];
+		if(S.gather_on) A.cnt_next.n_gather[seg] = s_count[3];
 		if(S.stats) S.stats[seg].shade_entries += n_a;
 	}
 }
@@ -2390,6 +2414,7 @@ struct PhotonArgs
 {
 	DevScene S;
 	PhotonState P;
+	PhotonSet L;         // the shooting lights and the map kind (diffuse / caustic)
 	uint32_t n_photons;  // photon paths (rounded like the reference, :437)
 	int max_bounces;
 	int bounce;          // k_photon_bounce: the bounce this launch traces
@@ -2412,20 +2437,21 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 		const float s_2 = ldsDim(S, 2, h);
 		const float s_3 = ldsDim(S, 3, h);
 		const float s_4 = ldsDim(S, 4, h);
-		const float s_l = float(h) * (1.f / static_cast<float>(A.n_photons));
+		// diffuseWorker: h * (1 / n) (:133); causticWorker: h / n (integrator_montecarlo.cc:444)
+		const float s_l = A.L.caustic ? float(h) / static_cast<float>(A.n_photons) : float(h) * (1.f / static_cast<float>(A.n_photons));
 		// sample_pdf1d.h:77-93 dSample (lower_bound over the cdf)
-		const int nl = S.n_ph_lights;
+		const int nl = A.L.n_lights;
 		int light_num;
 		if(s_l <= 0.f) light_num = 0;
 		else if(s_l >= 1.f) light_num = nl - 1;
 		else
 		{
 			light_num = 0;
-			while(light_num < nl && S.light_cdf[light_num] < s_l) ++light_num;
+			while(light_num < nl && A.L.cdf[light_num] < s_l) ++light_num;
 			if(light_num >= nl) light_num = nl - 1;
 		}
-		const float light_num_pdf = S.light_func[light_num] * S.light_inv_integral;
-		const DevLight &L = S.lights[S.ph_lights[light_num]];
+		const float light_num_pdf = A.L.func[light_num] * A.L.inv_integral;
+		const DevLight &L = S.lights[A.L.lights[light_num]];
 		float light_pdf;
 		// light_area.cc:98-104, light_point.cc:79-85
 		if(L.type == LIGHT_POINT)
@@ -2515,7 +2541,10 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 				const C3 lcol = rgb(pc);
 				uint32_t flags = __float_as_uint(pc.w);
 				const bool caustic = flags & 1u, direct = flags & 2u;
-				if((sp.flags & B_DIFFUSE) && !caustic)
+				// diffuse map: non-caustic photons on diffuse surfaces (:173-180); caustic map: caustic
+				// photons on diffuse / glossy surfaces (integrator_montecarlo.cc:480-488)
+				const bool store = A.L.caustic ? ((sp.flags & (B_DIFFUSE | B_GLOSSY)) && caustic) : ((sp.flags & B_DIFFUSE) && !caustic);
+				if(store)
 				{
 					const uint32_t slot = h * slots + (uint32_t)A.bounce;
 					A.P.dep_a[slot] = f4(sp.p, lcol.r);
@@ -2530,7 +2559,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 					s.s_1 = ldsDim(S, d_5, h);
 					s.s_2 = ldsDim(S, d_5 + 1, h);
 					const float s_3 = ldsDim(S, d_5 + 2, h);
-					s.flags = B_ALL;
+					// PSample flags: All (diffuse map), AllSpecular | Glossy | Filter | Dispersive (caustic
+					// map, integrator_montecarlo.cc:497)
+					s.flags = A.L.caustic ? (B_SPECULAR | B_REFLECT | B_TRANSMIT | B_GLOSSY | B_FILTER | B_DISPERSIVE) : B_ALL;
 					s.pdf = 0.f;
 					s.sampled = B_NONE;
 					float w = 0.f;
@@ -2552,7 +2583,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 							new_flags = (nc ? 1u : 0u) | (nd ? 2u : 0u);
 							new_o = sp.p;
 							new_d = wo;
-							cont = true;
+							// caustic-only shooting stops once the path is neither (:520-521)
+							cont = !A.L.caustic || nc || nd;
 						}
 					}
 				}
@@ -2656,8 +2688,8 @@ constexpr int kGatherPerSeg = 4;   // workgroups per queue segment (fills the ch
 struct GatherArgs
 {
 	DevScene S;
-	DevNeeQueue N;           // gather requests: (p, prim), (wo, sample id), (colour, alpha) bits
-	DevCounters cnt_next;    // n_nee = requests per segment
+	DevNeeQueue G;           // gather requests: (p, prim), (wo, sample id), (colour, alpha) bits, (extra, mode)
+	DevCounters cnt_next;    // n_gather = requests per segment
 	float4 *samples;
 	const DevJob *jobs;
 	int n_jobs;
@@ -2669,9 +2701,18 @@ __host__ __device__ inline size_t gatherTableBytes(const DevScene &S, bool small
 	return small ? (size_t)S.n_mats * sizeof(DevMaterial) + (size_t)S.n_tris * 16 : 0;
 }
 
+// heap slots: the larger k of the maps in use
+__host__ __device__ inline int gatherHeapSlots(const DevScene &S)
+{
+	const int kd = S.n_photons > 0 ? S.pm_search : 1;
+	const int kc = S.caus_map ? S.c_search : 1;
+	return kd > kc ? kd : kc;
+}
+
 __host__ __device__ inline size_t gatherLdsBytes(const DevScene &S)
 {
-	return (size_t)kGatherBlock * 8u * (size_t)S.pm_search + (YAF_GATHER_STACK_LDS ? (size_t)kGatherBlock * 8u * (size_t)S.pm_stack : 0u);
+	return (size_t)kGatherBlock * 8u * (size_t)gatherHeapSlots(S) +
+	       (YAF_GATHER_STACK_LDS ? (size_t)kGatherBlock * 8u * (size_t)S.pm_stack : 0u);
 }
 
 // workgroups are dealt to the 8 XCDs round-robin: renumber them so that XCD x gets the contiguous
@@ -2693,6 +2734,80 @@ __device__ __forceinline__ void gatherSegPart(uint32_t n_seg, uint32_t &seg, uin
 	}
 }
 
+// PhotonMap::gather (photon.cc:55-64): k-NN lookup in a point kd-tree (pkdtree.h:225-292,
+// NON_REC_LOOKUP) with PhotonGather's heap (photon.cc:31-52); returns the photons found, leaves
+// the heap in `heap` and the final squared radius in max_d2
+__device__ __forceinline__ int pkLookup(const uint4 *nodes, V3 p, int k, float &max_d2, const HeapRefPacked &heap, uint2 *stk, uint32_t gstride,
+                                        uint32_t &visits)
+{
+	// nodes: .w = flags (bits 0-1 axis, 3 = leaf; interior: right child << 2, leaf: photon << 2),
+	// interior .x = split position; leaf .xyz = the photon's position
+	int found = 0;
+	uint32_t curr = 0;
+	int sp_top = 0;   // entries above the reference's "nowhere" sentinel
+	for(;;)
+	{
+		uint4 nd = nodes[curr];
+		++visits;
+		while((nd.w & 3u) != 3u)
+		{
+			const int axis = (int)(nd.w & 3u);
+			const float split_val = __uint_as_float(nd.x);
+			const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+			uint32_t far_child;
+			if(pa <= split_val) { far_child = nd.w >> 2; curr = curr + 1; }
+			else { far_child = curr + 1; curr = nd.w >> 2; }
+			// the reference pushes every far child and discards it at pop time when (p - split)^2 >
+			// max_d2; max_d2 never grows, so one that already fails now is never visited
+			float d2 = pa - split_val;
+			d2 *= d2;
+			if(d2 <= max_d2)
+			{
+				stk[(size_t)sp_top * gstride] = make_uint2(far_child, __float_as_uint(d2));
+				++sp_top;
+			}
+			nd = nodes[curr];
+			++visits;
+		}
+		const uint32_t ph = nd.w >> 2;
+		const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
+		const float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
+		if(dist_2 < max_d2)
+		{
+			// photon.cc:31-52
+			if(found < k)
+			{
+				heap.i(found) = ph;
+				heap.d(found) = dist_2;
+				++found;
+				if(found == k)
+				{
+					heapMake(heap, k);
+					max_d2 = heap.d(0);
+				}
+			}
+			else
+			{
+				heapReplaceTop(heap, k, ph, dist_2);
+				max_d2 = heap.d(0);
+			}
+		}
+		if(sp_top == 0) break;
+		uint2 top = stk[(size_t)(sp_top - 1) * gstride];
+		bool done = false;
+		while(__uint_as_float(top.y) > max_d2)
+		{
+			--sp_top;
+			if(sp_top == 0) { done = true; break; }
+			top = stk[(size_t)(sp_top - 1) * gstride];
+		}
+		if(done) break;
+		curr = top.x;
+		--sp_top;
+	}
+	return found;
+}
+
 template<bool SMALL, bool EXT>
 __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 {
@@ -2712,7 +2827,6 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 	const bool ATTR = EXT && S.has_attr != 0;
 	// per-lane heap, lane-interleaved after the staged tables
 	uint32_t *lds_words = reinterpret_cast<uint32_t *>(gather_smem) + gatherTableBytes(A.S, SMALL) / 4;
-	const int k = S.pm_search;
 	const int lane = threadIdx.x;
 	HeapRefPacked heap;
 	heap.e = lds_words + 2 * lane;
@@ -2720,102 +2834,40 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 	// lookup stack: this lane's column, [level][lane] (LDS after the heap, or the HBM stack buffer)
 #if YAF_GATHER_STACK_LDS
 	const uint32_t gstride = kGatherBlock;
-	uint2 *stk = reinterpret_cast<uint2 *>(lds_words + (size_t)2 * k * kGatherBlock) + threadIdx.x;
+	uint2 *stk = reinterpret_cast<uint2 *>(lds_words + (size_t)2 * gatherHeapSlots(S) * kGatherBlock) + threadIdx.x;
 #else
 	const uint32_t gstride = gridDim.x * kGatherBlock;
 	uint2 *stk = S.pk_stack + blockIdx.x * kGatherBlock + threadIdx.x;
 #endif
 	uint32_t seg, part, parts;
 	gatherSegPart(S.n_seg, seg, part, parts);
-	const uint32_t n_req = A.cnt_next.n_nee[seg];
+	const uint32_t n_req = A.cnt_next.n_gather[seg];
 	const uint32_t a0 = seg * S.cap_a;
 	uint32_t visits = 0;
 	for(uint32_t base_j = part * kGatherBlock; base_j < n_req; base_j += parts * kGatherBlock)
 	{
 		if(base_j + threadIdx.x >= n_req) continue;
 		const uint32_t j = a0 + base_j + threadIdx.x;
-		const float4 pp = A.N.p_prim[j];
+		const float4 pp = A.G.p_prim[j];
+		const float4 ex = A.G.extra[j];
+		const uint32_t mode = __float_as_uint(ex.w);
 		const V3 p = xyz(pp);
-		// ---- k-NN lookup (pkdtree.h:225-292, NON_REC_LOOKUP) ----
-		// nodes: .w = flags (bits 0-1 axis, 3 = leaf; interior: right child << 2, leaf: photon << 2),
-		// interior .x = split position; leaf .xyz = the photon's position
 		float max_d2 = S.pm_radius2;
 		int found = 0;
-		uint32_t curr = 0;
-		int sp_top = 0;   // entries above the reference's "nowhere" sentinel
-		for(;;)
-		{
-			uint4 nd = S.pk_nodes[curr];
-			++visits;
-			while((nd.w & 3u) != 3u)
-			{
-				const int axis = (int)(nd.w & 3u);
-				const float split_val = __uint_as_float(nd.x);
-				const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
-				uint32_t far_child;
-				if(pa <= split_val) { far_child = nd.w >> 2; curr = curr + 1; }
-				else { far_child = curr + 1; curr = nd.w >> 2; }
-				// the reference pushes every far child and discards it at pop time when (p - split)^2 >
-				// max_d2; max_d2 never grows, so one that already fails now is never visited
-				float d2 = pa - split_val;
-				d2 *= d2;
-				if(d2 <= max_d2)
-				{
-					stk[(size_t)sp_top * gstride] = make_uint2(far_child, __float_as_uint(d2));
-					++sp_top;
-				}
-				nd = S.pk_nodes[curr];
-				++visits;
-			}
-			const uint32_t ph = nd.w >> 2;
-			const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
-			const float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
-			if(dist_2 < max_d2)
-			{
-				// photon.cc:31-52
-				if(found < k)
-				{
-					heap.i(found) = ph;
-					heap.d(found) = dist_2;
-					++found;
-					if(found == k)
-					{
-						heapMake(heap, k);
-						max_d2 = heap.d(0);
-					}
-				}
-				else
-				{
-					heapReplaceTop(heap, k, ph, dist_2);
-					max_d2 = heap.d(0);
-				}
-			}
-			if(sp_top == 0) break;
-			uint2 top = stk[(size_t)(sp_top - 1) * gstride];
-			bool done = false;
-			while(__uint_as_float(top.y) > max_d2)
-			{
-				--sp_top;
-				if(sp_top == 0) { done = true; break; }
-				top = stk[(size_t)(sp_top - 1) * gstride];
-			}
-			if(done) break;
-			curr = top.x;
-			--sp_top;
-		}
-		// ---- density estimate (:959-976), in heap-array order ----
-		const float4 wk = A.N.wo_k[j];
-		const uint4 cb = A.N.pix_mode[j];
+		if(mode & G_DIFFUSE) found = pkLookup(S.pk_nodes, p, S.pm_search, max_d2, heap, stk, gstride, visits);
+		const float4 wk = A.G.wo_k[j];
+		const uint4 cb = A.G.pix_mode[j];
 		Surf sp = surfFromPrim(S, p, __float_as_int(pp.w));
-		if(ATTR) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
+		if(ATTR) applyAttr(sp, A.G.attr[2 * (size_t)j], A.G.attr[2 * (size_t)j + 1]);
 		const V3 wo = xyz(wk);
 		const uint32_t sid = __float_as_uint(wk.w);
 		C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)};
 		const float alpha = __uint_as_float(cb.w);
+		const DevMaterial &m = S.mats[sp.mat];
+		// ---- diffuse-map density estimate (integrator_photon_mapping.cc:953-976), heap-array order ----
 		if(found > 0)
 		{
 			const float scale = x87recipMul(kPi, (float)S.pm_paths * max_d2);
-			const DevMaterial &m = S.mats[sp.mat];
 			for(int i = 0; i < found; ++i)
 			{
 				const uint32_t ph = heap.i(i);
@@ -2826,10 +2878,38 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 				col = col + col_tmp;
 			}
 		}
-		col = col + c3(0.f);   // caustic map empty for the supported materials (montecarlo.cc:644)
-		col = col + c3(0.f);   // recursiveRaytrace: no specular/glossy components
-		const SampleCoord sc = sampleAt(S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
-		A.samples[((size_t)sc.y * S.width + sc.x) * S.spp + sc.s] = f4(col, alpha > 1.f ? 1.f : alpha);
+		// ---- causticPhotons / estimateCausticPhotons (integrator_montecarlo.cc:410-419, 627-648) ----
+		if(mode & G_CAUSTIC)
+		{
+			float r2 = S.c_radius2;
+			const int nc = pkLookup(S.cpk_nodes, p, S.c_search, r2, heap, stk, gstride, visits);
+			const float ir2 = 1.f / r2;
+			C3 sum = c3(0.f);
+			if(nc > 0)
+			{
+				for(int i = 0; i < nc; ++i)
+				{
+					const uint32_t ph = heap.i(i);
+					const float4 a = S.cph_pos[ph], b = S.cph_dir[ph];
+					const C3 pc = C3{a.w, b.w, S.cph_colb[ph]};
+					const C3 surf_col = matEval<EXT>(m, sp, wo, xyz(b), B_ALL);
+					// sample.h:31-35 kernel(d^2, 1 / r^2) = 3 ir2 / pi (1 - d^2 ir2)^2 in long double
+					const float sk = 1.f - heap.d(i) * ir2;
+					const float kern = x87mul3(kDiv1ByPi, 3.f * ir2, sk, sk);
+					sum = sum + surf_col * kern * pc;
+				}
+				sum = sum * (1.f / static_cast<float>(S.c_paths));
+			}
+			col = col + sum;
+		}
+		if(mode & G_EXTRA) col = col + C3{ex.x, ex.y, ex.z};   // DirectLight AO / the path tracer's paths
+		col = col + c3(0.f);   // recursiveRaytrace: the specular tree's part is folded in by k_combine
+		if(EXT && S.tree) S.node_own[sid] = f4(col, alpha);
+		else
+		{
+			const SampleCoord sc = sampleAt(S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
+			A.samples[((size_t)sc.y * S.width + sc.x) * S.spp + sc.s] = f4(col, alpha > 1.f ? 1.f : alpha);
+		}
 	}
 	// counters: wave sums, then one atomic per workgroup (several workgroups share a segment)
 	for(int off = 32; off > 0; off >>= 1) visits += __shfl_down(visits, off);
@@ -2931,8 +3011,9 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 }
 
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
-                               const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, const DevCounters *cnt_next,
-                               float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st)
+                               const DevQueues *Qn, const DevNeeQueue *N, const DevNeeQueue *G, const DevCounters *cnt,
+                               const DevCounters *cnt_next, float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base,
+                               hipStream_t st)
 {
 	ShadeArgs A;
 	A.S = *S;
@@ -2941,6 +3022,7 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	A.Q = *Q;
 	A.Qn = *Qn;
 	A.N = *N;
+	A.G = *G;
 	A.cnt = *cnt;
 	A.cnt_next = *cnt_next;
 	A.samples = samples;
@@ -3006,11 +3088,13 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	return hipGetLastError();
 }
 
-hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, hipStream_t st)
+hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, int max_bounces,
+                              hipStream_t st)
 {
 	PhotonArgs A;
 	A.S = *S;
 	A.P = *P;
+	A.L = *L;
 	A.n_photons = n_photons;
 	A.max_bounces = max_bounces;
 	A.bounce = 0;
@@ -3022,12 +3106,13 @@ hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, uint32_t 
 	return hipGetLastError();
 }
 
-hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, int bounce,
-                                int cur, int stack_depth, int *spill, int grid, hipStream_t st)
+hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, int max_bounces,
+                                int bounce, int cur, int stack_depth, int *spill, int grid, hipStream_t st)
 {
 	PhotonArgs A;
 	A.S = *S;
 	A.P = *P;
+	A.L = *L;
 	A.n_photons = n_photons;
 	A.max_bounces = max_bounces;
 	A.bounce = bounce;
@@ -3068,12 +3153,12 @@ hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_
 	return hipGetLastError();
 }
 
-hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const DevCounters *cnt_next, float4 *samples,
+hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, float4 *samples,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st)
 {
 	GatherArgs A;
 	A.S = *S;
-	A.N = *N;
+	A.G = *G;
 	A.cnt_next = *cnt_next;
 	A.samples = samples;
 	A.jobs = jobs;

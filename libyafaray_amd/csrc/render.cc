@@ -32,17 +32,19 @@ int yafamd_shade_fused();
 int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds);
 int yafamd_shade_blocks_per_cu();
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
-                               const DevQueues *Qn, const DevNeeQueue *N, const DevCounters *cnt, const DevCounters *cnt_next,
-                               float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
+                               const DevQueues *Qn, const DevNeeQueue *N, const DevNeeQueue *G, const DevCounters *cnt,
+                               const DevCounters *cnt_next, float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base,
+                               hipStream_t st);
 hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
                              const DevCounters *cnt_next, hipStream_t st);
 int yafamd_nee_blocks_per_cu();
-hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, hipStream_t st);
-hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, uint32_t n_photons, int max_bounces, int bounce,
-                                int cur, int stack_depth, int *spill, int grid, hipStream_t st);
+hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, int max_bounces,
+                              hipStream_t st);
+hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, int max_bounces,
+                                int bounce, int cur, int stack_depth, int *spill, int grid, hipStream_t st);
 hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev,
                                  float4 *pos, float4 *dir, float *colb, hipStream_t st);
-hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *N, const DevCounters *cnt_next, float4 *samples,
+hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, float4 *samples,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
 size_t yafamd_gather_lds_bytes(const DevScene *S);
 size_t yafamd_gather_lanes(const DevScene *S);
@@ -116,6 +118,11 @@ struct GpuRenderer::Impl
 	Buf ph_lights, light_cdf, light_func;
 	float light_inv_integral = 0.f;
 	int n_ph_lights = 0;
+	Buf cph_lights, clight_cdf, clight_func;   // lights shooting caustic photons
+	float clight_inv_integral = 0.f;
+	int n_cph_lights = 0;
+	Buf cph_pos, cph_dir, cph_colb, cpk_nodes;   // caustic photon map + kd-tree
+	int c_photons = 0, c_paths = 0, c_depth = 0;
 	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
 	Buf ph_pos, ph_dir, ph_colb, pk_nodes, pk_stack;
 	// render group (RCCL communicator over the group's GPUs) and its exchange buffers
@@ -174,11 +181,14 @@ struct GpuRenderer::Impl
 	}
 	int trace_grid = 2048, shade_grid = 1024, nee_grid = 1024, n_cu = 256;
 	DevNeeQueue N{};
+	DevNeeQueue G{};   // k_gather requests (photon-map estimates)
+	bool g_alloc = false;
 
 	~Impl()
 	{
 		for(Buf *b : {&ph_lights, &light_cdf, &light_func, &ph_ray_o, &ph_ray_d, &ph_pcol, &ph_alive0, &ph_alive1, &ph_n_alive,
-		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes, &pk_stack})
+		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes, &pk_stack, &cph_lights,
+		              &clight_cdf, &clight_func, &cph_pos, &cph_dir, &cph_colb, &cpk_nodes})
 			b->release();
 		for(Buf *b : {&prim_attr, &shader_nodes, &textures, &texels, &spawn_o, &spawn_d, &spawn_pr, &node_own, &node_child, &node_w,
 		              &spawn_count})
@@ -322,23 +332,25 @@ bool GpuRenderer::upload(HostScene &hs)
 	d.n_mats = (int)hs.mats.size();
 	d.n_lights = (int)hs.lights.size();
 	{
-		// sample_pdf1d.h:52-66 over the lights shooting diffuse photons (render_view.cc:103-110),
-		// energies = totalEnergy().energy() (light_area.cc:64, light_point.h:41, color.h:59)
-		std::vector<int> idx;
-		std::vector<float> func;
-		for(int i = 0; i < d.n_lights; ++i)
+		// sample_pdf1d.h:52-66 over the lights shooting diffuse (bit 0) / caustic (bit 1) photons
+		// (render_view.cc:103-110), energies = totalEnergy().energy() (light_area.cc:64,
+		// light_point.h:41, color.h:59)
+		for(int set = 0; set < 2; ++set)
 		{
-			const DevLight &L = hs.lights[i];
-			if(!(L.shoot & 1u)) continue;
-			float e[3];
-			for(int k = 0; k < 3; ++k)
-				e[k] = (L.type == LIGHT_POINT) ? static_cast<float>(3.14159265358979323846264338327950288L) * (4.0f * L.color[k]) : L.area * L.color[k];
-			func.push_back((e[0] + e[1] + e[2]) * 0.333333f);
-			idx.push_back(i);
-		}
-		d.n_ph_lights = (int)idx.size();
-		if(!idx.empty())
-		{
+			std::vector<int> idx;
+			std::vector<float> func;
+			for(int i = 0; i < d.n_lights; ++i)
+			{
+				const DevLight &L = hs.lights[i];
+				if(!(L.shoot & (1u << set))) continue;
+				float e[3];
+				for(int k = 0; k < 3; ++k)
+					e[k] = (L.type == LIGHT_POINT) ? static_cast<float>(3.14159265358979323846264338327950288L) * (4.0f * L.color[k]) : L.area * L.color[k];
+				func.push_back((e[0] + e[1] + e[2]) * 0.333333f);
+				idx.push_back(i);
+			}
+			(set ? d.n_cph_lights : d.n_ph_lights) = (int)idx.size();
+			if(idx.empty()) continue;
 			std::vector<float> cdf(func.size());
 			const double delta = 1.0 / static_cast<double>(func.size());
 			double c = 0.0;
@@ -349,10 +361,10 @@ bool GpuRenderer::upload(HostScene &hs)
 			}
 			const float integral = static_cast<float>(c);
 			for(float &e : cdf) e /= integral;
-			d.light_inv_integral = 1.f / integral;
-			if(!allocCopy(log_, d.ph_lights, idx.data(), idx.size())) return false;
-			if(!allocCopy(log_, d.light_cdf, cdf.data(), cdf.size())) return false;
-			if(!allocCopy(log_, d.light_func, func.data(), func.size())) return false;
+			(set ? d.clight_inv_integral : d.light_inv_integral) = 1.f / integral;
+			if(!allocCopy(log_, set ? d.cph_lights : d.ph_lights, idx.data(), idx.size())) return false;
+			if(!allocCopy(log_, set ? d.clight_cdf : d.light_cdf, cdf.data(), cdf.size())) return false;
+			if(!allocCopy(log_, set ? d.clight_func : d.light_func, func.data(), func.size())) return false;
 		}
 	}
 	d.depth = hs.bvh.depth;
@@ -453,26 +465,18 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	if(S.has_attr) S.ext = 1;
 }
 
-bool GpuRenderer::buildPhotonMap(RenderParams &rp)
+// One photon map on the GPU: shoot N paths from the light set L (diffuseWorker /
+// causticWorker rules by L.caustic), compact the deposits in photon-id order (one reference
+// thread's append order) and build the point kd-tree node for node like the reference (pkd.hip).
+// which = 0: the diffuse map buffers, 1: the caustic map buffers.
+bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int bounces, int which, uint32_t &n_out, int &depth_out)
 {
 	Impl &d = *d_;
 	DevScene &S = rp.scene;
-	const PhotonParams &pm = rp.pm;
-	S.n_photons = 0;
-	S.pm_paths = 0;
-	S.pm_search = pm.search;
-	S.pm_radius2 = pm.radius2;
-	S.pm_stack = 8;
-	if(pm.photons <= 0 || d.n_ph_lights == 0)
-	{
-		if(pm.photons > 0) log_.warning("PhotonIntegrator: no lights shoot diffuse photons; diffuse photon map disabled");
-		return true;
-	}
+	n_out = 0;
+	depth_out = 0;
 	const auto t0 = std::chrono::steady_clock::now();
-	// integrator_photon_mapping.cc:437 (threads_photons <= 0 counts as one thread here)
-	const uint32_t T = (uint32_t)std::max(1, pm.threads);
-	const uint32_t N = std::max(T, ((uint32_t)pm.photons / T) * T);
-	const uint32_t slots = (uint32_t)pm.bounces + 1u;
+	const uint32_t slots = (uint32_t)bounces + 1u;
 	const size_t n_slots = (size_t)N * slots;
 	if(n_slots > 0xffffffffull) { log_.error("PhotonIntegrator: photons x (bounces + 1) exceeds 2^32 deposit slots"); return false; }
 	if(!ensure(log_, d.ph_ray_o, (size_t)N * 16) || !ensure(log_, d.ph_ray_d, (size_t)N * 16) || !ensure(log_, d.ph_pcol, (size_t)N * 16) ||
@@ -493,53 +497,133 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	P.dep_flag = (uint8_t *)d.dep_flag.p;
 	HIPCHECK(hipMemsetAsync(d.dep_flag.p, 0, n_slots, d.stream));
 	HIPCHECK(hipMemsetAsync(d.ph_n_alive.p, 0, 16, d.stream));
-	PROF(KK_PHOTON_EMIT, yafamd_photon_emit(&S, &P, N, pm.bounces, d.stream));
+	PROF(KK_PHOTON_EMIT, yafamd_photon_emit(&S, &P, &L, N, bounces, d.stream));
 	int cur = 0;
-	for(int b = 0; b <= pm.bounces; ++b)
+	for(int b = 0; b <= bounces; ++b)
 	{
 		HIPCHECK(hipMemsetAsync((uint32_t *)d.ph_n_alive.p + (cur ^ 1), 0, 4, d.stream));
-		PROF(KK_PHOTON_BOUNCE, yafamd_photon_bounce(&S, &P, N, pm.bounces, b, cur, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+		PROF(KK_PHOTON_BOUNCE, yafamd_photon_bounce(&S, &P, &L, N, bounces, b, cur, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 		cur ^= 1;
 	}
-	// the photon map in photon-id order (one reference thread's append order); outputs sized for
-	// the worst case (every slot stored), the count comes back from the scan
+	// the map in photon-id order; outputs sized for the worst case (every slot stored), the count
+	// comes back from the scan
+	Buf &pos = which ? d.cph_pos : d.ph_pos, &dir = which ? d.cph_dir : d.ph_dir, &colb = which ? d.cph_colb : d.ph_colb;
+	Buf &nodes = which ? d.cpk_nodes : d.pk_nodes;
 	uint32_t n = 0;
-	if(!ensure(log_, d.ph_pos, n_slots * 16) || !ensure(log_, d.ph_dir, n_slots * 16) || !ensure(log_, d.ph_colb, n_slots * 4)) return false;
-	PROF(KK_PHOTON_COMPACT, yafamd_photon_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)d.ph_pos.p,
-	                               (float4 *)d.ph_dir.p, (float *)d.ph_colb.p, d.stream));
+	if(!ensure(log_, pos, n_slots * 16) || !ensure(log_, dir, n_slots * 16) || !ensure(log_, colb, n_slots * 4)) return false;
+	PROF(KK_PHOTON_COMPACT, yafamd_photon_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)pos.p,
+	                               (float4 *)dir.p, (float *)colb.p, d.stream));
 	HIPCHECK(hipMemcpyAsync(&n, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
-	if(n < 50) { log_.error("PhotonIntegrator: Too few diffuse photons, stopping now."); return false; }   // :448-452
+	n_out = n;
 	const auto t1 = std::chrono::steady_clock::now();
+	stats_.photon_shoot_seconds += std::chrono::duration<double>(t1 - t0).count();
+	if(n == 0) return true;
 	// point kd-tree of the map, built on the GPU node for node like the reference's (pkd.hip)
-	if(!ensure(log_, d.pk_nodes, (2 * (size_t)n - 1) * sizeof(uint4))) return false;
+	if(!ensure(log_, nodes, (2 * (size_t)n - 1) * sizeof(uint4))) return false;
 	int depth = 0;
-	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)d.ph_pos.p, n, (uint4 *)d.pk_nodes.p, &depth, d.stream));
+	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)pos.p, n, (uint4 *)nodes.p, &depth, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
-	struct { int max_depth; } pb{depth};
+	depth_out = depth;
+	stats_.photon_tree_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+	return true;
+}
+
+bool GpuRenderer::buildPhotonMap(RenderParams &rp)
+{
+	Impl &d = *d_;
+	DevScene &S = rp.scene;
+	const PhotonParams &pm = rp.pm;
+	S.n_photons = 0;
+	S.pm_paths = 0;
+	S.pm_search = pm.search;
+	S.pm_radius2 = pm.radius2;
+	S.pm_stack = 8;
+	S.caus_map = 0;
+	S.c_photons = 0;
+	S.c_paths = 0;
+	S.c_search = std::max(1, pm.caustic_search);
+	S.c_radius2 = pm.caustic_radius * pm.caustic_radius;   // integrator_montecarlo.cc:629
+	S.gather_on = 0;
+	stats_.photon_shoot_seconds = stats_.photon_tree_seconds = 0.0;
+	const auto t0 = std::chrono::steady_clock::now();
+	// integrator_photon_mapping.cc:437 / integrator_montecarlo.cc:604 (threads_photons <= 0 counts as one)
+	const uint32_t T = (uint32_t)std::max(1, pm.threads);
+	int depth_c = 0, depth_d = 0;
+	d.c_photons = d.c_paths = d.c_depth = 0;
+	// ---- caustic map (createCausticMap, integrator_montecarlo.cc:565-625) ----
+	if(pm.caustic_map)
+	{
+		if(d.n_cph_lights == 0) log_.warning("Integrator: no lights shoot caustic photons; caustic photon map empty");
+		else if(pm.caustic_photons > 0)
+		{
+			const uint32_t N = std::max(T, ((uint32_t)pm.caustic_photons / T) * T);
+			PhotonSet L{(const int *)d.cph_lights.p, (const float *)d.clight_cdf.p, (const float *)d.clight_func.p, d.clight_inv_integral,
+			            d.n_cph_lights, 1};
+			uint32_t n = 0;
+			if(!shootMap(rp, L, N, std::max(0, pm.caustic_depth), 1, n, depth_c)) return false;
+			d.c_photons = (int)n;
+			d.c_paths = (int)N;
+			stats_.caustic_photons = n;
+			d.c_depth = depth_c;
+			std::ostringstream os;
+			os << "Integrator: shot " << N << " caustic photons, stored " << n << " (kd-tree depth " << depth_c << ")";
+			log_.info(os.str());
+			if(n > 0)
+			{
+				S.caus_map = 1;
+				S.c_photons = (int)n;
+				S.c_paths = (int)N;
+				S.cph_pos = (const float4 *)d.cph_pos.p;
+				S.cph_dir = (const float4 *)d.cph_dir.p;
+				S.cph_colb = (const float *)d.cph_colb.p;
+				S.cpk_nodes = (const uint4 *)d.cpk_nodes.p;
+			}
+		}
+	}
+	// ---- diffuse map (PhotonIntegrator::preprocess, integrator_photon_mapping.cc:242-638) ----
+	uint32_t n = 0;
+	uint32_t N = 0;
+	if(S.integrator == INT_PHOTON && pm.photons > 0)
+	{
+		if(d.n_ph_lights == 0) log_.warning("PhotonIntegrator: no lights shoot diffuse photons; diffuse photon map disabled");
+		else
+		{
+			N = std::max(T, ((uint32_t)pm.photons / T) * T);
+			PhotonSet L{(const int *)d.ph_lights.p, (const float *)d.light_cdf.p, (const float *)d.light_func.p, d.light_inv_integral,
+			            d.n_ph_lights, 0};
+			if(!shootMap(rp, L, N, pm.bounces, 0, n, depth_d)) return false;
+			if(n < 50) { log_.error("PhotonIntegrator: Too few diffuse photons, stopping now."); return false; }   // :448-452
+		}
+	}
 	d.n_photons = (int)n;
 	d.pm_paths = (int)N;
-	d.pm_stack = pb.max_depth + 1;
+	d.pm_stack = std::max(depth_d, depth_c) + 1;
 	S.ph_pos = (const float4 *)d.ph_pos.p;
 	S.ph_dir = (const float4 *)d.ph_dir.p;
 	S.ph_colb = (const float *)d.ph_colb.p;
 	S.pk_nodes = (const uint4 *)d.pk_nodes.p;
-	// k_gather's lookup stacks (pm_stack levels per gather lane, in HBM)
-	DevScene seg_probe = S;
-	seg_probe.n_seg = (uint32_t)d.shade_grid;   // the queue segments of the render that follows
-	if(!ensure(log_, d.pk_stack, (size_t)d.pm_stack * yafamd_gather_lanes(&seg_probe) * sizeof(uint2))) return false;
-	S.pk_stack = (uint2 *)d.pk_stack.p;
 	S.n_photons = (int)n;
 	S.pm_paths = (int)N;
 	S.pm_stack = d.pm_stack;
+	S.gather_on = (S.n_photons > 0 || S.caus_map) ? 1 : 0;
+	if(S.gather_on)
+	{
+		// k_gather's lookup stacks (pm_stack levels per gather lane, in HBM)
+		DevScene seg_probe = S;
+		seg_probe.n_seg = (uint32_t)d.shade_grid;   // the queue segments of the render that follows
+		if(!ensure(log_, d.pk_stack, (size_t)d.pm_stack * yafamd_gather_lanes(&seg_probe) * sizeof(uint2))) return false;
+		S.pk_stack = (uint2 *)d.pk_stack.p;
+	}
 	stats_.photons = n;
 	const auto t2 = std::chrono::steady_clock::now();
 	stats_.photon_seconds = std::chrono::duration<double>(t2 - t0).count();
-	stats_.photon_shoot_seconds = std::chrono::duration<double>(t1 - t0).count();
-	stats_.photon_tree_seconds = std::chrono::duration<double>(t2 - t1).count();
-	std::ostringstream os;
-	os << "PhotonIntegrator: shot " << N << " photons, stored " << n << " (kd-tree depth " << pb.max_depth << ") in " << stats_.photon_seconds << " s";
-	log_.info(os.str());
+	if(S.integrator == INT_PHOTON)
+	{
+		std::ostringstream os;
+		os << "PhotonIntegrator: shot " << N << " photons, stored " << n << " (kd-tree depth " << depth_d << ") in " << stats_.photon_seconds << " s";
+		log_.info(os.str());
+	}
 	return true;
 }
 
@@ -550,19 +634,24 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	DevScene &S = rp.scene;
 	fillScenePointers(d, S);
 	stats_.photons = 0;
+	stats_.caustic_photons = 0;
 	stats_.photon_seconds = 0.0;
 	d.prof_on = rp.profile;
 	d.ev_n = 2;
 	d.prof_recs.clear();
 	ktimes_ = KernelTimes{};
-	if(S.integrator == INT_PHOTON)
+	S.caus_map = 0;
+	S.gather_on = 0;
+	S.n_photons = 0;
+	if(S.integrator == INT_PHOTON || rp.pm.caustic_map)
 	{
-		// PhotonIntegrator::preprocess (integrator_photon_mapping.cc:242-638): the photon map is
-		// rebuilt for every render, as the reference's "generate" mode does
+		// PhotonIntegrator::preprocess (integrator_photon_mapping.cc:242-638) / createCausticMap
+		// (integrator_montecarlo.cc:565-625): the photon maps are rebuilt for every render, as the
+		// reference's "generate" mode does
 		if(!buildPhotonMap(rp)) return false;
 		if(yafamd_gather_lds_bytes(&S) > 64 * 1024)
 		{
-			log_.error("PhotonIntegrator: search " + std::to_string(S.pm_search) + " needs more LDS than the gather kernel has");
+			log_.error("Integrator: photon search " + std::to_string(std::max(S.pm_search, S.c_search)) + " needs more LDS than the gather kernel has");
 			return false;
 		}
 	}
@@ -690,13 +779,14 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		lightLayout(1.f, tmp);
 	}
 	const int K = std::max(1, S.nee_k);
-	const bool need_v0 = S.path_samples > 1 || S.integrator == INT_PHOTON;
+	const bool need_v0 = S.path_samples > 1 || S.integrator == INT_PHOTON || S.caus_map;
+	const bool need_g = S.gather_on != 0;
 	// segment capacity: the camera deals groups of 256 samples round-robin over the segments
 	const size_t R = (size_t)d.shade_grid;
 	auto shardCap = [R](size_t m) { return (((m + 255) / 256 + R - 1) / R) * 256; };
 	const bool need_attr = S.has_attr != 0;
 	const int need_ts = S.tr_shad ? std::max(1, S.s_depth) : 0;
-	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc || need_ts != d.ts_alloc)
+	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc || need_ts != d.ts_alloc || need_g != d.g_alloc)
 	{
 		// Wavefront buffers for M samples in flight (~0.7 KB each: 288 GB of HBM holds tens of millions,
 		// and big chunks amortise the per-launch cost).  On allocation failure the chunk is halved.
@@ -753,6 +843,12 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			d.N.wo_k = (float4 *)A(MA * 16);
 			d.N.pix_mode = (uint4 *)A(MA * 16);
 			d.N.attr = (float4 *)A(need_attr ? MA * 32 : 16);
+			d.N.extra = nullptr;
+			d.G.p_prim = (float4 *)A(need_g ? MA * 16 : 16);
+			d.G.wo_k = (float4 *)A(need_g ? MA * 16 : 16);
+			d.G.pix_mode = (uint4 *)A(need_g ? MA * 16 : 16);
+			d.G.extra = (float4 *)A(need_g ? MA * 16 : 16);
+			d.G.attr = (float4 *)A(need_g && need_attr ? MA * 32 : 16);
 			bool ok = true;
 			for(const Buf &b : d.chunk_bufs) ok = ok && b.p;
 			if(ok) break;
@@ -763,23 +859,25 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		d.v0_alloc = need_v0;
 		d.attr_alloc = need_attr;
 		d.ts_alloc = need_ts;
+		d.g_alloc = need_g;
 		d.slots_cap = M;
 		d.nee_cap = K;
 	}
 	S.n_seg = (uint32_t)R;
 	S.cap_a = (uint32_t)shardCap(d.slots_cap);
 	S.cap_s = S.cap_a * (uint32_t)K;
-	if(!ensure(log_, d.counters, 2 * 3 * R * sizeof(uint32_t))) return false;
+	if(!ensure(log_, d.counters, 2 * 4 * R * sizeof(uint32_t))) return false;
 	if(!ensure(log_, d.stats, sizeof(DevStats) * (size_t)d.trace_grid)) return false;
-	HIPCHECK(hipMemsetAsync(d.counters.p, 0, 2 * 3 * R * sizeof(uint32_t), d.stream));
+	HIPCHECK(hipMemsetAsync(d.counters.p, 0, 2 * 4 * R * sizeof(uint32_t), d.stream));
 	HIPCHECK(hipMemsetAsync(d.stats.p, 0, sizeof(DevStats) * (size_t)d.trace_grid, d.stream));
 	DevCounters cnt[2];
 	for(int q = 0; q < 2; ++q)
 	{
-		uint32_t *base_q = (uint32_t *)d.counters.p + (size_t)q * 3 * R;
+		uint32_t *base_q = (uint32_t *)d.counters.p + (size_t)q * 4 * R;
 		cnt[q].n_active = base_q;
 		cnt[q].n_shadow = base_q + R;
 		cnt[q].n_nee = base_q + 2 * R;
+		cnt[q].n_gather = base_q + 3 * R;
 	}
 	DevStats *dstats = (DevStats *)d.stats.p;
 	S.stats = dstats;
@@ -810,14 +908,18 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// transparent shadows: filter colours of the transparent surfaces the shadow rays crossed
 			if(S.tr_shad) PROF(KK_TSHADOW, yafamd_launch_tshadow(&S, &d.Q[cur], &cnt[cur], &d.P[cur], d.stream));
 			if(S.has_attr) PROF(KK_SURFACE, yafamd_launch_surface(&S, &d.Q[cur], &cnt[cur], d.stream));
-			PROF(KK_SHADE, yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &cnt[cur], &cnt[cur ^ 1],
+			PROF(KK_SHADE, yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &d.G, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 
-			// photon mapping follows the direct-lighting pipeline: NEE requests in iteration 0, the
-			// photon density estimates of the connected camera hits in iteration 1
-			if(S.integrator == INT_PHOTON && it == 1)
-				PROF(KK_GATHER, yafamd_launch_gather(&S, &d.N, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
-			else if(S.ext || !yafamd_shade_fused()) PROF(KK_NEE, yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));
+			// photon-map estimates of the finished diffuse first hits: the direct-lighting pipeline
+			// (photon mapping, DirectLight) connects its NEE in iteration 1 and finishes there; path
+			// tracing finishes paths in any iteration
+			const bool dl_pipeline = S.integrator != INT_PATH;
+			if(S.gather_on && (!dl_pipeline || it == 1))
+				PROF(KK_GATHER, yafamd_launch_gather(&S, &d.G, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
+			// NEE requests (none in iteration 1 of photon mapping, whose entries all finish there)
+			if((S.ext || !yafamd_shade_fused()) && !(S.integrator == INT_PHOTON && it == 1))
+				PROF(KK_NEE, yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));
 			// (non-EXT k_shade runs the NEE itself: FUSED)
 			cur ^= 1;
 		}

@@ -41,7 +41,11 @@ struct HostScene
 struct PhotonParams
 {
 	int photons = 0;           // diffuse photons to shoot (0: no diffuse map)
-	int caustic_photons = 0;   // caustic photons (shot; stored only after specular bounces)
+	int caustic_photons = 0;   // caustic photons to shoot
+	bool caustic_map = false;  // build the caustic map and add causticPhotons() at diffuse hits
+	int caustic_search = 50;   // "caustic_mix"
+	float caustic_radius = 0.25f;
+	int caustic_depth = 10;
 	int search = 50;           // k of the k-NN gather
 	float radius2 = 0.1f;      // "diffuseRadius" (squared radius of the gather)
 	int bounces = 5;
@@ -122,6 +126,7 @@ class GpuRenderer
 		bool filmToDevice(void *dst, int y0, int y1);
 		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
 		bool buildPhotonMap(RenderParams &rp);
+		bool shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int bounces, int which, uint32_t &n_out, int &depth_out);
 
 		// ---- render group: the film split into contiguous row bands over several GPUs ----
 		// One member per GPU (one process per GPU, each calling joinGroup with the same RCCL id).

@@ -84,6 +84,8 @@ class Light:
     point2: tuple = (0.0, 0.0, 0.0)
     samples: int = 1
     cast_shadows: bool = True
+    with_caustic: bool = True              # shoots caustic photons (light_area.cc / light_point.cc params)
+    with_diffuse: bool = True              # shoots diffuse photons
 
 
 @dataclass
@@ -158,8 +160,11 @@ class Render:
     pm_search: int = 50
     pm_diffuse_radius: float = 0.1
     pm_bounces: int = 5
-    pm_caustics: bool = False
-    pm_caustic_photons: int = 500000
+    pm_caustics: bool = False               # PhotonIntegrator / DirectLight "caustics"
+    pm_caustic_photons: int = 500000        # PM "cPhotons"; DirectLight / PathIntegrator "photons"
+    caustic_search: int = None              # "caustic_mix" (PM default: search; DL / PT: 100)
+    caustic_radius: float = None            # PM "causticRadius" (0.01); DL / PT "caustic_radius" (0.25)
+    caustic_depth: int = None               # DL / PT "caustic_depth" (10); PM uses "bounces"
     threads_photons: int = 1
     # DirectLight ambient occlusion (integrator_direct_light.cc:161-186)
     do_ao: bool = False
@@ -397,6 +402,29 @@ def set_typed(api, k, tv):
         raise ValueError(f"unknown parameter kind {kind!r}")
 
 
+@dataclass
+class CausticParams:
+    enabled: bool
+    photons: int
+    search: int
+    radius: float
+    depth: int
+
+
+def caustic_params(r) -> CausticParams:
+    """The caustic photon map settings of render spec `r` with each integrator's defaults
+    (PhotonIntegrator::factory integrator_photon_mapping.cc:765-850, DirectLightIntegrator::factory
+    integrator_direct_light.cc:147-190, PathIntegrator::factory integrator_path_tracer.cc:325-342)."""
+    if r.integrator == "photonmapping":
+        return CausticParams(bool(r.pm_caustics), r.pm_caustic_photons,
+                             r.caustic_search if r.caustic_search is not None else r.pm_search,
+                             r.caustic_radius if r.caustic_radius is not None else 0.01, r.pm_bounces)
+    enabled = bool(r.pm_caustics) if r.integrator == "directlighting" else r.caustic_type in ("photon", "both")
+    return CausticParams(enabled, r.pm_caustic_photons, r.caustic_search if r.caustic_search is not None else 100,
+                         r.caustic_radius if r.caustic_radius is not None else 0.25,
+                         r.caustic_depth if r.caustic_depth is not None else 10)
+
+
 def apply(spec: SceneSpec, api) -> None:
     """Issue the reference C-API call sequence for `spec` on `api` (a libyafaray_amd.Interface)."""
     api.createScene()
@@ -463,6 +491,10 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetColor("color", *l.color, 1.0)
         api.paramsSetFloat("power", l.power)
         api.paramsSetBool("cast_shadows", l.cast_shadows)
+        if not l.with_caustic:
+            api.paramsSetBool("with_caustic", False)
+        if not l.with_diffuse:
+            api.paramsSetBool("with_diffuse", False)
         if l.type == "pointlight":
             api.paramsSetVector("from", *l.from_)
         else:
@@ -549,6 +581,7 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetFloat("power", spec.background.power)
         api.createBackground("world_background")
     r = spec.render
+    cm = caustic_params(r)
     api.paramsClearAll()
     api.paramsSetString("type", r.integrator)
     api.paramsSetInt("raydepth", r.raydepth)
@@ -561,6 +594,11 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetInt("path_samples", r.path_samples)
         api.paramsSetInt("russian_roulette_min_bounces", r.rr_min_bounces)
         api.paramsSetString("caustic_type", r.caustic_type)
+    if r.integrator in ("pathtracing", "directlighting") and cm.enabled:
+        api.paramsSetInt("photons", cm.photons)
+        api.paramsSetInt("caustic_mix", cm.search)
+        api.paramsSetInt("caustic_depth", cm.depth)
+        api.paramsSetFloat("caustic_radius", cm.radius)
     if r.integrator == "photonmapping":
         api.paramsSetInt("photons", r.pm_photons)
         api.paramsSetInt("cPhotons", r.pm_caustic_photons)
@@ -568,6 +606,8 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetFloat("diffuseRadius", r.pm_diffuse_radius)
         api.paramsSetInt("bounces", r.pm_bounces)
         api.paramsSetBool("caustics", r.pm_caustics)
+        api.paramsSetInt("caustic_mix", cm.search)
+        api.paramsSetFloat("causticRadius", cm.radius)
         api.paramsSetBool("finalGather", False)
     if r.integrator == "directlighting" and r.pm_caustics:
         api.paramsSetBool("caustics", True)

@@ -63,7 +63,7 @@ class yc_object(C.Structure):
 class yc_light(C.Structure):
     _fields_ = [("type", C.c_int), ("color", C.c_float * 3), ("power", C.c_float), ("from_", C.c_float * 3),
                 ("point1", C.c_float * 3), ("point2", C.c_float * 3), ("samples", C.c_int),
-                ("cast_shadows", C.c_int)]
+                ("cast_shadows", C.c_int), ("shoot_caustic", C.c_int), ("shoot_diffuse", C.c_int)]
 
 
 class yc_camera(C.Structure):
@@ -88,7 +88,9 @@ class yc_render(C.Structure):
                 ("aa_dark_threshold_factor", C.c_float), ("aa_variance_edge_size", C.c_int), ("aa_variance_pixels", C.c_int),
                 ("raydepth", C.c_int), ("bg_transp_refract", C.c_int),
                 ("transp_shad", C.c_int), ("shadow_depth", C.c_int), ("do_ao", C.c_int), ("ao_samples", C.c_int),
-                ("ao_dist", C.c_float), ("ao_col", C.c_float * 3), ("aa_light_sample_multiplier_factor", C.c_float)]
+                ("ao_dist", C.c_float), ("ao_col", C.c_float * 3), ("aa_light_sample_multiplier_factor", C.c_float),
+                ("caus_map", C.c_int), ("caus_photons", C.c_int), ("caus_search", C.c_int), ("caus_depth", C.c_int),
+                ("caus_radius", C.c_float)]
 
 
 class yc_scene(C.Structure):
@@ -511,6 +513,8 @@ class OracleScene:
             lights[i].point1[:] = list(l.point1)
             lights[i].point2[:] = list(l.point2)
             lights[i].samples = l.samples
+            lights[i].shoot_caustic = int(getattr(l, "with_caustic", True))
+            lights[i].shoot_diffuse = int(getattr(l, "with_diffuse", True))
             lights[i].cast_shadows = int(l.cast_shadows)
         self.mats, self.lights = mats, lights
         sc = yc_scene()
@@ -555,6 +559,10 @@ class OracleScene:
         rp.rr_seed = rr_seed
         rp.pm_photons, rp.pm_search, rp.pm_diffuse_radius = r.pm_photons, r.pm_search, r.pm_diffuse_radius
         rp.pm_bounces, rp.pm_caustics, rp.pm_threads = r.pm_bounces, int(r.pm_caustics), r.threads_photons
+        from libyafaray_amd.scenes import caustic_params
+        cm = caustic_params(r)
+        rp.caus_map, rp.caus_photons, rp.caus_search = int(cm.enabled), cm.photons, cm.search
+        rp.caus_depth, rp.caus_radius = cm.depth, cm.radius
         rp.aa_passes = max(1, r.aa_passes)
         rp.aa_inc_samples = r.aa_inc_samples if r.aa_inc_samples > 0 else r.aa_samples
         rp.aa_threshold, rp.aa_resampled_floor = r.aa_threshold, r.aa_resampled_floor
@@ -581,18 +589,20 @@ class OracleScene:
                                      _p(w, C.c_float), C.byref(ctr))
         return rgba.reshape(r.height, r.width, 4), w.reshape(r.height, r.width), (ctr.closest_rays, ctr.shadow_rays)
 
-    def photon_map(self):
-        """(pos, dir, col [n x 3 each], kd nodes [m x 2 uint32], n_paths) of the diffuse photon map."""
+    def photon_map(self, which="diffuse"):
+        """(pos, dir, col [n x 3 each], kd nodes [m x 2 uint32], n_paths) of the diffuse or caustic map."""
         L = oracle_lib()
+        w = 1 if which == "caustic" else 0
         n_paths = C.c_int(0)
-        n = L.yc_photon_map(C.byref(self.sc), None, None, None, None, C.byref(n_paths))
+        n = L.yc_photon_map_ex(C.byref(self.sc), w, None, None, None, None, C.byref(n_paths))
         if n < 0:
             raise RuntimeError("photon map failed (too few photons)")
-        pos, d, col = (np.empty(3 * n, np.float32) for _ in range(3))
+        pos, d, col = (np.empty(3 * max(1, n), np.float32) for _ in range(3))
         nodes = np.empty(2 * max(1, 2 * n - 1), np.uint32)
-        L.yc_photon_map(C.byref(self.sc), _p(pos, C.c_float), _p(d, C.c_float), _p(col, C.c_float),
-                        _p(nodes, C.c_uint32), C.byref(n_paths))
-        return pos.reshape(n, 3), d.reshape(n, 3), col.reshape(n, 3), nodes.reshape(-1, 2)[:max(0, 2 * n - 1)], n_paths.value
+        L.yc_photon_map_ex(C.byref(self.sc), w, _p(pos, C.c_float), _p(d, C.c_float), _p(col, C.c_float),
+                           _p(nodes, C.c_uint32), C.byref(n_paths))
+        return (pos[:3 * n].reshape(n, 3), d[:3 * n].reshape(n, 3), col[:3 * n].reshape(n, 3),
+                nodes.reshape(-1, 2)[:max(0, 2 * n - 1)], n_paths.value)
 
     def render_samples(self, xys):
         xys = np.ascontiguousarray(xys, np.int32).reshape(-1)

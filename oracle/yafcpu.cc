@@ -486,6 +486,7 @@ struct Light
 	V3 corner, to_x, to_y, fnormal, normal, du, dv, c2, c3, c4;
 	float area = 0.f, inv_area = 0.f;
 	int samples = 1;
+	bool shoot_caustic = true, shoot_diffuse = true;   // "with_caustic" / "with_diffuse"
 };
 
 struct Tri
@@ -805,6 +806,8 @@ Scene::Scene(const yc_scene &s)
 		Light L;
 		L.type = l.type;
 		L.cast_shadows = l.cast_shadows != 0;
+		L.shoot_caustic = l.shoot_caustic != 0;
+		L.shoot_diffuse = l.shoot_diffuse != 0;
 		const C3 col(l.color[0], l.color[1], l.color[2]);
 		if(l.type == YC_LIGHT_POINT)
 		{
@@ -1708,6 +1711,7 @@ class Renderer
 		               int additional_depth = 0) const
 		{
 			if(sc_.rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha, ray_level, additional_depth);
+			else if(sc_.rp.integrator == YC_INT_PHOTON) integratePhoton(th, ray, rng, sample_idx, offset, col, alpha, ray_level, additional_depth);
 			else integrateDirect(th, ray, rng, sample_idx, offset, col, alpha, ray_level, additional_depth);
 		}
 
@@ -1978,6 +1982,7 @@ class Renderer
 				if(mat_bsdfs & BDiffuse)
 				{
 					col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+					if(sc_.rp.caus_map) col += causticPhotons(sp, wo);                                  // :120-123
 					if(sc_.rp.do_ao) col += sampleAmbientOcclusion(th, sp, wo, sample_idx, offset);   // :124
 				}
 				C3 rcol;
@@ -2001,7 +2006,11 @@ class Renderer
 			const V3 wo = -ray.dir;
 			additional_depth = std::max(additional_depth, sp.mat->additional_depth);   // path_tracer.cc:133
 			if(mat_bsdfs & BEmit) col += emit(sp, wo);
-			if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+			if(mat_bsdfs & BDiffuse)
+			{
+				col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+				if(sc_.rp.caus_map) col += causticPhotons(sp, wo);   // path_tracer.cc:149-152 (caustic_type photon | both)
+			}
 			unsigned path_flags = BDiffuse;
 			if(mat_bsdfs & path_flags)
 			{
@@ -2086,9 +2095,17 @@ class Renderer
 			float split() const { float f; std::memcpy(&f, &data, 4); return f; }
 			uint32_t right() const { return flags >> 2; }
 		};
-		std::vector<Photon> photons;
-		std::vector<PkNode> pk_nodes;
-		int n_paths = 0;
+		// photon.h:103-140 PhotonMap: photons in append order (photon-id order: one reference
+		// thread's order), the kd-tree over them, and the number of shot paths
+		struct PhotonMapData
+		{
+			std::vector<Photon> photons;
+			std::vector<PkNode> nodes;
+			int n_paths = 0;
+			bool ready() const { return !nodes.empty(); }   // updateTree ran on a non-empty map
+		};
+		PhotonMapData dmap;   // diffuse map (PhotonIntegrator)
+		PhotonMapData cmap;   // caustic map (MonteCarloIntegrator::createCausticMap)
 
 		// include/sampler/sample_pdf1d.h:52-93 (cumulateStep1DDf + dSample)
 		struct Pdf1D
@@ -2159,12 +2176,14 @@ class Renderer
 			return (e.r + e.g + e.b) * 0.333333f;
 		}
 
-		// material.cc:137-153 (Material::scatterPhoton) with PSample (material.h:260-268)
+		// material.cc:137-153 (Material::scatterPhoton) with PSample (material.h:260-268); `flags` is
+		// PSample's flag set: All for the diffuse map, AllSpecular | Glossy | Filter | Dispersive for
+		// the caustic map (integrator_montecarlo.cc:497)
 		bool scatterPhoton(const SurfacePoint &sp, const V3 &wi, V3 &wo, float s_1, float s_2, float s_3, const C3 &lcol,
-		                   C3 &color_out, unsigned &sampled) const
+		                   C3 &color_out, unsigned &sampled, unsigned flags = BAll) const
 		{
 			float w = 0.f;
-			Sample s(s_1, s_2, BAll);
+			Sample s(s_1, s_2, flags);
 			const C3 scol = sample(sp, wi, wo, s, w);
 			sampled = s.sampled_flags;
 			if(s.pdf > 1.0e-6f)
@@ -2183,15 +2202,26 @@ class Renderer
 			return false;
 		}
 
+		// render_view.cc:103-110 getLightsEmittingDiffusePhotons / getLightsEmittingCausticPhotons
+		std::vector<const Light *> photonLights(bool caustic) const
+		{
+			std::vector<const Light *> v;
+			for(const Light &L : sc_.lights)
+				if(caustic ? L.shoot_caustic : L.shoot_diffuse) v.push_back(&L);
+			return v;
+		}
+
 		// integrator_photon_mapping.cc:110-235 (diffuseWorker), photons in photon-id order
 		void shootDiffusePhotons(Thread &th)
 		{
 			const yc_render &rp = sc_.rp;
-			photons.clear();
-			const int num_lights = (int)sc_.lights.size();
-			if(num_lights == 0 || rp.pm_photons <= 0) { n_paths = 0; return; }
+			PhotonMapData &M = dmap;
+			M.photons.clear();
+			const std::vector<const Light *> lights = photonLights(false);
+			const int num_lights = (int)lights.size();
+			if(num_lights == 0 || rp.pm_photons <= 0) { M.n_paths = 0; return; }
 			std::vector<float> energies(num_lights);
-			for(int i = 0; i < num_lights; ++i) energies[i] = lightEnergy(sc_.lights[i]);
+			for(int i = 0; i < num_lights; ++i) energies[i] = lightEnergy(*lights[i]);
 			const Pdf1D light_power(energies);
 			const int T = std::max(1, rp.pm_threads);
 			const unsigned n_photons = std::max((unsigned)T, ((unsigned)rp.pm_photons / T) * T);   // :437
@@ -2208,7 +2238,7 @@ class Renderer
 				const int light_num = light_power.dSample(s_l, light_num_pdf);
 				Ray ray;
 				float light_pdf;
-				C3 pcol = emitPhoton(sc_.lights[light_num], s_1, s_2, s_3, s_4, ray, light_pdf);
+				C3 pcol = emitPhoton(*lights[light_num], s_1, s_2, s_3, s_4, ray, light_pdf);
 				ray.tmin = rp.ray_min_dist;
 				ray.tmax = -1.f;
 				pcol = pcol * (f_num_lights * light_pdf / light_num_pdf);
@@ -2222,7 +2252,7 @@ class Renderer
 					const V3 wi = -ray.dir;
 					if(sp.bsdf_flags & BDiffuse)
 					{
-						if(!caustic_photon) photons.push_back({sp.p, wi, pcol});
+						if(!caustic_photon) M.photons.push_back({sp.p, wi, pcol});
 					}
 					if(n_bounces == rp.pm_bounces) break;
 					const int d_5 = 3 * n_bounces + 5;
@@ -2244,33 +2274,104 @@ class Renderer
 					++n_bounces;
 				}
 			}
-			n_paths = (int)n_photons;
+			M.n_paths = (int)n_photons;
+		}
+
+		// integrator_montecarlo.cc:421-544 (causticWorker) with createCausticMap's photon count
+		// (:588-604), photons in photon-id order: a photon is stored on a diffuse / glossy surface
+		// only after a specular / glossy (/ filter) bounce, and paths scatter only specularly
+		void shootCausticPhotons(Thread &th)
+		{
+			const yc_render &rp = sc_.rp;
+			PhotonMapData &M = cmap;
+			M.photons.clear();
+			M.nodes.clear();
+			M.n_paths = 0;
+			const std::vector<const Light *> lights = photonLights(true);
+			const int num_lights = (int)lights.size();
+			if(num_lights == 0 || !rp.caus_map) return;
+			std::vector<float> energies(num_lights);
+			for(int i = 0; i < num_lights; ++i) energies[i] = lightEnergy(*lights[i]);
+			const Pdf1D light_power(energies);
+			const int T = std::max(1, rp.pm_threads);
+			const unsigned n_photons = std::max((unsigned)T, ((unsigned)std::max(0, rp.caus_photons) / T) * T);   // :604
+			const float f_num_lights = static_cast<float>(num_lights);
+			const unsigned flags = BSpecular | BReflect | BTransmit | BGlossy | BFilter | BDispersive;   // :497
+			for(unsigned h = 0; h < n_photons; ++h)
+			{
+				const float s_1 = riVdC(h);
+				const float s_2 = static_cast<float>(lowDiscrepancySampling(2, h));
+				const float s_3 = static_cast<float>(lowDiscrepancySampling(3, h));
+				const float s_4 = static_cast<float>(lowDiscrepancySampling(4, h));
+				const float s_l = static_cast<float>(h) / static_cast<float>(n_photons);   // :444
+				float light_num_pdf;
+				const int light_num = light_power.dSample(s_l, light_num_pdf);
+				Ray ray;
+				float light_pdf;
+				C3 pcol = emitPhoton(*lights[light_num], s_1, s_2, s_3, s_4, ray, light_pdf);
+				ray.tmin = rp.ray_min_dist;
+				ray.tmax = -1.f;
+				pcol = pcol * (f_num_lights * light_pdf / light_num_pdf);
+				if(pcol.r == 0.f && pcol.g == 0.f && pcol.b == 0.f) continue;
+				int n_bounces = 0;
+				bool caustic_photon = false, direct_photon = true;
+				for(;;)
+				{
+					SurfacePoint sp;
+					if(!intersect(th, ray, sp)) break;
+					const V3 wi = -ray.dir;
+					if(sp.bsdf_flags & (BDiffuse | BGlossy))
+					{
+						if(caustic_photon) M.photons.push_back({sp.p, wi, pcol});
+					}
+					if(n_bounces == rp.caus_depth) break;
+					const int d_5 = 3 * n_bounces + 5;
+					const float s_5 = static_cast<float>(lowDiscrepancySampling(d_5, h));
+					const float s_6 = static_cast<float>(lowDiscrepancySampling(d_5 + 1, h));
+					const float s_7 = static_cast<float>(lowDiscrepancySampling(d_5 + 2, h));
+					V3 wo;
+					C3 ncol;
+					unsigned sampled = BNone;
+					if(!scatterPhoton(sp, wi, wo, s_5, s_6, s_7, pcol, ncol, sampled, flags)) break;
+					pcol = ncol;
+					caustic_photon = ((sampled & (BGlossy | BSpecular | BDispersive)) && direct_photon) ||
+					                 ((sampled & (BGlossy | BSpecular | BFilter | BDispersive)) && caustic_photon);
+					direct_photon = (sampled & BFilter) && direct_photon;
+					if(!(caustic_photon || direct_photon)) break;   // :520-521
+					ray.from = sp.p;
+					ray.dir = wo;
+					ray.tmin = rp.ray_min_dist;
+					ray.tmax = -1.f;
+					++n_bounces;
+				}
+			}
+			M.n_paths = (int)n_photons;
 		}
 
 		// pkdtree.h:115-222 (the threaded and sequential builds produce the same DFS layout)
-		void buildPhotonTree()
+		static void buildPhotonTree(PhotonMapData &M)
 		{
-			const uint32_t n = (uint32_t)photons.size();
-			pk_nodes.assign(n ? 2 * (size_t)n - 1 : 0, PkNode());
+			const uint32_t n = (uint32_t)M.photons.size();
+			M.nodes.assign(n ? 2 * (size_t)n - 1 : 0, PkNode());
 			if(!n) return;
 			std::vector<uint32_t> el(n);
 			for(uint32_t i = 0; i < n; ++i) el[i] = i;
-			V3 lo = photons[0].pos, hi = photons[0].pos;
+			V3 lo = M.photons[0].pos, hi = M.photons[0].pos;
 			for(uint32_t i = 1; i < n; ++i)
 				for(int a = 0; a < 3; ++a)
 				{
-					lo[a] = std::min(lo[a], photons[i].pos[a]);
-					hi[a] = std::max(hi[a], photons[i].pos[a]);
+					lo[a] = std::min(lo[a], M.photons[i].pos[a]);
+					hi[a] = std::max(hi[a], M.photons[i].pos[a]);
 				}
 			uint32_t next = 0;
-			buildRec(0, n, lo, hi, el.data(), next);
+			buildRec(M, 0, n, lo, hi, el.data(), next);
 		}
-		void buildRec(uint32_t start, uint32_t end, V3 lo, V3 hi, uint32_t *el, uint32_t &next)
+		static void buildRec(PhotonMapData &M, uint32_t start, uint32_t end, V3 lo, V3 hi, uint32_t *el, uint32_t &next)
 		{
 			if(end - start == 1)
 			{
-				pk_nodes[next].flags = 3;
-				pk_nodes[next].data = el[start];
+				M.nodes[next].flags = 3;
+				M.nodes[next].data = el[start];
 				++next;
 				return;
 			}
@@ -2280,20 +2381,20 @@ class Renderer
 			const uint32_t split_el = (start + end) / 2;
 			// pkdtree.h:66-74 CompareNode: by coordinate, ties by element address (= index)
 			std::nth_element(el + start, el + split_el, el + end, [&](uint32_t a, uint32_t b) {
-				const float pa = photons[a].pos[axis], pb = photons[b].pos[axis];
+				const float pa = M.photons[a].pos[axis], pb = M.photons[b].pos[axis];
 				return pa == pb ? (a < b) : pa < pb;
 			});
 			const uint32_t cur = next;
-			const float split_pos = photons[el[split_el]].pos[axis];
-			std::memcpy(&pk_nodes[cur].data, &split_pos, 4);
-			pk_nodes[cur].flags = (uint32_t)axis;
+			const float split_pos = M.photons[el[split_el]].pos[axis];
+			std::memcpy(&M.nodes[cur].data, &split_pos, 4);
+			M.nodes[cur].flags = (uint32_t)axis;
 			++next;
 			V3 hi_l = hi, lo_r = lo;
 			hi_l[axis] = split_pos;
 			lo_r[axis] = split_pos;
-			buildRec(start, split_el, lo, hi_l, el, next);
-			pk_nodes[cur].flags = (pk_nodes[cur].flags & 3u) | (next << 2);
-			buildRec(split_el, end, lo_r, hi, el, next);
+			buildRec(M, start, split_el, lo, hi_l, el, next);
+			M.nodes[cur].flags = (M.nodes[cur].flags & 3u) | (next << 2);
+			buildRec(M, split_el, end, lo_r, hi, el, next);
 		}
 
 		// photon.h:93-100 FoundPhoton (operator< on the squared distance)
@@ -2305,7 +2406,7 @@ class Renderer
 		};
 
 		// pkdtree.h:225-292 (non-recursive lookup) + photon.cc:31-52 (PhotonGather heap management)
-		int gather(const V3 &p, Found *found, uint32_t k, float &max_dist_squared) const
+		static int gather(const PhotonMapData &M, const V3 &p, Found *found, uint32_t k, float &max_dist_squared)
 		{
 			struct Stack { int node; float s; int axis; };
 			Stack stack[64];
@@ -2315,26 +2416,26 @@ class Renderer
 			stack[sp].node = -1;
 			for(;;)
 			{
-				while(!pk_nodes[curr].isLeaf())
+				while(!M.nodes[curr].isLeaf())
 				{
-					const int axis = pk_nodes[curr].axis();
-					const float split_val = pk_nodes[curr].split();
+					const int axis = M.nodes[curr].axis();
+					const float split_val = M.nodes[curr].split();
 					int far_child;
-					if(p[axis] <= split_val) { far_child = (int)pk_nodes[curr].right(); curr = curr + 1; }
-					else { far_child = curr + 1; curr = (int)pk_nodes[curr].right(); }
+					if(p[axis] <= split_val) { far_child = (int)M.nodes[curr].right(); curr = curr + 1; }
+					else { far_child = curr + 1; curr = (int)M.nodes[curr].right(); }
 					++sp;
 					stack[sp].node = far_child;
 					stack[sp].axis = axis;
 					stack[sp].s = split_val;
 				}
-				const Photon &ph = photons[pk_nodes[curr].data];
+				const Photon &ph = M.photons[M.nodes[curr].data];
 				const V3 v = ph.pos - p;
 				float dist_2 = v.lengthSqr();
 				if(dist_2 < max_dist_squared)
 				{
 					if(n_found < k)
 					{
-						found[n_found++] = {pk_nodes[curr].data, dist_2};
+						found[n_found++] = {M.nodes[curr].data, dist_2};
 						if(n_found == k)
 						{
 							std::make_heap(found, found + k);
@@ -2344,7 +2445,7 @@ class Renderer
 					else
 					{
 						std::pop_heap(found, found + k);
-						found[k - 1] = {pk_nodes[curr].data, dist_2};
+						found[k - 1] = {M.nodes[curr].data, dist_2};
 						std::push_heap(found, found + k);
 						max_dist_squared = found[0].dist_square;
 					}
@@ -2366,8 +2467,42 @@ class Renderer
 			}
 		}
 
+		// sample.h:31-35 kernel: 3 / (pi r^2) (1 - d^2 / r^2)^2, the product formed in long double
+		static float photonKernel(float r_photon_2, float ir_gather_2)
+		{
+			const float s = (1.f - r_photon_2 * ir_gather_2);
+			return static_cast<float>(3.f * ir_gather_2 * div_1_by_pi * s * s);
+		}
+
+		// MonteCarloIntegrator::estimateCausticPhotons (integrator_montecarlo.cc:627-648) via
+		// causticPhotons (:410-419; clamp_indirect = 0)
+		C3 causticPhotons(const SurfacePoint &sp, const V3 &wo) const
+		{
+			const yc_render &rp = sc_.rp;
+			if(!cmap.ready()) return C3(0.f);
+			std::vector<Found> gathered((size_t)std::max(1, rp.caus_search));
+			const float caus_radius = rp.caus_radius;
+			float g_radius_square = caus_radius * caus_radius;
+			const int n_gathered = gather(cmap, sp.p, gathered.data(), (uint32_t)rp.caus_search, g_radius_square);
+			g_radius_square = 1.f / g_radius_square;
+			C3 sum(0.f);
+			if(n_gathered > 0)
+			{
+				for(int i = 0; i < n_gathered; ++i)
+				{
+					const Photon &ph = cmap.photons[gathered[i].photon];
+					const C3 surf_col = eval(sp, wo, ph.dir, BAll);
+					const float k = photonKernel(gathered[i].dist_square, g_radius_square);
+					sum += surf_col * k * ph.col;
+				}
+				sum *= 1.f / static_cast<float>(cmap.n_paths);
+			}
+			return sum;
+		}
+
 		// integrator_photon_mapping.cc:852-1004 with finalGather = false, show_map = false
-		void integratePhoton(Thread &th, Ray &ray, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha) const
+		void integratePhoton(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level = 0,
+		                     int additional_depth = 0) const
 		{
 			const yc_render &rp = sc_.rp;
 			col = C3(0.f);
@@ -2377,38 +2512,47 @@ class Renderer
 			{
 				const V3 wo = -ray.dir;
 				const unsigned mat_bsdfs = sp.bsdf_flags;
+				additional_depth = std::max(additional_depth, sp.mat->additional_depth);   // :863
 				col += emit(sp, wo);                                   // :868-869
 				if(mat_bsdfs & BEmit) col += emit(sp, wo);             // :938-946 (added a second time)
 				if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
 				std::vector<Found> gathered((size_t)std::max(1, rp.pm_search));
 				float radius = rp.pm_diffuse_radius;                   // "actually the square radius"
 				int n_gathered = 0;
-				if(!photons.empty()) n_gathered = gather(sp.p, gathered.data(), (uint32_t)rp.pm_search, radius);
+				if(!dmap.photons.empty()) n_gathered = gather(dmap, sp.p, gathered.data(), (uint32_t)rp.pm_search, radius);
 				if(n_gathered > 0)
 				{
-					const float scale = 1.f / ((float)n_paths * radius * num_pi);
+					const float scale = 1.f / ((float)dmap.n_paths * radius * num_pi);
 					for(int i = 0; i < n_gathered; ++i)
 					{
-						const Photon &ph = photons[gathered[i].photon];
+						const Photon &ph = dmap.photons[gathered[i].photon];
 						const C3 surf_col = eval(sp, wo, ph.dir, BDiffuse);
 						const C3 col_tmp = surf_col * scale * ph.col;
 						col += col_tmp;
 					}
 				}
-				if(rp.pm_caustics && (mat_bsdfs & BDiffuse)) col += C3(0.f);   // empty caustic map (:981-984, montecarlo.cc:644)
-				col += C3(0.f);   // recursiveRaytrace: no specular/glossy components
-				alpha = 1.f;
+				if(rp.caus_map && (mat_bsdfs & BDiffuse)) col += causticPhotons(sp, wo);   // :981-984
+				C3 rcol;
+				recursiveRaytrace(th, rng, ray_level + 1, mat_bsdfs, sp, wo, sample_idx, offset, rcol, alpha, additional_depth);   // :986
+				col += rcol;
 			}
-			else background(ray, col, alpha);
+			else background(ray, col, alpha, ray_level);
 		}
 
+		// preprocess: the caustic map (PathIntegrator / DirectLight / PhotonIntegrator, when enabled),
+		// then the diffuse map (PhotonIntegrator)
 		bool preprocessPhotons()
 		{
-			if(sc_.rp.integrator != YC_INT_PHOTON) return true;
 			Thread th;
+			if(sc_.rp.caus_map)
+			{
+				shootCausticPhotons(th);
+				if(!cmap.photons.empty()) buildPhotonTree(cmap);
+			}
+			if(sc_.rp.integrator != YC_INT_PHOTON) return true;
 			shootDiffusePhotons(th);
-			if(photons.size() < 50) return false;   // :448-452 "Too few diffuse photons"
-			buildPhotonTree();
+			if(dmap.photons.size() < 50) return false;   // :448-452 "Too few diffuse photons"
+			buildPhotonTree(dmap);
 			return true;
 		}
 
@@ -2461,7 +2605,7 @@ class Renderer
 				C3 col;
 				float alpha;
 				if(rp.integrator == YC_INT_PATH) integratePath(th, ray, rng, sample_idx, offset, col, alpha);
-				else if(rp.integrator == YC_INT_PHOTON) integratePhoton(th, ray, sample_idx, offset, col, alpha);
+				else if(rp.integrator == YC_INT_PHOTON) integratePhoton(th, ray, rng, sample_idx, offset, col, alpha);
 				else integrateDirect(th, ray, rng, sample_idx, offset, col, alpha);
 				if(alpha > 1.f) alpha = 1.f;
 				out[4 * sample] = col.r;
@@ -2799,7 +2943,7 @@ int yc_render_samples(const yc_scene *s, int n, const int *xys, float *rgba)
 		float alpha;
 		const uint32_t sample_idx = rp.base_sampling_offset + sample;
 		if(rp.integrator == YC_INT_PATH) R.integratePath(th, ray, rng, sample_idx, offset, col, alpha);
-		else if(rp.integrator == YC_INT_PHOTON) R.integratePhoton(th, ray, sample_idx, offset, col, alpha);
+		else if(rp.integrator == YC_INT_PHOTON) R.integratePhoton(th, ray, rng, sample_idx, offset, col, alpha);
 		else R.integrateDirect(th, ray, rng, sample_idx, offset, col, alpha);
 		rgba[4 * k] = col.r; rgba[4 * k + 1] = col.g; rgba[4 * k + 2] = col.b; rgba[4 * k + 3] = std::min(alpha, 1.f);
 	}
@@ -2940,23 +3084,30 @@ void yc_film_table(int filter, float filter_size, float *table, float *filterw, 
 }
 
 
-int yc_photon_map(const yc_scene *s, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths)
+// which: 0 the diffuse map (PhotonIntegrator), 1 the caustic map
+int yc_photon_map_ex(const yc_scene *s, int which, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths)
 {
 	Scene sc(*s);
 	Renderer R(sc);
 	if(!R.preprocessPhotons()) return -1;
-	const size_t n = R.photons.size();
-	if(n_paths) *n_paths = R.n_paths;
+	const auto &M = which == 1 ? R.cmap : R.dmap;
+	const size_t n = M.photons.size();
+	if(n_paths) *n_paths = M.n_paths;
 	for(size_t i = 0; i < n; ++i)
 	{
-		const auto &p = R.photons[i];
+		const auto &p = M.photons[i];
 		if(pos) { pos[3 * i] = p.pos.x; pos[3 * i + 1] = p.pos.y; pos[3 * i + 2] = p.pos.z; }
 		if(dir) { dir[3 * i] = p.dir.x; dir[3 * i + 1] = p.dir.y; dir[3 * i + 2] = p.dir.z; }
 		if(col) { col[3 * i] = p.col.r; col[3 * i + 1] = p.col.g; col[3 * i + 2] = p.col.b; }
 	}
 	if(nodes)
-		for(size_t i = 0; i < R.pk_nodes.size(); ++i) { nodes[2 * i] = R.pk_nodes[i].data; nodes[2 * i + 1] = R.pk_nodes[i].flags; }
+		for(size_t i = 0; i < M.nodes.size(); ++i) { nodes[2 * i] = M.nodes[i].data; nodes[2 * i + 1] = M.nodes[i].flags; }
 	return (int)n;
+}
+
+int yc_photon_map(const yc_scene *s, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths)
+{
+	return yc_photon_map_ex(s, 0, pos, dir, col, nodes, n_paths);
 }
 
 // ---- texturing building blocks (yaftex.h), pinned against oracle/_ref ref_tex_* ----

@@ -101,6 +101,8 @@ typedef struct {
 	float point2[3];          // area light
 	int samples;              // area light
 	int cast_shadows;
+	int shoot_caustic;        // "with_caustic" (getLightsEmittingCausticPhotons)
+	int shoot_diffuse;        // "with_diffuse" (getLightsEmittingDiffusePhotons)
 } yc_light;
 
 typedef struct {
@@ -136,8 +138,7 @@ typedef struct {
 	int pm_search;            // "search" (k of the k-NN gather)
 	float pm_diffuse_radius;  // "diffuseRadius" — used as the SQUARED gather radius (:954)
 	int pm_bounces;           // "bounces"
-	int pm_caustics;          // "caustics": caustic photons are shot but only stored after specular
-	                          // bounces, which the supported materials never produce
+	int pm_caustics;          // unused (kept for layout); the caustic map is caus_map below
 	int pm_threads;           // threads_photons: the photon count is rounded to a multiple (:437)
 	// adaptive anti-aliasing (scene.cc:582-595, aa_noise_params.h:27-46; integrator_tiled.cc:172-231)
 	int aa_passes;
@@ -160,6 +161,13 @@ typedef struct {
 	float ao_dist;
 	float ao_col[3];
 	float aa_light_sample_multiplier_factor;
+	// caustic photon map (MonteCarloIntegrator::createCausticMap / causticWorker, integrator_montecarlo.cc
+	// :410-640): PhotonIntegrator "caustics" (cPhotons, causticRadius, caustic_mix, bounces),
+	// DirectLight "caustics" and PathIntegrator caustic_type photon|both (photons, caustic_radius,
+	// caustic_mix, caustic_depth)
+	int caus_map;
+	int caus_photons, caus_search, caus_depth;
+	float caus_radius;
 } yc_render;
 
 typedef struct {
@@ -194,6 +202,7 @@ int yc_render_image(const yc_scene *scene, int y0, int y1, float *rgba, float *w
 // split-position bits or photon index, flags).  Returns the photon count (n_paths in *n_paths),
 // or -1.  Pass NULL buffers to query the count.
 int yc_photon_map(const yc_scene *scene, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths);
+int yc_photon_map_ex(const yc_scene *scene, int which, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths);
 
 // Per-sample radiance for a list of (x, y, s) camera samples (RGBA per sample).
 int yc_render_samples(const yc_scene *scene, int n, const int *xys, float *rgba);

@@ -202,14 +202,12 @@ def test_refused_features_fail_loudly(product):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["bounces12", "caustic_photon", "dl_caustics"])
+@pytest.mark.parametrize("case", ["bounces12"])
 def test_refused_render_settings(product, case):
+    """(photon caustics — PT caustic_type photon | both, DirectLight caustics — are supported since
+    round 2: tests/test_caustics.py)"""
     s = scenes.cornell(16, 16, spp=1, bounces=4)
     if case == "bounces12":
         s = s.with_render(bounces=12)
-    elif case == "caustic_photon":
-        s = s.with_render(caustic_type="photon")
-    else:
-        s = s.with_render(integrator="directlighting", pm_caustics=True)
     with pytest.raises(RuntimeError):
         product.render_spec(s)
