@@ -169,6 +169,7 @@ struct DevScene
 	int n_nodes, n_tris, n_mats, n_lights;
 	int node_f4;                   // float4 per BVH node: 4 (BVH2) or 8 (BVH4)
 	int scene_in_lds;              // nodes+tris copied to LDS by each trace workgroup
+	int brute;                     // YAFARAY_AMD_TRACE=brute: k_trace_brute tests every triangle of a tiny scene
 	int lds_nodes, lds_tris;
 
 	DevCamera cam;

@@ -707,6 +707,119 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_trace_brute (opt-in, YAFARAY_AMD_TRACE=brute; measured slower than the BVH on C2, see
+// render.cc): the same queries for scenes of at most kBruteTris triangles by testing every triangle — the reference's own AcceleratorSimpleTest semantics
+// (accelerator_simple_test.cc:61-139; closest = the lowest (t, primitive) in [tmin, tmax), any =
+// a hit in [0, tmax)), which equal the BVH's by construction.  The triangle loop is wave-uniform:
+// the vertices come through scalar loads shared by the 64 lanes, every lane does the same
+// arithmetic (no divergence, no stack), and a shadow wave stops when all its lanes are occluded.
+// ---------------------------------------------------------------------------------------------
+constexpr int kBruteTris = 64;
+
+template<bool ANY>
+__device__ __forceinline__ bool bruteTrace(const float4 *__restrict__ tris, int n_tris, V3 o, V3 d, float tmin, float tmax, float &t_best,
+                                           int &prim_best, uint32_t &tests, bool active)
+{
+	t_best = tmax;
+	prim_best = -1;
+	bool hit = false;
+	for(int q = 0; q < n_tris; ++q)
+	{
+		// wave-uniform index through the constant address space -> scalar loads (the K$ holds the
+		// whole scene)
+#ifdef __HIP_DEVICE_COMPILE__
+		typedef const float4 __attribute__((address_space(4))) *ConstF4;
+		const ConstF4 ct = (ConstF4)tris;
+		const int qs = __builtin_amdgcn_readfirstlane(q);
+		const float4 ta = ct[3 * qs], tb = ct[3 * qs + 1], tc = ct[3 * qs + 2];
+#else   // (host pass of the single-source compile: never executed)
+		const float4 ta = tris[3 * q], tb = tris[3 * q + 1], tc = tris[3 * q + 2];
+#endif
+		const float t = triTest(ta, tb, tc, o, d, t_best);
+		const int prim = __float_as_int(tb.w);
+		if(ANY)
+		{
+			if(!hit && t != -1.f && t < tmax && t >= 0.f) { hit = true; t_best = t; prim_best = prim; }
+			if((q & 3) == 3 && __all(hit || !active)) break;
+		}
+		else if(t != -1.f && t >= tmin && (t < t_best || (t == t_best && prim_best >= 0 && prim < prim_best)))
+		{
+			t_best = t;
+			prim_best = prim;
+		}
+	}
+	if(active) tests += (uint32_t)n_tris;
+	return prim_best >= 0;
+}
+
+__global__ void __launch_bounds__(kTraceBlock) k_trace_brute(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P, DevStats *stats)
+{
+	const float4 *__restrict__ tris = S.tris;
+	const int n_tris = S.n_tris;
+	const SegLoop L = segLoop(S.n_seg);
+	const uint32_t n_a = cnt.n_active[L.s], n_s = cnt.n_shadow[L.s];
+	const uint32_t total = n_a + n_s;
+	const uint32_t a0 = L.s * S.cap_a, s0 = L.s * S.cap_s;
+	uint32_t tests = 0, n_closest = 0, n_shadow = 0;
+	const uint32_t stride = L.nb * blockDim.x;
+	// closest rays fill the first n_a positions, shadow rays the rest: a wave is (almost always)
+	// all closest or all shadow, and runs one of the two uniform loops
+	for(uint32_t base = L.r * blockDim.x; base < total; base += stride)
+	{
+		const uint32_t j = base + threadIdx.x;
+		const bool closest = j < n_a, shadow = !closest && j < total;
+		if(__any(closest))
+		{
+			float4 od = make_float4(0.f, 0.f, 0.f, 0.f), dd = make_float4(0.f, 0.f, 1.f, __builtin_nanf(""));
+			if(closest) { od = Q.ray_o[a0 + j]; dd = Q.ray_d[a0 + j]; }
+			const bool ray = closest && !(dd.w != dd.w);   // NaN marks "no ray this iteration"
+			float t;
+			int prim;
+			const float tmax = (dd.w >= 0.f) ? dd.w : __builtin_huge_valf();
+			bruteTrace<false>(tris, n_tris, xyz(od), xyz(dd), od.w, tmax, t, prim, tests, ray);
+			if(ray)
+			{
+				Q.hit_t[a0 + j] = t;
+				Q.hit_prim[a0 + j] = prim;
+				++n_closest;
+			}
+		}
+		if(__any(shadow))
+		{
+			float4 od = make_float4(0.f, 0.f, 0.f, 0.f), dd = make_float4(0.f, 0.f, 1.f, 0.f);
+			const uint32_t k = s0 + (j - n_a);
+			if(shadow) { od = Q.sh_o[k]; dd = Q.sh_d[k]; }
+			float t;
+			int prim;
+			const bool occ = bruteTrace<true>(tris, n_tris, xyz(od), xyz(dd), 0.f, dd.w, t, prim, tests, shadow);
+			if(shadow)
+			{
+				P.occ[Q.sh_idx[k]] = occ ? 1 : 0;   // P = state set of the consumer shade
+				++n_shadow;
+			}
+		}
+	}
+	for(int off = 32; off > 0; off >>= 1)
+	{
+		tests += __shfl_down(tests, off);
+		n_closest += __shfl_down(n_closest, off);
+		n_shadow += __shfl_down(n_shadow, off);
+	}
+	__shared__ uint32_t red[kTraceBlock / 64][3];
+	const int wid = threadIdx.x >> 6;
+	if(laneId() == 0) { red[wid][0] = tests; red[wid][1] = n_closest; red[wid][2] = n_shadow; }
+	__syncthreads();
+	if(threadIdx.x < 3)
+	{
+		unsigned long long v = 0;
+		for(int w = 0; w < kTraceBlock / 64; ++w) v += red[w][threadIdx.x];
+		unsigned long long *rec = &stats[blockIdx.x].closest_rays;
+		const int slot = (threadIdx.x == 0) ? 3 : (threadIdx.x == 1) ? 0 : 1;   // tri_tests, closest, shadow
+		if(v) rec[slot] += v;
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_shade
 // ---------------------------------------------------------------------------------------------
 struct Surf
@@ -2996,6 +3109,11 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 	const bool wide = S->node_f4 == 8;
 	const size_t lds_scene = S->scene_in_lds ? (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) : 0;
 	const size_t bytes = stack_bytes + lds_scene;
+	if(S->brute && !S->tr_shad && S->n_tris <= kBruteTris)
+	{
+		hipLaunchKernelGGL(k_trace_brute, dim3(grid), dim3(kTraceBlock), 0, st, *S, *Q, *cnt, *P, stats);
+		return hipGetLastError();
+	}
 #define YAF_TRACE_LAUNCH(L, W, T) hipLaunchKernelGGL((k_trace<L, W, T>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill)
 	if(S->tr_shad)
 	{

@@ -451,6 +451,14 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.n_mats = d.n_mats;
 	S.n_lights = d.n_lights;
 	S.scene_in_lds = d.scene_in_lds ? 1 : 0;
+	// YAFARAY_AMD_TRACE=brute: scenes of at most 64 triangles test every triangle (k_trace_brute).
+	// Measured slower than the BVH on C2 (k_trace 39.0 vs 34.7 ms per frame: 34 exact triangle
+	// tests per ray at full lane occupancy cost more than ~3.4 node + 3.3 triangle visits at 0.35),
+	// so the BVH stays the default
+	{
+		const char *e = getenv("YAFARAY_AMD_TRACE");
+		S.brute = (e && std::string(e) == "brute") ? 1 : 0;
+	}
 	S.ph_lights = (const int *)d.ph_lights.p;
 	S.light_cdf = (const float *)d.light_cdf.p;
 	S.light_func = (const float *)d.light_func.p;

@@ -48,8 +48,13 @@ def product_scene(product, spec):
 # BVH layouts under test: BVH4 (default), BVH4 with a 4-level LDS stack (exercises the HBM spill
 # levels of k_trace / k_photon_bounce), and the binary BVH2
 # and the device-built BVH4 (bvhgpu.hip: PLOC + collapse; the default for >= 64 K triangles)
-BVH_VARIANTS = {"bvh4": {"YAFARAY_AMD_BVH_BUILD": "host"}, "bvh4-spill": {"YAFARAY_AMD_LDS_STACK": "4"},
-                "bvh2": {"YAFARAY_AMD_BVH_WIDTH": "2"}, "gpu-build": {"YAFARAY_AMD_BVH_BUILD": "gpu"}}
+# "brute": scenes of <= 64 triangles (the Cornell box) through k_trace_brute (opt-in; the other
+# variants pin the BVH traversal explicitly)
+BVH_VARIANTS = {"bvh4": {"YAFARAY_AMD_BVH_BUILD": "host", "YAFARAY_AMD_TRACE": "bvh"},
+                "bvh4-spill": {"YAFARAY_AMD_LDS_STACK": "4", "YAFARAY_AMD_TRACE": "bvh"},
+                "bvh2": {"YAFARAY_AMD_BVH_WIDTH": "2", "YAFARAY_AMD_TRACE": "bvh"},
+                "gpu-build": {"YAFARAY_AMD_BVH_BUILD": "gpu", "YAFARAY_AMD_TRACE": "bvh"},
+                "brute": {"YAFARAY_AMD_TRACE": "brute"}}
 
 
 def use_bvh(monkeypatch, variant):
