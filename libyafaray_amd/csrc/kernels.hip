@@ -390,6 +390,13 @@ __device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const
 	return miss ? -1.f : t;
 }
 
+// per-visit statistics of the traversal (node visits, triangle tests); -DYAF_TRACE_NOSTATS drops them
+#ifdef YAF_TRACE_NOSTATS
+#define TRACE_STAT(x) do {} while(0)
+#else
+#define TRACE_STAT(x) x
+#endif
+
 // Closest hit with t in [tmin, tmax) (ties -> lower primitive index), or any hit with t in
 // [0, tmax).  Box tests are conservative (boxes padded at build time + a relative slack), so
 // culling never drops a hit the exhaustive reference semantics would return.
@@ -410,7 +417,7 @@ __device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	int node = 0;
 	for(;;)
 	{
-		++visits;
+		TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 4 * node;
 		const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
@@ -431,7 +438,7 @@ __device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 			const int start = ~c;
 			for(int q = start; q < start + k; ++q)
 			{
-				++tests;
+				TRACE_STAT(++tests);
 				const float4 *tp = C.tris + 3 * q;
 				const float4 ta = tp[0], tb = tp[1], tc = tp[2];
 				const float t = triTest(ta, tb, tc, o, d, ANY ? tmax : t_best);
@@ -517,7 +524,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	};
 	for(;;)
 	{
-		++visits;
+		TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 8 * node;
 		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
@@ -546,7 +553,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 			const int start = ~child[k];
 			for(int q = start; q < start + count[k]; ++q)
 			{
-				++tests;
+				TRACE_STAT(++tests);
 				const float4 *tp = C.tris + 3 * q;
 				const float4 ta = tp[0], tb = tp[1], tc = tp[2];
 				const float t = triTest(ta, tb, tc, o, d, ANY ? tmax : t_best);
