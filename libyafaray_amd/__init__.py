@@ -108,6 +108,7 @@ def lib():
             "yafaray_createOutput": (b, [vp, cp]),
             "yafaray_setRenderPutPixelCallback": (None, [vp, PutPixelCb, vp]),
             "yafaray_setRenderFlushAreaCallback": (None, [vp, FlushAreaCb, vp]),
+            "yafaray_setRenderHighlightAreaCallback": (None, [vp, FlushAreaCb, vp]),
             "yafaray_setRenderFlushCallback": (None, [vp, FlushCb, vp]),
             "yafaray_setRenderNotifyViewCallback": (None, [vp, NotifyViewCb, vp]),
             "yafaray_setRenderNotifyLayerCallback": (None, [vp, NotifyLayerCb, vp]),
@@ -216,8 +217,12 @@ class Interface:
         return e.decode() if e else ""
 
     # --- render ---
-    def render(self, progress=None, put_pixel=None, flush_area=None, flush=None):
+    def render(self, progress=None, put_pixel=None, flush_area=None, flush=None, highlight_area=None):
         cbs = []
+        if highlight_area is not None:
+            cb = FlushAreaCb(lambda v, aid, x0, y0, x1, y1, d: highlight_area(aid, x0, y0, x1, y1))
+            self.L.yafaray_setRenderHighlightAreaCallback(self.h, cb, None)
+            cbs.append(cb)
         if put_pixel is not None:
             cb = PutPixelCb(lambda v, l, x, y, r, g, b, a, d: put_pixel(x, y, r, g, b, a))
             self.L.yafaray_setRenderPutPixelCallback(self.h, cb, None)

@@ -266,6 +266,13 @@ struct DevFilm
 	int width, height, spp, tile;
 	int multipass;                 // AA_passes > 1: riVdC / riS sub-pixel positions
 	uint32_t sample_offset;        // base sampling offset + this pass's offset
+	// tile order of the splats (ImageSplitter, imagesplitter.cc:30-107): rank of tile ty * ntx + tx
+	// in the one-thread render order; null = linear (rank = tile id)
+	const uint32_t *tile_rank;
+	int ntx;
+	// partial film: each pixel as ImageFilm::finishArea shows it when its tile finishes in a one-thread
+	// render (imagefilm.cc:489-520): only sources of tiles ranked <= its own; accum / weights untouched
+	int partial;
 };
 
 // Per-chunk wavefront state (structure of arrays, capacity = chunk slots).

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
+#include <random>
 #include <sstream>
 
 namespace yafamd
@@ -892,6 +893,31 @@ bool Scene::buildAccelerator()
 }
 
 // scene.cc:203-263 Scene::render + integrator_tiled.cc:97-233 (single AA pass)
+// ImageSplitter (imagesplitter.cc:30-107) for one render thread (no subdivision of the last tiles):
+// the tile ids ty * ntx + tx in render order.  "linear": row-major; "random": a fixed-seed shuffle
+// (the reference seeds from std::random_device); anything else, the reference's default "centre":
+// by squared distance of the tile corner to the image centre (ImageSpliterCentreSorter,
+// imagesplitter.h:97-109, integer arithmetic), ties in linear order (the reference breaks them by
+// a random shuffle before its unstable sort).
+static std::vector<int> tileOrder(int W, int H, int ts, const std::string &order)
+{
+	const int ntx = (W + ts - 1) / ts, nty = (H + ts - 1) / ts;
+	std::vector<int> ids((size_t)ntx * nty);
+	for(size_t i = 0; i < ids.size(); ++i) ids[i] = (int)i;
+	if(order == "linear") return ids;
+	if(order == "random")
+	{
+		std::shuffle(ids.begin(), ids.end(), std::mt19937(0x59414641u));
+		return ids;
+	}
+	auto key = [&](int id) {
+		const int x = (id % ntx) * ts, y = (id / ntx) * ts;
+		return (x - W / 2) * (x - W / 2) + (y - H / 2) * (y - H / 2);
+	};
+	std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) { return key(a) < key(b); });
+	return ids;
+}
+
 bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, void *progress_data, bool quiet)
 {
 	if(!setup.valid) { log.error("Scene: No ImageFilm present, bailing out..."); return false; }
@@ -1246,7 +1272,41 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 					autosave_last = now;
 				}
 			};
-		if(progress && !quiet)
+		// tile order of the film splats and of the per-tile callbacks
+		const std::vector<int> order = tileOrder(s.width, s.height, s.tile_size, s.tiles_order);
+		rp.tile_rank.assign(order.size(), 0u);
+		for(size_t k = 0; k < order.size(); ++k) rp.tile_rank[(size_t)order[k]] = (uint32_t)k;
+		const bool tile_cbs = !quiet && (cb.put_pixel || cb.flush_area || cb.highlight_area);
+		if(tile_cbs)
+		{
+			// ImageFilm::nextArea / finishArea per tile in render order (imagefilm.cc:447-568):
+			// highlightArea, putPixel over the tile (rows, then columns) with the values the one-thread
+			// render shows when the tile finishes, flushArea, progress by the tile's area
+			const int ntx = (s.width + s.tile_size - 1) / s.tile_size;
+			const std::string vname = view.first;
+			rp.on_tiles = [&, ntx, vname, order](int pass, const std::vector<float> &part) {
+				(void)pass;
+				const int n_pix = s.width * s.height;
+				int done_px = 0;
+				for(size_t k = 0; k < order.size(); ++k)
+				{
+					const int tx = (order[k] % ntx) * s.tile_size, ty = (order[k] / ntx) * s.tile_size;
+					const int x1 = std::min(s.width, tx + s.tile_size), y1 = std::min(s.height, ty + s.tile_size);
+					if(cb.highlight_area) cb.highlight_area(vname.c_str(), (int)k, tx, ty, x1, y1, cb.highlight_area_data);
+					if(cb.put_pixel)
+						for(int y = ty; y < y1; ++y)
+							for(int x = tx; x < x1; ++x)
+							{
+								const float *px = &part[4 * ((size_t)y * s.width + x)];
+								cb.put_pixel(vname.c_str(), "combined", x, y, px[0], px[1], px[2], px[3], cb.put_pixel_data);
+							}
+					if(cb.flush_area) cb.flush_area(vname.c_str(), (int)k, tx, ty, x1, y1, cb.flush_area_data);
+					done_px += (x1 - tx) * (y1 - ty);
+					if(progress) progress(n_pix, done_px, "Rendering...", progress_data);
+				}
+			};
+		}
+		else if(progress && !quiet)
 		{
 			const int n_pix = s.width * s.height;
 			rp.on_chunk = [&, n_pix](uint64_t done, uint64_t total) {
@@ -1273,36 +1333,13 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			   << " shadow rays in " << stats.render_seconds << " s";
 			log.info(os.str());
 		}
-		// imagefilm.cc:489-568 finishArea per tile (linear order) then :570-670 flush
+		// imagefilm.cc:570-670 flush: every owned pixel, then the flush callback (the per-tile
+		// finishArea callbacks ran inside the render, rp.on_tiles)
 		const auto owned = gpu()->ownedRows();
 		auto ownedRow = [&](int y) {
 			for(const auto &r : owned) if(y >= r.first && y < r.second) return true;
 			return false;
 		};
-		if(cb.put_pixel || cb.flush_area)
-		{
-			int area_id = 0;
-			const int ts = s.tile_size;
-			for(int ty = 0; ty < s.height; ty += ts)
-			{
-				for(int tx = 0; tx < s.width; tx += ts, ++area_id)
-				{
-					const int x1 = std::min(s.width, tx + ts), y1 = std::min(s.height, ty + ts);
-					bool any = false;
-					for(int y = ty; y < y1 && !any; ++y) any = ownedRow(y);
-					if(!any) continue;
-					if(cb.put_pixel)
-						for(int y = ty; y < y1; ++y)
-							if(ownedRow(y))
-							for(int x = tx; x < x1; ++x)
-							{
-								const float *px = &film_rgba[4 * ((size_t)y * s.width + x)];
-								cb.put_pixel(view.first.c_str(), "combined", x, y, px[0], px[1], px[2], px[3], cb.put_pixel_data);
-							}
-					if(cb.flush_area) cb.flush_area(view.first.c_str(), area_id, tx, ty, x1, y1, cb.flush_area_data);
-				}
-			}
-		}
 		if(cb.put_pixel)
 			for(int y = 0; y < s.height; ++y)
 			{

@@ -2334,12 +2334,18 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 __device__ __forceinline__ int roundToInt(double v) { return (int)(v + (.5 - 1.4e-11)); }
 __device__ __forceinline__ int floorToInt(double v) { return (int)floor(v); }
 
-// rank of a pixel in the single-thread linear tile order (imagesplitter.cc:30-49)
-__device__ __forceinline__ uint64_t pixelRank(int x, int y, int W, int H, int ts)
+// rank of a pixel in the single-thread tile order (imagesplitter.cc:30-107): tiles by their rank
+// (linear when F.tile_rank is null), pixels row-major inside a tile (integrator_tiled.cc:288-290)
+__device__ __forceinline__ uint32_t tileRankOf(const DevFilm &F, int x, int y)
+{
+	const int ty = y / F.tile, tx = x / F.tile;
+	return F.tile_rank ? F.tile_rank[ty * F.ntx + tx] : (uint32_t)(ty * F.ntx + tx);
+}
+__device__ __forceinline__ uint64_t pixelRank(const DevFilm &F, int x, int y, int W, int H, int ts)
 {
 	const int ty = y / ts, tx = x / ts;
-	const int th = min(ts, H - ty * ts), tw = min(ts, W - tx * ts);
-	return (uint64_t)ty * ts * W + (uint64_t)tx * ts * th + (uint64_t)(y - ty * ts) * tw + (x - tx * ts);
+	const int tw = min(ts, W - tx * ts);
+	return (uint64_t)tileRankOf(F, x, y) * (uint64_t)ts * ts + (uint64_t)(y - ty * ts) * tw + (x - tx * ts);
 }
 
 // RF / RB: compile-time footprint reach (box and gauss filters: RF = 1, RB = 0 -> a 2x2 window
@@ -2359,6 +2365,7 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 	int sx[kWin], sy[kWin];
 	uint64_t rk[kWin];
 	int n = 0;
+	const uint32_t own_tile = F.partial ? tileRankOf(F, x, y) : 0u;
 #pragma unroll
 	for(int dyy = 0; dyy < (kStatic ? RF + RB + 1 : 9); ++dyy)
 	{
@@ -2368,7 +2375,8 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 			if(!kStatic && (dyy > rf + rb || dxx > rf + rb)) continue;
 			const int yy = y - rf + dyy, xx = x - rf + dxx;
 			if(yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
-			const uint64_t r = pixelRank(xx, yy, W, H, F.tile);
+			if(F.partial && tileRankOf(F, xx, yy) > own_tile) continue;   // tile not finished yet
+			const uint64_t r = pixelRank(F, xx, yy, W, H, F.tile);
 			int p = n++;
 			while(p > 0 && rk[p - 1] > r) { rk[p] = rk[p - 1]; sx[p] = sx[p - 1]; sy[p] = sy[p - 1]; --p; }
 			rk[p] = r; sx[p] = xx; sy[p] = yy;
@@ -2430,8 +2438,11 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 			acc.w = acc.w + col.w * wt;
 		}
 	}
-	weights[p] = wsum;
-	accum[p] = acc;
+	if(!F.partial)
+	{
+		weights[p] = wsum;
+		accum[p] = acc;
+	}
 	// Rgba::normalized (color.h:554-558): colour * (1 / weight) — operator/ takes the reciprocal first
 	if(wsum != 0.f)
 	{

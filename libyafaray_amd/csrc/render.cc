@@ -122,6 +122,7 @@ struct GpuRenderer::Impl
 	float clight_inv_integral = 0.f;
 	int n_cph_lights = 0;
 	Buf cph_pos, cph_dir, cph_colb, cpk_nodes;   // caustic photon map + kd-tree
+	Buf tile_rank, pfilm;                        // tile order ranks; partial film of the per-tile callbacks
 	int c_photons = 0, c_paths = 0, c_depth = 0;
 	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
 	Buf ph_pos, ph_dir, ph_colb, pk_nodes, pk_stack;
@@ -188,7 +189,7 @@ struct GpuRenderer::Impl
 	{
 		for(Buf *b : {&ph_lights, &light_cdf, &light_func, &ph_ray_o, &ph_ray_d, &ph_pcol, &ph_alive0, &ph_alive1, &ph_n_alive,
 		              &dep_a, &dep_b, &dep_c, &dep_flag, &ph_scan, &ph_total, &ph_pos, &ph_dir, &ph_colb, &pk_nodes, &pk_stack, &cph_lights,
-		              &clight_cdf, &clight_func, &cph_pos, &cph_dir, &cph_colb, &cpk_nodes})
+		              &clight_cdf, &clight_func, &cph_pos, &cph_dir, &cph_colb, &cpk_nodes, &tile_rank, &pfilm})
 			b->release();
 		for(Buf *b : {&prim_attr, &shader_nodes, &textures, &texels, &spawn_o, &spawn_d, &spawn_pr, &node_own, &node_child, &node_w,
 		              &spawn_count})
@@ -994,6 +995,29 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	S.plist = nullptr;
 	rp.film.multipass = S.aa_multipass;
 	rp.film.sample_offset = S.base_offset;
+	rp.film.ntx = (W + ts - 1) / ts;
+	rp.film.tile_rank = nullptr;
+	rp.film.partial = 0;
+	if(!rp.tile_rank.empty())
+	{
+		if(!allocCopy(log_, d.tile_rank, rp.tile_rank.data(), rp.tile_rank.size())) return false;
+		rp.film.tile_rank = (const uint32_t *)d.tile_rank.p;
+	}
+	// per-tile callbacks: the partial film of a pass (before its film launch adds to the accumulators)
+	const bool tiles_cb = (bool)rp.on_tiles && rp.shard_world == 1 && groupWorld() <= 1;
+	auto emitTiles = [&](int pass, const uint8_t *flags, int accumulate) -> bool {
+		if(!tiles_cb) return true;
+		if(!ensure(log_, d.pfilm, (size_t)W * H * sizeof(float4))) return false;
+		DevFilm Fp = rp.film;
+		Fp.partial = 1;
+		PROF(KK_FILM, yafamd_launch_film(&Fp, (const float4 *)d.samples.p, flags, (float4 *)d.accum.p, (float4 *)d.pfilm.p, (float *)d.weights.p, 0, H,
+		                            S.clamp_samples, accumulate, d.stream));
+		std::vector<float> host((size_t)W * H * 4);
+		HIPCHECK(hipMemcpyAsync(host.data(), d.pfilm.p, host.size() * sizeof(float), hipMemcpyDeviceToHost, d.stream));
+		HIPCHECK(hipStreamSynchronize(d.stream));
+		rp.on_tiles(pass, host);
+		return true;
+	};
 	uint64_t samples_total = total;
 	if(rp.resumed)
 	{
@@ -1020,6 +1044,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			done_flags = (const uint8_t *)d.aa_flags.p;
 			samples_total = done / (uint64_t)spp * (uint64_t)spp;
 		}
+		if(done == total && !emitTiles(0, nullptr, 0)) return false;
 		for(const auto &r : owned_rows_)
 			PROF(KK_FILM, yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, done_flags, (float4 *)d.accum.p, (float4 *)d.film.p,
 			                            (float *)d.weights.p, r.first, r.second, S.clamp_samples, 0, d.stream));
@@ -1092,6 +1117,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				if(done < n_total)
 					HIPCHECK(yafamd_launch_done_flags(&S, (const DevJob *)d.jobs.p, n_jobs, (uint32_t)resampled, (uint32_t)(done / (uint64_t)n_pass),
 					                                  (uint8_t *)d.aa_flags.p, d.stream));
+				if(done == n_total && !emitTiles(passes_done_, (const uint8_t *)d.aa_flags.p, 1)) return false;
 				PROF(KK_FILM, yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (const uint8_t *)d.aa_flags.p, (float4 *)d.accum.p,
 				                            (float4 *)d.film.p, (float *)d.weights.p, 0, H, S.clamp_samples, 1, d.stream));
 				samples_total += done / (uint64_t)n_pass * (uint64_t)n_pass;

@@ -109,6 +109,12 @@ struct RenderParams
 	// progress hook after every completed chunk (the reference's per-tile progress updates,
 	// integrator_tiled.cc:258-262): samples done / samples of the pass.  Set -> one stream sync per chunk.
 	std::function<void(uint64_t done, uint64_t total)> on_chunk;
+	// tile order (ImageSplitter): rank of every tile id ty * ntx + tx; empty = linear
+	std::vector<uint32_t> tile_rank;
+	// per-pass hook for the per-tile callbacks (ImageFilm::finishArea, imagefilm.cc:489-568): the
+	// pass's partial film (RGBA, W x H) — each pixel as the one-thread render shows it when its tile
+	// finishes.  Single GPU, uncanceled passes.
+	std::function<void(int pass, const std::vector<float> &partial)> on_tiles;
 };
 
 class GpuRenderer

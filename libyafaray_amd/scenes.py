@@ -122,6 +122,7 @@ class Render:
     filter_type: str = "box"
     aa_pixelwidth: float = 1.0
     tile_size: int = 32
+    tiles_order: str = "linear"             # linear | centre (the reference default) | random
     bounces: int = 8
     path_samples: int = 1
     rr_min_bounces: int = 0
@@ -644,7 +645,7 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetFloat("AA_pixelwidth", r.aa_pixelwidth)
     api.paramsSetFloat("AA_clamp_samples", r.clamp_samples)
     api.paramsSetInt("tile_size", r.tile_size)
-    api.paramsSetString("tiles_order", "linear")
+    api.paramsSetString("tiles_order", r.tiles_order)
     api.paramsSetBool("adv_auto_shadow_bias_enabled", r.shadow_bias_auto)
     api.paramsSetFloat("adv_shadow_bias_value", r.shadow_bias)
     api.paramsSetBool("adv_auto_min_raydist_enabled", r.ray_min_dist_auto)

@@ -90,7 +90,7 @@ class yc_render(C.Structure):
                 ("transp_shad", C.c_int), ("shadow_depth", C.c_int), ("do_ao", C.c_int), ("ao_samples", C.c_int),
                 ("ao_dist", C.c_float), ("ao_col", C.c_float * 3), ("aa_light_sample_multiplier_factor", C.c_float),
                 ("caus_map", C.c_int), ("caus_photons", C.c_int), ("caus_search", C.c_int), ("caus_depth", C.c_int),
-                ("caus_radius", C.c_float)]
+                ("caus_radius", C.c_float), ("tiles_order", C.c_int)]
 
 
 class yc_scene(C.Structure):
@@ -563,6 +563,7 @@ class OracleScene:
         cm = caustic_params(r)
         rp.caus_map, rp.caus_photons, rp.caus_search = int(cm.enabled), cm.photons, cm.search
         rp.caus_depth, rp.caus_radius = cm.depth, cm.radius
+        rp.tiles_order = {"linear": 0, "random": 2}.get(getattr(r, "tiles_order", "linear"), 1)
         rp.aa_passes = max(1, r.aa_passes)
         rp.aa_inc_samples = r.aa_inc_samples if r.aa_inc_samples > 0 else r.aa_samples
         rp.aa_threshold, rp.aa_resampled_floor = r.aa_threshold, r.aa_resampled_floor

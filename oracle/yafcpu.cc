@@ -7,6 +7,7 @@
 #include "yafcpu.h"
 
 #include <algorithm>
+#include <random>
 #include <array>
 #include <cstdlib>
 #include <sstream>
@@ -2791,6 +2792,15 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 	const int passes = std::max(1, rp.aa_passes);
 	if(passes > 1 && (y0 != 0 || y1 != H)) return -2;   // adaptive passes need the whole film
 	std::vector<Tile> all = tilesLinear(W, H, rp.tile_size);
+	// imagesplitter.cc:30-107 tile order for one render thread: random (the reference seeds from
+	// std::random_device; a fixed seed here and in the GPU host), centre (ImageSpliterCentreSorter,
+	// imagesplitter.h:97-109: squared distance of the tile corner to the image centre; ties in
+	// linear order, the reference breaks them randomly)
+	if(rp.tiles_order == 2) std::shuffle(all.begin(), all.end(), std::mt19937(0x59414641u));
+	else if(rp.tiles_order == 1)
+		std::stable_sort(all.begin(), all.end(), [W, H](const Tile &a, const Tile &b) {
+			return (a.x - W / 2) * (a.x - W / 2) + (a.y - H / 2) * (a.y - H / 2) < (b.x - W / 2) * (b.x - W / 2) + (b.y - H / 2) * (b.y - H / 2);
+		});
 	std::vector<Tile> tiles;
 	for(const Tile &t : all)
 	{

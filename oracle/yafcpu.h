@@ -168,6 +168,7 @@ typedef struct {
 	int caus_map;
 	int caus_photons, caus_search, caus_depth;
 	float caus_radius;
+	int tiles_order;          // 0 linear, 1 centre (the reference default), 2 random (fixed seed)
 } yc_render;
 
 typedef struct {
