@@ -224,6 +224,36 @@ class Prims:
         return out
 
 
+def _shirley(self, r12):
+    r12 = np.ascontiguousarray(r12, np.float32).reshape(-1)
+    out = np.empty_like(r12)
+    self.f("shirley_disk")(_p(r12, C.c_float), _p(out, C.c_float), C.c_int(len(r12) // 2))
+    return out.reshape(-1, 2)
+
+
+def _rgbe(self, b):
+    b = np.ascontiguousarray(b, np.uint8).reshape(-1)
+    out = np.empty(3 * (len(b) // 4), np.float32)
+    self.f("rgbe_decode")(_p(b, C.c_uint8), _p(out, C.c_float), C.c_int(len(b) // 4))
+    return out.reshape(-1, 3)
+
+
+def _tiles(self, w, h, bs, order, nthreads=1):
+    """order: "linear" | "centre" | "random"; (x, y, w, h) per region in render order."""
+    cap = ((w + bs - 1) // bs) * ((h + bs - 1) // bs) * 16 + 16
+    out = np.empty(4 * cap, np.int32)
+    if self.px == "ref_":
+        code = {"linear": 0, "random": 1, "centre": 2}[order]
+        n = self.f("tiles")(C.c_int(w), C.c_int(h), C.c_int(bs), C.c_int(code), C.c_int(nthreads), _p(out, C.c_int), C.c_int(cap))
+    else:
+        code = {"linear": 0, "centre": 1, "random": 2}[order]
+        n = self.f("tiles")(C.c_int(w), C.c_int(h), C.c_int(bs), C.c_int(code), _p(out, C.c_int), C.c_int(cap))
+    return out[:4 * n].reshape(-1, 4)
+
+
+Prims.shirley, Prims.rgbe, Prims.tiles = _shirley, _rgbe, _tiles
+
+
 def oracle_prims() -> Prims:
     return Prims(oracle_lib(), "yc_")
 

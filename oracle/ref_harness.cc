@@ -17,8 +17,11 @@
 //   include/color/color.h          Rgb::clampProportionalRgb, colour-space conversions, HSV
 //   include/image/image_buffers.h  the image buffer pixel types (texture storage quantisation)
 //   include/math/interpolation.h   cubicInterpolate (bicubic texture lookups)
+//   src/geometry/vector.cc         Vec3::shirleyDisk (depth-of-field lens samples)
+//   src/render/imagesplitter.cc    ImageSplitter tile lists (linear / centre / random orders)
+//   src/color/color.cc             Rgbe (the HDR texture pixels; decoding is inline in color.h)
 //
-// oracle/Makefile compiles this file together with the two .cc files above, straight from
+// oracle/Makefile compiles this file together with the .cc files above, straight from
 // /root/reference, with the reference's Release flags (-O3 -DNDEBUG -DFAST_MATH -DFAST_TRIG,
 // C++11), into oracle/_ref/libyafref_prims.so.  tests/golden/make_golden_prims.py then records
 // input/output vectors from it, and the CPU oracle (oracle/yafcpu.cc) is pinned against them.
@@ -34,6 +37,8 @@
 #include "color/color.h"
 #include "image/image_buffers.h"
 #include "math/interpolation.h"
+#include "render/imagesplitter.h"
+#include "render/render_data.h"
 
 #include <cstdint>
 
@@ -255,6 +260,50 @@ void ref_cubic(const float *in, float *out, int n)
 void ref_pow(const float *ab, float *out, int n)
 {
 	for(int i = 0; i < n; ++i) out[i] = math::pow(ab[2 * i], ab[2 * i + 1]);
+}
+
+}
+
+extern "C" {
+
+// Vec3::shirleyDisk (vector.cc:127-160): (r1, r2) -> (u, v)
+void ref_shirley_disk(const float *r12, float *uv, int n)
+{
+	for(int i = 0; i < n; ++i) Vec3::shirleyDisk(r12[2 * i], r12[2 * i + 1], uv[2 * i], uv[2 * i + 1]);
+}
+
+// Rgbe -> Rgb (color.h:204-213): RGBE bytes -> linear RGB
+void ref_rgbe_decode(const uint8_t *rgbe, float *rgb, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		Rgbe p;
+		for(int k = 0; k < 4; ++k) p.rgbe_[k] = rgbe[4 * i + k];
+		const Rgb c = static_cast<Rgb>(p);
+		rgb[3 * i] = c.r_;
+		rgb[3 * i + 1] = c.g_;
+		rgb[3 * i + 2] = c.b_;
+	}
+}
+
+// ImageSplitter (imagesplitter.cc:30-107): the region list of an image, order 0 linear, 1 random,
+// 2 centre (TilesOrderType), for `nthreads` render threads; out = (x, y, w, h) per region, returns
+// the region count (<= cap)
+int ref_tiles(int w, int h, int bs, int order, int nthreads, int *out, int cap)
+{
+	const ImageSplitter::TilesOrderType t = order == 0 ? ImageSplitter::Linear : order == 1 ? ImageSplitter::Random : ImageSplitter::CentreRandom;
+	ImageSplitter sp(w, h, 0, 0, bs, t, nthreads);
+	int n = 0;
+	RenderArea a;
+	while(n < cap && sp.getArea(n, a))
+	{
+		out[4 * n] = a.x_;
+		out[4 * n + 1] = a.y_;
+		out[4 * n + 2] = a.w_;
+		out[4 * n + 3] = a.h_;
+		++n;
+	}
+	return n;
 }
 
 }

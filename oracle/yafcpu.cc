@@ -3094,6 +3094,32 @@ void yc_film_table(int filter, float filter_size, float *table, float *filterw, 
 }
 
 
+// pinned against oracle/_ref ref_shirley_disk (vector.cc:127-160)
+void yc_shirley_disk(const float *r12, float *uv, int n)
+{
+	for(int i = 0; i < n; ++i) shirleyDisk(r12[2 * i], r12[2 * i + 1], uv[2 * i], uv[2 * i + 1]);
+}
+
+// tile lists of renderImage (one render thread): order 0 linear, 1 centre, 2 random (fixed seed);
+// out = (x, y, w, h) per tile, pinned against ref_tiles (imagesplitter.cc:30-107)
+int yc_tiles(int w, int h, int bs, int order, int *out, int cap)
+{
+	std::vector<Tile> all = tilesLinear(w, h, bs);
+	if(order == 2) std::shuffle(all.begin(), all.end(), std::mt19937(0x59414641u));
+	else if(order == 1)
+		std::stable_sort(all.begin(), all.end(), [w, h](const Tile &a, const Tile &b) {
+			return (a.x - w / 2) * (a.x - w / 2) + (a.y - h / 2) * (a.y - h / 2) < (b.x - w / 2) * (b.x - w / 2) + (b.y - h / 2) * (b.y - h / 2);
+		});
+	int n = 0;
+	for(const Tile &t : all)
+	{
+		if(n >= cap) break;
+		out[4 * n] = t.x; out[4 * n + 1] = t.y; out[4 * n + 2] = t.w; out[4 * n + 3] = t.h;
+		++n;
+	}
+	return n;
+}
+
 // which: 0 the diffuse map (PhotonIntegrator), 1 the caustic map
 int yc_photon_map_ex(const yc_scene *s, int which, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths)
 {
@@ -3121,6 +3147,18 @@ int yc_photon_map(const yc_scene *s, float *pos, float *dir, float *col, uint32_
 }
 
 // ---- texturing building blocks (yaftex.h), pinned against oracle/_ref ref_tex_* ----
+// HDR pixels (format_hdr.cc via color.h:204-213), pinned against ref_rgbe_decode
+void yc_rgbe_decode(const uint8_t *rgbe, float *rgb, int n)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		const yc::Rgba c = yc::rgbeToRgba(rgbe + 4 * i);
+		rgb[3 * i] = c.r;
+		rgb[3 * i + 1] = c.g;
+		rgb[3 * i + 2] = c.b;
+	}
+}
+
 void yc_tex_quantize(int kind, const float *in, float *out, int n)
 {
 	for(int i = 0; i < n; ++i)

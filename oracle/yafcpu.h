@@ -203,6 +203,9 @@ int yc_render_image(const yc_scene *scene, int y0, int y1, float *rgba, float *w
 // split-position bits or photon index, flags).  Returns the photon count (n_paths in *n_paths),
 // or -1.  Pass NULL buffers to query the count.
 int yc_photon_map(const yc_scene *scene, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths);
+void yc_shirley_disk(const float *r12, float *uv, int n);
+int yc_tiles(int w, int h, int bs, int order, int *out, int cap);
+void yc_rgbe_decode(const uint8_t *rgbe, float *rgb, int n);
 int yc_photon_map_ex(const yc_scene *scene, int which, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths);
 
 // Per-sample radiance for a list of (x, y, s) camera samples (RGBA per sample).

@@ -87,6 +87,24 @@ def main():
     g["clamp_in"], g["clamp_1_5"], g["clamp_0"] = c, r.clamp_proportional(c, 1.5), r.clamp_proportional(c, 0.0)
     np.savez_compressed(OUT, **g)
     print("wrote", OUT, os.path.getsize(OUT), "bytes,", len(g), "arrays")
+    # round 2: src/geometry/vector.cc, src/color/color.cc, src/render/imagesplitter.cc
+    g2 = {}
+    r12 = rng.random((n, 2)).astype(np.float32)
+    r12[:9] = [[0.5, 0.5], [0, 0], [1, 1], [0, 1], [1, 0], [0.5, 0], [0, 0.5], [0.25, 0.75], [0.75, 0.25]]
+    g2["shirley_in"], g2["shirley"] = r12, r.shirley(r12)
+    rgbe = rng.integers(0, 256, (n, 4), dtype=np.uint8)
+    rgbe[:16, 3] = 0
+    rgbe[16:32, 3] = [1, 2, 100, 127, 128, 129, 130, 135, 136, 137, 150, 200, 250, 254, 255, 255]
+    g2["rgbe_in"], g2["rgbe"] = rgbe, r.rgbe(rgbe)
+    sizes = [(1920, 1080, 32), (64, 48, 16), (50, 38, 8), (33, 7, 4), (256, 256, 64), (100, 1, 32)]
+    g2["tiles_sizes"] = np.array(sizes, np.int32)
+    for k, (w, h, bs) in enumerate(sizes):
+        g2[f"tiles_linear_{k}"] = r.tiles(w, h, bs, "linear")
+        g2[f"tiles_centre_{k}"] = r.tiles(w, h, bs, "centre")      # ties broken by std::random_device
+        g2[f"tiles_linear_t8_{k}"] = r.tiles(w, h, bs, "linear", nthreads=8)
+    OUT2 = os.path.join(os.path.dirname(OUT), "prims_r02.npz")
+    np.savez_compressed(OUT2, **g2)
+    print("wrote", OUT2, os.path.getsize(OUT2), "bytes,", len(g2), "arrays")
 
 
 if __name__ == "__main__":

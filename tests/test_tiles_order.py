@@ -54,6 +54,16 @@ def test_centre_order_restatement():
     assert keys == sorted(keys)
 
 
+@pytest.mark.parametrize("order", ["linear", "centre"])
+def test_restatement_matches_oracle_tile_lists(oracle_built, order):
+    """tile_order() (used by the callback test) = the oracle's list, itself pinned against the
+    reference's ImageSplitter (tests/test_oracle_golden.py::test_tile_lists)."""
+    o = oracle_built.oracle_prims()
+    for W, H, ts in [(50, 38, 8), (64, 48, 16), (1920, 1080, 32)]:
+        t = o.tiles(W, H, ts, order)
+        assert [(x, y, x + w, y + h) for x, y, w, h in t.tolist()] == tile_order(W, H, ts, order)
+
+
 def test_oracle_orders_differ_only_by_summation_order(oracle_built):
     a, wa, _ = oracle_built.OracleScene(spec("linear"), threads=4).render()
     b, wb, _ = oracle_built.OracleScene(spec("centre"), threads=4).render()
