@@ -546,12 +546,23 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 			key[k] = (h && child[k] >= 0) ? lo : inf;
 			if(h && child[k] < 0 && count[k] > 0) leaves |= 1u << k;
 		}
-#pragma unroll
-		for(int k = 0; k < 4; ++k)
+		// the hit leaves' triangles as one per-lane list (leaf order, then triangle order), so that a
+		// wave runs max-over-lanes tests per node instead of one pass per leaf slot any lane hit
+		int e[4], s4[4];
 		{
-			if(!(leaves & (1u << k))) continue;
-			const int start = ~child[k];
-			for(int q = start; q < start + count[k]; ++q)
+			int acc = 0;
+#pragma unroll
+			for(int k = 0; k < 4; ++k)
+			{
+				const bool l = leaves & (1u << k);
+				s4[k] = ~child[k] - acc;
+				acc += l ? count[k] : 0;
+				e[k] = acc;
+			}
+		}
+		for(int i = 0; i < e[3]; ++i)
+		{
+			const int q = i + (i < e[0] ? s4[0] : i < e[1] ? s4[1] : i < e[2] ? s4[2] : s4[3]);
 			{
 				TRACE_STAT(++tests);
 				const float4 *tp = C.tris + 3 * q;
