@@ -607,6 +607,153 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	return prim_best >= 0;
 }
 
+// k_trace's BVH4 loop with per-lane ray refill: a lane works through its own sequence of queue
+// entries (j, j + stride, ...), closest rays then shadow rays, and starts its next ray as soon as
+// its traversal ends, so a wave runs as long as its longest lane's sum of rays instead of the sum
+// over rays of the longest lane.  Every ray runs the sequence of traverse4 (same visits, culling,
+// leaf order and early exits), so hits are identical.
+template<bool SPILL>
+__device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPaths &P, uint32_t n_a, uint32_t total,
+                             uint32_t a0, uint32_t s0, uint32_t j, uint32_t stride, uint32_t &visits, uint32_t &tests,
+                             uint32_t &n_closest, uint32_t &n_shadow)
+{
+	const int lane = threadIdx.x;
+	const uint32_t glane = blockIdx.x * blockDim.x + threadIdx.x;
+	const float inf = __builtin_huge_valf();
+	V3 o = v3(0.f, 0.f, 0.f), d = o, id = o, oid = o;
+	float tmin = 0.f, tmax = 0.f, box_t0 = 0.f, t_best = 0.f;
+	int prim_best = -1, sp = 0, node = -1;
+	bool any = false;
+	uint32_t cur = 0;
+	auto push = [&](int v) {
+		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + lane] = v;
+		else if(SPILL) C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane] = v;
+	};
+	for(;;)
+	{
+		if(node < 0)
+		{
+			// next ray of this lane (closest entries with a NaN direction carry no ray)
+			float4 od, dd;
+			bool got = false;
+			for(;;)
+			{
+				if(j >= total) break;
+				cur = j;
+				j += stride;
+				if(cur < n_a)
+				{
+					od = Q.ray_o[a0 + cur];
+					dd = Q.ray_d[a0 + cur];
+					if(dd.w != dd.w) continue;
+					tmin = od.w;
+					tmax = (dd.w >= 0.f) ? dd.w : inf;
+					any = false;
+					++n_closest;
+				}
+				else
+				{
+					od = Q.sh_o[s0 + (cur - n_a)];
+					dd = Q.sh_d[s0 + (cur - n_a)];
+					tmin = 0.f;
+					tmax = dd.w;
+					any = true;
+					++n_shadow;
+				}
+				got = true;
+				break;
+			}
+			if(!got) break;
+			o = xyz(od);
+			d = xyz(dd);
+			V3 dq = d;
+			if(fabsf(dq.x) < 1e-20f) dq.x = copysignf(1e-20f, dq.x);
+			if(fabsf(dq.y) < 1e-20f) dq.y = copysignf(1e-20f, dq.y);
+			if(fabsf(dq.z) < 1e-20f) dq.z = copysignf(1e-20f, dq.z);
+			id = v3(rcpExact(dq.x), rcpExact(dq.y), rcpExact(dq.z));
+			oid = v3(o.x * id.x, o.y * id.y, o.z * id.z);
+			box_t0 = any ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
+			t_best = tmax;
+			prim_best = -1;
+			sp = 0;
+			node = 0;
+		}
+		TRACE_STAT(++visits);
+		const float4 *np = C.nodes + 8 * node;
+		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
+		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
+		float key[4];
+		int child[4], e[4], s4[4];
+		int acc = 0;
+#pragma unroll
+		for(int k = 0; k < 4; ++k)
+		{
+			const float ax = __builtin_fmaf(lane4(lx, k), id.x, -oid.x), bx = __builtin_fmaf(lane4(hx, k), id.x, -oid.x);
+			const float ay = __builtin_fmaf(lane4(ly, k), id.y, -oid.y), by = __builtin_fmaf(lane4(hy, k), id.y, -oid.y);
+			const float az = __builtin_fmaf(lane4(lz, k), id.z, -oid.z), bz = __builtin_fmaf(lane4(hz, k), id.z, -oid.z);
+			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
+			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
+			const bool h = lo <= hi;
+			child[k] = __float_as_int(lane4(cf, k));
+			const int count = __float_as_int(lane4(kf, k));
+			key[k] = (h && child[k] >= 0) ? lo : inf;
+			s4[k] = ~child[k] - acc;
+			acc += (h && child[k] < 0) ? count : 0;
+			e[k] = acc;
+		}
+		bool done = false;
+		for(int i = 0; i < e[3]; ++i)
+		{
+			const int q = i + (i < e[0] ? s4[0] : i < e[1] ? s4[1] : i < e[2] ? s4[2] : s4[3]);
+			TRACE_STAT(++tests);
+			const float4 *tp = C.tris + 3 * q;
+			const float4 ta = tp[0], tb = tp[1], tc = tp[2];
+			const float t = triTest(ta, tb, tc, o, d, t_best);
+			if(t == -1.f) continue;
+			const int prim = __float_as_int(tb.w);
+			if(any)
+			{
+				if(t < tmax && t >= 0.f) { t_best = t; prim_best = prim; done = true; break; }
+			}
+			else if(t >= tmin && (t < t_best || (t == t_best && prim_best >= 0 && prim < prim_best)))
+			{
+				t_best = t;
+				prim_best = prim;
+			}
+		}
+		if(!done)
+		{
+			cswap(key[0], child[0], key[1], child[1]);
+			cswap(key[2], child[2], key[3], child[3]);
+			cswap(key[0], child[0], key[2], child[2]);
+			cswap(key[1], child[1], key[3], child[3]);
+			cswap(key[1], child[1], key[2], child[2]);
+			if(key[3] < inf) { push(child[3]); ++sp; }
+			if(key[2] < inf) { push(child[2]); ++sp; }
+			if(key[1] < inf) { push(child[1]); ++sp; }
+			int next = key[0] < inf ? child[0] : -1;
+			if(next < 0 && sp > 0)
+			{
+				--sp;
+				next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + lane]
+				                                    : C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane];
+			}
+			node = next;
+			done = next < 0;
+		}
+		if(done)
+		{
+			if(any) P.occ[Q.sh_idx[s0 + (cur - n_a)]] = prim_best >= 0 ? 1 : 0;   // P = state set of the consumer shade
+			else
+			{
+				Q.hit_t[a0 + cur] = t_best;
+				Q.hit_prim[a0 + cur] = prim_best;
+			}
+			node = -1;
+		}
+	}
+}
+
 template<bool ANY, bool WIDE, bool SPILL = true, bool TS = false>
 __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best,
                                          int &prim_best, uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
@@ -615,15 +762,14 @@ __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tm
 	return traverse2<ANY, TS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
 }
 
-// k_trace asks the register allocator for 8 waves per SIMD (<= 64 VGPRs; measured +3% on C2 over
-// the unconstrained 68); -DYAF_TRACE_WAVES=n overrides for tuning, 0 removes the constraint
-#ifndef YAF_TRACE_WAVES
-#define YAF_TRACE_WAVES 8
-#endif
-#if YAF_TRACE_WAVES > 0
+// k_trace asks the register allocator for 8 waves per SIMD for LDS-resident scenes (<= 64 VGPRs;
+// measured +3% on C2 over the unconstrained 68) and 6 for scenes in global memory, whose refill
+// loop (traceRefill4) needs the registers (C4: 226 -> 189 ms of k_trace per frame at 6, spills at 8);
+// -DYAF_TRACE_WAVES=n overrides both for tuning
+#ifdef YAF_TRACE_WAVES
 #define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(YAF_TRACE_WAVES)))
 #else
-#define YAF_TRACE_ATTR
+#define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LDS_SCENE ? 8 : 6)))
 #endif
 
 template<bool LDS_SCENE, bool WIDE, bool TS>
@@ -658,6 +804,13 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	const uint32_t a0 = L.s * S.cap_a, s0 = L.s * S.cap_s;
 	uint32_t visits = 0, tests = 0, n_closest = 0, n_shadow = 0;
 	const uint32_t stride = L.nb * blockDim.x;
+#ifndef YAF_TRACE_NOREFILL
+	// refill pays where traversals are long (meshes in global memory: C4 -16%); on the short
+	// LDS-resident traversals of small scenes its per-visit bookkeeping costs more (C2 +35%)
+	if(!LDS_SCENE && WIDE && !TS)
+		traceRefill4<true>(C, Q, P, n_a, total, a0, s0, L.r * blockDim.x + threadIdx.x, stride, visits, tests, n_closest, n_shadow);
+	else
+#endif
 	// one uniform trip count per workgroup so every lane reaches the same exits
 	for(uint32_t base = L.r * blockDim.x; base < total; base += stride)
 	{

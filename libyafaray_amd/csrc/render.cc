@@ -379,6 +379,7 @@ bool GpuRenderer::upload(HostScene &hs)
 	if(const char *e = getenv("YAFARAY_AMD_LDS_STACK"); e && *e) d.lds_stack = std::min(d.stack_depth, std::max(4, atoi(e)));
 	const size_t scene_bytes = (size_t)(d.node_f4 * d.n_nodes + 3 * d.n_tris) * 16;
 	d.scene_in_lds = scene_bytes + (size_t)d.lds_stack * yafamd_trace_block() * 4 <= 48 * 1024;
+	if(const char *e = getenv("YAFARAY_AMD_SCENE_LDS"); e && *e == '0') d.scene_in_lds = false;   // tests: global-memory traversal on small scenes
 	{
 		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy))
 		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : 0);

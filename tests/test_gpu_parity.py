@@ -54,6 +54,7 @@ BVH_VARIANTS = {"bvh4": {"YAFARAY_AMD_BVH_BUILD": "host", "YAFARAY_AMD_TRACE": "
                 "bvh4-spill": {"YAFARAY_AMD_LDS_STACK": "4", "YAFARAY_AMD_TRACE": "bvh"},
                 "bvh2": {"YAFARAY_AMD_BVH_WIDTH": "2", "YAFARAY_AMD_TRACE": "bvh"},
                 "gpu-build": {"YAFARAY_AMD_BVH_BUILD": "gpu", "YAFARAY_AMD_TRACE": "bvh"},
+                "bvh4-global": {"YAFARAY_AMD_SCENE_LDS": "0", "YAFARAY_AMD_TRACE": "bvh"},
                 "brute": {"YAFARAY_AMD_TRACE": "brute"}}
 
 
