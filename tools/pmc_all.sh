@@ -20,4 +20,6 @@ run A SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACT
 run B SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS
 run D TCC_HIT_sum TCC_MISS_sum
 run C SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT
-cd $R && python3 tools/pmc_aggregate.py $CFG gpurun_out/pmc_$CFG.json $dirs > /dev/null && echo "wrote gpurun_out/pmc_$CFG.json"
+# key the file the way bench.py's load_pmc() looks it up (workload + kernel source)
+KEY=$(cd $R && python3 -c "import sys; sys.argv=['bench.py']+sys.argv[1:]; import bench; a=bench.parse(); a.spp=a.spp or (1 if a.scene=='photon' else 64); print(bench.pmc_config(a, a.width, a.height))" "$@")
+cd $R && python3 tools/pmc_aggregate.py $KEY gpurun_out/pmc_$KEY.json $dirs > /dev/null && echo "wrote gpurun_out/pmc_$KEY.json (copy to profiles/)"
