@@ -221,6 +221,19 @@ struct DevScene
 	int caus_map, c_photons, c_paths, c_search;
 	float c_radius2;               // caustic_radius^2 (float product, :629)
 	int gather_on;                 // k_shade queues k_gather requests (diffuse and / or caustic estimates)
+	// PhotonIntegrator final gathering (integrator_photon_mapping.cc:39-88, 183-193, 540-591, 640-763):
+	// radiance points picked while shooting the diffuse map, thinned and pre-gathered into the
+	// radiance map (same layout as the photon maps, .xyz of rph_dir = the point's normal); k_fg
+	// traces the gather paths of every diffuse camera hit and looks the radiance map up
+	int fg_on, fg_samples, fg_bounces;
+	float fg_min_pathlen;          // gather_dist_
+	float fg_lookup_rad;           // lookup_rad_ = 4 diffuseRadius^2 (:245)
+	float fg_i_scale;              // preGatherWorker i_scale = 1 / (nPaths pi), long double on the host (:53)
+	const float4 *rph_pos;
+	const float4 *rph_dir;
+	const float *rph_colb;
+	const uint4 *rpk_nodes;
+	int n_rphotons;
 
 	// surface attributes and shader nodes: only when some material has nodes or some mesh has
 	// orco / uv / smooth normals (has_attr); k_surface then fills DevQueues::sattr per hit
@@ -327,6 +340,7 @@ enum : uint32_t
 	G_DIFFUSE = 1u,   // diffuse-map density estimate (PhotonIntegrator)
 	G_CAUSTIC = 2u,   // causticPhotons()
 	G_EXTRA = 4u,     // then add extra.xyz
+	G_FG = 8u,        // finalGathering() (k_fg, before k_gather): extra.xy = (pixel offset, sample index) bits
 };
 
 // Queues are segmented: segment b (capacity cap_a entries / cap_s shadow rays) belongs to workgroup
@@ -347,6 +361,11 @@ struct PhotonState
 	float4 *dep_b;       // (direction, colour.g)
 	float *dep_c;        // colour.b
 	uint8_t *dep_flag;   // 1 = a photon was stored in this slot
+	// final gathering (diffuse map only): radiance point per deposit slot (:184-193)
+	float4 *rad_a;       // (position, refl.r)
+	float4 *rad_b;       // (normal facing the photon, refl.g)
+	float4 *rad_c;       // (refl.b, transm.rgb)
+	uint8_t *rad_flag;   // 1 = this deposit is a radiance point (null: final gathering off)
 };
 
 // the lights one photon map is shot from (render_view.cc:103-110: lights emitting diffuse / caustic

@@ -653,15 +653,20 @@ bool Scene::createIntegrator(const std::string &name, const ParamMap &p)
 	if(type == "photonmapping")
 	{
 		// integrator_photon_mapping.cc:765-850.  The GPU core serves the diffuse photon map with the
-		// k-NN density estimate (finalGather = false); final gathering, map display, ambient
-		// occlusion and photon-map files are not part of it yet.
-		bool fg = true, show_map = false, ao = false;
+		// k-NN density estimate (finalGather = false) or final gathering (the default); map display,
+		// ambient occlusion and photon-map files are not part of it yet.
+		bool fg = true, show_map = false, ao = false, transp_shad = false;
 		std::string processing = "generate";
 		p.get("finalGather", fg);
 		p.get("show_map", show_map);
 		p.get("do_AO", ao);
+		p.get("transpShad", transp_shad);
 		p.get("photon_maps_processing", processing);
-		if(fg) { log.error("PhotonIntegrator: finalGather = true is not supported by the GPU core yet (set finalGather false)"); return false; }
+		if(fg && transp_shad)
+		{
+			log.error("PhotonIntegrator: finalGather with transpShad is not supported by the GPU core yet (gather paths test opaque shadows)");
+			return false;
+		}
 		if(show_map || ao) { log.error("PhotonIntegrator: show_map / do_AO are not supported by the GPU core yet"); return false; }
 		if(processing != "generate") { log.error("PhotonIntegrator: photon_maps_processing '" + processing + "' is not supported (generate only)"); return false; }
 	}
@@ -1015,6 +1020,23 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			rp.pm.radius2 = ds_rad;
 			rp.pm.bounces = std::max(0, pbounces);
 			rp.pm.threads = s.threads_photons;
+			// final gathering (:777-810): fg_samples, fg_bounces, fg_min_pathlen (default diffuseRadius)
+			bool fg = true;
+			int fg_samples = 32, fg_bounces = 2;
+			float gather_dist = ds_rad;
+			ip.get("finalGather", fg);
+			ip.get("fg_samples", fg_samples);
+			ip.get("fg_bounces", fg_bounces);
+			ip.get("fg_min_pathlen", gather_dist);
+			rp.pm.final_gather = fg && diffuse;
+			rp.pm.fg_samples = fg_samples;
+			rp.pm.fg_bounces = fg_bounces;
+			rp.pm.fg_min_pathlen = gather_dist;
+			if(rp.pm.final_gather && s.aa_passes > 1 && s.aa_indirect_sample_multiplier_factor != 1.f)
+			{
+				log.error("PhotonIntegrator: finalGather with AA_indirect_sample_multiplier_factor != 1 is not supported by the GPU core");
+				return false;
+			}
 		}
 		S.width = s.width;
 		S.height = s.height;

@@ -2124,7 +2124,9 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		uint32_t g_mode = 0;
 		if(want_gather)
 		{
-			g_mode = ((is_photon && S.n_photons > 0) ? G_DIFFUSE : 0u) | (S.caus_map ? G_CAUSTIC : 0u);
+			g_mode = ((is_photon && S.n_photons > 0) ? (S.fg_on ? G_FG : G_DIFFUSE) : 0u) | (S.caus_map ? G_CAUSTIC : 0u);
+			// final gathering (k_fg) needs the PixelSamplingData of the sample
+			if(g_mode & G_FG) g_extra = C3{__uint_as_float(offset), __uint_as_float(sample_idx), 0.f};
 			if(ao_after_caustic && S.do_ao) { g_extra = ao_extra; g_mode |= G_EXTRA; }
 			if(is_path) { g_extra = pcol / (float)n_paths; g_mode |= G_EXTRA; }   // path_tracer.cc:274-278
 		}
@@ -2775,6 +2777,36 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 	}
 }
 
+// Final gathering: :186 keeps a deposit as a radiance point when the global FastRandom draws
+// < 0.125 (shared by the photon threads, so schedule-dependent); a hash of the deposit slot (photon
+// id, bounce) keeps one in eight here — the oracle uses the same hash
+__device__ __forceinline__ bool fgRadSelect(uint32_t slot) { return (fnv32(slot ^ 0x6a09e667u) & 7u) == 0u; }
+
+// material.cc:156-174 Material::getReflectivity: the mean of 16 weighted material samples
+template<bool EXT>
+__device__ C3 getReflectivity(const DevScene &S, const DevMaterial &m, const Surf &sp, uint32_t flags)
+{
+	if(!(flags & (B_TRANSMIT | B_REFLECT) & sp.flags)) return c3(0.f);
+	C3 total = c3(0.f);
+	for(int i = 0; i < 16; ++i)
+	{
+		const float s_1 = 0.03125f + 0.0625f * static_cast<float>(i);
+		const float s_2 = riVdC((uint32_t)i);
+		BsdfSample s;
+		s.s_1 = ldsDim(S, 2, (uint32_t)i);
+		s.s_2 = ldsDim(S, 3, (uint32_t)i);
+		s.flags = flags;
+		s.pdf = 0.f;
+		s.sampled = B_NONE;
+		const V3 wo = cosHemisphere(sp.n, sp.nu, sp.nv, s_1, s_2);
+		V3 wi = v3(0.f, 0.f, 0.f);
+		float w = 0.f;
+		const C3 col = matSample<EXT>(m, sp, wo, wi, s, w);
+		total = total + col * w;
+	}
+	return total * 0.0625f;
+}
+
 // :162-219 — one bounce of every live photon path: intersect, deposit, scatter (material.cc:137-153)
 template<bool LDS_SCENE, bool WIDE, bool EXT>
 __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
@@ -2846,6 +2878,17 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 					A.P.dep_b[slot] = f4(wi, lcol.g);
 					A.P.dep_c[slot] = lcol.b;
 					A.P.dep_flag[slot] = 1;
+					// :184-193 radiance point (final gathering): normal faced to the photon, reflectivities
+					if(A.P.rad_flag && !A.L.caustic && fgRadSelect(slot))
+					{
+						const DevMaterial &m = S.mats[sp.mat];
+						const C3 refl = getReflectivity<EXT>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_REFLECT);
+						const C3 transm = getReflectivity<EXT>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_TRANSMIT);
+						A.P.rad_a[slot] = f4(sp.p, refl.r);
+						A.P.rad_b[slot] = f4(faceForward(sp.ng, sp.n, wi), refl.g);
+						A.P.rad_c[slot] = make_float4(refl.b, transm.r, transm.g, transm.b);
+						A.P.rad_flag[slot] = 1;
+					}
 				}
 				if(A.bounce < A.max_bounces)
 				{
@@ -3215,6 +3258,446 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 	}
 }
 
+// ---------------------------------------------------------------------------------------------
+// Final gathering (PhotonIntegrator, finalGather = true)
+// ---------------------------------------------------------------------------------------------
+// Stable compaction of the radiance points (deposit-slot order = one reference thread's order),
+// after k_photon_count / k_photon_scan over rad_flag
+__global__ void __launch_bounds__(1024) k_rad_scatter(PhotonState P, uint32_t n_slots, const uint32_t *offsets, float4 *out_a,
+                                                      float4 *out_b, float4 *out_c)
+{
+	__shared__ uint32_t wsum[16];
+	const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+	const bool f = k < n_slots && P.rad_flag[k];
+	const uint64_t m = __ballot(f);
+	const int wid = threadIdx.x >> 6;
+	if(laneId() == 0) wsum[wid] = (uint32_t)__popcll(m);
+	__syncthreads();
+	uint32_t base = offsets[blockIdx.x];
+	for(int w = 0; w < wid; ++w) base += wsum[w];
+	if(f)
+	{
+		const uint32_t o = base + (uint32_t)__popcll(m & ((1ull << laneId()) - 1ull));
+		out_a[o] = P.rad_a[k];
+		out_b[o] = P.rad_b[k];
+		out_c[o] = P.rad_c[k];
+	}
+}
+
+// preGatherWorker (integrator_photon_mapping.cc:39-88) for every kept radiance point: k-NN gather of
+// the diffuse map within diffuseRadius^2, sum in heap-array order (refl for photons arriving on the
+// normal's side, transm otherwise), stored as Photon(normal, pos, sum) of the radiance map
+struct PreGatherArgs
+{
+	DevScene S;
+	const float4 *rad_a, *rad_b, *rad_c;
+	const uint32_t *kept;
+	uint32_t n;
+	float4 *out_pos, *out_dir;
+	float *out_colb;
+};
+
+__global__ void __launch_bounds__(kGatherBlock) k_pregather(PreGatherArgs A)
+{
+	extern __shared__ uint4 gather_smem[];
+	const DevScene &S = A.S;
+	uint32_t *lds_words = reinterpret_cast<uint32_t *>(gather_smem);
+	HeapRefPacked heap;
+	heap.e = lds_words + 2 * threadIdx.x;
+	heap.stride = kGatherBlock;
+	const uint32_t gstride = gridDim.x * kGatherBlock;
+	uint2 *stk = S.pk_stack + blockIdx.x * kGatherBlock + threadIdx.x;
+	const float ds_radius_2 = S.pm_radius2 * S.pm_radius2;   // :42 ds_rad * ds_rad (pm_radius2 holds ds_rad)
+	uint32_t visits = 0;
+	for(uint32_t j = blockIdx.x * kGatherBlock + threadIdx.x; j < A.n; j += gstride)
+	{
+		const uint32_t r = A.kept[j];
+		const float4 a = A.rad_a[r], b = A.rad_b[r], c = A.rad_c[r];
+		const V3 pos = xyz(a), rnorm = xyz(b);
+		const C3 refl = C3{a.w, b.w, c.x}, transm = C3{c.y, c.z, c.w};
+		float radius = ds_radius_2;
+		const int found = pkLookup(S.pk_nodes, pos, S.pm_search, radius, heap, stk, gstride, visits);
+		C3 sum = c3(0.f);
+		if(found > 0)
+		{
+			const float scale = S.fg_i_scale / radius;
+			for(int i = 0; i < found; ++i)
+			{
+				const uint32_t ph = heap.i(i);
+				const float4 pa = S.ph_pos[ph], pb = S.ph_dir[ph];
+				const C3 pc = C3{pa.w, pb.w, S.ph_colb[ph]};
+				if(dot(rnorm, xyz(pb)) > 0.f) sum = sum + refl * scale * pc;
+				else sum = sum + transm * scale * pc;
+			}
+		}
+		A.out_pos[j] = f4(pos, sum.r);
+		A.out_dir[j] = f4(rnorm, sum.g);
+		A.out_colb[j] = sum.b;
+	}
+}
+
+// PhotonMap::findNearest (photon.cc:136-142): NearestPhoton (photon.h:159-169) over the
+// non-recursive lookup (pkdtree.h:225-292) — the last photon accepted (facing n, strictly closer
+// than the shrinking radius); far children that already fail the radius are not pushed (the radius
+// never grows, so the reference discards them at pop time).  -1: none.
+__device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2)
+{
+	uint2 stk[64];
+	int nearest = -1;
+	uint32_t curr = 0;
+	int sp_top = 0;
+	for(;;)
+	{
+		uint4 nd = nodes[curr];
+		while((nd.w & 3u) != 3u)
+		{
+			const int axis = (int)(nd.w & 3u);
+			const float split_val = __uint_as_float(nd.x);
+			const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+			uint32_t far_child;
+			if(pa <= split_val) { far_child = nd.w >> 2; curr = curr + 1; }
+			else { far_child = curr + 1; curr = nd.w >> 2; }
+			float d2 = pa - split_val;
+			d2 *= d2;
+			if(d2 <= max_d2 && sp_top < 64)
+			{
+				stk[sp_top] = make_uint2(far_child, __float_as_uint(d2));
+				++sp_top;
+			}
+			nd = nodes[curr];
+		}
+		const uint32_t ph = nd.w >> 2;
+		const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
+		const float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
+		if(dist_2 < max_d2)
+		{
+			if(dot(xyz(dirs[ph]), n) > 0.f) { nearest = (int)ph; max_d2 = dist_2; }
+		}
+		if(sp_top == 0) break;
+		uint2 top = stk[sp_top - 1];
+		bool done = false;
+		while(__uint_as_float(top.y) > max_d2)
+		{
+			--sp_top;
+			if(sp_top == 0) { done = true; break; }
+			top = stk[sp_top - 1];
+		}
+		if(done) break;
+		curr = top.x;
+		--sp_top;
+	}
+	return nearest;
+}
+
+// MonteCarloIntegrator::doLightEstimation for one light (integrator_montecarlo.cc:80-408) with the
+// shadow rays traced in place: neeLight's arithmetic, neeSum's addition order
+template<bool EXT, bool WIDE>
+__device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
+                                  uint32_t loffs, uint32_t sample_idx, uint32_t offset, uint32_t &visits, uint32_t &tests)
+{
+	const bool cast_shadows = L.cast_shadows && m.receive_shadows;
+	const float p_len = length(sp.p);
+	const float sh_tmin = S.shadow_bias_auto ? S.shadow_bias * fmaxf(1.f, p_len) : S.shadow_bias;
+	float t_hit;
+	int p_hit;
+	if(L.type == LIGHT_POINT)
+	{
+		C3 c = c3(0.f);
+		V3 ldir = lv(L.pos) - sp.p;
+		const float dist_sqr = ldir.x * ldir.x + ldir.y * ldir.y + ldir.z * ldir.z;
+		const float dist = sqrtf(dist_sqr);
+		if(!((double)dist == 0.0))
+		{
+			const float idist_sqr = rcpExact(dist_sqr);
+			ldir = ldir * rcpExact(dist);
+			const C3 lcol = C3{L.color[0], L.color[1], L.color[2]} * idist_sqr;
+			const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
+			const C3 surf_col = matEval<EXT>(m, sp, wo, ldir, B_ALL);
+			const C3 contrib = surf_col * lcol * angle * c3(1.f);
+			V3 so;
+			float st;
+			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
+			const bool occ = cast_shadows && traverse<true, WIDE>(C, so, ldir, 0.f, st, t_hit, p_hit, visits, tests);
+			if(!occ) c = c + contrib;
+		}
+		return c3(0.f) + c;
+	}
+	const uint32_t l_offs = loffs * 4567u;
+	const int num_samples = L.samples;
+	const uint32_t offs = (uint32_t)num_samples * sample_idx + offset + l_offs;
+	const V3 corner = lv(L.pos), to_x = lv(L.to_x), to_y = lv(L.to_y), fn = lv(L.fnormal);
+	const C3 lcolor = C3{L.color[0], L.color[1], L.color[2]};
+	HaltonInc<2> hal_2;
+	HaltonInc<3> hal_3;
+	hal_2.value = hal_3.value = 0.0;
+	hal_2.start(offs - 1u);
+	hal_3.start(offs - 1u);
+	C3 acc_l = c3(0.f), acc_m = c3(0.f);
+	const float b_tmin = S.ray_min_dist_auto ? S.ray_min_dist * fmaxf(1.f, p_len) : S.ray_min_dist;
+	for(int i = 0; i < num_samples; ++i)
+	{
+		const float s_1 = hal_2.next();
+		const float s_2 = hal_3.next();
+		// areaLightSampleLight (montecarlo.cc:156-282), light_area.cc:66-96
+		{
+			const V3 p = corner + s_1 * to_x + s_2 * to_y;
+			V3 ldir = p - sp.p;
+			const float dist_sqr = lengthSqr(ldir);
+			const float dist = sqrtf(dist_sqr);
+			bool ok = !((double)dist <= 0.0);
+			float cos_angle = 0.f;
+			if(ok)
+			{
+				ldir = ldir * rcpExact(dist);
+				cos_angle = dot(ldir, fn);
+				if(cos_angle <= 0) ok = false;
+			}
+			if(ok)
+			{
+				const float pdf = x87mulDiv(kPi, dist_sqr, L.area * cos_angle);
+				if(pdf > 1e-6f)
+				{
+					const C3 surf_col = matEval<EXT>(m, sp, wo, ldir, B_ALL);
+					const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
+					float w = 1.f;
+					const float m_pdf = matPdf<EXT>(m, sp, wo, ldir, B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT);
+					if(m_pdf > 1e-6f)
+					{
+						const float l_2 = pdf * pdf;
+						const float m_2 = m_pdf * m_pdf;
+						w = l_2 / (l_2 + m_2);
+					}
+					const C3 contrib = surf_col * lcolor * angle * w / pdf;
+					V3 so;
+					float st;
+					shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
+					const bool occ = cast_shadows && traverse<true, WIDE>(C, so, ldir, 0.f, st, t_hit, p_hit, visits, tests);
+					if(!occ) acc_l = acc_l + contrib;
+				}
+			}
+		}
+		// areaLightSampleMaterial (montecarlo.cc:284-383), light_area.cc:137-151
+		{
+			BsdfSample s;
+			s.s_1 = s_1;
+			s.s_2 = s_2;
+			s.flags = B_GLOSSY | B_DIFFUSE | B_DISPERSIVE | B_REFLECT | B_TRANSMIT;
+			s.pdf = 0.f;
+			s.sampled = B_NONE;
+			float W = 0.f;
+			V3 dir = v3(0.f, 0.f, 1.f);
+			const C3 surf_col = matSample<EXT>(m, sp, wo, dir, s, W);
+			bool ok = s.pdf > 1e-6f;
+			float t = 0.f, cos_angle = 0.f;
+			if(ok)
+			{
+				cos_angle = dot(dir, fn);
+				if(cos_angle <= 0) ok = false;
+				else if(!areaTri(corner, lv(L.c2), lv(L.c3), sp.p, dir, t))
+				{
+					if(!areaTri(corner, lv(L.c3), lv(L.c4), sp.p, dir, t)) ok = false;
+				}
+				if(ok && !(t > 1.0e-10f)) ok = false;
+			}
+			if(ok)
+			{
+				const float light_pdf = x87mul(kDiv1ByPi, rcpExact(t * t) * L.area * cos_angle);
+				if(light_pdf > 1e-6f)
+				{
+					const float l_pdf = rcpExact(light_pdf);
+					const float l_2 = l_pdf * l_pdf;
+					const float m_2 = s.pdf * s.pdf;
+					const float w = m_2 / (l_2 + m_2);
+					const C3 contrib = surf_col * lcolor * w * W;
+					V3 so;
+					float st;
+					shadowRayOf(sp.p, dir, b_tmin, t, so, st);
+					const bool occ = cast_shadows && traverse<true, WIDE>(C, so, dir, 0.f, st, t_hit, p_hit, visits, tests);
+					if(!occ) acc_m = acc_m + contrib;
+				}
+			}
+		}
+	}
+	const C3 col_l = acc_l * L.inv_samples;
+	const C3 col_m = acc_m * L.inv_samples;
+	return (c3(0.f) + col_l) + col_m;
+}
+
+// the hit of a gather ray: surface + (textured scenes) the shader-node colour at the hit, as
+// k_photon_bounce evaluates it
+template<bool EXT>
+__device__ __forceinline__ Surf fgSurf(const DevScene &S, V3 o, V3 d, float t, int prim)
+{
+	Surf sp = makeSurf(S, o, d, t, prim);
+	if(EXT && S.has_attr)
+	{
+		const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, o, d, sp.p);
+		const DevMaterial &m = S.mats[sp.mat];
+		C3 dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+		float drefl = 1.f, sigma = 0.f;
+		if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl, sigma);
+		applyAttr(sp, f4(sa.n, drefl), f4(dcol, sigma));
+	}
+	return sp;
+}
+
+// k_fg: PhotonIntegrator::finalGathering (integrator_photon_mapping.cc:640-763) for every gather
+// request with G_FG, one lane per request: fg_samples paths from the camera hit, each traced in
+// place (closest rays and the shadow rays of estimateOneDirectLight), ended by a radiance-map
+// lookup; the result is added to the request's colour (:908-910, clamp_indirect = 0) for k_gather.
+// `mat_bsd_fs` of the reference (:682) is a reference into the first gather hit's MaterialData,
+// which the next intersect() frees (:741): here the current hit's flags are read (YafaRay's intent).
+struct FgArgs
+{
+	DevScene S;
+	DevNeeQueue G;
+	DevCounters cnt_next;
+	int stack_depth;
+	int *spill;
+};
+
+template<bool LDS_SCENE, bool WIDE, bool EXT>
+__global__ void __launch_bounds__(kTraceBlock) k_fg(FgArgs A)
+{
+	const DevScene &S = A.S;
+	extern __shared__ float4 smem[];
+	TraceCtx C;
+	C.stack = reinterpret_cast<int *>(smem);
+	C.lds_depth = A.stack_depth;
+	C.spill = A.spill;
+	C.spill_stride = gridDim.x * blockDim.x;
+	if(LDS_SCENE)
+	{
+		float4 *lds_nodes = smem + (A.stack_depth * kTraceBlock) / 4;
+		float4 *lds_tris = lds_nodes + S.node_f4 * S.n_nodes;
+		for(int k = threadIdx.x; k < S.node_f4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = S.nodes[k];
+		for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = S.tris[k];
+		__syncthreads();
+		C.nodes = lds_nodes;
+		C.tris = lds_tris;
+	}
+	else
+	{
+		C.nodes = S.nodes;
+		C.tris = S.tris;
+	}
+	const bool ATTR = EXT && S.has_attr != 0;
+	const SegLoop L = segLoop(S.n_seg);
+	const uint32_t n_req = A.cnt_next.n_gather[L.s];
+	const uint32_t a0 = L.s * S.cap_a;
+	uint32_t visits = 0, tests = 0;
+	const int n_sampl = max(1, S.fg_samples);
+	for(uint32_t jj = L.r * blockDim.x + threadIdx.x; jj < n_req; jj += L.nb * blockDim.x)
+	{
+		const uint32_t j = a0 + jj;
+		const float4 ex = A.G.extra[j];
+		if(!(__float_as_uint(ex.w) & G_FG)) continue;
+		const uint32_t offset = __float_as_uint(ex.x), sample_idx = __float_as_uint(ex.y);
+		const float4 pp = A.G.p_prim[j];
+		Surf sp0 = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
+		if(ATTR) applyAttr(sp0, A.G.attr[2 * (size_t)j], A.G.attr[2 * (size_t)j + 1]);
+		const V3 wo0 = xyz(A.G.wo_k[j]);
+		const DevMaterial &m0 = S.mats[sp0.mat];
+		C3 path_col = c3(0.f);
+		for(int i = 0; i < n_sampl; ++i)
+		{
+			const uint32_t offs = (uint32_t)S.fg_samples * sample_idx + offset + (uint32_t)i;
+			BsdfSample s;
+			s.s_1 = riVdC(offs);
+			s.s_2 = ldsDim(S, 2, offs);
+			s.flags = B_DIFFUSE | B_REFLECT | B_TRANSMIT;
+			s.pdf = 0.f;
+			s.sampled = B_NONE;
+			float w = 0.f;
+			V3 dir = v3(0.f, 0.f, 0.f);
+			C3 scol = matSample<EXT>(m0, sp0, wo0, dir, s, w);
+			scol = scol * w;
+			if(isBlack(scol)) continue;
+			C3 throughput = scol;
+			float t;
+			int prim;
+			V3 from = sp0.p;
+			if(!traverse<false, WIDE>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests)) continue;
+			Surf hit = fgSurf<EXT>(S, from, dir, t, prim);
+			float length = t;
+			uint32_t mat_bsd_fs = hit.flags;
+			bool did_hit = true;
+			bool caustic = false;
+			bool close = length < S.fg_min_pathlen;
+			bool do_bounce = close || (mat_bsd_fs & B_SPECULAR);
+			C3 lcol = c3(0.f);
+			for(int depth = 0; depth < S.fg_bounces && do_bounce; ++depth)
+			{
+				const int d_4 = 4 * depth;
+				const V3 pwo = -dir;
+				const DevMaterial &mh = S.mats[hit.mat];
+				if(mat_bsd_fs & B_DIFFUSE)
+				{
+					if(close)
+					{
+						// estimateOneDirectLight (integrator_montecarlo.cc:70-78); the light pick draws a
+						// per-sample counter (the reference's runs per thread; one light is exact)
+						uint32_t lnum = 0;
+						if(S.n_lights > 1)
+						{
+							const uint32_t corr = 1u + (uint32_t)i * (uint32_t)max(1, S.fg_bounces) + (uint32_t)depth;
+							const float hv = haltonFirst(2u, 0.5, S.base_offset + corr - 1u);
+							lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
+						}
+						lcol = (S.n_lights > 0)
+						           ? lightEstimateInline<EXT, WIDE>(S, C, S.lights[lnum], mh, hit, pwo, lnum, sample_idx, offset, visits, tests) *
+						                 (float)S.n_lights
+						           : c3(0.f);
+					}
+					else if(caustic)
+					{
+						const V3 sf = faceForward(hit.ng, hit.n, pwo);
+						const int nearest = pkNearest(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad);
+						if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
+					}
+					if(close || caustic)
+					{
+						if(mat_bsd_fs & B_EMIT) lcol = lcol + matEmit<EXT>(mh, hit, pwo);
+						path_col = path_col + lcol * throughput;
+					}
+				}
+				BsdfSample sb;
+				sb.s_1 = ldsDim(S, d_4 + 3, offs);
+				sb.s_2 = ldsDim(S, d_4 + 4, offs);
+				sb.flags = close ? B_ALL : (B_SPECULAR | B_REFLECT | B_TRANSMIT | B_FILTER);
+				sb.pdf = 0.f;
+				sb.sampled = B_NONE;
+				V3 ndir = v3(0.f, 0.f, 0.f);
+				scol = matSample<EXT>(mh, hit, pwo, ndir, sb, w);
+				if(sb.pdf <= 1.0e-6f) { did_hit = false; break; }
+				scol = scol * w;
+				throughput = throughput * scol;
+				from = hit.p;
+				dir = ndir;
+				if(!traverse<false, WIDE>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests)) { did_hit = false; break; }
+				hit = fgSurf<EXT>(S, from, dir, t, prim);
+				mat_bsd_fs = hit.flags;
+				length += t;
+				caustic = (caustic || !depth) && (sb.sampled & (B_SPECULAR | B_FILTER));
+				close = length < S.fg_min_pathlen;
+				do_bounce = caustic || close;
+			}
+			if(did_hit && (mat_bsd_fs & (B_DIFFUSE | B_GLOSSY)))
+			{
+				const V3 sf = faceForward(hit.ng, hit.n, -dir);
+				const int nearest = pkNearest(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad);
+				if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
+				if(mat_bsd_fs & B_EMIT) lcol = lcol + matEmit<EXT>(S.mats[hit.mat], hit, -dir);
+				path_col = path_col + lcol * throughput;
+			}
+		}
+		const C3 fg = path_col / (float)n_sampl;
+		const uint4 cb = A.G.pix_mode[j];
+		const C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)} + fg;
+		A.G.pix_mode[j] = make_uint4(__float_as_uint(col.r), __float_as_uint(col.g), __float_as_uint(col.b), cb.w);
+	}
+}
+
 } // namespace yafamd
 
 // ---------------------------------------------------------------------------------------------
@@ -3473,6 +3956,67 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const D
 	}
 	else if(S->small_tables) hipLaunchKernelGGL((k_gather<true, false>), grid, dim3(kGatherBlock), lds, st, A);
 	else hipLaunchKernelGGL((k_gather<false, false>), grid, dim3(kGatherBlock), lds, st, A);
+	return hipGetLastError();
+}
+
+// Final gathering: compaction of the radiance points (reuses the photon count / scan kernels on
+// rad_flag); *total_dev receives the count
+hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b,
+                              float4 *c, hipStream_t st)
+{
+	const uint32_t nb = (n_slots + 1023u) / 1024u;
+	if(nb == 0) return hipSuccess;
+	hipLaunchKernelGGL(k_photon_count, dim3(nb), dim3(256), 0, st, P->rad_flag, n_slots, scratch_counts);
+	hipLaunchKernelGGL(k_photon_scan, dim3(1), dim3(1024), 0, st, scratch_counts, nb, total_dev);
+	hipLaunchKernelGGL(k_rad_scatter, dim3(nb), dim3(1024), 0, st, *P, n_slots, (const uint32_t *)scratch_counts, a, b, c);
+	return hipGetLastError();
+}
+
+// preGatherWorker over the kept radiance points (n of them, indices `kept` into the compacted
+// arrays); the grid is the gather grid, whose lanes the HBM lookup stack (S->pk_stack) is sized for
+hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
+                            float4 *out_pos, float4 *out_dir, float *out_colb, hipStream_t st)
+{
+	if(n == 0) return hipSuccess;
+	PreGatherArgs A;
+	A.S = *S;
+	A.rad_a = a;
+	A.rad_b = b;
+	A.rad_c = c;
+	A.kept = kept;
+	A.n = n;
+	A.out_pos = out_pos;
+	A.out_dir = out_dir;
+	A.out_colb = out_colb;
+	const size_t lds = (size_t)kGatherBlock * 8u * (size_t)max(1, S->pm_search);
+	hipLaunchKernelGGL(k_pregather, dim3(S->n_seg * kGatherPerSeg), dim3(kGatherBlock), lds, st, A);
+	return hipGetLastError();
+}
+
+// k_fg over the gather queue of one iteration (before k_gather), on the trace grid
+hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid,
+                            hipStream_t st)
+{
+	FgArgs A;
+	A.S = *S;
+	A.G = *G;
+	A.cnt_next = *cnt_next;
+	A.stack_depth = stack_depth;
+	A.spill = spill;
+	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
+	const bool wide = S->node_f4 == 8;
+#define YAF_FG_LAUNCH(L, W, E, B) hipLaunchKernelGGL((k_fg<L, W, E>), dim3(grid), dim3(kTraceBlock), B, st, A)
+	if(S->scene_in_lds)
+	{
+		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
+		if(S->ext) { if(wide) YAF_FG_LAUNCH(true, true, true, bytes); else YAF_FG_LAUNCH(true, false, true, bytes); }
+		else if(wide) YAF_FG_LAUNCH(true, true, false, bytes);
+		else YAF_FG_LAUNCH(true, false, false, bytes);
+	}
+	else if(S->ext) { if(wide) YAF_FG_LAUNCH(false, true, true, stack_bytes); else YAF_FG_LAUNCH(false, false, true, stack_bytes); }
+	else if(wide) YAF_FG_LAUNCH(false, true, false, stack_bytes);
+	else YAF_FG_LAUNCH(false, false, false, stack_bytes);
+#undef YAF_FG_LAUNCH
 	return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@
 #include <future>
 #include <mutex>
 #include <sstream>
+#include <unordered_map>
 
 using namespace yafamd;
 
@@ -47,6 +48,12 @@ hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, float4 *samples,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
 size_t yafamd_gather_lds_bytes(const DevScene *S);
+hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b,
+                              float4 *c, hipStream_t st);
+hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
+                            float4 *out_pos, float4 *out_dir, float *out_colb, hipStream_t st);
+hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid,
+                            hipStream_t st);
 size_t yafamd_gather_lanes(const DevScene *S);
 hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
                                 int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st);
@@ -100,6 +107,49 @@ std::vector<int> faurePerm(int b)
 	return out;
 }
 
+// Final gathering's radiance-point thinning (integrator_photon_mapping.cc:560-572): in shooting
+// order, a point still in use is kept and marks every point within the squared distance `maxrad`
+// (strictly less, the pkd lookup's test, pkdtree.h:263-268) whose normal faces the same side
+// (EliminatePhoton, photon.h:172-180) as unused.  The reference answers the range queries with a
+// point kd-tree; the kept set does not depend on how they are answered, so a uniform grid of cell
+// sqrt(maxrad) serves them here.  pos / nrm: 4 floats per point (xyz used).
+std::vector<uint32_t> eliminateRadPoints(const std::vector<float4> &pos, const std::vector<float4> &nrm, float maxrad)
+{
+	std::vector<uint32_t> kept;
+	const size_t n = pos.size();
+	if(!n) return kept;
+	const double cell = std::sqrt((double)maxrad) * 1.0001 + 1e-30;
+	auto cellOf = [&](const float4 &p, int dx, int dy, int dz) {
+		const int64_t x = (int64_t)std::floor(p.x / cell) + dx, y = (int64_t)std::floor(p.y / cell) + dy, z = (int64_t)std::floor(p.z / cell) + dz;
+		return (uint64_t)(x * 73856093) ^ (uint64_t)(y * 19349663) ^ (uint64_t)(z * 83492791);
+	};
+	std::unordered_map<uint64_t, std::vector<uint32_t>> grid;
+	grid.reserve(n);
+	for(uint32_t i = 0; i < n; ++i) grid[cellOf(pos[i], 0, 0, 0)].push_back(i);
+	std::vector<uint8_t> use(n, 1);
+	for(uint32_t i = 0; i < n; ++i)
+	{
+		if(!use[i]) continue;
+		kept.push_back(i);
+		const float4 q = pos[i], qn = nrm[i];
+		for(int dx = -1; dx <= 1; ++dx)
+			for(int dy = -1; dy <= 1; ++dy)
+				for(int dz = -1; dz <= 1; ++dz)
+				{
+					const auto it = grid.find(cellOf(q, dx, dy, dz));
+					if(it == grid.end()) continue;
+					for(uint32_t j : it->second)
+					{
+						const float vx = pos[j].x - q.x, vy = pos[j].y - q.y, vz = pos[j].z - q.z;
+						const float d2 = vx * vx + vy * vy + vz * vz;
+						const float nd = nrm[j].x * qn.x + nrm[j].y * qn.y + nrm[j].z * qn.z;
+						if(d2 < maxrad && nd > 0.f) use[j] = 0;
+					}
+				}
+	}
+	return kept;
+}
+
 } // namespace
 
 struct GpuRenderer::Impl
@@ -126,6 +176,10 @@ struct GpuRenderer::Impl
 	int c_photons = 0, c_paths = 0, c_depth = 0;
 	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
 	Buf ph_pos, ph_dir, ph_colb, pk_nodes, pk_stack;
+	// final gathering: radiance points per deposit slot, compacted, kept (indices), the radiance map
+	Buf rad_a, rad_b, rad_c, rad_flag, radc_a, radc_b, radc_c, rad_kept, rph_pos, rph_dir, rph_colb, rpk_nodes;
+	int n_rphotons = 0;
+	uint32_t n_rad_points = 0;
 	// render group (RCCL communicator over the group's GPUs) and its exchange buffers
 	ncclComm_t comm = nullptr;
 	Buf g_send, g_recv, g_wsend, g_wrecv, g_times;
@@ -506,6 +560,21 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	P.dep_c = (float *)d.dep_c.p;
 	P.dep_flag = (uint8_t *)d.dep_flag.p;
 	HIPCHECK(hipMemsetAsync(d.dep_flag.p, 0, n_slots, d.stream));
+	// final gathering: radiance points of the diffuse map's deposits (:184-193)
+	const bool want_rad = which == 0 && rp.pm.final_gather;
+	P.rad_a = P.rad_b = P.rad_c = nullptr;
+	P.rad_flag = nullptr;
+	if(want_rad)
+	{
+		if(!ensure(log_, d.rad_a, n_slots * 16) || !ensure(log_, d.rad_b, n_slots * 16) || !ensure(log_, d.rad_c, n_slots * 16) ||
+		   !ensure(log_, d.rad_flag, n_slots))
+			return false;
+		P.rad_a = (float4 *)d.rad_a.p;
+		P.rad_b = (float4 *)d.rad_b.p;
+		P.rad_c = (float4 *)d.rad_c.p;
+		P.rad_flag = (uint8_t *)d.rad_flag.p;
+		HIPCHECK(hipMemsetAsync(d.rad_flag.p, 0, n_slots, d.stream));
+	}
 	HIPCHECK(hipMemsetAsync(d.ph_n_alive.p, 0, 16, d.stream));
 	PROF(KK_PHOTON_EMIT, yafamd_photon_emit(&S, &P, &L, N, bounces, d.stream));
 	int cur = 0;
@@ -526,6 +595,16 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	HIPCHECK(hipMemcpyAsync(&n, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	n_out = n;
+	if(want_rad)
+	{
+		uint32_t nr = 0;
+		if(!ensure(log_, d.radc_a, n_slots * 16) || !ensure(log_, d.radc_b, n_slots * 16) || !ensure(log_, d.radc_c, n_slots * 16)) return false;
+		PROF(KK_PHOTON_COMPACT, yafamd_rad_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)d.radc_a.p,
+		                                          (float4 *)d.radc_b.p, (float4 *)d.radc_c.p, d.stream));
+		HIPCHECK(hipMemcpyAsync(&nr, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
+		HIPCHECK(hipStreamSynchronize(d.stream));
+		d.n_rad_points = nr;
+	}
 	const auto t1 = std::chrono::steady_clock::now();
 	stats_.photon_shoot_seconds += std::chrono::duration<double>(t1 - t0).count();
 	if(n == 0) return true;
@@ -536,6 +615,55 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	depth_out = depth;
 	stats_.photon_tree_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+	return true;
+}
+
+// Final gathering's radiance map (integrator_photon_mapping.cc:540-591): the radiance points shootMap
+// compacted are thinned on the host (eliminateRadPoints), pre-gathered on the GPU (k_pregather) and
+// the point kd-tree of the radiance map is built like the photon maps'.
+bool GpuRenderer::buildRadianceMap(RenderParams &rp)
+{
+	Impl &d = *d_;
+	DevScene &S = rp.scene;
+	const PhotonParams &pm = rp.pm;
+	const uint32_t nr = d.n_rad_points;
+	std::vector<float4> pos(nr), nrm(nr);
+	if(nr)
+	{
+		HIPCHECK(hipMemcpyAsync(pos.data(), d.radc_a.p, (size_t)nr * 16, hipMemcpyDeviceToHost, d.stream));
+		HIPCHECK(hipMemcpyAsync(nrm.data(), d.radc_b.p, (size_t)nr * 16, hipMemcpyDeviceToHost, d.stream));
+		HIPCHECK(hipStreamSynchronize(d.stream));
+	}
+	const std::vector<uint32_t> kept = eliminateRadPoints(pos, nrm, 0.01f * pm.radius2);
+	const uint32_t nk = (uint32_t)kept.size();
+	S.fg_on = 1;
+	S.fg_samples = pm.fg_samples;
+	S.fg_bounces = pm.fg_bounces;
+	S.fg_min_pathlen = pm.fg_min_pathlen;
+	S.fg_lookup_rad = 4 * pm.radius2 * pm.radius2;                                   // :245
+	S.fg_i_scale = static_cast<float>(1.f / ((float)S.pm_paths * 3.1415926535897932384626433832795L));   // :53 (math::num_pi)
+	S.n_rphotons = (int)nk;
+	std::ostringstream os;
+	os << "PhotonIntegrator: " << nr << " radiance points, " << nk << " kept for the radiance map";
+	log_.info(os.str());
+	if(nk == 0) { S.rpk_nodes = nullptr; return true; }
+	if(!ensure(log_, d.rad_kept, (size_t)nk * 4) || !ensure(log_, d.rph_pos, (size_t)nk * 16) || !ensure(log_, d.rph_dir, (size_t)nk * 16) ||
+	   !ensure(log_, d.rph_colb, (size_t)nk * 4) || !ensure(log_, d.rpk_nodes, (2 * (size_t)nk - 1) * sizeof(uint4)))
+		return false;
+	HIPCHECK(hipMemcpyAsync(d.rad_kept.p, kept.data(), (size_t)nk * 4, hipMemcpyHostToDevice, d.stream));
+	DevScene probe = S;
+	probe.n_seg = (uint32_t)d.shade_grid;   // the gather grid k_pregather shares pk_stack with
+	PROF(KK_PREGATHER, yafamd_pregather(&probe, (const float4 *)d.radc_a.p, (const float4 *)d.radc_b.p, (const float4 *)d.radc_c.p,
+	                                    (const uint32_t *)d.rad_kept.p, nk, (float4 *)d.rph_pos.p, (float4 *)d.rph_dir.p, (float *)d.rph_colb.p,
+	                                    d.stream));
+	int depth = 0;
+	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)d.rph_pos.p, nk, (uint4 *)d.rpk_nodes.p, &depth, d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	d.n_rphotons = (int)nk;
+	S.rph_pos = (const float4 *)d.rph_pos.p;
+	S.rph_dir = (const float4 *)d.rph_dir.p;
+	S.rph_colb = (const float *)d.rph_colb.p;
+	S.rpk_nodes = (const uint4 *)d.rpk_nodes.p;
 	return true;
 }
 
@@ -625,6 +753,9 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 		if(!ensure(log_, d.pk_stack, (size_t)d.pm_stack * yafamd_gather_lanes(&seg_probe) * sizeof(uint2))) return false;
 		S.pk_stack = (uint2 *)d.pk_stack.p;
 	}
+	S.fg_on = 0;
+	S.n_rphotons = 0;
+	if(S.integrator == INT_PHOTON && pm.final_gather && n > 0 && !buildRadianceMap(rp)) return false;
 	stats_.photons = n;
 	const auto t2 = std::chrono::steady_clock::now();
 	stats_.photon_seconds = std::chrono::duration<double>(t2 - t0).count();
@@ -653,6 +784,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	S.caus_map = 0;
 	S.gather_on = 0;
 	S.n_photons = 0;
+	S.fg_on = 0;
+	S.n_rphotons = 0;
 	if(S.integrator == INT_PHOTON || rp.pm.caustic_map)
 	{
 		// PhotonIntegrator::preprocess (integrator_photon_mapping.cc:242-638) / createCausticMap
@@ -926,6 +1059,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// tracing finishes paths in any iteration
 			const bool dl_pipeline = S.integrator != INT_PATH;
 			if(S.gather_on && (!dl_pipeline || it == 1))
+				if(S.fg_on)
+					PROF(KK_FG, yafamd_launch_fg(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 				PROF(KK_GATHER, yafamd_launch_gather(&S, &d.G, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 			// NEE requests (none in iteration 1 of photon mapping, whose entries all finish there)
 			if((S.ext || !yafamd_shade_fused()) && !(S.integrator == INT_PHOTON && it == 1))

@@ -50,6 +50,11 @@ struct PhotonParams
 	float radius2 = 0.1f;      // "diffuseRadius" (squared radius of the gather)
 	int bounces = 5;
 	int threads = -1;          // threads_photons: photon count rounded to a multiple (:437); <= 0 -> 1
+	// final gathering (integrator_photon_mapping.cc factory :777-810)
+	bool final_gather = false;
+	int fg_samples = 32;
+	int fg_bounces = 2;
+	float fg_min_pathlen = 0.1f;   // gather_dist_ (default diffuseRadius)
 };
 
 // adaptive anti-aliasing (scene.cc:582-595, aa_noise_params.h:27-46; TiledIntegrator::render,
@@ -69,13 +74,13 @@ struct AaParams
 enum KernelKind : int
 {
 	KK_CAMERA = 0, KK_TRACE, KK_SURFACE, KK_TSHADOW, KK_SHADE, KK_NEE, KK_GATHER, KK_SPAWN, KK_COMBINE, KK_FILM, KK_AA,
-	KK_PHOTON_EMIT, KK_PHOTON_BOUNCE, KK_PHOTON_COMPACT, KK_PHOTON_TREE, KK_COUNT
+	KK_PHOTON_EMIT, KK_PHOTON_BOUNCE, KK_PHOTON_COMPACT, KK_PHOTON_TREE, KK_FG, KK_PREGATHER, KK_COUNT
 };
 inline const char *kernelKindName(int k)
 {
 	static const char *n[KK_COUNT] = {"k_camera", "k_trace", "k_surface", "k_tshadow", "k_shade", "k_nee", "k_gather", "k_spawn",
 	                                  "k_combine", "k_film", "aa_next_pass", "k_photon_emit", "k_photon_bounce", "photon_compact",
-	                                  "pkd_build"};
+	                                  "pkd_build", "k_fg", "k_pregather"};
 	return (k >= 0 && k < KK_COUNT) ? n[k] : "";
 }
 struct KernelTimes
@@ -132,6 +137,7 @@ class GpuRenderer
 		bool filmToDevice(void *dst, int y0, int y1);
 		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
 		bool buildPhotonMap(RenderParams &rp);
+		bool buildRadianceMap(RenderParams &rp);
 		bool shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int bounces, int which, uint32_t &n_out, int &depth_out);
 
 		// ---- render group: the film split into contiguous row bands over several GPUs ----

@@ -156,7 +156,7 @@ class Render:
     aa_dark_threshold_factor: float = 0.0
     aa_variance_edge_size: int = 10
     aa_variance_pixels: int = 0
-    # photonmapping (integrator_photon_mapping.cc:765-850); final gathering is not supported
+    # photonmapping (integrator_photon_mapping.cc:765-850)
     pm_photons: int = 100000
     pm_search: int = 50
     pm_diffuse_radius: float = 0.1
@@ -167,6 +167,11 @@ class Render:
     caustic_radius: float = None            # PM "causticRadius" (0.01); DL / PT "caustic_radius" (0.25)
     caustic_depth: int = None               # DL / PT "caustic_depth" (10); PM uses "bounces"
     threads_photons: int = 1
+    # PhotonIntegrator final gathering (factory :777-810; the reference default is on)
+    pm_final_gather: bool = False
+    fg_samples: int = 32
+    fg_bounces: int = 2
+    fg_min_pathlen: float = None            # default: diffuseRadius
     # DirectLight ambient occlusion (integrator_direct_light.cc:161-186)
     do_ao: bool = False
     ao_samples: int = 32
@@ -609,7 +614,12 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetBool("caustics", r.pm_caustics)
         api.paramsSetInt("caustic_mix", cm.search)
         api.paramsSetFloat("causticRadius", cm.radius)
-        api.paramsSetBool("finalGather", False)
+        api.paramsSetBool("finalGather", bool(r.pm_final_gather))
+        if r.pm_final_gather:
+            api.paramsSetInt("fg_samples", r.fg_samples)
+            api.paramsSetInt("fg_bounces", r.fg_bounces)
+            if r.fg_min_pathlen is not None:
+                api.paramsSetFloat("fg_min_pathlen", r.fg_min_pathlen)
     if r.integrator == "directlighting" and r.pm_caustics:
         api.paramsSetBool("caustics", True)
     if r.integrator == "directlighting" and r.do_ao:

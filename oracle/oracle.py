@@ -90,7 +90,8 @@ class yc_render(C.Structure):
                 ("transp_shad", C.c_int), ("shadow_depth", C.c_int), ("do_ao", C.c_int), ("ao_samples", C.c_int),
                 ("ao_dist", C.c_float), ("ao_col", C.c_float * 3), ("aa_light_sample_multiplier_factor", C.c_float),
                 ("caus_map", C.c_int), ("caus_photons", C.c_int), ("caus_search", C.c_int), ("caus_depth", C.c_int),
-                ("caus_radius", C.c_float), ("tiles_order", C.c_int)]
+                ("caus_radius", C.c_float), ("tiles_order", C.c_int),
+                ("pm_fg", C.c_int), ("fg_samples", C.c_int), ("fg_bounces", C.c_int), ("fg_min_pathlen", C.c_float)]
 
 
 class yc_scene(C.Structure):
@@ -594,6 +595,9 @@ class OracleScene:
         rp.caus_map, rp.caus_photons, rp.caus_search = int(cm.enabled), cm.photons, cm.search
         rp.caus_depth, rp.caus_radius = cm.depth, cm.radius
         rp.tiles_order = {"linear": 0, "random": 2}.get(getattr(r, "tiles_order", "linear"), 1)
+        rp.pm_fg = int(r.integrator == "photonmapping" and r.pm_final_gather)
+        rp.fg_samples, rp.fg_bounces = r.fg_samples, r.fg_bounces
+        rp.fg_min_pathlen = r.fg_min_pathlen if r.fg_min_pathlen is not None else r.pm_diffuse_radius
         rp.aa_passes = max(1, r.aa_passes)
         rp.aa_inc_samples = r.aa_inc_samples if r.aa_inc_samples > 0 else r.aa_samples
         rp.aa_threshold, rp.aa_resampled_floor = r.aa_threshold, r.aa_resampled_floor
@@ -621,9 +625,10 @@ class OracleScene:
         return rgba.reshape(r.height, r.width, 4), w.reshape(r.height, r.width), (ctr.closest_rays, ctr.shadow_rays)
 
     def photon_map(self, which="diffuse"):
-        """(pos, dir, col [n x 3 each], kd nodes [m x 2 uint32], n_paths) of the diffuse or caustic map."""
+        """(pos, dir, col [n x 3 each], kd nodes [m x 2 uint32], n_paths) of the diffuse, caustic or
+        final-gather radiance map (dir = the radiance point's normal)."""
         L = oracle_lib()
-        w = 1 if which == "caustic" else 0
+        w = {"caustic": 1, "radiance": 2}.get(which, 0)
         n_paths = C.c_int(0)
         n = L.yc_photon_map_ex(C.byref(self.sc), w, None, None, None, None, C.byref(n_paths))
         if n < 0:

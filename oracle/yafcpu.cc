@@ -2107,6 +2107,37 @@ class Renderer
 		};
 		PhotonMapData dmap;   // diffuse map (PhotonIntegrator)
 		PhotonMapData cmap;   // caustic map (MonteCarloIntegrator::createCausticMap)
+		// final gathering: photon.h:91-99 RadData, and the radiance map of Photon(normal, pos,
+		// pre-gathered radiance) (integrator_photon_mapping.cc:80, 585-589)
+		struct RadData { V3 pos, normal; C3 refl, transm; };
+		std::vector<RadData> rad_points;
+		PhotonMapData rmap;
+
+		// :186 draws the global FastRandom (shared by the photon threads, so schedule-dependent)
+		// against 0.125; here a hash of the deposit slot (photon id, bounce) keeps one in eight, and
+		// the GPU uses the same hash (the radiance-point subset is matched statistically, like RR)
+		static bool fgRadSelect(uint32_t slot) { return (fnv32(slot ^ 0x6a09e667u) & 7u) == 0u; }
+
+		// material.cc:156-174 Material::getReflectivity
+		C3 getReflectivity(const SurfacePoint &sp, unsigned flags) const
+		{
+			if(!(flags & (BTransmit | BReflect) & sp.bsdf_flags)) return C3(0.f);
+			C3 total(0.f);
+			for(int i = 0; i < 16; ++i)
+			{
+				const float s_1 = 0.03125f + 0.0625f * static_cast<float>(i);
+				const float s_2 = riVdC((uint32_t)i);
+				const float s_3 = static_cast<float>(lowDiscrepancySampling(2, (uint32_t)i));
+				const float s_4 = static_cast<float>(lowDiscrepancySampling(3, (uint32_t)i));
+				const V3 wo = cosHemisphere(sp.n, sp.nu, sp.nv, s_1, s_2);
+				V3 wi;
+				Sample s(s_3, s_4, flags);
+				float w = 0.f;
+				const C3 col = sample(sp, wo, wi, s, w);
+				total += col * w;
+			}
+			return total * 0.0625f;
+		}
 
 		// include/sampler/sample_pdf1d.h:52-93 (cumulateStep1DDf + dSample)
 		struct Pdf1D
@@ -2218,6 +2249,7 @@ class Renderer
 			const yc_render &rp = sc_.rp;
 			PhotonMapData &M = dmap;
 			M.photons.clear();
+			rad_points.clear();
 			const std::vector<const Light *> lights = photonLights(false);
 			const int num_lights = (int)lights.size();
 			if(num_lights == 0 || rp.pm_photons <= 0) { M.n_paths = 0; return; }
@@ -2254,6 +2286,16 @@ class Renderer
 					if(sp.bsdf_flags & BDiffuse)
 					{
 						if(!caustic_photon) M.photons.push_back({sp.p, wi, pcol});
+						// :184-193 radiance point for final gathering (one deposit in eight)
+						if(rp.pm_fg && !caustic_photon && fgRadSelect(h * (uint32_t)(rp.pm_bounces + 1) + (uint32_t)n_bounces))
+						{
+							RadData rd;
+							rd.pos = sp.p;
+							rd.normal = faceForward(sp.ng, sp.n, wi);
+							rd.refl = getReflectivity(sp, BDiffuse | BGlossy | BReflect);
+							rd.transm = getReflectivity(sp, BDiffuse | BGlossy | BTransmit);
+							rad_points.push_back(rd);
+						}
 					}
 					if(n_bounces == rp.pm_bounces) break;
 					const int d_5 = 3 * n_bounces + 5;
@@ -2501,7 +2543,221 @@ class Renderer
 			return sum;
 		}
 
-		// integrator_photon_mapping.cc:852-1004 with finalGather = false, show_map = false
+		// :560-572: radiance points in shooting order; each kept point marks every point within the
+		// squared distance `maxrad` (strictly less, pkdtree.h:263-268) whose normal faces the same side
+		// (EliminatePhoton, photon.h:172-180) as unused, itself included — the kept set is the greedy
+		// one in index order whatever the lookup's visiting order.  A uniform grid of cell sqrt(maxrad)
+		// finds the candidates (the r_tree of the reference only serves this range query).
+		static std::vector<uint32_t> eliminateRadPoints(const std::vector<RadData> &pts, float maxrad)
+		{
+			std::vector<uint32_t> kept;
+			const size_t n = pts.size();
+			if(!n) return kept;
+			const double cell = std::sqrt((double)maxrad) * 1.0001 + 1e-30;
+			auto key = [&](const V3 &p, int dx, int dy, int dz) {
+				const int64_t x = (int64_t)std::floor(p.x / cell) + dx, y = (int64_t)std::floor(p.y / cell) + dy,
+				              z = (int64_t)std::floor(p.z / cell) + dz;
+				return (uint64_t)(x * 73856093) ^ (uint64_t)(y * 19349663) ^ (uint64_t)(z * 83492791);
+			};
+			std::unordered_map<uint64_t, std::vector<uint32_t>> grid;
+			for(uint32_t i = 0; i < n; ++i) grid[key(pts[i].pos, 0, 0, 0)].push_back(i);
+			std::vector<uint8_t> use(n, 1);
+			for(uint32_t i = 0; i < n; ++i)
+			{
+				if(!use[i]) continue;
+				kept.push_back(i);
+				const RadData &q = pts[i];
+				for(int dx = -1; dx <= 1; ++dx)
+					for(int dy = -1; dy <= 1; ++dy)
+						for(int dz = -1; dz <= 1; ++dz)
+						{
+							auto it = grid.find(key(q.pos, dx, dy, dz));
+							if(it == grid.end()) continue;
+							for(uint32_t j : it->second)
+							{
+								const V3 v = pts[j].pos - q.pos;
+								if(v.lengthSqr() < maxrad && dot(pts[j].normal, q.normal) > 0.f) use[j] = 0;
+							}
+						}
+			}
+			return kept;
+		}
+
+		// :540-591 + preGatherWorker (:39-88): the kept radiance points gather the diffuse map within
+		// diffuseRadius^2 (here the radius IS squared, unlike integrate()'s :954) and store
+		// Photon(normal, pos, sum) in the radiance map, whose tree updateTree builds (:589)
+		void buildRadianceMap()
+		{
+			const yc_render &rp = sc_.rp;
+			const std::vector<uint32_t> kept = eliminateRadPoints(rad_points, 0.01f * rp.pm_diffuse_radius);
+			const float ds_radius_2 = rp.pm_diffuse_radius * rp.pm_diffuse_radius;
+			const float i_scale = static_cast<float>(1.f / ((float)dmap.n_paths * num_pi));
+			rmap.photons.clear();
+			rmap.nodes.clear();
+			std::vector<Found> gathered((size_t)std::max(1, rp.pm_search));
+			for(uint32_t idx : kept)
+			{
+				const RadData &r = rad_points[idx];
+				float radius = ds_radius_2;
+				const int n_gathered = gather(dmap, r.pos, gathered.data(), (uint32_t)rp.pm_search, radius);
+				C3 sum(0.f);
+				if(n_gathered > 0)
+				{
+					const float scale = i_scale / radius;
+					for(int i = 0; i < n_gathered; ++i)
+					{
+						const Photon &ph = dmap.photons[gathered[i].photon];
+						if(dot(r.normal, ph.dir) > 0.f) sum += r.refl * scale * ph.col;
+						else sum += r.transm * scale * ph.col;
+					}
+				}
+				rmap.photons.push_back({r.pos, r.normal, sum});
+			}
+			rmap.n_paths = dmap.n_paths;
+			if(!rmap.photons.empty()) buildPhotonTree(rmap);
+		}
+
+		// photon.cc:136-142 findNearest: NearestPhoton (photon.h:159-169) over the non-recursive
+		// lookup — the last photon accepted (facing n, strictly closer than the shrinking radius)
+		static int findNearest(const PhotonMapData &M, const V3 &p, const V3 &n, float max_dist_squared)
+		{
+			if(!M.ready()) return -1;   // an empty radiance map has no tree (the reference would crash)
+			struct Stack { int node; float s; int axis; };
+			Stack stack[64];
+			int nearest = -1;
+			int curr = 0;
+			int sp = 1;
+			stack[sp].node = -1;
+			for(;;)
+			{
+				while(!M.nodes[curr].isLeaf())
+				{
+					const int axis = M.nodes[curr].axis();
+					const float split_val = M.nodes[curr].split();
+					int far_child;
+					if(p[axis] <= split_val) { far_child = (int)M.nodes[curr].right(); curr = curr + 1; }
+					else { far_child = curr + 1; curr = (int)M.nodes[curr].right(); }
+					++sp;
+					stack[sp].node = far_child;
+					stack[sp].axis = axis;
+					stack[sp].s = split_val;
+				}
+				const Photon &ph = M.photons[M.nodes[curr].data];
+				const V3 v = ph.pos - p;
+				float dist_2 = v.lengthSqr();
+				if(dist_2 < max_dist_squared)
+				{
+					if(dot(ph.dir, n) > 0.f) { nearest = (int)M.nodes[curr].data; max_dist_squared = dist_2; }
+				}
+				if(stack[sp].node < 0) return nearest;
+				int axis = stack[sp].axis;
+				dist_2 = p[axis] - stack[sp].s;
+				dist_2 *= dist_2;
+				while(dist_2 > max_dist_squared)
+				{
+					--sp;
+					if(stack[sp].node < 0) return nearest;
+					axis = stack[sp].axis;
+					dist_2 = p[axis] - stack[sp].s;
+					dist_2 *= dist_2;
+				}
+				curr = stack[sp].node;
+				--sp;
+			}
+		}
+
+		// :640-763 finalGathering, one ray division (no decorrelation) and indirect sample multiplier 1
+		// (AA_indirect_sample_multiplier_factor is refused with AA passes).  `mat_bsd_fs` (:682) is a
+		// reference into the first gather hit's MaterialData, which the next intersect() frees (:741):
+		// undefined from the second hit on; here it reads the current hit's flags (YafaRay's intent).
+		C3 finalGathering(Thread &th, const SurfacePoint &sp, const V3 &wo, uint32_t sample_idx, uint32_t offset) const
+		{
+			const yc_render &rp = sc_.rp;
+			const float lookup_rad = 4 * rp.pm_diffuse_radius * rp.pm_diffuse_radius;   // :245
+			C3 path_col(0.f);
+			float w = 0.f;
+			const int n_sampl = std::max(1, rp.fg_samples);
+			for(int i = 0; i < n_sampl; ++i)
+			{
+				C3 throughput(1.f);
+				float length = 0;
+				SurfacePoint hit = sp;
+				V3 pwo = wo;
+				Ray p_ray;
+				const unsigned offs = (unsigned)rp.fg_samples * sample_idx + offset + (unsigned)i;
+				C3 lcol(0.f), scol;
+				const float s_1 = riVdC(offs);
+				const float s_2 = static_cast<float>(lowDiscrepancySampling(2, offs));
+				Sample s(s_1, s_2, BDiffuse | BReflect | BTransmit);
+				scol = sample(hit, pwo, p_ray.dir, s, w);
+				scol *= w;
+				if(scol.isBlack()) continue;
+				p_ray.tmin = rp.ray_min_dist;
+				p_ray.tmax = -1.f;
+				p_ray.from = hit.p;
+				throughput = scol;
+				{
+					SurfacePoint nh;
+					if(!intersect(th, p_ray, nh)) continue;
+					hit = nh;
+				}
+				bool did_hit = true;
+				length = p_ray.tmax;
+				unsigned mat_bsd_fs = hit.bsdf_flags;
+				const bool has_spec = mat_bsd_fs & BSpecular;
+				bool caustic = false;
+				bool close = length < rp.fg_min_pathlen;
+				bool do_bounce = close || has_spec;
+				for(int depth = 0; depth < rp.fg_bounces && do_bounce; ++depth)
+				{
+					const int d_4 = 4 * depth;
+					pwo = -p_ray.dir;
+					if(mat_bsd_fs & BDiffuse)
+					{
+						if(close) lcol = estimateOneDirectLight(th, hit, pwo, sample_idx, offset);
+						else if(caustic)
+						{
+							const V3 sf = faceForward(hit.ng, hit.n, pwo);
+							const int nearest = findNearest(rmap, hit.p, sf, lookup_rad);
+							if(nearest >= 0) lcol = rmap.photons[nearest].col;
+						}
+						if(close || caustic)
+						{
+							if(mat_bsd_fs & BEmit) lcol += emit(hit, pwo);
+							path_col += lcol * throughput;
+						}
+					}
+					Sample sb(static_cast<float>(lowDiscrepancySampling(d_4 + 3, offs)), static_cast<float>(lowDiscrepancySampling(d_4 + 4, offs)),
+					          close ? BAll : (BSpecular | BReflect | BTransmit | BFilter));
+					scol = sample(hit, pwo, p_ray.dir, sb, w);
+					if(sb.pdf <= 1.0e-6f) { did_hit = false; break; }
+					scol *= w;
+					p_ray.tmin = rp.ray_min_dist;
+					p_ray.tmax = -1.f;
+					p_ray.from = hit.p;
+					throughput *= scol;
+					SurfacePoint nh;
+					if(!intersect(th, p_ray, nh)) { did_hit = false; break; }
+					hit = nh;
+					mat_bsd_fs = hit.bsdf_flags;
+					length += p_ray.tmax;
+					caustic = (caustic || !depth) && (sb.sampled_flags & (BSpecular | BFilter));
+					close = length < rp.fg_min_pathlen;
+					do_bounce = caustic || close;
+				}
+				if(did_hit && (mat_bsd_fs & (BDiffuse | BGlossy)))
+				{
+					const V3 sf = faceForward(hit.ng, hit.n, -p_ray.dir);
+					const int nearest = findNearest(rmap, hit.p, sf, lookup_rad);
+					if(nearest >= 0) lcol = rmap.photons[nearest].col;
+					if(mat_bsd_fs & BEmit) lcol += emit(hit, -p_ray.dir);
+					path_col += lcol * throughput;
+				}
+			}
+			return path_col / (float)n_sampl;
+		}
+
+		// integrator_photon_mapping.cc:852-1004 (show_map = false)
 		void integratePhoton(Thread &th, Ray &ray, Mwc &rng, uint32_t sample_idx, uint32_t offset, C3 &col, float &alpha, int ray_level = 0,
 		                     int additional_depth = 0) const
 		{
@@ -2515,6 +2771,18 @@ class Renderer
 				const unsigned mat_bsdfs = sp.bsdf_flags;
 				additional_depth = std::max(additional_depth, sp.mat->additional_depth);   // :863
 				col += emit(sp, wo);                                   // :868-869
+				if(rp.pm_fg)
+				{
+					// :874-917 (use_photon_diffuse_ && final_gather_), clamp_indirect = 0
+					if(mat_bsdfs & BEmit) col += emit(sp, wo);         // :895-903
+					if(mat_bsdfs & BDiffuse)
+					{
+						col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
+						col += finalGathering(th, sp, wo, sample_idx, offset);
+					}
+				}
+				else
+				{
 				if(mat_bsdfs & BEmit) col += emit(sp, wo);             // :938-946 (added a second time)
 				if(mat_bsdfs & BDiffuse) col += estimateAllDirectLight(th, sp, wo, sample_idx, offset);
 				std::vector<Found> gathered((size_t)std::max(1, rp.pm_search));
@@ -2531,6 +2799,7 @@ class Renderer
 						const C3 col_tmp = surf_col * scale * ph.col;
 						col += col_tmp;
 					}
+				}
 				}
 				if(rp.caus_map && (mat_bsdfs & BDiffuse)) col += causticPhotons(sp, wo);   // :981-984
 				C3 rcol;
@@ -2554,6 +2823,7 @@ class Renderer
 			shootDiffusePhotons(th);
 			if(dmap.photons.size() < 50) return false;   // :448-452 "Too few diffuse photons"
 			buildPhotonTree(dmap);
+			if(sc_.rp.pm_fg) buildRadianceMap();
 			return true;
 		}
 
@@ -3120,13 +3390,13 @@ int yc_tiles(int w, int h, int bs, int order, int *out, int cap)
 	return n;
 }
 
-// which: 0 the diffuse map (PhotonIntegrator), 1 the caustic map
+// which: 0 the diffuse map (PhotonIntegrator), 1 the caustic map, 2 the final-gather radiance map
 int yc_photon_map_ex(const yc_scene *s, int which, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths)
 {
 	Scene sc(*s);
 	Renderer R(sc);
 	if(!R.preprocessPhotons()) return -1;
-	const auto &M = which == 1 ? R.cmap : R.dmap;
+	const auto &M = which == 1 ? R.cmap : which == 2 ? R.rmap : R.dmap;
 	const size_t n = M.photons.size();
 	if(n_paths) *n_paths = M.n_paths;
 	for(size_t i = 0; i < n; ++i)

@@ -169,6 +169,11 @@ typedef struct {
 	int caus_photons, caus_search, caus_depth;
 	float caus_radius;
 	int tiles_order;          // 0 linear, 1 centre (the reference default), 2 random (fixed seed)
+	// PhotonIntegrator final gathering (integrator_photon_mapping.cc:39-88, 183-193, 540-591, 640-763,
+	// 874-917; factory :777-810): finalGather, fg_samples, fg_bounces, fg_min_pathlen
+	int pm_fg;
+	int fg_samples, fg_bounces;
+	float fg_min_pathlen;
 } yc_render;
 
 typedef struct {

@@ -1,0 +1,116 @@
+"""PhotonIntegrator final gathering (finalGather = true, the reference's default):
+integrator_photon_mapping.cc:183-193 (radiance points while shooting the diffuse map), :540-591
+(thinning with EliminatePhoton over a point kd-tree, pre-gathering, the radiance map's tree),
+:39-88 (preGatherWorker), :640-763 (finalGathering), :874-917 (integrate with final gathering);
+photon.cc:136-142 (findNearest).
+
+GPU: radiance points in k_photon_bounce, compaction, host thinning, k_pregather, the radiance map's
+point kd-tree (pkd.hip), k_fg (gather paths traced in place, estimateOneDirectLight with in-place
+shadow rays, radiance-map lookups) before k_gather.  Compared with the oracle restatement
+(oracle/yafcpu.cc finalGathering / buildRadianceMap): per value <= 4 ULP, weights equal.
+
+The radiance-point subset is drawn by the reference from the global FastRandom shared by the photon
+threads (:186, schedule-dependent); both sides here keep the deposits whose slot hash selects one
+in eight (fgRadSelect), so the radiance map is matched to the reference statistically, like RR.
+"""
+import dataclasses
+
+import numpy as np
+import pytest
+
+from libyafaray_amd import scenes
+
+ULP_TOL = 4
+
+
+def ulp_diff(a, b):
+    a = np.ascontiguousarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.ascontiguousarray(b, np.float32).view(np.int32).astype(np.int64)
+    a = np.where(a < 0, -(a & 0x7fffffff), a)
+    b = np.where(b < 0, -(b & 0x7fffffff), b)
+    return np.abs(a - b)
+
+
+def fg_spec(W=48, H=36, spp=1, photons=20000, specular=False, **kw):
+    if specular:
+        s = scenes.cornell_specular(W, H, spp=spp, integrator="photonmapping", raydepth=3)
+        r = dataclasses.replace(s.render, pm_photons=photons, pm_search=50, pm_diffuse_radius=0.1, pm_bounces=5,
+                                pm_caustics=False)
+        s = dataclasses.replace(s, render=r)
+    else:
+        s = scenes.cornell_photon(W, H, spp=spp, photons=photons, search=50, radius=0.1)
+    fg = dict(pm_final_gather=True, fg_samples=8)
+    fg.update(kw)
+    return dataclasses.replace(s, render=dataclasses.replace(s.render, **fg))
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU: the oracle restatement
+# ---------------------------------------------------------------------------------------------
+def test_oracle_radiance_map(oracle_built):
+    spec = fg_spec(16, 12, photons=20000)
+    o = oracle_built.OracleScene(spec, threads=4)
+    dpos, _, _, _, n_paths = o.photon_map("diffuse")
+    rpos, rn, rcol, nodes, rpaths = o.photon_map("radiance")
+    assert rpaths == n_paths
+    # one deposit in eight becomes a radiance point, and thinning removes some of them
+    assert 0 < len(rpos) < len(dpos) / 8 * 1.2
+    assert np.allclose(np.linalg.norm(rn, axis=1), 1.0, atol=1e-3)
+    assert np.all(np.isfinite(rcol)) and np.all(rcol >= 0) and rcol.max() > 0
+    # the kept points are pairwise "far" in the EliminatePhoton sense: no later kept point lies within
+    # the squared distance 0.01 * diffuseRadius of an earlier one with a normal on the same side
+    maxrad = np.float32(0.01) * np.float32(0.1)
+    for i in range(len(rpos)):
+        d2 = ((rpos[i + 1:] - rpos[i]) ** 2).sum(1)
+        same = (rn[i + 1:] * rn[i]).sum(1) > 0
+        assert not np.any((d2 < maxrad) & same)
+    # every point is a leaf of the radiance map's tree exactly once
+    leaves = nodes[(nodes[:, 1] & 3) == 3, 0]
+    assert sorted(leaves.tolist()) == list(range(len(rpos)))
+
+
+def test_oracle_final_gather_deterministic_and_indirect(oracle_built):
+    spec = fg_spec(20, 14, spp=1, photons=8000, fg_samples=4)
+    a, wa, _ = oracle_built.OracleScene(spec, threads=1).render()
+    b, wb, _ = oracle_built.OracleScene(spec, threads=6).render()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    # final gathering adds indirect light on top of the direct light everywhere on the walls
+    dl_spec = dataclasses.replace(spec, render=dataclasses.replace(spec.render, integrator="directlighting", pm_final_gather=False))
+    dl, _, _ = oracle_built.OracleScene(dl_spec, threads=4).render()
+    assert (a[..., :3] >= dl[..., :3] - 1e-6).all() and a[..., :3].mean() > 1.1 * dl[..., :3].mean()
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: the HIP path against the oracle
+# ---------------------------------------------------------------------------------------------
+def compare(product, oracle_built, spec):
+    rgba, w, st = product.render_spec(spec)
+    o = oracle_built.OracleScene(spec, threads=8)
+    orgba, ow, _ = o.render()
+    dpos, *_ = o.photon_map("diffuse")
+    assert st["photons"] == len(dpos)
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32)), "film weights differ"
+    u = ulp_diff(rgba, orgba)
+    assert u.max() <= ULP_TOL, (f"{(u > ULP_TOL).sum()} values > {ULP_TOL} ULP, max {u.max()} at "
+                                f"{np.unravel_index(u.argmax(), u.shape)}: {rgba.reshape(-1)[u.argmax()]} vs {orgba.reshape(-1)[u.argmax()]}")
+    return rgba
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(), dict(fg_bounces=0), dict(fg_min_pathlen=0.8, fg_bounces=3), dict(fg_samples=3, spp=2)],
+                         ids=["default", "bounces0", "close-paths", "spp2"])
+def test_final_gather_matches_oracle(product, oracle_built, kw):
+    compare(product, oracle_built, fg_spec(**kw))
+
+
+@pytest.mark.gpu
+def test_final_gather_specular_matches_oracle(product, oracle_built):
+    """Mirror and transparent surfaces: gather paths that bounce specularly (caustic gather paths
+    look the radiance map up inside the loop) and recursiveRaytrace nodes that final-gather again."""
+    compare(product, oracle_built, fg_spec(specular=True, fg_min_pathlen=0.3))
+
+
+@pytest.mark.gpu
+def test_final_gather_off_is_unchanged(product, oracle_built):
+    spec = fg_spec(pm_final_gather=False)
+    compare(product, oracle_built, spec)
