@@ -20,6 +20,7 @@ Prints ONE JSON line (rank 0).  Extra keys:
   * cpu_baseline                      the oracle restatement on this host's cores, bounded band
 """
 import argparse
+import dataclasses
 import json
 import os
 import platform
@@ -50,6 +51,7 @@ def parse():
     ap.add_argument("--no-rr", action="store_true", help="Russian roulette off (bit-parity variant)")
     ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere", "photon"])
     ap.add_argument("--photons", type=int, default=10_000_000, help="C5: diffuse photons")
+    ap.add_argument("--fg", type=int, default=0, help="C5 variant: PhotonIntegrator final gathering with this many fg_samples (0: off, as C5)")
     ap.add_argument("--chunk", type=int, default=1 << 26)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -60,7 +62,8 @@ def parse():
 
 def workload_name(a, W, H):
     if a.scene == "photon":
-        return (f"C5 Cornell PhotonIntegrator, {a.photons} diffuse photons, k=50 gather r^2=0.1, finalGather off, "
+        fg = f"finalGather on ({a.fg} fg_samples, fg_bounces 2)" if a.fg else "finalGather off"
+        return (f"C5 Cornell PhotonIntegrator, {a.photons} diffuse photons, k=50 gather r^2=0.1, {fg}, "
                 f"{W}x{H}x{a.spp}spp (photon map rebuilt every step)")
     return (f"C2 Cornell PathIntegrator depth {a.bounces}, {W}x{H}x{a.spp}spp"
             + (", RR off" if a.no_rr else ", RR on (reference default)")
@@ -70,7 +73,7 @@ def workload_name(a, W, H):
 def pmc_config(a, W, H):
     """Key of profiles/pmc_<key>.json (tools/pmc_all.sh): one workload, one kernel source."""
     return f"{a.scene}-{W}x{H}x{a.spp}-b{a.bounces}-rr{int(not a.no_rr)}-chunk{a.chunk}" + (
-        f"-ph{a.photons}" if a.scene == "photon" else "")
+        f"-ph{a.photons}" if a.scene == "photon" else "") + (f"-fg{a.fg}" if a.scene == "photon" and a.fg else "")
 
 
 def kernels_src_sha1():
@@ -148,6 +151,8 @@ def main():
         spec = scenes.cornell_sphere(width=a.width, height=a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
     elif a.scene == "photon":
         spec = scenes.cornell_photon(a.width, a.height, spp=a.spp, photons=a.photons)
+        if a.fg:
+            spec = dataclasses.replace(spec, render=dataclasses.replace(spec.render, pm_final_gather=True, fg_samples=a.fg))
     else:
         spec = scenes.cornell(a.width, a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
     yi = Y.Interface()
@@ -233,7 +238,11 @@ def main():
             "kernels": kernels,
             "kernel_ms_per_step": round(frame_ms, 3),
             "photon_map": ({"photons_stored": s["photons"], "seconds_per_step": round(s["photon_seconds"], 4),
-                            "shoot_seconds": round(s["photon_shoot_seconds"], 4), "tree_seconds": round(s["photon_tree_seconds"], 4)}
+                            "shoot_seconds": round(s["photon_shoot_seconds"], 4), "tree_seconds": round(s["photon_tree_seconds"], 4),
+                            **({"radiance_points": s["radiance_points"], "radiance_photons": s["radiance_photons"],
+                                "fg_thin_seconds": round(s["fg_thin_seconds"], 4), "fg_radiance_seconds": round(s["fg_radiance_seconds"], 4),
+                                "fg_thin_rounds": s["fg_thin_rounds"]}
+                               if a.fg else {})}
                            if a.scene == "photon" else None),
             "launch": {k: s[k] for k in ("trace_grid", "shade_grid", "trace_block", "stack_depth", "scene_in_lds", "bvh_nodes")},
             # accelerator build + scene upload, once before the timed region (the reference builds

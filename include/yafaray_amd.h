@@ -47,6 +47,11 @@ typedef struct
 	double photon_shoot_seconds, photon_tree_seconds;
 	uint64_t gather_visits;     /* point kd-tree nodes fetched by the photon density estimates */
 	uint64_t caustic_photons;   /* photons stored in the caustic photon map (0: none / disabled) */
+	uint64_t radiance_points;   /* final gathering: radiance points picked while shooting */
+	uint64_t radiance_photons;  /* final gathering: points kept (thinned) in the radiance map */
+	double fg_thin_seconds;     /* final gathering: radiance-point thinning (host) incl. their download */
+	double fg_radiance_seconds; /* final gathering: radiance map total (thinning, pre-gather, kd-tree) */
+	int64_t fg_thin_rounds;     /* final gathering: GPU thinning rounds (-1: thinned on the host) */
 } yafaray_amd_stats_t;
 
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */

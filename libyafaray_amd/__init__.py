@@ -39,7 +39,8 @@ class Stats(C.Structure):
                 ("trace_block", C.c_uint32), ("stack_depth", C.c_uint32), ("shade_kernel_ms", C.c_double),
                 ("nee_kernel_ms", C.c_double), ("photons", C.c_uint64), ("photon_seconds", C.c_double),
                 ("photon_shoot_seconds", C.c_double), ("photon_tree_seconds", C.c_double), ("gather_visits", C.c_uint64),
-                ("caustic_photons", C.c_uint64)]
+                ("caustic_photons", C.c_uint64), ("radiance_points", C.c_uint64), ("radiance_photons", C.c_uint64),
+                ("fg_thin_seconds", C.c_double), ("fg_radiance_seconds", C.c_double), ("fg_thin_rounds", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

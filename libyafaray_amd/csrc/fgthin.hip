@@ -1,0 +1,285 @@
+// Final gathering's radiance-point thinning on the GPU (reference integrator_photon_mapping.cc:560-572).
+//
+// The reference walks the radiance points in shooting order; a point still in use is kept and, by a
+// range lookup in a point kd-tree (EliminatePhoton, photon.h:172-180), marks every point within the
+// squared distance maxrad (strictly less) whose normal faces the same side as unused — itself
+// included.  The kept set is the lexicographically-first maximal independent set of the graph
+// "within maxrad and normals on the same side" (the relation is symmetric bit for bit: (a - b)^2 =
+// (b - a)^2 and the dot products commute), so it can be decided in rounds without the serial walk:
+//
+//   round r: an undecided point none of whose lower-index neighbours is undecided is kept (snapshot
+//            of the states, two buffers); then every point kept in this round marks its higher-index
+//            neighbours dead, as the reference's lookup from a kept point does
+//
+// The lowest undecided point is always kept, so the rounds end; in practice ~15 rounds decide
+// millions of points (C5: 2.46 M points, 16 K kept).  Neighbours come from a dense uniform grid of cell > sqrt(maxrad) (counting sort by
+// cell); the kept indices are compacted in shooting order.  Host twin: render.cc eliminateRadPoints.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+namespace
+{
+
+struct ThinBuf
+{
+	void *p = nullptr;
+	size_t bytes = 0;
+	template<class T> T *as() { return reinterpret_cast<T *>(p); }
+	hipError_t ensure(size_t b)
+	{
+		if(b < 16) b = 16;
+		if(p && bytes >= b) return hipSuccess;
+		if(p) (void)hipFree(p);
+		p = nullptr;
+		bytes = 0;
+		const hipError_t e = hipMalloc(&p, b);
+		if(e == hipSuccess) bytes = b;
+		return e;
+	}
+};
+
+// scratch kept between renders (the radiance map is rebuilt every frame)
+struct ThinScratch
+{
+	ThinBuf part, cid, count, start, order, st0, st1, counter, tmp, n_sel;
+} g_thin;
+
+constexpr int kBoundBlocks = 256;
+constexpr uint8_t kUndecided = 0, kKept = 1, kDead = 2;
+
+struct ThinGrid
+{
+	double lo[3];
+	double inv_cell;
+	int nx, ny, nz;
+};
+
+__device__ __forceinline__ int axisCell(float v, double lo, double inv_cell, int na)
+{
+	const int c = (int)floor(((double)v - lo) * inv_cell);
+	return c < 0 ? 0 : (c >= na ? na - 1 : c);
+}
+
+__global__ void __launch_bounds__(256) k_thin_bound(const float4 *pos, uint32_t n, float4 *part)
+{
+	float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+	for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+	{
+		const float4 p = pos[i];
+		lo[0] = fminf(lo[0], p.x); lo[1] = fminf(lo[1], p.y); lo[2] = fminf(lo[2], p.z);
+		hi[0] = fmaxf(hi[0], p.x); hi[1] = fmaxf(hi[1], p.y); hi[2] = fmaxf(hi[2], p.z);
+	}
+	__shared__ float s[6][256];
+	for(int a = 0; a < 3; ++a) { s[a][threadIdx.x] = lo[a]; s[3 + a][threadIdx.x] = hi[a]; }
+	__syncthreads();
+	for(int off = 128; off > 0; off >>= 1)
+	{
+		if((int)threadIdx.x < off)
+			for(int a = 0; a < 3; ++a)
+			{
+				s[a][threadIdx.x] = fminf(s[a][threadIdx.x], s[a][threadIdx.x + off]);
+				s[3 + a][threadIdx.x] = fmaxf(s[3 + a][threadIdx.x], s[3 + a][threadIdx.x + off]);
+			}
+		__syncthreads();
+	}
+	if(threadIdx.x == 0)
+	{
+		part[2 * blockIdx.x] = make_float4(s[0][0], s[1][0], s[2][0], 0.f);
+		part[2 * blockIdx.x + 1] = make_float4(s[3][0], s[4][0], s[5][0], 0.f);
+	}
+}
+
+__global__ void __launch_bounds__(256) k_thin_cells(const float4 *pos, uint32_t n, ThinGrid g, uint32_t *cid, uint32_t *count)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const float4 p = pos[i];
+	const int cx = axisCell(p.x, g.lo[0], g.inv_cell, g.nx), cy = axisCell(p.y, g.lo[1], g.inv_cell, g.ny),
+	          cz = axisCell(p.z, g.lo[2], g.inv_cell, g.nz);
+	const uint32_t c = (uint32_t)((cz * g.ny + cy) * g.nx + cx);
+	cid[i] = c;
+	atomicAdd(&count[c], 1u);
+}
+
+__global__ void __launch_bounds__(256) k_thin_fill(const uint32_t *cid, uint32_t n, const uint32_t *start, uint32_t *fill, uint32_t *order)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const uint32_t c = cid[i];
+	order[start[c] + atomicAdd(&fill[c], 1u)] = i;   // order inside a cell is irrelevant (marking is idempotent)
+}
+
+// neighbour cells of a point (clamped 3x3x3 block) — the relation's reach is < one cell per axis
+#define THIN_FOR_CELLS(q)                                                                                      \
+	const int cx_ = axisCell(q.x, g.lo[0], g.inv_cell, g.nx), cy_ = axisCell(q.y, g.lo[1], g.inv_cell, g.ny),   \
+	          cz_ = axisCell(q.z, g.lo[2], g.inv_cell, g.nz);                                                    \
+	for(int z = max(0, cz_ - 1); z <= min(g.nz - 1, cz_ + 1) && !stop; ++z)                                     \
+		for(int y = max(0, cy_ - 1); y <= min(g.ny - 1, cy_ + 1) && !stop; ++y)                                 \
+			for(int x = max(0, cx_ - 1); x <= min(g.nx - 1, cx_ + 1) && !stop; ++x)
+
+// EliminatePhoton's test (pkdtree.h:263-268 strict distance, photon.h:177 normals on one side),
+// symmetric bit for bit in the two points
+__device__ __forceinline__ bool thinRelated(const float4 &p, const float4 &pn, const float4 &q, const float4 &qn, float maxrad)
+{
+	const float vx = p.x - q.x, vy = p.y - q.y, vz = p.z - q.z;
+	const float d2 = vx * vx + vy * vy + vz * vz;
+	const float nd = pn.x * qn.x + pn.y * qn.y + pn.z * qn.z;
+	return d2 < maxrad && nd > 0.f;
+}
+
+// round, part 1: an undecided point none of whose lower-index related points is undecided (in the
+// snapshot `sin`) is kept; the kept points of earlier rounds have already killed their related
+// higher points (part 2), so the dead ones are skipped and the scan stops at the first undecided one
+__global__ void __launch_bounds__(256) k_thin_keep(const float4 *pos, const float4 *nrm, const uint32_t *order, const uint32_t *start,
+                                                  ThinGrid g, const uint8_t *sin, uint8_t *sout, uint32_t n, float maxrad)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const uint8_t s0 = sin[i];
+	if(s0 != kUndecided) { sout[i] = s0; return; }
+	const float4 q = pos[i], qn = nrm[i];
+	bool stop = false;
+	THIN_FOR_CELLS(q)
+	{
+		const uint32_t c = (uint32_t)((z * g.ny + y) * g.nx + x);
+		const uint32_t k1 = start[c + 1];
+		for(uint32_t k = start[c]; k < k1; ++k)
+		{
+			const uint32_t j = order[k];
+			if(j >= i || sin[j] != kUndecided) continue;
+			if(thinRelated(pos[j], nrm[j], q, qn, maxrad)) { stop = true; break; }
+		}
+	}
+	sout[i] = stop ? kUndecided : kKept;
+}
+
+// round, part 2: every point kept in this round marks its related higher points dead (the
+// reference's EliminatePhoton lookup from a kept point); none of them can have been kept in part 1
+// (it saw this point undecided below it)
+__global__ void __launch_bounds__(256) k_thin_kill(const float4 *pos, const float4 *nrm, const uint32_t *order, const uint32_t *start,
+                                                  ThinGrid g, const uint8_t *sin, uint8_t *sout, uint32_t n, float maxrad)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n || sin[i] != kUndecided || sout[i] != kKept) return;
+	const float4 q = pos[i], qn = nrm[i];
+	bool stop = false;
+	THIN_FOR_CELLS(q)
+	{
+		const uint32_t c = (uint32_t)((z * g.ny + y) * g.nx + x);
+		const uint32_t k1 = start[c + 1];
+		for(uint32_t k = start[c]; k < k1; ++k)
+		{
+			const uint32_t j = order[k];
+			if(j <= i) continue;
+			if(thinRelated(pos[j], nrm[j], q, qn, maxrad)) sout[j] = kDead;
+		}
+	}
+}
+
+__global__ void __launch_bounds__(256) k_thin_count(const uint8_t *st, uint32_t n, uint32_t *n_undecided)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const bool u = i < n && st[i] == kUndecided;
+	const uint64_t m = __ballot(u);
+	if(m && __lane_id() == 0) atomicAdd(n_undecided, (uint32_t)__popcll(m));
+}
+
+struct IsKept
+{
+	const uint8_t *st;
+	__host__ __device__ bool operator()(uint32_t i) const { return st[i] == kKept; }
+};
+
+} // namespace
+
+#define THCHECK(x)                                                                                             \
+	do                                                                                                         \
+	{                                                                                                          \
+		const hipError_t e_ = (x);                                                                             \
+		if(e_ != hipSuccess) return e_;                                                                        \
+	} while(0)
+
+// pos / nrm: the compacted radiance points (xyz used); kept_out: device, n entries of capacity.
+// Returns hipErrorNotSupported when the dense grid would exceed 2^26 cells (the caller thins on the
+// host then).
+extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out,
+                                             uint32_t *n_kept, int *rounds_out, hipStream_t st)
+{
+	*n_kept = 0;
+	*rounds_out = 0;
+	if(n == 0) return hipSuccess;
+	ThinScratch &S = g_thin;
+	THCHECK(S.part.ensure(2 * kBoundBlocks * sizeof(float4)));
+	hipLaunchKernelGGL(k_thin_bound, dim3(kBoundBlocks), dim3(256), 0, st, pos, n, S.part.as<float4>());
+	std::vector<float4> part(2 * kBoundBlocks);
+	THCHECK(hipMemcpyAsync(part.data(), S.part.p, part.size() * sizeof(float4), hipMemcpyDeviceToHost, st));
+	THCHECK(hipStreamSynchronize(st));
+	double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+	for(int b = 0; b < kBoundBlocks; ++b)
+	{
+		const float4 l = part[2 * b], h = part[2 * b + 1];
+		lo[0] = std::min(lo[0], (double)l.x); lo[1] = std::min(lo[1], (double)l.y); lo[2] = std::min(lo[2], (double)l.z);
+		hi[0] = std::max(hi[0], (double)h.x); hi[1] = std::max(hi[1], (double)h.y); hi[2] = std::max(hi[2], (double)h.z);
+	}
+	// cell a little larger than sqrt(maxrad): two points closer than that differ by <= 1 cell per axis
+	const double cell = std::sqrt((double)maxrad) * 1.001 + 1e-30;
+	double dims[3], ncell = 1.0;
+	for(int a = 0; a < 3; ++a) { dims[a] = std::floor((hi[a] - lo[a]) / cell) + 1.0; ncell *= dims[a]; }
+	if(!(ncell <= (double)(1 << 26))) return hipErrorNotSupported;
+	ThinGrid g;
+	for(int a = 0; a < 3; ++a) g.lo[a] = lo[a];
+	g.inv_cell = 1.0 / cell;
+	g.nx = (int)dims[0];
+	g.ny = (int)dims[1];
+	g.nz = (int)dims[2];
+	const uint32_t nc = (uint32_t)ncell;
+	THCHECK(S.cid.ensure((size_t)n * 4));
+	THCHECK(S.order.ensure((size_t)n * 4));
+	THCHECK(S.count.ensure(((size_t)nc + 1) * 4));
+	THCHECK(S.start.ensure(((size_t)nc + 1) * 4));
+	THCHECK(S.st0.ensure(n));
+	THCHECK(S.st1.ensure(n));
+	THCHECK(S.counter.ensure(16));
+	THCHECK(S.n_sel.ensure(16));
+	THCHECK(hipMemsetAsync(S.count.p, 0, ((size_t)nc + 1) * 4, st));
+	const dim3 blocks((n + 255) / 256);
+	hipLaunchKernelGGL(k_thin_cells, blocks, dim3(256), 0, st, pos, n, g, S.cid.as<uint32_t>(), S.count.as<uint32_t>());
+	size_t scan_bytes = 0;
+	THCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, S.count.as<uint32_t>(), S.start.as<uint32_t>(), (int)nc + 1, st));
+	size_t sel_bytes = 0;
+	hipcub::CountingInputIterator<uint32_t> iota(0);
+	hipcub::TransformInputIterator<bool, IsKept, hipcub::CountingInputIterator<uint32_t>> flags(iota, IsKept{S.st0.as<uint8_t>()});
+	THCHECK(hipcub::DeviceSelect::Flagged(nullptr, sel_bytes, iota, flags, kept_out, S.n_sel.as<uint32_t>(), (int)n, st));
+	THCHECK(S.tmp.ensure(std::max(scan_bytes, sel_bytes)));
+	THCHECK(hipcub::DeviceScan::ExclusiveSum(S.tmp.p, scan_bytes, S.count.as<uint32_t>(), S.start.as<uint32_t>(), (int)nc + 1, st));
+	THCHECK(hipMemsetAsync(S.count.p, 0, ((size_t)nc + 1) * 4, st));
+	hipLaunchKernelGGL(k_thin_fill, blocks, dim3(256), 0, st, S.cid.as<uint32_t>(), n, S.start.as<uint32_t>(), S.count.as<uint32_t>(),
+	                   S.order.as<uint32_t>());
+	THCHECK(hipMemsetAsync(S.st0.p, kUndecided, n, st));
+	uint8_t *sin = S.st0.as<uint8_t>(), *sout = S.st1.as<uint8_t>();
+	uint32_t undecided = n;
+	int rounds = 0;
+	while(undecided > 0)
+	{
+		THCHECK(hipMemsetAsync(S.counter.p, 0, 4, st));
+		hipLaunchKernelGGL(k_thin_keep, blocks, dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad);
+		hipLaunchKernelGGL(k_thin_kill, blocks, dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad);
+		hipLaunchKernelGGL(k_thin_count, blocks, dim3(256), 0, st, sout, n, S.counter.as<uint32_t>());
+		THCHECK(hipGetLastError());
+		THCHECK(hipMemcpyAsync(&undecided, S.counter.p, 4, hipMemcpyDeviceToHost, st));
+		THCHECK(hipStreamSynchronize(st));
+		std::swap(sin, sout);
+		++rounds;
+		if(rounds > 1000000) return hipErrorUnknown;   // cannot happen: every round decides the lowest undecided point
+	}
+	// the final states are in `sin`: kept indices in shooting order
+	hipcub::TransformInputIterator<bool, IsKept, hipcub::CountingInputIterator<uint32_t>> kflags(iota, IsKept{sin});
+	THCHECK(hipcub::DeviceSelect::Flagged(S.tmp.p, sel_bytes, iota, kflags, kept_out, S.n_sel.as<uint32_t>(), (int)n, st));
+	THCHECK(hipMemcpyAsync(n_kept, S.n_sel.p, 4, hipMemcpyDeviceToHost, st));
+	THCHECK(hipStreamSynchronize(st));
+	*rounds_out = rounds;
+	return hipSuccess;
+}

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <future>
 #include <mutex>
@@ -52,6 +53,8 @@ hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *
                               float4 *c, hipStream_t st);
 hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
                             float4 *out_pos, float4 *out_dir, float *out_colb, hipStream_t st);
+hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out, uint32_t *n_kept,
+                                  int *rounds_out, hipStream_t st);
 hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid,
                             hipStream_t st);
 size_t yafamd_gather_lanes(const DevScene *S);
@@ -119,6 +122,61 @@ std::vector<uint32_t> eliminateRadPoints(const std::vector<float4> &pos, const s
 	const size_t n = pos.size();
 	if(!n) return kept;
 	const double cell = std::sqrt((double)maxrad) * 1.0001 + 1e-30;
+	// dense grid over the points' bound (counting sort, O(n)) when it has at most 2^24 cells
+	double lo[3] = {pos[0].x, pos[0].y, pos[0].z}, hi[3] = {lo[0], lo[1], lo[2]};
+	for(size_t i = 1; i < n; ++i)
+	{
+		const double v[3] = {pos[i].x, pos[i].y, pos[i].z};
+		for(int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], v[a]); hi[a] = std::max(hi[a], v[a]); }
+	}
+	double dims[3];
+	double ncell_d = 1.0;
+	for(int a = 0; a < 3; ++a) { dims[a] = std::floor((hi[a] - lo[a]) / cell) + 1.0; ncell_d *= dims[a]; }
+	if(ncell_d <= (double)(1 << 24))
+	{
+		const int64_t nx = (int64_t)dims[0], ny = (int64_t)dims[1], nz = (int64_t)dims[2];
+		auto axisCell = [&](double v, int a, int64_t na) {
+			int64_t c = (int64_t)std::floor((v - lo[a]) / cell);
+			return c < 0 ? 0 : (c >= na ? na - 1 : c);
+		};
+		std::vector<uint32_t> cid(n), start((size_t)(nx * ny * nz) + 1, 0), order(n);
+		for(size_t i = 0; i < n; ++i)
+		{
+			const int64_t cx = axisCell(pos[i].x, 0, nx), cy = axisCell(pos[i].y, 1, ny), cz = axisCell(pos[i].z, 2, nz);
+			cid[i] = (uint32_t)((cz * ny + cy) * nx + cx);
+			++start[cid[i] + 1];
+		}
+		for(size_t c = 1; c < start.size(); ++c) start[c] += start[c - 1];
+		{
+			std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+			for(uint32_t i = 0; i < n; ++i) order[fill[cid[i]]++] = i;
+		}
+		std::vector<uint8_t> use(n, 1);
+		for(uint32_t i = 0; i < n; ++i)
+		{
+			if(!use[i]) continue;
+			kept.push_back(i);
+			const float4 q = pos[i], qn = nrm[i];
+			const int64_t cx = axisCell(q.x, 0, nx), cy = axisCell(q.y, 1, ny), cz = axisCell(q.z, 2, nz);
+			for(int64_t z = std::max<int64_t>(0, cz - 1); z <= std::min(nz - 1, cz + 1); ++z)
+				for(int64_t y = std::max<int64_t>(0, cy - 1); y <= std::min(ny - 1, cy + 1); ++y)
+					for(int64_t x = std::max<int64_t>(0, cx - 1); x <= std::min(nx - 1, cx + 1); ++x)
+					{
+						const size_t c = (size_t)((z * ny + y) * nx + x);
+						for(uint32_t k = start[c]; k < start[c + 1]; ++k)
+						{
+							const uint32_t j = order[k];
+							if(!use[j]) continue;
+							const float vx = pos[j].x - q.x, vy = pos[j].y - q.y, vz = pos[j].z - q.z;
+							const float d2 = vx * vx + vy * vy + vz * vz;
+							const float nd = nrm[j].x * qn.x + nrm[j].y * qn.y + nrm[j].z * qn.z;
+							if(d2 < maxrad && nd > 0.f) use[j] = 0;
+						}
+					}
+		}
+		return kept;
+	}
+	// sparse fallback: hashed cells
 	auto cellOf = [&](const float4 &p, int dx, int dy, int dz) {
 		const int64_t x = (int64_t)std::floor(p.x / cell) + dx, y = (int64_t)std::floor(p.y / cell) + dy, z = (int64_t)std::floor(p.z / cell) + dz;
 		return (uint64_t)(x * 73856093) ^ (uint64_t)(y * 19349663) ^ (uint64_t)(z * 83492791);
@@ -627,15 +685,35 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	DevScene &S = rp.scene;
 	const PhotonParams &pm = rp.pm;
 	const uint32_t nr = d.n_rad_points;
-	std::vector<float4> pos(nr), nrm(nr);
-	if(nr)
+	const auto tr0 = std::chrono::steady_clock::now();
+	const float maxrad = 0.01f * pm.radius2;   // :568 (used as a squared distance)
+	if(!ensure(log_, d.rad_kept, (size_t)std::max(1u, nr) * 4)) return false;
+	// thinning on the GPU (fgthin.hip); the host twin serves grids too large for a dense cell table
+	uint32_t nk = 0;
+	int rounds = 0;
+	// YAFARAY_AMD_FG_THIN=host forces the host twin (tests compare both)
+	const char *thin_env = std::getenv("YAFARAY_AMD_FG_THIN");
+	const bool host_thin = thin_env && std::string(thin_env) == "host";
+	const hipError_t te = host_thin ? hipErrorNotSupported
+	                                : yafamd_thin_rad_points((const float4 *)d.radc_a.p, (const float4 *)d.radc_b.p, nr, maxrad,
+	                                                         (uint32_t *)d.rad_kept.p, &nk, &rounds, d.stream);
+	if(te == hipErrorNotSupported)
 	{
+		std::vector<float4> pos(nr), nrm(nr);
 		HIPCHECK(hipMemcpyAsync(pos.data(), d.radc_a.p, (size_t)nr * 16, hipMemcpyDeviceToHost, d.stream));
 		HIPCHECK(hipMemcpyAsync(nrm.data(), d.radc_b.p, (size_t)nr * 16, hipMemcpyDeviceToHost, d.stream));
 		HIPCHECK(hipStreamSynchronize(d.stream));
+		const std::vector<uint32_t> kept = eliminateRadPoints(pos, nrm, maxrad);
+		nk = (uint32_t)kept.size();
+		if(nk) HIPCHECK(hipMemcpyAsync(d.rad_kept.p, kept.data(), (size_t)nk * 4, hipMemcpyHostToDevice, d.stream));
+		HIPCHECK(hipStreamSynchronize(d.stream));
+		rounds = -1;
 	}
-	const std::vector<uint32_t> kept = eliminateRadPoints(pos, nrm, 0.01f * pm.radius2);
-	const uint32_t nk = (uint32_t)kept.size();
+	else HIPCHECK(te);
+	stats_.radiance_points = nr;
+	stats_.radiance_photons = nk;
+	stats_.fg_thin_rounds = rounds;
+	stats_.fg_thin_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
 	S.fg_on = 1;
 	S.fg_samples = pm.fg_samples;
 	S.fg_bounces = pm.fg_bounces;
@@ -644,13 +722,14 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	S.fg_i_scale = static_cast<float>(1.f / ((float)S.pm_paths * 3.1415926535897932384626433832795L));   // :53 (math::num_pi)
 	S.n_rphotons = (int)nk;
 	std::ostringstream os;
-	os << "PhotonIntegrator: " << nr << " radiance points, " << nk << " kept for the radiance map";
+	os << "PhotonIntegrator: " << nr << " radiance points, " << nk << " kept for the radiance map ("
+	   << (rounds >= 0 ? "GPU thinning, " + std::to_string(rounds) + " rounds" : std::string("host thinning")) << ", "
+	   << stats_.fg_thin_seconds * 1e3 << " ms)";
 	log_.info(os.str());
 	if(nk == 0) { S.rpk_nodes = nullptr; return true; }
-	if(!ensure(log_, d.rad_kept, (size_t)nk * 4) || !ensure(log_, d.rph_pos, (size_t)nk * 16) || !ensure(log_, d.rph_dir, (size_t)nk * 16) ||
-	   !ensure(log_, d.rph_colb, (size_t)nk * 4) || !ensure(log_, d.rpk_nodes, (2 * (size_t)nk - 1) * sizeof(uint4)))
+	if(!ensure(log_, d.rph_pos, (size_t)nk * 16) || !ensure(log_, d.rph_dir, (size_t)nk * 16) || !ensure(log_, d.rph_colb, (size_t)nk * 4) ||
+	   !ensure(log_, d.rpk_nodes, (2 * (size_t)nk - 1) * sizeof(uint4)))
 		return false;
-	HIPCHECK(hipMemcpyAsync(d.rad_kept.p, kept.data(), (size_t)nk * 4, hipMemcpyHostToDevice, d.stream));
 	DevScene probe = S;
 	probe.n_seg = (uint32_t)d.shade_grid;   // the gather grid k_pregather shares pk_stack with
 	PROF(KK_PREGATHER, yafamd_pregather(&probe, (const float4 *)d.radc_a.p, (const float4 *)d.radc_b.p, (const float4 *)d.radc_c.p,
@@ -660,6 +739,7 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)d.rph_pos.p, nk, (uint4 *)d.rpk_nodes.p, &depth, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	d.n_rphotons = (int)nk;
+	stats_.fg_radiance_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
 	S.rph_pos = (const float4 *)d.rph_pos.p;
 	S.rph_dir = (const float4 *)d.rph_dir.p;
 	S.rph_colb = (const float *)d.rph_colb.p;
@@ -776,6 +856,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	fillScenePointers(d, S);
 	stats_.photons = 0;
 	stats_.caustic_photons = 0;
+	stats_.radiance_points = stats_.radiance_photons = 0;
+	stats_.fg_thin_seconds = stats_.fg_radiance_seconds = 0.0;
+	stats_.fg_thin_rounds = 0;
 	stats_.photon_seconds = 0.0;
 	d.prof_on = rp.profile;
 	d.ev_n = 2;

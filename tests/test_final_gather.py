@@ -4,7 +4,7 @@ integrator_photon_mapping.cc:183-193 (radiance points while shooting the diffuse
 :39-88 (preGatherWorker), :640-763 (finalGathering), :874-917 (integrate with final gathering);
 photon.cc:136-142 (findNearest).
 
-GPU: radiance points in k_photon_bounce, compaction, host thinning, k_pregather, the radiance map's
+GPU: radiance points in k_photon_bounce, compaction, thinning in rounds (fgthin.hip), k_pregather, the radiance map's
 point kd-tree (pkd.hip), k_fg (gather paths traced in place, estimateOneDirectLight with in-place
 shadow rays, radiance-map lookups) before k_gather.  Compared with the oracle restatement
 (oracle/yafcpu.cc finalGathering / buildRadianceMap): per value <= 4 ULP, weights equal.
@@ -108,6 +108,14 @@ def test_final_gather_specular_matches_oracle(product, oracle_built):
     """Mirror and transparent surfaces: gather paths that bounce specularly (caustic gather paths
     look the radiance map up inside the loop) and recursiveRaytrace nodes that final-gather again."""
     compare(product, oracle_built, fg_spec(specular=True, fg_min_pathlen=0.3))
+
+
+@pytest.mark.gpu
+def test_final_gather_host_thinning_matches_oracle(product, oracle_built, monkeypatch):
+    """The host twin of the radiance-point thinning (render.cc eliminateRadPoints, used when the
+    dense GPU grid would be too large) gives the same radiance map as the GPU rounds (fgthin.hip)."""
+    monkeypatch.setenv("YAFARAY_AMD_FG_THIN", "host")
+    compare(product, oracle_built, fg_spec(photons=30000))
 
 
 @pytest.mark.gpu
