@@ -71,7 +71,15 @@ def test_unsupported_plugins_rejected_reference_style(product):
     assert yi.createMaterial("g") == 0           # material.cc:52-61: unknown/unsupported -> null
     yi.paramsClearAll()
     yi.paramsSetString("type", "photonmapping")
+    yi.paramsSetBool("show_map", True)              # not served by the GPU core
     assert yi.createIntegrator("pm") == 0
+    yi.paramsClearAll()
+    yi.paramsSetString("type", "photonmapping")     # reference defaults (final gathering on)
+    assert yi.createIntegrator("pm2") == 1
+    yi.paramsClearAll()
+    yi.paramsSetString("type", "photonmapping")
+    yi.paramsSetBool("transpShad", True)            # final gathering traces opaque shadows only
+    assert yi.createIntegrator("pm3") == 0
     yi.paramsClearAll()
     yi.paramsSetString("type", "shinydiffusemat")
     assert yi.createMaterial("d") == 1
