@@ -122,3 +122,16 @@ def test_final_gather_host_thinning_matches_oracle(product, oracle_built, monkey
 def test_final_gather_off_is_unchanged(product, oracle_built):
     spec = fg_spec(pm_final_gather=False)
     compare(product, oracle_built, spec)
+
+
+@pytest.mark.gpu
+def test_final_gather_textured_point_light_matches_oracle(product, oracle_built):
+    """Textured / smooth materials and a point light: gather hits evaluate the shader-node colour
+    (k_fg<EXT> with surface attributes), radiance points the reflectivity of the textured hit, and
+    estimateOneDirectLight takes the point-light branch (shadow ray traced in place)."""
+    import texscenes as T
+    mats, imgs, texs = T.CASES["layers"]()
+    spec = T.grid_scene(mats, imgs, texs, width=40, height=30, spp=1, sphere_smooth=60.0)
+    spec = spec.with_render(integrator="photonmapping", pm_photons=20000, pm_search=30, pm_diffuse_radius=0.4,
+                            pm_final_gather=True, fg_samples=4, fg_min_pathlen=1.5)
+    compare(product, oracle_built, spec)
