@@ -3003,7 +3003,10 @@ __global__ void __launch_bounds__(1024) k_photon_scatter(PhotonState P, uint32_t
 // contributions are added to the sample's colour in heap-array order and the sample is written.
 // ---------------------------------------------------------------------------------------------
 constexpr int kGatherBlock = 64;
-constexpr int kGatherPerSeg = 4;   // workgroups per queue segment (fills the chip: 4 x 1024 x 64 lanes)
+#ifndef YAF_GATHER_PER_SEG
+#define YAF_GATHER_PER_SEG 4
+#endif
+constexpr int kGatherPerSeg = YAF_GATHER_PER_SEG;   // workgroups per queue segment (fills the chip: 4 x 1024 x 64 lanes)
 #ifndef YAF_GATHER_STACK_LDS
 #define YAF_GATHER_STACK_LDS 0     // 1: lookup stack in LDS (8 B x depth per lane) instead of HBM
 #endif
@@ -3556,8 +3559,14 @@ struct FgArgs
 	int *spill;
 };
 
+// k_fg: the gather-path megakernel wants ~230 VGPRs unconstrained (2 waves / SIMD); capped for 4
+// waves / SIMD it spills a little and runs faster (C5 + FG 32: 42.2 -> 31.0 ms; 3 waves: 34.8 ms)
+#ifndef YAF_FG_WAVES
+#define YAF_FG_WAVES 4
+#endif
+#define YAF_FG_ATTR __attribute__((amdgpu_waves_per_eu(YAF_FG_WAVES)))
 template<bool LDS_SCENE, bool WIDE, bool EXT>
-__global__ void __launch_bounds__(kTraceBlock) k_fg(FgArgs A)
+__global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 {
 	const DevScene &S = A.S;
 	extern __shared__ float4 smem[];
