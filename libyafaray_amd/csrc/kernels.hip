@@ -3957,13 +3957,18 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const D
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
 	const dim3 grid(S->n_seg * kGatherPerSeg);
-	const size_t lds = gatherTableBytes(*S, S->small_tables != 0) + gatherLdsBytes(*S);
+#ifdef YAF_GATHER_NO_SMALL
+	const bool small = false;
+#else
+	const bool small = S->small_tables != 0;
+#endif
+	const size_t lds = gatherTableBytes(*S, small) + gatherLdsBytes(*S);
 	if(S->ext)
 	{
-		if(S->small_tables) hipLaunchKernelGGL((k_gather<true, true>), grid, dim3(kGatherBlock), lds, st, A);
+		if(small) hipLaunchKernelGGL((k_gather<true, true>), grid, dim3(kGatherBlock), lds, st, A);
 		else hipLaunchKernelGGL((k_gather<false, true>), grid, dim3(kGatherBlock), lds, st, A);
 	}
-	else if(S->small_tables) hipLaunchKernelGGL((k_gather<true, false>), grid, dim3(kGatherBlock), lds, st, A);
+	else if(small) hipLaunchKernelGGL((k_gather<true, false>), grid, dim3(kGatherBlock), lds, st, A);
 	else hipLaunchKernelGGL((k_gather<false, false>), grid, dim3(kGatherBlock), lds, st, A);
 	return hipGetLastError();
 }
