@@ -349,5 +349,7 @@ def render_spec(spec, chunk_slots=None, profile=False, shard=None):
     rgba, w = yi.film()
     st = yi.stats()
     st["owned_rows"] = yi.owned_rows()
+    if profile:
+        st["kernel_times"] = yi.kernel_times()
     yi.close()
     return rgba, w, st

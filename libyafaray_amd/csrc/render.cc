@@ -1142,9 +1142,11 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// tracing finishes paths in any iteration
 			const bool dl_pipeline = S.integrator != INT_PATH;
 			if(S.gather_on && (!dl_pipeline || it == 1))
-				if(S.fg_on)
-					PROF(KK_FG, yafamd_launch_fg(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+			{
+				// final gathering adds its estimate to the requests' colour before k_gather ends them
+				if(S.fg_on) PROF(KK_FG, yafamd_launch_fg(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 				PROF(KK_GATHER, yafamd_launch_gather(&S, &d.G, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
+			}
 			// NEE requests (none in iteration 1 of photon mapping, whose entries all finish there)
 			if((S.ext || !yafamd_shade_fused()) && !(S.integrator == INT_PHOTON && it == 1))
 				PROF(KK_NEE, yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));

@@ -135,3 +135,17 @@ def test_final_gather_textured_point_light_matches_oracle(product, oracle_built)
     spec = spec.with_render(integrator="photonmapping", pm_photons=20000, pm_search=30, pm_diffuse_radius=0.4,
                             pm_final_gather=True, fg_samples=4, fg_min_pathlen=1.5)
     compare(product, oracle_built, spec)
+
+
+@pytest.mark.gpu
+def test_launch_sequence_per_integrator(product):
+    """k_gather / k_fg run only where the integrator has photon-map estimates to finish (a path
+    tracer without photon caustics launches neither; final gathering launches k_fg once per chunk,
+    in the iteration the direct-light pipeline finishes)."""
+    pt = scenes.cornell(32, 24, spp=1, bounces=3, rr=False)
+    _, _, st = product.render_spec(pt, profile=True)
+    kt = st["kernel_times"]
+    assert kt.get("k_gather", {}).get("launches", 0) == 0 and kt.get("k_fg", {}).get("launches", 0) == 0
+    _, _, st = product.render_spec(fg_spec(24, 18, fg_samples=2), profile=True)
+    kt = st["kernel_times"]
+    assert kt["k_fg"]["launches"] == 1 and kt["k_gather"]["launches"] == 1
