@@ -44,7 +44,7 @@ struct ThinBuf
 // scratch kept between renders (the radiance map is rebuilt every frame)
 struct ThinScratch
 {
-	ThinBuf part, cid, count, start, order, st0, st1, counter, tmp, n_sel;
+	ThinBuf part, cid, count, start, order, st0, st1, counter, tmp, n_sel, klist;
 } g_thin;
 
 constexpr int kBoundBlocks = 256;
@@ -134,7 +134,8 @@ __device__ __forceinline__ bool thinRelated(const float4 &p, const float4 &pn, c
 // snapshot `sin`) is kept; the kept points of earlier rounds have already killed their related
 // higher points (part 2), so the dead ones are skipped and the scan stops at the first undecided one
 __global__ void __launch_bounds__(256) k_thin_keep(const float4 *pos, const float4 *nrm, const uint32_t *order, const uint32_t *start,
-                                                  ThinGrid g, const uint8_t *sin, uint8_t *sout, uint32_t n, float maxrad)
+                                                  ThinGrid g, const uint8_t *sin, uint8_t *sout, uint32_t n, float maxrad, uint32_t *klist,
+                                                  uint32_t *n_klist)
 {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if(i >= n) return;
@@ -154,28 +155,37 @@ __global__ void __launch_bounds__(256) k_thin_keep(const float4 *pos, const floa
 		}
 	}
 	sout[i] = stop ? kUndecided : kKept;
+	if(!stop) klist[atomicAdd(n_klist, 1u)] = i;   // few per round: part 2 works on this list
 }
 
 // round, part 2: every point kept in this round marks its related higher points dead (the
 // reference's EliminatePhoton lookup from a kept point); none of them can have been kept in part 1
-// (it saw this point undecided below it)
+// (it saw this point undecided below it).  One wave per kept point: the lanes split the entries of
+// its 27 cells (a lane per point measured 2.5 ms per round — a few thousand long serial scans)
 __global__ void __launch_bounds__(256) k_thin_kill(const float4 *pos, const float4 *nrm, const uint32_t *order, const uint32_t *start,
-                                                  ThinGrid g, const uint8_t *sin, uint8_t *sout, uint32_t n, float maxrad)
+                                                  ThinGrid g, uint8_t *sout, const uint32_t *klist, const uint32_t *n_klist, float maxrad)
 {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if(i >= n || sin[i] != kUndecided || sout[i] != kKept) return;
-	const float4 q = pos[i], qn = nrm[i];
-	bool stop = false;
-	THIN_FOR_CELLS(q)
+	const uint32_t lane = __lane_id();
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+	const uint32_t nk = *n_klist;
+	for(uint32_t t = wave; t < nk; t += n_waves)
 	{
-		const uint32_t c = (uint32_t)((z * g.ny + y) * g.nx + x);
-		const uint32_t k1 = start[c + 1];
-		for(uint32_t k = start[c]; k < k1; ++k)
-		{
-			const uint32_t j = order[k];
-			if(j <= i) continue;
-			if(thinRelated(pos[j], nrm[j], q, qn, maxrad)) sout[j] = kDead;
-		}
+		const uint32_t i = klist[t];
+		const float4 q = pos[i], qn = nrm[i];
+		const int cx = axisCell(q.x, g.lo[0], g.inv_cell, g.nx), cy = axisCell(q.y, g.lo[1], g.inv_cell, g.ny),
+		          cz = axisCell(q.z, g.lo[2], g.inv_cell, g.nz);
+		for(int z = max(0, cz - 1); z <= min(g.nz - 1, cz + 1); ++z)
+			for(int y = max(0, cy - 1); y <= min(g.ny - 1, cy + 1); ++y)
+				for(int x = max(0, cx - 1); x <= min(g.nx - 1, cx + 1); ++x)
+				{
+					const uint32_t c = (uint32_t)((z * g.ny + y) * g.nx + x);
+					const uint32_t k1 = start[c + 1];
+					for(uint32_t k = start[c] + lane; k < k1; k += 64)
+					{
+						const uint32_t j = order[k];
+						if(j > i && thinRelated(pos[j], nrm[j], q, qn, maxrad)) sout[j] = kDead;
+					}
+				}
 	}
 }
 
@@ -243,6 +253,7 @@ extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nr
 	THCHECK(S.st0.ensure(n));
 	THCHECK(S.st1.ensure(n));
 	THCHECK(S.counter.ensure(16));
+	THCHECK(S.klist.ensure((size_t)n * 4));
 	THCHECK(S.n_sel.ensure(16));
 	THCHECK(hipMemsetAsync(S.count.p, 0, ((size_t)nc + 1) * 4, st));
 	const dim3 blocks((n + 255) / 256);
@@ -264,9 +275,12 @@ extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nr
 	int rounds = 0;
 	while(undecided > 0)
 	{
-		THCHECK(hipMemsetAsync(S.counter.p, 0, 4, st));
-		hipLaunchKernelGGL(k_thin_keep, blocks, dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad);
-		hipLaunchKernelGGL(k_thin_kill, blocks, dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad);
+		THCHECK(hipMemsetAsync(S.counter.p, 0, 8, st));   // [0] undecided count, [1] kept-list length
+		uint32_t *n_klist = S.counter.as<uint32_t>() + 1;
+		hipLaunchKernelGGL(k_thin_keep, blocks, dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad,
+		                   S.klist.as<uint32_t>(), n_klist);
+		hipLaunchKernelGGL(k_thin_kill, dim3(1024), dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sout,
+		                   S.klist.as<uint32_t>(), n_klist, maxrad);
 		hipLaunchKernelGGL(k_thin_count, blocks, dim3(256), 0, st, sout, n, S.counter.as<uint32_t>());
 		THCHECK(hipGetLastError());
 		THCHECK(hipMemcpyAsync(&undecided, S.counter.p, 4, hipMemcpyDeviceToHost, st));
