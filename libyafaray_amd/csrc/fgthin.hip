@@ -132,30 +132,47 @@ __device__ __forceinline__ bool thinRelated(const float4 &p, const float4 &pn, c
 
 // round, part 1: an undecided point none of whose lower-index related points is undecided (in the
 // snapshot `sin`) is kept; the kept points of earlier rounds have already killed their related
-// higher points (part 2), so the dead ones are skipped and the scan stops at the first undecided one
+// higher points (part 2), so the dead ones are skipped and the scan stops at the first undecided
+// one.  kKeepLanes lanes per point split the entries of each cell (uniform trip counts inside a
+// group, so every lane of the group sees its vote); one lane per point measured 2.7 ms per round.
+constexpr uint32_t kKeepLanes = 8;
 __global__ void __launch_bounds__(256) k_thin_keep(const float4 *pos, const float4 *nrm, const uint32_t *order, const uint32_t *start,
                                                   ThinGrid g, const uint8_t *sin, uint8_t *sout, uint32_t n, float maxrad, uint32_t *klist,
                                                   uint32_t *n_klist)
 {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if(i >= n) return;
+	const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = tid / kKeepLanes, sub = tid % kKeepLanes;
+	const uint64_t gmask = ((1ull << kKeepLanes) - 1ull) << (__lane_id() & ~(kKeepLanes - 1u));
+	if(i >= n) return;   // whole groups leave together (n * kKeepLanes threads, groups aligned)
 	const uint8_t s0 = sin[i];
-	if(s0 != kUndecided) { sout[i] = s0; return; }
+	if(s0 != kUndecided)
+	{
+		if(sub == 0) sout[i] = s0;
+		return;
+	}
 	const float4 q = pos[i], qn = nrm[i];
 	bool stop = false;
 	THIN_FOR_CELLS(q)
 	{
 		const uint32_t c = (uint32_t)((z * g.ny + y) * g.nx + x);
-		const uint32_t k1 = start[c + 1];
-		for(uint32_t k = start[c]; k < k1; ++k)
+		const uint32_t k0 = start[c], k1 = start[c + 1];
+		for(uint32_t base = k0; base < k1; base += kKeepLanes)
 		{
-			const uint32_t j = order[k];
-			if(j >= i || sin[j] != kUndecided) continue;
-			if(thinRelated(pos[j], nrm[j], q, qn, maxrad)) { stop = true; break; }
+			const uint32_t k = base + sub;
+			bool hit = false;
+			if(k < k1)
+			{
+				const uint32_t j = order[k];
+				hit = j < i && sin[j] == kUndecided && thinRelated(pos[j], nrm[j], q, qn, maxrad);
+			}
+			if(__ballot(hit) & gmask) { stop = true; break; }
 		}
 	}
-	sout[i] = stop ? kUndecided : kKept;
-	if(!stop) klist[atomicAdd(n_klist, 1u)] = i;   // few per round: part 2 works on this list
+	if(sub == 0)
+	{
+		sout[i] = stop ? kUndecided : kKept;
+		if(!stop) klist[atomicAdd(n_klist, 1u)] = i;   // few per round: part 2 works on this list
+	}
 }
 
 // round, part 2: every point kept in this round marks its related higher points dead (the
@@ -277,7 +294,7 @@ extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nr
 	{
 		THCHECK(hipMemsetAsync(S.counter.p, 0, 8, st));   // [0] undecided count, [1] kept-list length
 		uint32_t *n_klist = S.counter.as<uint32_t>() + 1;
-		hipLaunchKernelGGL(k_thin_keep, blocks, dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad,
+		hipLaunchKernelGGL(k_thin_keep, dim3((uint32_t)(((uint64_t)n * kKeepLanes + 255) / 256)), dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad,
 		                   S.klist.as<uint32_t>(), n_klist);
 		hipLaunchKernelGGL(k_thin_kill, dim3(1024), dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sout,
 		                   S.klist.as<uint32_t>(), n_klist, maxrad);
