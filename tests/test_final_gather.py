@@ -83,8 +83,8 @@ def test_oracle_final_gather_deterministic_and_indirect(oracle_built):
 # ---------------------------------------------------------------------------------------------
 # GPU: the HIP path against the oracle
 # ---------------------------------------------------------------------------------------------
-def compare(product, oracle_built, spec):
-    rgba, w, st = product.render_spec(spec)
+def compare(product, oracle_built, spec, chunk_slots=None):
+    rgba, w, st = product.render_spec(spec, chunk_slots=chunk_slots)
     o = oracle_built.OracleScene(spec, threads=8)
     orgba, ow, _ = o.render()
     dpos, *_ = o.photon_map("diffuse")
@@ -149,3 +149,12 @@ def test_launch_sequence_per_integrator(product):
     _, _, st = product.render_spec(fg_spec(24, 18, fg_samples=2), profile=True)
     kt = st["kernel_times"]
     assert kt["k_fg"]["launches"] == 1 and kt["k_gather"]["launches"] == 1
+
+
+@pytest.mark.gpu
+def test_final_gather_several_chunks_and_aa_passes(product, oracle_built):
+    """Final gathering over several wavefront chunks (the gather queue of each chunk) and with
+    adaptive AA passes (PixelSamplingData of the resampled pixels' later passes)."""
+    compare(product, oracle_built, fg_spec(32, 24, spp=2, fg_samples=3), chunk_slots=300)
+    spec = fg_spec(32, 24, spp=1, fg_samples=2, aa_passes=2, aa_inc_samples=1, aa_threshold=0.02)
+    compare(product, oracle_built, spec)
