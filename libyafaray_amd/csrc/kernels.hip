@@ -99,6 +99,47 @@ __device__ __forceinline__ uint32_t waveAppend(bool want, uint32_t *counter)
 	return base + (uint32_t)__popcll(below);
 }
 
+// Path-state stores of k_shade: the next state is read back only after k_trace / k_nee ran over
+// GBs of other data, so caching it buys nothing: they are non-temporal (YAF_NT_STORE), and so are
+// the queues, NEE requests and shadow rays (YAF_NT_STORE2).  C2, same box: 1697 / 1707 (plain),
+// 1702 / 1723 (state only), 1720 / 1733 Msamples/s (both).  -DYAF_NT_STORE=0 / -DYAF_NT_STORE2=0
+// restore plain stores.
+#ifndef YAF_NT_STORE
+#define YAF_NT_STORE 1
+#endif
+#ifndef YAF_NT_STORE2
+#define YAF_NT_STORE2 1
+#endif
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+template<class T>
+__device__ __forceinline__ void stStore(T *p, const T &v)
+{
+	static_assert(sizeof(T) == 16, "16-byte path-state records");
+#if YAF_NT_STORE
+	u32x4_t w;
+	__builtin_memcpy(&w, &v, 16);
+	__builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
+#else
+	*p = v;
+#endif
+}
+// wider use (queues, NEE requests and contributions, shadow rays): -DYAF_NT_STORE2
+template<class T>
+__device__ __forceinline__ void stStore2(T *p, const T &v)
+{
+#if YAF_NT_STORE2
+	if constexpr(sizeof(T) == 16)
+	{
+		u32x4_t w;
+		__builtin_memcpy(&w, &v, 16);
+		__builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
+	}
+	else __builtin_nontemporal_store(v, p);
+#else
+	*p = v;
+#endif
+}
+
 // Segment worked on by this k_trace workgroup, its rank among the segment's workgroups and their
 // number (the trace grid is a multiple of n_seg).
 struct SegLoop
@@ -1366,9 +1407,9 @@ __device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, f
 	const uint32_t k = out.sh_base + waveAppend(want, out.sh_count);
 	if(want)
 	{
-		out.Qn.sh_o[k] = f4(o, tmin);
-		out.Qn.sh_d[k] = f4(d, t_max);
-		out.Qn.sh_idx[k] = idx;
+		stStore2(&out.Qn.sh_o[k], f4(o, tmin));
+		stStore2(&out.Qn.sh_d[k], f4(d, t_max));
+		stStore2(&out.Qn.sh_idx[k], idx);
 	}
 }
 
@@ -2147,11 +2188,11 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		const uint32_t k = a0 + waveAppend(keep, &s_count[0]);
 		if(keep)
 		{
-			A.Qn.slot[k] = (int)sid;
+			stStore2(&A.Qn.slot[k], (int)sid);
 			if(want_ray)
 			{
-				A.Qn.ray_o[k] = f4(ray_o, S.ray_min_dist);
-				A.Qn.ray_d[k] = f4(ray_d, -1.f);
+				stStore2(&A.Qn.ray_o[k], f4(ray_o, S.ray_min_dist));
+				stStore2(&A.Qn.ray_d[k], f4(ray_d, -1.f));
 			}
 			else
 			{
@@ -2159,10 +2200,10 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				A.Qn.ray_d[k] = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));
 				stage = ST_NORAY | (subpath << 8) | ((uint32_t)depth << 20);
 			}
-			Pn.pr[k] = make_uint4(pix.x, pix.y, rng.x, rng.y);
-			Pn.thr[k] = f4(thr, w);
-			Pn.col[k] = f4(col, __uint_as_float(stage));
-			Pn.pcol[k] = f4(pcol, __uint_as_float(flags));
+			stStore(&Pn.pr[k], make_uint4(pix.x, pix.y, rng.x, rng.y));
+			stStore(&Pn.thr[k], f4(thr, w));
+			stStore(&Pn.col[k], f4(col, __uint_as_float(stage)));
+			stStore(&Pn.pcol[k], f4(pcol, __uint_as_float(flags)));
 			if((stage & 0xffu) == ST_FIRST) Pn.pwo[k] = f4(pwo, 0.f);
 			if(nee_one) Pn.pend_thr[k] = f4(pend_thr, 0.f);
 			if(flags & (F_PEND_EMIT | F_AO_EMIT)) Pn.pend_emit[k] = f4(emit_pend, 0.f);
@@ -2205,9 +2246,9 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		if(!FUSED && want_nee)
 		{
 			const uint32_t j = a0 + jn;
-			A.N.p_prim[j] = f4(sp.p, __int_as_float(hit_prim));
-			A.N.wo_k[j] = f4(wo, __uint_as_float(k));
-			A.N.pix_mode[j] = make_uint4(offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8), 0u);
+			stStore2(&A.N.p_prim[j], f4(sp.p, __int_as_float(hit_prim)));
+			stStore2(&A.N.wo_k[j], f4(wo, __uint_as_float(k)));
+			stStore2(&A.N.pix_mode[j], make_uint4(offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8), 0u));
 			if(ATTR)
 			{
 				A.N.attr[2 * (size_t)j] = f4(sp.n, sp.drefl);
