@@ -20,6 +20,7 @@
 #define YAFARAY_AMD_H
 
 #include "yafaray_c_api.h"
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -54,6 +55,11 @@ typedef struct
 	int64_t fg_thin_rounds;     /* final gathering: GPU thinning rounds (-1: thinned on the host) */
 } yafaray_amd_stats_t;
 
+/* Bytes of the LIBYAFARAY_AMD_1.0 struct (its fields end at photon_tree_seconds): yafaray_amd_getStats
+ * writes exactly these, so clients built against the 1.0 header keep working; newer clients call
+ * yafaray_amd_getStatsEx with sizeof(yafaray_amd_stats_t). */
+#define YAFARAY_AMD_STATS_V1_0_SIZE (offsetof(yafaray_amd_stats_t, gather_visits))
+
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */
 YAFARAY_C_API_EXPORT int yafaray_amd_addVertices(yafaray_Interface_t *interface, const double *xyz, int n);
 YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_addTriangles(yafaray_Interface_t *interface, const int *abc, int n);
@@ -87,8 +93,10 @@ YAFARAY_C_API_EXPORT int yafaray_amd_getOwnedRows(const yafaray_Interface_t *int
 /* Render without callbacks / console output (bench loop); same work as yafaray_render. */
 YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t *interface);
 
-/* Counters and timings of the last render. */
+/* Counters and timings of the last render: the LIBYAFARAY_AMD_1.0 fields (YAFARAY_AMD_STATS_V1_0_SIZE bytes). */
 YAFARAY_C_API_EXPORT void yafaray_amd_getStats(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats);
+/* (LIBYAFARAY_AMD_1.2) All counters: copies min(bytes, sizeof(yafaray_amd_stats_t)) bytes, returns how many. */
+YAFARAY_C_API_EXPORT size_t yafaray_amd_getStatsEx(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats, size_t bytes);
 
 /* Per-kernel timing of the last render with setProfileKernels on (HIP events before / after every
  * launch on the render stream): for each kernel kind k < return value (and < max): its name, summed
@@ -108,9 +116,33 @@ YAFARAY_C_API_EXPORT int yafaray_amd_getKernelTimes(const yafaray_Interface_t *i
  * world = 1 leaves the group.  getRenderGroupId returns the id size (0 on failure). */
 YAFARAY_C_API_EXPORT int yafaray_amd_getRenderGroupId(void *id, int bytes);
 YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_setRenderGroup(yafaray_Interface_t *interface, int rank, int world, const void *id, int bytes);
+/* Device group (LIBYAFARAY_AMD_1.2): ONE process renders one film on several GPUs — one member per
+ * GPU, each on its own host thread and HIP stream, rendering a contiguous row band (+ halo rows);
+ * the members exchange the accumulated film between adaptive passes and member 0 pulls every band
+ * over xGMI at the end, so the film is bit-identical to a one-GPU render.  By default the group is
+ * every visible device (render parameter "gpus": -1 = all, n = the first n devices starting at the
+ * current one; env YAFARAY_AMD_GPUS overrides), so an unmodified reference client's yafaray_render
+ * uses the whole node.  setDeviceGroup fixes the members explicitly: devices[m] is member m's HIP
+ * device (devices NULL: the current device + m, modulo the visible devices — several logical members
+ * may share one GPU, which rehearses the group on one device); members <= 0 returns to "gpus".
+ * A render group (setRenderGroup) always renders with one member per process. */
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_setDeviceGroup(yafaray_Interface_t *interface, int members, const int *devices);
+/* Members the next render uses (0 on failure, e.g. no GPU). */
+YAFARAY_C_API_EXPORT int yafaray_amd_getDeviceGroupSize(yafaray_Interface_t *interface);
+
 /* The group's band balancer: world + 1 boundaries and each band's render time -> new boundaries
  * (out, world + 1 ints); cap_rows > 0 rejects a split with a larger band.  Returns 1. */
 YAFARAY_C_API_EXPORT int yafaray_amd_rebalanceBands(const int *bounds, int world, const double *times, int cap_rows, int *out);
+
+/* (LIBYAFARAY_AMD_1.2) The render group's band exchange plan on host arrays, as the group runs it on
+ * device buffers: packBand writes member `rank`'s rows [bounds[rank], bounds[rank+1]) of a
+ * width x height x channels film into a zero-padded slot of the largest band's rows; after an
+ * all-gather of the slots (member order), unpackBands copies every other member's rows into the
+ * film.  Return 1 (0: bad arguments). */
+YAFARAY_C_API_EXPORT int yafaray_amd_packBand(const float *film, int width, int height, int channels, const int *bounds, int world, int rank,
+                                              float *send);
+YAFARAY_C_API_EXPORT int yafaray_amd_unpackBands(const float *recv, int width, int height, int channels, const int *bounds, int world,
+                                                 int rank, float *film);
 
 /* Tuning: samples in flight per wavefront chunk (default 1 << 25, halved automatically if it does not fit) and whether to time k_trace with events. */
 YAFARAY_C_API_EXPORT void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots);

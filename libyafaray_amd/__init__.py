@@ -135,6 +135,11 @@ def lib():
             "yafaray_amd_getOwnedRows": (i, [vp, C.POINTER(C.c_int), i]),
             "yafaray_amd_renderQuiet": (b, [vp]),
             "yafaray_amd_getStats": (None, [vp, C.POINTER(Stats)]),
+            "yafaray_amd_getStatsEx": (C.c_size_t, [vp, C.POINTER(Stats), C.c_size_t]),
+            "yafaray_amd_setDeviceGroup": (b, [vp, i, C.POINTER(C.c_int)]),
+            "yafaray_amd_getDeviceGroupSize": (i, [vp]),
+            "yafaray_amd_packBand": (i, [C.POINTER(C.c_float), i, i, i, C.POINTER(C.c_int), i, i, C.POINTER(C.c_float)]),
+            "yafaray_amd_unpackBands": (i, [C.POINTER(C.c_float), i, i, i, C.POINTER(C.c_int), i, i, C.POINTER(C.c_float)]),
             "yafaray_amd_setChunkSlots": (None, [vp, i]),
             "yafaray_amd_setProfileKernels": (None, [vp, b]),
             "yafaray_amd_lastError": (cp, [vp]),
@@ -260,8 +265,21 @@ class Interface:
 
     def stats(self) -> dict:
         s = Stats()
-        self.L.yafaray_amd_getStats(self.h, C.byref(s))
+        self.L.yafaray_amd_getStatsEx(self.h, C.byref(s), C.sizeof(s))
         return s.as_dict()
+
+    def set_device_group(self, members, devices=None):
+        """yafaray_amd_setDeviceGroup: `members` renderers of this process share the film (row bands);
+        devices[m] = member m's HIP device (None: current device + m modulo the visible devices, so
+        several logical members can share one GPU).  members <= 0: back to the "gpus" parameter."""
+        arr = None
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*[int(d) for d in devices])
+        if not self.L.yafaray_amd_setDeviceGroup(self.h, int(members), arr):
+            raise RuntimeError("setDeviceGroup failed: " + self.last_error())
+
+    def device_group_size(self) -> int:
+        return int(self.L.yafaray_amd_getDeviceGroupSize(self.h))
 
     def kernel_times(self) -> dict:
         """{kernel: {"ms", "launches", "items"}} of the last render with profiling on (yafaray_amd_getKernelTimes)."""
@@ -332,11 +350,45 @@ def rebalance_bands(bounds, times, cap_rows=0):
     return list(out)
 
 
-def render_spec(spec, chunk_slots=None, profile=False, shard=None):
-    """Replay a scenes.SceneSpec through the C API and render it; returns (rgba, weights, stats)."""
+def pack_band(film, bounds, rank):
+    """The library's band plan (yafaray_amd_packBand): `rank`'s rows of a (H, W, C) float32 film in a
+    zero-padded (max band rows, W, C) buffer, as the render group sends it."""
+    film = np.ascontiguousarray(film, np.float32)
+    H, W = film.shape[:2]
+    ch = 1 if film.ndim == 2 else film.shape[2]
+    world = len(bounds) - 1
+    rows = max(bounds[r + 1] - bounds[r] for r in range(world))
+    out = np.zeros((rows, W) + film.shape[2:], np.float32)
+    b = (C.c_int * (world + 1))(*bounds)
+    fp = C.POINTER(C.c_float)
+    if not lib().yafaray_amd_packBand(film.ctypes.data_as(fp), W, H, ch, b, world, int(rank), out.ctypes.data_as(fp)):
+        raise RuntimeError("packBand failed")
+    return out
+
+
+def unpack_bands(gathered, bounds, rank, film):
+    """The library's band plan (yafaray_amd_unpackBands): every other member's rows of an all-gather
+    result (world * max band rows, W, C) into `film` (H, W, C), in place; `rank`'s own rows stay."""
+    gathered = np.ascontiguousarray(gathered, np.float32)
+    assert film.dtype == np.float32 and film.flags["C_CONTIGUOUS"]
+    H, W = film.shape[:2]
+    ch = 1 if film.ndim == 2 else film.shape[2]
+    world = len(bounds) - 1
+    b = (C.c_int * (world + 1))(*bounds)
+    fp = C.POINTER(C.c_float)
+    if not lib().yafaray_amd_unpackBands(gathered.ctypes.data_as(fp), W, H, ch, b, world, int(rank), film.ctypes.data_as(fp)):
+        raise RuntimeError("unpackBands failed")
+    return film
+
+
+def render_spec(spec, chunk_slots=None, profile=False, shard=None, members=None, devices=None):
+    """Replay a scenes.SceneSpec through the C API and render it; returns (rgba, weights, stats).
+    members: a device group of this many members (set_device_group)."""
     from . import scenes
     yi = Interface()
     scenes.apply(spec, yi)
+    if members is not None:
+        yi.set_device_group(members, devices)
     if chunk_slots:
         yi.L.yafaray_amd_setChunkSlots(yi.h, int(chunk_slots))
     if profile:

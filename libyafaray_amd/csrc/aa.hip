@@ -175,14 +175,15 @@ __device__ __forceinline__ void visitPixel(uint32_t q, int W, int H, int ts, int
 	y = y0 + (int)(k / (uint32_t)tw);
 }
 
-__global__ void __launch_bounds__(kB) k_aa_order(const uint8_t *flags, int W, int H, int ts, uint32_t *fq)
+// fq[q] = pixel q of the visiting order is resampled and lies in rows [ry0, ry1)
+__global__ void __launch_bounds__(kB) k_aa_order(const uint8_t *flags, int W, int H, int ts, int ry0, int ry1, uint32_t *fq)
 {
 	const uint32_t q = blockIdx.x * kB + threadIdx.x, n = (uint32_t)W * (uint32_t)H;
 	if(q > n) return;
 	if(q == n) { fq[n] = 0; return; }
 	int x, y;
 	visitPixel(q, W, H, ts, x, y);
-	fq[q] = flags[(size_t)y * W + x];
+	fq[q] = (y >= ry0 && y < ry1) ? flags[(size_t)y * W + x] : 0u;
 }
 
 __global__ void __launch_bounds__(kB) k_aa_scatter(const uint32_t *fq, const uint32_t *pos, int W, int H, int ts, uint32_t *plist)
@@ -207,8 +208,11 @@ struct DevBuf
 
 // nextPass: flags (W*H bytes) and the resampled pixels in visiting order (plist, W*H entries);
 // *count = how many.  threshold <= 0 resamples every pixel (doMoreSamples, imagefilm.cc:672-675).
+// Rows [ry0, ry1) (a group member's band + halo rows): plist holds only the resampled pixels of those
+// rows, *local_count of them; *count stays the whole film's.
 extern "C" hipError_t yafamd_aa_next_pass(const float4 *accum, const float *weights, int W, int H, int tile, const DevAaParams *prm,
-                                          float threshold, uint8_t *flags, uint32_t *plist, uint32_t *count, hipStream_t st)
+                                          float threshold, uint8_t *flags, uint32_t *plist, uint32_t *count, int ry0, int ry1,
+                                          uint32_t *local_count, hipStream_t st)
 {
 	const uint32_t n = (uint32_t)W * (uint32_t)H;
 	Film F{accum, weights, W, H};
@@ -228,13 +232,24 @@ extern "C" hipError_t yafamd_aa_next_pass(const float4 *accum, const float *weig
 	DevBuf fq, pos, tmp;
 	AACHECK(fq.alloc((size_t)(n + 1) * 4));
 	AACHECK(pos.alloc((size_t)(n + 1) * 4));
-	hipLaunchKernelGGL(k_aa_order, dim3((n + 1 + kB - 1) / kB), dim3(kB), 0, st, flags, W, H, tile, (uint32_t *)fq.p);
+	const bool part = ry0 > 0 || ry1 < H;
 	size_t bytes = 0;
 	AACHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint32_t *)fq.p, (uint32_t *)pos.p, (int)n + 1, st));
 	AACHECK(tmp.alloc(bytes));
+	if(part)
+	{
+		// the whole film's count first (the pass loop's threshold decay uses it)
+		hipLaunchKernelGGL(k_aa_order, dim3((n + 1 + kB - 1) / kB), dim3(kB), 0, st, flags, W, H, tile, 0, H, (uint32_t *)fq.p);
+		AACHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, bytes, (uint32_t *)fq.p, (uint32_t *)pos.p, (int)n + 1, st));
+		AACHECK(hipMemcpyAsync(count, (uint32_t *)pos.p + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+		AACHECK(hipStreamSynchronize(st));
+	}
+	hipLaunchKernelGGL(k_aa_order, dim3((n + 1 + kB - 1) / kB), dim3(kB), 0, st, flags, W, H, tile, part ? ry0 : 0, part ? ry1 : H, (uint32_t *)fq.p);
 	AACHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, bytes, (uint32_t *)fq.p, (uint32_t *)pos.p, (int)n + 1, st));
 	hipLaunchKernelGGL(k_aa_scatter, dim3((n + kB - 1) / kB), dim3(kB), 0, st, (const uint32_t *)fq.p, (const uint32_t *)pos.p, W, H, tile, plist);
 	AACHECK(hipGetLastError());
-	AACHECK(hipMemcpyAsync(count, (uint32_t *)pos.p + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-	return hipStreamSynchronize(st);
+	AACHECK(hipMemcpyAsync(local_count, (uint32_t *)pos.p + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+	AACHECK(hipStreamSynchronize(st));
+	if(!part) *count = *local_count;
+	return hipSuccess;
 }

@@ -10,6 +10,7 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -562,8 +563,40 @@ yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t *interface)
 
 void yafaray_amd_getStats(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats)
 {
+	// LIBYAFARAY_AMD_1.0 clients allocate the 1.0 struct: copy only its fields
 	const Interface *it = I(interface);
-	if(it->scene && stats) *stats = it->scene->stats;
+	if(it->scene && stats) std::memcpy((void *)stats, &it->scene->stats, YAFARAY_AMD_STATS_V1_0_SIZE);
+}
+
+size_t yafaray_amd_getStatsEx(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats, size_t bytes)
+{
+	const Interface *it = I(interface);
+	if(!it->scene || !stats) return 0;
+	const size_t n = std::min(bytes, sizeof(yafaray_amd_stats_t));
+	std::memcpy((void *)stats, &it->scene->stats, n);
+	return n;
+}
+
+yafaray_bool_t yafaray_amd_setDeviceGroup(yafaray_Interface_t *interface, int members, const int *devices)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return YAFARAY_BOOL_FALSE;
+	s->device_group.clear();
+	for(int m = 0; m < members; ++m) s->device_group.push_back(devices ? devices[m] : -1);
+	if(members > 64)
+	{
+		I(interface)->logger.error("Device group: at most 64 members");
+		s->device_group.clear();
+		return YAFARAY_BOOL_FALSE;
+	}
+	return YAFARAY_BOOL_TRUE;
+}
+
+int yafaray_amd_getDeviceGroupSize(yafaray_Interface_t *interface)
+{
+	Scene *s = I(interface)->sc();
+	if(!s || !s->syncMembers()) return 0;
+	return s->memberCount();
 }
 
 void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots)
@@ -604,6 +637,18 @@ int yafaray_amd_rebalanceBands(const int *bounds, int world, const double *times
 	const std::vector<int> nb = rebalanceBands(b, t, cap_rows);
 	for(int r = 0; r <= world; ++r) out[r] = nb[r];
 	return 1;
+}
+
+int yafaray_amd_packBand(const float *film, int width, int height, int channels, const int *bounds, int world, int rank, float *send)
+{
+	if(!bounds || world < 1) return 0;
+	return bandPack(film, width, height, channels, std::vector<int>(bounds, bounds + world + 1), rank, send) ? 1 : 0;
+}
+
+int yafaray_amd_unpackBands(const float *recv, int width, int height, int channels, const int *bounds, int world, int rank, float *film)
+{
+	if(!bounds || world < 1) return 0;
+	return bandUnpack(recv, width, height, channels, std::vector<int>(bounds, bounds + world + 1), rank, film) ? 1 : 0;
 }
 
 int yafaray_amd_getKernelTimes(const yafaray_Interface_t *interface, const char **names, double *ms, uint64_t *launches, uint64_t *items,

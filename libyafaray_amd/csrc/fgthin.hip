@@ -41,11 +41,16 @@ struct ThinBuf
 	}
 };
 
-// scratch kept between renders (the radiance map is rebuilt every frame)
+// scratch kept between renders (the radiance map is rebuilt every frame); one per renderer
 struct ThinScratch
 {
 	ThinBuf part, cid, count, start, order, st0, st1, counter, tmp, n_sel, klist;
-} g_thin;
+	~ThinScratch()
+	{
+		for(ThinBuf *b : {&part, &cid, &count, &start, &order, &st0, &st1, &counter, &tmp, &n_sel, &klist})
+			if(b->p) (void)hipFree(b->p);
+	}
+};
 
 constexpr int kBoundBlocks = 256;
 constexpr uint8_t kUndecided = 0, kKept = 1, kDead = 2;
@@ -229,16 +234,20 @@ struct IsKept
 		if(e_ != hipSuccess) return e_;                                                                        \
 	} while(0)
 
+extern "C" void yafamd_thin_scratch_free(void *scratch) { delete static_cast<ThinScratch *>(scratch); }
+
 // pos / nrm: the compacted radiance points (xyz used); kept_out: device, n entries of capacity.
 // Returns hipErrorNotSupported when the dense grid would exceed 2^26 cells (the caller thins on the
-// host then).
+// host then).  *scratch: the caller's scratch (created on first use, yafamd_thin_scratch_free).
 extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out,
-                                             uint32_t *n_kept, int *rounds_out, hipStream_t st)
+                                             uint32_t *n_kept, int *rounds_out, hipStream_t st, void **scratch)
 {
 	*n_kept = 0;
 	*rounds_out = 0;
 	if(n == 0) return hipSuccess;
-	ThinScratch &S = g_thin;
+	if(!scratch) return hipErrorInvalidValue;
+	if(!*scratch) *scratch = new ThinScratch;
+	ThinScratch &S = *static_cast<ThinScratch *>(*scratch);
 	THCHECK(S.part.ensure(2 * kBoundBlocks * sizeof(float4)));
 	hipLaunchKernelGGL(k_thin_bound, dim3(kBoundBlocks), dim3(256), 0, st, pos, n, S.part.as<float4>());
 	std::vector<float4> part(2 * kBoundBlocks);

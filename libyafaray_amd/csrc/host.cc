@@ -12,7 +12,9 @@
 #include <cstdlib>
 #include <ctime>
 #include <random>
+#include <set>
 #include <sstream>
+#include <thread>
 
 namespace yafamd
 {
@@ -20,9 +22,10 @@ namespace yafamd
 // ---------------------------------------------------------------------------------------------
 // Logger (include/common/logger.h:62-166)
 // ---------------------------------------------------------------------------------------------
-void Logger::log(int level, const std::string &msg)
+void Logger::log(int level, const std::string &msg, bool set_error)
 {
 	std::lock_guard<std::mutex> g(mtx_);
+	if(set_error) last_error_ = msg;
 	const std::time_t now = std::time(nullptr);
 	char tod[16];
 	std::strftime(tod, sizeof(tod), "%H:%M:%S", std::localtime(&now));
@@ -106,7 +109,140 @@ GpuRenderer *Scene::gpu()
 	return gpu_.get();
 }
 
-const KernelTimes &Scene::kernelTimes() { return gpu()->kernelTimes(); }
+GpuRenderer *Scene::member(int m) { return m == 0 ? gpu() : extra_[(size_t)m - 1].get(); }
+
+const KernelTimes &Scene::kernelTimes()
+{
+	if(kt_sum_) return *kt_sum_;
+	return gpu()->kernelTimes();
+}
+
+// The device group of this process (the analogue of the reference's render threads, scene.cc:547-610
+// and integrator_tiled.cc:246-264: there `threads` workers share the film's tiles; here one member per
+// GPU renders a row band of it).  Member 0 is the renderer on the caller's current device; a render
+// group over RCCL (one process per GPU) has exactly one member per process.
+bool Scene::syncMembers()
+{
+	if(!gpu()->ready()) return false;
+	const int count = GpuRenderer::deviceCount();
+	const int d0 = gpu()->device();
+	std::vector<int> devs;
+	if(gpu()->groupWorld() > 1) devs = {d0};
+	else if(!device_group.empty())
+	{
+		for(size_t m = 0; m < device_group.size(); ++m)
+		{
+			const int d = device_group[m] >= 0 ? device_group[m] : (int)((d0 + (int)m) % std::max(1, count));
+			if(d >= count)
+			{
+				log.error("Device group: device " + std::to_string(d) + " requested, " + std::to_string(count) + " visible");
+				return false;
+			}
+			devs.push_back(d);
+		}
+	}
+	else
+	{
+		int n = setup.gpus;
+		if(const char *e = getenv("YAFARAY_AMD_GPUS"); e && *e) n = atoi(e);
+		if(n <= 0 || n > count) n = count;
+		devs.push_back(d0);
+		for(int d = 0; d < count && (int)devs.size() < n; ++d)
+			if(d != d0) devs.push_back(d);
+	}
+	if(devs == member_devs_) return true;
+	extra_.clear();
+	if(devs[0] != d0)
+	{
+		if(gpu()->groupWorld() > 1)
+		{
+			log.error("Device group: a render-group member renders on its own device only");
+			return false;
+		}
+		gpu_.reset(new GpuRenderer(log, devs[0]));
+		if(!gpu_->ready()) return false;
+	}
+	for(size_t m = 1; m < devs.size(); ++m) extra_.emplace_back(new GpuRenderer(log, devs[m]));
+	{
+		const std::set<int> uniq(devs.begin(), devs.end());
+		GpuRenderer::enablePeerAccess(std::vector<int>(uniq.begin(), uniq.end()));
+	}
+	member_devs_ = devs;
+	geometry_dirty = true;   // every member holds its own copy of the scene
+	group_bounds.clear();
+	kt_sum_.reset();
+	if(devs.size() > 1)
+	{
+		std::ostringstream os;
+		os << "Device group: " << devs.size() << " members on devices";
+		for(int d : devs) os << " " << d;
+		log.info(os.str());
+	}
+	return true;
+}
+
+// One film rendered by every member of the device group, each on its own host thread (member 0 on
+// the caller's): row bands + halo rows; the members meet between adaptive passes and at the end,
+// where member 0 pulls every band over xGMI (GpuRenderer::renderMember / exchangeRows).
+bool Scene::renderDeviceGroup(RenderParams &rp)
+{
+	const int n = memberCount();
+	std::vector<GpuRenderer *> ms;
+	for(int m = 0; m < n; ++m) ms.push_back(member(m));
+	auto group = std::make_shared<PeerGroup>(ms);
+	std::vector<RenderParams> rps((size_t)n, rp);
+	std::vector<char> ok((size_t)n, 0);
+	for(int m = 0; m < n; ++m)
+	{
+		RenderParams &r = rps[(size_t)m];
+		r.shard_rank = m;
+		r.shard_y0 = rp.band_bounds[(size_t)m];
+		r.shard_y1 = rp.band_bounds[(size_t)m + 1];
+		if(m > 0)
+		{
+			// the client's callbacks run on the caller's thread only (member 0)
+			r.on_chunk = nullptr;
+			r.on_next_pass = nullptr;
+			r.on_tiles = nullptr;
+		}
+		ms[(size_t)m]->setPeers(group, m);
+	}
+	std::vector<std::thread> th;
+	for(int m = 1; m < n; ++m) th.emplace_back([&, m] { ok[(size_t)m] = ms[(size_t)m]->renderMember(rps[(size_t)m], &canceled) ? 1 : 0; });
+	ok[0] = ms[0]->renderMember(rps[0], &canceled) ? 1 : 0;
+	for(std::thread &t : th) t.join();
+	for(GpuRenderer *g : ms) g->setPeers(nullptr, 0);
+	// counters and per-kernel times summed over the members (GPU time), wall time of the slowest
+	yafaray_amd_stats_t st = ms[0]->stats();
+	if(!kt_sum_) kt_sum_.reset(new KernelTimes);
+	*kt_sum_ = ms[0]->kernelTimes();
+	for(int m = 1; m < n; ++m)
+	{
+		const yafaray_amd_stats_t &o = ms[(size_t)m]->stats();
+		st.closest_rays += o.closest_rays;
+		st.shadow_rays += o.shadow_rays;
+		st.node_visits += o.node_visits;
+		st.tri_tests += o.tri_tests;
+		st.samples += o.samples;
+		st.gather_visits += o.gather_visits;
+		st.trace_kernel_ms += o.trace_kernel_ms;
+		st.shade_kernel_ms += o.shade_kernel_ms;
+		st.nee_kernel_ms += o.nee_kernel_ms;
+		st.trace_launches += o.trace_launches;
+		st.render_seconds = std::max(st.render_seconds, o.render_seconds);
+		const KernelTimes &k = ms[(size_t)m]->kernelTimes();
+		for(int q = 0; q < KK_COUNT; ++q)
+		{
+			kt_sum_->ms[q] += k.ms[q];
+			kt_sum_->launches[q] += k.launches[q];
+			kt_sum_->items[q] += k.items[q];
+		}
+	}
+	group_stats_ = st;
+	for(char c : ok)
+		if(!c) return false;
+	return true;
+}
 
 // scene.cc:977-1004, object_mesh.cc:35-86
 bool Scene::createObject(const std::string &name, const ParamMap &p)
@@ -715,12 +851,14 @@ bool Scene::setupRender(const ParamMap &p)
 	p.get("AA_variance_pixels", s.aa_variance_pixels);
 	p.get("AA_clamp_samples", s.clamp_samples);
 	p.get("threads", s.threads);
+	p.get("gpus", s.gpus);
 	p.get("threads_photons", s.threads_photons);
 	p.get("adv_auto_shadow_bias_enabled", s.shadow_bias_auto);
 	p.get("adv_shadow_bias_value", s.shadow_bias);
 	p.get("adv_auto_min_raydist_enabled", s.ray_min_dist_auto);
 	p.get("adv_min_raydist_value", s.ray_min_dist);
 	p.get("adv_base_sampling_offset", s.base_sampling_offset);
+	p.get("adv_rr_seed", s.rr_seed);
 	p.get("adv_computer_node", s.computer_node);
 	p.get("film_load_save_mode", s.film_load_save_mode);
 	p.get("film_load_save_path", s.film_load_save_path);
@@ -753,6 +891,7 @@ bool Scene::setupRender(const ParamMap &p)
 
 bool Scene::buildAccelerator()
 {
+	if(!syncMembers()) return false;
 	// scene.cc:1032-1060 updateObjects: gather visible, non-base mesh primitives
 	std::vector<float> verts;
 	std::vector<int> tris, tri_mat;
@@ -886,7 +1025,8 @@ bool Scene::buildAccelerator()
 	for(auto &kv : lights) hs.lights.push_back(kv.second);
 	uint32_t base = 0;
 	for(DevLight &L : hs.lights) { L.nee_base = base; base += L.nee_count; }
-	if(!gpu()->upload(hs)) return false;
+	for(int m = 0; m < memberCount(); ++m)
+		if(!member(m)->upload(hs)) return false;
 	const auto t1 = std::chrono::steady_clock::now();
 	stats.build_seconds = std::chrono::duration<double>(t1 - t0).count();
 	std::ostringstream os;
@@ -928,6 +1068,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 	if(!setup.valid) { log.error("Scene: No ImageFilm present, bailing out..."); return false; }
 	if(views.empty()) { log.error("Scene: no render view defined"); return false; }
 	canceled = false;
+	if(!syncMembers()) return false;
 	if(geometry_dirty && !buildAccelerator()) return false;
 	const RenderSetup &s = setup;
 	const ParamMap &ip = integrators[s.integrator_name];
@@ -1148,7 +1289,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		S.ray_min_dist = s.ray_min_dist;
 		S.base_offset = (uint32_t)s.base_sampling_offset;
 		S.clamp_samples = s.clamp_samples;
-		S.rr_seed = 0;
+		S.rr_seed = (uint32_t)s.rr_seed;
 		uint32_t nee_all = 0, nee_max_one = 1;
 		for(auto &kv : lights)
 		{
@@ -1190,24 +1331,36 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		rp.shard_mode = shard_mode;
 		rp.shard_y0 = shard_y0;
 		rp.shard_y1 = shard_y1;
+		// Several GPUs render this film: the render group (one process per GPU, RCCL) or the device
+		// group of this process (one host thread per GPU).  Each member renders its row band (+ halo
+		// rows); the members exchange the accumulated film between adaptive passes and combine the
+		// bands at the end (GpuRenderer::renderMember).
 		const int group_world = gpu()->groupWorld();
-		if(group_world > 1)
+		const int n_members = memberCount();
+		const int world = group_world > 1 ? group_world : n_members;
+		const bool grouped = world > 1;
+		if(grouped)
 		{
-			// render group: this member renders its row band (+ halo rows), groupCombine below
-			// all-gathers the bands over RCCL into every member's film
-			if((int)group_bounds.size() != group_world + 1 || group_bounds.back() != s.height) group_bounds = equalBands(s.height, group_world);
-			rp.shard_world = group_world;
-			rp.shard_rank = gpu()->groupRank();
+			if((int)group_bounds.size() != world + 1 || group_bounds.back() != s.height) group_bounds = equalBands(s.height, world);
+			if(s.height < world)
+			{
+				log.error("Scene: the film has fewer rows than GPUs rendering it");
+				return false;
+			}
+			rp.shard_world = world;
+			rp.shard_rank = group_world > 1 ? gpu()->groupRank() : 0;
 			rp.shard_mode = 2;
+			rp.band_bounds = group_bounds;
 			rp.shard_y0 = group_bounds[rp.shard_rank];
 			rp.shard_y1 = group_bounds[rp.shard_rank + 1];
+			rp.combine_all = group_world > 1;
 		}
 		rp.aa.passes = std::max(1, s.aa_passes);
-		if(rp.aa.passes > 1 && rp.shard_world > 1)
+		if(rp.aa.passes > 1 && rp.shard_world > 1 && !grouped)
 		{
-			// nextPass compares neighbouring pixels across the whole film; the tile-row shards only
-			// hold their own rows
-			log.error("Scene: AA_passes > 1 with the film sharded over several GPUs is not supported");
+			// nextPass compares neighbouring pixels across the whole film; a caller-side shard
+			// (setTileRowShard / setRowBandShard) only holds its own rows and has no exchange
+			log.error("Scene: AA_passes > 1 with a caller-sharded film is not supported (use a render or device group)");
 			return false;
 		}
 		rp.aa.inc_samples = s.aa_inc_samples;
@@ -1247,11 +1400,15 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		film_io.cy0 = s.ystart;
 		film_io.cy1 = s.ystart + s.height;
 		const std::string film_file = filmio::filmPath(s.film_load_save_path, s.computer_node);
-		if(fmode != filmio::None && rp.shard_world > 1)
+		if(fmode != filmio::None && rp.shard_world > 1 && !grouped)
 		{
-			log.error("Scene: film load/save with the film sharded over several GPUs is not supported");
+			log.error("Scene: film load/save with a caller-sharded film is not supported (use a render or device group)");
 			return false;
 		}
+		// a group render combines the accumulators too (the film file is saved from them); in a render
+		// group only member 0 writes the files, every member reads them
+		rp.combine_accum = fmode != filmio::None;
+		const bool io_member = group_world <= 1 || gpu()->groupRank() == 0;
 		if(fmode == filmio::LoadAndSave)
 		{
 			film_io.weights.assign((size_t)s.width * s.height, 0.f);
@@ -1267,7 +1424,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 				log.info(itype + ": Combining ImageFilm files, skipping pass 1...");
 			}
 		}
-		if(fmode != filmio::None) filmio::backup(log, film_file);
+		if(fmode != filmio::None && io_member) filmio::backup(log, film_file);
 		auto saveFilm = [&]() {
 			filmio::Film out = film_io;
 			out.sampling_offset = gpu()->samplingOffset();
@@ -1276,7 +1433,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		int autosave_passes = 0;
 		const auto autosave_t0 = std::chrono::steady_clock::now();
 		auto autosave_last = autosave_t0;
-		if(fmode != filmio::None && s.film_autosave_interval_type != "none")
+		if(fmode != filmio::None && io_member && s.film_autosave_interval_type != "none")
 			rp.on_next_pass = [&](bool skipped) {
 				++autosave_passes;
 				if(skipped) return;
@@ -1299,7 +1456,10 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		rp.tile_rank.assign(order.size(), 0u);
 		for(size_t k = 0; k < order.size(); ++k) rp.tile_rank[(size_t)order[k]] = (uint32_t)k;
 		const bool tile_cbs = !quiet && (cb.put_pixel || cb.flush_area || cb.highlight_area);
-		if(tile_cbs)
+		// per-tile callbacks with the one-thread partial film inside the render (one GPU); a group or
+		// caller-sharded render reports the tiles after the film is complete (below)
+		const bool tiles_in_render = tile_cbs && rp.shard_world == 1;
+		if(tiles_in_render)
 		{
 			// ImageFilm::nextArea / finishArea per tile in render order (imagefilm.cc:447-568):
 			// highlightArea, putPixel over the tile (rows, then columns) with the values the one-thread
@@ -1335,16 +1495,27 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 				progress(n_pix, (int)((double)n_pix * (double)done / (double)std::max<uint64_t>(1, total)), "Rendering...", progress_data);
 			};
 		}
-		if(!gpu()->render(rp, &canceled)) return false;
-		if(group_world > 1)
+		bool ok;
+		if(!grouped)
 		{
-			std::vector<double> all_ms;
-			if(!gpu()->groupCombine(group_bounds, gpu()->stats().render_seconds * 1e3, all_ms)) return false;
-			group_bounds = rebalanceBands(group_bounds, all_ms, 0);
+			kt_sum_.reset();
+			ok = gpu()->render(rp, &canceled);
 		}
-		if(fmode != filmio::None) saveFilm();
+		else if(group_world > 1)
+		{
+			kt_sum_.reset();
+			ok = gpu()->renderMember(rp, &canceled);
+		}
+		else ok = renderDeviceGroup(rp);
+		if(!ok) return false;
+		if(grouped)
+		{
+			const std::vector<double> &ms = gpu()->memberMs();
+			if((int)ms.size() == world) group_bounds = rebalanceBands(group_bounds, ms, 0);
+		}
+		if(fmode != filmio::None && io_member) saveFilm();
 		const double build = stats.build_seconds;
-		stats = gpu()->stats();
+		stats = (grouped && group_world <= 1) ? group_stats_ : gpu()->stats();
 		stats.build_seconds = build;
 		film_on_gpu_only = quiet;
 		if(quiet) continue;
@@ -1362,6 +1533,26 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			for(const auto &r : owned) if(y >= r.first && y < r.second) return true;
 			return false;
 		};
+		if(tile_cbs && !tiles_in_render)
+		{
+			// ImageFilm::nextArea / finishArea of every tile this process owns, in render order, after the
+			// group combined the film (the put-pixel values follow in the flush below)
+			const int ntx = (s.width + s.tile_size - 1) / s.tile_size, n_pix = s.width * s.height;
+			int done_px = 0;
+			for(size_t k = 0; k < order.size(); ++k)
+			{
+				const int tx = (order[k] % ntx) * s.tile_size, ty = (order[k] / ntx) * s.tile_size;
+				const int x1 = std::min(s.width, tx + s.tile_size), y1 = std::min(s.height, ty + s.tile_size);
+				int oy0 = y1, oy1 = ty;
+				for(int y = ty; y < y1; ++y)
+					if(ownedRow(y)) { oy0 = std::min(oy0, y); oy1 = std::max(oy1, y + 1); }
+				if(oy1 <= oy0) continue;
+				if(cb.highlight_area) cb.highlight_area(view.first.c_str(), (int)k, tx, oy0, x1, oy1, cb.highlight_area_data);
+				if(cb.flush_area) cb.flush_area(view.first.c_str(), (int)k, tx, oy0, x1, oy1, cb.flush_area_data);
+				done_px += (x1 - tx) * (oy1 - oy0);
+				if(progress) progress(n_pix, done_px, "Rendering...", progress_data);
+			}
+		}
 		if(cb.put_pixel)
 			for(int y = 0; y < s.height; ++y)
 			{

@@ -75,8 +75,9 @@ class Logger
 		void setLogLevel(int l) { log_level_ = l; }
 		void setPrintDateTime(bool b) { print_datetime_ = b; }
 		void setColors(bool b) { colors_ = b; }
-		void log(int level, const std::string &msg);
-		void error(const std::string &m) { log(YAFARAY_LOG_LEVEL_ERROR, m); last_error_ = m; }
+		void log(int level, const std::string &msg, bool set_error = false);
+		// thread-safe: the members of a device group log from their own threads
+		void error(const std::string &m) { log(YAFARAY_LOG_LEVEL_ERROR, m, true); }
 		void warning(const std::string &m) { log(YAFARAY_LOG_LEVEL_WARNING, m); }
 		void params(const std::string &m) { log(YAFARAY_LOG_LEVEL_PARAMS, m); }
 		void info(const std::string &m) { log(YAFARAY_LOG_LEVEL_INFO, m); }
@@ -84,7 +85,11 @@ class Logger
 		void debug(const std::string &m) { log(YAFARAY_LOG_LEVEL_DEBUG, m); }
 		bool isDebug() const { return console_level_ >= YAFARAY_LOG_LEVEL_DEBUG || log_level_ >= YAFARAY_LOG_LEVEL_DEBUG; }
 		const std::string &lastError() const { return last_error_; }
-		void clearError() { last_error_.clear(); }
+		void clearError()
+		{
+			std::lock_guard<std::mutex> g(mtx_);
+			last_error_.clear();
+		}
 
 	private:
 		yafaray_LoggerCallback_t cb_;
@@ -144,9 +149,17 @@ struct RenderSetup
 	int tile_size = 32;
 	std::string tiles_order = "centre";
 	int threads = -1, threads_photons = -1;
+	// GPUs of this process that render the film together (the device group, one host thread and
+	// HIP stream per GPU, row bands combined over xGMI): -1 = every visible device, as the
+	// reference's threads = -1 uses every core (scene.cc:547-610); YAFARAY_AMD_GPUS overrides
+	int gpus = -1;
 	bool shadow_bias_auto = true, ray_min_dist_auto = true;
 	float shadow_bias = 0.0005f, ray_min_dist = 0.00005f;
 	int base_sampling_offset = 0, computer_node = 0;
+	// GPU-core extension: seed of the per-sample Russian-roulette generators (the reference seeds one
+	// per tile from rand(), integrator_tiled.cc:272 — matched statistically; the seed lets the parity
+	// checks draw independent RR streams)
+	int rr_seed = 0;
 	// film load/save (imagefilm.cc:55-118)
 	std::string film_load_save_mode = "none", film_load_save_path = "./", film_autosave_interval_type = "none";
 	int film_autosave_interval_passes = 1;
@@ -168,6 +181,7 @@ struct Callbacks
 
 class GpuRenderer;
 struct KernelTimes;
+struct RenderParams;
 struct HostImage;
 struct HostTexture;
 
@@ -199,7 +213,10 @@ class Scene
 		bool geometry_dirty = true;
 		int shard_rank = 0, shard_world = 1, shard_mode = 1;
 		int shard_y0 = 0, shard_y1 = 0;   // shard_mode 2: explicit row band
-		std::vector<int> group_bounds;    // render group: row-band boundaries of the members (rebalanced per frame)
+		std::vector<int> group_bounds;    // render / device group: row-band boundaries of the members (rebalanced per frame)
+		// explicit device group (yafaray_amd_setDeviceGroup): the device of each member (-1: device of
+		// member 0 + m, modulo the visible devices); empty: the "gpus" render parameter decides
+		std::vector<int> device_group;
 		int chunk_slots = 1 << 26;   // samples in flight per wavefront chunk (64 M: the C2 frame in two chunks)
 		bool profile_kernels = false;
 		volatile bool canceled = false;
@@ -223,8 +240,11 @@ class Scene
 		bool setupRender(const ParamMap &p);
 		bool render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, void *progress_data, bool quiet);
 		bool buildAccelerator();
-		GpuRenderer *gpu();
-		const KernelTimes &kernelTimes();   // per-kernel timing of the last profiled render
+		GpuRenderer *gpu();                 // member 0 (holds the film, serves the ray seam)
+		int memberCount() const { return 1 + (int)extra_.size(); }
+		GpuRenderer *member(int m);
+		bool syncMembers();                 // (re)create the device group's members for the current settings
+		const KernelTimes &kernelTimes();   // per-kernel timing of the last profiled render (summed over members)
 
 		// film of the last render
 		std::vector<float> film_rgba, film_weights;
@@ -233,7 +253,12 @@ class Scene
 		yafaray_amd_stats_t stats{};
 
 	private:
+		bool renderDeviceGroup(RenderParams &rp);
 		std::unique_ptr<GpuRenderer> gpu_;
+		std::vector<std::unique_ptr<GpuRenderer>> extra_;   // device group members 1..
+		std::vector<int> member_devs_;                      // devices of the current members
+		std::unique_ptr<KernelTimes> kt_sum_;
+		yafaray_amd_stats_t group_stats_{};                 // counters of the last device-group render
 };
 
 class Interface

@@ -68,18 +68,23 @@ struct PkdScratch
 			b->release();
 	}
 };
-PkdScratch g_pkd;
 
 #define PKCHECK(x) do { hipError_t e_ = (x); if(e_ != hipSuccess) return e_; } while(0)
 
 } // namespace
 
+// The build scratch belongs to the caller (one per renderer, so per device): *scratch is created on
+// the first build and reused; yafamd_pkd_scratch_free releases it.
+extern "C" void yafamd_pkd_scratch_free(void *scratch) { delete static_cast<PkdScratch *>(scratch); }
+
 // pos_dev: n photons (position in .xyz); nodes_dev: 2n - 1 nodes (uint4, see the header comment).
 // *depth_out: deepest level (root = 0) — the lookup stack needs depth + 1 entries.
-extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st)
+extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch)
 {
 	if(n == 0) return hipSuccess;
-	PkdScratch &S = g_pkd;
+	if(!scratch) return hipErrorInvalidValue;
+	if(!*scratch) *scratch = new PkdScratch;
+	PkdScratch &S = *static_cast<PkdScratch *>(*scratch);
 	const uint32_t B = 256, G = (n + B - 1) / B;
 	for(DevBuf *b : {&S.kx, &S.ky, &S.kz, &S.iota, &S.sorted_keys, &S.sorted_idx, &S.seg_of}) PKCHECK(b->ensure((size_t)n * 4));
 	PKCHECK(S.scan.ensure(((size_t)n + 1) * 4));
@@ -162,10 +167,12 @@ extern "C" uint32_t yafamd_pkd_check_error()
 	return e;
 }
 // checked build only: the three record lists as the subtree phase saw them (3 x n uint4)
-extern "C" hipError_t yafamd_pkd_check_lists(uint4 *host, uint32_t n)
+extern "C" hipError_t yafamd_pkd_check_lists(void *scratch, uint4 *host, uint32_t n)
 {
+	if(!scratch) return hipErrorInvalidValue;
+	PkdScratch &S = *static_cast<PkdScratch *>(scratch);
 	for(int a = 0; a < 3; ++a)
-		PKCHECK(hipMemcpy(host + (size_t)a * n, g_pkd.rec[a].p, (size_t)n * 16, hipMemcpyDeviceToHost));
+		PKCHECK(hipMemcpy(host + (size_t)a * n, S.rec[a].p, (size_t)n * 16, hipMemcpyDeviceToHost));
 	return hipSuccess;
 }
 #endif

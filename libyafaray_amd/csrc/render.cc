@@ -54,25 +54,44 @@ hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *
 hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
                             float4 *out_pos, float4 *out_dir, float *out_colb, hipStream_t st);
 hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out, uint32_t *n_kept,
-                                  int *rounds_out, hipStream_t st);
+                                  int *rounds_out, hipStream_t st, void **scratch);
+void yafamd_thin_scratch_free(void *scratch);
 hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid,
                             hipStream_t st);
 size_t yafamd_gather_lanes(const DevScene *S);
 hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
                                 int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st);
-hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st);
+hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch);
+void yafamd_pkd_scratch_free(void *scratch);
 hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix, uint8_t *flags,
                                     hipStream_t st);
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, const uint8_t *flags, float4 *accum, float4 *out,
                               float *weights, int y0, int y1, float clamp_samples, int accumulate, hipStream_t st);
 hipError_t yafamd_aa_next_pass(const float4 *accum, const float *weights, int W, int H, int tile, const DevAaParams *prm,
-                               float threshold, uint8_t *flags, uint32_t *plist, uint32_t *count, hipStream_t st);
+                               float threshold, uint8_t *flags, uint32_t *plist, uint32_t *count, int ry0, int ry1, uint32_t *local_count,
+                               hipStream_t st);
 hipError_t yafamd_launch_trace_rays(const DevScene *S, int any, const float4 *ro, const float4 *rd, int n, float *t_out,
                                     int *prim_out, int stack_depth, hipStream_t st);
 }
 
 namespace
 {
+
+// The renderer's device made current for the duration of a call; the caller's device is restored
+// (several renderers of one process, on different devices, may be driven from one thread).
+struct DeviceGuard
+{
+	int prev = -1;
+	bool set = false;
+	explicit DeviceGuard(int dev)
+	{
+		if(dev >= 0 && hipGetDevice(&prev) == hipSuccess && prev != dev) set = hipSetDevice(dev) == hipSuccess;
+	}
+	~DeviceGuard()
+	{
+		if(set) (void)hipSetDevice(prev);
+	}
+};
 
 struct Buf
 {
@@ -240,7 +259,9 @@ struct GpuRenderer::Impl
 	uint32_t n_rad_points = 0;
 	// render group (RCCL communicator over the group's GPUs) and its exchange buffers
 	ncclComm_t comm = nullptr;
-	Buf g_send, g_recv, g_wsend, g_wrecv, g_times;
+	Buf g_send, g_recv, g_wsend, g_wrecv, g_times, g_status;
+	// scratch of the photon kd-tree build (pkd.hip) and of the radiance-point thinning (fgthin.hip)
+	void *pkd_scratch = nullptr, *thin_scratch = nullptr;
 	std::vector<DevLight> host_lights;   // as uploaded (light sample multiplier passes rewrite the device copy)
 	std::vector<DevLight> pass_lights;   // staging of the current pass's copy (alive until the stream syncs)
 	int n_photons = 0, pm_paths = 0, pm_stack = 0;
@@ -310,7 +331,9 @@ struct GpuRenderer::Impl
 		              &weights, &jobs, &counters, &stats, &accum, &aa_flags, &aa_plist})
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
-		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times}) b->release();
+		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
+		yafamd_pkd_scratch_free(pkd_scratch);
+		yafamd_thin_scratch_free(thin_scratch);
 		if(comm) (void)ncclCommDestroy(comm);
 		for(hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
 		if(stream) (void)hipStreamDestroy(stream);
@@ -339,8 +362,40 @@ struct GpuRenderer::Impl
 		d_->profEnd(kind, e0_);                                                                                \
 	} while(0)
 
-GpuRenderer::GpuRenderer(Logger &log) : d_(new Impl), log_(log) {}
-GpuRenderer::~GpuRenderer() { delete d_; }
+GpuRenderer::GpuRenderer(Logger &log, int device) : d_(new Impl), log_(log), device_(device) {}
+GpuRenderer::~GpuRenderer()
+{
+	DeviceGuard g(device_);
+	delete d_;
+}
+
+void *GpuRenderer::d_comm() const { return (void *)d_->comm; }
+
+int GpuRenderer::deviceCount()
+{
+	int n = 0;
+	return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+int GpuRenderer::currentDevice()
+{
+	int d = 0;
+	return hipGetDevice(&d) == hipSuccess ? d : 0;
+}
+
+void GpuRenderer::enablePeerAccess(const std::vector<int> &devices)
+{
+	// direct loads / copies between the group's GPUs over xGMI (hipMemcpyPeer works without it, staged)
+	for(int a : devices)
+		for(int b : devices)
+		{
+			if(a == b) continue;
+			int can = 0;
+			if(hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+			DeviceGuard g(a);
+			if(hipDeviceEnablePeerAccess(b, 0) != hipSuccess) (void)hipGetLastError();   // already enabled
+		}
+}
 
 bool GpuRenderer::ready()
 {
@@ -352,9 +407,15 @@ bool GpuRenderer::ready()
 		log_.error("GPU: no HIP device available — the MI355X core has no CPU fallback");
 		return false;
 	}
+	if(device_ >= n)
+	{
+		log_.error("GPU: device " + std::to_string(device_) + " requested, " + std::to_string(n) + " visible");
+		return false;
+	}
+	if(device_ < 0) HIPCHECK(hipGetDevice(&device_));
+	DeviceGuard guard(device_);
 	HIPCHECK(hipStreamCreateWithFlags(&d_->stream, hipStreamNonBlocking));
-	int dev = 0;
-	HIPCHECK(hipGetDevice(&dev));
+	int dev = device_;
 	hipDeviceProp_t prop;
 	HIPCHECK(hipGetDeviceProperties(&prop, dev));
 	d_->n_cu = prop.multiProcessorCount;
@@ -395,6 +456,7 @@ static bool ensure(Logger &log_, Buf &b, size_t bytes)
 bool GpuRenderer::upload(HostScene &hs)
 {
 	if(!ready()) return false;
+	DeviceGuard guard(device_);
 	Impl &d = *d_;
 	if(hs.gpu_build)
 	{
@@ -669,7 +731,7 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	// point kd-tree of the map, built on the GPU node for node like the reference's (pkd.hip)
 	if(!ensure(log_, nodes, (2 * (size_t)n - 1) * sizeof(uint4))) return false;
 	int depth = 0;
-	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)pos.p, n, (uint4 *)nodes.p, &depth, d.stream));
+	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)pos.p, n, (uint4 *)nodes.p, &depth, d.stream, &d.pkd_scratch));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	depth_out = depth;
 	stats_.photon_tree_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
@@ -696,7 +758,7 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	const bool host_thin = thin_env && std::string(thin_env) == "host";
 	const hipError_t te = host_thin ? hipErrorNotSupported
 	                                : yafamd_thin_rad_points((const float4 *)d.radc_a.p, (const float4 *)d.radc_b.p, nr, maxrad,
-	                                                         (uint32_t *)d.rad_kept.p, &nk, &rounds, d.stream);
+	                                                         (uint32_t *)d.rad_kept.p, &nk, &rounds, d.stream, &d.thin_scratch);
 	if(te == hipErrorNotSupported)
 	{
 		std::vector<float4> pos(nr), nrm(nr);
@@ -736,7 +798,7 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	                                    (const uint32_t *)d.rad_kept.p, nk, (float4 *)d.rph_pos.p, (float4 *)d.rph_dir.p, (float *)d.rph_colb.p,
 	                                    d.stream));
 	int depth = 0;
-	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)d.rph_pos.p, nk, (uint4 *)d.rpk_nodes.p, &depth, d.stream));
+	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)d.rph_pos.p, nk, (uint4 *)d.rpk_nodes.p, &depth, d.stream, &d.pkd_scratch));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	d.n_rphotons = (int)nk;
 	stats_.fg_radiance_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
@@ -851,7 +913,15 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 {
 	if(!ready()) return false;
+	DeviceGuard guard(device_);
 	Impl &d = *d_;
+	// a group render: the members meet between adaptive passes (status + accumulator exchange)
+	const bool group_render = !rp.band_bounds.empty() && grouped();
+	if(group_render && ((int)rp.band_bounds.size() != rp.shard_world + 1 || rp.shard_mode != 2))
+	{
+		log_.error("GPU group: band bounds do not match the group");
+		return false;
+	}
 	DevScene &S = rp.scene;
 	fillScenePointers(d, S);
 	stats_.photons = 0;
@@ -1280,10 +1350,31 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		float threshold = rp.aa.threshold, sample_multiplier = 1.f, light_multiplier = 1.f;
 		bool threshold_changed = true;
 		int acum = spp, resampled = 0;
+		int resampled_local = 0;   // of them in this member's rows (+ halo rows): the pixels it renders
 		const int floor_pixels = (int)floorf(rp.aa.resampled_floor * (float)(W * H) / 100.f);
 		for(int pass = 1; pass < passes; ++pass)
 		{
-			if(canceled && *canceled) break;
+			if(group_render && fault_pass_ == pass)
+			{
+				log_.error("GPU group: injected failure of member " + std::to_string(rp.shard_rank) + " at pass " + std::to_string(pass + 1));
+				return false;
+			}
+			if(group_render)
+			{
+				// every member's film of the last pass is complete: agree on going on (a member that was
+				// canceled or failed stops everyone here), then every member assembles the whole accumulated
+				// film — nextPass compares pixels with their neighbours across band boundaries
+				HIPCHECK(hipStreamSynchronize(d.stream));
+				const int st = groupStatus((canceled && *canceled) ? 1 : 0);
+				if(st >= 2)
+				{
+					log_.error("GPU group: a member failed; render abandoned");
+					return false;
+				}
+				if(st == 1) break;
+				if(!exchangeRows(rp.band_bounds, XR_ACCUM, true)) return false;
+			}
+			else if(canceled && *canceled) break;
 			sample_multiplier *= rp.aa.sample_multiplier_factor;
 			light_multiplier *= rp.aa.light_sample_multiplier_factor;
 			if(light_mult)
@@ -1302,10 +1393,19 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			if(skip) {}   // nextPass(..., skipNextPass = true)
 			else
 			{
-				uint32_t count = 0;
+				// the flags of the whole film; the pixel list restricted to the rows whose samples this
+				// member's film rows gather (its band + halo rows)
+				uint32_t count = 0, local = 0;
+				int ry0 = 0, ry1 = H;
+				if(group_render)
+				{
+					ry0 = std::max(0, rp.shard_y0 - rp.film.reach_fwd);
+					ry1 = std::min(H, rp.shard_y1 + rp.film.reach_back);
+				}
 				PROF(KK_AA, yafamd_aa_next_pass((const float4 *)d.accum.p, (const float *)d.weights.p, W, H, ts, &rp.aa.dev, threshold,
-				                             (uint8_t *)d.aa_flags.p, (uint32_t *)d.aa_plist.p, &count, d.stream));
+				                             (uint8_t *)d.aa_flags.p, (uint32_t *)d.aa_plist.p, &count, ry0, ry1, &local, d.stream));
 				resampled = (int)count;
+				resampled_local = (int)local;
 				threshold_changed = false;
 				if(const char *dump = getenv("YAFARAY_AMD_AA_DUMP"); dump && *dump)
 				{
@@ -1333,17 +1433,27 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				S.plist = (const uint32_t *)d.aa_plist.p;
 				rp.film.spp = n_pass;
 				rp.film.sample_offset = S.base_offset + (uint32_t)acum;
-				const uint64_t n_total = (uint64_t)resampled * (uint64_t)n_pass;
+				const uint64_t n_total = (uint64_t)resampled_local * (uint64_t)n_pass;
 				if(!runSamples(n_total)) return false;
 				if(done < n_total)
-					HIPCHECK(yafamd_launch_done_flags(&S, (const DevJob *)d.jobs.p, n_jobs, (uint32_t)resampled, (uint32_t)(done / (uint64_t)n_pass),
+					HIPCHECK(yafamd_launch_done_flags(&S, (const DevJob *)d.jobs.p, n_jobs, (uint32_t)resampled_local, (uint32_t)(done / (uint64_t)n_pass),
 					                                  (uint8_t *)d.aa_flags.p, d.stream));
 				if(done == n_total && !emitTiles(passes_done_, (const uint8_t *)d.aa_flags.p, 1)) return false;
-				PROF(KK_FILM, yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (const uint8_t *)d.aa_flags.p, (float4 *)d.accum.p,
-				                            (float4 *)d.film.p, (float *)d.weights.p, 0, H, S.clamp_samples, 1, d.stream));
+				for(const auto &r : owned_rows_)
+					PROF(KK_FILM, yafamd_launch_film(&rp.film, (const float4 *)d.samples.p, (const uint8_t *)d.aa_flags.p, (float4 *)d.accum.p,
+					                            (float4 *)d.film.p, (float *)d.weights.p, r.first, r.second, S.clamp_samples, 1, d.stream));
 				samples_total += done / (uint64_t)n_pass * (uint64_t)n_pass;
 				sampling_offset_ = (uint32_t)(acum + n_pass);   // renderPass: setSamplingOffset(offset + samples), :244
-				if(done < n_total) break;   // canceled mid-pass
+				if(done < n_total)
+				{
+					// canceled mid-pass; a group member stops at the next status agreement, with the others
+					if(group_render)
+					{
+						acum += n_pass;
+						continue;
+					}
+					break;
+				}
 				++passes_done_;
 			}
 			acum += n_pass;
@@ -1424,6 +1534,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 
 bool GpuRenderer::download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h)
 {
+	DeviceGuard guard(device_);
 	Impl &d = *d_;
 	if(!d.film.p || w != d.film_w || h != d.film_h) { log_.error("GPU: no film to download"); return false; }
 	rgba.resize((size_t)w * h * 4);
@@ -1435,6 +1546,7 @@ bool GpuRenderer::download(std::vector<float> &rgba, std::vector<float> &weights
 
 bool GpuRenderer::downloadAccum(std::vector<float> &rgba, std::vector<float> &weights)
 {
+	DeviceGuard guard(device_);
 	Impl &d = *d_;
 	if(!d.accum.p || !d.weights.p) { log_.error("GPU: no film to download"); return false; }
 	rgba.resize((size_t)d.film_w * d.film_h * 4);
@@ -1447,6 +1559,7 @@ bool GpuRenderer::downloadAccum(std::vector<float> &rgba, std::vector<float> &we
 
 bool GpuRenderer::filmToDevice(void *dst, int y0, int y1)
 {
+	DeviceGuard guard(device_);
 	Impl &d = *d_;
 	if(!d.film.p || y0 < 0 || y1 > d.film_h || y1 < y0) { log_.error("GPU: bad film row range"); return false; }
 	const size_t row = (size_t)d.film_w * sizeof(float4);
@@ -1457,6 +1570,7 @@ bool GpuRenderer::filmToDevice(void *dst, int y0, int y1)
 bool GpuRenderer::traceRays(bool any, const float *rays, int n, float *t, int *prim)
 {
 	if(!ready()) return false;
+	DeviceGuard guard(device_);
 	Impl &d = *d_;
 	if(!d.nodes.p) { log_.error("GPU: no acceleration structure built"); return false; }
 	std::vector<float> o((size_t)n * 4), dd((size_t)n * 4);
@@ -1504,6 +1618,7 @@ bool GpuRenderer::traceRays(bool any, const float *rays, int n, float *t, int *p
 bool GpuRenderer::joinGroup(int rank, int world, const void *rccl_id, size_t id_bytes)
 {
 	if(!ready()) return false;
+	DeviceGuard guard(device_);
 	Impl &d = *d_;
 	if(d.comm)
 	{
@@ -1529,52 +1644,230 @@ bool GpuRenderer::joinGroup(int rank, int world, const void *rccl_id, size_t id_
 	return true;
 }
 
-bool GpuRenderer::groupCombine(const std::vector<int> &bounds, double render_ms, std::vector<double> &all_ms)
+int PeerGroup::arrive(int status)
+{
+	std::unique_lock<std::mutex> lk(mtx_);
+	cur_max_ = std::max(cur_max_, status);
+	if(++count_ == (int)members_.size())
+	{
+		last_max_ = cur_max_;
+		cur_max_ = 0;
+		count_ = 0;
+		++gen_;
+		cv_.notify_all();
+		return last_max_;
+	}
+	const int g = gen_;
+	cv_.wait(lk, [&] { return gen_ != g; });
+	// last_max_ stays valid: the next generation cannot complete before this member arrives again
+	return last_max_;
+}
+
+int GpuRenderer::groupStatus(int mine)
 {
 	Impl &d = *d_;
-	const int world = group_world_;
-	all_ms.assign((size_t)world, render_ms);
-	if(world <= 1 || !d.comm) return true;
+	int st = mine;
+	if(peers_ && peers_->size() > 1) st = peers_->arrive(mine);
+	else if(d.comm)
+	{
+		DeviceGuard guard(device_);
+		// the maximum over the members (RCCL all-reduce of one int)
+		if(!ensure(log_, d.g_status, 16)) st = 2;
+		else
+		{
+			int out = 2;
+			const bool ok = hipMemcpyAsync(d.g_status.p, &mine, sizeof(int), hipMemcpyHostToDevice, d.stream) == hipSuccess &&
+			                ncclAllReduce(d.g_status.p, (char *)d.g_status.p + 4, 1, ncclInt32, ncclMax, d.comm, d.stream) == ncclSuccess &&
+			                hipMemcpyAsync(&out, (char *)d.g_status.p + 4, sizeof(int), hipMemcpyDeviceToHost, d.stream) == hipSuccess &&
+			                hipStreamSynchronize(d.stream) == hipSuccess;
+			st = ok ? out : 2;
+			if(!ok) log_.error("GPU group: status all-reduce failed");
+		}
+	}
+	if(st >= 2) failure_seen_ = true;
+	return st;
+}
+
+void GpuRenderer::groupAbort()
+{
+	if(!failure_seen_ && grouped()) (void)groupStatus(2);
+	failure_seen_ = true;
+}
+
+bool GpuRenderer::exchangeRows(const std::vector<int> &bounds, int what, bool to_all)
+{
+	Impl &d = *d_;
+	DeviceGuard guard(device_);
 	const int W = d.film_w, H = d.film_h;
-	if((int)bounds.size() != world + 1 || bounds.back() != H) { log_.error("GPU group: band bounds do not cover the film"); return false; }
-	int max_rows = 1;
-	for(int r = 0; r < world; ++r) max_rows = std::max(max_rows, bounds[r + 1] - bounds[r]);
-	const size_t band_px = (size_t)max_rows * W;
+	const bool peer_mode = peers_ && peers_->size() > 1;
+	const int world = peer_mode ? peers_->size() : group_world_;
+	const int me = peer_mode ? peer_rank_ : group_rank_;
+	if(world <= 1) return true;
+	if((int)bounds.size() != world + 1 || bounds.front() != 0 || bounds.back() != H)
+	{
+		log_.error("GPU group: band bounds do not cover the film");
+		return false;
+	}
+	const size_t row4 = (size_t)W * sizeof(float4), row1 = (size_t)W * sizeof(float);
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	if(peer_mode)
+	{
+		// every member's buffers are final when all have arrived; the receivers pull the other bands
+		// (hipMemcpyPeer: xGMI between GPUs, a device copy between logical members of one GPU), and
+		// nobody touches its buffers again before the second arrival
+		peers_->arrive(0);
+		bool ok = true;
+		if(to_all || me == 0)
+			for(int r = 0; r < world && ok; ++r)
+			{
+				const int a = bounds[r], b = bounds[r + 1];
+				if(r == me || b <= a) continue;
+				GpuRenderer *src = peers_->member(r);
+				Impl &o = *src->d_;
+				auto pull = [&](void *dst, const void *sp, size_t row) {
+					return hipMemcpyPeerAsync((char *)dst + row * a, device_, (const char *)sp + row * a, src->device_, row * (b - a), d.stream) == hipSuccess;
+				};
+				if(what & XR_FILM) ok = ok && pull(d.film.p, o.film.p, row4);
+				if(what & XR_ACCUM) ok = ok && pull(d.accum.p, o.accum.p, row4);
+				if(what & (XR_FILM | XR_ACCUM)) ok = ok && pull(d.weights.p, o.weights.p, row1);
+			}
+		ok = ok && hipStreamSynchronize(d.stream) == hipSuccess;
+		if(!ok) log_.error("GPU group: band copy between members failed");
+		if(what & XR_TIMES)
+		{
+			member_ms_.assign((size_t)world, 0.0);
+			for(int r = 0; r < world; ++r) member_ms_[r] = peers_->member(r)->stats_.render_seconds * 1e3;
+		}
+		peers_->arrive(0);
+		if(ok && (to_all || me == 0)) owned_rows_.assign(1, {0, H});
+		return ok;
+	}
+	// RCCL: all-gather fixed-size band slots (bandPack / bandUnpack's plan) and scatter them into the film
+	const size_t band_px = (size_t)bandSlotRows(bounds) * W;
 	if(!ensure(log_, d.g_send, band_px * sizeof(float4)) || !ensure(log_, d.g_recv, band_px * world * sizeof(float4)) ||
 	   !ensure(log_, d.g_wsend, band_px * sizeof(float)) || !ensure(log_, d.g_wrecv, band_px * world * sizeof(float)) ||
 	   !ensure(log_, d.g_times, 2 * (size_t)world * sizeof(double)))
 		return false;
-	const int y0 = bounds[group_rank_], y1 = bounds[group_rank_ + 1];
-	const size_t row4 = (size_t)W * sizeof(float4), row1 = (size_t)W * sizeof(float);
-	if(y1 > y0)
+	const int y0 = bounds[me], y1 = bounds[me + 1];
+	const int kinds[2] = {XR_FILM, XR_ACCUM};
+	for(int kind : kinds)
 	{
-		HIPCHECK(hipMemcpyAsync(d.g_send.p, (char *)d.film.p + row4 * y0, row4 * (y1 - y0), hipMemcpyDeviceToDevice, d.stream));
-		HIPCHECK(hipMemcpyAsync(d.g_wsend.p, (char *)d.weights.p + row1 * y0, row1 * (y1 - y0), hipMemcpyDeviceToDevice, d.stream));
+		if(!(what & kind)) continue;
+		void *src4 = kind == XR_FILM ? d.film.p : d.accum.p;
+		if(y1 > y0)
+		{
+			HIPCHECK(hipMemcpyAsync(d.g_send.p, (char *)src4 + row4 * y0, row4 * (y1 - y0), hipMemcpyDeviceToDevice, d.stream));
+			HIPCHECK(hipMemcpyAsync(d.g_wsend.p, (char *)d.weights.p + row1 * y0, row1 * (y1 - y0), hipMemcpyDeviceToDevice, d.stream));
+		}
+		NCCLCHECK(ncclGroupStart());
+		NCCLCHECK(ncclAllGather(d.g_send.p, d.g_recv.p, band_px * 4, ncclFloat32, d.comm, d.stream));
+		NCCLCHECK(ncclAllGather(d.g_wsend.p, d.g_wrecv.p, band_px, ncclFloat32, d.comm, d.stream));
+		NCCLCHECK(ncclGroupEnd());
+		for(int r = 0; r < world; ++r)
+		{
+			const int a = bounds[r], b = bounds[r + 1];
+			if(b <= a || r == me) continue;
+			HIPCHECK(hipMemcpyAsync((char *)src4 + row4 * a, (char *)d.g_recv.p + (size_t)r * band_px * sizeof(float4), row4 * (b - a),
+			                        hipMemcpyDeviceToDevice, d.stream));
+			HIPCHECK(hipMemcpyAsync((char *)d.weights.p + row1 * a, (char *)d.g_wrecv.p + (size_t)r * band_px * sizeof(float), row1 * (b - a),
+			                        hipMemcpyDeviceToDevice, d.stream));
+		}
 	}
-	double *times = (double *)d.g_times.p;
-	HIPCHECK(hipMemcpyAsync(times, &render_ms, sizeof(double), hipMemcpyHostToDevice, d.stream));
-	NCCLCHECK(ncclGroupStart());
-	NCCLCHECK(ncclAllGather(d.g_send.p, d.g_recv.p, band_px * 4, ncclFloat32, d.comm, d.stream));
-	NCCLCHECK(ncclAllGather(d.g_wsend.p, d.g_wrecv.p, band_px, ncclFloat32, d.comm, d.stream));
-	NCCLCHECK(ncclAllGather(times, times + world, 1, ncclFloat64, d.comm, d.stream));
-	NCCLCHECK(ncclGroupEnd());
-	for(int r = 0; r < world; ++r)
+	if(what & XR_TIMES)
 	{
-		const int a = bounds[r], b = bounds[r + 1];
-		if(b <= a || r == group_rank_) continue;
-		HIPCHECK(hipMemcpyAsync((char *)d.film.p + row4 * a, (char *)d.g_recv.p + (size_t)r * band_px * sizeof(float4), row4 * (b - a),
-		                        hipMemcpyDeviceToDevice, d.stream));
-		HIPCHECK(hipMemcpyAsync((char *)d.weights.p + row1 * a, (char *)d.g_wrecv.p + (size_t)r * band_px * sizeof(float), row1 * (b - a),
-		                        hipMemcpyDeviceToDevice, d.stream));
+		double *times = (double *)d.g_times.p;
+		const double mine = stats_.render_seconds * 1e3;
+		HIPCHECK(hipMemcpyAsync(times, &mine, sizeof(double), hipMemcpyHostToDevice, d.stream));
+		NCCLCHECK(ncclAllGather(times, times + world, 1, ncclFloat64, d.comm, d.stream));
+		member_ms_.assign((size_t)world, 0.0);
+		HIPCHECK(hipMemcpyAsync(member_ms_.data(), times + world, sizeof(double) * world, hipMemcpyDeviceToHost, d.stream));
 	}
-	HIPCHECK(hipMemcpyAsync(all_ms.data(), times + world, sizeof(double) * world, hipMemcpyDeviceToHost, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	owned_rows_.assign(1, {0, H});
 	return true;
 }
 
+bool GpuRenderer::renderMember(RenderParams &rp, volatile bool *canceled)
+{
+	failure_seen_ = false;
+	member_ms_.clear();
+	// YAFARAY_AMD_FAULT_MEMBER=m[:p] (tests of the failure protocol): member m fails before rendering
+	// (p = 0, default) or at the start of adaptive pass p + 1
+	fault_pass_ = -1;
+	if(const char *e = getenv("YAFARAY_AMD_FAULT_MEMBER"); e && *e && atoi(e) == rp.shard_rank)
+	{
+		const char *c = std::strchr(e, ':');
+		fault_pass_ = c ? atoi(c + 1) : 0;
+		if(fault_pass_ == 0)
+		{
+			log_.error("GPU group: injected failure of member " + std::to_string(rp.shard_rank) + " before rendering");
+			groupAbort();
+			return false;
+		}
+	}
+	if(!render(rp, canceled))
+	{
+		groupAbort();
+		return false;
+	}
+	// the final status agreement: a failed member stops everyone, a canceled one still combines (the
+	// partial film, as a canceled one-GPU render)
+	const int st = groupStatus(0);
+	if(st >= 2)
+	{
+		log_.error("GPU group: a member failed; render abandoned");
+		return false;
+	}
+	const int what = XR_FILM | XR_TIMES | (rp.combine_accum ? XR_ACCUM : 0);
+	if(!exchangeRows(rp.band_bounds, what, rp.combine_all))
+	{
+		failure_seen_ = true;   // the exchange itself failed: no further agreement can be trusted
+		return false;
+	}
+	return true;
+}
+
 namespace yafamd
 {
+
+int bandSlotRows(const std::vector<int> &bounds)
+{
+	int rows = 1;
+	for(size_t r = 0; r + 1 < bounds.size(); ++r) rows = std::max(rows, bounds[r + 1] - bounds[r]);
+	return rows;
+}
+
+static bool bandsValid(const std::vector<int> &bounds, int H, int rank)
+{
+	const int world = (int)bounds.size() - 1;
+	if(world < 1 || rank < 0 || rank >= world || bounds.front() != 0 || bounds.back() != H) return false;
+	for(int r = 0; r < world; ++r)
+		if(bounds[r + 1] < bounds[r]) return false;
+	return true;
+}
+
+bool bandPack(const float *film, int W, int H, int ch, const std::vector<int> &bounds, int rank, float *send)
+{
+	if(!film || !send || W < 1 || ch < 1 || !bandsValid(bounds, H, rank)) return false;
+	const size_t row = (size_t)W * ch;
+	const int y0 = bounds[rank], y1 = bounds[rank + 1];
+	std::memset(send, 0, (size_t)bandSlotRows(bounds) * row * sizeof(float));
+	std::memcpy(send, film + row * y0, (size_t)(y1 - y0) * row * sizeof(float));
+	return true;
+}
+
+bool bandUnpack(const float *recv, int W, int H, int ch, const std::vector<int> &bounds, int rank, float *film)
+{
+	if(!film || !recv || W < 1 || ch < 1 || !bandsValid(bounds, H, rank)) return false;
+	const size_t row = (size_t)W * ch, slot = (size_t)bandSlotRows(bounds) * row;
+	for(int r = 0; r + 1 < (int)bounds.size(); ++r)
+	{
+		const int a = bounds[r], b = bounds[r + 1];
+		if(r == rank || b <= a) continue;
+		std::memcpy(film + row * a, recv + slot * r, (size_t)(b - a) * row * sizeof(float));
+	}
+	return true;
+}
 
 std::vector<int> equalBands(int height, int world)
 {

@@ -11,9 +11,12 @@
 #include "devscene.h"
 #include "host.h"
 
+#include <condition_variable>
 #include <cstdint>
-#include <string>
 #include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
 #include <vector>
 
 namespace yafamd
@@ -120,14 +123,52 @@ struct RenderParams
 	// pass's partial film (RGBA, W x H) — each pixel as the one-thread render shows it when its tile
 	// finishes.  Single GPU, uncanceled passes.
 	std::function<void(int pass, const std::vector<float> &partial)> on_tiles;
+	// Group render (the film split into contiguous row bands over the members of a device group or
+	// a render group, GpuRenderer::renderMember): the members' band boundaries (world + 1 rows; this
+	// member is shard_rank).  Empty: not a group render.  Between adaptive passes the members agree
+	// on their status and exchange the accumulated film rows (nextPass reads neighbouring pixels).
+	std::vector<int> band_bounds;
+	// final combine: every member receives the whole film (render group: each process owns a film)
+	// or only member 0 (device group: the scene's film lives on member 0)
+	bool combine_all = true;
+	// final combine also carries the unnormalised accumulators (film files are saved from them)
+	bool combine_accum = false;
+};
+
+class GpuRenderer;
+
+// Device group: the member renderers of ONE process (one per GPU, or several logical members on one
+// GPU for rehearsals) rendering one film.  Each member runs on its own host thread; they meet at
+// arrive(), a barrier that also agrees on a status (0 ok, 1 canceled, 2 failed: the maximum over the
+// members), and copy band rows from each other's device buffers (hipMemcpyPeer over xGMI) while
+// every member waits inside the exchange.
+class PeerGroup
+{
+	public:
+		explicit PeerGroup(std::vector<GpuRenderer *> members) : members_(std::move(members)) {}
+		int size() const { return (int)members_.size(); }
+		GpuRenderer *member(int m) const { return members_[(size_t)m]; }
+		int arrive(int status);
+
+	private:
+		std::vector<GpuRenderer *> members_;
+		std::mutex mtx_;
+		std::condition_variable cv_;
+		int count_ = 0, gen_ = 0, cur_max_ = 0, last_max_ = 0;
 };
 
 class GpuRenderer
 {
 	public:
-		explicit GpuRenderer(Logger &log);
+		// device: the HIP device of this renderer (-1: the calling thread's current device at first use).
+		// Every public method makes it current for its duration (and restores the caller's device).
+		explicit GpuRenderer(Logger &log, int device = -1);
 		~GpuRenderer();
 		bool ready();
+		int device() const { return device_; }
+		static int deviceCount();
+		static int currentDevice();
+		static void enablePeerAccess(const std::vector<int> &devices);
 		bool upload(HostScene &hs);   // fills hs.bvh's metadata when the BVH is built on the device
 		bool render(RenderParams &rp, volatile bool *canceled);
 		int lastPassCount() const { return passes_done_; }
@@ -148,9 +189,27 @@ class GpuRenderer
 		// come from rebalanceBands over the gathered times.  imagesplitter.cc:30-107 partitions the
 		// reference's film into tiles for threads; imagefilm.cc:997-1008 sums film files of nodes.
 		bool joinGroup(int rank, int world, const void *rccl_id, size_t id_bytes);
-		bool groupCombine(const std::vector<int> &bounds, double render_ms, std::vector<double> &all_ms);
 		int groupRank() const { return group_rank_; }
 		int groupWorld() const { return group_world_; }
+		// device group membership (one process): member `m` of `g` (null: none)
+		void setPeers(std::shared_ptr<PeerGroup> g, int m) { peers_ = std::move(g); peer_rank_ = m; }
+		bool grouped() const { return (d_comm() != nullptr) || (peers_ && peers_->size() > 1); }
+		// Render this member's band (rp.band_bounds, rp.shard_rank) and combine the bands: render() +
+		// the final status agreement + the band exchange; on failure the member still takes part in
+		// the next status agreement (with "failed") so that no member waits for it forever.
+		bool renderMember(RenderParams &rp, volatile bool *canceled);
+		// the members' render times (ms) of the last group render, in member order
+		const std::vector<double> &memberMs() const { return member_ms_; }
+		// Status agreement (every member calls it at the same point): the maximum of the members'
+		// statuses (0 ok, 1 canceled, 2 failed); a transport error counts as failed.
+		int groupStatus(int mine);
+		// Tell the others this member failed, unless a failure was already agreed on.
+		void groupAbort();
+		enum : int { XR_FILM = 1, XR_ACCUM = 2, XR_TIMES = 4 };
+		// Copy every other member's band rows of the chosen buffers into this member (to_all: every
+		// member receives; else member 0 only).  XR_FILM: normalised film + weights, XR_ACCUM:
+		// accumulators + weights, XR_TIMES: the members' render times (memberMs).
+		bool exchangeRows(const std::vector<int> &bounds, int what, bool to_all);
 		const yafaray_amd_stats_t &stats() const { return stats_; }
 		const KernelTimes &kernelTimes() const { return ktimes_; }
 		std::vector<std::pair<int, int>> ownedRows() const { return owned_rows_; }
@@ -158,8 +217,15 @@ class GpuRenderer
 		struct Impl;
 
 	private:
+		void *d_comm() const;
 		Impl *d_;
 		Logger &log_;
+		int device_ = -1;
+		std::shared_ptr<PeerGroup> peers_;
+		int peer_rank_ = 0;
+		bool failure_seen_ = false;   // a group status agreement of this render returned "failed"
+		int fault_pass_ = -1;         // failure injection (tests of the group protocol): fail at this pass
+		std::vector<double> member_ms_;
 		yafaray_amd_stats_t stats_{};
 		KernelTimes ktimes_{};
 		std::vector<std::pair<int, int>> owned_rows_;
@@ -175,5 +241,14 @@ class GpuRenderer
 // computes the same bounds from the same gathered times (libyafaray_amd/tiles.py mirrors it).
 std::vector<int> rebalanceBands(const std::vector<int> &bounds, const std::vector<double> &times, int cap_rows);
 std::vector<int> equalBands(int height, int world);
+
+// The render group's band exchange plan (GpuRenderer::exchangeRows does it with device copies and an
+// RCCL all-gather; the host twins below let tests run the same plan over gloo): member r sends its
+// rows [bounds[r], bounds[r + 1]) in a slot of bandSlotRows() rows (zero-padded), the all-gather
+// concatenates the slots in member order, every member copies the other members' rows back into
+// its film.  ch = floats per pixel (4: RGBA, 1: weights).
+int bandSlotRows(const std::vector<int> &bounds);
+bool bandPack(const float *film, int W, int H, int ch, const std::vector<int> &bounds, int rank, float *send);
+bool bandUnpack(const float *recv, int W, int H, int ch, const std::vector<int> &bounds, int rank, float *film);
 
 } // namespace yafamd

@@ -137,6 +137,7 @@ class Render:
     ray_min_dist_auto: bool = True
     ray_min_dist: float = 0.00005
     base_sampling_offset: int = 0
+    rr_seed: int = 0                        # GPU-core "adv_rr_seed" (the oracle's OracleScene rr_seed)
     computer_node: int = 0
     # film load/save (imagefilm.cc:55-118)
     film_load_save_mode: str = "none"       # "save" | "load-save"
@@ -661,6 +662,8 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetBool("adv_auto_min_raydist_enabled", r.ray_min_dist_auto)
     api.paramsSetFloat("adv_min_raydist_value", r.ray_min_dist)
     api.paramsSetInt("adv_base_sampling_offset", r.base_sampling_offset)
+    if r.rr_seed:
+        api.paramsSetInt("adv_rr_seed", r.rr_seed)
     api.paramsSetInt("adv_computer_node", r.computer_node)
     api.paramsSetString("film_load_save_mode", r.film_load_save_mode)
     api.paramsSetString("film_load_save_path", r.film_load_save_path)

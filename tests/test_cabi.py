@@ -120,3 +120,22 @@ def test_reference_clients_link_and_run(product, tmp_path, t):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-2000:]
     assert "symbol lookup error" not in out and "error while loading" not in out
+
+
+def test_get_stats_keeps_the_1_0_struct_size(product):
+    """yafaray_amd_getStats (LIBYAFARAY_AMD_1.0) writes only the 1.0 struct's bytes — a client built
+    against the 1.0 header allocates no more; getStatsEx copies min(size, sizeof) bytes."""
+    import ctypes as C
+    yi = product.Interface()
+    yi.createScene()
+    v1 = product.Stats.gather_visits.offset
+    buf = (C.c_ubyte * (C.sizeof(product.Stats) + 64))()
+    C.memset(buf, 0xA5, C.sizeof(buf))
+    yi.L.yafaray_amd_getStats(yi.h, C.cast(buf, C.POINTER(product.Stats)))
+    assert all(b == 0xA5 for b in bytes(buf)[v1:]), "getStats wrote past the 1.0 struct"
+    assert any(b != 0xA5 for b in bytes(buf)[:v1])
+    C.memset(buf, 0xA5, C.sizeof(buf))
+    n = yi.L.yafaray_amd_getStatsEx(yi.h, C.cast(buf, C.POINTER(product.Stats)), 24)
+    assert n == 24 and all(b == 0xA5 for b in bytes(buf)[24:])
+    assert yi.L.yafaray_amd_getStatsEx(yi.h, C.cast(buf, C.POINTER(product.Stats)), 1 << 20) == C.sizeof(product.Stats)
+    yi.close()

@@ -230,17 +230,21 @@ def test_path_gauss_filter_and_multichunk(product, oracle_built):
     assert ulp_diff(rgba, orgba).max() <= 4
 
 
-def test_path_RR_statistical(product, oracle_built):
-    spec = scenes.cornell(64, 64, spp=32, bounces=8, rr=True)
-    rgba, _, _ = product.render_spec(spec)
-    orgba, _, _ = oracle_built.OracleScene(spec, threads=8).render()
-    a = rgba[..., :3].reshape(8, 8, 8, 8, 3).mean((1, 3))
-    b = orgba[..., :3].reshape(8, 8, 8, 8, 3).mean((1, 3))
-    # per-block standard error from the pixel spread
-    s = np.sqrt(orgba[..., :3].reshape(8, 8, 8, 8, 3).var((1, 3)) / 64 * 2) + 1e-3
-    z = np.abs(a - b) / s
-    assert z.max() < 5.0, z.max()
-    assert abs(a.mean() - b.mean()) / b.mean() < 0.02
+@pytest.mark.parametrize("seed", [0, 7919])
+def test_path_RR_statistical(product, oracle_built, seed):
+    """Russian roulette on (the reference default): the GPU's per-sample RR streams against the
+    oracle's per-tile ones (integrator_path_tracer.cc:249-255, integrator_tiled.cc:272) — unbiased
+    means a paired global z of the difference image within 4 (oracle/stats.py), for two independent
+    seeds on both sides; no 8x8 block may stand out either."""
+    from oracle.stats import paired_z
+    spec = scenes.cornell(256, 256, spp=64, bounces=8, rr=True).with_render(rr_seed=seed)
+    rgba, w, _ = product.render_spec(spec)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=16, rr_seed=seed).render()
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    z = paired_z(rgba, orgba)
+    assert abs(z["mean_z"]) < 4.0, z
+    assert z["max_abs_block_z"] < 6.0, z
+    assert abs(z["mean_rel_diff"]) < 0.01, z
 
 
 def test_reference_client_test01_renders(tmp_path):

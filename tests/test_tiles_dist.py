@@ -145,3 +145,60 @@ def test_library_band_balancer_matches_python(product, world):
             assert lib == [int(v) for v in py], (lib, py)
             assert lib[0] == 0 and lib[-1] == H and all(b > a for a, b in zip(lib, lib[1:]))
             bounds = tiles_bounds = lib
+
+
+def _lib_band_worker(rank, world, port, image, weights, bounds, q):
+    """One render-group member on gloo running the LIBRARY's band plan (yafaray_amd_packBand /
+    unpackBands, the host twins of GpuRenderer::exchangeRows): it holds the film only in its own band
+    (NaN elsewhere), packs its slot, all-gathers, unpacks the other members' rows."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import libyafaray_amd as Y
+    film = np.full_like(image, np.nan)
+    wt = np.full_like(weights, np.nan)
+    y0, y1 = bounds[rank], bounds[rank + 1]
+    film[y0:y1] = image[y0:y1]
+    wt[y0:y1] = weights[y0:y1]
+    out = []
+    for arr in (film, wt):
+        send = torch.from_numpy(Y.pack_band(arr, bounds, rank))
+        parts = [torch.zeros_like(send) for _ in range(world)]
+        dist.all_gather(parts, send)
+        out.append(Y.unpack_bands(torch.cat(parts).numpy(), bounds, rank, arr))
+    q.put((rank, out[0], out[1]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_library_band_plan_over_gloo(product, oracle_built, world):
+    """The in-library render group's combine plan on CPU ranks: uneven (rebalanced) bands packed and
+    unpacked by libyafaray4.so around a gloo all-gather give every member the whole film, bit for bit."""
+    from libyafaray_amd import scenes
+    spec = scenes.cornell(96, 70, spp=2, bounces=3, rr=False)
+    image, weights, _ = oracle_built.OracleScene(spec, threads=4).render()
+    H = image.shape[0]
+    bounds = [H * r // world for r in range(world + 1)]
+    bounds = product.rebalance_bands(bounds, [1.0 + 0.8 * r for r in range(world)])
+    assert len(set(b - a for a, b in zip(bounds, bounds[1:]))) > 1, bounds
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lib_band_worker, args=(r, world, port, image, weights, bounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, film, wt in got:
+        assert np.array_equal(film.view(np.uint32), image.view(np.uint32)), rank
+        assert np.array_equal(wt.view(np.uint32), weights.view(np.uint32)), rank
+
+
+def test_library_band_plan_rejects_bad_bounds(product):
+    film = np.zeros((10, 4, 4), np.float32)
+    with pytest.raises(RuntimeError):
+        product.pack_band(film, [0, 5, 9], 0)       # does not end at the film height
+    with pytest.raises(RuntimeError):
+        product.pack_band(film, [0, 6, 5, 10], 1)   # bounds out of order

@@ -68,9 +68,12 @@ def positions(n, rng):
 def main():
     lib = ctypes.CDLL(os.path.join(HERE, "..", "libyafaray_amd", "pkd_check.so"))
     lib.yafamd_build_pkd.restype = ctypes.c_int
-    lib.yafamd_build_pkd.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
+    lib.yafamd_build_pkd.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_void_p)]
     lib.yafamd_pkd_check_error.restype = ctypes.c_uint32
-    lib.yafamd_pkd_check_lists.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    lib.yafamd_pkd_check_lists.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+    lib.yafamd_pkd_scratch_free.argtypes = [ctypes.c_void_p]
+    scratch = ctypes.c_void_p(None)   # the build scratch (caller-owned, reused across sizes)
     sizes = [int(a) for a in sys.argv[1:]] or [1, 2, 3, 255, 256, 257, 513, 1000, 30000, 60000]
     rng = np.random.default_rng(7)
     ok = True
@@ -82,11 +85,11 @@ def main():
         dnodes = torch.zeros((2 * n - 1, 4), dtype=torch.int32, device="cuda")
         torch.cuda.synchronize()
         depth = ctypes.c_int(0)
-        rc = lib.yafamd_build_pkd(dpos.data_ptr(), n, dnodes.data_ptr(), ctypes.byref(depth), None)
+        rc = lib.yafamd_build_pkd(dpos.data_ptr(), n, dnodes.data_ptr(), ctypes.byref(depth), None, ctypes.byref(scratch))
         torch.cuda.synchronize()
         err = lib.yafamd_pkd_check_error()
         lists = np.zeros((3, n, 4), np.uint32)
-        lib.yafamd_pkd_check_lists(lists.ctypes.data, n)
+        lib.yafamd_pkd_check_lists(scratch, lists.ctypes.data, n)
         keys = [okey(pos[:, a]) for a in range(3)]
         for a in range(3):
             o = np.lexsort((np.arange(n), keys[a]))
@@ -112,6 +115,7 @@ def main():
             leaves = got[(got[:, 3] & 3) == 3, 3] >> 2
             line += f" leaves_perm={np.array_equal(np.sort(leaves), np.arange(n))}"
         print(line, flush=True)
+    lib.yafamd_pkd_scratch_free(scratch)
     print("OK" if ok else "FAILED")
     sys.exit(0 if ok else 1)
 
