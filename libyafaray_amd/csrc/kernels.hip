@@ -2753,7 +2753,9 @@ struct PhotonArgs
 	DevScene S;
 	PhotonState P;
 	PhotonSet L;         // the shooting lights and the map kind (diffuse / caustic)
-	uint32_t n_photons;  // photon paths (rounded like the reference, :437)
+	uint32_t n_photons;  // photon paths of the whole map (rounded like the reference, :437)
+	uint32_t h0, n_local;   // this launch's photon ids [h0, h0 + n_local) (a group member's share); the
+	                        // path buffers and deposit slots are indexed by the local id h - h0
 	int max_bounces;
 	int bounce;          // k_photon_bounce: the bounce this launch traces
 	int cur;             // alive list read by this launch
@@ -2765,8 +2767,9 @@ struct PhotonArgs
 __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 {
 	const DevScene &S = A.S;
-	const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
-	bool ok = h < A.n_photons;
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;   // local id
+	const uint32_t h = A.h0 + i;                                 // photon id
+	bool ok = i < A.n_local;
 	V3 o = v3(0.f, 0.f, 0.f), d = o;
 	C3 pcol = c3(0.f);
 	if(ok)
@@ -2811,10 +2814,10 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 	const uint32_t j = waveAppend(ok, &A.P.n_alive[A.cur]);
 	if(ok)
 	{
-		A.P.alive[A.cur][j] = h;
-		A.P.ray_o[h] = f4(o, S.ray_min_dist);
-		A.P.ray_d[h] = f4(d, -1.f);
-		A.P.pcol[h] = f4(pcol, __uint_as_float(2u));   // caustic = false, direct = true
+		A.P.alive[A.cur][j] = i;
+		A.P.ray_o[i] = f4(o, S.ray_min_dist);
+		A.P.ray_d[i] = f4(d, -1.f);
+		A.P.pcol[i] = f4(pcol, __uint_as_float(2u));   // caustic = false, direct = true
 	}
 }
 
@@ -2882,14 +2885,15 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 	{
 		const uint32_t j = base + threadIdx.x;
 		bool cont = false;
-		uint32_t h = 0;
+		uint32_t i = 0, h = 0;   // local id, photon id
 		V3 new_o = v3(0.f, 0.f, 0.f), new_d = new_o;
 		C3 new_col = c3(0.f);
 		uint32_t new_flags = 0;
 		if(j < n)
 		{
-			h = A.P.alive[A.cur][j];
-			const float4 ro = A.P.ray_o[h], rd = A.P.ray_d[h], pc = A.P.pcol[h];
+			i = A.P.alive[A.cur][j];
+			h = A.h0 + i;
+			const float4 ro = A.P.ray_o[i], rd = A.P.ray_d[i], pc = A.P.pcol[i];
 			float t;
 			int prim;
 			if(traverse<false, WIDE>(C, xyz(ro), xyz(rd), ro.w, __builtin_huge_valf(), t, prim, visits, tests))
@@ -2914,13 +2918,13 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 				const bool store = A.L.caustic ? ((sp.flags & (B_DIFFUSE | B_GLOSSY)) && caustic) : ((sp.flags & B_DIFFUSE) && !caustic);
 				if(store)
 				{
-					const uint32_t slot = h * slots + (uint32_t)A.bounce;
+					const uint32_t slot = i * slots + (uint32_t)A.bounce;
 					A.P.dep_a[slot] = f4(sp.p, lcol.r);
 					A.P.dep_b[slot] = f4(wi, lcol.g);
 					A.P.dep_c[slot] = lcol.b;
 					A.P.dep_flag[slot] = 1;
 					// :184-193 radiance point (final gathering): normal faced to the photon, reflectivities
-					if(A.P.rad_flag && !A.L.caustic && fgRadSelect(slot))
+					if(A.P.rad_flag && !A.L.caustic && fgRadSelect(h * slots + (uint32_t)A.bounce))
 					{
 						const DevMaterial &m = S.mats[sp.mat];
 						const C3 refl = getReflectivity<EXT>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_REFLECT);
@@ -2972,10 +2976,10 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 		const uint32_t k = waveAppend(cont, &A.P.n_alive[nxt]);
 		if(cont)
 		{
-			A.P.alive[nxt][k] = h;
-			A.P.ray_o[h] = f4(new_o, S.ray_min_dist);
-			A.P.ray_d[h] = f4(new_d, -1.f);
-			A.P.pcol[h] = f4(new_col, __uint_as_float(new_flags));
+			A.P.alive[nxt][k] = i;
+			A.P.ray_o[i] = f4(new_o, S.ray_min_dist);
+			A.P.ray_d[i] = f4(new_d, -1.f);
+			A.P.pcol[i] = f4(new_col, __uint_as_float(new_flags));
 		}
 	}
 }
@@ -3921,32 +3925,37 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	return hipGetLastError();
 }
 
-hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, int max_bounces,
-                              hipStream_t st)
+// photon ids [h0, h0 + n_local) of a map of n_photons paths
+hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, uint32_t h0, uint32_t n_local,
+                              int max_bounces, hipStream_t st)
 {
 	PhotonArgs A;
 	A.S = *S;
 	A.P = *P;
 	A.L = *L;
 	A.n_photons = n_photons;
+	A.h0 = h0;
+	A.n_local = n_local;
 	A.max_bounces = max_bounces;
 	A.bounce = 0;
 	A.cur = 0;
 	A.stack_depth = 0;
 	A.spill = nullptr;
-	if(n_photons == 0) return hipSuccess;
-	hipLaunchKernelGGL(k_photon_emit, dim3((n_photons + 255) / 256), dim3(256), 0, st, A);
+	if(n_local == 0) return hipSuccess;
+	hipLaunchKernelGGL(k_photon_emit, dim3((n_local + 255) / 256), dim3(256), 0, st, A);
 	return hipGetLastError();
 }
 
-hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, int max_bounces,
-                                int bounce, int cur, int stack_depth, int *spill, int grid, hipStream_t st)
+hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, uint32_t h0,
+                                uint32_t n_local, int max_bounces, int bounce, int cur, int stack_depth, int *spill, int grid, hipStream_t st)
 {
 	PhotonArgs A;
 	A.S = *S;
 	A.P = *P;
 	A.L = *L;
 	A.n_photons = n_photons;
+	A.h0 = h0;
+	A.n_local = n_local;
 	A.max_bounces = max_bounces;
 	A.bounce = bounce;
 	A.cur = cur;

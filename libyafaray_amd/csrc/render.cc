@@ -40,10 +40,10 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
                              const DevCounters *cnt_next, hipStream_t st);
 int yafamd_nee_blocks_per_cu();
-hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, int max_bounces,
-                              hipStream_t st);
-hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, int max_bounces,
-                                int bounce, int cur, int stack_depth, int *spill, int grid, hipStream_t st);
+hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, uint32_t h0, uint32_t n_local,
+                              int max_bounces, hipStream_t st);
+hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, uint32_t h0,
+                                uint32_t n_local, int max_bounces, int bounce, int cur, int stack_depth, int *spill, int grid, hipStream_t st);
 hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev,
                                  float4 *pos, float4 *dir, float *colb, hipStream_t st);
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, float4 *samples,
@@ -255,6 +255,8 @@ struct GpuRenderer::Impl
 	Buf ph_pos, ph_dir, ph_colb, pk_nodes, pk_stack;
 	// final gathering: radiance points per deposit slot, compacted, kept (indices), the radiance map
 	Buf rad_a, rad_b, rad_c, rad_flag, radc_a, radc_b, radc_c, rad_kept, rph_pos, rph_dir, rph_colb, rpk_nodes;
+	// a group member's own segment of a photon map / of the radiance points before the concatenation
+	Buf seg_pos, seg_dir, seg_colb, seg_ra, seg_rb, seg_rc;
 	int n_rphotons = 0;
 	uint32_t n_rad_points = 0;
 	// render group (RCCL communicator over the group's GPUs) and its exchange buffers
@@ -265,6 +267,7 @@ struct GpuRenderer::Impl
 	std::vector<DevLight> host_lights;   // as uploaded (light sample multiplier passes rewrite the device copy)
 	std::vector<DevLight> pass_lights;   // staging of the current pass's copy (alive until the stream syncs)
 	int n_photons = 0, pm_paths = 0, pm_stack = 0;
+	uint32_t pm_local = 0;   // diffuse photon paths this member shot (its share in a group render)
 	int n_nodes = 0, n_tris = 0, n_mats = 0, n_lights = 0, depth = 0, stack_depth = 32, node_f4 = 4;
 	int lds_stack = 32;    // k_trace stack levels held in LDS; levels [lds_stack, stack_depth) spill to `spill`
 	Buf spill;
@@ -332,6 +335,9 @@ struct GpuRenderer::Impl
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
+		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
+		              &seg_dir, &seg_colb, &seg_ra, &seg_rb, &seg_rc})
+			b->release();
 		yafamd_pkd_scratch_free(pkd_scratch);
 		yafamd_thin_scratch_free(thin_scratch);
 		if(comm) (void)ncclCommDestroy(comm);
@@ -349,6 +355,17 @@ struct GpuRenderer::Impl
 			std::ostringstream os_;                                                                            \
 			os_ << "GPU: " << #expr << " failed: " << hipGetErrorString(e_) << " (" << __FILE__ << ":" << __LINE__ << ")"; \
 			log_.error(os_.str());                                                                             \
+			return false;                                                                                      \
+		}                                                                                                      \
+	} while(0)
+
+#define NCCLCHECK(expr)                                                                                        \
+	do                                                                                                         \
+	{                                                                                                          \
+		const ncclResult_t r_ = (expr);                                                                        \
+		if(r_ != ncclSuccess)                                                                                  \
+		{                                                                                                      \
+			log_.error(std::string("GPU group: ") + #expr + " failed: " + ncclGetErrorString(r_));            \
 			return false;                                                                                      \
 		}                                                                                                      \
 	} while(0)
@@ -661,10 +678,19 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	depth_out = 0;
 	const auto t0 = std::chrono::steady_clock::now();
 	const uint32_t slots = (uint32_t)bounces + 1u;
-	const size_t n_slots = (size_t)N * slots;
-	if(n_slots > 0xffffffffull) { log_.error("PhotonIntegrator: photons x (bounces + 1) exceeds 2^32 deposit slots"); return false; }
-	if(!ensure(log_, d.ph_ray_o, (size_t)N * 16) || !ensure(log_, d.ph_ray_d, (size_t)N * 16) || !ensure(log_, d.ph_pcol, (size_t)N * 16) ||
-	   !ensure(log_, d.ph_alive0, (size_t)N * 4) || !ensure(log_, d.ph_alive1, (size_t)N * 4) || !ensure(log_, d.ph_n_alive, 16) ||
+	if((uint64_t)N * slots > 0xffffffffull) { log_.error("PhotonIntegrator: photons x (bounces + 1) exceeds 2^32 deposit slots"); return false; }
+	// A group render splits the photon paths: member r shoots the contiguous photon ids
+	// [N r / world, N (r + 1) / world) — the reference's threads shoot contiguous id ranges too
+	// (integrator_photon_mapping.cc:118-127, 437-441) — and the members concatenate their maps in
+	// member order, which is photon-id order: every member then holds the one-GPU map.
+	const bool group_render = !rp.band_bounds.empty() && grouped();
+	const int world = group_render ? rp.shard_world : 1, me = group_render ? rp.shard_rank : 0;
+	const uint32_t h0 = (uint32_t)((uint64_t)N * me / world), h1 = (uint32_t)((uint64_t)N * (me + 1) / world);
+	const uint32_t NL = h1 - h0;
+	if(which == 0) d.pm_local = NL;
+	const size_t n_slots = (size_t)NL * slots;
+	if(!ensure(log_, d.ph_ray_o, (size_t)NL * 16) || !ensure(log_, d.ph_ray_d, (size_t)NL * 16) || !ensure(log_, d.ph_pcol, (size_t)NL * 16) ||
+	   !ensure(log_, d.ph_alive0, (size_t)NL * 4) || !ensure(log_, d.ph_alive1, (size_t)NL * 4) || !ensure(log_, d.ph_n_alive, 16) ||
 	   !ensure(log_, d.dep_a, n_slots * 16) || !ensure(log_, d.dep_b, n_slots * 16) || !ensure(log_, d.dep_c, n_slots * 4) ||
 	   !ensure(log_, d.dep_flag, n_slots) || !ensure(log_, d.ph_scan, ((n_slots + 1023) / 1024) * 4 + 16) || !ensure(log_, d.ph_total, 16))
 		return false;
@@ -679,7 +705,7 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	P.dep_b = (float4 *)d.dep_b.p;
 	P.dep_c = (float *)d.dep_c.p;
 	P.dep_flag = (uint8_t *)d.dep_flag.p;
-	HIPCHECK(hipMemsetAsync(d.dep_flag.p, 0, n_slots, d.stream));
+	if(n_slots) HIPCHECK(hipMemsetAsync(d.dep_flag.p, 0, n_slots, d.stream));
 	// final gathering: radiance points of the diffuse map's deposits (:184-193)
 	const bool want_rad = which == 0 && rp.pm.final_gather;
 	P.rad_a = P.rad_b = P.rad_c = nullptr;
@@ -693,38 +719,65 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 		P.rad_b = (float4 *)d.rad_b.p;
 		P.rad_c = (float4 *)d.rad_c.p;
 		P.rad_flag = (uint8_t *)d.rad_flag.p;
-		HIPCHECK(hipMemsetAsync(d.rad_flag.p, 0, n_slots, d.stream));
+		if(n_slots) HIPCHECK(hipMemsetAsync(d.rad_flag.p, 0, n_slots, d.stream));
 	}
 	HIPCHECK(hipMemsetAsync(d.ph_n_alive.p, 0, 16, d.stream));
-	PROF(KK_PHOTON_EMIT, yafamd_photon_emit(&S, &P, &L, N, bounces, d.stream));
+	PROF(KK_PHOTON_EMIT, yafamd_photon_emit(&S, &P, &L, N, h0, NL, bounces, d.stream));
 	int cur = 0;
 	for(int b = 0; b <= bounces; ++b)
 	{
 		HIPCHECK(hipMemsetAsync((uint32_t *)d.ph_n_alive.p + (cur ^ 1), 0, 4, d.stream));
-		PROF(KK_PHOTON_BOUNCE, yafamd_photon_bounce(&S, &P, &L, N, bounces, b, cur, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+		PROF(KK_PHOTON_BOUNCE, yafamd_photon_bounce(&S, &P, &L, N, h0, NL, bounces, b, cur, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 		cur ^= 1;
 	}
-	// the map in photon-id order; outputs sized for the worst case (every slot stored), the count
-	// comes back from the scan
+	// the member's map in photon-id order (outputs sized for the worst case: every slot stored); a group
+	// member compacts into its segment buffers, the concatenation fills the map buffers below
 	Buf &pos = which ? d.cph_pos : d.ph_pos, &dir = which ? d.cph_dir : d.ph_dir, &colb = which ? d.cph_colb : d.ph_colb;
 	Buf &nodes = which ? d.cpk_nodes : d.pk_nodes;
+	Buf &cpos = group_render ? d.seg_pos : pos, &cdir = group_render ? d.seg_dir : dir, &ccolb = group_render ? d.seg_colb : colb;
 	uint32_t n = 0;
-	if(!ensure(log_, pos, n_slots * 16) || !ensure(log_, dir, n_slots * 16) || !ensure(log_, colb, n_slots * 4)) return false;
-	PROF(KK_PHOTON_COMPACT, yafamd_photon_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)pos.p,
-	                               (float4 *)dir.p, (float *)colb.p, d.stream));
+	if(!ensure(log_, cpos, n_slots * 16) || !ensure(log_, cdir, n_slots * 16) || !ensure(log_, ccolb, n_slots * 4)) return false;
+	PROF(KK_PHOTON_COMPACT, yafamd_photon_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)cpos.p,
+	                               (float4 *)cdir.p, (float *)ccolb.p, d.stream));
 	HIPCHECK(hipMemcpyAsync(&n, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
-	n_out = n;
+	uint32_t nr = 0;
 	if(want_rad)
 	{
-		uint32_t nr = 0;
-		if(!ensure(log_, d.radc_a, n_slots * 16) || !ensure(log_, d.radc_b, n_slots * 16) || !ensure(log_, d.radc_c, n_slots * 16)) return false;
-		PROF(KK_PHOTON_COMPACT, yafamd_rad_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)d.radc_a.p,
-		                                          (float4 *)d.radc_b.p, (float4 *)d.radc_c.p, d.stream));
+		Buf &ra = group_render ? d.seg_ra : d.radc_a, &rb = group_render ? d.seg_rb : d.radc_b, &rc = group_render ? d.seg_rc : d.radc_c;
+		if(!ensure(log_, ra, n_slots * 16) || !ensure(log_, rb, n_slots * 16) || !ensure(log_, rc, n_slots * 16)) return false;
+		PROF(KK_PHOTON_COMPACT, yafamd_rad_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)ra.p,
+		                                          (float4 *)rb.p, (float4 *)rc.p, d.stream));
 		HIPCHECK(hipMemcpyAsync(&nr, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
 		HIPCHECK(hipStreamSynchronize(d.stream));
-		d.n_rad_points = nr;
 	}
+	if(group_render)
+	{
+		// agree, exchange the members' counts, then concatenate the segments in member order
+		const int st = groupStatus(0);
+		if(st >= 2)
+		{
+			log_.error("GPU group: a member failed; render abandoned");
+			return false;
+		}
+		std::vector<uint32_t> counts, rcounts;
+		if(!groupCounts(n, counts) || (want_rad && !groupCounts(nr, rcounts))) return false;
+		uint64_t tot = 0, rtot = 0;
+		for(uint32_t c : counts) tot += c;
+		for(uint32_t c : rcounts) rtot += c;
+		if(tot > 0xffffffffull || rtot > 0xffffffffull) { log_.error("PhotonIntegrator: photon map exceeds 2^32 photons"); return false; }
+		if(!ensure(log_, pos, std::max<uint64_t>(tot, 1) * 16) || !ensure(log_, dir, std::max<uint64_t>(tot, 1) * 16) ||
+		   !ensure(log_, colb, std::max<uint64_t>(tot, 1) * 4))
+			return false;
+		if(want_rad && (!ensure(log_, d.radc_a, std::max<uint64_t>(rtot, 1) * 16) || !ensure(log_, d.radc_b, std::max<uint64_t>(rtot, 1) * 16) ||
+		                !ensure(log_, d.radc_c, std::max<uint64_t>(rtot, 1) * 16)))
+			return false;
+		if(!groupConcat(which ? 1 : 0, counts) || (want_rad && !groupConcat(2, rcounts))) return false;
+		n = (uint32_t)tot;
+		nr = (uint32_t)rtot;
+	}
+	n_out = n;
+	if(want_rad) d.n_rad_points = nr;
 	const auto t1 = std::chrono::steady_clock::now();
 	stats_.photon_shoot_seconds += std::chrono::duration<double>(t1 - t0).count();
 	if(n == 0) return true;
@@ -735,6 +788,75 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	depth_out = depth;
 	stats_.photon_tree_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+	return true;
+}
+
+// The members' counts of a photon-map segment, in member order (a status agreement precedes).
+bool GpuRenderer::groupCounts(uint32_t mine, std::vector<uint32_t> &all)
+{
+	Impl &d = *d_;
+	if(peers_ && peers_->size() > 1)
+	{
+		seg_count_ = mine;
+		peers_->arrive(0);
+		all.assign((size_t)peers_->size(), 0u);
+		for(int r = 0; r < peers_->size(); ++r) all[(size_t)r] = peers_->member(r)->seg_count_;
+		peers_->arrive(0);   // nobody overwrites its count before everyone read it
+		return true;
+	}
+	const int world = group_world_;
+	all.assign((size_t)world, 0u);
+	if(!ensure(log_, d.g_status, 16 + 4 * (size_t)world)) return false;
+	uint32_t *dev = (uint32_t *)d.g_status.p + 4;
+	HIPCHECK(hipMemcpyAsync(dev, &mine, 4, hipMemcpyHostToDevice, d.stream));
+	NCCLCHECK(ncclAllGather(dev, dev + 1, 1, ncclUint32, d.comm, d.stream));
+	HIPCHECK(hipMemcpyAsync(all.data(), dev + 1, 4 * (size_t)world, hipMemcpyDeviceToHost, d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	return true;
+}
+
+// Concatenate every member's segment (counts[r] entries) in member order into this member's arrays:
+// kind 0 the diffuse photon map, 1 the caustic map, 2 the radiance points (final gathering).
+bool GpuRenderer::groupConcat(int kind, const std::vector<uint32_t> &counts)
+{
+	Impl &d = *d_;
+	struct Arr { Buf Impl::*src, Impl::*dst; size_t elem; };
+	std::vector<Arr> arrs;
+	if(kind == 2) arrs = {{&Impl::seg_ra, &Impl::radc_a, 16}, {&Impl::seg_rb, &Impl::radc_b, 16}, {&Impl::seg_rc, &Impl::radc_c, 16}};
+	else if(kind == 1) arrs = {{&Impl::seg_pos, &Impl::cph_pos, 16}, {&Impl::seg_dir, &Impl::cph_dir, 16}, {&Impl::seg_colb, &Impl::cph_colb, 4}};
+	else arrs = {{&Impl::seg_pos, &Impl::ph_pos, 16}, {&Impl::seg_dir, &Impl::ph_dir, 16}, {&Impl::seg_colb, &Impl::ph_colb, 4}};
+	std::vector<uint64_t> off(counts.size() + 1, 0);
+	for(size_t r = 0; r < counts.size(); ++r) off[r + 1] = off[r] + counts[r];
+	if(peers_ && peers_->size() > 1)
+	{
+		peers_->arrive(0);
+		bool ok = true;
+		for(int r = 0; r < peers_->size() && ok; ++r)
+		{
+			if(!counts[(size_t)r]) continue;
+			GpuRenderer *src = peers_->member(r);
+			for(const Arr &a : arrs)
+				ok = ok && hipMemcpyPeerAsync((char *)(d.*(a.dst)).p + off[(size_t)r] * a.elem, device_, (*src->d_.*(a.src)).p, src->device_,
+				                              counts[(size_t)r] * a.elem, d.stream) == hipSuccess;
+		}
+		ok = ok && hipStreamSynchronize(d.stream) == hipSuccess;
+		if(!ok) log_.error("GPU group: photon map copy between members failed");
+		peers_->arrive(0);
+		return ok;
+	}
+	NCCLCHECK(ncclGroupStart());
+	for(int r = 0; r < group_world_; ++r)
+	{
+		if(!counts[(size_t)r]) continue;
+		for(const Arr &a : arrs)
+		{
+			char *dst = (char *)(d.*(a.dst)).p + off[(size_t)r] * a.elem;
+			const void *src = r == group_rank_ ? (d.*(a.src)).p : dst;
+			NCCLCHECK(ncclBroadcast(src, dst, counts[(size_t)r] * a.elem, ncclChar, r, d.comm, d.stream));
+		}
+	}
+	NCCLCHECK(ncclGroupEnd());
+	HIPCHECK(hipStreamSynchronize(d.stream));
 	return true;
 }
 
@@ -1520,7 +1642,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		ktimes_.items[KK_SHADE] = hs.shade_entries;
 		ktimes_.items[KK_NEE] = hs.nee_requests;
 		ktimes_.items[KK_GATHER] = hs.gather_queries;
-		ktimes_.items[KK_PHOTON_EMIT] = ktimes_.items[KK_PHOTON_BOUNCE] = (uint64_t)d.pm_paths;
+		ktimes_.items[KK_PHOTON_EMIT] = ktimes_.items[KK_PHOTON_BOUNCE] = (uint64_t)d.pm_local;
 		ktimes_.items[KK_PHOTON_COMPACT] = ktimes_.items[KK_PHOTON_TREE] = stats_.photons;
 		stats_.trace_kernel_ms = ktimes_.ms[KK_TRACE];
 		stats_.shade_kernel_ms = ktimes_.ms[KK_SHADE];
@@ -1604,16 +1726,6 @@ bool GpuRenderer::traceRays(bool any, const float *rays, int n, float *t, int *p
 // ---------------------------------------------------------------------------------------------
 // render group
 // ---------------------------------------------------------------------------------------------
-#define NCCLCHECK(expr)                                                                                        \
-	do                                                                                                         \
-	{                                                                                                          \
-		const ncclResult_t r_ = (expr);                                                                        \
-		if(r_ != ncclSuccess)                                                                                  \
-		{                                                                                                      \
-			log_.error(std::string("GPU group: ") + #expr + " failed: " + ncclGetErrorString(r_));            \
-			return false;                                                                                      \
-		}                                                                                                      \
-	} while(0)
 
 bool GpuRenderer::joinGroup(int rank, int world, const void *rccl_id, size_t id_bytes)
 {

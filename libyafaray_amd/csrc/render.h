@@ -218,6 +218,9 @@ class GpuRenderer
 
 	private:
 		void *d_comm() const;
+		bool groupCounts(uint32_t mine, std::vector<uint32_t> &all);
+		bool groupConcat(int kind, const std::vector<uint32_t> &counts);
+		uint32_t seg_count_ = 0;   // this member's photon-map segment count (read by the peers)
 		Impl *d_;
 		Logger &log_;
 		int device_ = -1;

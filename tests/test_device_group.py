@@ -208,3 +208,48 @@ def test_device_group_cancel(product):
     assert (w <= fw).all()
     assert _same(a[complete], full[complete])
     assert (a[w == 0] == 0).all()
+
+
+def _ulp(a, b):
+    a = np.ascontiguousarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.ascontiguousarray(b, np.float32).view(np.int32).astype(np.int64)
+    a = np.where(a < 0, -(a & 0x7fffffff), a)
+    b = np.where(b < 0, -(b & 0x7fffffff), b)
+    return np.abs(a - b)
+
+
+def _specular_photon_spec(integrator, **kw):
+    s = scenes.cornell_specular(48, 36, spp=1, integrator=integrator, raydepth=3)
+    r = dataclasses.replace(s.render, pm_caustic_photons=20000, caustic_radius=kw.pop("radius", 0.1), **kw)
+    if integrator == "photonmapping":
+        r = dataclasses.replace(r, pm_photons=20000, pm_search=50, pm_diffuse_radius=0.1, pm_bounces=5)
+    return dataclasses.replace(s, render=r)
+
+
+SHARDED_PHOTONS = {
+    "dl-caustics": lambda: _specular_photon_spec("directlighting", pm_caustics=True, caustic_search=40),
+    "pm-caustics": lambda: _specular_photon_spec("photonmapping", pm_caustics=True, radius=0.05),
+    "pm-final-gather": lambda: dataclasses.replace(
+        scenes.cornell_photon(40, 30, spp=1, photons=20000, search=50, radius=0.1),
+        render=dataclasses.replace(scenes.cornell_photon(40, 30, spp=1, photons=20000, search=50, radius=0.1).render,
+                                   pm_final_gather=True, fg_samples=4)),
+}
+
+
+@pytest.mark.parametrize("members", [2, 3])
+@pytest.mark.parametrize("case", list(SHARDED_PHOTONS))
+def test_device_group_sharded_photon_maps_match_oracle(product, oracle_built, case, members):
+    """Photon shooting split across the members (contiguous photon-id ranges, the reference threads'
+    split, integrator_photon_mapping.cc:118-127, 437-441), the maps concatenated in member order:
+    the same maps (counts) and film as the oracle's one-thread shooting."""
+    spec = SHARDED_PHOTONS[case]()
+    rgba, w, st = product.render_spec(spec, members=members)
+    o = oracle_built.OracleScene(spec, threads=8)
+    orgba, ow, _ = o.render()
+    assert np.array_equal(w, ow)
+    u = _ulp(rgba, orgba)
+    assert u.max() <= 4, f"{(u > 4).sum()} values > 4 ULP"
+    if spec.render.pm_caustics:
+        assert st["caustic_photons"] == len(o.photon_map("caustic")[0]) > 0
+    if spec.render.integrator == "photonmapping":
+        assert st["photons"] == len(o.photon_map("diffuse")[0])
