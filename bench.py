@@ -108,6 +108,15 @@ def load_pmc(a, W, H):
 # ---------------------------------------------------------------------------------------------
 # algorithmic bytes per work item (DESIGN.md §4 restates each with our design's bytes)
 # ---------------------------------------------------------------------------------------------
+# kernel kinds that are one kernel (per-launch PMC instruction counts map onto their launches); the
+# others (pkd_build, photon_compact, aa_next_pass) are sequences of several kernels per launch record
+SINGLE_KERNEL_KINDS = {"k_trace", "k_shade", "k_nee", "k_camera", "k_film", "k_gather", "k_fg", "k_pregather", "k_surface",
+                       "k_tshadow", "k_photon_emit", "k_photon_bounce", "k_spawn", "k_combine"}
+# SURVEY §8d per-ray algorithmic bytes with the reference kd-tree's measured counts
+# (B_ray = N_node * 8 + N_tri * 40 + ray I/O): C2 closest 273 / shadow 235 B, C4 509 / 793 B
+SURVEY_B_RAY = {"cornell": (273.0, 235.0), "sphere": (509.0, 793.0)}
+
+
 def algo_bytes(kind, s, kt, in_lds, a):
     """Total algorithmic HBM bytes of all launches of one kernel kind in one frame."""
     it = kt["items"]
@@ -127,8 +136,16 @@ def algo_bytes(kind, s, kt, in_lds, a):
     if kind == "k_film":
         return 16.0 * it + 20.0 * a.width * a.height   # the samples (float4) + RGBA + weight per pixel
     if kind == "k_gather":
-        # §8d: N_visit * 16 B (kd nodes 8 B + photon position) + k * 36 B photon records per query
-        return 16.0 * s.get("gather_visits", 0) + 36.0 * 50 * it
+        # §8d: N_visit * 16 B (kd node; a leaf carries the photon position) + 36 B per photon record the
+        # estimates read (position.w + direction + colour.b, counted in-kernel: under final gathering
+        # the diffuse estimate moves to k_fg, so the records are counted, not k per request), plus the
+        # request (64 B) and the sample it writes (16 B)
+        return 16.0 * s.get("gather_visits", 0) + 36.0 * s.get("gather_photons", 0) + 80.0 * it
+    if kind == "k_fg":
+        # per request: 64 B in (point, wo + sample id, colour, extra) + 16 B out; the gather paths'
+        # traversals (LDS-resident scene) and the radiance-map lookups (16 K points, L2-resident) do
+        # not reach HBM
+        return 80.0 * it
     if kind == "k_photon_bounce":
         return (32.0 + 36.0) * s["photons"] + 32.0 * it   # deposits + one ray per path per bounce
     return None
@@ -214,7 +231,7 @@ def main():
     s, kt = stats_acc[-1], kt_acc[-1]
     pmc = load_pmc(a, W, H)
     kernels, frame_ms = kernel_table(a, s, kt, pmc)
-    roof = dominant_roofline(s, kt, kernels, pmc)
+    roof = dominant_roofline(s, kt, kernels, pmc, a.scene)
 
     cpu, parity = None, None
     if rank == 0 and n_gpus == 1:
@@ -295,13 +312,13 @@ def kernel_table(a, s, kt, pmc):
             e["traffic_frac"] = round(e["traffic_gbs"] / HBM_PEAK_GBS, 4)
             if "valu_lane_util" in p:
                 e["valu_lane_util"] = p["valu_lane_util"]
-            if "sq_insts_valu_per_launch" in p and v["launches"]:
+            if "sq_insts_valu_per_launch" in p and v["launches"] and kind in SINGLE_KERNEL_KINDS:
                 e["valu_issue_frac"] = round(p["sq_insts_valu_per_launch"] / (v["ms"] / v["launches"] * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4)
         out[kind] = e
     return out, frame_ms
 
 
-def dominant_roofline(s, kt, kernels, pmc):
+def dominant_roofline(s, kt, kernels, pmc, scene=None):
     """The contract's roofline object for the kernel with the largest share of the frame."""
     if not kt:
         return None
@@ -316,6 +333,22 @@ def dominant_roofline(s, kt, kernels, pmc):
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": p.get("hbm_bytes_per_launch"),
             "kernel": kind, "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
             "algo_bytes_per_launch": round(per_launch)}
+    if kind == "k_trace" and scene in SURVEY_B_RAY:
+        # §8d's per-ray model (the reference kd-tree's node / triangle counts) next to our BVH4 bytes
+        bc, bs = SURVEY_B_RAY[scene]
+        model = (bc * s["closest_rays"] + bs * s["shadow_rays"]) / launches
+        rate = model / (avg_ms * 1e-3) / 1e9
+        roof["survey_per_ray_model"] = {"closest_B": bc, "shadow_B": bs, "bytes_per_launch": round(model),
+                                        "achieved": round(rate, 1), "frac": round(rate / HBM_PEAK_GBS, 4)}
+        if not s["scene_in_lds"]:
+            # the scene streams from L2 / MALL / HBM: the per-ray model is the headline (the BVH4
+            # bytes of every visit, 128 B, overstate the node data a kd-tree ray would touch)
+            roof["achieved"] = round(rate, 1)
+            roof["frac"] = round(rate / HBM_PEAK_GBS, 4)
+            roof["algo_bytes_per_launch"] = round(model)
+            roof["model"] = "SURVEY §8d per-ray bytes"
+        else:
+            roof["model"] = "ray I/O (the LDS-resident scene's traversal bytes never reach HBM)"
     if kind == "k_trace":
         trav = (128.0 if s["bvh_width"] == 4 else 64.0) * s["node_visits"] + 48.0 * s["tri_tests"]
         rate = trav / launches / (avg_ms * 1e-3) / 1e9
@@ -326,6 +359,13 @@ def dominant_roofline(s, kt, kernels, pmc):
                              "node_visits_per_ray": round(s["node_visits"] / rays, 2), "tri_tests_per_ray": round(s["tri_tests"] / rays, 2)}
         if "valu_issue_frac" in e:
             roof["valu"] = {"issue_frac": e["valu_issue_frac"], "lane_util": e.get("valu_lane_util")}
+            if e.get("valu_lane_util") is not None:
+                useful = round(e["valu_issue_frac"] * e["valu_lane_util"], 4)
+                roof["valu"]["useful_frac"] = useful
+                if s["scene_in_lds"]:
+                    # C2: what bounds the kernel is instruction issue under divergence, not HBM
+                    roof["limiter"] = (f"VALU: issue {e['valu_issue_frac']} x lane utilisation {e['valu_lane_util']} = "
+                                       f"{useful} of peak useful lanes (LDS-resident scene)")
     return roof
 
 

@@ -53,6 +53,8 @@ typedef struct
 	double fg_thin_seconds;     /* final gathering: radiance-point thinning (host) incl. their download */
 	double fg_radiance_seconds; /* final gathering: radiance map total (thinning, pre-gather, kd-tree) */
 	int64_t fg_thin_rounds;     /* final gathering: GPU thinning rounds (-1: thinned on the host) */
+	uint64_t gather_queries;    /* photon-map estimate requests k_gather served (1.2) */
+	uint64_t gather_photons;    /* photon records the density estimates read (1.2) */
 } yafaray_amd_stats_t;
 
 /* Bytes of the LIBYAFARAY_AMD_1.0 struct (its fields end at photon_tree_seconds): yafaray_amd_getStats

@@ -299,7 +299,12 @@ struct DevPaths
 	float4 *pend_emit;     // emission pending at that vertex
 	float4 *v0p;           // first hit p .w = prim (bits)   — only used when path_samples > 1
 	float4 *v0wo;          // first hit wo
-	uint4 *pr;             // (PixelSamplingData::offset_, PixelSamplingData::sample_, MWC x, MWC c)
+	uint4 *pr;             // compact record (no specular recursion tree): (sample id, stage, MWC x, MWC c) —
+	                       // the pixel, PixelSamplingData offset_ / sample_ derive from the sample id;
+	                       // tree renders: (PixelSamplingData::offset_, sample_, MWC x, MWC c) with the
+	                       // sample / node id in DevQueues::slot and the stage in col.w
+	float4 *csmp;          // compact record: the first-vertex estimate `col` per chunk sample (indexed by
+	                       // sample id), written when it changes, read where it is used (F_COLS)
 	float4 *nee;           // [slots * nee_k] contributions .w = valid
 	uint8_t *occ;          // [slots * nee_k] shadow results
 	float4 *ts;            // [3 * slots * nee_k] transparent shadows: the contribution's factors
@@ -407,6 +412,7 @@ struct DevStats
 	unsigned long long nee_requests;     // NEE requests k_nee served
 	unsigned long long gather_queries;   // photon density estimates k_gather computed
 	unsigned long long gather_visits;    // point kd-tree nodes k_gather fetched
+	unsigned long long gather_photons;   // photons the density estimates read (heap entries summed)
 };
 
 } // namespace yafamd

@@ -225,6 +225,8 @@ bool Scene::renderDeviceGroup(RenderParams &rp)
 		st.tri_tests += o.tri_tests;
 		st.samples += o.samples;
 		st.gather_visits += o.gather_visits;
+		st.gather_queries += o.gather_queries;
+		st.gather_photons += o.gather_photons;
 		st.trace_kernel_ms += o.trace_kernel_ms;
 		st.shade_kernel_ms += o.shade_kernel_ms;
 		st.nee_kernel_ms += o.nee_kernel_ms;

@@ -72,7 +72,7 @@ enum : uint32_t
 	F_PEND_ONE = 1u << 19,       // pending: estimateOneDirectLight at v_k
 	F_PEND_EMIT = 1u << 20,      // pending emission add
 	F_V0_DIFFUSE = 1u << 21,     // v0 had the Diffuse flag (NEE estimated there)
-	F_END_SUBPATH = 1u << 22,    // after the connect: the current subpath ends
+	F_COLS = 1u << 22,           // compact record: a nonzero first-vertex estimate is stored in csmp[sample id]
 	F_AO_EMIT = 1u << 23,        // ambient occlusion at an emitting v0: pend_emit holds emit(wo)
 	F_LNUM_SHIFT = 24            // light picked by estimateOneDirectLight (8 bits)
 };
@@ -325,12 +325,24 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 		from = from + li;
 		dir = normalize(dir * c.dof_distance - li);
 	}
-	Q.slot[a] = i;          // sample id within the chunk travels with the queue entry
-	Q.ray_o[a] = f4(from, tmin);
-	Q.ray_d[a] = f4(dir, tmax);
-	P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
-	P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));   // stage
-	P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
+	// the compact record carries the sample id and the stage in pr (offset / sample index derive
+	// from the sample id); a specular recursion tree keeps them in the queue's slot and col.w
+	if(!S.tree)
+	{
+		Q.ray_o[a] = f4(from, tmin);
+		Q.ray_d[a] = f4(dir, tmax);
+		P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
+		P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
+	}
+	else
+	{
+		Q.slot[a] = i;          // sample id within the chunk travels with the queue entry
+		Q.ray_o[a] = f4(from, tmin);
+		Q.ray_d[a] = f4(dir, tmax);
+		P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
+		P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));   // stage
+		P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
+	}
 	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
 	// output is matched statistically — integrator_tiled.cc:272), seeded from the pixel-major sample
 	// id so that the image does not depend on how the film is split over GPUs or chunks
@@ -338,7 +350,7 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	const uint64_t gid = ((uint64_t)sc.y * (uint64_t)S.width + (uint64_t)sc.x) * (uint64_t)S.spp + (uint64_t)sc.s;
 	const uint32_t gid32 = (uint32_t)gid ^ fnv32((uint32_t)(gid >> 32));
 	const uint32_t seed = fnv32(gid32 ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)) + 123u;
-	P.pr[a] = make_uint4(offset, sample_idx, 30903u, seed);
+	P.pr[a] = S.tree ? make_uint4(offset, sample_idx, 30903u, seed) : make_uint4((uint32_t)i, ST_CAMERA, 30903u, seed);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1759,11 +1771,15 @@ struct ShadeArgs
 	uint64_t chunk_base;
 };
 
-__device__ __forceinline__ void writeSample(const ShadeArgs &A, uint32_t sid, C3 col, float alpha)
+__device__ __forceinline__ void writeSampleAt(const ShadeArgs &A, const SampleCoord &sc, C3 col, float alpha)
 {
-	const SampleCoord sc = sampleAt(A.S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
 	if(alpha > 1.f) alpha = 1.f;   // integrator_tiled.cc:399
 	A.samples[((size_t)sc.y * A.S.width + sc.x) * A.S.spp + sc.s] = f4(col, alpha);
+}
+
+__device__ __forceinline__ void writeSample(const ShadeArgs &A, uint32_t sid, C3 col, float alpha)
+{
+	writeSampleAt(A, sampleAt(A.S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid), col, alpha);
 }
 
 // First hit v0 of a later subpath, rebuilt from the primitive stored with the camera hit.
@@ -1870,6 +1886,11 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
 	const int K = S.nee_k;
 	const uint32_t stride = blockDim.x;
+	// compact record (every render without a specular recursion tree): pr = (sample id, stage, MWC);
+	// the pixel and its sampling offsets are recomputed from the sample id, the first-vertex estimate
+	// lives in csmp[sample id] (written when it changes, read where it is used) instead of travelling
+	// with every vertex
+	const bool compact = !(EXT && S.tree);
 	PHASE_DECL
 	for(uint32_t base_j = 0; base_j < n_a; base_j += stride)
 	{
@@ -1882,19 +1903,30 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		float4 thr4 = make_float4(0.f, 0.f, 0.f, 0.f), col4 = thr4, pcol4 = thr4, pwo4 = thr4, pthr4 = thr4, pem4 = thr4;
 		float4 v0p4 = thr4, v0wo4 = thr4;
 		float4 v0a0 = thr4, v0a1 = thr4;   // first-hit surface attributes (ATTR && keep_v0)
+		SampleCoord sc{0, 0, 0};
 		if(live)
 		{
-			sid = (uint32_t)A.Q.slot[i];
 			const uint4 pr = Pc.pr[i];
-			pix = make_uint2(pr.x, pr.y);
 			rng = make_uint2(pr.z, pr.w);
+			if(compact)
+			{
+				sid = pr.x;
+				stage = pr.y;
+				sc = sampleAt(S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
+				pix = make_uint2(fnv32((uint32_t)sc.y * fnv32((uint32_t)sc.x)), S.base_offset + S.pass_offset + (uint32_t)sc.s);
+			}
+			else
+			{
+				sid = (uint32_t)A.Q.slot[i];
+				pix = make_uint2(pr.x, pr.y);
+				col4 = Pc.col[i];
+				stage = __float_as_uint(col4.w);
+			}
 			thr4 = Pc.thr[i];
-			col4 = Pc.col[i];
 			pcol4 = Pc.pcol[i];
 			if(keep_v0) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
 			if(ATTR && keep_v0) { v0a0 = Pc.v0attr[2 * (size_t)i]; v0a1 = Pc.v0attr[2 * (size_t)i + 1]; }
 			w = thr4.w;
-			stage = __float_as_uint(col4.w);
 			flags = __float_as_uint(pcol4.w);
 			// only the first segment of a subpath reads the previous wo (path_tracer.cc:193-197)
 			if((stage & 0xffu) == ST_FIRST) pwo4 = Pc.pwo[i];
@@ -1909,11 +1941,22 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		int depth = (int)(stage >> 20);
 		const uint32_t offset = pix.x, sample_idx = pix.y;
 		C3 ao_extra = c3(0.f);
+		// compact record: col comes from csmp on first use; col_dirty = changed this iteration
+		bool col_ld = !compact, col_dirty = false;
+		auto loadCol = [&]() {
+			if(!col_ld)
+			{
+				col = (flags & F_COLS) ? rgb(Pc.csmp[sid]) : c3(0.f);
+				col_ld = true;
+			}
+		};
 
 		PHASE(0);
 		// ---- 1. connect the pending next-event estimate ----
 		if(live && (flags & F_PEND_V0))
 		{
+			loadCol();
+			col_dirty = true;
 			// estimateAllDirectLight (montecarlo.cc:54-68): col += sum over lights in name order
 			C3 total = c3(0.f);
 			for(int l = 0; l < S.n_lights; ++l) total = total + neeSum(S, S.lights[l], Pc.nee, Pc.occ, (int)i * K + (int)S.lights[l].nee_base);
@@ -1984,6 +2027,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 						S.node_own[sid] = f4(bg, a);
 						S.node_child[sid] = make_int2(-1, -1);
 					}
+					else if(compact) writeSampleAt(A, sc, bg, a);
 					else writeSample(A, sid, bg, a);
 				}
 				else
@@ -1991,6 +2035,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 					const DevMaterial &m = S.mats[sp.mat];
 					if(EXT && S.tree) spawnSpecular(S, m, sp, wo, sid, make_uint2(offset, sample_idx), rng, add_depth_in);
 					col = c3(0.f);
+					col_ld = true;
+					col_dirty = true;
 					// photon_mapping.cc:868-869 adds emit(wo) unconditionally and :938-946 adds it again
 					// for emitting materials; the other integrators add it once (direct_light.cc:120)
 					if(is_photon) col = col + matEmit<EXT>(m, sp, wo);
@@ -2165,6 +2211,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		uint32_t g_mode = 0;
 		if(want_gather)
 		{
+			loadCol();
 			g_mode = ((is_photon && S.n_photons > 0) ? (S.fg_on ? G_FG : G_DIFFUSE) : 0u) | (S.caus_map ? G_CAUSTIC : 0u);
 			// final gathering (k_fg) needs the PixelSamplingData of the sample
 			if(g_mode & G_FG) g_extra = C3{__uint_as_float(offset), __uint_as_float(sample_idx), 0.f};
@@ -2173,10 +2220,12 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		}
 		if(live && finalize && !want_gather)
 		{
+			loadCol();
 			// path_tracer.cc:274-278 / direct_light.cc:129-131
 			if(is_path && (flags & F_V0_DIFFUSE)) col = col + pcol / (float)n_paths;
 			col = col + c3(0.f);   // recursiveRaytrace: no specular/glossy component
 			if(EXT && S.tree) S.node_own[sid] = f4(col, alpha);   // recursiveRaytrace's part: k_combine
+			else if(compact) writeSampleAt(A, sc, col, alpha);
 			else writeSample(A, sid, col, alpha);
 		}
 
@@ -2186,9 +2235,19 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		const bool want_nee = live && (nee_v0 || nee_one);
 		// the entry stays in its shard: at most one next entry per entry, so the shard never overflows
 		const uint32_t k = a0 + waveAppend(keep, &s_count[0]);
+		if(keep && compact && col_dirty)
+		{
+			// the first-vertex estimate changed: store it by sample id (zero is implied by a clear F_COLS)
+			if((__float_as_uint(col.r) | __float_as_uint(col.g) | __float_as_uint(col.b)) != 0u)
+			{
+				Pc.csmp[sid] = f4(col, 0.f);
+				flags |= F_COLS;
+			}
+			else flags &= ~F_COLS;
+		}
 		if(keep)
 		{
-			stStore2(&A.Qn.slot[k], (int)sid);
+			if(!compact) stStore2(&A.Qn.slot[k], (int)sid);
 			if(want_ray)
 			{
 				stStore2(&A.Qn.ray_o[k], f4(ray_o, S.ray_min_dist));
@@ -2200,9 +2259,13 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				A.Qn.ray_d[k] = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));
 				stage = ST_NORAY | (subpath << 8) | ((uint32_t)depth << 20);
 			}
-			stStore(&Pn.pr[k], make_uint4(pix.x, pix.y, rng.x, rng.y));
+			if(compact) stStore(&Pn.pr[k], make_uint4(sid, stage, rng.x, rng.y));
+			else
+			{
+				stStore(&Pn.pr[k], make_uint4(pix.x, pix.y, rng.x, rng.y));
+				stStore(&Pn.col[k], f4(col, __uint_as_float(stage)));
+			}
 			stStore(&Pn.thr[k], f4(thr, w));
-			stStore(&Pn.col[k], f4(col, __uint_as_float(stage)));
 			stStore(&Pn.pcol[k], f4(pcol, __uint_as_float(flags)));
 			if((stage & 0xffu) == ST_FIRST) Pn.pwo[k] = f4(pwo, 0.f);
 			if(nee_one) Pn.pend_thr[k] = f4(pend_thr, 0.f);
@@ -3229,7 +3292,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 	gatherSegPart(S.n_seg, seg, part, parts);
 	const uint32_t n_req = A.cnt_next.n_gather[seg];
 	const uint32_t a0 = seg * S.cap_a;
-	uint32_t visits = 0;
+	uint32_t visits = 0, photons = 0;
 	for(uint32_t base_j = part * kGatherBlock; base_j < n_req; base_j += parts * kGatherBlock)
 	{
 		if(base_j + threadIdx.x >= n_req) continue;
@@ -3241,6 +3304,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		float max_d2 = S.pm_radius2;
 		int found = 0;
 		if(mode & G_DIFFUSE) found = pkLookup(S.pk_nodes, p, S.pm_search, max_d2, heap, stk, gstride, visits);
+		photons += (uint32_t)found;
 		const float4 wk = A.G.wo_k[j];
 		const uint4 cb = A.G.pix_mode[j];
 		Surf sp = surfFromPrim(S, p, __float_as_int(pp.w));
@@ -3269,6 +3333,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		{
 			float r2 = S.c_radius2;
 			const int nc = pkLookup(S.cpk_nodes, p, S.c_search, r2, heap, stk, gstride, visits);
+			photons += (uint32_t)nc;
 			const float ir2 = 1.f / r2;
 			C3 sum = c3(0.f);
 			if(nc > 0)
@@ -3298,10 +3363,15 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		}
 	}
 	// counters: wave sums, then one atomic per workgroup (several workgroups share a segment)
-	for(int off = 32; off > 0; off >>= 1) visits += __shfl_down(visits, off);
+	for(int off = 32; off > 0; off >>= 1)
+	{
+		visits += __shfl_down(visits, off);
+		photons += __shfl_down(photons, off);
+	}
 	if(threadIdx.x == 0 && S.stats)
 	{
 		atomicAdd(&S.stats[seg].gather_visits, (unsigned long long)visits);
+		atomicAdd(&S.stats[seg].gather_photons, (unsigned long long)photons);
 		if(part == 0) atomicAdd(&S.stats[seg].gather_queries, (unsigned long long)n_req);
 	}
 }

@@ -279,7 +279,7 @@ struct GpuRenderer::Impl
 	int film_w = 0, film_h = 0;
 	// chunk buffers
 	size_t slots_cap = 0;
-	bool v0_alloc = false;
+	bool v0_alloc = false, tree_alloc = false;
 	int nee_cap = 0;
 	std::vector<Buf> chunk_bufs;
 	DevPaths P[2]{};       // path state, parallel to Q[q] (indexed by queue position)
@@ -1204,7 +1204,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	auto shardCap = [R](size_t m) { return (((m + 255) / 256 + R - 1) / R) * 256; };
 	const bool need_attr = S.has_attr != 0;
 	const int need_ts = S.tr_shad ? std::max(1, S.s_depth) : 0;
-	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc || need_ts != d.ts_alloc || need_g != d.g_alloc)
+	const bool need_tree = S.tree != 0;   // the full record (slot + col.w stage) only with a specular recursion tree
+	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc || need_ts != d.ts_alloc || need_g != d.g_alloc ||
+	   need_tree != d.tree_alloc)
 	{
 		// Wavefront buffers for M samples in flight (~0.7 KB each: 288 GB of HBM holds tens of millions,
 		// and big chunks amortise the per-launch cost).  On allocation failure the chunk is halved.
@@ -1229,7 +1231,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			{
 				DevPaths &P = d.P[q];
 				P.thr = (float4 *)A(MA * 16);
-				P.col = (float4 *)A(MA * 16);
+				P.col = (float4 *)A(need_tree ? MA * 16 : 16);
 				P.pcol = (float4 *)A(MA * 16);
 				P.pwo = (float4 *)A(MA * 16);
 				P.pend_thr = (float4 *)A(MA * 16);
@@ -1245,7 +1247,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			for(int q = 0; q < 2; ++q)
 			{
 				DevQueues &Q = d.Q[q];
-				Q.slot = (int *)A(MA * 4);
+				Q.slot = (int *)A(need_tree ? MA * 4 : 16);
 				Q.ray_o = (float4 *)A(MA * 16);
 				Q.ray_d = (float4 *)A(MA * 16);
 				Q.hit_t = (float *)A(MA * 4);
@@ -1257,6 +1259,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				Q.ts_hit = (float2 *)A(need_ts ? MA * K * 8 * (size_t)need_ts : 16);
 				Q.ts_n = (int *)A(need_ts ? MA * K * 4 : 16);
 			}
+			// the compact record's first-vertex estimates, by chunk sample id (shared by both state sets)
+			d.P[0].csmp = d.P[1].csmp = (float4 *)A(need_tree ? 16 : MA * 16);
 			d.N.p_prim = (float4 *)A(MA * 16);
 			d.N.wo_k = (float4 *)A(MA * 16);
 			d.N.pix_mode = (uint4 *)A(MA * 16);
@@ -1278,6 +1282,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		d.attr_alloc = need_attr;
 		d.ts_alloc = need_ts;
 		d.g_alloc = need_g;
+		d.tree_alloc = need_tree;
 		d.slots_cap = M;
 		d.nee_cap = K;
 	}
@@ -1615,6 +1620,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			hs.nee_requests += b.nee_requests;
 			hs.gather_queries += b.gather_queries;
 			hs.gather_visits += b.gather_visits;
+			hs.gather_photons += b.gather_photons;
 		}
 	}
 	stats_.closest_rays = hs.closest_rays;
@@ -1642,6 +1648,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		ktimes_.items[KK_SHADE] = hs.shade_entries;
 		ktimes_.items[KK_NEE] = hs.nee_requests;
 		ktimes_.items[KK_GATHER] = hs.gather_queries;
+		ktimes_.items[KK_FG] = S.fg_on ? hs.gather_queries : 0;   // every diffuse-map request runs its final gathering first
+		ktimes_.items[KK_PREGATHER] = (uint64_t)d.n_rphotons;
 		ktimes_.items[KK_PHOTON_EMIT] = ktimes_.items[KK_PHOTON_BOUNCE] = (uint64_t)d.pm_local;
 		ktimes_.items[KK_PHOTON_COMPACT] = ktimes_.items[KK_PHOTON_TREE] = stats_.photons;
 		stats_.trace_kernel_ms = ktimes_.ms[KK_TRACE];
@@ -1650,6 +1658,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		stats_.trace_launches = ktimes_.launches[KK_TRACE];
 	}
 	stats_.gather_visits = hs.gather_visits;
+	stats_.gather_photons = hs.gather_photons;
+	stats_.gather_queries = hs.gather_queries;
 	d.prof_on = false;
 	return true;
 }

@@ -2889,7 +2889,28 @@ class Renderer
 
 // integrator_tiled.cc:56-67 + imagefilm.cc:447-487 + imagesplitter.cc:30-107 (linear order,
 // one thread: no tail subdivision)
-struct Tile { int x, y, w, h; };
+struct Tile { int x, y, w, h, rank = 0; };
+
+// glibc rand() (random_r TYPE_3: r[i] = r[i-3] + r[i-31], output r >> 1, seeded by srand's
+// 16807-LCG fill and 310 discarded outputs): the reference seeds each tile's Russian-roulette
+// generator with the next rand() (integrator_tiled.cc:272), one call per tile in render order.
+static std::vector<uint32_t> glibcRandSequence(uint32_t seed, size_t n)
+{
+	std::vector<int32_t> r(344 + n);
+	r[0] = (int32_t)(seed == 0 ? 1 : seed);
+	for(int i = 1; i < 31; ++i)
+	{
+		const int64_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+		int64_t word = 16807 * lo - 2836 * hi;
+		if(word < 0) word += 2147483647;
+		r[i] = (int32_t)word;
+	}
+	for(int i = 31; i < 34; ++i) r[i] = r[i - 31];
+	for(size_t i = 34; i < r.size(); ++i) r[i] = (int32_t)((uint32_t)r[i - 31] + (uint32_t)r[i - 3]);
+	std::vector<uint32_t> out(n);
+	for(size_t k = 0; k < n; ++k) out[k] = ((uint32_t)r[k + 344]) >> 1;
+	return out;
+}
 
 static std::vector<Tile> tilesLinear(int w, int h, int bs)
 {
@@ -3072,11 +3093,14 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 			return (a.x - W / 2) * (a.x - W / 2) + (a.y - H / 2) * (a.y - H / 2) < (b.x - W / 2) * (b.x - W / 2) + (b.y - H / 2) * (b.y - H / 2);
 		});
 	std::vector<Tile> tiles;
-	for(const Tile &t : all)
+	for(size_t k = 0; k < all.size(); ++k)
 	{
+		const Tile &t = all[k];
 		const int ya = std::max(t.y, y0), yb = std::min(t.y + t.h, y1);
-		if(ya < yb) tiles.push_back({t.x, ya, t.w, yb - ya});
+		if(ya < yb) tiles.push_back({t.x, ya, t.w, yb - ya, (int)k});
 	}
+	// each tile's rand() in the one-thread render order (srand(1 + rr_seed))
+	const std::vector<uint32_t> tile_rand = glibcRandSequence(1u + rp.rr_seed, all.size());
 	const int nthreads = std::max(1, rp.threads);
 	std::vector<Renderer::Thread> th(nthreads);
 	std::vector<uint8_t> flags;   // imagefilm flags_ (adaptive passes)
@@ -3099,7 +3123,7 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 					std::vector<float> &b = buf[k - t0];
 					b.resize((size_t)a.w * a.h * n_samples * 4);
 					// integrator_tiled.cc:272 — RandomGenerator(rand() + offset*(resx*y0+x0) + 123)
-					Mwc rng(rp.rr_seed + pass_offs * (sc.cam.resx * a.y + a.x) + 123);
+					Mwc rng(tile_rand[(size_t)a.rank] + pass_offs * (sc.cam.resx * a.y + a.x) + 123);
 					for(int i = a.y; i < a.y + a.h; ++i)
 						for(int j = a.x; j < a.x + a.w; ++j)
 						{
