@@ -9,13 +9,23 @@
  *
  * Behind it, scene data is staged host-side exactly like the reference's Interface/Scene
  * (params -> create*), and yafaray_render() runs the hot path — camera sampling, BVH traversal,
- * path-tracing / direct-lighting integration and film splatting — as HIP kernels on the GPU.
+ * path-tracing / direct-lighting / photon-mapping integration and film splatting — as HIP kernels
+ * on the GPU.  By default the render uses every visible GPU of the node (render parameter "gpus",
+ * the analogue of the reference's "threads"; see yafaray_amd.h, device group).
  *
- * Plugin types served by the GPU core: materials shinydiffusemat / light_mat; lights pointlight /
- * arealight; camera perspective; background constant; integrators directlighting / pathtracing;
- * accelerators yafaray-kdtree-original / yafaray-kdtree-multi-thread / yafaray-simpletest (all map
- * to the GPU BVH).  Other plugin types are rejected the reference's way: the create* call logs an
- * error and returns YAFARAY_BOOL_FALSE / NULL (reference src/material/material.cc:52-61).
+ * Plugin types served by the GPU core:
+ *   materials     shinydiffusemat (all components, Fresnel, Oren-Nayar, shader nodes), light_mat,
+ *                 mirror, null
+ *   textures      image (TGA / HDR) and the node shaders texture_mapper / value / mix / layer
+ *   lights        pointlight, arealight
+ *   camera        perspective (with depth of field and the bokeh shapes)
+ *   background    constant
+ *   integrators   directlighting (+ caustics, ambient occlusion), pathtracing (caustic_type none /
+ *                 path / photon / both), photonmapping (diffuse + caustic maps, final gathering)
+ *   accelerators  yafaray-kdtree-original / yafaray-kdtree-multi-thread / yafaray-simpletest (all
+ *                 map to the GPU BVH)
+ * Other plugin types and unsupported options are rejected the reference's way: the create* call
+ * logs an error and returns YAFARAY_BOOL_FALSE / NULL (reference src/material/material.cc:52-61).
  */
 #ifndef YAFARAY_C_API_H
 #define YAFARAY_C_API_H

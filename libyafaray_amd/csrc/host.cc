@@ -1262,8 +1262,10 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		S.s_depth = std::max(0, shadow_depth);
 		if(transp_shad && shadow_depth > 64)
 		{
-			log.warning("Integrator: shadowDepth " + std::to_string(shadow_depth) + " clamped to 64 by the GPU core");
-			S.s_depth = 64;
+			// k_tshadow sorts each shadow ray's transparent-surface list in a 64-entry buffer: a deeper
+			// list would silently drop surfaces the reference filters through, so refuse instead
+			log.error("Integrator: shadowDepth " + std::to_string(shadow_depth) + " > 64 is not supported by the GPU core");
+			return false;
 		}
 		S.tree = 0;
 		S.ext = 0;

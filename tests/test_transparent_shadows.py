@@ -98,3 +98,14 @@ def test_transparent_shadows_off_is_unchanged(product, oracle_built):
     """transpShad false keeps the opaque any-hit path (same scene, same oracle)."""
     spec = scenes.cornell_transparent_shadows(64, 48, spp=2).with_render(transp_shad=False)
     _compare(product, oracle_built, spec)
+
+
+@pytest.mark.gpu
+def test_shadow_depth_above_the_gpu_limit_is_refused(product):
+    """shadowDepth > 64 would overflow k_tshadow's per-ray surface list: the render is refused with an
+    error (no silent clamp), and 64 itself renders."""
+    spec = scenes.cornell_transparent_shadows(32, 24, spp=1)
+    with pytest.raises(RuntimeError, match="shadowDepth"):
+        product.render_spec(spec.with_render(shadow_depth=65))
+    rgba, w, _ = product.render_spec(spec.with_render(shadow_depth=64))
+    assert (w > 0).all()
