@@ -203,6 +203,11 @@ def main():
 
     for _ in range(a.warmup):
         yi.render_quiet()
+    # the traversal's per-visit node / triangle counters of this (deterministic) frame: one untimed
+    # frame with them, the timed frames without (yafaray_amd_setTraceStats; rays are counted always)
+    yi.render_quiet()
+    trav = {k: yi.stats()[k] for k in ("node_visits", "tri_tests")}
+    yi.L.yafaray_amd_setTraceStats(yi.h, 0)
     # timed region: every launch bracketed by HIP events on the render stream (profile mode)
     yi.L.yafaray_amd_setProfileKernels(yi.h, 1)
     sync()
@@ -228,7 +233,8 @@ def main():
     msps = samples_total / elapsed / 1e6
     mrays = rays_total / elapsed / 1e6
 
-    s, kt = stats_acc[-1], kt_acc[-1]
+    s, kt = dict(stats_acc[-1]), kt_acc[-1]
+    s.update(trav)   # node visits / triangle tests of the stats frame
     pmc = load_pmc(a, W, H)
     kernels, frame_ms = kernel_table(a, s, kt, pmc)
     roof = dominant_roofline(s, kt, kernels, pmc, a.scene)

@@ -149,6 +149,9 @@ YAFARAY_C_API_EXPORT int yafaray_amd_unpackBands(const float *recv, int width, i
 /* Tuning: samples in flight per wavefront chunk (default 1 << 25, halved automatically if it does not fit) and whether to time k_trace with events. */
 YAFARAY_C_API_EXPORT void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots);
 YAFARAY_C_API_EXPORT void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_t enable);
+/* (LIBYAFARAY_AMD_1.2) Per-visit BVH node / triangle counters in the traversal kernels (default on).
+ * Off: the stats report rays only (node_visits / tri_tests stay 0) and k_trace runs ~1-2% faster. */
+YAFARAY_C_API_EXPORT void yafaray_amd_setTraceStats(yafaray_Interface_t *interface, yafaray_bool_t enable);
 
 /* Diagnostic: summed wave cycles of the k_shade phases (load, connect, hit, next segment, compaction,
  * NEE) since the last reset; returns the number of counters, 0 unless the library was built with

@@ -143,6 +143,7 @@ def lib():
             "yafaray_amd_unpackBands": (i, [C.POINTER(C.c_float), i, i, i, C.POINTER(C.c_int), i, i, C.POINTER(C.c_float)]),
             "yafaray_amd_setChunkSlots": (None, [vp, i]),
             "yafaray_amd_setProfileKernels": (None, [vp, b]),
+            "yafaray_amd_setTraceStats": (None, [vp, b]),
             "yafaray_amd_lastError": (cp, [vp]),
             "yafaray_amd_getRenderGroupId": (i, [vp, i]),
             "yafaray_amd_setRenderGroup": (b, [vp, i, i, vp, i]),

@@ -605,6 +605,12 @@ void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots)
 	if(s) s->chunk_slots = slots < 1024 ? 1024 : slots;
 }
 
+void yafaray_amd_setTraceStats(yafaray_Interface_t *interface, yafaray_bool_t enable)
+{
+	Scene *s = I(interface)->sc();
+	if(s) s->trace_stats = enable != YAFARAY_BOOL_FALSE;
+}
+
 void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_t enable)
 {
 	Scene *s = I(interface)->sc();

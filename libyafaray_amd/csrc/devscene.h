@@ -261,6 +261,7 @@ struct DevScene
 	float ao_dist;
 	float ao_col[3];
 	struct DevStats *stats;        // per-workgroup counters (null: not counted)
+	int trace_stats;               // k_trace counts node visits / triangle tests (0: rays only)
 	uint32_t node_base;            // node id of spawn slot 0 (= level-0 capacity of the chunk)
 	uint32_t spawn_cap;
 	float4 *node_own;              // per node: colour before recursiveRaytrace's result, alpha

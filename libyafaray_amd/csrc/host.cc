@@ -1379,6 +1379,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		rp.aa.dev.variance_pixels = s.aa_variance_pixels;
 		rp.chunk_slots = chunk_slots;
 		rp.profile = profile_kernels;
+		S.trace_stats = trace_stats ? 1 : 0;
 		film_w = s.width;
 		film_h = s.height;
 		if(!quiet)

@@ -219,6 +219,7 @@ class Scene
 		std::vector<int> device_group;
 		int chunk_slots = 1 << 26;   // samples in flight per wavefront chunk (64 M: the C2 frame in two chunks)
 		bool profile_kernels = false;
+		bool trace_stats = true;   // per-visit node / triangle counters in k_trace (yafaray_amd_setTraceStats)
 		volatile bool canceled = false;
 
 		bool createObject(const std::string &name, const ParamMap &p);

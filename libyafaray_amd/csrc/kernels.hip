@@ -453,7 +453,7 @@ __device__ __forceinline__ float triTest(const float4 &a, const float4 &b, const
 // Closest hit with t in [tmin, tmax) (ties -> lower primitive index), or any hit with t in
 // [0, tmax).  Box tests are conservative (boxes padded at build time + a relative slack), so
 // culling never drops a hit the exhaustive reference semantics would return.
-template<bool ANY, bool TS = false>
+template<bool ANY, bool TS = false, bool STATS = true>
 __device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
                           uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
@@ -470,7 +470,7 @@ __device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	int node = 0;
 	for(;;)
 	{
-		TRACE_STAT(++visits);
+		if(STATS) TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 4 * node;
 		const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
@@ -491,7 +491,7 @@ __device__ bool traverse2(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 			const int start = ~c;
 			for(int q = start; q < start + k; ++q)
 			{
-				TRACE_STAT(++tests);
+				if(STATS) TRACE_STAT(++tests);
 				const float4 *tp = C.tris + 3 * q;
 				const float4 ta = tp[0], tb = tp[1], tc = tp[2];
 				const float t = triTest(ta, tb, tc, o, d, ANY ? tmax : t_best);
@@ -550,7 +550,7 @@ __device__ __forceinline__ void cswap(float &ka, int &va, float &kb, int &vb)
 // BVH4 (bvh.cc: collapsed binary SAH tree, 128 B nodes with the four child boxes in SoA form).
 // Same hit semantics as traverse2: leaf children are tested as soon as their box is hit, inner
 // children are sorted by entry distance (5-exchange network) and descended nearest-first.
-template<bool ANY, bool SPILL, bool TS = false>
+template<bool ANY, bool SPILL, bool TS = false, bool STATS = true>
 __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
                           uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
@@ -577,7 +577,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	};
 	for(;;)
 	{
-		TRACE_STAT(++visits);
+		if(STATS) TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 8 * node;
 		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
@@ -593,11 +593,13 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 			const float az = __builtin_fmaf(lane4(lz, k), id.z, -oid.z), bz = __builtin_fmaf(lane4(hz, k), id.z, -oid.z);
 			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
 			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
-			const bool h = lo <= hi;
+			// selects, not branches: a lane-varying `if` here costs an exec-mask save / restore per child
+			const uint32_t h = lo <= hi ? 1u : 0u;
 			child[k] = __float_as_int(lane4(cf, k));
 			count[k] = __float_as_int(lane4(kf, k));
-			key[k] = (h && child[k] >= 0) ? lo : inf;
-			if(h && child[k] < 0 && count[k] > 0) leaves |= 1u << k;
+			const uint32_t inner = child[k] >= 0 ? 1u : 0u;
+			key[k] = (h & inner) ? lo : inf;
+			leaves |= (h & (inner ^ 1u) & (count[k] > 0 ? 1u : 0u)) << k;
 		}
 		// the hit leaves' triangles as one per-lane list (leaf order, then triangle order), so that a
 		// wave runs max-over-lanes tests per node instead of one pass per leaf slot any lane hit
@@ -617,7 +619,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 		{
 			const int q = i + (i < e[0] ? s4[0] : i < e[1] ? s4[1] : i < e[2] ? s4[2] : s4[3]);
 			{
-				TRACE_STAT(++tests);
+				if(STATS) TRACE_STAT(++tests);
 				const float4 *tp = C.tris + 3 * q;
 				const float4 ta = tp[0], tb = tp[1], tc = tp[2];
 				const float t = triTest(ta, tb, tc, o, d, ANY ? tmax : t_best);
@@ -665,7 +667,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 // its traversal ends, so a wave runs as long as its longest lane's sum of rays instead of the sum
 // over rays of the longest lane.  Every ray runs the sequence of traverse4 (same visits, culling,
 // leaf order and early exits), so hits are identical.
-template<bool SPILL>
+template<bool SPILL, bool STATS = true>
 __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPaths &P, uint32_t n_a, uint32_t total,
                              uint32_t a0, uint32_t s0, uint32_t j, uint32_t stride, uint32_t &visits, uint32_t &tests,
                              uint32_t &n_closest, uint32_t &n_shadow)
@@ -731,7 +733,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 			sp = 0;
 			node = 0;
 		}
-		TRACE_STAT(++visits);
+		if(STATS) TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 8 * node;
 		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
@@ -746,19 +748,20 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 			const float az = __builtin_fmaf(lane4(lz, k), id.z, -oid.z), bz = __builtin_fmaf(lane4(hz, k), id.z, -oid.z);
 			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
 			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
-			const bool h = lo <= hi;
+			const uint32_t h = lo <= hi ? 1u : 0u;
 			child[k] = __float_as_int(lane4(cf, k));
 			const int count = __float_as_int(lane4(kf, k));
-			key[k] = (h && child[k] >= 0) ? lo : inf;
+			const uint32_t inner = child[k] >= 0 ? 1u : 0u;
+			key[k] = (h & inner) ? lo : inf;
 			s4[k] = ~child[k] - acc;
-			acc += (h && child[k] < 0) ? count : 0;
+			acc += (h & (inner ^ 1u)) ? count : 0;
 			e[k] = acc;
 		}
 		bool done = false;
 		for(int i = 0; i < e[3]; ++i)
 		{
 			const int q = i + (i < e[0] ? s4[0] : i < e[1] ? s4[1] : i < e[2] ? s4[2] : s4[3]);
-			TRACE_STAT(++tests);
+			if(STATS) TRACE_STAT(++tests);
 			const float4 *tp = C.tris + 3 * q;
 			const float4 ta = tp[0], tb = tp[1], tc = tp[2];
 			const float t = triTest(ta, tb, tc, o, d, t_best);
@@ -807,12 +810,12 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 	}
 }
 
-template<bool ANY, bool WIDE, bool SPILL = true, bool TS = false>
+template<bool ANY, bool WIDE, bool SPILL = true, bool TS = false, bool STATS = true>
 __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best,
                                          int &prim_best, uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
-	if(WIDE) return traverse4<ANY, SPILL, TS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
-	return traverse2<ANY, TS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
+	if(WIDE) return traverse4<ANY, SPILL, TS, STATS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
+	return traverse2<ANY, TS, STATS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
 }
 
 // k_trace asks the register allocator for 8 waves per SIMD for LDS-resident scenes (<= 64 VGPRs;
@@ -825,7 +828,12 @@ __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tm
 #define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LDS_SCENE ? 8 : 6)))
 #endif
 
-template<bool LDS_SCENE, bool WIDE, bool TS>
+// SPILL = false: the whole stack bound fits the LDS levels (no spill column): pushes and pops are
+// plain LDS accesses (with a possible spill the compiler merges both address spaces into flat
+// accesses, whose pops wait for every outstanding vector-memory operation)
+// STATS = false: no per-visit node / triangle counters (timed frames; the counts come from a frame
+// rendered with them — the frame is deterministic, so they are the same)
+template<bool LDS_SCENE, bool WIDE, bool TS, bool SPILL = true, bool STATS = true>
 __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P,
                                                       DevStats *stats, int stack_depth, int *spill)
 {
@@ -861,7 +869,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	// refill pays where traversals are long (meshes in global memory: C4 -16%); on the short
 	// LDS-resident traversals of small scenes its per-visit bookkeeping costs more (C2 +35%)
 	if(!LDS_SCENE && WIDE && !TS)
-		traceRefill4<true>(C, Q, P, n_a, total, a0, s0, L.r * blockDim.x + threadIdx.x, stride, visits, tests, n_closest, n_shadow);
+		traceRefill4<true, STATS>(C, Q, P, n_a, total, a0, s0, L.r * blockDim.x + threadIdx.x, stride, visits, tests, n_closest, n_shadow);
 	else
 #endif
 	// one uniform trip count per workgroup so every lane reaches the same exits
@@ -877,7 +885,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 				float t;
 				int prim;
 				const float tmax = (dd.w >= 0.f) ? dd.w : __builtin_huge_valf();
-				traverse<false, WIDE>(C, xyz(od), xyz(dd), od.w, tmax, t, prim, visits, tests);
+				traverse<false, WIDE, SPILL, false, STATS>(C, xyz(od), xyz(dd), od.w, tmax, t, prim, visits, tests);
 				Q.hit_t[i] = t;
 				Q.hit_prim[i] = prim;
 				++n_closest;
@@ -898,10 +906,10 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 				L.cap = S.s_depth;
 				L.prim_ng = S.prim_ng;
 				L.mats = S.mats;
-				occ = traverse<true, WIDE, true, true>(C, xyz(od), xyz(dd), od.w, dd.w, t, prim, visits, tests, &L);
+				occ = traverse<true, WIDE, SPILL, true>(C, xyz(od), xyz(dd), od.w, dd.w, t, prim, visits, tests, &L);
 				Q.ts_n[k] = occ ? 0 : L.n;
 			}
-			else occ = traverse<true, WIDE>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
+			else occ = traverse<true, WIDE, SPILL, false, STATS>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
 			P.occ[Q.sh_idx[k]] = occ ? 1 : 0;   // P = state set of the consumer shade
 			++n_shadow;
 		}
@@ -2915,7 +2923,7 @@ __device__ C3 getReflectivity(const DevScene &S, const DevMaterial &m, const Sur
 }
 
 // :162-219 — one bounce of every live photon path: intersect, deposit, scatter (material.cc:137-153)
-template<bool LDS_SCENE, bool WIDE, bool EXT>
+template<bool LDS_SCENE, bool WIDE, bool EXT, bool SPILL = true>
 __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 {
 	const DevScene &S = A.S;
@@ -2959,7 +2967,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 			const float4 ro = A.P.ray_o[i], rd = A.P.ray_d[i], pc = A.P.pcol[i];
 			float t;
 			int prim;
-			if(traverse<false, WIDE>(C, xyz(ro), xyz(rd), ro.w, __builtin_huge_valf(), t, prim, visits, tests))
+			if(traverse<false, WIDE, SPILL>(C, xyz(ro), xyz(rd), ro.w, __builtin_huge_valf(), t, prim, visits, tests))
 			{
 				Surf sp = makeSurf(S, xyz(ro), xyz(rd), t, prim);
 				if(EXT && S.has_attr)
@@ -3509,7 +3517,7 @@ __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, flo
 
 // MonteCarloIntegrator::doLightEstimation for one light (integrator_montecarlo.cc:80-408) with the
 // shadow rays traced in place: neeLight's arithmetic, neeSum's addition order
-template<bool EXT, bool WIDE>
+template<bool EXT, bool WIDE, bool SPILL = true>
 __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                                   uint32_t loffs, uint32_t sample_idx, uint32_t offset, uint32_t &visits, uint32_t &tests)
 {
@@ -3535,7 +3543,7 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 			V3 so;
 			float st;
 			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
-			const bool occ = cast_shadows && traverse<true, WIDE>(C, so, ldir, 0.f, st, t_hit, p_hit, visits, tests);
+			const bool occ = cast_shadows && traverse<true, WIDE, SPILL>(C, so, ldir, 0.f, st, t_hit, p_hit, visits, tests);
 			if(!occ) c = c + contrib;
 		}
 		return c3(0.f) + c;
@@ -3589,7 +3597,7 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 					V3 so;
 					float st;
 					shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
-					const bool occ = cast_shadows && traverse<true, WIDE>(C, so, ldir, 0.f, st, t_hit, p_hit, visits, tests);
+					const bool occ = cast_shadows && traverse<true, WIDE, SPILL>(C, so, ldir, 0.f, st, t_hit, p_hit, visits, tests);
 					if(!occ) acc_l = acc_l + contrib;
 				}
 			}
@@ -3630,7 +3638,7 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 					V3 so;
 					float st;
 					shadowRayOf(sp.p, dir, b_tmin, t, so, st);
-					const bool occ = cast_shadows && traverse<true, WIDE>(C, so, dir, 0.f, st, t_hit, p_hit, visits, tests);
+					const bool occ = cast_shadows && traverse<true, WIDE, SPILL>(C, so, dir, 0.f, st, t_hit, p_hit, visits, tests);
 					if(!occ) acc_m = acc_m + contrib;
 				}
 			}
@@ -3680,7 +3688,7 @@ struct FgArgs
 #define YAF_FG_WAVES 4
 #endif
 #define YAF_FG_ATTR __attribute__((amdgpu_waves_per_eu(YAF_FG_WAVES)))
-template<bool LDS_SCENE, bool WIDE, bool EXT>
+template<bool LDS_SCENE, bool WIDE, bool EXT, bool SPILL = true>
 __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 {
 	const DevScene &S = A.S;
@@ -3741,7 +3749,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 			float t;
 			int prim;
 			V3 from = sp0.p;
-			if(!traverse<false, WIDE>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests)) continue;
+			if(!traverse<false, WIDE, SPILL>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests)) continue;
 			Surf hit = fgSurf<EXT>(S, from, dir, t, prim);
 			float length = t;
 			uint32_t mat_bsd_fs = hit.flags;
@@ -3769,7 +3777,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 							lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
 						}
 						lcol = (S.n_lights > 0)
-						           ? lightEstimateInline<EXT, WIDE>(S, C, S.lights[lnum], mh, hit, pwo, lnum, sample_idx, offset, visits, tests) *
+						           ? lightEstimateInline<EXT, WIDE, SPILL>(S, C, S.lights[lnum], mh, hit, pwo, lnum, sample_idx, offset, visits, tests) *
 						                 (float)S.n_lights
 						           : c3(0.f);
 					}
@@ -3798,7 +3806,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 				throughput = throughput * scol;
 				from = hit.p;
 				dir = ndir;
-				if(!traverse<false, WIDE>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests)) { did_hit = false; break; }
+				if(!traverse<false, WIDE, SPILL>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests)) { did_hit = false; break; }
 				hit = fgSurf<EXT>(S, from, dir, t, prim);
 				mat_bsd_fs = hit.flags;
 				length += t;
@@ -3903,16 +3911,34 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 		hipLaunchKernelGGL(k_trace_brute, dim3(grid), dim3(kTraceBlock), 0, st, *S, *Q, *cnt, *P, stats);
 		return hipGetLastError();
 	}
-#define YAF_TRACE_LAUNCH(L, W, T) hipLaunchKernelGGL((k_trace<L, W, T>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill)
+#define YAF_TRACE_LAUNCH(L, W, T, SP) hipLaunchKernelGGL((k_trace<L, W, T, SP>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill)
+	// no spill column: the LDS levels hold the whole stack bound (LDS-resident scenes)
+	const bool nospill = spill == nullptr;
 	if(S->tr_shad)
 	{
-		if(S->scene_in_lds) { if(wide) YAF_TRACE_LAUNCH(true, true, true); else YAF_TRACE_LAUNCH(true, false, true); }
-		else if(wide) YAF_TRACE_LAUNCH(false, true, true);
-		else YAF_TRACE_LAUNCH(false, false, true);
+		if(S->scene_in_lds)
+		{
+			if(nospill) { if(wide) YAF_TRACE_LAUNCH(true, true, true, false); else YAF_TRACE_LAUNCH(true, false, true, false); }
+			else if(wide) YAF_TRACE_LAUNCH(true, true, true, true);
+			else YAF_TRACE_LAUNCH(true, false, true, true);
+		}
+		else if(wide) YAF_TRACE_LAUNCH(false, true, true, true);
+		else YAF_TRACE_LAUNCH(false, false, true, true);
 	}
-	else if(S->scene_in_lds) { if(wide) YAF_TRACE_LAUNCH(true, true, false); else YAF_TRACE_LAUNCH(true, false, false); }
-	else if(wide) YAF_TRACE_LAUNCH(false, true, false);
-	else YAF_TRACE_LAUNCH(false, false, false);
+	else if(S->scene_in_lds)
+	{
+		if(nospill && wide && !S->trace_stats)
+			hipLaunchKernelGGL((k_trace<true, true, false, false, false>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
+			                   stack_depth, spill);
+		else if(nospill) { if(wide) YAF_TRACE_LAUNCH(true, true, false, false); else YAF_TRACE_LAUNCH(true, false, false, false); }
+		else if(wide) YAF_TRACE_LAUNCH(true, true, false, true);
+		else YAF_TRACE_LAUNCH(true, false, false, true);
+	}
+	else if(wide && !S->trace_stats)
+		hipLaunchKernelGGL((k_trace<false, true, false, true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
+		                   stack_depth, spill);
+	else if(wide) YAF_TRACE_LAUNCH(false, true, false, true);
+	else YAF_TRACE_LAUNCH(false, false, false, true);
 #undef YAF_TRACE_LAUNCH
 	return hipGetLastError();
 }
@@ -4035,12 +4061,21 @@ hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const P
 	if(S->scene_in_lds)
 	{
 		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
+		const bool ns = spill == nullptr;   // no spill column: plain LDS stack
 		if(S->ext)
 		{
-			if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<true, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+			if(S->node_f4 == 8)
+			{
+				if(ns) hipLaunchKernelGGL((k_photon_bounce<true, true, true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+				else hipLaunchKernelGGL((k_photon_bounce<true, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+			}
 			else hipLaunchKernelGGL((k_photon_bounce<true, false, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
 		}
-		else if(S->node_f4 == 8) hipLaunchKernelGGL((k_photon_bounce<true, true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+		else if(S->node_f4 == 8)
+		{
+			if(ns) hipLaunchKernelGGL((k_photon_bounce<true, true, false, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+			else hipLaunchKernelGGL((k_photon_bounce<true, true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
+		}
 		else hipLaunchKernelGGL((k_photon_bounce<true, false, false>), dim3(grid), dim3(kTraceBlock), bytes, st, A);
 	}
 	else if(S->ext)
@@ -4140,10 +4175,17 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	const bool wide = S->node_f4 == 8;
 #define YAF_FG_LAUNCH(L, W, E, B) hipLaunchKernelGGL((k_fg<L, W, E>), dim3(grid), dim3(kTraceBlock), B, st, A)
+#define YAF_FG_LAUNCH_NS(W, E, B) hipLaunchKernelGGL((k_fg<true, W, E, false>), dim3(grid), dim3(kTraceBlock), B, st, A)
 	if(S->scene_in_lds)
 	{
 		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
-		if(S->ext) { if(wide) YAF_FG_LAUNCH(true, true, true, bytes); else YAF_FG_LAUNCH(true, false, true, bytes); }
+		if(spill == nullptr)   // the LDS levels hold the whole stack bound: plain LDS pushes / pops
+		{
+			if(S->ext) { if(wide) YAF_FG_LAUNCH_NS(true, true, bytes); else YAF_FG_LAUNCH_NS(false, true, bytes); }
+			else if(wide) YAF_FG_LAUNCH_NS(true, false, bytes);
+			else YAF_FG_LAUNCH_NS(false, false, bytes);
+		}
+		else if(S->ext) { if(wide) YAF_FG_LAUNCH(true, true, true, bytes); else YAF_FG_LAUNCH(true, false, true, bytes); }
 		else if(wide) YAF_FG_LAUNCH(true, true, false, bytes);
 		else YAF_FG_LAUNCH(true, false, false, bytes);
 	}
@@ -4151,6 +4193,7 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 	else if(wide) YAF_FG_LAUNCH(false, true, false, stack_bytes);
 	else YAF_FG_LAUNCH(false, false, false, stack_bytes);
 #undef YAF_FG_LAUNCH
+#undef YAF_FG_LAUNCH_NS
 	return hipGetLastError();
 }
 
