@@ -262,6 +262,7 @@ struct DevScene
 	float ao_col[3];
 	struct DevStats *stats;        // per-workgroup counters (null: not counted)
 	int trace_stats;               // k_trace counts node visits / triangle tests (0: rays only)
+	int crop_x0, crop_y0;          // cropped film (xstart / ystart): film pixel (x, y) = camera pixel (x + crop_x0, y + crop_y0)
 	uint32_t node_base;            // node id of spawn slot 0 (= level-0 capacity of the chunk)
 	uint32_t spawn_cap;
 	float4 *node_own;              // per node: colour before recursiveRaytrace's result, alpha
@@ -287,6 +288,7 @@ struct DevFilm
 	// partial film: each pixel as ImageFilm::finishArea shows it when its tile finishes in a one-thread
 	// render (imagefilm.cc:489-520): only sources of tiles ranked <= its own; accum / weights untouched
 	int partial;
+	int crop_x0, crop_y0;          // cropped film: the sample positions hash the camera pixel (x + crop_x0, y + crop_y0)
 };
 
 // Per-chunk wavefront state (structure of arrays, capacity = chunk slots).

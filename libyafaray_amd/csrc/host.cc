@@ -878,7 +878,6 @@ bool Scene::setupRender(const ParamMap &p)
 	p.get("tiles_order", s.tiles_order);
 	if(s.accelerator != "yafaray-kdtree-original" && s.accelerator != "yafaray-kdtree-multi-thread" && s.accelerator != "yafaray-simpletest")
 		log.warning("Accelerator type '" + s.accelerator + "' could not be created, using the GPU BVH instead.");  // accelerator.cc:47-51
-	if(s.xstart != 0 || s.ystart != 0) { log.error("Scene: cropped films (xstart/ystart != 0) are not supported by the GPU core yet"); return false; }
 	if(s.filter != "box" && s.filter != "gauss" && s.filter != "mitchell" && s.filter != "lanczos")
 	{
 		log.warning("ImageFilm: No AA filter defined defaulting to Box!");
@@ -1292,6 +1291,9 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		S.ray_min_dist_auto = s.ray_min_dist_auto ? 1 : 0;
 		S.ray_min_dist = s.ray_min_dist;
 		S.base_offset = (uint32_t)s.base_sampling_offset;
+		// cropped film (imagefilm.cc:66, 129-132): film pixel (x, y) is camera pixel (x + xstart, y + ystart)
+		S.crop_x0 = s.xstart;
+		S.crop_y0 = s.ystart;
 		S.clamp_samples = s.clamp_samples;
 		S.rr_seed = (uint32_t)s.rr_seed;
 		uint32_t nee_all = 0, nee_max_one = 1;
@@ -1328,6 +1330,8 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		F.reach_back = std::max(0, -(int)(-(double)filterw + (.5 - 1.4e-11)));
 		F.width = s.width;
 		F.height = s.height;
+		F.crop_x0 = s.xstart;
+		F.crop_y0 = s.ystart;
 		F.spp = s.aa_samples;
 		F.tile = s.tile_size;
 		rp.shard_rank = shard_rank;
@@ -1479,7 +1483,9 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 				{
 					const int tx = (order[k] % ntx) * s.tile_size, ty = (order[k] / ntx) * s.tile_size;
 					const int x1 = std::min(s.width, tx + s.tile_size), y1 = std::min(s.height, ty + s.tile_size);
-					if(cb.highlight_area) cb.highlight_area(vname.c_str(), (int)k, tx, ty, x1, y1, cb.highlight_area_data);
+					// areas in camera coordinates (imagefilm.cc:462-467, 533), pixels in film coordinates (:527)
+					if(cb.highlight_area)
+						cb.highlight_area(vname.c_str(), (int)k, tx + s.xstart, ty + s.ystart, x1 + s.xstart, y1 + s.ystart, cb.highlight_area_data);
 					if(cb.put_pixel)
 						for(int y = ty; y < y1; ++y)
 							for(int x = tx; x < x1; ++x)
@@ -1487,7 +1493,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 								const float *px = &part[4 * ((size_t)y * s.width + x)];
 								cb.put_pixel(vname.c_str(), "combined", x, y, px[0], px[1], px[2], px[3], cb.put_pixel_data);
 							}
-					if(cb.flush_area) cb.flush_area(vname.c_str(), (int)k, tx, ty, x1, y1, cb.flush_area_data);
+					if(cb.flush_area) cb.flush_area(vname.c_str(), (int)k, tx + s.xstart, ty + s.ystart, x1 + s.xstart, y1 + s.ystart, cb.flush_area_data);
 					done_px += (x1 - tx) * (y1 - ty);
 					if(progress) progress(n_pix, done_px, "Rendering...", progress_data);
 				}
@@ -1552,8 +1558,10 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 				for(int y = ty; y < y1; ++y)
 					if(ownedRow(y)) { oy0 = std::min(oy0, y); oy1 = std::max(oy1, y + 1); }
 				if(oy1 <= oy0) continue;
-				if(cb.highlight_area) cb.highlight_area(view.first.c_str(), (int)k, tx, oy0, x1, oy1, cb.highlight_area_data);
-				if(cb.flush_area) cb.flush_area(view.first.c_str(), (int)k, tx, oy0, x1, oy1, cb.flush_area_data);
+				if(cb.highlight_area)
+					cb.highlight_area(view.first.c_str(), (int)k, tx + s.xstart, oy0 + s.ystart, x1 + s.xstart, oy1 + s.ystart, cb.highlight_area_data);
+				if(cb.flush_area)
+					cb.flush_area(view.first.c_str(), (int)k, tx + s.xstart, oy0 + s.ystart, x1 + s.xstart, oy1 + s.ystart, cb.flush_area_data);
 				done_px += (x1 - tx) * (oy1 - oy0);
 				if(progress) progress(n_pix, done_px, "Rendering...", progress_data);
 			}

@@ -288,8 +288,9 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	const uint32_t g = (uint32_t)i / 256u;
 	const uint32_t a = (g % S.n_seg) * S.cap_a + (g / S.n_seg) * 256u + (uint32_t)i % 256u;
 	const SampleCoord sc = sampleAt(S, jobs, n_jobs, chunk_base + (uint64_t)i);
-	// integrator_tiled.cc:313-335
-	const uint32_t offset = fnv32((uint32_t)sc.y * fnv32((uint32_t)sc.x));
+	// integrator_tiled.cc:313-335 (camera pixel coordinates: a cropped film starts at crop_x0 / crop_y0)
+	const int cx = sc.x + S.crop_x0, cy = sc.y + S.crop_y0;
+	const uint32_t offset = fnv32((uint32_t)cy * fnv32((uint32_t)cx));
 	const uint32_t sample_idx = S.base_offset + S.pass_offset + (uint32_t)sc.s;   // PixelSamplingData::sample_
 	float dx = 0.5f, dy = 0.5f;
 	if(S.aa_multipass)
@@ -303,7 +304,7 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 		dx = (0.5f + (float)sc.s) * d_1;
 		dy = riLp((uint32_t)sc.s + offset);
 	}
-	const float px = (float)sc.x + dx, py = (float)sc.y + dy;
+	const float px = (float)cx + dx, py = (float)cy + dy;
 	// camera_perspective.cc:128-146, plane.h:37-40
 	const DevCamera &c = S.cam;
 	const V3 pos = v3(c.pos[0], c.pos[1], c.pos[2]);
@@ -1921,7 +1922,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				sid = pr.x;
 				stage = pr.y;
 				sc = sampleAt(S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
-				pix = make_uint2(fnv32((uint32_t)sc.y * fnv32((uint32_t)sc.x)), S.base_offset + S.pass_offset + (uint32_t)sc.s);
+				pix = make_uint2(fnv32((uint32_t)(sc.y + S.crop_y0) * fnv32((uint32_t)(sc.x + S.crop_x0))),
+				                 S.base_offset + S.pass_offset + (uint32_t)sc.s);
 			}
 			else
 			{
@@ -2668,7 +2670,7 @@ __global__ void __launch_bounds__(256) k_film(DevFilm F, const float4 *samples, 
 	for(int c = 0; c < n; ++c)
 	{
 		const int px = sx[c], py = sy[c];
-		const uint32_t offset = fnv32((uint32_t)py * fnv32((uint32_t)px));
+		const uint32_t offset = fnv32((uint32_t)(py + F.crop_y0) * fnv32((uint32_t)(px + F.crop_x0)));
 		const int ox = x - px, oy = y - py;
 		// adaptive pass: only resampled pixels splat.  (Skipping them while building the candidate list
 		// instead lost diagonal candidates in the unrolled k_film<1, 0> — tools/film_probe.hip.)

@@ -137,6 +137,8 @@ class Render:
     ray_min_dist_auto: bool = True
     ray_min_dist: float = 0.00005
     base_sampling_offset: int = 0
+    xstart: int = 0                         # cropped film: its origin in camera pixels (imagefilm.cc:66)
+    ystart: int = 0
     rr_seed: int = 0                        # GPU-core "adv_rr_seed" (the oracle's OracleScene rr_seed)
     computer_node: int = 0
     # film load/save (imagefilm.cc:55-118)
@@ -639,6 +641,9 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetString("background_name", "world_background")
     api.paramsSetInt("width", r.width)
     api.paramsSetInt("height", r.height)
+    if r.xstart or r.ystart:
+        api.paramsSetInt("xstart", r.xstart)
+        api.paramsSetInt("ystart", r.ystart)
     api.paramsSetInt("AA_minsamples", r.aa_samples)
     api.paramsSetInt("AA_passes", r.aa_passes)
     if r.aa_inc_samples > 0:

@@ -2856,6 +2856,10 @@ class Renderer
 		void renderPixel(Thread &th, Mwc &rng, int i, int j, float *out, int n_samples, int pass_offs) const
 		{
 			const yc_render &rp = sc_.rp;
+			// film pixel (j, i) is camera pixel (j + crop_x0, i + crop_y0): renderTile's loops run over
+			// the splitter's areas in camera coordinates (imagesplitter.cc:43-46, integrator_tiled.cc:288-342)
+			i += rp.crop_y0;
+			j += rp.crop_x0;
 			const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
 			// :284-285, 315-316: lens streams Halton(3) / Halton(5) started at pass offset + pixel offset
 			HaltonSeq hal_u(3), hal_v(5);
@@ -3148,7 +3152,7 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 					for(int j = a.x; j < a.x + a.w; ++j)
 					{
 						if(adaptive && !flags[(size_t)i * W + j]) continue;
-						const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
+						const uint32_t offset = fnv32(static_cast<uint32_t>(i + rp.crop_y0) * fnv32(static_cast<uint32_t>(j + rp.crop_x0)));
 						for(int sample = 0; sample < n_samples; ++sample)
 						{
 							float dx, dy;
@@ -3233,7 +3237,7 @@ int yc_render_samples(const yc_scene *s, int n, const int *xys, float *rgba)
 	const float d_1 = 1.f / static_cast<float>(spp);
 	for(int k = 0; k < n; ++k)
 	{
-		const int j = xys[3 * k], i = xys[3 * k + 1], sample = xys[3 * k + 2];
+		const int j = xys[3 * k] + rp.crop_x0, i = xys[3 * k + 1] + rp.crop_y0, sample = xys[3 * k + 2];
 		const uint32_t offset = fnv32(static_cast<uint32_t>(i) * fnv32(static_cast<uint32_t>(j)));
 		float dx = 0.5f, dy = 0.5f;
 		if(spp > 1)

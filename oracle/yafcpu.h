@@ -174,6 +174,9 @@ typedef struct {
 	int pm_fg;
 	int fg_samples, fg_bounces;
 	float fg_min_pathlen;
+	// cropped film (imagefilm.cc:66, 129-132): the film covers camera pixels [crop_x0, crop_x0 + width)
+	// x [crop_y0, crop_y0 + height); pixel sampling and camera rays use the camera's coordinates
+	int crop_x0, crop_y0;
 } yc_render;
 
 typedef struct {
