@@ -263,6 +263,7 @@ struct DevScene
 	struct DevStats *stats;        // per-workgroup counters (null: not counted)
 	int trace_stats;               // k_trace counts node visits / triangle tests (0: rays only)
 	int crop_x0, crop_y0;          // cropped film (xstart / ystart): film pixel (x, y) = camera pixel (x + crop_x0, y + crop_y0)
+	int show_map;                  // PhotonIntegrator show_map: camera hits show the nearest photon (k_gather, G_SHOWMAP)
 	uint32_t node_base;            // node id of spawn slot 0 (= level-0 capacity of the chunk)
 	uint32_t spawn_cap;
 	float4 *node_own;              // per node: colour before recursiveRaytrace's result, alpha
@@ -349,6 +350,7 @@ enum : uint32_t
 	G_CAUSTIC = 2u,   // causticPhotons()
 	G_EXTRA = 4u,     // then add extra.xyz
 	G_FG = 8u,        // finalGathering() (k_fg, before k_gather): extra.xy = (pixel offset, sample index) bits
+	G_SHOWMAP = 16u,  // show_map: the nearest photon's colour (radiance map with final gathering, else the diffuse map)
 };
 
 // Queues are segmented: segment b (capacity cap_a entries / cap_s shadow rays) belongs to workgroup

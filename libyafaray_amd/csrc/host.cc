@@ -805,7 +805,11 @@ bool Scene::createIntegrator(const std::string &name, const ParamMap &p)
 			log.error("PhotonIntegrator: finalGather with transpShad is not supported by the GPU core yet (gather paths test opaque shadows)");
 			return false;
 		}
-		if(show_map || ao) { log.error("PhotonIntegrator: show_map / do_AO are not supported by the GPU core yet"); return false; }
+		// do_AO only feeds the ambient-occlusion render layers (generateOcclusionLayers,
+		// integrator_photon_mapping.cc:991-995); the combined image the GPU core produces does not use it
+		// (PhotonIntegrator::integrate never calls sampleAmbientOcclusion)
+		if(ao) log.info("PhotonIntegrator: do_AO only affects the AO render layers; the combined layer is unchanged");
+		(void)show_map;
 		if(processing != "generate") { log.error("PhotonIntegrator: photon_maps_processing '" + processing + "' is not supported (generate only)"); return false; }
 	}
 	integrators[name] = p;
@@ -1171,6 +1175,9 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			ip.get("fg_bounces", fg_bounces);
 			ip.get("fg_min_pathlen", gather_dist);
 			rp.pm.final_gather = fg && diffuse;
+			bool show_map = false;
+			ip.get("show_map", show_map);
+			S.show_map = (show_map && diffuse && rp.pm.photons > 0) ? 1 : 0;
 			rp.pm.fg_samples = fg_samples;
 			rp.pm.fg_bounces = fg_bounces;
 			rp.pm.fg_min_pathlen = gather_dist;

@@ -73,6 +73,7 @@ enum : uint32_t
 	F_PEND_EMIT = 1u << 20,      // pending emission add
 	F_V0_DIFFUSE = 1u << 21,     // v0 had the Diffuse flag (NEE estimated there)
 	F_COLS = 1u << 22,           // compact record: a nonzero first-vertex estimate is stored in csmp[sample id]
+	F_SHOWMAP = 1u << 16,        // PhotonIntegrator show_map camera hit (shares bit 16 with F_SAMPLED: path tracing only)
 	F_AO_EMIT = 1u << 23,        // ambient occlusion at an emitting v0: pend_emit holds emit(wo)
 	F_LNUM_SHIFT = 24            // light picked by estimateOneDirectLight (8 bits)
 };
@@ -2048,10 +2049,13 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 					col_ld = true;
 					col_dirty = true;
 					// photon_mapping.cc:868-869 adds emit(wo) unconditionally and :938-946 adds it again
-					// for emitting materials; the other integrators add it once (direct_light.cc:120)
+					// for emitting materials; the other integrators add it once (direct_light.cc:120);
+					// show_map (:876-881, 924-929): the first emit, then the nearest photon (k_gather)
+					const bool show = is_photon && S.show_map;
 					if(is_photon) col = col + matEmit<EXT>(m, sp, wo);
-					if(sp.flags & B_EMIT) col = col + matEmit<EXT>(m, sp, wo);
-					if(sp.flags & B_DIFFUSE) { nee_v0 = true; flags |= F_V0_DIFFUSE; }
+					if((sp.flags & B_EMIT) && !show) col = col + matEmit<EXT>(m, sp, wo);
+					if(sp.flags & B_DIFFUSE) { nee_v0 = !show; flags |= F_V0_DIFFUSE; }
+					if(show) flags |= F_SHOWMAP;
 					if(S.do_ao && (sp.flags & B_DIFFUSE) && (sp.flags & B_EMIT))
 					{
 						emit_pend = matEmit<EXT>(m, sp, wo);   // sampleAmbientOcclusion adds sp.emit(wo) * pdf per sample
@@ -2216,13 +2220,16 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		// a diffuse first hit still owes its photon-map estimates (k_gather): the diffuse map's
 		// density estimate (photon mapping) and / or causticPhotons(); whatever the integrator adds
 		// after them rides along as `extra` (DirectLight: the AO sum; path tracing: the paths)
-		const bool want_gather = live && finalize && (flags & F_V0_DIFFUSE) && ((is_photon && S.n_photons > 0) || S.caus_map);
+		// show_map: every camera hit asks for its nearest photon (and the caustics at diffuse hits)
+		const bool want_show = live && finalize && is_photon && (flags & F_SHOWMAP);
+		const bool want_gather = want_show || (live && finalize && (flags & F_V0_DIFFUSE) && ((is_photon && S.n_photons > 0) || S.caus_map));
 		C3 g_extra = c3(0.f);
 		uint32_t g_mode = 0;
 		if(want_gather)
 		{
 			loadCol();
 			g_mode = ((is_photon && S.n_photons > 0) ? (S.fg_on ? G_FG : G_DIFFUSE) : 0u) | (S.caus_map ? G_CAUSTIC : 0u);
+			if(want_show) g_mode = G_SHOWMAP | ((S.caus_map && (flags & F_V0_DIFFUSE)) ? G_CAUSTIC : 0u);
 			// final gathering (k_fg) needs the PixelSamplingData of the sample
 			if(g_mode & G_FG) g_extra = C3{__uint_as_float(offset), __uint_as_float(sample_idx), 0.f};
 			if(ao_after_caustic && S.do_ao) { g_extra = ao_extra; g_mode |= G_EXTRA; }
@@ -3267,6 +3274,8 @@ __device__ __forceinline__ int pkLookup(const uint4 *nodes, V3 p, int k, float &
 	return found;
 }
 
+__device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2);
+
 template<bool SMALL, bool EXT>
 __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 {
@@ -3336,6 +3345,22 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 				const C3 surf_col = matEval<EXT>(m, sp, wo, xyz(b), B_DIFFUSE);
 				const C3 col_tmp = surf_col * scale * pc;
 				col = col + col_tmp;
+			}
+		}
+		// ---- show_map (integrator_photon_mapping.cc:876-881 final gathering: the radiance map within
+		// lookup_rad_; :924-929: the diffuse map within ds_radius_): the nearest photon facing the shading normal
+		if(mode & G_SHOWMAP)
+		{
+			const V3 n = faceForward(sp.ng, sp.n, wo);
+			if(S.fg_on)
+			{
+				const int nn = S.n_rphotons > 0 ? pkNearest(S.rpk_nodes, S.rph_dir, p, n, S.fg_lookup_rad) : -1;
+				if(nn >= 0) col = col + C3{S.rph_pos[nn].w, S.rph_dir[nn].w, S.rph_colb[nn]};
+			}
+			else
+			{
+				const int nn = S.n_photons > 0 ? pkNearest(S.pk_nodes, S.ph_dir, p, n, S.pm_radius2) : -1;
+				if(nn >= 0) col = col + C3{S.ph_pos[nn].w, S.ph_dir[nn].w, S.ph_colb[nn]};
 			}
 		}
 		// ---- causticPhotons / estimateCausticPhotons (integrator_montecarlo.cc:410-419, 627-648) ----

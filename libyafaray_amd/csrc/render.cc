@@ -1338,7 +1338,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// (photon mapping, DirectLight) connects its NEE in iteration 1 and finishes there; path
 			// tracing finishes paths in any iteration
 			const bool dl_pipeline = S.integrator != INT_PATH;
-			if(S.gather_on && (!dl_pipeline || it == 1))
+			// (show_map: the camera hits finish in iteration 0, with their nearest-photon requests)
+			if(S.gather_on && (!dl_pipeline || it == 1 || (S.show_map && it == 0)))
 			{
 				// final gathering adds its estimate to the requests' colour before k_gather ends them
 				if(S.fg_on) PROF(KK_FG, yafamd_launch_fg(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));

@@ -173,6 +173,8 @@ class Render:
     # PhotonIntegrator final gathering (factory :777-810; the reference default is on)
     pm_final_gather: bool = False
     fg_samples: int = 32
+    pm_show_map: bool = False               # PhotonIntegrator "show_map" (integrator_photon_mapping.cc:876-881, 924-929)
+    pm_do_ao: bool = False                  # PhotonIntegrator "do_AO" (affects only the AO render layers)
     fg_bounces: int = 2
     fg_min_pathlen: float = None            # default: diffuseRadius
     # DirectLight ambient occlusion (integrator_direct_light.cc:161-186)
@@ -618,6 +620,10 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetInt("caustic_mix", cm.search)
         api.paramsSetFloat("causticRadius", cm.radius)
         api.paramsSetBool("finalGather", bool(r.pm_final_gather))
+        if r.pm_show_map:
+            api.paramsSetBool("show_map", True)
+        if r.pm_do_ao:
+            api.paramsSetBool("do_AO", True)
         if r.pm_final_gather:
             api.paramsSetInt("fg_samples", r.fg_samples)
             api.paramsSetInt("fg_bounces", r.fg_bounces)

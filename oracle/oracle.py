@@ -92,7 +92,7 @@ class yc_render(C.Structure):
                 ("caus_map", C.c_int), ("caus_photons", C.c_int), ("caus_search", C.c_int), ("caus_depth", C.c_int),
                 ("caus_radius", C.c_float), ("tiles_order", C.c_int),
                 ("pm_fg", C.c_int), ("fg_samples", C.c_int), ("fg_bounces", C.c_int), ("fg_min_pathlen", C.c_float),
-                ("crop_x0", C.c_int), ("crop_y0", C.c_int)]
+                ("crop_x0", C.c_int), ("crop_y0", C.c_int), ("pm_show_map", C.c_int)]
 
 
 class yc_scene(C.Structure):
@@ -587,6 +587,7 @@ class OracleScene:
         rp.ray_min_dist_auto, rp.ray_min_dist = int(r.ray_min_dist_auto), r.ray_min_dist
         rp.base_sampling_offset = r.base_sampling_offset
         rp.crop_x0, rp.crop_y0 = getattr(r, "xstart", 0), getattr(r, "ystart", 0)
+        rp.pm_show_map = int(bool(getattr(r, "pm_show_map", False)))
         rp.clamp_samples = r.clamp_samples
         rp.threads = threads
         rp.rr_seed = rr_seed

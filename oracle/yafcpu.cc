@@ -2771,7 +2771,17 @@ class Renderer
 				const unsigned mat_bsdfs = sp.bsdf_flags;
 				additional_depth = std::max(additional_depth, sp.mat->additional_depth);   // :863
 				col += emit(sp, wo);                                   // :868-869
-				if(rp.pm_fg)
+				if(rp.pm_show_map && !dmap.photons.empty())
+				{
+					// :876-881 (final gathering: the radiance map within lookup_rad_) / :924-929 (the
+					// diffuse map within ds_radius_): the nearest photon facing the shading normal
+					const V3 n = faceForward(sp.ng, sp.n, wo);
+					const PhotonMapData &M = rp.pm_fg ? rmap : dmap;
+					const float r2 = rp.pm_fg ? 4 * rp.pm_diffuse_radius * rp.pm_diffuse_radius : rp.pm_diffuse_radius;   // :245
+					const int nearest = M.photons.empty() ? -1 : findNearest(M, sp.p, n, r2);
+					if(nearest >= 0) col += M.photons[nearest].col;
+				}
+				else if(rp.pm_fg)
 				{
 					// :874-917 (use_photon_diffuse_ && final_gather_), clamp_indirect = 0
 					if(mat_bsdfs & BEmit) col += emit(sp, wo);         // :895-903

@@ -177,6 +177,9 @@ typedef struct {
 	// cropped film (imagefilm.cc:66, 129-132): the film covers camera pixels [crop_x0, crop_x0 + width)
 	// x [crop_y0, crop_y0 + height); pixel sampling and camera rays use the camera's coordinates
 	int crop_x0, crop_y0;
+	// PhotonIntegrator "show_map" (integrator_photon_mapping.cc:876-881, 924-929): the nearest photon's
+	// colour (radiance map with final gathering, else the diffuse map) instead of the estimates
+	int pm_show_map;
 } yc_render;
 
 typedef struct {

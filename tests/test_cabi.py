@@ -56,7 +56,7 @@ def test_scene_staging_and_loud_failure_without_gpu(product):
     spec = scenes.cornell(32, 24, spp=2)
     scenes.apply(spec, yi)
     assert yi.getSceneFilmWidth() == 32 and yi.getSceneFilmHeight() == 24
-    if torch.cuda.is_available():
+    if torch.cuda.is_available() or os.path.exists("/dev/kfd"):
         pytest.skip("GPU present: the render path is covered by the gpu tests")
     with pytest.raises(RuntimeError, match="no HIP device"):
         yi.render()
@@ -71,8 +71,12 @@ def test_unsupported_plugins_rejected_reference_style(product):
     assert yi.createMaterial("g") == 0           # material.cc:52-61: unknown/unsupported -> null
     yi.paramsClearAll()
     yi.paramsSetString("type", "photonmapping")
-    yi.paramsSetBool("show_map", True)              # not served by the GPU core
-    assert yi.createIntegrator("pm") == 0
+    yi.paramsSetBool("show_map", True)              # served (k_gather's nearest-photon requests)
+    assert yi.createIntegrator("pm") == 1
+    yi.paramsClearAll()
+    yi.paramsSetString("type", "photonmapping")
+    yi.paramsSetString("photon_maps_processing", "bogus")   # unknown mode
+    assert yi.createIntegrator("pm_bad") == 0
     yi.paramsClearAll()
     yi.paramsSetString("type", "photonmapping")     # reference defaults (final gathering on)
     assert yi.createIntegrator("pm2") == 1
