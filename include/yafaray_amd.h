@@ -55,6 +55,9 @@ typedef struct
 	int64_t fg_thin_rounds;     /* final gathering: GPU thinning rounds (-1: thinned on the host) */
 	uint64_t gather_queries;    /* photon-map estimate requests k_gather served (1.2) */
 	uint64_t gather_photons;    /* photon records the density estimates read (1.2) */
+	int32_t photon_maps_mode;   /* photon_maps_processing the last render used after its fallbacks: 0 generate,
+	                               1 generate-save, 2 load, 3 reuse-previous (1.2) */
+	int32_t reserved0;
 } yafaray_amd_stats_t;
 
 /* Bytes of the LIBYAFARAY_AMD_1.0 struct (its fields end at photon_tree_seconds): yafaray_amd_getStats

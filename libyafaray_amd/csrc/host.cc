@@ -198,6 +198,7 @@ bool Scene::renderDeviceGroup(RenderParams &rp)
 		r.shard_rank = m;
 		r.shard_y0 = rp.band_bounds[(size_t)m];
 		r.shard_y1 = rp.band_bounds[(size_t)m + 1];
+		r.pm.write_files = m == 0;
 		if(m > 0)
 		{
 			// the client's callbacks run on the caller's thread only (member 0)
@@ -212,6 +213,7 @@ bool Scene::renderDeviceGroup(RenderParams &rp)
 	ok[0] = ms[0]->renderMember(rps[0], &canceled) ? 1 : 0;
 	for(std::thread &t : th) t.join();
 	for(GpuRenderer *g : ms) g->setPeers(nullptr, 0);
+	rp.pm.processing = rps[0].pm.processing;
 	// counters and per-kernel times summed over the members (GPU time), wall time of the slowest
 	yafaray_amd_stats_t st = ms[0]->stats();
 	if(!kt_sum_) kt_sum_.reset(new KernelTimes);
@@ -788,18 +790,21 @@ bool Scene::createIntegrator(const std::string &name, const ParamMap &p)
 		log.error("Scene: integrator type '" + type + "' is not supported by the GPU core (directlighting, pathtracing, photonmapping)");
 		return false;
 	}
+	if(integrators.count(name))
+	{
+		log.warning("Scene: Integrator '" + name + "' already exists!");   // scene.cc:419-422 (createMapItem)
+		return false;
+	}
 	if(type == "photonmapping")
 	{
 		// integrator_photon_mapping.cc:765-850.  The GPU core serves the diffuse photon map with the
-		// k-NN density estimate (finalGather = false) or final gathering (the default); map display,
-		// ambient occlusion and photon-map files are not part of it yet.
+		// k-NN density estimate (finalGather = false) or final gathering (the default), the map display
+		// (show_map) and the photon map files / reuse (photon_maps_processing).
 		bool fg = true, show_map = false, ao = false, transp_shad = false;
-		std::string processing = "generate";
 		p.get("finalGather", fg);
 		p.get("show_map", show_map);
 		p.get("do_AO", ao);
 		p.get("transpShad", transp_shad);
-		p.get("photon_maps_processing", processing);
 		if(fg && transp_shad)
 		{
 			log.error("PhotonIntegrator: finalGather with transpShad is not supported by the GPU core yet (gather paths test opaque shadows)");
@@ -810,9 +815,20 @@ bool Scene::createIntegrator(const std::string &name, const ParamMap &p)
 		// (PhotonIntegrator::integrate never calls sampleAmbientOcclusion)
 		if(ao) log.info("PhotonIntegrator: do_AO only affects the AO render layers; the combined layer is unchanged");
 		(void)show_map;
-		if(processing != "generate") { log.error("PhotonIntegrator: photon_maps_processing '" + processing + "' is not supported (generate only)"); return false; }
 	}
 	integrators[name] = p;
+	// photon_maps_processing (integrator_photon_mapping.cc:844-847, integrator_path_tracer.cc:360-363;
+	// other integrators keep MonteCarloIntegrator's PhotonsGenerateOnly): an unknown value generates
+	IntegratorState &st = integrator_state[name];
+	st.id = ++integrator_ids_;
+	st.processing = PhotonParams::PM_GENERATE;
+	std::string processing = "generate";
+	if((type == "photonmapping" || type == "pathtracing") && p.get("photon_maps_processing", processing))
+	{
+		if(processing == "generate-save") st.processing = PhotonParams::PM_GENERATE_SAVE;
+		else if(processing == "load") st.processing = PhotonParams::PM_LOAD;
+		else if(processing == "reuse-previous") st.processing = PhotonParams::PM_REUSE;
+	}
 	return true;
 }
 
@@ -1156,6 +1172,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			ip.get("caustics", caustics);
 			ip.get("diffuse", diffuse);
 			rp.pm.photons = diffuse ? std::max(0, photons) : 0;
+			rp.pm.diffuse_map = diffuse;
 			// the caustic map: MonteCarloIntegrator::createCausticMap with caus_depth = bounces
 			rp.pm.caustic_map = caustics;
 			rp.pm.caustic_photons = std::max(0, cphotons);
@@ -1513,6 +1530,13 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 				progress(n_pix, (int)((double)n_pix * (double)done / (double)std::max<uint64_t>(1, total)), "Rendering...", progress_data);
 			};
 		}
+		// photon_maps_processing: files next to the film's load / save path (getFilmSavePath), written by
+		// one member of a group
+		IntegratorState &ist = integrator_state[s.integrator_name];
+		rp.pm.processing = ist.processing;
+		rp.pm.owner = ist.id;
+		rp.pm.map_path = s.film_load_save_path;
+		rp.pm.write_files = io_member;
 		bool ok;
 		if(!grouped)
 		{
@@ -1525,6 +1549,8 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			ok = gpu()->renderMember(rp, &canceled);
 		}
 		else ok = renderDeviceGroup(rp);
+		if(ist.processing == PhotonParams::PM_LOAD && rp.pm.processing == PhotonParams::PM_GENERATE_SAVE)
+			ist.processing = PhotonParams::PM_GENERATE_SAVE;   // integrator_photon_mapping.cc:323, montecarlo.cc:560
 		if(!ok) return false;
 		if(grouped)
 		{

@@ -201,6 +201,12 @@ class Scene
 		std::map<std::string, std::string> views;     // view name -> camera name
 		std::map<std::string, std::vector<float>> backgrounds;   // colour * power
 		std::map<std::string, ParamMap> integrators;
+		// per integrator: its instance id (the photon maps a render keeps belong to it) and its
+		// photon_maps_processing mode (a failed "load" turns into "generate-save" for good, as the
+		// reference's PhotonIntegrator rewrites its photon_map_processing_)
+		struct IntegratorState { uint64_t id = 0; int processing = 0; };
+		std::map<std::string, IntegratorState> integrator_state;
+		uint64_t integrator_ids_ = 0;
 		std::vector<std::string> layers;
 		std::map<std::string, ParamMap> outputs;
 		std::map<std::string, std::shared_ptr<HostImage>> images;

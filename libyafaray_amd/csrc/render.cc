@@ -2,6 +2,7 @@
 // through the extern "C" wrappers at the end of kernels.hip.
 #include "render.h"
 #include "devmath.h"
+#include "photonfile.h"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -259,6 +260,8 @@ struct GpuRenderer::Impl
 	Buf seg_pos, seg_dir, seg_colb, seg_ra, seg_rb, seg_rc;
 	int n_rphotons = 0;
 	uint32_t n_rad_points = 0;
+	int d_depth = 0, r_depth = 0;           // kd-tree depths of the diffuse / radiance maps
+	uint64_t map_owner[3] = {0, 0, 0};      // integrator instance that built / loaded each map (diffuse, caustic, radiance)
 	// render group (RCCL communicator over the group's GPUs) and its exchange buffers
 	ncclComm_t comm = nullptr;
 	Buf g_send, g_recv, g_wsend, g_wrecv, g_times, g_status;
@@ -898,19 +901,15 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	stats_.radiance_photons = nk;
 	stats_.fg_thin_rounds = rounds;
 	stats_.fg_thin_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
-	S.fg_on = 1;
-	S.fg_samples = pm.fg_samples;
-	S.fg_bounces = pm.fg_bounces;
-	S.fg_min_pathlen = pm.fg_min_pathlen;
-	S.fg_lookup_rad = 4 * pm.radius2 * pm.radius2;                                   // :245
-	S.fg_i_scale = static_cast<float>(1.f / ((float)S.pm_paths * 3.1415926535897932384626433832795L));   // :53 (math::num_pi)
-	S.n_rphotons = (int)nk;
+	d.n_rphotons = 0;
+	d.r_depth = 0;
+	publishRadianceMap(S, pm, 0);
 	std::ostringstream os;
 	os << "PhotonIntegrator: " << nr << " radiance points, " << nk << " kept for the radiance map ("
 	   << (rounds >= 0 ? "GPU thinning, " + std::to_string(rounds) + " rounds" : std::string("host thinning")) << ", "
 	   << stats_.fg_thin_seconds * 1e3 << " ms)";
 	log_.info(os.str());
-	if(nk == 0) { S.rpk_nodes = nullptr; return true; }
+	if(nk == 0) return true;
 	if(!ensure(log_, d.rph_pos, (size_t)nk * 16) || !ensure(log_, d.rph_dir, (size_t)nk * 16) || !ensure(log_, d.rph_colb, (size_t)nk * 4) ||
 	   !ensure(log_, d.rpk_nodes, (2 * (size_t)nk - 1) * sizeof(uint4)))
 		return false;
@@ -923,19 +922,124 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)d.rph_pos.p, nk, (uint4 *)d.rpk_nodes.p, &depth, d.stream, &d.pkd_scratch));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	d.n_rphotons = (int)nk;
+	d.r_depth = depth;
 	stats_.fg_radiance_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
-	S.rph_pos = (const float4 *)d.rph_pos.p;
-	S.rph_dir = (const float4 *)d.rph_dir.p;
-	S.rph_colb = (const float *)d.rph_colb.p;
-	S.rpk_nodes = (const uint4 *)d.rpk_nodes.p;
+	publishRadianceMap(S, pm, nk);
 	return true;
+}
+
+// The scene fields of final gathering over a radiance map of nk photons (built, loaded or kept).
+void GpuRenderer::publishRadianceMap(DevScene &S, const PhotonParams &pm, uint32_t nk)
+{
+	Impl &d = *d_;
+	S.fg_on = 1;
+	S.fg_samples = pm.fg_samples;
+	S.fg_bounces = pm.fg_bounces;
+	S.fg_min_pathlen = pm.fg_min_pathlen;
+	S.fg_lookup_rad = 4 * pm.radius2 * pm.radius2;                                   // :245
+	S.fg_i_scale = static_cast<float>(1.f / ((float)S.pm_paths * 3.1415926535897932384626433832795L));   // :53 (math::num_pi)
+	S.n_rphotons = (int)nk;
+	S.rph_pos = nk ? (const float4 *)d.rph_pos.p : nullptr;
+	S.rph_dir = nk ? (const float4 *)d.rph_dir.p : nullptr;
+	S.rph_colb = nk ? (const float *)d.rph_colb.p : nullptr;
+	S.rpk_nodes = nk ? (const uint4 *)d.rpk_nodes.p : nullptr;
+}
+
+namespace
+{
+const char *const kMapNames[3] = {"Diffuse Photon Map", "Caustic Photon Map", "FG Radiance Photon Map"};   // :105-107, montecarlo.cc:49
+}
+
+// PhotonMap::load (photon.cc:54-87) into the device map `which` (0 diffuse, 1 caustic, 2 radiance)
+// and its kd-tree (updateTree).
+bool GpuRenderer::loadMap(RenderParams &rp, int which, const std::string &file)
+{
+	Impl &d = *d_;
+	log_.info(std::string("Integrator: Loading ") + kMapNames[which] + " from: " + file +
+	          ". If it does not match the scene you could have crashes and/or incorrect renders, USE WITH CARE!");
+	photonfile::Map m;
+	if(!photonfile::load(log_, file, m)) return false;
+	if(!m.has_dir)
+		log_.warning(std::string("Integrator: ") + file + " holds no photon directions (a reference-format file): they load as zero, "
+		             "as the reference's PhotonMap::load leaves them");
+	const uint32_t n = m.size();
+	Buf &pos = which == 0 ? d.ph_pos : which == 1 ? d.cph_pos : d.rph_pos;
+	Buf &dir = which == 0 ? d.ph_dir : which == 1 ? d.cph_dir : d.rph_dir;
+	Buf &colb = which == 0 ? d.ph_colb : which == 1 ? d.cph_colb : d.rph_colb;
+	Buf &nodes = which == 0 ? d.pk_nodes : which == 1 ? d.cpk_nodes : d.rpk_nodes;
+	std::vector<float4> hp(n), hd(n);
+	std::vector<float> hb(n);
+	for(size_t i = 0; i < n; ++i)
+	{
+		hp[i] = make_float4(m.pos[i * 3], m.pos[i * 3 + 1], m.pos[i * 3 + 2], m.col[i * 3]);
+		hd[i] = make_float4(m.dir[i * 3], m.dir[i * 3 + 1], m.dir[i * 3 + 2], m.col[i * 3 + 1]);
+		hb[i] = m.col[i * 3 + 2];
+	}
+	const size_t cap = std::max<size_t>(n, 1);
+	if(!ensure(log_, pos, cap * 16) || !ensure(log_, dir, cap * 16) || !ensure(log_, colb, cap * 4) || !ensure(log_, nodes, (2 * cap - 1) * sizeof(uint4)))
+		return false;
+	int depth = 0;
+	if(n)
+	{
+		HIPCHECK(hipMemcpyAsync(pos.p, hp.data(), (size_t)n * 16, hipMemcpyHostToDevice, d.stream));
+		HIPCHECK(hipMemcpyAsync(dir.p, hd.data(), (size_t)n * 16, hipMemcpyHostToDevice, d.stream));
+		HIPCHECK(hipMemcpyAsync(colb.p, hb.data(), (size_t)n * 4, hipMemcpyHostToDevice, d.stream));
+		PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)pos.p, n, (uint4 *)nodes.p, &depth, d.stream, &d.pkd_scratch));
+	}
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	if(which == 0) { d.n_photons = (int)n; d.pm_paths = m.paths; d.d_depth = depth; }
+	else if(which == 1) { d.c_photons = (int)n; d.c_paths = m.paths; d.c_depth = depth; }
+	else { d.n_rphotons = (int)n; d.r_depth = depth; }
+	d.map_owner[which] = rp.pm.owner;
+	std::ostringstream os;
+	os << "Integrator: " << kMapNames[which] << " loaded: " << n << " photons, " << m.paths << " paths (kd-tree depth " << depth << ")";
+	log_.info(os.str());
+	return true;
+}
+
+// PhotonMap::save (photon.cc:89-110) of the device map `which`, plus the direction block (photonfile.h).
+bool GpuRenderer::saveMap(RenderParams &rp, int which, const std::string &file)
+{
+	Impl &d = *d_;
+	const uint32_t n = (uint32_t)(which == 0 ? d.n_photons : which == 1 ? d.c_photons : d.n_rphotons);
+	const Buf &pos = which == 0 ? d.ph_pos : which == 1 ? d.cph_pos : d.rph_pos;
+	const Buf &dir = which == 0 ? d.ph_dir : which == 1 ? d.cph_dir : d.rph_dir;
+	const Buf &colb = which == 0 ? d.ph_colb : which == 1 ? d.cph_colb : d.rph_colb;
+	std::vector<float4> hp(n), hd(n);
+	std::vector<float> hb(n);
+	if(n)
+	{
+		HIPCHECK(hipMemcpyAsync(hp.data(), pos.p, (size_t)n * 16, hipMemcpyDeviceToHost, d.stream));
+		HIPCHECK(hipMemcpyAsync(hd.data(), dir.p, (size_t)n * 16, hipMemcpyDeviceToHost, d.stream));
+		HIPCHECK(hipMemcpyAsync(hb.data(), colb.p, (size_t)n * 4, hipMemcpyDeviceToHost, d.stream));
+		HIPCHECK(hipStreamSynchronize(d.stream));
+	}
+	photonfile::Map m;
+	m.name = kMapNames[which];
+	m.paths = which == 0 ? d.pm_paths : which == 1 ? d.c_paths : 0;   // the radiance map's paths stay 0 (:398, 585)
+	m.threads_pkd_tree = std::max(1, rp.pm.threads);
+	m.pos.resize((size_t)n * 3);
+	m.col.resize((size_t)n * 3);
+	m.dir.resize((size_t)n * 3);
+	for(size_t i = 0; i < n; ++i)
+	{
+		const float p[3] = {hp[i].x, hp[i].y, hp[i].z}, c[3] = {hp[i].w, hd[i].w, hb[i]}, w[3] = {hd[i].x, hd[i].y, hd[i].z};
+		for(int k = 0; k < 3; ++k)
+		{
+			m.pos[i * 3 + k] = p[k];
+			m.col[i * 3 + k] = c[k];
+			m.dir[i * 3 + k] = w[k];
+		}
+	}
+	log_.info(std::string("Integrator: Saving ") + kMapNames[which] + " to: " + file);
+	return photonfile::save(log_, file, m);
 }
 
 bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 {
 	Impl &d = *d_;
 	DevScene &S = rp.scene;
-	const PhotonParams &pm = rp.pm;
+	PhotonParams &pm = rp.pm;
 	S.n_photons = 0;
 	S.pm_paths = 0;
 	S.pm_search = pm.search;
@@ -951,62 +1055,134 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	const auto t0 = std::chrono::steady_clock::now();
 	// integrator_photon_mapping.cc:437 / integrator_montecarlo.cc:604 (threads_photons <= 0 counts as one)
 	const uint32_t T = (uint32_t)std::max(1, pm.threads);
-	int depth_c = 0, depth_d = 0;
-	d.c_photons = d.c_paths = d.c_depth = 0;
-	// ---- caustic map (createCausticMap, integrator_montecarlo.cc:565-625) ----
-	if(pm.caustic_map)
+	const bool want_diffuse = S.integrator == INT_PHOTON && pm.diffuse_map;
+	const bool want_fg = want_diffuse && pm.final_gather;
+	const bool want_caustic = pm.caustic_map;
+	d.pm_local = 0;
+	// ---- photon_maps_processing (integrator_photon_mapping.cc:279-385, integrator_montecarlo.cc:546-573) ----
+	int mode = pm.processing;
+	if(mode == PhotonParams::PM_LOAD)
 	{
-		if(d.n_cph_lights == 0) log_.warning("Integrator: no lights shoot caustic photons; caustic photon map empty");
-		else if(pm.caustic_photons > 0)
+		// every enabled map is read (caustic, diffuse, radiance); one failure regenerates all and saves them
+		bool failed = false;
+		if(want_caustic && !loadMap(rp, 1, pm.map_path + "_caustic.photonmap")) failed = true;
+		if(want_diffuse && !loadMap(rp, 0, pm.map_path + "_diffuse.photonmap")) failed = true;
+		if(want_fg && !loadMap(rp, 2, pm.map_path + "_fg_radiance.photonmap")) failed = true;
+		if(failed)
 		{
-			const uint32_t N = std::max(T, ((uint32_t)pm.caustic_photons / T) * T);
-			PhotonSet L{(const int *)d.cph_lights.p, (const float *)d.clight_cdf.p, (const float *)d.clight_func.p, d.clight_inv_integral,
-			            d.n_cph_lights, 1};
-			uint32_t n = 0;
-			if(!shootMap(rp, L, N, std::max(0, pm.caustic_depth), 1, n, depth_c)) return false;
-			d.c_photons = (int)n;
-			d.c_paths = (int)N;
-			stats_.caustic_photons = n;
-			d.c_depth = depth_c;
-			std::ostringstream os;
-			os << "Integrator: shot " << N << " caustic photons, stored " << n << " (kd-tree depth " << depth_c << ")";
-			log_.info(os.str());
-			if(n > 0)
+			log_.warning("Integrator: photon maps loading failed, changing to Generate and Save mode.");
+			mode = PhotonParams::PM_GENERATE_SAVE;
+		}
+	}
+	if(mode == PhotonParams::PM_REUSE)
+	{
+		// the maps of the previous render of this integrator, if it left them (an empty one cannot be reused)
+		auto keep = [&](bool want, int which, int count, const char *what) {
+			if(!want) return;
+			log_.info(std::string("Integrator: Reusing ") + what + " photon map from memory. If it does not match the scene you could have "
+			          "crashes and/or incorrect renders, USE WITH CARE!");
+			if(d.map_owner[which] != pm.owner || count == 0)
 			{
-				S.caus_map = 1;
-				S.c_photons = (int)n;
-				S.c_paths = (int)N;
-				S.cph_pos = (const float4 *)d.cph_pos.p;
-				S.cph_dir = (const float4 *)d.cph_dir.p;
-				S.cph_colb = (const float *)d.cph_colb.p;
-				S.cpk_nodes = (const uint4 *)d.cpk_nodes.p;
+				log_.warning(std::string("Integrator: ") + what + " photon map enabled but empty, cannot be reused: changing to Generate mode.");
+				mode = PhotonParams::PM_GENERATE;
+			}
+		};
+		keep(want_caustic, 1, d.c_photons, "caustics");
+		keep(want_diffuse, 0, d.n_photons, "diffuse");
+		keep(want_fg, 2, d.n_rphotons, "FG radiance");
+	}
+	// a group render: every member generates (the shooting is sharded) if any member has to
+	if(!rp.band_bounds.empty() && grouped())
+	{
+		const bool mine = mode == PhotonParams::PM_GENERATE || mode == PhotonParams::PM_GENERATE_SAVE;
+		const int st = groupStatus(mine ? 1 : 0);
+		if(st >= 2)
+		{
+			log_.error("GPU group: a member failed; render abandoned");
+			return false;
+		}
+		if(st == 1 && !mine)
+		{
+			log_.warning("GPU group: another member has to generate its photon maps; generating them here too");
+			mode = pm.processing == PhotonParams::PM_LOAD ? PhotonParams::PM_GENERATE_SAVE : PhotonParams::PM_GENERATE;
+		}
+	}
+	pm.processing = mode;
+	stats_.photon_maps_mode = mode;
+	const bool generate = mode == PhotonParams::PM_GENERATE || mode == PhotonParams::PM_GENERATE_SAVE;
+	if(generate)
+	{
+		int depth_c = 0, depth_d = 0;
+		d.c_photons = d.c_paths = d.c_depth = 0;
+		d.n_photons = d.pm_paths = d.d_depth = 0;
+		d.n_rphotons = d.r_depth = 0;
+		d.map_owner[0] = d.map_owner[1] = d.map_owner[2] = 0;
+		// ---- caustic map (createCausticMap, integrator_montecarlo.cc:565-625) ----
+		if(want_caustic)
+		{
+			if(d.n_cph_lights == 0) log_.warning("Integrator: no lights shoot caustic photons; caustic photon map empty");
+			else if(pm.caustic_photons > 0)
+			{
+				const uint32_t N = std::max(T, ((uint32_t)pm.caustic_photons / T) * T);
+				PhotonSet L{(const int *)d.cph_lights.p, (const float *)d.clight_cdf.p, (const float *)d.clight_func.p, d.clight_inv_integral,
+				            d.n_cph_lights, 1};
+				uint32_t n = 0;
+				if(!shootMap(rp, L, N, std::max(0, pm.caustic_depth), 1, n, depth_c)) return false;
+				d.c_photons = (int)n;
+				d.c_paths = (int)N;
+				d.c_depth = depth_c;
+				std::ostringstream os;
+				os << "Integrator: shot " << N << " caustic photons, stored " << n << " (kd-tree depth " << depth_c << ")";
+				log_.info(os.str());
+			}
+			d.map_owner[1] = pm.owner;
+		}
+		// ---- diffuse map (PhotonIntegrator::preprocess, integrator_photon_mapping.cc:242-638) ----
+		uint32_t n = 0;
+		uint32_t N = 0;
+		if(S.integrator == INT_PHOTON && pm.photons > 0)
+		{
+			if(d.n_ph_lights == 0) log_.warning("PhotonIntegrator: no lights shoot diffuse photons; diffuse photon map disabled");
+			else
+			{
+				N = std::max(T, ((uint32_t)pm.photons / T) * T);
+				PhotonSet L{(const int *)d.ph_lights.p, (const float *)d.light_cdf.p, (const float *)d.light_func.p, d.light_inv_integral,
+				            d.n_ph_lights, 0};
+				if(!shootMap(rp, L, N, pm.bounces, 0, n, depth_d)) return false;
+				if(n < 50) { log_.error("PhotonIntegrator: Too few diffuse photons, stopping now."); return false; }   // :448-452
 			}
 		}
-	}
-	// ---- diffuse map (PhotonIntegrator::preprocess, integrator_photon_mapping.cc:242-638) ----
-	uint32_t n = 0;
-	uint32_t N = 0;
-	if(S.integrator == INT_PHOTON && pm.photons > 0)
-	{
-		if(d.n_ph_lights == 0) log_.warning("PhotonIntegrator: no lights shoot diffuse photons; diffuse photon map disabled");
-		else
+		d.n_photons = (int)n;
+		d.pm_paths = (int)N;
+		d.d_depth = depth_d;
+		if(want_diffuse) d.map_owner[0] = pm.owner;
+		std::ostringstream os;
+		if(S.integrator == INT_PHOTON)
 		{
-			N = std::max(T, ((uint32_t)pm.photons / T) * T);
-			PhotonSet L{(const int *)d.ph_lights.p, (const float *)d.light_cdf.p, (const float *)d.light_func.p, d.light_inv_integral,
-			            d.n_ph_lights, 0};
-			if(!shootMap(rp, L, N, pm.bounces, 0, n, depth_d)) return false;
-			if(n < 50) { log_.error("PhotonIntegrator: Too few diffuse photons, stopping now."); return false; }   // :448-452
+			os << "PhotonIntegrator: shot " << N << " photons, stored " << n << " (kd-tree depth " << depth_d << ")";
+			log_.info(os.str());
 		}
 	}
-	d.n_photons = (int)n;
-	d.pm_paths = (int)N;
-	d.pm_stack = std::max(depth_d, depth_c) + 1;
+	// ---- the maps the render reads (generated, loaded or kept) ----
+	if(want_caustic && d.c_photons > 0)
+	{
+		S.caus_map = 1;
+		S.c_photons = d.c_photons;
+		S.c_paths = d.c_paths;
+		S.cph_pos = (const float4 *)d.cph_pos.p;
+		S.cph_dir = (const float4 *)d.cph_dir.p;
+		S.cph_colb = (const float *)d.cph_colb.p;
+		S.cpk_nodes = (const uint4 *)d.cpk_nodes.p;
+	}
+	const int n_diffuse = S.integrator == INT_PHOTON ? d.n_photons : 0;
+	// the radiance map of a generating render is at most as deep as the diffuse map it came from
+	d.pm_stack = std::max({d.d_depth, d.c_depth, generate ? 0 : d.r_depth}) + 1;
 	S.ph_pos = (const float4 *)d.ph_pos.p;
 	S.ph_dir = (const float4 *)d.ph_dir.p;
 	S.ph_colb = (const float *)d.ph_colb.p;
 	S.pk_nodes = (const uint4 *)d.pk_nodes.p;
-	S.n_photons = (int)n;
-	S.pm_paths = (int)N;
+	S.n_photons = n_diffuse;
+	S.pm_paths = S.integrator == INT_PHOTON ? d.pm_paths : 0;
 	S.pm_stack = d.pm_stack;
 	S.gather_on = (S.n_photons > 0 || S.caus_map) ? 1 : 0;
 	if(S.gather_on)
@@ -1019,14 +1195,34 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	}
 	S.fg_on = 0;
 	S.n_rphotons = 0;
-	if(S.integrator == INT_PHOTON && pm.final_gather && n > 0 && !buildRadianceMap(rp)) return false;
-	stats_.photons = n;
+	if(want_fg && n_diffuse > 0)
+	{
+		if(generate)
+		{
+			if(!buildRadianceMap(rp)) return false;
+			d.map_owner[2] = pm.owner;
+		}
+		else
+			publishRadianceMap(S, pm, (uint32_t)d.n_rphotons);
+	}
+	stats_.photons = (uint64_t)n_diffuse;
+	stats_.caustic_photons = S.caus_map ? (uint64_t)d.c_photons : 0;
+	if(S.fg_on) stats_.radiance_photons = (uint64_t)d.n_rphotons;
+	// ---- generate-save: the maps to files (integrator_photon_mapping.cc:599-624, montecarlo.cc:630-636) ----
+	if(mode == PhotonParams::PM_GENERATE_SAVE && pm.write_files)
+	{
+		bool ok = true;
+		if(want_diffuse) ok = saveMap(rp, 0, pm.map_path + "_diffuse.photonmap") && ok;
+		if(want_caustic) ok = saveMap(rp, 1, pm.map_path + "_caustic.photonmap") && ok;
+		if(want_fg && S.fg_on) ok = saveMap(rp, 2, pm.map_path + "_fg_radiance.photonmap") && ok;
+		if(!ok) log_.warning("Integrator: saving the photon maps failed; the render goes on");
+	}
 	const auto t2 = std::chrono::steady_clock::now();
 	stats_.photon_seconds = std::chrono::duration<double>(t2 - t0).count();
 	if(S.integrator == INT_PHOTON)
 	{
 		std::ostringstream os;
-		os << "PhotonIntegrator: shot " << N << " photons, stored " << n << " (kd-tree depth " << depth_d << ") in " << stats_.photon_seconds << " s";
+		os << "PhotonIntegrator: photon maps ready in " << stats_.photon_seconds << " s";
 		log_.info(os.str());
 	}
 	return true;

@@ -58,6 +58,13 @@ struct PhotonParams
 	int fg_samples = 32;
 	int fg_bounces = 2;
 	float fg_min_pathlen = 0.1f;   // gather_dist_ (default diffuseRadius)
+	// photon_maps_processing (integrator_photon_mapping.cc:844-847, integrator_path_tracer.cc:360-363)
+	int processing = PM_GENERATE;  // in: the integrator's mode; out: the mode the render used after fallbacks
+	bool diffuse_map = false;      // PhotonIntegrator "diffuse" (use_photon_diffuse_)
+	std::string map_path;          // film_load_save_path: <path>_diffuse / _caustic / _fg_radiance.photonmap
+	uint64_t owner = 0;            // the integrator instance the maps belong to ("reuse-previous")
+	bool write_files = true;       // this member writes the files (member 0 of a group)
+	enum : int { PM_GENERATE = 0, PM_GENERATE_SAVE = 1, PM_LOAD = 2, PM_REUSE = 3 };
 };
 
 // adaptive anti-aliasing (scene.cc:582-595, aa_noise_params.h:27-46; TiledIntegrator::render,
@@ -180,6 +187,11 @@ class GpuRenderer
 		bool buildPhotonMap(RenderParams &rp);
 		bool buildRadianceMap(RenderParams &rp);
 		bool shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int bounces, int which, uint32_t &n_out, int &depth_out);
+		// photon map files / maps kept from the previous render (photon_maps_processing); which: 0
+		// diffuse, 1 caustic, 2 radiance map
+		bool loadMap(RenderParams &rp, int which, const std::string &file);
+		bool saveMap(RenderParams &rp, int which, const std::string &file);
+		void publishRadianceMap(DevScene &S, const PhotonParams &pm, uint32_t nk);
 
 		// ---- render group: the film split into contiguous row bands over several GPUs ----
 		// One member per GPU (one process per GPU, each calling joinGroup with the same RCCL id).

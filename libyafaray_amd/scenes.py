@@ -175,6 +175,9 @@ class Render:
     fg_samples: int = 32
     pm_show_map: bool = False               # PhotonIntegrator "show_map" (integrator_photon_mapping.cc:876-881, 924-929)
     pm_do_ao: bool = False                  # PhotonIntegrator "do_AO" (affects only the AO render layers)
+    # photon_maps_processing (PhotonIntegrator / PathIntegrator): generate, generate-save, load, reuse-previous;
+    # the files are <film_load_save_path>_diffuse / _caustic / _fg_radiance.photonmap
+    pm_maps_processing: str = "generate"
     fg_bounces: int = 2
     fg_min_pathlen: float = None            # default: diffuseRadius
     # DirectLight ambient occlusion (integrator_direct_light.cc:161-186)
@@ -636,6 +639,8 @@ def apply(spec: SceneSpec, api) -> None:
         api.paramsSetInt("AO_samples", r.ao_samples)
         api.paramsSetFloat("AO_distance", r.ao_distance)
         api.paramsSetColor("AO_color", *r.ao_color, 1.0)
+    if r.integrator in ("pathtracing", "photonmapping") and r.pm_maps_processing != "generate":
+        api.paramsSetString("photon_maps_processing", r.pm_maps_processing)
     api.createIntegrator("default")
     api.paramsClearAll()
     api.paramsSetString("type", "combined")

@@ -92,7 +92,8 @@ class yc_render(C.Structure):
                 ("caus_map", C.c_int), ("caus_photons", C.c_int), ("caus_search", C.c_int), ("caus_depth", C.c_int),
                 ("caus_radius", C.c_float), ("tiles_order", C.c_int),
                 ("pm_fg", C.c_int), ("fg_samples", C.c_int), ("fg_bounces", C.c_int), ("fg_min_pathlen", C.c_float),
-                ("crop_x0", C.c_int), ("crop_y0", C.c_int), ("pm_show_map", C.c_int)]
+                ("crop_x0", C.c_int), ("crop_y0", C.c_int), ("pm_show_map", C.c_int),
+                ("pm_load_path", C.c_char_p)]
 
 
 class yc_scene(C.Structure):
@@ -588,6 +589,11 @@ class OracleScene:
         rp.base_sampling_offset = r.base_sampling_offset
         rp.crop_x0, rp.crop_y0 = getattr(r, "xstart", 0), getattr(r, "ystart", 0)
         rp.pm_show_map = int(bool(getattr(r, "pm_show_map", False)))
+        # photon_maps_processing "load": the maps from <film_load_save_path>_*.photonmap
+        self._load_path = None
+        if getattr(r, "pm_maps_processing", "generate") == "load":
+            self._load_path = getattr(r, "film_load_save_path", "./").encode()
+        rp.pm_load_path = self._load_path
         rp.clamp_samples = r.clamp_samples
         rp.threads = threads
         rp.rr_seed = rr_seed

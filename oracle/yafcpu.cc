@@ -2819,11 +2819,67 @@ class Renderer
 			else background(ray, col, alpha, ray_level);
 		}
 
+		// PhotonMap::load (photon.cc:54-87): "YAF_PHOTONMAPv1\0", name, paths, search radius, kd-tree
+		// threads, count, then position + colour per photon, and updateTree.  The file holds no
+		// directions and Photon() leaves dir_ uninitialised (photon.h:33): zero here, as fresh memory.
+		static bool loadPhotonMap(const std::string &file, PhotonMapData &M)
+		{
+			M = PhotonMapData{};
+			FILE *fp = std::fopen(file.c_str(), "rb");
+			if(!fp) return false;
+			auto readStr = [&](std::string &str) {
+				str.clear();
+				int c;
+				while((c = std::fgetc(fp)) != EOF && c != 0) str += (char)c;
+				return c == 0;
+			};
+			std::string header, name;
+			int32_t paths = 0, threads = 0;
+			float radius = 0.f;
+			uint32_t n = 0;
+			bool ok = readStr(header) && header == "YAF_PHOTONMAPv1" && readStr(name) && std::fread(&paths, 4, 1, fp) == 1 &&
+			          std::fread(&radius, 4, 1, fp) == 1 && std::fread(&threads, 4, 1, fp) == 1 && std::fread(&n, 4, 1, fp) == 1;
+			if(ok)
+			{
+				M.photons.resize(n);
+				for(Photon &p : M.photons)
+				{
+					float v[6];
+					if(std::fread(v, 4, 6, fp) != 6) { ok = false; break; }
+					p.pos = V3(v[0], v[1], v[2]);
+					p.dir = V3();
+					p.col.r = v[3];
+					p.col.g = v[4];
+					p.col.b = v[5];
+				}
+			}
+			std::fclose(fp);
+			if(!ok) { M = PhotonMapData{}; return false; }
+			M.n_paths = paths;
+			if(!M.photons.empty()) buildPhotonTree(M);
+			return true;
+		}
+
 		// preprocess: the caustic map (PathIntegrator / DirectLight / PhotonIntegrator, when enabled),
 		// then the diffuse map (PhotonIntegrator)
 		bool preprocessPhotons()
 		{
 			Thread th;
+			if(sc_.rp.pm_load_path)
+			{
+				const std::string base = sc_.rp.pm_load_path;
+				bool ok = true;
+				if(sc_.rp.caus_map) ok = loadPhotonMap(base + "_caustic.photonmap", cmap) && ok;
+				if(sc_.rp.integrator == YC_INT_PHOTON)
+				{
+					ok = loadPhotonMap(base + "_diffuse.photonmap", dmap) && ok;
+					if(sc_.rp.pm_fg) ok = loadPhotonMap(base + "_fg_radiance.photonmap", rmap) && ok;
+				}
+				if(ok) return true;
+				cmap = PhotonMapData{};   // a failed load generates every map (and would save them)
+				dmap = PhotonMapData{};
+				rmap = PhotonMapData{};
+			}
 			if(sc_.rp.caus_map)
 			{
 				shootCausticPhotons(th);

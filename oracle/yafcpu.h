@@ -180,6 +180,10 @@ typedef struct {
 	// PhotonIntegrator "show_map" (integrator_photon_mapping.cc:876-881, 924-929): the nearest photon's
 	// colour (radiance map with final gathering, else the diffuse map) instead of the estimates
 	int pm_show_map;
+	// photon_maps_processing "load" (integrator_photon_mapping.cc:279-326, montecarlo.cc:548-563): the
+	// maps come from <pm_load_path>_caustic / _diffuse / _fg_radiance.photonmap (PhotonMap::load,
+	// photon.cc:54-87); a failed load generates them.  NULL: generate.
+	const char *pm_load_path;
 } yc_render;
 
 typedef struct {

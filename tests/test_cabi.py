@@ -75,11 +75,14 @@ def test_unsupported_plugins_rejected_reference_style(product):
     assert yi.createIntegrator("pm") == 1
     yi.paramsClearAll()
     yi.paramsSetString("type", "photonmapping")
-    yi.paramsSetString("photon_maps_processing", "bogus")   # unknown mode
-    assert yi.createIntegrator("pm_bad") == 0
+    yi.paramsSetString("photon_maps_processing", "bogus")   # unknown mode: generate (factory :847)
+    assert yi.createIntegrator("pm_bad") == 1
     yi.paramsClearAll()
     yi.paramsSetString("type", "photonmapping")     # reference defaults (final gathering on)
     assert yi.createIntegrator("pm2") == 1
+    yi.paramsClearAll()
+    yi.paramsSetString("type", "pathtracing")
+    assert yi.createIntegrator("pm2") == 0          # duplicate name (scene.cc:419-422)
     yi.paramsClearAll()
     yi.paramsSetString("type", "photonmapping")
     yi.paramsSetBool("transpShad", True)            # final gathering traces opaque shadows only
