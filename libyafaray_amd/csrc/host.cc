@@ -798,23 +798,15 @@ bool Scene::createIntegrator(const std::string &name, const ParamMap &p)
 	if(type == "photonmapping")
 	{
 		// integrator_photon_mapping.cc:765-850.  The GPU core serves the diffuse photon map with the
-		// k-NN density estimate (finalGather = false) or final gathering (the default), the map display
-		// (show_map) and the photon map files / reuse (photon_maps_processing).
-		bool fg = true, show_map = false, ao = false, transp_shad = false;
-		p.get("finalGather", fg);
-		p.get("show_map", show_map);
+		// k-NN density estimate (finalGather = false) or final gathering (the default, with opaque or
+		// transparent shadows), the map display (show_map) and the photon map files / reuse
+		// (photon_maps_processing); the options are read at render time.
+		bool ao = false;
 		p.get("do_AO", ao);
-		p.get("transpShad", transp_shad);
-		if(fg && transp_shad)
-		{
-			log.error("PhotonIntegrator: finalGather with transpShad is not supported by the GPU core yet (gather paths test opaque shadows)");
-			return false;
-		}
 		// do_AO only feeds the ambient-occlusion render layers (generateOcclusionLayers,
 		// integrator_photon_mapping.cc:991-995); the combined image the GPU core produces does not use it
 		// (PhotonIntegrator::integrate never calls sampleAmbientOcclusion)
 		if(ao) log.info("PhotonIntegrator: do_AO only affects the AO render layers; the combined layer is unchanged");
-		(void)show_map;
 	}
 	integrators[name] = p;
 	// photon_maps_processing (integrator_photon_mapping.cc:844-847, integrator_path_tracer.cc:360-363;

@@ -2471,6 +2471,51 @@ __global__ void __launch_bounds__(kShadeBlock) k_surface(DevScene S, DevQueues Q
 // wo = the ray direction) at the surface point getSurface builds from the moved ray; then the NEE
 // contribution is rebuilt with `lcol *= scol` where the reference applies it.  Factors multiply in
 // ascending (t, primitive) order (the kd-tree's cell order: the same value for up to two surfaces).
+// tsFilterColor: that product for one ray (h: its n (t, prim) pairs; o, d: the moved shadow ray).
+__device__ C3 tsFilterColor(const DevScene &S, float2 *h, int n, V3 o, V3 d)
+{
+	// insertion sort by (t, prim)
+	for(int a = 1; a < n; ++a)
+	{
+		const float2 x = h[a];
+		int b = a - 1;
+		while(b >= 0 && (h[b].x > x.x || (h[b].x == x.x && __float_as_int(h[b].y) > __float_as_int(x.y))))
+		{
+			h[b + 1] = h[b];
+			--b;
+		}
+		h[b + 1] = x;
+	}
+	C3 scol = c3(1.f);
+	for(int a = 0; a < n; ++a)
+	{
+		const float t = h[a].x;
+		const int prim = __float_as_int(h[a].y);
+		const V3 p = o + t * d;
+		const float4 g = S.prim_ng[prim];
+		const V3 ng = xyz(g);
+		const DevMaterial &m = S.mats[__float_as_int(g.w)];
+		V3 nrm = ng;
+		C3 dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+		if(S.has_attr)
+		{
+			const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, o, d, p);
+			nrm = sa.n;
+			float drefl = 1.f, sigma = 0.f;
+			if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl, sigma);
+		}
+		const V3 nf = faceForward(ng, nrm, d);
+		const float kr = fresnelKr(m, d, nf);
+		float accum = 1.f;
+		if(m.sd_flags & SD_MIRROR) accum = 1.f - kr * m.comp[0];
+		accum *= m.comp[1] * accum;
+		const C3 tcol = m.tfilter * dcol + c3(1.f - m.tfilter);
+		scol = scol * (accum * tcol);
+	}
+	return scol;
+}
+
+// k_tshadow: the filter colour of each such ray times the NEE factors tsFactors stored
 __global__ void __launch_bounds__(kShadeBlock) k_tshadow(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P)
 {
 	const uint32_t seg = blockIdx.x;
@@ -2482,46 +2527,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_tshadow(DevScene S, DevQueues Q
 		const uint32_t k = s0 + j;
 		const int n = Q.ts_n[k];
 		if(n <= 0) continue;
-		float2 *h = Q.ts_hit + (size_t)k * cap;
-		// insertion sort by (t, prim)
-		for(int a = 1; a < n; ++a)
-		{
-			const float2 x = h[a];
-			int b = a - 1;
-			while(b >= 0 && (h[b].x > x.x || (h[b].x == x.x && __float_as_int(h[b].y) > __float_as_int(x.y))))
-			{
-				h[b + 1] = h[b];
-				--b;
-			}
-			h[b + 1] = x;
-		}
-		const V3 o = xyz(Q.sh_o[k]), d = xyz(Q.sh_d[k]);
-		C3 scol = c3(1.f);
-		for(int a = 0; a < n; ++a)
-		{
-			const float t = h[a].x;
-			const int prim = __float_as_int(h[a].y);
-			const V3 p = o + t * d;
-			const float4 g = S.prim_ng[prim];
-			const V3 ng = xyz(g);
-			const DevMaterial &m = S.mats[__float_as_int(g.w)];
-			V3 nrm = ng;
-			C3 dcol = C3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
-			if(S.has_attr)
-			{
-				const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, o, d, p);
-				nrm = sa.n;
-				float drefl = 1.f, sigma = 0.f;
-				if(m.n_nodes > 0) evalNodes(m, S.shader_nodes, S.textures, S.texels, sa, dcol, drefl, sigma);
-			}
-			const V3 nf = faceForward(ng, nrm, d);
-			const float kr = fresnelKr(m, d, nf);
-			float accum = 1.f;
-			if(m.sd_flags & SD_MIRROR) accum = 1.f - kr * m.comp[0];
-			accum *= m.comp[1] * accum;
-			const C3 tcol = m.tfilter * dcol + c3(1.f - m.tfilter);
-			scol = scol * (accum * tcol);
-		}
+		const C3 scol = tsFilterColor(S, Q.ts_hit + (size_t)k * cap, n, xyz(Q.sh_o[k]), xyz(Q.sh_d[k]));
 		const uint32_t e = (uint32_t)Q.sh_idx[k];
 		const float4 f0 = P.ts[3 * (size_t)e], f1 = P.ts[3 * (size_t)e + 1], f2 = P.ts[3 * (size_t)e + 2];
 		C3 x = rgb(f0) * (rgb(f1) * scol);
@@ -3543,16 +3549,38 @@ __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, flo
 }
 
 // MonteCarloIntegrator::doLightEstimation for one light (integrator_montecarlo.cc:80-408) with the
-// shadow rays traced in place: neeLight's arithmetic, neeSum's addition order
-template<bool EXT, bool WIDE, bool SPILL = true>
+// shadow rays traced in place: neeLight's arithmetic, neeSum's addition order.  TSH: transparent
+// shadows (tr_shad_, :112, 206, 330): the surfaces a shadow ray crosses are collected in ts_buf
+// (s_depth entries of this lane) and their filter colour scol multiplies the light colour
+// (:122, 212, 335) as k_tshadow does for the wavefront path.
+template<bool EXT, bool WIDE, bool SPILL = true, bool TSH = false>
 __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
-                                  uint32_t loffs, uint32_t sample_idx, uint32_t offset, uint32_t &visits, uint32_t &tests)
+                                  uint32_t loffs, uint32_t sample_idx, uint32_t offset, uint32_t &visits, uint32_t &tests,
+                                  float2 *ts_buf = nullptr)
 {
 	const bool cast_shadows = L.cast_shadows && m.receive_shadows;
 	const float p_len = length(sp.p);
 	const float sh_tmin = S.shadow_bias_auto ? S.shadow_bias * fmaxf(1.f, p_len) : S.shadow_bias;
 	float t_hit;
 	int p_hit;
+	// the shadow test of a moved shadow ray (origin so, [tmin, st)); scol = its filter colour
+	auto shadowed = [&](V3 so, V3 dir, float tmin, float st, C3 &scol) -> bool {
+		scol = c3(1.f);
+		if(!cast_shadows) return false;
+		if(TSH)
+		{
+			TsList Lt;
+			Lt.hit = ts_buf;
+			Lt.n = 0;
+			Lt.cap = S.s_depth;
+			Lt.prim_ng = S.prim_ng;
+			Lt.mats = S.mats;
+			if(traverse<true, WIDE, SPILL, true>(C, so, dir, tmin, st, t_hit, p_hit, visits, tests, &Lt)) return true;
+			if(Lt.n > 0) scol = tsFilterColor(S, ts_buf, Lt.n, so, dir);
+			return false;
+		}
+		return traverse<true, WIDE, SPILL>(C, so, dir, 0.f, st, t_hit, p_hit, visits, tests);
+	};
 	if(L.type == LIGHT_POINT)
 	{
 		C3 c = c3(0.f);
@@ -3566,12 +3594,11 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 			const C3 lcol = C3{L.color[0], L.color[1], L.color[2]} * idist_sqr;
 			const float angle = m.flat ? 1.f : fabsf(dot(sp.n, ldir));
 			const C3 surf_col = matEval<EXT>(m, sp, wo, ldir, B_ALL);
-			const C3 contrib = surf_col * lcol * angle * c3(1.f);
 			V3 so;
 			float st;
 			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
-			const bool occ = cast_shadows && traverse<true, WIDE, SPILL>(C, so, ldir, 0.f, st, t_hit, p_hit, visits, tests);
-			if(!occ) c = c + contrib;
+			C3 scol;
+			if(!shadowed(so, ldir, sh_tmin, st, scol)) c = c + surf_col * (TSH && cast_shadows ? lcol * scol : lcol) * angle * c3(1.f);
 		}
 		return c3(0.f) + c;
 	}
@@ -3620,12 +3647,12 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 						const float m_2 = m_pdf * m_pdf;
 						w = l_2 / (l_2 + m_2);
 					}
-					const C3 contrib = surf_col * lcolor * angle * w / pdf;
 					V3 so;
 					float st;
 					shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
-					const bool occ = cast_shadows && traverse<true, WIDE, SPILL>(C, so, ldir, 0.f, st, t_hit, p_hit, visits, tests);
-					if(!occ) acc_l = acc_l + contrib;
+					C3 scol;
+					if(!shadowed(so, ldir, sh_tmin, st, scol))
+						acc_l = acc_l + surf_col * (TSH && cast_shadows ? lcolor * scol : lcolor) * angle * w / pdf;
 				}
 			}
 		}
@@ -3661,12 +3688,12 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 					const float l_2 = l_pdf * l_pdf;
 					const float m_2 = s.pdf * s.pdf;
 					const float w = m_2 / (l_2 + m_2);
-					const C3 contrib = surf_col * lcolor * w * W;
 					V3 so;
 					float st;
 					shadowRayOf(sp.p, dir, b_tmin, t, so, st);
-					const bool occ = cast_shadows && traverse<true, WIDE, SPILL>(C, so, dir, 0.f, st, t_hit, p_hit, visits, tests);
-					if(!occ) acc_m = acc_m + contrib;
+					C3 scol;
+					if(!shadowed(so, dir, b_tmin, st, scol))
+						acc_m = acc_m + surf_col * (TSH && cast_shadows ? lcolor * scol : lcolor) * w * W;
 				}
 			}
 		}
@@ -3707,6 +3734,7 @@ struct FgArgs
 	DevCounters cnt_next;
 	int stack_depth;
 	int *spill;
+	float2 *ts_scratch;   // transparent shadows: s_depth (t, prim) entries per lane of the grid
 };
 
 // k_fg: the gather-path megakernel wants ~230 VGPRs unconstrained (2 waves / SIMD); capped for 4
@@ -3715,7 +3743,7 @@ struct FgArgs
 #define YAF_FG_WAVES 4
 #endif
 #define YAF_FG_ATTR __attribute__((amdgpu_waves_per_eu(YAF_FG_WAVES)))
-template<bool LDS_SCENE, bool WIDE, bool EXT, bool SPILL = true>
+template<bool LDS_SCENE, bool WIDE, bool EXT, bool SPILL = true, bool TSH = false>
 __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 {
 	const DevScene &S = A.S;
@@ -3746,6 +3774,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 	const uint32_t a0 = L.s * S.cap_a;
 	uint32_t visits = 0, tests = 0;
 	const int n_sampl = max(1, S.fg_samples);
+	float2 *ts_buf = TSH ? A.ts_scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * (size_t)S.s_depth : nullptr;
 	for(uint32_t jj = L.r * blockDim.x + threadIdx.x; jj < n_req; jj += L.nb * blockDim.x)
 	{
 		const uint32_t j = a0 + jj;
@@ -3804,7 +3833,8 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 							lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
 						}
 						lcol = (S.n_lights > 0)
-						           ? lightEstimateInline<EXT, WIDE, SPILL>(S, C, S.lights[lnum], mh, hit, pwo, lnum, sample_idx, offset, visits, tests) *
+						           ? lightEstimateInline<EXT, WIDE, SPILL, TSH>(S, C, S.lights[lnum], mh, hit, pwo, lnum, sample_idx, offset, visits, tests,
+						                                                        ts_buf) *
 						                 (float)S.n_lights
 						           : c3(0.f);
 					}
@@ -4191,7 +4221,7 @@ hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b,
 
 // k_fg over the gather queue of one iteration (before k_gather), on the trace grid
 hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid,
-                            hipStream_t st)
+                            float2 *ts_scratch, hipStream_t st)
 {
 	FgArgs A;
 	A.S = *S;
@@ -4199,8 +4229,27 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 	A.cnt_next = *cnt_next;
 	A.stack_depth = stack_depth;
 	A.spill = spill;
+	A.ts_scratch = ts_scratch;
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	const bool wide = S->node_f4 == 8;
+	if(S->tr_shad)
+	{
+		// transparent shadows (the spilling variants: without a spill column they never spill)
+		if(!ts_scratch) return hipErrorInvalidValue;
+		const size_t bytes = S->scene_in_lds ? stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) : stack_bytes;
+#define YAF_FG_LAUNCH_TS(L, W, E) hipLaunchKernelGGL((k_fg<L, W, E, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A)
+		if(S->scene_in_lds)
+		{
+			if(S->ext) { if(wide) YAF_FG_LAUNCH_TS(true, true, true); else YAF_FG_LAUNCH_TS(true, false, true); }
+			else if(wide) YAF_FG_LAUNCH_TS(true, true, false);
+			else YAF_FG_LAUNCH_TS(true, false, false);
+		}
+		else if(S->ext) { if(wide) YAF_FG_LAUNCH_TS(false, true, true); else YAF_FG_LAUNCH_TS(false, false, true); }
+		else if(wide) YAF_FG_LAUNCH_TS(false, true, false);
+		else YAF_FG_LAUNCH_TS(false, false, false);
+#undef YAF_FG_LAUNCH_TS
+		return hipGetLastError();
+	}
 #define YAF_FG_LAUNCH(L, W, E, B) hipLaunchKernelGGL((k_fg<L, W, E>), dim3(grid), dim3(kTraceBlock), B, st, A)
 #define YAF_FG_LAUNCH_NS(W, E, B) hipLaunchKernelGGL((k_fg<true, W, E, false>), dim3(grid), dim3(kTraceBlock), B, st, A)
 	if(S->scene_in_lds)

@@ -57,7 +57,7 @@ hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b,
 hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out, uint32_t *n_kept,
                                   int *rounds_out, hipStream_t st, void **scratch);
 void yafamd_thin_scratch_free(void *scratch);
-hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid,
+hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid, float2 *ts_scratch,
                             hipStream_t st);
 size_t yafamd_gather_lanes(const DevScene *S);
 hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
@@ -258,6 +258,7 @@ struct GpuRenderer::Impl
 	Buf rad_a, rad_b, rad_c, rad_flag, radc_a, radc_b, radc_c, rad_kept, rph_pos, rph_dir, rph_colb, rpk_nodes;
 	// a group member's own segment of a photon map / of the radiance points before the concatenation
 	Buf seg_pos, seg_dir, seg_colb, seg_ra, seg_rb, seg_rc;
+	Buf fg_ts;   // k_fg's transparent-shadow hit lists (s_depth per lane of the trace grid)
 	int n_rphotons = 0;
 	uint32_t n_rad_points = 0;
 	int d_depth = 0, r_depth = 0;           // kd-tree depths of the diffuse / radiance maps
@@ -1263,6 +1264,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		// (integrator_montecarlo.cc:565-625): the photon maps are rebuilt for every render, as the
 		// reference's "generate" mode does
 		if(!buildPhotonMap(rp)) return false;
+		if(S.fg_on && S.tr_shad &&
+		   !ensure(log_, d.fg_ts, (size_t)d.trace_grid * yafamd_trace_block() * (size_t)std::max(1, S.s_depth) * sizeof(float2)))
+			return false;
 		if(yafamd_gather_lds_bytes(&S) > 64 * 1024)
 		{
 			log_.error("Integrator: photon search " + std::to_string(std::max(S.pm_search, S.c_search)) + " needs more LDS than the gather kernel has");
@@ -1538,7 +1542,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			if(S.gather_on && (!dl_pipeline || it == 1 || (S.show_map && it == 0)))
 			{
 				// final gathering adds its estimate to the requests' colour before k_gather ends them
-				if(S.fg_on) PROF(KK_FG, yafamd_launch_fg(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+				if(S.fg_on)
+					PROF(KK_FG, yafamd_launch_fg(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, (float2 *)d.fg_ts.p, d.stream));
 				PROF(KK_GATHER, yafamd_launch_gather(&S, &d.G, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 			}
 			// NEE requests (none in iteration 1 of photon mapping, whose entries all finish there)

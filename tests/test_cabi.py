@@ -85,8 +85,8 @@ def test_unsupported_plugins_rejected_reference_style(product):
     assert yi.createIntegrator("pm2") == 0          # duplicate name (scene.cc:419-422)
     yi.paramsClearAll()
     yi.paramsSetString("type", "photonmapping")
-    yi.paramsSetBool("transpShad", True)            # final gathering traces opaque shadows only
-    assert yi.createIntegrator("pm3") == 0
+    yi.paramsSetBool("transpShad", True)            # final gathering with transparent shadows (k_fg<TSH>)
+    assert yi.createIntegrator("pm3") == 1
     yi.paramsClearAll()
     yi.paramsSetString("type", "shinydiffusemat")
     assert yi.createMaterial("d") == 1

@@ -109,3 +109,32 @@ def test_shadow_depth_above_the_gpu_limit_is_refused(product):
         product.render_spec(spec.with_render(shadow_depth=65))
     rgba, w, _ = product.render_spec(spec.with_render(shadow_depth=64))
     assert (w > 0).all()
+
+
+def _pm_fg_spec(**kw):
+    """PhotonIntegrator with final gathering over the transparent-shadow Cornell box: close gather
+    paths (fg_min_pathlen 0.8) run estimateOneDirectLight (integrator_photon_mapping.cc:703), whose
+    shadow rays take the transparent-shadow test (integrator_montecarlo.cc:112, 206, 330)."""
+    spec = scenes.cornell_transparent_shadows(48, 36, spp=1, integrator="photonmapping", **kw)
+    return spec.with_render(pm_photons=20000, pm_search=50, pm_diffuse_radius=0.1, pm_bounces=5, pm_caustics=False,
+                            pm_final_gather=True, fg_samples=4, fg_bounces=3, fg_min_pathlen=0.8)
+
+
+def test_oracle_final_gather_transparent_shadows_add_light(oracle_built):
+    a, w, _ = oracle_built.OracleScene(_pm_fg_spec(), threads=4).render()
+    b, _, _ = oracle_built.OracleScene(_pm_fg_spec().with_render(transp_shad=False), threads=4).render()
+    assert np.isfinite(a).all() and (w > 0).all()
+    assert a[..., :3].mean() > b[..., :3].mean()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(), dict(point_light=True), dict(shadow_depth=1, panes=3)], ids=["area", "point", "depth1"])
+def test_final_gather_transparent_shadows_match_oracle(product, oracle_built, kw):
+    """k_fg<TSH>: the gather paths' inline shadow rays collect the transparent surfaces in a per-lane
+    list and multiply their filter colour into the light colour (tsFilterColor, as k_tshadow)."""
+    spec = _pm_fg_spec(**kw)
+    rgba, w, _ = product.render_spec(spec)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
+    assert np.array_equal(w, ow)
+    u = ulp_diff(rgba, orgba)
+    assert u.max() <= ULP_TOL, f"{(u > ULP_TOL).sum()} values > {ULP_TOL} ULP, max {u.max()}"
