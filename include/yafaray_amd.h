@@ -58,6 +58,8 @@ typedef struct
 	int32_t photon_maps_mode;   /* photon_maps_processing the last render used after its fallbacks: 0 generate,
 	                               1 generate-save, 2 load, 3 reuse-previous (1.2) */
 	int32_t reserved0;
+	uint64_t gather_accepts;    /* two-pass gather: photons the k_gather_walk logged (1.2) */
+	uint64_t gather_overflows;  /* two-pass gather: requests whose log overflowed and were walked again (1.2) */
 } yafaray_amd_stats_t;
 
 /* Bytes of the LIBYAFARAY_AMD_1.0 struct (its fields end at photon_tree_seconds): yafaray_amd_getStats

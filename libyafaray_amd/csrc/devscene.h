@@ -418,6 +418,17 @@ struct DevStats
 	unsigned long long gather_queries;   // photon density estimates k_gather computed
 	unsigned long long gather_visits;    // point kd-tree nodes k_gather fetched
 	unsigned long long gather_photons;   // photons the density estimates read (heap entries summed)
+	unsigned long long gather_accepts;   // two-pass gather: photons the walk accepted (log entries)
+	unsigned long long gather_overflows; // two-pass gather: requests whose log overflowed (walked again)
+};
+
+// the two-pass diffuse gather's accepted-photon log for one batch of the gather queue (kernels.hip
+// GatherLog): cap entries of 8 bytes per request, seg_cap queue positions per segment from j0
+struct GatherLogDesc
+{
+	void *e;
+	uint32_t *n;
+	uint32_t cap, seg_cap, j0;
 };
 
 } // namespace yafamd

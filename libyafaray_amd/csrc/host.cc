@@ -229,6 +229,8 @@ bool Scene::renderDeviceGroup(RenderParams &rp)
 		st.gather_visits += o.gather_visits;
 		st.gather_queries += o.gather_queries;
 		st.gather_photons += o.gather_photons;
+		st.gather_accepts += o.gather_accepts;
+		st.gather_overflows += o.gather_overflows;
 		st.trace_kernel_ms += o.trace_kernel_ms;
 		st.shade_kernel_ms += o.shade_kernel_ms;
 		st.nee_kernel_ms += o.nee_kernel_ms;

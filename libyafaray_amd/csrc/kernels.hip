@@ -3157,6 +3157,19 @@ constexpr int kGatherPerSeg = YAF_GATHER_PER_SEG;   // workgroups per queue segm
 //     image (56 -> 53 ms);
 //   * tried and dropped: one node per loop trip (if-if, 67 ms), lanes refilling independently with
 //     the estimate in a second kernel (lanes drift apart and stop sharing cache lines, 59-70 ms).
+// The accepted-photon log of the two-pass diffuse gather (k_gather_walk -> k_gather<REPLAY>), for
+// the queue positions [j0, j0 + seg_cap) of every segment (one batch): batch query q = seg * seg_cap
+// + (position - j0); its entries at e[q * cap ..) (written in 16-byte pairs, so a request fills its
+// own cache lines); n[q] = entries (> cap: overflowed, not replayable).
+struct GatherLog
+{
+	uint2 *e;          // (photon index, squared distance bits)
+	uint32_t *n;
+	uint32_t cap;      // entries per query
+	uint32_t seg_cap;  // queue positions per segment in this batch (a multiple of 64)
+	uint32_t j0;       // first queue position of the batch
+};
+
 struct GatherArgs
 {
 	DevScene S;
@@ -3166,6 +3179,7 @@ struct GatherArgs
 	const DevJob *jobs;
 	int n_jobs;
 	uint64_t chunk_base;
+	GatherLog log;           // REPLAY: the walk's log of this batch
 };
 
 __host__ __device__ inline size_t gatherTableBytes(const DevScene &S, bool small)
@@ -3280,9 +3294,156 @@ __device__ __forceinline__ int pkLookup(const uint4 *nodes, V3 p, int k, float &
 	return found;
 }
 
+// ---- two-pass diffuse gather ----
+// The walk of pkLookup depends on the heap only through max_d2, the largest of the k smallest
+// distances accepted so far — a function of the accepted multiset, not of the heap's layout.
+// Pass 1 (k_gather_walk) keeps those k distances in registers (unrolled over kWalkK; no LDS, so
+// several times the resident waves of k_gather for the latency-bound walk) and logs every accepted
+// photon (index, distance) in visit order.  Pass 2 (k_gather<REPLAY>) feeds the log through
+// PhotonGather's heap in LDS — the reference's element moves exactly — and computes the estimate.
+constexpr int kWalkK = 64;
+#ifndef YAF_WALK_PER_SEG
+#define YAF_WALK_PER_SEG 16
+#endif
+constexpr int kWalkPerSeg = YAF_WALK_PER_SEG;   // walk workgroups per queue segment
+
+// pkLookup's walk with the k smallest distances in registers, sorted descending (unused slots -1,
+// so kd[0] is the heap's top once k were found): an insertion is one v_med3 per slot.  The stack is an LDS column of
+// far-child indices (4 B; stk[level * kGatherBlock]): a popped interior node carries its parent's
+// plane (pkd.hip), from which the plane distance the reference stacked is recomputed; a popped leaf
+// is tested directly (its photon lies beyond that plane, so the reference's pop-time rejection and
+// the distance test agree).  The accepted photons go to this request's log lg[0 ..) in pairs
+// (16-byte stores; the first `cap`); returns how many were accepted.
+__device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, float max_d2, uint2 *lg, uint32_t cap, uint32_t *stk,
+                                           uint32_t &visits)
+{
+	float kd[kWalkK];
+#pragma unroll
+	for(int i = 0; i < kWalkK; ++i) kd[i] = -1.f;
+	int found = 0;
+	uint32_t n_acc = 0;
+	uint2 pend = make_uint2(0u, 0u);
+	uint32_t curr = 0;
+	int sp_top = 0;
+	uint4 nd = nodes[0];
+	++visits;
+	for(;;)
+	{
+		while((nd.w & 3u) != 3u)
+		{
+			const int axis = (int)(nd.w & 3u);
+			const float split_val = __uint_as_float(nd.x);
+			const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+			uint32_t far_child;
+			if(pa <= split_val) { far_child = nd.w >> 2; curr = curr + 1; }
+			else { far_child = curr + 1; curr = nd.w >> 2; }
+			float d2 = pa - split_val;
+			d2 *= d2;
+			if(d2 <= max_d2)
+			{
+				stk[sp_top * kGatherBlock] = far_child;
+				++sp_top;
+			}
+			nd = nodes[curr];
+			++visits;
+		}
+		const uint32_t ph = nd.w >> 2;
+		const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
+		const float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
+		if(dist_2 < max_d2)
+		{
+			const uint2 e = make_uint2(ph, __float_as_uint(dist_2));
+			if(n_acc & 1u)
+			{
+				if(n_acc < cap) *reinterpret_cast<uint4 *>(lg + (n_acc - 1u)) = make_uint4(pend.x, pend.y, e.x, e.y);
+			}
+			else pend = e;
+			++n_acc;
+			if(found < k)
+			{
+				// insert: the slot where dist_2 belongs takes it, the smaller ones shift down
+#pragma unroll
+				for(int i = kWalkK - 1; i > 0; --i) kd[i] = __builtin_amdgcn_fmed3f(kd[i - 1], kd[i], dist_2);
+				kd[0] = fmaxf(kd[0], dist_2);
+				++found;
+				if(found == k) max_d2 = kd[0];
+			}
+			else
+			{
+				// pop_heap removes the top (kd[0] = max_d2), push_heap adds dist_2: the larger ones
+				// shift up
+#pragma unroll
+				for(int i = 0; i < kWalkK - 1; ++i) kd[i] = __builtin_amdgcn_fmed3f(kd[i], kd[i + 1], dist_2);
+				kd[kWalkK - 1] = fminf(kd[kWalkK - 1], dist_2);
+				max_d2 = kd[0];
+			}
+		}
+		// pop the next far child the current radius still reaches
+		bool more = false;
+		while(sp_top > 0)
+		{
+			--sp_top;
+			curr = stk[sp_top * kGatherBlock];
+			nd = nodes[curr];
+			++visits;
+			if((nd.w & 3u) != 3u)
+			{
+				const uint32_t pax = nd.z;
+				const float pa = pax == 0u ? p.x : (pax == 1u ? p.y : p.z);
+				float d2 = pa - __uint_as_float(nd.y);
+				d2 *= d2;
+				if(d2 > max_d2) continue;
+			}
+			more = true;
+			break;
+		}
+		if(!more) break;
+	}
+	if((n_acc & 1u) && n_acc <= cap) lg[n_acc - 1u] = pend;
+	return n_acc;
+}
+
+__device__ __forceinline__ uint2 *gatherLogAt(const GatherLog &L, uint32_t q)
+{
+	return L.e + (size_t)q * L.cap;
+}
+
+// pass 1 over one batch of the gather queue (diffuse-map requests; the others log nothing)
+__global__ void __launch_bounds__(kGatherBlock) k_gather_walk(GatherArgs A)
+{
+	extern __shared__ uint32_t walk_stack[];
+	const DevScene &S = A.S;
+	uint32_t *stk = walk_stack + threadIdx.x;
+	uint32_t seg, part, parts;
+	gatherSegPart(S.n_seg, seg, part, parts);
+	const uint32_t j1 = min(A.cnt_next.n_gather[seg], A.log.j0 + A.log.seg_cap);
+	const uint32_t a0 = seg * S.cap_a;
+	uint32_t visits = 0, accepts = 0;
+	for(uint32_t jj = A.log.j0 + part * kGatherBlock + threadIdx.x; jj < j1; jj += parts * kGatherBlock)
+	{
+		const uint32_t j = a0 + jj;
+		const uint32_t q = seg * A.log.seg_cap + (jj - A.log.j0);
+		uint32_t n_acc = 0;
+		if(__float_as_uint(A.G.extra[j].w) & G_DIFFUSE)
+			n_acc = pkWalk(S.pk_nodes, xyz(A.G.p_prim[j]), S.pm_search, S.pm_radius2, gatherLogAt(A.log, q), A.log.cap, stk, visits);
+		A.log.n[q] = n_acc;
+		accepts += n_acc;
+	}
+	for(int off = 32; off > 0; off >>= 1)
+	{
+		visits += __shfl_down(visits, off);
+		accepts += __shfl_down(accepts, off);
+	}
+	if(threadIdx.x == 0 && S.stats)
+	{
+		atomicAdd(&S.stats[seg].gather_visits, (unsigned long long)visits);
+		atomicAdd(&S.stats[seg].gather_accepts, (unsigned long long)accepts);
+	}
+}
+
 __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2);
 
-template<bool SMALL, bool EXT>
+template<bool SMALL, bool EXT, bool REPLAY = false>
 __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 {
 	extern __shared__ uint4 gather_smem[];
@@ -3315,10 +3476,13 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 #endif
 	uint32_t seg, part, parts;
 	gatherSegPart(S.n_seg, seg, part, parts);
-	const uint32_t n_req = A.cnt_next.n_gather[seg];
+	const uint32_t n_all = A.cnt_next.n_gather[seg];
+	// REPLAY: this batch's queue positions [j0, j0 + seg_cap) only
+	const uint32_t jb = REPLAY ? A.log.j0 : 0u;
+	const uint32_t n_req = REPLAY ? min(n_all, A.log.j0 + A.log.seg_cap) : n_all;
 	const uint32_t a0 = seg * S.cap_a;
-	uint32_t visits = 0, photons = 0;
-	for(uint32_t base_j = part * kGatherBlock; base_j < n_req; base_j += parts * kGatherBlock)
+	uint32_t visits = 0, photons = 0, overflows = 0;
+	for(uint32_t base_j = jb + part * kGatherBlock; base_j < n_req; base_j += parts * kGatherBlock)
 	{
 		if(base_j + threadIdx.x >= n_req) continue;
 		const uint32_t j = a0 + base_j + threadIdx.x;
@@ -3328,7 +3492,45 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		const V3 p = xyz(pp);
 		float max_d2 = S.pm_radius2;
 		int found = 0;
-		if(mode & G_DIFFUSE) found = pkLookup(S.pk_nodes, p, S.pm_search, max_d2, heap, stk, gstride, visits);
+		if(mode & G_DIFFUSE)
+		{
+			const uint32_t q = seg * A.log.seg_cap + (base_j + threadIdx.x - jb);
+			const uint32_t n_acc = REPLAY ? A.log.n[q] : 0u;
+			if(REPLAY && n_acc <= A.log.cap)
+			{
+				// PhotonGather (photon.cc:31-52) over the walk's accepted photons, in visit order
+				const int k = S.pm_search;
+				const uint2 *lg = gatherLogAt(A.log, q);
+				uint4 pair = make_uint4(0u, 0u, 0u, 0u);
+				for(uint32_t a = 0; a < n_acc; ++a)
+				{
+					if(!(a & 1u)) pair = (a + 1u < n_acc) ? *reinterpret_cast<const uint4 *>(lg + a) : make_uint4(lg[a].x, lg[a].y, 0u, 0u);
+					const uint2 e = (a & 1u) ? make_uint2(pair.z, pair.w) : make_uint2(pair.x, pair.y);
+					const float d = __uint_as_float(e.y);
+					if(found < k)
+					{
+						heap.i(found) = e.x;
+						heap.d(found) = d;
+						++found;
+						if(found == k)
+						{
+							heapMake(heap, k);
+							max_d2 = heap.d(0);
+						}
+					}
+					else
+					{
+						heapReplaceTop(heap, k, e.x, d);
+						max_d2 = heap.d(0);
+					}
+				}
+			}
+			else
+			{
+				if(REPLAY) ++overflows;   // the log overflowed: walk again with the heap
+				found = pkLookup(S.pk_nodes, p, S.pm_search, max_d2, heap, stk, gstride, visits);
+			}
+		}
 		photons += (uint32_t)found;
 		const float4 wk = A.G.wo_k[j];
 		const uint4 cb = A.G.pix_mode[j];
@@ -3408,12 +3610,14 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 	{
 		visits += __shfl_down(visits, off);
 		photons += __shfl_down(photons, off);
+		overflows += __shfl_down(overflows, off);
 	}
 	if(threadIdx.x == 0 && S.stats)
 	{
 		atomicAdd(&S.stats[seg].gather_visits, (unsigned long long)visits);
 		atomicAdd(&S.stats[seg].gather_photons, (unsigned long long)photons);
-		if(part == 0) atomicAdd(&S.stats[seg].gather_queries, (unsigned long long)n_req);
+		if(REPLAY && overflows) atomicAdd(&S.stats[seg].gather_overflows, (unsigned long long)overflows);
+		if(part == 0) atomicAdd(&S.stats[seg].gather_queries, (unsigned long long)(n_req > jb ? n_req - jb : 0u));
 	}
 }
 
@@ -4158,7 +4362,7 @@ hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_
 }
 
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, float4 *samples,
-                                const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st)
+                                const DevJob *jobs, int n_jobs, uint64_t chunk_base, const GatherLogDesc *log, hipStream_t st)
 {
 	GatherArgs A;
 	A.S = *S;
@@ -4168,6 +4372,9 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const D
 	A.jobs = jobs;
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
+	A.log = GatherLog{nullptr, nullptr, 0u, 0u, 0u};
+	const bool replay = log != nullptr;
+	if(replay) A.log = GatherLog{(uint2 *)log->e, log->n, log->cap, log->seg_cap, log->j0};
 	const dim3 grid(S->n_seg * kGatherPerSeg);
 #ifdef YAF_GATHER_NO_SMALL
 	const bool small = false;
@@ -4175,15 +4382,41 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const D
 	const bool small = S->small_tables != 0;
 #endif
 	const size_t lds = gatherTableBytes(*S, small) + gatherLdsBytes(*S);
+#define YAF_GATHER_LAUNCH(SM, E) \
+	do { if(replay) hipLaunchKernelGGL((k_gather<SM, E, true>), grid, dim3(kGatherBlock), lds, st, A); \
+	     else hipLaunchKernelGGL((k_gather<SM, E, false>), grid, dim3(kGatherBlock), lds, st, A); } while(0)
 	if(S->ext)
 	{
-		if(small) hipLaunchKernelGGL((k_gather<true, true>), grid, dim3(kGatherBlock), lds, st, A);
-		else hipLaunchKernelGGL((k_gather<false, true>), grid, dim3(kGatherBlock), lds, st, A);
+		if(small) YAF_GATHER_LAUNCH(true, true);
+		else YAF_GATHER_LAUNCH(false, true);
 	}
-	else if(small) hipLaunchKernelGGL((k_gather<true, false>), grid, dim3(kGatherBlock), lds, st, A);
-	else hipLaunchKernelGGL((k_gather<false, false>), grid, dim3(kGatherBlock), lds, st, A);
+	else if(small) YAF_GATHER_LAUNCH(true, false);
+	else YAF_GATHER_LAUNCH(false, false);
+#undef YAF_GATHER_LAUNCH
 	return hipGetLastError();
 }
+
+// pass 1 of the two-pass diffuse gather over one batch (see k_gather_walk)
+hipError_t yafamd_launch_gather_walk(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, const GatherLogDesc *log,
+                                     hipStream_t st)
+{
+	if(S->pm_search > kWalkK || (log->seg_cap & 63u) || (log->cap & 1u)) return hipErrorInvalidValue;
+	GatherArgs A;
+	A.S = *S;
+	A.G = *G;
+	A.cnt_next = *cnt_next;
+	A.samples = nullptr;
+	A.jobs = nullptr;
+	A.n_jobs = 0;
+	A.chunk_base = 0;
+	A.log = GatherLog{(uint2 *)log->e, log->n, log->cap, log->seg_cap, log->j0};
+	const size_t lds = (size_t)max(1, S->pm_stack) * kGatherBlock * sizeof(uint32_t);
+	hipLaunchKernelGGL(k_gather_walk, dim3(S->n_seg * kWalkPerSeg), dim3(kGatherBlock), lds, st, A);
+	return hipGetLastError();
+}
+
+// the two-pass gather serves diffuse maps whose k fits the walk's registers
+int yafamd_gather_walk_k() { return kWalkK; }
 
 // Final gathering: compaction of the radiance points (reuses the photon count / scan kernels on
 // rad_flag); *total_dev receives the count
@@ -4274,7 +4507,7 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 }
 
 // lanes of one gather launch (the HBM lookup stack holds pm_stack levels per lane)
-size_t yafamd_gather_lanes(const DevScene *S) { return (size_t)S->n_seg * kGatherPerSeg * kGatherBlock; }
+size_t yafamd_gather_lanes(const DevScene *S) { return (size_t)S->n_seg * (kWalkPerSeg > kGatherPerSeg ? kWalkPerSeg : kGatherPerSeg) * kGatherBlock; }
 
 size_t yafamd_gather_lds_bytes(const DevScene *S) { return gatherTableBytes(*S, S->small_tables != 0) + gatherLdsBytes(*S); }
 

@@ -22,7 +22,10 @@
 // Node layout is the reference's depth-first one: a subtree of m photons has 2m - 1 nodes, node i's
 // left child is i + 1 and its right child i + 2 nl.  Node record (uint4): .w = flags (bits 0-1 axis,
 // 3 = leaf; interior: right child << 2, leaf: photon index << 2), interior .x = split position bits,
-// leaf .xyz = the photon's position bits (k_gather reads them without a second load).
+// leaf .xyz = the photon's position bits (k_gather reads them without a second load).  Interior
+// nodes also carry their parent's splitting plane (.y = split bits, .z = axis; the root: 0, 3), so a
+// walk that stacks only far-child indices can re-derive the plane distance when it pops one
+// (k_gather_walk); the reference's tree is unaffected.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <cstdint>
@@ -79,6 +82,23 @@ extern "C" void yafamd_pkd_scratch_free(void *scratch) { delete static_cast<PkdS
 
 // pos_dev: n photons (position in .xyz); nodes_dev: 2n - 1 nodes (uint4, see the header comment).
 // *depth_out: deepest level (root = 0) — the lookup stack needs depth + 1 entries.
+// every interior node's children: the interior ones get its splitting plane (.y split, .z axis)
+__global__ void __launch_bounds__(256) k_parent_planes(uint4 *nodes, uint32_t n_nodes)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if(i >= n_nodes) return;
+	const uint4 nd = nodes[i];
+	if((nd.w & 3u) == 3u) return;
+	const uint32_t kids[2] = {i + 1u, nd.w >> 2};
+	for(uint32_t c : kids)
+		if(c < n_nodes && (nodes[c].w & 3u) != 3u)
+		{
+			nodes[c].y = nd.x;
+			nodes[c].z = nd.w & 3u;
+		}
+	if(i == 0u) { nodes[0].y = 0u; nodes[0].z = 3u; }
+}
+
 extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch)
 {
 	if(n == 0) return hipSuccess;
@@ -150,6 +170,7 @@ extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 
 	// bottom phase: one workgroup per subtree
 	hipLaunchKernelGGL(k_subtrees, dim3(n_seg), dim3(kSubThreads), 0, st, S.segs[cur].as<Seg>(), S.rec[0].as<uint4>(), S.rec[1].as<uint4>(),
 	                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, n, level, S.max_level.as<int>());
+	hipLaunchKernelGGL(k_parent_planes, dim3((2 * n - 1 + 255) / 256), dim3(256), 0, st, nodes_dev, 2 * n - 1);
 	int depth = 0;
 	PKCHECK(hipMemcpyAsync(&depth, S.max_level.p, 4, hipMemcpyDeviceToHost, st));
 	PKCHECK(hipStreamSynchronize(st));

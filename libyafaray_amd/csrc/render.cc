@@ -48,7 +48,10 @@ hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const P
 hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev,
                                  float4 *pos, float4 *dir, float *colb, hipStream_t st);
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, float4 *samples,
-                                const DevJob *jobs, int n_jobs, uint64_t chunk_base, hipStream_t st);
+                                const DevJob *jobs, int n_jobs, uint64_t chunk_base, const GatherLogDesc *log, hipStream_t st);
+hipError_t yafamd_launch_gather_walk(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, const GatherLogDesc *log,
+                                     hipStream_t st);
+int yafamd_gather_walk_k();
 size_t yafamd_gather_lds_bytes(const DevScene *S);
 hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b,
                               float4 *c, hipStream_t st);
@@ -259,6 +262,7 @@ struct GpuRenderer::Impl
 	// a group member's own segment of a photon map / of the radiance points before the concatenation
 	Buf seg_pos, seg_dir, seg_colb, seg_ra, seg_rb, seg_rc;
 	Buf fg_ts;   // k_fg's transparent-shadow hit lists (s_depth per lane of the trace grid)
+	Buf g_log, g_log_n;   // the two-pass diffuse gather's accepted-photon log (one batch of the gather queue)
 	int n_rphotons = 0;
 	uint32_t n_rad_points = 0;
 	int d_depth = 0, r_depth = 0;           // kd-tree depths of the diffuse / radiance maps
@@ -1489,6 +1493,25 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	S.n_seg = (uint32_t)R;
 	S.cap_a = (uint32_t)shardCap(d.slots_cap);
 	S.cap_s = S.cap_a * (uint32_t)K;
+	// The two-pass diffuse gather (k_gather_walk + k_gather<REPLAY>, kernels.hip) for diffuse maps whose
+	// k fits the walk's registers: its log holds `cap` accepted photons per request for a batch of
+	// seg_cap queue positions per segment (within 16 GB); YAFARAY_AMD_GATHER=single keeps one pass.
+	GatherLogDesc glog{nullptr, nullptr, 0u, 0u, 0u};
+	bool walk_gather = false;
+	{
+		const char *ge = std::getenv("YAFARAY_AMD_GATHER");
+		const bool single = ge && std::string(ge) == "single";
+		if(S.gather_on && S.n_photons > 0 && S.pm_search <= yafamd_gather_walk_k() && !single)
+		{
+			const char *ce = std::getenv("YAFARAY_AMD_GATHER_LOG");
+			const uint32_t cap = ((uint32_t)std::max(S.pm_search, ce ? atoi(ce) : 512) + 1u) & ~1u;   // even: pairs
+			size_t seg_cap = S.cap_a;
+			while((size_t)R * seg_cap * cap * 8 > (16ull << 30) && seg_cap > 64) seg_cap = ((seg_cap / 2 + 63) / 64) * 64;
+			if(!ensure(log_, d.g_log, (size_t)R * seg_cap * cap * 8) || !ensure(log_, d.g_log_n, (size_t)R * seg_cap * 4)) return false;
+			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u};
+			walk_gather = true;
+		}
+	}
 	if(!ensure(log_, d.counters, 2 * 4 * R * sizeof(uint32_t))) return false;
 	if(!ensure(log_, d.stats, sizeof(DevStats) * (size_t)d.trace_grid)) return false;
 	HIPCHECK(hipMemsetAsync(d.counters.p, 0, 2 * 4 * R * sizeof(uint32_t), d.stream));
@@ -1544,7 +1567,18 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				// final gathering adds its estimate to the requests' colour before k_gather ends them
 				if(S.fg_on)
 					PROF(KK_FG, yafamd_launch_fg(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, (float2 *)d.fg_ts.p, d.stream));
-				PROF(KK_GATHER, yafamd_launch_gather(&S, &d.G, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
+				if(walk_gather)
+					for(uint32_t j0 = 0; j0 < S.cap_a; j0 += glog.seg_cap)
+					{
+						GatherLogDesc L = glog;
+						L.j0 = j0;
+						PROF(KK_GATHER_WALK, yafamd_launch_gather_walk(&S, &d.G, &cnt[cur ^ 1], &L, d.stream));
+						PROF(KK_GATHER, yafamd_launch_gather(&S, &d.G, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base,
+						                                     &L, d.stream));
+					}
+				else
+					PROF(KK_GATHER, yafamd_launch_gather(&S, &d.G, &cnt[cur ^ 1], (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base,
+					                                     nullptr, d.stream));
 			}
 			// NEE requests (none in iteration 1 of photon mapping, whose entries all finish there)
 			if((S.ext || !yafamd_shade_fused()) && !(S.integrator == INT_PHOTON && it == 1))
@@ -1823,6 +1857,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			hs.gather_queries += b.gather_queries;
 			hs.gather_visits += b.gather_visits;
 			hs.gather_photons += b.gather_photons;
+			hs.gather_accepts += b.gather_accepts;
+			hs.gather_overflows += b.gather_overflows;
 		}
 	}
 	stats_.closest_rays = hs.closest_rays;
@@ -1850,18 +1886,21 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		ktimes_.items[KK_SHADE] = hs.shade_entries;
 		ktimes_.items[KK_NEE] = hs.nee_requests;
 		ktimes_.items[KK_GATHER] = hs.gather_queries;
+		ktimes_.items[KK_GATHER_WALK] = ktimes_.launches[KK_GATHER_WALK] ? hs.gather_queries : 0;
 		ktimes_.items[KK_FG] = S.fg_on ? hs.gather_queries : 0;   // every diffuse-map request runs its final gathering first
 		ktimes_.items[KK_PREGATHER] = (uint64_t)d.n_rphotons;
 		ktimes_.items[KK_PHOTON_EMIT] = ktimes_.items[KK_PHOTON_BOUNCE] = (uint64_t)d.pm_local;
 		ktimes_.items[KK_PHOTON_COMPACT] = ktimes_.items[KK_PHOTON_TREE] = stats_.photons;
 		stats_.trace_kernel_ms = ktimes_.ms[KK_TRACE];
 		stats_.shade_kernel_ms = ktimes_.ms[KK_SHADE];
-		stats_.nee_kernel_ms = ktimes_.ms[KK_NEE] + ktimes_.ms[KK_GATHER];
+		stats_.nee_kernel_ms = ktimes_.ms[KK_NEE] + ktimes_.ms[KK_GATHER] + ktimes_.ms[KK_GATHER_WALK];
 		stats_.trace_launches = ktimes_.launches[KK_TRACE];
 	}
 	stats_.gather_visits = hs.gather_visits;
 	stats_.gather_photons = hs.gather_photons;
 	stats_.gather_queries = hs.gather_queries;
+	stats_.gather_accepts = hs.gather_accepts;
+	stats_.gather_overflows = hs.gather_overflows;
 	d.prof_on = false;
 	return true;
 }
