@@ -9,5 +9,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
 	python3 $R/bench.py --no-cpu-baseline --no-parity "$@" > $R/gpurun_out/prof_$TAG.log 2>&1
 rc=$?
 tail -2 $R/gpurun_out/prof_$TAG.log
-[ -f $R/gpurun_out/prof_$TAG/run_kernel_stats.csv ] && python3 $R/tools/prof_summary.py $R/gpurun_out/prof_$TAG/run_kernel_stats.csv | head -25
+[ -f $R/gpurun_out/prof_$TAG/run_kernel_stats.csv ] && python3 $R/tools/prof_summary.py $R/gpurun_out/prof_$TAG/run_kernel_stats.csv 
 exit $rc
