@@ -170,6 +170,7 @@ struct DevScene
 	int node_f4;                   // float4 per BVH node: 4 (BVH2) or 8 (BVH4)
 	int scene_in_lds;              // nodes+tris copied to LDS by each trace workgroup
 	int brute;                     // YAFARAY_AMD_TRACE=brute: k_trace_brute tests every triangle of a tiny scene
+	int ray_sort;                  // k_trace orders each wave's window of queue entries by ray kind + direction (LDS counting sort)
 	int lds_nodes, lds_tris;
 
 	DevCamera cam;

@@ -413,7 +413,9 @@ __device__ __forceinline__ void boxPair(const float4 &n0, const float4 &n1, cons
 // primitive_triangle.cc:44-71.  Returns t or -1.  The reference's arithmetic (correctly rounded
 // 1/det, then products) evaluated branch-free: every lane computes the same instruction stream
 // and the reference's early returns become one combined predicate (NaN comparisons keep their
-// reference outcome).  `t_cut` is unused by the exact test.
+// reference outcome).  `t_cut` is unused by the exact test.  (The short-circuit form is kept on
+// purpose: the compiler turns it into det -> u -> (v, t) early outs; a bitwise predicate that
+// computes every term measured k_trace 27.6 -> 35.4 ms per C2 frame.)
 // Correctly rounded 1/x: v_rcp_f32 + one FMA Newton step, which tools/rcp_check.hip
 // verified exhaustively on gfx950 to equal the IEEE quotient for every float with
 // 2^-125 <= |x| <= 2^125 (other magnitudes, zero, inf and NaN take the IEEE division).
@@ -830,12 +832,89 @@ __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tm
 #define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LDS_SCENE ? 8 : 6)))
 #endif
 
+// ---------------------------------------------------------------------------------------------
+// Ray-stream sorting.  The queues hold rays in sample order (neighbouring pixels, 64 samples each),
+// so the rays of one window of a segment start close together but leave in every direction: lanes
+// of one wave then visit different BVH nodes in different orders (C2: 0.42 of the VALU lanes do
+// useful work).  Each wave takes a window of kSortWin consecutive queue entries, orders them by a
+// key (closest / shadow, direction octant, major axis) with a counting sort in its own LDS slice —
+// ranks from ballot-matched key groups, no LDS atomics — and traces them in that order, so a wave
+// holds one kind of ray of one octant.  Every ray's query is unchanged (its hit goes back to its
+// own queue address), so results are identical to the unsorted loop.
+// ---------------------------------------------------------------------------------------------
+#ifndef YAF_SORT_PER
+#define YAF_SORT_PER 4
+#endif
+constexpr int kSortPer = YAF_SORT_PER;        // entries per lane and window
+constexpr int kSortWin = 64 * kSortPer;
+constexpr int kSortBins = 64;                 // = wave width: one bin per lane in the scan
+
+struct WaveSort
+{
+	uint16_t perm[kSortWin];
+	uint32_t base[kSortBins];
+};
+
+// kind bit (shadow), octant (3 bits), major axis (0..2); 63 = no ray
+__device__ __forceinline__ uint32_t rayKey(const float4 &d, bool shadow)
+{
+	const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+	const uint32_t major = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
+	const uint32_t oct = (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
+	return (shadow ? 32u : 0u) | (oct << 2) | major;
+}
+
+// W.perm = the window's entry indices (0 .. kSortWin-1, entry r * 64 + lane has key[r]) in key order
+__device__ __forceinline__ void waveSortWindow(WaveSort &W, const uint32_t (&key)[kSortPer])
+{
+	const int lane = laneId();
+	const uint64_t lt = (1ull << lane) - 1ull;
+	W.base[lane] = 0;
+	__builtin_amdgcn_wave_barrier();
+	uint32_t off[kSortPer];
+#pragma unroll
+	for(int r = 0; r < kSortPer; ++r)
+	{
+		const uint32_t k = key[r];
+		uint64_t m = ~0ull;
+#pragma unroll
+		for(int b = 0; b < 6; ++b)
+		{
+			const bool bit = (k >> b) & 1u;
+			const uint64_t bal = __ballot(bit);
+			m &= bit ? bal : ~bal;
+		}
+		const uint32_t below = (uint32_t)__popcll(m & lt);
+		const uint32_t old = W.base[k];
+		off[r] = old + below;
+		__builtin_amdgcn_wave_barrier();
+		if(below == 0) W.base[k] = old + (uint32_t)__popcll(m);   // one lane per key group
+		__builtin_amdgcn_wave_barrier();
+	}
+	// exclusive scan of the 64 bin counts, one bin per lane
+	const uint32_t c = W.base[lane];
+	uint32_t inc = c;
+#pragma unroll
+	for(int o = 1; o < 64; o <<= 1)
+	{
+		const uint32_t v = __shfl_up(inc, o);
+		if(lane >= o) inc += v;
+	}
+	__builtin_amdgcn_wave_barrier();
+	W.base[lane] = inc - c;
+	__builtin_amdgcn_wave_barrier();
+#pragma unroll
+	for(int r = 0; r < kSortPer; ++r) W.perm[W.base[key[r]] + off[r]] = (uint16_t)(r * 64 + lane);
+	__builtin_amdgcn_wave_barrier();
+}
+
 // SPILL = false: the whole stack bound fits the LDS levels (no spill column): pushes and pops are
 // plain LDS accesses (with a possible spill the compiler merges both address spaces into flat
 // accesses, whose pops wait for every outstanding vector-memory operation)
 // STATS = false: no per-visit node / triangle counters (timed frames; the counts come from a frame
 // rendered with them — the frame is deterministic, so they are the same)
-template<bool LDS_SCENE, bool WIDE, bool TS, bool SPILL = true, bool STATS = true>
+// SORT: ray-stream sorting of each wave's window (above)
+template<bool LDS_SCENE, bool WIDE, bool TS, bool SPILL = true, bool STATS = true, bool SORT = false>
 __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P,
                                                       DevStats *stats, int stack_depth, int *spill)
 {
@@ -867,17 +946,8 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	const uint32_t a0 = L.s * S.cap_a, s0 = L.s * S.cap_s;
 	uint32_t visits = 0, tests = 0, n_closest = 0, n_shadow = 0;
 	const uint32_t stride = L.nb * blockDim.x;
-#ifndef YAF_TRACE_NOREFILL
-	// refill pays where traversals are long (meshes in global memory: C4 -16%); on the short
-	// LDS-resident traversals of small scenes its per-visit bookkeeping costs more (C2 +35%)
-	if(!LDS_SCENE && WIDE && !TS)
-		traceRefill4<true, STATS>(C, Q, P, n_a, total, a0, s0, L.r * blockDim.x + threadIdx.x, stride, visits, tests, n_closest, n_shadow);
-	else
-#endif
-	// one uniform trip count per workgroup so every lane reaches the same exits
-	for(uint32_t base = L.r * blockDim.x; base < total; base += stride)
-	{
-		const uint32_t j = base + threadIdx.x;
+	// one queue entry: closest ray (j < n_a) or shadow ray (n_a <= j < total)
+	auto traceEntry = [&](uint32_t j) {
 		if(j < n_a)
 		{
 			const uint32_t i = a0 + j;
@@ -915,6 +985,46 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 			P.occ[Q.sh_idx[k]] = occ ? 1 : 0;   // P = state set of the consumer shade
 			++n_shadow;
 		}
+	};
+	if constexpr(SORT)
+	{
+		// wave-private windows of kSortWin entries, dealt round-robin over the segment's waves
+		__shared__ WaveSort wsort[kTraceBlock / 64];
+		WaveSort &W = wsort[threadIdx.x >> 6];
+		const uint32_t nwv = blockDim.x >> 6;
+		const uint32_t gw = L.r * nwv + (threadIdx.x >> 6), nw = L.nb * nwv;
+		for(uint32_t w0 = gw * kSortWin; w0 < total; w0 += nw * kSortWin)
+		{
+			uint32_t key[kSortPer];
+#pragma unroll
+			for(int r = 0; r < kSortPer; ++r)
+			{
+				const uint32_t j = w0 + (uint32_t)(r * 64) + laneId();
+				uint32_t k = kSortBins - 1;
+				if(j < n_a)
+				{
+					const float4 dd = Q.ray_d[a0 + j];
+					if(!(dd.w != dd.w)) k = rayKey(dd, false);
+				}
+				else if(j < total) k = rayKey(Q.sh_d[s0 + (j - n_a)], true);
+				key[r] = k;
+			}
+			waveSortWindow(W, key);
+#pragma unroll 1
+			for(int r = 0; r < kSortPer; ++r) traceEntry(w0 + W.perm[r * 64 + laneId()]);
+		}
+	}
+	else
+	{
+#ifndef YAF_TRACE_NOREFILL
+	// refill pays where traversals are long (meshes in global memory: C4 -16%); on the short
+	// LDS-resident traversals of small scenes its per-visit bookkeeping costs more (C2 +35%)
+	if(!LDS_SCENE && WIDE && !TS)
+		traceRefill4<true, STATS>(C, Q, P, n_a, total, a0, s0, L.r * blockDim.x + threadIdx.x, stride, visits, tests, n_closest, n_shadow);
+	else
+#endif
+	// one uniform trip count per workgroup so every lane reaches the same exits
+	for(uint32_t base = L.r * blockDim.x; base < total; base += stride) traceEntry(base + threadIdx.x);
 	}
 	// statistics (rays issued, nodes visited, triangles tested): wave reduce, then one plain
 	// read-modify-write per workgroup into its own record (no atomics: the same block index owns
@@ -4188,7 +4298,16 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 	}
 	else if(S->scene_in_lds)
 	{
-		if(nospill && wide && !S->trace_stats)
+		if(nospill && wide && S->ray_sort)
+		{
+			if(S->trace_stats)
+				hipLaunchKernelGGL((k_trace<true, true, false, false, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
+				                   stack_depth, spill);
+			else
+				hipLaunchKernelGGL((k_trace<true, true, false, false, false, true>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
+				                   stack_depth, spill);
+		}
+		else if(nospill && wide && !S->trace_stats)
 			hipLaunchKernelGGL((k_trace<true, true, false, false, false>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
 			                   stack_depth, spill);
 		else if(nospill) { if(wide) YAF_TRACE_LAUNCH(true, true, false, false); else YAF_TRACE_LAUNCH(true, false, false, false); }

@@ -660,6 +660,13 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 		const char *e = getenv("YAFARAY_AMD_TRACE");
 		S.brute = (e && std::string(e) == "brute") ? 1 : 0;
 	}
+	// ray-stream sorting in k_trace (opt-in, YAFARAY_AMD_RAY_SORT=1): measured on C2 it lifts the
+	// VALU lane utilisation 0.44 -> 0.50 but costs more than it saves (k_trace 27.6 -> 28.9 ms per
+	// frame: the key pass reads every direction twice and the sort's registers spill), DESIGN.md §5
+	{
+		const char *e = getenv("YAFARAY_AMD_RAY_SORT");
+		S.ray_sort = (e && *e == '1') ? 1 : 0;
+	}
 	S.ph_lights = (const int *)d.ph_lights.p;
 	S.light_cdf = (const float *)d.light_cdf.p;
 	S.light_func = (const float *)d.light_func.p;

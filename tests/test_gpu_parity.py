@@ -49,13 +49,15 @@ def product_scene(product, spec):
 # levels of k_trace / k_photon_bounce), and the binary BVH2
 # and the device-built BVH4 (bvhgpu.hip: PLOC + collapse; the default for >= 64 K triangles)
 # "brute": scenes of <= 64 triangles (the Cornell box) through k_trace_brute (opt-in; the other
-# variants pin the BVH traversal explicitly)
+# variants pin the BVH traversal explicitly); "ray-sort": k_trace<SORT> (LDS-resident scenes)
 BVH_VARIANTS = {"bvh4": {"YAFARAY_AMD_BVH_BUILD": "host", "YAFARAY_AMD_TRACE": "bvh"},
                 "bvh4-spill": {"YAFARAY_AMD_LDS_STACK": "4", "YAFARAY_AMD_TRACE": "bvh"},
                 "bvh2": {"YAFARAY_AMD_BVH_WIDTH": "2", "YAFARAY_AMD_TRACE": "bvh"},
                 "gpu-build": {"YAFARAY_AMD_BVH_BUILD": "gpu", "YAFARAY_AMD_TRACE": "bvh"},
                 "bvh4-global": {"YAFARAY_AMD_SCENE_LDS": "0", "YAFARAY_AMD_TRACE": "bvh"},
-                "brute": {"YAFARAY_AMD_TRACE": "brute"}}
+                "brute": {"YAFARAY_AMD_TRACE": "brute"},
+                # ray-stream sorting (opt-in): each wave's window of queue entries in key order
+                "ray-sort": {"YAFARAY_AMD_RAY_SORT": "1", "YAFARAY_AMD_TRACE": "bvh"}}
 
 
 def use_bvh(monkeypatch, variant):
