@@ -3411,14 +3411,21 @@ __device__ __forceinline__ int pkLookup(const uint4 *nodes, V3 p, int k, float &
 // several times the resident waves of k_gather for the latency-bound walk) and logs every accepted
 // photon (index, distance) in visit order.  Pass 2 (k_gather<REPLAY>) feeds the log through
 // PhotonGather's heap in LDS — the reference's element moves exactly — and computes the estimate.
-constexpr int kWalkK = 64;
+#ifndef YAF_WALK_K
+#define YAF_WALK_K 64
+#endif
+constexpr int kWalkK = YAF_WALK_K;   // register slots of the walk (>= the search's k)
 #ifndef YAF_WALK_PER_SEG
 #define YAF_WALK_PER_SEG 16
 #endif
 constexpr int kWalkPerSeg = YAF_WALK_PER_SEG;   // walk workgroups per queue segment
 
-// pkLookup's walk with the k smallest distances in registers, sorted descending (unused slots -1,
-// so kd[0] is the heap's top once k were found): an insertion is one v_med3 per slot.  The stack is an LDS column of
+// pkLookup's walk with the k smallest distances in registers: kd[] ascending, its first kWalkK - k
+// slots pinned at -1 (below every distance) and the rest +inf, so after any number of insertions
+// kd[kWalkK - 1] is the largest of the k smallest accepted distances (+inf while fewer than k were
+// accepted) and the reference's max_d2 is min(radius, kd[kWalkK - 1]).  One insertion is one v_med3
+// per slot with no "heap full" branch, so the compiler keeps one copy of the array (the two-case
+// form held two: 153 VGPRs, 3 waves / SIMD).  The stack is an LDS column of
 // far-child indices (4 B; stk[level * kGatherBlock]): a popped interior node carries its parent's
 // plane (pkd.hip), from which the plane distance the reference stacked is recomputed; a popped leaf
 // is tested directly (its photon lies beyond that plane, so the reference's pop-time rejection and
@@ -3427,10 +3434,14 @@ constexpr int kWalkPerSeg = YAF_WALK_PER_SEG;   // walk workgroups per queue seg
 __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, float max_d2, uint2 *lg, uint32_t cap, uint32_t *stk,
                                            uint32_t &visits)
 {
+	const float radius2 = max_d2;
+	// (an opaque bound: otherwise the 64 initial values are hoisted out of the request loop and
+	// stay live across every walk — 64 more VGPRs)
+	int pinned = kWalkK - k;
+	asm volatile("" : "+s"(pinned));
 	float kd[kWalkK];
 #pragma unroll
-	for(int i = 0; i < kWalkK; ++i) kd[i] = -1.f;
-	int found = 0;
+	for(int i = 0; i < kWalkK; ++i) kd[i] = (i < pinned) ? -1.f : __builtin_huge_valf();
 	uint32_t n_acc = 0;
 	uint2 pend = make_uint2(0u, 0u);
 	uint32_t curr = 0;
@@ -3469,24 +3480,12 @@ __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, floa
 			}
 			else pend = e;
 			++n_acc;
-			if(found < k)
-			{
-				// insert: the slot where dist_2 belongs takes it, the smaller ones shift down
+			// insert (the largest slot drops out): below k accepted this fills a +inf slot (the heap
+			// grows); from then on it removes the top and adds dist_2 (pop_heap + push_heap)
 #pragma unroll
-				for(int i = kWalkK - 1; i > 0; --i) kd[i] = __builtin_amdgcn_fmed3f(kd[i - 1], kd[i], dist_2);
-				kd[0] = fmaxf(kd[0], dist_2);
-				++found;
-				if(found == k) max_d2 = kd[0];
-			}
-			else
-			{
-				// pop_heap removes the top (kd[0] = max_d2), push_heap adds dist_2: the larger ones
-				// shift up
-#pragma unroll
-				for(int i = 0; i < kWalkK - 1; ++i) kd[i] = __builtin_amdgcn_fmed3f(kd[i], kd[i + 1], dist_2);
-				kd[kWalkK - 1] = fminf(kd[kWalkK - 1], dist_2);
-				max_d2 = kd[0];
-			}
+			for(int i = kWalkK - 1; i > 0; --i) kd[i] = __builtin_amdgcn_fmed3f(kd[i - 1], kd[i], dist_2);
+			kd[0] = fminf(kd[0], dist_2);
+			max_d2 = fminf(radius2, kd[kWalkK - 1]);
 		}
 		// pop the next far child the current radius still reaches
 		bool more = false;
@@ -3519,7 +3518,10 @@ __device__ __forceinline__ uint2 *gatherLogAt(const GatherLog &L, uint32_t q)
 }
 
 // pass 1 over one batch of the gather queue (diffuse-map requests; the others log nothing)
-__global__ void __launch_bounds__(kGatherBlock) k_gather_walk(GatherArgs A)
+#ifndef YAF_WALK_WAVES
+#define YAF_WALK_WAVES 5
+#endif
+__global__ void __launch_bounds__(kGatherBlock) __attribute__((amdgpu_waves_per_eu(YAF_WALK_WAVES))) k_gather_walk(GatherArgs A)
 {
 	extern __shared__ uint32_t walk_stack[];
 	const DevScene &S = A.S;
@@ -4313,6 +4315,15 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 		else if(nospill) { if(wide) YAF_TRACE_LAUNCH(true, true, false, false); else YAF_TRACE_LAUNCH(true, false, false, false); }
 		else if(wide) YAF_TRACE_LAUNCH(true, true, false, true);
 		else YAF_TRACE_LAUNCH(true, false, false, true);
+	}
+	else if(wide && S->ray_sort)
+	{
+		if(S->trace_stats)
+			hipLaunchKernelGGL((k_trace<false, true, false, true, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
+			                   stack_depth, spill);
+		else
+			hipLaunchKernelGGL((k_trace<false, true, false, true, false, true>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
+			                   stack_depth, spill);
 	}
 	else if(wide && !S->trace_stats)
 		hipLaunchKernelGGL((k_trace<false, true, false, true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
