@@ -152,6 +152,12 @@ YAFARAY_C_API_EXPORT int yafaray_amd_unpackBands(const float *recv, int width, i
                                                  int rank, float *film);
 
 /* Tuning: samples in flight per wavefront chunk (default 1 << 25, halved automatically if it does not fit) and whether to time k_trace with events. */
+/* (LIBYAFARAY_AMD_1.3) The photon map's point kd-tree on its own (batched seam for
+ * PointKdTree<T>::PointKdTree, reference include/photon/pkdtree.h:115-222): n positions (x, y, z) in,
+ * 2n - 1 nodes of 4 uint32 out in the reference's depth-first layout (.w: bits 0-1 axis or 3 = leaf,
+ * interior: right child << 2 and .x the split position bits, .y / .z the parent's plane; leaf:
+ * photon index << 2 and .xyz its position bits), *depth = deepest level (root 0).  Current device. */
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_buildPhotonTree(const float *xyz, int n, unsigned int *nodes, int *depth);
 YAFARAY_C_API_EXPORT void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots);
 YAFARAY_C_API_EXPORT void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_t enable);
 /* (LIBYAFARAY_AMD_1.2) Per-visit BVH node / triangle counters in the traversal kernels (default on).

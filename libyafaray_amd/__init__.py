@@ -143,6 +143,7 @@ def lib():
             "yafaray_amd_getDeviceGroupSize": (i, [vp]),
             "yafaray_amd_packBand": (i, [C.POINTER(C.c_float), i, i, i, C.POINTER(C.c_int), i, i, C.POINTER(C.c_float)]),
             "yafaray_amd_unpackBands": (i, [C.POINTER(C.c_float), i, i, i, C.POINTER(C.c_int), i, i, C.POINTER(C.c_float)]),
+            "yafaray_amd_buildPhotonTree": (b, [C.POINTER(C.c_float), i, C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
             "yafaray_amd_setChunkSlots": (None, [vp, i]),
             "yafaray_amd_setProfileKernels": (None, [vp, b]),
             "yafaray_amd_setTraceStats": (None, [vp, b]),
@@ -342,6 +343,21 @@ def join_render_group(yi, rank, world, dist):
     gid = obj[0]
     if not yi.L.yafaray_amd_setRenderGroup(yi.h, int(rank), int(world), gid, len(gid)):
         raise RuntimeError("setRenderGroup failed: " + yi.last_error())
+
+
+def build_photon_tree(xyz):
+    """The GPU point kd-tree of n positions ((n, 3) float32): ((2n - 1, 4) uint32 nodes, depth) in
+    the reference's depth-first layout (yafaray_amd_buildPhotonTree)."""
+    import numpy as np
+    xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+    n = int(xyz.shape[0])
+    nodes = np.zeros((2 * n - 1, 4), np.uint32)
+    depth = C.c_int(0)
+    ok = lib().yafaray_amd_buildPhotonTree(xyz.ctypes.data_as(C.POINTER(C.c_float)), n,
+                                           nodes.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(depth))
+    if not ok:
+        raise RuntimeError("yafaray_amd_buildPhotonTree failed")
+    return nodes, depth.value
 
 
 def rebalance_bands(bounds, times, cap_rows=0):

@@ -8,12 +8,14 @@
 #include "hostmath.h"
 #include "render.h"
 
+#include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 using namespace yafamd;
 
@@ -643,6 +645,33 @@ int yafaray_amd_rebalanceBands(const int *bounds, int world, const double *times
 	const std::vector<int> nb = rebalanceBands(b, t, cap_rows);
 	for(int r = 0; r <= world; ++r) out[r] = nb[r];
 	return 1;
+}
+
+// the point kd-tree build on its own (a batched seam for PointKdTree<T>::PointKdTree,
+// include/photon/pkdtree.h:115-222): n positions (xyz) in, 2n - 1 nodes (4 x uint32 each, the
+// layout of pkd.hip) and the deepest level out; runs on the current HIP device with its own stream
+extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch);
+extern "C" void yafamd_pkd_scratch_free(void *scratch);
+yafaray_bool_t yafaray_amd_buildPhotonTree(const float *xyz, int n, unsigned int *nodes, int *depth)
+{
+	if(!xyz || !nodes || !depth || n < 1) return YAFARAY_BOOL_FALSE;
+	std::vector<float4> pos((size_t)n);
+	for(int i = 0; i < n; ++i) pos[(size_t)i] = make_float4(xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1], xyz[3 * (size_t)i + 2], 0.f);
+	float4 *pos_dev = nullptr;
+	uint4 *nodes_dev = nullptr;
+	hipStream_t st = nullptr;
+	void *scratch = nullptr;
+	bool ok = hipStreamCreate(&st) == hipSuccess && hipMalloc(&pos_dev, pos.size() * sizeof(float4)) == hipSuccess &&
+	          hipMalloc(&nodes_dev, (2 * (size_t)n - 1) * sizeof(uint4)) == hipSuccess &&
+	          hipMemcpyAsync(pos_dev, pos.data(), pos.size() * sizeof(float4), hipMemcpyHostToDevice, st) == hipSuccess &&
+	          yafamd_build_pkd(pos_dev, (uint32_t)n, nodes_dev, depth, st, &scratch) == hipSuccess &&
+	          hipMemcpyAsync(nodes, nodes_dev, (2 * (size_t)n - 1) * sizeof(uint4), hipMemcpyDeviceToHost, st) == hipSuccess &&
+	          hipStreamSynchronize(st) == hipSuccess;
+	if(scratch) yafamd_pkd_scratch_free(scratch);
+	if(pos_dev) (void)hipFree(pos_dev);
+	if(nodes_dev) (void)hipFree(nodes_dev);
+	if(st) (void)hipStreamDestroy(st);
+	return ok ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
 }
 
 int yafaray_amd_packBand(const float *film, int width, int height, int channels, const int *bounds, int world, int rank, float *send)

@@ -13,8 +13,9 @@
 //            [start, end) in all three lists.
 //   top      level-synchronous while nodes hold more than kSub photons: per node the largest axis of
 //            its bound picks the list whose element (start + end) / 2 is the median; each list is
-//            stably partitioned around it ((key, index) < median goes left: one exclusive scan per
-//            list whose input is that comparison).  A node of m > 1 photons always has two children,
+//            stably partitioned around it ((key, index) < median goes left): the three lists in one
+//            single-pass launch with a decoupled look-back (k_level_partition; the level-wise
+//            exclusive scan + partition per list remains as YAFARAY_AMD_PKD_PARTITION=scan).  A node of m > 1 photons always has two children,
 //            so level d holds exactly 2^d nodes of floor / ceil(n / 2^d) photons and all nodes of a
 //            level leave the top phase together.
 //   bottom   one workgroup per remaining subtree (<= kSub photons) finishes it in LDS, level by
@@ -29,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <cstdint>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "pkd_kernels.h"
@@ -63,11 +66,14 @@ struct DevBuf
 // scratch of the build, kept between builds (the photon map is rebuilt every frame)
 struct PkdScratch
 {
-	DevBuf kx, ky, kz, iota, sorted_keys, sorted_idx, sort_tmp, rec[3], rec_out, segs[2], seg_of, scan, scan_tmp, splits, partial, max_level;
+	DevBuf kx, ky, kz, kxyz, iota, sorted_keys, sorted_idx, sort_tmp, rec[3], rec_out, segs[2], seg_of, scan, scan_tmp, splits, partial, max_level;
+	// fused level partition (k_level_partition)
+	DevBuf rec_out2[2], seg_of2, seg_nl, seg_left, status, part_misc;
 	~PkdScratch()
 	{
-		for(DevBuf *b : {&kx, &ky, &kz, &iota, &sorted_keys, &sorted_idx, &sort_tmp, &rec[0], &rec[1], &rec[2], &rec_out, &segs[0], &segs[1],
-		                 &seg_of, &scan, &scan_tmp, &splits, &partial, &max_level})
+		for(DevBuf *b : {&kx, &ky, &kz, &kxyz, &iota, &sorted_keys, &sorted_idx, &sort_tmp, &rec[0], &rec[1], &rec[2], &rec_out, &segs[0], &segs[1],
+		                 &seg_of, &scan, &scan_tmp, &splits, &partial, &max_level, &rec_out2[0], &rec_out2[1], &seg_of2, &seg_nl, &seg_left,
+		                 &status, &part_misc})
 			b->release();
 	}
 };
@@ -108,10 +114,10 @@ extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 
 	const uint32_t B = 256, G = (n + B - 1) / B;
 	for(DevBuf *b : {&S.kx, &S.ky, &S.kz, &S.iota, &S.sorted_keys, &S.sorted_idx, &S.seg_of}) PKCHECK(b->ensure((size_t)n * 4));
 	PKCHECK(S.scan.ensure(((size_t)n + 1) * 4));
-	for(DevBuf *b : {&S.rec[0], &S.rec[1], &S.rec[2], &S.rec_out}) PKCHECK(b->ensure((size_t)n * 16));
+	for(DevBuf *b : {&S.rec[0], &S.rec[1], &S.rec[2], &S.rec_out, &S.kxyz}) PKCHECK(b->ensure((size_t)n * 16));
 	// lists sorted by (coordinate, index): stable radix sorts of the keys over index order
 	hipLaunchKernelGGL(k_keys, dim3(G), dim3(B), 0, st, pos_dev, n, S.kx.as<uint32_t>(), S.ky.as<uint32_t>(), S.kz.as<uint32_t>(),
-	                   S.iota.as<uint32_t>());
+	                   S.iota.as<uint32_t>(), S.kxyz.as<uint4>());
 	size_t sort_bytes = 0;
 	PKCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, S.kx.as<uint32_t>(), S.sorted_keys.as<uint32_t>(), S.iota.as<uint32_t>(),
 	                                           S.sorted_idx.as<uint32_t>(), (int)n, 0, 32, st));
@@ -121,7 +127,7 @@ extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 
 	{
 		PKCHECK(hipcub::DeviceRadixSort::SortPairs(S.sort_tmp.p, sort_bytes, keys[a], S.sorted_keys.as<uint32_t>(), S.iota.as<uint32_t>(),
 		                                           S.sorted_idx.as<uint32_t>(), (int)n, 0, 32, st));
-		hipLaunchKernelGGL(k_records, dim3(G), dim3(B), 0, st, S.sorted_idx.as<uint32_t>(), n, keys[0], keys[1], keys[2], S.rec[a].as<uint4>());
+		hipLaunchKernelGGL(k_records, dim3(G), dim3(B), 0, st, S.sorted_idx.as<uint32_t>(), n, S.kxyz.as<uint4>(), S.rec[a].as<uint4>());
 	}
 	// root bound (pkdtree.h:98-101) and the root segment
 	const uint32_t n_part = std::min<uint32_t>(G, 1024);
@@ -141,6 +147,22 @@ extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 
 		PKCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, in, S.scan.as<uint32_t>(), (int)n, st));
 	}
 	PKCHECK(S.scan_tmp.ensure(scan_bytes));
+	// fused partitions (default) or the scan + partition passes per list (YAFARAY_AMD_PKD_PARTITION=scan)
+	const char *pe = getenv("YAFARAY_AMD_PKD_PARTITION");
+	const bool fused = !(pe && std::string(pe) == "scan");
+	const uint32_t n_tiles = (n + kPartTile - 1) / kPartTile;
+	size_t left_scan_bytes = 0;
+	if(fused)
+	{
+		for(DevBuf *b : {&S.rec_out2[0], &S.rec_out2[1]}) PKCHECK(b->ensure((size_t)n * 16));
+		for(DevBuf *b : {&S.seg_of2, &S.seg_nl, &S.seg_left}) PKCHECK(b->ensure((size_t)n * 4));
+		PKCHECK(S.status.ensure((size_t)3 * n_tiles * 8));
+		PKCHECK(S.part_misc.ensure(64));   // [0] ticket, [1] error
+		PKCHECK(hipMemsetAsync(S.status.p, 0, (size_t)3 * n_tiles * 8, st));
+		PKCHECK(hipMemsetAsync(S.part_misc.p, 0, 64, st));
+		PKCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, left_scan_bytes, S.seg_nl.as<uint32_t>(), S.seg_left.as<uint32_t>(), (int)n, st));
+		PKCHECK(S.scan_tmp.ensure(std::max(scan_bytes, left_scan_bytes)));
+	}
 	// top phase: level d has 2^d nodes of floor / ceil(n / 2^d) photons
 	uint32_t n_seg = 1;
 	int cur = 0, level = 0;
@@ -149,7 +171,44 @@ extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 
 	{
 		const uint32_t Gs = (n_seg + B - 1) / B;
 		hipLaunchKernelGGL(k_level_split, dim3(Gs), dim3(B), 0, st, S.segs[cur].as<Seg>(), n_seg, n, S.rec[0].as<uint4>(), S.rec[1].as<uint4>(),
-		                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, S.splits.as<Split>(), S.segs[cur ^ 1].as<Seg>());
+		                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, S.splits.as<Split>(), S.segs[cur ^ 1].as<Seg>(),
+		                   fused ? S.seg_nl.as<uint32_t>() : nullptr);
+		if(fused)
+		{
+			PKCHECK(hipcub::DeviceScan::ExclusiveSum(S.scan_tmp.p, left_scan_bytes, S.seg_nl.as<uint32_t>(), S.seg_left.as<uint32_t>(), (int)n_seg, st));
+			PKCHECK(hipMemsetAsync(S.part_misc.p, 0, 4, st));   // ticket
+			PartArgs P;
+			DevBuf *outs[3] = {&S.rec_out, &S.rec_out2[0], &S.rec_out2[1]};
+			for(int a = 0; a < 3; ++a)
+			{
+				P.in[a] = S.rec[a].as<uint4>();
+				P.out[a] = outs[a]->as<uint4>();
+			}
+			P.seg_of = S.seg_of.as<uint32_t>();
+			P.seg_of_next = S.seg_of2.as<uint32_t>();
+			P.segs = S.segs[cur].as<Seg>();
+			P.splits = S.splits.as<Split>();
+			P.seg_left = S.seg_left.as<uint32_t>();
+			P.n = n;
+			P.n_tiles = n_tiles;
+			P.epoch = (uint32_t)level + 1u;
+			P.ticket = S.part_misc.as<uint32_t>();
+			P.err = S.part_misc.as<uint32_t>() + 1;
+			P.status = S.status.as<uint64_t>();
+			hipLaunchKernelGGL(k_level_partition, dim3(3 * n_tiles), dim3(kPartThreads), 0, st, P);
+			for(int a = 0; a < 3; ++a)
+			{
+				std::swap(S.rec[a].p, outs[a]->p);
+				std::swap(S.rec[a].bytes, outs[a]->bytes);
+			}
+			std::swap(S.seg_of.p, S.seg_of2.p);
+			std::swap(S.seg_of.bytes, S.seg_of2.bytes);
+			n_seg *= 2;
+			max_m = (max_m + 1) / 2;
+			cur ^= 1;
+			++level;
+			continue;
+		}
 		for(int a = 0; a < 3; ++a)
 		{
 			hipcub::CountingInputIterator<uint32_t> it(0);
@@ -172,8 +231,11 @@ extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 
 	                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, n, level, S.max_level.as<int>());
 	hipLaunchKernelGGL(k_parent_planes, dim3((2 * n - 1 + 255) / 256), dim3(256), 0, st, nodes_dev, 2 * n - 1);
 	int depth = 0;
+	uint32_t part_err = 0;
 	PKCHECK(hipMemcpyAsync(&depth, S.max_level.p, 4, hipMemcpyDeviceToHost, st));
+	if(fused && level > 0) PKCHECK(hipMemcpyAsync(&part_err, S.part_misc.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
 	PKCHECK(hipStreamSynchronize(st));
+	if(part_err) return hipErrorLaunchFailure;   // a look-back gave up: the tree is not trustworthy
 	*depth_out = depth;
 	return hipGetLastError();
 }

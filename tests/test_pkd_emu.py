@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_pkd_kernels_emulated(tmp_path):
     exe = tmp_path / "pkd_emu"
     subprocess.run(["g++", "-std=c++20", "-O1", "-pthread", os.path.join(ROOT, "tools", "pkd_emu.cc"), "-o", str(exe)], check=True)
-    sizes = ["1", "2", "3", "17", "64", "65", "256", "257", "1000", "3000"]
+    sizes = ["1", "2", "3", "17", "64", "65", "256", "257", "1000", "3000", "9000"]
     out = subprocess.run([str(exe)] + sizes, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.strip().endswith("OK")

@@ -73,6 +73,14 @@ inline int atomicMax(int *a, int v)
 #define __shared__ static
 #define __launch_bounds__(x)
 #define PKD_CHECK 1
+#define PKD_EMU 1
+inline uint32_t atomicAdd(uint32_t *a, uint32_t v) { return __atomic_fetch_add(a, v, __ATOMIC_SEQ_CST); }
+inline uint32_t atomicMin(uint32_t *a, uint32_t v)
+{
+	uint32_t o = __atomic_load_n(a, __ATOMIC_SEQ_CST);
+	while(v < o && !__atomic_compare_exchange_n(a, &o, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {}
+	return o;
+}
 
 #include "../libyafaray_amd/csrc/pkd_kernels.h"
 
@@ -144,7 +152,7 @@ static int refBuild(const std::vector<float4> &pos, std::vector<uint32_t> idx, u
 	return std::max(a, b);
 }
 
-static bool run(uint32_t n, uint32_t seed)
+static bool run(uint32_t n, uint32_t seed, bool fused)
 {
 	std::mt19937 rng(seed);
 	std::uniform_real_distribution<float> U(-2.f, 2.f);
@@ -158,7 +166,8 @@ static bool run(uint32_t n, uint32_t seed)
 	}
 	const uint32_t B = 256, G = (n + B - 1) / B;
 	std::vector<uint32_t> kx(n), ky(n), kz(n), iota(n);
-	launchFlat(G, B, [&] { k_keys(pos.data(), n, kx.data(), ky.data(), kz.data(), iota.data()); });
+	std::vector<uint4> kxyz(n);
+	launchFlat(G, B, [&] { k_keys(pos.data(), n, kx.data(), ky.data(), kz.data(), iota.data(), kxyz.data()); });
 	std::vector<uint4> rec[3], rec_out(n);
 	const std::vector<uint32_t> *keys[3] = {&kx, &ky, &kz};
 	for(int a = 0; a < 3; ++a)
@@ -166,13 +175,13 @@ static bool run(uint32_t n, uint32_t seed)
 		std::vector<uint32_t> si(iota);
 		std::stable_sort(si.begin(), si.end(), [&](uint32_t i, uint32_t j) { return (*keys[a])[i] < (*keys[a])[j]; });
 		rec[a].resize(n);
-		launchFlat(G, B, [&] { k_records(si.data(), n, kx.data(), ky.data(), kz.data(), rec[a].data()); });
+		launchFlat(G, B, [&] { k_records(si.data(), n, kxyz.data(), rec[a].data()); });
 	}
 	const uint32_t n_part = std::min<uint32_t>(G, 1024);
 	std::vector<float> partial(n_part * 6);
 	std::vector<Seg> segs[2] = {std::vector<Seg>(n), std::vector<Seg>(n)};
 	std::vector<Split> splits(n);
-	std::vector<uint32_t> seg_of(n, 0), scan(n + 1);
+	std::vector<uint32_t> seg_of(n, 0), scan(n + 1), seg_nl(n), seg_left(n);
 	std::vector<uint4> nodes(2 * n - 1, make_uint4(0xdead, 0xdead, 0xdead, 0xdead));
 	launch(n_part, 256, [&] { k_bound(pos.data(), n, partial.data()); });
 	launch(1, 256, [&] { k_root(partial.data(), n_part, n, segs[0].data()); });
@@ -183,8 +192,43 @@ static bool run(uint32_t n, uint32_t seed)
 	{
 		launchFlat((n_seg + B - 1) / B, B, [&] {
 			k_level_split(segs[cur].data(), n_seg, n, rec[0].data(), rec[1].data(), rec[2].data(), pos.data(), nodes.data(), splits.data(),
-			              segs[cur ^ 1].data());
+			              segs[cur ^ 1].data(), seg_nl.data());
 		});
+		if(fused)
+		{
+			// pkd.hip's fused level: seg_left = exclusive sum of the left counts, one k_level_partition
+			// launch over the three lists (workgroups run one after another here, so every look-back
+			// finds its predecessor's inclusive prefix)
+			uint32_t acc = 0;
+			for(uint32_t k = 0; k < n_seg; ++k) { seg_left[k] = acc; acc += seg_nl[k]; }
+			const uint32_t n_tiles = (n + kPartTile - 1) / kPartTile;
+			std::vector<uint64_t> status(3 * n_tiles, 0);
+			uint32_t misc[2] = {0, 0};
+			std::vector<uint4> outs[3] = {std::vector<uint4>(n), std::vector<uint4>(n), std::vector<uint4>(n)};
+			std::vector<uint32_t> seg_of2(n);
+			PartArgs P;
+			for(int a = 0; a < 3; ++a) { P.in[a] = rec[a].data(); P.out[a] = outs[a].data(); }
+			P.seg_of = seg_of.data();
+			P.seg_of_next = seg_of2.data();
+			P.segs = segs[cur].data();
+			P.splits = splits.data();
+			P.seg_left = seg_left.data();
+			P.n = n;
+			P.n_tiles = n_tiles;
+			P.epoch = (uint32_t)level + 1u;
+			P.ticket = &misc[0];
+			P.err = &misc[1];
+			P.status = status.data();
+			launch(3 * n_tiles, kPartThreads, [&] { k_level_partition(P); });
+			if(misc[1]) { std::printf("look-back gave up\n"); return false; }
+			for(int a = 0; a < 3; ++a) std::swap(rec[a], outs[a]);
+			std::swap(seg_of, seg_of2);
+			n_seg *= 2;
+			max_m = (max_m + 1) / 2;
+			cur ^= 1;
+			++level;
+			continue;
+		}
 		for(int a = 0; a < 3; ++a)
 		{
 			LeftFlag f{rec[a].data(), seg_of.data(), splits.data(), n};
@@ -215,7 +259,7 @@ static bool run(uint32_t n, uint32_t seed)
 	size_t bad = 0, first = 0;
 	for(size_t i = 0; i < want.size(); ++i)
 		if(std::memcmp(&want[i], &nodes[i], 16) != 0 && bad++ == 0) first = i;
-	std::printf("n=%u top_levels=%d check_line=%u depth=%d ref_depth=%d mismatching_nodes=%zu", n, level, g_pkd_err, max_level, depth, bad);
+	std::printf("%s n=%u top_levels=%d check_line=%u depth=%d ref_depth=%d mismatching_nodes=%zu", fused ? "fused" : "scan", n, level, g_pkd_err, max_level, depth, bad);
 	if(bad) std::printf(" first=%zu got=(%x %x %x %x) want=(%x %x %x %x)", first, nodes[first].x, nodes[first].y, nodes[first].z, nodes[first].w,
 	                    want[first].x, want[first].y, want[first].z, want[first].w);
 	std::printf("\n");
@@ -227,7 +271,8 @@ static bool run(uint32_t n, uint32_t seed)
 int main(int argc, char **argv)
 {
 	bool ok = true;
-	for(int i = 1; i < argc; ++i) ok = run((uint32_t)std::atoi(argv[i]), 7u + (uint32_t)i) && ok;
+	for(int i = 1; i < argc; ++i)
+		for(bool fused : {false, true}) ok = run((uint32_t)std::atoi(argv[i]), 7u + (uint32_t)i, fused) && ok;
 	std::printf(ok ? "OK\n" : "FAILED\n");
 	return ok ? 0 : 1;
 }
