@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KINDS = ["k_camera", "k_trace", "k_surface", "k_tshadow", "k_shade", "k_nee", "k_gather", "k_spawn", "k_combine", "k_film",
          "k_photon_emit", "k_photon_bounce", "k_fg", "k_pregather", "k_gather_walk"]
 COMPACT = ("k_photon_count", "k_photon_scan", "k_photon_scatter")
-PKD = ("k_keys", "k_records", "k_bound", "k_root", "k_level_split", "k_partition", "k_seg_of", "k_subtrees")
+PKD = ("k_keys", "k_records", "k_bound", "k_root", "k_level_split", "k_level_partition", "k_partition", "k_seg_of", "k_subtrees", "k_parent_planes")
 
 
 def kernel_src_sha1():
