@@ -312,9 +312,10 @@ def kernel_table(a, s, kt, pmc):
             e["achieved_gbs"] = round(ab / (v["ms"] * 1e-3) / 1e9, 1)
             e["frac"] = round(ab / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         p = (pmc or {}).get("kernels", {}).get(kind)
-        if p and "hbm_bytes_total" in p and v["ms"] > 0:
-            e["traffic_bytes"] = p["hbm_bytes_total"]                 # measured, one frame (PMC pass)
-            e["traffic_gbs"] = round(p["hbm_bytes_total"] / (v["ms"] * 1e-3) / 1e9, 1)
+        if p and "hbm_bytes_per_launch" in p and v["ms"] > 0 and v["launches"]:
+            # measured per launch (the PMC pass may span several frames: its total is not one frame's)
+            e["traffic_bytes"] = int(p["hbm_bytes_per_launch"] * v["launches"])
+            e["traffic_gbs"] = round(e["traffic_bytes"] / (v["ms"] * 1e-3) / 1e9, 1)
             e["traffic_frac"] = round(e["traffic_gbs"] / HBM_PEAK_GBS, 4)
             if "valu_lane_util" in p:
                 e["valu_lane_util"] = p["valu_lane_util"]

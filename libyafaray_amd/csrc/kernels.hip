@@ -274,21 +274,11 @@ __device__ __forceinline__ SampleCoord sampleAt(const DevScene &S, const DevJob 
 	return sampleCoord(jobs, n_jobs, S.width, S.tile, S.spp, sid);
 }
 
-__global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueues Q, DevCounters cnt,
-                                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n)
+// One camera sample: TiledIntegrator::renderTile's sample position (integrator_tiled.cc:313-340) and
+// PerspectiveCamera::shootRay (camera_perspective.cc:128-146), plus the sample's Russian-roulette seed.
+// k_camera (wavefront) and k_path (megakernel) both start their samples here.
+__device__ __forceinline__ void cameraRay(const DevScene &S, const SampleCoord &sc, V3 &from, V3 &dir, float &tmin, float &tmax, uint32_t &seed)
 {
-	// sample i of the chunk -> segment (i / 256) % n_seg, groups of 256 dense within the segment
-	const int i = blockIdx.x * blockDim.x + threadIdx.x;
-	if((uint32_t)i < S.n_seg)
-	{
-		const uint32_t groups = (uint32_t)n / 256u, rem = (uint32_t)n % 256u, sg = (uint32_t)i, R = S.n_seg;
-		cnt.n_active[sg] = (groups / R) * 256u + (sg < groups % R ? 256u : 0u) + (sg == groups % R ? rem : 0u);
-		cnt.n_shadow[sg] = 0;
-	}
-	if(i >= n) return;
-	const uint32_t g = (uint32_t)i / 256u;
-	const uint32_t a = (g % S.n_seg) * S.cap_a + (g / S.n_seg) * 256u + (uint32_t)i % 256u;
-	const SampleCoord sc = sampleAt(S, jobs, n_jobs, chunk_base + (uint64_t)i);
 	// integrator_tiled.cc:313-335 (camera pixel coordinates: a cropped film starts at crop_x0 / crop_y0)
 	const int cx = sc.x + S.crop_x0, cy = sc.y + S.crop_y0;
 	const uint32_t offset = fnv32((uint32_t)cy * fnv32((uint32_t)cx));
@@ -309,12 +299,12 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	// camera_perspective.cc:128-146, plane.h:37-40
 	const DevCamera &c = S.cam;
 	const V3 pos = v3(c.pos[0], c.pos[1], c.pos[2]);
-	V3 dir = v3(c.vright[0], c.vright[1], c.vright[2]) * px + v3(c.vup[0], c.vup[1], c.vup[2]) * py + v3(c.vto[0], c.vto[1], c.vto[2]);
+	dir = v3(c.vright[0], c.vright[1], c.vright[2]) * px + v3(c.vup[0], c.vup[1], c.vup[2]) * py + v3(c.vto[0], c.vto[1], c.vto[2]);
 	dir = normalize(dir);
 	const V3 cz = v3(c.cam_z[0], c.cam_z[1], c.cam_z[2]);
-	const float tmin = dot(cz, v3(c.near_p[0], c.near_p[1], c.near_p[2]) - pos) / dot(dir, cz);
-	const float tmax = dot(cz, v3(c.far_p[0], c.far_p[1], c.far_p[2]) - pos) / dot(dir, cz);
-	V3 from = pos;
+	tmin = dot(cz, v3(c.near_p[0], c.near_p[1], c.near_p[2]) - pos) / dot(dir, cz);
+	tmax = dot(cz, v3(c.far_p[0], c.far_p[1], c.far_p[2]) - pos) / dot(dir, cz);
+	from = pos;
 	if(c.aperture != 0.f)
 	{
 		// integrator_tiled.cc:314-316, 336-340: Halton(3) / Halton(5) lens streams started at the
@@ -327,6 +317,34 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 		from = from + li;
 		dir = normalize(dir * c.dof_distance - li);
 	}
+	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
+	// output is matched statistically — integrator_tiled.cc:272), seeded from the pixel-major sample
+	// id so that the image does not depend on how the film is split over GPUs or chunks
+	// (64-bit id: W * H * spp passes 2^32 at 4K x 1024 spp; both halves are hashed)
+	const uint64_t gid = ((uint64_t)sc.y * (uint64_t)S.width + (uint64_t)sc.x) * (uint64_t)S.spp + (uint64_t)sc.s;
+	const uint32_t gid32 = (uint32_t)gid ^ fnv32((uint32_t)(gid >> 32));
+	seed = fnv32(gid32 ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)) + 123u;
+}
+
+__global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueues Q, DevCounters cnt,
+                                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n)
+{
+	// sample i of the chunk -> segment (i / 256) % n_seg, groups of 256 dense within the segment
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if((uint32_t)i < S.n_seg)
+	{
+		const uint32_t groups = (uint32_t)n / 256u, rem = (uint32_t)n % 256u, sg = (uint32_t)i, R = S.n_seg;
+		cnt.n_active[sg] = (groups / R) * 256u + (sg < groups % R ? 256u : 0u) + (sg == groups % R ? rem : 0u);
+		cnt.n_shadow[sg] = 0;
+	}
+	if(i >= n) return;
+	const uint32_t g = (uint32_t)i / 256u;
+	const uint32_t a = (g % S.n_seg) * S.cap_a + (g / S.n_seg) * 256u + (uint32_t)i % 256u;
+	const SampleCoord sc = sampleAt(S, jobs, n_jobs, chunk_base + (uint64_t)i);
+	V3 from, dir;
+	float tmin, tmax;
+	uint32_t seed;
+	cameraRay(S, sc, from, dir, tmin, tmax, seed);
 	// the compact record carries the sample id and the stage in pr (offset / sample index derive
 	// from the sample id); a specular recursion tree keeps them in the queue's slot and col.w
 	if(!S.tree)
@@ -335,24 +353,21 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 		Q.ray_d[a] = f4(dir, tmax);
 		P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
 		P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
+		P.pr[a] = make_uint4((uint32_t)i, ST_CAMERA, 30903u, seed);
 	}
 	else
 	{
+		const int cx = sc.x + S.crop_x0, cy = sc.y + S.crop_y0;
+		const uint32_t offset = fnv32((uint32_t)cy * fnv32((uint32_t)cx));
+		const uint32_t sample_idx = S.base_offset + S.pass_offset + (uint32_t)sc.s;
 		Q.slot[a] = i;          // sample id within the chunk travels with the queue entry
 		Q.ray_o[a] = f4(from, tmin);
 		Q.ray_d[a] = f4(dir, tmax);
 		P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
 		P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));   // stage
 		P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
+		P.pr[a] = make_uint4(offset, sample_idx, 30903u, seed);
 	}
-	// RR generator: per-sample MWC (the reference seeds one per tile from rand(), so RR
-	// output is matched statistically — integrator_tiled.cc:272), seeded from the pixel-major sample
-	// id so that the image does not depend on how the film is split over GPUs or chunks
-	// (64-bit id: W * H * spp passes 2^32 at 4K x 1024 spp; both halves are hashed)
-	const uint64_t gid = ((uint64_t)sc.y * (uint64_t)S.width + (uint64_t)sc.x) * (uint64_t)S.spp + (uint64_t)sc.s;
-	const uint32_t gid32 = (uint32_t)gid ^ fnv32((uint32_t)(gid >> 32));
-	const uint32_t seed = fnv32(gid32 ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)) + 123u;
-	P.pr[a] = S.tree ? make_uint4(offset, sample_idx, 30903u, seed) : make_uint4((uint32_t)i, ST_CAMERA, 30903u, seed);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1522,11 +1537,20 @@ __device__ __forceinline__ bool areaTri(V3 a, V3 b, V3 c, V3 o, V3 d, float &t)
 	return true;
 }
 
+struct ShadeOut;
+__device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, float tmin, int idx, const ShadeOut &out);
+
+// where neeLight's shadow rays go: ShadeOut appends them to the next queue (k_trace traces them);
+// k_path's emitter keeps them per lane and traces them in place
 struct ShadeOut
 {
 	uint32_t *sh_count;    // shadow-ray counter of the shard
 	uint32_t sh_base;      // first address of the shard's shadow queue
 	DevQueues Qn;
+	__device__ __forceinline__ void emit(bool want, V3 o, V3 d, float t_max, float tmin, int idx) const
+	{
+		emitShadow(want, o, d, t_max, tmin, idx, *this);
+	}
 };
 
 // Appends (or not) one shadow ray per lane — every lane of the wave must call.
@@ -1565,10 +1589,10 @@ __device__ __forceinline__ void tsFactors(float4 *ts, int e, C3 surf, float a, C
 // nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
 // Wave-uniform structure: `active` lanes do the work, every lane of the wave walks the same loop
 // bounds (the shadow-ray appends are wave-level).
-template<bool EXT>
+template<bool EXT, class Out>
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
-                         float4 *nee, uint8_t *occ, const ShadeOut &out, float4 *ts = nullptr)
+                         float4 *nee, uint8_t *occ, const Out &out, float4 *ts = nullptr)
 {
 	const bool cast_shadows = L.cast_shadows && m.receive_shadows;
 	const float p_len = length(sp.p);
@@ -1599,7 +1623,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 		}
 		else if(active) nee[e0] = make_float4(0.f, 0.f, 0.f, 0.f);
 		if(active) occ[e0] = 0;
-		emitShadow(ok && cast_shadows, so, ldir, st, sh_tmin, e0, out);
+		out.emit(ok && cast_shadows, so, ldir, st, sh_tmin, e0);
 		return;
 	}
 	// area light: montecarlo.cc:393-405
@@ -1672,7 +1696,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			nee[e0 + i] = f4(contrib, ok ? 1.f : 0.f);
 			occ[e0 + i] = 0;
 		}
-		emitShadow(ok && cast_shadows, so, ldir, st, sh_tmin, e0 + i, out);
+		out.emit(ok && cast_shadows, so, ldir, st, sh_tmin, e0 + i);
 
 		// areaLightSampleMaterial (montecarlo.cc:284-383)
 		ok = active;
@@ -1725,7 +1749,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			nee[e0 + num_samples + i] = f4(contrib, ok ? 1.f : 0.f);
 			occ[e0 + num_samples + i] = 0;
 		}
-		emitShadow(ok && cast_shadows, so, dir, st, b_tmin, e0 + num_samples + i, out);
+		out.emit(ok && cast_shadows, so, dir, st, b_tmin, e0 + num_samples + i);
 	}
 }
 
@@ -2728,6 +2752,589 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 	{
 		A.cnt_next.n_shadow[seg] = s_count;
 		if(S.stats) S.stats[seg].nee_requests += n_req;
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_path: the megakernel form of the same integrator for scenes that live in LDS.  One lane carries
+// one camera sample through its whole integrate() — k_camera's ray, then per vertex k_trace's
+// closest hit, k_shade's state machine (the compact record's stages, flags and deferred
+// connection) and k_nee's light sampling, whose shadow rays the lane traces in place — and takes the
+// next sample of its wave's pool when the sample is written.  The path state stays in registers and
+// the NEE contributions in LDS, so none of the wavefront's per-vertex HBM traffic (~270 B of state
+// and queues per vertex, ~125 B per NEE request) exists; HBM sees the camera samples' film records
+// only.  Every function on the way is the wavefront's own (cameraRay, traverse4, makeSurf,
+// matSample / matEmit, neeLight, neeSum), called in the same order per sample, so the film is
+// bit-identical to the wavefront's.  Eligible: non-EXT materials, BVH4 scene + stack bound in LDS,
+// PathIntegrator / DirectLight without AO, photon or caustic maps, transparent shadows (render.cc
+// pathEligible).
+// ---------------------------------------------------------------------------------------------
+constexpr int kPathMaxK = 8;        // NEE entries per vertex kept per lane in LDS
+constexpr int kPathBatch = 256;     // samples a wave takes from the chunk counter at a time
+
+struct PathArgs
+{
+	DevScene S;
+	float4 *samples;       // frame sample buffer [(y * W + x) * spp + s]
+	const DevJob *jobs;
+	int n_jobs;
+	uint64_t chunk_base;
+	uint32_t n;            // samples of the chunk
+	uint32_t *next;        // the chunk's sample counter (zero at launch)
+	int stack_depth;       // traversal stack levels (all in LDS)
+};
+
+// k_path's shadow-ray emitter: neeLight's rays are recorded per lane (origin + t_max, direction +
+// want) and traced after the light sampling; lanes that emit nothing leave their cleared records
+struct PathShadows
+{
+	float4 *rec;
+	__device__ __forceinline__ void emit(bool want, V3 o, V3 d, float t_max, float tmin, int idx) const
+	{
+		(void)tmin;   // the origin is already moved (shadowRayOf); the any-hit test starts at 0
+		if(want)
+		{
+			rec[2 * idx] = f4(o, t_max);
+			rec[2 * idx + 1] = f4(d, 1.f);
+		}
+	}
+};
+
+__host__ __device__ inline size_t pathLdsBytes(const DevScene &S, int stack_depth)
+{
+	return shadeLdsBytes(S, true) + (size_t)(S.node_f4 * S.n_nodes + 3 * S.n_tris) * 16 + (size_t)stack_depth * kTraceBlock * 4 +
+	       (size_t)kTraceBlock * S.nee_k * (16 + 32) + (((size_t)kTraceBlock * S.nee_k + 15) & ~(size_t)15);
+}
+
+// The rays one k_path lane owes before its next vertex: the shadow rays its last NEE recorded
+// (rec entries with `want`, when `shadows`) and its closest ray (when `closest`).  traceRefill4's
+// scheme: one BVH4 visit per loop trip and a lane starts its next ray as soon as one ends, so the
+// wave runs for its busiest lane's sum of traversals (not one full traversal per ray slot, most of
+// whose lanes would idle: the MIS material-sample shadow ray exists for a few lanes only).  Every ray
+// runs traverse4's exact sequence of visits, culling, leaf order and exits: hits are identical.
+template<bool STATS>
+__device__ __forceinline__ void traceLaneRays(const TraceCtx &C, const float4 *rec, uint8_t *occ, int K, bool shadows, bool closest, V3 co,
+                                              V3 cd, float ctmin, float ctmax, float &hit_t, int &hit_prim, uint32_t &visits,
+                                              uint32_t &tests, uint32_t &n_closest, uint32_t &n_shadow)
+{
+	const int lane = threadIdx.x;
+	const float inf = __builtin_huge_valf();
+	V3 o = v3(0.f, 0.f, 0.f), d = o, id = o, oid = o;
+	float tmax = 0.f, tmin = 0.f, box_t0 = 0.f, t_best = 0.f;
+	int prim_best = -1, sp = 0, node = -1, cur = 0;
+	int e = shadows ? 0 : K;
+	bool any = false, cl = closest;
+	for(;;)
+	{
+		if(node < 0)
+		{
+			// this lane's next ray: the recorded shadow rays in entry order, then the closest ray
+			bool got = false;
+			while(e < K)
+			{
+				const int ee = e++;
+				const float4 dd = rec[2 * ee + 1];
+				if(dd.w == 0.f) continue;
+				const float4 od = rec[2 * ee];
+				o = xyz(od);
+				d = xyz(dd);
+				tmin = 0.f;
+				tmax = od.w;
+				any = true;
+				cur = ee;
+				++n_shadow;
+				got = true;
+				break;
+			}
+			if(!got && cl)
+			{
+				cl = false;
+				o = co;
+				d = cd;
+				tmin = ctmin;
+				tmax = ctmax;
+				any = false;
+				++n_closest;
+				got = true;
+			}
+			if(!got) break;
+			V3 dq = d;
+			if(fabsf(dq.x) < 1e-20f) dq.x = copysignf(1e-20f, dq.x);
+			if(fabsf(dq.y) < 1e-20f) dq.y = copysignf(1e-20f, dq.y);
+			if(fabsf(dq.z) < 1e-20f) dq.z = copysignf(1e-20f, dq.z);
+			id = v3(rcpExact(dq.x), rcpExact(dq.y), rcpExact(dq.z));
+			oid = v3(o.x * id.x, o.y * id.y, o.z * id.z);
+			box_t0 = any ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
+			t_best = tmax;
+			prim_best = -1;
+			sp = 0;
+			node = 0;
+		}
+		if(STATS) TRACE_STAT(++visits);
+		const float4 *np = C.nodes + 8 * node;
+		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
+		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
+		float key[4];
+		int child[4], e4[4], s4[4];
+		int acc = 0;
+#pragma unroll
+		for(int k = 0; k < 4; ++k)
+		{
+			const float ax = __builtin_fmaf(lane4(lx, k), id.x, -oid.x), bx = __builtin_fmaf(lane4(hx, k), id.x, -oid.x);
+			const float ay = __builtin_fmaf(lane4(ly, k), id.y, -oid.y), by = __builtin_fmaf(lane4(hy, k), id.y, -oid.y);
+			const float az = __builtin_fmaf(lane4(lz, k), id.z, -oid.z), bz = __builtin_fmaf(lane4(hz, k), id.z, -oid.z);
+			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
+			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
+			const uint32_t h = lo <= hi ? 1u : 0u;
+			child[k] = __float_as_int(lane4(cf, k));
+			const int count = __float_as_int(lane4(kf, k));
+			const uint32_t inner = child[k] >= 0 ? 1u : 0u;
+			key[k] = (h & inner) ? lo : inf;
+			s4[k] = ~child[k] - acc;
+			acc += (h & (inner ^ 1u)) ? count : 0;
+			e4[k] = acc;
+		}
+		bool done = false;
+		for(int i = 0; i < e4[3]; ++i)
+		{
+			const int q = i + (i < e4[0] ? s4[0] : i < e4[1] ? s4[1] : i < e4[2] ? s4[2] : s4[3]);
+			if(STATS) TRACE_STAT(++tests);
+			const float4 *tp = C.tris + 3 * q;
+			const float4 ta = tp[0], tb = tp[1], tc = tp[2];
+			const float t = triTest(ta, tb, tc, o, d, t_best);
+			if(t == -1.f) continue;
+			const int prim = __float_as_int(tb.w);
+			if(any)
+			{
+				if(t < tmax && t >= 0.f) { t_best = t; prim_best = prim; done = true; break; }
+			}
+			else if(t >= tmin && (t < t_best || (t == t_best && prim_best >= 0 && prim < prim_best)))
+			{
+				t_best = t;
+				prim_best = prim;
+			}
+		}
+		if(!done)
+		{
+			cswap(key[0], child[0], key[1], child[1]);
+			cswap(key[2], child[2], key[3], child[3]);
+			cswap(key[0], child[0], key[2], child[2]);
+			cswap(key[1], child[1], key[3], child[3]);
+			cswap(key[1], child[1], key[2], child[2]);
+			if(key[3] < inf) { C.stack[sp * kTraceBlock + lane] = child[3]; ++sp; }
+			if(key[2] < inf) { C.stack[sp * kTraceBlock + lane] = child[2]; ++sp; }
+			if(key[1] < inf) { C.stack[sp * kTraceBlock + lane] = child[1]; ++sp; }
+			int next = key[0] < inf ? child[0] : -1;
+			if(next < 0 && sp > 0)
+			{
+				--sp;
+				next = C.stack[sp * kTraceBlock + lane];
+			}
+			node = next;
+			done = next < 0;
+		}
+		if(done)
+		{
+			if(any) occ[cur] = prim_best >= 0 ? 1 : 0;
+			else
+			{
+				hit_t = t_best;
+				hit_prim = prim_best;
+			}
+			node = -1;
+		}
+	}
+}
+
+// k_path's register budget: 2 waves per SIMD (<= 256 VGPRs incl. AGPRs; the unconstrained
+// allocation took 260 -> 1 wave); -DYAF_PATH_WAVES=n for tuning
+#ifndef YAF_PATH_WAVES
+#define YAF_PATH_WAVES 2
+#endif
+template<bool STATS>
+__global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(YAF_PATH_WAVES))) k_path(PathArgs A)
+{
+	extern __shared__ uint4 path_smem[];
+	const DevScene S = stageTables<true>(A.S, path_smem);
+	const int K = S.nee_k;
+	const int lane = threadIdx.x;
+	float4 *lds_nodes = reinterpret_cast<float4 *>(path_smem) + shadeLdsBytes(S, true) / 16;
+	float4 *lds_tris = lds_nodes + S.node_f4 * S.n_nodes;
+	int *stack = reinterpret_cast<int *>(lds_tris + 3 * S.n_tris);
+	float4 *nee_all = reinterpret_cast<float4 *>(stack + A.stack_depth * kTraceBlock);
+	float4 *rec_all = nee_all + kTraceBlock * K;
+	uint8_t *occ_all = reinterpret_cast<uint8_t *>(rec_all + 2 * kTraceBlock * K);
+	for(int k = threadIdx.x; k < S.node_f4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = A.S.nodes[k];
+	for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = A.S.tris[k];
+	__syncthreads();
+	TraceCtx C;
+	C.nodes = lds_nodes;
+	C.tris = lds_tris;
+	C.stack = stack;
+	C.lds_depth = A.stack_depth;
+	C.spill = nullptr;
+	C.spill_stride = 0;
+	float4 *nee = nee_all + lane * K;
+	float4 *rec = rec_all + 2 * lane * K;
+	uint8_t *occ = occ_all + lane * K;
+	const PathShadows out{rec};
+	const bool is_path = S.integrator == INT_PATH;
+	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
+	const float inf = __builtin_huge_valf();
+
+	// the lane's sample: record of k_shade's compact form, in registers
+	bool active = false;
+	uint32_t sid = 0, stage = ST_NORAY, flags = 0, offset = 0, sample_idx = 0;
+	uint2 rng = make_uint2(0u, 0u);
+	float w = 0.f;
+	C3 thr = c3(0.f), col = c3(0.f), pcol = c3(0.f), pthr = c3(0.f), pem = c3(0.f);
+	V3 pwo = v3(0.f, 0.f, 0.f), ray_o = pwo, ray_d = pwo;
+	float ray_tmin = 0.f, ray_tmax = 0.f;
+	float4 v0p4 = make_float4(0.f, 0.f, 0.f, 0.f), v0wo4 = v0p4;
+	SampleCoord sc{0, 0, 0};
+	// the wave's pool of chunk samples [pool, pool_end) (wave-uniform)
+	uint32_t pool = 0, pool_end = 0;
+	bool exhausted = false;
+	uint32_t n_closest = 0, n_shadow = 0, n_vert = 0, n_nee = 0, visits = 0, tests = 0;
+	PHASE_DECL
+	for(;;)
+	{
+		// ---- samples for the idle lanes (k_camera) ----
+		const uint64_t need = __ballot(!active);
+		if(need && !exhausted)
+		{
+			if(pool == pool_end)
+			{
+				uint32_t b = 0;
+				if(laneId() == 0) b = atomicAdd(A.next, (uint32_t)kPathBatch);
+				b = __shfl(b, 0);
+				pool = min(b, A.n);
+				pool_end = (uint32_t)min((uint64_t)b + kPathBatch, (uint64_t)A.n);
+				if(pool == pool_end) exhausted = true;
+			}
+			const uint32_t avail = pool_end - pool;
+			const uint32_t rank = (uint32_t)__popcll(need & ((1ull << laneId()) - 1ull));
+			if(!active && rank < avail)
+			{
+				sid = pool + rank;
+				sc = sampleAt(S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
+				uint32_t seed;
+				cameraRay(S, sc, ray_o, ray_d, ray_tmin, ray_tmax, seed);
+				offset = fnv32((uint32_t)(sc.y + S.crop_y0) * fnv32((uint32_t)(sc.x + S.crop_x0)));
+				sample_idx = S.base_offset + S.pass_offset + (uint32_t)sc.s;
+				rng = make_uint2(30903u, seed);
+				stage = ST_CAMERA;
+				flags = 0;
+				w = 0.f;
+				thr = col = pcol = c3(0.f);
+				active = true;
+			}
+			pool += min(avail, (uint32_t)__popcll(need));
+		}
+		if(!__any(active))
+		{
+			if(exhausted) break;
+			continue;
+		}
+		PHASE(0);
+		const bool live = active;
+		const uint32_t st = stage & 0xffu;
+		uint32_t subpath = (stage >> 8) & 0xfffu;
+		int depth = (int)(stage >> 20);
+
+		// ---- the rays this sample owes: the last NEE's shadow rays + the closest ray (k_trace) ----
+		float hit_t = 0.f;
+		int hit_prim = -1;
+		{
+			const bool sh = live && (flags & (F_PEND_V0 | F_PEND_ONE)) != 0;
+			const bool cl = live && st != ST_NORAY;
+			if(__any(sh || cl))
+				traceLaneRays<STATS>(C, rec, occ, K, sh, cl, ray_o, ray_d, ray_tmin, ray_tmax >= 0.f ? ray_tmax : inf, hit_t, hit_prim, visits, tests,
+				                     n_closest, n_shadow);
+		}
+		if(live) ++n_vert;
+		PHASE(1);
+
+		// ---- 1. connect the pending next-event estimate (k_shade step 1) ----
+		if(live && (flags & F_PEND_V0))
+		{
+			C3 total = c3(0.f);
+			for(int l = 0; l < S.n_lights; ++l) total = total + neeSum(S, S.lights[l], nee, occ, (int)S.lights[l].nee_base);
+			col = col + total;
+		}
+		if(live && (flags & F_PEND_ONE))
+		{
+			const int lnum = (int)(flags >> F_LNUM_SHIFT);
+			C3 lcol = neeSum(S, S.lights[lnum], nee, occ, 0) * (float)S.n_lights;
+			if(flags & F_PEND_EMIT) lcol = lcol + pem;
+			pcol = pcol + lcol * pthr;
+		}
+		flags &= ~(F_PEND_V0 | F_PEND_ONE | F_PEND_EMIT | F_AO_EMIT);
+
+		// ---- 2. the new hit ----
+		Surf sp;
+		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
+		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
+		V3 wo = v3(0.f, 0.f, 1.f);
+		bool have_hit = false;
+		if(live && st != ST_NORAY && hit_prim >= 0)
+		{
+			have_hit = true;
+			sp = makeSurf(S, ray_o, ray_d, hit_t, hit_prim);
+			wo = -ray_d;
+		}
+		bool nee_v0 = false, nee_one = false, sample_next = false, end_sub = false, finalize = false, start_sub = false;
+		C3 emit_pend = c3(0.f), pend_thr = c3(0.f);
+		if(live)
+		{
+			if(st == ST_NORAY) end_sub = true;
+			else if(st == ST_CAMERA)
+			{
+				if(!have_hit)
+				{
+					// integrator_tiled.cc:707-720 background
+					C3 bg = c3(0.f);
+					float a = 1.f;
+					if(S.bg_transp) a = 0.f;
+					else if(S.has_bg) bg = C3{S.bg[0], S.bg[1], S.bg[2]};
+					A.samples[((size_t)sc.y * S.width + sc.x) * S.spp + sc.s] = f4(bg, a);
+				}
+				else
+				{
+					const DevMaterial &m = S.mats[sp.mat];
+					col = c3(0.f);
+					if(sp.flags & B_EMIT) col = col + matEmit<false>(m, sp, wo);
+					if(sp.flags & B_DIFFUSE) { nee_v0 = true; flags |= F_V0_DIFFUSE; }
+					if(is_path && (sp.flags & B_DIFFUSE))
+					{
+						v0p4 = f4(sp.p, __int_as_float(hit_prim));
+						v0wo4 = f4(wo, 0.f);
+						start_sub = true;
+						subpath = 0;
+					}
+					else end_sub = true;
+				}
+			}
+			else if(st == ST_FIRST)
+			{
+				if(!have_hit) end_sub = true;     // path_tracer.cc:192 `continue`
+				else
+				{
+					// path_tracer.cc:193-207
+					if(flags & F_SAMPLED) pwo = wo;
+					else wo = pwo;
+					nee_one = true;
+					flags = (flags & ~F_MATFLAGS) | (sp.flags & F_MATFLAGS);
+					if(sp.flags & B_EMIT) { emit_pend = matEmit<false>(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
+					pend_thr = thr;
+					depth = 1;
+					sample_next = true;
+				}
+			}
+			else   // ST_BOUNCE
+			{
+				if(!have_hit) end_sub = true;     // path_tracer.cc:235
+				else
+				{
+					const uint32_t mfl = flags & F_MATFLAGS;
+					pwo = wo;
+					bool killed = false;
+					if(depth > S.rr_min_bounces)
+					{
+						// path_tracer.cc:249-255
+						Mwc g{rng.x, rng.y};
+						const float random_value = (float)g.next();
+						rng = make_uint2(g.x, g.c);
+						const float probability = maxComp(thr);
+						if(probability <= 0.f || probability < random_value) killed = true;
+						else thr = thr * rcpExact(probability);
+					}
+					if(killed) end_sub = true;
+					else
+					{
+						if((mfl & B_EMIT) && (flags & F_CAUSTIC)) { emit_pend = matEmit<false>(S.mats[sp.mat], sp, wo); flags |= F_PEND_EMIT; }
+						if(mfl & B_DIFFUSE) { nee_one = true; pend_thr = thr; }
+						else
+						{
+							C3 lcol = c3(0.f);
+							if(flags & F_PEND_EMIT) lcol = lcol + emit_pend;
+							pcol = pcol + lcol * thr;
+							flags &= ~F_PEND_EMIT;
+						}
+						++depth;
+						sample_next = true;
+					}
+				}
+			}
+		}
+		uint32_t lnum = 0;
+		if(nee_one)
+		{
+			// integrator_montecarlo.cc:70-78 light pick (per-sample counter, as k_shade)
+			if(S.n_lights > 1)
+			{
+				const uint32_t corr = (uint32_t)depth + subpath * (uint32_t)S.bounces;
+				const float hv = haltonFirst(2u, 0.5, S.base_offset + corr - 1u);
+				lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
+			}
+			flags = (flags & ((1u << F_LNUM_SHIFT) - 1u)) | (lnum << F_LNUM_SHIFT) | F_PEND_ONE;
+		}
+		if(nee_v0) flags |= F_PEND_V0;
+		const bool pending = (flags & (F_PEND_V0 | F_PEND_ONE)) != 0;
+
+		PHASE(2);
+		// ---- 3. next segment: one material sample per lane (k_shade's two sampling sites merged) ----
+		bool want_ray = false;
+		V3 nray_o = v3(0.f, 0.f, 0.f), nray_d = v3(0.f, 0.f, 1.f);
+		const bool try_next = live && sample_next && depth < S.bounces;
+		if(live && sample_next && !try_next) end_sub = true;
+		// the end of a subpath known before sampling: next subpath (path_tracer.cc:166) or the end
+		if(live && !try_next && end_sub && !pending)
+		{
+			if(is_path && (flags & F_V0_DIFFUSE) && subpath + 1 < n_paths) { start_sub = true; ++subpath; }
+			else finalize = true;
+		}
+		for(int pass = 0; pass < 2; ++pass)
+		{
+			// pass 0: the continuing lanes (path_tracer.cc:211-234, loop iteration `depth`) and the lanes
+			// starting a subpath (:168-191); pass 1: the lanes whose continuation drew nothing and start
+			// their next subpath (path_samples > 1)
+			const bool smp = pass == 0 ? (try_next || (live && start_sub)) : (live && start_sub);
+			if(!__any(smp)) continue;
+			const bool cont = pass == 0 && try_next;
+			Surf ss = sp;
+			V3 wos = wo;
+			const uint32_t offs = n_paths * sample_idx + offset + subpath;
+			BsdfSample s;
+			s.pdf = 0.f;
+			s.sampled = B_NONE;
+			if(cont)
+			{
+				const int d_4 = 4 * depth;
+				s.s_1 = ldsDim(S, d_4 + 3, offs);
+				s.s_2 = ldsDim(S, d_4 + 4, offs);
+				s.flags = B_ALL;
+			}
+			else
+			{
+				if(st != ST_CAMERA && smp) ss = surfFromPrim(S, xyz(v0p4), __float_as_int(v0p4.w));
+				if(st != ST_CAMERA) wos = xyz(v0wo4);
+				s.s_1 = riVdC(offs);
+				s.s_2 = ldsDim(S, 2, offs);
+				s.flags = B_DIFFUSE | B_REFLECT | B_TRANSMIT;
+			}
+			V3 dir = v3(0.f, 0.f, 0.f);
+			float wnew = w;
+			C3 scol = c3(0.f);
+			if(smp) scol = matSample<false>(S.mats[ss.mat], ss, wos, dir, s, wnew);
+			if(smp) w = wnew;
+			if(cont)
+			{
+				scol = scol * w;
+				if(isBlack(scol)) end_sub = true;
+				else
+				{
+					thr = thr * scol;
+					if(S.caustic_path && (s.sampled & (B_SPECULAR | B_GLOSSY | B_FILTER))) flags |= F_CAUSTIC;
+					else flags &= ~F_CAUSTIC;
+					nray_o = sp.p;
+					nray_d = dir;
+					want_ray = true;
+					stage = ST_BOUNCE | (subpath << 8) | ((uint32_t)depth << 20);
+				}
+			}
+			else if(smp)
+			{
+				thr = scol * w;
+				pwo = wos;
+				if(s.sampled != B_NONE) flags |= F_SAMPLED;
+				else flags &= ~F_SAMPLED;
+				flags &= ~F_CAUSTIC;
+				nray_o = ss.p;
+				nray_d = dir;
+				want_ray = true;
+				stage = ST_FIRST | (subpath << 8);
+			}
+			if(pass == 0)
+			{
+				start_sub = false;
+				if(cont && end_sub && !pending)
+				{
+					if(is_path && (flags & F_V0_DIFFUSE) && subpath + 1 < n_paths) { start_sub = true; ++subpath; }
+					else finalize = true;
+				}
+			}
+		}
+		PHASE(3);
+		if(live && finalize)
+		{
+			// path_tracer.cc:274-278 / direct_light.cc:129-131
+			if(is_path && (flags & F_V0_DIFFUSE)) col = col + pcol / (float)n_paths;
+			col = col + c3(0.f);   // recursiveRaytrace: no specular/glossy component
+			A.samples[((size_t)sc.y * S.width + sc.x) * S.spp + sc.s] = f4(col, 1.f);
+		}
+		// ---- 4. the sample goes on (k_shade's compaction) ----
+		active = live && (want_ray || pending);
+		if(active)
+		{
+			if(want_ray)
+			{
+				ray_o = nray_o;
+				ray_d = nray_d;
+				ray_tmin = S.ray_min_dist;
+				ray_tmax = -1.f;
+			}
+			else stage = ST_NORAY | (subpath << 8) | ((uint32_t)depth << 20);
+			if(nee_one) pthr = pend_thr;
+			if(flags & F_PEND_EMIT) pem = emit_pend;
+		}
+
+		PHASE(4);
+		// ---- 5. next-event estimation (k_nee): contributions into LDS, shadow rays recorded for the
+		// next trip's trace ----
+		const bool all = live && nee_v0, one = live && nee_one;
+		if(__any(all || one))
+		{
+			if(all || one)
+				for(int e = 0; e < K; ++e) rec[2 * e + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+			const DevMaterial &m = S.mats[sp.mat];
+			// estimateAllDirectLight (montecarlo.cc:54-68: every light, at its nee_base) and
+			// estimateOneDirectLight (:70-78: light `lnum`, at 0) in one pass over the lights
+			for(int l = 0; l < S.n_lights; ++l)
+			{
+				const bool mine = all || (one && lnum == (uint32_t)l);
+				if(!__any(mine)) continue;
+				neeLight<false>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, mine, all ? (int)S.lights[l].nee_base : 0, nee, occ, out);
+			}
+			if(all || one) ++n_nee;
+		}
+		PHASE(5);
+	}
+	PHASE_FLUSH;
+	// statistics: the wave sums, one read-modify-write per workgroup into its own record
+	for(int off = 32; off > 0; off >>= 1)
+	{
+		n_closest += __shfl_down(n_closest, off);
+		n_shadow += __shfl_down(n_shadow, off);
+		n_vert += __shfl_down(n_vert, off);
+		n_nee += __shfl_down(n_nee, off);
+		visits += __shfl_down(visits, off);
+		tests += __shfl_down(tests, off);
+	}
+	__shared__ uint32_t red[kTraceBlock / 64][6];
+	const int wid = threadIdx.x >> 6;
+	if(laneId() == 0)
+	{
+		red[wid][0] = n_closest; red[wid][1] = n_shadow; red[wid][2] = visits;
+		red[wid][3] = tests; red[wid][4] = n_vert; red[wid][5] = n_nee;
+	}
+	__syncthreads();
+	if(threadIdx.x < 6 && S.stats)
+	{
+		unsigned long long v = 0;
+		for(int k = 0; k < kTraceBlock / 64; ++k) v += red[k][threadIdx.x];
+		unsigned long long *r = &S.stats[blockIdx.x].closest_rays;   // closest, shadow, visits, tests, shade entries, NEE requests
+		if(v) r[threadIdx.x] += v;
 	}
 }
 
@@ -4249,6 +4856,13 @@ int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds)
 	return e == hipSuccess ? nb : 0;
 }
 
+int yafamd_path_blocks_per_cu(const DevScene *S, int stack_depth)
+{
+	int nb = 0;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path<false>, kTraceBlock, pathLdsBytes(*S, stack_depth)) != hipSuccess) nb = 0;
+	return nb;
+}
+
 int yafamd_nee_blocks_per_cu()
 {
 	int nb = 0;
@@ -4389,6 +5003,37 @@ hipError_t yafamd_launch_surface(const DevScene *S, const DevQueues *Q, const De
 hipError_t yafamd_launch_tshadow(const DevScene *S, const DevQueues *Q, const DevCounters *cnt, const DevPaths *P, hipStream_t st)
 {
 	hipLaunchKernelGGL(k_tshadow, dim3(S->n_seg), dim3(kShadeBlock), 0, st, *S, *Q, *cnt, *P);
+	return hipGetLastError();
+}
+
+// k_path (megakernel) for one chunk of n samples; `next` = a zeroed device counter.  Returns
+// hipErrorInvalidValue when the scene is not eligible (yafamd_path_eligible).
+int yafamd_path_eligible(const DevScene *S, int stack_depth, int spill)
+{
+	return (!S->ext && !S->tree && !S->tr_shad && !S->has_attr && !S->do_ao && !S->gather_on && !S->caus_map && S->integrator != INT_PHOTON &&
+	        S->scene_in_lds && S->node_f4 == 8 && !spill && S->small_tables && S->nee_k >= 1 && S->nee_k <= kPathMaxK && !S->brute &&
+	        pathLdsBytes(*S, stack_depth) <= 64 * 1024)
+	           ? 1
+	           : 0;
+}
+
+hipError_t yafamd_launch_path(const DevScene *S, float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, uint32_t n,
+                              uint32_t *next, int stack_depth, int grid, hipStream_t st)
+{
+	if(!yafamd_path_eligible(S, stack_depth, 0)) return hipErrorInvalidValue;
+	if(n == 0) return hipSuccess;
+	PathArgs A;
+	A.S = *S;
+	A.samples = samples;
+	A.jobs = jobs;
+	A.n_jobs = n_jobs;
+	A.chunk_base = chunk_base;
+	A.n = n;
+	A.next = next;
+	A.stack_depth = stack_depth;
+	const size_t lds = pathLdsBytes(*S, stack_depth);
+	if(S->trace_stats) hipLaunchKernelGGL(k_path<true>, dim3(grid), dim3(kTraceBlock), lds, st, A);
+	else hipLaunchKernelGGL(k_path<false>, dim3(grid), dim3(kTraceBlock), lds, st, A);
 	return hipGetLastError();
 }
 

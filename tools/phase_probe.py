@@ -1,4 +1,4 @@
-"""Phase breakdown of k_shade (diagnostic build with -DYAF_PHASE_TIMING).
+"""Phase breakdown of k_shade (or, with YAFARAY_AMD_PATH=mega, k_path) — diagnostic build with -DYAF_PHASE_TIMING.
 
     YAFARAY_AMD_LIB=libyafaray_amd/variants/phase.so python tools/phase_probe.py [W H SPP]
 """
@@ -20,7 +20,8 @@ Y.render_spec(spec)                      # warm-up
 L.yafaray_amd_getPhaseCycles(buf, 16, 1)
 _, _, st = Y.render_spec(spec)
 n = L.yafaray_amd_getPhaseCycles(buf, 16, 1)
-names = ["load", "connect", "hit", "next-seg", "compact+write", "nee"]
+names = (["refill+camera", "trace", "connect+hit", "next-seg", "finalize+keep", "nee"] if os.environ.get("YAFARAY_AMD_PATH") == "mega"
+         else ["load", "connect", "hit", "next-seg", "compact+write", "nee"])   # k_path / k_shade phases
 tot = sum(buf[k] for k in range(6))
 print(f"render {st['render_seconds'] * 1e3:.1f} ms; phase counters: {n}")
 for k, nm in enumerate(names):
