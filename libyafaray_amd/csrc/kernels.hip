@@ -566,6 +566,13 @@ __device__ __forceinline__ void cswap(float &ka, int &va, float &kb, int &vb)
 	va = v;
 }
 
+// Near / far planes of a BVH4 node's boxes for one ray.  By the sign of the inverse direction the
+// slab's entry plane is the low bound (1/d >= 0) or the high one for every box, and fma(b, 1/d, -o/d)
+// is monotone in b, so max(near distances) / min(far distances) are exactly the values of the
+// per-child min / max over both planes — 4 x 6 fewer min / max per visit for six per-lane addresses.
+struct SlabSel { int nx, ny, nz; };   // float4 index in the node of the near plane per axis (far: ^ 1)
+__device__ __forceinline__ SlabSel slabSel(V3 id) { return SlabSel{id.x >= 0.f ? 0 : 1, id.y >= 0.f ? 2 : 3, id.z >= 0.f ? 4 : 5}; }
+
 // BVH4 (bvh.cc: collapsed binary SAH tree, 128 B nodes with the four child boxes in SoA form).
 // Same hit semantics as traverse2: leaf children are tested as soon as their box is hit, inner
 // children are sorted by entry distance (5-exchange network) and descended nearest-first.
@@ -582,6 +589,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	// slab distances as fma(bound, 1/d, -o/d): the rounding of o/d is covered by the boxes' build-time
 	// padding (mag * 1e-5, bvh.cc padBox) as the rounding of (bound - o) is
 	const V3 oid = v3(o.x * id.x, o.y * id.y, o.z * id.z);
+	const SlabSel sel = slabSel(id);
 	const float box_t0 = ANY ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
 	const float inf = __builtin_huge_valf();
 	const uint32_t glane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -598,7 +606,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	{
 		if(STATS) TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 8 * node;
-		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
+		const float4 nx = np[sel.nx], fx = np[sel.nx ^ 1], ny = np[sel.ny], fy = np[sel.ny ^ 1], nz = np[sel.nz], fz = np[sel.nz ^ 1], cf = np[6], kf = np[7];
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
 		float key[4];
 		int child[4], count[4];
@@ -607,11 +615,10 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 #pragma unroll
 		for(int k = 0; k < 4; ++k)
 		{
-			const float ax = __builtin_fmaf(lane4(lx, k), id.x, -oid.x), bx = __builtin_fmaf(lane4(hx, k), id.x, -oid.x);
-			const float ay = __builtin_fmaf(lane4(ly, k), id.y, -oid.y), by = __builtin_fmaf(lane4(hy, k), id.y, -oid.y);
-			const float az = __builtin_fmaf(lane4(lz, k), id.z, -oid.z), bz = __builtin_fmaf(lane4(hz, k), id.z, -oid.z);
-			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
-			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
+			const float lo = fmaxf(fmaxf(__builtin_fmaf(lane4(nx, k), id.x, -oid.x), __builtin_fmaf(lane4(ny, k), id.y, -oid.y)),
+			                       fmaxf(__builtin_fmaf(lane4(nz, k), id.z, -oid.z), box_t0));
+			const float hi = fminf(fminf(__builtin_fmaf(lane4(fx, k), id.x, -oid.x), __builtin_fmaf(lane4(fy, k), id.y, -oid.y)),
+			                       fminf(__builtin_fmaf(lane4(fz, k), id.z, -oid.z), slack_t));
 			// selects, not branches: a lane-varying `if` here costs an exec-mask save / restore per child
 			const uint32_t h = lo <= hi ? 1u : 0u;
 			child[k] = __float_as_int(lane4(cf, k));
@@ -695,6 +702,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 	const uint32_t glane = blockIdx.x * blockDim.x + threadIdx.x;
 	const float inf = __builtin_huge_valf();
 	V3 o = v3(0.f, 0.f, 0.f), d = o, id = o, oid = o;
+	SlabSel sel{0, 2, 4};
 	float tmin = 0.f, tmax = 0.f, box_t0 = 0.f, t_best = 0.f;
 	int prim_best = -1, sp = 0, node = -1;
 	bool any = false;
@@ -746,6 +754,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 			if(fabsf(dq.z) < 1e-20f) dq.z = copysignf(1e-20f, dq.z);
 			id = v3(rcpExact(dq.x), rcpExact(dq.y), rcpExact(dq.z));
 			oid = v3(o.x * id.x, o.y * id.y, o.z * id.z);
+			sel = slabSel(id);
 			box_t0 = any ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
 			t_best = tmax;
 			prim_best = -1;
@@ -754,7 +763,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 		}
 		if(STATS) TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 8 * node;
-		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
+		const float4 nx = np[sel.nx], fx = np[sel.nx ^ 1], ny = np[sel.ny], fy = np[sel.ny ^ 1], nz = np[sel.nz], fz = np[sel.nz ^ 1], cf = np[6], kf = np[7];
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
 		float key[4];
 		int child[4], e[4], s4[4];
@@ -762,11 +771,10 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 #pragma unroll
 		for(int k = 0; k < 4; ++k)
 		{
-			const float ax = __builtin_fmaf(lane4(lx, k), id.x, -oid.x), bx = __builtin_fmaf(lane4(hx, k), id.x, -oid.x);
-			const float ay = __builtin_fmaf(lane4(ly, k), id.y, -oid.y), by = __builtin_fmaf(lane4(hy, k), id.y, -oid.y);
-			const float az = __builtin_fmaf(lane4(lz, k), id.z, -oid.z), bz = __builtin_fmaf(lane4(hz, k), id.z, -oid.z);
-			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
-			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
+			const float lo = fmaxf(fmaxf(__builtin_fmaf(lane4(nx, k), id.x, -oid.x), __builtin_fmaf(lane4(ny, k), id.y, -oid.y)),
+			                       fmaxf(__builtin_fmaf(lane4(nz, k), id.z, -oid.z), box_t0));
+			const float hi = fminf(fminf(__builtin_fmaf(lane4(fx, k), id.x, -oid.x), __builtin_fmaf(lane4(fy, k), id.y, -oid.y)),
+			                       fminf(__builtin_fmaf(lane4(fz, k), id.z, -oid.z), slack_t));
 			const uint32_t h = lo <= hi ? 1u : 0u;
 			child[k] = __float_as_int(lane4(cf, k));
 			const int count = __float_as_int(lane4(kf, k));
@@ -2820,6 +2828,7 @@ __device__ __forceinline__ void traceLaneRays(const TraceCtx &C, const float4 *r
 	const int lane = threadIdx.x;
 	const float inf = __builtin_huge_valf();
 	V3 o = v3(0.f, 0.f, 0.f), d = o, id = o, oid = o;
+	SlabSel sel{0, 2, 4};
 	float tmax = 0.f, tmin = 0.f, box_t0 = 0.f, t_best = 0.f;
 	int prim_best = -1, sp = 0, node = -1, cur = 0;
 	int e = shadows ? 0 : K;
@@ -2864,6 +2873,7 @@ __device__ __forceinline__ void traceLaneRays(const TraceCtx &C, const float4 *r
 			if(fabsf(dq.z) < 1e-20f) dq.z = copysignf(1e-20f, dq.z);
 			id = v3(rcpExact(dq.x), rcpExact(dq.y), rcpExact(dq.z));
 			oid = v3(o.x * id.x, o.y * id.y, o.z * id.z);
+			sel = slabSel(id);
 			box_t0 = any ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
 			t_best = tmax;
 			prim_best = -1;
@@ -2872,7 +2882,7 @@ __device__ __forceinline__ void traceLaneRays(const TraceCtx &C, const float4 *r
 		}
 		if(STATS) TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 8 * node;
-		const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5], cf = np[6], kf = np[7];
+		const float4 nx = np[sel.nx], fx = np[sel.nx ^ 1], ny = np[sel.ny], fy = np[sel.ny ^ 1], nz = np[sel.nz], fz = np[sel.nz ^ 1], cf = np[6], kf = np[7];
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
 		float key[4];
 		int child[4], e4[4], s4[4];
@@ -2880,11 +2890,10 @@ __device__ __forceinline__ void traceLaneRays(const TraceCtx &C, const float4 *r
 #pragma unroll
 		for(int k = 0; k < 4; ++k)
 		{
-			const float ax = __builtin_fmaf(lane4(lx, k), id.x, -oid.x), bx = __builtin_fmaf(lane4(hx, k), id.x, -oid.x);
-			const float ay = __builtin_fmaf(lane4(ly, k), id.y, -oid.y), by = __builtin_fmaf(lane4(hy, k), id.y, -oid.y);
-			const float az = __builtin_fmaf(lane4(lz, k), id.z, -oid.z), bz = __builtin_fmaf(lane4(hz, k), id.z, -oid.z);
-			const float lo = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), box_t0));
-			const float hi = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), slack_t));
+			const float lo = fmaxf(fmaxf(__builtin_fmaf(lane4(nx, k), id.x, -oid.x), __builtin_fmaf(lane4(ny, k), id.y, -oid.y)),
+			                       fmaxf(__builtin_fmaf(lane4(nz, k), id.z, -oid.z), box_t0));
+			const float hi = fminf(fminf(__builtin_fmaf(lane4(fx, k), id.x, -oid.x), __builtin_fmaf(lane4(fy, k), id.y, -oid.y)),
+			                       fminf(__builtin_fmaf(lane4(fz, k), id.z, -oid.z), slack_t));
 			const uint32_t h = lo <= hi ? 1u : 0u;
 			child[k] = __float_as_int(lane4(cf, k));
 			const int count = __float_as_int(lane4(kf, k));
