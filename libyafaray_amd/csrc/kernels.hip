@@ -2680,139 +2680,23 @@ __global__ void __launch_bounds__(kShadeBlock) k_tshadow(DevScene S, DevQueues Q
 	}
 }
 
-struct NeeArgs
-{
-	DevScene S;
-	DevNeeQueue N;
-	DevPaths Pn;
-	DevQueues Qn;
-	DevCounters cnt_next;
-};
-
-#ifndef YAF_NEE_MIN_WAVES
-#define YAF_NEE_MIN_WAVES 4
-#endif
-template<bool SMALL, bool EXT>
-__global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
-{
-	extern __shared__ uint4 shade_smem[];
-	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
-	const bool ATTR = EXT && S.has_attr != 0;
-	// workgroup b serves the NEE requests of segment b, shadow rays go to segment b
-	const uint32_t seg = blockIdx.x;
-	__shared__ uint32_t s_count;
-	if(threadIdx.x == 0) s_count = 0;
-	__syncthreads();
-	ShadeOut out;
-	out.sh_count = &s_count;
-	out.sh_base = seg * S.cap_s;
-	out.Qn = A.Qn;
-	const uint32_t n_req = A.cnt_next.n_nee[seg];
-	const uint32_t a0 = seg * S.cap_a;
-	const int K = S.nee_k;
-	const uint32_t stride = blockDim.x;
-	for(uint32_t base_j = 0; base_j < n_req; base_j += stride)
-	{
-		const bool live = base_j + threadIdx.x < n_req;
-		const uint32_t j = a0 + base_j + threadIdx.x;
-		float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), wk = pp;
-		uint4 pm = make_uint4(0u, 0u, 0u, 0u);
-		if(live)
-		{
-			pp = A.N.p_prim[j];
-			wk = A.N.wo_k[j];
-			pm = A.N.pix_mode[j];
-		}
-		Surf sp;
-		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
-		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
-		if(live) sp = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
-		if(ATTR && live) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
-		const V3 wo = xyz(wk);
-		const int e0 = (int)__float_as_uint(wk.w) * K;
-		const bool all = live && (pm.z & 1u);
-		const bool one = live && !(pm.z & 1u);
-		const uint32_t lnum = pm.z >> 8;
-		if(__any(all))
-		{
-			// estimateAllDirectLight (montecarlo.cc:54-68)
-			for(int l = 0; l < S.n_lights; ++l)
-				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
-				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out, S.tr_shad ? A.Pn.ts : nullptr);
-			if(S.do_ao)
-				aoSamples<EXT>(S, S.mats[sp.mat], sp, wo, pm.y, pm.x, all, e0 + S.nee_all_count, A.Pn.nee, A.Pn.occ, out,
-				               S.tr_shad ? A.Pn.ts : nullptr);
-		}
-		if(__any(one))
-		{
-			// estimateOneDirectLight (montecarlo.cc:70-78), light `lnum`
-			for(int l = 0; l < S.n_lights; ++l)
-			{
-				const bool mine = one && lnum == (uint32_t)l;
-				if(!__any(mine)) continue;
-				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out,
-				              S.tr_shad ? A.Pn.ts : nullptr);
-			}
-		}
-	}
-	__syncthreads();
-	if(threadIdx.x == 0)
-	{
-		A.cnt_next.n_shadow[seg] = s_count;
-		if(S.stats) S.stats[seg].nee_requests += n_req;
-	}
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_path: the megakernel form of the same integrator for scenes that live in LDS.  One lane carries
-// one camera sample through its whole integrate() — k_camera's ray, then per vertex k_trace's
-// closest hit, k_shade's state machine (the compact record's stages, flags and deferred
-// connection) and k_nee's light sampling, whose shadow rays the lane traces in place — and takes the
-// next sample of its wave's pool when the sample is written.  The path state stays in registers and
-// the NEE contributions in LDS, so none of the wavefront's per-vertex HBM traffic (~270 B of state
-// and queues per vertex, ~125 B per NEE request) exists; HBM sees the camera samples' film records
-// only.  Every function on the way is the wavefront's own (cameraRay, traverse4, makeSurf,
-// matSample / matEmit, neeLight, neeSum), called in the same order per sample, so the film is
-// bit-identical to the wavefront's.  Eligible: non-EXT materials, BVH4 scene + stack bound in LDS,
-// PathIntegrator / DirectLight without AO, photon or caustic maps, transparent shadows (render.cc
-// pathEligible).
-// ---------------------------------------------------------------------------------------------
-constexpr int kPathMaxK = 8;        // NEE entries per vertex kept per lane in LDS
-constexpr int kPathBatch = 256;     // samples a wave takes from the chunk counter at a time
-
-struct PathArgs
-{
-	DevScene S;
-	float4 *samples;       // frame sample buffer [(y * W + x) * spp + s]
-	const DevJob *jobs;
-	int n_jobs;
-	uint64_t chunk_base;
-	uint32_t n;            // samples of the chunk
-	uint32_t *next;        // the chunk's sample counter (zero at launch)
-	int stack_depth;       // traversal stack levels (all in LDS)
-};
-
-// k_path's shadow-ray emitter: neeLight's rays are recorded per lane (origin + t_max, direction +
-// want) and traced after the light sampling; lanes that emit nothing leave their cleared records
+// Shadow-ray emitter of k_path and of k_nee's in-place variant: neeLight's rays are recorded per lane
+// (origin + t_max, direction + want; entry idx - base) and traced after the light sampling; lanes
+// that emit nothing leave their cleared records
 struct PathShadows
 {
 	float4 *rec;
+	int base;
 	__device__ __forceinline__ void emit(bool want, V3 o, V3 d, float t_max, float tmin, int idx) const
 	{
 		(void)tmin;   // the origin is already moved (shadowRayOf); the any-hit test starts at 0
 		if(want)
 		{
-			rec[2 * idx] = f4(o, t_max);
-			rec[2 * idx + 1] = f4(d, 1.f);
+			rec[2 * (idx - base)] = f4(o, t_max);
+			rec[2 * (idx - base) + 1] = f4(d, 1.f);
 		}
 	}
 };
-
-__host__ __device__ inline size_t pathLdsBytes(const DevScene &S, int stack_depth)
-{
-	return shadeLdsBytes(S, true) + (size_t)(S.node_f4 * S.n_nodes + 3 * S.n_tris) * 16 + (size_t)stack_depth * kTraceBlock * 4 +
-	       (size_t)kTraceBlock * S.nee_k * (16 + 32) + (((size_t)kTraceBlock * S.nee_k + 15) & ~(size_t)15);
-}
 
 // The rays one k_path lane owes before its next vertex: the shadow rays its last NEE recorded
 // (rec entries with `want`, when `shadows`) and its closest ray (when `closest`).  traceRefill4's
@@ -2820,7 +2704,7 @@ __host__ __device__ inline size_t pathLdsBytes(const DevScene &S, int stack_dept
 // wave runs for its busiest lane's sum of traversals (not one full traversal per ray slot, most of
 // whose lanes would idle: the MIS material-sample shadow ray exists for a few lanes only).  Every ray
 // runs traverse4's exact sequence of visits, culling, leaf order and exits: hits are identical.
-template<bool STATS>
+template<bool STATS, int STRIDE = kTraceBlock>
 __device__ __forceinline__ void traceLaneRays(const TraceCtx &C, const float4 *rec, uint8_t *occ, int K, bool shadows, bool closest, V3 co,
                                               V3 cd, float ctmin, float ctmax, float &hit_t, int &hit_prim, uint32_t &visits,
                                               uint32_t &tests, uint32_t &n_closest, uint32_t &n_shadow)
@@ -2930,14 +2814,14 @@ __device__ __forceinline__ void traceLaneRays(const TraceCtx &C, const float4 *r
 			cswap(key[0], child[0], key[2], child[2]);
 			cswap(key[1], child[1], key[3], child[3]);
 			cswap(key[1], child[1], key[2], child[2]);
-			if(key[3] < inf) { C.stack[sp * kTraceBlock + lane] = child[3]; ++sp; }
-			if(key[2] < inf) { C.stack[sp * kTraceBlock + lane] = child[2]; ++sp; }
-			if(key[1] < inf) { C.stack[sp * kTraceBlock + lane] = child[1]; ++sp; }
+			if(key[3] < inf) { C.stack[sp * STRIDE + lane] = child[3]; ++sp; }
+			if(key[2] < inf) { C.stack[sp * STRIDE + lane] = child[2]; ++sp; }
+			if(key[1] < inf) { C.stack[sp * STRIDE + lane] = child[1]; ++sp; }
 			int next = key[0] < inf ? child[0] : -1;
 			if(next < 0 && sp > 0)
 			{
 				--sp;
-				next = C.stack[sp * kTraceBlock + lane];
+				next = C.stack[sp * STRIDE + lane];
 			}
 			node = next;
 			done = next < 0;
@@ -2953,6 +2837,199 @@ __device__ __forceinline__ void traceLaneRays(const TraceCtx &C, const float4 *r
 			node = -1;
 		}
 	}
+}
+
+struct NeeArgs
+{
+	DevScene S;
+	DevNeeQueue N;
+	DevPaths Pn;
+	DevQueues Qn;
+	DevCounters cnt_next;
+	int stack_depth;     // TR: traversal stack levels (all in LDS)
+};
+
+// k_nee<.., TR = true> (LDS-resident BVH4 scenes without transparent shadows): the shadow rays are
+// traced by the lane that sampled them, right after the light sampling (traceLaneRays over the
+// scene staged in LDS), and the occlusion bytes written in place — the shadow rays never go through
+// HBM (36 B written by k_nee and read back by k_trace per ray) and k_trace traces closest rays only.
+__host__ __device__ inline size_t neeTraceLdsBytes(const DevScene &S, int stack_depth)
+{
+	return shadeLdsBytes(S, true) + (size_t)(S.node_f4 * S.n_nodes + 3 * S.n_tris) * 16 + (size_t)stack_depth * kShadeBlock * 4 +
+	       (size_t)kShadeBlock * S.nee_k * 32;
+}
+
+#ifndef YAF_NEE_MIN_WAVES
+#define YAF_NEE_MIN_WAVES 4
+#endif
+template<bool SMALL, bool EXT, bool TR = false, bool TSTATS = false>
+__global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
+{
+	extern __shared__ uint4 shade_smem[];
+	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
+	const bool ATTR = EXT && S.has_attr != 0;
+	TraceCtx C;
+	float4 *rec = nullptr;
+	if(TR)
+	{
+		float4 *lds_nodes = reinterpret_cast<float4 *>(shade_smem) + shadeLdsBytes(S, SMALL) / 16;
+		float4 *lds_tris = lds_nodes + S.node_f4 * S.n_nodes;
+		int *stack = reinterpret_cast<int *>(lds_tris + 3 * S.n_tris);
+		rec = reinterpret_cast<float4 *>(stack + A.stack_depth * kShadeBlock) + 2 * threadIdx.x * S.nee_k;
+		for(int k = threadIdx.x; k < S.node_f4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = A.S.nodes[k];
+		for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = A.S.tris[k];
+		__syncthreads();
+		C.nodes = lds_nodes;
+		C.tris = lds_tris;
+		C.stack = stack;
+		C.lds_depth = A.stack_depth;
+		C.spill = nullptr;
+		C.spill_stride = 0;
+	}
+	uint32_t n_shadow = 0, n_dummy = 0, visits = 0, tests = 0;
+	// workgroup b serves the NEE requests of segment b, shadow rays go to segment b
+	const uint32_t seg = blockIdx.x;
+	__shared__ uint32_t s_count;
+	if(threadIdx.x == 0) s_count = 0;
+	__syncthreads();
+	ShadeOut out;
+	out.sh_count = &s_count;
+	out.sh_base = seg * S.cap_s;
+	out.Qn = A.Qn;
+	const uint32_t n_req = A.cnt_next.n_nee[seg];
+	const uint32_t a0 = seg * S.cap_a;
+	const int K = S.nee_k;
+	const uint32_t stride = blockDim.x;
+	for(uint32_t base_j = 0; base_j < n_req; base_j += stride)
+	{
+		const bool live = base_j + threadIdx.x < n_req;
+		const uint32_t j = a0 + base_j + threadIdx.x;
+		float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), wk = pp;
+		uint4 pm = make_uint4(0u, 0u, 0u, 0u);
+		if(live)
+		{
+			pp = A.N.p_prim[j];
+			wk = A.N.wo_k[j];
+			pm = A.N.pix_mode[j];
+		}
+		Surf sp;
+		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
+		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
+		if(live) sp = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
+		if(ATTR && live) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
+		const V3 wo = xyz(wk);
+		const int e0 = (int)__float_as_uint(wk.w) * K;
+		const bool all = live && (pm.z & 1u);
+		const bool one = live && !(pm.z & 1u);
+		const uint32_t lnum = pm.z >> 8;
+		if constexpr(TR)
+		{
+			// the same light sampling with the shadow rays recorded in LDS, then traced by this lane
+			// (estimateAllDirectLight at every light's nee_base, estimateOneDirectLight at 0)
+			if(live)
+				for(int e = 0; e < K; ++e) rec[2 * e + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+			const PathShadows rs{rec, e0};
+			for(int l = 0; l < S.n_lights; ++l)
+			{
+				const bool mine = all || (one && lnum == (uint32_t)l);
+				if(!__any(mine)) continue;
+				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0 + (all ? (int)S.lights[l].nee_base : 0),
+				              A.Pn.nee, A.Pn.occ, rs);
+			}
+			float t_dummy;
+			int p_dummy;
+			if(__any(live))
+				traceLaneRays<TSTATS, kShadeBlock>(C, rec, A.Pn.occ + e0, K, live, false, v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 1.f), 0.f, 0.f, t_dummy,
+				                                  p_dummy, visits, tests, n_dummy, n_shadow);
+			continue;
+		}
+		if(__any(all))
+		{
+			// estimateAllDirectLight (montecarlo.cc:54-68)
+			for(int l = 0; l < S.n_lights; ++l)
+				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
+				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out, S.tr_shad ? A.Pn.ts : nullptr);
+			if(S.do_ao)
+				aoSamples<EXT>(S, S.mats[sp.mat], sp, wo, pm.y, pm.x, all, e0 + S.nee_all_count, A.Pn.nee, A.Pn.occ, out,
+				               S.tr_shad ? A.Pn.ts : nullptr);
+		}
+		if(__any(one))
+		{
+			// estimateOneDirectLight (montecarlo.cc:70-78), light `lnum`
+			for(int l = 0; l < S.n_lights; ++l)
+			{
+				const bool mine = one && lnum == (uint32_t)l;
+				if(!__any(mine)) continue;
+				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out,
+				              S.tr_shad ? A.Pn.ts : nullptr);
+			}
+		}
+	}
+	if(TR)
+	{
+		// the in-place shadow rays join the frame's ray count (k_trace counts the queued ones)
+		for(int off = 32; off > 0; off >>= 1) n_shadow += __shfl_down(n_shadow, off);
+		if(laneId() == 0 && n_shadow) atomicAdd(&s_count, n_shadow);
+	}
+	__syncthreads();
+	if(threadIdx.x == 0)
+	{
+		A.cnt_next.n_shadow[seg] = TR ? 0u : s_count;
+		if(S.stats)
+		{
+			S.stats[seg].nee_requests += n_req;
+			if(TR) S.stats[seg].shadow_rays += s_count;
+		}
+	}
+	if(TR && TSTATS && S.stats)
+	{
+		// per-visit counters of the in-place shadow rays (the statistics frame only)
+		for(int off = 32; off > 0; off >>= 1)
+		{
+			visits += __shfl_down(visits, off);
+			tests += __shfl_down(tests, off);
+		}
+		if(laneId() == 0)
+		{
+			atomicAdd(&S.stats[seg].node_visits, (unsigned long long)visits);
+			atomicAdd(&S.stats[seg].tri_tests, (unsigned long long)tests);
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_path: the megakernel form of the same integrator for scenes that live in LDS.  One lane carries
+// one camera sample through its whole integrate() — k_camera's ray, then per vertex k_trace's
+// closest hit, k_shade's state machine (the compact record's stages, flags and deferred
+// connection) and k_nee's light sampling, whose shadow rays the lane traces in place — and takes the
+// next sample of its wave's pool when the sample is written.  The path state stays in registers and
+// the NEE contributions in LDS, so none of the wavefront's per-vertex HBM traffic (~270 B of state
+// and queues per vertex, ~125 B per NEE request) exists; HBM sees the camera samples' film records
+// only.  Every function on the way is the wavefront's own (cameraRay, traverse4, makeSurf,
+// matSample / matEmit, neeLight, neeSum), called in the same order per sample, so the film is
+// bit-identical to the wavefront's.  Eligible: non-EXT materials, BVH4 scene + stack bound in LDS,
+// PathIntegrator / DirectLight without AO, photon or caustic maps, transparent shadows (render.cc
+// pathEligible).
+// ---------------------------------------------------------------------------------------------
+constexpr int kPathMaxK = 8;        // NEE entries per vertex kept per lane in LDS
+constexpr int kPathBatch = 256;     // samples a wave takes from the chunk counter at a time
+
+struct PathArgs
+{
+	DevScene S;
+	float4 *samples;       // frame sample buffer [(y * W + x) * spp + s]
+	const DevJob *jobs;
+	int n_jobs;
+	uint64_t chunk_base;
+	uint32_t n;            // samples of the chunk
+	uint32_t *next;        // the chunk's sample counter (zero at launch)
+	int stack_depth;       // traversal stack levels (all in LDS)
+};
+
+__host__ __device__ inline size_t pathLdsBytes(const DevScene &S, int stack_depth)
+{
+	return shadeLdsBytes(S, true) + (size_t)(S.node_f4 * S.n_nodes + 3 * S.n_tris) * 16 + (size_t)stack_depth * kTraceBlock * 4 +
+	       (size_t)kTraceBlock * S.nee_k * (16 + 32) + (((size_t)kTraceBlock * S.nee_k + 15) & ~(size_t)15);
 }
 
 // k_path's register budget: 2 waves per SIMD (<= 256 VGPRs incl. AGPRs; the unconstrained
@@ -2986,7 +3063,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 	float4 *nee = nee_all + lane * K;
 	float4 *rec = rec_all + 2 * lane * K;
 	uint8_t *occ = occ_all + lane * K;
-	const PathShadows out{rec};
+	const PathShadows out{rec, 0};
 	const bool is_path = S.integrator == INT_PATH;
 	const uint32_t n_paths = (uint32_t)max(1, S.path_samples);
 	const float inf = __builtin_huge_valf();
@@ -5046,8 +5123,18 @@ hipError_t yafamd_launch_path(const DevScene *S, float4 *samples, const DevJob *
 	return hipGetLastError();
 }
 
+// k_nee traces its shadow rays in place (TR) for non-EXT LDS-resident BVH4 scenes whose stack bound
+// fits LDS, without transparent shadows (their filter colours need k_tshadow's lists)
+int yafamd_nee_trace_eligible(const DevScene *S, int stack_depth)
+{
+	return (!S->ext && !S->tr_shad && !S->has_attr && S->scene_in_lds && S->node_f4 == 8 && S->small_tables && S->nee_k >= 1 &&
+	        S->nee_k <= kPathMaxK && !S->brute && neeTraceLdsBytes(*S, stack_depth) <= 64 * 1024)
+	           ? 1
+	           : 0;
+}
+
 hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
-                             const DevCounters *cnt_next, hipStream_t st)
+                             const DevCounters *cnt_next, int stack_depth, hipStream_t st)
 {
 	NeeArgs A;
 	A.S = *S;
@@ -5056,6 +5143,13 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	A.Qn = *Qn;
 	A.cnt_next = *cnt_next;
 	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
+	A.stack_depth = stack_depth;
+	if(stack_depth > 0 && yafamd_nee_trace_eligible(S, stack_depth))
+	{
+		if(S->trace_stats) hipLaunchKernelGGL((k_nee<true, false, true, true>), dim3(S->n_seg), dim3(kShadeBlock), neeTraceLdsBytes(*S, stack_depth), st, A);
+		else hipLaunchKernelGGL((k_nee<true, false, true>), dim3(S->n_seg), dim3(kShadeBlock), neeTraceLdsBytes(*S, stack_depth), st, A);
+		return hipGetLastError();
+	}
 	if(S->ext)
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_nee<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);

@@ -43,7 +43,7 @@ int yafamd_path_blocks_per_cu(const DevScene *S, int stack_depth);
 hipError_t yafamd_launch_path(const DevScene *S, float4 *samples, const DevJob *jobs, int n_jobs, uint64_t chunk_base, uint32_t n,
                               uint32_t *next, int stack_depth, int grid, hipStream_t st);
 hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevPaths *Pn, const DevQueues *Qn,
-                             const DevCounters *cnt_next, hipStream_t st);
+                             const DevCounters *cnt_next, int stack_depth, hipStream_t st);
 int yafamd_nee_blocks_per_cu();
 hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, uint32_t h0, uint32_t n_local,
                               int max_bounces, hipStream_t st);
@@ -1539,6 +1539,15 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	}
 	DevStats *dstats = (DevStats *)d.stats.p;
 	S.stats = dstats;
+	// Opt-in YAFARAY_AMD_NEE_TRACE=1: k_nee traces its shadow rays in place for LDS-resident scenes
+	// (kernels.hip k_nee<.., TR>) when the whole stack bound fits LDS.  Measured on C2: k_trace
+	// 26.9 -> 18.2 ms per frame but k_nee 15.1 -> 29.4 ms (the traversal at k_nee's 4 waves / SIMD
+	// instead of k_trace's 8), frame 72.6 -> 79.0 ms — so the shadow rays stay queued for k_trace.
+	int nee_trace_stack = 0;
+	{
+		const char *ne = std::getenv("YAFARAY_AMD_NEE_TRACE");
+		if(ne && std::string(ne) == "1" && d.lds_stack >= d.stack_depth) nee_trace_stack = d.lds_stack;
+	}
 	// The megakernel (k_path, kernels.hip; opt-in YAFARAY_AMD_PATH=mega) for scenes whose BVH, stack
 	// and tables live in LDS and need none of the wavefront-only stages (EXT shading, transparent
 	// shadows, photon maps, AO): one lane per sample, the same functions in the same order, the film
@@ -1610,7 +1619,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			}
 			// NEE requests (none in iteration 1 of photon mapping, whose entries all finish there)
 			if((S.ext || !yafamd_shade_fused()) && !(S.integrator == INT_PHOTON && it == 1))
-				PROF(KK_NEE, yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], d.stream));
+				PROF(KK_NEE, yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], nee_trace_stack, d.stream));
 			// (non-EXT k_shade runs the NEE itself: FUSED)
 			cur ^= 1;
 		}

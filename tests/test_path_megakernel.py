@@ -92,3 +92,26 @@ def test_path_megakernel_not_used_where_ineligible(product):
     os.environ.pop("YAFARAY_AMD_PATH", None)
     _, _, st = product.render_spec(scenes.cornell(32, 24, spp=2, bounces=3), profile=True)
     assert st["kernel_times"].get("k_path", {}).get("launches", 0) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pt_rr_gauss_chunks", "pt_norr_paths2_lsamples2", "direct_light_two_lights", "pt_two_lights"])
+def test_nee_inplace_shadow_rays_equal_queued(product, name):
+    """k_nee<.., TR> (opt-in YAFARAY_AMD_NEE_TRACE=1): the lane that sampled a light traces its shadow
+    rays in place instead of queueing them for k_trace — same occlusion, same film bits, same ray
+    counts."""
+    spec, chunk = CASES[name]
+    old = os.environ.get("YAFARAY_AMD_NEE_TRACE")
+    try:
+        os.environ["YAFARAY_AMD_NEE_TRACE"] = "1"
+        a, w, st = product.render_spec(spec, chunk_slots=chunk, profile=True)
+        os.environ["YAFARAY_AMD_NEE_TRACE"] = "0"
+        b, wb, stb = product.render_spec(spec, chunk_slots=chunk, profile=True)
+    finally:
+        if old is None:
+            os.environ.pop("YAFARAY_AMD_NEE_TRACE", None)
+        else:
+            os.environ["YAFARAY_AMD_NEE_TRACE"] = old
+    assert np.array_equal(w.view(np.uint32), wb.view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert st["closest_rays"] == stb["closest_rays"] and st["shadow_rays"] == stb["shadow_rays"]
