@@ -414,6 +414,26 @@ YD uint32_t fnv32(uint32_t value)
 	return hash;
 }
 
+// The digit weights of halton.h:53-63's loop (factor = 1/B, then factor *= 1/B per digit) as
+// compile-time constants: the same sequence of double roundings, evaluated by the compiler
+template<uint32_t B>
+struct HaltonFactors
+{
+	static constexpr int n = 34;
+	static constexpr int digits = B == 3 ? 21 : B == 5 ? 14 : 32;   // base-B digits of a 32-bit start
+	double f[n];
+	constexpr HaltonFactors() : f()
+	{
+		const double inv = 1.0 / static_cast<double>(B);
+		double x = inv;
+		for(int k = 0; k < n; ++k)
+		{
+			f[k] = x;
+			x *= inv;
+		}
+	}
+};
+
 // Halton(base, start) as a running generator (halton.h:41-81: setStart, then getNext per draw) —
 // for loops that draw consecutive numbers of one sequence (area-light samples, AO samples)
 template<uint32_t B>
@@ -429,13 +449,17 @@ struct HaltonInc
 			value = static_cast<double>(bitReverse32(s)) * 2.3283064365386962890625e-10;
 			return;
 		}
-		double factor = inv_base;
+		// the digit loop unrolled over the constant weights (no running factor product) and run for
+		// every digit position a 32-bit start can have: past the last digit the terms are +0, which
+		// leaves the (non-negative) sum unchanged, so the value is the loop's bit for bit
+		constexpr HaltonFactors<B> F;
+		constexpr int nd = HaltonFactors<B>::digits;
 		value = 0.0;
-		while(s > 0)
+#pragma unroll
+		for(int k = 0; k < nd; ++k)
 		{
-			value += static_cast<double>(s % B) * factor;
+			value += static_cast<double>(s % B) * F.f[k];
 			s /= B;
-			factor *= inv_base;
 		}
 	}
 	YD float next()
