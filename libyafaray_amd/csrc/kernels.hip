@@ -347,12 +347,12 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	cameraRay(S, sc, from, dir, tmin, tmax, seed);
 	// the compact record carries the sample id and the stage in pr (offset / sample index derive
 	// from the sample id); a specular recursion tree keeps them in the queue's slot and col.w
+	// (compact record: the zero throughput, path colour, w and flags of a camera entry are implied by
+	// its stage — k_shade does not read them — so they are not written: 32 B per sample each way)
 	if(!S.tree)
 	{
 		Q.ray_o[a] = f4(from, tmin);
 		Q.ray_d[a] = f4(dir, tmax);
-		P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
-		P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
 		P.pr[a] = make_uint4((uint32_t)i, ST_CAMERA, 30903u, seed);
 	}
 	else
@@ -2075,10 +2075,15 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				col4 = Pc.col[i];
 				stage = __float_as_uint(col4.w);
 			}
-			thr4 = Pc.thr[i];
-			pcol4 = Pc.pcol[i];
-			if(keep_v0) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
-			if(ATTR && keep_v0) { v0a0 = Pc.v0attr[2 * (size_t)i]; v0a1 = Pc.v0attr[2 * (size_t)i + 1]; }
+			// a compact camera entry starts from zero throughput, colour, w and flags (k_camera does not
+			// write them) and has no first-hit data yet
+			if(!compact || (stage & 0xffu) != ST_CAMERA)
+			{
+				thr4 = Pc.thr[i];
+				pcol4 = Pc.pcol[i];
+				if(keep_v0) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
+				if(ATTR && keep_v0) { v0a0 = Pc.v0attr[2 * (size_t)i]; v0a1 = Pc.v0attr[2 * (size_t)i + 1]; }
+			}
 			w = thr4.w;
 			flags = __float_as_uint(pcol4.w);
 			// only the first segment of a subpath reads the previous wo (path_tracer.cc:193-197)
