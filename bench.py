@@ -340,6 +340,16 @@ def dominant_roofline(s, kt, kernels, pmc, scene=None):
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": p.get("hbm_bytes_per_launch"),
             "kernel": kind, "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
             "algo_bytes_per_launch": round(per_launch)}
+    if e.get("traffic_gbs") is not None:
+        # the PMC-measured HBM rate of the same kernel next to the algorithmic one
+        roof["traffic_gbs"] = e["traffic_gbs"]
+        roof["traffic_frac"] = e["traffic_frac"]
+    if kind == "k_shade":
+        roof["model"] = "SURVEY §8d: 64 B of path state per segment"
+        if e.get("traffic_gbs") is not None:
+            roof["limiter"] = (f"HBM: {round(p['hbm_bytes_per_launch'] / max(1, v['items'] / launches))} B per vertex measured "
+                               f"(the wavefront keeps path state, queues and the deferred NEE estimate in HBM between launches; "
+                               f"DESIGN.md §5 byte accounting) at {e['traffic_gbs']} GB/s = {e['traffic_frac']} of peak")
     if kind == "k_trace" and scene in SURVEY_B_RAY:
         # §8d's per-ray model (the reference kd-tree's node / triangle counts) next to our BVH4 bytes
         bc, bs = SURVEY_B_RAY[scene]
