@@ -138,9 +138,9 @@ YD bool safeToRound(double d, float &f)
 	__builtin_memcpy(&b, &f, 4);
 	const int ef = (int)((b >> 23) & 0xffu);
 	if(ef == 0 || ef >= 254) return false;      // zero / subnormal / huge: take the exact path
-	const double ulp = ldexp(1.0, ef - 127 - 23);
 	const double df = (double)f;
-	const double t = fabs(d - df) / ulp;         // in [0, 0.5]
+	// |d - df| in units of the float ulp 2^(ef - 150): an exact power-of-two scaling (no double division)
+	const double t = ldexp(fabs(d - df), 150 - ef);   // in [0, 0.5]
 	const bool low_binade = ((b & 0x7fffffu) == 0) && (fabs(d) < fabs(df));
 	return (low_binade ? 0.25 : 0.5) - t > 1e-6;
 }
