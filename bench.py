@@ -84,7 +84,9 @@ def pmc_config(a, W, H):
 def kernels_src_sha1():
     import hashlib
     h = hashlib.sha1()
-    for f in ("kernels.hip", "pkd.hip", "pkd_kernels.h", "aa.hip"):
+    # every source the profiled device code is compiled from (kernels and the headers they inline)
+    for f in ("kernels.hip", "pkd.hip", "pkd_kernels.h", "aa.hip", "fgthin.hip", "bvhgpu.hip", "devmath.h", "devscene.h", "texeval.h",
+              "photonheap.h"):
         with open(os.path.join(ROOT, "libyafaray_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()

@@ -12,7 +12,6 @@ write / total HBM bytes per launch, and the SQ ratios (VALU lane utilisation, wa
 import collections
 import csv
 import glob
-import hashlib
 import json
 import os
 import re
@@ -27,11 +26,10 @@ PKD = ("k_keys", "k_records", "k_bound", "k_root", "k_level_split", "k_level_par
 
 
 def kernel_src_sha1():
-    h = hashlib.sha1()
-    for f in ("kernels.hip", "pkd.hip", "pkd_kernels.h", "aa.hip"):
-        with open(os.path.join(ROOT, "libyafaray_amd", "csrc", f), "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()
+    # the same key as bench.py kernels_src_sha1 (one definition: bench's)
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.kernels_src_sha1()
 
 
 def kind_of(name, photon):
