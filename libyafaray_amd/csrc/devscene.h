@@ -235,6 +235,8 @@ struct DevScene
 	const float *rph_colb;
 	const uint4 *rpk_nodes;
 	int n_rphotons;
+	int rpk_lds;                   // k_fg: levels of the radiance-map nearest search held in an LDS column (tree depth + 1;
+	                               // 0: the private-array stack)
 
 	// surface attributes and shader nodes: only when some material has nodes or some mesh has
 	// orco / uv / smooth normals (has_attr); k_surface then fills DevQueues::sattr per hit

@@ -4562,6 +4562,66 @@ __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, flo
 	return nearest;
 }
 
+// pkNearest with its far-child stack in an LDS column (4 B per level, stk[level * STRIDE]; cap >= the
+// tree depth, so nothing is dropped): a popped interior node carries its parent's plane (pkd.hip), from
+// which the distance pkNearest stacked is recomputed for its pop-time test; a popped leaf goes to the
+// distance test directly (its photon lies beyond that plane: the two tests agree, as in pkWalk).  Same
+// visits in the same order as pkNearest, so the same nearest photon.
+template<int STRIDE>
+__device__ __forceinline__ int pkNearestLds(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2, uint32_t *stk, int cap)
+{
+	int nearest = -1;
+	uint32_t curr = 0;
+	int sp_top = 0;
+	uint4 nd = nodes[0];
+	for(;;)
+	{
+		while((nd.w & 3u) != 3u)
+		{
+			const int axis = (int)(nd.w & 3u);
+			const float split_val = __uint_as_float(nd.x);
+			const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+			uint32_t far_child;
+			if(pa <= split_val) { far_child = nd.w >> 2; curr = curr + 1; }
+			else { far_child = curr + 1; curr = nd.w >> 2; }
+			float d2 = pa - split_val;
+			d2 *= d2;
+			if(d2 <= max_d2 && sp_top < cap)
+			{
+				stk[sp_top * STRIDE] = far_child;
+				++sp_top;
+			}
+			nd = nodes[curr];
+		}
+		const uint32_t ph = nd.w >> 2;
+		const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
+		const float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
+		if(dist_2 < max_d2)
+		{
+			if(dot(xyz(dirs[ph]), n) > 0.f) { nearest = (int)ph; max_d2 = dist_2; }
+		}
+		bool more = false;
+		while(sp_top > 0)
+		{
+			--sp_top;
+			curr = stk[sp_top * STRIDE];
+			nd = nodes[curr];
+			if((nd.w & 3u) != 3u)
+			{
+				const uint32_t pax = nd.z;
+				const float pa = pax == 0u ? p.x : (pax == 1u ? p.y : p.z);
+				float d2 = pa - __uint_as_float(nd.y);
+				d2 *= d2;
+				if(d2 > max_d2) continue;
+			}
+			more = true;
+			break;
+		}
+		if(!more) break;
+	}
+	return nearest;
+}
+
 // MonteCarloIntegrator::doLightEstimation for one light (integrator_montecarlo.cc:80-408) with the
 // shadow rays traced in place: neeLight's arithmetic, neeSum's addition order.  TSH: transparent
 // shadows (tr_shad_, :112, 206, 330): the surfaces a shadow ray crosses are collected in ts_buf
@@ -4782,6 +4842,13 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 		C.nodes = S.nodes;
 		C.tris = S.tris;
 	}
+	// the radiance-map nearest searches' LDS stack column (S.rpk_lds levels), after the stack and scene
+	uint32_t *nstk = reinterpret_cast<uint32_t *>(smem + (A.stack_depth * kTraceBlock) / 4 +
+	                                              (LDS_SCENE ? S.node_f4 * S.n_nodes + 3 * S.n_tris : 0)) + threadIdx.x;
+	auto nearestRad = [&](V3 hp, V3 sf) -> int {
+		return S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, nstk, S.rpk_lds)
+		                     : pkNearest(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad);
+	};
 	const bool ATTR = EXT && S.has_attr != 0;
 	const SegLoop L = segLoop(S.n_seg);
 	const uint32_t n_req = A.cnt_next.n_gather[L.s];
@@ -4855,7 +4922,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 					else if(caustic)
 					{
 						const V3 sf = faceForward(hit.ng, hit.n, pwo);
-						const int nearest = pkNearest(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad);
+						const int nearest = nearestRad(hit.p, sf);
 						if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
 					}
 					if(close || caustic)
@@ -4888,7 +4955,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 			if(did_hit && (mat_bsd_fs & (B_DIFFUSE | B_GLOSSY)))
 			{
 				const V3 sf = faceForward(hit.ng, hit.n, -dir);
-				const int nearest = pkNearest(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad);
+				const int nearest = nearestRad(hit.p, sf);
 				if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
 				if(mat_bsd_fs & B_EMIT) lcol = lcol + matEmit<EXT>(S.mats[hit.mat], hit, -dir);
 				path_col = path_col + lcol * throughput;
@@ -5346,13 +5413,16 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 	A.stack_depth = stack_depth;
 	A.spill = spill;
 	A.ts_scratch = ts_scratch;
+	// (+ the nearest-search column: S->rpk_lds levels of 4 B per lane, after the stack and scene)
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
+	const size_t nstk_bytes = (size_t)S->rpk_lds * kTraceBlock * sizeof(uint32_t);
 	const bool wide = S->node_f4 == 8;
 	if(S->tr_shad)
 	{
 		// transparent shadows (the spilling variants: without a spill column they never spill)
 		if(!ts_scratch) return hipErrorInvalidValue;
-		const size_t bytes = S->scene_in_lds ? stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) : stack_bytes;
+		const size_t bytes = (S->scene_in_lds ? stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) : stack_bytes) +
+		                     nstk_bytes;
 #define YAF_FG_LAUNCH_TS(L, W, E) hipLaunchKernelGGL((k_fg<L, W, E, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A)
 		if(S->scene_in_lds)
 		{
@@ -5370,7 +5440,7 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 #define YAF_FG_LAUNCH_NS(W, E, B) hipLaunchKernelGGL((k_fg<true, W, E, false>), dim3(grid), dim3(kTraceBlock), B, st, A)
 	if(S->scene_in_lds)
 	{
-		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4);
+		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) + nstk_bytes;
 		if(spill == nullptr)   // the LDS levels hold the whole stack bound: plain LDS pushes / pops
 		{
 			if(S->ext) { if(wide) YAF_FG_LAUNCH_NS(true, true, bytes); else YAF_FG_LAUNCH_NS(false, true, bytes); }
@@ -5381,9 +5451,9 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 		else if(wide) YAF_FG_LAUNCH(true, true, false, bytes);
 		else YAF_FG_LAUNCH(true, false, false, bytes);
 	}
-	else if(S->ext) { if(wide) YAF_FG_LAUNCH(false, true, true, stack_bytes); else YAF_FG_LAUNCH(false, false, true, stack_bytes); }
-	else if(wide) YAF_FG_LAUNCH(false, true, false, stack_bytes);
-	else YAF_FG_LAUNCH(false, false, false, stack_bytes);
+	else if(S->ext) { if(wide) YAF_FG_LAUNCH(false, true, true, stack_bytes + nstk_bytes); else YAF_FG_LAUNCH(false, false, true, stack_bytes + nstk_bytes); }
+	else if(wide) YAF_FG_LAUNCH(false, true, false, stack_bytes + nstk_bytes);
+	else YAF_FG_LAUNCH(false, false, false, stack_bytes + nstk_bytes);
 #undef YAF_FG_LAUNCH
 #undef YAF_FG_LAUNCH_NS
 	return hipGetLastError();

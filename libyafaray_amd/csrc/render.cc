@@ -960,6 +960,9 @@ void GpuRenderer::publishRadianceMap(DevScene &S, const PhotonParams &pm, uint32
 	S.rph_dir = nk ? (const float4 *)d.rph_dir.p : nullptr;
 	S.rph_colb = nk ? (const float *)d.rph_colb.p : nullptr;
 	S.rpk_nodes = nk ? (const uint4 *)d.rpk_nodes.p : nullptr;
+	// k_fg's nearest searches keep their far-child stack in LDS when the tree is shallow enough
+	S.rpk_lds = (nk && d.r_depth + 1 <= 32) ? d.r_depth + 1 : 0;
+	if(const char *e = getenv("YAFARAY_AMD_FG_NEAREST"); e && std::string(e) == "private") S.rpk_lds = 0;
 }
 
 namespace
@@ -1212,6 +1215,7 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	}
 	S.fg_on = 0;
 	S.n_rphotons = 0;
+	S.rpk_lds = 0;
 	if(want_fg && n_diffuse > 0)
 	{
 		if(generate)
@@ -1274,6 +1278,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	S.n_photons = 0;
 	S.fg_on = 0;
 	S.n_rphotons = 0;
+	S.rpk_lds = 0;
 	if(S.integrator == INT_PHOTON || rp.pm.caustic_map)
 	{
 		// PhotonIntegrator::preprocess (integrator_photon_mapping.cc:242-638) / createCausticMap

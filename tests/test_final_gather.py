@@ -158,3 +158,16 @@ def test_final_gather_several_chunks_and_aa_passes(product, oracle_built):
     compare(product, oracle_built, fg_spec(32, 24, spp=2, fg_samples=3), chunk_slots=300)
     spec = fg_spec(32, 24, spp=1, fg_samples=2, aa_passes=2, aa_inc_samples=1, aa_threshold=0.02)
     compare(product, oracle_built, spec)
+
+
+@pytest.mark.gpu
+def test_final_gather_nearest_lds_stack_equals_private(product, monkeypatch):
+    """k_fg's radiance-map nearest searches with the far-child stack in an LDS column (pkNearestLds,
+    the parent plane recomputing the stacked distance) visit what the private-array stack visits:
+    the film is bit-identical."""
+    spec = fg_spec(48, 36, fg_samples=8)
+    a, w, _ = product.render_spec(spec)
+    monkeypatch.setenv("YAFARAY_AMD_FG_NEAREST", "private")
+    b, wb, _ = product.render_spec(spec)
+    assert np.array_equal(w.view(np.uint32), wb.view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
