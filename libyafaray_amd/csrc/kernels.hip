@@ -707,6 +707,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 	int prim_best = -1, sp = 0, node = -1;
 	bool any = false;
 	uint32_t cur = 0;
+	int sh_e = 0;
 	auto push = [&](int v) {
 		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + lane] = v;
 		else if(SPILL) C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane] = v;
@@ -740,6 +741,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 					tmin = 0.f;
 					tmax = dd.w;
 					any = true;
+					sh_e = __float_as_int(od.w);   // the NEE entry (opaque shadows: carried in sh_o.w)
 					++n_shadow;
 				}
 				got = true;
@@ -826,7 +828,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 		}
 		if(done)
 		{
-			if(any) P.occ[Q.sh_idx[s0 + (cur - n_a)]] = prim_best >= 0 ? 1 : 0;   // P = state set of the consumer shade
+			if(any) P.occ[sh_e] = prim_best >= 0 ? 1 : 0;   // P = state set of the consumer shade
 			else
 			{
 				Q.hit_t[a0 + cur] = t_best;
@@ -1005,7 +1007,8 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 				Q.ts_n[k] = occ ? 0 : L.n;
 			}
 			else occ = traverse<true, WIDE, SPILL, false, STATS>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
-			P.occ[Q.sh_idx[k]] = occ ? 1 : 0;   // P = state set of the consumer shade
+			// (opaque shadows: the NEE entry index rides in sh_o.w)
+			P.occ[TS ? Q.sh_idx[k] : __float_as_int(od.w)] = occ ? 1 : 0;   // P = state set of the consumer shade
 			++n_shadow;
 		}
 	};
@@ -1161,7 +1164,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_brute(DevScene S, DevQueu
 			const bool occ = bruteTrace<true>(tris, n_tris, xyz(od), xyz(dd), 0.f, dd.w, t, prim, tests, shadow);
 			if(shadow)
 			{
-				P.occ[Q.sh_idx[k]] = occ ? 1 : 0;   // P = state set of the consumer shade
+				P.occ[__float_as_int(od.w)] = occ ? 1 : 0;   // P = state set of the consumer shade (index in sh_o.w)
 				++n_shadow;
 			}
 		}
@@ -1555,6 +1558,8 @@ struct ShadeOut
 	uint32_t *sh_count;    // shadow-ray counter of the shard
 	uint32_t sh_base;      // first address of the shard's shadow queue
 	DevQueues Qn;
+	bool idx_in_o;         // opaque shadows: the NEE entry index rides in sh_o.w (no sh_idx array traffic);
+	                       // transparent shadows keep tmin there (k_tshadow) and the index in sh_idx
 	__device__ __forceinline__ void emit(bool want, V3 o, V3 d, float t_max, float tmin, int idx) const
 	{
 		emitShadow(want, o, d, t_max, tmin, idx, *this);
@@ -1571,9 +1576,9 @@ __device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, f
 	const uint32_t k = out.sh_base + waveAppend(want, out.sh_count);
 	if(want)
 	{
-		stStore2(&out.Qn.sh_o[k], f4(o, tmin));
+		stStore2(&out.Qn.sh_o[k], f4(o, out.idx_in_o ? __int_as_float(idx) : tmin));
 		stStore2(&out.Qn.sh_d[k], f4(d, t_max));
-		stStore2(&out.Qn.sh_idx[k], idx);
+		if(!out.idx_in_o) stStore2(&out.Qn.sh_idx[k], idx);
 	}
 }
 
@@ -2028,6 +2033,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 	out.sh_count = &s_count[2];
 	out.sh_base = seg * S.cap_s;
 	out.Qn = A.Qn;
+	out.idx_in_o = !S.tr_shad;
 	const bool is_path = S.integrator == INT_PATH;
 	const bool is_photon = S.integrator == INT_PHOTON;
 	// first-hit data carried to the end (the photon-map estimates of k_gather read it)
@@ -2901,6 +2907,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 	out.sh_count = &s_count;
 	out.sh_base = seg * S.cap_s;
 	out.Qn = A.Qn;
+	out.idx_in_o = !S.tr_shad;
 	const uint32_t n_req = A.cnt_next.n_nee[seg];
 	const uint32_t a0 = seg * S.cap_a;
 	const int K = S.nee_k;
