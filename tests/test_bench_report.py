@@ -1,0 +1,68 @@
+"""bench.py's reporting arithmetic on synthetic inputs (no GPU): the per-kernel table and the contract's
+roofline object must never report rates from mismatched frames (a PMC pass that spans two frames
+is per launch, scaled to the launches of one frame), and the dominant kernel's object carries both
+the algorithmic and the measured HBM rate."""
+import types
+
+import bench
+
+
+def _args(scene="cornell"):
+    return types.SimpleNamespace(width=1920, height=1080, spp=64, scene=scene, fg=0)
+
+
+def _stats():
+    return {"closest_rays": 460_000_000, "shadow_rays": 290_000_000, "node_visits": 2_500_000_000, "tri_tests": 2_450_000_000,
+            "bvh_width": 4, "scene_in_lds": 1, "photons": 0}
+
+
+def _kt():
+    # ms per frame, launches per frame, items per frame
+    return {"k_shade": {"ms": 27.0, "launches": 24, "items": 460_000_000},
+            "k_trace": {"ms": 26.5, "launches": 24, "items": 750_000_000},
+            "k_nee": {"ms": 13.7, "launches": 24, "items": 328_000_000},
+            "k_camera": {"ms": 1.0, "launches": 2, "items": 132_710_400},
+            "k_film": {"ms": 1.1, "launches": 1, "items": 132_710_400}}
+
+
+def _pmc():
+    # a PMC pass over two frames: 48 dispatches of the per-iteration kernels, totals twice one frame's
+    per = {"k_shade": 4.66e9, "k_trace": 1.58e9, "k_nee": 1.70e9, "k_camera": 3.18e9, "k_film": 5.5e9}
+    disp = {"k_shade": 48, "k_trace": 48, "k_nee": 48, "k_camera": 4, "k_film": 2}
+    return {"kernels": {k: {"dispatches": disp[k], "hbm_bytes_per_launch": v, "hbm_bytes_total": v * disp[k], "valu_lane_util": 0.5,
+                            "sq_insts_valu_per_launch": 4e8} for k, v in per.items()}}
+
+
+def test_traffic_is_per_frame_even_when_the_pmc_pass_spans_two_frames():
+    a, s, kt = _args(), _stats(), _kt()
+    kernels, frame_ms = bench.kernel_table(a, s, kt, _pmc())
+    assert abs(frame_ms - sum(v["ms"] for v in kt.values())) < 1e-9
+    for k, e in kernels.items():
+        # bytes per frame = per launch x this frame's launches, so the rate is physical (< HBM peak)
+        assert e["traffic_bytes"] == int(_pmc()["kernels"][k]["hbm_bytes_per_launch"] * kt[k]["launches"])
+        assert e["traffic_frac"] < 1.0, (k, e)
+    assert kernels["k_shade"]["algo_bytes_per_item"] == 64.0          # SURVEY §8d path-state model
+
+
+def test_dominant_roofline_reports_algorithmic_and_measured_rates():
+    a, s, kt = _args(), _stats(), _kt()
+    kernels, _ = bench.kernel_table(a, s, kt, _pmc())
+    roof = bench.dominant_roofline(s, kt, kernels, _pmc(), scene="cornell")
+    assert roof["kernel"] == "k_shade" and roof["bound"] == "hbm"
+    assert roof["peak"] == bench.HBM_PEAK_GBS
+    assert abs(roof["frac"] - roof["achieved"] / bench.HBM_PEAK_GBS) < 1e-3
+    assert roof["traffic"] == _pmc()["kernels"]["k_shade"]["hbm_bytes_per_launch"]
+    assert 0.0 < roof["traffic_frac"] < 1.0
+    # measured bytes per vertex in the limiter: 4.66e9 B per launch over 460 M / 24 entries
+    assert "243 B per vertex" in roof["limiter"]
+
+
+def test_dominant_roofline_for_trace_carries_the_survey_model_and_valu_limiter():
+    a, s, kt = _args(), _stats(), _kt()
+    kt["k_trace"]["ms"] = 40.0   # make k_trace the largest kernel
+    kernels, _ = bench.kernel_table(a, s, kt, _pmc())
+    roof = bench.dominant_roofline(s, kt, kernels, _pmc(), scene="cornell")
+    assert roof["kernel"] == "k_trace"
+    assert roof["survey_per_ray_model"]["closest_B"] == 273.0
+    assert roof["traversal"]["served_from"] == "LDS"
+    assert roof["limiter"].startswith("VALU")
