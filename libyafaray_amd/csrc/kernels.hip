@@ -707,7 +707,6 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 	int prim_best = -1, sp = 0, node = -1;
 	bool any = false;
 	uint32_t cur = 0;
-	int sh_e = 0;
 	auto push = [&](int v) {
 		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + lane] = v;
 		else if(SPILL) C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane] = v;
@@ -741,7 +740,6 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 					tmin = 0.f;
 					tmax = dd.w;
 					any = true;
-					sh_e = __float_as_int(od.w);   // the NEE entry (opaque shadows: carried in sh_o.w)
 					++n_shadow;
 				}
 				got = true;
@@ -828,7 +826,9 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 		}
 		if(done)
 		{
-			if(any) P.occ[sh_e] = prim_best >= 0 ? 1 : 0;   // P = state set of the consumer shade
+			// (the NEE entry of an opaque shadow ray rides in sh_o.w: re-read at the end rather than held
+			// in a register through the traversal, which spilled at this kernel's 6-wave budget)
+			if(any) P.occ[__float_as_int(Q.sh_o[s0 + (cur - n_a)].w)] = prim_best >= 0 ? 1 : 0;   // P = state set of the consumer shade
 			else
 			{
 				Q.hit_t[a0 + cur] = t_best;
