@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere", "photon"])
     ap.add_argument("--photons", type=int, default=10_000_000, help="C5: diffuse photons")
     ap.add_argument("--fg", type=int, default=0, help="C5 variant: PhotonIntegrator final gathering with this many fg_samples (0: off, as C5)")
-    ap.add_argument("--chunk", type=int, default=1 << 26)
+    ap.add_argument("--chunk", type=int, default=1 << 27)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size parity checks")
@@ -134,7 +134,9 @@ def algo_bytes(kind, s, kt, in_lds, a):
         # sample (o, d, index 36 B) + contribution (16 B) + occlusion byte
         return 48.0 * it + 53.0 * (s["shadow_rays"] / max(1, s["closest_rays"])) * it
     if kind == "k_camera":
-        return 96.0 * it          # camera ray 32 B + initial path state 64 B (§8d)
+        # camera ray 32 B + the compact record (sample id, stage, MWC) 16 B: a camera entry's zero
+        # throughput / colour / flags are implied by its stage (§8d counted 64 B of initial state)
+        return 48.0 * it
     if kind == "k_film":
         return 16.0 * it + 20.0 * a.width * a.height   # the samples (float4) + RGBA + weight per pixel
     if kind == "k_gather":

@@ -223,7 +223,7 @@ class Scene
 		// explicit device group (yafaray_amd_setDeviceGroup): the device of each member (-1: device of
 		// member 0 + m, modulo the visible devices); empty: the "gpus" render parameter decides
 		std::vector<int> device_group;
-		int chunk_slots = 1 << 26;   // samples in flight per wavefront chunk (64 M: the C2 frame in two chunks)
+		int chunk_slots = 1 << 27;   // samples in flight per wavefront chunk (134 M: the C2 frame in one chunk)
 		bool profile_kernels = false;
 		bool trace_stats = true;   // per-visit node / triangle counters in k_trace (yafaray_amd_setTraceStats)
 		volatile bool canceled = false;

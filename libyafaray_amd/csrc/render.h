@@ -111,7 +111,7 @@ struct RenderParams
 	int shard_mode = 1;   // 0: tile rows r % world == rank, 1: contiguous row band [H rank / world, H (rank + 1) / world),
 	                      // 2: the explicit band [shard_y0, shard_y1) (host-side load balancing)
 	int shard_y0 = 0, shard_y1 = 0;
-	int chunk_slots = 1 << 26;   // samples in flight per wavefront chunk (64 M: the C2 frame in two chunks)
+	int chunk_slots = 1 << 27;   // samples in flight per wavefront chunk (134 M: the C2 frame in one chunk)
 	bool profile = false;
 	// film load/save (filmio.h): accumulators loaded from film files, uploaded before the first pass;
 	// resumed = the first pass renders no samples (integrator_tiled.cc:174-177)
