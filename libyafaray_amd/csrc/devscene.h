@@ -432,6 +432,7 @@ struct GatherLogDesc
 	void *e;
 	uint32_t *n;
 	uint32_t cap, seg_cap, j0;
+	uint32_t split;   // k_gather<REPLAY>: the 6-byte split heap where eligible (YAFARAY_AMD_GATHER_HEAP=packed: 0)
 };
 
 } // namespace yafamd

@@ -4260,7 +4260,40 @@ __global__ void __launch_bounds__(kGatherBlock) __attribute__((amdgpu_waves_per_
 
 __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2);
 
-template<bool SMALL, bool EXT, bool REPLAY = false>
+// PhotonGather (photon.cc:31-52) over one request's accepted photons, in the walk's visit order.
+// POS: the heap keeps the entry's log position (HeapRefSplit), else the photon index.
+template<bool POS, class H>
+__device__ __forceinline__ void replayLog(const H &heap, const uint2 *lg, uint32_t n_acc, int k, int &found, float &max_d2)
+{
+	uint4 pair = make_uint4(0u, 0u, 0u, 0u);
+	for(uint32_t a = 0; a < n_acc; ++a)
+	{
+		if(!(a & 1u)) pair = (a + 1u < n_acc) ? *reinterpret_cast<const uint4 *>(lg + a) : make_uint4(lg[a].x, lg[a].y, 0u, 0u);
+		const uint2 e = (a & 1u) ? make_uint2(pair.z, pair.w) : make_uint2(pair.x, pair.y);
+		const float d = __uint_as_float(e.y);
+		const uint32_t v = POS ? a : e.x;
+		if(found < k)
+		{
+			heap.i(found) = v;
+			heap.d(found) = d;
+			++found;
+			if(found == k)
+			{
+				heapMake(heap, k);
+				max_d2 = heap.d(0);
+			}
+		}
+		else
+		{
+			heapReplaceTop(heap, k, v, d);
+			max_d2 = heap.d(0);
+		}
+	}
+}
+
+// HS (REPLAY without a caustic map): the split 6-byte heap (HeapRefSplit) — 1.5 -> 2 waves / SIMD at
+// k = 50; a request whose log overflowed walks again with the heap in its own log (8 B slots in HBM).
+template<bool SMALL, bool EXT, bool REPLAY = false, bool HS = false>
 __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 {
 	extern __shared__ uint4 gather_smem[];
@@ -4283,6 +4316,10 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 	HeapRefPacked heap;
 	heap.e = lds_words + 2 * lane;
 	heap.stride = kGatherBlock;
+	HeapRefSplit hsplit;
+	hsplit.dw = lds_words + lane;
+	hsplit.iw = reinterpret_cast<uint16_t *>(lds_words + (size_t)gatherHeapSlots(S) * kGatherBlock) + lane;
+	hsplit.stride = kGatherBlock;
 	// lookup stack: this lane's column, [level][lane] (LDS after the heap, or the HBM stack buffer)
 #if YAF_GATHER_STACK_LDS
 	const uint32_t gstride = kGatherBlock;
@@ -4309,43 +4346,33 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 		const V3 p = xyz(pp);
 		float max_d2 = S.pm_radius2;
 		int found = 0;
+		const uint2 *lg = nullptr;   // HS: the request's log (heap slots hold positions in it)
+		bool from_log = false;       // HS: true after a replay, false when the heap is the log itself
 		if(mode & G_DIFFUSE)
 		{
 			const uint32_t q = seg * A.log.seg_cap + (base_j + threadIdx.x - jb);
 			const uint32_t n_acc = REPLAY ? A.log.n[q] : 0u;
+			if(REPLAY) lg = gatherLogAt(A.log, q);
 			if(REPLAY && n_acc <= A.log.cap)
 			{
-				// PhotonGather (photon.cc:31-52) over the walk's accepted photons, in visit order
-				const int k = S.pm_search;
-				const uint2 *lg = gatherLogAt(A.log, q);
-				uint4 pair = make_uint4(0u, 0u, 0u, 0u);
-				for(uint32_t a = 0; a < n_acc; ++a)
+				if(HS)
 				{
-					if(!(a & 1u)) pair = (a + 1u < n_acc) ? *reinterpret_cast<const uint4 *>(lg + a) : make_uint4(lg[a].x, lg[a].y, 0u, 0u);
-					const uint2 e = (a & 1u) ? make_uint2(pair.z, pair.w) : make_uint2(pair.x, pair.y);
-					const float d = __uint_as_float(e.y);
-					if(found < k)
-					{
-						heap.i(found) = e.x;
-						heap.d(found) = d;
-						++found;
-						if(found == k)
-						{
-							heapMake(heap, k);
-							max_d2 = heap.d(0);
-						}
-					}
-					else
-					{
-						heapReplaceTop(heap, k, e.x, d);
-						max_d2 = heap.d(0);
-					}
+					replayLog<true>(hsplit, lg, n_acc, S.pm_search, found, max_d2);
+					from_log = true;
 				}
+				else replayLog<false>(heap, lg, n_acc, S.pm_search, found, max_d2);
 			}
 			else
 			{
 				if(REPLAY) ++overflows;   // the log overflowed: walk again with the heap
-				found = pkLookup(S.pk_nodes, p, S.pm_search, max_d2, heap, stk, gstride, visits);
+				if(HS)
+				{
+					HeapRefPacked gh;
+					gh.e = reinterpret_cast<uint32_t *>(const_cast<uint2 *>(lg));
+					gh.stride = 1;
+					found = pkLookup(S.pk_nodes, p, S.pm_search, max_d2, gh, stk, gstride, visits);
+				}
+				else found = pkLookup(S.pk_nodes, p, S.pm_search, max_d2, heap, stk, gstride, visits);
 			}
 		}
 		photons += (uint32_t)found;
@@ -4364,7 +4391,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 			const float scale = x87recipMul(kPi, (float)S.pm_paths * max_d2);
 			for(int i = 0; i < found; ++i)
 			{
-				const uint32_t ph = heap.i(i);
+				const uint32_t ph = HS ? lg[from_log ? (uint32_t)hsplit.i(i) : (uint32_t)i].x : heap.i(i);
 				const float4 a = S.ph_pos[ph], b = S.ph_dir[ph];
 				const C3 pc = C3{a.w, b.w, S.ph_colb[ph]};
 				const C3 surf_col = matEval<EXT>(m, sp, wo, xyz(b), B_DIFFUSE);
@@ -4389,7 +4416,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 			}
 		}
 		// ---- causticPhotons / estimateCausticPhotons (integrator_montecarlo.cc:410-419, 627-648) ----
-		if(mode & G_CAUSTIC)
+		if(!HS && (mode & G_CAUSTIC))   // HS is only launched without a caustic map
 		{
 			float r2 = S.c_radius2;
 			const int nc = pkLookup(S.cpk_nodes, p, S.c_search, r2, heap, stk, gstride, visits);
@@ -5338,9 +5365,13 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const D
 #else
 	const bool small = S->small_tables != 0;
 #endif
-	const size_t lds = gatherTableBytes(*S, small) + gatherLdsBytes(*S);
+	// the split heap: a replay without a caustic map (its lookups need photon indices in the heap)
+	const bool split = replay && log->split && !S->caus_map && log->cap <= 65536u && !YAF_GATHER_STACK_LDS;
+	const size_t lds = gatherTableBytes(*S, small) +
+	                   (split ? (size_t)kGatherBlock * 6u * (size_t)gatherHeapSlots(*S) : gatherLdsBytes(*S));
 #define YAF_GATHER_LAUNCH(SM, E) \
-	do { if(replay) hipLaunchKernelGGL((k_gather<SM, E, true>), grid, dim3(kGatherBlock), lds, st, A); \
+	do { if(split) hipLaunchKernelGGL((k_gather<SM, E, true, true>), grid, dim3(kGatherBlock), lds, st, A); \
+	     else if(replay) hipLaunchKernelGGL((k_gather<SM, E, true>), grid, dim3(kGatherBlock), lds, st, A); \
 	     else hipLaunchKernelGGL((k_gather<SM, E, false>), grid, dim3(kGatherBlock), lds, st, A); } while(0)
 	if(S->ext)
 	{

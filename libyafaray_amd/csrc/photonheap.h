@@ -8,6 +8,7 @@
 #pragma once
 
 #include <cstdint>
+#include <type_traits>
 
 #if defined(__HIPCC__)
 #define YPH __host__ __device__ __forceinline__
@@ -38,6 +39,18 @@ struct HeapRefPacked
 	YPH float &d(int k) const { return reinterpret_cast<float *>(e)[2 * k * stride + 1]; }
 };
 
+// Split storage for a replayed gather (k_gather<REPLAY>): slot k = distance (32-bit column) + the
+// entry's position in the request's accepted-photon log (16-bit column), 6 B per slot instead of 8,
+// so more waves fit the CU's LDS; the photon index is read from the log when the estimate is summed.
+struct HeapRefSplit
+{
+	uint32_t *dw;   // dw[k * stride] = distance bits
+	uint16_t *iw;   // iw[k * stride] = log position
+	int stride;
+	YPH uint16_t &i(int k) const { return iw[k * stride]; }
+	YPH float &d(int k) const { return reinterpret_cast<float *>(dw)[k * stride]; }
+};
+
 // __push_heap(first, holeIndex, topIndex, value)
 template<class H> YPH void heapPushUp(const H &h, int hole, int top, uint32_t vi, float vd)
 {
@@ -49,7 +62,7 @@ template<class H> YPH void heapPushUp(const H &h, int hole, int top, uint32_t vi
 		hole = parent;
 		parent = (hole - 1) / 2;
 	}
-	h.i(hole) = vi;
+	h.i(hole) = static_cast<typename std::remove_reference<decltype(h.i(0))>::type>(vi);
 	h.d(hole) = vd;
 }
 
@@ -102,7 +115,7 @@ template<class H> YPH void heapReplaceTop(const H &h, int len, uint32_t ni, floa
 		h.d(len - 1) = h.d(0);
 		heapAdjust(h, 0, len - 1, vi, vd);
 	}
-	h.i(len - 1) = ni;
+	h.i(len - 1) = static_cast<typename std::remove_reference<decltype(h.i(0))>::type>(ni);
 	h.d(len - 1) = nd;
 	// __push_heap(first, len - 1, 0, value)
 	heapPushUp(h, len - 1, 0, ni, nd);

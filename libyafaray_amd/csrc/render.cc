@@ -1513,7 +1513,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	// The two-pass diffuse gather (k_gather_walk + k_gather<REPLAY>, kernels.hip) for diffuse maps whose
 	// k fits the walk's registers: its log holds `cap` accepted photons per request for a batch of
 	// seg_cap queue positions per segment (within 16 GB); YAFARAY_AMD_GATHER=single keeps one pass.
-	GatherLogDesc glog{nullptr, nullptr, 0u, 0u, 0u};
+	GatherLogDesc glog{nullptr, nullptr, 0u, 0u, 0u, 0u};
 	bool walk_gather = false;
 	{
 		const char *ge = std::getenv("YAFARAY_AMD_GATHER");
@@ -1525,7 +1525,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			size_t seg_cap = S.cap_a;
 			while((size_t)R * seg_cap * cap * 8 > (16ull << 30) && seg_cap > 64) seg_cap = ((seg_cap / 2 + 63) / 64) * 64;
 			if(!ensure(log_, d.g_log, (size_t)R * seg_cap * cap * 8) || !ensure(log_, d.g_log_n, (size_t)R * seg_cap * 4)) return false;
-			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u};
+			const char *he = std::getenv("YAFARAY_AMD_GATHER_HEAP");
+			const uint32_t split = (he && std::string(he) == "packed") ? 0u : 1u;
+			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u, split};
 			walk_gather = true;
 		}
 	}

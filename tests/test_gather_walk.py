@@ -34,11 +34,12 @@ CASES = {
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("heap", ["split", "packed"])
 @pytest.mark.parametrize("case", list(CASES))
-def test_two_pass_gather_equals_one_pass(product, case):
+def test_two_pass_gather_equals_one_pass(product, case, heap):
     spec = CASES[case]()
     a, wa, sa = _render(product, spec, {"YAFARAY_AMD_GATHER": "single"})
-    b, wb, sb = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk"})
+    b, wb, sb = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_HEAP": heap})
     assert sa["gather_accepts"] == 0 and sb["gather_overflows"] == 0
     if case != "fg-specular":   # (final gathering replaces the diffuse estimate: caustic lookups only)
         assert sb["gather_accepts"] >= sb["gather_photons"] > 0
@@ -47,9 +48,11 @@ def test_two_pass_gather_equals_one_pass(product, case):
 
 
 @pytest.mark.gpu
-def test_two_pass_gather_log_overflow_falls_back(product):
+@pytest.mark.parametrize("heap", ["split", "packed"])
+def test_two_pass_gather_log_overflow_falls_back(product, heap):
     spec = CASES["diffuse"]()
     a, _, _ = _render(product, spec, {"YAFARAY_AMD_GATHER": "single"})
-    b, _, sb = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_LOG": "1"})   # cap = k = 50
+    b, _, sb = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_LOG": "1",   # cap = k = 50
+                                       "YAFARAY_AMD_GATHER_HEAP": heap})
     assert sb["gather_overflows"] > 0
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
