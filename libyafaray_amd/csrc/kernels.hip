@@ -970,9 +970,17 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	const uint32_t total = n_a + n_s;
 	const uint32_t a0 = L.s * S.cap_a, s0 = L.s * S.cap_s;
 	uint32_t visits = 0, tests = 0, n_closest = 0, n_shadow = 0;
+	// rays traced by traceEntry, counted per wave (ballots into scalar registers): per-lane counters
+	// bumped on the two branches were merged into one address-selected increment of a private array,
+	// a scratch load + store per ray, or spilled at the 64-VGPR budget
+	uint32_t w_closest = 0, w_shadow = 0;
+	auto countWave = [&](int kind) {
+		w_closest += (uint32_t)__popcll(__ballot(kind == 1));
+		w_shadow += (uint32_t)__popcll(__ballot(kind == 2));
+	};
 	const uint32_t stride = L.nb * blockDim.x;
 	// one queue entry: closest ray (j < n_a) or shadow ray (n_a <= j < total)
-	auto traceEntry = [&](uint32_t j) {
+	auto traceEntry = [&](uint32_t j) -> int {
 		if(j < n_a)
 		{
 			const uint32_t i = a0 + j;
@@ -985,7 +993,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 				traverse<false, WIDE, SPILL, false, STATS>(C, xyz(od), xyz(dd), od.w, tmax, t, prim, visits, tests);
 				Q.hit_t[i] = t;
 				Q.hit_prim[i] = prim;
-				++n_closest;
+				return 1;
 			}
 		}
 		else if(j < total)
@@ -1009,8 +1017,9 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 			else occ = traverse<true, WIDE, SPILL, false, STATS>(C, xyz(od), xyz(dd), 0.f, dd.w, t, prim, visits, tests);
 			// (opaque shadows: the NEE entry index rides in sh_o.w)
 			P.occ[TS ? Q.sh_idx[k] : __float_as_int(od.w)] = occ ? 1 : 0;   // P = state set of the consumer shade
-			++n_shadow;
+			return 2;
 		}
+		return 0;
 	};
 	if constexpr(SORT)
 	{
@@ -1037,7 +1046,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 			}
 			waveSortWindow(W, key);
 #pragma unroll 1
-			for(int r = 0; r < kSortPer; ++r) traceEntry(w0 + W.perm[r * 64 + laneId()]);
+			for(int r = 0; r < kSortPer; ++r) countWave(traceEntry(w0 + W.perm[r * 64 + laneId()]));
 		}
 	}
 	else
@@ -1050,7 +1059,12 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	else
 #endif
 	// one uniform trip count per workgroup so every lane reaches the same exits
-	for(uint32_t base = L.r * blockDim.x; base < total; base += stride) traceEntry(base + threadIdx.x);
+	for(uint32_t base = L.r * blockDim.x; base < total; base += stride) countWave(traceEntry(base + threadIdx.x));
+	}
+	if(laneId() == 0)
+	{
+		n_closest += w_closest;
+		n_shadow += w_shadow;
 	}
 	// statistics (rays issued, nodes visited, triangles tested): wave reduce, then one plain
 	// read-modify-write per workgroup into its own record (no atomics: the same block index owns
