@@ -263,6 +263,9 @@ __global__ void k_seg_of(uint32_t *seg_of, uint32_t n, const Split *splits)
 #ifndef YAF_PART_ITEMS
 #define YAF_PART_ITEMS 8
 #endif
+#ifndef YAF_PART_NT
+#define YAF_PART_NT 1
+#endif
 constexpr int kPartItems = YAF_PART_ITEMS;
 constexpr uint32_t kPartThreads = 256;
 constexpr uint32_t kPartTile = kPartThreads * kPartItems;
@@ -400,8 +403,17 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 		const uint32_t left_before = excl + pre[i] - A.seg_left[s];
 		uint32_t np = f[i] ? start + left_before : split_el + ((e - start) - left_before);
 		PK_GUARD(np < A.n, np);
+#if YAF_PART_NT
+		// written once, read by the next level's launch (2.2 GB per level: nothing to keep in L2)
+		typedef uint32_t pk_u32x4 __attribute__((ext_vector_type(4)));
+		pk_u32x4 w;
+		__builtin_memcpy(&w, &r[i], 16);
+		__builtin_nontemporal_store(w, reinterpret_cast<pk_u32x4 *>(&out[np]));
+		if(list == 0) __builtin_nontemporal_store(2u * s + (e < split_el ? 0u : 1u), &A.seg_of_next[e]);
+#else
 		out[np] = r[i];
 		if(list == 0) A.seg_of_next[e] = 2u * s + (e < split_el ? 0u : 1u);
+#endif
 	}
 }
 
