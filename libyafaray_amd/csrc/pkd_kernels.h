@@ -403,7 +403,7 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 		const uint32_t left_before = excl + pre[i] - A.seg_left[s];
 		uint32_t np = f[i] ? start + left_before : split_el + ((e - start) - left_before);
 		PK_GUARD(np < A.n, np);
-#if YAF_PART_NT
+#if YAF_PART_NT && defined(__HIP_DEVICE_COMPILE__)
 		// written once, read by the next level's launch (2.2 GB per level: nothing to keep in L2)
 		typedef uint32_t pk_u32x4 __attribute__((ext_vector_type(4)));
 		pk_u32x4 w;
