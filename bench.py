@@ -23,6 +23,12 @@ Prints ONE JSON line (rank 0).  Extra keys:
                                       image's 8x8 block means, oracle/stats.py, for two RR seeds)
                                       and an RR-off band bit for bit
   * cpu_baseline                      the oracle restatement on this host's cores, bounded band
+  * build                             sha256 of libyafaray4.so and its compile flags (yafaray_amd_buildInfo)
+  * group (N > 1)                     the library's report of the split: devices, peer-access matrix,
+                                      band copy path, band bounds, each member's render ms
+With N > 1 GPUs `parity` is group_parity's (always run): the group's frame bit for bit against a
+one-member render, and an RR-off group frame against the oracle on rows around the band boundaries;
+the process exits with status 3 when either differs.
 """
 import argparse
 import dataclasses
@@ -244,6 +250,17 @@ def main():
     roof = dominant_roofline(s, kt, kernels, pmc, a.scene)
 
     cpu, parity = None, None
+    group = None
+    if n_gpus > 1:
+        # a multi-GPU speed never goes out without its parity verdict (--no-parity does not apply):
+        # the group's frame against a one-member render, and an RR-off group frame against the oracle
+        # around the band boundaries (group_parity)
+        report = yi.group_report()
+        film = yi.film() if rank == 0 else None
+        rr_off = scenes.cornell(W, H, spp=a.spp, bounces=a.bounces, rr=False) if a.scene == "cornell" else None
+        parity = group_parity(Y, spec, film, report, n_gpus, devices=None if world > 1 else list(range(n_gpus)), rr_off_spec=rr_off,
+                              chunk=a.chunk, world=world, rank=rank, dist=dist)
+        group = report
     if rank == 0 and n_gpus == 1:
         if not a.no_cpu_baseline:
             cpu, band = cpu_baseline(spec, a)
@@ -295,11 +312,18 @@ def main():
             "scene_build_seconds": round(s["build_seconds"], 4),
             "parity": parity,
             "cpu_baseline": cpu,
+            "build": {"lib_sha256": Y.lib_sha256(), "flags": Y.build_info()},
         }
+        if group is not None:
+            out["group"] = {k: group.get(k) for k in ("mode", "members", "devices", "peer_devices", "peer_access", "copy_path", "bounds",
+                                                      "member_ms")}
         print(json.dumps(out))
     yi.close()
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and n_gpus > 1 and not parity.get("pass", False):
+        print("bench: multi-GPU parity FAILED (see the line's parity object)", file=sys.stderr)
+        sys.exit(3)
 
 
 def kernel_table(a, s, kt, pmc):
@@ -506,6 +530,92 @@ def second_seed_parity(Y, spec, a, band, seed=7919):
     orgba, ow, _ = O.OracleScene(s2, threads=cores, rr_seed=seed).render(y0, y1)   # full-size arrays, rows y0..y1 filled
     res = band_parity(s2, rgba, w, (y0, y1, orgba, ow))
     res["rr_seed"] = seed
+    return res
+
+
+def _bits_equal(x, y):
+    return bool(np.array_equal(np.ascontiguousarray(x, np.float32).view(np.uint32), np.ascontiguousarray(y, np.float32).view(np.uint32)))
+
+
+def group_parity(Y, spec, group_film, report, members, devices=None, rr_off_spec=None, chunk=None, world=1, rank=0, dist=None,
+                 rows_per_boundary=6):
+    """The multi-GPU frame checked against what it must equal (imagesplitter.cc:30-107 and
+    integrator_tiled.cc:246-264: the film does not depend on how many workers render it):
+      (a) `group_film` (rgba, weights) — the group's frame — bit for bit against a one-member render of
+          the same frame on this process's first device (the band split is bit-invariant by design:
+          pixel-major RR seeds, halo rows, the one-thread splat order);
+      (b) `rr_off_spec` (the same scene, Russian roulette off) rendered by a group of the same shape,
+          against the CPU oracle on rows around the first and the last band boundary, bit for bit.
+    `report` is the library's group report of the checked render (yafaray_amd_getGroupReport): devices,
+    peer-access matrix, copy path, band bounds, per-member ms.  One process: a device group of
+    `members` on `devices` (None: logical members on the current device).  torch.distributed (world > 1):
+    every rank calls this; (b) renders with a fresh render group of all ranks, rank 0 compares, and the
+    verdict is broadcast so every rank agrees.  Returns the parity dict (rank 0; other ranks: pass only)."""
+    from libyafaray_amd import scenes
+    res = {"group": report, "members": members if world <= 1 else world}
+    ok = True
+    # (a) one member, same frame
+    if rank == 0:
+        yi = Y.Interface()
+        scenes.apply(spec, yi)
+        dev0 = devices[0] if devices else (report.get("devices") or [0])[0]
+        yi.set_device_group(1, [dev0])
+        if chunk:
+            yi.L.yafaray_amd_setChunkSlots(yi.h, chunk)
+        t0 = time.perf_counter()
+        yi.render_quiet()
+        t1 = time.perf_counter() - t0
+        one_rgba, one_w = yi.film()
+        yi.close()
+        g_rgba, g_w = group_film
+        diff = np.ascontiguousarray(g_rgba, np.float32).view(np.uint32) != np.ascontiguousarray(one_rgba, np.float32).view(np.uint32)
+        rows_bad = np.nonzero(diff.any(axis=(1, 2)))[0]
+        res["vs_one_member"] = {"bit_identical": _bits_equal(g_rgba, one_rgba), "weights_equal": _bits_equal(g_w, one_w),
+                                "rows_differing": int(len(rows_bad)), "first_bad_rows": [int(r) for r in rows_bad[:8]],
+                                "one_member_frame_s": round(t1, 3)}
+        ok = ok and res["vs_one_member"]["bit_identical"] and res["vs_one_member"]["weights_equal"]
+    # (b) RR off on the group against the oracle, rows around the band boundaries
+    if rr_off_spec is not None:
+        yi = Y.Interface()
+        scenes.apply(rr_off_spec, yi)
+        if world > 1:
+            Y.join_render_group(yi, rank, world, dist)
+            yi.set_device_group(1, [(report.get("devices") or [0])[0]])
+        else:
+            yi.set_device_group(members, devices)
+        if chunk:
+            yi.L.yafaray_amd_setChunkSlots(yi.h, chunk)
+        yi.render_quiet()
+        rep = yi.group_report()
+        if rank == 0:
+            rgba, w = yi.film()
+        yi.close()
+        if rank == 0:
+            from oracle import oracle as O
+            H = rr_off_spec.render.height
+            b = rep["bounds"] or [0, H]
+            inner = b[1:-1] or [H // 2]
+            picks = sorted({inner[0], inner[-1]})
+            cores, _, _ = host_cpu()
+            osc = O.OracleScene(rr_off_spec, threads=cores)
+            checks = []
+            t0 = time.perf_counter()
+            for yb in picks:
+                y0, y1 = max(0, yb - rows_per_boundary // 2 - 1), min(H, yb + rows_per_boundary // 2)
+                orgba, ow, _ = osc.render(y0, y1)
+                a_ = rgba[y0 + 1:y1].view(np.uint32).astype(np.int64)
+                o_ = orgba[y0 + 1:y1].view(np.uint32).astype(np.int64)
+                checks.append({"boundary": int(yb), "rows": [y0 + 1, y1], "bit_identical": bool(np.array_equal(a_, o_)),
+                               "max_ulp": int(np.abs(a_ - o_).max()) if a_.size else 0,
+                               "weights_equal": bool(np.array_equal(w[y0 + 1:y1], ow[y0 + 1:y1]))})
+            res["rr_off_vs_oracle"] = {"bounds": b, "checks": checks, "cpu_s": round(time.perf_counter() - t0, 2)}
+            ok = ok and all(c["bit_identical"] and c["weights_equal"] for c in checks)
+    if world > 1 and dist is not None:
+        import torch
+        t = torch.tensor([1 if ok else 0], device="cuda", dtype=torch.int32)
+        dist.broadcast(t, src=0)
+        ok = bool(t.item())
+    res["pass"] = bool(ok)
     return res
 
 

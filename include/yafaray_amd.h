@@ -66,6 +66,10 @@ typedef struct
  * writes exactly these, so clients built against the 1.0 header keep working; newer clients call
  * yafaray_amd_getStatsEx with sizeof(yafaray_amd_stats_t). */
 #define YAFARAY_AMD_STATS_V1_0_SIZE (offsetof(yafaray_amd_stats_t, gather_visits))
+/* Bytes yafaray_amd_getStats@@LIBYAFARAY_AMD_1.4 (the default a client links against now) writes: every
+ * field through fg_thin_rounds, which the header carried before getStatsEx existed.  Clients linked
+ * against the 1.0 symbol keep receiving YAFARAY_AMD_STATS_V1_0_SIZE bytes. */
+#define YAFARAY_AMD_STATS_V1_4_SIZE (offsetof(yafaray_amd_stats_t, gather_queries))
 
 /* Bulk geometry: n vertices (xyz doubles, as addVertex) / n triangles (abc ints, as addTriangle). */
 YAFARAY_C_API_EXPORT int yafaray_amd_addVertices(yafaray_Interface_t *interface, const double *xyz, int n);
@@ -100,7 +104,8 @@ YAFARAY_C_API_EXPORT int yafaray_amd_getOwnedRows(const yafaray_Interface_t *int
 /* Render without callbacks / console output (bench loop); same work as yafaray_render. */
 YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t *interface);
 
-/* Counters and timings of the last render: the LIBYAFARAY_AMD_1.0 fields (YAFARAY_AMD_STATS_V1_0_SIZE bytes). */
+/* Counters and timings of the last render: YAFARAY_AMD_STATS_V1_4_SIZE bytes (a client linked against the
+ * LIBYAFARAY_AMD_1.0 version of this symbol: YAFARAY_AMD_STATS_V1_0_SIZE bytes). */
 YAFARAY_C_API_EXPORT void yafaray_amd_getStats(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats);
 /* (LIBYAFARAY_AMD_1.2) All counters: copies min(bytes, sizeof(yafaray_amd_stats_t)) bytes, returns how many. */
 YAFARAY_C_API_EXPORT size_t yafaray_amd_getStatsEx(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats, size_t bytes);
@@ -168,6 +173,17 @@ YAFARAY_C_API_EXPORT void yafaray_amd_setTraceStats(yafaray_Interface_t *interfa
  * NEE) since the last reset; returns the number of counters, 0 unless the library was built with
  * -DYAF_PHASE_TIMING (never in the product build). */
 YAFARAY_C_API_EXPORT int yafaray_amd_getPhaseCycles(unsigned long long *cycles, int n, yafaray_bool_t reset);
+
+/* (LIBYAFARAY_AMD_1.4) The library's build: the device objects' architecture and extra compile flags
+ * (a variant build, e.g. -DYAF_PHASE_TIMING, shows here) and the host compiler.  Static storage. */
+YAFARAY_C_API_EXPORT const char *yafaray_amd_buildInfo(void);
+/* (LIBYAFARAY_AMD_1.4) How the last render was split across GPUs, as one JSON object: "mode" ("one GPU",
+ * "device group", "render group"), "members", "devices", the hipDeviceCanAccessPeer matrix over this
+ * process's distinct member devices ("peer_devices", "peer_access"), "copy_path" (how the bands
+ * travel), "bounds" (the row-band boundaries the render used), "member_ms" (each member's render time)
+ * and "next_bounds" (the rebalanced boundaries of the next frame).  Writes at most bytes - 1 characters
+ * + NUL into buf (may be NULL) and returns the length the whole report needs, NUL included (0: no scene). */
+YAFARAY_C_API_EXPORT size_t yafaray_amd_getGroupReport(yafaray_Interface_t *interface, char *buf, size_t bytes);
 
 /* Last error message (empty if none); owned by the interface. */
 YAFARAY_C_API_EXPORT const char *yafaray_amd_lastError(const yafaray_Interface_t *interface);

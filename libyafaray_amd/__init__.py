@@ -138,6 +138,8 @@ def lib():
             "yafaray_amd_getOwnedRows": (i, [vp, C.POINTER(C.c_int), i]),
             "yafaray_amd_renderQuiet": (b, [vp]),
             "yafaray_amd_getStats": (None, [vp, C.POINTER(Stats)]),
+            "yafaray_amd_buildInfo": (cp, []),
+            "yafaray_amd_getGroupReport": (C.c_size_t, [vp, C.c_char_p, C.c_size_t]),
             "yafaray_amd_getStatsEx": (C.c_size_t, [vp, C.POINTER(Stats), C.c_size_t]),
             "yafaray_amd_setDeviceGroup": (b, [vp, i, C.POINTER(C.c_int)]),
             "yafaray_amd_getDeviceGroupSize": (i, [vp]),
@@ -160,6 +162,18 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def build_info() -> str:
+    """The library's build flags (yafaray_amd_buildInfo): device arch + extra flags, host compiler."""
+    return lib().yafaray_amd_buildInfo().decode()
+
+
+def lib_sha256() -> str:
+    """sha256 of the loaded libyafaray4.so (bench.py prints it with build_info)."""
+    import hashlib
+    with open(LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 
 def version() -> str:
@@ -285,6 +299,17 @@ class Interface:
 
     def device_group_size(self) -> int:
         return int(self.L.yafaray_amd_getDeviceGroupSize(self.h))
+
+    def group_report(self) -> dict:
+        """How the last render was split across GPUs (yafaray_amd_getGroupReport): mode, devices, the
+        peer-access matrix, the band copy path, band bounds and each member's render time."""
+        import json
+        n = int(self.L.yafaray_amd_getGroupReport(self.h, None, 0))
+        if n <= 0:
+            raise RuntimeError("getGroupReport failed: " + self.last_error())
+        buf = C.create_string_buffer(n)
+        self.L.yafaray_amd_getGroupReport(self.h, buf, n)
+        return json.loads(buf.value.decode())
 
     def kernel_times(self) -> dict:
         """{kernel: {"ms", "launches", "items"}} of the last render with profiling on (yafaray_amd_getKernelTimes)."""

@@ -30,6 +30,8 @@ static char *dupString(const std::string &s)
 }
 
 extern "C" int yafamd_phase_cycles(unsigned long long *out, int n, int reset);
+extern "C" const char *yafamd_device_build();
+#define YAF_HOST_BUILD "hipcc/clang " __VERSION__ " -O3 -ffp-contract=off"
 
 extern "C" {
 
@@ -563,11 +565,43 @@ yafaray_bool_t yafaray_amd_renderQuiet(yafaray_Interface_t *interface)
 	return (s && s->render(none, nullptr, nullptr, true)) ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
 }
 
-void yafaray_amd_getStats(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats)
+// yafaray_amd_getStats has two versions.  @LIBYAFARAY_AMD_1.0 (what clients linked before 1.4
+// bound to) copies the 1.0 struct's fields only: the oldest clients allocate no more.  The default
+// @@LIBYAFARAY_AMD_1.4 (what a client linking now binds to) copies every field the header carried
+// while getStats was the only accessor — through fg_thin_rounds — so a client built against that header
+// reads them all; getStatsEx copies any length.
+void yafamd_getStats_v1_0(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats)
 {
-	// LIBYAFARAY_AMD_1.0 clients allocate the 1.0 struct: copy only its fields
 	const Interface *it = I(interface);
 	if(it->scene && stats) std::memcpy((void *)stats, &it->scene->stats, YAFARAY_AMD_STATS_V1_0_SIZE);
+}
+
+void yafamd_getStats_v1_4(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats)
+{
+	const Interface *it = I(interface);
+	if(it->scene && stats) std::memcpy((void *)stats, &it->scene->stats, YAFARAY_AMD_STATS_V1_4_SIZE);
+}
+__asm__(".symver yafamd_getStats_v1_0, yafaray_amd_getStats@LIBYAFARAY_AMD_1.0");
+__asm__(".symver yafamd_getStats_v1_4, yafaray_amd_getStats@@LIBYAFARAY_AMD_1.4");
+
+const char *yafaray_amd_buildInfo()
+{
+	static const std::string info = std::string("device: ") + yafamd_device_build() + "; host: " + YAF_HOST_BUILD;
+	return info.c_str();
+}
+
+size_t yafaray_amd_getGroupReport(yafaray_Interface_t *interface, char *buf, size_t bytes)
+{
+	Scene *s = I(interface)->sc();
+	if(!s) return 0;
+	const std::string r = s->groupReport();
+	if(buf && bytes)
+	{
+		const size_t n = std::min(bytes - 1, r.size());
+		std::memcpy(buf, r.data(), n);
+		buf[n] = 0;
+	}
+	return r.size() + 1;
 }
 
 size_t yafaray_amd_getStatsEx(const yafaray_Interface_t *interface, yafaray_amd_stats_t *stats, size_t bytes)

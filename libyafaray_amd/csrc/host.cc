@@ -5,6 +5,8 @@
 #include "render.h"
 #include "texture.h"
 
+#include <hip/hip_runtime_api.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -179,6 +181,61 @@ bool Scene::syncMembers()
 		log.info(os.str());
 	}
 	return true;
+}
+
+// What the last render's split looked like, for a caller that wants to check or log it (bench.py's
+// multi-GPU line): the group kind, the members' devices, which device pairs can access each other
+// directly (hipDeviceCanAccessPeer: the band copies then run over xGMI without staging), how the bands
+// travel, the band boundaries the render used and each member's render time.
+std::string Scene::groupReport()
+{
+	std::ostringstream os;
+	auto list = [&os](const auto &v) {
+		os << "[";
+		for(size_t k = 0; k < v.size(); ++k) os << (k ? ", " : "") << v[k];
+		os << "]";
+	};
+	const int gw = gpu_ ? gpu_->groupWorld() : 1;
+	const int n = gw > 1 ? gw : memberCount();
+	const char *mode = gw > 1 ? "render group" : n > 1 ? "device group" : "one GPU";
+	os << "{\"mode\": \"" << mode << "\", \"members\": " << n;
+	if(gw > 1) os << ", \"rank\": " << gpu_->groupRank() << ", \"device\": " << gpu_->device();
+	std::vector<int> devs = member_devs_;
+	if(gw > 1 && gpu_) devs = {gpu_->device()};
+	os << ", \"devices\": ";
+	list(devs);
+	// peer-access matrix over the distinct devices of this process's members
+	const std::set<int> uniq(devs.begin(), devs.end());
+	const std::vector<int> ud(uniq.begin(), uniq.end());
+	bool all_peer = true;
+	os << ", \"peer_devices\": ";
+	list(ud);
+	os << ", \"peer_access\": [";
+	for(size_t a = 0; a < ud.size(); ++a)
+	{
+		os << (a ? ", " : "") << "[";
+		for(size_t b = 0; b < ud.size(); ++b)
+		{
+			int can = a == b ? 1 : 0;
+			if(a != b && hipDeviceCanAccessPeer(&can, ud[a], ud[b]) != hipSuccess) can = 0;
+			if(a != b && !can) all_peer = false;
+			os << (b ? ", " : "") << can;
+		}
+		os << "]";
+	}
+	os << "]";
+	const char *path = "none (one member)";
+	if(gw > 1) path = "RCCL all-gather of band slots (xGMI between GPUs)";
+	else if(n > 1 && ud.size() == 1) path = "hipMemcpyPeerAsync between logical members of one device (device-to-device copy)";
+	else if(n > 1) path = all_peer ? "hipMemcpyPeerAsync with peer access enabled (direct xGMI)" : "hipMemcpyPeerAsync, staged (no peer access on some pair)";
+	os << ", \"copy_path\": \"" << path << "\", \"bounds\": ";
+	list(last_bounds_);
+	os << ", \"member_ms\": ";
+	list(last_member_ms_);
+	os << ", \"next_bounds\": ";
+	list(group_bounds);
+	os << "}";
+	return os.str();
 }
 
 // One film rendered by every member of the device group, each on its own host thread (member 0 on
@@ -1365,6 +1422,8 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		const int n_members = memberCount();
 		const int world = group_world > 1 ? group_world : n_members;
 		const bool grouped = world > 1;
+		last_bounds_.clear();
+		last_member_ms_.clear();
 		if(grouped)
 		{
 			if((int)group_bounds.size() != world + 1 || group_bounds.back() != s.height) group_bounds = equalBands(s.height, world);
@@ -1549,6 +1608,8 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		if(grouped)
 		{
 			const std::vector<double> &ms = gpu()->memberMs();
+			last_bounds_ = group_bounds;
+			last_member_ms_ = ms;
 			if((int)ms.size() == world) group_bounds = rebalanceBands(group_bounds, ms, 0);
 		}
 		if(fmode != filmio::None && io_member) saveFilm();

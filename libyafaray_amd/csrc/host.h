@@ -252,6 +252,7 @@ class Scene
 		GpuRenderer *member(int m);
 		bool syncMembers();                 // (re)create the device group's members for the current settings
 		const KernelTimes &kernelTimes();   // per-kernel timing of the last profiled render (summed over members)
+		std::string groupReport();          // JSON: how the last render was split (yafaray_amd_getGroupReport)
 
 		// film of the last render
 		std::vector<float> film_rgba, film_weights;
@@ -266,6 +267,8 @@ class Scene
 		std::vector<int> member_devs_;                      // devices of the current members
 		std::unique_ptr<KernelTimes> kt_sum_;
 		yafaray_amd_stats_t group_stats_{};                 // counters of the last device-group render
+		std::vector<int> last_bounds_;                      // band boundaries the last group render used
+		std::vector<double> last_member_ms_;                // and each member's render time
 };
 
 class Interface

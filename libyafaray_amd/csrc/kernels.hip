@@ -1580,13 +1580,28 @@ struct ShadeOut
 	}
 };
 
+// estimateOneDirectLight's light pick (integrator_montecarlo.cc:70-78): lnum = the light that
+// Halton(2, base_sampling_offset + n - 1).getNext() selects, where the reference's n is a per-thread
+// running counter of the calls (integrator_tiled.cc:48, reset at render start, :169-171) — its value
+// depends on which samples the thread rendered before, i.e. on the thread schedule.  Here n of a call
+// is u * stride + local: u mixes the pixel's sampling offset and the sample number (PixelSamplingData,
+// so the pick does not depend on how the film is split across GPUs or chunks), local counts the
+// calls of the sample's path (depth + subpath * bounces), and the stride is odd, so the low bits of
+// n — which decide the leading digits of the radical inverse, hence the light — run through every
+// residue as u varies: every light is picked with its 1 / num_lights share at every depth, as by the
+// reference's counter.  (A counter that is the same for every sample — e.g. local alone — picks the
+// same light at a given depth for the whole film: a biased image once there are >= 2 lights.)
+__device__ __forceinline__ uint32_t pickLight(const DevScene &S, uint32_t offset, uint32_t sample_idx, uint32_t local, uint32_t stride)
+{
+	if(S.n_lights <= 1) return 0u;
+	const uint32_t u = offset + sample_idx * 0x9E3779B1u;
+	const float hv = haltonFirst(2u, 0.5, S.base_offset + (u * (stride | 1u) + local) - 1u);
+	return (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
+}
+
 // Appends (or not) one shadow ray per lane — every lane of the wave must call.
 __device__ __forceinline__ void emitShadow(bool want, V3 o, V3 d, float t_max, float tmin, int idx, const ShadeOut &out)
 {
-#ifdef YAF_EXP_NO_EMIT
-	if(want) out.Qn.sh_idx[idx] = idx;   // timing experiment only: no append (wrong images)
-	return;
-#endif
 	const uint32_t k = out.sh_base + waveAppend(want, out.sh_count);
 	if(want)
 	{
@@ -1871,9 +1886,6 @@ __device__ C3 neeSum(const DevScene &S, const DevLight &L, const float4 *nee, co
 
 __device__ __forceinline__ float ldsDim(const DevScene &S, int dim, uint32_t n)
 {
-#ifdef YAF_EXP_CHEAP_LDS
-	return riVdC(n * (uint32_t)(dim + 1));   // timing experiment only (wrong images)
-#endif
 	const uint4 fd = S.faure_dim[dim];
 	UDiv dv;
 	dv.m = fd.z;
@@ -2298,22 +2310,12 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				}
 			}
 		}
-#ifdef YAF_EXP_NO_NEE
-		nee_one = false;   // timing experiment only (wrong images)
-		nee_v0 = false;
-#endif
 		uint32_t lnum = 0;
 		if(nee_one)
 		{
-			// integrator_montecarlo.cc:70-78 light pick.  The reference draws from a running
-			// per-thread counter; a per-sample counter keeps the GPU deterministic (multi-light
-			// PT is therefore matched statistically; one light is exact).
-			if(S.n_lights > 1)
-			{
-				const uint32_t corr = (uint32_t)depth + subpath * (uint32_t)S.bounces;
-				const float hv = haltonFirst(2u, 0.5, S.base_offset + corr - 1u);
-				lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
-			}
+			// integrator_montecarlo.cc:70-78 light pick (pickLight: multi-light PT is matched
+			// statistically, one light exactly)
+			lnum = pickLight(S, offset, sample_idx, (uint32_t)depth + subpath * (uint32_t)S.bounces, n_paths * (uint32_t)(S.bounces + 1));
 			flags = (flags & ((1u << F_LNUM_SHIFT) - 1u)) | (lnum << F_LNUM_SHIFT) | F_PEND_ONE;
 		}
 		if(nee_v0) flags |= F_PEND_V0;
@@ -3282,13 +3284,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 		uint32_t lnum = 0;
 		if(nee_one)
 		{
-			// integrator_montecarlo.cc:70-78 light pick (per-sample counter, as k_shade)
-			if(S.n_lights > 1)
-			{
-				const uint32_t corr = (uint32_t)depth + subpath * (uint32_t)S.bounces;
-				const float hv = haltonFirst(2u, 0.5, S.base_offset + corr - 1u);
-				lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
-			}
+			// integrator_montecarlo.cc:70-78 light pick (as k_shade)
+			lnum = pickLight(S, offset, sample_idx, (uint32_t)depth + subpath * (uint32_t)S.bounces, n_paths * (uint32_t)(S.bounces + 1));
 			flags = (flags & ((1u << F_LNUM_SHIFT) - 1u)) | (lnum << F_LNUM_SHIFT) | F_PEND_ONE;
 		}
 		if(nee_v0) flags |= F_PEND_V0;
@@ -4952,15 +4949,10 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 				{
 					if(close)
 					{
-						// estimateOneDirectLight (integrator_montecarlo.cc:70-78); the light pick draws a
-						// per-sample counter (the reference's runs per thread; one light is exact)
-						uint32_t lnum = 0;
-						if(S.n_lights > 1)
-						{
-							const uint32_t corr = 1u + (uint32_t)i * (uint32_t)max(1, S.fg_bounces) + (uint32_t)depth;
-							const float hv = haltonFirst(2u, 0.5, S.base_offset + corr - 1u);
-							lnum = (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
-						}
+						// estimateOneDirectLight (integrator_montecarlo.cc:70-78); the light pick as pickLight
+						// describes (the reference's counter runs per thread; one light is exact)
+						const uint32_t lnum = pickLight(S, offset, sample_idx, (uint32_t)i * (uint32_t)max(1, S.fg_bounces) + (uint32_t)depth,
+						                                (uint32_t)n_sampl * (uint32_t)(max(1, S.fg_bounces) + 1));
 						lcol = (S.n_lights > 0)
 						           ? lightEstimateInline<EXT, WIDE, SPILL, TSH>(S, C, S.lights[lnum], mh, hit, pwo, lnum, sample_idx, offset, visits, tests,
 						                                                        ts_buf) *
@@ -5030,6 +5022,16 @@ int yafamd_trace_block() { return kTraceBlock; }
 // Whether the non-EXT k_shade runs the next-event estimation itself (then render.cc launches no
 // k_nee for those scenes); -DYAF_FUSE builds that variant (measured slower, see kShadeFused).
 int yafamd_shade_fused() { return kShadeFused ? 1 : 0; }
+
+// The flags this device object was compiled with (Makefile DEVINFO): yafaray_amd_buildInfo.
+#ifndef YAF_DEVICE_BUILD
+#define YAF_DEVICE_BUILD "arch=? extra=[?] (built outside csrc/Makefile)"
+#endif
+const char *yafamd_device_build() { return YAF_DEVICE_BUILD
+#ifdef YAF_PHASE_TIMING
+	" phase-timing"
+#endif
+	; }
 
 // Diagnostic: k_shade phase cycles (only a -DYAF_PHASE_TIMING build records them).
 int yafamd_phase_cycles(unsigned long long *out, int n, int reset)

@@ -64,7 +64,22 @@ bool load(Logger &log, const std::string &file, Map &out)
 		log.warning("PhotonMap file '" + file + "' is truncated");
 		return false;
 	}
-	// the reference reads position xyz then colour rgb per photon (photon.cc:78-85)
+	// the reference reads position xyz then colour rgb per photon (photon.cc:78-85).  The count comes
+	// from the file: check that the file holds that many records before allocating for them (a corrupt
+	// count would otherwise ask for up to 96 GB and throw)
+	const long here = std::ftell(fp.get());
+	if(here < 0 || std::fseek(fp.get(), 0, SEEK_END) != 0)
+	{
+		log.warning("PhotonMap file '" + file + "' is truncated");
+		return false;
+	}
+	const long end = std::ftell(fp.get());
+	if(end < here || (uint64_t)(end - here) < (uint64_t)n * 24u || std::fseek(fp.get(), here, SEEK_SET) != 0)
+	{
+		log.warning("PhotonMap file '" + file + "' is truncated");
+		out = Map{};
+		return false;
+	}
 	std::vector<float> rec((size_t)n * 6);
 	if(n && fread(rec.data(), sizeof(float) * 6, n, fp.get()) != n)
 	{

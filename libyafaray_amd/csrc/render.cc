@@ -785,13 +785,29 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 		uint64_t tot = 0, rtot = 0;
 		for(uint32_t c : counts) tot += c;
 		for(uint32_t c : rcounts) rtot += c;
-		if(tot > 0xffffffffull || rtot > 0xffffffffull) { log_.error("PhotonIntegrator: photon map exceeds 2^32 photons"); return false; }
-		if(!ensure(log_, pos, std::max<uint64_t>(tot, 1) * 16) || !ensure(log_, dir, std::max<uint64_t>(tot, 1) * 16) ||
-		   !ensure(log_, colb, std::max<uint64_t>(tot, 1) * 4))
+		bool ok = true;
+		if(tot > 0xffffffffull || rtot > 0xffffffffull)
+		{
+			log_.error("PhotonIntegrator: photon map exceeds 2^32 photons");
+			ok = false;
+		}
+		ok = ok && ensure(log_, pos, std::max<uint64_t>(tot, 1) * 16) && ensure(log_, dir, std::max<uint64_t>(tot, 1) * 16) &&
+		     ensure(log_, colb, std::max<uint64_t>(tot, 1) * 4);
+		ok = ok && (!want_rad || (ensure(log_, d.radc_a, std::max<uint64_t>(rtot, 1) * 16) && ensure(log_, d.radc_b, std::max<uint64_t>(rtot, 1) * 16) &&
+		                          ensure(log_, d.radc_c, std::max<uint64_t>(rtot, 1) * 16)));
+		if(fault_concat_)
+		{
+			log_.error("GPU group: injected failure of member " + std::to_string(me) + " between the photon counts and the concatenation");
+			ok = false;
+		}
+		// every member allocates the concatenated map before anyone copies: agree on the outcome, so a
+		// member that could not allocate stops the group here instead of leaving the others waiting
+		// inside groupConcat (its groupAbort would pair with their first arrival there)
+		if(groupStatus(ok ? 0 : 2) >= 2)
+		{
+			if(ok) log_.error("GPU group: a member failed; render abandoned");
 			return false;
-		if(want_rad && (!ensure(log_, d.radc_a, std::max<uint64_t>(rtot, 1) * 16) || !ensure(log_, d.radc_b, std::max<uint64_t>(rtot, 1) * 16) ||
-		                !ensure(log_, d.radc_c, std::max<uint64_t>(rtot, 1) * 16)))
-			return false;
+		}
 		if(!groupConcat(which ? 1 : 0, counts) || (want_rad && !groupConcat(2, rcounts))) return false;
 		n = (uint32_t)tot;
 		nr = (uint32_t)rtot;
@@ -2207,12 +2223,15 @@ bool GpuRenderer::renderMember(RenderParams &rp, volatile bool *canceled)
 	failure_seen_ = false;
 	member_ms_.clear();
 	// YAFARAY_AMD_FAULT_MEMBER=m[:p] (tests of the failure protocol): member m fails before rendering
-	// (p = 0, default) or at the start of adaptive pass p + 1
+	// (p = 0, default), at the start of adaptive pass p + 1, or (p = "concat") after the members
+	// exchanged their photon-map counts, before the maps are concatenated
 	fault_pass_ = -1;
+	fault_concat_ = false;
 	if(const char *e = getenv("YAFARAY_AMD_FAULT_MEMBER"); e && *e && atoi(e) == rp.shard_rank)
 	{
 		const char *c = std::strchr(e, ':');
-		fault_pass_ = c ? atoi(c + 1) : 0;
+		fault_concat_ = c && std::strcmp(c + 1, "concat") == 0;
+		fault_pass_ = fault_concat_ ? -1 : c ? atoi(c + 1) : 0;
 		if(fault_pass_ == 0)
 		{
 			log_.error("GPU group: injected failure of member " + std::to_string(rp.shard_rank) + " before rendering");

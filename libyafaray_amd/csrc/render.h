@@ -240,6 +240,7 @@ class GpuRenderer
 		int peer_rank_ = 0;
 		bool failure_seen_ = false;   // a group status agreement of this render returned "failed"
 		int fault_pass_ = -1;         // failure injection (tests of the group protocol): fail at this pass
+		bool fault_concat_ = false;   // ... or between the photon-map counts and their concatenation
 		std::vector<double> member_ms_;
 		yafaray_amd_stats_t stats_{};
 		KernelTimes ktimes_{};

@@ -133,6 +133,13 @@ def oracle_lib():
     return _oracle
 
 
+def glibc_rand(seed: int, n: int) -> np.ndarray:
+    """The oracle's restatement of glibc rand() after srand(seed): the first n values (uint32)."""
+    out = np.empty(max(1, n), np.uint32)
+    oracle_lib().yc_glibc_rand(C.c_uint32(seed), C.c_int(n), _p(out, C.c_uint32))
+    return out[:n]
+
+
 def ref_lib():
     """The reference's own building blocks, or None when oracle/_ref was not built."""
     global _ref

@@ -3464,6 +3464,14 @@ void yc_shirley_disk(const float *r12, float *uv, int n)
 	for(int i = 0; i < n; ++i) shirleyDisk(r12[2 * i], r12[2 * i + 1], uv[2 * i], uv[2 * i + 1]);
 }
 
+// the RR tile seeds' generator on its own: the first n values glibc's rand() returns after
+// srand(seed) (pinned against libc by tests/test_oracle_golden.py::test_glibc_rand_restatement)
+void yc_glibc_rand(uint32_t seed, int n, uint32_t *out)
+{
+	const std::vector<uint32_t> v = glibcRandSequence(seed, n > 0 ? (size_t)n : 0);
+	for(int i = 0; i < n; ++i) out[i] = v[(size_t)i];
+}
+
 // tile lists of renderImage (one render thread): order 0 linear, 1 centre, 2 random (fixed seed);
 // out = (x, y, w, h) per tile, pinned against ref_tiles (imagesplitter.cc:30-107)
 int yc_tiles(int w, int h, int bs, int order, int *out, int cap)

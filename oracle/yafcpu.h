@@ -220,6 +220,7 @@ int yc_render_image(const yc_scene *scene, int y0, int y1, float *rgba, float *w
 int yc_photon_map(const yc_scene *scene, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths);
 void yc_shirley_disk(const float *r12, float *uv, int n);
 int yc_tiles(int w, int h, int bs, int order, int *out, int cap);
+void yc_glibc_rand(uint32_t seed, int n, uint32_t *out);
 void yc_rgbe_decode(const uint8_t *rgbe, float *rgb, int n);
 int yc_photon_map_ex(const yc_scene *scene, int which, float *pos, float *dir, float *col, uint32_t *nodes, int *n_paths);
 

@@ -129,20 +129,52 @@ def test_reference_clients_link_and_run(product, tmp_path, t):
     assert "symbol lookup error" not in out and "error while loading" not in out
 
 
-def test_get_stats_keeps_the_1_0_struct_size(product):
-    """yafaray_amd_getStats (LIBYAFARAY_AMD_1.0) writes only the 1.0 struct's bytes — a client built
-    against the 1.0 header allocates no more; getStatsEx copies min(size, sizeof) bytes."""
+def _versioned(product, name, version):
+    """dlvsym: the given version of a versioned symbol (ctypes' getattr binds the default @@ one)."""
+    import ctypes as C
+    libc = C.CDLL(None)
+    dlvsym = libc.dlvsym
+    dlvsym.restype = C.c_void_p
+    dlvsym.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p]
+    addr = dlvsym(product.lib()._handle, name.encode(), version.encode())
+    assert addr, f"{name}@{version} not found"
+    return C.CFUNCTYPE(None, C.c_void_p, C.c_void_p)(addr)
+
+
+def test_get_stats_versions_keep_their_struct_sizes(product):
+    """yafaray_amd_getStats@LIBYAFARAY_AMD_1.0 writes only the 1.0 struct's bytes (a client linked
+    against it allocates no more); the default @@LIBYAFARAY_AMD_1.4 writes every field through
+    fg_thin_rounds (the header carried those before getStatsEx existed); getStatsEx copies
+    min(size, sizeof) bytes."""
     import ctypes as C
     yi = product.Interface()
     yi.createScene()
-    v1 = product.Stats.gather_visits.offset
+    v10 = product.Stats.gather_visits.offset
+    v14 = product.Stats.gather_queries.offset
+    assert v14 > v10
     buf = (C.c_ubyte * (C.sizeof(product.Stats) + 64))()
-    C.memset(buf, 0xA5, C.sizeof(buf))
-    yi.L.yafaray_amd_getStats(yi.h, C.cast(buf, C.POINTER(product.Stats)))
-    assert all(b == 0xA5 for b in bytes(buf)[v1:]), "getStats wrote past the 1.0 struct"
-    assert any(b != 0xA5 for b in bytes(buf)[:v1])
+    for fn, size in ((_versioned(product, "yafaray_amd_getStats", "LIBYAFARAY_AMD_1.0"), v10),
+                     (_versioned(product, "yafaray_amd_getStats", "LIBYAFARAY_AMD_1.4"), v14),
+                     (lambda h, p: yi.L.yafaray_amd_getStats(h, C.cast(p, C.POINTER(product.Stats))), v14)):
+        C.memset(buf, 0xA5, C.sizeof(buf))
+        fn(yi.h, C.addressof(buf))
+        assert all(b == 0xA5 for b in bytes(buf)[size:]), "getStats wrote past its struct"
+        assert any(b != 0xA5 for b in bytes(buf)[:v10])
     C.memset(buf, 0xA5, C.sizeof(buf))
     n = yi.L.yafaray_amd_getStatsEx(yi.h, C.cast(buf, C.POINTER(product.Stats)), 24)
     assert n == 24 and all(b == 0xA5 for b in bytes(buf)[24:])
     assert yi.L.yafaray_amd_getStatsEx(yi.h, C.cast(buf, C.POINTER(product.Stats)), 1 << 20) == C.sizeof(product.Stats)
+    yi.close()
+
+
+def test_build_info_and_group_report(product):
+    """yafaray_amd_buildInfo names the device objects' flags (no variant flags in the product build);
+    getGroupReport is valid JSON before any render (one GPU, no bounds)."""
+    import json
+    info = product.build_info()
+    assert "arch=gfx950" in info and "extra=[]" in info, info
+    yi = product.Interface()
+    yi.createScene()
+    r = yi.group_report()
+    assert r["mode"] == "one GPU" and r["bounds"] == [] and r["member_ms"] == []
     yi.close()

@@ -179,6 +179,28 @@ def test_device_group_member_failure_ends_every_member(product, monkeypatch, fau
     assert _same(a, full) and _same(w, fw)
 
 
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("fault", ["1:concat", "0:concat", "2:concat"])
+def test_device_group_photon_concat_failure_ends_every_member(product, monkeypatch, fault):
+    """a member that fails after the photon-map counts were exchanged and before the maps
+    are concatenated (injected: as if the concatenated map's allocation failed) stops the group at
+    the agreement in front of the copies — no member is left waiting inside the concatenation — and
+    the next render (no fault) is complete again."""
+    spec = scenes.cornell_photon(40, 30, spp=1, photons=20000, search=50, radius=0.1).with_render(pm_final_gather=True, fg_samples=4)
+    yi = product.Interface()
+    scenes.apply(spec, yi)
+    yi.set_device_group(3)
+    monkeypatch.setenv("YAFARAY_AMD_FAULT_MEMBER", fault)
+    with pytest.raises(RuntimeError, match="failure|failed"):
+        yi.render_quiet()
+    monkeypatch.delenv("YAFARAY_AMD_FAULT_MEMBER")
+    yi.render_quiet()
+    a, w = yi.film()
+    yi.close()
+    full, fw, _ = product.render_spec(spec, members=1)
+    assert _same(a, full) and _same(w, fw)
+
+
 def test_device_group_cancel(product):
     """yafaray_cancelRendering during a group render: every member stops at its next chunk, the
     members still combine, and every pixel is either complete or empty (as a canceled one-GPU

@@ -181,3 +181,19 @@ def test_product_image_buffers_quantise_like_the_reference(product, tex_golden):
         ref = tex_golden[f"quant{kind}"][:1024]
         assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), f"{TEX_KINDS[kind]}: {(out != ref).sum()} mismatches"
     yi.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 7920, 0x7fffffff, 0])
+def test_glibc_rand_restatement(oracle_built, seed):
+    """The oracle seeds each tile's Russian-roulette generator from a restatement of glibc's rand()
+    (integrator_tiled.cc:272, the reference's scene setup reseeds with srand); pinned here against
+    the real libc: srand(seed) then 2000 rand() calls (seed 0 behaves as seed 1 in glibc)."""
+    import ctypes as C
+    libc = C.CDLL("libc.so.6")
+    libc.srand.argtypes = [C.c_uint]
+    libc.rand.restype = C.c_int
+    n = 2000
+    libc.srand(seed)
+    want = np.array([libc.rand() for _ in range(n)], np.uint32)
+    got = oracle_built.glibc_rand(seed, n)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:5]

@@ -220,6 +220,14 @@ def test_load_fallbacks(product, tmp_path):
         f.write(b"NOT_A_MAP")
     b, _, st = product.render_spec(pm_spec(base, "load", fg=True))
     assert st["photon_maps_mode"] == 1 and np.array_equal(b.view(np.uint32), ref.view(np.uint32))
+    # a corrupt photon count (2^32 - 1 records announced, none present) is a truncated file: the
+    # loader checks the file length before it allocates, and the integrator generates and saves
+    write_ref_map(files(base)["diffuse"], "Diffuse Photon Map", 1, np.zeros((0, 3)), np.zeros((0, 3)))
+    with open(files(base)["diffuse"], "r+b") as f:
+        f.seek(len(HEADER) + len(b"Diffuse Photon Map\0") + 12)
+        f.write(struct.pack("<I", 0xFFFFFFFF))
+    b, _, st = product.render_spec(pm_spec(base, "load", fg=True))
+    assert st["photon_maps_mode"] == 1 and np.array_equal(b.view(np.uint32), ref.view(np.uint32))
     # an unknown value generates (factory :847)
     c, _, st = product.render_spec(pm_spec(base, "bogus", fg=True))
     assert st["photon_maps_mode"] == 0 and np.array_equal(c.view(np.uint32), ref.view(np.uint32))
@@ -227,6 +235,10 @@ def test_load_fallbacks(product, tmp_path):
 
 @pytest.mark.gpu
 def test_reuse_previous(product, tmp_path):
+    """Deliberate extension: the reference turns a reuse-previous integrator whose
+    maps are empty into PhotonsGenerateOnly for good (integrator_photon_mapping.cc:328-358), so a
+    fresh integrator there never reuses anything; here the fallback holds for that render only and
+    the second render reuses the maps the first one generated (the feature's documented intent)."""
     spec = pm_spec(tmp_path / "r", "reuse-previous", fg=True)
     ref, _, _ = product.render_spec(pm_spec(tmp_path / "r", fg=True))
     yi = product.Interface()

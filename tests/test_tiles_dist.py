@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from libyafaray_amd import tiles
+import tiles
 
 
 def _free_port():
