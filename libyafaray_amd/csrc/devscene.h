@@ -275,6 +275,14 @@ struct DevScene
 	float4 *spawn_o, *spawn_d;     // spawned rays (origin, tmin) (direction, tmax)
 	uint4 *spawn_pr;               // (pixel offset, sample index, MWC x, MWC c)
 	uint32_t *spawn_count;         // [0] spawned records, [1] overflow flag
+	// estimateOneDirectLight's light pick in the reference's one-thread order (integrator_montecarlo.cc:70-78,
+	// the counter integrator_tiled.cc:48 / :169-171): lpc holds one counter per camera sample of the pass,
+	// pixel-major ((y * width + x) * spp + s).  lpc_mode 1 (count run): each call adds one to its sample's
+	// counter and estimates nothing; 2: the counter starts at the calls of every sample the one-thread
+	// render visits before it (render.cc lpcBases: an exclusive scan in tile order) and each call takes
+	// the next value; 0: pickLight
+	uint32_t *lpc;
+	int lpc_mode;
 };
 
 struct DevFilm

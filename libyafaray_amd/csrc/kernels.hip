@@ -1584,17 +1584,39 @@ struct ShadeOut
 // Halton(2, base_sampling_offset + n - 1).getNext() selects, where the reference's n is a per-thread
 // running counter of the calls (integrator_tiled.cc:48, reset at render start, :169-171) — its value
 // depends on which samples the thread rendered before, i.e. on the thread schedule.  Here n of a call
-// is u * stride + local: u mixes the pixel's sampling offset and the sample number (PixelSamplingData,
+// is u * stride + local: u hashes the pixel's sampling offset and the sample number (PixelSamplingData,
 // so the pick does not depend on how the film is split across GPUs or chunks), local counts the
 // calls of the sample's path (depth + subpath * bounces), and the stride is odd, so the low bits of
 // n — which decide the leading digits of the radical inverse, hence the light — run through every
-// residue as u varies: every light is picked with its 1 / num_lights share at every depth, as by the
-// reference's counter.  (A counter that is the same for every sample — e.g. local alone — picks the
-// same light at a given depth for the whole film: a biased image once there are >= 2 lights.)
+// residue as u varies: every light is picked with its 1 / num_lights share at every depth.  (A
+// counter that is the same for every sample — local alone — picks the same light at a given depth
+// for the whole film: a biased image once there are >= 2 lights.)  Path tracing uses the reference's
+// one-thread counter instead (DevScene::lpc); this pick serves final gathering and recursion trees.
+// The light of the call whose running counter is n: Halton(2, base_sampling_offset + n - 1).getNext()
+// (integrator_montecarlo.cc:74-75).
+__device__ __forceinline__ uint32_t lightOfCounter(const DevScene &S, uint32_t n)
+{
+	const float hv = haltonFirst(2u, 0.5, S.base_offset + n - 1u);
+	return (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t h)
+{
+	h ^= h >> 16;
+	h *= 0x7feb352du;
+	h ^= h >> 15;
+	h *= 0x846ca68bu;
+	h ^= h >> 16;
+	return h;
+}
+
 __device__ __forceinline__ uint32_t pickLight(const DevScene &S, uint32_t offset, uint32_t sample_idx, uint32_t local, uint32_t stride)
 {
 	if(S.n_lights <= 1) return 0u;
-	const uint32_t u = offset + sample_idx * 0x9E3779B1u;
+	// hashed, not linear in the sample number: the sample's low-discrepancy dimensions (sub-pixel
+	// position, BSDF directions) are functions of the same number, and a pick that follows its low
+	// bits would select one light for one stratum of directions — a biased image
+	const uint32_t u = mix32(offset ^ mix32(sample_idx + 0x9E3779B9u));
 	const float hv = haltonFirst(2u, 0.5, S.base_offset + (u * (stride | 1u) + local) - 1u);
 	return (uint32_t)min((int)(hv * (float)S.n_lights), S.n_lights - 1);
 }
@@ -1859,29 +1881,36 @@ __device__ C3 aoSum(const DevScene &S, const float4 *nee, const uint8_t *occ, in
 }
 
 // Sum of one light's entries with the reference's addition order (montecarlo.cc:385-408).
-__device__ C3 neeSum(const DevScene &S, const DevLight &L, const float4 *nee, const uint8_t *occ, int k0)
+// ge(k) / go(k): NEE entry k and its occlusion byte (from memory, or from values loaded earlier)
+template<class GetE, class GetO>
+__device__ __forceinline__ C3 neeSumT(const DevLight &L, int k0, GetE ge, GetO go)
 {
 	if(L.type == LIGHT_POINT)
 	{
-		const float4 e = nee[k0];
+		const float4 e = ge(k0);
 		C3 c = c3(0.f);
-		if(e.w != 0.f && !occ[k0]) c = c + rgb(e);
+		if(e.w != 0.f && !go(k0)) c = c + rgb(e);
 		return c3(0.f) + c;
 	}
 	C3 acc_l = c3(0.f), acc_m = c3(0.f);
 	for(int i = 0; i < L.samples; ++i)
 	{
-		const float4 e = nee[k0 + i];
-		if(e.w != 0.f && !occ[k0 + i]) acc_l = acc_l + rgb(e);
+		const float4 e = ge(k0 + i);
+		if(e.w != 0.f && !go(k0 + i)) acc_l = acc_l + rgb(e);
 	}
 	for(int i = 0; i < L.samples; ++i)
 	{
-		const float4 e = nee[k0 + L.samples + i];
-		if(e.w != 0.f && !occ[k0 + L.samples + i]) acc_m = acc_m + rgb(e);
+		const float4 e = ge(k0 + L.samples + i);
+		if(e.w != 0.f && !go(k0 + L.samples + i)) acc_m = acc_m + rgb(e);
 	}
 	const C3 col_l = acc_l * L.inv_samples;
 	const C3 col_m = acc_m * L.inv_samples;
 	return (c3(0.f) + col_l) + col_m;
+}
+
+__device__ C3 neeSum(const DevScene &S, const DevLight &L, const float4 *nee, const uint8_t *occ, int k0)
+{
+	return neeSumT(L, k0, [&](int k) { return nee[k]; }, [&](int k) { return occ[k] != 0; });
 }
 
 __device__ __forceinline__ float ldsDim(const DevScene &S, int dim, uint32_t n)
@@ -2143,13 +2172,16 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 
 		PHASE(0);
 		// ---- 1. connect the pending next-event estimate ----
+		const int kb = (int)i * K;
+		auto ge = [&](int k) { return Pc.nee[k]; };
+		auto go = [&](int k) { return Pc.occ[k] != 0; };
 		if(live && (flags & F_PEND_V0))
 		{
 			loadCol();
 			col_dirty = true;
 			// estimateAllDirectLight (montecarlo.cc:54-68): col += sum over lights in name order
 			C3 total = c3(0.f);
-			for(int l = 0; l < S.n_lights; ++l) total = total + neeSum(S, S.lights[l], Pc.nee, Pc.occ, (int)i * K + (int)S.lights[l].nee_base);
+			for(int l = 0; l < S.n_lights; ++l) total = total + neeSumT(S.lights[l], kb + (int)S.lights[l].nee_base, ge, go);
 			col = col + total;
 			// DirectLight: col += sampleAmbientOcclusion (integrator_direct_light.cc:124)
 			if(S.do_ao)
@@ -2163,7 +2195,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		{
 			// path_tracer.cc:201-207 / :244-266: lcol = estimateOne * nlights (+ emit); path_col += lcol * thr
 			const int lnum = (int)(flags >> F_LNUM_SHIFT);
-			C3 lcol = neeSum(S, S.lights[lnum], Pc.nee, Pc.occ, (int)i * K) * (float)S.n_lights;
+			C3 lcol = neeSumT(S.lights[lnum], kb, ge, go) * (float)S.n_lights;
 			if(flags & F_PEND_EMIT) lcol = lcol + rgb(pem4);
 			pcol = pcol + lcol * rgb(pthr4);
 		}
@@ -2311,13 +2343,25 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			}
 		}
 		uint32_t lnum = 0;
-		if(nee_one)
+		if(nee_one && S.lpc_mode != 0 && compact)
+		{
+			// integrator_montecarlo.cc:70-78 light pick with the one-thread render's running counter:
+			// the sample's calls are sequential (one entry per sample), so the counter is read and
+			// advanced in place
+			uint32_t *c = &S.lpc[((size_t)sc.y * (size_t)S.width + (size_t)sc.x) * (size_t)S.spp + (size_t)sc.s];
+			const uint32_t n = *c;
+			*c = n + 1u;
+			if(S.lpc_mode == 1) nee_one = false;   // count run: the call is counted, nothing is estimated
+			else lnum = lightOfCounter(S, n);
+		}
+		else if(nee_one)
 		{
 			// integrator_montecarlo.cc:70-78 light pick (pickLight: multi-light PT is matched
 			// statistically, one light exactly)
 			lnum = pickLight(S, offset, sample_idx, (uint32_t)depth + subpath * (uint32_t)S.bounces, n_paths * (uint32_t)(S.bounces + 1));
-			flags = (flags & ((1u << F_LNUM_SHIFT) - 1u)) | (lnum << F_LNUM_SHIFT) | F_PEND_ONE;
 		}
+		if(S.lpc_mode == 1) nee_v0 = false;   // count run: no estimateAllDirectLight either
+		if(nee_one) flags = (flags & ((1u << F_LNUM_SHIFT) - 1u)) | (lnum << F_LNUM_SHIFT) | F_PEND_ONE;
 		if(nee_v0) flags |= F_PEND_V0;
 		const bool pending = (flags & (F_PEND_V0 | F_PEND_ONE)) != 0;
 
@@ -3587,6 +3631,53 @@ __global__ void __launch_bounds__(256) k_done_flags(DevScene S, const DevJob *jo
 	}
 	const SampleCoord c = sampleCoord(jobs, n_jobs, S.width, S.tile, S.spp, (uint64_t)p * (uint64_t)S.spp);
 	flags[(size_t)c.y * S.width + c.x] = p < done_pix ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// light-pick counters (DevScene::lpc, render.cc lpcBases).  A row segment = one row of one tile: its
+// pixels' counters (spp each) are contiguous in the pixel-major layout, and the one-thread render
+// visits them in that order (renderTile, integrator_tiled.cc:281-345: rows, then pixels, then
+// samples).  k_lpc_seg sums each segment of rows [y0, y1); k_lpc_prefix turns each segment's
+// counts into the counter values its samples start from: the segment's base (the calls of every
+// sample visited before the segment, from the host) + the exclusive prefix sum inside it.
+// One wave per segment.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_lpc_seg(const uint32_t *lpc, int W, int spp, int ts, int y0, int y1, uint32_t *seg)
+{
+	const int ntx = (W + ts - 1) / ts;
+	const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) / 64u), lane = (int)(threadIdx.x & 63u);
+	if(wave >= (y1 - y0) * ntx) return;
+	const int y = y0 + wave / ntx, tx = wave % ntx;
+	const int x0 = tx * ts, x1 = min(W, x0 + ts);
+	const size_t b = ((size_t)y * W + x0) * spp, n = (size_t)(x1 - x0) * spp;
+	uint32_t acc = 0;
+	for(size_t k = lane; k < n; k += 64) acc += lpc[b + k];
+	for(int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+	if(lane == 0) seg[(size_t)y * ntx + tx] = acc;
+}
+
+__global__ void __launch_bounds__(256) k_lpc_prefix(uint32_t *lpc, int W, int spp, int ts, int y0, int y1, const uint32_t *segbase)
+{
+	const int ntx = (W + ts - 1) / ts;
+	const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) / 64u), lane = (int)(threadIdx.x & 63u);
+	if(wave >= (y1 - y0) * ntx) return;
+	const int y = y0 + wave / ntx, tx = wave % ntx;
+	const int x0 = tx * ts, x1 = min(W, x0 + ts);
+	const size_t b = ((size_t)y * W + x0) * spp, n = (size_t)(x1 - x0) * spp;
+	uint32_t carry = segbase[(size_t)y * ntx + tx];
+	for(size_t k0 = 0; k0 < n; k0 += 64)
+	{
+		const size_t k = k0 + (size_t)lane;
+		const uint32_t v = k < n ? lpc[b + k] : 0u;
+		uint32_t x = v;
+		for(int off = 1; off < 64; off <<= 1)
+		{
+			const uint32_t t = __shfl_up(x, off);
+			if(lane >= off) x += t;
+		}
+		if(k < n) lpc[b + k] = carry + (x - v);
+		carry += __shfl(x, 63);
+	}
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -5523,6 +5614,22 @@ hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n
 {
 	if(n_pix == 0) return hipSuccess;
 	hipLaunchKernelGGL(k_done_flags, dim3((n_pix + 255) / 256), dim3(256), 0, st, *S, jobs, n_jobs, n_pix, done_pix, flags);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_lpc_seg(const uint32_t *lpc, int W, int spp, int ts, int y0, int y1, uint32_t *seg, hipStream_t st)
+{
+	const int n = (y1 - y0) * ((W + ts - 1) / ts);
+	if(n <= 0) return hipSuccess;
+	hipLaunchKernelGGL(k_lpc_seg, dim3((n + 3) / 4), dim3(256), 0, st, lpc, W, spp, ts, y0, y1, seg);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_lpc_prefix(uint32_t *lpc, int W, int spp, int ts, int y0, int y1, const uint32_t *segbase, hipStream_t st)
+{
+	const int n = (y1 - y0) * ((W + ts - 1) / ts);
+	if(n <= 0) return hipSuccess;
+	hipLaunchKernelGGL(k_lpc_prefix, dim3((n + 3) / 4), dim3(256), 0, st, lpc, W, spp, ts, y0, y1, segbase);
 	return hipGetLastError();
 }
 

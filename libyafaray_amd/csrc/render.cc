@@ -73,6 +73,8 @@ hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev,
 void yafamd_pkd_scratch_free(void *scratch);
 hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix, uint8_t *flags,
                                     hipStream_t st);
+hipError_t yafamd_lpc_seg(const uint32_t *lpc, int W, int spp, int ts, int y0, int y1, uint32_t *seg, hipStream_t st);
+hipError_t yafamd_lpc_prefix(uint32_t *lpc, int W, int spp, int ts, int y0, int y1, const uint32_t *segbase, hipStream_t st);
 hipError_t yafamd_launch_film(const DevFilm *F, const float4 *samples, const uint8_t *flags, float4 *accum, float4 *out,
                               float *weights, int y0, int y1, float clamp_samples, int accumulate, hipStream_t st);
 hipError_t yafamd_aa_next_pass(const float4 *accum, const float *weights, int W, int H, int tile, const DevAaParams *prm,
@@ -298,6 +300,9 @@ struct GpuRenderer::Impl
 	DevQueues Q[2]{};
 	Buf counters, stats;
 	Buf path_next;         // k_path: the chunk's sample counter
+	// estimateOneDirectLight's one-thread light-pick counters (lpcBases): one per sample of the pass,
+	// the row segments' sums and bases, and the count run's own statistics (not the frame's)
+	Buf lpc, lpc_seg, lpc_stats;
 	std::vector<hipEvent_t> ev_pool;   // [0], [1]: the render's start / end; then the profile events
 	// profile mode: HIP events before / after every launch on the render stream
 	bool prof_on = false;
@@ -348,6 +353,7 @@ struct GpuRenderer::Impl
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
+		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &path_next, &lpc, &lpc_seg, &lpc_stats}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
 		              &seg_dir, &seg_colb, &seg_ra, &seg_rb, &seg_rc})
 			b->release();
@@ -824,6 +830,86 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	depth_out = depth;
 	stats_.photon_tree_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+	return true;
+}
+
+// estimateOneDirectLight's light pick in the reference's one-thread order (integrator_montecarlo.cc:70-78
+// with the counter of integrator_tiled.cc:48, reset at render start, :169-171).  The count run left
+// each sample's number of calls in d.lpc (pixel-major, `spp` per pixel).  The one-thread render visits
+// the tiles in rank order and inside a tile the rows, pixels and samples in order, so a sample's
+// counter starts at: the calls of the render's earlier passes + those of every row segment (one tile
+// row) visited before its segment + those of the samples before it in the segment.  The segment sums
+// come from the rows each member owns (a group sums the members' tables: every row has one owner),
+// the bases are laid out on the host in tile order, and k_lpc_prefix writes every counter of the rows
+// [jy0, jy1) this member renders (its band + halo rows).  cut: the count run was canceled (in a group:
+// any member's was): the pass renders nothing.
+bool GpuRenderer::lpcBases(RenderParams &rp, int spp, int jy0, int jy1, bool group_render, bool &cut)
+{
+	Impl &d = *d_;
+	const DevScene &S = rp.scene;
+	const int W = S.width, H = S.height, ts = S.tile, ntx = (W + ts - 1) / ts, nty = (H + ts - 1) / ts;
+	const size_t n_seg = (size_t)H * ntx;
+	if(!ensure(log_, d.lpc_seg, n_seg * 4)) return false;
+	HIPCHECK(hipMemsetAsync(d.lpc_seg.p, 0, n_seg * 4, d.stream));
+	// the rows this member owns: its band in a group (owned_rows_ covers the whole film once the
+	// accumulators were exchanged before an adaptive pass; the halo rows belong to the neighbours)
+	std::vector<std::pair<int, int>> own = owned_rows_;
+	if(group_render) own.assign(1, {std::max(0, rp.shard_y0), std::min(H, rp.shard_y1)});
+	for(const auto &o : own)
+		HIPCHECK(yafamd_lpc_seg((const uint32_t *)d.lpc.p, W, spp, ts, o.first, o.second, (uint32_t *)d.lpc_seg.p, d.stream));
+	lpc_seg_host_.assign(n_seg, 0u);
+	HIPCHECK(hipMemcpyAsync(lpc_seg_host_.data(), d.lpc_seg.p, n_seg * 4, hipMemcpyDeviceToHost, d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	std::vector<uint32_t> seg = lpc_seg_host_;
+	if(group_render)
+	{
+		// every member's table is complete when all have arrived; sum them, and nobody overwrites its
+		// table before everyone summed (the second arrival)
+		const int st = groupStatus(cut ? 1 : 0);
+		if(st >= 2)
+		{
+			log_.error("GPU group: a member failed; render abandoned");
+			return false;
+		}
+		if(peers_ && peers_->size() > 1)
+		{
+			for(int r = 0; r < peers_->size(); ++r)
+			{
+				if(r == peer_rank_) continue;
+				const std::vector<uint32_t> &o = peers_->member(r)->lpc_seg_host_;
+				for(size_t k = 0; k < n_seg && k < o.size(); ++k) seg[k] += o[k];
+			}
+			peers_->arrive(0);
+		}
+		else if(d.comm)
+		{
+			NCCLCHECK(ncclAllReduce(d.lpc_seg.p, d.lpc_seg.p, n_seg, ncclUint32, ncclSum, d.comm, d.stream));
+			HIPCHECK(hipMemcpyAsync(seg.data(), d.lpc_seg.p, n_seg * 4, hipMemcpyDeviceToHost, d.stream));
+			HIPCHECK(hipStreamSynchronize(d.stream));
+		}
+		if(st == 1) cut = true;
+	}
+	if(cut) return true;
+	// bases in the one-thread visiting order: tiles by rank, rows inside a tile
+	std::vector<int> by_rank((size_t)ntx * nty);
+	for(int t = 0; t < ntx * nty; ++t) by_rank[t] = t;
+	if(rp.tile_rank.size() == by_rank.size())
+		for(int t = 0; t < ntx * nty; ++t) by_rank[rp.tile_rank[(size_t)t]] = t;
+	std::vector<uint32_t> base(n_seg, 0u);
+	uint32_t carry = lpc_carry_;
+	for(int t : by_rank)
+	{
+		const int tx = t % ntx, ty = t / ntx;
+		for(int y = ty * ts; y < std::min(H, ty * ts + ts); ++y)
+		{
+			base[(size_t)y * ntx + tx] = carry;
+			carry += seg[(size_t)y * ntx + tx];
+		}
+	}
+	lpc_carry_ = carry;
+	HIPCHECK(hipMemcpyAsync(d.lpc_seg.p, base.data(), n_seg * 4, hipMemcpyHostToDevice, d.stream));
+	HIPCHECK(yafamd_lpc_prefix((uint32_t *)d.lpc.p, W, spp, ts, jy0, jy1, (const uint32_t *)d.lpc_seg.p, d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));   // `base` is consumed
 	return true;
 }
 
@@ -1576,7 +1662,17 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	// shadows, photon maps, AO): one lane per sample, the same functions in the same order, the film
 	// bit-identical.  Measured on C2: 124 ms per frame at its best occupancy vs 73 ms for the wavefront
 	//  — so the wavefront stays the default.
+	// estimateOneDirectLight with several lights (path tracing) picks its light from the one-thread
+	// render's running counter: every pass runs a count run first (lpcBases).  A specular recursion tree
+	// (several integrate() nodes per sample) and caller-side shards (no exchange of the other rows'
+	// counts) keep pickLight; YAFARAY_AMD_LIGHT_PICK=hash forces it.
+	bool lpc_on = S.integrator == INT_PATH && S.n_lights > 1 && !S.tree && (rp.shard_world <= 1 || group_render);
+	if(const char *lp = std::getenv("YAFARAY_AMD_LIGHT_PICK"); lp && std::string(lp) == "hash") lpc_on = false;
+	lpc_carry_ = 0;
+	S.lpc = nullptr;
+	S.lpc_mode = 0;
 	int path_grid = 0;
+	if(!lpc_on)
 	{
 		const char *pe = std::getenv("YAFARAY_AMD_PATH");
 		const bool on = pe && std::string(pe) == "mega";
@@ -1604,15 +1700,18 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	HIPCHECK(hipEventRecord(d.ev_pool[0], d.stream));
 	// one pass: `n_total` camera samples (the jobs' enumeration, or S.plist x S.spp) through the wavefront
 	// one wavefront pass over the active list started by k_camera / k_spawn
+	DevStats *run_stats = dstats;   // the light-pick count runs count into their own statistics
 	auto iterate = [&](uint64_t base) -> bool {
 		int cur = 0;
+		// a light-pick count run (S.lpc_mode 1) follows the paths only: no estimates, no shadow rays
+		const bool count_run = S.lpc_mode == 1;
 		for(int it = 0; it < iters; ++it)
 		{
-			PROF(KK_TRACE, yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], dstats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+			PROF(KK_TRACE, yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], run_stats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 			// material-shade dispatch for textured / smooth scenes: surface attributes + shader nodes
 			// of every hit, before k_shade reads them
 			// transparent shadows: filter colours of the transparent surfaces the shadow rays crossed
-			if(S.tr_shad) PROF(KK_TSHADOW, yafamd_launch_tshadow(&S, &d.Q[cur], &cnt[cur], &d.P[cur], d.stream));
+			if(S.tr_shad && !count_run) PROF(KK_TSHADOW, yafamd_launch_tshadow(&S, &d.Q[cur], &cnt[cur], &d.P[cur], d.stream));
 			if(S.has_attr) PROF(KK_SURFACE, yafamd_launch_surface(&S, &d.Q[cur], &cnt[cur], d.stream));
 			PROF(KK_SHADE, yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &d.G, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
@@ -1622,7 +1721,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// tracing finishes paths in any iteration
 			const bool dl_pipeline = S.integrator != INT_PATH;
 			// (show_map: the camera hits finish in iteration 0, with their nearest-photon requests)
-			if(S.gather_on && (!dl_pipeline || it == 1 || (S.show_map && it == 0)))
+			if(S.gather_on && !count_run && (!dl_pipeline || it == 1 || (S.show_map && it == 0)))
 			{
 				// final gathering adds its estimate to the requests' colour before k_gather ends them
 				if(S.fg_on)
@@ -1641,7 +1740,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 					                                     nullptr, d.stream));
 			}
 			// NEE requests (none in iteration 1 of photon mapping, whose entries all finish there)
-			if((S.ext || !yafamd_shade_fused()) && !(S.integrator == INT_PHOTON && it == 1))
+			if((S.ext || !yafamd_shade_fused()) && !(S.integrator == INT_PHOTON && it == 1) && !count_run)
 				PROF(KK_NEE, yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], nee_trace_stack, d.stream));
 			// (non-EXT k_shade runs the NEE itself: FUSED)
 			cur ^= 1;
@@ -1708,6 +1807,44 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	}
 	return true;
 	};
+	// one pass's samples; with the one-thread light pick a count run first (the paths only: closest
+	// rays and shading, no estimates), then the counters' bases (lpcBases), then the render proper
+	int jy0 = H, jy1 = 0;
+	for(const DevJob &j : jobs)
+	{
+		jy0 = std::min(jy0, j.y0);
+		jy1 = std::max(jy1, j.y1);
+	}
+	auto runPass = [&](uint64_t n_total, int pass_spp) -> bool {
+		if(!lpc_on) return runSamples(n_total);
+		const size_t n_ctr = (size_t)W * H * (size_t)pass_spp;
+		if(!ensure(log_, d.lpc, n_ctr * 4) || !ensure(log_, d.lpc_stats, sizeof(DevStats) * (size_t)d.trace_grid)) return false;
+		HIPCHECK(hipMemsetAsync(d.lpc.p, 0, n_ctr * 4, d.stream));
+		HIPCHECK(hipMemsetAsync(d.lpc_stats.p, 0, sizeof(DevStats) * (size_t)d.trace_grid, d.stream));
+		S.lpc = (uint32_t *)d.lpc.p;
+		S.lpc_mode = 1;
+		S.stats = (DevStats *)d.lpc_stats.p;
+		run_stats = S.stats;
+		auto on_chunk = rp.on_chunk;
+		rp.on_chunk = nullptr;   // progress is reported by the render proper
+		const bool ok = runSamples(n_total);
+		rp.on_chunk = on_chunk;
+		S.stats = dstats;
+		run_stats = dstats;
+		S.lpc_mode = 0;
+		if(!ok) return false;
+		bool cut = done < n_total;
+		if(!lpcBases(rp, pass_spp, jy0, jy1, group_render, cut)) return false;
+		if(cut)
+		{
+			done = 0;   // canceled before the pass rendered anything
+			return true;
+		}
+		S.lpc_mode = 2;
+		const bool ok2 = runSamples(n_total);
+		S.lpc_mode = 0;
+		return ok2;
+	};
 
 	// ---- pass 0 (every pixel), then the adaptive passes (TiledIntegrator::render, integrator_tiled.cc:172-231) ----
 	const int passes = std::max(1, rp.aa.passes);
@@ -1753,7 +1890,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	}
 	else
 	{
-		if(!runSamples(total)) return false;
+		if(!runPass(total, spp)) return false;
 		const uint8_t *done_flags = nullptr;
 		if(done < total)
 		{
@@ -1864,7 +2001,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				rp.film.spp = n_pass;
 				rp.film.sample_offset = S.base_offset + (uint32_t)acum;
 				const uint64_t n_total = (uint64_t)resampled_local * (uint64_t)n_pass;
-				if(!runSamples(n_total)) return false;
+				if(!runPass(n_total, n_pass)) return false;
 				if(done < n_total)
 					HIPCHECK(yafamd_launch_done_flags(&S, (const DevJob *)d.jobs.p, n_jobs, (uint32_t)resampled_local, (uint32_t)(done / (uint64_t)n_pass),
 					                                  (uint8_t *)d.aa_flags.p, d.stream));

@@ -233,6 +233,10 @@ class GpuRenderer
 		bool groupCounts(uint32_t mine, std::vector<uint32_t> &all);
 		bool groupConcat(int kind, const std::vector<uint32_t> &counts);
 		uint32_t seg_count_ = 0;   // this member's photon-map segment count (read by the peers)
+		// estimateOneDirectLight's one-thread counter: bases of a pass's samples from its count run
+		bool lpcBases(RenderParams &rp, int spp, int jy0, int jy1, bool group_render, bool &cut);
+		std::vector<uint32_t> lpc_seg_host_;   // this member's row-segment call counts (read by the peers)
+		uint32_t lpc_carry_ = 0;               // calls of the render's earlier passes
 		Impl *d_;
 		Logger &log_;
 		int device_ = -1;

@@ -3,15 +3,19 @@
 * DirectLightIntegrator and the first vertex of PathIntegrator sum every light
   (estimateAllDirectLight, integrator_montecarlo.cc:54-68, lights in name order): bit-exact against
   the oracle (<= 4 ULP, 0 observed).
-* Later path vertices and final gathering call estimateOneDirectLight (:70-78): ONE light, picked by
-  Halton(2, base_sampling_offset + n - 1) with n a per-thread running counter
-  (integrator_tiled.cc:48, :169-171) — schedule-dependent in the reference itself.  The GPU's pick
-  (kernels.hip pickLight: the pixel's sampling offset and sample number mixed into an odd stride, so
-  every light takes its 1 / num_lights share at every depth) is matched statistically against the
-  oracle's per-thread counter: the paired global z of the difference image within 4 and no 8x8
-  block beyond 6 (oracle/stats.py), for two seeds, area + point lights.  A counter that is the same
-  for every sample (the r03 GPU pick) fails this test: it picks one light per depth for the whole
-  film."""
+* Later path vertices call estimateOneDirectLight (:70-78): ONE light, picked by
+  Halton(2, base_sampling_offset + n - 1) with n a running counter of the calls
+  (integrator_tiled.cc:48, reset at render start :169-171).  The reference keeps one counter per
+  render thread, so n depends on the thread schedule; with one thread it is the number of calls of
+  every sample rendered before.  The GPU reproduces the one-thread counter exactly: a count run
+  follows every path (closest rays and shading only), an exclusive scan in tile order gives each
+  sample its first counter value (render.cc lpcBases), and the render proper takes consecutive values
+  — so Russian roulette off, the image is bit-identical to the one-thread oracle, on one GPU, with
+  adaptive passes and in a device group.  With RR on (RR streams are statistical by design) the
+  image is compared with the 16-thread oracle (per-thread counters) by the paired z test.
+* Final gathering (integrator_photon_mapping.cc:703) and specular recursion trees keep a pick
+  that mixes the pixel and sample into the counter (kernels.hip pickLight): matched statistically.
+"""
 import dataclasses
 
 import numpy as np
@@ -49,12 +53,48 @@ def test_direct_light_all_lights_bitexact(product, oracle_built, n):
     assert u.max() <= 4, f"{(u > 4).sum()} values > 4 ULP"
 
 
+EXACT = {
+    "2-lights": lambda: with_lights(scenes.cornell(96, 72, spp=4, bounces=5, rr=False), 2),
+    "3-lights-paths2": lambda: with_lights(scenes.cornell(80, 64, spp=2, bounces=4, rr=False), 3).with_render(path_samples=2),
+    "3-lights-adaptive": lambda: with_lights(scenes.cornell(64, 48, spp=2, bounces=4, rr=False), 3).with_render(
+        aa_passes=3, aa_inc_samples=2, aa_threshold=0.01),
+    "2-lights-centre-order": lambda: with_lights(scenes.cornell(96, 72, spp=2, bounces=4, rr=False, tile_size=16), 2).with_render(
+        tiles_order="centre"),
+}
+
+
+@pytest.mark.parametrize("case", list(EXACT))
+@pytest.mark.parametrize("members", [1, 3])
+def test_path_multi_light_one_thread_order_bitexact(product, oracle_built, case, members):
+    spec = EXACT[case]()
+    rgba, w, st = product.render_spec(spec, members=members, chunk_slots=4096)
+    orgba, ow, octr = oracle_built.OracleScene(spec, threads=1).render()
+    assert np.array_equal(w, ow)
+    u = _ulp(rgba, orgba)
+    assert u.max() <= 4, f"{(u > 4).sum()} values > 4 ULP"
+
+
+def test_path_multi_light_hash_pick_is_not_the_reference_order(product, oracle_built, monkeypatch):
+    """YAFARAY_AMD_LIGHT_PICK=hash (pickLight) renders a different image (the counter matters)."""
+    spec = EXACT["2-lights"]()
+    monkeypatch.setenv("YAFARAY_AMD_LIGHT_PICK", "hash")
+    rgba, _, _ = product.render_spec(spec)
+    monkeypatch.delenv("YAFARAY_AMD_LIGHT_PICK")
+    orgba, _, _ = oracle_built.OracleScene(spec, threads=1).render()
+    assert _ulp(rgba, orgba).max() > 4
+
+
+@pytest.mark.parametrize("pick", ["counter", "hash"])
 @pytest.mark.parametrize("n", [2, 3])
 @pytest.mark.parametrize("seed", [0, 7919])
-def test_path_multi_light_statistical(product, oracle_built, n, seed):
+def test_path_multi_light_statistical(product, oracle_built, n, seed, pick, monkeypatch):
+    """pick "hash": the fallback pick (recursion trees, final gathering) must be unbiased too."""
     from oracle.stats import paired_z
     spec = with_lights(scenes.cornell(256, 256, spp=64, bounces=8, rr=True), n).with_render(rr_seed=seed)
+    if pick == "hash":
+        monkeypatch.setenv("YAFARAY_AMD_LIGHT_PICK", "hash")
     rgba, w, _ = product.render_spec(spec)
+    monkeypatch.delenv("YAFARAY_AMD_LIGHT_PICK", raising=False)
     orgba, ow, _ = oracle_built.OracleScene(spec, threads=16, rr_seed=seed).render()
     assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
     z = paired_z(rgba, orgba)
