@@ -156,7 +156,10 @@ def lib():
             "yafaray_amd_getKernelTimes": (i, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                                                C.POINTER(C.c_uint64), i]),
         }
+        optional = {"yafaray_amd_buildInfo", "yafaray_amd_getGroupReport"}   # LIBYAFARAY_AMD_1.4 (variant builds of older sources lack them)
         for name, (res, args) in sig.items():
+            if name in optional and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -166,7 +169,8 @@ def lib():
 
 def build_info() -> str:
     """The library's build flags (yafaray_amd_buildInfo): device arch + extra flags, host compiler."""
-    return lib().yafaray_amd_buildInfo().decode()
+    L = lib()
+    return L.yafaray_amd_buildInfo().decode() if hasattr(L, "yafaray_amd_buildInfo") else "unknown (library before LIBYAFARAY_AMD_1.4)"
 
 
 def lib_sha256() -> str:

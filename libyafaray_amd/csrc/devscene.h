@@ -28,7 +28,8 @@ enum : uint32_t { MAT_SHINYDIFFUSE = 0, MAT_LIGHT = 1, MAT_MIRROR = 2, MAT_NULL 
 // ShinyDiffuseMaterial components and options (material_shiny_diffuse.cc:38-87, 548-566)
 enum : uint32_t { SD_MIRROR = 1u, SD_TRANSPARENT = 2u, SD_TRANSLUCENT = 4u, SD_DIFFUSE = 8u, SD_FRESNEL = 16u, SD_TBIAS_MULT = 32u,
                   SD_OREN_NAYAR = 64u };
-enum : uint32_t { LIGHT_POINT = 0, LIGHT_AREA = 1 };
+enum : uint32_t { LIGHT_POINT = 0, LIGHT_AREA = 1, LIGHT_MESH = 2 };
+constexpr int kMeshTriF4 = 7;   // float4 per meshlight face (DevScene::mesh_tris)
 enum : int { INT_DIRECT = 0, INT_PATH = 1, INT_PHOTON = 2 };
 
 struct DevMaterial
@@ -135,6 +136,9 @@ struct DevLight
 	uint32_t nee_base;      // first NEE entry of this light in the estimateAllDirectLight layout
 	uint32_t nee_count;     // point: 1, area: 2 * samples
 	uint32_t shoot;         // bit 0: diffuse photons, bit 1: caustic photons
+	// meshlight / objectlight (light_object_light.cc): triangles [mesh0, mesh0 + mesh_n) of
+	// DevScene::mesh_tris / mesh_cdf (the mesh's faces in creation order), double-sided emission
+	uint32_t mesh0, mesh_n, double_sided, pad0;
 };
 
 struct DevCamera
@@ -172,6 +176,12 @@ struct DevScene
 	int brute;                     // YAFARAY_AMD_TRACE=brute: k_trace_brute tests every triangle of a tiny scene
 	int ray_sort;                  // k_trace orders each wave's window of queue entries by ray kind + direction (LDS counting sort)
 	int lds_nodes, lds_tris;
+	int lds_top;                   // BVH4 in global memory: k_trace stages nodes [0, lds_top) in LDS (the top treelet)
+	// meshlight triangles (DevLight::mesh0 / mesh_n): kMeshTriF4 float4 each — the exact-test record
+	// (v0 + eps, e1 + index, e2), the vertices v0, v1, v2 and the geometric normal — and the area
+	// distribution's normalised cdf (sample_pdf1d.h)
+	const float4 *mesh_tris;
+	const float *mesh_cdf;
 
 	DevCamera cam;
 

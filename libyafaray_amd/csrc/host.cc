@@ -785,6 +785,25 @@ bool Scene::createLight(const std::string &name, const ParamMap &p)
 		L.inv_samples = 1.f / (float)L.samples;
 		L.nee_count = 2 * (uint32_t)L.samples;
 	}
+	else if(type == "meshlight" || type == "objectlight")
+	{
+		// ObjectLight::factory (light_object_light.cc:221-254): color * power * pi, samples 4, the faces
+		// of `object_name` (resolved when the scene is built: ObjectLight::init, :75-87)
+		std::string object_name;
+		int samples = 4;
+		bool dbl = false;
+		p.get("object_name", object_name);
+		p.get("samples", samples);
+		p.get("double_sided", dbl);
+		L.type = LIGHT_MESH;
+		const float pi_f = static_cast<float>(hm::num_pi);
+		for(int k = 0; k < 3; ++k) L.color[k] = (col[k] * power) * pi_f;
+		L.double_sided = dbl ? 1u : 0u;
+		L.samples = std::max(1, (int)std::ceil((float)samples * 1.f));
+		L.inv_samples = 1.f / (float)L.samples;
+		L.nee_count = 2 * (uint32_t)L.samples;   // light samples + material samples (canIntersect)
+		if(enabled && !photon_only) light_objects[name] = object_name;
+	}
 	else
 	{
 		log.error("Scene: light type '" + type + "' is not supported by the GPU core");
@@ -961,6 +980,56 @@ bool Scene::setupRender(const ParamMap &p)
 	return true;
 }
 
+// ObjectLight::initIs (light_object_light.cc:46-73): the faces of the light's object in creation
+// order, their areas (TrianglePrimitive::surfaceArea, primitive_triangle.cc:208-213), the area
+// distribution (sample_pdf1d.h:52-66, the cdf accumulated in double) and the total area (summed in
+// double, stored as float); per face the exact-test record, the vertices and the geometric normal.
+bool Scene::meshLightFaces(const std::string &name, DevLight &L, HostScene &hs)
+{
+	auto lo = light_objects.find(name);
+	auto it = lo == light_objects.end() ? objects.end() : objects.find(lo->second);
+	if(it == objects.end() || it->second.tri_mat.empty())
+	{
+		log.error("Light '" + name + "': object '" + (lo == light_objects.end() ? std::string() : lo->second) + "' not found or empty");
+		return false;
+	}
+	const MeshObject &o = it->second;
+	const size_t nt = o.tri_mat.size();
+	L.mesh0 = (uint32_t)(hs.mesh_cdf.size());
+	L.mesh_n = (uint32_t)nt;
+	std::vector<float> areas(nt);
+	double total = 0.0;
+	for(size_t t = 0; t < nt; ++t)
+	{
+		const F3 a = f3(&o.verts[3 * (size_t)o.tris[3 * t]]), b = f3(&o.verts[3 * (size_t)o.tris[3 * t + 1]]),
+		         c = f3(&o.verts[3 * (size_t)o.tris[3 * t + 2]]);
+		areas[t] = 0.5f * std::sqrt(lsq(crs(sub(b, a), sub(c, a))));
+		total += areas[t];
+		float rec[kMeshTriF4 * 4];
+		packTriangle(&o.verts[3 * (size_t)o.tris[3 * t]], &o.verts[3 * (size_t)o.tris[3 * t + 1]], &o.verts[3 * (size_t)o.tris[3 * t + 2]], (int)t, rec);
+		put(rec + 12, a);
+		put(rec + 16, b);
+		put(rec + 20, c);
+		put(rec + 24, nrm(crs(sub(b, a), sub(c, a))));
+		hs.mesh_tris.insert(hs.mesh_tris.end(), rec, rec + kMeshTriF4 * 4);
+	}
+	const double delta = 1.0 / static_cast<double>(nt);
+	double cum = 0.0;
+	std::vector<float> cdf(nt);
+	for(size_t t = 0; t < nt; ++t)
+	{
+		cum += static_cast<double>(areas[t]) * delta;
+		cdf[t] = static_cast<float>(cum);
+	}
+	const float integral = static_cast<float>(cum);
+	for(float &e : cdf) e /= integral;
+	hs.mesh_cdf.insert(hs.mesh_cdf.end(), cdf.begin(), cdf.end());
+	L.area = static_cast<float>(total);
+	if(nt > 4096)
+		log.warning("Light '" + name + "': " + std::to_string(nt) + " faces; the material-sampled rays test every face of the light");
+	return true;
+}
+
 bool Scene::buildAccelerator()
 {
 	if(!syncMembers()) return false;
@@ -1094,7 +1163,12 @@ bool Scene::buildAccelerator()
 			}
 		}
 	}
-	for(auto &kv : lights) hs.lights.push_back(kv.second);
+	for(auto &kv : lights)
+	{
+		DevLight L = kv.second;
+		if(L.type == LIGHT_MESH && !meshLightFaces(kv.first, L, hs)) return false;
+		hs.lights.push_back(L);
+	}
 	uint32_t base = 0;
 	for(DevLight &L : hs.lights) { L.nee_base = base; base += L.nee_count; }
 	for(int m = 0; m < memberCount(); ++m)

@@ -17,6 +17,8 @@
 
 namespace yafamd
 {
+struct HostScene;
+
 
 // ---- ParamMap (include/common/param.h:38-112: strictly typed getVal) ----
 struct Param
@@ -195,6 +197,7 @@ class Scene
 		std::map<std::string, int> material_index;    // creation order index
 		std::vector<std::string> material_order;
 		std::map<std::string, DevLight> lights;        // std::map: name order (render_view.cc:61)
+		std::map<std::string, std::string> light_objects;   // meshlight / objectlight -> its object (resolved when the scene is built)
 		std::map<std::string, MeshObject> objects;
 		std::vector<std::string> object_order;
 		std::map<std::string, CameraDesc> cameras;
@@ -262,6 +265,7 @@ class Scene
 
 	private:
 		bool renderDeviceGroup(RenderParams &rp);
+		bool meshLightFaces(const std::string &name, DevLight &L, HostScene &hs);
 		std::unique_ptr<GpuRenderer> gpu_;
 		std::vector<std::unique_ptr<GpuRenderer>> extra_;   // device group members 1..
 		std::vector<int> member_devs_;                      // devices of the current members

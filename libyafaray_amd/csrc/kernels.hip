@@ -381,6 +381,10 @@ struct TraceCtx
 	int lds_depth;
 	int *spill;     // HBM, [(level - lds_depth) * spill_stride + global lane] (BVH4 deep levels)
 	uint32_t spill_stride;
+	// the top treelet of a BVH4 in global memory staged in LDS: nodes [0, n_top) (both builders number
+	// the wide nodes level by level, so these are the levels every ray starts with)
+	const float4 *top = nullptr;
+	int n_top = 0;
 };
 
 // Transparent-shadow hit list of one shadow ray (accelerator_kdtree.cc:1001-1023): an opaque
@@ -762,8 +766,24 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 			node = 0;
 		}
 		if(STATS) TRACE_STAT(++visits);
-		const float4 *np = C.nodes + 8 * node;
-		const float4 nx = np[sel.nx], fx = np[sel.nx ^ 1], ny = np[sel.ny], fy = np[sel.ny ^ 1], nz = np[sel.nz], fz = np[sel.nz ^ 1], cf = np[6], kf = np[7];
+		float4 nx, fx, ny, fy, nz, fz, cf, kf;
+		if(node < C.n_top)
+		{
+			// the top treelet from LDS (an explicit LDS pointer: ds_read, not flat loads)
+			typedef float V4 __attribute__((ext_vector_type(4)));
+			typedef const __attribute__((address_space(3))) V4 *LdsV4;
+			const LdsV4 tp = (LdsV4)(C.top + 8 * node);
+			auto ld = [&](int k) {
+				const V4 v = tp[k];
+				return make_float4(v.x, v.y, v.z, v.w);
+			};
+			nx = ld(sel.nx); fx = ld(sel.nx ^ 1); ny = ld(sel.ny); fy = ld(sel.ny ^ 1); nz = ld(sel.nz); fz = ld(sel.nz ^ 1); cf = ld(6); kf = ld(7);
+		}
+		else
+		{
+			const float4 *np = C.nodes + 8 * node;
+			nx = np[sel.nx]; fx = np[sel.nx ^ 1]; ny = np[sel.ny]; fy = np[sel.ny ^ 1]; nz = np[sel.nz]; fz = np[sel.nz ^ 1]; cf = np[6]; kf = np[7];
+		}
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
 		float key[4];
 		int child[4], e[4], s4[4];
@@ -964,6 +984,15 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	{
 		C.nodes = S.nodes;
 		C.tris = S.tris;
+		if(WIDE && S.lds_top > 0)
+		{
+			// the top treelet (refill loop only): nodes [0, lds_top) after the stack
+			float4 *top = smem + (stack_depth * kTraceBlock) / 4;
+			for(int k = threadIdx.x; k < 8 * S.lds_top; k += blockDim.x) top[k] = S.nodes[k];
+			__syncthreads();
+			C.top = top;
+			C.n_top = S.lds_top;
+		}
 	}
 	const SegLoop L = segLoop(S.n_seg);
 	const uint32_t n_a = cnt.n_active[L.s], n_s = cnt.n_shadow[L.s];
@@ -1653,6 +1682,130 @@ __device__ __forceinline__ void tsFactors(float4 *ts, int e, C3 surf, float a, C
 // nee[base ...] and emits the shadow rays.  integrator_montecarlo.cc:80-408.
 // Wave-uniform structure: `active` lanes do the work, every lane of the wave walks the same loop
 // bounds (the shadow-ray appends are wave-level).
+// ---- meshlight / objectlight (light_object_light.cc) ----
+// ObjectLight::sampleSurface (:89-107): a face by the area distribution (Pdf1D::dSample, a
+// lower_bound over the cdf), s_1 rescaled inside its cdf step, then TrianglePrimitive::sample
+// (primitive_triangle.cc:220-234) and the face's geometric normal
+__device__ __forceinline__ void meshSampleSurface(const DevScene &S, const DevLight &L, float s_1, float s_2, V3 &p, V3 &n)
+{
+	const float *cdf = S.mesh_cdf + L.mesh0;
+	const int nt = (int)L.mesh_n;
+	int k;
+	if(s_1 <= 0.f) k = 0;
+	else if(s_1 >= 1.f) k = nt - 1;
+	else
+	{
+		int lo = 0, hi = nt;   // first index with cdf >= s_1 (std::lower_bound)
+		while(lo < hi)
+		{
+			const int mid = (lo + hi) >> 1;
+			if(cdf[mid] < s_1) lo = mid + 1;
+			else hi = mid;
+		}
+		k = lo;
+	}
+	if(k >= nt)
+	{
+		// the reference's "Sampling error" branch: default point and normal
+		p = v3(0.f, 0.f, 0.f);
+		n = p;
+		return;
+	}
+	float delta = cdf[k], ss_1;
+	if(k > 0)
+	{
+		delta -= cdf[k - 1];
+		ss_1 = (s_1 - cdf[k - 1]) / delta;
+	}
+	else ss_1 = s_1 / delta;
+	const float4 *t = S.mesh_tris + (size_t)kMeshTriF4 * (L.mesh0 + (uint32_t)k);
+	const V3 v0 = xyz(t[3]), v1 = xyz(t[4]), v2 = xyz(t[5]);
+	n = xyz(t[6]);
+	const float su_1 = sqrtf(ss_1);
+	const float u = 1.f - su_1;
+	const float v = s_2 * su_1;
+	p = (u * v0 + v * v1) + (1.f - u - v) * v2;
+}
+
+// The light-sample half of areaLightSampleLight for an area light (light_area.cc:66-96) or a mesh
+// light (light_object_light.cc:111-146): direction and distance to the sampled point and the pdf.
+__device__ __forceinline__ bool lightIllumSample(const DevScene &S, const DevLight &L, V3 sp_p, float s_1, float s_2, V3 &ldir, float &dist, float &pdf)
+{
+	V3 p, fn;
+	if(L.type == LIGHT_MESH) meshSampleSurface(S, L, s_1, s_2, p, fn);
+	else
+	{
+		p = lv(L.pos) + s_1 * lv(L.to_x) + s_2 * lv(L.to_y);
+		fn = lv(L.fnormal);
+	}
+	ldir = p - sp_p;
+	const float dist_sqr = lengthSqr(ldir);
+	dist = sqrtf(dist_sqr);
+	if((double)dist <= 0.0) return false;
+	ldir = ldir * rcpExact(dist);
+	if(L.type == LIGHT_MESH)
+	{
+		float cos_angle = -dot(ldir, fn);
+		if(cos_angle <= 0)
+		{
+			if(L.double_sided) cos_angle = -cos_angle;
+			else return false;
+		}
+		const float amc = L.area * cos_angle;
+		pdf = x87mulDiv(kPi, dist_sqr, (amc == 0.f) ? 1e-8f : amc);
+		return true;
+	}
+	const float cos_angle = dot(ldir, fn);
+	if(cos_angle <= 0) return false;
+	pdf = x87mulDiv(kPi, dist_sqr, L.area * cos_angle);
+	return true;
+}
+
+// Light::intersect of areaLightSampleMaterial's material-sampled ray (origin p, direction dir, tmin
+// b_tmin): the light's pdf and the shadow ray's t (< 0: unbounded).  Area light: light_area.cc:137-151.
+// Mesh light: light_object_light.cc:183-201 — the closest face (the light's own kd-tree, faces with
+// t >= tmin) gives the normal; the reference never stores the hit distance in `t` (the caller's ray
+// tmax, -1), so 1 / (t * t) is 1 and the shadow ray is unbounded: both reproduced.
+__device__ __forceinline__ bool lightMatHit(const DevScene &S, const DevLight &L, V3 p, V3 dir, float b_tmin, float &t, float &light_pdf)
+{
+	if(L.type == LIGHT_MESH)
+	{
+		float t_best = __builtin_huge_valf();
+		int best = -1;
+		const float4 *tr = S.mesh_tris + (size_t)kMeshTriF4 * L.mesh0;
+		for(int k = 0; k < (int)L.mesh_n; ++k)
+		{
+			const float th = triTest(tr[kMeshTriF4 * k], tr[kMeshTriF4 * k + 1], tr[kMeshTriF4 * k + 2], p, dir, t_best);
+			if(th != -1.f && th >= b_tmin && th < t_best)
+			{
+				t_best = th;
+				best = k;
+			}
+		}
+		if(best < 0) return false;
+		const V3 n = xyz(tr[kMeshTriF4 * best + 6]);
+		float cos_angle = -dot(dir, n);
+		if(cos_angle <= 0.f)
+		{
+			if(L.double_sided) cos_angle = fabsf(cos_angle);
+			else return false;
+		}
+		t = -1.f;
+		light_pdf = x87mul(kDiv1ByPi, 1.f * L.area * cos_angle);
+		return true;
+	}
+	const V3 fn = lv(L.fnormal);
+	const float cos_angle = dot(dir, fn);
+	if(cos_angle <= 0) return false;
+	if(!areaTri(lv(L.pos), lv(L.c2), lv(L.c3), p, dir, t))
+	{
+		if(!areaTri(lv(L.pos), lv(L.c3), lv(L.c4), p, dir, t)) return false;
+	}
+	if(!(t > 1.0e-10f)) return false;
+	light_pdf = x87mul(kDiv1ByPi, rcpExact(t * t) * L.area * cos_angle);
+	return true;
+}
+
 template<bool EXT, class Out>
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
@@ -1694,7 +1847,6 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 	const uint32_t l_offs = loffs * 4567u;
 	const int num_samples = L.samples;
 	const uint32_t offs = (uint32_t)num_samples * sample_idx + offset + l_offs;
-	const V3 corner = lv(L.pos), to_x = lv(L.to_x), to_y = lv(L.to_y), fn = lv(L.fnormal);
 	const C3 lcolor = C3{L.color[0], L.color[1], L.color[2]};
 	// areaLightSampleLight (montecarlo.cc:156-282) and areaLightSampleMaterial (:284-383) draw the
 	// same Halton(2/3) sequences from setStart(offs - 1) (:399-403): computed once for both
@@ -1720,22 +1872,11 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 		float st = 0.f;
 		if(ok)
 		{
-			// light_area.cc:66-96
-			const V3 p = corner + s_1 * to_x + s_2 * to_y;
-			ldir = p - sp.p;
-			const float dist_sqr = lengthSqr(ldir);
-			const float dist = sqrtf(dist_sqr);
-			if((double)dist <= 0.0) ok = false;
-			float cos_angle = 0.f;
+			// light_area.cc:66-96 / light_object_light.cc:111-146
+			float dist = 0.f, pdf = 0.f;
+			ok = lightIllumSample(S, L, sp.p, s_1, s_2, ldir, dist, pdf);
 			if(ok)
 			{
-				ldir = ldir * rcpExact(dist);
-				cos_angle = dot(ldir, fn);
-				if(cos_angle <= 0) ok = false;
-			}
-			if(ok)
-			{
-				const float pdf = x87mulDiv(kPi, dist_sqr, L.area * cos_angle);
 				if(pdf > 1e-6f)
 				{
 					const C3 surf_col = matEval<EXT>(m, sp, wo, ldir, B_ALL);
@@ -1780,21 +1921,16 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			float W = 0.f;
 			const C3 surf_col = matSample<EXT>(m, sp, wo, dir, s, W);
 			ok = s.pdf > 1e-6f;
-			float t = 0.f, cos_angle = 0.f;
+			float t = 0.f, lpdf = 0.f;
 			if(ok)
 			{
 				// light_area.cc:137-151
-				cos_angle = dot(dir, fn);
-				if(cos_angle <= 0) ok = false;
-				else if(!areaTri(corner, lv(L.c2), lv(L.c3), sp.p, dir, t))
-				{
-					if(!areaTri(corner, lv(L.c3), lv(L.c4), sp.p, dir, t)) ok = false;
-				}
-				if(ok && !(t > 1.0e-10f)) ok = false;
+				// light_area.cc:137-151 / light_object_light.cc:183-201
+				ok = lightMatHit(S, L, sp.p, dir, b_tmin, t, lpdf);
 			}
 			if(ok)
 			{
-				const float light_pdf = x87mul(kDiv1ByPi, rcpExact(t * t) * L.area * cos_angle);
+				const float light_pdf = lpdf;
 				if(light_pdf > 1e-6f)
 				{
 					const float l_pdf = rcpExact(light_pdf);
@@ -3804,6 +3940,22 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 			d = sphereDir(s_1, s_2);
 			light_pdf = x87mul(kPi, 4.0f);
 		}
+		else if(L.type == LIGHT_MESH)
+		{
+			// light_object_light.cc:148-163
+			light_pdf = L.area;
+			V3 n;
+			meshSampleSurface(S, L, s_3, s_4, o, n);
+			V3 cu, cv;
+			coordsSystem(n, cu, cv);
+			if(L.double_sided)
+			{
+				light_pdf *= 2.f;
+				if(s_1 > 0.5f) d = cosHemisphere(-n, cu, cv, (s_1 - 0.5f) * 2.f, s_2);
+				else d = cosHemisphere(n, cu, cv, s_1 * 2.f, s_2);
+			}
+			else d = cosHemisphere(n, cu, cv, s_1, s_2);
+		}
 		else
 		{
 			light_pdf = L.area;
@@ -4815,7 +4967,6 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 	const uint32_t l_offs = loffs * 4567u;
 	const int num_samples = L.samples;
 	const uint32_t offs = (uint32_t)num_samples * sample_idx + offset + l_offs;
-	const V3 corner = lv(L.pos), to_x = lv(L.to_x), to_y = lv(L.to_y), fn = lv(L.fnormal);
 	const C3 lcolor = C3{L.color[0], L.color[1], L.color[2]};
 	HaltonInc<2> hal_2;
 	HaltonInc<3> hal_3;
@@ -4828,23 +4979,13 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 	{
 		const float s_1 = hal_2.next();
 		const float s_2 = hal_3.next();
-		// areaLightSampleLight (montecarlo.cc:156-282), light_area.cc:66-96
+		// areaLightSampleLight (montecarlo.cc:156-282), light_area.cc:66-96 / light_object_light.cc:111-146
 		{
-			const V3 p = corner + s_1 * to_x + s_2 * to_y;
-			V3 ldir = p - sp.p;
-			const float dist_sqr = lengthSqr(ldir);
-			const float dist = sqrtf(dist_sqr);
-			bool ok = !((double)dist <= 0.0);
-			float cos_angle = 0.f;
+			V3 ldir = v3(0.f, 0.f, 1.f);
+			float dist = 0.f, pdf = 0.f;
+			const bool ok = lightIllumSample(S, L, sp.p, s_1, s_2, ldir, dist, pdf);
 			if(ok)
 			{
-				ldir = ldir * rcpExact(dist);
-				cos_angle = dot(ldir, fn);
-				if(cos_angle <= 0) ok = false;
-			}
-			if(ok)
-			{
-				const float pdf = x87mulDiv(kPi, dist_sqr, L.area * cos_angle);
 				if(pdf > 1e-6f)
 				{
 					const C3 surf_col = matEval<EXT>(m, sp, wo, ldir, B_ALL);
@@ -4878,20 +5019,15 @@ __device__ C3 lightEstimateInline(const DevScene &S, const TraceCtx &C, const De
 			V3 dir = v3(0.f, 0.f, 1.f);
 			const C3 surf_col = matSample<EXT>(m, sp, wo, dir, s, W);
 			bool ok = s.pdf > 1e-6f;
-			float t = 0.f, cos_angle = 0.f;
+			float t = 0.f, lpdf = 0.f;
 			if(ok)
 			{
-				cos_angle = dot(dir, fn);
-				if(cos_angle <= 0) ok = false;
-				else if(!areaTri(corner, lv(L.c2), lv(L.c3), sp.p, dir, t))
-				{
-					if(!areaTri(corner, lv(L.c3), lv(L.c4), sp.p, dir, t)) ok = false;
-				}
-				if(ok && !(t > 1.0e-10f)) ok = false;
+				// light_area.cc:137-151 / light_object_light.cc:183-201
+				ok = lightMatHit(S, L, sp.p, dir, b_tmin, t, lpdf);
 			}
 			if(ok)
 			{
-				const float light_pdf = x87mul(kDiv1ByPi, rcpExact(t * t) * L.area * cos_angle);
+				const float light_pdf = lpdf;
 				if(light_pdf > 1e-6f)
 				{
 					const float l_pdf = rcpExact(light_pdf);
@@ -5190,7 +5326,8 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 {
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	const bool wide = S->node_f4 == 8;
-	const size_t lds_scene = S->scene_in_lds ? (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) : 0;
+	const size_t lds_scene = S->scene_in_lds ? (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4)
+	                                         : (wide ? (size_t)S->lds_top * 8 * sizeof(float4) : 0);
 	const size_t bytes = stack_bytes + lds_scene;
 	if(S->brute && !S->tr_shad && S->n_tris <= kBruteTris)
 	{

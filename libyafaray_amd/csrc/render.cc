@@ -260,6 +260,7 @@ struct GpuRenderer::Impl
 	int n_cph_lights = 0;
 	Buf cph_pos, cph_dir, cph_colb, cpk_nodes;   // caustic photon map + kd-tree
 	Buf tile_rank, pfilm;                        // tile order ranks; partial film of the per-tile callbacks
+	Buf mesh_tris, mesh_cdf;                     // meshlight faces and area distributions
 	int c_photons = 0, c_paths = 0, c_depth = 0;
 	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
 	Buf ph_pos, ph_dir, ph_colb, pk_nodes, pk_stack;
@@ -286,6 +287,7 @@ struct GpuRenderer::Impl
 	int lds_stack = 32;    // k_trace stack levels held in LDS; levels [lds_stack, stack_depth) spill to `spill`
 	Buf spill;
 	bool scene_in_lds = false;
+	int lds_top = 0;   // BVH4 in global memory: nodes k_trace stages in LDS (the top treelet)
 	int faure_bytes = 0;
 	// frame buffers
 	Buf samples, film, weights, jobs;
@@ -353,7 +355,7 @@ struct GpuRenderer::Impl
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
-		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &path_next, &lpc, &lpc_seg, &lpc_stats}) b->release();
+		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
 		              &seg_dir, &seg_colb, &seg_ra, &seg_rb, &seg_rc})
 			b->release();
@@ -528,6 +530,12 @@ bool GpuRenderer::upload(HostScene &hs)
 	if(!allocCopy(log_, d.mats, hs.mats.data(), hs.mats.size())) return false;
 	if(!allocCopy(log_, d.lights, hs.lights.data(), hs.lights.size())) return false;
 	d.host_lights = hs.lights;
+	if(!hs.mesh_cdf.empty())
+	{
+		if(!allocCopy(log_, d.mesh_tris, hs.mesh_tris.data(), hs.mesh_tris.size()) || !allocCopy(log_, d.mesh_cdf, hs.mesh_cdf.data(), hs.mesh_cdf.size()))
+			return false;
+	}
+	else for(Buf *b : {&d.mesh_tris, &d.mesh_cdf}) b->release();
 	d.has_attr = hs.has_attr;
 	d.n_textures = (int)hs.textures.size();
 	if(hs.has_attr)
@@ -555,8 +563,11 @@ bool GpuRenderer::upload(HostScene &hs)
 				const DevLight &L = hs.lights[i];
 				if(!(L.shoot & (1u << set))) continue;
 				float e[3];
+				// point: 4 pi color; area: color * area; mesh (light_object_light.cc:109): double-sided ? 2 color area : color area
 				for(int k = 0; k < 3; ++k)
-					e[k] = (L.type == LIGHT_POINT) ? static_cast<float>(3.14159265358979323846264338327950288L) * (4.0f * L.color[k]) : L.area * L.color[k];
+					e[k] = (L.type == LIGHT_POINT)   ? static_cast<float>(3.14159265358979323846264338327950288L) * (4.0f * L.color[k])
+					       : (L.type == LIGHT_MESH) ? (L.double_sided ? (2.f * L.color[k]) * L.area : L.color[k] * L.area)
+					                                : L.area * L.color[k];
 				func.push_back((e[0] + e[1] + e[2]) * 0.333333f);
 				idx.push_back(i);
 			}
@@ -590,9 +601,19 @@ bool GpuRenderer::upload(HostScene &hs)
 	const size_t scene_bytes = (size_t)(d.node_f4 * d.n_nodes + 3 * d.n_tris) * 16;
 	d.scene_in_lds = scene_bytes + (size_t)d.lds_stack * yafamd_trace_block() * 4 <= 48 * 1024;
 	if(const char *e = getenv("YAFARAY_AMD_SCENE_LDS"); e && *e == '0') d.scene_in_lds = false;   // tests: global-memory traversal on small scenes
+	// a BVH4 in global memory: k_trace's refill loop reads the top treelet (the first levels, which
+	// every ray visits) from LDS — 21 nodes = the root and two full levels below it, 2.7 KB per
+	// workgroup; YAFARAY_AMD_LDS_TOP=n stages n nodes (0: none)
+	d.lds_top = 0;
+	if(d.node_f4 == 8 && !d.scene_in_lds)
 	{
-		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy))
-		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : 0);
+		int top = 21;
+		if(const char *e = getenv("YAFARAY_AMD_LDS_TOP"); e && *e) top = std::max(0, atoi(e));
+		d.lds_top = std::min(top, d.n_nodes);
+	}
+	{
+		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy or top treelet))
+		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : (size_t)d.lds_top * 128);
 		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, d.node_f4 == 8 ? 1 : 0, dyn));
 		if(const char *e = getenv("YAFARAY_AMD_TRACE_GRID")) d.trace_grid = std::max(1, atoi(e));
 		// a whole number of workgroups per queue segment
@@ -651,6 +672,8 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.prim_ng = (const float4 *)d.prim_ng.p;
 	S.mats = (const DevMaterial *)d.mats.p;
 	S.lights = (const DevLight *)d.lights.p;
+	S.mesh_tris = (const float4 *)d.mesh_tris.p;
+	S.mesh_cdf = (const float *)d.mesh_cdf.p;
 	S.faure = (const uint8_t *)d.faure.p;
 	S.faure_bytes = d.faure_bytes;
 	// materials + per-primitive normals staged in LDS by k_shade / k_nee when they are small
@@ -663,6 +686,7 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.n_mats = d.n_mats;
 	S.n_lights = d.n_lights;
 	S.scene_in_lds = d.scene_in_lds ? 1 : 0;
+	S.lds_top = d.lds_top;
 	// YAFARAY_AMD_TRACE=brute: scenes of at most 64 triangles test every triangle (k_trace_brute).
 	// Measured slower than the BVH on C2 (k_trace 39.0 vs 34.7 ms per frame: 34 exact triangle
 	// tests per ray at full lane occupancy cost more than ~3.4 node + 3.3 triangle visits at 0.35),
@@ -1495,7 +1519,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		uint32_t base = 0, max_one = 1;
 		for(DevLight &L : ls)
 		{
-			if(L.type == LIGHT_AREA)
+			if(L.type == LIGHT_AREA || L.type == LIGHT_MESH)
 			{
 				L.samples = (int)ceilf((float)L.samples * mult);
 				L.inv_samples = 1.f / (float)L.samples;

@@ -32,6 +32,8 @@ struct HostScene
 	std::vector<float> prim_ng;          // 4 floats per primitive
 	std::vector<DevMaterial> mats;
 	std::vector<DevLight> lights;        // render order (by name)
+	std::vector<float> mesh_tris;        // meshlight faces: kMeshTriF4 float4 each (DevScene::mesh_tris)
+	std::vector<float> mesh_cdf;         // their area distributions' normalised cdf, per light
 	int n_prims = 0;
 	// surface attributes / textures / shader nodes (texeval.h), only when has_attr
 	bool has_attr = false;

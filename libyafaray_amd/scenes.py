@@ -86,6 +86,8 @@ class Light:
     cast_shadows: bool = True
     with_caustic: bool = True              # shoots caustic photons (light_area.cc / light_point.cc params)
     with_diffuse: bool = True              # shoots diffuse photons
+    object_name: str = ""                  # meshlight / objectlight: the emitting object
+    double_sided: bool = False             # meshlight
 
 
 @dataclass
@@ -293,6 +295,32 @@ def cornell(width=1920, height=1080, spp=64, bounces=8, rr=False, integrator="pa
                   aa_pixelwidth=pixelwidth, tile_size=tile_size, bounces=bounces, path_samples=1,
                   rr_min_bounces=(0 if rr else bounces), caustic_type="none")
     return SceneSpec(verts, tris, tri_mat, mats, [light], cam, rend, Background((0.0, 0.0, 0.0), 1.0), b.objects)
+
+
+def cornell_meshlight(width=96, height=72, spp=4, bounces=4, rr=False, integrator="pathtracing", shape="panel",
+                      double_sided=False, samples=2, keep_area=False, power=3.0, **kw) -> SceneSpec:
+    """The Cornell box lit by a meshlight (light_object_light.cc): an emitting object with a light_mat
+    material whose faces the light samples.  shape "panel": a 0.6 x 0.6 quad (2 faces) under the
+    ceiling facing down; "sphere": a low-poly UV sphere (72 faces of different areas) hanging in the
+    box.  keep_area: the box's area light stays as a second light."""
+    s = cornell(width, height, spp=spp, bounces=bounces, rr=rr, integrator=integrator, **kw)
+    if shape == "panel":
+        lv, lt = _quad((-0.3, -0.3, 1.9), (-0.3, 0.3, 1.9), (0.3, 0.3, 1.9), (0.3, -0.3, 1.9))
+        lv = np.asarray(lv, np.float32)
+        lt = np.asarray(lt, np.int32)
+    else:
+        lv, lt = uv_sphere(6, center=(0.35, -0.3, 1.45), r=0.18)
+    mats = list(s.materials) + [Material("lamp", type="light_mat", color=(1.0, 0.9, 0.75), power=power, double_sided=double_sided)]
+    v0 = len(s.verts)
+    verts = np.concatenate([s.verts, np.asarray(lv, np.float32)])
+    tris = np.concatenate([s.tris, np.asarray(lt, np.int32) + v0])
+    tri_mat = np.concatenate([s.tri_mat, np.full(len(lt), len(mats) - 1, np.int32)])
+    objs = list(s.objects) + [Object("lamp_mesh", v0, len(lv), len(s.tris), len(lt))]
+    ml = Light("lamp", type="meshlight", color=(1.0, 0.9, 0.75), power=power, object_name="lamp_mesh", double_sided=double_sided,
+               samples=samples)
+    lights = (list(s.lights) if keep_area else []) + [ml]
+    import dataclasses
+    return dataclasses.replace(s, verts=verts, tris=tris, tri_mat=tri_mat, materials=mats, lights=lights, objects=objs)
 
 
 def cornell_photon(width=1920, height=1080, spp=1, photons=10_000_000, search=50, radius=0.1, bounces=5,
@@ -511,6 +539,10 @@ def apply(spec: SceneSpec, api) -> None:
             api.paramsSetBool("with_diffuse", False)
         if l.type == "pointlight":
             api.paramsSetVector("from", *l.from_)
+        elif l.type in ("meshlight", "objectlight"):
+            api.paramsSetString("object_name", l.object_name)
+            api.paramsSetBool("double_sided", l.double_sided)
+            api.paramsSetInt("samples", l.samples)
         else:
             api.paramsSetVector("corner", *l.corner)
             api.paramsSetVector("point1", *l.point1)

@@ -17,7 +17,7 @@ ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libyafref_prims.so")
 
 YC_MAT_SHINYDIFFUSE, YC_MAT_LIGHT = 0, 1
-YC_LIGHT_POINT, YC_LIGHT_AREA = 0, 1
+YC_LIGHT_POINT, YC_LIGHT_AREA, YC_LIGHT_MESH = 0, 1, 2
 YC_INT_DIRECT, YC_INT_PATH, YC_INT_PHOTON = 0, 1, 2
 FILTERS = {"box": 0, "gauss": 1, "mitchell": 2, "lanczos": 3}
 
@@ -63,7 +63,8 @@ class yc_object(C.Structure):
 class yc_light(C.Structure):
     _fields_ = [("type", C.c_int), ("color", C.c_float * 3), ("power", C.c_float), ("from_", C.c_float * 3),
                 ("point1", C.c_float * 3), ("point2", C.c_float * 3), ("samples", C.c_int),
-                ("cast_shadows", C.c_int), ("shoot_caustic", C.c_int), ("shoot_diffuse", C.c_int)]
+                ("cast_shadows", C.c_int), ("shoot_caustic", C.c_int), ("shoot_diffuse", C.c_int),
+                ("object", C.c_int), ("double_sided", C.c_int)]
 
 
 class yc_camera(C.Structure):
@@ -546,7 +547,10 @@ class OracleScene:
             mats[i].sigma_shader = -1
         lights = (yc_light * max(1, len(s.lights)))()
         for i, l in enumerate(s.render_lights()):
-            lights[i].type = YC_LIGHT_POINT if l.type == "pointlight" else YC_LIGHT_AREA
+            lights[i].type = {"pointlight": YC_LIGHT_POINT, "meshlight": YC_LIGHT_MESH, "objectlight": YC_LIGHT_MESH}.get(l.type, YC_LIGHT_AREA)
+            if lights[i].type == YC_LIGHT_MESH:
+                lights[i].object = [o.name for o in s.objects].index(l.object_name)
+                lights[i].double_sided = int(l.double_sided)
             lights[i].color[:] = list(l.color)
             lights[i].power = l.power
             lights[i].from_[:] = list(l.from_ if l.type == "pointlight" else l.corner)

@@ -488,6 +488,10 @@ struct Light
 	float area = 0.f, inv_area = 0.f;
 	int samples = 1;
 	bool shoot_caustic = true, shoot_diffuse = true;   // "with_caustic" / "with_diffuse"
+	// meshlight (light_object_light.cc:46-73): the object's faces, their area cdf (sample_pdf1d.h)
+	std::vector<V3> mv0, mv1, mv2, mng;
+	std::vector<float> mcdf;
+	bool double_sided = false;
 };
 
 struct Tri
@@ -815,6 +819,13 @@ Scene::Scene(const yc_scene &s)
 			L.position = V3(l.from[0], l.from[1], l.from[2]);
 			L.color = col * l.power;
 		}
+		else if(l.type == YC_LIGHT_MESH)
+		{
+			// ObjectLight::factory (:221-254) + initIs (:46-73); faces resolved after the geometry below
+			L.color = col * l.power * static_cast<float>(num_pi);
+			L.samples = l.samples;
+			L.double_sided = l.double_sided != 0;
+		}
 		else
 		{
 			L.corner = V3(l.from[0], l.from[1], l.from[2]);
@@ -847,6 +858,38 @@ Scene::Scene(const yc_scene &s)
 		t.ng = ((t.v1 - t.v0) ^ (t.v2 - t.v0)).normalize();
 		t.mat = s.tri_mat[i];
 		tris.push_back(t);
+	}
+	// meshlights: ObjectLight::initIs (light_object_light.cc:46-73) over the object's faces in creation
+	// order — areas (primitive_triangle.cc:208-213), cdf (sample_pdf1d.h:52-66), total area in double
+	for(int i = 0; i < s.n_lights; ++i)
+	{
+		if(s.lights[i].type != YC_LIGHT_MESH) continue;
+		Light &L = lights[(size_t)i];
+		const yc_object &o = s.objects[s.lights[i].object];
+		std::vector<float> areas;
+		double total = 0.0;
+		for(int k = o.t0; k < o.t0 + o.nt; ++k)
+		{
+			const Tri &t = tris[(size_t)k];
+			L.mv0.push_back(t.v0);
+			L.mv1.push_back(t.v1);
+			L.mv2.push_back(t.v2);
+			L.mng.push_back(t.ng);
+			const V3 e01 = t.v1 - t.v0, e02 = t.v2 - t.v0;
+			areas.push_back(0.5f * (e01 ^ e02).length());
+			total += areas.back();
+		}
+		const double delta = 1.0 / static_cast<double>(areas.size());
+		double c = 0.0;
+		for(float a : areas)
+		{
+			c += static_cast<double>(a) * delta;
+			L.mcdf.push_back(static_cast<float>(c));
+		}
+		const float integral = static_cast<float>(c);
+		for(float &e : L.mcdf) e /= integral;
+		L.area = static_cast<float>(total);
+		L.inv_area = static_cast<float>(1.f / total);
 	}
 	// camera: camera.cc:51-71, camera_perspective.cc:28-69 (no depth of field)
 	const yc_camera &c = s.cam;
@@ -1722,8 +1765,87 @@ class Renderer
 		}
 
 		// light_area.cc:66-96
+		// ObjectLight::sampleSurface (light_object_light.cc:89-107) + TrianglePrimitive::sample
+		// (primitive_triangle.cc:220-234): (point, geometric normal); zeros on the "Sampling error" branch
+		static std::pair<V3, V3> meshSampleSurface(const Light &L, float s_1, float s_2)
+		{
+			const size_t n = L.mcdf.size();
+			size_t k;
+			if(s_1 <= 0.f) k = 0;
+			else if(s_1 >= 1.f) k = n - 1;
+			else k = (size_t)(std::lower_bound(L.mcdf.begin(), L.mcdf.end(), s_1) - L.mcdf.begin());
+			if(k >= n) return {V3(0.f, 0.f, 0.f), V3(0.f, 0.f, 0.f)};
+			float ss_1, delta = L.mcdf[k];
+			if(k > 0)
+			{
+				delta -= L.mcdf[k - 1];
+				ss_1 = (s_1 - L.mcdf[k - 1]) / delta;
+			}
+			else ss_1 = s_1 / delta;
+			const float su_1 = fsqrt(ss_1);
+			const float u = 1.f - su_1;
+			const float v = s_2 * su_1;
+			return {u * L.mv0[k] + v * L.mv1[k] + (1.f - u - v) * L.mv2[k], L.mng[k]};
+		}
+		// light_object_light.cc:111-146
+		static bool meshIllumSample(const Light &L, const SurfacePoint &sp, LSample &s, Ray &wi)
+		{
+			const auto sampled = meshSampleSurface(L, s.s_1, s.s_2);
+			const V3 &p = sampled.first, &n = sampled.second;
+			V3 ldir = p - sp.p;
+			const float dist_sqr = ldir.lengthSqr();
+			const float dist = fsqrt(dist_sqr);
+			if(dist <= 0.0) return false;
+			ldir *= 1.f / dist;
+			float cos_angle = -dot(ldir, n);
+			if(cos_angle <= 0)
+			{
+				if(L.double_sided) cos_angle = -cos_angle;
+				else return false;
+			}
+			wi.tmax = dist;
+			wi.dir = ldir;
+			s.col = L.color;
+			const float area_mul_cosangle = L.area * cos_angle;
+			s.pdf = static_cast<float>(dist_sqr * num_pi / ((area_mul_cosangle == 0.f) ? 1e-8f : area_mul_cosangle));
+			return true;
+		}
+		// light_object_light.cc:183-201: the closest face of the light's own tree (faces with
+		// t >= ray.tmin, accelerator_kdtree.cc:731) gives the normal; `t` is never written there, so the
+		// caller's value stays (areaLightSampleMaterial passes its ray's tmax, -1: 1 / (t * t) = 1)
+		static bool meshIntersect(const Light &L, const Ray &ray, float &t, C3 &col, float &ipdf)
+		{
+			float t_hit = std::numeric_limits<float>::infinity();
+			int best = -1;
+			for(size_t k = 0; k < L.mv0.size(); ++k)
+			{
+				Tri tr;
+				tr.v0 = L.mv0[k];
+				tr.v1 = L.mv1[k];
+				tr.v2 = L.mv2[k];
+				const IsectData d = triIntersect(tr, ray);
+				if(d.hit && d.t < t_hit && d.t >= ray.tmin)
+				{
+					t_hit = d.t;
+					best = (int)k;
+				}
+			}
+			if(best < 0) return false;
+			const V3 n = L.mng[(size_t)best];
+			float cos_angle = dot(ray.dir, -n);
+			if(cos_angle <= 0.f)
+			{
+				if(L.double_sided) cos_angle = std::abs(cos_angle);
+				else return false;
+			}
+			const float idist_sqr = 1.f / (t * t);
+			ipdf = static_cast<float>(idist_sqr * L.area * cos_angle * div_1_by_pi);
+			col = L.color;
+			return true;
+		}
 		static bool areaIllumSample(const Light &L, const SurfacePoint &sp, LSample &s, Ray &wi)
 		{
+			if(L.type == YC_LIGHT_MESH) return meshIllumSample(L, sp, s, wi);
 			const V3 p = L.corner + s.s_1 * L.to_x + s.s_2 * L.to_y;
 			V3 ldir = p - sp.p;
 			const float dist_sqr = ldir.lengthSqr();
@@ -1759,6 +1881,7 @@ class Renderer
 		// light_area.cc:137-151
 		static bool areaIntersect(const Light &L, const Ray &ray, float &t, C3 &col, float &ipdf)
 		{
+			if(L.type == YC_LIGHT_MESH) return meshIntersect(L, ray, t, col, ipdf);
 			const float cos_angle = dot(ray.dir, L.fnormal);
 			if(cos_angle <= 0) return false;
 			if(!areaTri(L.corner, L.c2, L.c3, ray, t))
@@ -2195,6 +2318,24 @@ class Renderer
 				ipdf = static_cast<float>(4.0f * num_pi);
 				return L.color;
 			}
+			if(L.type == YC_LIGHT_MESH)
+			{
+				// light_object_light.cc:148-163
+				ipdf = L.area;
+				const auto sampled = meshSampleSurface(L, s_3, s_4);
+				ray.from = sampled.first;
+				const V3 normal = sampled.second;
+				V3 cu, cv;
+				createCoordsSystem(normal, cu, cv);
+				if(L.double_sided)
+				{
+					ipdf *= 2.f;
+					if(s_1 > 0.5f) ray.dir = cosHemisphere(-normal, cu, cv, (s_1 - 0.5f) * 2.f, s_2);
+					else ray.dir = cosHemisphere(normal, cu, cv, s_1 * 2.f, s_2);
+				}
+				else ray.dir = cosHemisphere(normal, cu, cv, s_1, s_2);
+				return L.color;
+			}
 			ipdf = L.area;
 			ray.from = L.corner + s_3 * L.to_x + s_4 * L.to_y;
 			ray.dir = cosHemisphere(L.normal, L.du, L.dv, s_1, s_2);
@@ -2204,7 +2345,10 @@ class Renderer
 		// light_area.cc:64, light_point.h:41 (Rgb::energy, color.h:59)
 		static float lightEnergy(const Light &L)
 		{
-			const C3 e = (L.type == YC_LIGHT_POINT) ? (L.color * 4.0f) * static_cast<float>(num_pi) : L.color * L.area;
+			// light_object_light.cc:109: double-sided ? 2 color area : color area
+			const C3 e = (L.type == YC_LIGHT_POINT)  ? (L.color * 4.0f) * static_cast<float>(num_pi)
+			             : (L.type == YC_LIGHT_MESH) ? (L.double_sided ? (2.f * L.color) * L.area : L.color * L.area)
+			                                         : L.color * L.area;
 			return (e.r + e.g + e.b) * 0.333333f;
 		}
 

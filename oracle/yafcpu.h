@@ -18,7 +18,7 @@
 extern "C" {
 
 enum { YC_MAT_SHINYDIFFUSE = 0, YC_MAT_LIGHT = 1, YC_MAT_MIRROR = 2, YC_MAT_NULL = 3 };
-enum { YC_LIGHT_POINT = 0, YC_LIGHT_AREA = 1 };
+enum { YC_LIGHT_POINT = 0, YC_LIGHT_AREA = 1, YC_LIGHT_MESH = 2 };
 enum { YC_INT_DIRECT = 0, YC_INT_PATH = 1, YC_INT_PHOTON = 2 };
 enum { YC_FILTER_BOX = 0, YC_FILTER_GAUSS = 1, YC_FILTER_MITCHELL = 2, YC_FILTER_LANCZOS = 3 };
 
@@ -103,6 +103,8 @@ typedef struct {
 	int cast_shadows;
 	int shoot_caustic;        // "with_caustic" (getLightsEmittingCausticPhotons)
 	int shoot_diffuse;        // "with_diffuse" (getLightsEmittingDiffusePhotons)
+	int object;               // meshlight: index into yc_scene::objects
+	int double_sided;         // meshlight
 } yc_light;
 
 typedef struct {

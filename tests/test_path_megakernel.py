@@ -60,6 +60,12 @@ def test_path_megakernel_equals_wavefront(product, name):
     spec, chunk = CASES[name]
     a, w, st = _render(product, spec, wavefront=False, chunk=chunk)
     b, wb, stb = _render(product, spec, wavefront=True, chunk=chunk)
+    if name == "pt_two_lights":
+        # several lights under path tracing pick their light from the one-thread counter, whose count
+        # run the wavefront provides (render.cc lpcBases): the megakernel steps aside
+        assert st["kernel_times"].get("k_path", {}).get("launches", 0) == 0
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        return
     assert "k_path" in st["kernel_times"] and st["kernel_times"]["k_path"]["launches"] > 0, st["kernel_times"].keys()
     assert stb["kernel_times"].get("k_path", {}).get("launches", 0) == 0
     assert "k_shade" not in st["kernel_times"] or st["kernel_times"]["k_shade"]["launches"] == 0
