@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size parity checks")
     ap.add_argument("--parity-rows", type=int, default=12, help="rows of the RR-off bit-exact band")
+    ap.add_argument("--members-per-gpu", type=int, default=1,
+                    help="device-group members per GPU (experiment: several logical members on one GPU run on concurrent streams)")
     return ap.parse_args()
 
 
@@ -200,7 +202,9 @@ def main():
         # the library renders this rank's row band and all-gathers the bands over RCCL itself
         Y.join_render_group(yi, rank, world, dist)
     # one process: exactly n_gpus devices (the default "gpus" = -1 would take every visible GPU)
-    yi.set_device_group(1 if world > 1 else n_gpus, [local_rank] if world > 1 else list(range(n_gpus)))
+    mpg = max(1, a.members_per_gpu)
+    yi.set_device_group(mpg if world > 1 else n_gpus * mpg,
+                        [local_rank] * mpg if world > 1 else [d for d in range(n_gpus) for _ in range(mpg)])
     if not yi.L.yafaray_amd_buildAccelerator(yi.h):
         raise RuntimeError(yi.last_error())
     W, H = a.width, a.height

@@ -237,6 +237,7 @@ struct DevScene
 	// radiance map (same layout as the photon maps, .xyz of rph_dir = the point's normal); k_fg
 	// traces the gather paths of every diffuse camera hit and looks the radiance map up
 	int fg_on, fg_samples, fg_bounces;
+	int fg_pass_samples;           // gather paths of this pass: ceilf(fg_samples * AA indirect multiplier) (:648); 0: fg_samples
 	float fg_min_pathlen;          // gather_dist_
 	float fg_lookup_rad;           // lookup_rad_ = 4 diffuseRadius^2 (:245)
 	float fg_i_scale;              // preGatherWorker i_scale = 1 / (nPaths pi), long double on the host (:53)

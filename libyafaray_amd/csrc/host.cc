@@ -1323,11 +1323,6 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			rp.pm.fg_samples = fg_samples;
 			rp.pm.fg_bounces = fg_bounces;
 			rp.pm.fg_min_pathlen = gather_dist;
-			if(rp.pm.final_gather && s.aa_passes > 1 && s.aa_indirect_sample_multiplier_factor != 1.f)
-			{
-				log.error("PhotonIntegrator: finalGather with AA_indirect_sample_multiplier_factor != 1 is not supported by the GPU core");
-				return false;
-			}
 		}
 		S.width = s.width;
 		S.height = s.height;
@@ -1408,13 +1403,6 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		ip.get("shadowDepth", shadow_depth);
 		S.tr_shad = transp_shad ? 1 : 0;
 		S.s_depth = std::max(0, shadow_depth);
-		if(transp_shad && shadow_depth > 64)
-		{
-			// k_tshadow sorts each shadow ray's transparent-surface list in a 64-entry buffer: a deeper
-			// list would silently drop surfaces the reference filters through, so refuse instead
-			log.error("Integrator: shadowDepth " + std::to_string(shadow_depth) + " > 64 is not supported by the GPU core");
-			return false;
-		}
 		S.tree = 0;
 		S.ext = 0;
 		S.max_add_depth = 0;
@@ -1524,6 +1512,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		}
 		rp.aa.inc_samples = s.aa_inc_samples;
 		rp.aa.light_sample_multiplier_factor = s.aa_light_sample_multiplier_factor;
+		rp.aa.indirect_sample_multiplier_factor = s.aa_indirect_sample_multiplier_factor;
 		rp.aa.threshold = s.aa_threshold;
 		rp.aa.resampled_floor = s.aa_resampled_floor;
 		rp.aa.sample_multiplier_factor = s.aa_sample_multiplier_factor;

@@ -5126,7 +5126,8 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 	const uint32_t n_req = A.cnt_next.n_gather[L.s];
 	const uint32_t a0 = L.s * S.cap_a;
 	uint32_t visits = 0, tests = 0;
-	const int n_sampl = max(1, S.fg_samples);
+	// finalGathering (integrator_photon_mapping.cc:648): ceilf(max(1, n_paths) * aa_indirect_sample_multiplier_)
+	const int n_sampl = S.fg_pass_samples > 0 ? S.fg_pass_samples : max(1, S.fg_samples);
 	float2 *ts_buf = TSH ? A.ts_scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * (size_t)S.s_depth : nullptr;
 	for(uint32_t jj = L.r * blockDim.x + threadIdx.x; jj < n_req; jj += L.nb * blockDim.x)
 	{

@@ -1340,6 +1340,7 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 		S.pk_stack = (uint2 *)d.pk_stack.p;
 	}
 	S.fg_on = 0;
+	S.fg_pass_samples = 0;
 	S.n_rphotons = 0;
 	S.rpk_lds = 0;
 	if(want_fg && n_diffuse > 0)
@@ -1552,6 +1553,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	const bool need_attr = S.has_attr != 0;
 	const int need_ts = S.tr_shad ? std::max(1, S.s_depth) : 0;
 	const bool need_tree = S.tree != 0;   // the full record (slot + col.w stage) only with a specular recursion tree
+	// transparent shadows keep shadowDepth (t, primitive) pairs per shadow ray: deep lists shrink the chunk
+	// so that the lists stay within 16 GB
+	if(need_ts > 0) M = std::min(M, std::max<size_t>(65536, ((size_t)16 << 30) / ((size_t)K * 8 * (size_t)need_ts)));
 	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc || need_ts != d.ts_alloc || need_g != d.g_alloc ||
 	   need_tree != d.tree_alloc)
 	{
@@ -1938,7 +1942,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	if(passes > 1)
 	{
 		if(!ensure(log_, d.aa_flags, (size_t)W * H) || !ensure(log_, d.aa_plist, (size_t)W * H * 4)) return false;
-		float threshold = rp.aa.threshold, sample_multiplier = 1.f, light_multiplier = 1.f;
+		float threshold = rp.aa.threshold, sample_multiplier = 1.f, light_multiplier = 1.f, indirect_multiplier = 1.f;
 		bool threshold_changed = true;
 		int acum = spp, resampled = 0;
 		int resampled_local = 0;   // of them in this member's rows (+ halo rows): the pixels it renders
@@ -1968,6 +1972,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			else if(canceled && *canceled) break;
 			sample_multiplier *= rp.aa.sample_multiplier_factor;
 			light_multiplier *= rp.aa.light_sample_multiplier_factor;
+			indirect_multiplier *= rp.aa.indirect_sample_multiplier_factor;
+			S.fg_pass_samples = (int)ceilf((float)std::max(1, S.fg_samples) * indirect_multiplier);
 			if(light_mult)
 			{
 				HIPCHECK(hipStreamSynchronize(d.stream));   // the previous pass's staging copy is consumed
@@ -2058,6 +2064,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		S.spp = spp;
 		S.pass_offset = 0;
 		S.plist = nullptr;
+		S.fg_pass_samples = 0;
 		rp.film.spp = spp;
 		if(light_mult)
 		{

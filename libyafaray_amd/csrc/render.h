@@ -76,6 +76,7 @@ struct AaParams
 	int passes = 1;
 	int inc_samples = 1;               // AA_inc_samples (defaults to AA_minsamples)
 	float light_sample_multiplier_factor = 1.f;   // AA_light_sample_multiplier_factor (integrator_tiled.cc:190)
+	float indirect_sample_multiplier_factor = 1.f;   // AA_indirect_sample_multiplier_factor (:191; final gathering's path count)
 	float threshold = 0.05f;
 	float resampled_floor = 0.f;       // % of the pixels
 	float sample_multiplier_factor = 1.f;

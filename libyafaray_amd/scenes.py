@@ -188,6 +188,7 @@ class Render:
     ao_distance: float = 1.0
     ao_color: tuple = (1.0, 1.0, 1.0)
     aa_light_sample_multiplier_factor: float = 1.0
+    aa_indirect_sample_multiplier_factor: float = 1.0
 
 
 @dataclass
@@ -695,6 +696,7 @@ def apply(spec: SceneSpec, api) -> None:
     api.paramsSetFloat("AA_resampled_floor", r.aa_resampled_floor)
     api.paramsSetFloat("AA_sample_multiplier_factor", r.aa_sample_multiplier_factor)
     api.paramsSetFloat("AA_light_sample_multiplier_factor", r.aa_light_sample_multiplier_factor)
+    api.paramsSetFloat("AA_indirect_sample_multiplier_factor", r.aa_indirect_sample_multiplier_factor)
     api.paramsSetBool("AA_detect_color_noise", r.aa_detect_color_noise)
     api.paramsSetString("AA_dark_detection_type", r.aa_dark_detection_type)
     api.paramsSetFloat("AA_dark_threshold_factor", r.aa_dark_threshold_factor)
@@ -752,7 +754,8 @@ def cornell_specular(width=64, height=48, spp=2, integrator="directlighting", bo
 
 
 def cornell_transparent_shadows(width=64, height=48, spp=2, integrator="directlighting", panes=2, shadow_depth=5,
-                                point_light=False, bounces=3, **kw) -> SceneSpec:
+                                point_light=False, bounces=3, pane_step=0.15, pane_shrink=0.05, pane_alpha=None,
+                                **kw) -> SceneSpec:
     """Transparent shadows (MonteCarloIntegrator tr_shad_, accelerator_kdtree.cc:916-1061): the C2
     Cornell box with `panes` stacked transparent shinydiffuse panes under the light (tinted, with
     transmit filters), a transparent Fresnel + mirror tall box and a transparent + translucent short
@@ -768,10 +771,11 @@ def cornell_transparent_shadows(width=64, height=48, spp=2, integrator="directli
     tints = [(0.9, 0.3, 0.3), (0.3, 0.9, 0.4), (0.35, 0.45, 0.95), (0.9, 0.9, 0.3)]
     mats = list(s.materials)
     for k in range(panes):
-        z = 1.6 - 0.15 * k
-        h = 0.45 - 0.05 * k
-        mats.append(Material(f"pane{k}", color=tints[k % len(tints)], transparency=0.8 - 0.1 * k,
-                             transmit_filter=0.9 - 0.2 * k, diffuse_reflect=0.6))
+        z = 1.6 - pane_step * k
+        h = 0.45 - pane_shrink * k
+        # pane_alpha: every pane equally transparent (deep stacks: shadowDepth tests)
+        mats.append(Material(f"pane{k}", color=tints[k % len(tints)], transparency=(0.8 - 0.1 * k) if pane_alpha is None else pane_alpha,
+                             transmit_filter=(0.9 - 0.2 * k) if pane_alpha is None else 0.5, diffuse_reflect=0.6))
         b.add_object(f"pane{k}", *_quad((-h, -h, z), (h, -h, z), (h, h, z), (-h, h, z)), len(mats) - 1)
     verts, tris, tri_mat = b.arrays()
     mats.append(Material("tall_glass", color=(0.6, 0.7, 0.9), transparency=0.6, transmit_filter=0.5,

@@ -94,7 +94,7 @@ class yc_render(C.Structure):
                 ("caus_radius", C.c_float), ("tiles_order", C.c_int),
                 ("pm_fg", C.c_int), ("fg_samples", C.c_int), ("fg_bounces", C.c_int), ("fg_min_pathlen", C.c_float),
                 ("crop_x0", C.c_int), ("crop_y0", C.c_int), ("pm_show_map", C.c_int),
-                ("pm_load_path", C.c_char_p)]
+                ("pm_load_path", C.c_char_p), ("aa_indirect_sample_multiplier_factor", C.c_float)]
 
 
 class yc_scene(C.Structure):
@@ -631,6 +631,7 @@ class OracleScene:
         rp.do_ao, rp.ao_samples, rp.ao_dist = int(r.do_ao), r.ao_samples, r.ao_distance
         rp.ao_col[:] = list(r.ao_color)
         rp.aa_light_sample_multiplier_factor = r.aa_light_sample_multiplier_factor
+        rp.aa_indirect_sample_multiplier_factor = r.aa_indirect_sample_multiplier_factor
         self.sc = sc
         self.spec = spec
         _texturing(self, spec, mats)

@@ -1352,6 +1352,7 @@ class Renderer
 		const Scene &sc_;
 		std::atomic<uint64_t> n_closest{0}, n_shadow{0};
 		float light_mult = 1.f;   // TiledIntegrator::aa_light_sample_multiplier_ of the current pass
+		float indirect_mult = 1.f;   // TiledIntegrator::aa_indirect_sample_multiplier_ of the current pass
 
 		// per-thread state
 		struct Thread
@@ -2820,7 +2821,8 @@ class Renderer
 			const float lookup_rad = 4 * rp.pm_diffuse_radius * rp.pm_diffuse_radius;   // :245
 			C3 path_col(0.f);
 			float w = 0.f;
-			const int n_sampl = std::max(1, rp.fg_samples);
+			// integrator_photon_mapping.cc:648
+			const int n_sampl = (int)ceilf(std::max(1, rp.fg_samples) * indirect_mult);
 			for(int i = 0; i < n_sampl; ++i)
 			{
 				C3 throughput(1.f);
@@ -3385,6 +3387,7 @@ static int renderImage(const yc_scene *s, int y0, int y1, float *out_rgba, float
 	{
 		sample_multiplier *= rp.aa_sample_multiplier_factor;
 		R.light_mult *= rp.aa_light_sample_multiplier_factor;   // integrator_tiled.cc:190
+		R.indirect_mult *= rp.aa_indirect_sample_multiplier_factor;   // :191
 		if(resampled <= 0.f && !threshold_changed) {}   // nextPass(..., skipNextPass = true): flags untouched
 		else
 		{

@@ -186,6 +186,8 @@ typedef struct {
 	// maps come from <pm_load_path>_caustic / _diffuse / _fg_radiance.photonmap (PhotonMap::load,
 	// photon.cc:54-87); a failed load generates them.  NULL: generate.
 	const char *pm_load_path;
+	// AA_indirect_sample_multiplier_factor (integrator_tiled.cc:191): final gathering's paths per pass
+	float aa_indirect_sample_multiplier_factor;
 } yc_render;
 
 typedef struct {

@@ -161,6 +161,17 @@ def test_final_gather_several_chunks_and_aa_passes(product, oracle_built):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("factor", [1.5, 0.6])
+def test_final_gather_indirect_sample_multiplier(product, oracle_built, factor):
+    """AA_indirect_sample_multiplier_factor with adaptive passes: pass p final-gathers
+    ceilf(fg_samples * factor^p) paths per hit (integrator_photon_mapping.cc:648, integrator_tiled.cc:191),
+    the PixelSamplingData offsets still stride by fg_samples."""
+    spec = fg_spec(32, 24, spp=1, fg_samples=3, aa_passes=3, aa_inc_samples=1, aa_threshold=0.01,
+                   aa_indirect_sample_multiplier_factor=factor)
+    compare(product, oracle_built, spec)
+
+
+@pytest.mark.gpu
 def test_final_gather_nearest_lds_stack_equals_private(product, monkeypatch):
     """k_fg's radiance-map nearest searches with the far-child stack in an LDS column (pkNearestLds,
     the parent plane recomputing the stacked distance) visit what the private-array stack visits:

@@ -101,14 +101,14 @@ def test_transparent_shadows_off_is_unchanged(product, oracle_built):
 
 
 @pytest.mark.gpu
-def test_shadow_depth_above_the_gpu_limit_is_refused(product):
-    """shadowDepth > 64 would overflow k_tshadow's per-ray surface list: the render is refused with an
-    error (no silent clamp), and 64 itself renders."""
-    spec = scenes.cornell_transparent_shadows(32, 24, spp=1)
-    with pytest.raises(RuntimeError, match="shadowDepth"):
-        product.render_spec(spec.with_render(shadow_depth=65))
-    rgba, w, _ = product.render_spec(spec.with_render(shadow_depth=64))
-    assert (w > 0).all()
+@pytest.mark.parametrize("depth", [70, 100])
+def test_deep_shadow_depth_matches_oracle(product, oracle_built, depth):
+    """shadowDepth beyond 64 (the reference's intersectTs takes any depth, accelerator_kdtree.cc:916-1061):
+    a stack of 72 equally transparent panes under the light, so shadow rays cross up to 72 transparent
+    surfaces — with shadowDepth 70 the ones crossing more are shadowed, with 100 all are filtered."""
+    spec = scenes.cornell_transparent_shadows(32, 24, spp=1, panes=72, pane_step=0.015, pane_shrink=0.0, pane_alpha=0.97,
+                                              shadow_depth=depth)
+    _compare(product, oracle_built, spec)
 
 
 def _pm_fg_spec(**kw):
