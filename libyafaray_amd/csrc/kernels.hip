@@ -4471,6 +4471,129 @@ __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, floa
 	return n_acc;
 }
 
+// pkLookup's walk with a conservative radius (the default walk).  The walk may prune and log with any
+// bound T(t) >= the reference's max_d2(t): every photon the reference accepts is then logged in visit
+// order (pruning never drops one: a photon beyond a split plane is at least the plane distance away,
+// in float as in reals, since rounding is monotonic), and the replay (replayLog) re-applies the exact
+// test d < max_d2, which rejects the extra entries — photons of subtrees the reference pruned, or
+// farther than its radius at the time.  The k-th smallest logged distance equals the k-th smallest
+// accepted one (an extra entry is never below the radius of its time, which only shrinks), so a
+// histogram of the logged distances bounds max_d2 from above: bin j holds distances with
+// (bits(radius2) - bits(d)) >> kWalkBinShift = j (the last bin open below; 2 bins per octave), and
+// T = the upper edge of the deepest bin B with >= k logged entries at or below it.  One insertion is
+// a byte increment in the lane's own LDS column and, rarely, a step of B — no k-slot array
+// (k_gather_walk's exact form keeps k sorted distances in 64 VGPRs and pays 64 v_med3 per insertion),
+// so any k is served.  Byte counters saturate at 255: counts are then lower bounds, T stays
+// conservative.  tools/walk_sim.cc models the visits and log entries per request of both bounds.
+#ifndef YAF_WALK_BINS
+#define YAF_WALK_BINS 32
+#endif
+#ifndef YAF_WALK_BIN_SHIFT
+#define YAF_WALK_BIN_SHIFT 22
+#endif
+constexpr int kWalkBins = YAF_WALK_BINS;   // multiple of 4 (four byte counters per LDS word)
+constexpr int kWalkBinShift = YAF_WALK_BIN_SHIFT;
+static_assert(kWalkBins % 4 == 0, "byte counters in words");
+
+__host__ __device__ inline size_t walkLdsBytes(int pm_stack, bool hist)
+{
+	return (size_t)(pm_stack > 1 ? pm_stack : 1) * kGatherBlock * 4u + (hist ? (size_t)kWalkBins * kGatherBlock : 0u);
+}
+
+__device__ __forceinline__ uint32_t pkWalkBound(const uint4 *nodes, V3 p, int k, float radius2, uint2 *lg, uint32_t cap, uint32_t *stk,
+                                                uint32_t *hist, uint32_t &visits)
+{
+	const uint32_t rb = __float_as_uint(radius2);
+	// deepest usable bin: its edge bits(radius2) - (B << shift) + 1 stays a positive float
+	const int top_bin = min(kWalkBins - 1, (int)(rb >> kWalkBinShift) - 1);
+#pragma unroll
+	for(int w = 0; w < kWalkBins / 4; ++w) hist[w * kGatherBlock] = 0u;
+	float T = radius2;
+	int B = 0;              // T = edge(B): radius2 for B = 0
+	uint32_t below = 0;     // counted entries in bins > B
+	uint32_t n_acc = 0;
+	uint2 pend = make_uint2(0u, 0u);
+	uint32_t curr = 0;
+	int sp_top = 0;
+	uint4 nd = nodes[0];
+	++visits;
+	for(;;)
+	{
+		while((nd.w & 3u) != 3u)
+		{
+			const int axis = (int)(nd.w & 3u);
+			const float split_val = __uint_as_float(nd.x);
+			const float pa = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+			uint32_t far_child;
+			if(pa <= split_val) { far_child = nd.w >> 2; curr = curr + 1; }
+			else { far_child = curr + 1; curr = nd.w >> 2; }
+			float d2 = pa - split_val;
+			d2 *= d2;
+			if(d2 <= T)
+			{
+				stk[sp_top * kGatherBlock] = far_child;
+				++sp_top;
+			}
+			nd = nodes[curr];
+			++visits;
+		}
+		const uint32_t ph = nd.w >> 2;
+		const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
+		const float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
+		if(dist_2 < T)
+		{
+			const uint2 e = make_uint2(ph, __float_as_uint(dist_2));
+			if(n_acc & 1u)
+			{
+				if(n_acc < cap) *reinterpret_cast<uint4 *>(lg + (n_acc - 1u)) = make_uint4(pend.x, pend.y, e.x, e.y);
+			}
+			else pend = e;
+			++n_acc;
+			if(top_bin > 0)
+			{
+				const int j = (int)min((rb - __float_as_uint(dist_2)) >> kWalkBinShift, (uint32_t)top_bin);
+				uint32_t *w = hist + (j >> 2) * kGatherBlock;
+				const uint32_t sh = (uint32_t)(j & 3) * 8u, word = *w;
+				if(((word >> sh) & 255u) != 255u)
+				{
+					*w = word + (1u << sh);
+					if(j > B) ++below;
+				}
+				if(below >= (uint32_t)k)
+				{
+					do
+					{
+						++B;
+						below -= (hist[(B >> 2) * kGatherBlock] >> ((uint32_t)(B & 3) * 8u)) & 255u;
+					} while(B < top_bin && below >= (uint32_t)k);
+					T = __uint_as_float(rb - ((uint32_t)B << kWalkBinShift) + 1u);
+				}
+			}
+		}
+		bool more = false;
+		while(sp_top > 0)
+		{
+			--sp_top;
+			curr = stk[sp_top * kGatherBlock];
+			nd = nodes[curr];
+			++visits;
+			if((nd.w & 3u) != 3u)
+			{
+				const uint32_t pax = nd.z;
+				const float pa = pax == 0u ? p.x : (pax == 1u ? p.y : p.z);
+				float d2 = pa - __uint_as_float(nd.y);
+				d2 *= d2;
+				if(d2 > T) continue;
+			}
+			more = true;
+			break;
+		}
+		if(!more) break;
+	}
+	if((n_acc & 1u) && n_acc <= cap) lg[n_acc - 1u] = pend;
+	return n_acc;
+}
+
 __device__ __forceinline__ uint2 *gatherLogAt(const GatherLog &L, uint32_t q)
 {
 	return L.e + (size_t)q * L.cap;
@@ -4480,11 +4603,13 @@ __device__ __forceinline__ uint2 *gatherLogAt(const GatherLog &L, uint32_t q)
 #ifndef YAF_WALK_WAVES
 #define YAF_WALK_WAVES 5
 #endif
+template<bool BOUND>
 __global__ void __launch_bounds__(kGatherBlock) __attribute__((amdgpu_waves_per_eu(YAF_WALK_WAVES))) k_gather_walk(GatherArgs A)
 {
 	extern __shared__ uint32_t walk_stack[];
 	const DevScene &S = A.S;
 	uint32_t *stk = walk_stack + threadIdx.x;
+	uint32_t *hist = walk_stack + (size_t)max(1, S.pm_stack) * kGatherBlock + threadIdx.x;
 	uint32_t seg, part, parts;
 	gatherSegPart(S.n_seg, seg, part, parts);
 	const uint32_t j1 = min(A.cnt_next.n_gather[seg], A.log.j0 + A.log.seg_cap);
@@ -4496,7 +4621,10 @@ __global__ void __launch_bounds__(kGatherBlock) __attribute__((amdgpu_waves_per_
 		const uint32_t q = seg * A.log.seg_cap + (jj - A.log.j0);
 		uint32_t n_acc = 0;
 		if(__float_as_uint(A.G.extra[j].w) & G_DIFFUSE)
-			n_acc = pkWalk(S.pk_nodes, xyz(A.G.p_prim[j]), S.pm_search, S.pm_radius2, gatherLogAt(A.log, q), A.log.cap, stk, visits);
+		{
+			if(BOUND) n_acc = pkWalkBound(S.pk_nodes, xyz(A.G.p_prim[j]), S.pm_search, S.pm_radius2, gatherLogAt(A.log, q), A.log.cap, stk, hist, visits);
+			else n_acc = pkWalk(S.pk_nodes, xyz(A.G.p_prim[j]), S.pm_search, S.pm_radius2, gatherLogAt(A.log, q), A.log.cap, stk, visits);
+		}
 		A.log.n[q] = n_acc;
 		accepts += n_acc;
 	}
@@ -4514,7 +4642,8 @@ __global__ void __launch_bounds__(kGatherBlock) __attribute__((amdgpu_waves_per_
 
 __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2);
 
-// PhotonGather (photon.cc:31-52) over one request's accepted photons, in the walk's visit order.
+// PhotonGather (photon.cc:31-52) over one request's logged photons, in the walk's visit order, with
+// the reference's acceptance test d < max_d2 (pkdtree.h:270; the bounded walk logs a superset).
 // POS: the heap keeps the entry's log position (HeapRefSplit), else the photon index.
 template<bool POS, class H>
 __device__ __forceinline__ void replayLog(const H &heap, const uint2 *lg, uint32_t n_acc, int k, int &found, float &max_d2)
@@ -4537,7 +4666,7 @@ __device__ __forceinline__ void replayLog(const H &heap, const uint2 *lg, uint32
 				max_d2 = heap.d(0);
 			}
 		}
-		else
+		else if(d < max_d2)
 		{
 			heapReplaceTop(heap, k, v, d);
 			max_d2 = heap.d(0);
@@ -5633,7 +5762,9 @@ hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const D
 hipError_t yafamd_launch_gather_walk(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, const GatherLogDesc *log,
                                      hipStream_t st)
 {
-	if(S->pm_search > kWalkK || (log->seg_cap & 63u) || (log->cap & 1u)) return hipErrorInvalidValue;
+	// the walk with the k smallest distances in registers (k <= kWalkK), else the bounded walk
+	const bool exact = log->exact && S->pm_search <= kWalkK;
+	if((log->seg_cap & 63u) || (log->cap & 1u) || S->pm_search < 1) return hipErrorInvalidValue;
 	GatherArgs A;
 	A.S = *S;
 	A.G = *G;
@@ -5643,13 +5774,14 @@ hipError_t yafamd_launch_gather_walk(const DevScene *S, const DevNeeQueue *G, co
 	A.n_jobs = 0;
 	A.chunk_base = 0;
 	A.log = GatherLog{(uint2 *)log->e, log->n, log->cap, log->seg_cap, log->j0};
-	const size_t lds = (size_t)max(1, S->pm_stack) * kGatherBlock * sizeof(uint32_t);
-	hipLaunchKernelGGL(k_gather_walk, dim3(S->n_seg * kWalkPerSeg), dim3(kGatherBlock), lds, st, A);
+	const size_t lds = walkLdsBytes(S->pm_stack, !exact);
+	if(exact) hipLaunchKernelGGL(k_gather_walk<false>, dim3(S->n_seg * kWalkPerSeg), dim3(kGatherBlock), lds, st, A);
+	else hipLaunchKernelGGL(k_gather_walk<true>, dim3(S->n_seg * kWalkPerSeg), dim3(kGatherBlock), lds, st, A);
 	return hipGetLastError();
 }
 
-// the two-pass gather serves diffuse maps whose k fits the walk's registers
-int yafamd_gather_walk_k() { return kWalkK; }
+// the largest k the two-pass gather serves (the split replay heap's 16-bit log positions)
+int yafamd_gather_walk_k() { return 65535; }
 
 // Final gathering: compaction of the radiance points (reuses the photon count / scan kernels on
 // rad_flag); *total_dev receives the count

@@ -105,7 +105,29 @@ __global__ void __launch_bounds__(256) k_parent_planes(uint4 *nodes, uint32_t n_
 	if(i == 0u) { nodes[0].y = 0u; nodes[0].z = 3u; }
 }
 
+static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch, const KdPayload &kp);
+
 extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch)
+{
+	return buildPkd(pos_dev, n, nodes_dev, depth_out, st, scratch, KdPayload{});
+}
+
+// The same build, and the map's records copied into kd (leaf) order by the subtree pass: leaves
+// then carry kd positions (KdPayload, pkd_kernels.h); kpos / kdir / kcolb hold n records each.
+extern "C" hipError_t yafamd_build_pkd_kd(const float4 *pos_dev, const float4 *dir_dev, const float *colb_dev, uint32_t n, uint4 *nodes_dev,
+                                          float4 *kpos, float4 *kdir, float *kcolb, int *depth_out, hipStream_t st, void **scratch)
+{
+	if(n && (!dir_dev || !colb_dev || !kpos || !kdir || !kcolb)) return hipErrorInvalidValue;
+	KdPayload kp;
+	kp.dir = dir_dev;
+	kp.colb = colb_dev;
+	kp.kpos = kpos;
+	kp.kdir = kdir;
+	kp.kcolb = kcolb;
+	return buildPkd(pos_dev, n, nodes_dev, depth_out, st, scratch, kp);
+}
+
+static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch, const KdPayload &kp)
 {
 	if(n == 0) return hipSuccess;
 	if(!scratch) return hipErrorInvalidValue;
@@ -228,7 +250,7 @@ extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 
 	}
 	// bottom phase: one workgroup per subtree
 	hipLaunchKernelGGL(k_subtrees, dim3(n_seg), dim3(kSubThreads), 0, st, S.segs[cur].as<Seg>(), S.rec[0].as<uint4>(), S.rec[1].as<uint4>(),
-	                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, n, level, S.max_level.as<int>());
+	                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, n, level, S.max_level.as<int>(), kp);
 	hipLaunchKernelGGL(k_parent_planes, dim3((2 * n - 1 + 255) / 256), dim3(256), 0, st, nodes_dev, 2 * n - 1);
 	int depth = 0;
 	uint32_t part_err = 0;

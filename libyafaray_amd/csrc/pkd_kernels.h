@@ -429,6 +429,21 @@ struct LSeg
 	float lo[3], hi[3];
 };
 
+// Optional output of the subtree pass: the map's photons in kd (leaf) order.  Leaf i of the
+// depth-first layout holds list position s (the photon's rank in the tree's in-order leaf
+// sequence); with a payload, the leaf's index field is s instead of the photon index and the
+// photon's three records are copied to kpos / kdir / kcolb[s].  The k nearest photons of a lookup
+// then sit in a few neighbouring cache lines instead of one line per photon and field (k_gather,
+// k_pregather, k_fg).  Search order and results are unchanged: the index only rides along in the
+// heaps, no comparison reads it.
+struct KdPayload
+{
+	const float4 *dir = nullptr;
+	const float *colb = nullptr;
+	float4 *kpos = nullptr, *kdir = nullptr;
+	float *kcolb = nullptr;
+};
+
 constexpr int kSubWaves = kSubThreads / 64;
 static_assert(kSub == kSubThreads && kSubWaves == 4, "one lane per entry, four waves");
 
@@ -438,7 +453,7 @@ __device__ __forceinline__ uint32_t lanePrefix(uint64_t ballot)
 }
 
 __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const uint4 *gx, const uint4 *gy, const uint4 *gz, const float4 *pos,
-                                                        uint4 *nodes, uint32_t n, int base_level, int *max_level)
+                                                        uint4 *nodes, uint32_t n, int base_level, int *max_level, KdPayload kp = KdPayload{})
 {
 	constexpr uint16_t kNone = 0xffffu;
 	__shared__ uint4 buf[2][3][kSub];
@@ -486,7 +501,16 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 				const float4 ph = pos[idx];
 				uint32_t nd = l.node;
 				PK_GUARD(nd < 2 * n - 1, nd);
-				nodes[nd] = make_uint4(__float_as_uint(ph.x), __float_as_uint(ph.y), __float_as_uint(ph.z), 3u | (idx << 2));
+				uint32_t tag = idx;
+				if(kp.kpos)
+				{
+					tag = g.start + l.start;
+					PK_GUARD(tag < n, tag);
+					kp.kpos[tag] = ph;
+					kp.kdir[tag] = kp.dir[idx];
+					kp.kcolb[tag] = kp.colb[idx];
+				}
+				nodes[nd] = make_uint4(__float_as_uint(ph.x), __float_as_uint(ph.y), __float_as_uint(ph.z), 3u | (tag << 2));
 				lsplit[t] = {3u, 0u, 0u, 0u};
 			}
 			else

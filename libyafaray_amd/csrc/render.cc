@@ -70,6 +70,8 @@ size_t yafamd_gather_lanes(const DevScene *S);
 hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
                                 int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st);
 hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch);
+hipError_t yafamd_build_pkd_kd(const float4 *pos_dev, const float4 *dir_dev, const float *colb_dev, uint32_t n, uint4 *nodes_dev, float4 *kpos,
+                               float4 *kdir, float *kcolb, int *depth_out, hipStream_t st, void **scratch);
 void yafamd_pkd_scratch_free(void *scratch);
 hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix, uint8_t *flags,
                                     hipStream_t st);
@@ -270,6 +272,10 @@ struct GpuRenderer::Impl
 	Buf seg_pos, seg_dir, seg_colb, seg_ra, seg_rb, seg_rc;
 	Buf fg_ts;   // k_fg's transparent-shadow hit lists (s_depth per lane of the trace grid)
 	Buf g_log, g_log_n;   // the two-pass diffuse gather's accepted-photon log (one batch of the gather queue)
+	// the maps' records in kd (leaf) order, written by the tree build (diffuse, caustic, radiance): the
+	// kernels read these; the arrays above stay in photon order (saveMap, the group concatenation)
+	Buf kd_pos[3], kd_dir[3], kd_colb[3];
+	bool kd_on[3] = {false, false, false};
 	int n_rphotons = 0;
 	uint32_t n_rad_points = 0;
 	int d_depth = 0, r_depth = 0;           // kd-tree depths of the diffuse / radiance maps
@@ -356,6 +362,8 @@ struct GpuRenderer::Impl
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
 		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf}) b->release();
+		for(int m = 0; m < 3; ++m)
+			for(Buf *b : {&kd_pos[m], &kd_dir[m], &kd_colb[m]}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
 		              &seg_dir, &seg_colb, &seg_ra, &seg_rb, &seg_rc})
 			b->release();
@@ -846,12 +854,12 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	if(want_rad) d.n_rad_points = nr;
 	const auto t1 = std::chrono::steady_clock::now();
 	stats_.photon_shoot_seconds += std::chrono::duration<double>(t1 - t0).count();
+	d.kd_on[which] = false;
 	if(n == 0) return true;
 	// point kd-tree of the map, built on the GPU node for node like the reference's (pkd.hip)
 	if(!ensure(log_, nodes, (2 * (size_t)n - 1) * sizeof(uint4))) return false;
 	int depth = 0;
-	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)pos.p, n, (uint4 *)nodes.p, &depth, d.stream, &d.pkd_scratch));
-	HIPCHECK(hipStreamSynchronize(d.stream));
+	if(!buildMapTree(which, pos.p, dir.p, colb.p, n, nodes.p, depth)) return false;
 	depth_out = depth;
 	stats_.photon_tree_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
 	return true;
@@ -1006,6 +1014,40 @@ bool GpuRenderer::groupConcat(int kind, const std::vector<uint32_t> &counts)
 	return true;
 }
 
+// The point kd-tree of map `which` (0 diffuse, 1 caustic, 2 radiance) over its n records, built on the
+// GPU node for node like the reference's (pkd.hip).  The subtree pass also copies the records into kd
+// (leaf) order (kd_pos / kd_dir / kd_colb) and the leaves index those copies, so a k-NN lookup's
+// photons are read from neighbouring lines; YAFARAY_AMD_PKD_ORDER=photon keeps photon-order leaves
+// (measurement switch; the estimates are identical either way).
+bool GpuRenderer::buildMapTree(int which, const void *pos, const void *dir, const void *colb, uint32_t n, void *nodes, int &depth)
+{
+	Impl &d = *d_;
+	const char *oe = std::getenv("YAFARAY_AMD_PKD_ORDER");
+	const bool kd = !(oe && std::string(oe) == "photon");
+	d.kd_on[which] = false;
+	if(kd && n)
+	{
+		if(!ensure(log_, d.kd_pos[which], (size_t)n * 16) || !ensure(log_, d.kd_dir[which], (size_t)n * 16) ||
+		   !ensure(log_, d.kd_colb[which], (size_t)n * 4))
+			return false;
+		PROF(KK_PHOTON_TREE, yafamd_build_pkd_kd((const float4 *)pos, (const float4 *)dir, (const float *)colb, n, (uint4 *)nodes,
+		                                         (float4 *)d.kd_pos[which].p, (float4 *)d.kd_dir[which].p, (float *)d.kd_colb[which].p, &depth,
+		                                         d.stream, &d.pkd_scratch));
+		d.kd_on[which] = true;
+	}
+	else if(n) PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)pos, n, (uint4 *)nodes, &depth, d.stream, &d.pkd_scratch));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	return true;
+}
+
+// the records the kernels read for map `which`, field f (0 pos, 1 dir, 2 colb): the kd-order copies
+// when its tree indexes them
+const void *GpuRenderer::mapView(int which, int f, const void *photon_order) const
+{
+	if(!d_->kd_on[which]) return photon_order;
+	return f == 0 ? d_->kd_pos[which].p : f == 1 ? d_->kd_dir[which].p : d_->kd_colb[which].p;
+}
+
 // Final gathering's radiance map (integrator_photon_mapping.cc:540-591): the radiance points shootMap
 // compacted are thinned on the host (eliminateRadPoints), pre-gathered on the GPU (k_pregather) and
 // the point kd-tree of the radiance map is built like the photon maps'.
@@ -1062,8 +1104,7 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	                                    (const uint32_t *)d.rad_kept.p, nk, (float4 *)d.rph_pos.p, (float4 *)d.rph_dir.p, (float *)d.rph_colb.p,
 	                                    d.stream));
 	int depth = 0;
-	PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)d.rph_pos.p, nk, (uint4 *)d.rpk_nodes.p, &depth, d.stream, &d.pkd_scratch));
-	HIPCHECK(hipStreamSynchronize(d.stream));
+	if(!buildMapTree(2, d.rph_pos.p, d.rph_dir.p, d.rph_colb.p, nk, d.rpk_nodes.p, depth)) return false;
 	d.n_rphotons = (int)nk;
 	d.r_depth = depth;
 	stats_.fg_radiance_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
@@ -1082,9 +1123,9 @@ void GpuRenderer::publishRadianceMap(DevScene &S, const PhotonParams &pm, uint32
 	S.fg_lookup_rad = 4 * pm.radius2 * pm.radius2;                                   // :245
 	S.fg_i_scale = static_cast<float>(1.f / ((float)S.pm_paths * 3.1415926535897932384626433832795L));   // :53 (math::num_pi)
 	S.n_rphotons = (int)nk;
-	S.rph_pos = nk ? (const float4 *)d.rph_pos.p : nullptr;
-	S.rph_dir = nk ? (const float4 *)d.rph_dir.p : nullptr;
-	S.rph_colb = nk ? (const float *)d.rph_colb.p : nullptr;
+	S.rph_pos = nk ? (const float4 *)mapView(2, 0, d.rph_pos.p) : nullptr;
+	S.rph_dir = nk ? (const float4 *)mapView(2, 1, d.rph_dir.p) : nullptr;
+	S.rph_colb = nk ? (const float *)mapView(2, 2, d.rph_colb.p) : nullptr;
 	S.rpk_nodes = nk ? (const uint4 *)d.rpk_nodes.p : nullptr;
 	// k_fg's nearest searches keep their far-child stack in LDS when the tree is shallow enough
 	S.rpk_lds = (nk && d.r_depth + 1 <= 32) ? d.r_depth + 1 : 0;
@@ -1109,6 +1150,7 @@ bool GpuRenderer::loadMap(RenderParams &rp, int which, const std::string &file)
 		log_.warning(std::string("Integrator: ") + file + " holds no photon directions (a reference-format file): they load as zero, "
 		             "as the reference's PhotonMap::load leaves them");
 	const uint32_t n = m.size();
+	d.kd_on[which] = false;
 	Buf &pos = which == 0 ? d.ph_pos : which == 1 ? d.cph_pos : d.rph_pos;
 	Buf &dir = which == 0 ? d.ph_dir : which == 1 ? d.cph_dir : d.rph_dir;
 	Buf &colb = which == 0 ? d.ph_colb : which == 1 ? d.cph_colb : d.rph_colb;
@@ -1130,7 +1172,7 @@ bool GpuRenderer::loadMap(RenderParams &rp, int which, const std::string &file)
 		HIPCHECK(hipMemcpyAsync(pos.p, hp.data(), (size_t)n * 16, hipMemcpyHostToDevice, d.stream));
 		HIPCHECK(hipMemcpyAsync(dir.p, hd.data(), (size_t)n * 16, hipMemcpyHostToDevice, d.stream));
 		HIPCHECK(hipMemcpyAsync(colb.p, hb.data(), (size_t)n * 4, hipMemcpyHostToDevice, d.stream));
-		PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)pos.p, n, (uint4 *)nodes.p, &depth, d.stream, &d.pkd_scratch));
+		if(!buildMapTree(which, pos.p, dir.p, colb.p, n, nodes.p, depth)) return false;
 	}
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	if(which == 0) { d.n_photons = (int)n; d.pm_paths = m.paths; d.d_depth = depth; }
@@ -1315,17 +1357,17 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 		S.caus_map = 1;
 		S.c_photons = d.c_photons;
 		S.c_paths = d.c_paths;
-		S.cph_pos = (const float4 *)d.cph_pos.p;
-		S.cph_dir = (const float4 *)d.cph_dir.p;
-		S.cph_colb = (const float *)d.cph_colb.p;
+		S.cph_pos = (const float4 *)mapView(1, 0, d.cph_pos.p);
+		S.cph_dir = (const float4 *)mapView(1, 1, d.cph_dir.p);
+		S.cph_colb = (const float *)mapView(1, 2, d.cph_colb.p);
 		S.cpk_nodes = (const uint4 *)d.cpk_nodes.p;
 	}
 	const int n_diffuse = S.integrator == INT_PHOTON ? d.n_photons : 0;
 	// the radiance map of a generating render is at most as deep as the diffuse map it came from
 	d.pm_stack = std::max({d.d_depth, d.c_depth, generate ? 0 : d.r_depth}) + 1;
-	S.ph_pos = (const float4 *)d.ph_pos.p;
-	S.ph_dir = (const float4 *)d.ph_dir.p;
-	S.ph_colb = (const float *)d.ph_colb.p;
+	S.ph_pos = (const float4 *)mapView(0, 0, d.ph_pos.p);
+	S.ph_dir = (const float4 *)mapView(0, 1, d.ph_dir.p);
+	S.ph_colb = (const float *)mapView(0, 2, d.ph_colb.p);
 	S.pk_nodes = (const uint4 *)d.pk_nodes.p;
 	S.n_photons = n_diffuse;
 	S.pm_paths = S.integrator == INT_PHOTON ? d.pm_paths : 0;
@@ -1640,10 +1682,10 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	S.n_seg = (uint32_t)R;
 	S.cap_a = (uint32_t)shardCap(d.slots_cap);
 	S.cap_s = S.cap_a * (uint32_t)K;
-	// The two-pass diffuse gather (k_gather_walk + k_gather<REPLAY>, kernels.hip) for diffuse maps whose
-	// k fits the walk's registers: its log holds `cap` accepted photons per request for a batch of
+	// The two-pass diffuse gather (k_gather_walk + k_gather<REPLAY>, kernels.hip): its log holds `cap`
+	// logged photons per request for a batch of
 	// seg_cap queue positions per segment (within 16 GB); YAFARAY_AMD_GATHER=single keeps one pass.
-	GatherLogDesc glog{nullptr, nullptr, 0u, 0u, 0u, 0u};
+	GatherLogDesc glog{nullptr, nullptr, 0u, 0u, 0u, 0u, 0u};
 	bool walk_gather = false;
 	{
 		const char *ge = std::getenv("YAFARAY_AMD_GATHER");
@@ -1657,7 +1699,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			if(!ensure(log_, d.g_log, (size_t)R * seg_cap * cap * 8) || !ensure(log_, d.g_log_n, (size_t)R * seg_cap * 4)) return false;
 			const char *he = std::getenv("YAFARAY_AMD_GATHER_HEAP");
 			const uint32_t split = (he && std::string(he) == "packed") ? 0u : 1u;
-			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u, split};
+			const char *we = std::getenv("YAFARAY_AMD_GATHER_WALK");
+			const uint32_t exact = (we && std::string(we) == "exact") ? 1u : 0u;
+			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u, split, exact};
 			walk_gather = true;
 		}
 	}

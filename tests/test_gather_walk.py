@@ -1,8 +1,10 @@
-"""Two-pass diffuse gather (kernels.hip k_gather_walk + k_gather<REPLAY>): the walk keeps the k
-smallest distances in registers and logs the accepted photons in visit order; the replay feeds the
-log through PhotonGather's heap (photon.cc:31-52).  The result must equal the one-pass k_gather
-(pkLookup with the heap in LDS) bit for bit — both equal the oracle in the photon-mapping parity
-tests — including requests whose log overflows (they are walked again by the one-pass lookup)."""
+"""Two-pass diffuse gather (kernels.hip k_gather_walk + k_gather<REPLAY>): the walk logs photons in
+visit order — with the exact radius (the k smallest distances in registers, YAFARAY_AMD_GATHER_WALK=exact)
+or with the bounded radius of a distance histogram (default: a superset of the accepted photons) —
+and the replay feeds the log through PhotonGather's heap (photon.cc:31-52) with the reference's
+acceptance test.  The result must equal the one-pass k_gather (pkLookup with the heap in LDS) bit for
+bit — both equal the oracle in the photon-mapping parity tests — including requests whose log
+overflows (they are walked again by the one-pass lookup)."""
 import os
 
 import numpy as np
@@ -27,6 +29,7 @@ def _render(product, spec, env):
 CASES = {
     "diffuse": lambda: scenes.cornell_photon(96, 72, spp=1, photons=50000, search=50, radius=0.1),
     "k7": lambda: scenes.cornell_photon(64, 48, spp=2, photons=30000, search=7, radius=0.2),
+    "k100": lambda: scenes.cornell_photon(64, 48, spp=1, photons=60000, search=100, radius=0.15),
     "fg-specular": lambda: scenes.cornell_specular(64, 48, spp=1, integrator="photonmapping", raydepth=3).with_render(
         pm_photons=30000, pm_search=50, pm_diffuse_radius=0.1, pm_bounces=5, pm_caustics=True, pm_caustic_photons=20000,
         caustic_radius=0.05, pm_final_gather=True, fg_samples=4),
@@ -34,12 +37,15 @@ CASES = {
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("walk", ["bound", "exact"])
 @pytest.mark.parametrize("heap", ["split", "packed"])
 @pytest.mark.parametrize("case", list(CASES))
-def test_two_pass_gather_equals_one_pass(product, case, heap):
+def test_two_pass_gather_equals_one_pass(product, case, heap, walk):
+    if walk == "exact" and case == "k100":
+        pytest.skip("the exact walk keeps at most 64 distances (k = 100 takes the bounded walk)")
     spec = CASES[case]()
     a, wa, sa = _render(product, spec, {"YAFARAY_AMD_GATHER": "single"})
-    b, wb, sb = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_HEAP": heap})
+    b, wb, sb = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_HEAP": heap, "YAFARAY_AMD_GATHER_WALK": walk})
     assert sa["gather_accepts"] == 0 and sb["gather_overflows"] == 0
     if case != "fg-specular":   # (final gathering replaces the diffuse estimate: caustic lookups only)
         assert sb["gather_accepts"] >= sb["gather_photons"] > 0
@@ -56,3 +62,26 @@ def test_two_pass_gather_log_overflow_falls_back(product, heap):
                                        "YAFARAY_AMD_GATHER_HEAP": heap})
     assert sb["gather_overflows"] > 0
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_bounded_walk_logs_a_superset(product):
+    """The bounded walk logs every photon the exact walk accepts plus the ones the replay rejects."""
+    spec = CASES["diffuse"]()
+    a, _, sa = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_WALK": "exact"})
+    b, _, sb = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_WALK": "bound"})
+    assert sb["gather_accepts"] >= sa["gather_accepts"] > 0
+    assert sb["gather_photons"] == sa["gather_photons"]
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["diffuse", "fg-specular"])
+def test_kd_order_records_equal_photon_order(product, case):
+    """The maps' records copied into kd (leaf) order by the tree build (pkd_kernels.h KdPayload) only
+    move where the lookups read them: every estimate is bit-identical to the photon-order records."""
+    spec = CASES[case]()
+    a, wa, sa = _render(product, spec, {"YAFARAY_AMD_PKD_ORDER": "photon"})
+    b, wb, sb = _render(product, spec, {"YAFARAY_AMD_PKD_ORDER": "kd"})
+    assert sa["gather_photons"] == sb["gather_photons"] > 0
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and np.array_equal(wa, wb)
