@@ -160,7 +160,26 @@ def algo_bytes(kind, s, kt, in_lds, a):
         return 80.0 * it
     if kind == "k_photon_bounce":
         return (32.0 + 36.0) * s["photons"] + 32.0 * it   # deposits + one ray per path per bounce
+    if kind == "pkd_build":
+        return pkd_build_bytes(it) * kt["launches"]
     return None
+
+
+def pkd_build_bytes(n):
+    """Algorithmic bytes of one point kd-tree build over n photons (pkd.hip): the three presorted
+    (coordinate, index) lists — keys 28 B per photon (position in, three keys out), three stable
+    (key, index) sorts at 16 B per photon each (one read + one write of the 8-B pair), the 16-B records
+    gathered (4 B index + 16 B gather + 16 B write per list); per top level (while nodes hold more than
+    256 photons) each list's 16-B record read and written plus its 4-B segment number read; the subtree
+    pass reads the three lists (48 B), writes 2n - 1 nodes (32 B per photon) and the map's records in kd
+    order (position + direction + colour, 36 B)."""
+    if n <= 0:
+        return 0.0
+    levels, m = 0, n
+    while m > 256:
+        m = (m + 1) // 2
+        levels += 1
+    return n * (28.0 + 3 * 16.0 + 3 * 36.0 + levels * 3 * 36.0 + 48.0 + 32.0 + 36.0)
 
 
 def main():

@@ -1700,7 +1700,10 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			const char *he = std::getenv("YAFARAY_AMD_GATHER_HEAP");
 			const uint32_t split = (he && std::string(he) == "packed") ? 0u : 1u;
 			const char *we = std::getenv("YAFARAY_AMD_GATHER_WALK");
-			const uint32_t exact = (we && std::string(we) == "exact") ? 1u : 0u;
+			// the walk with the k smallest distances in registers (k <= 64) by default: the bounded walk
+			// (YAFARAY_AMD_GATHER_WALK=bound, and any k > 64) measured slower on C5 (walk 13.9 -> 16.3 ms,
+			// replay 7.4 -> 12.1 ms per frame: its superset log)
+			const uint32_t exact = (we && std::string(we) == "bound") ? 0u : 1u;
 			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u, split, exact};
 			walk_gather = true;
 		}

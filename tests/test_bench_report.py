@@ -66,3 +66,21 @@ def test_dominant_roofline_for_trace_carries_the_survey_model_and_valu_limiter()
     assert roof["survey_per_ray_model"]["closest_B"] == 273.0
     assert roof["traversal"]["served_from"] == "LDS"
     assert roof["limiter"].startswith("VALU")
+
+
+def test_pkd_build_has_an_algorithmic_model():
+    """C5's dominant kernel record (the kd-tree build) reports a roofline, not 0 GB/s: the model counts
+    the top levels of the exact-median build (nodes of more than 256 photons)."""
+    n = 19_646_342
+    levels, m = 0, n
+    while m > 256:
+        m = (m + 1) // 2
+        levels += 1
+    assert levels == 17
+    assert bench.pkd_build_bytes(0) == 0.0
+    assert abs(bench.pkd_build_bytes(n) - n * (28 + 48 + 108 + 17 * 108 + 48 + 32 + 36)) < 1.0
+    a, s = _args("photon"), dict(_stats(), photons=n)
+    kt = {"pkd_build": {"ms": 20.0, "launches": 1, "items": n}, "k_gather": {"ms": 7.0, "launches": 1, "items": 2_000_000}}
+    kernels, _ = bench.kernel_table(a, s, kt, None)
+    roof = bench.dominant_roofline(s, kt, kernels, None, "photon")
+    assert roof["kernel"] == "pkd_build" and roof["achieved"] > 1000.0 and 0.0 < roof["frac"] < 1.0

@@ -1,6 +1,7 @@
 """Two-pass diffuse gather (kernels.hip k_gather_walk + k_gather<REPLAY>): the walk logs photons in
-visit order — with the exact radius (the k smallest distances in registers, YAFARAY_AMD_GATHER_WALK=exact)
-or with the bounded radius of a distance histogram (default: a superset of the accepted photons) —
+visit order — with the exact radius (default: the k smallest distances in registers, k <= 64)
+or with the bounded radius of a distance histogram (YAFARAY_AMD_GATHER_WALK=bound and any k > 64: a
+superset of the accepted photons) —
 and the replay feeds the log through PhotonGather's heap (photon.cc:31-52) with the reference's
 acceptance test.  The result must equal the one-pass k_gather (pkLookup with the heap in LDS) bit for
 bit — both equal the oracle in the photon-mapping parity tests — including requests whose log

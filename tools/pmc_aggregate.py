@@ -6,8 +6,14 @@ Each DIR holds one pass's *counter_collection.csv (tools/pmc_all.sh: FETCH_SIZE,
 three SQ groups in separate runs, no trace domains).  Dispatches are grouped by kernel kind (the
 names yafaray_amd_getKernelTimes reports; every kernel of the photon kd-tree build counts as
 pkd_build).  MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KB; on gfx950 FETCH_SIZE reads
-half the bytes of a wide coalesced load, so it is doubled.  Output per kind: dispatches, read /
-write / total HBM bytes per launch, and the SQ ratios (VALU lane utilisation, wait fractions).
+half the bytes of a wide coalesced load.  Read bytes come from the L2's fabric read requests by size
+(pass R: TCC_EA0_RDREQ_32B / _64B / _128B, 32 / 64 / 128 B each) when that pass ran — calibrated on
+known byte counts by tools/pmc_probe.hip (profiles/pmc_calibration.json: streaming 16-B loads and
+128-B node reads are 128-B requests, a scattered 16-B load is one 64-B request) — else FETCH_SIZE x 2
+(exact only for wide streaming reads).  Output per kind: dispatches, read / write / total bytes per
+launch, the raw FETCH_SIZE bytes, the request mix, and the SQ ratios (VALU lane utilisation, wait
+fractions).  Infinity-Cache (MALL) hits are fabric requests too: the read bytes are L2-miss bytes,
+an upper bound of the HBM bytes.
 """
 import collections
 import csv
@@ -70,21 +76,36 @@ def main():
                     vals[k][c] += float(r["Counter_Value"])
                     disp[k][c].add(r["Dispatch_Id"])
     res = {"config": config, "kernels_src_sha1": kernel_src_sha1(),
-           "method": "rocprofv3 --pmc, one counter group per run (FETCH_SIZE | WRITE_SIZE | 3 SQ groups), one frame; "
-                     "FETCH_SIZE x2 (gfx950 wide loads), KB -> B; per launch = sum / dispatches",
+           "method": "rocprofv3 --pmc, one counter group per run (FETCH_SIZE | WRITE_SIZE | TCC_EA0_RDREQ_32B/64B/128B | SQ "
+                     "groups), one frame; read bytes = 32 / 64 / 128 B per fabric read request by size (FETCH_SIZE x2 where "
+                     "the request pass is missing), KB -> B; per launch = sum / dispatches",
            "kernels": {}}
     for k, v in sorted(vals.items()):
         e = {}
         nf = len(disp[k].get("FETCH_SIZE", ())) or None
         nw = len(disp[k].get("WRITE_SIZE", ())) or None
+        nr = len(disp[k].get("TCC_EA0_RDREQ_128B_sum", ())) or None
+        read_total = None
         if nf:
             e["dispatches"] = nf
-            e["read_bytes_per_launch"] = round(2.0 * 1024.0 * v["FETCH_SIZE"] / nf)
+            e["fetch_size_bytes_per_launch"] = round(1024.0 * v["FETCH_SIZE"] / nf)
+            read_total, nread = 2.0 * 1024.0 * v["FETCH_SIZE"], nf
+            e["read_bytes_source"] = "FETCH_SIZE x2"
+        if nr:
+            r32, r64, r128 = (v.get(f"TCC_EA0_RDREQ_{b}B_sum", 0.0) for b in (32, 64, 128))
+            read_total, nread = 32.0 * r32 + 64.0 * r64 + 128.0 * r128, nr
+            e["dispatches"] = e.get("dispatches", nr)
+            e["read_bytes_source"] = "TCC_EA0_RDREQ by size"
+            tot = max(1.0, r32 + r64 + r128)
+            e["read_requests_per_launch"] = {"32B": round(r32 / nr), "64B": round(r64 / nr), "128B": round(r128 / nr)}
+            e["read_request_mix"] = {"32B": round(r32 / tot, 4), "64B": round(r64 / tot, 4), "128B": round(r128 / tot, 4)}
+        if read_total is not None:
+            e["read_bytes_per_launch"] = round(read_total / nread)
         if nw:
             e["write_bytes_per_launch"] = round(1024.0 * v["WRITE_SIZE"] / nw)
-        if nf and nw:
+        if read_total is not None and nw:
             e["hbm_bytes_per_launch"] = e["read_bytes_per_launch"] + e["write_bytes_per_launch"]
-            e["hbm_bytes_total"] = round(2.0 * 1024.0 * v["FETCH_SIZE"] + 1024.0 * v["WRITE_SIZE"])
+            e["hbm_bytes_total"] = round(read_total + 1024.0 * v["WRITE_SIZE"])
         wc = v.get("SQ_WAVE_CYCLES")
         if wc:
             for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
