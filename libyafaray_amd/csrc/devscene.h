@@ -294,6 +294,7 @@ struct DevScene
 	// the next value; 0: pickLight
 	uint32_t *lpc;
 	int lpc_mode;
+	int nee_pm16;          // 1: NEE requests keep the 16-B pixel / mode word (YAFARAY_AMD_NEE_PM16=1; else 8 B where it fits)
 };
 
 struct DevFilm
@@ -321,7 +322,7 @@ struct DevPaths
 	float4 *col;           // col (first-vertex estimate), .w = stage | subpath << 8 | depth << 20 (bits)
 	float4 *pcol;          // path_col, .w = flags: mat_bsd_fs (v1 flags) | bits below (bits)
 	float4 *pwo;           // pwo (outgoing direction at the current path vertex): ST_FIRST entries only
-	float4 *pend_thr;      // throughput at the pending vertex (after Russian roulette)
+	float4 *pend_thr;      // throughput at the pending vertex (after Russian roulette), 12 B per entry (kernels.hip F3)
 	float4 *pend_emit;     // emission pending at that vertex
 	float4 *v0p;           // first hit p .w = prim (bits)   — only used when path_samples > 1
 	float4 *v0wo;          // first hit wo
@@ -360,7 +361,8 @@ struct DevNeeQueue
 {
 	float4 *p_prim;        // hit point, .w = primitive (bits)
 	float4 *wo_k;          // outgoing direction, .w = index k of the path in the next active list (bits)
-	uint4 *pix_mode;       // (PixelSamplingData offset, sample index, mode | light << 8, 0)
+	uint4 *pix_mode;       // NEE: (PixelSamplingData offset, sample index, mode | light << 8, 0), packed to 8 B
+	                       // per request while neePm8 (kernels.hip); gather: the first-vertex colour + alpha
 	float4 *attr;          // [2 * requests] surface attributes of the vertex (has_attr only)
 	float4 *extra;         // gather requests only: colour added after the estimates, .w = G_* mode bits
 };

@@ -141,6 +141,50 @@ __device__ __forceinline__ void stStore2(T *p, const T &v)
 #endif
 }
 
+// 12-byte records (one dwordx3 per lane, 4-byte aligned): the pending throughput, whose fourth
+// component was never read
+struct F3
+{
+	float x, y, z;
+};
+
+// NEE request's third word pair, 8 B instead of 16 (k_shade writes it, k_nee reads it): (PixelSamplingData
+// offset, s | mode << 20 | light << 21) with s = the sample index minus the pass's first index
+// (base_offset + pass_offset, the same for every sample of a launch).  Used while the pass has fewer
+// than 2^20 samples per pixel and the scene at most 2^11 lights (neePm8); else the 16-B form.
+constexpr uint32_t kPmSBits = 20, kPmLBits = 11;
+__device__ __forceinline__ bool neePm8(const DevScene &S)
+{
+	return !S.nee_pm16 && (uint32_t)S.spp < (1u << kPmSBits) && S.n_lights <= (1 << kPmLBits);
+}
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void neePmStore(const DevScene &S, uint4 *pm, uint32_t j, uint32_t offset, uint32_t sample_idx, uint32_t mode_l)
+{
+	if(neePm8(S))
+	{
+		u32x2_t w;
+		w.x = offset;
+		w.y = (sample_idx - S.base_offset - S.pass_offset) | ((mode_l & 1u) << kPmSBits) | ((mode_l >> 8) << (kPmSBits + 1));
+#if YAF_NT_STORE2
+		__builtin_nontemporal_store(w, reinterpret_cast<u32x2_t *>(pm) + j);
+#else
+		reinterpret_cast<u32x2_t *>(pm)[j] = w;
+#endif
+	}
+	else stStore2(&pm[j], make_uint4(offset, sample_idx, mode_l, 0u));
+}
+// (offset, sample index, mode | light << 8, 0) as k_shade queued it
+__device__ __forceinline__ uint4 neePmLoad(const DevScene &S, const uint4 *pm, uint32_t j)
+{
+	if(neePm8(S))
+	{
+		const uint2 w = reinterpret_cast<const uint2 *>(pm)[j];
+		const uint32_t rel = w.y & ((1u << kPmSBits) - 1u);
+		return make_uint4(w.x, S.base_offset + S.pass_offset + rel, ((w.y >> kPmSBits) & 1u) | ((w.y >> (kPmSBits + 1)) << 8), 0u);
+	}
+	return pm[j];
+}
+
 // Segment worked on by this k_trace workgroup, its rank among the segment's workgroups and their
 // number (the trace grid is a multiple of n_seg).
 struct SegLoop
@@ -2285,7 +2329,11 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			flags = __float_as_uint(pcol4.w);
 			// only the first segment of a subpath reads the previous wo (path_tracer.cc:193-197)
 			if((stage & 0xffu) == ST_FIRST) pwo4 = Pc.pwo[i];
-			if(flags & F_PEND_ONE) pthr4 = Pc.pend_thr[i];
+			if(flags & F_PEND_ONE)
+			{
+				const F3 t = reinterpret_cast<const F3 *>(Pc.pend_thr)[i];
+				pthr4 = make_float4(t.x, t.y, t.z, 0.f);
+			}
 			if(flags & (F_PEND_EMIT | F_AO_EMIT)) pem4 = Pc.pend_emit[i];
 		}
 		C3 thr = rgb(thr4), col = rgb(col4), pcol = rgb(pcol4);
@@ -2634,7 +2682,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			stStore(&Pn.thr[k], f4(thr, w));
 			stStore(&Pn.pcol[k], f4(pcol, __uint_as_float(flags)));
 			if((stage & 0xffu) == ST_FIRST) Pn.pwo[k] = f4(pwo, 0.f);
-			if(nee_one) Pn.pend_thr[k] = f4(pend_thr, 0.f);
+			if(nee_one) reinterpret_cast<F3 *>(Pn.pend_thr)[k] = F3{pend_thr.r, pend_thr.g, pend_thr.b};
 			if(flags & (F_PEND_EMIT | F_AO_EMIT)) Pn.pend_emit[k] = f4(emit_pend, 0.f);
 			if(keep_v0) { Pn.v0p[k] = v0p4; Pn.v0wo[k] = v0wo4; }
 			if(ATTR && keep_v0) { Pn.v0attr[2 * (size_t)k] = v0a0; Pn.v0attr[2 * (size_t)k + 1] = v0a1; }
@@ -2677,7 +2725,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			const uint32_t j = a0 + jn;
 			stStore2(&A.N.p_prim[j], f4(sp.p, __int_as_float(hit_prim)));
 			stStore2(&A.N.wo_k[j], f4(wo, __uint_as_float(k)));
-			stStore2(&A.N.pix_mode[j], make_uint4(offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8), 0u));
+			neePmStore(S, A.N.pix_mode, j, offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8));
 			if(ATTR)
 			{
 				A.N.attr[2 * (size_t)j] = f4(sp.n, sp.drefl);
@@ -3118,7 +3166,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 		{
 			pp = A.N.p_prim[j];
 			wk = A.N.wo_k[j];
-			pm = A.N.pix_mode[j];
+			pm = neePmLoad(S, A.N.pix_mode, j);
 		}
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;

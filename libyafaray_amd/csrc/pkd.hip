@@ -160,7 +160,6 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 	PKCHECK(S.max_level.ensure(16));
 	hipLaunchKernelGGL(k_bound, dim3(n_part), dim3(256), 0, st, pos_dev, n, S.partial.as<float>());
 	hipLaunchKernelGGL(k_root, dim3(1), dim3(256), 0, st, S.partial.as<float>(), n_part, n, S.segs[0].as<Seg>());
-	PKCHECK(hipMemsetAsync(S.seg_of.p, 0, (size_t)n * 4, st));
 	PKCHECK(hipMemsetAsync(S.max_level.p, 0, 4, st));
 	size_t scan_bytes = 0;
 	{
@@ -172,12 +171,13 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 	// fused partitions (default) or the scan + partition passes per list (YAFARAY_AMD_PKD_PARTITION=scan)
 	const char *pe = getenv("YAFARAY_AMD_PKD_PARTITION");
 	const bool fused = !(pe && std::string(pe) == "scan");
+	if(!fused) PKCHECK(hipMemsetAsync(S.seg_of.p, 0, (size_t)n * 4, st));   // the scan passes' per-entry segments
 	const uint32_t n_tiles = (n + kPartTile - 1) / kPartTile;
 	size_t left_scan_bytes = 0;
 	if(fused)
 	{
 		for(DevBuf *b : {&S.rec_out2[0], &S.rec_out2[1]}) PKCHECK(b->ensure((size_t)n * 16));
-		for(DevBuf *b : {&S.seg_of2, &S.seg_nl, &S.seg_left}) PKCHECK(b->ensure((size_t)n * 4));
+		for(DevBuf *b : {&S.seg_nl, &S.seg_left}) PKCHECK(b->ensure((size_t)n * 4));
 		PKCHECK(S.status.ensure((size_t)3 * n_tiles * 8));
 		PKCHECK(S.part_misc.ensure(64));   // [0] ticket, [1] error
 		PKCHECK(hipMemsetAsync(S.status.p, 0, (size_t)3 * n_tiles * 8, st));
@@ -206,8 +206,7 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 				P.in[a] = S.rec[a].as<uint4>();
 				P.out[a] = outs[a]->as<uint4>();
 			}
-			P.seg_of = S.seg_of.as<uint32_t>();
-			P.seg_of_next = S.seg_of2.as<uint32_t>();
+			P.level = (uint32_t)level;
 			P.segs = S.segs[cur].as<Seg>();
 			P.splits = S.splits.as<Split>();
 			P.seg_left = S.seg_left.as<uint32_t>();
@@ -223,8 +222,6 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 				std::swap(S.rec[a].p, outs[a]->p);
 				std::swap(S.rec[a].bytes, outs[a]->bytes);
 			}
-			std::swap(S.seg_of.p, S.seg_of2.p);
-			std::swap(S.seg_of.bytes, S.seg_of2.bytes);
 			n_seg *= 2;
 			max_m = (max_m + 1) / 2;
 			cur ^= 1;

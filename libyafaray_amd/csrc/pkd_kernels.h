@@ -256,8 +256,9 @@ __global__ void k_seg_of(uint32_t *seg_of, uint32_t n, const Split *splits)
 // sum over the segments); the first is a single-pass scan: each tile of kPartTile entries counts
 // its flags, publishes the count, and looks back over its predecessors' published counts / prefixes
 // (Merrill & Garland's decoupled look-back).  Tiles are numbered by a ticket taken at start, so every
-// tile a workgroup waits on has already started.  Per entry: the record (16 B) and its segment (4 B)
-// read once, the record written once, the next level's segment written once (list 0).  Measured on
+// tile a workgroup waits on has already started.  Per entry: the record (16 B) read once and written
+// once; its segment follows from its position (segOfPos: r04, replacing a per-entry segment array
+// read per list and rewritten per level).  Measured on
 // C5 (19.6 M photons, 17 top levels): 0.76 ms per level for the three lists, kd build 22.2 -> 20.3 ms
 // per frame against the scan + partition passes (tiles of 4 / 16 items per thread: 20.8 / 24.6 ms).
 #ifndef YAF_PART_ITEMS
@@ -275,8 +276,7 @@ struct PartArgs
 {
 	const uint4 *in[3];
 	uint4 *out[3];
-	const uint32_t *seg_of;
-	uint32_t *seg_of_next;
+	uint32_t level;      // top level d: 2^d segments, segment s = the path bits of the recursive halving
 	const Seg *segs;
 	const Split *splits;
 	const uint32_t *seg_left;
@@ -286,10 +286,32 @@ struct PartArgs
 	uint32_t *err;       // set when a look-back gave up (spin limit): the build reports an error
 };
 
+// Segment of list position e at top level d: level d's segments are the recursive halving of [0, n)
+// at (start + end) / 2 (every node of the top phase splits, k_level_split), segment s = the path bits.
+__device__ __forceinline__ uint32_t segOfPos(uint32_t e, uint32_t n, uint32_t level)
+{
+	uint32_t s = 0, lo = 0, hi = n;
+	for(uint32_t l = 0; l < level; ++l)
+	{
+		const uint32_t mid = (lo + hi) / 2u;
+		const bool right = e >= mid;
+		s = 2u * s + (right ? 1u : 0u);
+		lo = right ? mid : lo;
+		hi = right ? hi : mid;
+	}
+	return s;
+}
+
+// segments a tile can touch: top-phase segments hold >= kSub entries (the phase runs while a node
+// holds more than kSub, and sizes differ by at most one), so a tile spans at most
+// kPartTile / kSub + 1 of them
+constexpr uint32_t kPartSegs = kPartTile / (uint32_t)kSub + 2u;
+
 __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 {
-	__shared__ uint32_t s_id, s_first, s_acc;
+	__shared__ uint32_t s_id, s_first, s_acc, s_seg0;
 	__shared__ uint32_t s_wsum[kPartItems][kPartThreads / 64];
+	__shared__ uint32_t s_start[kPartSegs];
 	const uint32_t t = threadIdx.x, wv = t >> 6;
 	if(t == 0) s_id = atomicAdd(A.ticket, 1u);
 	__syncthreads();
@@ -299,6 +321,13 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 	uint4 *out = A.out[list];
 	uint64_t *st = A.status + (size_t)list * A.n_tiles;
 	const uint32_t base = tile * kPartTile;
+	// the tile's segments: the first by descent, the starts of it and its successors from the segment
+	// list (no per-entry segment array: 16 B per photon and level less traffic)
+	if(t == 0) s_seg0 = segOfPos(base, A.n, A.level);
+	__syncthreads();
+	const uint32_t seg0 = s_seg0, n_seg = 1u << A.level;
+	if(t < kPartSegs) s_start[t] = seg0 + t < n_seg ? A.segs[seg0 + t].start : 0xffffffffu;
+	__syncthreads();
 	uint4 r[kPartItems];
 	uint32_t so[kPartItems], pre[kPartItems];
 	bool f[kPartItems];
@@ -311,8 +340,10 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 		if(e < A.n)
 		{
 			r[i] = in[e];
-			so[i] = A.seg_of[e];
-			PK_GUARD(so[i] < A.n, so[i]);
+			uint32_t j = 0;
+			while(j + 1u < kPartSegs && s_start[j + 1u] <= e) ++j;
+			so[i] = seg0 + j;
+			PK_GUARD(so[i] < n_seg && A.segs[so[i]].start <= e && e < A.segs[so[i]].end, so[i]);
 			const Split sp = A.splits[so[i]];
 			f[i] = leftOf(r[i], sp.axis, sp.med_key, sp.med_idx);
 		}
@@ -399,7 +430,7 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 		const uint32_t e = base + (uint32_t)i * kPartThreads + t;
 		if(e >= A.n) continue;
 		const uint32_t s = so[i];
-		const uint32_t start = A.segs[s].start, split_el = A.splits[s].split_el;
+		const uint32_t start = s_start[s - seg0], split_el = A.splits[s].split_el;
 		const uint32_t left_before = excl + pre[i] - A.seg_left[s];
 		uint32_t np = f[i] ? start + left_before : split_el + ((e - start) - left_before);
 		PK_GUARD(np < A.n, np);
@@ -409,10 +440,8 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 		pk_u32x4 w;
 		__builtin_memcpy(&w, &r[i], 16);
 		__builtin_nontemporal_store(w, reinterpret_cast<pk_u32x4 *>(&out[np]));
-		if(list == 0) __builtin_nontemporal_store(2u * s + (e < split_el ? 0u : 1u), &A.seg_of_next[e]);
 #else
 		out[np] = r[i];
-		if(list == 0) A.seg_of_next[e] = 2u * s + (e < split_el ? 0u : 1u);
 #endif
 	}
 }

@@ -1746,6 +1746,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	lpc_carry_ = 0;
 	S.lpc = nullptr;
 	S.lpc_mode = 0;
+	S.nee_pm16 = 0;
+	if(const char *e = std::getenv("YAFARAY_AMD_NEE_PM16"); e && *e == '1') S.nee_pm16 = 1;   // tests: the 16-B request word
 	int path_grid = 0;
 	if(!lpc_on)
 	{

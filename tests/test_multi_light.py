@@ -118,3 +118,21 @@ def test_final_gather_two_lights_statistical(product, oracle_built):
     z = paired_z(rgba, orgba)
     assert abs(z["mean_z"]) < 4.0, z
     assert z["max_abs_block_z"] < 6.0, z
+
+
+@pytest.mark.parametrize("case", ["3-lights-adaptive", "dl-3-lights"])
+def test_nee_request_word_packing(product, oracle_built, case, monkeypatch):
+    """k_shade packs each NEE request's (pixel offset, sample index, mode, light) word into 8 B
+    (kernels.hip neePmStore: the sample index relative to the pass's first one); the 16-B form
+    (YAFARAY_AMD_NEE_PM16=1, used when a pass has >= 2^20 samples per pixel or > 2^11 lights)
+    must render the same image bit for bit, and both equal the one-thread oracle."""
+    spec = EXACT["3-lights-adaptive"]() if case == "3-lights-adaptive" else with_lights(
+        scenes.cornell(64, 48, spp=4, integrator="directlighting"), 3)
+    a, wa, _ = product.render_spec(spec)
+    monkeypatch.setenv("YAFARAY_AMD_NEE_PM16", "1")
+    b, wb, _ = product.render_spec(spec)
+    assert np.array_equal(wa, wb)
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+    o, wo, _ = oracle_built.OracleScene(spec, threads=1).render()
+    assert np.array_equal(wa, wo)
+    assert _ulp(a, o).max() <= 4

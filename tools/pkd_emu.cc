@@ -205,11 +205,9 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 			std::vector<uint64_t> status(3 * n_tiles, 0);
 			uint32_t misc[2] = {0, 0};
 			std::vector<uint4> outs[3] = {std::vector<uint4>(n), std::vector<uint4>(n), std::vector<uint4>(n)};
-			std::vector<uint32_t> seg_of2(n);
 			PartArgs P;
 			for(int a = 0; a < 3; ++a) { P.in[a] = rec[a].data(); P.out[a] = outs[a].data(); }
-			P.seg_of = seg_of.data();
-			P.seg_of_next = seg_of2.data();
+			P.level = (uint32_t)level;
 			P.segs = segs[cur].data();
 			P.splits = splits.data();
 			P.seg_left = seg_left.data();
@@ -222,7 +220,6 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 			launch(3 * n_tiles, kPartThreads, [&] { k_level_partition(P); });
 			if(misc[1]) { std::printf("look-back gave up\n"); return false; }
 			for(int a = 0; a < 3; ++a) std::swap(rec[a], outs[a]);
-			std::swap(seg_of, seg_of2);
 			n_seg *= 2;
 			max_m = (max_m + 1) / 2;
 			cur ^= 1;
