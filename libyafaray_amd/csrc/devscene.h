@@ -389,8 +389,10 @@ struct PhotonState
 	float4 *ray_o;       // origin, tmin
 	float4 *ray_d;       // direction
 	float4 *pcol;        // photon colour, .w = flags (bit 0 caustic, bit 1 direct)
-	uint32_t *alive[2];  // photon ids of the current / next bounce
-	uint32_t *n_alive;   // [2]
+	uint32_t *alive[2];  // photon ids of the current / next bounce, segmented: segment s (= k_photon_bounce
+	                     // workgroup s) holds seg_cap entries at s * seg_cap; kDeadPhoton marks a hole
+	uint32_t *n_alive;   // [2 * n_segs] entries per segment (bounce 0: derived from the local id layout)
+	uint32_t seg_cap, n_segs;
 	float4 *dep_a;       // deposit slots: (position, colour.r)
 	float4 *dep_b;       // (direction, colour.g)
 	float *dep_c;        // colour.b

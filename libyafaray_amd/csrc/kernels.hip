@@ -3935,6 +3935,8 @@ __device__ __forceinline__ V3 sphereDir(float s_1, float s_2)
 }
 
 
+constexpr uint32_t kDeadPhoton = 0xffffffffu;   // a hole in the segmented alive list (k_photon_emit)
+
 struct PhotonArgs
 {
 	DevScene S;
@@ -4014,10 +4016,12 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 		pcol = C3{L.color[0], L.color[1], L.color[2]} * (f_num_lights * light_pdf / light_num_pdf);
 		ok = !isBlack(pcol);
 	}
-	const uint32_t j = waveAppend(ok, &A.P.n_alive[A.cur]);
+	// the path's place in the alive list: segment i mod n_segs (the bounce workgroup that traces it),
+	// position i / n_segs — no counter (a global per-wave atomic here serialised 156 K appends on one
+	// address: 1.8 ms for 10 M photons); a photon that carries no energy leaves a hole
+	if(i < A.n_local) A.P.alive[0][(i % A.P.n_segs) * A.P.seg_cap + i / A.P.n_segs] = ok ? i : kDeadPhoton;
 	if(ok)
 	{
-		A.P.alive[A.cur][j] = i;
 		A.P.ray_o[i] = f4(o, S.ray_min_dist);
 		A.P.ray_d[i] = f4(d, -1.f);
 		A.P.pcol[i] = f4(pcol, __uint_as_float(2u));   // caustic = false, direct = true
@@ -4080,11 +4084,20 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 		C.nodes = S.nodes;
 		C.tris = S.tris;
 	}
-	const uint32_t n = A.P.n_alive[A.cur];
+	// workgroup `seg` traces segment `seg` of the alive list and appends the paths that continue to
+	// segment `seg` of the next list through an LDS counter (an entry yields at most one next entry, so
+	// a segment never outgrows its share; no global atomics — the main wavefront's queue scheme)
+	__shared__ uint32_t s_next;
+	if(threadIdx.x == 0) s_next = 0;
+	__syncthreads();
+	const uint32_t seg = blockIdx.x, G = A.P.n_segs, cap = A.P.seg_cap;
+	const uint32_t n = A.bounce == 0 ? (A.n_local > seg ? (A.n_local - seg + G - 1u) / G : 0u) : A.P.n_alive[(uint32_t)A.cur * G + seg];
+	const uint32_t *alive_cur = A.P.alive[A.cur] + (size_t)seg * cap;
 	const int nxt = A.cur ^ 1;
+	uint32_t *alive_nxt = A.P.alive[nxt] + (size_t)seg * cap;
 	const uint32_t slots = (uint32_t)A.max_bounces + 1u;
 	uint32_t visits = 0, tests = 0;
-	for(uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x)
+	for(uint32_t base = 0; base < n; base += blockDim.x)
 	{
 		const uint32_t j = base + threadIdx.x;
 		bool cont = false;
@@ -4092,9 +4105,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 		V3 new_o = v3(0.f, 0.f, 0.f), new_d = new_o;
 		C3 new_col = c3(0.f);
 		uint32_t new_flags = 0;
-		if(j < n)
+		if(j < n) i = alive_cur[j];
+		if(j < n && i != kDeadPhoton)
 		{
-			i = A.P.alive[A.cur][j];
 			h = A.h0 + i;
 			const float4 ro = A.P.ray_o[i], rd = A.P.ray_d[i], pc = A.P.pcol[i];
 			float t;
@@ -4176,15 +4189,17 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 				}
 			}
 		}
-		const uint32_t k = waveAppend(cont, &A.P.n_alive[nxt]);
+		const uint32_t k = waveAppend(cont, &s_next);
 		if(cont)
 		{
-			A.P.alive[nxt][k] = i;
+			alive_nxt[k] = i;
 			A.P.ray_o[i] = f4(new_o, S.ray_min_dist);
 			A.P.ray_d[i] = f4(new_d, -1.f);
 			A.P.pcol[i] = f4(new_col, __uint_as_float(new_flags));
 		}
 	}
+	__syncthreads();
+	if(threadIdx.x == 0) A.P.n_alive[(uint32_t)nxt * G + seg] = s_next;
 }
 
 // Stable compaction of the deposit slots (photon-id order): per-1024-slot counts, an exclusive
@@ -5724,6 +5739,7 @@ hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const P
 	A.cur = cur;
 	A.stack_depth = stack_depth;
 	A.spill = spill;
+	if((uint32_t)grid != P->n_segs) return hipErrorInvalidValue;   // one workgroup per alive-list segment
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	if(S->scene_in_lds)
 	{

@@ -747,8 +747,11 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	const uint32_t NL = h1 - h0;
 	if(which == 0) d.pm_local = NL;
 	const size_t n_slots = (size_t)NL * slots;
+	// segmented alive lists: one segment per k_photon_bounce workgroup (the trace grid)
+	const uint32_t ph_segs = (uint32_t)std::max(1, d.trace_grid), ph_cap = (NL + ph_segs - 1) / ph_segs;
 	if(!ensure(log_, d.ph_ray_o, (size_t)NL * 16) || !ensure(log_, d.ph_ray_d, (size_t)NL * 16) || !ensure(log_, d.ph_pcol, (size_t)NL * 16) ||
-	   !ensure(log_, d.ph_alive0, (size_t)NL * 4) || !ensure(log_, d.ph_alive1, (size_t)NL * 4) || !ensure(log_, d.ph_n_alive, 16) ||
+	   !ensure(log_, d.ph_alive0, (size_t)ph_segs * ph_cap * 4 + 4) || !ensure(log_, d.ph_alive1, (size_t)ph_segs * ph_cap * 4 + 4) ||
+	   !ensure(log_, d.ph_n_alive, (size_t)2 * ph_segs * 4) ||
 	   !ensure(log_, d.dep_a, n_slots * 16) || !ensure(log_, d.dep_b, n_slots * 16) || !ensure(log_, d.dep_c, n_slots * 4) ||
 	   !ensure(log_, d.dep_flag, n_slots) || !ensure(log_, d.ph_scan, ((n_slots + 1023) / 1024) * 4 + 16) || !ensure(log_, d.ph_total, 16))
 		return false;
@@ -759,6 +762,8 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	P.alive[0] = (uint32_t *)d.ph_alive0.p;
 	P.alive[1] = (uint32_t *)d.ph_alive1.p;
 	P.n_alive = (uint32_t *)d.ph_n_alive.p;
+	P.seg_cap = ph_cap;
+	P.n_segs = ph_segs;
 	P.dep_a = (float4 *)d.dep_a.p;
 	P.dep_b = (float4 *)d.dep_b.p;
 	P.dep_c = (float *)d.dep_c.p;
@@ -779,12 +784,10 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 		P.rad_flag = (uint8_t *)d.rad_flag.p;
 		if(n_slots) HIPCHECK(hipMemsetAsync(d.rad_flag.p, 0, n_slots, d.stream));
 	}
-	HIPCHECK(hipMemsetAsync(d.ph_n_alive.p, 0, 16, d.stream));
 	PROF(KK_PHOTON_EMIT, yafamd_photon_emit(&S, &P, &L, N, h0, NL, bounces, d.stream));
 	int cur = 0;
 	for(int b = 0; b <= bounces; ++b)
 	{
-		HIPCHECK(hipMemsetAsync((uint32_t *)d.ph_n_alive.p + (cur ^ 1), 0, 4, d.stream));
 		PROF(KK_PHOTON_BOUNCE, yafamd_photon_bounce(&S, &P, &L, N, h0, NL, bounces, b, cur, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 		cur ^= 1;
 	}

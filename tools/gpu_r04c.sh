@@ -3,7 +3,7 @@
 # Selected GPU tests, then same-box A/B against the previous commit's library (variants/head.so).
 cd ${GRAFT_REPO_ROOT:-/root/repo}
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests/test_pkd_gpu.py tests/test_photon.py tests/test_gather_walk.py tests/test_multi_light.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/sel_tests.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_pkd_gpu.py tests/test_photon.py tests/test_gather_walk.py tests/test_multi_light.py tests/test_gpu_parity.py tests/test_pm_options.py tests/test_final_gather.py tests/test_caustics.py tests/test_meshlight.py tests/test_device_group.py tests/test_photon_files.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/sel_tests.log 2>&1
 rc=$?; tail -4 gpurun_out/sel_tests.log; [ $rc -eq 0 ] || exit $rc
 ab() {   # tag lib bench-args...
   local tag=$1 lib=$2; shift 2
