@@ -246,15 +246,30 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 		++level;
 	}
 	// bottom phase: one workgroup per subtree
+	// the deepest level: the largest subtree (ceil(n / 2^level) photons) halves (its larger half
+	// rounding up) until single photons — the device build computes it here instead of one atomicMax per
+	// subtree on a single address; the checked build still takes the atomic and compares
+#ifdef PKD_CHECK
+	int *dev_max_level = S.max_level.as<int>();
+#else
+	int *dev_max_level = nullptr;
+#endif
 	hipLaunchKernelGGL(k_subtrees, dim3(n_seg), dim3(kSubThreads), 0, st, S.segs[cur].as<Seg>(), S.rec[0].as<uint4>(), S.rec[1].as<uint4>(),
-	                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, n, level, S.max_level.as<int>(), kp);
+	                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, n, level, dev_max_level, kp);
 	hipLaunchKernelGGL(k_parent_planes, dim3((2 * n - 1 + 255) / 256), dim3(256), 0, st, nodes_dev, 2 * n - 1);
-	int depth = 0;
+	int depth = level;
+	for(uint32_t m = max_m; m > 1u; m = (m + 1u) / 2u) ++depth;
 	uint32_t part_err = 0;
-	PKCHECK(hipMemcpyAsync(&depth, S.max_level.p, 4, hipMemcpyDeviceToHost, st));
+#ifdef PKD_CHECK
+	int dev_depth = 0;
+	PKCHECK(hipMemcpyAsync(&dev_depth, S.max_level.p, 4, hipMemcpyDeviceToHost, st));
+#endif
 	if(fused && level > 0) PKCHECK(hipMemcpyAsync(&part_err, S.part_misc.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
 	PKCHECK(hipStreamSynchronize(st));
 	if(part_err) return hipErrorLaunchFailure;   // a look-back gave up: the tree is not trustworthy
+#ifdef PKD_CHECK
+	if(dev_depth != depth) return hipErrorLaunchFailure;
+#endif
 	*depth_out = depth;
 	return hipGetLastError();
 }

@@ -570,8 +570,10 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 		}
 		if(n_split == 0)
 		{
-			// every segment of this level was a leaf: the deepest level of this subtree
-			if(t == 0) atomicMax(max_level, level);
+			// every segment of this level was a leaf: the deepest level of this subtree (the device build
+			// passes no max_level: one atomic per subtree on a single address serialised 131 K workgroups;
+			// the depth follows from the largest subtree, pkd.hip)
+			if(t == 0 && max_level) atomicMax(max_level, level);
 			break;
 		}
 		if(split) cb[t] = 2u * (split_before + lanePrefix(bs));

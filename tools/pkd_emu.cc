@@ -260,7 +260,11 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 	if(bad) std::printf(" first=%zu got=(%x %x %x %x) want=(%x %x %x %x)", first, nodes[first].x, nodes[first].y, nodes[first].z, nodes[first].w,
 	                    want[first].x, want[first].y, want[first].z, want[first].w);
 	std::printf("\n");
-	const bool ok = bad == 0 && g_pkd_err == 0 && depth == max_level;
+	// pkd.hip's arithmetic depth (the largest subtree halved down to single photons)
+	int calc = level;
+	for(uint32_t m = max_m; m > 1u; m = (m + 1u) / 2u) ++calc;
+	if(calc != max_level) std::printf("arithmetic depth %d != %d\n", calc, max_level);
+	const bool ok = bad == 0 && g_pkd_err == 0 && depth == max_level && calc == max_level;
 	g_pkd_err = 0;
 	return ok;
 }
