@@ -363,9 +363,16 @@ def kernel_table(a, s, kt, pmc):
             e["achieved_gbs"] = round(ab / (v["ms"] * 1e-3) / 1e9, 1)
             e["frac"] = round(ab / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         p = (pmc or {}).get("kernels", {}).get(kind)
+        # frames the PMC pass rendered: one k_film per (single-pass) frame
+        frames = ((pmc or {}).get("kernels", {}).get("k_film") or {}).get("dispatches")
         if p and "hbm_bytes_per_launch" in p and v["ms"] > 0 and v["launches"]:
-            # measured per launch (the PMC pass may span several frames: its total is not one frame's)
-            e["traffic_bytes"] = int(p["hbm_bytes_per_launch"] * v["launches"])
+            # measured per launch (the PMC pass may span several frames: its total is not one frame's); a
+            # kind made of several kernels (pkd_build, photon_compact: one launch record per frame) is its
+            # total over the pass's frames
+            if kind not in SINGLE_KERNEL_KINDS and frames and "hbm_bytes_total" in p:
+                e["traffic_bytes"] = int(p["hbm_bytes_total"] / frames * v["launches"])
+            else:
+                e["traffic_bytes"] = int(p["hbm_bytes_per_launch"] * v["launches"])
             e["traffic_gbs"] = round(e["traffic_bytes"] / (v["ms"] * 1e-3) / 1e9, 1)
             e["traffic_frac"] = round(e["traffic_gbs"] / HBM_PEAK_GBS, 4)
             if "valu_lane_util" in p:
@@ -387,8 +394,11 @@ def dominant_roofline(s, kt, kernels, pmc, scene=None):
     achieved = e.get("achieved_gbs", 0.0)
     per_launch = achieved * 1e9 * avg_ms * 1e-3
     p = (pmc or {}).get("kernels", {}).get(kind, {})
+    traffic = p.get("hbm_bytes_per_launch")
+    if e.get("traffic_bytes") is not None:
+        traffic = round(e["traffic_bytes"] / launches)   # per launch record of this kind (multi-kernel kinds: per frame)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": p.get("hbm_bytes_per_launch"),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": kind, "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
             "algo_bytes_per_launch": round(per_launch)}
     if e.get("traffic_gbs") is not None:

@@ -4142,12 +4142,23 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 					// :184-193 radiance point (final gathering): normal faced to the photon, reflectivities
 					if(A.P.rad_flag && !A.L.caustic && fgRadSelect(h * slots + (uint32_t)A.bounce))
 					{
-						const DevMaterial &m = S.mats[sp.mat];
-						const C3 refl = getReflectivity<EXT>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_REFLECT);
-						const C3 transm = getReflectivity<EXT>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_TRANSMIT);
-						A.P.rad_a[slot] = f4(sp.p, refl.r);
-						A.P.rad_b[slot] = f4(faceForward(sp.ng, sp.n, wi), refl.g);
-						A.P.rad_c[slot] = make_float4(refl.b, transm.r, transm.g, transm.b);
+						if constexpr(EXT)
+						{
+							const DevMaterial &m = S.mats[sp.mat];
+							const C3 refl = getReflectivity<EXT>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_REFLECT);
+							const C3 transm = getReflectivity<EXT>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_TRANSMIT);
+							A.P.rad_a[slot] = f4(sp.p, refl.r);
+							A.P.rad_b[slot] = f4(faceForward(sp.ng, sp.n, wi), refl.g);
+							A.P.rad_c[slot] = make_float4(refl.b, transm.r, transm.g, transm.b);
+						}
+						else
+						{
+							// the reflectivities (32 material samples, for one deposit in eight: the other lanes of
+							// the wave waited) are computed by k_rad_refl for the points the thinning keeps, one
+							// lane each; the point carries its primitive (flat shading: surfFromPrim rebuilds sp)
+							A.P.rad_a[slot] = f4(sp.p, __int_as_float(prim));
+							A.P.rad_b[slot] = f4(faceForward(sp.ng, sp.n, wi), 0.f);
+						}
 						A.P.rad_flag[slot] = 1;
 					}
 				}
@@ -4935,6 +4946,25 @@ __global__ void __launch_bounds__(1024) k_rad_scatter(PhotonState P, uint32_t n_
 		out_b[o] = P.rad_b[k];
 		out_c[o] = P.rad_c[k];
 	}
+}
+
+// The radiance points' getReflectivity means (integrator_photon_mapping.cc:188-190, material.cc:156-174)
+// for the kept points of a scene without EXT materials (k_photon_bounce deferred them: .w of a holds
+// the primitive): a = (p, refl.r), b = (normal, refl.g), c = (refl.b, transm) as the bounce writes
+// them for EXT scenes
+__global__ void __launch_bounds__(256) k_rad_refl(DevScene S, float4 *a, float4 *b, float4 *c, const uint32_t *kept, uint32_t n)
+{
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if(t >= n) return;
+	const uint32_t q = kept[t];
+	const float4 pa = a[q];
+	const Surf sp = surfFromPrim(S, xyz(pa), __float_as_int(pa.w));
+	const DevMaterial &m = S.mats[sp.mat];
+	const C3 refl = getReflectivity<false>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_REFLECT);
+	const C3 transm = getReflectivity<false>(S, m, sp, B_DIFFUSE | B_GLOSSY | B_TRANSMIT);
+	a[q].w = refl.r;
+	b[q].w = refl.g;
+	c[q] = make_float4(refl.b, transm.r, transm.g, transm.b);
 }
 
 // preGatherWorker (integrator_photon_mapping.cc:39-88) for every kept radiance point: k-NN gather of
@@ -5857,6 +5887,14 @@ hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *
 	hipLaunchKernelGGL(k_photon_count, dim3(nb), dim3(256), 0, st, P->rad_flag, n_slots, scratch_counts);
 	hipLaunchKernelGGL(k_photon_scan, dim3(1), dim3(1024), 0, st, scratch_counts, nb, total_dev);
 	hipLaunchKernelGGL(k_rad_scatter, dim3(nb), dim3(1024), 0, st, *P, n_slots, (const uint32_t *)scratch_counts, a, b, c);
+	return hipGetLastError();
+}
+
+// k_rad_refl over the kept radiance points (scenes without EXT materials)
+hipError_t yafamd_rad_refl(const DevScene *S, float4 *a, float4 *b, float4 *c, const uint32_t *kept, uint32_t n, hipStream_t st)
+{
+	if(n == 0 || S->ext) return hipSuccess;
+	hipLaunchKernelGGL(k_rad_refl, dim3((n + 255) / 256), dim3(256), 0, st, *S, a, b, c, kept, n);
 	return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ int yafamd_gather_walk_k();
 size_t yafamd_gather_lds_bytes(const DevScene *S);
 hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b,
                               float4 *c, hipStream_t st);
+hipError_t yafamd_rad_refl(const DevScene *S, float4 *a, float4 *b, float4 *c, const uint32_t *kept, uint32_t n, hipStream_t st);
 hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
                             float4 *out_pos, float4 *out_dir, float *out_colb, hipStream_t st);
 hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out, uint32_t *n_kept,
@@ -1101,6 +1102,9 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	if(!ensure(log_, d.rph_pos, (size_t)nk * 16) || !ensure(log_, d.rph_dir, (size_t)nk * 16) || !ensure(log_, d.rph_colb, (size_t)nk * 4) ||
 	   !ensure(log_, d.rpk_nodes, (2 * (size_t)nk - 1) * sizeof(uint4)))
 		return false;
+	// the kept points' reflectivities (deferred by k_photon_bounce in scenes without EXT materials)
+	PROF(KK_PREGATHER, yafamd_rad_refl(&S, (float4 *)d.radc_a.p, (float4 *)d.radc_b.p, (float4 *)d.radc_c.p, (const uint32_t *)d.rad_kept.p, nk,
+	                                   d.stream));
 	DevScene probe = S;
 	probe.n_seg = (uint32_t)d.shade_grid;   // the gather grid k_pregather shares pk_stack with
 	PROF(KK_PREGATHER, yafamd_pregather(&probe, (const float4 *)d.radc_a.p, (const float4 *)d.radc_b.p, (const float4 *)d.radc_c.p,

@@ -84,3 +84,18 @@ def test_pkd_build_has_an_algorithmic_model():
     kernels, _ = bench.kernel_table(a, s, kt, None)
     roof = bench.dominant_roofline(s, kt, kernels, None, "photon")
     assert roof["kernel"] == "pkd_build" and roof["achieved"] > 1000.0 and 0.0 < roof["frac"] < 1.0
+
+
+def test_multi_kernel_kind_traffic_is_per_frame():
+    """pkd_build is ~160 dispatches per PMC pass (levels, sorts, subtrees) but one launch record per frame:
+    its traffic is the pass's total over the frames the pass rendered (k_film dispatches), not one
+    dispatch's average."""
+    n = 19_646_342
+    a, s = _args("photon"), dict(_stats(), photons=n)
+    kt = {"pkd_build": {"ms": 19.3, "launches": 1, "items": n}, "k_film": {"ms": 0.07, "launches": 1, "items": 2_073_600}}
+    pmc = {"kernels": {"pkd_build": {"dispatches": 162, "hbm_bytes_per_launch": 0.74e9, "hbm_bytes_total": 162 * 0.74e9},
+                       "k_film": {"dispatches": 2, "hbm_bytes_per_launch": 0.33e9, "hbm_bytes_total": 0.66e9}}}
+    kernels, _ = bench.kernel_table(a, s, kt, pmc)
+    assert abs(kernels["pkd_build"]["traffic_bytes"] - 162 * 0.74e9 / 2) < 1e3
+    roof = bench.dominant_roofline(s, kt, kernels, pmc, "photon")
+    assert roof["kernel"] == "pkd_build" and abs(roof["traffic"] - 162 * 0.74e9 / 2) < 1e3
