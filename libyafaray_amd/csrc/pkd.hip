@@ -254,7 +254,8 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 #else
 	int *dev_max_level = nullptr;
 #endif
-	hipLaunchKernelGGL(k_subtrees, dim3(n_seg), dim3(kSubThreads), 0, st, S.segs[cur].as<Seg>(), S.rec[0].as<uint4>(), S.rec[1].as<uint4>(),
+	const uint32_t sub_threads = std::min<uint32_t>((uint32_t)kSubThreads, (std::max<uint32_t>(max_m, 1u) + 63u) & ~63u);
+	hipLaunchKernelGGL(k_subtrees, dim3(n_seg), dim3(sub_threads), 0, st, S.segs[cur].as<Seg>(), S.rec[0].as<uint4>(), S.rec[1].as<uint4>(),
 	                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, n, level, dev_max_level, kp);
 	hipLaunchKernelGGL(k_parent_planes, dim3((2 * n - 1 + 255) / 256), dim3(256), 0, st, nodes_dev, 2 * n - 1);
 	int depth = level;

@@ -494,8 +494,10 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 	__shared__ uint32_t wsum[4][kSubWaves];    // per-wave ballot totals: lists 0-2, splitting segments
 	const Seg g = segs[blockIdx.x];
 	uint32_t m = g.end - g.start;
-	PK_GUARD(m >= 1 && m <= (uint32_t)kSub && g.end <= n, m);
-	const uint32_t t = threadIdx.x, wv = t >> 6;
+	PK_GUARD(m >= 1 && m <= blockDim.x && blockDim.x <= (uint32_t)kSub && g.end <= n, m);
+	// one lane per entry: the launch takes the largest subtree rounded up to whole waves (<= kSub), so a
+	// level of 150-photon subtrees runs three waves per workgroup instead of four
+	const uint32_t t = threadIdx.x, wv = t >> 6, nw = blockDim.x >> 6;
 	const bool act = t < m;
 	if(act)
 	{
@@ -562,7 +564,7 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 		if((t & 63) == 0) wsum[3][wv] = (uint32_t)__popcll(bs);
 		__syncthreads();
 		uint32_t n_split = 0, split_before = 0;
-		for(uint32_t w = 0; w < (uint32_t)kSubWaves; ++w)
+		for(uint32_t w = 0; w < nw; ++w)
 		{
 			const uint32_t c = wsum[3][w];
 			split_before += (w < wv) ? c : 0u;

@@ -240,7 +240,7 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 		cur ^= 1;
 		++level;
 	}
-	launch(n_seg, kSubThreads, [&] {
+	launch(n_seg, std::min<uint32_t>((uint32_t)kSubThreads, (std::max<uint32_t>(max_m, 1u) + 63u) & ~63u), [&] {
 		k_subtrees(segs[cur].data(), rec[0].data(), rec[1].data(), rec[2].data(), pos.data(), nodes.data(), n, level, &max_level);
 	});
 	std::vector<uint4> want(2 * n - 1);
