@@ -131,16 +131,18 @@ def algo_bytes(kind, s, kt, in_lds, a):
     """Total algorithmic HBM bytes of all launches of one kernel kind in one frame."""
     it = kt["items"]
     if kind == "k_trace":
-        # ray I/O: closest 32 B in + 8 B out (t, prim); shadow 32 B in + 4 B index + 1 B out; traversal
-        # bytes (128 B per BVH4 node, 48 B per triangle) only when the scene is not LDS-resident
+        # ray I/O: closest 24 B in (12-B origin + direction records; the camera rays' 8-B (tmin, tmax)
+        # ignored) + 8 B out (t, prim); shadow 32 B in (o + index, d + tmax) + 1 B out; traversal bytes
+        # (128 B per BVH4 node, 48 B per triangle) only when the scene is not LDS-resident
         trav = (128.0 if s["bvh_width"] == 4 else 64.0) * s["node_visits"] + 48.0 * s["tri_tests"]
-        return 40.0 * s["closest_rays"] + 37.0 * s["shadow_rays"] + (0.0 if in_lds else trav)
+        return 32.0 * s["closest_rays"] + 33.0 * s["shadow_rays"] + (0.0 if in_lds else trav)
     if kind == "k_shade":
         return 64.0 * it          # §8d: path-state read + write per path segment
     if kind == "k_nee":
-        # per request: the vertex in (p, prim, wo, pixel, sample) 48 B; out: one shadow ray per light
-        # sample (o, d, index 36 B) + contribution (16 B) + occlusion byte
-        return 48.0 * it + 53.0 * (s["shadow_rays"] / max(1, s["closest_rays"])) * it
+        # per request: the vertex in (p + prim, wo + index, the 8-B pixel / sample / mode word) 40 B;
+        # out: one shadow ray per light sample (o + index, d + tmax: 32 B) + contribution (12-B record)
+        # + occlusion byte
+        return 40.0 * it + 45.0 * (s["shadow_rays"] / max(1, s["closest_rays"])) * it
     if kind == "k_camera":
         # camera ray 32 B + the compact record (sample id, stage, MWC) 16 B: a camera entry's zero
         # throughput / colour / flags are implied by its stage (§8d counted 64 B of initial state)

@@ -332,7 +332,9 @@ struct DevPaths
 	                       // sample / node id in DevQueues::slot and the stage in col.w
 	float4 *csmp;          // compact record: the first-vertex estimate `col` per chunk sample (indexed by
 	                       // sample id), written when it changes, read where it is used (F_COLS)
-	float4 *nee;           // [slots * nee_k] contributions .w = valid
+	float *nee;            // [slots * nee_k] contributions as 12-B records (3 floats); an entry without a valid
+	                       // sample has its occlusion byte set (k_trace writes only the bytes of emitted rays)
+	float *nee_aw;         // [slots * nee_k] the AO entries' material-sample pdf (sampleAmbientOcclusion)
 	uint8_t *occ;          // [slots * nee_k] shadow results
 	float4 *ts;            // [3 * slots * nee_k] transparent shadows: the contribution's factors
 	                       // (surf colour, a) (light colour, b) (c, c divides) — contrib = ((surf * (L * scol)) * a) * b  (* or /) c
@@ -343,8 +345,13 @@ struct DevQueues
 {
 	// active list (parallel to the closest-ray queue)
 	int *slot;
-	float4 *ray_o;         // origin, .w = tmin
-	float4 *ray_d;         // direction, .w = tmax (< 0: infinite); NaN: no ray this iteration
+	// closest rays as 12-B records (3 floats per entry): origin, direction (x = NaN: no ray this
+	// iteration).  The queue of a pass's first iteration (camera / spawned rays) carries each ray's
+	// (tmin, tmax) in ray_tt (tmax < 0: infinite; a spawned node's additional depth in it); every later
+	// iteration's rays (k_shade's bounces) have (ray_min_dist, infinite) and ray_tt == nullptr
+	float *ray_o;
+	float *ray_d;
+	float2 *ray_tt;
 	float *hit_t;
 	int *hit_prim;
 	// shadow rays
@@ -356,11 +363,15 @@ struct DevQueues
 	float4 *sattr;         // [2 * entries] k_surface output for the hit: (N, diffuse_refl), (diffuse colour, -)
 };
 
-// Next-event-estimation requests written by k_shade, consumed by k_nee in the same iteration.
+// Next-event-estimation requests written by k_shade, consumed by k_nee in the same iteration, and
+// k_gather's requests.  NEE (r04): one slot per entry k of the next active list (request of entry k
+// at k, so the index is implicit): wo_k = (outgoing direction, primitive bits), x = NaN for an entry
+// without a request; the hit point is the next queue's ray origin at k (the vertex's continuation
+// ray starts there, a pending-only entry stores it), p_prim unused.
 struct DevNeeQueue
 {
-	float4 *p_prim;        // hit point, .w = primitive (bits)
-	float4 *wo_k;          // outgoing direction, .w = index k of the path in the next active list (bits)
+	float4 *p_prim;        // gather: hit point, .w = primitive (bits)
+	float4 *wo_k;          // gather: outgoing direction, .w = sample id (bits); NEE: (wo, primitive bits)
 	uint4 *pix_mode;       // NEE: (PixelSamplingData offset, sample index, mode | light << 8, 0), packed to 8 B
 	                       // per request while neePm8 (kernels.hip); gather: the first-vertex colour + alpha
 	float4 *attr;          // [2 * requests] surface attributes of the vertex (has_attr only)

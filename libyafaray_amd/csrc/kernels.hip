@@ -148,6 +148,49 @@ struct F3
 	float x, y, z;
 };
 
+// Closest-ray queue entry i (DevQueues::ray_o / ray_d: 12-B records, 24 B per ray instead of 32):
+// false when the entry carries no ray this iteration (NaN direction x).  tmin / tmax (< 0:
+// infinite) come from ray_tt in a pass's first iteration (camera / spawned rays), else every ray is
+// one of k_shade's bounces: (ray_min_dist, infinite).
+__device__ __forceinline__ bool loadQRay(float ray_min_dist, const DevQueues &Q, uint32_t i, V3 &o, V3 &d, float &tmin, float &tmax_w)
+{
+	const F3 dd = reinterpret_cast<const F3 *>(Q.ray_d)[i];
+	d = v3(dd.x, dd.y, dd.z);
+	if(dd.x != dd.x) return false;
+	const F3 oo = reinterpret_cast<const F3 *>(Q.ray_o)[i];
+	o = v3(oo.x, oo.y, oo.z);
+	if(Q.ray_tt)
+	{
+		const float2 tt = Q.ray_tt[i];
+		tmin = tt.x;
+		tmax_w = tt.y;
+	}
+	else
+	{
+		tmin = ray_min_dist;
+		tmax_w = -1.f;
+	}
+	return true;
+}
+typedef float f32x3a4_t __attribute__((ext_vector_type(3))) __attribute__((aligned(4)));
+__device__ __forceinline__ void storeQRay(const DevQueues &Q, uint32_t i, V3 o, V3 d)
+{
+#if YAF_NT_STORE2
+	f32x3a4_t vo, vd;
+	vo.x = o.x; vo.y = o.y; vo.z = o.z;
+	vd.x = d.x; vd.y = d.y; vd.z = d.z;
+	__builtin_nontemporal_store(vo, reinterpret_cast<f32x3a4_t *>(Q.ray_o + 3 * (size_t)i));
+	__builtin_nontemporal_store(vd, reinterpret_cast<f32x3a4_t *>(Q.ray_d + 3 * (size_t)i));
+#else
+	reinterpret_cast<F3 *>(Q.ray_o)[i] = F3{o.x, o.y, o.z};
+	reinterpret_cast<F3 *>(Q.ray_d)[i] = F3{d.x, d.y, d.z};
+#endif
+}
+__device__ __forceinline__ void storeQNoRay(const DevQueues &Q, uint32_t i)
+{
+	Q.ray_d[3 * (size_t)i] = __builtin_nanf("");
+}
+
 // NEE request's third word pair, 8 B instead of 16 (k_shade writes it, k_nee reads it): (PixelSamplingData
 // offset, s | mode << 20 | light << 21) with s = the sample index minus the pass's first index
 // (base_offset + pass_offset, the same for every sample of a launch).  Used while the pass has fewer
@@ -393,20 +436,15 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	// from the sample id); a specular recursion tree keeps them in the queue's slot and col.w
 	// (compact record: the zero throughput, path colour, w and flags of a camera entry are implied by
 	// its stage — k_shade does not read them — so they are not written: 32 B per sample each way)
-	if(!S.tree)
-	{
-		Q.ray_o[a] = f4(from, tmin);
-		Q.ray_d[a] = f4(dir, tmax);
-		P.pr[a] = make_uint4((uint32_t)i, ST_CAMERA, 30903u, seed);
-	}
+	storeQRay(Q, a, from, dir);
+	Q.ray_tt[a] = make_float2(tmin, tmax);
+	if(!S.tree) P.pr[a] = make_uint4((uint32_t)i, ST_CAMERA, 30903u, seed);
 	else
 	{
 		const int cx = sc.x + S.crop_x0, cy = sc.y + S.crop_y0;
 		const uint32_t offset = fnv32((uint32_t)cy * fnv32((uint32_t)cx));
 		const uint32_t sample_idx = S.base_offset + S.pass_offset + (uint32_t)sc.s;
 		Q.slot[a] = i;          // sample id within the chunk travels with the queue entry
-		Q.ray_o[a] = f4(from, tmin);
-		Q.ray_d[a] = f4(dir, tmax);
 		P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);                        // w = 0
 		P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));   // stage
 		P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));         // flags
@@ -429,6 +467,7 @@ struct TraceCtx
 	// the wide nodes level by level, so these are the levels every ray starts with)
 	const float4 *top = nullptr;
 	int n_top = 0;
+	float ray_min_dist = 0.f;   // tmin of the closest rays after a pass's first iteration (loadQRay)
 };
 
 // Transparent-shadow hit list of one shadow ray (accelerator_kdtree.cc:1001-1023): an opaque
@@ -764,7 +803,6 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 		if(node < 0)
 		{
 			// next ray of this lane (closest entries with a NaN direction carry no ray)
-			float4 od, dd;
 			bool got = false;
 			for(;;)
 			{
@@ -773,18 +811,18 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 				j += stride;
 				if(cur < n_a)
 				{
-					od = Q.ray_o[a0 + cur];
-					dd = Q.ray_d[a0 + cur];
-					if(dd.w != dd.w) continue;
-					tmin = od.w;
-					tmax = (dd.w >= 0.f) ? dd.w : inf;
+					float tw;
+					if(!loadQRay(C.ray_min_dist, Q, a0 + cur, o, d, tmin, tw)) continue;
+					tmax = (tw >= 0.f) ? tw : inf;
 					any = false;
 					++n_closest;
 				}
 				else
 				{
-					od = Q.sh_o[s0 + (cur - n_a)];
-					dd = Q.sh_d[s0 + (cur - n_a)];
+					const float4 od = Q.sh_o[s0 + (cur - n_a)];
+					const float4 dd = Q.sh_d[s0 + (cur - n_a)];
+					o = xyz(od);
+					d = xyz(dd);
 					tmin = 0.f;
 					tmax = dd.w;
 					any = true;
@@ -794,8 +832,6 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 				break;
 			}
 			if(!got) break;
-			o = xyz(od);
-			d = xyz(dd);
 			V3 dq = d;
 			if(fabsf(dq.x) < 1e-20f) dq.x = copysignf(1e-20f, dq.x);
 			if(fabsf(dq.y) < 1e-20f) dq.y = copysignf(1e-20f, dq.y);
@@ -1014,6 +1050,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	C.lds_depth = stack_depth;
 	C.spill = spill;
 	C.spill_stride = gridDim.x * blockDim.x;
+	C.ray_min_dist = S.ray_min_dist;
 	if(LDS_SCENE)
 	{
 		float4 *lds_nodes = smem + (stack_depth * kTraceBlock) / 4;
@@ -1057,13 +1094,14 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 		if(j < n_a)
 		{
 			const uint32_t i = a0 + j;
-			const float4 od = Q.ray_o[i], dd = Q.ray_d[i];
-			if(!(dd.w != dd.w))   // NaN marks "no ray this iteration"
+			V3 o, d;
+			float tmin, tw;
+			if(loadQRay(S.ray_min_dist, Q, i, o, d, tmin, tw))   // (a NaN direction marks "no ray this iteration")
 			{
 				float t;
 				int prim;
-				const float tmax = (dd.w >= 0.f) ? dd.w : __builtin_huge_valf();
-				traverse<false, WIDE, SPILL, false, STATS>(C, xyz(od), xyz(dd), od.w, tmax, t, prim, visits, tests);
+				const float tmax = (tw >= 0.f) ? tw : __builtin_huge_valf();
+				traverse<false, WIDE, SPILL, false, STATS>(C, o, d, tmin, tmax, t, prim, visits, tests);
 				Q.hit_t[i] = t;
 				Q.hit_prim[i] = prim;
 				return 1;
@@ -1111,8 +1149,8 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 				uint32_t k = kSortBins - 1;
 				if(j < n_a)
 				{
-					const float4 dd = Q.ray_d[a0 + j];
-					if(!(dd.w != dd.w)) k = rayKey(dd, false);
+					const F3 dd = reinterpret_cast<const F3 *>(Q.ray_d)[a0 + j];
+					if(!(dd.x != dd.x)) k = rayKey(make_float4(dd.x, dd.y, dd.z, 0.f), false);
 				}
 				else if(j < total) k = rayKey(Q.sh_d[s0 + (j - n_a)], true);
 				key[r] = k;
@@ -1227,13 +1265,14 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_brute(DevScene S, DevQueu
 		const bool closest = j < n_a, shadow = !closest && j < total;
 		if(__any(closest))
 		{
-			float4 od = make_float4(0.f, 0.f, 0.f, 0.f), dd = make_float4(0.f, 0.f, 1.f, __builtin_nanf(""));
-			if(closest) { od = Q.ray_o[a0 + j]; dd = Q.ray_d[a0 + j]; }
-			const bool ray = closest && !(dd.w != dd.w);   // NaN marks "no ray this iteration"
+			V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 1.f);
+			float tmin = 0.f, tw = -1.f;
+			const bool ray = closest && loadQRay(S.ray_min_dist, Q, a0 + j, o, d, tmin, tw);   // NaN direction: no ray this iteration
+			if(!ray) { o = v3(0.f, 0.f, 0.f); d = v3(0.f, 0.f, 1.f); }
 			float t;
 			int prim;
-			const float tmax = (dd.w >= 0.f) ? dd.w : __builtin_huge_valf();
-			bruteTrace<false>(tris, n_tris, xyz(od), xyz(dd), od.w, tmax, t, prim, tests, ray);
+			const float tmax = (tw >= 0.f) ? tw : __builtin_huge_valf();
+			bruteTrace<false>(tris, n_tris, o, d, tmin, tmax, t, prim, tests, ray);
 			if(ray)
 			{
 				Q.hit_t[a0 + j] = t;
@@ -1850,10 +1889,36 @@ __device__ __forceinline__ bool lightMatHit(const DevScene &S, const DevLight &L
 	return true;
 }
 
-template<bool EXT, class Out>
+// NEE contribution slots.  In HBM (DevPaths::nee) a 12-B colour record per entry: an entry without a
+// valid sample gets its occlusion byte set (k_trace writes the bytes of emitted shadow rays only), so
+// the connection's `valid && !occluded` test is the occlusion byte alone; the AO entries' pdf goes to
+// nee_aw.  The megakernel's LDS slots keep float4 (contribution, valid) — and the byte, too.
+struct NeeHbm
+{
+	float *c;
+	float *aw;
+};
+__device__ __forceinline__ NeeHbm neeHbm(const DevPaths &P) { return NeeHbm{P.nee, P.nee_aw}; }
+__device__ __forceinline__ void neePut(float4 *nee, uint8_t *occ, int e, C3 c, bool ok)
+{
+	nee[e] = f4(c, ok ? 1.f : 0.f);
+	occ[e] = ok ? 0 : 1;
+}
+__device__ __forceinline__ void neePut(const NeeHbm &nee, uint8_t *occ, int e, C3 c, bool ok)
+{
+	reinterpret_cast<F3 *>(nee.c)[e] = F3{c.r, c.g, c.b};
+	occ[e] = ok ? 0 : 1;
+}
+__device__ __forceinline__ C3 neeGet(const NeeHbm &nee, int e)
+{
+	const F3 c = reinterpret_cast<const F3 *>(nee.c)[e];
+	return C3{c.x, c.y, c.z};
+}
+
+template<bool EXT, class Out, class NeeT>
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
-                         float4 *nee, uint8_t *occ, const Out &out, float4 *ts = nullptr)
+                         NeeT nee, uint8_t *occ, const Out &out, float4 *ts = nullptr)
 {
 	const bool cast_shadows = L.cast_shadows && m.receive_shadows;
 	const float p_len = length(sp.p);
@@ -1879,11 +1944,9 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			const C3 transmit = c3(1.f);
 			contrib = surf_col * lcol * angle * transmit;
 			shadowRayOf(sp.p, ldir, sh_tmin, dist, so, st);
-			nee[e0] = f4(contrib, 1.f);
 			if(ts && cast_shadows) tsFactors(ts, e0, surf_col, angle, lcol, 1.f, 1.f, false);
 		}
-		else if(active) nee[e0] = make_float4(0.f, 0.f, 0.f, 0.f);
-		if(active) occ[e0] = 0;
+		if(active) neePut(nee, occ, e0, contrib, ok);
 		out.emit(ok && cast_shadows, so, ldir, st, sh_tmin, e0);
 		return;
 	}
@@ -1940,11 +2003,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 				else ok = false;
 			}
 		}
-		if(active)
-		{
-			nee[e0 + i] = f4(contrib, ok ? 1.f : 0.f);
-			occ[e0 + i] = 0;
-		}
+		if(active) neePut(nee, occ, e0 + i, contrib, ok);
 		out.emit(ok && cast_shadows, so, ldir, st, sh_tmin, e0 + i);
 
 		// areaLightSampleMaterial (montecarlo.cc:284-383)
@@ -1988,11 +2047,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 				else ok = false;
 			}
 		}
-		if(active)
-		{
-			nee[e0 + num_samples + i] = f4(contrib, ok ? 1.f : 0.f);
-			occ[e0 + num_samples + i] = 0;
-		}
+		if(active) neePut(nee, occ, e0 + num_samples + i, contrib, ok);
 		out.emit(ok && cast_shadows, so, dir, st, b_tmin, e0 + num_samples + i);
 	}
 }
@@ -2003,7 +2058,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 // previous direction when it draws none (light_ray.dir_ persists, :647); such samples weigh 0.
 template<bool EXT>
 __device__ void aoSamples(const DevScene &S, const DevMaterial &m, const Surf &sp, V3 wo, uint32_t sample_idx, uint32_t offset,
-                          bool active, int e0, float4 *nee, uint8_t *occ, const ShadeOut &out, float4 *ts)
+                          bool active, int e0, const NeeHbm &nee, uint8_t *occ, const ShadeOut &out, float4 *ts)
 {
 	const int n = S.ao_samples;
 	const uint32_t offs = (uint32_t)n * sample_idx + offset;
@@ -2039,7 +2094,8 @@ __device__ void aoSamples(const DevScene &S, const DevMaterial &m, const Surf &s
 			want = !(contrib.r == 0.f && contrib.g == 0.f && contrib.b == 0.f);
 			shadowRayOf(sp.p, dir, sh_tmin, S.ao_dist, so, st);
 			if(ts && want) tsFactors(ts, e0 + i, surf_col, cos, ao_col, w, 1.f, false);
-			nee[e0 + i] = f4(contrib, s.pdf);
+			reinterpret_cast<F3 *>(nee.c)[e0 + i] = F3{contrib.r, contrib.g, contrib.b};
+			nee.aw[e0 + i] = s.pdf;
 			occ[e0 + i] = 0;
 		}
 		emitShadow(want, so, dir, st, sh_tmin, e0 + i, out);
@@ -2048,14 +2104,13 @@ __device__ void aoSamples(const DevScene &S, const DevMaterial &m, const Surf &s
 
 // AO result of a vertex: sum in sample order of emit * pdf (emitting materials) and the unoccluded
 // contributions, divided by the sample count (integrator_tiled.cc:672-690)
-__device__ C3 aoSum(const DevScene &S, const float4 *nee, const uint8_t *occ, int k0, bool emitting, C3 emit)
+__device__ C3 aoSum(const DevScene &S, const NeeHbm &nee, const uint8_t *occ, int k0, bool emitting, C3 emit)
 {
 	C3 col = c3(0.f);
 	for(int i = 0; i < S.ao_samples; ++i)
 	{
-		const float4 e = nee[k0 + i];
-		if(emitting) col = col + emit * e.w;
-		if(!occ[k0 + i]) col = col + rgb(e);
+		if(emitting) col = col + emit * nee.aw[k0 + i];
+		if(!occ[k0 + i]) col = col + neeGet(nee, k0 + i);
 	}
 	return col / (float)S.ao_samples;
 }
@@ -2357,7 +2412,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		PHASE(0);
 		// ---- 1. connect the pending next-event estimate ----
 		const int kb = (int)i * K;
-		auto ge = [&](int k) { return Pc.nee[k]; };
+		// (HBM slots: validity is in the occlusion byte)
+		auto ge = [&](int k) { return f4(neeGet(neeHbm(Pc), k), 1.f); };
 		auto go = [&](int k) { return Pc.occ[k] != 0; };
 		if(live && (flags & F_PEND_V0))
 		{
@@ -2370,7 +2426,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			// DirectLight: col += sampleAmbientOcclusion (integrator_direct_light.cc:124)
 			if(S.do_ao)
 			{
-				const C3 ao = aoSum(S, Pc.nee, Pc.occ, (int)i * K + S.nee_all_count, (flags & F_AO_EMIT) != 0, rgb(pem4));
+				const C3 ao = aoSum(S, neeHbm(Pc), Pc.occ, (int)i * K + S.nee_all_count, (flags & F_AO_EMIT) != 0, rgb(pem4));
 				if(ao_after_caustic) ao_extra = ao;
 				else col = col + ao;
 			}
@@ -2400,17 +2456,19 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			hit_prim = A.Q.hit_prim[i];
 			if(hit_prim >= 0)
 			{
-				const float4 ro = A.Q.ray_o[i], rd = A.Q.ray_d[i];
-				if(EXT && S.cur_level > 0) add_depth_in = (int)(-rd.w) - 1;
+				V3 ro, rd;
+				float tmin_unused, tw;
+				loadQRay(S.ray_min_dist, A.Q, i, ro, rd, tmin_unused, tw);
+				if(EXT && S.cur_level > 0) add_depth_in = (int)(-tw) - 1;
 				have_hit = true;
-				sp = makeSurf(S, xyz(ro), xyz(rd), A.Q.hit_t[i], hit_prim);
+				sp = makeSurf(S, ro, rd, A.Q.hit_t[i], hit_prim);
 				if(ATTR)
 				{
 					sa0 = A.Q.sattr[2 * (size_t)i];
 					sa1 = A.Q.sattr[2 * (size_t)i + 1];
 					applyAttr(sp, sa0, sa1);
 				}
-				wo = -xyz(rd);
+				wo = -rd;
 			}
 		}
 		bool nee_v0 = false, nee_one = false, sample_next = false, end_sub = false, finalize = false, start_sub = false;
@@ -2662,15 +2720,13 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		if(keep)
 		{
 			if(!compact) stStore2(&A.Qn.slot[k], (int)sid);
-			if(want_ray)
-			{
-				stStore2(&A.Qn.ray_o[k], f4(ray_o, S.ray_min_dist));
-				stStore2(&A.Qn.ray_d[k], f4(ray_d, -1.f));
-			}
+			if(want_ray) storeQRay(A.Qn, k, ray_o, ray_d);   // (tmin = ray_min_dist, tmax infinite: loadQRay)
 			else
 			{
-				A.Qn.ray_o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-				A.Qn.ray_d[k] = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));
+				storeQNoRay(A.Qn, k);
+				// a pending-only entry keeps its hit point here for its NEE request (k_nee reads the
+				// vertex from the ray origin; a continuing entry's ray starts at the vertex)
+				if(!FUSED && want_nee) reinterpret_cast<F3 *>(A.Qn.ray_o)[k] = F3{sp.p.x, sp.p.y, sp.p.z};
 				stage = ST_NORAY | (subpath << 8) | ((uint32_t)depth << 20);
 			}
 			if(compact) stStore(&Pn.pr[k], make_uint4(sid, stage, rng.x, rng.y));
@@ -2704,9 +2760,9 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			if(__any(all))
 			{
 				for(int l = 0; l < S.n_lights; ++l)
-					neeLight<EXT>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, all, e0 + (int)S.lights[l].nee_base, Pn.nee,
+					neeLight<EXT>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, all, e0 + (int)S.lights[l].nee_base, neeHbm(Pn),
 					              Pn.occ, out, ts);
-				if(S.do_ao) aoSamples<EXT>(S, m, sp, wo, sample_idx, offset, all, e0 + S.nee_all_count, Pn.nee, Pn.occ, out, ts);
+				if(S.do_ao) aoSamples<EXT>(S, m, sp, wo, sample_idx, offset, all, e0 + S.nee_all_count, neeHbm(Pn), Pn.occ, out, ts);
 			}
 			if(__any(one))
 			{
@@ -2714,23 +2770,28 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				{
 					const bool mine = one && lnum == (uint32_t)l;
 					if(!__any(mine)) continue;
-					neeLight<EXT>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, mine, e0, Pn.nee, Pn.occ, out, ts);
+					neeLight<EXT>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, mine, e0, neeHbm(Pn), Pn.occ, out, ts);
 				}
 			}
 		}
-		const uint32_t jn = waveAppend(!FUSED && want_nee, &s_count[1]);
+		// NEE requests sit at the entry's own next-queue position k (DevNeeQueue): no index and no hit
+		// point travel with them (k_nee reads the vertex from the next queue's ray origin at k); the
+		// append only counts them (statistics)
+		(void)waveAppend(!FUSED && want_nee, &s_count[1]);
 		const uint32_t jg = waveAppend(want_gather, &s_count[3]);
-		if(!FUSED && want_nee)
+		if(!FUSED && keep)
 		{
-			const uint32_t j = a0 + jn;
-			stStore2(&A.N.p_prim[j], f4(sp.p, __int_as_float(hit_prim)));
-			stStore2(&A.N.wo_k[j], f4(wo, __uint_as_float(k)));
-			neePmStore(S, A.N.pix_mode, j, offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8));
-			if(ATTR)
+			if(want_nee)
 			{
-				A.N.attr[2 * (size_t)j] = f4(sp.n, sp.drefl);
-				A.N.attr[2 * (size_t)j + 1] = f4(sp.dcol, sp.sigma);
+				stStore2(&A.N.wo_k[k], f4(wo, __int_as_float(hit_prim)));
+				neePmStore(S, A.N.pix_mode, k, offset, sample_idx, (nee_v0 ? 1u : 0u) | (lnum << 8));
+				if(ATTR)
+				{
+					A.N.attr[2 * (size_t)k] = f4(sp.n, sp.drefl);
+					A.N.attr[2 * (size_t)k + 1] = f4(sp.dcol, sp.sigma);
+				}
 			}
+			else reinterpret_cast<float *>(A.N.wo_k)[4 * (size_t)k] = __builtin_nanf("");   // no request
 		}
 		if(want_gather)
 		{
@@ -2785,8 +2846,9 @@ __global__ void __launch_bounds__(256) k_spawn(DevScene S, DevPaths P, DevQueues
 	const uint32_t a = (g % S.n_seg) * S.cap_a + (g / S.n_seg) * 256u + (uint32_t)i % 256u;
 	const uint32_t idx = s0 + (uint32_t)i;
 	Q.slot[a] = (int)(S.node_base + idx);
-	Q.ray_o[a] = S.spawn_o[idx];
-	Q.ray_d[a] = S.spawn_d[idx];
+	const float4 so = S.spawn_o[idx], sd = S.spawn_d[idx];
+	storeQRay(Q, a, xyz(so), xyz(sd));
+	Q.ray_tt[a] = make_float2(so.w, sd.w);
 	P.thr[a] = make_float4(0.f, 0.f, 0.f, 0.f);
 	P.col[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(ST_CAMERA));
 	P.pcol[a] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
@@ -2845,12 +2907,11 @@ __global__ void __launch_bounds__(kShadeBlock) k_surface(DevScene S, DevQueues Q
 	for(uint32_t j = threadIdx.x; j < n_a; j += blockDim.x)
 	{
 		const uint32_t i = a0 + j;
-		const float4 rd = Q.ray_d[i];
-		if(rd.w != rd.w) continue;   // no ray this iteration (NaN marker)
+		V3 o, d;
+		float tmin_unused, tw_unused;
+		if(!loadQRay(S.ray_min_dist, Q, i, o, d, tmin_unused, tw_unused)) continue;   // no ray this iteration (NaN marker)
 		const int prim = Q.hit_prim[i];
 		if(prim < 0) continue;
-		const float4 ro = Q.ray_o[i];
-		const V3 o = xyz(ro), d = xyz(rd);
 		const V3 p = o + Q.hit_t[i] * d;   // accelerator.cc:61
 		const SurfAttr sa = surfAttr(S.prim_attr, S.prim_ng, prim, o, d, p);
 		const DevMaterial &m = S.mats[__float_as_int(S.prim_ng[prim].w)];
@@ -2931,7 +2992,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_tshadow(DevScene S, DevQueues Q
 		x = x * f0.w;
 		x = x * f1.w;
 		x = (f2.y != 0.f) ? x / f2.x : x * f2.x;
-		P.nee[e] = f4(x, P.nee[e].w);
+		reinterpret_cast<F3 *>(P.nee)[e] = F3{x.r, x.g, x.b};
 	}
 }
 
@@ -3152,29 +3213,38 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 	out.sh_base = seg * S.cap_s;
 	out.Qn = A.Qn;
 	out.idx_in_o = !S.tr_shad;
+	// one request slot per entry of the next active list (k_shade writes entry k's request at k; a
+	// NaN direction marks an entry without one)
 	const uint32_t n_req = A.cnt_next.n_nee[seg];
+	const uint32_t n_slots = A.cnt_next.n_active[seg];
 	const uint32_t a0 = seg * S.cap_a;
 	const int K = S.nee_k;
 	const uint32_t stride = blockDim.x;
-	for(uint32_t base_j = 0; base_j < n_req; base_j += stride)
+	for(uint32_t base_j = 0; base_j < n_slots; base_j += stride)
 	{
-		const bool live = base_j + threadIdx.x < n_req;
 		const uint32_t j = a0 + base_j + threadIdx.x;
-		float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), wk = pp;
+		float4 wk = make_float4(0.f, 0.f, 0.f, 0.f);
+		V3 p = v3(0.f, 0.f, 0.f);
 		uint4 pm = make_uint4(0u, 0u, 0u, 0u);
+		bool live = base_j + threadIdx.x < n_slots;
 		if(live)
 		{
-			pp = A.N.p_prim[j];
 			wk = A.N.wo_k[j];
+			live = !(wk.x != wk.x);
+		}
+		if(live)
+		{
+			const F3 o = reinterpret_cast<const F3 *>(A.Qn.ray_o)[j];
+			p = v3(o.x, o.y, o.z);
 			pm = neePmLoad(S, A.N.pix_mode, j);
 		}
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
 		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
-		if(live) sp = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
+		if(live) sp = surfFromPrim(S, p, __float_as_int(wk.w));
 		if(ATTR && live) applyAttr(sp, A.N.attr[2 * (size_t)j], A.N.attr[2 * (size_t)j + 1]);
 		const V3 wo = xyz(wk);
-		const int e0 = (int)__float_as_uint(wk.w) * K;
+		const int e0 = (int)j * K;
 		const bool all = live && (pm.z & 1u);
 		const bool one = live && !(pm.z & 1u);
 		const uint32_t lnum = pm.z >> 8;
@@ -3190,7 +3260,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 				const bool mine = all || (one && lnum == (uint32_t)l);
 				if(!__any(mine)) continue;
 				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0 + (all ? (int)S.lights[l].nee_base : 0),
-				              A.Pn.nee, A.Pn.occ, rs);
+				              neeHbm(A.Pn), A.Pn.occ, rs);
 			}
 			float t_dummy;
 			int p_dummy;
@@ -3204,9 +3274,9 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 			// estimateAllDirectLight (montecarlo.cc:54-68)
 			for(int l = 0; l < S.n_lights; ++l)
 				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
-				         e0 + (int)S.lights[l].nee_base, A.Pn.nee, A.Pn.occ, out, S.tr_shad ? A.Pn.ts : nullptr);
+				         e0 + (int)S.lights[l].nee_base, neeHbm(A.Pn), A.Pn.occ, out, S.tr_shad ? A.Pn.ts : nullptr);
 			if(S.do_ao)
-				aoSamples<EXT>(S, S.mats[sp.mat], sp, wo, pm.y, pm.x, all, e0 + S.nee_all_count, A.Pn.nee, A.Pn.occ, out,
+				aoSamples<EXT>(S, S.mats[sp.mat], sp, wo, pm.y, pm.x, all, e0 + S.nee_all_count, neeHbm(A.Pn), A.Pn.occ, out,
 				               S.tr_shad ? A.Pn.ts : nullptr);
 		}
 		if(__any(one))
@@ -3216,7 +3286,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 			{
 				const bool mine = one && lnum == (uint32_t)l;
 				if(!__any(mine)) continue;
-				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, A.Pn.nee, A.Pn.occ, out,
+				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, neeHbm(A.Pn), A.Pn.occ, out,
 				              S.tr_shad ? A.Pn.ts : nullptr);
 			}
 		}

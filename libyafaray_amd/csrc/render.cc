@@ -302,7 +302,7 @@ struct GpuRenderer::Impl
 	int film_w = 0, film_h = 0;
 	// chunk buffers
 	size_t slots_cap = 0;
-	bool v0_alloc = false, tree_alloc = false;
+	bool v0_alloc = false, tree_alloc = false, ao_alloc = false;
 	int nee_cap = 0;
 	std::vector<Buf> chunk_bufs;
 	DevPaths P[2]{};       // path state, parallel to Q[q] (indexed by queue position)
@@ -1605,7 +1605,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	// transparent shadows keep shadowDepth (t, primitive) pairs per shadow ray: deep lists shrink the chunk
 	// so that the lists stay within 16 GB
 	if(need_ts > 0) M = std::min(M, std::max<size_t>(65536, ((size_t)16 << 30) / ((size_t)K * 8 * (size_t)need_ts)));
-	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc || need_ts != d.ts_alloc || need_g != d.g_alloc ||
+	if(M > d.slots_cap || K > d.nee_cap || need_v0 != d.v0_alloc || need_attr != d.attr_alloc || need_ts != d.ts_alloc || need_g != d.g_alloc || (S.do_ao != 0) != d.ao_alloc ||
 	   need_tree != d.tree_alloc)
 	{
 		// Wavefront buffers for M samples in flight (~0.7 KB each: 288 GB of HBM holds tens of millions,
@@ -1639,7 +1639,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				P.v0p = (float4 *)A(need_v0 ? MA * 16 : 16);      // first-hit data: path_samples > 1 only
 				P.v0wo = (float4 *)A(need_v0 ? MA * 16 : 16);
 				P.pr = (uint4 *)A(MA * 16);
-				P.nee = (float4 *)A(MA * K * 16);
+				P.nee = (float *)A(MA * K * 12);
+				P.nee_aw = (float *)A(S.do_ao ? MA * K * 4 : 16);
 				P.occ = (uint8_t *)A(MA * K);
 				P.v0attr = (float4 *)A(need_v0 && need_attr ? MA * 32 : 16);
 				P.ts = (float4 *)A(need_ts ? MA * K * 48 : 16);
@@ -1648,8 +1649,10 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			{
 				DevQueues &Q = d.Q[q];
 				Q.slot = (int *)A(need_tree ? MA * 4 : 16);
-				Q.ray_o = (float4 *)A(MA * 16);
-				Q.ray_d = (float4 *)A(MA * 16);
+				Q.ray_o = (float *)A(MA * 12);
+				Q.ray_d = (float *)A(MA * 12);
+				// (tmin, tmax) of the camera / spawned rays: a pass's first iteration, always queue 0
+				Q.ray_tt = q == 0 ? (float2 *)A(MA * 8) : nullptr;
 				Q.hit_t = (float *)A(MA * 4);
 				Q.hit_prim = (int *)A(MA * 4);
 				Q.sh_o = (float4 *)A(MA * K * 16);
@@ -1661,7 +1664,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			}
 			// the compact record's first-vertex estimates, by chunk sample id (shared by both state sets)
 			d.P[0].csmp = d.P[1].csmp = (float4 *)A(need_tree ? 16 : MA * 16);
-			d.N.p_prim = (float4 *)A(MA * 16);
+			d.N.p_prim = (float4 *)A(16);   // (NEE: the hit point is the next queue's ray origin)
 			d.N.wo_k = (float4 *)A(MA * 16);
 			d.N.pix_mode = (uint4 *)A(MA * 16);
 			d.N.attr = (float4 *)A(need_attr ? MA * 32 : 16);
@@ -1683,6 +1686,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		d.ts_alloc = need_ts;
 		d.g_alloc = need_g;
 		d.tree_alloc = need_tree;
+		d.ao_alloc = S.do_ao != 0;
 		d.slots_cap = M;
 		d.nee_cap = K;
 	}
@@ -1791,13 +1795,17 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		const bool count_run = S.lpc_mode == 1;
 		for(int it = 0; it < iters; ++it)
 		{
-			PROF(KK_TRACE, yafamd_launch_trace(&S, &d.Q[cur], &cnt[cur], &d.P[cur], run_stats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+			// the first iteration's closest rays (camera / spawned, queue 0) carry their own (tmin, tmax);
+			// k_shade's bounce rays all have (ray_min_dist, infinite)
+			DevQueues qc = d.Q[cur];
+			if(it != 0) qc.ray_tt = nullptr;
+			PROF(KK_TRACE, yafamd_launch_trace(&S, &qc, &cnt[cur], &d.P[cur], run_stats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 			// material-shade dispatch for textured / smooth scenes: surface attributes + shader nodes
 			// of every hit, before k_shade reads them
 			// transparent shadows: filter colours of the transparent surfaces the shadow rays crossed
-			if(S.tr_shad && !count_run) PROF(KK_TSHADOW, yafamd_launch_tshadow(&S, &d.Q[cur], &cnt[cur], &d.P[cur], d.stream));
-			if(S.has_attr) PROF(KK_SURFACE, yafamd_launch_surface(&S, &d.Q[cur], &cnt[cur], d.stream));
-			PROF(KK_SHADE, yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &d.Q[cur], &d.Q[cur ^ 1], &d.N, &d.G, &cnt[cur], &cnt[cur ^ 1],
+			if(S.tr_shad && !count_run) PROF(KK_TSHADOW, yafamd_launch_tshadow(&S, &qc, &cnt[cur], &d.P[cur], d.stream));
+			if(S.has_attr) PROF(KK_SURFACE, yafamd_launch_surface(&S, &qc, &cnt[cur], d.stream));
+			PROF(KK_SHADE, yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &qc, &d.Q[cur ^ 1], &d.N, &d.G, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 
 			// photon-map estimates of the finished diffuse first hits: the direct-lighting pipeline
