@@ -154,11 +154,12 @@ struct F3
 // one of k_shade's bounces: (ray_min_dist, infinite).
 __device__ __forceinline__ bool loadQRay(float ray_min_dist, const DevQueues &Q, uint32_t i, V3 &o, V3 &d, float &tmin, float &tmax_w)
 {
+	// (both records loaded before the test: one memory round trip, not two dependent ones)
 	const F3 dd = reinterpret_cast<const F3 *>(Q.ray_d)[i];
-	d = v3(dd.x, dd.y, dd.z);
-	if(dd.x != dd.x) return false;
 	const F3 oo = reinterpret_cast<const F3 *>(Q.ray_o)[i];
+	d = v3(dd.x, dd.y, dd.z);
 	o = v3(oo.x, oo.y, oo.z);
+	if(dd.x != dd.x) return false;
 	if(Q.ray_tt)
 	{
 		const float2 tt = Q.ray_tt[i];
@@ -3229,14 +3230,12 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 		bool live = base_j + threadIdx.x < n_slots;
 		if(live)
 		{
+			// every load issued before the request test (one memory round trip)
 			wk = A.N.wo_k[j];
-			live = !(wk.x != wk.x);
-		}
-		if(live)
-		{
 			const F3 o = reinterpret_cast<const F3 *>(A.Qn.ray_o)[j];
 			p = v3(o.x, o.y, o.z);
 			pm = neePmLoad(S, A.N.pix_mode, j);
+			live = !(wk.x != wk.x);
 		}
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;

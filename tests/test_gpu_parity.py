@@ -214,6 +214,18 @@ def test_depth_of_field_matches_oracle(product, oracle_built, case):
     assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
 
 
+@pytest.mark.parametrize("clip", [(3.4, -1.0), (0.0, 4.6), (3.4, 4.6)])
+def test_camera_clip_planes_match_oracle(product, oracle_built, clip):
+    """nearClip / farClip (camera.cc:51-71, camera_perspective.cc:128-146): every camera ray carries
+    its own (tmin, tmax) — the queue's side array of a pass's first iteration (the bounce rays'
+    12-B records carry neither) — PT without RR against the oracle, <= 4 ULP."""
+    spec = scenes.cornell(48, 36, spp=2, bounces=3, rr=False).with_camera(near_clip=clip[0], far_clip=clip[1])
+    rgba, w, _ = product.render_spec(spec, chunk_slots=2048)
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=8).render()
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    assert ulp_diff(rgba, orgba).max() <= 4
+
+
 def test_depth_of_field_with_adaptive_passes(product, oracle_built):
     """DOF lens streams restart at every pass's offset (integrator_tiled.cc:314-316)."""
     spec = scenes.test01(40, 40, spp=2).with_camera(aperture=0.3, dof_distance=8.0, bokeh_type="pentagon").with_render(
