@@ -152,11 +152,45 @@ struct F3
 // false when the entry carries no ray this iteration (NaN direction x).  tmin / tmax (< 0:
 // infinite) come from ray_tt in a pass's first iteration (camera / spawned rays), else every ray is
 // one of k_shade's bounces: (ray_min_dist, infinite).
+// -DYAF_NT_RAYLOAD=1: the ray streams of k_trace are loaded / stored non-temporally (streaming
+// lines evicted first: the node working set of a BVH in global memory keeps more of the L2)
+#ifndef YAF_NT_RAYLOAD
+#define YAF_NT_RAYLOAD 0
+#endif
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ F3 rayLd3(const float *p, uint32_t i)
+{
+#if YAF_NT_RAYLOAD
+	const float *q = p + 3 * (size_t)i;
+	return F3{__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1), __builtin_nontemporal_load(q + 2)};
+#else
+	return reinterpret_cast<const F3 *>(p)[i];
+#endif
+}
+__device__ __forceinline__ float4 rayLd4(const float4 *p)
+{
+#if YAF_NT_RAYLOAD
+	const f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(p));
+	return make_float4(v.x, v.y, v.z, v.w);
+#else
+	return *p;
+#endif
+}
+template<class T>
+__device__ __forceinline__ void raySt(T *p, T v)
+{
+#if YAF_NT_RAYLOAD
+	__builtin_nontemporal_store(v, p);
+#else
+	*p = v;
+#endif
+}
+
 __device__ __forceinline__ bool loadQRay(float ray_min_dist, const DevQueues &Q, uint32_t i, V3 &o, V3 &d, float &tmin, float &tmax_w)
 {
 	// (both records loaded before the test: one memory round trip, not two dependent ones)
-	const F3 dd = reinterpret_cast<const F3 *>(Q.ray_d)[i];
-	const F3 oo = reinterpret_cast<const F3 *>(Q.ray_o)[i];
+	const F3 dd = rayLd3(Q.ray_d, i);
+	const F3 oo = rayLd3(Q.ray_o, i);
 	d = v3(dd.x, dd.y, dd.z);
 	o = v3(oo.x, oo.y, oo.z);
 	if(dd.x != dd.x) return false;
@@ -820,8 +854,8 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 				}
 				else
 				{
-					const float4 od = Q.sh_o[s0 + (cur - n_a)];
-					const float4 dd = Q.sh_d[s0 + (cur - n_a)];
+					const float4 od = rayLd4(&Q.sh_o[s0 + (cur - n_a)]);
+					const float4 dd = rayLd4(&Q.sh_d[s0 + (cur - n_a)]);
 					o = xyz(od);
 					d = xyz(dd);
 					tmin = 0.f;
@@ -932,8 +966,8 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 			if(any) P.occ[__float_as_int(Q.sh_o[s0 + (cur - n_a)].w)] = prim_best >= 0 ? 1 : 0;   // P = state set of the consumer shade
 			else
 			{
-				Q.hit_t[a0 + cur] = t_best;
-				Q.hit_prim[a0 + cur] = prim_best;
+				raySt(&Q.hit_t[a0 + cur], t_best);
+				raySt(&Q.hit_prim[a0 + cur], prim_best);
 			}
 			node = -1;
 		}
@@ -1103,15 +1137,15 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 				int prim;
 				const float tmax = (tw >= 0.f) ? tw : __builtin_huge_valf();
 				traverse<false, WIDE, SPILL, false, STATS>(C, o, d, tmin, tmax, t, prim, visits, tests);
-				Q.hit_t[i] = t;
-				Q.hit_prim[i] = prim;
+				raySt(&Q.hit_t[i], t);
+				raySt(&Q.hit_prim[i], prim);
 				return 1;
 			}
 		}
 		else if(j < total)
 		{
 			const uint32_t k = s0 + (j - n_a);
-			const float4 od = Q.sh_o[k], dd = Q.sh_d[k];
+			const float4 od = rayLd4(&Q.sh_o[k]), dd = rayLd4(&Q.sh_d[k]);
 			float t;
 			int prim;
 			bool occ;
