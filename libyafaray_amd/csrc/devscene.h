@@ -144,7 +144,10 @@ struct DevLight
 struct DevCamera
 {
 	float pos[4], vright[4], vup[4], vto[4], cam_z[4], near_p[4], far_p[4];
-	int resx, resy, pad0, pad1;
+	int resx, resy;
+	int ray_tt;                    // the camera rays need their own (tmin, tmax): a near plane off the camera
+	                               // position or a far plane in front of it (else every ray has (0, unbounded))
+	int pad1;
 	// depth of field (camera_perspective.cc:28-52, 71-146): aperture * camera axes, bokeh polygon
 	float dof_rt[4], dof_up[4];
 	float aperture, dof_distance;
@@ -352,6 +355,8 @@ struct DevQueues
 	float *ray_o;
 	float *ray_d;
 	float2 *ray_tt;
+	float tmin_dflt;       // tmin of the rays without ray_tt (camera rays with the default clip planes: 0;
+	                       // bounce rays: ray_min_dist); tmax unbounded
 	float *hit_t;
 	int *hit_prim;
 	// shadow rays

@@ -1247,6 +1247,15 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		put(S.cam.cam_z, cam_z);
 		put(S.cam.near_p, add(pos, mul(cam_z, c.near_clip)));
 		put(S.cam.far_p, add(pos, mul(cam_z, c.far_clip)));
+		{
+			// cameraRay's numerators (dot(cam_z, plane point - pos), the device's float operations): a near
+			// plane through the position gives tmin = 0 and a far numerator < 0 a negative (unbounded) tmax
+			// for every ray — then k_camera writes no per-ray (tmin, tmax) and k_trace takes (0, unbounded)
+			const F3 dn = sub(add(pos, mul(cam_z, c.near_clip)), pos), df = sub(add(pos, mul(cam_z, c.far_clip)), pos);
+			const bool near0 = dn.x == 0.f && dn.y == 0.f && dn.z == 0.f;
+			const float far_num = cam_z.x * df.x + cam_z.y * df.y + cam_z.z * df.z;
+			S.cam.ray_tt = (near0 && far_num < -1e-20f) ? 0 : 1;
+		}
 		S.cam.resx = c.resx;
 		S.cam.resy = c.resy;
 		// depth of field (camera_perspective.cc:28-52, 59-62, 212-224)

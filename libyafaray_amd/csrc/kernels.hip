@@ -150,8 +150,9 @@ struct F3
 
 // Closest-ray queue entry i (DevQueues::ray_o / ray_d: 12-B records, 24 B per ray instead of 32):
 // false when the entry carries no ray this iteration (NaN direction x).  tmin / tmax (< 0:
-// infinite) come from ray_tt in a pass's first iteration (camera / spawned rays), else every ray is
-// one of k_shade's bounces: (ray_min_dist, infinite).
+// infinite) come from ray_tt in a pass's first iteration when its rays carry their own (spawned rays;
+// camera rays with clip planes), else (Q.tmin_dflt, infinite): camera rays 0, k_shade's bounces
+// ray_min_dist.
 // -DYAF_NT_RAYLOAD=1: the ray streams of k_trace are loaded / stored non-temporally (streaming
 // lines evicted first: the node working set of a BVH in global memory keeps more of the L2)
 #ifndef YAF_NT_RAYLOAD
@@ -186,7 +187,7 @@ __device__ __forceinline__ void raySt(T *p, T v)
 #endif
 }
 
-__device__ __forceinline__ bool loadQRay(float ray_min_dist, const DevQueues &Q, uint32_t i, V3 &o, V3 &d, float &tmin, float &tmax_w)
+__device__ __forceinline__ bool loadQRay(const DevQueues &Q, uint32_t i, V3 &o, V3 &d, float &tmin, float &tmax_w)
 {
 	// (both records loaded before the test: one memory round trip, not two dependent ones)
 	const F3 dd = rayLd3(Q.ray_d, i);
@@ -202,7 +203,7 @@ __device__ __forceinline__ bool loadQRay(float ray_min_dist, const DevQueues &Q,
 	}
 	else
 	{
-		tmin = ray_min_dist;
+		tmin = Q.tmin_dflt;
 		tmax_w = -1.f;
 	}
 	return true;
@@ -472,7 +473,7 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	// (compact record: the zero throughput, path colour, w and flags of a camera entry are implied by
 	// its stage — k_shade does not read them — so they are not written: 32 B per sample each way)
 	storeQRay(Q, a, from, dir);
-	Q.ray_tt[a] = make_float2(tmin, tmax);
+	if(S.cam.ray_tt) Q.ray_tt[a] = make_float2(tmin, tmax);
 	if(!S.tree) P.pr[a] = make_uint4((uint32_t)i, ST_CAMERA, 30903u, seed);
 	else
 	{
@@ -502,7 +503,6 @@ struct TraceCtx
 	// the wide nodes level by level, so these are the levels every ray starts with)
 	const float4 *top = nullptr;
 	int n_top = 0;
-	float ray_min_dist = 0.f;   // tmin of the closest rays after a pass's first iteration (loadQRay)
 };
 
 // Transparent-shadow hit list of one shadow ray (accelerator_kdtree.cc:1001-1023): an opaque
@@ -847,7 +847,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 				if(cur < n_a)
 				{
 					float tw;
-					if(!loadQRay(C.ray_min_dist, Q, a0 + cur, o, d, tmin, tw)) continue;
+					if(!loadQRay(Q, a0 + cur, o, d, tmin, tw)) continue;
 					tmax = (tw >= 0.f) ? tw : inf;
 					any = false;
 					++n_closest;
@@ -1085,7 +1085,6 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	C.lds_depth = stack_depth;
 	C.spill = spill;
 	C.spill_stride = gridDim.x * blockDim.x;
-	C.ray_min_dist = S.ray_min_dist;
 	if(LDS_SCENE)
 	{
 		float4 *lds_nodes = smem + (stack_depth * kTraceBlock) / 4;
@@ -1131,7 +1130,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 			const uint32_t i = a0 + j;
 			V3 o, d;
 			float tmin, tw;
-			if(loadQRay(S.ray_min_dist, Q, i, o, d, tmin, tw))   // (a NaN direction marks "no ray this iteration")
+			if(loadQRay(Q, i, o, d, tmin, tw))   // (a NaN direction marks "no ray this iteration")
 			{
 				float t;
 				int prim;
@@ -1302,7 +1301,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_brute(DevScene S, DevQueu
 		{
 			V3 o = v3(0.f, 0.f, 0.f), d = v3(0.f, 0.f, 1.f);
 			float tmin = 0.f, tw = -1.f;
-			const bool ray = closest && loadQRay(S.ray_min_dist, Q, a0 + j, o, d, tmin, tw);   // NaN direction: no ray this iteration
+			const bool ray = closest && loadQRay(Q, a0 + j, o, d, tmin, tw);   // NaN direction: no ray this iteration
 			if(!ray) { o = v3(0.f, 0.f, 0.f); d = v3(0.f, 0.f, 1.f); }
 			float t;
 			int prim;
@@ -2493,7 +2492,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			{
 				V3 ro, rd;
 				float tmin_unused, tw;
-				loadQRay(S.ray_min_dist, A.Q, i, ro, rd, tmin_unused, tw);
+				loadQRay(A.Q, i, ro, rd, tmin_unused, tw);
 				if(EXT && S.cur_level > 0) add_depth_in = (int)(-tw) - 1;
 				have_hit = true;
 				sp = makeSurf(S, ro, rd, A.Q.hit_t[i], hit_prim);
@@ -2944,7 +2943,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_surface(DevScene S, DevQueues Q
 		const uint32_t i = a0 + j;
 		V3 o, d;
 		float tmin_unused, tw_unused;
-		if(!loadQRay(S.ray_min_dist, Q, i, o, d, tmin_unused, tw_unused)) continue;   // no ray this iteration (NaN marker)
+		if(!loadQRay(Q, i, o, d, tmin_unused, tw_unused)) continue;   // no ray this iteration (NaN marker)
 		const int prim = Q.hit_prim[i];
 		if(prim < 0) continue;
 		const V3 p = o + Q.hit_t[i] * d;   // accelerator.cc:61

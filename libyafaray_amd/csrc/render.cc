@@ -1798,7 +1798,9 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// the first iteration's closest rays (camera / spawned, queue 0) carry their own (tmin, tmax);
 			// k_shade's bounce rays all have (ray_min_dist, infinite)
 			DevQueues qc = d.Q[cur];
-			if(it != 0) qc.ray_tt = nullptr;
+			// (camera rays with the default clip planes all have (0, unbounded): k_camera writes no ray_tt)
+			if(it != 0 || (S.cur_level == 0 && !S.cam.ray_tt)) qc.ray_tt = nullptr;
+			qc.tmin_dflt = it == 0 ? 0.f : S.ray_min_dist;
 			PROF(KK_TRACE, yafamd_launch_trace(&S, &qc, &cnt[cur], &d.P[cur], run_stats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
 			// material-shade dispatch for textured / smooth scenes: surface attributes + shader nodes
 			// of every hit, before k_shade reads them
