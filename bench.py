@@ -139,10 +139,11 @@ def algo_bytes(kind, s, kt, in_lds, a):
     if kind == "k_shade":
         return 64.0 * it          # §8d: path-state read + write per path segment
     if kind == "k_nee":
-        # per request: the vertex in (p + prim, wo + index, the 8-B pixel / sample / mode word) 40 B;
+        # per request: the vertex in ((wo, prim) 16 B, the 8-B pixel / sample / mode word, the hit point
+        # as the next ray origin 12 B) 36 B;
         # out: one shadow ray per light sample (o + index, d + tmax: 32 B) + contribution (12-B record)
         # + occlusion byte
-        return 40.0 * it + 45.0 * (s["shadow_rays"] / max(1, s["closest_rays"])) * it
+        return 36.0 * it + 45.0 * (s["shadow_rays"] / max(1, s["closest_rays"])) * it
     if kind == "k_camera":
         # camera ray 32 B + the compact record (sample id, stage, MWC) 16 B: a camera entry's zero
         # throughput / colour / flags are implied by its stage (§8d counted 64 B of initial state)
