@@ -41,10 +41,6 @@ namespace yafamd
 // k_shade / k_nee (non-EXT instantiations): at least 4 waves per SIMD (<= 128 VGPRs; the unconstrained allocation took
 // 132 / 143 and 3 waves).  Measured on C2: 1400 -> 1500 Msamples/s (shade 0.70 -> 0.62 ms per
 // launch, NEE 17.7 -> 15.6 ms per frame), -DYAF_*_MIN_WAVES=n overrides for tuning
-// k_shade loads the entry's first two NEE slots with its record (-DYAF_SHADE_PREF_NEE=0: on use)
-#ifndef YAF_SHADE_PREF_NEE
-#define YAF_SHADE_PREF_NEE 1
-#endif
 #ifndef YAF_SHADE_MIN_WAVES
 #define YAF_SHADE_MIN_WAVES 4
 #endif
@@ -2390,34 +2386,9 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		float4 v0p4 = thr4, v0wo4 = thr4;
 		float4 v0a0 = thr4, v0a1 = thr4;   // first-hit surface attributes (ATTR && keep_v0)
 		SampleCoord sc{0, 0, 0};
-		const int kb = (int)i * K;
-		// the records nearly every entry needs, loaded together with pr (one memory round trip instead
-		// of the chain pr -> stage -> thr / pcol -> flags -> pending throughput / NEE slots -> hit -> ray);
-		// entries that do not need one (a camera entry's state, a finished subpath's hit) ignore it
-		float4 thr_l = make_float4(0.f, 0.f, 0.f, 0.f), pcol_l = thr_l;
-		F3 pthr_l{0.f, 0.f, 0.f}, nee_l0{0.f, 0.f, 0.f}, nee_l1{0.f, 0.f, 0.f};
-		uint8_t occ_l0 = 1, occ_l1 = 1;
-		int hp_l = -1;
-		float ht_l = 0.f, ttmin_l = 0.f, tw_l = -1.f;
-		V3 ro_l = v3(0.f, 0.f, 0.f), rd_l = ro_l;
 		if(live)
 		{
 			const uint4 pr = Pc.pr[i];
-			thr_l = Pc.thr[i];
-			pcol_l = Pc.pcol[i];
-			pthr_l = reinterpret_cast<const F3 *>(Pc.pend_thr)[i];
-#if YAF_SHADE_PREF_NEE
-			nee_l0 = reinterpret_cast<const F3 *>(Pc.nee)[kb];
-			occ_l0 = Pc.occ[kb];
-			if(K >= 2)
-			{
-				nee_l1 = reinterpret_cast<const F3 *>(Pc.nee)[kb + 1];
-				occ_l1 = Pc.occ[kb + 1];
-			}
-#endif
-			hp_l = A.Q.hit_prim[i];
-			ht_l = A.Q.hit_t[i];
-			loadQRay(A.Q, i, ro_l, rd_l, ttmin_l, tw_l);
 			rng = make_uint2(pr.z, pr.w);
 			if(compact)
 			{
@@ -2438,8 +2409,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			// write them) and has no first-hit data yet
 			if(!compact || (stage & 0xffu) != ST_CAMERA)
 			{
-				thr4 = thr_l;
-				pcol4 = pcol_l;
+				thr4 = Pc.thr[i];
+				pcol4 = Pc.pcol[i];
 				if(keep_v0) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
 				if(ATTR && keep_v0) { v0a0 = Pc.v0attr[2 * (size_t)i]; v0a1 = Pc.v0attr[2 * (size_t)i + 1]; }
 			}
@@ -2447,7 +2418,11 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			flags = __float_as_uint(pcol4.w);
 			// only the first segment of a subpath reads the previous wo (path_tracer.cc:193-197)
 			if((stage & 0xffu) == ST_FIRST) pwo4 = Pc.pwo[i];
-			if(flags & F_PEND_ONE) pthr4 = make_float4(pthr_l.x, pthr_l.y, pthr_l.z, 0.f);
+			if(flags & F_PEND_ONE)
+			{
+				const F3 t = reinterpret_cast<const F3 *>(Pc.pend_thr)[i];
+				pthr4 = make_float4(t.x, t.y, t.z, 0.f);
+			}
 			if(flags & (F_PEND_EMIT | F_AO_EMIT)) pem4 = Pc.pend_emit[i];
 		}
 		C3 thr = rgb(thr4), col = rgb(col4), pcol = rgb(pcol4);
@@ -2470,18 +2445,10 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 
 		PHASE(0);
 		// ---- 1. connect the pending next-event estimate ----
-		// (HBM slots: validity is in the occlusion byte; the entry's first two slots came with the record)
-		auto ge = [&](int k) {
-			if(!YAF_SHADE_PREF_NEE) return f4(neeGet(neeHbm(Pc), k), 1.f);
-			const int r = k - kb;
-			return r == 0 ? make_float4(nee_l0.x, nee_l0.y, nee_l0.z, 1.f)
-			              : (r == 1 && K >= 2) ? make_float4(nee_l1.x, nee_l1.y, nee_l1.z, 1.f) : f4(neeGet(neeHbm(Pc), k), 1.f);
-		};
-		auto go = [&](int k) {
-			if(!YAF_SHADE_PREF_NEE) return Pc.occ[k] != 0;
-			const int r = k - kb;
-			return (r == 0 ? occ_l0 : (r == 1 && K >= 2) ? occ_l1 : Pc.occ[k]) != 0;
-		};
+		const int kb = (int)i * K;
+		// (HBM slots: validity is in the occlusion byte)
+		auto ge = [&](int k) { return f4(neeGet(neeHbm(Pc), k), 1.f); };
+		auto go = [&](int k) { return Pc.occ[k] != 0; };
 		if(live && (flags & F_PEND_V0))
 		{
 			loadCol();
@@ -2520,13 +2487,15 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		int add_depth_in = 0;   // additional_depth of a spawned specular node (spawnSpecular)
 		if(live && st != ST_NORAY)
 		{
-			hit_prim = hp_l;
+			hit_prim = A.Q.hit_prim[i];
 			if(hit_prim >= 0)
 			{
-				const V3 ro = ro_l, rd = rd_l;
-				if(EXT && S.cur_level > 0) add_depth_in = (int)(-tw_l) - 1;
+				V3 ro, rd;
+				float tmin_unused, tw;
+				loadQRay(A.Q, i, ro, rd, tmin_unused, tw);
+				if(EXT && S.cur_level > 0) add_depth_in = (int)(-tw) - 1;
 				have_hit = true;
-				sp = makeSurf(S, ro, rd, ht_l, hit_prim);
+				sp = makeSurf(S, ro, rd, A.Q.hit_t[i], hit_prim);
 				if(ATTR)
 				{
 					sa0 = A.Q.sattr[2 * (size_t)i];

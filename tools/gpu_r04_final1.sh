@@ -7,3 +7,4 @@ rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.log 2>&1 || { tail -5 gpurun_out/bench_default.log; exit 1; }
 tail -1 gpurun_out/bench_default.log | cut -c1-400
 bash tools/pmc_all.sh cornell
+bash tools/prof_stats.sh c2 --steps 3
