@@ -145,9 +145,10 @@ def algo_bytes(kind, s, kt, in_lds, a):
         # + occlusion byte
         return 36.0 * it + 45.0 * (s["shadow_rays"] / max(1, s["closest_rays"])) * it
     if kind == "k_camera":
-        # camera ray 32 B + the compact record (sample id, stage, MWC) 16 B: a camera entry's zero
-        # throughput / colour / flags are implied by its stage (§8d counted 64 B of initial state)
-        return 48.0 * it
+        # camera ray (12-B origin + direction records) 24 B + the compact record (sample id, stage, MWC)
+        # 16 B: a camera entry's zero throughput / colour / flags are implied by its stage (§8d counted
+        # 64 B of initial state); the per-ray (tmin, tmax) 8 B only with clip planes (not counted)
+        return 40.0 * it
     if kind == "k_film":
         return 16.0 * it + 20.0 * a.width * a.height   # the samples (float4) + RGBA + weight per pixel
     if kind == "k_gather":
