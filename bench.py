@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size parity checks")
     ap.add_argument("--parity-rows", type=int, default=12, help="rows of the RR-off bit-exact band")
+    ap.add_argument("--flush-steps", type=int, default=2, help="frames timed through yafaray_render with the film flush (ms_per_step_flush)")
     ap.add_argument("--members-per-gpu", type=int, default=1,
                     help="device-group members per GPU (experiment: several logical members on one GPU run on concurrent streams)")
     return ap.parse_args()
@@ -120,16 +121,18 @@ def load_pmc(a, W, H):
 # ---------------------------------------------------------------------------------------------
 # kernel kinds that are one kernel (per-launch PMC instruction counts map onto their launches); the
 # others (pkd_build, photon_compact, aa_next_pass) are sequences of several kernels per launch record
-SINGLE_KERNEL_KINDS = {"k_trace", "k_shade", "k_nee", "k_camera", "k_film", "k_gather", "k_fg", "k_pregather", "k_surface",
+SINGLE_KERNEL_KINDS = {"k_trace", "k_shade", "k_nee", "k_camera", "k_film", "k_gather", "k_gather_walk", "k_fg", "k_pregather", "k_surface",
                        "k_tshadow", "k_photon_emit", "k_photon_bounce", "k_spawn", "k_combine"}
 # SURVEY §8d per-ray algorithmic bytes with the reference kd-tree's measured counts
 # (B_ray = N_node * 8 + N_tri * 40 + ray I/O): C2 closest 273 / shadow 235 B, C4 509 / 793 B
 SURVEY_B_RAY = {"cornell": (273.0, 235.0), "sphere": (509.0, 793.0)}
 
 
-def algo_bytes(kind, s, kt, in_lds, a):
-    """Total algorithmic HBM bytes of all launches of one kernel kind in one frame."""
+def algo_bytes(kind, s, kt, in_lds, a, kt_all=None):
+    """Total algorithmic HBM bytes of all launches of one kernel kind in one frame (kt_all: every kind's
+    record of the frame, for the models that depend on another kernel's work)."""
     it = kt["items"]
+    kt_all = kt_all or {}
     if kind == "k_trace":
         # ray I/O: closest 24 B in (12-B origin + direction records; the camera rays' 8-B (tmin, tmax)
         # ignored) + 8 B out (t, prim); shadow 32 B in (o + index, d + tmax) + 1 B out; traversal bytes
@@ -151,19 +154,43 @@ def algo_bytes(kind, s, kt, in_lds, a):
         return 40.0 * it
     if kind == "k_film":
         return 16.0 * it + 20.0 * a.width * a.height   # the samples (float4) + RGBA + weight per pixel
+    if kind == "k_gather_walk":
+        # pass 1 of the two-pass diffuse estimate: §8d's N_visit * 16 B (kd node; a leaf carries the photon
+        # position) + 8 B per photon it logs (index + distance) + the request's point (16 B) and its log
+        # count (4 B)
+        return 16.0 * s.get("gather_visits", 0) + 8.0 * s.get("gather_accepts", 0) + 20.0 * it
     if kind == "k_gather":
-        # §8d: N_visit * 16 B (kd node; a leaf carries the photon position) + 36 B per photon record the
-        # estimates read (position.w + direction + colour.b, counted in-kernel: under final gathering
-        # the diffuse estimate moves to k_fg, so the records are counted, not k per request), plus the
-        # request (64 B) and the sample it writes (16 B)
-        return 16.0 * s.get("gather_visits", 0) + 36.0 * s.get("gather_photons", 0) + 80.0 * it
+        # 36 B per photon record the estimates read (position.w + direction + colour.b, counted in-kernel:
+        # under final gathering the diffuse estimate moves to k_fg, so the records are counted, not k per
+        # request), plus the request (64 B) and the sample it writes (16 B).  Two-pass gather: the node
+        # visits belong to k_gather_walk; this replay reads the walk's log (8 B per logged photon) instead
+        walk = kt_all.get("k_gather_walk", {}).get("launches", 0) > 0
+        visits = 8.0 * s.get("gather_accepts", 0) if walk else 16.0 * s.get("gather_visits", 0)
+        return visits + 36.0 * s.get("gather_photons", 0) + 80.0 * it
+    if kind == "k_photon_emit":
+        # per photon path: its alive-list slot (4 B) + the path record (origin, direction, colour: 48 B)
+        return 52.0 * it
+    if kind == "photon_compact":
+        # both passes read every deposit slot's flag (1 B each); each stored photon's record is read and
+        # written in photon-id order (36 B each way); final gathering: the radiance points' flags likewise
+        # and 48 B each way per point
+        stored = s.get("photons", 0) + s.get("caustic_photons", 0)
+        rad = s.get("radiance_points", 0)
+        slots = s.get("photon_slots", 0)
+        return 2.0 * slots + 72.0 * stored + ((2.0 * slots + 96.0 * rad) if rad else 0.0)
     if kind == "k_fg":
         # per request: 64 B in (point, wo + sample id, colour, extra) + 16 B out; the gather paths'
         # traversals (LDS-resident scene) and the radiance-map lookups (16 K points, L2-resident) do
         # not reach HBM
         return 80.0 * it
     if kind == "k_photon_bounce":
-        return (32.0 + 36.0) * s["photons"] + 32.0 * it   # deposits + one ray per path per bounce
+        # per traced path record (items = paths traced over all bounces): its alive-list slot + origin,
+        # direction and colour read (52 B); the paths that continue write the same 52 B (every traced
+        # path after bounce 0 was written by the previous bounce, the emitted ones by k_photon_emit);
+        # each stored photon's deposit (position, direction, colour.b, flag: 37 B)
+        emitted = kt_all.get("k_photon_emit", {}).get("items", 0)
+        stored = s.get("photons", 0) + s.get("caustic_photons", 0)
+        return 52.0 * it + 52.0 * max(0, it - emitted) + 37.0 * stored
     if kind == "pkd_build":
         return pkd_build_bytes(it) * kt["launches"]
     return None
@@ -270,6 +297,19 @@ def main():
     msps = samples_total / elapsed / 1e6
     mrays = rays_total / elapsed / 1e6
 
+    # the reference's render() ends with the film's flush to the client (imagefilm.cc:570-670 via
+    # scene.cc:203-263); renderQuiet keeps the normalised film on the GPU.  yafaray_render with a flush
+    # callback (the film downloaded to the host, then the callback), timed beside the value's frames
+    flush_ms = None
+    if world <= 1 and a.flush_steps > 0:
+        yi.L.yafaray_amd_setProfileKernels(yi.h, 0)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(a.flush_steps):
+            yi.render(flush=lambda: None)
+        sync()
+        flush_ms = (time.perf_counter() - t0) / a.flush_steps * 1e3
+
     s, kt = dict(stats_acc[-1]), kt_acc[-1]
     s.update(trav)   # node visits / triangle tests of the stats frame
     pmc = load_pmc(a, W, H)
@@ -309,6 +349,8 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            # yafaray_render incl. the film's download to the host and the flush callback (not the value)
+            "ms_per_step_flush": round(flush_ms, 3) if flush_ms is not None else None,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -361,7 +403,7 @@ def kernel_table(a, s, kt, pmc):
     for kind, v in sorted(kt.items(), key=lambda kv: -kv[1]["ms"]):
         e = {"ms": round(v["ms"], 3), "share": round(v["ms"] / frame_ms, 4) if frame_ms else None, "launches": v["launches"],
              "items": v["items"]}
-        ab = algo_bytes(kind, s, v, in_lds, a)
+        ab = algo_bytes(kind, s, v, in_lds, a, kt)
         if ab is not None and v["ms"] > 0:
             e["algo_bytes_per_item"] = round(ab / max(1, v["items"]), 1)
             e["achieved_gbs"] = round(ab / (v["ms"] * 1e-3) / 1e9, 1)

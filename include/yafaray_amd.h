@@ -60,6 +60,8 @@ typedef struct
 	int32_t reserved0;
 	uint64_t gather_accepts;    /* two-pass gather: photons the k_gather_walk logged (1.2) */
 	uint64_t gather_overflows;  /* two-pass gather: requests whose log overflowed and were walked again (1.2) */
+	uint64_t photon_paths_traced; /* photon shooting: path records the bounce launches traced, summed over bounces and maps (1.5) */
+	uint64_t photon_slots;      /* photon shooting: deposit slots scanned by the compactions (paths x (bounces + 1)) (1.5) */
 } yafaray_amd_stats_t;
 
 /* Bytes of the LIBYAFARAY_AMD_1.0 struct (its fields end at photon_tree_seconds): yafaray_amd_getStats

@@ -43,7 +43,8 @@ class Stats(C.Structure):
                 ("fg_thin_seconds", C.c_double), ("fg_radiance_seconds", C.c_double), ("fg_thin_rounds", C.c_int64),
                 ("gather_queries", C.c_uint64), ("gather_photons", C.c_uint64),
                 ("photon_maps_mode", C.c_int32), ("reserved0", C.c_int32),
-                ("gather_accepts", C.c_uint64), ("gather_overflows", C.c_uint64)]
+                ("gather_accepts", C.c_uint64), ("gather_overflows", C.c_uint64),
+                ("photon_paths_traced", C.c_uint64), ("photon_slots", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -252,6 +252,156 @@ YD float x87mulDiv(const X87Const &c, float a, float b)
 	return x87mulDivExact(c.hi, c.lo, a, b);
 }
 
+// (float)(1.f - 2.f * ((long double)x * C)) for x >= 0 (TextureMapperNode::sphereMap's v coordinate,
+// shader_node_basic.cc:78: the acos times div_1_by_pi is rounded to 64 bits, doubled (exact), subtracted
+// from one and rounded to 64 bits, then to float).  Textured scenes only: always the exact path.
+YD_COLD float x87oneMinus2Mul(const X87Const &c, float x)
+{
+	if(x == 0.f) return 1.f;
+	const DD t = round64(exactMul(c, (double)x));
+	// 1 - 2 t as an exact double-double: two-sum of 1 and -2 t.hi, then the -2 t.lo tail
+	const double b = -2.0 * t.hi;
+	const double s = 1.0 + b;
+	const double bb = s - 1.0;
+	const double err = (1.0 - (s - bb)) + (b - bb);
+	DD v = fastTwoSum(s, err - 2.0 * t.lo);
+	if(v.hi == 0.0) return (float)v.lo;
+	const bool neg = v.hi < 0.0;
+	if(neg) v = DD{-v.hi, -v.lo};
+	const float r = round24(round64(v));
+	return neg ? -r : r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// libm's float atan2f / atanf / acosf as the reference's x86-64 build calls them (std::atan2 /
+// std::acos on floats, shader_node_basic.cc:67, 77-78 via math.h:252-258).  glibc 2.35 implements them
+// as the fdlibm float algorithms (sysdeps/ieee754/flt-32 e_atan2f.c, s_atanf.c, e_acosf.c — not
+// correctly rounded: 15 % of atan2f and 8 % of acosf results differ from the double-rounded value), so
+// the device restates those algorithms operation for operation; tests/test_devmath.py checks this host
+// build against the host's libm bit for bit on millions of inputs.
+// ---------------------------------------------------------------------------------------------
+YD uint32_t fbits(float f)
+{
+	uint32_t u;
+	__builtin_memcpy(&u, &f, 4);
+	return u;
+}
+YD float bitsf(uint32_t u)
+{
+	float f;
+	__builtin_memcpy(&f, &u, 4);
+	return f;
+}
+
+YD float libmAtanf(float x)
+{
+	// atan(0.5), atan(1), atan(1.5), atan(inf) split in (hi, lo); the odd / even polynomial of atan
+	constexpr float hi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+	constexpr float lo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+	constexpr float a0 = 3.3333334327e-01f, a1 = -2.0000000298e-01f, a2 = 1.4285714924e-01f, a3 = -1.1111110449e-01f,
+	                a4 = 9.0908870101e-02f, a5 = -7.6918758452e-02f, a6 = 6.6610731184e-02f, a7 = -5.8335702866e-02f,
+	                a8 = 4.9768779427e-02f, a9 = -3.6531571299e-02f, a10 = 1.6285819933e-02f;
+	const int32_t hx = (int32_t)fbits(x), ix = hx & 0x7fffffff;
+	int id;
+	if(ix >= 0x4c000000)   // |x| >= 2^25
+	{
+		if(ix > 0x7f800000) return x + x;
+		return hx > 0 ? hi[3] + lo[3] : -hi[3] - lo[3];
+	}
+	if(ix < 0x3ee00000)    // |x| < 0.4375
+	{
+		if(ix < 0x31000000) return x;
+		id = -1;
+	}
+	else
+	{
+		x = fabsf(x);
+		if(ix < 0x3f980000)
+		{
+			if(ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
+			else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
+		}
+		else if(ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
+		else { id = 3; x = -1.0f / x; }
+	}
+	const float z = x * x, w = z * z;
+	const float s1 = z * (a0 + w * (a2 + w * (a4 + w * (a6 + w * (a8 + w * a10)))));
+	const float s2 = w * (a1 + w * (a3 + w * (a5 + w * (a7 + w * a9))));
+	if(id < 0) return x - x * (s1 + s2);
+	const float r = hi[id] - ((x * (s1 + s2) - lo[id]) - x);
+	return hx < 0 ? -r : r;
+}
+
+YD float libmAtan2f(float y, float x)
+{
+	constexpr float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
+	                pi_lo = -8.7422776573e-08f;
+	const int32_t hx = (int32_t)fbits(x), ix = hx & 0x7fffffff, hy = (int32_t)fbits(y), iy = hy & 0x7fffffff;
+	if(ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+	if(hx == 0x3f800000) return libmAtanf(y);
+	const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+	if(iy == 0) return m <= 1 ? y : (m == 2 ? pi + tiny : -pi - tiny);
+	if(ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+	if(ix == 0x7f800000)
+	{
+		if(iy == 0x7f800000)
+			return m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny : m == 2 ? 3.0f * pi_o_4 + tiny : -3.0f * pi_o_4 - tiny;
+		return m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? pi + tiny : -pi - tiny;
+	}
+	if(iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+	const int k = (iy - ix) >> 23;
+	float z;
+	if(k > 60) z = pi_o_2 + 0.5f * pi_lo;
+	else if(hx < 0 && k < -60) z = 0.0f;
+	else z = libmAtanf(fabsf(y / x));
+	switch(m)
+	{
+		case 0: return z;
+		case 1: return bitsf(fbits(z) ^ 0x80000000u);
+		case 2: return pi - (z - pi_lo);
+		default: return (z - pi_lo) - pi;
+	}
+}
+
+YD float libmAcosf(float x)
+{
+	constexpr float pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
+	constexpr float pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f, pS3 = -4.0055535734e-02f,
+	                pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f, qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f,
+	                qS3 = -6.8828397989e-01f, qS4 = 7.7038154006e-02f;
+	const int32_t hx = (int32_t)fbits(x), ix = hx & 0x7fffffff;
+	if(ix == 0x3f800000) return hx > 0 ? 0.0f : pi + 2.0f * pio2_lo;
+	if(ix > 0x3f800000) return (x - x) / (x - x);
+	if(ix < 0x3f000000)   // |x| < 0.5
+	{
+		if(ix <= 0x23000000) return pio2_hi + pio2_lo;
+		const float z = x * x;
+		const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+		const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+		const float r = p / q;
+		return pio2_hi - (x - (pio2_lo - x * r));
+	}
+	if(hx < 0)            // x < -0.5
+	{
+		const float z = (1.0f + x) * 0.5f;
+		const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+		const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+		const float s = sqrtf(z);
+		const float r = p / q;
+		const float w = r * s - pio2_lo;
+		return pi - 2.0f * (s + w);
+	}
+	const float z = (1.0f - x) * 0.5f;   // x > 0.5
+	const float s = sqrtf(z);
+	const float df = bitsf(fbits(s) & 0xfffff000u);
+	const float c = (z - df * df) / (s + df);
+	const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+	const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+	const float r = p / q;
+	const float w = r * s + c;
+	return 2.0f * (df + w);
+}
+
 // x > C / x < -C with C long double (exact for float x, see DESIGN.md numerics note)
 YD bool gtC(float x, const X87Const &c) { return (double)x > c.hi || ((double)x == c.hi && c.lo < 0.0); }
 YD bool ltNegC(float x, const X87Const &c) { return (double)x < -c.hi || ((double)x == -c.hi && c.lo < 0.0); }

@@ -138,7 +138,10 @@ struct DevLight
 	uint32_t shoot;         // bit 0: diffuse photons, bit 1: caustic photons
 	// meshlight / objectlight (light_object_light.cc): triangles [mesh0, mesh0 + mesh_n) of
 	// DevScene::mesh_tris / mesh_cdf (the mesh's faces in creation order), double-sided emission
-	uint32_t mesh0, mesh_n, double_sided, pad0;
+	uint32_t mesh0, mesh_n, double_sided;
+	// photon_only (Light::photonOnly): the light shoots photons but the integrators do not see it
+	// (render_view.cc:83-91) — it sits after the DevScene::n_lights visible lights and has no NEE entries
+	uint32_t photon_only;
 };
 
 struct DevCamera
@@ -406,9 +409,16 @@ struct PhotonState
 	float4 *ray_d;       // direction
 	float4 *pcol;        // photon colour, .w = flags (bit 0 caustic, bit 1 direct)
 	uint32_t *alive[2];  // photon ids of the current / next bounce, segmented: segment s (= k_photon_bounce
-	                     // workgroup s) holds seg_cap entries at s * seg_cap; kDeadPhoton marks a hole
-	uint32_t *n_alive;   // [2 * n_segs] entries per segment (bounce 0: derived from the local id layout)
+	                     // workgroup s) holds seg_cap entries at s * seg_cap; kDeadPhoton marks a hole.  Bounce 0:
+	                     // local id i at position i (segment s = the contiguous ids [s seg_cap, (s + 1) seg_cap)),
+	                     // so a wave's lanes read consecutive path records
+	uint32_t *n_alive;   // [(bounces + 2) * n_segs] entries per segment and bounce (bounce 0: derived from the id
+	                     // layout); the host sums them for the paths traced (the bounce kernel's work items)
 	uint32_t seg_cap, n_segs;
+	// deposit slots, bounce-major: slot (i, b) = b * n_local + i, so a bounce's lanes (consecutive local ids)
+	// store consecutive records; the compaction (k_photon_count / k_photon_scatter) emits them in photon-id
+	// order, bounces in order — the reference's one-thread order
+	uint32_t n_local, n_slot_rows;   // local ids, bounces + 1
 	float4 *dep_a;       // deposit slots: (position, colour.r)
 	float4 *dep_b;       // (direction, colour.g)
 	float *dep_c;        // colour.b

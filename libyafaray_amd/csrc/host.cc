@@ -288,6 +288,8 @@ bool Scene::renderDeviceGroup(RenderParams &rp)
 		st.gather_photons += o.gather_photons;
 		st.gather_accepts += o.gather_accepts;
 		st.gather_overflows += o.gather_overflows;
+		st.photon_paths_traced += o.photon_paths_traced;
+		st.photon_slots += o.photon_slots;
 		st.trace_kernel_ms += o.trace_kernel_ms;
 		st.shade_kernel_ms += o.shade_kernel_ms;
 		st.nee_kernel_ms += o.nee_kernel_ms;
@@ -802,14 +804,23 @@ bool Scene::createLight(const std::string &name, const ParamMap &p)
 		L.samples = std::max(1, (int)std::ceil((float)samples * 1.f));
 		L.inv_samples = 1.f / (float)L.samples;
 		L.nee_count = 2 * (uint32_t)L.samples;   // light samples + material samples (canIntersect)
-		if(enabled && !photon_only) light_objects[name] = object_name;
+		if(enabled) light_objects[name] = object_name;
 	}
 	else
 	{
 		log.error("Scene: light type '" + type + "' is not supported by the GPU core");
 		return false;
 	}
-	if(!enabled || photon_only) { log.verbose("Light '" + name + "' disabled / photon-only: not used by the integrators"); return true; }
+	if(!enabled) { log.verbose("Light '" + name + "' disabled: not used"); return true; }
+	if(photon_only)
+	{
+		// render_view.cc:83-111: left out of the integrators' light list (getLightsVisible) but still in
+		// the lists of lights shooting diffuse / caustic photons; its illumSample refuses anyway
+		// (light_area.cc:68, light_point.cc:40, light_object_light.cc:110)
+		L.photon_only = 1;
+		L.nee_count = 0;
+		log.verbose("Light '" + name + "' is photon-only: it shoots photons, the integrators do not sample it");
+	}
 	lights[name] = L;
 	return true;
 }
@@ -1163,11 +1174,20 @@ bool Scene::buildAccelerator()
 			}
 		}
 	}
-	for(auto &kv : lights)
+	// the visible lights in name order (render_view.cc:83-91: the integrators' list), then the photon-only
+	// ones (only the photon maps' light sets refer to them)
 	{
-		DevLight L = kv.second;
-		if(L.type == LIGHT_MESH && !meshLightFaces(kv.first, L, hs)) return false;
-		hs.lights.push_back(L);
+		std::map<std::string, int> at;
+		for(int pass = 0; pass < 2; ++pass)
+			for(auto &kv : lights)
+			{
+				DevLight L = kv.second;
+				if((L.photon_only != 0) != (pass == 1)) continue;
+				if(L.type == LIGHT_MESH && !meshLightFaces(kv.first, L, hs)) return false;
+				at[kv.first] = (int)hs.lights.size();
+				hs.lights.push_back(L);
+			}
+		for(const auto &kv : at) hs.light_name_order.push_back(kv.second);
 	}
 	uint32_t base = 0;
 	for(DevLight &L : hs.lights) { L.nee_base = base; base += L.nee_count; }

@@ -45,10 +45,19 @@ namespace yafamd
 #define YAF_SHADE_MIN_WAVES 4
 #endif
 constexpr int kTraceBlock = YAF_TRACE_BLOCK;
-// -DYAF_FUSE: the non-EXT k_shade runs the NEE itself (no k_nee launch).  Measured on C2 (r02):
+// -DYAF_EXPERIMENTS: the pipelines measured and dropped stay buildable for re-measurement but out of
+// the product library (kExperiments; yafaray_amd_buildInfo records the flag): k_trace_brute, ray-stream
+// sorting in k_trace, the megakernel k_path, k_nee tracing its shadow rays in place, the bounded-radius
+// gather walk and the fused shade (-DYAF_FUSE on top).
+#ifdef YAF_EXPERIMENTS
+constexpr bool kExperiments = true;
+#else
+constexpr bool kExperiments = false;
+#endif
+// -DYAF_EXPERIMENTS -DYAF_FUSE: the non-EXT k_shade runs the NEE itself (no k_nee launch).  Measured on C2 (r02):
 // 1591 Msamples/s split vs 1455 fused at 3 waves/SIMD (1347 at 4 with 240 B/lane of scratch, 1154
 // at 2) — the HBM-bound shade loses more occupancy than the request round trip costs.
-#ifdef YAF_FUSE
+#if defined(YAF_FUSE) && defined(YAF_EXPERIMENTS)
 constexpr bool kShadeFused = true;
 #else
 constexpr bool kShadeFused = false;
@@ -237,10 +246,20 @@ __device__ __forceinline__ bool neePm8(const DevScene &S)
 	return !S.nee_pm16 && (uint32_t)S.spp < (1u << kPmSBits) && S.n_lights <= (1 << kPmLBits);
 }
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+#ifdef YAF_CHECKED
+// checked builds (-DYAF_CHECKED, as pkd's PK_GUARD): a request whose sample index lies outside the pass's
+// [base + pass_offset, + spp) window would alias another sample's NEE sequence in the 8-B word; the
+// first offending source line is recorded here (yafaray_amd_buildInfo reports the flag, tests read it)
+__device__ uint32_t g_nee_pm_err = 0;
+#define NEE_PM_GUARD(cond) do { if(!(cond)) atomicCAS(&g_nee_pm_err, 0u, (uint32_t)__LINE__); } while(0)
+#else
+#define NEE_PM_GUARD(cond) do {} while(0)
+#endif
 __device__ __forceinline__ void neePmStore(const DevScene &S, uint4 *pm, uint32_t j, uint32_t offset, uint32_t sample_idx, uint32_t mode_l)
 {
 	if(neePm8(S))
 	{
+		NEE_PM_GUARD(sample_idx - S.base_offset - S.pass_offset < (uint32_t)S.spp);
 		u32x2_t w;
 		w.x = offset;
 		w.y = (sample_idx - S.base_offset - S.pass_offset) | ((mode_l & 1u) << kPmSBits) | ((mode_l >> 8) << (kPmSBits + 1));
@@ -1244,6 +1263,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 // arithmetic (no divergence, no stack), and a shadow wave stops when all its lanes are occluded.
 // ---------------------------------------------------------------------------------------------
 constexpr int kBruteTris = 64;
+#ifdef YAF_EXPERIMENTS
 
 template<bool ANY>
 __device__ __forceinline__ bool bruteTrace(const float4 *__restrict__ tris, int n_tris, V3 o, V3 d, float tmin, float tmax, float &t_best,
@@ -1348,6 +1368,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_brute(DevScene S, DevQueu
 		if(v) rec[slot] += v;
 	}
 }
+#endif   // YAF_EXPERIMENTS (k_trace_brute)
 
 // ---------------------------------------------------------------------------------------------
 // k_shade
@@ -4118,10 +4139,12 @@ __global__ void __launch_bounds__(256) k_photon_emit(PhotonArgs A)
 		pcol = C3{L.color[0], L.color[1], L.color[2]} * (f_num_lights * light_pdf / light_num_pdf);
 		ok = !isBlack(pcol);
 	}
-	// the path's place in the alive list: segment i mod n_segs (the bounce workgroup that traces it),
-	// position i / n_segs — no counter (a global per-wave atomic here serialised 156 K appends on one
-	// address: 1.8 ms for 10 M photons); a photon that carries no energy leaves a hole
-	if(i < A.n_local) A.P.alive[0][(i % A.P.n_segs) * A.P.seg_cap + i / A.P.n_segs] = ok ? i : kDeadPhoton;
+	// the path's place in the alive list: position i, i.e. segment i / seg_cap (the bounce workgroup that
+	// traces it) — no counter (a global per-wave atomic here serialised 156 K appends on one address: 1.8 ms
+	// for 10 M photons), and a wave of the bounce kernel reads consecutive path records (r04 dealt ids
+	// round-robin over the segments: every lane's 16-B loads touched its own 128-B line, 7.9x the model's
+	// bytes); a photon that carries no energy leaves a hole
+	if(i < A.n_local) A.P.alive[0][i] = ok ? i : kDeadPhoton;
 	if(ok)
 	{
 		A.P.ray_o[i] = f4(o, S.ray_min_dist);
@@ -4193,11 +4216,12 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 	if(threadIdx.x == 0) s_next = 0;
 	__syncthreads();
 	const uint32_t seg = blockIdx.x, G = A.P.n_segs, cap = A.P.seg_cap;
-	const uint32_t n = A.bounce == 0 ? (A.n_local > seg ? (A.n_local - seg + G - 1u) / G : 0u) : A.P.n_alive[(uint32_t)A.cur * G + seg];
+	const uint32_t n = A.bounce == 0 ? (A.n_local > seg * cap ? min(cap, A.n_local - seg * cap) : 0u) : A.P.n_alive[(uint32_t)A.bounce * G + seg];
 	const uint32_t *alive_cur = A.P.alive[A.cur] + (size_t)seg * cap;
 	const int nxt = A.cur ^ 1;
 	uint32_t *alive_nxt = A.P.alive[nxt] + (size_t)seg * cap;
 	const uint32_t slots = (uint32_t)A.max_bounces + 1u;
+	const size_t row = (size_t)A.bounce * A.P.n_local;   // this bounce's deposit slots: row + local id
 	uint32_t visits = 0, tests = 0;
 	for(uint32_t base = 0; base < n; base += blockDim.x)
 	{
@@ -4236,7 +4260,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 				const bool store = A.L.caustic ? ((sp.flags & (B_DIFFUSE | B_GLOSSY)) && caustic) : ((sp.flags & B_DIFFUSE) && !caustic);
 				if(store)
 				{
-					const uint32_t slot = i * slots + (uint32_t)A.bounce;
+					const size_t slot = row + i;
 					A.P.dep_a[slot] = f4(sp.p, lcol.r);
 					A.P.dep_b[slot] = f4(wi, lcol.g);
 					A.P.dep_c[slot] = lcol.b;
@@ -4312,17 +4336,19 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 		}
 	}
 	__syncthreads();
-	if(threadIdx.x == 0) A.P.n_alive[(uint32_t)nxt * G + seg] = s_next;
+	if(threadIdx.x == 0) A.P.n_alive[(uint32_t)(A.bounce + 1) * G + seg] = s_next;
 }
 
-// Stable compaction of the deposit slots (photon-id order): per-1024-slot counts, an exclusive
-// scan of the counts in one workgroup, then each workgroup writes its photons in slot order.
-__global__ void __launch_bounds__(256) k_photon_count(const uint8_t *flag, uint32_t n_slots, uint32_t *counts)
+// Stable compaction of the bounce-major deposit slots into photon-id order (bounces in order per
+// photon): per block of 1024 local ids the stored deposits are counted, the counts scanned in one
+// workgroup, then each thread writes its photon's deposits at its place in the block.
+__global__ void __launch_bounds__(256) k_photon_count(const uint8_t *flag, uint32_t n_local, uint32_t rows, uint32_t *counts)
 {
 	const uint32_t b0 = blockIdx.x * 1024u;
 	uint32_t c = 0;
 	for(uint32_t k = threadIdx.x; k < 1024u; k += 256u)
-		if(b0 + k < n_slots) c += flag[b0 + k];
+		if(b0 + k < n_local)
+			for(uint32_t b = 0; b < rows; ++b) c += flag[(size_t)b * n_local + b0 + k];
 	for(int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
 	__shared__ uint32_t red[4];
 	if(laneId() == 0) red[threadIdx.x >> 6] = c;
@@ -4351,24 +4377,44 @@ __global__ void __launch_bounds__(1024) k_photon_scan(uint32_t *counts, uint32_t
 	for(uint32_t k = a; k < b; ++k) { const uint32_t v = counts[k]; counts[k] = run; run += v; }
 }
 
-__global__ void __launch_bounds__(1024) k_photon_scatter(PhotonState P, uint32_t n_slots, const uint32_t *offsets,
-                                                         float4 *pos, float4 *dir, float *colb)
+// The first output position of local id (blockIdx.x * 1024 + threadIdx.x)'s deposits: the block's
+// offset + the deposits of the block's earlier ids (flags of `rows` bounce rows; c = this id's count).
+__device__ __forceinline__ uint32_t depositBase(const uint8_t *flag, uint32_t n_local, uint32_t rows, const uint32_t *offsets, uint32_t &c)
 {
 	__shared__ uint32_t wsum[16];
-	const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
-	const bool f = k < n_slots && P.dep_flag[k];
-	const uint64_t m = __ballot(f);
+	const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
+	c = 0;
+	if(i < n_local)
+		for(uint32_t b = 0; b < rows; ++b) c += flag[(size_t)b * n_local + i];
+	// inclusive scan over the wave, then the earlier waves' totals
+	uint32_t s = c;
+	for(int off = 1; off < 64; off <<= 1)
+	{
+		const uint32_t v = __shfl_up(s, off);
+		if(laneId() >= off) s += v;
+	}
 	const int wid = threadIdx.x >> 6;
-	if(laneId() == 0) wsum[wid] = (uint32_t)__popcll(m);
+	if(laneId() == 63) wsum[wid] = s;
 	__syncthreads();
 	uint32_t base = offsets[blockIdx.x];
 	for(int w = 0; w < wid; ++w) base += wsum[w];
-	if(f)
+	return base + s - c;
+}
+
+__global__ void __launch_bounds__(1024) k_photon_scatter(PhotonState P, const uint32_t *offsets, float4 *pos, float4 *dir, float *colb)
+{
+	uint32_t c;
+	uint32_t o = depositBase(P.dep_flag, P.n_local, P.n_slot_rows, offsets, c);
+	const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
+	for(uint32_t b = 0; c > 0 && b < P.n_slot_rows; ++b)
 	{
-		const uint32_t o = base + (uint32_t)__popcll(m & ((1ull << laneId()) - 1ull));
+		const size_t k = (size_t)b * P.n_local + i;
+		if(!P.dep_flag[k]) continue;
 		pos[o] = P.dep_a[k];
 		dir[o] = P.dep_b[k];
 		colb[o] = P.dep_c[k];
+		++o;
+		--c;
 	}
 }
 
@@ -5029,24 +5075,20 @@ __global__ void __launch_bounds__(kGatherBlock) k_gather(GatherArgs A)
 // ---------------------------------------------------------------------------------------------
 // Stable compaction of the radiance points (deposit-slot order = one reference thread's order),
 // after k_photon_count / k_photon_scan over rad_flag
-__global__ void __launch_bounds__(1024) k_rad_scatter(PhotonState P, uint32_t n_slots, const uint32_t *offsets, float4 *out_a,
-                                                      float4 *out_b, float4 *out_c)
+__global__ void __launch_bounds__(1024) k_rad_scatter(PhotonState P, const uint32_t *offsets, float4 *out_a, float4 *out_b, float4 *out_c)
 {
-	__shared__ uint32_t wsum[16];
-	const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
-	const bool f = k < n_slots && P.rad_flag[k];
-	const uint64_t m = __ballot(f);
-	const int wid = threadIdx.x >> 6;
-	if(laneId() == 0) wsum[wid] = (uint32_t)__popcll(m);
-	__syncthreads();
-	uint32_t base = offsets[blockIdx.x];
-	for(int w = 0; w < wid; ++w) base += wsum[w];
-	if(f)
+	uint32_t c;
+	uint32_t o = depositBase(P.rad_flag, P.n_local, P.n_slot_rows, offsets, c);
+	const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
+	for(uint32_t b = 0; c > 0 && b < P.n_slot_rows; ++b)
 	{
-		const uint32_t o = base + (uint32_t)__popcll(m & ((1ull << laneId()) - 1ull));
+		const size_t k = (size_t)b * P.n_local + i;
+		if(!P.rad_flag[k]) continue;
 		out_a[o] = P.rad_a[k];
 		out_b[o] = P.rad_b[k];
 		out_c[o] = P.rad_c[k];
+		++o;
+		--c;
 	}
 }
 
@@ -5575,6 +5617,9 @@ int yafamd_trace_block() { return kTraceBlock; }
 // k_nee for those scenes); -DYAF_FUSE builds that variant (measured slower, see kShadeFused).
 int yafamd_shade_fused() { return kShadeFused ? 1 : 0; }
 
+// Whether the measured-and-dropped pipelines are compiled in (-DYAF_EXPERIMENTS)
+int yafamd_experiments() { return kExperiments ? 1 : 0; }
+
 // The flags this device object was compiled with (Makefile DEVINFO): yafaray_amd_buildInfo.
 #ifndef YAF_DEVICE_BUILD
 #define YAF_DEVICE_BUILD "arch=? extra=[?] (built outside csrc/Makefile)"
@@ -5619,7 +5664,11 @@ int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds)
 int yafamd_path_blocks_per_cu(const DevScene *S, int stack_depth)
 {
 	int nb = 0;
+#ifdef YAF_EXPERIMENTS
 	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path<false>, kTraceBlock, pathLdsBytes(*S, stack_depth)) != hipSuccess) nb = 0;
+#else
+	(void)S; (void)stack_depth;
+#endif
 	return nb;
 }
 
@@ -5654,11 +5703,13 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 	const size_t lds_scene = S->scene_in_lds ? (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4)
 	                                         : (wide ? (size_t)S->lds_top * 8 * sizeof(float4) : 0);
 	const size_t bytes = stack_bytes + lds_scene;
+#ifdef YAF_EXPERIMENTS
 	if(S->brute && !S->tr_shad && S->n_tris <= kBruteTris)
 	{
 		hipLaunchKernelGGL(k_trace_brute, dim3(grid), dim3(kTraceBlock), 0, st, *S, *Q, *cnt, *P, stats);
 		return hipGetLastError();
 	}
+#endif
 #define YAF_TRACE_LAUNCH(L, W, T, SP) hipLaunchKernelGGL((k_trace<L, W, T, SP>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats, stack_depth, spill)
 	// no spill column: the LDS levels hold the whole stack bound (LDS-resident scenes)
 	const bool nospill = spill == nullptr;
@@ -5675,6 +5726,7 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 	}
 	else if(S->scene_in_lds)
 	{
+#ifdef YAF_EXPERIMENTS
 		if(nospill && wide && S->ray_sort)
 		{
 			if(S->trace_stats)
@@ -5684,13 +5736,16 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 				hipLaunchKernelGGL((k_trace<true, true, false, false, false, true>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
 				                   stack_depth, spill);
 		}
-		else if(nospill && wide && !S->trace_stats)
+		else
+#endif
+		if(nospill && wide && !S->trace_stats)
 			hipLaunchKernelGGL((k_trace<true, true, false, false, false>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
 			                   stack_depth, spill);
 		else if(nospill) { if(wide) YAF_TRACE_LAUNCH(true, true, false, false); else YAF_TRACE_LAUNCH(true, false, false, false); }
 		else if(wide) YAF_TRACE_LAUNCH(true, true, false, true);
 		else YAF_TRACE_LAUNCH(true, false, false, true);
 	}
+#ifdef YAF_EXPERIMENTS
 	else if(wide && S->ray_sort)
 	{
 		if(S->trace_stats)
@@ -5700,6 +5755,7 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 			hipLaunchKernelGGL((k_trace<false, true, false, true, false, true>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
 			                   stack_depth, spill);
 	}
+#endif
 	else if(wide && !S->trace_stats)
 		hipLaunchKernelGGL((k_trace<false, true, false, true, false>), dim3(grid), dim3(kTraceBlock), bytes, st, *S, *Q, *cnt, *P, stats,
 		                   stack_depth, spill);
@@ -5771,7 +5827,7 @@ hipError_t yafamd_launch_tshadow(const DevScene *S, const DevQueues *Q, const De
 // hipErrorInvalidValue when the scene is not eligible (yafamd_path_eligible).
 int yafamd_path_eligible(const DevScene *S, int stack_depth, int spill)
 {
-	return (!S->ext && !S->tree && !S->tr_shad && !S->has_attr && !S->do_ao && !S->gather_on && !S->caus_map && S->integrator != INT_PHOTON &&
+	return (kExperiments && !S->ext && !S->tree && !S->tr_shad && !S->has_attr && !S->do_ao && !S->gather_on && !S->caus_map && S->integrator != INT_PHOTON &&
 	        S->scene_in_lds && S->node_f4 == 8 && !spill && S->small_tables && S->nee_k >= 1 && S->nee_k <= kPathMaxK && !S->brute &&
 	        pathLdsBytes(*S, stack_depth) <= 64 * 1024)
 	           ? 1
@@ -5792,17 +5848,22 @@ hipError_t yafamd_launch_path(const DevScene *S, float4 *samples, const DevJob *
 	A.n = n;
 	A.next = next;
 	A.stack_depth = stack_depth;
+#ifdef YAF_EXPERIMENTS
 	const size_t lds = pathLdsBytes(*S, stack_depth);
 	if(S->trace_stats) hipLaunchKernelGGL(k_path<true>, dim3(grid), dim3(kTraceBlock), lds, st, A);
 	else hipLaunchKernelGGL(k_path<false>, dim3(grid), dim3(kTraceBlock), lds, st, A);
 	return hipGetLastError();
+#else
+	(void)grid; (void)st;
+	return hipErrorInvalidValue;
+#endif
 }
 
 // k_nee traces its shadow rays in place (TR) for non-EXT LDS-resident BVH4 scenes whose stack bound
 // fits LDS, without transparent shadows (their filter colours need k_tshadow's lists)
 int yafamd_nee_trace_eligible(const DevScene *S, int stack_depth)
 {
-	return (!S->ext && !S->tr_shad && !S->has_attr && S->scene_in_lds && S->node_f4 == 8 && S->small_tables && S->nee_k >= 1 &&
+	return (kExperiments && !S->ext && !S->tr_shad && !S->has_attr && S->scene_in_lds && S->node_f4 == 8 && S->small_tables && S->nee_k >= 1 &&
 	        S->nee_k <= kPathMaxK && !S->brute && neeTraceLdsBytes(*S, stack_depth) <= 64 * 1024)
 	           ? 1
 	           : 0;
@@ -5819,12 +5880,14 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	A.cnt_next = *cnt_next;
 	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
 	A.stack_depth = stack_depth;
+#ifdef YAF_EXPERIMENTS
 	if(stack_depth > 0 && yafamd_nee_trace_eligible(S, stack_depth))
 	{
 		if(S->trace_stats) hipLaunchKernelGGL((k_nee<true, false, true, true>), dim3(S->n_seg), dim3(kShadeBlock), neeTraceLdsBytes(*S, stack_depth), st, A);
 		else hipLaunchKernelGGL((k_nee<true, false, true>), dim3(S->n_seg), dim3(kShadeBlock), neeTraceLdsBytes(*S, stack_depth), st, A);
 		return hipGetLastError();
 	}
+#endif
 	if(S->ext)
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_nee<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
@@ -5904,14 +5967,15 @@ hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const P
 }
 
 // Stable compaction of the deposit slots into the photon map; *total_dev receives the count.
-hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev,
-                                 float4 *pos, float4 *dir, float *colb, hipStream_t st)
+// (scratch_counts: one count per 1024 local ids)
+hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t *scratch_counts, uint32_t *total_dev, float4 *pos, float4 *dir, float *colb,
+                                 hipStream_t st)
 {
-	const uint32_t nb = (n_slots + 1023u) / 1024u;
+	const uint32_t nb = (P->n_local + 1023u) / 1024u;
 	if(nb == 0) return hipSuccess;
-	hipLaunchKernelGGL(k_photon_count, dim3(nb), dim3(256), 0, st, P->dep_flag, n_slots, scratch_counts);
+	hipLaunchKernelGGL(k_photon_count, dim3(nb), dim3(256), 0, st, P->dep_flag, P->n_local, P->n_slot_rows, scratch_counts);
 	hipLaunchKernelGGL(k_photon_scan, dim3(1), dim3(1024), 0, st, scratch_counts, nb, total_dev);
-	hipLaunchKernelGGL(k_photon_scatter, dim3(nb), dim3(1024), 0, st, *P, n_slots, (const uint32_t *)scratch_counts, pos, dir, colb);
+	hipLaunchKernelGGL(k_photon_scatter, dim3(nb), dim3(1024), 0, st, *P, (const uint32_t *)scratch_counts, pos, dir, colb);
 	return hipGetLastError();
 }
 
@@ -5972,23 +6036,27 @@ hipError_t yafamd_launch_gather_walk(const DevScene *S, const DevNeeQueue *G, co
 	A.log = GatherLog{(uint2 *)log->e, log->n, log->cap, log->seg_cap, log->j0};
 	const size_t lds = walkLdsBytes(S->pm_stack, !exact);
 	if(exact) hipLaunchKernelGGL(k_gather_walk<false>, dim3(S->n_seg * kWalkPerSeg), dim3(kGatherBlock), lds, st, A);
+#ifdef YAF_EXPERIMENTS
 	else hipLaunchKernelGGL(k_gather_walk<true>, dim3(S->n_seg * kWalkPerSeg), dim3(kGatherBlock), lds, st, A);
+#else
+	else return hipErrorInvalidValue;
+#endif
 	return hipGetLastError();
 }
 
-// the largest k the two-pass gather serves (the split replay heap's 16-bit log positions)
-int yafamd_gather_walk_k() { return 65535; }
+// the largest k the two-pass gather serves: the register walk's k; experiments builds also the bounded
+// walk (the split replay heap's 16-bit log positions bound it)
+int yafamd_gather_walk_k() { return kExperiments ? 65535 : kWalkK; }
 
 // Final gathering: compaction of the radiance points (reuses the photon count / scan kernels on
 // rad_flag); *total_dev receives the count
-hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b,
-                              float4 *c, hipStream_t st)
+hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b, float4 *c, hipStream_t st)
 {
-	const uint32_t nb = (n_slots + 1023u) / 1024u;
+	const uint32_t nb = (P->n_local + 1023u) / 1024u;
 	if(nb == 0) return hipSuccess;
-	hipLaunchKernelGGL(k_photon_count, dim3(nb), dim3(256), 0, st, P->rad_flag, n_slots, scratch_counts);
+	hipLaunchKernelGGL(k_photon_count, dim3(nb), dim3(256), 0, st, P->rad_flag, P->n_local, P->n_slot_rows, scratch_counts);
 	hipLaunchKernelGGL(k_photon_scan, dim3(1), dim3(1024), 0, st, scratch_counts, nb, total_dev);
-	hipLaunchKernelGGL(k_rad_scatter, dim3(nb), dim3(1024), 0, st, *P, n_slots, (const uint32_t *)scratch_counts, a, b, c);
+	hipLaunchKernelGGL(k_rad_scatter, dim3(nb), dim3(1024), 0, st, *P, (const uint32_t *)scratch_counts, a, b, c);
 	return hipGetLastError();
 }
 

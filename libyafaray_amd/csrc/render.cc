@@ -32,6 +32,7 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
                                DevStats *stats, int stack_depth, int *spill, int grid, hipStream_t st);
 int yafamd_trace_block();
 int yafamd_shade_fused();
+int yafamd_experiments();
 int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds);
 int yafamd_shade_blocks_per_cu();
 hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevPaths *Pn, const DevQueues *Q,
@@ -49,16 +50,15 @@ hipError_t yafamd_photon_emit(const DevScene *S, const PhotonState *P, const Pho
                               int max_bounces, hipStream_t st);
 hipError_t yafamd_photon_bounce(const DevScene *S, const PhotonState *P, const PhotonSet *L, uint32_t n_photons, uint32_t h0,
                                 uint32_t n_local, int max_bounces, int bounce, int cur, int stack_depth, int *spill, int grid, hipStream_t st);
-hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev,
-                                 float4 *pos, float4 *dir, float *colb, hipStream_t st);
+hipError_t yafamd_photon_compact(const PhotonState *P, uint32_t *scratch_counts, uint32_t *total_dev, float4 *pos, float4 *dir, float *colb,
+                                 hipStream_t st);
 hipError_t yafamd_launch_gather(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, float4 *samples,
                                 const DevJob *jobs, int n_jobs, uint64_t chunk_base, const GatherLogDesc *log, hipStream_t st);
 hipError_t yafamd_launch_gather_walk(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, const GatherLogDesc *log,
                                      hipStream_t st);
 int yafamd_gather_walk_k();
 size_t yafamd_gather_lds_bytes(const DevScene *S);
-hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t n_slots, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b,
-                              float4 *c, hipStream_t st);
+hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b, float4 *c, hipStream_t st);
 hipError_t yafamd_rad_refl(const DevScene *S, float4 *a, float4 *b, float4 *c, const uint32_t *kept, uint32_t n, hipStream_t st);
 hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
                             float4 *out_pos, float4 *out_dir, float *out_colb, hipStream_t st);
@@ -558,7 +558,10 @@ bool GpuRenderer::upload(HostScene &hs)
 	d.n_nodes = hs.bvh.n_nodes;
 	d.n_tris = hs.n_prims;
 	d.n_mats = (int)hs.mats.size();
-	d.n_lights = (int)hs.lights.size();
+	// the visible lights come first (Scene::buildAccelerator); photon-only ones follow and only the photon
+	// sets below refer to them
+	d.n_lights = 0;
+	for(const DevLight &L : hs.lights) d.n_lights += L.photon_only ? 0 : 1;
 	{
 		// sample_pdf1d.h:52-66 over the lights shooting diffuse (bit 0) / caustic (bit 1) photons
 		// (render_view.cc:103-110), energies = totalEnergy().energy() (light_area.cc:64,
@@ -567,7 +570,7 @@ bool GpuRenderer::upload(HostScene &hs)
 		{
 			std::vector<int> idx;
 			std::vector<float> func;
-			for(int i = 0; i < d.n_lights; ++i)
+			for(int i : hs.light_name_order)
 			{
 				const DevLight &L = hs.lights[i];
 				if(!(L.shoot & (1u << set))) continue;
@@ -619,6 +622,16 @@ bool GpuRenderer::upload(HostScene &hs)
 		int top = 21;
 		if(const char *e = getenv("YAFARAY_AMD_LDS_TOP"); e && *e) top = std::max(0, atoi(e));
 		d.lds_top = std::min(top, d.n_nodes);
+		// the treelet and the stack share the workgroup's LDS: clamp the treelet so that k_trace still
+		// launches — 64 KB per workgroup, the launch limit
+		const size_t stack_b = (size_t)d.lds_stack * yafamd_trace_block() * 4, lds_max = 64 * 1024;
+		const int fit = stack_b >= lds_max ? 0 : (int)((lds_max - stack_b) / 128);
+		if(d.lds_top > fit)
+		{
+			log_.warning("GPU: YAFARAY_AMD_LDS_TOP=" + std::to_string(d.lds_top) + " does not fit the trace workgroup's LDS; using " +
+			             std::to_string(fit) + " nodes");
+			d.lds_top = fit;
+		}
 	}
 	{
 		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy or top treelet))
@@ -700,16 +713,18 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	// Measured slower than the BVH on C2 (k_trace 39.0 vs 34.7 ms per frame: 34 exact triangle
 	// tests per ray at full lane occupancy cost more than ~3.4 node + 3.3 triangle visits at 0.35),
 	// so the BVH stays the default
+	// (the measured-and-dropped pipelines — k_trace_brute, ray sorting, the megakernel, in-place NEE
+	// shadow rays, the bounded gather walk, the fused shade — exist only in a -DYAF_EXPERIMENTS build)
 	{
 		const char *e = getenv("YAFARAY_AMD_TRACE");
-		S.brute = (e && std::string(e) == "brute") ? 1 : 0;
+		S.brute = (yafamd_experiments() && e && std::string(e) == "brute") ? 1 : 0;
 	}
 	// ray-stream sorting in k_trace (opt-in, YAFARAY_AMD_RAY_SORT=1): measured on C2 it lifts the
 	// VALU lane utilisation 0.44 -> 0.50 but costs more than it saves (k_trace 27.6 -> 28.9 ms per
 	// frame: the key pass reads every direction twice and the sort's registers spill), DESIGN.md §5
 	{
 		const char *e = getenv("YAFARAY_AMD_RAY_SORT");
-		S.ray_sort = (e && *e == '1') ? 1 : 0;
+		S.ray_sort = (yafamd_experiments() && e && *e == '1') ? 1 : 0;
 	}
 	S.ph_lights = (const int *)d.ph_lights.p;
 	S.light_cdf = (const float *)d.light_cdf.p;
@@ -752,9 +767,9 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	const uint32_t ph_segs = (uint32_t)std::max(1, d.trace_grid), ph_cap = (NL + ph_segs - 1) / ph_segs;
 	if(!ensure(log_, d.ph_ray_o, (size_t)NL * 16) || !ensure(log_, d.ph_ray_d, (size_t)NL * 16) || !ensure(log_, d.ph_pcol, (size_t)NL * 16) ||
 	   !ensure(log_, d.ph_alive0, (size_t)ph_segs * ph_cap * 4 + 4) || !ensure(log_, d.ph_alive1, (size_t)ph_segs * ph_cap * 4 + 4) ||
-	   !ensure(log_, d.ph_n_alive, (size_t)2 * ph_segs * 4) ||
+	   !ensure(log_, d.ph_n_alive, (size_t)(slots + 1) * ph_segs * 4) ||
 	   !ensure(log_, d.dep_a, n_slots * 16) || !ensure(log_, d.dep_b, n_slots * 16) || !ensure(log_, d.dep_c, n_slots * 4) ||
-	   !ensure(log_, d.dep_flag, n_slots) || !ensure(log_, d.ph_scan, ((n_slots + 1023) / 1024) * 4 + 16) || !ensure(log_, d.ph_total, 16))
+	   !ensure(log_, d.dep_flag, n_slots) || !ensure(log_, d.ph_scan, (((size_t)NL + 1023) / 1024) * 4 + 16) || !ensure(log_, d.ph_total, 16))
 		return false;
 	PhotonState P{};
 	P.ray_o = (float4 *)d.ph_ray_o.p;
@@ -765,6 +780,8 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	P.n_alive = (uint32_t *)d.ph_n_alive.p;
 	P.seg_cap = ph_cap;
 	P.n_segs = ph_segs;
+	P.n_local = NL;
+	P.n_slot_rows = slots;
 	P.dep_a = (float4 *)d.dep_a.p;
 	P.dep_b = (float4 *)d.dep_b.p;
 	P.dep_c = (float *)d.dep_c.p;
@@ -799,17 +816,26 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	Buf &cpos = group_render ? d.seg_pos : pos, &cdir = group_render ? d.seg_dir : dir, &ccolb = group_render ? d.seg_colb : colb;
 	uint32_t n = 0;
 	if(!ensure(log_, cpos, n_slots * 16) || !ensure(log_, cdir, n_slots * 16) || !ensure(log_, ccolb, n_slots * 4)) return false;
-	PROF(KK_PHOTON_COMPACT, yafamd_photon_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)cpos.p,
-	                               (float4 *)cdir.p, (float *)ccolb.p, d.stream));
+	PROF(KK_PHOTON_COMPACT, yafamd_photon_compact(&P, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)cpos.p, (float4 *)cdir.p,
+	                                              (float *)ccolb.p, d.stream));
 	HIPCHECK(hipMemcpyAsync(&n, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
-	HIPCHECK(hipStreamSynchronize(d.stream));
+	{
+		// the bounce launches' work: every slot of bounce 0's list, then the paths each bounce kept
+		std::vector<uint32_t> alive((size_t)(slots + 1) * ph_segs);
+		HIPCHECK(hipMemcpyAsync(alive.data(), d.ph_n_alive.p, alive.size() * 4, hipMemcpyDeviceToHost, d.stream));
+		HIPCHECK(hipStreamSynchronize(d.stream));
+		uint64_t traced = NL;
+		for(size_t k = ph_segs; k < (size_t)slots * ph_segs; ++k) traced += alive[k];
+		stats_.photon_paths_traced += traced;
+		stats_.photon_slots += n_slots;
+	}
 	uint32_t nr = 0;
 	if(want_rad)
 	{
 		Buf &ra = group_render ? d.seg_ra : d.radc_a, &rb = group_render ? d.seg_rb : d.radc_b, &rc = group_render ? d.seg_rc : d.radc_c;
 		if(!ensure(log_, ra, n_slots * 16) || !ensure(log_, rb, n_slots * 16) || !ensure(log_, rc, n_slots * 16)) return false;
-		PROF(KK_PHOTON_COMPACT, yafamd_rad_compact(&P, (uint32_t)n_slots, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)ra.p,
-		                                          (float4 *)rb.p, (float4 *)rc.p, d.stream));
+		PROF(KK_PHOTON_COMPACT, yafamd_rad_compact(&P, (uint32_t *)d.ph_scan.p, (uint32_t *)d.ph_total.p, (float4 *)ra.p, (float4 *)rb.p,
+		                                           (float4 *)rc.p, d.stream));
 		HIPCHECK(hipMemcpyAsync(&nr, d.ph_total.p, 4, hipMemcpyDeviceToHost, d.stream));
 		HIPCHECK(hipStreamSynchronize(d.stream));
 	}
@@ -1440,6 +1466,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	DevScene &S = rp.scene;
 	fillScenePointers(d, S);
 	stats_.photons = 0;
+	stats_.photon_paths_traced = stats_.photon_slots = 0;
 	stats_.caustic_photons = 0;
 	stats_.radiance_points = stats_.radiance_photons = 0;
 	stats_.fg_thin_seconds = stats_.fg_radiance_seconds = 0.0;
@@ -1569,6 +1596,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		uint32_t base = 0, max_one = 1;
 		for(DevLight &L : ls)
 		{
+			if(L.photon_only) continue;   // no NEE entries (after the visible lights)
 			if(L.type == LIGHT_AREA || L.type == LIGHT_MESH)
 			{
 				L.samples = (int)ceilf((float)L.samples * mult);
@@ -1711,10 +1739,11 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			const char *he = std::getenv("YAFARAY_AMD_GATHER_HEAP");
 			const uint32_t split = (he && std::string(he) == "packed") ? 0u : 1u;
 			const char *we = std::getenv("YAFARAY_AMD_GATHER_WALK");
-			// the walk with the k smallest distances in registers (k <= 64) by default: the bounded walk
-			// (YAFARAY_AMD_GATHER_WALK=bound, and any k > 64) measured slower on C5 (walk 13.9 -> 16.3 ms,
-			// replay 7.4 -> 12.1 ms per frame: its superset log)
-			const uint32_t exact = (we && std::string(we) == "bound") ? 0u : 1u;
+			// the walk with the k smallest distances in registers (k <= 64): the bounded walk
+			// (YAFARAY_AMD_GATHER_WALK=bound, experiments builds; there also any k > 64) measured slower on C5
+			// (walk 13.9 -> 16.3 ms, replay 7.4 -> 12.1 ms per frame: its superset log); without it a larger
+			// k takes the one-pass gather (yafamd_gather_walk_k)
+			const uint32_t exact = (yafamd_experiments() && we && std::string(we) == "bound") ? 0u : 1u;
 			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u, split, exact};
 			walk_gather = true;
 		}
@@ -1741,7 +1770,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	int nee_trace_stack = 0;
 	{
 		const char *ne = std::getenv("YAFARAY_AMD_NEE_TRACE");
-		if(ne && std::string(ne) == "1" && d.lds_stack >= d.stack_depth) nee_trace_stack = d.lds_stack;
+		if(yafamd_experiments() && ne && std::string(ne) == "1" && d.lds_stack >= d.stack_depth) nee_trace_stack = d.lds_stack;
 	}
 	// The megakernel (k_path, kernels.hip; opt-in YAFARAY_AMD_PATH=mega) for scenes whose BVH, stack
 	// and tables live in LDS and need none of the wavefront-only stages (EXT shading, transparent
@@ -1763,7 +1792,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	if(!lpc_on)
 	{
 		const char *pe = std::getenv("YAFARAY_AMD_PATH");
-		const bool on = pe && std::string(pe) == "mega";
+		const bool on = yafamd_experiments() && pe && std::string(pe) == "mega";
 		if(on && yafamd_path_eligible(&S, d.lds_stack, d.lds_stack < d.stack_depth ? 1 : 0))
 		{
 			path_grid = std::min(d.trace_grid, d.n_cu * std::max(1, yafamd_path_blocks_per_cu(&S, d.lds_stack)));
@@ -1912,7 +1941,45 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	auto runPass = [&](uint64_t n_total, int pass_spp) -> bool {
 		if(!lpc_on) return runSamples(n_total);
 		const size_t n_ctr = (size_t)W * H * (size_t)pass_spp;
-		if(!ensure(log_, d.lpc, n_ctr * 4) || !ensure(log_, d.lpc_stats, sizeof(DevStats) * (size_t)d.trace_grid)) return false;
+		// one 4-B counter per camera sample of the pass (8.5 GB at 1080p x 1024 spp): above a budget of a
+		// quarter of the device's free memory, or when the allocation fails, the pass falls back to the
+		// hashed pick (matched statistically) instead of failing the render
+		{
+			size_t free_b = 0, total_b = 0;
+			const bool have = hipMemGetInfo(&free_b, &total_b) == hipSuccess;
+			bool fits = d.lpc.bytes >= n_ctr * 4 || (have && n_ctr * 4 <= (free_b + d.lpc.bytes) / 4);
+			if(const char *e = std::getenv("YAFARAY_AMD_LPC_MAX_MB"); e && *e) fits = fits && (n_ctr * 4 >> 20) < (size_t)std::max(0, atoi(e));
+			auto tryEnsure = [](Buf &b, size_t bytes) {
+				if(b.p && b.bytes >= bytes) return true;
+				b.release();
+				if(hipMalloc(&b.p, std::max<size_t>(bytes, 16)) != hipSuccess)
+				{
+					b.p = nullptr;
+					(void)hipGetLastError();
+					return false;
+				}
+				b.bytes = std::max<size_t>(bytes, 16);
+				return true;
+			};
+			bool can = fits && tryEnsure(d.lpc, n_ctr * 4) && tryEnsure(d.lpc_stats, sizeof(DevStats) * (size_t)d.trace_grid);
+			if(group_render)
+			{
+				// every member takes the same pick (the count run's bases are exchanged): fall back together
+				const int st = groupStatus(can ? 0 : 1);
+				if(st >= 2)
+				{
+					log_.error("GPU group: a member failed; render abandoned");
+					return false;
+				}
+				can = st == 0;
+			}
+			if(!can)
+			{
+				log_.warning("Integrator: the one-thread light-pick counters (" + std::to_string(n_ctr * 4 >> 20) +
+				             " MB) exceed the memory budget; this pass picks lights by sample hash");
+				return runSamples(n_total);
+			}
+		}
 		HIPCHECK(hipMemsetAsync(d.lpc.p, 0, n_ctr * 4, d.stream));
 		HIPCHECK(hipMemsetAsync(d.lpc_stats.p, 0, sizeof(DevStats) * (size_t)d.trace_grid, d.stream));
 		S.lpc = (uint32_t *)d.lpc.p;
@@ -2191,7 +2258,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 		ktimes_.items[KK_GATHER_WALK] = ktimes_.launches[KK_GATHER_WALK] ? hs.gather_queries : 0;
 		ktimes_.items[KK_FG] = S.fg_on ? hs.gather_queries : 0;   // every diffuse-map request runs its final gathering first
 		ktimes_.items[KK_PREGATHER] = (uint64_t)d.n_rphotons;
-		ktimes_.items[KK_PHOTON_EMIT] = ktimes_.items[KK_PHOTON_BOUNCE] = (uint64_t)d.pm_local;
+		ktimes_.items[KK_PHOTON_EMIT] = (uint64_t)d.pm_local;
+		ktimes_.items[KK_PHOTON_BOUNCE] = stats_.photon_paths_traced;
 		ktimes_.items[KK_PHOTON_COMPACT] = ktimes_.items[KK_PHOTON_TREE] = stats_.photons;
 		stats_.trace_kernel_ms = ktimes_.ms[KK_TRACE];
 		stats_.shade_kernel_ms = ktimes_.ms[KK_SHADE];

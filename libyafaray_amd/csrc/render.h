@@ -31,7 +31,8 @@ struct HostScene
 	int ploc_iters = 0;                  // PLOC iterations of the GPU build
 	std::vector<float> prim_ng;          // 4 floats per primitive
 	std::vector<DevMaterial> mats;
-	std::vector<DevLight> lights;        // render order (by name)
+	std::vector<DevLight> lights;        // the visible lights by name (the integrators' order), then the photon-only ones
+	std::vector<int> light_name_order;   // every light by name (the photon maps' light lists, render_view.cc:93-111)
 	std::vector<float> mesh_tris;        // meshlight faces: kMeshTriF4 float4 each (DevScene::mesh_tris)
 	std::vector<float> mesh_cdf;         // their area distributions' normalised cdf, per light
 	int n_prims = 0;

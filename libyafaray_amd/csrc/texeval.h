@@ -364,7 +364,7 @@ YD V3 mapTube(V3 p)
 	if(d > 0.f)
 	{
 		res.z = 1.f / sqrtf(d);
-		res.x = x87mul(kDiv1ByPi, -atan2f(p.x, p.y));
+		res.x = x87mul(kDiv1ByPi, -libmAtan2f(p.x, p.y));
 	}
 	else res.x = res.z = 0.f;
 	return res;
@@ -376,13 +376,12 @@ YD V3 mapSphere(V3 p)
 	if(d > 0.f)
 	{
 		res.z = sqrtf(d);
-		if((p.x != 0.f) && (p.y != 0.f)) res.x = x87mul(kDiv1ByPi, -atan2f(p.x, p.y));
-		// math.h:252-258 acos with the domain clamp; the long double expression is evaluated in
-		// double (atan2f / acosf differ between libm and the device by an ulp anyway: the tube and
-		// sphere projections are compared with a tolerance, not bit for bit)
+		if((p.x != 0.f) && (p.y != 0.f)) res.x = x87mul(kDiv1ByPi, -libmAtan2f(p.x, p.y));
+		// math.h:252-258 acos with the domain clamp (libm's acosf, restated in devmath.h), then
+		// 1.f - 2.f * (acos * div_1_by_pi) with the long double product and difference (x87oneMinus2Mul)
 		const float q = p.z / res.z;
-		const float ac = (q <= -1.f) ? kPiF : (q >= 1.f) ? 0.f : acosf(q);
-		res.y = (float)(1.0 - 2.0 * ((double)ac * kDiv1ByPi.hi));
+		const float ac = (q <= -1.f) ? kPiF : (q >= 1.f) ? 0.f : libmAcosf(q);
+		res.y = x87oneMinus2Mul(kDiv1ByPi, ac);
 	}
 	return res;
 }

@@ -88,6 +88,7 @@ class Light:
     with_diffuse: bool = True              # shoots diffuse photons
     object_name: str = ""                  # meshlight / objectlight: the emitting object
     double_sided: bool = False             # meshlight
+    photon_only: bool = False              # shoots photons only (Light::photonOnly, render_view.cc:83-111)
 
 
 @dataclass
@@ -538,6 +539,8 @@ def apply(spec: SceneSpec, api) -> None:
             api.paramsSetBool("with_caustic", False)
         if not l.with_diffuse:
             api.paramsSetBool("with_diffuse", False)
+        if l.photon_only:
+            api.paramsSetBool("photon_only", True)
         if l.type == "pointlight":
             api.paramsSetVector("from", *l.from_)
         elif l.type in ("meshlight", "objectlight"):

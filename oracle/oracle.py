@@ -64,7 +64,7 @@ class yc_light(C.Structure):
     _fields_ = [("type", C.c_int), ("color", C.c_float * 3), ("power", C.c_float), ("from_", C.c_float * 3),
                 ("point1", C.c_float * 3), ("point2", C.c_float * 3), ("samples", C.c_int),
                 ("cast_shadows", C.c_int), ("shoot_caustic", C.c_int), ("shoot_diffuse", C.c_int),
-                ("object", C.c_int), ("double_sided", C.c_int)]
+                ("object", C.c_int), ("double_sided", C.c_int), ("photon_only", C.c_int)]
 
 
 class yc_camera(C.Structure):
@@ -560,6 +560,7 @@ class OracleScene:
             lights[i].shoot_caustic = int(getattr(l, "with_caustic", True))
             lights[i].shoot_diffuse = int(getattr(l, "with_diffuse", True))
             lights[i].cast_shadows = int(l.cast_shadows)
+            lights[i].photon_only = int(getattr(l, "photon_only", False))
         self.mats, self.lights = mats, lights
         sc = yc_scene()
         sc.n_verts = len(self.verts) // 3

@@ -488,6 +488,7 @@ struct Light
 	float area = 0.f, inv_area = 0.f;
 	int samples = 1;
 	bool shoot_caustic = true, shoot_diffuse = true;   // "with_caustic" / "with_diffuse"
+	bool photon_only = false;   // "photon_only": in the photon lists only (render_view.cc:83-111)
 	// meshlight (light_object_light.cc:46-73): the object's faces, their area cdf (sample_pdf1d.h)
 	std::vector<V3> mv0, mv1, mv2, mng;
 	std::vector<float> mcdf;
@@ -691,6 +692,7 @@ class Scene
 		std::vector<Tri> tris;
 		std::vector<Material> mats;
 		std::vector<Light> lights;
+		std::vector<const Light *> visible;   // RenderView::getLightsVisible (render_view.cc:83-91): the integrators' lights
 		Camera cam;
 		yc_render rp;
 		std::unique_ptr<FilmTable> film;
@@ -813,6 +815,7 @@ Scene::Scene(const yc_scene &s)
 		L.cast_shadows = l.cast_shadows != 0;
 		L.shoot_caustic = l.shoot_caustic != 0;
 		L.shoot_diffuse = l.shoot_diffuse != 0;
+		L.photon_only = l.photon_only != 0;
 		const C3 col(l.color[0], l.color[1], l.color[2]);
 		if(l.type == YC_LIGHT_POINT)
 		{
@@ -891,6 +894,8 @@ Scene::Scene(const yc_scene &s)
 		L.area = static_cast<float>(total);
 		L.inv_area = static_cast<float>(1.f / total);
 	}
+	for(const Light &L : lights)
+		if(!L.photon_only) visible.push_back(&L);
 	// camera: camera.cc:51-71, camera_perspective.cc:28-69 (no depth of field)
 	const yc_camera &c = s.cam;
 	const V3 pos(c.from[0], c.from[1], c.from[2]), look(c.to[0], c.to[1], c.to[2]), up(c.up[0], c.up[1], c.up[2]);
@@ -2026,9 +2031,9 @@ class Renderer
 		{
 			C3 col(0.f);
 			unsigned loffs = 0;
-			for(const Light &L : sc_.lights)
+			for(const Light *L : sc_.visible)
 			{
-				col += doLightEstimation(th, L, sp, wo, loffs, sample_idx, offset);
+				col += doLightEstimation(th, *L, sp, wo, loffs, sample_idx, offset);
 				++loffs;
 			}
 			return col;
@@ -2037,12 +2042,12 @@ class Renderer
 		// integrator_montecarlo.cc:70-78 (the light pick uses a per-thread running counter)
 		C3 estimateOneDirectLight(Thread &th, const SurfacePoint &sp, const V3 &wo, uint32_t sample_idx, uint32_t offset) const
 		{
-			const int num_lights = (int)sc_.lights.size();
+			const int num_lights = (int)sc_.visible.size();
 			if(num_lights == 0) return C3(0.f);
 			Halton hal_2(2, sc_.rp.base_sampling_offset + th.correlative - 1);
 			const int lnum = std::min(static_cast<int>(hal_2.getNext() * static_cast<float>(num_lights)), num_lights - 1);
 			++th.correlative;
-			return doLightEstimation(th, sc_.lights[lnum], sp, wo, lnum, sample_idx, offset) * static_cast<float>(num_lights);
+			return doLightEstimation(th, *sc_.visible[lnum], sp, wo, lnum, sample_idx, offset) * static_cast<float>(num_lights);
 		}
 
 		// integrator_tiled.cc:707-720

@@ -105,6 +105,7 @@ typedef struct {
 	int shoot_diffuse;        // "with_diffuse" (getLightsEmittingDiffusePhotons)
 	int object;               // meshlight: index into yc_scene::objects
 	int double_sided;         // meshlight
+	int photon_only;          // shoots photons only: not in the integrators' light list (render_view.cc:83-91)
 } yc_light;
 
 typedef struct {

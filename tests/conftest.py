@@ -26,3 +26,17 @@ def product():
     if not os.path.exists(Y.LIB_PATH):
         Y.build()
     return Y
+
+
+def experiments_built() -> bool:
+    """Whether libyafaray4.so carries the measured-and-dropped pipelines (-DYAF_EXPERIMENTS: k_trace_brute,
+    ray sorting, k_path, in-place NEE shadow rays, the bounded gather walk); the product build does not."""
+    import libyafaray_amd as Y
+    return "YAF_EXPERIMENTS" in Y.build_info()
+
+
+@pytest.fixture
+def experiments(product):
+    if not experiments_built():
+        pytest.skip("needs a -DYAF_EXPERIMENTS build of libyafaray4.so (tools/build_variants.sh)")
+    return True

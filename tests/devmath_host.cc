@@ -57,4 +57,25 @@ void dm_mwc(uint32_t seed, int steps, double *o)
 	Mwc m{30903u, seed};
 	for(int i = 0; i < steps; ++i) o[i] = m.next();
 }
+// libm restatements (devmath.h libmAtan2f / libmAcosf) next to the host's own libm on the same inputs;
+// the sphere mapping's long double expression next to real x87 long double
+void dm_libm(const float *y, const float *x, int n, float *dev_atan2, float *libm_atan2, float *dev_acos, float *libm_acos)
+{
+	for(int i = 0; i < n; ++i)
+	{
+		dev_atan2[i] = libmAtan2f(y[i], x[i]);
+		libm_atan2[i] = ::atan2f(y[i], x[i]);
+		dev_acos[i] = libmAcosf(y[i]);
+		libm_acos[i] = ::acosf(y[i]);
+	}
+}
+void dm_sphere_v(const float *a, int n, float *dev, float *ref)
+{
+	const long double div_1_by_pi = 0.31830988618379067153776752674503L;   // include/math/math.h
+	for(int i = 0; i < n; ++i)
+	{
+		dev[i] = x87oneMinus2Mul(kDiv1ByPi, a[i]);
+		ref[i] = static_cast<float>(1.f - 2.f * (a[i] * div_1_by_pi));
+	}
+}
 }

@@ -129,3 +129,40 @@ def test_magic_division_exact(dm):
         nn = np.concatenate([nn, nn - 1, nn + 1]).astype(np.uint32)
         bad = dm.dm_udiv_check(d, P(nn, C.c_uint32), len(nn))
         assert bad == -1, (d, int(nn[bad]))
+
+
+def test_libm_restatements_match_host_libm(dm):
+    """TextureMapperNode's tube / sphere projections call libm's float atan2 / acos
+    (shader_node_basic.cc:67, 77-78); devmath.h restates glibc's fdlibm algorithms so the device
+    matches the reference build bit for bit.  2.4 M inputs: uniform in [-1, 1]^2, random exponents, and
+    raw bit patterns (NaN, inf, zero, subnormal included)."""
+    rng = np.random.default_rng(11)
+    n = 800_000
+    parts_y = [rng.uniform(-1, 1, n).astype(np.float32),
+               (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-30, 30, n)).astype(np.float32),
+               rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32)]
+    parts_x = [rng.uniform(-1, 1, n).astype(np.float32),
+               (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-30, 30, n)).astype(np.float32),
+               rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32)]
+    y = np.ascontiguousarray(np.concatenate(parts_y))
+    x = np.ascontiguousarray(np.concatenate(parts_x))
+    m = len(y)
+    outs = [np.empty(m, np.float32) for _ in range(4)]
+    dm.dm_libm(P(y, C.c_float), P(x, C.c_float), m, *[P(o, C.c_float) for o in outs])
+    for dev, ref, name in ((outs[0], outs[1], "atan2f"), (outs[2], outs[3], "acosf")):
+        both_nan = np.isnan(dev) & np.isnan(ref)
+        same = (dev.view(np.uint32) == ref.view(np.uint32)) | both_nan
+        assert same.all(), f"{name}: {(~same).sum()} of {m} differ, e.g. {y[~same][:3]} {x[~same][:3]}"
+
+
+def test_sphere_v_long_double(dm):
+    """1.f - 2.f * (acos * div_1_by_pi) with the long double product and difference: every acos value
+    in [0, pi] on a fine grid plus random floats, against real x87 long double."""
+    rng = np.random.default_rng(12)
+    a = np.concatenate([np.linspace(0, np.pi, 1_000_001, dtype=np.float32), rng.uniform(0, np.pi, 1_000_000).astype(np.float32),
+                        np.float32([0.0, np.float32(np.pi), np.float32(np.pi / 2)])])
+    a = np.ascontiguousarray(a)
+    dev, ref = np.empty_like(a), np.empty_like(a)
+    dm.dm_sphere_v(P(a, C.c_float), len(a), P(dev, C.c_float), P(ref, C.c_float))
+    bad = dev.view(np.uint32) != ref.view(np.uint32)
+    assert not bad.any(), f"{bad.sum()} differ, e.g. {a[bad][:3]}"

@@ -44,6 +44,10 @@ CASES = {
 def test_two_pass_gather_equals_one_pass(product, case, heap, walk):
     if walk == "exact" and case == "k100":
         pytest.skip("the exact walk keeps at most 64 distances (k = 100 takes the bounded walk)")
+    if walk == "bound":
+        from conftest import experiments_built
+        if not experiments_built():
+            pytest.skip("the bounded walk lives in -DYAF_EXPERIMENTS builds only (k > 64 takes the one-pass gather)")
     spec = CASES[case]()
     a, wa, sa = _render(product, spec, {"YAFARAY_AMD_GATHER": "single"})
     b, wb, sb = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_HEAP": heap, "YAFARAY_AMD_GATHER_WALK": walk})
@@ -66,7 +70,7 @@ def test_two_pass_gather_log_overflow_falls_back(product, heap):
 
 
 @pytest.mark.gpu
-def test_bounded_walk_logs_a_superset(product):
+def test_bounded_walk_logs_a_superset(product, experiments):
     """The bounded walk logs every photon the exact walk accepts plus the ones the replay rejects."""
     spec = CASES["diffuse"]()
     a, _, sa = _render(product, spec, {"YAFARAY_AMD_GATHER": "walk", "YAFARAY_AMD_GATHER_WALK": "exact"})

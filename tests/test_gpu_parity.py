@@ -61,6 +61,10 @@ BVH_VARIANTS = {"bvh4": {"YAFARAY_AMD_BVH_BUILD": "host", "YAFARAY_AMD_TRACE": "
 
 
 def use_bvh(monkeypatch, variant):
+    if variant in ("brute", "ray-sort"):
+        from conftest import experiments_built
+        if not experiments_built():
+            pytest.skip("k_trace_brute / ray sorting live in -DYAF_EXPERIMENTS builds only")
     for k, v in BVH_VARIANTS[variant].items():
         monkeypatch.setenv(k, v)
 

@@ -120,14 +120,35 @@ def test_final_gather_two_lights_statistical(product, oracle_built):
     assert z["max_abs_block_z"] < 6.0, z
 
 
-@pytest.mark.parametrize("case", ["3-lights-adaptive", "dl-3-lights"])
+@pytest.mark.parametrize("members", [1, 3])
+def test_light_pick_counters_over_budget_fall_back_to_hash(product, members, monkeypatch):
+    """the one-thread pick's per-sample counters (4 B per camera sample of a pass) that do
+    not fit the memory budget make the pass fall back to the hashed pick instead of failing the render
+    (YAFARAY_AMD_LPC_MAX_MB forces it here): the image equals the YAFARAY_AMD_LIGHT_PICK=hash render bit
+    for bit, on one GPU and in a device group (whose members agree on the fallback)."""
+    spec = EXACT["2-lights"]()
+    monkeypatch.setenv("YAFARAY_AMD_LPC_MAX_MB", "0")
+    a, wa, _ = product.render_spec(spec, members=members)
+    monkeypatch.delenv("YAFARAY_AMD_LPC_MAX_MB")
+    monkeypatch.setenv("YAFARAY_AMD_LIGHT_PICK", "hash")
+    b, wb, _ = product.render_spec(spec, members=members)
+    assert np.array_equal(wa, wb)
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+
+
+@pytest.mark.parametrize("case", ["3-lights-adaptive", "dl-3-lights", "dl-specular-tree"])
 def test_nee_request_word_packing(product, oracle_built, case, monkeypatch):
     """k_shade packs each NEE request's (pixel offset, sample index, mode, light) word into 8 B
     (kernels.hip neePmStore: the sample index relative to the pass's first one); the 16-B form
     (YAFARAY_AMD_NEE_PM16=1, used when a pass has >= 2^20 samples per pixel or > 2^11 lights)
     must render the same image bit for bit, and both equal the one-thread oracle."""
-    spec = EXACT["3-lights-adaptive"]() if case == "3-lights-adaptive" else with_lights(
-        scenes.cornell(64, 48, spp=4, integrator="directlighting"), 3)
+    if case == "3-lights-adaptive":
+        spec = EXACT["3-lights-adaptive"]()
+    elif case == "dl-3-lights":
+        spec = with_lights(scenes.cornell(64, 48, spp=4, integrator="directlighting"), 3)
+    else:
+        # a specular recursion tree: the spawned nodes' NEE requests carry their sample's index (ADVICE r04)
+        spec = with_lights(scenes.cornell_specular(48, 36, spp=2, integrator="directlighting", raydepth=3), 2)
     a, wa, _ = product.render_spec(spec)
     monkeypatch.setenv("YAFARAY_AMD_NEE_PM16", "1")
     b, wb, _ = product.render_spec(spec)

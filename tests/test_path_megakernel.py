@@ -14,6 +14,11 @@ import pytest
 from libyafaray_amd import scenes
 
 
+@pytest.fixture(autouse=True)
+def _needs_experiments(experiments):
+    """k_path and k_nee<TR> are compiled only into -DYAF_EXPERIMENTS builds (measured slower)."""
+
+
 def _render(product, spec, wavefront, chunk=None):
     old = os.environ.get("YAFARAY_AMD_PATH")
     try:
