@@ -301,6 +301,7 @@ struct DevScene
 	uint32_t *lpc;
 	int lpc_mode;
 	int nee_pm16;          // 1: NEE requests keep the 16-B pixel / mode word (YAFARAY_AMD_NEE_PM16=1; else 8 B where it fits)
+	int w_live;            // 1: the integrator's sample weight w must persist across vertices (DevPaths::thr.w); 0: thr is a 12-B record
 };
 
 struct DevFilm

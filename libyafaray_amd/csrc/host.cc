@@ -1434,6 +1434,7 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		S.s_depth = std::max(0, shadow_depth);
 		S.tree = 0;
 		S.ext = 0;
+		S.w_live = 0;
 		S.max_add_depth = 0;
 		for(const auto &kv : materials)
 		{
@@ -1443,7 +1444,14 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			if(m.type == MAT_MIRROR || m.type == MAT_NULL || m.n_nodes > 0 ||
 			   (m.sd_flags & (SD_MIRROR | SD_TRANSPARENT | SD_TRANSLUCENT | SD_FRESNEL | SD_OREN_NAYAR)))
 				S.ext = 1;
+			// a shinydiffuse sample() that matches no component returns before it sets w
+			// (material_shiny_diffuse.cc:259-262), and the path tracer multiplies by the previous w
+			if(m.type == MAT_SHINYDIFFUSE && (m.n_bsdf == 0 || (double)m.comp[3] < 0.00001)) S.w_live = 1;
 		}
+		// the sample weight w persists across vertices only when some sample() can leave it unset: the
+		// EXT materials (Fresnel / transparency can shrink the diffuse share) or a non-diffuse shinydiffuse;
+		// else k_shade keeps the throughput as a 12-B record
+		if(S.ext) S.w_live = 1;
 
 		S.has_bg = 0;
 		if(!s.background_name.empty() && backgrounds.count(s.background_name))

@@ -44,6 +44,9 @@ namespace yafamd
 #ifndef YAF_SHADE_MIN_WAVES
 #define YAF_SHADE_MIN_WAVES 4
 #endif
+#ifndef YAF_SHADE_PREFETCH
+#define YAF_SHADE_PREFETCH 1
+#endif
 constexpr int kTraceBlock = YAF_TRACE_BLOCK;
 // -DYAF_EXPERIMENTS: the pipelines measured and dropped stay buildable for re-measurement but out of
 // the product library (kExperiments; yafaray_amd_buildInfo records the flag): k_trace_brute, ray-stream
@@ -131,6 +134,19 @@ __device__ __forceinline__ void stStore(T *p, const T &v)
 	__builtin_nontemporal_store(w, reinterpret_cast<u32x4_t *>(p));
 #else
 	*p = v;
+#endif
+}
+// the compact path record (sample id, stage): 8 B, non-temporal as the 16-B records
+__device__ __forceinline__ void stStoreU2(uint2 *p, uint2 v)
+{
+	typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
+	u2_t w;
+	w.x = v.x;
+	w.y = v.y;
+#if YAF_NT_STORE
+	__builtin_nontemporal_store(w, reinterpret_cast<u2_t *>(p));
+#else
+	*reinterpret_cast<u2_t *>(p) = w;
 #endif
 }
 // wider use (queues, NEE requests and contributions, shadow rays): -DYAF_NT_STORE2
@@ -229,6 +245,17 @@ __device__ __forceinline__ void storeQRay(const DevQueues &Q, uint32_t i, V3 o, 
 #else
 	reinterpret_cast<F3 *>(Q.ray_o)[i] = F3{o.x, o.y, o.z};
 	reinterpret_cast<F3 *>(Q.ray_d)[i] = F3{d.x, d.y, d.z};
+#endif
+}
+// a 12-B path-state record (the throughput without w), non-temporal as the 16-B ones
+__device__ __forceinline__ void stStoreF3(float4 *base, uint32_t k, C3 c)
+{
+#if YAF_NT_STORE
+	f32x3a4_t v;
+	v.x = c.r; v.y = c.g; v.z = c.b;
+	__builtin_nontemporal_store(v, reinterpret_cast<f32x3a4_t *>(reinterpret_cast<float *>(base) + 3 * (size_t)k));
+#else
+	reinterpret_cast<F3 *>(base)[k] = F3{c.r, c.g, c.b};
 #endif
 }
 __device__ __forceinline__ void storeQNoRay(const DevQueues &Q, uint32_t i)
@@ -493,7 +520,7 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 	// its stage — k_shade does not read them — so they are not written: 32 B per sample each way)
 	storeQRay(Q, a, from, dir);
 	if(S.cam.ray_tt) Q.ray_tt[a] = make_float2(tmin, tmax);
-	if(!S.tree) P.pr[a] = make_uint4((uint32_t)i, ST_CAMERA, 30903u, seed);
+	if(!S.tree) reinterpret_cast<uint2 *>(P.pr)[a] = make_uint2((uint32_t)i, ST_CAMERA);   // (RR: rrRandom)
 	else
 	{
 		const int cx = sc.x + S.crop_x0, cy = sc.y + S.crop_y0;
@@ -714,6 +741,15 @@ __device__ __forceinline__ void cswap(float &ka, int &va, float &kb, int &vb)
 struct SlabSel { int nx, ny, nz; };   // float4 index in the node of the near plane per axis (far: ^ 1)
 __device__ __forceinline__ SlabSel slabSel(V3 id) { return SlabSel{id.x >= 0.f ? 0 : 1, id.y >= 0.f ? 2 : 3, id.z >= 0.f ? 4 : 5}; }
 
+// Child order after a BVH4 visit (results never depend on it: closest hits tie-break on the primitive
+// index, any hits answer occluded / not): closest rays sort the hit inner children by entry distance
+// (YAF_CLOSEST_SORT, the culling order); any-hit rays skip the network (YAF_ANY_SORT=1 restores it)
+#ifndef YAF_ANY_SORT
+#define YAF_ANY_SORT 0
+#endif
+#ifndef YAF_CLOSEST_SORT
+#define YAF_CLOSEST_SORT 1
+#endif
 // BVH4 (bvh.cc: collapsed binary SAH tree, 128 B nodes with the four child boxes in SoA form).
 // Same hit semantics as traverse2: leaf children are tested as soon as their box is hit, inner
 // children are sorted by entry distance (5-exchange network) and descended nearest-first.
@@ -743,12 +779,14 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + lane] = v;
 		else if(SPILL) C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane] = v;
 	};
+	// the box culling distance: recomputed only where t_best changes (a closest hit), not per visit
+	auto slackOf = [](float t) { return (t < 3.0e38f) ? t * 1.0000005f + 1e-6f : 3.4e38f; };
+	float slack_t = slackOf(t_best);
 	for(;;)
 	{
 		if(STATS) TRACE_STAT(++visits);
 		const float4 *np = C.nodes + 8 * node;
 		const float4 nx = np[sel.nx], fx = np[sel.nx ^ 1], ny = np[sel.ny], fy = np[sel.ny ^ 1], nz = np[sel.nz], fz = np[sel.nz ^ 1], cf = np[6], kf = np[7];
-		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
 		float key[4];
 		int child[4], count[4];
 		uint32_t leaves = 0;
@@ -805,18 +843,48 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 				{
 					t_best = t;
 					prim_best = prim;
+					slack_t = slackOf(t_best);
 				}
 			}
 		}
-		cswap(key[0], child[0], key[1], child[1]);
-		cswap(key[2], child[2], key[3], child[3]);
-		cswap(key[0], child[0], key[2], child[2]);
-		cswap(key[1], child[1], key[3], child[3]);
-		cswap(key[1], child[1], key[2], child[2]);
-		if(key[3] < inf) { push(child[3]); ++sp; }
-		if(key[2] < inf) { push(child[2]); ++sp; }
-		if(key[1] < inf) { push(child[1]); ++sp; }
-		int next = key[0] < inf ? child[0] : -1;
+		int next;
+		if constexpr(ANY && !YAF_ANY_SORT)
+		{
+			// any hit: the answer does not depend on the order the hit children are visited in (there is
+			// no distance to cull against), so no sorting network — the first hit inner child is descended,
+			// the others pushed in node order
+			next = -1;
+#pragma unroll
+			for(int k = 0; k < 4; ++k)
+			{
+				if(!(key[k] < inf)) continue;
+				if(next < 0) next = child[k];
+				else { push(child[k]); ++sp; }
+			}
+		}
+		else if constexpr(!YAF_CLOSEST_SORT)
+		{
+			// (tuning variant) the nearest hit child descended, the others pushed in node order
+			int kmin = 0;
+#pragma unroll
+			for(int k = 1; k < 4; ++k) kmin = key[k] < key[kmin] ? k : kmin;
+			next = key[kmin] < inf ? child[kmin] : -1;
+#pragma unroll
+			for(int k = 3; k >= 0; --k)
+				if(k != kmin && key[k] < inf) { push(child[k]); ++sp; }
+		}
+		else
+		{
+			cswap(key[0], child[0], key[1], child[1]);
+			cswap(key[2], child[2], key[3], child[3]);
+			cswap(key[0], child[0], key[2], child[2]);
+			cswap(key[1], child[1], key[3], child[3]);
+			cswap(key[1], child[1], key[2], child[2]);
+			if(key[3] < inf) { push(child[3]); ++sp; }
+			if(key[2] < inf) { push(child[2]); ++sp; }
+			if(key[1] < inf) { push(child[1]); ++sp; }
+			next = key[0] < inf ? child[0] : -1;
+		}
 		if(next < 0)
 		{
 			if(sp == 0) break;
@@ -1777,6 +1845,19 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h)
 	return h;
 }
 
+// Russian roulette draw (path_tracer.cc:249-251: random_generator(), the reference's per-tile
+// generator seeded from rand() — schedule-dependent, so RR is matched statistically): a
+// hash of the sample's pixel-major global id (as k_camera's seed), the RR seed, the pass, the subpath
+// and the bounce.  Stateless: the compact path record carries no generator state (8 B instead of 16
+// per vertex each way), and the image does not depend on how the film is split over GPUs or chunks.
+__device__ __forceinline__ float rrRandom(const DevScene &S, const SampleCoord &sc, uint32_t subpath, int depth)
+{
+	const uint64_t gid = ((uint64_t)sc.y * (uint64_t)S.width + (uint64_t)sc.x) * (uint64_t)S.spp + (uint64_t)sc.s;
+	uint32_t h = mix32((uint32_t)gid ^ mix32((uint32_t)(gid >> 32) ^ S.rr_seed ^ (S.pass_offset * 0x9e3779b9u)));
+	h = mix32(h ^ (subpath * 0x85ebca6bu + (uint32_t)depth * 0xc2b2ae35u));
+	return (float)((double)h * kSampleMultRatio);
+}
+
 __device__ __forceinline__ uint32_t pickLight(const DevScene &S, uint32_t offset, uint32_t sample_idx, uint32_t local, uint32_t stride)
 {
 	if(S.n_lights <= 1) return 0u;
@@ -2395,10 +2476,20 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 	// with every vertex
 	const bool compact = !(EXT && S.tree);
 	PHASE_DECL
+#if YAF_SHADE_PREFETCH
+	// the next iteration's compact record (the head of the entry's dependent load chain) is loaded while
+	// this one is shaded
+	uint2 pr_n = make_uint2(0u, ST_NORAY);
+	if(compact && threadIdx.x < n_a) pr_n = reinterpret_cast<const uint2 *>(Pc.pr)[a0 + threadIdx.x];
+#endif
 	for(uint32_t base_j = 0; base_j < n_a; base_j += stride)
 	{
 		const bool live = base_j + threadIdx.x < n_a;
 		const uint32_t i = a0 + base_j + threadIdx.x;   // address of the entry (shard base + position)
+#if YAF_SHADE_PREFETCH
+		const uint2 pr_cur = pr_n;
+		if(compact && base_j + stride + threadIdx.x < n_a) pr_n = reinterpret_cast<const uint2 *>(Pc.pr)[i + stride];
+#endif
 		// ---- 0. load the entry (coalesced loads; stage, flags and w ride in the .w lanes) ----
 		uint32_t sid = 0, stage = ST_NORAY, flags = 0;
 		uint2 pix = make_uint2(0u, 0u), rng = make_uint2(0u, 0u);
@@ -2409,10 +2500,14 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 		SampleCoord sc{0, 0, 0};
 		if(live)
 		{
-			const uint4 pr = Pc.pr[i];
-			rng = make_uint2(pr.z, pr.w);
 			if(compact)
 			{
+				// compact record: (sample id, stage), 8 B — the RR draw is a hash (rrRandom)
+#if YAF_SHADE_PREFETCH
+				const uint2 pr = pr_cur;
+#else
+				const uint2 pr = reinterpret_cast<const uint2 *>(Pc.pr)[i];
+#endif
 				sid = pr.x;
 				stage = pr.y;
 				sc = sampleAt(S, A.jobs, A.n_jobs, A.chunk_base + (uint64_t)sid);
@@ -2421,6 +2516,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			}
 			else
 			{
+				const uint4 pr = Pc.pr[i];
+				rng = make_uint2(pr.z, pr.w);
 				sid = (uint32_t)A.Q.slot[i];
 				pix = make_uint2(pr.x, pr.y);
 				col4 = Pc.col[i];
@@ -2430,7 +2527,13 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 			// write them) and has no first-hit data yet
 			if(!compact || (stage & 0xffu) != ST_CAMERA)
 			{
-				thr4 = Pc.thr[i];
+				if(S.w_live) thr4 = Pc.thr[i];
+				else
+				{
+					// w is set by every sample() of this scene before it is read: a 12-B throughput record
+					const F3 t = reinterpret_cast<const F3 *>(Pc.thr)[i];
+					thr4 = make_float4(t.x, t.y, t.z, 0.f);
+				}
 				pcol4 = Pc.pcol[i];
 				if(keep_v0) { v0p4 = Pc.v0p[i]; v0wo4 = Pc.v0wo[i]; }
 				if(ATTR && keep_v0) { v0a0 = Pc.v0attr[2 * (size_t)i]; v0a1 = Pc.v0attr[2 * (size_t)i + 1]; }
@@ -2612,10 +2715,16 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 					bool killed = false;
 					if(depth > S.rr_min_bounces)
 					{
-						// path_tracer.cc:249-255 (the draw does not depend on the light estimate)
-						Mwc g{rng.x, rng.y};
-						const float random_value = (float)g.next();
-						rng = make_uint2(g.x, g.c);
+						// path_tracer.cc:249-255 (the draw does not depend on the light estimate); the
+						// specular recursion tree's nodes keep a per-node MWC stream in their full record
+						float random_value;
+						if(compact) random_value = rrRandom(S, sc, subpath, depth);
+						else
+						{
+							Mwc g{rng.x, rng.y};
+							random_value = (float)g.next();
+							rng = make_uint2(g.x, g.c);
+						}
 						const float probability = maxComp(thr);
 						if(probability <= 0.f || probability < random_value) killed = true;
 						else thr = thr * rcpExact(probability);
@@ -2784,13 +2893,14 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_
 				if(!FUSED && want_nee) reinterpret_cast<F3 *>(A.Qn.ray_o)[k] = F3{sp.p.x, sp.p.y, sp.p.z};
 				stage = ST_NORAY | (subpath << 8) | ((uint32_t)depth << 20);
 			}
-			if(compact) stStore(&Pn.pr[k], make_uint4(sid, stage, rng.x, rng.y));
+			if(compact) stStoreU2(reinterpret_cast<uint2 *>(Pn.pr) + k, make_uint2(sid, stage));
 			else
 			{
 				stStore(&Pn.pr[k], make_uint4(pix.x, pix.y, rng.x, rng.y));
 				stStore(&Pn.col[k], f4(col, __uint_as_float(stage)));
 			}
-			stStore(&Pn.thr[k], f4(thr, w));
+			if(S.w_live) stStore(&Pn.thr[k], f4(thr, w));
+			else stStoreF3(Pn.thr, k, thr);
 			stStore(&Pn.pcol[k], f4(pcol, __uint_as_float(flags)));
 			if((stage & 0xffu) == ST_FIRST) Pn.pwo[k] = f4(pwo, 0.f);
 			if(nee_one) reinterpret_cast<F3 *>(Pn.pend_thr)[k] = F3{pend_thr.r, pend_thr.g, pend_thr.b};
@@ -3233,6 +3343,9 @@ __host__ __device__ inline size_t neeTraceLdsBytes(const DevScene &S, int stack_
 #ifndef YAF_NEE_MIN_WAVES
 #define YAF_NEE_MIN_WAVES 4
 #endif
+#ifndef YAF_NEE_PREFETCH
+#define YAF_NEE_PREFETCH 0
+#endif
 template<bool SMALL, bool EXT, bool TR = false, bool TSTATS = false>
 __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
 {
@@ -3275,6 +3388,19 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 	const uint32_t a0 = seg * S.cap_a;
 	const int K = S.nee_k;
 	const uint32_t stride = blockDim.x;
+#if YAF_NEE_PREFETCH
+	// the next iteration's request is loaded while this one is computed (software pipelining: k_nee
+	// waits on these loads, SQ_WAIT_ANY 0.52 at VALU issue 0.19)
+	float4 wk_n = make_float4(0.f, 0.f, 0.f, 0.f);
+	F3 o_n{0.f, 0.f, 0.f};
+	uint4 pm_n = make_uint4(0u, 0u, 0u, 0u);
+	if(threadIdx.x < n_slots)
+	{
+		wk_n = A.N.wo_k[a0 + threadIdx.x];
+		o_n = reinterpret_cast<const F3 *>(A.Qn.ray_o)[a0 + threadIdx.x];
+		pm_n = neePmLoad(S, A.N.pix_mode, a0 + threadIdx.x);
+	}
+#endif
 	for(uint32_t base_j = 0; base_j < n_slots; base_j += stride)
 	{
 		const uint32_t j = a0 + base_j + threadIdx.x;
@@ -3282,6 +3408,21 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 		V3 p = v3(0.f, 0.f, 0.f);
 		uint4 pm = make_uint4(0u, 0u, 0u, 0u);
 		bool live = base_j + threadIdx.x < n_slots;
+#if YAF_NEE_PREFETCH
+		if(live)
+		{
+			wk = wk_n;
+			p = v3(o_n.x, o_n.y, o_n.z);
+			pm = pm_n;
+			live = !(wk.x != wk.x);
+		}
+		if(base_j + stride + threadIdx.x < n_slots)
+		{
+			wk_n = A.N.wo_k[j + stride];
+			o_n = reinterpret_cast<const F3 *>(A.Qn.ray_o)[j + stride];
+			pm_n = neePmLoad(S, A.N.pix_mode, j + stride);
+		}
+#else
 		if(live)
 		{
 			// every load issued before the request test (one memory round trip)
@@ -3291,6 +3432,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 			pm = neePmLoad(S, A.N.pix_mode, j);
 			live = !(wk.x != wk.x);
 		}
+#endif
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
 		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
@@ -3606,10 +3748,8 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 					bool killed = false;
 					if(depth > S.rr_min_bounces)
 					{
-						// path_tracer.cc:249-255
-						Mwc g{rng.x, rng.y};
-						const float random_value = (float)g.next();
-						rng = make_uint2(g.x, g.c);
+						// path_tracer.cc:249-255 (the wavefront's stateless draw)
+						const float random_value = rrRandom(S, sc, subpath, depth);
 						const float probability = maxComp(thr);
 						if(probability <= 0.f || probability < random_value) killed = true;
 						else thr = thr * rcpExact(probability);

@@ -737,7 +737,7 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.shader_nodes = (const DevNode *)d.shader_nodes.p;
 	S.textures = (const DevTexture *)d.textures.p;
 	S.texels = (const float4 *)d.texels.p;
-	if(S.has_attr) S.ext = 1;
+	if(S.has_attr) { S.ext = 1; S.w_live = 1; }
 }
 
 // One photon map on the GPU: shoot N paths from the light set L (diffuseWorker /
@@ -1788,6 +1788,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	S.lpc_mode = 0;
 	S.nee_pm16 = 0;
 	if(const char *e = std::getenv("YAFARAY_AMD_NEE_PM16"); e && *e == '1') S.nee_pm16 = 1;   // tests: the 16-B request word
+	if(const char *e = std::getenv("YAFARAY_AMD_W_LIVE"); e && *e == '1') S.w_live = 1;        // tests: the 16-B throughput record
 	int path_grid = 0;
 	if(!lpc_on)
 	{

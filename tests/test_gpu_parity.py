@@ -319,3 +319,17 @@ def test_photon_map_sizes_match_oracle(product, oracle_built, photons):
     d = ulp_diff(rgba, orgba)
     assert d.max() <= 4, f"{(d > 4).sum()} values > 4 ULP, max {d.max()} at {np.unravel_index(d.argmax(), d.shape)}"
     assert st["gather_visits"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rr", [False, True])
+def test_throughput_record_without_w_equals_full_record(product, monkeypatch, rr):
+    """r05: scenes whose every sample() sets the weight w before it is read keep the throughput as a
+    12-B record (DevScene::w_live = 0, host.cc); YAFARAY_AMD_W_LIVE=1 forces the 16-B record that carries
+    w — the two renders must be bit-identical (RR off and on: the stateless RR draw is the same)."""
+    spec = scenes.cornell(80, 60, spp=8, bounces=6, rr=rr)
+    a, wa, _ = product.render_spec(spec)
+    monkeypatch.setenv("YAFARAY_AMD_W_LIVE", "1")
+    b, wb, _ = product.render_spec(spec)
+    assert np.array_equal(wa, wb)
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
