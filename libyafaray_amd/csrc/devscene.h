@@ -302,6 +302,8 @@ struct DevScene
 	int lpc_mode;
 	int nee_pm16;          // 1: NEE requests keep the 16-B pixel / mode word (YAFARAY_AMD_NEE_PM16=1; else 8 B where it fits)
 	int w_live;            // 1: the integrator's sample weight w must persist across vertices (DevPaths::thr.w); 0: thr is a 12-B record
+	int no_lean;           // 1: the general k_shade / k_nee instantiations even where a lean one applies (YAFARAY_AMD_SHADE_LEAN=0: tests, A/B)
+	int has_mesh_light;    // some light is a meshlight (k_nee's lean instantiation has no meshlight code)
 };
 
 struct DevFilm

@@ -44,6 +44,9 @@ namespace yafamd
 #ifndef YAF_SHADE_MIN_WAVES
 #define YAF_SHADE_MIN_WAVES 4
 #endif
+#ifndef YAF_SHADE_LEAN_WAVES
+#define YAF_SHADE_LEAN_WAVES 4
+#endif
 #ifndef YAF_SHADE_PREFETCH
 #define YAF_SHADE_PREFETCH 1
 #endif
@@ -537,6 +540,10 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 // ---------------------------------------------------------------------------------------------
 // k_trace: BVH2 / BVH4 traversal
 // ---------------------------------------------------------------------------------------------
+#ifndef YAF_TOP_STRIDE
+#define YAF_TOP_STRIDE 9
+#endif
+constexpr int kTopStride = YAF_TOP_STRIDE;   // float4 per node of the LDS top treelet (8 used + 1 pad)
 struct TraceCtx
 {
 	const float4 *nodes;
@@ -545,7 +552,10 @@ struct TraceCtx
 	int lds_depth;
 	int *spill;     // HBM, [(level - lds_depth) * spill_stride + global lane] (BVH4 deep levels)
 	uint32_t spill_stride;
-	// the top treelet of a BVH4 in global memory staged in LDS: nodes [0, n_top) (both builders number
+	// the top treelet of a BVH4 in global memory staged in LDS: nodes [0, n_top) at kTopStride float4 each
+	// (144 B: a 128-B stride put every node's plane p on the same 4 of the 64 banks, so the 16 lanes of a
+	// ds_read_b128 group at different nodes conflicted up to 8-way; 36-dword strides spread 16 nodes
+	// over 16 distinct bank quads) (both builders number
 	// the wide nodes level by level, so these are the levels every ray starts with)
 	const float4 *top = nullptr;
 	int n_top = 0;
@@ -974,7 +984,7 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 			// the top treelet from LDS (an explicit LDS pointer: ds_read, not flat loads)
 			typedef float V4 __attribute__((ext_vector_type(4)));
 			typedef const __attribute__((address_space(3))) V4 *LdsV4;
-			const LdsV4 tp = (LdsV4)(C.top + 8 * node);
+			const LdsV4 tp = (LdsV4)(C.top + kTopStride * node);
 			auto ld = [&](int k) {
 				const V4 v = tp[k];
 				return make_float4(v.x, v.y, v.z, v.w);
@@ -1190,7 +1200,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 		{
 			// the top treelet (refill loop only): nodes [0, lds_top) after the stack
 			float4 *top = smem + (stack_depth * kTraceBlock) / 4;
-			for(int k = threadIdx.x; k < 8 * S.lds_top; k += blockDim.x) top[k] = S.nodes[k];
+			for(int k = threadIdx.x; k < 8 * S.lds_top; k += blockDim.x) top[(k >> 3) * kTopStride + (k & 7)] = S.nodes[k];
 			__syncthreads();
 			C.top = top;
 			C.n_top = S.lds_top;
@@ -1948,10 +1958,11 @@ __device__ __forceinline__ void meshSampleSurface(const DevScene &S, const DevLi
 
 // The light-sample half of areaLightSampleLight for an area light (light_area.cc:66-96) or a mesh
 // light (light_object_light.cc:111-146): direction and distance to the sampled point and the pdf.
+template<bool NOMESH = false>
 __device__ __forceinline__ bool lightIllumSample(const DevScene &S, const DevLight &L, V3 sp_p, float s_1, float s_2, V3 &ldir, float &dist, float &pdf)
 {
 	V3 p, fn;
-	if(L.type == LIGHT_MESH) meshSampleSurface(S, L, s_1, s_2, p, fn);
+	if(!NOMESH && L.type == LIGHT_MESH) meshSampleSurface(S, L, s_1, s_2, p, fn);
 	else
 	{
 		p = lv(L.pos) + s_1 * lv(L.to_x) + s_2 * lv(L.to_y);
@@ -1962,7 +1973,7 @@ __device__ __forceinline__ bool lightIllumSample(const DevScene &S, const DevLig
 	dist = sqrtf(dist_sqr);
 	if((double)dist <= 0.0) return false;
 	ldir = ldir * rcpExact(dist);
-	if(L.type == LIGHT_MESH)
+	if(!NOMESH && L.type == LIGHT_MESH)
 	{
 		float cos_angle = -dot(ldir, fn);
 		if(cos_angle <= 0)
@@ -1985,9 +1996,10 @@ __device__ __forceinline__ bool lightIllumSample(const DevScene &S, const DevLig
 // Mesh light: light_object_light.cc:183-201 — the closest face (the light's own kd-tree, faces with
 // t >= tmin) gives the normal; the reference never stores the hit distance in `t` (the caller's ray
 // tmax, -1), so 1 / (t * t) is 1 and the shadow ray is unbounded: both reproduced.
+template<bool NOMESH = false>
 __device__ __forceinline__ bool lightMatHit(const DevScene &S, const DevLight &L, V3 p, V3 dir, float b_tmin, float &t, float &light_pdf)
 {
-	if(L.type == LIGHT_MESH)
+	if(!NOMESH && L.type == LIGHT_MESH)
 	{
 		float t_best = __builtin_huge_valf();
 		int best = -1;
@@ -2051,7 +2063,8 @@ __device__ __forceinline__ C3 neeGet(const NeeHbm &nee, int e)
 	return C3{c.x, c.y, c.z};
 }
 
-template<bool EXT, class Out, class NeeT>
+// NOMESH: the scene has no meshlight (k_nee's lean instantiation drops that code)
+template<bool EXT, class Out, class NeeT, bool NOMESH = false>
 __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial &m, const Surf &sp, V3 wo,
                          uint32_t loffs, uint32_t sample_idx, uint32_t offset, bool active, int e0,
                          NeeT nee, uint8_t *occ, const Out &out, float4 *ts = nullptr)
@@ -2117,7 +2130,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 		{
 			// light_area.cc:66-96 / light_object_light.cc:111-146
 			float dist = 0.f, pdf = 0.f;
-			ok = lightIllumSample(S, L, sp.p, s_1, s_2, ldir, dist, pdf);
+			ok = lightIllumSample<NOMESH>(S, L, sp.p, s_1, s_2, ldir, dist, pdf);
 			if(ok)
 			{
 				if(pdf > 1e-6f)
@@ -2165,7 +2178,7 @@ __device__ void neeLight(const DevScene &S, const DevLight &L, const DevMaterial
 			{
 				// light_area.cc:137-151
 				// light_area.cc:137-151 / light_object_light.cc:183-201
-				ok = lightMatHit(S, L, sp.p, dir, b_tmin, t, lpdf);
+				ok = lightMatHit<NOMESH>(S, L, sp.p, dir, b_tmin, t, lpdf);
 			}
 			if(ok)
 			{
@@ -2440,11 +2453,28 @@ __device__ void spawnSpecular(const DevScene &S, const DevMaterial &m, const Sur
 // queueing requests for k_nee — the NEE request round trip through HBM (48 B written + read per
 // vertex) and one launch per iteration disappear; the shade loop is HBM-bound, so the light
 // sampling arithmetic overlaps its memory traffic.
-template<bool SMALL, bool EXT, bool FUSED = false>
-__global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_SHADE_MIN_WAVES) k_shade(ShadeArgs A)
+// LEAN: the plain path tracer (PathIntegrator, one path per sample, no AO / photon maps / caustic map /
+// gather queue) with those scene switches fixed at compile time, so the other integrators' state
+// (first-hit records, gather requests, AO sums) costs no registers (launch_shade picks it)
+template<bool SMALL, bool EXT, bool FUSED = false, bool LEAN = false>
+__global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_WAVES : YAF_SHADE_MIN_WAVES)) k_shade(ShadeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
-	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
+	DevScene S_ = stageTables<SMALL>(A.S, shade_smem);
+	if constexpr(LEAN)
+	{
+		S_.integrator = INT_PATH;
+		S_.path_samples = 1;
+		S_.do_ao = 0;
+		S_.caus_map = 0;
+		S_.show_map = 0;
+		S_.gather_on = 0;
+		S_.n_photons = 0;
+		S_.fg_on = 0;
+		S_.tree = 0;
+		S_.has_attr = 0;
+	}
+	const DevScene S = S_;
 	const bool ATTR = EXT && S.has_attr != 0;   // k_surface output present
 	const DevPaths &Pc = A.Pc;
 	const DevPaths &Pn = A.Pn;
@@ -3343,14 +3373,26 @@ __host__ __device__ inline size_t neeTraceLdsBytes(const DevScene &S, int stack_
 #ifndef YAF_NEE_MIN_WAVES
 #define YAF_NEE_MIN_WAVES 4
 #endif
+#ifndef YAF_NEE_LEAN_WAVES
+#define YAF_NEE_LEAN_WAVES 4
+#endif
 #ifndef YAF_NEE_PREFETCH
 #define YAF_NEE_PREFETCH 0
 #endif
-template<bool SMALL, bool EXT, bool TR = false, bool TSTATS = false>
-__global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_nee(NeeArgs A)
+// LEAN: no ambient occlusion, transparent shadows or meshlights (launch_nee picks it), so their code and
+// registers drop out
+template<bool SMALL, bool EXT, bool TR = false, bool TSTATS = false, bool LEAN = false>
+__global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_NEE_LEAN_WAVES : YAF_NEE_MIN_WAVES)) k_nee(NeeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
-	const DevScene S = stageTables<SMALL>(A.S, shade_smem);
+	DevScene S_ = stageTables<SMALL>(A.S, shade_smem);
+	if constexpr(LEAN)
+	{
+		S_.do_ao = 0;
+		S_.tr_shad = 0;
+		S_.has_attr = 0;
+	}
+	const DevScene S = S_;
 	const bool ATTR = EXT && S.has_attr != 0;
 	TraceCtx C;
 	float4 *rec = nullptr;
@@ -3468,7 +3510,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 		{
 			// estimateAllDirectLight (montecarlo.cc:54-68)
 			for(int l = 0; l < S.n_lights; ++l)
-				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
+				neeLight<EXT, ShadeOut, NeeHbm, LEAN>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, all,
 				         e0 + (int)S.lights[l].nee_base, neeHbm(A.Pn), A.Pn.occ, out, S.tr_shad ? A.Pn.ts : nullptr);
 			if(S.do_ao)
 				aoSamples<EXT>(S, S.mats[sp.mat], sp, wo, pm.y, pm.x, all, e0 + S.nee_all_count, neeHbm(A.Pn), A.Pn.occ, out,
@@ -3481,7 +3523,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : YAF_NEE_MIN_WAVES) k_ne
 			{
 				const bool mine = one && lnum == (uint32_t)l;
 				if(!__any(mine)) continue;
-				neeLight<EXT>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, neeHbm(A.Pn), A.Pn.occ, out,
+				neeLight<EXT, ShadeOut, NeeHbm, LEAN>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pm.y, pm.x, mine, e0, neeHbm(A.Pn), A.Pn.occ, out,
 				              S.tr_shad ? A.Pn.ts : nullptr);
 			}
 		}
@@ -5841,7 +5883,7 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	const bool wide = S->node_f4 == 8;
 	const size_t lds_scene = S->scene_in_lds ? (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4)
-	                                         : (wide ? (size_t)S->lds_top * 8 * sizeof(float4) : 0);
+	                                         : (wide ? (size_t)S->lds_top * kTopStride * sizeof(float4) : 0);
 	const size_t bytes = stack_bytes + lds_scene;
 #ifdef YAF_EXPERIMENTS
 	if(S->brute && !S->tr_shad && S->n_tris <= kBruteTris)
@@ -5929,6 +5971,12 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_shade<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 		else hipLaunchKernelGGL((k_shade<false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	}
+	else if(!kShadeFused && S->integrator == INT_PATH && S->path_samples <= 1 && !S->do_ao && !S->caus_map && !S->gather_on && !S->show_map &&
+	        S->n_photons == 0 && !S->tree && !S->has_attr && !S->no_lean)
+	{
+		if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		else hipLaunchKernelGGL((k_shade<false, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	}
 	else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, kShadeFused>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	else hipLaunchKernelGGL((k_shade<false, false, kShadeFused>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
@@ -6032,6 +6080,11 @@ hipError_t yafamd_launch_nee(const DevScene *S, const DevNeeQueue *N, const DevP
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_nee<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 		else hipLaunchKernelGGL((k_nee<false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	}
+	else if(!S->do_ao && !S->tr_shad && !S->has_mesh_light && !S->no_lean)
+	{
+		if(S->small_tables) hipLaunchKernelGGL((k_nee<true, false, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		else hipLaunchKernelGGL((k_nee<false, false, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	}
 	else if(S->small_tables) hipLaunchKernelGGL((k_nee<true, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	else hipLaunchKernelGGL((k_nee<false, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);

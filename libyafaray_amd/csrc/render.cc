@@ -625,7 +625,7 @@ bool GpuRenderer::upload(HostScene &hs)
 		// the treelet and the stack share the workgroup's LDS: clamp the treelet so that k_trace still
 		// launches — 64 KB per workgroup, the launch limit
 		const size_t stack_b = (size_t)d.lds_stack * yafamd_trace_block() * 4, lds_max = 64 * 1024;
-		const int fit = stack_b >= lds_max ? 0 : (int)((lds_max - stack_b) / 128);
+		const int fit = stack_b >= lds_max ? 0 : (int)((lds_max - stack_b) / 144);   // 144 B per staged node (kernels.hip kTopStride)
 		if(d.lds_top > fit)
 		{
 			log_.warning("GPU: YAFARAY_AMD_LDS_TOP=" + std::to_string(d.lds_top) + " does not fit the trace workgroup's LDS; using " +
@@ -635,7 +635,7 @@ bool GpuRenderer::upload(HostScene &hs)
 	}
 	{
 		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy or top treelet))
-		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : (size_t)d.lds_top * 128);
+		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : (size_t)d.lds_top * 144);
 		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, d.node_f4 == 8 ? 1 : 0, dyn));
 		if(const char *e = getenv("YAFARAY_AMD_TRACE_GRID")) d.trace_grid = std::max(1, atoi(e));
 		// a whole number of workgroups per queue segment
@@ -694,6 +694,8 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.prim_ng = (const float4 *)d.prim_ng.p;
 	S.mats = (const DevMaterial *)d.mats.p;
 	S.lights = (const DevLight *)d.lights.p;
+	S.has_mesh_light = 0;
+	for(const DevLight &L : d.host_lights) S.has_mesh_light |= L.type == LIGHT_MESH ? 1 : 0;
 	S.mesh_tris = (const float4 *)d.mesh_tris.p;
 	S.mesh_cdf = (const float *)d.mesh_cdf.p;
 	S.faure = (const uint8_t *)d.faure.p;
@@ -1789,6 +1791,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	S.nee_pm16 = 0;
 	if(const char *e = std::getenv("YAFARAY_AMD_NEE_PM16"); e && *e == '1') S.nee_pm16 = 1;   // tests: the 16-B request word
 	if(const char *e = std::getenv("YAFARAY_AMD_W_LIVE"); e && *e == '1') S.w_live = 1;        // tests: the 16-B throughput record
+	S.no_lean = 0;
+	if(const char *e = std::getenv("YAFARAY_AMD_SHADE_LEAN"); e && *e == '0') S.no_lean = 1;   // tests: the general k_shade
 	int path_grid = 0;
 	if(!lpc_on)
 	{
