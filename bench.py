@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size parity checks")
     ap.add_argument("--parity-rows", type=int, default=12, help="rows of the RR-off bit-exact band")
+    ap.add_argument("--lights", type=int, default=1, help="C2 variant: 2 or 3 lights (scenes.with_extra_lights); multi-light path tracing "
+                    "runs the one-thread light-pick count run per pass (YAFARAY_AMD_LIGHT_PICK=hash skips it)")
     ap.add_argument("--flush-steps", type=int, default=2, help="frames timed through yafaray_render with the film flush (ms_per_step_flush)")
     ap.add_argument("--members-per-gpu", type=int, default=1,
                     help="device-group members per GPU (experiment: several logical members on one GPU run on concurrent streams)")
@@ -81,13 +83,15 @@ def workload_name(a, W, H):
                 f"{W}x{H}x{a.spp}spp (photon map rebuilt every step)")
     return (f"C2 Cornell PathIntegrator depth {a.bounces}, {W}x{H}x{a.spp}spp"
             + (", RR off" if a.no_rr else ", RR on (reference default)")
+            + (f", {a.lights} lights" if a.lights > 1 else "")
             + ("" if a.scene == "cornell" else " + 1M-triangle sphere (C4)"))
 
 
 def pmc_config(a, W, H):
     """Key of profiles/pmc_<key>.json (tools/pmc_all.sh): one workload, one kernel source."""
     return f"{a.scene}-{W}x{H}x{a.spp}-b{a.bounces}-rr{int(not a.no_rr)}-chunk{a.chunk}" + (
-        f"-ph{a.photons}" if a.scene == "photon" else "") + (f"-fg{a.fg}" if a.scene == "photon" and a.fg else "")
+        f"-ph{a.photons}" if a.scene == "photon" else "") + (f"-fg{a.fg}" if a.scene == "photon" and a.fg else "") + (
+        f"-l{a.lights}" if getattr(a, "lights", 1) > 1 else "")
 
 
 def kernels_src_sha1():
@@ -245,6 +249,8 @@ def main():
             spec = dataclasses.replace(spec, render=dataclasses.replace(spec.render, pm_final_gather=True, fg_samples=a.fg))
     else:
         spec = scenes.cornell(a.width, a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
+    if a.lights > 1:
+        spec = scenes.with_extra_lights(spec, a.lights)
     yi = Y.Interface()
     scenes.apply(spec, yi)
     yi.L.yafaray_amd_setChunkSlots(yi.h, a.chunk)
@@ -318,17 +324,23 @@ def main():
 
     cpu, parity = None, None
     group = None
-    if n_gpus > 1:
+    grouped = n_gpus > 1 or mpg > 1
+    if grouped:
         # a multi-GPU speed never goes out without its parity verdict (--no-parity does not apply):
         # the group's frame against a one-member render, and an RR-off group frame against the oracle
-        # around the band boundaries (group_parity)
+        # around the band boundaries (group_parity).  --members-per-gpu > 1 on one GPU rehearses the
+        # same code path (logical members, one stream each) and is checked the same way
         report = yi.group_report()
         film = yi.film() if rank == 0 else None
         rr_off = scenes.cornell(W, H, spp=a.spp, bounces=a.bounces, rr=False) if a.scene == "cornell" else None
-        parity = group_parity(Y, spec, film, report, n_gpus, devices=None if world > 1 else list(range(n_gpus)), rr_off_spec=rr_off,
+        members = n_gpus * mpg if world <= 1 else world
+        devices = None if world > 1 else [d for d in range(n_gpus) for _ in range(mpg)]
+        t_gp = time.perf_counter()
+        parity = group_parity(Y, spec, film, report, members, devices=devices, rr_off_spec=rr_off,
                               chunk=a.chunk, world=world, rank=rank, dist=dist)
+        parity["check_seconds"] = round(time.perf_counter() - t_gp, 2)
         group = report
-    if rank == 0 and n_gpus == 1:
+    if rank == 0 and not grouped:
         if not a.no_cpu_baseline:
             cpu, band = cpu_baseline(spec, a)
             if not a.no_parity and band is not None:
@@ -390,7 +402,7 @@ def main():
     yi.close()
     if world > 1:
         dist.destroy_process_group()
-    if parity is not None and n_gpus > 1 and not parity.get("pass", False):
+    if parity is not None and grouped and not parity.get("pass", False):
         print("bench: multi-GPU parity FAILED (see the line's parity object)", file=sys.stderr)
         sys.exit(3)
 

@@ -299,6 +299,16 @@ def cornell(width=1920, height=1080, spp=64, bounces=8, rr=False, integrator="pa
     return SceneSpec(verts, tris, tri_mat, mats, [light], cam, rend, Background((0.0, 0.0, 0.0), 1.0), b.objects)
 
 
+def with_extra_lights(spec, n):
+    """The scene with n lights: its own light, then a warm point bulb and a second (smaller, bluish) area
+    light off-centre under the ceiling (multi-light tests; bench.py --lights)."""
+    import dataclasses
+    extra = [Light("bulb", type="pointlight", color=(1.0, 0.85, 0.7), power=1.2, from_=(0.45, -0.3, 1.5)),
+             Light("panel", type="arealight", color=(0.6, 0.7, 1.0), power=2.5, corner=(-0.8, 0.5, 1.9),
+                   point1=(-0.8, 0.8, 1.9), point2=(-0.5, 0.5, 1.9), samples=1)]
+    return dataclasses.replace(spec, lights=list(spec.lights) + extra[:max(0, n - 1)])
+
+
 def cornell_meshlight(width=96, height=72, spp=4, bounces=4, rr=False, integrator="pathtracing", shape="panel",
                       double_sided=False, samples=2, keep_area=False, power=3.0, **kw) -> SceneSpec:
     """The Cornell box lit by a meshlight (light_object_light.cc): an emitting object with a light_mat

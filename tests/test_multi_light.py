@@ -35,12 +35,9 @@ def _ulp(a, b):
 
 
 def with_lights(spec, n):
-    """The Cornell box with n lights: its area light, a warm point bulb and a second (smaller,
-    bluish) area light off-centre under the ceiling."""
-    extra = [scenes.Light("bulb", type="pointlight", color=(1.0, 0.85, 0.7), power=1.2, from_=(0.45, -0.3, 1.5)),
-             scenes.Light("panel", type="arealight", color=(0.6, 0.7, 1.0), power=2.5, corner=(-0.8, 0.5, 1.9),
-                          point1=(-0.8, 0.8, 1.9), point2=(-0.5, 0.5, 1.9), samples=1)]
-    return dataclasses.replace(spec, lights=spec.lights + extra[:n - 1])
+    """The Cornell box with n lights (scenes.with_extra_lights: its area light, a warm point bulb and a
+    second, smaller, bluish area light off-centre under the ceiling)."""
+    return scenes.with_extra_lights(spec, n)
 
 
 @pytest.mark.parametrize("n", [2, 3])
