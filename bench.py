@@ -60,7 +60,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=None, help="default 64 (C2/C4), 1 (C5 photon)")
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--no-rr", action="store_true", help="Russian roulette off (bit-parity variant)")
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere", "photon"])
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "sphere", "photon", "meshlight"],
+                    help="meshlight: C2 with a 10082-face double-sided meshlight sphere next to the area light (frame time of the meshlight BVH)")
     ap.add_argument("--photons", type=int, default=10_000_000, help="C5: diffuse photons")
     ap.add_argument("--fg", type=int, default=0, help="C5 variant: PhotonIntegrator final gathering with this many fg_samples (0: off, as C5)")
     ap.add_argument("--chunk", type=int, default=1 << 27)
@@ -84,7 +85,8 @@ def workload_name(a, W, H):
     return (f"C2 Cornell PathIntegrator depth {a.bounces}, {W}x{H}x{a.spp}spp"
             + (", RR off" if a.no_rr else ", RR on (reference default)")
             + (f", {a.lights} lights" if a.lights > 1 else "")
-            + ("" if a.scene == "cornell" else " + 1M-triangle sphere (C4)"))
+            + {"cornell": "", "sphere": " + 1M-triangle sphere (C4)",
+               "meshlight": " + 10082-face double-sided meshlight sphere"}[a.scene])
 
 
 def pmc_config(a, W, H):
@@ -247,6 +249,9 @@ def main():
         spec = scenes.cornell_photon(a.width, a.height, spp=a.spp, photons=a.photons)
         if a.fg:
             spec = dataclasses.replace(spec, render=dataclasses.replace(spec.render, pm_final_gather=True, fg_samples=a.fg))
+    elif a.scene == "meshlight":
+        spec = scenes.cornell_meshlight(a.width, a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr, shape="bigsphere",
+                                        double_sided=True, keep_area=True, samples=1)
     else:
         spec = scenes.cornell(a.width, a.height, spp=a.spp, bounces=a.bounces, rr=not a.no_rr)
     if a.lights > 1:

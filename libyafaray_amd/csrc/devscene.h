@@ -142,6 +142,10 @@ struct DevLight
 	// photon_only (Light::photonOnly): the light shoots photons but the integrators do not see it
 	// (render_view.cc:83-91) — it sits after the DevScene::n_lights visible lights and has no NEE entries
 	uint32_t photon_only;
+	// meshlight: its faces' own BVH2 (the reference's per-light kd-tree, light_object_light.cc:62-70) for the
+	// material-sampled rays — nodes [bvh_node0, ...) of DevScene::mesh_nodes, triangle records from
+	// bvh_tri0 of DevScene::mesh_btris (leaf order, the face index in e1.w); bvh_depth 0: test every face
+	uint32_t bvh_node0, bvh_tri0, bvh_depth, pad1;
 };
 
 struct DevCamera
@@ -188,6 +192,8 @@ struct DevScene
 	// distribution's normalised cdf (sample_pdf1d.h)
 	const float4 *mesh_tris;
 	const float *mesh_cdf;
+	const float4 *mesh_nodes;      // meshlight BVH2 nodes (4 float4 each, DevLight::bvh_node0)
+	const float4 *mesh_btris;      // meshlight BVH2 triangle records (3 float4 each, leaf order)
 
 	DevCamera cam;
 

@@ -1036,8 +1036,28 @@ bool Scene::meshLightFaces(const std::string &name, DevLight &L, HostScene &hs)
 	for(float &e : cdf) e /= integral;
 	hs.mesh_cdf.insert(hs.mesh_cdf.end(), cdf.begin(), cdf.end());
 	L.area = static_cast<float>(total);
-	if(nt > 4096)
-		log.warning("Light '" + name + "': " + std::to_string(nt) + " faces; the material-sampled rays test every face of the light");
+	// the light's own BVH2 over its faces (the reference's per-light kd-tree, light_object_light.cc:62-70):
+	// the material-sampled rays find the closest face through it instead of testing every face
+	L.bvh_depth = 0;
+	const char *mb = std::getenv("YAFARAY_AMD_MESHLIGHT_BVH");   // "0": test every face (A/B, tests)
+	if(nt > 8 && !(mb && *mb == '0'))
+	{
+		BvhInput bi;
+		bi.verts = o.verts.data();
+		bi.tris = o.tris.data();
+		bi.n_tris = (int)nt;
+		bi.width = 2;
+		const BvhOutput bo = buildBvh(bi, 4, 1);
+		if(bo.depth > 0 && bo.depth <= 60)
+		{
+			L.bvh_node0 = (uint32_t)(hs.mesh_nodes.size() / 16);
+			L.bvh_tri0 = (uint32_t)(hs.mesh_btris.size() / 12);
+			L.bvh_depth = (uint32_t)bo.depth;
+			hs.mesh_nodes.insert(hs.mesh_nodes.end(), bo.nodes.begin(), bo.nodes.end());
+			hs.mesh_btris.insert(hs.mesh_btris.end(), bo.tris.begin(), bo.tris.end());
+		}
+		else log.warning("Light '" + name + "': the BVH over its " + std::to_string(nt) + " faces is too deep; every face is tested");
+	}
 	return true;
 }
 

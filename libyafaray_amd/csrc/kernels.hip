@@ -1991,6 +1991,72 @@ __device__ __forceinline__ bool lightIllumSample(const DevScene &S, const DevLig
 	return true;
 }
 
+// The closest face of a meshlight along (p, dir) with t >= tmin through the light's BVH2 (its faces'
+// own tree, as the reference's per-light kd-tree, light_object_light.cc:62-70, 186-204): the same exact
+// triangle test and the same answer as testing every face in creation order — the smallest t, equal t
+// resolved to the lowest face index; boxes are culled conservatively (padded at build time, relative
+// slack on t).  Returns the face index or -1.  A private per-lane stack (the tree is <= 60 levels deep).
+__device__ int meshLightClosest(const DevScene &S, const DevLight &L, V3 o, V3 d, float tmin)
+{
+	const float4 *nodes = S.mesh_nodes + 4 * (size_t)L.bvh_node0;
+	const float4 *tris = S.mesh_btris + 3 * (size_t)L.bvh_tri0;
+	V3 dd = d;
+	if(fabsf(dd.x) < 1e-20f) dd.x = copysignf(1e-20f, dd.x);
+	if(fabsf(dd.y) < 1e-20f) dd.y = copysignf(1e-20f, dd.y);
+	if(fabsf(dd.z) < 1e-20f) dd.z = copysignf(1e-20f, dd.z);
+	const V3 id = v3(rcpExact(dd.x), rcpExact(dd.y), rcpExact(dd.z));
+	const float box_t0 = tmin - 1e-3f * (1.f + fabsf(tmin));
+	float t_best = __builtin_huge_valf();
+	int best = -1;
+	int stk[64];
+	int sp = 0, node = 0;
+	for(;;)
+	{
+		const float4 *np = nodes + 4 * node;
+		const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
+		bool h0, h1;
+		float tn0, tn1;
+		boxPair(n0, n1, n2, o, id, box_t0, slack_t, h0, h1, tn0, tn1);
+		const int c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y), k0 = __float_as_int(n3.z), k1 = __float_as_int(n3.w);
+#pragma unroll
+		for(int side = 0; side < 2; ++side)
+		{
+			const bool h = side ? h1 : h0;
+			const int c = side ? c1 : c0, k = side ? k1 : k0;
+			if(!h || c >= 0 || k == 0) continue;
+			for(int q = ~c; q < ~c + k; ++q)
+			{
+				const float4 ta = tris[3 * q], tb = tris[3 * q + 1], tc = tris[3 * q + 2];
+				const float t = triTest(ta, tb, tc, o, d, t_best);
+				const int face = __float_as_int(tb.w);
+				if(t != -1.f && t >= tmin && (t < t_best || (t == t_best && face < best)))
+				{
+					t_best = t;
+					best = face;
+				}
+			}
+		}
+		const bool i0 = h0 && c0 >= 0, i1 = h1 && c1 >= 0;
+		int next = -1;
+		if(i0 && i1)
+		{
+			const bool first0 = tn0 <= tn1;
+			next = first0 ? c0 : c1;
+			stk[sp++] = first0 ? c1 : c0;
+		}
+		else if(i0) next = c0;
+		else if(i1) next = c1;
+		if(next < 0)
+		{
+			if(sp == 0) break;
+			next = stk[--sp];
+		}
+		node = next;
+	}
+	return best;
+}
+
 // Light::intersect of areaLightSampleMaterial's material-sampled ray (origin p, direction dir, tmin
 // b_tmin): the light's pdf and the shadow ray's t (< 0: unbounded).  Area light: light_area.cc:137-151.
 // Mesh light: light_object_light.cc:183-201 — the closest face (the light's own kd-tree, faces with
@@ -2004,15 +2070,17 @@ __device__ __forceinline__ bool lightMatHit(const DevScene &S, const DevLight &L
 		float t_best = __builtin_huge_valf();
 		int best = -1;
 		const float4 *tr = S.mesh_tris + (size_t)kMeshTriF4 * L.mesh0;
-		for(int k = 0; k < (int)L.mesh_n; ++k)
-		{
-			const float th = triTest(tr[kMeshTriF4 * k], tr[kMeshTriF4 * k + 1], tr[kMeshTriF4 * k + 2], p, dir, t_best);
-			if(th != -1.f && th >= b_tmin && th < t_best)
+		if(L.bvh_depth > 0) best = meshLightClosest(S, L, p, dir, b_tmin);
+		else
+			for(int k = 0; k < (int)L.mesh_n; ++k)
 			{
-				t_best = th;
-				best = k;
+				const float th = triTest(tr[kMeshTriF4 * k], tr[kMeshTriF4 * k + 1], tr[kMeshTriF4 * k + 2], p, dir, t_best);
+				if(th != -1.f && th >= b_tmin && th < t_best)
+				{
+					t_best = th;
+					best = k;
+				}
 			}
-		}
 		if(best < 0) return false;
 		const V3 n = xyz(tr[kMeshTriF4 * best + 6]);
 		float cos_angle = -dot(dir, n);

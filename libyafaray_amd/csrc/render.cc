@@ -264,6 +264,7 @@ struct GpuRenderer::Impl
 	Buf cph_pos, cph_dir, cph_colb, cpk_nodes;   // caustic photon map + kd-tree
 	Buf tile_rank, pfilm;                        // tile order ranks; partial film of the per-tile callbacks
 	Buf mesh_tris, mesh_cdf;                     // meshlight faces and area distributions
+	Buf mesh_nodes, mesh_btris;                  // meshlight BVH2s (nodes, triangle records)
 	int c_photons = 0, c_paths = 0, c_depth = 0;
 	Buf ph_ray_o, ph_ray_d, ph_pcol, ph_alive0, ph_alive1, ph_n_alive, dep_a, dep_b, dep_c, dep_flag, ph_scan, ph_total;
 	Buf ph_pos, ph_dir, ph_colb, pk_nodes, pk_stack;
@@ -362,7 +363,7 @@ struct GpuRenderer::Impl
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
-		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf}) b->release();
+		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris}) b->release();
 		for(int m = 0; m < 3; ++m)
 			for(Buf *b : {&kd_pos[m], &kd_dir[m], &kd_colb[m]}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
@@ -541,10 +542,11 @@ bool GpuRenderer::upload(HostScene &hs)
 	d.host_lights = hs.lights;
 	if(!hs.mesh_cdf.empty())
 	{
-		if(!allocCopy(log_, d.mesh_tris, hs.mesh_tris.data(), hs.mesh_tris.size()) || !allocCopy(log_, d.mesh_cdf, hs.mesh_cdf.data(), hs.mesh_cdf.size()))
+		if(!allocCopy(log_, d.mesh_tris, hs.mesh_tris.data(), hs.mesh_tris.size()) || !allocCopy(log_, d.mesh_cdf, hs.mesh_cdf.data(), hs.mesh_cdf.size()) ||
+		   !allocCopy(log_, d.mesh_nodes, hs.mesh_nodes.data(), hs.mesh_nodes.size()) || !allocCopy(log_, d.mesh_btris, hs.mesh_btris.data(), hs.mesh_btris.size()))
 			return false;
 	}
-	else for(Buf *b : {&d.mesh_tris, &d.mesh_cdf}) b->release();
+	else for(Buf *b : {&d.mesh_tris, &d.mesh_cdf, &d.mesh_nodes, &d.mesh_btris}) b->release();
 	d.has_attr = hs.has_attr;
 	d.n_textures = (int)hs.textures.size();
 	if(hs.has_attr)
@@ -697,6 +699,8 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.has_mesh_light = 0;
 	for(const DevLight &L : d.host_lights) S.has_mesh_light |= L.type == LIGHT_MESH ? 1 : 0;
 	S.mesh_tris = (const float4 *)d.mesh_tris.p;
+	S.mesh_nodes = (const float4 *)d.mesh_nodes.p;
+	S.mesh_btris = (const float4 *)d.mesh_btris.p;
 	S.mesh_cdf = (const float *)d.mesh_cdf.p;
 	S.faure = (const uint8_t *)d.faure.p;
 	S.faure_bytes = d.faure_bytes;

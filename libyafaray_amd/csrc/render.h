@@ -35,6 +35,8 @@ struct HostScene
 	std::vector<int> light_name_order;   // every light by name (the photon maps' light lists, render_view.cc:93-111)
 	std::vector<float> mesh_tris;        // meshlight faces: kMeshTriF4 float4 each (DevScene::mesh_tris)
 	std::vector<float> mesh_cdf;         // their area distributions' normalised cdf, per light
+	std::vector<float> mesh_nodes;       // each meshlight's BVH2 over its faces (16 floats per node)
+	std::vector<float> mesh_btris;       // ... and its triangle records in leaf order (12 floats each)
 	int n_prims = 0;
 	// surface attributes / textures / shader nodes (texeval.h), only when has_attr
 	bool has_attr = false;

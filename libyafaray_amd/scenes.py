@@ -314,14 +314,15 @@ def cornell_meshlight(width=96, height=72, spp=4, bounces=4, rr=False, integrato
     """The Cornell box lit by a meshlight (light_object_light.cc): an emitting object with a light_mat
     material whose faces the light samples.  shape "panel": a 0.6 x 0.6 quad (2 faces) under the
     ceiling facing down; "sphere": a low-poly UV sphere (72 faces of different areas) hanging in the
-    box.  keep_area: the box's area light stays as a second light."""
+    box; "bigsphere": the same sphere with 71 x 71 x 2 = 10082 faces (the meshlight BVH case).
+    keep_area: the box's area light stays as a second light."""
     s = cornell(width, height, spp=spp, bounces=bounces, rr=rr, integrator=integrator, **kw)
     if shape == "panel":
         lv, lt = _quad((-0.3, -0.3, 1.9), (-0.3, 0.3, 1.9), (0.3, 0.3, 1.9), (0.3, -0.3, 1.9))
         lv = np.asarray(lv, np.float32)
         lt = np.asarray(lt, np.int32)
     else:
-        lv, lt = uv_sphere(6, center=(0.35, -0.3, 1.45), r=0.18)
+        lv, lt = uv_sphere(71 if shape == "bigsphere" else 6, center=(0.35, -0.3, 1.45), r=0.18)
     mats = list(s.materials) + [Material("lamp", type="light_mat", color=(1.0, 0.9, 0.75), power=power, double_sided=double_sided)]
     v0 = len(s.verts)
     verts = np.concatenate([s.verts, np.asarray(lv, np.float32)])

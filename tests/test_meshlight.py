@@ -10,7 +10,7 @@ Checked against the oracle's restatement (oracle/yafcpu.cc meshSampleSurface / m
 meshIntersect): DirectLight and PathIntegrator (Russian roulette off) within 4 ULP (0 expected), a
 single-sided panel and a double-sided 72-face sphere, alone and next to the box's area light (two
 lights: the one-thread light-pick counter); the PhotonIntegrator's photon map (counts) and image,
-with and without final gathering.  Parity is pinned by the restatement only (no
+with and without final gathering; a 10082-face double-sided sphere through the light's BVH2.  Parity is pinned by the restatement only (no
 reference golden images)."""
 import dataclasses
 
@@ -70,6 +70,32 @@ def test_meshlight_photon_mapping_matches_oracle(product, oracle_built, fg):
     assert np.array_equal(w, ow)
     u = _ulp(rgba, orgba)
     assert u.max() <= 4, f"{(u > 4).sum()} values > 4 ULP"
+
+
+BIG = {
+    "dl-bigsphere-2sided": dict(integrator="directlighting", double_sided=True),
+    "pt-bigsphere-2sided-and-area": dict(integrator="pathtracing", double_sided=True, keep_area=True),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(BIG))
+def test_meshlight_bvh_10k_faces_matches_oracle(product, oracle_built, monkeypatch, case):
+    """A 10082-face double-sided meshlight: the material-sampled rays find the closest face through the
+    light's BVH2 (the oracle tests every face, as the reference's kd-tree answers); within 4 ULP of the
+    oracle, and bit-identical to the per-face loop (YAFARAY_AMD_MESHLIGHT_BVH=0)."""
+    spec = scenes.cornell_meshlight(48, 36, spp=2, bounces=3, rr=False, shape="bigsphere", **BIG[case])
+    assert spec.objects[-1].nt > 10000
+    rgba, w, st = product.render_spec(spec)
+    # one oracle thread: with two lights the path tracer's light pick is the one-thread counter
+    orgba, ow, _ = oracle_built.OracleScene(spec, threads=1).render()
+    assert np.array_equal(w, ow)
+    u = _ulp(rgba, orgba)
+    assert u.max() <= 4, f"{(u > 4).sum()} values > 4 ULP"
+    assert rgba[..., :3].mean() > 0.0
+    monkeypatch.setenv("YAFARAY_AMD_MESHLIGHT_BVH", "0")
+    lin, lw, _ = product.render_spec(spec)
+    assert np.array_equal(lin.view(np.uint32), rgba.view(np.uint32)) and np.array_equal(lw, w)
 
 
 @pytest.mark.gpu
