@@ -15,7 +15,8 @@ import dataclasses
 import numpy as np
 import pytest
 
-from libyafaray_amd import filmfile, scenes
+import filmfile
+from libyafaray_amd import scenes
 
 pytestmark = pytest.mark.gpu
 

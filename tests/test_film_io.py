@@ -14,7 +14,8 @@ import os
 import numpy as np
 import pytest
 
-from libyafaray_amd import filmfile, scenes
+import filmfile
+from libyafaray_amd import scenes
 
 
 def _spec(**kw):
