@@ -4862,6 +4862,27 @@ constexpr int kWalkPerSeg = YAF_WALK_PER_SEG;   // walk workgroups per queue seg
 // is tested directly (its photon lies beyond that plane, so the reference's pop-time rejection and
 // the distance test agree).  The accepted photons go to this request's log lg[0 ..) in pairs
 // (16-byte stores; the first `cap`); returns how many were accepted.
+#ifndef YAF_WALK_PACK
+#define YAF_WALK_PACK 0
+#endif
+#if YAF_WALK_PACK
+// The walk's slots as 16-bit keys, two per VGPR: the bfloat16 bits of each distance rounded UP (for
+// non-negative floats the bits are monotone, so the k-th smallest key bounds the k-th smallest
+// distance from above).  The walk then prunes and logs with a bound >= the reference's max_d2 — a
+// superset log in the same visit order, which the replay filters with the exact test (as the
+// bounded walk's, pkWalkBound) — in 32 VGPRs instead of 64.  Insertion of key x into the ascending
+// slots: slot i <- max(slot i-1, min(slot i, x)) for every pair at once (alignbit + packed min / max).
+typedef unsigned short walk_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t walkKey(float d2) { return (__float_as_uint(d2) + 0xffffu) >> 16; }
+__device__ __forceinline__ uint32_t pkMaxU16(uint32_t a, uint32_t b)
+{
+	return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(walk_u16x2, a), __builtin_bit_cast(walk_u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pkMinU16(uint32_t a, uint32_t b)
+{
+	return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(walk_u16x2, a), __builtin_bit_cast(walk_u16x2, b)));
+}
+#endif
 __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, float max_d2, uint2 *lg, uint32_t cap, uint32_t *stk,
                                            uint32_t &visits)
 {
@@ -4870,9 +4891,17 @@ __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, floa
 	// stay live across every walk — 64 more VGPRs)
 	int pinned = kWalkK - k;
 	asm volatile("" : "+s"(pinned));
+#if YAF_WALK_PACK
+	constexpr uint32_t kEmpty = 0x7f80u;   // +inf
+	uint32_t kp[kWalkK / 2];
+#pragma unroll
+	for(int i = 0; i < kWalkK / 2; ++i)
+		kp[i] = ((2 * i < pinned) ? 0u : kEmpty) | (((2 * i + 1 < pinned) ? 0u : kEmpty) << 16);
+#else
 	float kd[kWalkK];
 #pragma unroll
 	for(int i = 0; i < kWalkK; ++i) kd[i] = (i < pinned) ? -1.f : __builtin_huge_valf();
+#endif
 	uint32_t n_acc = 0;
 	uint2 pend = make_uint2(0u, 0u);
 	uint32_t curr = 0;
@@ -4913,10 +4942,19 @@ __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, floa
 			++n_acc;
 			// insert (the largest slot drops out): below k accepted this fills a +inf slot (the heap
 			// grows); from then on it removes the top and adds dist_2 (pop_heap + push_heap)
+#if YAF_WALK_PACK
+			const uint32_t x = walkKey(dist_2), xx = x | (x << 16);
+#pragma unroll
+			for(int i = kWalkK / 2 - 1; i > 0; --i)
+				kp[i] = pkMaxU16(__builtin_amdgcn_alignbit(kp[i], kp[i - 1], 16u), pkMinU16(kp[i], xx));
+			kp[0] = pkMaxU16(kp[0] << 16, pkMinU16(kp[0], xx));
+			max_d2 = fminf(radius2, __uint_as_float(kp[kWalkK / 2 - 1] & 0xffff0000u));
+#else
 #pragma unroll
 			for(int i = kWalkK - 1; i > 0; --i) kd[i] = __builtin_amdgcn_fmed3f(kd[i - 1], kd[i], dist_2);
 			kd[0] = fminf(kd[0], dist_2);
 			max_d2 = fminf(radius2, kd[kWalkK - 1]);
+#endif
 		}
 		// pop the next far child the current radius still reaches
 		bool more = false;

@@ -267,6 +267,9 @@ __global__ void k_seg_of(uint32_t *seg_of, uint32_t n, const Split *splits)
 #ifndef YAF_PART_NT
 #define YAF_PART_NT 1
 #endif
+#ifndef YAF_PART_PRELOAD
+#define YAF_PART_PRELOAD 1
+#endif
 constexpr int kPartItems = YAF_PART_ITEMS;
 constexpr uint32_t kPartThreads = 256;
 constexpr uint32_t kPartTile = kPartThreads * kPartItems;
@@ -326,9 +329,30 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 	if(t == 0) s_seg0 = segOfPos(base, A.n, A.level);
 	__syncthreads();
 	const uint32_t seg0 = s_seg0, n_seg = 1u << A.level;
+#if YAF_PART_PRELOAD
+	// the tile's splits staged with the segment starts, and every record loaded before the first flag is
+	// computed: the eight 16-B loads of a thread are in flight together (computing each flag right after
+	// its load kept one HBM round trip per item in the dependence chain)
+	__shared__ Split s_split[kPartSegs];
+	if(t < kPartSegs)
+	{
+		const bool ok = seg0 + t < n_seg;
+		s_start[t] = ok ? A.segs[seg0 + t].start : 0xffffffffu;
+		if(ok) s_split[t] = A.splits[seg0 + t];
+	}
+	uint4 r[kPartItems];
+#pragma unroll
+	for(int i = 0; i < kPartItems; ++i)
+	{
+		const uint32_t e = base + (uint32_t)i * kPartThreads + t;
+		r[i] = e < A.n ? in[e] : make_uint4(0u, 0u, 0u, 0u);
+	}
+	__syncthreads();
+#else
 	if(t < kPartSegs) s_start[t] = seg0 + t < n_seg ? A.segs[seg0 + t].start : 0xffffffffu;
 	__syncthreads();
 	uint4 r[kPartItems];
+#endif
 	uint32_t so[kPartItems], pre[kPartItems];
 	bool f[kPartItems];
 	for(int i = 0; i < kPartItems; ++i)
@@ -336,15 +360,23 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 		const uint32_t e = base + (uint32_t)i * kPartThreads + t;
 		f[i] = false;
 		so[i] = 0;
+#if !YAF_PART_PRELOAD
 		r[i] = make_uint4(0u, 0u, 0u, 0u);
+#endif
 		if(e < A.n)
 		{
+#if !YAF_PART_PRELOAD
 			r[i] = in[e];
+#endif
 			uint32_t j = 0;
 			while(j + 1u < kPartSegs && s_start[j + 1u] <= e) ++j;
 			so[i] = seg0 + j;
 			PK_GUARD(so[i] < n_seg && A.segs[so[i]].start <= e && e < A.segs[so[i]].end, so[i]);
+#if YAF_PART_PRELOAD
+			const Split sp = s_split[j];
+#else
 			const Split sp = A.splits[so[i]];
+#endif
 			f[i] = leftOf(r[i], sp.axis, sp.med_key, sp.med_idx);
 		}
 		const uint64_t b = __ballot(f[i]);
@@ -430,7 +462,11 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 		const uint32_t e = base + (uint32_t)i * kPartThreads + t;
 		if(e >= A.n) continue;
 		const uint32_t s = so[i];
+#if YAF_PART_PRELOAD
+		const uint32_t start = s_start[s - seg0], split_el = s_split[s - seg0].split_el;
+#else
 		const uint32_t start = s_start[s - seg0], split_el = A.splits[s].split_el;
+#endif
 		const uint32_t left_before = excl + pre[i] - A.seg_left[s];
 		uint32_t np = f[i] ? start + left_before : split_el + ((e - start) - left_before);
 		PK_GUARD(np < A.n, np);
