@@ -72,6 +72,14 @@ __device__ __forceinline__ uint32_t orderKey(float f)
 	return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// the coordinate back from its orderable key (exact: the key keeps every bit of the float, except that
+// -0 became +0 — callers load the coordinate itself for a zero key)
+__device__ __forceinline__ float keyCoord(uint32_t k)
+{
+	return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+constexpr uint32_t kZeroKey = 0x80000000u;
+
 // "left of the median" in the (coordinate, index) order of `axis`
 __device__ __forceinline__ bool leftOf(const uint4 r, uint32_t axis, uint32_t med_key, uint32_t med_idx)
 {
@@ -269,6 +277,9 @@ __global__ void k_seg_of(uint32_t *seg_of, uint32_t n, const Split *splits)
 #endif
 #ifndef YAF_PART_PRELOAD
 #define YAF_PART_PRELOAD 1
+#endif
+#ifndef YAF_SUB_FAST
+#define YAF_SUB_FAST 1
 #endif
 constexpr int kPartItems = YAF_PART_ITEMS;
 constexpr uint32_t kPartThreads = 256;
@@ -528,6 +539,9 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 	__shared__ uint32_t cb[kSub];              // first child segment of splitting segment s
 	__shared__ uint16_t seg_of[kSub];          // segment of entry position e (kNone once a leaf)
 	__shared__ uint32_t wsum[4][kSubWaves];    // per-wave ballot totals: lists 0-2, splitting segments
+#if YAF_SUB_FAST
+	__shared__ uint32_t leaf_node[kSub];       // node of the leaf at entry position e
+#endif
 	const Seg g = segs[blockIdx.x];
 	uint32_t m = g.end - g.start;
 	PK_GUARD(m >= 1 && m <= blockDim.x && blockDim.x <= (uint32_t)kSub && g.end <= n, m);
@@ -563,6 +577,11 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 			const LSeg l = lsegs[cs][t];
 			if(l.end - l.start == 1)
 			{
+#if YAF_SUB_FAST
+				// the leaf's node record and payload are written after the last level (leaf_node, below): its
+				// gathers then overlap with every other leaf's instead of stalling the level they finish in
+				leaf_node[l.start] = l.node;
+#else
 				uint32_t idx = buf[cur][0][l.start].w;
 				PK_GUARD(idx < n, idx);
 				const float4 ph = pos[idx];
@@ -578,6 +597,7 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 					kp.kcolb[tag] = kp.colb[idx];
 				}
 				nodes[nd] = make_uint4(__float_as_uint(ph.x), __float_as_uint(ph.y), __float_as_uint(ph.z), 3u | (tag << 2));
+#endif
 				lsplit[t] = {3u, 0u, 0u, 0u};
 			}
 			else
@@ -587,7 +607,13 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 				PK_GUARD(se > l.start && l.end <= m, se);
 				uint4 med = buf[cur][axis][se];
 				PK_GUARD(med.w < n, med.w);
+#if YAF_SUB_FAST
+				// the split position from the median's key (no dependent load per level; a zero key may be -0)
+				const uint32_t mk = keyOf(med, axis);
+				const float split_pos = mk != kZeroKey ? keyCoord(mk) : coordOf(pos[med.w], axis);
+#else
 				const float split_pos = coordOf(pos[med.w], axis);
+#endif
 				const uint32_t right = l.node + 2u * (se - l.start);
 				uint32_t nd = l.node;
 				PK_GUARD(right < 2 * n - 1, nd);
@@ -668,7 +694,11 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 		{
 			const LSeg l = lsegs[cs][t];
 			const Split ls = lsplit[t];
+#if YAF_SUB_FAST
+			const float split_pos = ls.med_key != kZeroKey ? keyCoord(ls.med_key) : coordOf(pos[ls.med_idx], (int)ls.axis);
+#else
 			const float split_pos = coordOf(pos[ls.med_idx], (int)ls.axis);
+#endif
 			uint32_t c0 = cb[t];
 			PK_GUARD(c0 + 1 < 2 * n_split, c0);
 			LSeg lo = l, hi = l;
@@ -691,6 +721,28 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 		++level;
 		__syncthreads();
 	}
+#if YAF_SUB_FAST
+	// every entry position is one leaf (a subtree of m photons has m leaves): its record sits at that
+	// position of the lists, which leaves never move
+	if(act)
+	{
+		uint32_t idx = buf[cur][0][t].w;
+		PK_GUARD(idx < n, idx);
+		const float4 ph = pos[idx];
+		uint32_t nd = leaf_node[t];
+		PK_GUARD(nd < 2 * n - 1, nd);
+		uint32_t tag = idx;
+		if(kp.kpos)
+		{
+			tag = g.start + t;
+			PK_GUARD(tag < n, tag);
+			kp.kpos[tag] = ph;
+			kp.kdir[tag] = kp.dir[idx];
+			kp.kcolb[tag] = kp.colb[idx];
+		}
+		nodes[nd] = make_uint4(__float_as_uint(ph.x), __float_as_uint(ph.y), __float_as_uint(ph.z), 3u | (tag << 2));
+	}
+#endif
 }
 
 } // namespace yafamd_pkd

@@ -24,6 +24,7 @@ struct float4 { float x, y, z, w; };
 struct uint2 { uint32_t x, y; };
 inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return {x, y, z, w}; }
 inline uint32_t __float_as_uint(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 struct Dim3 { uint32_t x = 0, y = 0, z = 0; };
 thread_local Dim3 threadIdx, blockIdx;
 Dim3 blockDim, gridDim;
