@@ -501,7 +501,9 @@ __device__ __forceinline__ void cameraRay(const DevScene &S, const SampleCoord &
 __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueues Q, DevCounters cnt,
                                                  const DevJob *jobs, int n_jobs, uint64_t chunk_base, int n)
 {
-	// sample i of the chunk -> segment (i / 256) % n_seg, groups of 256 dense within the segment
+	// sample i of the chunk -> segment (i / 256) % n_seg, groups of 256 dense within the segment (r05: dealing
+	// the groups in eight contiguous runs, one per XCD's segments, was measured 18 % / 50 % slower on C2 / C4 —
+	// the regions' different path lengths leave whole XCDs idle at the end of each launch)
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
 	if((uint32_t)i < S.n_seg)
 	{
@@ -2120,9 +2122,14 @@ __device__ __forceinline__ void neePut(float4 *nee, uint8_t *occ, int e, C3 c, b
 	nee[e] = f4(c, ok ? 1.f : 0.f);
 	occ[e] = ok ? 0 : 1;
 }
+#ifndef YAF_NEE_SKIP_INVALID
+#define YAF_NEE_SKIP_INVALID 1
+#endif
 __device__ __forceinline__ void neePut(const NeeHbm &nee, uint8_t *occ, int e, C3 c, bool ok)
 {
-	reinterpret_cast<F3 *>(nee.c)[e] = F3{c.r, c.g, c.b};
+	// an entry without a sample (most material-sampled entries: the direction misses the light) writes its
+	// occlusion byte only — every reader tests the byte before it uses the record (neeSumT, aoSum)
+	if(!YAF_NEE_SKIP_INVALID || ok) reinterpret_cast<F3 *>(nee.c)[e] = F3{c.r, c.g, c.b};
 	occ[e] = ok ? 0 : 1;
 }
 __device__ __forceinline__ C3 neeGet(const NeeHbm &nee, int e)
