@@ -19,7 +19,10 @@
 #include <hipcub/hipcub.hpp>
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 #include <vector>
+
+#include "bvh.h"
 
 namespace
 {
@@ -231,7 +234,9 @@ __device__ __forceinline__ void padAxis(float lo, float hi, float &plo, float &p
 	phi = hi + pad;
 }
 
-// collapse step 1: the (up to) four binary children of each wide node of this level
+// collapse step 1: the (up to) W binary children of each wide node of this level (W = 4: the BVH4 every
+// traversal reads; W = 8: the BVH8 k_trace's refill loop reads for scenes in global memory)
+template<int W>
 __global__ void __launch_bounds__(kB) k_collapse_list(const int *wl, int L, const float4 *bn_lo, const float4 *bn_hi,
                                                       const int2 *bn_child, int4 *lists, uint32_t *n_inner)
 {
@@ -239,7 +244,9 @@ __global__ void __launch_bounds__(kB) k_collapse_list(const int *wl, int L, cons
 	if(k > L) return;
 	if(k == L) { n_inner[L] = 0; return; }
 	const int code = wl[k];
-	int list[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
+	int list[W];
+#pragma unroll
+	for(int s = 0; s < W; ++s) list[s] = kEmpty;
 	int cnt;
 	if(code < 0) { list[0] = code; cnt = 1; }   // a leaf root (one triangle)
 	else
@@ -248,7 +255,7 @@ __global__ void __launch_bounds__(kB) k_collapse_list(const int *wl, int L, cons
 		list[0] = ch.x;
 		list[1] = ch.y;
 		cnt = 2;
-		while(cnt < 4)
+		while(cnt < W)
 		{
 			int best = -1;
 			float best_area = -1.f;
@@ -269,23 +276,33 @@ __global__ void __launch_bounds__(kB) k_collapse_list(const int *wl, int L, cons
 		}
 	}
 	uint32_t inner = 0;
-	for(int s = 0; s < 4; ++s) inner += (list[s] != kEmpty && list[s] >= 0) ? 1u : 0u;
-	lists[k] = make_int4(list[0], list[1], list[2], list[3]);
+#pragma unroll
+	for(int s = 0; s < W; ++s) inner += (list[s] != kEmpty && list[s] >= 0) ? 1u : 0u;
+#pragma unroll
+	for(int q = 0; q < W / 4; ++q) lists[(size_t)k * (W / 4) + q] = make_int4(list[4 * q], list[4 * q + 1], list[4 * q + 2], list[4 * q + 3]);
 	n_inner[k] = inner;
 }
 
-// collapse step 2: write the wide nodes of this level, queue their inner children as the next level
+// collapse step 2: write the wide nodes of this level, queue their inner children as the next level.
+// W = 4: 8 float4 (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, child, count — four lanes each); W = 8: 16 float4,
+// the same eight arrays with eight lanes (two float4 each)
+template<int W>
 __global__ void __launch_bounds__(kB) k_collapse_write(const int4 *lists, int L, const uint32_t *off, int ls, int le,
                                                        const float4 *bn_lo, const float4 *bn_hi, const float4 *lbox_lo,
                                                        const float4 *lbox_hi, float4 *nodes, int *wl_next)
 {
 	const int k = blockIdx.x * kB + threadIdx.x;
 	if(k >= L) return;
-	const int4 l4 = lists[k];
-	const int list[4] = {l4.x, l4.y, l4.z, l4.w};
-	float o[32];
+	int list[W];
+#pragma unroll
+	for(int q = 0; q < W / 4; ++q)
+	{
+		const int4 l4 = lists[(size_t)k * (W / 4) + q];
+		list[4 * q] = l4.x; list[4 * q + 1] = l4.y; list[4 * q + 2] = l4.z; list[4 * q + 3] = l4.w;
+	}
+	float o[8 * W];
 	int r = 0;
-	for(int s = 0; s < 4; ++s)
+	for(int s = 0; s < W; ++s)
 	{
 		const int c = list[s];
 		float lo[3] = {1.f, 1.f, 1.f}, hi[3] = {-1.f, -1.f, -1.f};
@@ -307,27 +324,29 @@ __global__ void __launch_bounds__(kB) k_collapse_write(const int4 *lists, int L,
 			padAxis(blo.y, bhi.y, lo[1], hi[1]);
 			padAxis(blo.z, bhi.z, lo[2], hi[2]);
 		}
-		o[0 + s] = lo[0]; o[4 + s] = hi[0];
-		o[8 + s] = lo[1]; o[12 + s] = hi[1];
-		o[16 + s] = lo[2]; o[20 + s] = hi[2];
-		o[24 + s] = __int_as_float(child);
-		o[28 + s] = __int_as_float(count);
+		o[0 * W + s] = lo[0]; o[1 * W + s] = hi[0];
+		o[2 * W + s] = lo[1]; o[3 * W + s] = hi[1];
+		o[4 * W + s] = lo[2]; o[5 * W + s] = hi[2];
+		o[6 * W + s] = __int_as_float(child);
+		o[7 * W + s] = __int_as_float(count);
 	}
-	float4 *dst = nodes + 8 * (size_t)(ls + k);
-	for(int q = 0; q < 8; ++q) dst[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+	float4 *dst = nodes + 2 * W * (size_t)(ls + k);
+	for(int q = 0; q < 2 * W; ++q) dst[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
 }
 
 // worst-case traversal stack entries below each wide node (bvh.cc: deferred siblings along a path)
+template<int W>
 __global__ void __launch_bounds__(kB) k_need(const float4 *nodes, int ls, int le, int *need)
 {
 	const int w = ls + blockIdx.x * kB + threadIdx.x;
 	if(w >= le) return;
-	const float4 cf = nodes[8 * (size_t)w + 6], kf = nodes[8 * (size_t)w + 7];
-	const int c[4] = {__float_as_int(cf.x), __float_as_int(cf.y), __float_as_int(cf.z), __float_as_int(cf.w)};
-	const int k[4] = {__float_as_int(kf.x), __float_as_int(kf.y), __float_as_int(kf.z), __float_as_int(kf.w)};
+	const float *nd = reinterpret_cast<const float *>(nodes + 2 * W * (size_t)w);
 	int inner = 0, deep = 0;
-	for(int s = 0; s < 4; ++s)
-		if(c[s] >= 0 && k[s] == 0) { ++inner; deep = max(deep, need[c[s]]); }
+	for(int s = 0; s < W; ++s)
+	{
+		const int c = __float_as_int(nd[6 * W + s]), k = __float_as_int(nd[7 * W + s]);
+		if(c >= 0 && k == 0) { ++inner; deep = max(deep, need[c]); }
+	}
 	need[w] = max(0, inner - 1) + deep;
 }
 
@@ -366,10 +385,13 @@ inline int blocks(long n) { return (int)((n + kB - 1) / kB); }
 // verts_dev: xyz floats, tris_dev: 3 vertex indices per triangle (both on the device).
 // Allocates *nodes_out (8 float4 per wide node) and *tris_out (3 float4 per triangle, Morton
 // order); the caller owns them (hipFree).  *n_nodes, *depth (wide levels), *stack_need as bvh.h.
+// w8 (optional): the same binary tree collapsed to a BVH8 as well (16 float4 per node, the same triangle
+// records); the caller owns w8->nodes.
 extern "C" hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
-                                           int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st)
+                                           int *n_nodes, int *depth, int *stack_need, int *ploc_iters, yafamd::YafBvh8 *w8, hipStream_t st)
 {
 	*nodes_out = *tris_out = nullptr;
+	if(w8) *w8 = yafamd::YafBvh8{};
 	DevBuf nodes, trisb;
 	const int cap_nodes = n > 1 ? n - 1 : 1;
 	BVCHECK(nodes.alloc((size_t)cap_nodes * 8 * sizeof(float4)));
@@ -451,49 +473,58 @@ extern "C" hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tr
 	}
 	if(n > 1 && node_base != n - 1) return hipErrorUnknown;
 
-	// collapse to BVH4, level by level; the lists reuse the cluster buffers
+	// collapse to BVH4 (and BVH8), level by level
 	DevBuf wl[2], lists, n_inner, off, need;
 	BVCHECK(wl[0].alloc((size_t)cap_nodes * 4));
 	BVCHECK(wl[1].alloc((size_t)cap_nodes * 4));
-	BVCHECK(lists.alloc((size_t)cap_nodes * 16));
+	BVCHECK(lists.alloc((size_t)cap_nodes * 32));
 	BVCHECK(n_inner.alloc((size_t)(cap_nodes + 1) * 4));
 	BVCHECK(off.alloc((size_t)(cap_nodes + 1) * 4));
+	BVCHECK(need.alloc((size_t)cap_nodes * 4));
 	const int root = n == 1 ? ~0 : n - 2;   // the last merge made the root
-	BVCHECK(hipMemcpyAsync(wl[0].p, &root, sizeof(int), hipMemcpyHostToDevice, st));
-	std::vector<std::pair<int, int>> levels;
-	int ls = 0, L = 1, w = 0;
 	uint32_t *tot32 = reinterpret_cast<uint32_t *>(tot);
-	while(L > 0)
-	{
-		const int le = ls + L;
-		levels.push_back({ls, le});
-		hipLaunchKernelGGL(k_collapse_list, dim3(blocks(L + 1)), dim3(kB), 0, st, wl[w].as<int>(), L, bn_lo.as<float4>(), bn_hi.as<float4>(),
-		                   bn_child.as<int2>(), lists.as<int4>(), n_inner.as<uint32_t>());
-		BVCHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, scan32_bytes, n_inner.as<uint32_t>(), off.as<uint32_t>(), L + 1, st));
-		hipLaunchKernelGGL(k_collapse_write, dim3(blocks(L)), dim3(kB), 0, st, lists.as<int4>(), L, off.as<uint32_t>(), ls, le,
-		                   bn_lo.as<float4>(), bn_hi.as<float4>(), lbox_lo.as<float4>(), lbox_hi.as<float4>(), nodes.as<float4>(),
-		                   wl[w ^ 1].as<int>());
+	auto collapse = [&](auto width, float4 *dst, int *n_out, int *depth_out, int *need_out) -> hipError_t {
+		constexpr int W = decltype(width)::value;
+		BVCHECK(hipMemcpyAsync(wl[0].p, &root, sizeof(int), hipMemcpyHostToDevice, st));
+		std::vector<std::pair<int, int>> levels;
+		int ls = 0, L = 1, w = 0;
+		while(L > 0)
+		{
+			const int le = ls + L;
+			levels.push_back({ls, le});
+			hipLaunchKernelGGL(k_collapse_list<W>, dim3(blocks(L + 1)), dim3(kB), 0, st, wl[w].as<int>(), L, bn_lo.as<float4>(), bn_hi.as<float4>(),
+			                   bn_child.as<int2>(), lists.as<int4>(), n_inner.as<uint32_t>());
+			BVCHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, scan32_bytes, n_inner.as<uint32_t>(), off.as<uint32_t>(), L + 1, st));
+			hipLaunchKernelGGL(k_collapse_write<W>, dim3(blocks(L)), dim3(kB), 0, st, lists.as<int4>(), L, off.as<uint32_t>(), ls, le,
+			                   bn_lo.as<float4>(), bn_hi.as<float4>(), lbox_lo.as<float4>(), lbox_hi.as<float4>(), dst, wl[w ^ 1].as<int>());
+			BVCHECK(hipGetLastError());
+			BVCHECK(hipMemcpyAsync(tot32, off.as<uint32_t>() + L, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+			BVCHECK(hipStreamSynchronize(st));
+			const int next = (int)*tot32;
+			if(le + next > cap_nodes) return hipErrorUnknown;
+			ls = le;
+			L = next;
+			w ^= 1;
+		}
+		*n_out = ls;
+		*depth_out = (int)levels.size();
+		for(int l = (int)levels.size() - 1; l >= 0; --l)
+			hipLaunchKernelGGL(k_need<W>, dim3(blocks(levels[l].second - levels[l].first)), dim3(kB), 0, st, dst, levels[l].first, levels[l].second,
+			                   need.as<int>());
 		BVCHECK(hipGetLastError());
-		BVCHECK(hipMemcpyAsync(tot32, off.as<uint32_t>() + L, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+		BVCHECK(hipMemcpyAsync(tot32, need.p, sizeof(int), hipMemcpyDeviceToHost, st));
 		BVCHECK(hipStreamSynchronize(st));
-		const int next = (int)*tot32;
-		if(le + next > cap_nodes) return hipErrorUnknown;
-		ls = le;
-		L = next;
-		w ^= 1;
+		*need_out = (int)*tot32;
+		return hipSuccess;
+	};
+	BVCHECK(collapse(std::integral_constant<int, 4>{}, nodes.as<float4>(), n_nodes, depth, stack_need));
+	if(w8)
+	{
+		DevBuf nodes8;
+		BVCHECK(nodes8.alloc((size_t)cap_nodes * 16 * sizeof(float4)));
+		BVCHECK(collapse(std::integral_constant<int, 8>{}, nodes8.as<float4>(), &w8->n_nodes, &w8->depth, &w8->stack_need));
+		w8->nodes = nodes8.release();
 	}
-	*n_nodes = ls;
-	*depth = (int)levels.size();
-	BVCHECK(need.alloc((size_t)ls * 4));
-	for(int l = (int)levels.size() - 1; l >= 0; --l)
-		hipLaunchKernelGGL(k_need, dim3(blocks(levels[l].second - levels[l].first)), dim3(kB), 0, st, nodes.as<float4>(),
-		                   levels[l].first, levels[l].second, need.as<int>());
-	BVCHECK(hipGetLastError());
-	int need0 = 0;
-	BVCHECK(hipMemcpyAsync(tot32, need.p, sizeof(int), hipMemcpyDeviceToHost, st));
-	BVCHECK(hipStreamSynchronize(st));
-	need0 = (int)*tot32;
-	*stack_need = need0;
 	*nodes_out = nodes.release();
 	*tris_out = trisb.release();
 	return hipSuccess;

@@ -1073,6 +1073,211 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 	}
 }
 
+// ---- BVH8 (bvhgpu.hip's 8-wide collapse of the device-built tree, scenes in global memory) ----
+// Node: 16 float4 = lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, child, count as eight-lane arrays (two float4
+// each).  Leaves of the device build hold one triangle (count 1), empty slots an inverted box, so a
+// visit reads the six plane arrays and the children: 14 float4 in two 128-B lines.  Half as many
+// dependent node fetches per ray as the BVH4 (≈ 10 levels of four → ≈ 6–7 of eight) for twice the box
+// tests per fetch: the trade k_trace wants where its visits are L2 / MALL latency (C4) and not VALU (C2,
+// whose tree stays a BVH4 in LDS).  Hits are the BVH4's: the same exact triangle test, ties to the lower
+// primitive, conservative padded boxes and slack.
+#ifndef YAF_W8_SORT
+#define YAF_W8_SORT 1
+#endif
+constexpr int kTop8Stride = 17;   // float4 per staged BVH8 node in LDS (16 used + 1 pad: 68 dwords)
+__device__ __forceinline__ float lane8(const float4 &a, const float4 &b, int k) { return k < 4 ? lane4(a, k) : lane4(b, k - 4); }
+
+template<bool SPILL, bool STATS = true>
+__device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPaths &P, uint32_t n_a, uint32_t total,
+                             uint32_t a0, uint32_t s0, uint32_t j, uint32_t stride, uint32_t &visits, uint32_t &tests,
+                             uint32_t &n_closest, uint32_t &n_shadow)
+{
+	const int lane = threadIdx.x;
+	const uint32_t glane = blockIdx.x * blockDim.x + threadIdx.x;
+	const float inf = __builtin_huge_valf();
+	V3 o = v3(0.f, 0.f, 0.f), d = o, id = o, oid = o;
+	SlabSel sel{0, 2, 4};
+	float tmin = 0.f, tmax = 0.f, box_t0 = 0.f, t_best = 0.f;
+	int prim_best = -1, sp = 0, node = -1;
+	bool any = false;
+	uint32_t cur = 0;
+	auto push = [&](int v) {
+		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + lane] = v;
+		else if(SPILL) C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane] = v;
+	};
+	for(;;)
+	{
+		if(node < 0)
+		{
+			bool got = false;
+			for(;;)
+			{
+				if(j >= total) break;
+				cur = j;
+				j += stride;
+				if(cur < n_a)
+				{
+					float tw;
+					if(!loadQRay(Q, a0 + cur, o, d, tmin, tw)) continue;
+					tmax = (tw >= 0.f) ? tw : inf;
+					any = false;
+					++n_closest;
+				}
+				else
+				{
+					const float4 od = rayLd4(&Q.sh_o[s0 + (cur - n_a)]);
+					const float4 dd = rayLd4(&Q.sh_d[s0 + (cur - n_a)]);
+					o = xyz(od);
+					d = xyz(dd);
+					tmin = 0.f;
+					tmax = dd.w;
+					any = true;
+					++n_shadow;
+				}
+				got = true;
+				break;
+			}
+			if(!got) break;
+			V3 dq = d;
+			if(fabsf(dq.x) < 1e-20f) dq.x = copysignf(1e-20f, dq.x);
+			if(fabsf(dq.y) < 1e-20f) dq.y = copysignf(1e-20f, dq.y);
+			if(fabsf(dq.z) < 1e-20f) dq.z = copysignf(1e-20f, dq.z);
+			id = v3(rcpExact(dq.x), rcpExact(dq.y), rcpExact(dq.z));
+			oid = v3(o.x * id.x, o.y * id.y, o.z * id.z);
+			sel = slabSel(id);
+			box_t0 = any ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
+			t_best = tmax;
+			prim_best = -1;
+			sp = 0;
+			node = 0;
+		}
+		if(STATS) TRACE_STAT(++visits);
+		float4 nx0, nx1, fx0, fx1, ny0, ny1, fy0, fy1, nz0, nz1, fz0, fz1, c0, c1;
+		{
+			// plane p of the node = float4s 2p, 2p + 1; sel picks the near / far plane per axis
+			const int px = 2 * sel.nx, py = 2 * sel.ny, pz = 2 * sel.nz, qx = 2 * (sel.nx ^ 1), qy = 2 * (sel.ny ^ 1), qz = 2 * (sel.nz ^ 1);
+			if(node < C.n_top)
+			{
+				typedef float V4 __attribute__((ext_vector_type(4)));
+				typedef const __attribute__((address_space(3))) V4 *LdsV4;
+				const LdsV4 tp = (LdsV4)(C.top + kTop8Stride * node);
+				auto ld = [&](int k) {
+					const V4 v = tp[k];
+					return make_float4(v.x, v.y, v.z, v.w);
+				};
+				nx0 = ld(px); nx1 = ld(px + 1); fx0 = ld(qx); fx1 = ld(qx + 1);
+				ny0 = ld(py); ny1 = ld(py + 1); fy0 = ld(qy); fy1 = ld(qy + 1);
+				nz0 = ld(pz); nz1 = ld(pz + 1); fz0 = ld(qz); fz1 = ld(qz + 1);
+				c0 = ld(12); c1 = ld(13);
+			}
+			else
+			{
+				const float4 *np = C.nodes + 16 * node;
+				nx0 = np[px]; nx1 = np[px + 1]; fx0 = np[qx]; fx1 = np[qx + 1];
+				ny0 = np[py]; ny1 = np[py + 1]; fy0 = np[qy]; fy1 = np[qy + 1];
+				nz0 = np[pz]; nz1 = np[pz + 1]; fz0 = np[qz]; fz1 = np[qz + 1];
+				c0 = np[12]; c1 = np[13];
+			}
+		}
+		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
+		float key[8];
+		int child[8], e[8], s8[8];
+		int acc = 0;
+#pragma unroll
+		for(int k = 0; k < 8; ++k)
+		{
+			const float lo = fmaxf(fmaxf(__builtin_fmaf(lane8(nx0, nx1, k), id.x, -oid.x), __builtin_fmaf(lane8(ny0, ny1, k), id.y, -oid.y)),
+			                       fmaxf(__builtin_fmaf(lane8(nz0, nz1, k), id.z, -oid.z), box_t0));
+			const float hi = fminf(fminf(__builtin_fmaf(lane8(fx0, fx1, k), id.x, -oid.x), __builtin_fmaf(lane8(fy0, fy1, k), id.y, -oid.y)),
+			                       fminf(__builtin_fmaf(lane8(fz0, fz1, k), id.z, -oid.z), slack_t));
+			const uint32_t h = lo <= hi ? 1u : 0u;
+			child[k] = __float_as_int(lane8(c0, c1, k));
+			const uint32_t inner = child[k] >= 0 ? 1u : 0u;
+			key[k] = (h & inner) ? lo : inf;
+			s8[k] = ~child[k] - acc;
+			acc += (h & (inner ^ 1u)) ? 1 : 0;   // a hit leaf: its one triangle
+			e[k] = acc;
+		}
+		bool done = false;
+		for(int i = 0; i < e[7]; ++i)
+		{
+			const int q = i + (i < e[0] ? s8[0] : i < e[1] ? s8[1] : i < e[2] ? s8[2] : i < e[3] ? s8[3]
+			                   : i < e[4] ? s8[4] : i < e[5] ? s8[5] : i < e[6] ? s8[6] : s8[7]);
+			if(STATS) TRACE_STAT(++tests);
+			const float4 *tp = C.tris + 3 * q;
+			const float4 ta = tp[0], tb = tp[1], tc = tp[2];
+			const float t = triTest(ta, tb, tc, o, d, t_best);
+			if(t == -1.f) continue;
+			const int prim = __float_as_int(tb.w);
+			if(any)
+			{
+				if(t < tmax && t >= 0.f) { t_best = t; prim_best = prim; done = true; break; }
+			}
+			else if(t >= tmin && (t < t_best || (t == t_best && prim_best >= 0 && prim < prim_best)))
+			{
+				t_best = t;
+				prim_best = prim;
+			}
+		}
+		if(!done && !YAF_W8_SORT)
+		{
+			// (tuning variant) the nearest hit child descended, the others pushed in node order
+			int kmin = 0;
+#pragma unroll
+			for(int k = 1; k < 8; ++k) kmin = key[k] < key[kmin] ? k : kmin;
+			int next = key[kmin] < inf ? child[kmin] : -1;
+#pragma unroll
+			for(int k = 7; k >= 0; --k)
+				if(k != kmin && key[k] < inf) { push(child[k]); ++sp; }
+			if(next < 0 && sp > 0)
+			{
+				--sp;
+				next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + lane]
+				                                    : C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane];
+			}
+			node = next;
+			done = next < 0;
+		}
+		else if(!done)
+		{
+			// Batcher's odd-even merge network (19 compare-exchanges): nearest child descended first, the
+			// others pushed farthest first
+			cswap(key[0], child[0], key[1], child[1]); cswap(key[2], child[2], key[3], child[3]);
+			cswap(key[4], child[4], key[5], child[5]); cswap(key[6], child[6], key[7], child[7]);
+			cswap(key[0], child[0], key[2], child[2]); cswap(key[1], child[1], key[3], child[3]);
+			cswap(key[4], child[4], key[6], child[6]); cswap(key[5], child[5], key[7], child[7]);
+			cswap(key[1], child[1], key[2], child[2]); cswap(key[5], child[5], key[6], child[6]);
+			cswap(key[0], child[0], key[4], child[4]); cswap(key[1], child[1], key[5], child[5]);
+			cswap(key[2], child[2], key[6], child[6]); cswap(key[3], child[3], key[7], child[7]);
+			cswap(key[2], child[2], key[4], child[4]); cswap(key[3], child[3], key[5], child[5]);
+			cswap(key[1], child[1], key[2], child[2]); cswap(key[3], child[3], key[4], child[4]);
+			cswap(key[5], child[5], key[6], child[6]);
+#pragma unroll
+			for(int k = 7; k >= 1; --k)
+				if(key[k] < inf) { push(child[k]); ++sp; }
+			int next = key[0] < inf ? child[0] : -1;
+			if(next < 0 && sp > 0)
+			{
+				--sp;
+				next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + lane]
+				                                    : C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane];
+			}
+			node = next;
+			done = next < 0;
+		}
+		if(done)
+		{
+			if(any) P.occ[__float_as_int(Q.sh_o[s0 + (cur - n_a)].w)] = prim_best >= 0 ? 1 : 0;
+			else
+			{
+				raySt(&Q.hit_t[a0 + cur], t_best);
+				raySt(&Q.hit_prim[a0 + cur], prim_best);
+			}
+			node = -1;
+		}
+	}
+}
+
 template<bool ANY, bool WIDE, bool SPILL = true, bool TS = false, bool STATS = true>
 __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best,
                                          int &prim_best, uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
@@ -1088,7 +1293,10 @@ __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tm
 #ifdef YAF_TRACE_WAVES
 #define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(YAF_TRACE_WAVES)))
 #else
-#define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LDS_SCENE ? 8 : 6)))
+#ifndef YAF_TRACE8_WAVES
+#define YAF_TRACE8_WAVES 4
+#endif
+#define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LDS_SCENE ? 8 : (W8 ? YAF_TRACE8_WAVES : 6))))
 #endif
 
 // ---------------------------------------------------------------------------------------------
@@ -1173,7 +1381,8 @@ __device__ __forceinline__ void waveSortWindow(WaveSort &W, const uint32_t (&key
 // STATS = false: no per-visit node / triangle counters (timed frames; the counts come from a frame
 // rendered with them — the frame is deterministic, so they are the same)
 // SORT: ray-stream sorting of each wave's window (above)
-template<bool LDS_SCENE, bool WIDE, bool TS, bool SPILL = true, bool STATS = true, bool SORT = false>
+// W8: the refill loop over the BVH8 (S.nodes8; global-memory scenes without transparent shadows)
+template<bool LDS_SCENE, bool WIDE, bool TS, bool SPILL = true, bool STATS = true, bool SORT = false, bool W8 = false>
 __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S, DevQueues Q, DevCounters cnt, DevPaths P,
                                                       DevStats *stats, int stack_depth, int *spill)
 {
@@ -1198,7 +1407,19 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	{
 		C.nodes = S.nodes;
 		C.tris = S.tris;
-		if(WIDE && S.lds_top > 0)
+		if constexpr(W8)
+		{
+			C.nodes = S.nodes8;
+			if(S.lds_top8 > 0)
+			{
+				float4 *top = smem + (stack_depth * kTraceBlock) / 4;
+				for(int k = threadIdx.x; k < 16 * S.lds_top8; k += blockDim.x) top[(k >> 4) * kTop8Stride + (k & 15)] = S.nodes8[k];
+				__syncthreads();
+				C.top = top;
+				C.n_top = S.lds_top8;
+			}
+		}
+		else if(WIDE && S.lds_top > 0)
 		{
 			// the top treelet (refill loop only): nodes [0, lds_top) after the stack
 			float4 *top = smem + (stack_depth * kTraceBlock) / 4;
@@ -1298,7 +1519,9 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 #ifndef YAF_TRACE_NOREFILL
 	// refill pays where traversals are long (meshes in global memory: C4 -16%); on the short
 	// LDS-resident traversals of small scenes its per-visit bookkeeping costs more (C2 +35%)
-	if(!LDS_SCENE && WIDE && !TS)
+	if(W8)
+		traceRefill8<true, STATS>(C, Q, P, n_a, total, a0, s0, L.r * blockDim.x + threadIdx.x, stride, visits, tests, n_closest, n_shadow);
+	else if(!LDS_SCENE && WIDE && !TS)
 		traceRefill4<true, STATS>(C, Q, P, n_a, total, a0, s0, L.r * blockDim.x + threadIdx.x, stride, visits, tests, n_closest, n_shadow);
 	else
 #endif
@@ -5949,7 +6172,8 @@ int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds)
 {
 	int nb = 0;
 	hipError_t e;
-	if(lds_scene) e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, true, false>, kTraceBlock, dyn_lds)
+	if(wide == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, true, false, true, false, false, true>, kTraceBlock, dyn_lds);
+	else if(lds_scene) e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, true, false>, kTraceBlock, dyn_lds)
 	                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<true, false, false>, kTraceBlock, dyn_lds);
 	else e = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, true, false>, kTraceBlock, dyn_lds)
 	              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace<false, false, false>, kTraceBlock, dyn_lds);
@@ -5998,6 +6222,18 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
 	const size_t lds_scene = S->scene_in_lds ? (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4)
 	                                         : (wide ? (size_t)S->lds_top * kTopStride * sizeof(float4) : 0);
 	const size_t bytes = stack_bytes + lds_scene;
+	if(S->nodes8 && !S->scene_in_lds && !S->tr_shad)
+	{
+		// the BVH8 refill loop (global-memory scenes; its top treelet instead of the BVH4's)
+		const size_t bytes8 = stack_bytes + (size_t)S->lds_top8 * kTop8Stride * sizeof(float4);
+		if(S->trace_stats)
+			hipLaunchKernelGGL((k_trace<false, true, false, true, true, false, true>), dim3(grid), dim3(kTraceBlock), bytes8, st, *S, *Q, *cnt, *P, stats,
+			                   stack_depth, spill);
+		else
+			hipLaunchKernelGGL((k_trace<false, true, false, true, false, false, true>), dim3(grid), dim3(kTraceBlock), bytes8, st, *S, *Q, *cnt, *P, stats,
+			                   stack_depth, spill);
+		return hipGetLastError();
+	}
 #ifdef YAF_EXPERIMENTS
 	if(S->brute && !S->tr_shad && S->n_tris <= kBruteTris)
 	{

@@ -69,7 +69,7 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
                             hipStream_t st);
 size_t yafamd_gather_lanes(const DevScene *S);
 hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tris_dev, int n, void **nodes_out, void **tris_out,
-                                int *n_nodes, int *depth, int *stack_need, int *ploc_iters, hipStream_t st);
+                                int *n_nodes, int *depth, int *stack_need, int *ploc_iters, YafBvh8 *w8, hipStream_t st);
 hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch);
 hipError_t yafamd_build_pkd_kd(const float4 *pos_dev, const float4 *dir_dev, const float *colb_dev, uint32_t n, uint4 *nodes_dev, float4 *kpos,
                                float4 *kdir, float *kcolb, int *depth_out, hipStream_t st, void **scratch);
@@ -247,6 +247,8 @@ struct GpuRenderer::Impl
 	bool ok = false, init_done = false;
 	hipStream_t stream = nullptr;
 	Buf nodes, tris, prim_ng, mats, lights, faure, faure_dim, faure_inv;
+	Buf nodes8;                 // BVH8 of the device-built tree (k_trace's refill loop), or empty
+	int n_nodes8 = 0, need8 = 0, lds_top8 = 0;
 	// surface attributes, textures and shader-node programs (texeval.h)
 	Buf prim_attr, shader_nodes, textures, texels;
 	// specular recursion tree (k_spawn / k_combine): spawned rays and per-node records
@@ -514,11 +516,26 @@ bool GpuRenderer::upload(HostScene &hs)
 		if(!allocCopy(log_, t, hs.tris.data(), hs.tris.size())) return false;
 		d.nodes.release();
 		d.tris.release();
+		d.nodes8.release();
 		void *np = nullptr, *tp = nullptr;
 		int nn = 0, depth = 0, need = 0, iters = 0;
-		const hipError_t e = yafamd_build_bvh_gpu((const float *)v.p, (const int *)t.p, hs.n_prims, &np, &tp, &nn, &depth, &need, &iters, d.stream);
+		// opt-in YAFARAY_AMD_BVH8=1: the 8-wide collapse too, traversed by k_trace's refill loop for scenes in
+		// global memory.  Measured on C4: 6.78 node visits per ray instead of 10.04, but k_trace
+		// 141 -> 162 ms per frame (106 VGPRs: 4 waves per SIMD instead of 6, twice the box tests and a 19-exchange
+		// sort per visit) — the BVH4 stays the default
+		const char *b8 = std::getenv("YAFARAY_AMD_BVH8");
+		YafBvh8 w8;
+		const hipError_t e = yafamd_build_bvh_gpu((const float *)v.p, (const int *)t.p, hs.n_prims, &np, &tp, &nn, &depth, &need, &iters,
+		                                          (b8 && *b8 == '1') ? &w8 : nullptr, d.stream);
 		v.release();
 		t.release();
+		if(w8.nodes)
+		{
+			d.nodes8.p = w8.nodes;
+			d.nodes8.bytes = (size_t)std::max(1, w8.n_nodes) * 256;
+			d.n_nodes8 = w8.n_nodes;
+			d.need8 = w8.stack_need;
+		}
 		HIPCHECK(e);
 		d.nodes.p = np;
 		d.nodes.bytes = (size_t)std::max(1, nn) * 128;
@@ -533,6 +550,8 @@ bool GpuRenderer::upload(HostScene &hs)
 	}
 	else
 	{
+		d.nodes8.release();
+		d.n_nodes8 = 0;
 		if(!allocCopy(log_, d.nodes, hs.bvh.nodes.data(), hs.bvh.nodes.size())) return false;
 		if(!allocCopy(log_, d.tris, hs.bvh.tris.data(), hs.bvh.tris.size())) return false;
 	}
@@ -605,7 +624,8 @@ bool GpuRenderer::upload(HostScene &hs)
 	}
 	d.depth = hs.bvh.depth;
 	d.node_f4 = hs.bvh.width == 4 ? 8 : 4;
-	const int need = hs.bvh.width == 4 ? hs.bvh.stack_need : hs.bvh.depth;
+	int need = hs.bvh.width == 4 ? hs.bvh.stack_need : hs.bvh.depth;
+	if(d.nodes8.p) need = std::max(need, d.need8);   // one stack serves both trees
 	d.stack_depth = std::max(8, ((need + 2 + 7) / 8) * 8);
 	// BVH4's worst-case bound (3 deferred siblings per level) is far above what rays use: k_trace
 	// keeps the first levels in LDS (occupancy) and spills deeper ones to HBM
@@ -635,10 +655,22 @@ bool GpuRenderer::upload(HostScene &hs)
 			d.lds_top = fit;
 		}
 	}
+	// the BVH8's top treelet: the root and its eight children (272 B per node, kernels.hip kTop8Stride)
+	d.lds_top8 = 0;
+	if(d.nodes8.p && !d.scene_in_lds)
+	{
+		int top = 9;
+		if(const char *e = getenv("YAFARAY_AMD_LDS_TOP8"); e && *e) top = std::max(0, atoi(e));
+		const size_t stack_b = (size_t)d.lds_stack * yafamd_trace_block() * 4, lds_max = 64 * 1024;
+		const int fit = stack_b >= lds_max ? 0 : (int)((lds_max - stack_b) / 272);
+		d.lds_top8 = std::min(std::min(top, d.n_nodes8), fit);
+	}
 	{
 		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy or top treelet))
-		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 + (d.scene_in_lds ? scene_bytes : (size_t)d.lds_top * 144);
-		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, d.node_f4 == 8 ? 1 : 0, dyn));
+		const bool w8 = d.nodes8.p && !d.scene_in_lds;
+		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 +
+		                   (d.scene_in_lds ? scene_bytes : w8 ? (size_t)d.lds_top8 * 272 : (size_t)d.lds_top * 144);
+		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, w8 ? 8 : (d.node_f4 == 8 ? 1 : 0), dyn));
 		if(const char *e = getenv("YAFARAY_AMD_TRACE_GRID")) d.trace_grid = std::max(1, atoi(e));
 		// a whole number of workgroups per queue segment
 		d.trace_grid = std::max(1, d.trace_grid / d.shade_grid) * d.shade_grid;
@@ -693,6 +725,8 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 {
 	S.nodes = (const float4 *)d.nodes.p;
 	S.tris = (const float4 *)d.tris.p;
+	S.nodes8 = (d.nodes8.p && !d.scene_in_lds) ? (const float4 *)d.nodes8.p : nullptr;
+	S.lds_top8 = d.lds_top8;
 	S.prim_ng = (const float4 *)d.prim_ng.p;
 	S.mats = (const DevMaterial *)d.mats.p;
 	S.lights = (const DevLight *)d.lights.p;

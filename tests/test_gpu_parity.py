@@ -55,6 +55,9 @@ BVH_VARIANTS = {"bvh4": {"YAFARAY_AMD_BVH_BUILD": "host", "YAFARAY_AMD_TRACE": "
                 "bvh2": {"YAFARAY_AMD_BVH_WIDTH": "2", "YAFARAY_AMD_TRACE": "bvh"},
                 "gpu-build": {"YAFARAY_AMD_BVH_BUILD": "gpu", "YAFARAY_AMD_TRACE": "bvh"},
                 "bvh4-global": {"YAFARAY_AMD_SCENE_LDS": "0", "YAFARAY_AMD_TRACE": "bvh"},
+                # r05: the device-built tree in global memory traced through its BVH8 (opt-in, k_trace's refill loop)
+                "bvh8-global": {"YAFARAY_AMD_BVH_BUILD": "gpu", "YAFARAY_AMD_SCENE_LDS": "0", "YAFARAY_AMD_TRACE": "bvh",
+                                "YAFARAY_AMD_BVH8": "1"},
                 "brute": {"YAFARAY_AMD_TRACE": "brute"},
                 # ray-stream sorting (opt-in): each wave's window of queue entries in key order
                 "ray-sort": {"YAFARAY_AMD_RAY_SORT": "1", "YAFARAY_AMD_TRACE": "bvh"}}
@@ -120,6 +123,28 @@ def test_gpu_bvh_build_small_and_ragged(product, oracle_built, n_tris, monkeypat
     assert np.array_equal(t[hit].view(np.uint32), ohit[hit, 0].view(np.uint32))
     assert np.array_equal(yi.trace_shadow(rays), osc.trace_shadow(rays))
     yi.close()
+
+
+@pytest.mark.parametrize("n_tris", [1, 2, 3, 5, 34, 3200])
+def test_bvh8_refill_equals_bvh4(product, n_tris, monkeypatch):
+    """r05: k_trace's refill loop over the device build's BVH8 (opt-in YAFARAY_AMD_BVH8=1, scenes in global
+    memory) against the same tree's BVH4 (the default) on 1, 2, 3, 5 triangles, the Cornell box and a 3,200-triangle
+    sphere, a 4-level LDS stack (the HBM spill levels): bit-identical path-traced films."""
+    use_bvh(monkeypatch, "bvh8-global")
+    monkeypatch.setenv("YAFARAY_AMD_LDS_STACK", "4")
+    if n_tris == 3200:
+        spec = scenes.cornell_sphere(n=40, width=40, height=30, spp=4, bounces=6, rr=True)
+    else:
+        import dataclasses
+        base = scenes.cornell(40, 30, spp=4, bounces=6, rr=True)
+        spec = dataclasses.replace(_subset(base, n_tris), lights=base.lights, materials=base.materials) if n_tris < 34 else base
+    a, wa, sa = product.render_spec(spec)
+    assert sa["scene_in_lds"] == 0
+    monkeypatch.setenv("YAFARAY_AMD_BVH8", "0")
+    b, wb, sb = product.render_spec(spec)
+    assert np.array_equal(wa, wb)
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+    assert sa["closest_rays"] == sb["closest_rays"] and sa["shadow_rays"] == sb["shadow_rays"]
 
 
 def test_direct_light_test01_matches_oracle(product, oracle_built):
