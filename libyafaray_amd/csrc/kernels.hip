@@ -68,6 +68,10 @@ constexpr bool kShadeFused = true;
 #else
 constexpr bool kShadeFused = false;
 #endif
+// -DYAF_FUSE_LEAN=1 (tuning build): the lean k_shade of the plain path tracer runs the NEE itself
+#ifndef YAF_FUSE_LEAN
+#define YAF_FUSE_LEAN 0
+#endif
 constexpr int kShadeBlock = 256;
 
 enum : uint32_t
@@ -3253,8 +3257,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_
 			if(__any(all))
 			{
 				for(int l = 0; l < S.n_lights; ++l)
-					neeLight<EXT>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, all, e0 + (int)S.lights[l].nee_base, neeHbm(Pn),
-					              Pn.occ, out, ts);
+					neeLight<EXT, ShadeOut, NeeHbm, LEAN>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, all, e0 + (int)S.lights[l].nee_base,
+					                                    neeHbm(Pn), Pn.occ, out, ts);
 				if(S.do_ao) aoSamples<EXT>(S, m, sp, wo, sample_idx, offset, all, e0 + S.nee_all_count, neeHbm(Pn), Pn.occ, out, ts);
 			}
 			if(__any(one))
@@ -3263,7 +3267,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_
 				{
 					const bool mine = one && lnum == (uint32_t)l;
 					if(!__any(mine)) continue;
-					neeLight<EXT>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, mine, e0, neeHbm(Pn), Pn.occ, out, ts);
+					neeLight<EXT, ShadeOut, NeeHbm, LEAN>(S, S.lights[l], m, sp, wo, (uint32_t)l, sample_idx, offset, mine, e0, neeHbm(Pn), Pn.occ, out, ts);
 				}
 			}
 		}
@@ -6134,6 +6138,14 @@ int yafamd_trace_block() { return kTraceBlock; }
 // Whether the non-EXT k_shade runs the next-event estimation itself (then render.cc launches no
 // k_nee for those scenes); -DYAF_FUSE builds that variant (measured slower, see kShadeFused).
 int yafamd_shade_fused() { return kShadeFused ? 1 : 0; }
+// the k_shade this scene launches runs the NEE itself (kShadeFused, or the lean fused tuning build)
+int yafamd_shade_fused_for(const DevScene *S)
+{
+	if(S->ext) return 0;
+	if(kShadeFused) return 1;
+	return (YAF_FUSE_LEAN && S->integrator == INT_PATH && S->path_samples <= 1 && !S->do_ao && !S->caus_map && !S->gather_on && !S->show_map &&
+	        S->n_photons == 0 && !S->tree && !S->has_attr && !S->no_lean && !S->tr_shad && !S->has_mesh_light) ? 1 : 0;
+}
 
 // Whether the measured-and-dropped pipelines are compiled in (-DYAF_EXPERIMENTS)
 int yafamd_experiments() { return kExperiments ? 1 : 0; }
@@ -6324,7 +6336,12 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	else if(!kShadeFused && S->integrator == INT_PATH && S->path_samples <= 1 && !S->do_ao && !S->caus_map && !S->gather_on && !S->show_map &&
 	        S->n_photons == 0 && !S->tree && !S->has_attr && !S->no_lean)
 	{
-		if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		if(yafamd_shade_fused_for(S))
+		{
+			if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+			else hipLaunchKernelGGL((k_shade<false, false, true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		}
+		else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 		else hipLaunchKernelGGL((k_shade<false, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	}
 	else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, kShadeFused>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);

@@ -32,6 +32,7 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
                                DevStats *stats, int stack_depth, int *spill, int grid, hipStream_t st);
 int yafamd_trace_block();
 int yafamd_shade_fused();
+int yafamd_shade_fused_for(const DevScene *S);
 int yafamd_experiments();
 int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds);
 int yafamd_shade_blocks_per_cu();
@@ -1906,7 +1907,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 					                                     nullptr, d.stream));
 			}
 			// NEE requests (none in iteration 1 of photon mapping, whose entries all finish there)
-			if((S.ext || !yafamd_shade_fused()) && !(S.integrator == INT_PHOTON && it == 1) && !count_run)
+			if(!yafamd_shade_fused_for(&S) && !(S.integrator == INT_PHOTON && it == 1) && !count_run)
 				PROF(KK_NEE, yafamd_launch_nee(&S, &d.N, &d.P[cur ^ 1], &d.Q[cur ^ 1], &cnt[cur ^ 1], nee_trace_stack, d.stream));
 			// (non-EXT k_shade runs the NEE itself: FUSED)
 			cur ^= 1;
