@@ -549,7 +549,10 @@ __global__ void __launch_bounds__(256) k_camera(DevScene S, DevPaths P, DevQueue
 #ifndef YAF_TOP_STRIDE
 #define YAF_TOP_STRIDE 9
 #endif
-constexpr int kTopStride = YAF_TOP_STRIDE;   // float4 per node of the LDS top treelet (8 used + 1 pad)
+constexpr int kTopStride = YAF_TOP_STRIDE;
+#ifndef YAF_LANE_REMAT
+#define YAF_LANE_REMAT 1
+#endif   // float4 per node of the LDS top treelet (8 used + 1 pad)
 struct TraceCtx
 {
 	const float4 *nodes;
@@ -773,7 +776,21 @@ template<bool ANY, bool SPILL, bool TS = false, bool STATS = true>
 __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
                           uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
+#if YAF_LANE_REMAT
+	// the lane's stack column from the wave's first thread (scalar) and the lane id (v_mbcnt, re-derived at
+	// every push / pop — opaque, so not hoisted): at the 64-VGPR budget a loop-invariant column address
+	// was spilled and reloaded from scratch at every push (a vector-memory wait per push)
+	const uint32_t wave_base = __builtin_amdgcn_readfirstlane((uint32_t)threadIdx.x) & ~63u;
+	auto laneNow = [&]() -> int {
+		uint32_t l;
+		asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+		return (int)(wave_base + l);
+	};
+#define YAF_LANE laneNow()
+#else
 	const int lane = threadIdx.x;
+#define YAF_LANE lane
+#endif
 	V3 dd = d;
 	if(fabsf(dd.x) < 1e-20f) dd.x = copysignf(1e-20f, dd.x);
 	if(fabsf(dd.y) < 1e-20f) dd.y = copysignf(1e-20f, dd.y);
@@ -792,7 +809,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	int node = 0;
 	// the first lds_depth levels live in LDS; deeper ones (rare) spill to this lane's HBM column
 	auto push = [&](int v) {
-		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + lane] = v;
+		if(!SPILL || sp < C.lds_depth) C.stack[sp * kTraceBlock + YAF_LANE] = v;   // (!SPILL: the bound fits the LDS levels)
 		else if(SPILL) C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane] = v;
 	};
 	// the box culling distance: recomputed only where t_best changes (a closest hit), not per visit
@@ -905,7 +922,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 		{
 			if(sp == 0) break;
 			--sp;
-			next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + lane]
+			next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + YAF_LANE]
 			                                    : C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane];
 		}
 		node = next;
@@ -918,6 +935,8 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 // its traversal ends, so a wave runs as long as its longest lane's sum of rays instead of the sum
 // over rays of the longest lane.  Every ray runs the sequence of traverse4 (same visits, culling,
 // leaf order and early exits), so hits are identical.
+#undef YAF_LANE
+
 template<bool SPILL, bool STATS = true>
 __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPaths &P, uint32_t n_a, uint32_t total,
                              uint32_t a0, uint32_t s0, uint32_t j, uint32_t stride, uint32_t &visits, uint32_t &tests,
