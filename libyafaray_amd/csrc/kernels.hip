@@ -568,7 +568,17 @@ struct TraceCtx
 	// the wide nodes level by level, so these are the levels every ray starts with)
 	const float4 *top = nullptr;
 	int n_top = 0;
+	uint32_t wave_base = 0;   // threadIdx.x of the wave's lane 0 (scalar; set with the context: waveBase())
 };
+// threadIdx.x of the wave's first lane, and this lane's threadIdx.x re-derived from it (v_mbcnt, opaque so
+// that it is recomputed where used instead of keeping threadIdx.x live — or spilled — across the loops)
+__device__ __forceinline__ uint32_t waveBase() { return __builtin_amdgcn_readfirstlane((uint32_t)threadIdx.x) & ~63u; }
+__device__ __forceinline__ uint32_t tidFrom(uint32_t wave_base)
+{
+	uint32_t l;
+	asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+	return wave_base + l;
+}
 
 // Transparent-shadow hit list of one shadow ray (accelerator_kdtree.cc:1001-1023): an opaque
 // surface shadows; each transparent one is recorded until `cap` (= shadowDepth) are recorded, the
@@ -780,13 +790,7 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 	// the lane's stack column from the wave's first thread (scalar) and the lane id (v_mbcnt, re-derived at
 	// every push / pop — opaque, so not hoisted): at the 64-VGPR budget a loop-invariant column address
 	// was spilled and reloaded from scratch at every push (a vector-memory wait per push)
-	const uint32_t wave_base = __builtin_amdgcn_readfirstlane((uint32_t)threadIdx.x) & ~63u;
-	auto laneNow = [&]() -> int {
-		uint32_t l;
-		asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-		return (int)(wave_base + l);
-	};
-#define YAF_LANE laneNow()
+#define YAF_LANE ((int)tidFrom(C.wave_base))
 #else
 	const int lane = threadIdx.x;
 #define YAF_LANE lane
@@ -1412,6 +1416,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	extern __shared__ float4 smem[];
 	int *stack = reinterpret_cast<int *>(smem);
 	TraceCtx C;
+	C.wave_base = waveBase();
 	C.stack = stack;
 	C.lds_depth = stack_depth;
 	C.spill = spill;
@@ -1548,8 +1553,9 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 		traceRefill4<true, STATS>(C, Q, P, n_a, total, a0, s0, L.r * blockDim.x + threadIdx.x, stride, visits, tests, n_closest, n_shadow);
 	else
 #endif
-	// one uniform trip count per workgroup so every lane reaches the same exits
-	for(uint32_t base = L.r * blockDim.x; base < total; base += stride) countWave(traceEntry(base + threadIdx.x));
+	// one uniform trip count per workgroup so every lane reaches the same exits (the lane's thread index
+	// re-derived per entry: threadIdx.x kept live across the traversal was spilled and reloaded per visit)
+	for(uint32_t base = L.r * blockDim.x; base < total; base += stride) countWave(traceEntry(base + (YAF_LANE_REMAT ? tidFrom(C.wave_base) : threadIdx.x)));
 	}
 	if(laneId() == 0)
 	{
@@ -3716,6 +3722,7 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_NEE_LEAN_WA
 	const DevScene S = S_;
 	const bool ATTR = EXT && S.has_attr != 0;
 	TraceCtx C;
+	C.wave_base = waveBase();
 	float4 *rec = nullptr;
 	if(TR)
 	{
@@ -3938,6 +3945,7 @@ __global__ void __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_e
 	for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = A.S.tris[k];
 	__syncthreads();
 	TraceCtx C;
+	C.wave_base = waveBase();
 	C.nodes = lds_nodes;
 	C.tris = lds_tris;
 	C.stack = stack;
@@ -4499,6 +4507,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_rays(DevScene S, const fl
 {
 	extern __shared__ float4 smem[];
 	TraceCtx C;
+	C.wave_base = waveBase();
 	C.stack = reinterpret_cast<int *>(smem);
 	C.lds_depth = stack_depth;   // the full bound: no spill (traverse<..., SPILL = false>)
 	C.spill = nullptr;
@@ -4693,6 +4702,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_photon_bounce(PhotonArgs A)
 	const DevScene &S = A.S;
 	extern __shared__ float4 smem[];
 	TraceCtx C;
+	C.wave_base = waveBase();
 	C.stack = reinterpret_cast<int *>(smem);
 	C.lds_depth = A.stack_depth;
 	C.spill = A.spill;
@@ -6002,6 +6012,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 	const DevScene &S = A.S;
 	extern __shared__ float4 smem[];
 	TraceCtx C;
+	C.wave_base = waveBase();
 	C.stack = reinterpret_cast<int *>(smem);
 	C.lds_depth = A.stack_depth;
 	C.spill = A.spill;
