@@ -63,6 +63,19 @@ def test_resumed_render_equals_uninterrupted(product, tmp_path, autosave):
 
 
 @pytest.mark.gpu
+def test_resumed_render_with_16_byte_nee_words(product, tmp_path, monkeypatch):
+    """a resumed render (sampling offsets carried in the film file) with the 16-B NEE request
+    word (YAFARAY_AMD_NEE_PM16=1) equals the uninterrupted render with the default 8-B word, bit for bit."""
+    path = str(tmp_path / "render")
+    full, fw, _ = product.render_spec(_spec(aa_passes=3))
+    monkeypatch.setenv("YAFARAY_AMD_NEE_PM16", "1")
+    product.render_spec(_spec(aa_passes=3, film_load_save_mode="save", film_load_save_path=path).with_render(aa_threshold=1e30))
+    a2, w2, _ = product.render_spec(_spec(aa_passes=3, film_load_save_mode="load-save", film_load_save_path=path))
+    assert np.array_equal(_bits(w2), _bits(fw))
+    assert np.array_equal(_bits(a2), _bits(full))
+
+
+@pytest.mark.gpu
 def test_load_sums_every_node_film(product, tmp_path):
     path = str(tmp_path / "farm")
     films = []
