@@ -22,12 +22,13 @@ struct BvhInput
 	int width = 4;           // 2: BVH2 (4 float4 per node), 4: BVH4 (8 float4 per node)
 };
 
-// The device build's optional 8-wide collapse of the same binary tree (bvhgpu.hip): 16 float4 per node —
-// lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, child, count as eight-lane arrays (two float4 each) — over the BVH4's
-// triangle records; k_trace's refill loop traverses it for scenes in global memory.
+// The device build's optional 8-wide collapse of the same binary tree, quantised (bvhgpu.hip k_q8_write:
+// 8 float4 per node) with its own copy of the triangle records in node order; k_trace's refill loop
+// traverses it for scenes in global memory (opt-in YAFARAY_AMD_BVH8=1).
 struct YafBvh8
 {
 	void *nodes = nullptr;   // device memory, owned by the caller
+	void *tris = nullptr;    // device memory (3 float4 per triangle), owned by the caller
 	int n_nodes = 0, depth = 0, stack_need = 0;
 };
 

@@ -350,6 +350,109 @@ __global__ void __launch_bounds__(kB) k_need(const float4 *nodes, int ls, int le
 	need[w] = max(0, inner - 1) + deep;
 }
 
+// ---- quantised BVH8 (k_trace's refill loop over global-memory scenes, opt-in) ----
+// Node (128 B, the first 80 B read per visit): origin (the children's padded lower corner), per axis a
+// power-of-two quantum (biased exponent byte), inner / leaf child masks, the first inner child's node
+// index (inner children are consecutive) and the first of the node's leaf triangles (copied
+// consecutively into the BVH8's own triangle array), then per axis the children's lower / upper planes
+// as bytes: plane = origin + q · 2^e with q rounded outwards (one quantum of margin) — every decoded box
+// contains the float box, which contains the padded triangle box.
+//   dw0-2 origin, dw3 exps x/y/z | inner mask << 24, dw4 leaf mask, dw5 inner base, dw6 tri base, dw7 0,
+//   dw8-9 lo.x[8], dw10-11 hi.x[8], dw12-13 lo.y, dw14-15 hi.y, dw16-17 lo.z, dw18-19 hi.z
+__global__ void __launch_bounds__(kB) k_q8_count(const float4 *nodes8, int n, uint32_t *leaves)
+{
+	const int w = blockIdx.x * kB + threadIdx.x;
+	if(w > n) return;
+	if(w == n) { leaves[n] = 0; return; }
+	const float *nd = reinterpret_cast<const float *>(nodes8 + 16 * (size_t)w);
+	uint32_t c = 0;
+	for(int s = 0; s < 8; ++s) c += (__float_as_int(nd[6 * 8 + s]) < 0 && __float_as_int(nd[7 * 8 + s]) == 1) ? 1u : 0u;
+	leaves[w] = c;
+}
+
+__device__ __forceinline__ int q8Exp(float extent)
+{
+	// the smallest power of two s with extent <= 254 s (so that ceil + one quantum of margin stays <= 255)
+	const float need = extent / 254.f;
+	int e = -126;
+	if(need > 0.f)
+	{
+		int ex;
+		const float m = frexpf(need, &ex);   // need = m 2^ex, m in [0.5, 1)
+		e = (m == 0.5f) ? ex - 1 : ex;
+		// float division rounding: make sure extent <= 254 * 2^e holds
+		while(ldexpf(254.f, e) < extent) ++e;
+	}
+	return max(-126, min(127, e));
+}
+
+__global__ void __launch_bounds__(kB) k_q8_write(const float4 *nodes8, int n, const uint32_t *tri_base, const float4 *tris_in,
+                                                 float4 *qnodes, float4 *tris8)
+{
+	const int w = blockIdx.x * kB + threadIdx.x;
+	if(w >= n) return;
+	const float *nd = reinterpret_cast<const float *>(nodes8 + 16 * (size_t)w);
+	float lo[3] = {3.4e38f, 3.4e38f, 3.4e38f}, hi[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+	uint32_t inner = 0, leaf = 0;
+	int inner_base = -1;
+	for(int s = 0; s < 8; ++s)
+	{
+		const int c = __float_as_int(nd[6 * 8 + s]), k = __float_as_int(nd[7 * 8 + s]);
+		const bool isl = c < 0 && k == 1, isi = c >= 0;
+		if(!isl && !isi) continue;
+		if(isi) { inner |= 1u << s; if(inner_base < 0) inner_base = c; }
+		else leaf |= 1u << s;
+		for(int a = 0; a < 3; ++a)
+		{
+			lo[a] = fminf(lo[a], nd[(2 * a) * 8 + s]);
+			hi[a] = fmaxf(hi[a], nd[(2 * a + 1) * 8 + s]);
+		}
+	}
+	uint32_t q[6][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+	int ex[3] = {0, 0, 0};
+	for(int a = 0; a < 3; ++a)
+	{
+		if(!(lo[a] <= hi[a])) { lo[a] = 0.f; hi[a] = 0.f; }
+		ex[a] = q8Exp(hi[a] - lo[a]);
+	}
+	uint32_t rank = 0;
+	for(int s = 0; s < 8; ++s)
+	{
+		const int c = __float_as_int(nd[6 * 8 + s]);
+		uint32_t bl[3] = {255u, 255u, 255u}, bh[3] = {0u, 0u, 0u};   // empty slot: inverted box
+		if((inner | leaf) & (1u << s))
+			for(int a = 0; a < 3; ++a)
+			{
+				const float sc = ldexpf(1.f, ex[a]);
+				const float fl = floorf((nd[(2 * a) * 8 + s] - lo[a]) / sc) - 1.f;
+				const float fh = ceilf((nd[(2 * a + 1) * 8 + s] - lo[a]) / sc) + 1.f;
+				bl[a] = (uint32_t)fminf(fmaxf(fl, 0.f), 255.f);
+				bh[a] = (uint32_t)fminf(fmaxf(fh, 0.f), 255.f);
+			}
+		for(int a = 0; a < 3; ++a)
+		{
+			q[2 * a][s >> 2] |= bl[a] << (8 * (s & 3));
+			q[2 * a + 1][s >> 2] |= bh[a] << (8 * (s & 3));
+		}
+		if(leaf & (1u << s))
+		{
+			const size_t dst = (size_t)tri_base[w] + rank++;
+			for(int r = 0; r < 3; ++r) tris8[3 * dst + r] = tris_in[3 * (size_t)(~c) + r];
+		}
+	}
+	uint32_t o[32];
+	o[0] = __float_as_uint(lo[0]); o[1] = __float_as_uint(lo[1]); o[2] = __float_as_uint(lo[2]);
+	o[3] = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16) | (inner << 24);
+	o[4] = leaf;
+	o[5] = (uint32_t)max(inner_base, 0);
+	o[6] = tri_base[w];
+	o[7] = 0u;
+	for(int p = 0; p < 6; ++p) { o[8 + 2 * p] = q[p][0]; o[9 + 2 * p] = q[p][1]; }
+	for(int k = 20; k < 32; ++k) o[k] = 0u;
+	float4 *dst = qnodes + 8 * (size_t)w;
+	for(int k = 0; k < 8; ++k) dst[k] = make_float4(__uint_as_float(o[4 * k]), __uint_as_float(o[4 * k + 1]), __uint_as_float(o[4 * k + 2]), __uint_as_float(o[4 * k + 3]));
+}
+
 // bvh.cc packTriangle, same float operations (the eps of the exact test must match the oracle's)
 __global__ void __launch_bounds__(kB) k_pack(const int *order, int n, const float *verts, const int *tris, float4 *out)
 {
@@ -520,10 +623,27 @@ extern "C" hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tr
 	BVCHECK(collapse(std::integral_constant<int, 4>{}, nodes.as<float4>(), n_nodes, depth, stack_need));
 	if(w8)
 	{
-		DevBuf nodes8;
+		// the 8-wide collapse in float, then quantised (k_q8_*) with the leaves' triangles in node order
+		DevBuf nodes8, qnodes, tris8, leaves, base;
 		BVCHECK(nodes8.alloc((size_t)cap_nodes * 16 * sizeof(float4)));
 		BVCHECK(collapse(std::integral_constant<int, 8>{}, nodes8.as<float4>(), &w8->n_nodes, &w8->depth, &w8->stack_need));
-		w8->nodes = nodes8.release();
+		const int n8 = w8->n_nodes;
+		BVCHECK(leaves.alloc((size_t)(n8 + 1) * 4));
+		BVCHECK(base.alloc((size_t)(n8 + 1) * 4));
+		hipLaunchKernelGGL(k_q8_count, dim3(blocks(n8 + 1)), dim3(kB), 0, st, nodes8.as<float4>(), n8, leaves.as<uint32_t>());
+		size_t qb = 0;
+		BVCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, qb, leaves.as<uint32_t>(), base.as<uint32_t>(), n8 + 1, st));
+		DevBuf qtmp;
+		BVCHECK(qtmp.alloc(qb));
+		BVCHECK(hipcub::DeviceScan::ExclusiveSum(qtmp.p, qb, leaves.as<uint32_t>(), base.as<uint32_t>(), n8 + 1, st));
+		BVCHECK(qnodes.alloc((size_t)std::max(1, n8) * 8 * sizeof(float4)));
+		BVCHECK(tris8.alloc((size_t)n * 3 * sizeof(float4)));
+		hipLaunchKernelGGL(k_q8_write, dim3(blocks(n8)), dim3(kB), 0, st, nodes8.as<float4>(), n8, base.as<uint32_t>(), trisb.as<float4>(),
+		                   qnodes.as<float4>(), tris8.as<float4>());
+		BVCHECK(hipGetLastError());
+		BVCHECK(hipStreamSynchronize(st));
+		w8->nodes = qnodes.release();
+		w8->tris = tris8.release();
 	}
 	*nodes_out = nodes.release();
 	*tris_out = trisb.release();

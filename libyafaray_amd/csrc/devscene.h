@@ -187,7 +187,8 @@ struct DevScene
 	int ray_sort;                  // k_trace orders each wave's window of queue entries by ray kind + direction (LDS counting sort)
 	int lds_nodes, lds_tris;
 	int lds_top;                   // BVH4 in global memory: k_trace stages nodes [0, lds_top) in LDS (the top treelet)
-	const float4 *nodes8;          // BVH8 of a device-built tree (16 float4 per node) for k_trace's refill loop, or null
+	const float4 *nodes8;          // quantised BVH8 of a device-built tree (8 float4 per node) for k_trace's refill loop, or null
+	const float4 *tris8;           // its triangle records (leaves in node order)
 	int lds_top8;                  // its nodes k_trace stages in LDS
 	// meshlight triangles (DevLight::mesh0 / mesh_n): kMeshTriF4 float4 each — the exact-test record
 	// (v0 + eps, e1 + index, e2), the vertices v0, v1, v2 and the geometric normal — and the area

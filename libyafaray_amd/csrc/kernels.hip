@@ -1100,36 +1100,37 @@ __device__ void traceRefill4(const TraceCtx &C, const DevQueues &Q, const DevPat
 	}
 }
 
-// ---- BVH8 (bvhgpu.hip's 8-wide collapse of the device-built tree, scenes in global memory) ----
-// Node: 16 float4 = lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, child, count as eight-lane arrays (two float4
-// each).  Leaves of the device build hold one triangle (count 1), empty slots an inverted box, so a
-// visit reads the six plane arrays and the children: 14 float4 in two 128-B lines.  Half as many
-// dependent node fetches per ray as the BVH4 (≈ 10 levels of four → ≈ 6–7 of eight) for twice the box
-// tests per fetch: the trade k_trace wants where its visits are L2 / MALL latency (C4) and not VALU (C2,
-// whose tree stays a BVH4 in LDS).  Hits are the BVH4's: the same exact triangle test, ties to the lower
-// primitive, conservative padded boxes and slack.
+// ---- quantised BVH8 (bvhgpu.hip k_q8_write: the device-built tree collapsed to eight children, child
+// boxes as bytes over a per-node origin and power-of-two quanta, rounded outwards; opt-in for scenes in
+// global memory).  A visit reads 80 B (one line): origin, quanta, child masks, the first inner child, the
+// first leaf triangle (the BVH8's own triangle array, leaves in node order) and the six byte planes;
+// the slab test decodes t = q · (2^e / d) + (origin − o) / d.  The decoded boxes contain the float boxes
+// (which carry the BVH4's padding), the triangle test and the tie rule are the BVH4's: the same hits.
 #ifndef YAF_W8_SORT
 #define YAF_W8_SORT 1
 #endif
-constexpr int kTop8Stride = 17;   // float4 per staged BVH8 node in LDS (16 used + 1 pad: 68 dwords)
-__device__ __forceinline__ float lane8(const float4 &a, const float4 &b, int k) { return k < 4 ? lane4(a, k) : lane4(b, k - 4); }
+constexpr int kTop8Stride = 5;   // float4 per staged node in LDS (the 80 B a visit reads: 20 dwords, so 16
+                                 // consecutive nodes start on 16 distinct bank quads)
+__device__ __forceinline__ float q8Byte(uint32_t lo4, uint32_t hi4, int k)
+{
+	const uint32_t w = k < 4 ? lo4 : hi4;
+	return (float)((w >> (8 * (k & 3))) & 0xffu);   // (v_cvt_f32_ubyteN)
+}
 
 template<bool SPILL, bool STATS = true>
 __device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPaths &P, uint32_t n_a, uint32_t total,
                              uint32_t a0, uint32_t s0, uint32_t j, uint32_t stride, uint32_t &visits, uint32_t &tests,
                              uint32_t &n_closest, uint32_t &n_shadow)
 {
-	const int lane = threadIdx.x;
 	const uint32_t glane = blockIdx.x * blockDim.x + threadIdx.x;
 	const float inf = __builtin_huge_valf();
-	V3 o = v3(0.f, 0.f, 0.f), d = o, id = o, oid = o;
-	SlabSel sel{0, 2, 4};
+	V3 o = v3(0.f, 0.f, 0.f), d = o, id = o;
 	float tmin = 0.f, tmax = 0.f, box_t0 = 0.f, t_best = 0.f;
 	int prim_best = -1, sp = 0, node = -1;
 	bool any = false;
 	uint32_t cur = 0;
 	auto push = [&](int v) {
-		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + lane] = v;
+		if(sp < C.lds_depth) C.stack[sp * kTraceBlock + (int)tidFrom(C.wave_base)] = v;
 		else if(SPILL) C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane] = v;
 	};
 	for(;;)
@@ -1170,8 +1171,6 @@ __device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPat
 			if(fabsf(dq.y) < 1e-20f) dq.y = copysignf(1e-20f, dq.y);
 			if(fabsf(dq.z) < 1e-20f) dq.z = copysignf(1e-20f, dq.z);
 			id = v3(rcpExact(dq.x), rcpExact(dq.y), rcpExact(dq.z));
-			oid = v3(o.x * id.x, o.y * id.y, o.z * id.z);
-			sel = slabSel(id);
 			box_t0 = any ? -1e-3f : (tmin - 1e-3f * (1.f + fabsf(tmin)));
 			t_best = tmax;
 			prim_best = -1;
@@ -1179,57 +1178,59 @@ __device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPat
 			node = 0;
 		}
 		if(STATS) TRACE_STAT(++visits);
-		float4 nx0, nx1, fx0, fx1, ny0, ny1, fy0, fy1, nz0, nz1, fz0, fz1, c0, c1;
+		float4 n0, n1, n2, n3, n4;
+		if(node < C.n_top)
 		{
-			// plane p of the node = float4s 2p, 2p + 1; sel picks the near / far plane per axis
-			const int px = 2 * sel.nx, py = 2 * sel.ny, pz = 2 * sel.nz, qx = 2 * (sel.nx ^ 1), qy = 2 * (sel.ny ^ 1), qz = 2 * (sel.nz ^ 1);
-			if(node < C.n_top)
-			{
-				typedef float V4 __attribute__((ext_vector_type(4)));
-				typedef const __attribute__((address_space(3))) V4 *LdsV4;
-				const LdsV4 tp = (LdsV4)(C.top + kTop8Stride * node);
-				auto ld = [&](int k) {
-					const V4 v = tp[k];
-					return make_float4(v.x, v.y, v.z, v.w);
-				};
-				nx0 = ld(px); nx1 = ld(px + 1); fx0 = ld(qx); fx1 = ld(qx + 1);
-				ny0 = ld(py); ny1 = ld(py + 1); fy0 = ld(qy); fy1 = ld(qy + 1);
-				nz0 = ld(pz); nz1 = ld(pz + 1); fz0 = ld(qz); fz1 = ld(qz + 1);
-				c0 = ld(12); c1 = ld(13);
-			}
-			else
-			{
-				const float4 *np = C.nodes + 16 * node;
-				nx0 = np[px]; nx1 = np[px + 1]; fx0 = np[qx]; fx1 = np[qx + 1];
-				ny0 = np[py]; ny1 = np[py + 1]; fy0 = np[qy]; fy1 = np[qy + 1];
-				nz0 = np[pz]; nz1 = np[pz + 1]; fz0 = np[qz]; fz1 = np[qz + 1];
-				c0 = np[12]; c1 = np[13];
-			}
+			typedef float V4 __attribute__((ext_vector_type(4)));
+			typedef const __attribute__((address_space(3))) V4 *LdsV4;
+			const LdsV4 tp = (LdsV4)(C.top + kTop8Stride * node);
+			auto ld = [&](int k) {
+				const V4 v = tp[k];
+				return make_float4(v.x, v.y, v.z, v.w);
+			};
+			n0 = ld(0); n1 = ld(1); n2 = ld(2); n3 = ld(3); n4 = ld(4);
 		}
+		else
+		{
+			const float4 *np = C.nodes + 8 * node;
+			n0 = np[0]; n1 = np[1]; n2 = np[2]; n3 = np[3]; n4 = np[4];
+		}
+		const uint32_t meta = __float_as_uint(n0.w);
+		const uint32_t inner = meta >> 24, leaf = __float_as_uint(n1.x) & 0xffu;
+		const int inner_base = __float_as_int(n1.y), tri_base = __float_as_int(n1.z);
+		// per axis: t of plane q = q * A + B (A = 2^e / d, B = (origin - o) / d), near / far byte rows by the sign of 1/d
+		const float ax = __uint_as_float((meta & 0xffu) << 23) * id.x, ay = __uint_as_float(((meta >> 8) & 0xffu) << 23) * id.y,
+		            az = __uint_as_float(((meta >> 16) & 0xffu) << 23) * id.z;
+		const float bx = (n0.x - o.x) * id.x, by = (n0.y - o.y) * id.y, bz = (n0.z - o.z) * id.z;
+		const bool px = id.x >= 0.f, py = id.y >= 0.f, pz = id.z >= 0.f;
+		const uint32_t nx0 = __float_as_uint(px ? n2.x : n2.z), nx1 = __float_as_uint(px ? n2.y : n2.w);
+		const uint32_t fx0 = __float_as_uint(px ? n2.z : n2.x), fx1 = __float_as_uint(px ? n2.w : n2.y);
+		const uint32_t ny0 = __float_as_uint(py ? n3.x : n3.z), ny1 = __float_as_uint(py ? n3.y : n3.w);
+		const uint32_t fy0 = __float_as_uint(py ? n3.z : n3.x), fy1 = __float_as_uint(py ? n3.w : n3.y);
+		const uint32_t nz0 = __float_as_uint(pz ? n4.x : n4.z), nz1 = __float_as_uint(pz ? n4.y : n4.w);
+		const uint32_t fz0 = __float_as_uint(pz ? n4.z : n4.x), fz1 = __float_as_uint(pz ? n4.w : n4.y);
 		const float slack_t = (t_best < 3.0e38f) ? t_best * 1.0000005f + 1e-6f : 3.4e38f;
 		float key[8];
-		int child[8], e[8], s8[8];
-		int acc = 0;
+		int child[8];
+		uint32_t leaves = 0;
 #pragma unroll
 		for(int k = 0; k < 8; ++k)
 		{
-			const float lo = fmaxf(fmaxf(__builtin_fmaf(lane8(nx0, nx1, k), id.x, -oid.x), __builtin_fmaf(lane8(ny0, ny1, k), id.y, -oid.y)),
-			                       fmaxf(__builtin_fmaf(lane8(nz0, nz1, k), id.z, -oid.z), box_t0));
-			const float hi = fminf(fminf(__builtin_fmaf(lane8(fx0, fx1, k), id.x, -oid.x), __builtin_fmaf(lane8(fy0, fy1, k), id.y, -oid.y)),
-			                       fminf(__builtin_fmaf(lane8(fz0, fz1, k), id.z, -oid.z), slack_t));
+			const float lo = fmaxf(fmaxf(__builtin_fmaf(q8Byte(nx0, nx1, k), ax, bx), __builtin_fmaf(q8Byte(ny0, ny1, k), ay, by)),
+			                       fmaxf(__builtin_fmaf(q8Byte(nz0, nz1, k), az, bz), box_t0));
+			const float hi = fminf(fminf(__builtin_fmaf(q8Byte(fx0, fx1, k), ax, bx), __builtin_fmaf(q8Byte(fy0, fy1, k), ay, by)),
+			                       fminf(__builtin_fmaf(q8Byte(fz0, fz1, k), az, bz), slack_t));
 			const uint32_t h = lo <= hi ? 1u : 0u;
-			child[k] = __float_as_int(lane8(c0, c1, k));
-			const uint32_t inner = child[k] >= 0 ? 1u : 0u;
-			key[k] = (h & inner) ? lo : inf;
-			s8[k] = ~child[k] - acc;
-			acc += (h & (inner ^ 1u)) ? 1 : 0;   // a hit leaf: its one triangle
-			e[k] = acc;
+			const uint32_t isi = (inner >> k) & 1u;
+			key[k] = (h & isi) ? lo : inf;
+			child[k] = inner_base + __builtin_popcount(inner & ((1u << k) - 1u));
+			leaves |= (h & (leaf >> k) & 1u) << k;
 		}
 		bool done = false;
-		for(int i = 0; i < e[7]; ++i)
+		for(uint32_t m = leaves; m; m &= m - 1u)
 		{
-			const int q = i + (i < e[0] ? s8[0] : i < e[1] ? s8[1] : i < e[2] ? s8[2] : i < e[3] ? s8[3]
-			                   : i < e[4] ? s8[4] : i < e[5] ? s8[5] : i < e[6] ? s8[6] : s8[7]);
+			const int k = __builtin_ctz(m);
+			const int q = tri_base + __builtin_popcount(leaf & ((1u << k) - 1u));
 			if(STATS) TRACE_STAT(++tests);
 			const float4 *tp = C.tris + 3 * q;
 			const float4 ta = tp[0], tb = tp[1], tc = tp[2];
@@ -1246,39 +1247,32 @@ __device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPat
 				prim_best = prim;
 			}
 		}
-		if(!done && !YAF_W8_SORT)
+		if(!done)
 		{
-			// (tuning variant) the nearest hit child descended, the others pushed in node order
-			int kmin = 0;
-#pragma unroll
-			for(int k = 1; k < 8; ++k) kmin = key[k] < key[kmin] ? k : kmin;
-			int next = key[kmin] < inf ? child[kmin] : -1;
-#pragma unroll
-			for(int k = 7; k >= 0; --k)
-				if(k != kmin && key[k] < inf) { push(child[k]); ++sp; }
-			if(next < 0 && sp > 0)
+			if(YAF_W8_SORT)
 			{
-				--sp;
-				next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + lane]
-				                                    : C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane];
+				// Batcher's odd-even merge network (19 compare-exchanges): nearest child descended first, the
+				// others pushed farthest first
+				cswap(key[0], child[0], key[1], child[1]); cswap(key[2], child[2], key[3], child[3]);
+				cswap(key[4], child[4], key[5], child[5]); cswap(key[6], child[6], key[7], child[7]);
+				cswap(key[0], child[0], key[2], child[2]); cswap(key[1], child[1], key[3], child[3]);
+				cswap(key[4], child[4], key[6], child[6]); cswap(key[5], child[5], key[7], child[7]);
+				cswap(key[1], child[1], key[2], child[2]); cswap(key[5], child[5], key[6], child[6]);
+				cswap(key[0], child[0], key[4], child[4]); cswap(key[1], child[1], key[5], child[5]);
+				cswap(key[2], child[2], key[6], child[6]); cswap(key[3], child[3], key[7], child[7]);
+				cswap(key[2], child[2], key[4], child[4]); cswap(key[3], child[3], key[5], child[5]);
+				cswap(key[1], child[1], key[2], child[2]); cswap(key[3], child[3], key[4], child[4]);
+				cswap(key[5], child[5], key[6], child[6]);
 			}
-			node = next;
-			done = next < 0;
-		}
-		else if(!done)
-		{
-			// Batcher's odd-even merge network (19 compare-exchanges): nearest child descended first, the
-			// others pushed farthest first
-			cswap(key[0], child[0], key[1], child[1]); cswap(key[2], child[2], key[3], child[3]);
-			cswap(key[4], child[4], key[5], child[5]); cswap(key[6], child[6], key[7], child[7]);
-			cswap(key[0], child[0], key[2], child[2]); cswap(key[1], child[1], key[3], child[3]);
-			cswap(key[4], child[4], key[6], child[6]); cswap(key[5], child[5], key[7], child[7]);
-			cswap(key[1], child[1], key[2], child[2]); cswap(key[5], child[5], key[6], child[6]);
-			cswap(key[0], child[0], key[4], child[4]); cswap(key[1], child[1], key[5], child[5]);
-			cswap(key[2], child[2], key[6], child[6]); cswap(key[3], child[3], key[7], child[7]);
-			cswap(key[2], child[2], key[4], child[4]); cswap(key[3], child[3], key[5], child[5]);
-			cswap(key[1], child[1], key[2], child[2]); cswap(key[3], child[3], key[4], child[4]);
-			cswap(key[5], child[5], key[6], child[6]);
+			else
+			{
+				int kmin = 0;
+#pragma unroll
+				for(int k = 1; k < 8; ++k) kmin = key[k] < key[kmin] ? k : kmin;
+#pragma unroll
+				for(int k = 1; k < 8; ++k)
+					if(k == kmin) { cswap(key[0], child[0], key[k], child[k]); }
+			}
 #pragma unroll
 			for(int k = 7; k >= 1; --k)
 				if(key[k] < inf) { push(child[k]); ++sp; }
@@ -1286,7 +1280,7 @@ __device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPat
 			if(next < 0 && sp > 0)
 			{
 				--sp;
-				next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + lane]
+				next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + (int)tidFrom(C.wave_base)]
 				                                    : C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane];
 			}
 			node = next;
@@ -1321,7 +1315,7 @@ __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tm
 #define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(YAF_TRACE_WAVES)))
 #else
 #ifndef YAF_TRACE8_WAVES
-#define YAF_TRACE8_WAVES 4
+#define YAF_TRACE8_WAVES 6
 #endif
 #define YAF_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LDS_SCENE ? 8 : (W8 ? YAF_TRACE8_WAVES : 6))))
 #endif
@@ -1438,10 +1432,11 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 		if constexpr(W8)
 		{
 			C.nodes = S.nodes8;
+			C.tris = S.tris8;
 			if(S.lds_top8 > 0)
 			{
 				float4 *top = smem + (stack_depth * kTraceBlock) / 4;
-				for(int k = threadIdx.x; k < 16 * S.lds_top8; k += blockDim.x) top[(k >> 4) * kTop8Stride + (k & 15)] = S.nodes8[k];
+				for(int k = threadIdx.x; k < 5 * S.lds_top8; k += blockDim.x) top[(k / 5) * kTop8Stride + (k % 5)] = S.nodes8[8 * (k / 5) + (k % 5)];
 				__syncthreads();
 				C.top = top;
 				C.n_top = S.lds_top8;

@@ -248,7 +248,7 @@ struct GpuRenderer::Impl
 	bool ok = false, init_done = false;
 	hipStream_t stream = nullptr;
 	Buf nodes, tris, prim_ng, mats, lights, faure, faure_dim, faure_inv;
-	Buf nodes8;                 // BVH8 of the device-built tree (k_trace's refill loop), or empty
+	Buf nodes8, tris8;          // quantised BVH8 of the device-built tree and its triangles (k_trace's refill loop), or empty
 	int n_nodes8 = 0, need8 = 0, lds_top8 = 0;
 	// surface attributes, textures and shader-node programs (texeval.h)
 	Buf prim_attr, shader_nodes, textures, texels;
@@ -518,22 +518,24 @@ bool GpuRenderer::upload(HostScene &hs)
 		d.nodes.release();
 		d.tris.release();
 		d.nodes8.release();
+		d.tris8.release();
 		void *np = nullptr, *tp = nullptr;
 		int nn = 0, depth = 0, need = 0, iters = 0;
-		// opt-in YAFARAY_AMD_BVH8=1: the 8-wide collapse too, traversed by k_trace's refill loop for scenes in
-		// global memory.  Measured on C4: 6.78 node visits per ray instead of 10.04, but k_trace
-		// 141 -> 162 ms per frame (106 VGPRs: 4 waves per SIMD instead of 6, twice the box tests and a 19-exchange
-		// sort per visit) — the BVH4 stays the default
+		// the 8-wide collapse too, quantised (bvhgpu.hip k_q8_write), traversed by k_trace's refill loop for
+		// scenes in global memory: C4 k_trace 140 -> 125 ms per frame (the float BVH8 was slower:
+		// 106 VGPRs); YAFARAY_AMD_BVH8=0 keeps the BVH4 there
 		const char *b8 = std::getenv("YAFARAY_AMD_BVH8");
 		YafBvh8 w8;
 		const hipError_t e = yafamd_build_bvh_gpu((const float *)v.p, (const int *)t.p, hs.n_prims, &np, &tp, &nn, &depth, &need, &iters,
-		                                          (b8 && *b8 == '1') ? &w8 : nullptr, d.stream);
+		                                          (b8 && *b8 == '0') ? nullptr : &w8, d.stream);
 		v.release();
 		t.release();
 		if(w8.nodes)
 		{
 			d.nodes8.p = w8.nodes;
-			d.nodes8.bytes = (size_t)std::max(1, w8.n_nodes) * 256;
+			d.nodes8.bytes = (size_t)std::max(1, w8.n_nodes) * 128;
+			d.tris8.p = w8.tris;
+			d.tris8.bytes = (size_t)std::max(1, hs.n_prims) * 48;
 			d.n_nodes8 = w8.n_nodes;
 			d.need8 = w8.stack_need;
 		}
@@ -552,6 +554,7 @@ bool GpuRenderer::upload(HostScene &hs)
 	else
 	{
 		d.nodes8.release();
+		d.tris8.release();
 		d.n_nodes8 = 0;
 		if(!allocCopy(log_, d.nodes, hs.bvh.nodes.data(), hs.bvh.nodes.size())) return false;
 		if(!allocCopy(log_, d.tris, hs.bvh.tris.data(), hs.bvh.tris.size())) return false;
@@ -656,21 +659,21 @@ bool GpuRenderer::upload(HostScene &hs)
 			d.lds_top = fit;
 		}
 	}
-	// the BVH8's top treelet: the root and its eight children (272 B per node, kernels.hip kTop8Stride)
+	// the BVH8's top treelet: the root and its eight children (80 B per node, kernels.hip kTop8Stride)
 	d.lds_top8 = 0;
 	if(d.nodes8.p && !d.scene_in_lds)
 	{
 		int top = 9;
 		if(const char *e = getenv("YAFARAY_AMD_LDS_TOP8"); e && *e) top = std::max(0, atoi(e));
 		const size_t stack_b = (size_t)d.lds_stack * yafamd_trace_block() * 4, lds_max = 64 * 1024;
-		const int fit = stack_b >= lds_max ? 0 : (int)((lds_max - stack_b) / 272);
+		const int fit = stack_b >= lds_max ? 0 : (int)((lds_max - stack_b) / 80);
 		d.lds_top8 = std::min(std::min(top, d.n_nodes8), fit);
 	}
 	{
 		// persistent trace grid = every resident workgroup once (LDS: per-lane stack (+ scene copy or top treelet))
 		const bool w8 = d.nodes8.p && !d.scene_in_lds;
 		const size_t dyn = (size_t)d.lds_stack * yafamd_trace_block() * 4 +
-		                   (d.scene_in_lds ? scene_bytes : w8 ? (size_t)d.lds_top8 * 272 : (size_t)d.lds_top * 144);
+		                   (d.scene_in_lds ? scene_bytes : w8 ? (size_t)d.lds_top8 * 80 : (size_t)d.lds_top * 144);
 		d.trace_grid = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(d.scene_in_lds ? 1 : 0, w8 ? 8 : (d.node_f4 == 8 ? 1 : 0), dyn));
 		if(const char *e = getenv("YAFARAY_AMD_TRACE_GRID")) d.trace_grid = std::max(1, atoi(e));
 		// a whole number of workgroups per queue segment
@@ -728,6 +731,7 @@ static void fillScenePointers(GpuRenderer::Impl &d, DevScene &S)
 	S.tris = (const float4 *)d.tris.p;
 	S.nodes8 = (d.nodes8.p && !d.scene_in_lds) ? (const float4 *)d.nodes8.p : nullptr;
 	S.lds_top8 = d.lds_top8;
+	S.tris8 = (const float4 *)d.tris8.p;
 	S.prim_ng = (const float4 *)d.prim_ng.p;
 	S.mats = (const DevMaterial *)d.mats.p;
 	S.lights = (const DevLight *)d.lights.p;
