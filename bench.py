@@ -46,6 +46,8 @@ import numpy as np  # noqa: E402
 
 METRIC = "Mrays/sec + Msamples/sec, 1920×1080×64spp path-trace at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# bytes a traversal visit reads per node: BVH2 64, BVH4 128, quantised BVH8 80 (the first 80 B of its 128-B node)
+NODE_BYTES = {2: 64.0, 4: 128.0, 8: 80.0}
 LDS_PEAK_GBS = 256 * 256 * 2.4   # 256 CUs x 256 B/clk (ds_read_b128, MI355X_MICROARCH.md §LDS) x 2.4 GHz
 VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instructions: 4 SIMD-32 per CU, 2 cycles each (MI355X_MICROARCH.md)
 
@@ -143,7 +145,7 @@ def algo_bytes(kind, s, kt, in_lds, a, kt_all=None):
         # ray I/O: closest 24 B in (12-B origin + direction records; the camera rays' 8-B (tmin, tmax)
         # ignored) + 8 B out (t, prim); shadow 32 B in (o + index, d + tmax) + 1 B out; traversal bytes
         # (128 B per BVH4 node, 48 B per triangle) only when the scene is not LDS-resident
-        trav = (128.0 if s["bvh_width"] == 4 else 64.0) * s["node_visits"] + 48.0 * s["tri_tests"]
+        trav = NODE_BYTES.get(s["bvh_width"], 64.0) * s["node_visits"] + 48.0 * s["tri_tests"]
         return 32.0 * s["closest_rays"] + 33.0 * s["shadow_rays"] + (0.0 if in_lds else trav)
     if kind == "k_shade":
         return 64.0 * it          # §8d: path-state read + write per path segment
@@ -491,7 +493,7 @@ def dominant_roofline(s, kt, kernels, pmc, scene=None):
         else:
             roof["model"] = "ray I/O (the LDS-resident scene's traversal bytes never reach HBM)"
     if kind == "k_trace":
-        trav = (128.0 if s["bvh_width"] == 4 else 64.0) * s["node_visits"] + 48.0 * s["tri_tests"]
+        trav = NODE_BYTES.get(s["bvh_width"], 64.0) * s["node_visits"] + 48.0 * s["tri_tests"]
         rate = trav / launches / (avg_ms * 1e-3) / 1e9
         rays = max(1, s["closest_rays"] + s["shadow_rays"])
         roof["traversal"] = {"bytes_per_launch": round(trav / launches), "served_from": "LDS" if s["scene_in_lds"] else "L2/MALL/HBM",

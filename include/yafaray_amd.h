@@ -38,7 +38,7 @@ typedef struct
 	double render_seconds;      /* GPU wall time of the sample loop + film (hipEvent) */
 	double trace_kernel_ms;     /* summed k_trace time (hipEvent pairs), 0 if not profiled */
 	uint64_t trace_launches;
-	uint32_t bvh_nodes, bvh_depth, scene_in_lds, bvh_width;   /* bvh_width: 2 or 4 children per node */
+	uint32_t bvh_nodes, bvh_depth, scene_in_lds, bvh_width;   /* bvh_width: children per node of the tree k_trace traverses (2, 4, or 8: the quantised BVH8) */
 	uint32_t trace_grid, shade_grid;   /* persistent grids (workgroups) of k_trace / k_shade */
 	uint32_t trace_block, stack_depth;
 	double shade_kernel_ms;     /* summed k_shade time (hipEvent pairs), 0 if not profiled */

@@ -714,9 +714,9 @@ bool GpuRenderer::upload(HostScene &hs)
 	}
 	if(!allocCopy(log_, d.faure_dim, fdim.data(), fdim.size())) return false;
 	if(!allocCopy(log_, d.faure_inv, inv.data(), inv.size())) return false;
-	stats_.bvh_nodes = (uint32_t)d.n_nodes;
+	stats_.bvh_nodes = (uint32_t)((d.nodes8.p && !d.scene_in_lds) ? d.n_nodes8 : d.n_nodes);
 	stats_.bvh_depth = (uint32_t)d.depth;
-	stats_.bvh_width = d.node_f4 == 8 ? 4u : 2u;
+	stats_.bvh_width = (d.nodes8.p && !d.scene_in_lds) ? 8u : d.node_f4 == 8 ? 4u : 2u;   // the tree k_trace traverses
 	stats_.scene_in_lds = d.scene_in_lds ? 1u : 0u;
 	stats_.trace_grid = (uint32_t)d.trace_grid;
 	stats_.shade_grid = (uint32_t)d.shade_grid;
