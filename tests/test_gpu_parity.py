@@ -147,6 +147,38 @@ def test_bvh8_refill_equals_bvh4(product, n_tris, monkeypatch):
     assert sa["closest_rays"] == sb["closest_rays"] and sa["shadow_rays"] == sb["shadow_rays"]
 
 
+@pytest.mark.parametrize("offset", [(1000.0, -500.0, 250.0), (0.0, 0.0, 0.0)])
+def test_bvh8_far_from_origin_and_thin_geometry(product, monkeypatch, offset):
+    """r05: the quantised BVH8's byte planes are rounded outwards over the node origin; geometry far from
+    the origin (large coordinates, small quanta relative to them) and a sliver of near-degenerate triangles
+    must still give the BVH4's hits: bit-identical films (device build, scene in global memory)."""
+    import dataclasses
+    spec = scenes.cornell_sphere(n=40, width=40, height=30, spp=2, bounces=5, rr=True)
+    # a fan of thin triangles (1e-4 wide) across the box
+    base = len(spec.verts)
+    sl = []
+    for k in range(16):
+        x = -0.8 + 0.1 * k
+        sl += [(x, -0.5, 0.2), (x + 1e-4, 0.5, 0.2), (x + 2e-4, 0.0, 1.6)]
+    verts = np.concatenate([spec.verts, np.asarray(sl, np.float32)]) + np.asarray(offset, np.float32)
+    tris = np.concatenate([spec.tris, np.arange(base, base + len(sl), dtype=np.int32).reshape(-1, 3)])
+    tri_mat = np.concatenate([spec.tri_mat, np.zeros(len(sl) // 3, np.int32)])
+    objs = list(spec.objects) + [scenes.Object("slivers", base, len(sl), len(spec.tris), len(sl) // 3)]
+    sh = lambda p: tuple(float(a) + float(b) for a, b in zip(p, offset))
+    cam = dataclasses.replace(spec.camera, from_=sh(spec.camera.from_), to=sh(spec.camera.to), up=sh(spec.camera.up))
+    lights = [dataclasses.replace(l, from_=sh(l.from_), corner=sh(l.corner), point1=sh(l.point1), point2=sh(l.point2)) for l in spec.lights]
+    spec = dataclasses.replace(spec, verts=verts, tris=tris, tri_mat=tri_mat, objects=objs, camera=cam, lights=lights)
+    use_bvh(monkeypatch, "bvh8-global")
+    a, wa, sa = product.render_spec(spec)
+    assert sa["scene_in_lds"] == 0 and sa["bvh_width"] == 8
+    monkeypatch.setenv("YAFARAY_AMD_BVH8", "0")
+    b, wb, sb = product.render_spec(spec)
+    assert sb["bvh_width"] == 4
+    assert np.array_equal(wa, wb)
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+    assert a[..., :3].mean() > 0.0
+
+
 def test_direct_light_test01_matches_oracle(product, oracle_built):
     spec = scenes.test01(96, 96, spp=4)
     rgba, w, st = product.render_spec(spec)
