@@ -495,6 +495,7 @@ struct GatherLogDesc
 	uint32_t cap, seg_cap, j0;
 	uint32_t split;   // k_gather<REPLAY>: the 6-byte split heap where eligible (YAFARAY_AMD_GATHER_HEAP=packed: 0)
 	uint32_t exact;   // k_gather_walk: the exact-radius walk (k <= 64; YAFARAY_AMD_GATHER_WALK=exact), else the bounded walk
+	uint32_t *spill;  // k_gather_walk: far-child stack levels beyond the LDS ones (-DYAF_WALK_LDS_LEVELS), per walk thread
 };
 
 } // namespace yafamd

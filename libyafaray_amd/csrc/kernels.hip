@@ -4967,6 +4967,7 @@ struct GatherLog
 	uint32_t cap;      // entries per query
 	uint32_t seg_cap;  // queue positions per segment in this batch (a multiple of 64)
 	uint32_t j0;       // first queue position of the batch
+	uint32_t *spill = nullptr;   // the walk's stack levels beyond YAF_WALK_LDS_LEVELS ([level][walk thread])
 };
 
 struct GatherArgs
@@ -5103,7 +5104,15 @@ __device__ __forceinline__ int pkLookup(const uint4 *nodes, V3 p, int k, float &
 #ifndef YAF_WALK_K
 #define YAF_WALK_K 64
 #endif
-constexpr int kWalkK = YAF_WALK_K;   // register slots of the walk (>= the search's k)
+constexpr int kWalkK = YAF_WALK_K;
+// The exact walk keeps YAF_WALK_LDS_LEVELS far-child stack levels in LDS and the deeper ones in an HBM
+// column per walk thread (0: every level in LDS): with the 16-bit key slots (68 VGPRs) the 26-level LDS
+// column capped residency at 6 waves per SIMD; 20 levels: C5 walk 14.0 -> 13.3-13.7 ms (16 levels: 14.8,
+// the deeper pushes go to HBM; 22: 13.4-14.1)
+#ifndef YAF_WALK_LDS_LEVELS
+#define YAF_WALK_LDS_LEVELS 20
+#endif
+constexpr int kWalkLdsLevels = YAF_WALK_LDS_LEVELS;   // register slots of the walk (>= the search's k)
 #ifndef YAF_WALK_PER_SEG
 #define YAF_WALK_PER_SEG 16
 #endif
@@ -5121,7 +5130,7 @@ constexpr int kWalkPerSeg = YAF_WALK_PER_SEG;   // walk workgroups per queue seg
 // the distance test agree).  The accepted photons go to this request's log lg[0 ..) in pairs
 // (16-byte stores; the first `cap`); returns how many were accepted.
 #ifndef YAF_WALK_PACK
-#define YAF_WALK_PACK 0
+#define YAF_WALK_PACK 1
 #endif
 #if YAF_WALK_PACK
 // The walk's slots as 16-bit keys, two per VGPR: the bfloat16 bits of each distance rounded UP (for
@@ -5142,8 +5151,15 @@ __device__ __forceinline__ uint32_t pkMinU16(uint32_t a, uint32_t b)
 }
 #endif
 __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, float max_d2, uint2 *lg, uint32_t cap, uint32_t *stk,
-                                           uint32_t &visits)
+                                           uint32_t &visits, int lds_lv = 1 << 30, uint32_t *spill = nullptr, uint32_t spill_stride = 0)
 {
+	auto spush = [&](int lv, uint32_t v) {
+		if(kWalkLdsLevels == 0 || lv < lds_lv) stk[lv * kGatherBlock] = v;
+		else spill[(size_t)(lv - lds_lv) * spill_stride] = v;
+	};
+	auto spop = [&](int lv) -> uint32_t {
+		return (kWalkLdsLevels == 0 || lv < lds_lv) ? stk[lv * kGatherBlock] : spill[(size_t)(lv - lds_lv) * spill_stride];
+	};
 	const float radius2 = max_d2;
 	// (an opaque bound: otherwise the 64 initial values are hoisted out of the request loop and
 	// stay live across every walk — 64 more VGPRs)
@@ -5180,7 +5196,7 @@ __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, floa
 			d2 *= d2;
 			if(d2 <= max_d2)
 			{
-				stk[sp_top * kGatherBlock] = far_child;
+				spush(sp_top, far_child);
 				++sp_top;
 			}
 			nd = nodes[curr];
@@ -5219,7 +5235,7 @@ __device__ __forceinline__ uint32_t pkWalk(const uint4 *nodes, V3 p, int k, floa
 		while(sp_top > 0)
 		{
 			--sp_top;
-			curr = stk[sp_top * kGatherBlock];
+			curr = spop(sp_top);
 			nd = nodes[curr];
 			++visits;
 			if((nd.w & 3u) != 3u)
@@ -5263,9 +5279,15 @@ constexpr int kWalkBins = YAF_WALK_BINS;   // multiple of 4 (four byte counters 
 constexpr int kWalkBinShift = YAF_WALK_BIN_SHIFT;
 static_assert(kWalkBins % 4 == 0, "byte counters in words");
 
+__host__ __device__ inline int walkLdsLevels(int pm_stack)
+{
+	const int all = pm_stack > 1 ? pm_stack : 1;
+	return (kWalkLdsLevels > 0 && kWalkLdsLevels < all) ? kWalkLdsLevels : all;
+}
 __host__ __device__ inline size_t walkLdsBytes(int pm_stack, bool hist)
 {
-	return (size_t)(pm_stack > 1 ? pm_stack : 1) * kGatherBlock * 4u + (hist ? (size_t)kWalkBins * kGatherBlock : 0u);
+	// (the bounded walk keeps its whole stack in LDS)
+	return (size_t)(hist ? (pm_stack > 1 ? pm_stack : 1) : walkLdsLevels(pm_stack)) * kGatherBlock * 4u + (hist ? (size_t)kWalkBins * kGatherBlock : 0u);
 }
 
 __device__ __forceinline__ uint32_t pkWalkBound(const uint4 *nodes, V3 p, int k, float radius2, uint2 *lg, uint32_t cap, uint32_t *stk,
@@ -5369,7 +5391,7 @@ __device__ __forceinline__ uint2 *gatherLogAt(const GatherLog &L, uint32_t q)
 
 // pass 1 over one batch of the gather queue (diffuse-map requests; the others log nothing)
 #ifndef YAF_WALK_WAVES
-#define YAF_WALK_WAVES 5
+#define YAF_WALK_WAVES 6
 #endif
 template<bool BOUND>
 __global__ void __launch_bounds__(kGatherBlock) __attribute__((amdgpu_waves_per_eu(YAF_WALK_WAVES))) k_gather_walk(GatherArgs A)
@@ -5391,7 +5413,8 @@ __global__ void __launch_bounds__(kGatherBlock) __attribute__((amdgpu_waves_per_
 		if(__float_as_uint(A.G.extra[j].w) & G_DIFFUSE)
 		{
 			if(BOUND) n_acc = pkWalkBound(S.pk_nodes, xyz(A.G.p_prim[j]), S.pm_search, S.pm_radius2, gatherLogAt(A.log, q), A.log.cap, stk, hist, visits);
-			else n_acc = pkWalk(S.pk_nodes, xyz(A.G.p_prim[j]), S.pm_search, S.pm_radius2, gatherLogAt(A.log, q), A.log.cap, stk, visits);
+			else n_acc = pkWalk(S.pk_nodes, xyz(A.G.p_prim[j]), S.pm_search, S.pm_radius2, gatherLogAt(A.log, q), A.log.cap, stk, visits,
+			                    walkLdsLevels(S.pm_stack), A.log.spill + (blockIdx.x * blockDim.x + threadIdx.x), gridDim.x * blockDim.x);
 		}
 		A.log.n[q] = n_acc;
 		accepts += n_acc;
@@ -6617,7 +6640,8 @@ hipError_t yafamd_launch_gather_walk(const DevScene *S, const DevNeeQueue *G, co
 	A.jobs = nullptr;
 	A.n_jobs = 0;
 	A.chunk_base = 0;
-	A.log = GatherLog{(uint2 *)log->e, log->n, log->cap, log->seg_cap, log->j0};
+	A.log = GatherLog{(uint2 *)log->e, log->n, log->cap, log->seg_cap, log->j0, log->spill};
+	if(exact && walkLdsLevels(S->pm_stack) < max(1, S->pm_stack) && !log->spill) return hipErrorInvalidValue;
 	const size_t lds = walkLdsBytes(S->pm_stack, !exact);
 	if(exact) hipLaunchKernelGGL(k_gather_walk<false>, dim3(S->n_seg * kWalkPerSeg), dim3(kGatherBlock), lds, st, A);
 #ifdef YAF_EXPERIMENTS
@@ -6627,6 +6651,10 @@ hipError_t yafamd_launch_gather_walk(const DevScene *S, const DevNeeQueue *G, co
 #endif
 	return hipGetLastError();
 }
+
+// k_gather_walk's stack column: levels kept in LDS and the walk grid's threads (render.cc sizes the spill)
+int yafamd_walk_lds_levels(int pm_stack) { return walkLdsLevels(pm_stack); }
+int yafamd_walk_threads(const DevScene *S) { return (int)(S->n_seg * kWalkPerSeg * kGatherBlock); }
 
 // the largest k the two-pass gather serves: the register walk's k; experiments builds also the bounded
 // walk (the split replay heap's 16-bit log positions bound it)

@@ -32,6 +32,8 @@ hipError_t yafamd_launch_trace(const DevScene *S, const DevQueues *Q, const DevC
                                DevStats *stats, int stack_depth, int *spill, int grid, hipStream_t st);
 int yafamd_trace_block();
 int yafamd_shade_fused();
+int yafamd_walk_lds_levels(int pm_stack);
+int yafamd_walk_threads(const DevScene *S);
 int yafamd_shade_fused_for(const DevScene *S);
 int yafamd_experiments();
 int yafamd_trace_blocks_per_cu(int lds_scene, int wide, size_t dyn_lds);
@@ -277,6 +279,7 @@ struct GpuRenderer::Impl
 	Buf seg_pos, seg_dir, seg_colb, seg_ra, seg_rb, seg_rc;
 	Buf fg_ts;   // k_fg's transparent-shadow hit lists (s_depth per lane of the trace grid)
 	Buf g_log, g_log_n;   // the two-pass diffuse gather's accepted-photon log (one batch of the gather queue)
+	Buf walk_spill;       // k_gather_walk's stack levels beyond the LDS ones (tuning builds)
 	// the maps' records in kd (leaf) order, written by the tree build (diffuse, caustic, radiance): the
 	// kernels read these; the arrays above stay in photon order (saveMap, the group concatenation)
 	Buf kd_pos[3], kd_dir[3], kd_colb[3];
@@ -366,7 +369,7 @@ struct GpuRenderer::Impl
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
-		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris}) b->release();
+		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &walk_spill, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris}) b->release();
 		for(int m = 0; m < 3; ++m)
 			for(Buf *b : {&kd_pos[m], &kd_dir[m], &kd_colb[m]}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
@@ -1789,7 +1792,14 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// (walk 13.9 -> 16.3 ms, replay 7.4 -> 12.1 ms per frame: its superset log); without it a larger
 			// k takes the one-pass gather (yafamd_gather_walk_k)
 			const uint32_t exact = (yafamd_experiments() && we && std::string(we) == "bound") ? 0u : 1u;
-			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u, split, exact};
+			glog = GatherLogDesc{d.g_log.p, (uint32_t *)d.g_log_n.p, cap, (uint32_t)seg_cap, 0u, split, exact, nullptr};
+			// the walk's far-child stack levels beyond the LDS ones (tuning builds: -DYAF_WALK_LDS_LEVELS)
+			const int lv = yafamd_walk_lds_levels(d.pm_stack), deep = std::max(1, d.pm_stack) - lv;
+			if(deep > 0)
+			{
+				if(!ensure(log_, d.walk_spill, (size_t)deep * yafamd_walk_threads(&S) * 4)) return false;
+				glog.spill = (uint32_t *)d.walk_spill.p;
+			}
 			walk_gather = true;
 		}
 	}
