@@ -2638,10 +2638,21 @@ __device__ __forceinline__ void copy16(uint4 *dst, const void *src, int n)
 	for(int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = s4[k];
 }
 
+// scenes whose primitive records do not fit (C4) still get their materials in LDS when those are small:
+// the material read after each hit's primitive record is then an LDS access, not a second L2 round trip
+#ifndef YAF_STAGE_MATS
+#define YAF_STAGE_MATS 1
+#endif
+constexpr size_t kStageMatsMax = 8192;
+__host__ __device__ inline bool stageMatsOnly(const DevScene &S, bool small)
+{
+	return YAF_STAGE_MATS && !small && (size_t)S.n_mats * sizeof(DevMaterial) <= kStageMatsMax;
+}
 __host__ __device__ inline size_t shadeLdsBytes(const DevScene &S, bool small)
 {
 	size_t b = 50 * 16 + 25 * 16 + (size_t)S.faure_bytes;
 	if(small) b += (size_t)S.n_mats * sizeof(DevMaterial) + (size_t)S.n_tris * 16;
+	else if(stageMatsOnly(S, small)) b += (size_t)S.n_mats * sizeof(DevMaterial);
 	return b;
 }
 
@@ -2665,6 +2676,13 @@ __device__ __forceinline__ DevScene stageTables(const DevScene &G, uint4 *smem)
 		copy16(p, G.prim_ng, G.n_tris);
 		S.prim_ng = reinterpret_cast<const float4 *>(p);
 		p += G.n_tris;
+	}
+	else if(stageMatsOnly(G, false))
+	{
+		const int nm = G.n_mats * (int)(sizeof(DevMaterial) / 16);
+		copy16(p, G.mats, nm);
+		S.mats = reinterpret_cast<const DevMaterial *>(p);
+		p += nm;
 	}
 	copy16(p, G.faure, G.faure_bytes / 16);
 	S.faure = reinterpret_cast<const uint8_t *>(p);
