@@ -13,7 +13,9 @@
 //
 // The lowest undecided point is always kept, so the rounds end; in practice ~15 rounds decide
 // millions of points (C5: 2.46 M points, 16 K kept).  Neighbours come from a dense uniform grid of cell > sqrt(maxrad) (counting sort by
-// cell); the kept indices are compacted in shooting order.  Host twin: render.cc eliminateRadPoints.
+// cell); the rounds work in cell order (positions, normals and states copied into the counting sort's
+// order, so a cell's entries are read contiguously), and the kept indices are compacted in shooting
+// order at the end.  Host twin: render.cc eliminateRadPoints.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <cmath>
@@ -44,10 +46,10 @@ struct ThinBuf
 // scratch kept between renders (the radiance map is rebuilt every frame); one per renderer
 struct ThinScratch
 {
-	ThinBuf part, cid, count, start, order, st0, st1, counter, tmp, n_sel, klist;
+	ThinBuf part, cid, count, start, order, st0, st1, counter, tmp, n_sel, klist, spos, snrm;
 	~ThinScratch()
 	{
-		for(ThinBuf *b : {&part, &cid, &count, &start, &order, &st0, &st1, &counter, &tmp, &n_sel, &klist})
+		for(ThinBuf *b : {&part, &cid, &count, &start, &order, &st0, &st1, &counter, &tmp, &n_sel, &klist, &spos, &snrm})
 			if(b->p) (void)hipFree(b->p);
 	}
 };
@@ -117,13 +119,33 @@ __global__ void __launch_bounds__(256) k_thin_fill(const uint32_t *cid, uint32_t
 	order[start[c] + atomicAdd(&fill[c], 1u)] = i;   // order inside a cell is irrelevant (marking is idempotent)
 }
 
-// neighbour cells of a point (clamped 3x3x3 block) — the relation's reach is < one cell per axis
+// the points in cell order: spos[k] / snrm[k] of point order[k]
+__global__ void __launch_bounds__(256) k_thin_sort(const float4 *pos, const float4 *nrm, const uint32_t *order, uint32_t n, float4 *spos,
+                                                  float4 *snrm)
+{
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if(k >= n) return;
+	const uint32_t j = order[k];
+	spos[k] = pos[j];
+	snrm[k] = nrm[j];
+}
+
+// the final states back in shooting order
+__global__ void __launch_bounds__(256) k_thin_unsort(const uint8_t *sst, const uint32_t *order, uint32_t n, uint8_t *st)
+{
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if(k < n) st[order[k]] = sst[k];
+}
+
+// neighbour cells of a point (clamped 3x3x3 block) — the relation's reach is < one cell per axis.  The
+// point's own cell comes first (most likely to hold a related point, which ends the keep scan), then
+// the other 26 in z, y, x order
 #define THIN_FOR_CELLS(q)                                                                                      \
 	const int cx_ = axisCell(q.x, g.lo[0], g.inv_cell, g.nx), cy_ = axisCell(q.y, g.lo[1], g.inv_cell, g.ny),   \
 	          cz_ = axisCell(q.z, g.lo[2], g.inv_cell, g.nz);                                                    \
-	for(int z = max(0, cz_ - 1); z <= min(g.nz - 1, cz_ + 1) && !stop; ++z)                                     \
-		for(int y = max(0, cy_ - 1); y <= min(g.ny - 1, cy_ + 1) && !stop; ++y)                                 \
-			for(int x = max(0, cx_ - 1); x <= min(g.nx - 1, cx_ + 1) && !stop; ++x)
+	for(int t_ = 0, u_ = 13; t_ < 27 && !stop; u_ = t_ < 13 ? t_ : t_ + 1, ++t_)                                 \
+		if(const int z = cz_ + u_ / 9 - 1, y = cy_ + (u_ / 3) % 3 - 1, x = cx_ + u_ % 3 - 1;                      \
+		   z >= 0 && z < g.nz && y >= 0 && y < g.ny && x >= 0 && x < g.nx)
 
 // EliminatePhoton's test (pkdtree.h:263-268 strict distance, photon.h:177 normals on one side),
 // symmetric bit for bit in the two points
@@ -140,22 +162,25 @@ __device__ __forceinline__ bool thinRelated(const float4 &p, const float4 &pn, c
 // higher points (part 2), so the dead ones are skipped and the scan stops at the first undecided
 // one.  kKeepLanes lanes per point split the entries of each cell (uniform trip counts inside a
 // group, so every lane of the group sees its vote); one lane per point measured 2.7 ms per round.
+// Everything is indexed by cell-order position p (the point's shooting index is order[p]; states,
+// positions and normals are in cell order, so a group reads a cell's entries contiguously).
 constexpr uint32_t kKeepLanes = 8;
 __global__ void __launch_bounds__(256) k_thin_keep(const float4 *pos, const float4 *nrm, const uint32_t *order, const uint32_t *start,
                                                   ThinGrid g, const uint8_t *sin, uint8_t *sout, uint32_t n, float maxrad, uint32_t *klist,
                                                   uint32_t *n_klist)
 {
 	const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t i = tid / kKeepLanes, sub = tid % kKeepLanes;
+	const uint32_t p = tid / kKeepLanes, sub = tid % kKeepLanes;
 	const uint64_t gmask = ((1ull << kKeepLanes) - 1ull) << (__lane_id() & ~(kKeepLanes - 1u));
-	if(i >= n) return;   // whole groups leave together (n * kKeepLanes threads, groups aligned)
-	const uint8_t s0 = sin[i];
+	if(p >= n) return;   // whole groups leave together (n * kKeepLanes threads, groups aligned)
+	const uint8_t s0 = sin[p];
 	if(s0 != kUndecided)
 	{
-		if(sub == 0) sout[i] = s0;
+		if(sub == 0) sout[p] = s0;
 		return;
 	}
-	const float4 q = pos[i], qn = nrm[i];
+	const uint32_t i = order[p];
+	const float4 q = pos[p], qn = nrm[p];
 	bool stop = false;
 	THIN_FOR_CELLS(q)
 	{
@@ -167,15 +192,14 @@ __global__ void __launch_bounds__(256) k_thin_keep(const float4 *pos, const floa
 			bool hit = false;
 			if(k < k1)
 			{
-				const uint32_t j = order[k];
-				hit = j < i && sin[j] == kUndecided && thinRelated(pos[j], nrm[j], q, qn, maxrad);
+				hit = sin[k] == kUndecided && order[k] < i && thinRelated(pos[k], nrm[k], q, qn, maxrad);
 			}
 			if(__ballot(hit) & gmask) { stop = true; break; }
 		}
 	}
 	if(sub == 0)
 	{
-		sout[i] = stop ? kUndecided : kKept;
+		sout[p] = stop ? kUndecided : kKept;
 		// part 2 works on this list (its order is irrelevant: the kills are idempotent); one atomic per
 		// wave on the list's single counter instead of one per kept point
 		const uint64_t want = __ballot(!stop);
@@ -185,7 +209,7 @@ __global__ void __launch_bounds__(256) k_thin_keep(const float4 *pos, const floa
 			uint32_t base = 0;
 			if(__lane_id() == leader) base = atomicAdd(n_klist, (uint32_t)__popcll(want));
 			base = __shfl(base, (int)leader);
-			if(!stop) klist[base + (uint32_t)__popcll(want & ((1ull << __lane_id()) - 1ull))] = i;
+			if(!stop) klist[base + (uint32_t)__popcll(want & ((1ull << __lane_id()) - 1ull))] = p;
 		}
 	}
 }
@@ -202,8 +226,8 @@ __global__ void __launch_bounds__(256) k_thin_kill(const float4 *pos, const floa
 	const uint32_t nk = *n_klist;
 	for(uint32_t t = wave; t < nk; t += n_waves)
 	{
-		const uint32_t i = klist[t];
-		const float4 q = pos[i], qn = nrm[i];
+		const uint32_t p = klist[t], i = order[p];
+		const float4 q = pos[p], qn = nrm[p];
 		const int cx = axisCell(q.x, g.lo[0], g.inv_cell, g.nx), cy = axisCell(q.y, g.lo[1], g.inv_cell, g.ny),
 		          cz = axisCell(q.z, g.lo[2], g.inv_cell, g.nz);
 		for(int z = max(0, cz - 1); z <= min(g.nz - 1, cz + 1); ++z)
@@ -214,8 +238,7 @@ __global__ void __launch_bounds__(256) k_thin_kill(const float4 *pos, const floa
 					const uint32_t k1 = start[c + 1];
 					for(uint32_t k = start[c] + lane; k < k1; k += 64)
 					{
-						const uint32_t j = order[k];
-						if(j > i && thinRelated(pos[j], nrm[j], q, qn, maxrad)) sout[j] = kDead;
+						if(order[k] > i && thinRelated(pos[k], nrm[k], q, qn, maxrad)) sout[k] = kDead;
 					}
 				}
 	}
@@ -294,6 +317,8 @@ extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nr
 	THCHECK(S.counter.ensure(16));
 	THCHECK(S.klist.ensure((size_t)n * 4));
 	THCHECK(S.n_sel.ensure(16));
+	THCHECK(S.spos.ensure((size_t)n * sizeof(float4)));
+	THCHECK(S.snrm.ensure((size_t)n * sizeof(float4)));
 	THCHECK(hipMemsetAsync(S.count.p, 0, ((size_t)nc + 1) * 4, st));
 	const dim3 blocks((n + 255) / 256);
 	hipLaunchKernelGGL(k_thin_cells, blocks, dim3(256), 0, st, pos, n, g, S.cid.as<uint32_t>(), S.count.as<uint32_t>());
@@ -308,6 +333,8 @@ extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nr
 	THCHECK(hipMemsetAsync(S.count.p, 0, ((size_t)nc + 1) * 4, st));
 	hipLaunchKernelGGL(k_thin_fill, blocks, dim3(256), 0, st, S.cid.as<uint32_t>(), n, S.start.as<uint32_t>(), S.count.as<uint32_t>(),
 	                   S.order.as<uint32_t>());
+	hipLaunchKernelGGL(k_thin_sort, blocks, dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), n, S.spos.as<float4>(), S.snrm.as<float4>());
+	const float4 *spos = S.spos.as<float4>(), *snrm = S.snrm.as<float4>();
 	THCHECK(hipMemsetAsync(S.st0.p, kUndecided, n, st));
 	uint8_t *sin = S.st0.as<uint8_t>(), *sout = S.st1.as<uint8_t>();
 	uint32_t undecided = n;
@@ -316,9 +343,9 @@ extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nr
 	{
 		THCHECK(hipMemsetAsync(S.counter.p, 0, 8, st));   // [0] any point undecided (0 / 1), [1] kept-list length
 		uint32_t *n_klist = S.counter.as<uint32_t>() + 1;
-		hipLaunchKernelGGL(k_thin_keep, dim3((uint32_t)(((uint64_t)n * kKeepLanes + 255) / 256)), dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad,
+		hipLaunchKernelGGL(k_thin_keep, dim3((uint32_t)(((uint64_t)n * kKeepLanes + 255) / 256)), dim3(256), 0, st, spos, snrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sin, sout, n, maxrad,
 		                   S.klist.as<uint32_t>(), n_klist);
-		hipLaunchKernelGGL(k_thin_kill, dim3(1024), dim3(256), 0, st, pos, nrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sout,
+		hipLaunchKernelGGL(k_thin_kill, dim3(1024), dim3(256), 0, st, spos, snrm, S.order.as<uint32_t>(), S.start.as<uint32_t>(), g, sout,
 		                   S.klist.as<uint32_t>(), n_klist, maxrad);
 		hipLaunchKernelGGL(k_thin_count, blocks, dim3(256), 0, st, sout, n, S.counter.as<uint32_t>());
 		THCHECK(hipGetLastError());
@@ -328,8 +355,9 @@ extern "C" hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nr
 		++rounds;
 		if(rounds > 1000000) return hipErrorUnknown;   // cannot happen: every round decides the lowest undecided point
 	}
-	// the final states are in `sin`: kept indices in shooting order
-	hipcub::TransformInputIterator<bool, IsKept, hipcub::CountingInputIterator<uint32_t>> kflags(iota, IsKept{sin});
+	// the final states are in `sin` (cell order): back to shooting order in `sout`, then the kept indices
+	hipLaunchKernelGGL(k_thin_unsort, blocks, dim3(256), 0, st, sin, S.order.as<uint32_t>(), n, sout);
+	hipcub::TransformInputIterator<bool, IsKept, hipcub::CountingInputIterator<uint32_t>> kflags(iota, IsKept{sout});
 	THCHECK(hipcub::DeviceSelect::Flagged(S.tmp.p, sel_bytes, iota, kflags, kept_out, S.n_sel.as<uint32_t>(), (int)n, st));
 	THCHECK(hipMemcpyAsync(n_kept, S.n_sel.p, 4, hipMemcpyDeviceToHost, st));
 	THCHECK(hipStreamSynchronize(st));

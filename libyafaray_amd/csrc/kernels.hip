@@ -6042,10 +6042,20 @@ struct FgArgs
 #define YAF_FG_WAVES 4
 #endif
 #define YAF_FG_ATTR __attribute__((amdgpu_waves_per_eu(YAF_FG_WAVES)))
+// YAF_FG_STAGE: an LDS-resident scene's primitive records and materials are staged after the stacks as
+// well (the gather paths' surface lookups from LDS instead of L2)
+#ifndef YAF_FG_STAGE
+#define YAF_FG_STAGE 1
+#endif
+__host__ __device__ inline bool fgStageTables(const DevScene &S, bool lds_scene, bool ext)
+{
+	return YAF_FG_STAGE && lds_scene && !ext && S.small_tables;
+}
 template<bool LDS_SCENE, bool WIDE, bool EXT, bool SPILL = true, bool TSH = false>
 __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 {
-	const DevScene &S = A.S;
+	DevScene S_ = A.S;
+	const DevScene &S = S_;
 	extern __shared__ float4 smem[];
 	TraceCtx C;
 	C.wave_base = waveBase();
@@ -6071,6 +6081,18 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 	// the radiance-map nearest searches' LDS stack column (S.rpk_lds levels), after the stack and scene
 	uint32_t *nstk = reinterpret_cast<uint32_t *>(smem + (A.stack_depth * kTraceBlock) / 4 +
 	                                              (LDS_SCENE ? S.node_f4 * S.n_nodes + 3 * S.n_tris : 0)) + threadIdx.x;
+	if(fgStageTables(A.S, LDS_SCENE, EXT))
+	{
+		// after the nearest-search column (S.rpk_lds levels of one word per lane)
+		uint4 *tp = reinterpret_cast<uint4 *>(smem + (A.stack_depth * kTraceBlock) / 4 + (S.node_f4 * S.n_nodes + 3 * S.n_tris) +
+		                                      ((size_t)S.rpk_lds * kTraceBlock + 3) / 4);
+		const int nm = A.S.n_mats * (int)(sizeof(DevMaterial) / 16);
+		copy16(tp, A.S.mats, nm);
+		copy16(tp + nm, A.S.prim_ng, A.S.n_tris);
+		__syncthreads();
+		S_.mats = reinterpret_cast<const DevMaterial *>(tp);
+		S_.prim_ng = reinterpret_cast<const float4 *>(tp + nm);
+	}
 	auto nearestRad = [&](V3 hp, V3 sf) -> int {
 		return S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, nstk, S.rpk_lds)
 		                     : pkNearest(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad);
@@ -6734,12 +6756,16 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
 	const size_t nstk_bytes = (size_t)S->rpk_lds * kTraceBlock * sizeof(uint32_t);
 	const bool wide = S->node_f4 == 8;
+	// an LDS-resident scene: the column rounded to 16 B, then the staged tables (fgStageTables)
+	const size_t stage_bytes = fgStageTables(*S, S->scene_in_lds != 0, S->ext != 0)
+	                               ? ((nstk_bytes + 15) & ~(size_t)15) + (size_t)S->n_mats * sizeof(DevMaterial) + (size_t)S->n_tris * 16
+	                               : nstk_bytes;
 	if(S->tr_shad)
 	{
 		// transparent shadows (the spilling variants: without a spill column they never spill)
 		if(!ts_scratch) return hipErrorInvalidValue;
 		const size_t bytes = (S->scene_in_lds ? stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) : stack_bytes) +
-		                     nstk_bytes;
+		                     (S->scene_in_lds ? stage_bytes : nstk_bytes);
 #define YAF_FG_LAUNCH_TS(L, W, E) hipLaunchKernelGGL((k_fg<L, W, E, true, true>), dim3(grid), dim3(kTraceBlock), bytes, st, A)
 		if(S->scene_in_lds)
 		{
@@ -6757,7 +6783,7 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 #define YAF_FG_LAUNCH_NS(W, E, B) hipLaunchKernelGGL((k_fg<true, W, E, false>), dim3(grid), dim3(kTraceBlock), B, st, A)
 	if(S->scene_in_lds)
 	{
-		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) + nstk_bytes;
+		const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) + stage_bytes;
 		if(spill == nullptr)   // the LDS levels hold the whole stack bound: plain LDS pushes / pops
 		{
 			if(S->ext) { if(wide) YAF_FG_LAUNCH_NS(true, true, bytes); else YAF_FG_LAUNCH_NS(false, true, bytes); }
