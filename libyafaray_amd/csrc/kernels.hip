@@ -6042,6 +6042,10 @@ struct FgArgs
 #define YAF_FG_WAVES 4
 #endif
 #define YAF_FG_ATTR __attribute__((amdgpu_waves_per_eu(YAF_FG_WAVES)))
+// YAF_FG_REMAT: each gather path rebuilds the request's surface (fewer registers live through the traversals)
+#ifndef YAF_FG_REMAT
+#define YAF_FG_REMAT 1
+#endif
 // YAF_FG_STAGE: an LDS-resident scene's primitive records and materials are staged after the stacks as
 // well (the gather paths' surface lookups from LDS instead of L2)
 #ifndef YAF_FG_STAGE
@@ -6112,13 +6116,24 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 		if(!(__float_as_uint(ex.w) & G_FG)) continue;
 		const uint32_t offset = __float_as_uint(ex.x), sample_idx = __float_as_uint(ex.y);
 		const float4 pp = A.G.p_prim[j];
+#if !YAF_FG_REMAT
 		Surf sp0 = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
 		if(ATTR) applyAttr(sp0, A.G.attr[2 * (size_t)j], A.G.attr[2 * (size_t)j + 1]);
-		const V3 wo0 = xyz(A.G.wo_k[j]);
 		const DevMaterial &m0 = S.mats[sp0.mat];
+#endif
+		const V3 wo0 = xyz(A.G.wo_k[j]);
 		C3 path_col = c3(0.f);
 		for(int i = 0; i < n_sampl; ++i)
 		{
+#if YAF_FG_REMAT
+			// the request's surface is rebuilt for every gather path (bit for bit the same) instead of being
+			// kept in registers through the traversals: the opaque copy keeps it inside the loop
+			float4 ppi = pp;
+			asm volatile("" : "+v"(ppi.x), "+v"(ppi.y), "+v"(ppi.z), "+v"(ppi.w));
+			Surf sp0 = surfFromPrim(S, xyz(ppi), __float_as_int(ppi.w));
+			if(ATTR) applyAttr(sp0, A.G.attr[2 * (size_t)j], A.G.attr[2 * (size_t)j + 1]);
+			const DevMaterial &m0 = S.mats[sp0.mat];
+#endif
 			const uint32_t offs = (uint32_t)S.fg_samples * sample_idx + offset + (uint32_t)i;
 			BsdfSample s;
 			s.s_1 = riVdC(offs);
@@ -6201,7 +6216,16 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 				const V3 sf = faceForward(hit.ng, hit.n, -dir);
 				const int nearest = nearestRad(hit.p, sf);
 				if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
-				if(mat_bsd_fs & B_EMIT) lcol = lcol + matEmit<EXT>(S.mats[hit.mat], hit, -dir);
+				if(mat_bsd_fs & B_EMIT)
+				{
+#if YAF_FG_REMAT
+					// the hit rebuilt (bit for bit) rather than kept live through the nearest search
+					float tt = t;
+					asm volatile("" : "+v"(tt));
+					hit = fgSurf<EXT>(S, from, dir, tt, prim);
+#endif
+					lcol = lcol + matEmit<EXT>(S.mats[hit.mat], hit, -dir);
+				}
 				path_col = path_col + lcol * throughput;
 			}
 		}
