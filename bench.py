@@ -156,10 +156,12 @@ def algo_bytes(kind, s, kt, in_lds, a, kt_all=None):
         # + occlusion byte
         return 36.0 * it + 45.0 * (s["shadow_rays"] / max(1, s["closest_rays"])) * it
     if kind == "k_camera":
-        # camera ray (12-B origin + direction records) 24 B + the compact record (sample id, stage, MWC)
-        # 16 B: a camera entry's zero throughput / colour / flags are implied by its stage (§8d counted
-        # 64 B of initial state); the per-ray (tmin, tmax) 8 B only with clip planes (not counted)
-        return 40.0 * it
+        # camera ray (12-B origin + direction records) 24 B + the 8-B compact record (sample id + stage; the
+        # r05 stateless RR draw keeps no MWC state in it): 32 B per sample, as kernels.hip k_camera writes
+        # and PMC WRITE_SIZE measures (32.0 B x samples); a camera entry's zero throughput / colour / flags
+        # are implied by its stage (§8d counted 64 B of initial state); the per-ray (tmin, tmax) 8 B only
+        # with clip planes (not counted)
+        return 32.0 * it
     if kind == "k_film":
         return 16.0 * it + 20.0 * a.width * a.height   # the samples (float4) + RGBA + weight per pixel
     if kind == "k_gather_walk":
@@ -187,10 +189,13 @@ def algo_bytes(kind, s, kt, in_lds, a, kt_all=None):
         slots = s.get("photon_slots", 0)
         return 2.0 * slots + 72.0 * stored + ((2.0 * slots + 96.0 * rad) if rad else 0.0)
     if kind == "k_fg":
-        # per request: 64 B in (point, wo + sample id, colour, extra) + 16 B out; the gather paths'
-        # traversals (LDS-resident scene) and the radiance-map lookups (16 K points, L2-resident) do
-        # not reach HBM
-        return 80.0 * it
+        # per request: 64 B in (point, wo + sample id, colour, extra) + 16 B out; per radiance-map nearest
+        # search the kd nodes it fetched (16 B each, counted in-kernel) and the found point's radiance
+        # (three 4-B words of the position / direction / colour arrays, 12 B); per gather path the hit's
+        # primitive record (normal + material, 16 B).  The gather rays' traversal bytes count only for a
+        # scene in global memory (an LDS-resident scene's never reach HBM)
+        return (80.0 * it + 16.0 * s.get("fg_nearest_visits", 0) + 12.0 * s.get("fg_lookups", 0)
+                + 16.0 * s.get("fg_paths", 0))
     if kind == "k_photon_bounce":
         # per traced path record (items = paths traced over all bounces): its alive-list slot + origin,
         # direction and colour read (52 B); the paths that continue write the same 52 B (every traced
@@ -199,9 +204,24 @@ def algo_bytes(kind, s, kt, in_lds, a, kt_all=None):
         emitted = kt_all.get("k_photon_emit", {}).get("items", 0)
         stored = s.get("photons", 0) + s.get("caustic_photons", 0)
         return 52.0 * it + 52.0 * max(0, it - emitted) + 37.0 * stored
+    if kind == "k_pregather":
+        # two launches per radiance map: k_rad_refl (per kept point: its 16-B position + primitive read, the
+        # two reflectivities written: 16 + 16 + 8 + 16 B) and k_pregather (per kept point: the 48-B point in,
+        # the radiance photon out 36 B; the diffuse-map kd nodes it fetched, 16 B each, and the photons it
+        # summed, 36 B each — both counted in-kernel)
+        return 56.0 * it + 84.0 * it + 16.0 * s.get("pregather_visits", 0) + 36.0 * s.get("pregather_photons", 0)
     if kind == "pkd_build":
-        return pkd_build_bytes(it) * kt["launches"]
+        # one launch record per tree: each tree over its own points (the diffuse map, the caustic map, the
+        # final-gathering radiance map of the kept points)
+        return sum(pkd_build_bytes(n) for n in pkd_trees(s, kt["launches"]))
     return None
+
+
+def pkd_trees(s, launches):
+    """Item counts of the point kd-trees built in one frame (one pkd_build launch record each): the diffuse
+    map, then the caustic map and the radiance map when present."""
+    trees = [n for n in (s.get("photons", 0), s.get("caustic_photons", 0), s.get("radiance_photons", 0)) if n]
+    return trees[:max(1, launches)] if trees else []
 
 
 def pkd_build_bytes(n):
@@ -435,7 +455,9 @@ def kernel_table(a, s, kt, pmc):
             # kind made of several kernels (pkd_build, photon_compact: one launch record per frame) is its
             # total over the pass's frames
             if kind not in SINGLE_KERNEL_KINDS and frames and "hbm_bytes_total" in p:
-                e["traffic_bytes"] = int(p["hbm_bytes_total"] / frames * v["launches"])
+                # the pass's total over its frames = one frame's bytes of this kind, whatever the number of
+                # launch records per frame (C5 + FG: two trees)
+                e["traffic_bytes"] = int(p["hbm_bytes_total"] / frames)
             else:
                 e["traffic_bytes"] = int(p["hbm_bytes_per_launch"] * v["launches"])
             e["traffic_gbs"] = round(e["traffic_bytes"] / (v["ms"] * 1e-3) / 1e9, 1)

@@ -62,6 +62,11 @@ typedef struct
 	uint64_t gather_overflows;  /* two-pass gather: requests whose log overflowed and were walked again (1.2) */
 	uint64_t photon_paths_traced; /* photon shooting: path records the bounce launches traced, summed over bounces and maps (1.5) */
 	uint64_t photon_slots;      /* photon shooting: deposit slots scanned by the compactions (paths x (bounces + 1)) (1.5) */
+	uint64_t fg_paths;          /* final gathering: gather paths traced by k_fg (1.6) */
+	uint64_t fg_lookups;        /* final gathering: radiance-map nearest searches (1.6) */
+	uint64_t fg_nearest_visits; /* final gathering: radiance-map kd nodes those searches fetched (1.6) */
+	uint64_t pregather_visits;  /* final gathering: diffuse-map kd nodes the radiance-map pre-gather fetched (1.6) */
+	uint64_t pregather_photons; /* final gathering: photons summed by the pre-gather (1.6) */
 } yafaray_amd_stats_t;
 
 /* Bytes of the LIBYAFARAY_AMD_1.0 struct (its fields end at photon_tree_seconds): yafaray_amd_getStats

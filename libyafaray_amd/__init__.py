@@ -44,7 +44,9 @@ class Stats(C.Structure):
                 ("gather_queries", C.c_uint64), ("gather_photons", C.c_uint64),
                 ("photon_maps_mode", C.c_int32), ("reserved0", C.c_int32),
                 ("gather_accepts", C.c_uint64), ("gather_overflows", C.c_uint64),
-                ("photon_paths_traced", C.c_uint64), ("photon_slots", C.c_uint64)]
+                ("photon_paths_traced", C.c_uint64), ("photon_slots", C.c_uint64),
+                ("fg_paths", C.c_uint64), ("fg_lookups", C.c_uint64), ("fg_nearest_visits", C.c_uint64),
+                ("pregather_visits", C.c_uint64), ("pregather_photons", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

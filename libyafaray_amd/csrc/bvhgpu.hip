@@ -580,7 +580,9 @@ extern "C" hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tr
 	DevBuf wl[2], lists, n_inner, off, need;
 	BVCHECK(wl[0].alloc((size_t)cap_nodes * 4));
 	BVCHECK(wl[1].alloc((size_t)cap_nodes * 4));
-	BVCHECK(lists.alloc((size_t)cap_nodes * 32));
+	// W / 4 int4 per wide node of a level (k_collapse_list): at most 2 x 16 B for the BVH8, and a level never
+	// holds more wide nodes than the binary tree has inner nodes (cap_nodes)
+	BVCHECK(lists.alloc((size_t)cap_nodes * 2 * sizeof(int4)));
 	BVCHECK(n_inner.alloc((size_t)(cap_nodes + 1) * 4));
 	BVCHECK(off.alloc((size_t)(cap_nodes + 1) * 4));
 	BVCHECK(need.alloc((size_t)cap_nodes * 4));

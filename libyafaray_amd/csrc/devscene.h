@@ -484,6 +484,11 @@ struct DevStats
 	unsigned long long gather_photons;   // photons the density estimates read (heap entries summed)
 	unsigned long long gather_accepts;   // two-pass gather: photons the walk accepted (log entries)
 	unsigned long long gather_overflows; // two-pass gather: requests whose log overflowed (walked again)
+	unsigned long long fg_paths;         // final gathering: gather paths k_fg traced
+	unsigned long long fg_lookups;       // final gathering: radiance-map nearest searches
+	unsigned long long fg_nearest_visits;// final gathering: radiance-map kd nodes those searches fetched
+	unsigned long long pre_visits;       // k_pregather: diffuse-map kd nodes fetched
+	unsigned long long pre_photons;      // k_pregather: photons summed into the radiance estimates
 };
 
 // the two-pass diffuse gather's accepted-photon log for one batch of the gather queue (kernels.hip

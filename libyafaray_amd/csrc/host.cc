@@ -290,6 +290,11 @@ bool Scene::renderDeviceGroup(RenderParams &rp)
 		st.gather_overflows += o.gather_overflows;
 		st.photon_paths_traced += o.photon_paths_traced;
 		st.photon_slots += o.photon_slots;
+		st.fg_paths += o.fg_paths;
+		st.fg_lookups += o.fg_lookups;
+		st.fg_nearest_visits += o.fg_nearest_visits;
+		st.pregather_visits += o.pregather_visits;
+		st.pregather_photons += o.pregather_photons;
 		st.trace_kernel_ms += o.trace_kernel_ms;
 		st.shade_kernel_ms += o.shade_kernel_ms;
 		st.nee_kernel_ms += o.nee_kernel_ms;
@@ -1730,7 +1735,14 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 			const std::vector<double> &ms = gpu()->memberMs();
 			last_bounds_ = group_bounds;
 			last_member_ms_ = ms;
-			if((int)ms.size() == world) group_bounds = rebalanceBands(group_bounds, ms, 0);
+			// the first frame on the initial equal split moves the boundaries all the way to the measured
+			// equal-cost split (the second frame is balanced); later frames move half way
+			// (damped against frame-to-frame noise).  Every member sees the same bounds and times: same result
+			if((int)ms.size() == world)
+			{
+				const bool initial = group_bounds == equalBands(s.height, world);
+				group_bounds = rebalanceBands(group_bounds, ms, 0, initial ? 0.0 : 0.5);
+			}
 		}
 		if(fmode != filmio::None && io_member) saveFilm();
 		const double build = stats.build_seconds;

@@ -4,6 +4,7 @@
 // include/common/logger.h:62-166).  Only the GPU renderer (render.h) touches HIP.
 #pragma once
 
+#include "pinned.h"
 #include "../../include/yafaray_c_api.h"
 #include "../../include/yafaray_amd.h"
 #include "devscene.h"
@@ -258,7 +259,7 @@ class Scene
 		std::string groupReport();          // JSON: how the last render was split (yafaray_amd_getGroupReport)
 
 		// film of the last render
-		std::vector<float> film_rgba, film_weights;
+		PinnedFloats film_rgba, film_weights;   // page-locked: the per-frame download is a DMA
 		int film_w = 0, film_h = 0;
 		bool film_on_gpu_only = false;   // the last render was quiet: film_rgba / film_weights are stale
 		yafaray_amd_stats_t stats{};

@@ -1539,7 +1539,11 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 	}
 	else
 	{
-#ifndef YAF_TRACE_NOREFILL
+#ifdef YAF_TRACE_NOREFILL
+	// the BVH8 (quantised 80-B nodes, its own triangle order) is only walked by traceRefill8; traceEntry
+	// reads C.nodes as a BVH4
+	static_assert(!W8, "YAF_TRACE_NOREFILL builds cannot traverse the quantised BVH8: set YAFARAY_AMD_BVH8=0 and drop the W8 instantiations");
+#else
 	// refill pays where traversals are long (meshes in global memory: C4 -16%); on the short
 	// LDS-resident traversals of small scenes its per-visit bookkeeping costs more (C2 +35%)
 	if(W8)
@@ -5449,7 +5453,7 @@ __global__ void __launch_bounds__(kGatherBlock) __attribute__((amdgpu_waves_per_
 	}
 }
 
-__device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2);
+__device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2, uint32_t *visits = nullptr);
 
 // PhotonGather (photon.cc:31-52) over one request's logged photons, in the walk's visit order, with
 // the reference's acceptance test d < max_d2 (pkdtree.h:270; the bounded walk logs a superset).
@@ -5709,6 +5713,7 @@ struct PreGatherArgs
 	uint32_t n;
 	float4 *out_pos, *out_dir;
 	float *out_colb;
+	DevStats *stats;   // [0]: pre_visits / pre_photons of the launch (bench.py's byte model), or null
 };
 
 __global__ void __launch_bounds__(kGatherBlock) k_pregather(PreGatherArgs A)
@@ -5722,7 +5727,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_pregather(PreGatherArgs A)
 	const uint32_t gstride = gridDim.x * kGatherBlock;
 	uint2 *stk = S.pk_stack + blockIdx.x * kGatherBlock + threadIdx.x;
 	const float ds_radius_2 = S.pm_radius2 * S.pm_radius2;   // :42 ds_rad * ds_rad (pm_radius2 holds ds_rad)
-	uint32_t visits = 0;
+	uint32_t visits = 0, found_sum = 0;
 	for(uint32_t j = blockIdx.x * kGatherBlock + threadIdx.x; j < A.n; j += gstride)
 	{
 		const uint32_t r = A.kept[j];
@@ -5734,6 +5739,7 @@ __global__ void __launch_bounds__(kGatherBlock) k_pregather(PreGatherArgs A)
 		C3 sum = c3(0.f);
 		if(found > 0)
 		{
+			found_sum += (uint32_t)found;
 			const float scale = S.fg_i_scale / radius;
 			for(int i = 0; i < found; ++i)
 			{
@@ -5748,18 +5754,32 @@ __global__ void __launch_bounds__(kGatherBlock) k_pregather(PreGatherArgs A)
 		A.out_dir[j] = f4(rnorm, sum.g);
 		A.out_colb[j] = sum.b;
 	}
+	if(A.stats)
+	{
+		for(int off = 32; off > 0; off >>= 1)
+		{
+			visits += __shfl_down(visits, off);
+			found_sum += __shfl_down(found_sum, off);
+		}
+		if(laneId() == 0)
+		{
+			atomicAdd(&A.stats->pre_visits, (unsigned long long)visits);
+			atomicAdd(&A.stats->pre_photons, (unsigned long long)found_sum);
+		}
+	}
 }
 
 // PhotonMap::findNearest (photon.cc:136-142): NearestPhoton (photon.h:159-169) over the
 // non-recursive lookup (pkdtree.h:225-292) — the last photon accepted (facing n, strictly closer
 // than the shrinking radius); far children that already fail the radius are not pushed (the radius
 // never grows, so the reference discards them at pop time).  -1: none.
-__device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2)
+__device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2, uint32_t *visits)
 {
 	uint2 stk[64];
 	int nearest = -1;
 	uint32_t curr = 0;
 	int sp_top = 0;
+	uint32_t nv = 1;
 	for(;;)
 	{
 		uint4 nd = nodes[curr];
@@ -5779,6 +5799,7 @@ __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, flo
 				++sp_top;
 			}
 			nd = nodes[curr];
+			++nv;
 		}
 		const uint32_t ph = nd.w >> 2;
 		const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
@@ -5799,7 +5820,9 @@ __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, flo
 		if(done) break;
 		curr = top.x;
 		--sp_top;
+		++nv;
 	}
+	if(visits) *visits += nv;
 	return nearest;
 }
 
@@ -5809,12 +5832,14 @@ __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, flo
 // distance test directly (its photon lies beyond that plane: the two tests agree, as in pkWalk).  Same
 // visits in the same order as pkNearest, so the same nearest photon.
 template<int STRIDE>
-__device__ __forceinline__ int pkNearestLds(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2, uint32_t *stk, int cap)
+__device__ __forceinline__ int pkNearestLds(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, float max_d2, uint32_t *stk, int cap,
+                                            uint32_t &visits)
 {
 	int nearest = -1;
 	uint32_t curr = 0;
 	int sp_top = 0;
 	uint4 nd = nodes[0];
+	++visits;
 	for(;;)
 	{
 		while((nd.w & 3u) != 3u)
@@ -5833,6 +5858,7 @@ __device__ __forceinline__ int pkNearestLds(const uint4 *nodes, const float4 *di
 				++sp_top;
 			}
 			nd = nodes[curr];
+			++visits;
 		}
 		const uint32_t ph = nd.w >> 2;
 		const V3 v = v3(__uint_as_float(nd.x), __uint_as_float(nd.y), __uint_as_float(nd.z)) - p;
@@ -5847,6 +5873,7 @@ __device__ __forceinline__ int pkNearestLds(const uint4 *nodes, const float4 *di
 			--sp_top;
 			curr = stk[sp_top * STRIDE];
 			nd = nodes[curr];
+			++visits;
 			if((nd.w & 3u) != 3u)
 			{
 				const uint32_t pax = nd.z;
@@ -6051,9 +6078,17 @@ struct FgArgs
 #ifndef YAF_FG_STAGE
 #define YAF_FG_STAGE 1
 #endif
-__host__ __device__ inline bool fgStageTables(const DevScene &S, bool lds_scene, bool ext)
+// Staging only when the whole dynamic LDS of the launch stays within 64 KB: the trace stack, the scene,
+// the nearest-search column rounded to 16 B, then the materials and primitive records.  The kernel and
+// yafamd_launch_fg take the same decision from the same (uniform) arguments.
+__host__ __device__ inline bool fgStageTables(const DevScene &S, bool lds_scene, bool ext, int stack_depth)
 {
-	return YAF_FG_STAGE && lds_scene && !ext && S.small_tables;
+	if(!(YAF_FG_STAGE && lds_scene && !ext && S.small_tables)) return false;
+	const size_t stack_b = (size_t)stack_depth * kTraceBlock * sizeof(int);
+	const size_t scene_b = (size_t)(S.node_f4 * S.n_nodes + 3 * S.n_tris) * 16u;
+	const size_t nstk_b = (((size_t)S.rpk_lds * kTraceBlock * sizeof(uint32_t)) + 15u) & ~(size_t)15u;
+	const size_t tab_b = (size_t)S.n_mats * sizeof(DevMaterial) + (size_t)S.n_tris * 16u;
+	return stack_b + scene_b + nstk_b + tab_b <= (size_t)64 * 1024;
 }
 template<bool LDS_SCENE, bool WIDE, bool EXT, bool SPILL = true, bool TSH = false>
 __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
@@ -6085,7 +6120,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 	// the radiance-map nearest searches' LDS stack column (S.rpk_lds levels), after the stack and scene
 	uint32_t *nstk = reinterpret_cast<uint32_t *>(smem + (A.stack_depth * kTraceBlock) / 4 +
 	                                              (LDS_SCENE ? S.node_f4 * S.n_nodes + 3 * S.n_tris : 0)) + threadIdx.x;
-	if(fgStageTables(A.S, LDS_SCENE, EXT))
+	if(fgStageTables(A.S, LDS_SCENE, EXT, A.stack_depth))
 	{
 		// after the nearest-search column (S.rpk_lds levels of one word per lane)
 		uint4 *tp = reinterpret_cast<uint4 *>(smem + (A.stack_depth * kTraceBlock) / 4 + (S.node_f4 * S.n_nodes + 3 * S.n_tris) +
@@ -6097,9 +6132,13 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 		S_.mats = reinterpret_cast<const DevMaterial *>(tp);
 		S_.prim_ng = reinterpret_cast<const float4 *>(tp + nm);
 	}
+	// statistics of the frame (bench.py's k_fg byte model): gather paths traced, radiance-map lookups and
+	// the radiance-map kd nodes they fetched
+	uint32_t n_paths = 0, n_lookups = 0, n_nvisits = 0;
 	auto nearestRad = [&](V3 hp, V3 sf) -> int {
-		return S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, nstk, S.rpk_lds)
-		                     : pkNearest(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad);
+		++n_lookups;
+		return S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, nstk, S.rpk_lds, n_nvisits)
+		                     : pkNearest(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, &n_nvisits);
 	};
 	const bool ATTR = EXT && S.has_attr != 0;
 	const SegLoop L = segLoop(S.n_seg);
@@ -6150,6 +6189,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 			float t;
 			int prim;
 			V3 from = sp0.p;
+			++n_paths;
 			if(!traverse<false, WIDE, SPILL>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests)) continue;
 			Surf hit = fgSurf<EXT>(S, from, dir, t, prim);
 			float length = t;
@@ -6233,6 +6273,21 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 		const uint4 cb = A.G.pix_mode[j];
 		const C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)} + fg;
 		A.G.pix_mode[j] = make_uint4(__float_as_uint(col.r), __float_as_uint(col.g), __float_as_uint(col.b), cb.w);
+	}
+	if(S.stats)
+	{
+		for(int off = 32; off > 0; off >>= 1)
+		{
+			n_paths += __shfl_down(n_paths, off);
+			n_lookups += __shfl_down(n_lookups, off);
+			n_nvisits += __shfl_down(n_nvisits, off);
+		}
+		if(laneId() == 0)
+		{
+			atomicAdd(&S.stats[L.s].fg_paths, (unsigned long long)n_paths);
+			atomicAdd(&S.stats[L.s].fg_lookups, (unsigned long long)n_lookups);
+			atomicAdd(&S.stats[L.s].fg_nearest_visits, (unsigned long long)n_nvisits);
+		}
 	}
 }
 
@@ -6747,7 +6802,7 @@ hipError_t yafamd_rad_refl(const DevScene *S, float4 *a, float4 *b, float4 *c, c
 // preGatherWorker over the kept radiance points (n of them, indices `kept` into the compacted
 // arrays); the grid is the gather grid, whose lanes the HBM lookup stack (S->pk_stack) is sized for
 hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
-                            float4 *out_pos, float4 *out_dir, float *out_colb, hipStream_t st)
+                            float4 *out_pos, float4 *out_dir, float *out_colb, DevStats *stats, hipStream_t st)
 {
 	if(n == 0) return hipSuccess;
 	PreGatherArgs A;
@@ -6760,6 +6815,7 @@ hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b,
 	A.out_pos = out_pos;
 	A.out_dir = out_dir;
 	A.out_colb = out_colb;
+	A.stats = stats;
 	const size_t lds = (size_t)kGatherBlock * 8u * (size_t)max(1, S->pm_search);
 	hipLaunchKernelGGL(k_pregather, dim3(S->n_seg * kGatherPerSeg), dim3(kGatherBlock), lds, st, A);
 	return hipGetLastError();
@@ -6781,7 +6837,7 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 	const size_t nstk_bytes = (size_t)S->rpk_lds * kTraceBlock * sizeof(uint32_t);
 	const bool wide = S->node_f4 == 8;
 	// an LDS-resident scene: the column rounded to 16 B, then the staged tables (fgStageTables)
-	const size_t stage_bytes = fgStageTables(*S, S->scene_in_lds != 0, S->ext != 0)
+	const size_t stage_bytes = fgStageTables(*S, S->scene_in_lds != 0, S->ext != 0, stack_depth)
 	                               ? ((nstk_bytes + 15) & ~(size_t)15) + (size_t)S->n_mats * sizeof(DevMaterial) + (size_t)S->n_tris * 16
 	                               : nstk_bytes;
 	if(S->tr_shad)

@@ -64,7 +64,7 @@ size_t yafamd_gather_lds_bytes(const DevScene *S);
 hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t *scratch_counts, uint32_t *total_dev, float4 *a, float4 *b, float4 *c, hipStream_t st);
 hipError_t yafamd_rad_refl(const DevScene *S, float4 *a, float4 *b, float4 *c, const uint32_t *kept, uint32_t n, hipStream_t st);
 hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
-                            float4 *out_pos, float4 *out_dir, float *out_colb, hipStream_t st);
+                            float4 *out_pos, float4 *out_dir, float *out_colb, DevStats *stats, hipStream_t st);
 hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out, uint32_t *n_kept,
                                   int *rounds_out, hipStream_t st, void **scratch);
 void yafamd_thin_scratch_free(void *scratch);
@@ -251,7 +251,10 @@ struct GpuRenderer::Impl
 	hipStream_t stream = nullptr;
 	Buf nodes, tris, prim_ng, mats, lights, faure, faure_dim, faure_inv;
 	Buf nodes8, tris8;          // quantised BVH8 of the device-built tree and its triangles (k_trace's refill loop), or empty
-	int n_nodes8 = 0, need8 = 0, lds_top8 = 0;
+	int n_nodes8 = 0, need8 = 0, lds_top8 = 0, depth8 = 0;
+	int trace_grid_bvh4 = 0;   // the grid of the BVH4 k_trace when a BVH8 exists (transparent shadows)
+	Buf pre_stats;             // k_pregather's counters (one DevStats)
+	bool pre_stats_valid = false;
 	// surface attributes, textures and shader-node programs (texeval.h)
 	Buf prim_attr, shader_nodes, textures, texels;
 	// specular recursion tree (k_spawn / k_combine): spawned rays and per-node records
@@ -369,7 +372,7 @@ struct GpuRenderer::Impl
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
-		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &walk_spill, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris}) b->release();
+		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &walk_spill, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris, &pre_stats}) b->release();
 		for(int m = 0; m < 3; ++m)
 			for(Buf *b : {&kd_pos[m], &kd_dir[m], &kd_colb[m]}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
@@ -541,6 +544,7 @@ bool GpuRenderer::upload(HostScene &hs)
 			d.tris8.bytes = (size_t)std::max(1, hs.n_prims) * 48;
 			d.n_nodes8 = w8.n_nodes;
 			d.need8 = w8.stack_need;
+			d.depth8 = w8.depth;
 		}
 		HIPCHECK(e);
 		d.nodes.p = np;
@@ -681,6 +685,16 @@ bool GpuRenderer::upload(HostScene &hs)
 		if(const char *e = getenv("YAFARAY_AMD_TRACE_GRID")) d.trace_grid = std::max(1, atoi(e));
 		// a whole number of workgroups per queue segment
 		d.trace_grid = std::max(1, d.trace_grid / d.shade_grid) * d.shade_grid;
+		// transparent shadows launch the BVH4 kernels even when a BVH8 exists (launch_trace): their own
+		// resident grid, never above trace_grid (the spill column and statistics are sized for that)
+		d.trace_grid_bvh4 = d.trace_grid;
+		if(w8 && !getenv("YAFARAY_AMD_TRACE_GRID"))
+		{
+			const size_t dyn4 = (size_t)d.lds_stack * yafamd_trace_block() * 4 + (size_t)d.lds_top * 144;
+			int g4 = d.n_cu * std::max(1, yafamd_trace_blocks_per_cu(0, d.node_f4 == 8 ? 1 : 0, dyn4));
+			g4 = std::max(1, g4 / d.shade_grid) * d.shade_grid;
+			d.trace_grid_bvh4 = std::min(g4, d.trace_grid);
+		}
 	}
 	d.spill.release();
 	if(d.lds_stack < d.stack_depth &&
@@ -718,7 +732,7 @@ bool GpuRenderer::upload(HostScene &hs)
 	if(!allocCopy(log_, d.faure_dim, fdim.data(), fdim.size())) return false;
 	if(!allocCopy(log_, d.faure_inv, inv.data(), inv.size())) return false;
 	stats_.bvh_nodes = (uint32_t)((d.nodes8.p && !d.scene_in_lds) ? d.n_nodes8 : d.n_nodes);
-	stats_.bvh_depth = (uint32_t)d.depth;
+	stats_.bvh_depth = (uint32_t)((d.nodes8.p && !d.scene_in_lds) ? d.depth8 : d.depth);   // of the tree k_trace traverses
 	stats_.bvh_width = (d.nodes8.p && !d.scene_in_lds) ? 8u : d.node_f4 == 8 ? 4u : 2u;   // the tree k_trace traverses
 	stats_.scene_in_lds = d.scene_in_lds ? 1u : 0u;
 	stats_.trace_grid = (uint32_t)d.trace_grid;
@@ -1181,9 +1195,13 @@ bool GpuRenderer::buildRadianceMap(RenderParams &rp)
 	                                   d.stream));
 	DevScene probe = S;
 	probe.n_seg = (uint32_t)d.shade_grid;   // the gather grid k_pregather shares pk_stack with
+	// its node visits and summed photons (statistics; read with the render's)
+	if(!ensure(log_, d.pre_stats, sizeof(DevStats))) return false;
+	HIPCHECK(hipMemsetAsync(d.pre_stats.p, 0, sizeof(DevStats), d.stream));
+	d.pre_stats_valid = true;
 	PROF(KK_PREGATHER, yafamd_pregather(&probe, (const float4 *)d.radc_a.p, (const float4 *)d.radc_b.p, (const float4 *)d.radc_c.p,
 	                                    (const uint32_t *)d.rad_kept.p, nk, (float4 *)d.rph_pos.p, (float4 *)d.rph_dir.p, (float *)d.rph_colb.p,
-	                                    d.stream));
+	                                    (DevStats *)d.pre_stats.p, d.stream));
 	int depth = 0;
 	if(!buildMapTree(2, d.rph_pos.p, d.rph_dir.p, d.rph_colb.p, nk, d.rpk_nodes.p, depth)) return false;
 	d.n_rphotons = (int)nk;
@@ -1888,7 +1906,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// (camera rays with the default clip planes all have (0, unbounded): k_camera writes no ray_tt)
 			if(it != 0 || (S.cur_level == 0 && !S.cam.ray_tt)) qc.ray_tt = nullptr;
 			qc.tmin_dflt = it == 0 ? 0.f : S.ray_min_dist;
-			PROF(KK_TRACE, yafamd_launch_trace(&S, &qc, &cnt[cur], &d.P[cur], run_stats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+			PROF(KK_TRACE, yafamd_launch_trace(&S, &qc, &cnt[cur], &d.P[cur], run_stats, d.lds_stack, (int *)d.spill.p,
+			                                    S.tr_shad ? d.trace_grid_bvh4 : d.trace_grid, d.stream));
 			// material-shade dispatch for textured / smooth scenes: surface attributes + shader nodes
 			// of every hit, before k_shade reads them
 			// transparent shadows: filter colours of the transparent surfaces the shadow rays crossed
@@ -2285,6 +2304,17 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			hs.gather_photons += b.gather_photons;
 			hs.gather_accepts += b.gather_accepts;
 			hs.gather_overflows += b.gather_overflows;
+			hs.fg_paths += b.fg_paths;
+			hs.fg_lookups += b.fg_lookups;
+			hs.fg_nearest_visits += b.fg_nearest_visits;
+		}
+		if(d.pre_stats_valid)
+		{
+			DevStats pre{};
+			HIPCHECK(hipMemcpy(&pre, d.pre_stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+			hs.pre_visits = pre.pre_visits;
+			hs.pre_photons = pre.pre_photons;
+			d.pre_stats_valid = false;   // counted once: a reused radiance map is not pre-gathered again
 		}
 	}
 	stats_.closest_rays = hs.closest_rays;
@@ -2329,19 +2359,54 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	stats_.gather_queries = hs.gather_queries;
 	stats_.gather_accepts = hs.gather_accepts;
 	stats_.gather_overflows = hs.gather_overflows;
+	stats_.fg_paths = hs.fg_paths;
+	stats_.fg_lookups = hs.fg_lookups;
+	stats_.fg_nearest_visits = hs.fg_nearest_visits;
+	stats_.pregather_visits = hs.pre_visits;
+	stats_.pregather_photons = hs.pre_photons;
 	d.prof_on = false;
 	return true;
 }
 
-bool GpuRenderer::download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h)
+// a 64-B header records how the block was obtained (1: hipHostMalloc, 0: malloc when pinning failed,
+// e.g. without a device), so that pinnedFree releases it the same way
+void *yafamd::pinnedAlloc(size_t bytes)
+{
+	const size_t n = bytes + 64;
+	void *p = nullptr;
+	uint32_t tag = 1;
+	if(hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess || !p)
+	{
+		(void)hipGetLastError();
+		p = std::malloc(n);
+		tag = 0;
+		if(!p) return nullptr;
+	}
+	std::memcpy(p, &tag, sizeof(tag));
+	return static_cast<char *>(p) + 64;
+}
+
+void yafamd::pinnedFree(void *q)
+{
+	if(!q) return;
+	void *p = static_cast<char *>(q) - 64;
+	uint32_t tag = 0;
+	std::memcpy(&tag, p, sizeof(tag));
+	if(tag == 1) (void)hipHostFree(p);
+	else std::free(p);
+}
+
+bool GpuRenderer::download(PinnedFloats &rgba, PinnedFloats &weights, int w, int h)
 {
 	DeviceGuard guard(device_);
 	Impl &d = *d_;
 	if(!d.film.p || w != d.film_w || h != d.film_h) { log_.error("GPU: no film to download"); return false; }
-	rgba.resize((size_t)w * h * 4);
-	weights.resize((size_t)w * h);
-	HIPCHECK(hipMemcpy(rgba.data(), d.film.p, rgba.size() * 4, hipMemcpyDeviceToHost));
-	HIPCHECK(hipMemcpy(weights.data(), d.weights.p, weights.size() * 4, hipMemcpyDeviceToHost));
+	// the buffers keep their size across frames (no re-allocation, no re-pinning after the first)
+	if(rgba.size() != (size_t)w * h * 4) rgba.resize((size_t)w * h * 4);
+	if(weights.size() != (size_t)w * h) weights.resize((size_t)w * h);
+	HIPCHECK(hipMemcpyAsync(rgba.data(), d.film.p, rgba.size() * 4, hipMemcpyDeviceToHost, d.stream));
+	HIPCHECK(hipMemcpyAsync(weights.data(), d.weights.p, weights.size() * 4, hipMemcpyDeviceToHost, d.stream));
+	HIPCHECK(hipStreamSynchronize(d.stream));
 	return true;
 }
 
@@ -2670,7 +2735,7 @@ std::vector<int> equalBands(int height, int world)
 	return b;
 }
 
-std::vector<int> rebalanceBands(const std::vector<int> &bounds, const std::vector<double> &times, int cap_rows)
+std::vector<int> rebalanceBands(const std::vector<int> &bounds, const std::vector<double> &times, int cap_rows, double damping)
 {
 	const int world = (int)bounds.size() - 1;
 	const int H = bounds.back();
@@ -2692,7 +2757,7 @@ std::vector<int> rebalanceBands(const std::vector<int> &bounds, const std::vecto
 		const double target = cum[H] * r / world;
 		int y = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
 		if(y > 0 && y <= H && (cum[y] - target) > (target - cum[y - 1])) --y;
-		y = (int)std::nearbyint(0.5 * bounds[r] + 0.5 * y);   // round half to even, as Python's round()
+		y = (int)std::nearbyint(damping * bounds[r] + (1.0 - damping) * y);   // round half to even, as Python's round()
 		nb.push_back(y);
 	}
 	nb.push_back(H);

@@ -22,6 +22,7 @@
 namespace yafamd
 {
 
+
 struct HostScene
 {
 	BvhOutput bvh;                       // host build (nodes + triangle records), or metadata of the GPU build
@@ -187,7 +188,7 @@ class GpuRenderer
 		int lastPassCount() const { return passes_done_; }
 		uint32_t samplingOffset() const { return sampling_offset_; }   // ImageFilm::sampling_offset_ after the last pass
 		bool downloadAccum(std::vector<float> &rgba, std::vector<float> &weights);   // unnormalised film (film files)   // AA passes rendered by the last render()
-		bool download(std::vector<float> &rgba, std::vector<float> &weights, int w, int h);
+		bool download(PinnedFloats &rgba, PinnedFloats &weights, int w, int h);   // one stream sync, DMA into pinned memory
 		bool filmToDevice(void *dst, int y0, int y1);
 		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
 		bool buildPhotonMap(RenderParams &rp);
@@ -264,10 +265,11 @@ class GpuRenderer
 
 // Band boundaries (world + 1 rows) moved towards equal cost from each band's last render time:
 // each band's time is spread evenly over its rows (piecewise-constant cost density), boundaries
-// move half way to the equal-cost split, every band keeps >= 1 row; a result with a band above
-// cap_rows rows (0: no cap) keeps the old bounds.  Pure and deterministic, so every group member
-// computes the same bounds from the same gathered times (libyafaray_amd/tiles.py mirrors it).
-std::vector<int> rebalanceBands(const std::vector<int> &bounds, const std::vector<double> &times, int cap_rows);
+// move towards the equal-cost split (damping: the fraction of the old boundary kept; 0.5 half way, 0 all
+// the way), every band keeps >= 1 row; a result with a band above cap_rows rows (0: no cap) keeps the old
+// bounds.  Pure and deterministic, so every group member computes the same bounds from the same gathered
+// times (tests/tiles.py mirrors it).
+std::vector<int> rebalanceBands(const std::vector<int> &bounds, const std::vector<double> &times, int cap_rows, double damping = 0.5);
 std::vector<int> equalBands(int height, int world);
 
 // The render group's band exchange plan (GpuRenderer::exchangeRows does it with device copies and an

@@ -99,3 +99,97 @@ def test_multi_kernel_kind_traffic_is_per_frame():
     assert abs(kernels["pkd_build"]["traffic_bytes"] - 162 * 0.74e9 / 2) < 1e3
     roof = bench.dominant_roofline(s, kt, kernels, pmc, "photon")
     assert roof["kernel"] == "pkd_build" and abs(roof["traffic"] - 162 * 0.74e9 / 2) < 1e3
+
+
+# --------------------------------------------------------------------------------------------------
+# physical-possibility checks: no kernel may report an algorithmic rate above the
+# HBM spec, nor a PMC-measured rate above the guide's measured achievable HBM bandwidth
+# --------------------------------------------------------------------------------------------------
+ACHIEVABLE_GBS = 6290.0   # MI355X_MICROARCH.md: measured achievable HBM read+write rate
+
+
+def _physical(line):
+    bad = []
+    for k, e in (line.get("kernels") or {}).items():
+        if e.get("frac") is not None and e["frac"] > 1.0:
+            bad.append((k, "frac", e["frac"]))
+        if e.get("traffic_gbs") is not None and e["traffic_gbs"] > ACHIEVABLE_GBS:
+            bad.append((k, "traffic_gbs", e["traffic_gbs"]))
+    roof = line.get("roofline") or {}
+    if roof.get("frac") is not None and roof["frac"] > 1.0:
+        bad.append(("roofline", "frac", roof["frac"]))
+    return bad
+
+
+def test_k_camera_model_matches_its_32_byte_writes():
+    """r05's line printed k_camera frac 1.026 with a stale 40-B model; the kernel writes 32 B per sample
+    (24-B ray records + 8-B compact record; PMC WRITE_SIZE = 32.0 B x samples)."""
+    a, s = _args(), _stats()
+    kt = {"k_camera": {"ms": 0.647, "launches": 1, "items": 132_710_400}}   # r05: 0.647 ms per frame
+    kernels, _ = bench.kernel_table(a, s, kt, None)
+    assert kernels["k_camera"]["algo_bytes_per_item"] == 32.0
+    assert kernels["k_camera"]["frac"] < 1.0
+    assert not _physical({"kernels": kernels})
+
+
+def test_pkd_build_charges_each_tree_its_own_points_and_pmc_is_per_frame():
+    """C5 + FG builds two trees per frame (the 19.6 M-photon diffuse map and the 16 K-point radiance map):
+    each is charged its own item count, and the PMC total of a frame is not multiplied by the two launch
+    records (r05 printed 7.36 TB/s)."""
+    n, nk = 19_646_342, 16_409
+    s = dict(_stats(), photons=n, radiance_photons=nk)
+    assert bench.pkd_trees(s, 2) == [n, nk]
+    a = _args("photon")
+    kt = {"pkd_build": {"ms": 16.2, "launches": 2, "items": n}, "k_film": {"ms": 0.07, "launches": 1, "items": 2_073_600}}
+    # profiles/pmc_photon-...-fg32.json (r05): 556 pkd dispatches, 238.3 GB over the pass's 4 frames
+    pmc = {"kernels": {"pkd_build": {"dispatches": 556, "hbm_bytes_per_launch": 0.4286e9, "hbm_bytes_total": 238.3e9},
+                       "k_film": {"dispatches": 4, "hbm_bytes_per_launch": 0.334e9, "hbm_bytes_total": 1.336e9}}}
+    kernels, _ = bench.kernel_table(a, s, kt, pmc)
+    e = kernels["pkd_build"]
+    assert abs(e["algo_bytes_per_item"] * n - (bench.pkd_build_bytes(n) + bench.pkd_build_bytes(nk))) < n
+    assert abs(e["traffic_bytes"] - 238.3e9 / 4) < 1e3   # one frame's bytes, not x 2 launch records
+    assert not _physical({"kernels": kernels}), _physical({"kernels": kernels})
+
+
+def test_fg_and_pregather_models_count_their_lookups():
+    a = _args("photon")
+    s = dict(_stats(), fg_paths=60_000_000, fg_lookups=55_000_000, fg_nearest_visits=1_600_000_000,
+             pregather_visits=20_000_000, pregather_photons=800_000)
+    kt = {"k_fg": {"ms": 27.2, "launches": 1, "items": 2_000_000}, "k_pregather": {"ms": 2.7, "launches": 2, "items": 16_409}}
+    kernels, _ = bench.kernel_table(a, s, kt, None)
+    fg = kernels["k_fg"]["algo_bytes_per_item"] * 2_000_000
+    assert abs(fg - (80 * 2e6 + 16 * 1.6e9 + 12 * 55e6 + 16 * 60e6)) < 2e6
+    assert kernels["k_pregather"]["algo_bytes_per_item"] > 140.0
+    assert kernels["k_fg"]["frac"] > 0.01   # r05's model excluded all of k_fg's work (frac 0.0007)
+    assert not _physical({"kernels": kernels})
+
+
+def test_committed_round6_lines_are_physically_possible():
+    """Every committed bench line of this round (profiles/r06_*.json, BENCH_r06.json when present)."""
+    import glob
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = sorted(glob.glob(os.path.join(root, "profiles", "r06_*.json"))) + [p for p in [os.path.join(root, "BENCH_r06.json")]
+                                                                              if os.path.exists(p)]
+    for p in paths:
+        with open(p) as f:
+            txt = f.read()
+        lines = []
+        for raw in txt.splitlines():
+            raw = raw.strip()
+            if raw.startswith("{") and '"kernels"' in raw:
+                try:
+                    lines.append(json.loads(raw))
+                except ValueError:
+                    pass
+        if not lines:
+            try:
+                obj = json.loads(txt)
+            except ValueError:
+                continue
+            obj = obj.get("parsed", obj) if isinstance(obj, dict) else None
+            if isinstance(obj, dict) and "kernels" in obj:
+                lines.append(obj)
+        for line in lines:
+            assert not _physical(line), (os.path.basename(p), _physical(line))

@@ -44,6 +44,8 @@ def kind_of(name, photon):
     base = m.group(1) if m else n
     if base == "k_trace_rays":
         return "k_trace_rays"
+    if base == "k_rad_refl":
+        return "k_pregather"   # one launch record of the pre-gather kind (render.cc KK_PREGATHER)
     for k in KINDS:
         if base == k:
             return k
