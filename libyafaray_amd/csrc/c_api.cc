@@ -499,7 +499,17 @@ yafaray_bool_t yafaray_amd_getFilm(const yafaray_Interface_t *interface, float *
 	if(!it->scene) return YAFARAY_BOOL_FALSE;
 	Scene *s = it->scene.get();
 	// a quiet render (renderQuiet) leaves the film on the GPU: fetch it now
-	if(s->film_on_gpu_only && !s->gpu()->download(s->film_rgba, s->film_weights, s->film_w, s->film_h)) return YAFARAY_BOOL_FALSE;
+	if(s->film_on_gpu_only)
+	{
+		if(!s->gpu()->download(s->film_rgba, s->film_weights, s->film_w, s->film_h)) return YAFARAY_BOOL_FALSE;
+		s->film_weights_stale = false;
+	}
+	else if(s->film_weights_stale && weights)
+	{
+		// a flushed render downloaded the colours only (the put-pixel values): the weights on demand
+		if(!s->gpu()->download(s->film_rgba, s->film_weights, s->film_w, s->film_h, false)) return YAFARAY_BOOL_FALSE;
+		s->film_weights_stale = false;
+	}
 	s->film_on_gpu_only = false;
 	if(s->film_rgba.empty()) return YAFARAY_BOOL_FALSE;
 	if(rgba) std::memcpy(rgba, it->scene->film_rgba.data(), it->scene->film_rgba.size() * 4);

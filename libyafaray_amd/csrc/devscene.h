@@ -503,4 +503,17 @@ struct GatherLogDesc
 	uint32_t *spill;  // k_gather_walk: far-child stack levels beyond the LDS ones (-DYAF_WALK_LDS_LEVELS), per walk thread
 };
 
+// one batch of final gathering with one lane per gather path (kernels.hip k_fg_first / k_fg_long / k_fg_sum)
+struct FgBatch
+{
+	uint32_t j0, seg_cap;   // request positions of this batch in every segment
+	int n_sampl;            // gather paths per request of this pass
+	int n_terms;            // terms a bouncing path can add: fg_bounces + 1
+	float4 *terms;          // [seg][pos - j0][path]: (term, tag): tag 0 no term, 1 one term, 2 + i: bouncing path i of the segment
+	float4 *longs;          // [seg][i][3]: (origin, t) (direction, prim) (throughput, path id in the segment's batch)
+	float4 *long_terms;     // [seg][i][n_terms]: (term, 1) or (0, 0)
+	uint32_t *long_count;   // [seg]
+	uint32_t long_cap;      // bouncing paths per segment (= seg_cap * n_sampl: every path may bounce)
+};
+
 } // namespace yafamd

@@ -1750,7 +1750,9 @@ bool Scene::render(const Callbacks &cb, yafaray_ProgressBarCallback_t progress, 
 		stats.build_seconds = build;
 		film_on_gpu_only = quiet;
 		if(quiet) continue;
-		if(!gpu()->download(film_rgba, film_weights, s.width, s.height)) return false;
+		// the flush needs the colours (putPixel); the weights stay on the GPU until getFilm asks for them
+		if(!gpu()->download(film_rgba, film_weights, s.width, s.height, true, false)) return false;
+		film_weights_stale = true;
 		{
 			std::ostringstream os;
 			os << "Render: " << stats.samples << " samples, " << stats.closest_rays << " closest + " << stats.shadow_rays

@@ -262,6 +262,7 @@ class Scene
 		PinnedFloats film_rgba, film_weights;   // page-locked: the per-frame download is a DMA
 		int film_w = 0, film_h = 0;
 		bool film_on_gpu_only = false;   // the last render was quiet: film_rgba / film_weights are stale
+		bool film_weights_stale = false; // the last flush downloaded film_rgba only (getFilm fetches the weights)
 		yafaray_amd_stats_t stats{};
 
 	private:

@@ -27,6 +27,8 @@
 // Compiled with -ffp-contract=off: every float expression keeps the reference's order.
 
 #include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <string>
 #include "devmath.h"
 #include "photonheap.h"
 #include "devscene.h"
@@ -782,7 +784,15 @@ __device__ __forceinline__ SlabSel slabSel(V3 id) { return SlabSel{id.x >= 0.f ?
 // BVH4 (bvh.cc: collapsed binary SAH tree, 128 B nodes with the four child boxes in SoA form).
 // Same hit semantics as traverse2: leaf children are tested as soon as their box is hit, inner
 // children are sorted by entry distance (5-exchange network) and descended nearest-first.
-template<bool ANY, bool SPILL, bool TS = false, bool STATS = true>
+// PACK (LDS-resident trees, < 512 nodes): the closest rays' child order from packed integer keys (below);
+// -DYAF_PACKED_SORT=1 also packs the BVH8 refill loop's 19-exchange network.  Measured and off (r06, same
+// box A/B): C2 k_trace 25.9 -> 27.2 ms per frame (fewer VALU per exchange, but the key packing and the
+// child masks cost more than the selects they replace at the 64-VGPR budget), C4 unchanged (126.4 ms)
+#ifndef YAF_PACKED_SORT
+#define YAF_PACKED_SORT 0
+#endif
+constexpr uint32_t kPackNodeBits = 9;   // node index bits of a packed key: LDS-resident BVH4s have <= 384 nodes (48 KB)
+template<bool ANY, bool SPILL, bool TS = false, bool STATS = true, bool PACK = false>
 __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best, int &prim_best,
                           uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
@@ -898,6 +908,33 @@ __device__ bool traverse4(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax,
 				if(next < 0) next = child[k];
 				else { push(child[k]); ++sp; }
 			}
+		}
+		else if constexpr(PACK && YAF_PACKED_SORT && YAF_CLOSEST_SORT)
+		{
+			// one 32-bit key per hit inner child: the entry distance clamped at 0 with the child's node index in
+			// the low kPackNodeBits bits (the order is a culling heuristic only — closest hits tie-break on the
+			// primitive index, so neither the clamp nor the dropped mantissa bits change a result), sorted as
+			// unsigned integers: a compare-exchange is one v_min_u32 + v_max_u32 instead of a compare and four
+			// selects, and the child comes back with a mask; a missed child is all ones
+			constexpr uint32_t nm = (1u << kPackNodeBits) - 1u;
+			uint32_t pk[4];
+#pragma unroll
+			for(int k = 0; k < 4; ++k)
+				pk[k] = key[k] < inf ? ((__float_as_uint(fmaxf(key[k], 0.f)) & ~nm) | (uint32_t)child[k]) : 0xffffffffu;
+			auto cx = [](uint32_t &a, uint32_t &b) {
+				const uint32_t lo = min(a, b);
+				b = max(a, b);
+				a = lo;
+			};
+			cx(pk[0], pk[1]);
+			cx(pk[2], pk[3]);
+			cx(pk[0], pk[2]);
+			cx(pk[1], pk[3]);
+			cx(pk[1], pk[2]);
+			if(pk[3] != 0xffffffffu) { push((int)(pk[3] & nm)); ++sp; }
+			if(pk[2] != 0xffffffffu) { push((int)(pk[2] & nm)); ++sp; }
+			if(pk[1] != 0xffffffffu) { push((int)(pk[1] & nm)); ++sp; }
+			next = pk[0] != 0xffffffffu ? (int)(pk[0] & nm) : -1;
 		}
 		else if constexpr(!YAF_CLOSEST_SORT)
 		{
@@ -1247,7 +1284,44 @@ __device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPat
 				prim_best = prim;
 			}
 		}
-		if(!done)
+		if(!done && YAF_W8_SORT && YAF_PACKED_SORT)
+		{
+			// the same network over packed 32-bit keys: the entry distance clamped at 0 with the child's rank
+			// among the node's inner children (consecutive from inner_base) in the low 3 bits, compared as
+			// unsigned integers (v_min_u32 + v_max_u32 per exchange instead of a compare and four selects; no
+			// child array).  The order is a culling heuristic only: closest hits tie-break on the primitive
+			// index and any-hit rays answer occluded or not, so the clamp and the 3 dropped mantissa bits
+			// change no result.  A missed child is all ones.
+			uint32_t pk[8];
+#pragma unroll
+			for(int k = 0; k < 8; ++k)
+				pk[k] = key[k] < inf ? ((__float_as_uint(fmaxf(key[k], 0.f)) & ~7u) | (uint32_t)__builtin_popcount(inner & ((1u << k) - 1u)))
+				                     : 0xffffffffu;
+			auto cx = [](uint32_t &a, uint32_t &b) {
+				const uint32_t lo = min(a, b);
+				b = max(a, b);
+				a = lo;
+			};
+			cx(pk[0], pk[1]); cx(pk[2], pk[3]); cx(pk[4], pk[5]); cx(pk[6], pk[7]);
+			cx(pk[0], pk[2]); cx(pk[1], pk[3]); cx(pk[4], pk[6]); cx(pk[5], pk[7]);
+			cx(pk[1], pk[2]); cx(pk[5], pk[6]);
+			cx(pk[0], pk[4]); cx(pk[1], pk[5]); cx(pk[2], pk[6]); cx(pk[3], pk[7]);
+			cx(pk[2], pk[4]); cx(pk[3], pk[5]);
+			cx(pk[1], pk[2]); cx(pk[3], pk[4]); cx(pk[5], pk[6]);
+#pragma unroll
+			for(int k = 7; k >= 1; --k)
+				if(pk[k] != 0xffffffffu) { push(inner_base + (int)(pk[k] & 7u)); ++sp; }
+			int next = pk[0] != 0xffffffffu ? inner_base + (int)(pk[0] & 7u) : -1;
+			if(next < 0 && sp > 0)
+			{
+				--sp;
+				next = (!SPILL || sp < C.lds_depth) ? C.stack[sp * kTraceBlock + (int)tidFrom(C.wave_base)]
+				                                    : C.spill[(uint32_t)(sp - C.lds_depth) * C.spill_stride + glane];
+			}
+			node = next;
+			done = next < 0;
+		}
+		else if(!done)
 		{
 			if(YAF_W8_SORT)
 			{
@@ -1299,11 +1373,11 @@ __device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPat
 	}
 }
 
-template<bool ANY, bool WIDE, bool SPILL = true, bool TS = false, bool STATS = true>
+template<bool ANY, bool WIDE, bool SPILL = true, bool TS = false, bool STATS = true, bool PACK = false>
 __device__ __forceinline__ bool traverse(const TraceCtx &C, V3 o, V3 d, float tmin, float tmax, float &t_best,
                                          int &prim_best, uint32_t &visits, uint32_t &tests, TsList *ts = nullptr)
 {
-	if(WIDE) return traverse4<ANY, SPILL, TS, STATS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
+	if(WIDE) return traverse4<ANY, SPILL, TS, STATS, PACK>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
 	return traverse2<ANY, TS, STATS>(C, o, d, tmin, tmax, t_best, prim_best, visits, tests, ts);
 }
 
@@ -1478,7 +1552,7 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_TRACE_ATTR k_trace(DevScene S
 				float t;
 				int prim;
 				const float tmax = (tw >= 0.f) ? tw : __builtin_huge_valf();
-				traverse<false, WIDE, SPILL, false, STATS>(C, o, d, tmin, tmax, t, prim, visits, tests);
+				traverse<false, WIDE, SPILL, false, STATS, LDS_SCENE>(C, o, d, tmin, tmax, t, prim, visits, tests);
 				raySt(&Q.hit_t[i], t);
 				raySt(&Q.hit_prim[i], prim);
 				return 1;
@@ -6291,6 +6365,326 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 	}
 }
 
+// ---------------------------------------------------------------------------------------------
+// Final gathering with one lane per gather path (r06; k_fg kept for transparent shadows and scenes in
+// global memory).  k_fg ran one lane per request through its fg_samples paths: the rare paths that bounce
+// (a close or specular first hit: the light estimate with its shadow rays, further traversals) kept
+// ~230 registers live for every lane (89 spilled at 4 waves per SIMD, 4.8 GB of scratch traffic per
+// launch) and held their wave at VALU lane utilisation 0.28.  Here a batch of requests runs as
+//   k_fg_first  one lane per (request, path): the path's first segment (matSample, closest ray), the
+//               radiance-map lookup of the paths that end at their first hit — their one term — and the
+//               paths that bounce appended to a per-segment list with the state after their first hit;
+//   k_fg_long   one lane per bouncing path: finalGathering's bounce loop and last lookup (k_fg's code),
+//               every addition to the path colour kept as a term;
+//   k_fg_sum    one lane per request: the terms summed path by path, in the order k_fg added them
+//               (path_col = path_col + term, integrator_photon_mapping.cc:707-755), bit for bit k_fg's.
+// A batch is the request positions [j0, j0 + seg_cap) of every segment of the gather queue.
+// ---------------------------------------------------------------------------------------------
+
+struct FgPathArgs
+{
+	FgArgs A;
+	FgBatch B;
+};
+
+// k_fg's prologue: the trace context (stack, LDS scene), the nearest-search column, the staged tables
+template<bool LDS_SCENE, bool EXT>
+__device__ __forceinline__ uint32_t *fgPrologue(const FgArgs &A, DevScene &S_, TraceCtx &C, float4 *smem)
+{
+	const DevScene &S = S_;
+	C.wave_base = waveBase();
+	C.stack = reinterpret_cast<int *>(smem);
+	C.lds_depth = A.stack_depth;
+	C.spill = A.spill;
+	C.spill_stride = gridDim.x * blockDim.x;
+	if(LDS_SCENE)
+	{
+		float4 *lds_nodes = smem + (A.stack_depth * kTraceBlock) / 4;
+		float4 *lds_tris = lds_nodes + S.node_f4 * S.n_nodes;
+		for(int k = threadIdx.x; k < S.node_f4 * S.n_nodes; k += blockDim.x) lds_nodes[k] = S.nodes[k];
+		for(int k = threadIdx.x; k < 3 * S.n_tris; k += blockDim.x) lds_tris[k] = S.tris[k];
+		__syncthreads();
+		C.nodes = lds_nodes;
+		C.tris = lds_tris;
+	}
+	else
+	{
+		C.nodes = S.nodes;
+		C.tris = S.tris;
+	}
+	uint32_t *nstk = reinterpret_cast<uint32_t *>(smem + (A.stack_depth * kTraceBlock) / 4 +
+	                                              (LDS_SCENE ? S.node_f4 * S.n_nodes + 3 * S.n_tris : 0)) + threadIdx.x;
+	if(fgStageTables(A.S, LDS_SCENE, EXT, A.stack_depth))
+	{
+		uint4 *tp = reinterpret_cast<uint4 *>(smem + (A.stack_depth * kTraceBlock) / 4 + (S.node_f4 * S.n_nodes + 3 * S.n_tris) +
+		                                      ((size_t)S.rpk_lds * kTraceBlock + 3) / 4);
+		const int nm = A.S.n_mats * (int)(sizeof(DevMaterial) / 16);
+		copy16(tp, A.S.mats, nm);
+		copy16(tp + nm, A.S.prim_ng, A.S.n_tris);
+		__syncthreads();
+		S_.mats = reinterpret_cast<const DevMaterial *>(tp);
+		S_.prim_ng = reinterpret_cast<const float4 *>(tp + nm);
+	}
+	return nstk;
+}
+
+__device__ __forceinline__ void fgStats(const DevScene &S, uint32_t seg, uint32_t n_paths, uint32_t n_lookups, uint32_t n_nvisits)
+{
+	if(!S.stats) return;
+	for(int off = 32; off > 0; off >>= 1)
+	{
+		n_paths += __shfl_down(n_paths, off);
+		n_lookups += __shfl_down(n_lookups, off);
+		n_nvisits += __shfl_down(n_nvisits, off);
+	}
+	if(laneId() == 0)
+	{
+		atomicAdd(&S.stats[seg].fg_paths, (unsigned long long)n_paths);
+		atomicAdd(&S.stats[seg].fg_lookups, (unsigned long long)n_lookups);
+		atomicAdd(&S.stats[seg].fg_nearest_visits, (unsigned long long)n_nvisits);
+	}
+}
+
+// requests of segment `s` in this batch
+__device__ __forceinline__ uint32_t fgBatchRequests(const FgArgs &A, const FgBatch &B, uint32_t s)
+{
+	const uint32_t n_req = A.cnt_next.n_gather[s];
+	return n_req > B.j0 ? min(n_req - B.j0, B.seg_cap) : 0u;
+}
+
+template<bool LDS_SCENE, bool WIDE, bool EXT, bool SPILL>
+__global__ void __launch_bounds__(kTraceBlock) k_fg_first(FgPathArgs PA)
+{
+	const FgArgs &A = PA.A;
+	const FgBatch &B = PA.B;
+	DevScene S_ = A.S;
+	const DevScene &S = S_;
+	extern __shared__ float4 smem[];
+	TraceCtx C;
+	uint32_t *nstk = fgPrologue<LDS_SCENE, EXT>(A, S_, C, smem);
+	uint32_t n_paths = 0, n_lookups = 0, n_nvisits = 0, visits = 0, tests = 0;
+	const bool ATTR = EXT && S.has_attr != 0;
+	const SegLoop L = segLoop(S.n_seg);
+	const uint32_t n_b = fgBatchRequests(A, B, L.s);
+	const uint32_t ns = (uint32_t)B.n_sampl;
+	const uint32_t n_p = n_b * ns;
+	const uint32_t a0 = L.s * S.cap_a;
+	float4 *terms = B.terms + (size_t)L.s * B.seg_cap * ns;
+	for(uint32_t p = L.r * blockDim.x + threadIdx.x; p < n_p; p += L.nb * blockDim.x)
+	{
+		const uint32_t jj = p / ns, i = p - jj * ns;
+		const uint32_t j = a0 + B.j0 + jj;
+		const float4 ex = A.G.extra[j];
+		if(!(__float_as_uint(ex.w) & G_FG)) continue;   // (k_fg_sum skips the request as well)
+		const uint32_t offset = __float_as_uint(ex.x), sample_idx = __float_as_uint(ex.y);
+		const float4 pp = A.G.p_prim[j];
+		Surf sp0 = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
+		if(ATTR) applyAttr(sp0, A.G.attr[2 * (size_t)j], A.G.attr[2 * (size_t)j + 1]);
+		const DevMaterial &m0 = S.mats[sp0.mat];
+		const V3 wo0 = xyz(A.G.wo_k[j]);
+		const uint32_t offs = (uint32_t)S.fg_samples * sample_idx + offset + i;
+		BsdfSample s;
+		s.s_1 = riVdC(offs);
+		s.s_2 = ldsDim(S, 2, offs);
+		s.flags = B_DIFFUSE | B_REFLECT | B_TRANSMIT;
+		s.pdf = 0.f;
+		s.sampled = B_NONE;
+		float w = 0.f;
+		V3 dir = v3(0.f, 0.f, 0.f);
+		C3 scol = matSample<EXT>(m0, sp0, wo0, dir, s, w);
+		scol = scol * w;
+		float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+		if(!isBlack(scol))
+		{
+			const C3 throughput = scol;
+			const V3 from = sp0.p;
+			float t;
+			int prim;
+			++n_paths;
+			if(traverse<false, WIDE, SPILL, false, false, LDS_SCENE>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests))
+			{
+				const Surf hit = fgSurf<EXT>(S, from, dir, t, prim);
+				const uint32_t mat_bsd_fs = hit.flags;
+				const bool close = t < S.fg_min_pathlen;
+				const bool do_bounce = close || (mat_bsd_fs & B_SPECULAR);
+				if(do_bounce && S.fg_bounces > 0)
+				{
+					// the bounce loop runs in k_fg_long (compacted: a wave of bouncing paths)
+					const uint32_t q = atomicAdd(&B.long_count[L.s], 1u);
+					float4 *rec = B.longs + ((size_t)L.s * B.long_cap + q) * 3;
+					rec[0] = f4(from, t);
+					rec[1] = f4(dir, __int_as_float(prim));
+					rec[2] = f4(throughput, __uint_as_float(p));
+					out.w = __uint_as_float(2u + q);
+				}
+				else if(mat_bsd_fs & (B_DIFFUSE | B_GLOSSY))
+				{
+					// the path ends at its first hit: k_fg's last lookup (lcol is still zero here)
+					C3 lcol = c3(0.f);
+					const V3 sf = faceForward(hit.ng, hit.n, -dir);
+					++n_lookups;
+					const int nearest = S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad, nstk, S.rpk_lds, n_nvisits)
+					                                   : pkNearest(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad, &n_nvisits);
+					if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
+					if(mat_bsd_fs & B_EMIT) lcol = lcol + matEmit<EXT>(S.mats[hit.mat], hit, -dir);
+					out = f4(lcol * throughput, __uint_as_float(1u));
+				}
+			}
+		}
+		terms[p] = out;
+	}
+	fgStats(S, L.s, n_paths, n_lookups, n_nvisits);
+}
+
+template<bool LDS_SCENE, bool WIDE, bool EXT, bool SPILL, bool TSH>
+__global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg_long(FgPathArgs PA)
+{
+	const FgArgs &A = PA.A;
+	const FgBatch &B = PA.B;
+	DevScene S_ = A.S;
+	const DevScene &S = S_;
+	extern __shared__ float4 smem[];
+	TraceCtx C;
+	uint32_t *nstk = fgPrologue<LDS_SCENE, EXT>(A, S_, C, smem);
+	uint32_t n_lookups = 0, n_nvisits = 0, visits = 0, tests = 0;
+	auto nearestRad = [&](V3 hp, V3 sf) -> int {
+		++n_lookups;
+		return S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, nstk, S.rpk_lds, n_nvisits)
+		                     : pkNearest(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, &n_nvisits);
+	};
+	const SegLoop L = segLoop(S.n_seg);
+	const uint32_t n_long = B.long_count[L.s];
+	const uint32_t ns = (uint32_t)B.n_sampl;
+	const uint32_t a0 = L.s * S.cap_a;
+	const int n_sampl = B.n_sampl;
+	float2 *ts_buf = TSH ? A.ts_scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * (size_t)S.s_depth : nullptr;
+	for(uint32_t q = L.r * blockDim.x + threadIdx.x; q < n_long; q += L.nb * blockDim.x)
+	{
+		const float4 *rec = B.longs + ((size_t)L.s * B.long_cap + q) * 3;
+		const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+		const uint32_t p = __float_as_uint(r2.w);
+		const uint32_t jj = p / ns, i = p - jj * ns;
+		const uint32_t j = a0 + B.j0 + jj;
+		const float4 ex = A.G.extra[j];
+		const uint32_t offset = __float_as_uint(ex.x), sample_idx = __float_as_uint(ex.y);
+		const uint32_t offs = (uint32_t)S.fg_samples * sample_idx + offset + i;
+		float4 *out = B.long_terms + ((size_t)L.s * B.long_cap + q) * (size_t)B.n_terms;
+		int nt = 0;
+		C3 throughput = rgb(r2);
+		V3 from = xyz(r0), dir = xyz(r1);
+		float t = r0.w;
+		int prim = __float_as_int(r1.w);
+		float w = 0.f;
+		C3 scol;
+		// k_fg from the first hit on (the same statements; path_col additions become terms)
+		Surf hit = fgSurf<EXT>(S, from, dir, t, prim);
+		float length = t;
+		uint32_t mat_bsd_fs = hit.flags;
+		bool did_hit = true;
+		bool caustic = false;
+		bool close = length < S.fg_min_pathlen;
+		bool do_bounce = close || (mat_bsd_fs & B_SPECULAR);
+		C3 lcol = c3(0.f);
+		for(int depth = 0; depth < S.fg_bounces && do_bounce; ++depth)
+		{
+			const int d_4 = 4 * depth;
+			const V3 pwo = -dir;
+			const DevMaterial &mh = S.mats[hit.mat];
+			if(mat_bsd_fs & B_DIFFUSE)
+			{
+				if(close)
+				{
+					const uint32_t lnum = pickLight(S, offset, sample_idx, (uint32_t)i * (uint32_t)max(1, S.fg_bounces) + (uint32_t)depth,
+					                                (uint32_t)n_sampl * (uint32_t)(max(1, S.fg_bounces) + 1));
+					lcol = (S.n_lights > 0)
+					           ? lightEstimateInline<EXT, WIDE, SPILL, TSH>(S, C, S.lights[lnum], mh, hit, pwo, lnum, sample_idx, offset, visits, tests,
+					                                                        ts_buf) *
+					                 (float)S.n_lights
+					           : c3(0.f);
+				}
+				else if(caustic)
+				{
+					const V3 sf = faceForward(hit.ng, hit.n, pwo);
+					const int nearest = nearestRad(hit.p, sf);
+					if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
+				}
+				if(close || caustic)
+				{
+					if(mat_bsd_fs & B_EMIT) lcol = lcol + matEmit<EXT>(mh, hit, pwo);
+					if(nt < B.n_terms) out[nt++] = f4(lcol * throughput, 1.f);
+				}
+			}
+			BsdfSample sb;
+			sb.s_1 = ldsDim(S, d_4 + 3, offs);
+			sb.s_2 = ldsDim(S, d_4 + 4, offs);
+			sb.flags = close ? B_ALL : (B_SPECULAR | B_REFLECT | B_TRANSMIT | B_FILTER);
+			sb.pdf = 0.f;
+			sb.sampled = B_NONE;
+			V3 ndir = v3(0.f, 0.f, 0.f);
+			scol = matSample<EXT>(mh, hit, pwo, ndir, sb, w);
+			if(sb.pdf <= 1.0e-6f) { did_hit = false; break; }
+			scol = scol * w;
+			throughput = throughput * scol;
+			from = hit.p;
+			dir = ndir;
+			if(!traverse<false, WIDE, SPILL>(C, from, dir, S.ray_min_dist, __builtin_huge_valf(), t, prim, visits, tests)) { did_hit = false; break; }
+			hit = fgSurf<EXT>(S, from, dir, t, prim);
+			mat_bsd_fs = hit.flags;
+			length += t;
+			caustic = (caustic || !depth) && (sb.sampled & (B_SPECULAR | B_FILTER));
+			close = length < S.fg_min_pathlen;
+			do_bounce = caustic || close;
+		}
+		if(did_hit && (mat_bsd_fs & (B_DIFFUSE | B_GLOSSY)))
+		{
+			const V3 sf = faceForward(hit.ng, hit.n, -dir);
+			const int nearest = nearestRad(hit.p, sf);
+			if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
+			if(mat_bsd_fs & B_EMIT) lcol = lcol + matEmit<EXT>(S.mats[hit.mat], hit, -dir);
+			if(nt < B.n_terms) out[nt++] = f4(lcol * throughput, 1.f);
+		}
+		for(int k = nt; k < B.n_terms; ++k) out[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+	}
+	fgStats(S, L.s, 0u, n_lookups, n_nvisits);
+}
+
+__global__ void __launch_bounds__(256) k_fg_sum(FgPathArgs PA)
+{
+	const FgArgs &A = PA.A;
+	const FgBatch &B = PA.B;
+	const DevScene &S = A.S;
+	const uint32_t s = blockIdx.y;
+	const uint32_t n_b = fgBatchRequests(A, B, s);
+	const uint32_t ns = (uint32_t)B.n_sampl;
+	const uint32_t a0 = s * S.cap_a;
+	for(uint32_t jj = blockIdx.x * blockDim.x + threadIdx.x; jj < n_b; jj += gridDim.x * blockDim.x)
+	{
+		const uint32_t j = a0 + B.j0 + jj;
+		if(!(__float_as_uint(A.G.extra[j].w) & G_FG)) continue;
+		const float4 *tp = B.terms + ((size_t)s * B.seg_cap + jj) * ns;
+		C3 path_col = c3(0.f);
+		for(uint32_t i = 0; i < ns; ++i)
+		{
+			const float4 tv = tp[i];
+			const uint32_t tag = __float_as_uint(tv.w);
+			if(tag == 1u) path_col = path_col + rgb(tv);
+			else if(tag >= 2u)
+			{
+				const float4 *lt = B.long_terms + ((size_t)s * B.long_cap + (tag - 2u)) * (size_t)B.n_terms;
+				for(int k = 0; k < B.n_terms; ++k)
+				{
+					const float4 v = lt[k];
+					if(v.w != 0.f) path_col = path_col + rgb(v);
+				}
+			}
+		}
+		const C3 fg = path_col / (float)B.n_sampl;
+		const uint4 cb = A.G.pix_mode[j];
+		const C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)} + fg;
+		A.G.pix_mode[j] = make_uint4(__float_as_uint(col.r), __float_as_uint(col.g), __float_as_uint(col.b), cb.w);
+	}
+}
+
 } // namespace yafamd
 
 // ---------------------------------------------------------------------------------------------
@@ -6879,6 +7273,49 @@ hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCo
 	else YAF_FG_LAUNCH(false, false, false, stack_bytes + nstk_bytes);
 #undef YAF_FG_LAUNCH
 #undef YAF_FG_LAUNCH_NS
+	return hipGetLastError();
+}
+
+// the per-path final gathering (k_fg_first / k_fg_long / k_fg_sum) serves this scene: LDS-resident scenes
+// without transparent shadows (k_fg keeps the others); YAFARAY_AMD_FG=lane forces k_fg (tests, A/B)
+int yafamd_fg_paths_eligible(const DevScene *S)
+{
+	if(!S->scene_in_lds || S->tr_shad) return 0;
+	const char *e = getenv("YAFARAY_AMD_FG");
+	return (e && std::string(e) == "lane") ? 0 : 1;
+}
+
+// one batch of the per-path final gathering: the caller zeroed B->long_count (n_seg words)
+hipError_t yafamd_launch_fg_paths(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid,
+                                  const FgBatch *B, hipStream_t st)
+{
+	if(!yafamd_fg_paths_eligible(S)) return hipErrorInvalidValue;
+	FgPathArgs PA;
+	PA.A.S = *S;
+	PA.A.G = *G;
+	PA.A.cnt_next = *cnt_next;
+	PA.A.stack_depth = stack_depth;
+	PA.A.spill = spill;
+	PA.A.ts_scratch = nullptr;
+	PA.B = *B;
+	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
+	const size_t nstk_bytes = (size_t)S->rpk_lds * kTraceBlock * sizeof(uint32_t);
+	const size_t stage_bytes = fgStageTables(*S, true, S->ext != 0, stack_depth)
+	                               ? ((nstk_bytes + 15) & ~(size_t)15) + (size_t)S->n_mats * sizeof(DevMaterial) + (size_t)S->n_tris * 16
+	                               : nstk_bytes;
+	const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) + stage_bytes;
+	const bool wide = S->node_f4 == 8, ext = S->ext != 0, sp = spill != nullptr;
+#define YAF_FGP(W, E, SP)                                                                                                      \
+	do                                                                                                                         \
+	{                                                                                                                          \
+		hipLaunchKernelGGL((k_fg_first<true, W, E, SP>), dim3(grid), dim3(kTraceBlock), bytes, st, PA);                       \
+		hipLaunchKernelGGL((k_fg_long<true, W, E, SP, false>), dim3(grid), dim3(kTraceBlock), bytes, st, PA);                 \
+	} while(0)
+	if(wide) { if(ext) { if(sp) YAF_FGP(true, true, true); else YAF_FGP(true, true, false); } else { if(sp) YAF_FGP(true, false, true); else YAF_FGP(true, false, false); } }
+	else { if(ext) { if(sp) YAF_FGP(false, true, true); else YAF_FGP(false, true, false); } else { if(sp) YAF_FGP(false, false, true); else YAF_FGP(false, false, false); } }
+#undef YAF_FGP
+	const uint32_t gx = min((B->seg_cap + 255u) / 256u, 64u);
+	hipLaunchKernelGGL(k_fg_sum, dim3(gx, S->n_seg), dim3(256), 0, st, PA);
 	return hipGetLastError();
 }
 

@@ -65,6 +65,9 @@ hipError_t yafamd_rad_compact(const PhotonState *P, uint32_t *scratch_counts, ui
 hipError_t yafamd_rad_refl(const DevScene *S, float4 *a, float4 *b, float4 *c, const uint32_t *kept, uint32_t n, hipStream_t st);
 hipError_t yafamd_pregather(const DevScene *S, const float4 *a, const float4 *b, const float4 *c, const uint32_t *kept, uint32_t n,
                             float4 *out_pos, float4 *out_dir, float *out_colb, DevStats *stats, hipStream_t st);
+int yafamd_fg_paths_eligible(const DevScene *S);
+hipError_t yafamd_launch_fg_paths(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid,
+                                  const FgBatch *B, hipStream_t st);
 hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out, uint32_t *n_kept,
                                   int *rounds_out, hipStream_t st, void **scratch);
 void yafamd_thin_scratch_free(void *scratch);
@@ -254,6 +257,7 @@ struct GpuRenderer::Impl
 	int n_nodes8 = 0, need8 = 0, lds_top8 = 0, depth8 = 0;
 	int trace_grid_bvh4 = 0;   // the grid of the BVH4 k_trace when a BVH8 exists (transparent shadows)
 	Buf pre_stats;             // k_pregather's counters (one DevStats)
+	Buf fg_terms, fg_longs, fg_long_terms, fg_long_count;   // the per-path final gathering's batch buffers (FgBatch)
 	bool pre_stats_valid = false;
 	// surface attributes, textures and shader-node programs (texeval.h)
 	Buf prim_attr, shader_nodes, textures, texels;
@@ -372,7 +376,8 @@ struct GpuRenderer::Impl
 			b->release();
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
-		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &walk_spill, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris, &pre_stats}) b->release();
+		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &walk_spill, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris, &pre_stats, &fg_terms, &fg_longs,
+		              &fg_long_terms, &fg_long_count}) b->release();
 		for(int m = 0; m < 3; ++m)
 			for(Buf *b : {&kd_pos[m], &kd_dir[m], &kd_colb[m]}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
@@ -645,6 +650,8 @@ bool GpuRenderer::upload(HostScene &hs)
 	if(const char *e = getenv("YAFARAY_AMD_LDS_STACK"); e && *e) d.lds_stack = std::min(d.stack_depth, std::max(4, atoi(e)));
 	const size_t scene_bytes = (size_t)(d.node_f4 * d.n_nodes + 3 * d.n_tris) * 16;
 	d.scene_in_lds = scene_bytes + (size_t)d.lds_stack * yafamd_trace_block() * 4 <= 48 * 1024;
+	// (k_trace's packed child keys carry a node index in 9 bits: 48 KB holds at most 384 BVH4 nodes)
+	if(d.node_f4 == 8 && d.n_nodes >= 512) d.scene_in_lds = false;
 	if(const char *e = getenv("YAFARAY_AMD_SCENE_LDS"); e && *e == '0') d.scene_in_lds = false;   // tests: global-memory traversal on small scenes
 	// a BVH4 in global memory: k_trace's refill loop reads the top treelet (the first levels, which
 	// every ray visits) from LDS — 21 nodes = the root and two full levels below it, 2.7 KB per
@@ -1821,6 +1828,28 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			walk_gather = true;
 		}
 	}
+	// final gathering with one lane per gather path (kernels.hip k_fg_first / k_fg_long / k_fg_sum): its batch
+	// buffers, sized for the pass's path count (AA_indirect_sample_multiplier_factor changes it per pass) with
+	// room for every path to bounce (no overflow); a batch is seg_cap request positions of every segment,
+	// within 6 GB
+	const bool fg_paths = yafamd_fg_paths_eligible(&S) != 0;
+	FgBatch fgb{};
+	auto fgPrepare = [&]() -> bool {
+		const int ns = S.fg_pass_samples > 0 ? S.fg_pass_samples : std::max(1, S.fg_samples);
+		const int nt = std::max(0, S.fg_bounces) + 1;
+		const size_t per_pos = (size_t)R * (size_t)ns * (16 + 48 + 16 * (size_t)nt);
+		size_t cap_max = std::max<size_t>(1, ((size_t)6 << 30) / per_pos);
+		if(const char *e = getenv("YAFARAY_AMD_FG_BATCH"); e && atoi(e) > 0) cap_max = std::min(cap_max, (size_t)atoi(e));   // tests: several batches
+		const size_t nb = ((size_t)S.cap_a + cap_max - 1) / cap_max;
+		const size_t seg_cap = std::max<size_t>(1, ((size_t)S.cap_a + nb - 1) / std::max<size_t>(1, nb));
+		const size_t paths = (size_t)R * seg_cap * (size_t)ns;
+		if(!ensure(log_, d.fg_terms, paths * 16) || !ensure(log_, d.fg_longs, paths * 48) || !ensure(log_, d.fg_long_terms, paths * 16 * (size_t)nt) ||
+		   !ensure(log_, d.fg_long_count, (size_t)R * 4))
+			return false;
+		fgb = FgBatch{0u, (uint32_t)seg_cap, ns, nt, (float4 *)d.fg_terms.p, (float4 *)d.fg_longs.p, (float4 *)d.fg_long_terms.p,
+		              (uint32_t *)d.fg_long_count.p, (uint32_t)(seg_cap * (size_t)ns)};
+		return true;
+	};
 	if(!ensure(log_, d.counters, 2 * 4 * R * sizeof(uint32_t))) return false;
 	if(!ensure(log_, d.stats, sizeof(DevStats) * (size_t)d.trace_grid)) return false;
 	HIPCHECK(hipMemsetAsync(d.counters.p, 0, 2 * 4 * R * sizeof(uint32_t), d.stream));
@@ -1924,7 +1953,19 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			if(S.gather_on && !count_run && (!dl_pipeline || it == 1 || (S.show_map && it == 0)))
 			{
 				// final gathering adds its estimate to the requests' colour before k_gather ends them
-				if(S.fg_on)
+				if(S.fg_on && fg_paths)
+				{
+					if(!fgPrepare()) return false;
+					// one lane per gather path, in batches of request positions (every segment's [j0, j0 + seg_cap))
+					for(uint32_t j0 = 0; j0 < S.cap_a; j0 += fgb.seg_cap)
+					{
+						FgBatch B = fgb;
+						B.j0 = j0;
+						HIPCHECK(hipMemsetAsync(fgb.long_count, 0, (size_t)S.n_seg * 4, d.stream));
+						PROF(KK_FG, yafamd_launch_fg_paths(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, &B, d.stream));
+					}
+				}
+				else if(S.fg_on)
 					PROF(KK_FG, yafamd_launch_fg(&S, &d.G, &cnt[cur ^ 1], d.lds_stack, (int *)d.spill.p, d.trace_grid, (float2 *)d.fg_ts.p, d.stream));
 				if(walk_gather)
 					for(uint32_t j0 = 0; j0 < S.cap_a; j0 += glog.seg_cap)
@@ -2396,7 +2437,7 @@ void yafamd::pinnedFree(void *q)
 	else std::free(p);
 }
 
-bool GpuRenderer::download(PinnedFloats &rgba, PinnedFloats &weights, int w, int h)
+bool GpuRenderer::download(PinnedFloats &rgba, PinnedFloats &weights, int w, int h, bool with_rgba, bool with_weights)
 {
 	DeviceGuard guard(device_);
 	Impl &d = *d_;
@@ -2404,8 +2445,8 @@ bool GpuRenderer::download(PinnedFloats &rgba, PinnedFloats &weights, int w, int
 	// the buffers keep their size across frames (no re-allocation, no re-pinning after the first)
 	if(rgba.size() != (size_t)w * h * 4) rgba.resize((size_t)w * h * 4);
 	if(weights.size() != (size_t)w * h) weights.resize((size_t)w * h);
-	HIPCHECK(hipMemcpyAsync(rgba.data(), d.film.p, rgba.size() * 4, hipMemcpyDeviceToHost, d.stream));
-	HIPCHECK(hipMemcpyAsync(weights.data(), d.weights.p, weights.size() * 4, hipMemcpyDeviceToHost, d.stream));
+	if(with_rgba) HIPCHECK(hipMemcpyAsync(rgba.data(), d.film.p, rgba.size() * 4, hipMemcpyDeviceToHost, d.stream));
+	if(with_weights) HIPCHECK(hipMemcpyAsync(weights.data(), d.weights.p, weights.size() * 4, hipMemcpyDeviceToHost, d.stream));
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	return true;
 }

@@ -188,7 +188,8 @@ class GpuRenderer
 		int lastPassCount() const { return passes_done_; }
 		uint32_t samplingOffset() const { return sampling_offset_; }   // ImageFilm::sampling_offset_ after the last pass
 		bool downloadAccum(std::vector<float> &rgba, std::vector<float> &weights);   // unnormalised film (film files)   // AA passes rendered by the last render()
-		bool download(PinnedFloats &rgba, PinnedFloats &weights, int w, int h);   // one stream sync, DMA into pinned memory
+		// one stream sync, DMA into pinned memory; either part can be skipped
+		bool download(PinnedFloats &rgba, PinnedFloats &weights, int w, int h, bool with_rgba = true, bool with_weights = true);
 		bool filmToDevice(void *dst, int y0, int y1);
 		bool traceRays(bool any, const float *rays, int n, float *t, int *prim);
 		bool buildPhotonMap(RenderParams &rp);

@@ -182,3 +182,35 @@ def test_final_gather_nearest_lds_stack_equals_private(product, monkeypatch):
     b, wb, _ = product.render_spec(spec)
     assert np.array_equal(w.view(np.uint32), wb.view(np.uint32))
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["default", "close-paths", "specular", "textured", "batches"])
+def test_final_gather_per_path_lanes_equal_lane_per_request(product, monkeypatch, case):
+    """r06: final gathering with one lane per gather path (k_fg_first / k_fg_long / k_fg_sum: the bouncing
+    paths compacted into their own launch, each path's additions kept as terms and summed per request in
+    path order) gives the film of k_fg's one lane per request (YAFARAY_AMD_FG=lane) bit for bit — the
+    reference's addition order (integrator_photon_mapping.cc:707-755) is unchanged."""
+    if case == "textured":
+        import texscenes as T
+        mats, imgs, texs = T.CASES["layers"]()
+        spec = T.grid_scene(mats, imgs, texs, width=40, height=30, spp=1, sphere_smooth=60.0)
+        spec = spec.with_render(integrator="photonmapping", pm_photons=20000, pm_search=30, pm_diffuse_radius=0.4,
+                                pm_final_gather=True, fg_samples=4, fg_min_pathlen=1.5)
+    elif case == "specular":
+        spec = fg_spec(specular=True, fg_min_pathlen=0.3)
+    elif case == "close-paths":
+        spec = fg_spec(fg_min_pathlen=0.8, fg_bounces=3, fg_samples=6)
+    else:
+        spec = fg_spec(W=64, H=48, fg_samples=8)
+    if case == "batches":
+        monkeypatch.setenv("YAFARAY_AMD_FG_BATCH", "7")   # request positions per segment and batch: several batches
+    a, w, st = product.render_spec(spec, profile=True)
+    monkeypatch.delenv("YAFARAY_AMD_FG_BATCH", raising=False)
+    monkeypatch.setenv("YAFARAY_AMD_FG", "lane")
+    b, wb, st_b = product.render_spec(spec, profile=True)
+    assert np.array_equal(w.view(np.uint32), wb.view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), int(ulp_diff(a, b).max())
+    # the same paths and radiance-map lookups were counted by both kernels
+    for k in ("fg_paths", "fg_lookups", "fg_nearest_visits"):
+        assert st[k] == st_b[k] and st[k] > 0, (k, st[k], st_b[k])
