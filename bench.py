@@ -129,7 +129,8 @@ def load_pmc(a, W, H):
 # ---------------------------------------------------------------------------------------------
 # kernel kinds that are one kernel (per-launch PMC instruction counts map onto their launches); the
 # others (pkd_build, photon_compact, aa_next_pass) are sequences of several kernels per launch record
-SINGLE_KERNEL_KINDS = {"k_trace", "k_shade", "k_nee", "k_camera", "k_film", "k_gather", "k_gather_walk", "k_fg", "k_pregather", "k_surface",
+# (k_fg: k_fg_first + k_fg_long + k_fg_sum per batch record, r06; k_pregather: k_rad_refl + k_pregather)
+SINGLE_KERNEL_KINDS = {"k_trace", "k_shade", "k_nee", "k_camera", "k_film", "k_gather", "k_gather_walk", "k_surface",
                        "k_tshadow", "k_photon_emit", "k_photon_bounce", "k_spawn", "k_combine"}
 # SURVEY §8d per-ray algorithmic bytes with the reference kd-tree's measured counts
 # (B_ray = N_node * 8 + N_tri * 40 + ray I/O): C2 closest 273 / shadow 235 B, C4 509 / 793 B

@@ -17,6 +17,21 @@ namespace yafamd
 {
 struct DevStats;
 
+// Final gathering's radiance map as a dense uniform grid (fgthin.hip yafamd_rad_grid, r06), next to its point
+// kd-tree: cells of `cell` >= half the lookup radius, the photons in cell order (pos: position + the photon's
+// index in the map's arrays as bits; dir: its normal), start[c] .. start[c + 1] the photons of cell c (cells
+// x-fastest).  findNearest over it (kernels.hip gridNearest) returns the kd search's photon whenever the nearest
+// facing distance is unique; a tie falls back to the kd search (the reference's visit order decides it).
+struct RadGrid
+{
+	const uint32_t *start;   // null: no grid
+	const float4 *pos;
+	const float4 *dir;
+	float lo[3];
+	float cell, inv_cell;
+	int nx, ny, nz;
+};
+
 enum : uint32_t
 {
 	B_NONE = 0, B_SPECULAR = 1u << 0, B_GLOSSY = 1u << 1, B_DIFFUSE = 1u << 2, B_DISPERSIVE = 1u << 3,
@@ -263,6 +278,7 @@ struct DevScene
 	int n_rphotons;
 	int rpk_lds;                   // k_fg: levels of the radiance-map nearest search held in an LDS column (tree depth + 1;
 	                               // 0: the private-array stack)
+	RadGrid rgrid;                 // the radiance map's uniform grid (k_fg_first / k_fg_long; start null: the kd search)
 
 	// surface attributes and shader nodes: only when some material has nodes or some mesh has
 	// orco / uv / smooth normals (has_attr); k_surface then fills DevQueues::sattr per hit
@@ -313,6 +329,7 @@ struct DevScene
 	int w_live;            // 1: the integrator's sample weight w must persist across vertices (DevPaths::thr.w); 0: thr is a 12-B record
 	int no_lean;           // 1: the general k_shade / k_nee instantiations even where a lean one applies (YAFARAY_AMD_SHADE_LEAN=0: tests, A/B)
 	int has_mesh_light;    // some light is a meshlight (k_nee's lean instantiation has no meshlight code)
+	int fg_probe;          // diagnostic (YAFARAY_AMD_FG_PROBE, wrong images): 1 = k_fg_first skips its radiance-map lookups
 };
 
 struct DevFilm

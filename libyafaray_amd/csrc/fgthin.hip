@@ -18,9 +18,12 @@
 // order at the end.  Host twin: render.cc eliminateRadPoints.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <vector>
+
+#include "devscene.h"
 
 namespace
 {
@@ -271,6 +274,113 @@ struct IsKept
 	} while(0)
 
 extern "C" void yafamd_thin_scratch_free(void *scratch) { delete static_cast<ThinScratch *>(scratch); }
+
+// ---- final gathering's radiance-map grid (findNearest over cells, kernels.hip gridNearest) ----
+struct RadGridScratch
+{
+	ThinBuf part, cid, count, start, order, tmp, gpos, gdir;
+	~RadGridScratch()
+	{
+		for(ThinBuf *b : {&part, &cid, &count, &start, &order, &tmp, &gpos, &gdir})
+			if(b->p) (void)hipFree(b->p);
+	}
+};
+
+__device__ __forceinline__ int radCell(float v, float lo, float inv_cell, int na)
+{
+	const int c = (int)floorf((v - lo) * inv_cell);
+	return c < 0 ? 0 : (c >= na ? na - 1 : c);
+}
+
+__global__ void __launch_bounds__(256) k_rg_cells(const float4 *pos, uint32_t n, yafamd::RadGrid g, uint32_t *cid, uint32_t *count)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const float4 p = pos[i];
+	const uint32_t c = (uint32_t)((radCell(p.z, g.lo[2], g.inv_cell, g.nz) * g.ny + radCell(p.y, g.lo[1], g.inv_cell, g.ny)) * g.nx +
+	                              radCell(p.x, g.lo[0], g.inv_cell, g.nx));
+	cid[i] = c;
+	atomicAdd(&count[c], 1u);
+}
+
+// cell order: the photon's position + its index (bits) and its normal
+__global__ void __launch_bounds__(256) k_rg_fill(const float4 *pos, const float4 *dir, const uint32_t *cid, uint32_t n, const uint32_t *start,
+                                                uint32_t *fill, float4 *gpos, float4 *gdir)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const uint32_t c = cid[i];
+	const uint32_t k = start[c] + atomicAdd(&fill[c], 1u);   // order inside a cell is irrelevant (minimum + tie test)
+	const float4 p = pos[i];
+	gpos[k] = make_float4(p.x, p.y, p.z, __uint_as_float(i));
+	gdir[k] = dir[i];
+}
+
+extern "C" void yafamd_rad_grid_free(void *scratch) { delete static_cast<RadGridScratch *>(scratch); }
+
+// The grid over the radiance map's n photons (pos / dir: the arrays the lookups index, kd order), cell =
+// sqrt(lookup_rad) / 3: the nearest radiance photon is mostly within the 3 x 3 x 3 cells around a point
+// (gridNearest grows its block only when it is not).  hipErrorNotSupported above 2^22 cells (the kd search serves then).  The grid lives in *scratch
+// until the next build.
+extern "C" hipError_t yafamd_rad_grid(const float4 *pos, const float4 *dir, uint32_t n, float lookup_rad, yafamd::RadGrid *out, hipStream_t st,
+                                      void **scratch)
+{
+	*out = yafamd::RadGrid{};
+	if(n == 0 || !(lookup_rad > 0.f)) return hipErrorNotSupported;
+	if(!scratch) return hipErrorInvalidValue;
+	if(!*scratch) *scratch = new RadGridScratch;
+	RadGridScratch &S = *static_cast<RadGridScratch *>(*scratch);
+	THCHECK(S.part.ensure(2 * kBoundBlocks * sizeof(float4)));
+	hipLaunchKernelGGL(k_thin_bound, dim3(kBoundBlocks), dim3(256), 0, st, pos, n, S.part.as<float4>());
+	std::vector<float4> part(2 * kBoundBlocks);
+	THCHECK(hipMemcpyAsync(part.data(), S.part.p, part.size() * sizeof(float4), hipMemcpyDeviceToHost, st));
+	THCHECK(hipStreamSynchronize(st));
+	float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+	for(int b = 0; b < kBoundBlocks; ++b)
+	{
+		const float4 l = part[2 * b], h = part[2 * b + 1];
+		lo[0] = std::min(lo[0], l.x); lo[1] = std::min(lo[1], l.y); lo[2] = std::min(lo[2], l.z);
+		hi[0] = std::max(hi[0], h.x); hi[1] = std::max(hi[1], h.y); hi[2] = std::max(hi[2], h.z);
+	}
+	const double cell = std::sqrt((double)lookup_rad) / 3.0;
+	double dims[3], ncell = 1.0;
+	for(int a = 0; a < 3; ++a)
+	{
+		if(!std::isfinite(lo[a]) || !std::isfinite(hi[a])) return hipErrorNotSupported;
+		dims[a] = std::floor(((double)hi[a] - (double)lo[a]) / cell) + 1.0;
+		ncell *= dims[a];
+	}
+	if(!(ncell <= (double)(1 << 22))) return hipErrorNotSupported;
+	yafamd::RadGrid g{};
+	for(int a = 0; a < 3; ++a) g.lo[a] = lo[a];
+	g.cell = (float)cell;
+	g.inv_cell = (float)(1.0 / cell);
+	g.nx = (int)dims[0];
+	g.ny = (int)dims[1];
+	g.nz = (int)dims[2];
+	const uint32_t nc = (uint32_t)ncell;
+	THCHECK(S.cid.ensure((size_t)n * 4));
+	THCHECK(S.count.ensure(((size_t)nc + 1) * 4));
+	THCHECK(S.start.ensure(((size_t)nc + 1) * 4));
+	THCHECK(S.gpos.ensure((size_t)n * sizeof(float4)));
+	THCHECK(S.gdir.ensure((size_t)n * sizeof(float4)));
+	THCHECK(hipMemsetAsync(S.count.p, 0, ((size_t)nc + 1) * 4, st));
+	const dim3 blocks((n + 255) / 256);
+	hipLaunchKernelGGL(k_rg_cells, blocks, dim3(256), 0, st, pos, n, g, S.cid.as<uint32_t>(), S.count.as<uint32_t>());
+	size_t scan_bytes = 0;
+	THCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, S.count.as<uint32_t>(), S.start.as<uint32_t>(), (int)nc + 1, st));
+	THCHECK(S.tmp.ensure(scan_bytes));
+	THCHECK(hipcub::DeviceScan::ExclusiveSum(S.tmp.p, scan_bytes, S.count.as<uint32_t>(), S.start.as<uint32_t>(), (int)nc + 1, st));
+	THCHECK(hipMemsetAsync(S.count.p, 0, ((size_t)nc + 1) * 4, st));
+	hipLaunchKernelGGL(k_rg_fill, blocks, dim3(256), 0, st, pos, dir, S.cid.as<uint32_t>(), n, S.start.as<uint32_t>(), S.count.as<uint32_t>(),
+	                   S.gpos.as<float4>(), S.gdir.as<float4>());
+	THCHECK(hipGetLastError());
+	g.start = S.start.as<uint32_t>();
+	g.pos = S.gpos.as<float4>();
+	g.dir = S.gdir.as<float4>();
+	*out = g;
+	return hipSuccess;
+}
 
 // pos / nrm: the compacted radiance points (xyz used); kept_out: device, n entries of capacity.
 // Returns hipErrorNotSupported when the dense grid would exceed 2^26 cells (the caller thins on the

@@ -5900,6 +5900,75 @@ __device__ int pkNearest(const uint4 *nodes, const float4 *dirs, V3 p, V3 n, flo
 	return nearest;
 }
 
+// PhotonMap::findNearest over the radiance map's uniform grid (RadGrid, fgthin.hip yafamd_rad_grid): the
+// facing photon of smallest distance below max_d2 — the photon the kd search (pkNearest) returns, whose only
+// dependence on its visit order is which of several facing photons at exactly the same smallest distance it
+// keeps (its test is strict: the first one visited).  Such a tie returns -2 and the caller asks the kd search.
+// The search grows a block of cells around the point's cell: R = 1 (3 x 3 x 3 cells) first, and a larger block
+// only while the best distance so far is not below the block's reach (R cells: every photon outside the block
+// is at least that far); rows of 2R + 1 cells along x are contiguous in cell order, and a row farther than the
+// best distance (its box, with a margin for the cell rounding) is skipped.  A photon tested again in a larger
+// block changes nothing (not below the best, and the tie test skips the kept photon).  The distance and facing
+// tests are pkNearest's expressions, so an accepted photon is one it accepts.
+__device__ int gridNearest(const RadGrid &g, V3 p, V3 n, float max_d2, uint32_t &visits)
+{
+	auto cellOf = [](float v, float lo, float inv, int na) {
+		const int c = (int)floorf((v - lo) * inv);
+		return c < 0 ? 0 : (c >= na ? na - 1 : c);
+	};
+	const int cx = cellOf(p.x, g.lo[0], g.inv_cell, g.nx), cy = cellOf(p.y, g.lo[1], g.inv_cell, g.ny), cz = cellOf(p.z, g.lo[2], g.inv_cell, g.nz);
+	const float margin = 1e-3f * g.cell;
+	// squared distance from p to the slab [a, b] of one axis (0 inside)
+	auto axisD = [](float v, float a, float b) {
+		const float d = v < a ? a - v : (v > b ? v - b : 0.f);
+		return d * d;
+	};
+	// cells per axis that cover the lookup radius (RadGrid: cell >= half of it)
+	const int r_max = (int)ceilf(sqrtf(max_d2) * g.inv_cell * 1.001f) + 1;
+	float best = max_d2;
+	int res = -1;
+	bool tie = false;
+#pragma unroll 1
+	for(int R = 1;; ++R)
+	{
+		const int x0 = max(cx - R, 0), x1 = min(cx + R, g.nx - 1);
+		const float dxx = axisD(p.x, g.lo[0] + (float)x0 * g.cell - margin, g.lo[0] + (float)(x1 + 1) * g.cell + margin);
+#pragma unroll 1
+		for(int z = max(cz - R, 0); z <= min(cz + R, g.nz - 1); ++z)
+		{
+			const float dz = axisD(p.z, g.lo[2] + (float)z * g.cell - margin, g.lo[2] + (float)(z + 1) * g.cell + margin);
+#pragma unroll 1
+			for(int y = max(cy - R, 0); y <= min(cy + R, g.ny - 1); ++y)
+			{
+				const float dy = axisD(p.y, g.lo[1] + (float)y * g.cell - margin, g.lo[1] + (float)(y + 1) * g.cell + margin);
+				if(dxx + dy + dz > best) continue;   // no photon of this row is as close as the best
+				const uint32_t base = (uint32_t)((z * g.ny + y) * g.nx);
+				const uint32_t k0 = g.start[base + (uint32_t)x0], k1 = g.start[base + (uint32_t)x1 + 1u];
+				visits += 1u + (k1 - k0);   // (statistics: the row's start words and its photon records, 16 B each)
+				for(uint32_t k = k0; k < k1; ++k)
+				{
+					const float4 q = g.pos[k];
+					const V3 v = v3(q.x, q.y, q.z) - p;
+					const float dist_2 = v.x * v.x + v.y * v.y + v.z * v.z;
+					if(dist_2 <= best)
+					{
+						const int idx = (int)__float_as_uint(q.w);
+						if(dot(xyz(g.dir[k]), n) > 0.f)
+						{
+							if(dist_2 < best) { best = dist_2; res = idx; tie = false; }
+							else if(res >= 0 && idx != res) tie = true;   // same smallest distance as the photon kept
+						}
+					}
+				}
+			}
+		}
+		// every photon outside this block is at least R cells (less the margin) from p, whose cell is its centre
+		const float reach = fmaxf((float)R * g.cell - 2.f * margin, 0.f);
+		if(R >= r_max || best < reach * reach) break;
+	}
+	return tie ? -2 : res;
+}
+
 // pkNearest with its far-child stack in an LDS column (4 B per level, stk[level * STRIDE]; cap >= the
 // tree depth, so nothing is dropped): a popped interior node carries its parent's plane (pkd.hip), from
 // which the distance pkNearest stacked is recomputed for its pop-time test; a popped leaf goes to the
@@ -6381,6 +6450,8 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg(FgArgs A)
 // A batch is the request positions [j0, j0 + seg_cap) of every segment of the gather queue.
 // ---------------------------------------------------------------------------------------------
 
+constexpr uint32_t kFgDone = 0xffffffffu;   // terms tag of a request's first path: k_fg_first already added its paths
+
 struct FgPathArgs
 {
 	FgArgs A;
@@ -6470,12 +6541,18 @@ __global__ void __launch_bounds__(kTraceBlock) k_fg_first(FgPathArgs PA)
 	const uint32_t n_p = n_b * ns;
 	const uint32_t a0 = L.s * S.cap_a;
 	float4 *terms = B.terms + (size_t)L.s * B.seg_cap * ns;
+	// a request's paths are one aligned group of ns lanes when ns divides the wave: a group without a bouncing
+	// path folds its terms in path order right here (k_fg_sum then skips the request)
+	const bool fold = (64u % ns) == 0u;
 	for(uint32_t p = L.r * blockDim.x + threadIdx.x; p < n_p; p += L.nb * blockDim.x)
 	{
 		const uint32_t jj = p / ns, i = p - jj * ns;
 		const uint32_t j = a0 + B.j0 + jj;
 		const float4 ex = A.G.extra[j];
-		if(!(__float_as_uint(ex.w) & G_FG)) continue;   // (k_fg_sum skips the request as well)
+		const bool req_fg = (__float_as_uint(ex.w) & G_FG) != 0u;   // (k_fg_sum skips the others as well)
+		float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+		if(req_fg)
+		{
 		const uint32_t offset = __float_as_uint(ex.x), sample_idx = __float_as_uint(ex.y);
 		const float4 pp = A.G.p_prim[j];
 		Surf sp0 = surfFromPrim(S, xyz(pp), __float_as_int(pp.w));
@@ -6493,7 +6570,6 @@ __global__ void __launch_bounds__(kTraceBlock) k_fg_first(FgPathArgs PA)
 		V3 dir = v3(0.f, 0.f, 0.f);
 		C3 scol = matSample<EXT>(m0, sp0, wo0, dir, s, w);
 		scol = scol * w;
-		float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
 		if(!isBlack(scol))
 		{
 			const C3 throughput = scol;
@@ -6523,15 +6599,47 @@ __global__ void __launch_bounds__(kTraceBlock) k_fg_first(FgPathArgs PA)
 					C3 lcol = c3(0.f);
 					const V3 sf = faceForward(hit.ng, hit.n, -dir);
 					++n_lookups;
-					const int nearest = S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad, nstk, S.rpk_lds, n_nvisits)
-					                                   : pkNearest(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad, &n_nvisits);
+					int nearest = S.fg_probe == 1 ? -1 : S.rgrid.start ? gridNearest(S.rgrid, hit.p, sf, S.fg_lookup_rad, n_nvisits) : -2;
+					if(nearest == -2)
+						nearest = S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad, nstk, S.rpk_lds, n_nvisits)
+						                        : pkNearest(S.rpk_nodes, S.rph_dir, hit.p, sf, S.fg_lookup_rad, &n_nvisits);
 					if(nearest >= 0) lcol = C3{S.rph_pos[nearest].w, S.rph_dir[nearest].w, S.rph_colb[nearest]};
 					if(mat_bsd_fs & B_EMIT) lcol = lcol + matEmit<EXT>(S.mats[hit.mat], hit, -dir);
 					out = f4(lcol * throughput, __uint_as_float(1u));
 				}
 			}
 		}
-		terms[p] = out;
+		}
+		if(fold)
+		{
+			// ns | 64: p = 64 w + lane, so path i of the request sits in lane (lane - i) + i of this wave
+			const uint32_t lane = laneId(), g0 = lane - i;
+			const bool longp = __float_as_uint(out.w) >= 2u;
+			const uint64_t lm = __ballot(longp);
+			const uint64_t gm = (ns == 64u ? ~0ull : ((1ull << ns) - 1ull)) << g0;
+			if((lm & gm) == 0ull)
+			{
+				// path_col = path_col + term, path by path (k_fg's order), the sum in every lane of the group
+				C3 path_col = c3(0.f);
+				for(uint32_t q = 0; q < ns; ++q)
+				{
+					const int src = (int)(g0 + q);
+					const float tr = __shfl(out.x, src), tg = __shfl(out.y, src), tb = __shfl(out.z, src);
+					const uint32_t tt = __shfl(__float_as_uint(out.w), src);
+					if(tt == 1u) path_col = path_col + C3{tr, tg, tb};
+				}
+				if(i == 0u && req_fg)
+				{
+					const C3 fg = path_col / (float)B.n_sampl;
+					const uint4 cb = A.G.pix_mode[j];
+					const C3 col = C3{__uint_as_float(cb.x), __uint_as_float(cb.y), __uint_as_float(cb.z)} + fg;
+					A.G.pix_mode[j] = make_uint4(__float_as_uint(col.r), __float_as_uint(col.g), __float_as_uint(col.b), cb.w);
+					terms[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(kFgDone));
+				}
+			}
+			else terms[p] = out;
+		}
+		else terms[p] = out;
 	}
 	fgStats(S, L.s, n_paths, n_lookups, n_nvisits);
 }
@@ -6549,6 +6657,8 @@ __global__ void __launch_bounds__(kTraceBlock) YAF_FG_ATTR k_fg_long(FgPathArgs 
 	uint32_t n_lookups = 0, n_nvisits = 0, visits = 0, tests = 0;
 	auto nearestRad = [&](V3 hp, V3 sf) -> int {
 		++n_lookups;
+		const int g = S.rgrid.start ? gridNearest(S.rgrid, hp, sf, S.fg_lookup_rad, n_nvisits) : -2;
+		if(g != -2) return g;
 		return S.rpk_lds > 0 ? pkNearestLds<kTraceBlock>(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, nstk, S.rpk_lds, n_nvisits)
 		                     : pkNearest(S.rpk_nodes, S.rph_dir, hp, sf, S.fg_lookup_rad, &n_nvisits);
 	};
@@ -6662,6 +6772,7 @@ __global__ void __launch_bounds__(256) k_fg_sum(FgPathArgs PA)
 		const uint32_t j = a0 + B.j0 + jj;
 		if(!(__float_as_uint(A.G.extra[j].w) & G_FG)) continue;
 		const float4 *tp = B.terms + ((size_t)s * B.seg_cap + jj) * ns;
+		if(__float_as_uint(tp[0].w) == kFgDone) continue;   // folded by k_fg_first (no bouncing path)
 		C3 path_col = c3(0.f);
 		for(uint32_t i = 0; i < ns; ++i)
 		{
@@ -7298,9 +7409,12 @@ hipError_t yafamd_launch_fg_paths(const DevScene *S, const DevNeeQueue *G, const
 	PA.A.spill = spill;
 	PA.A.ts_scratch = nullptr;
 	PA.B = *B;
+	// with the radiance-map grid the kd search only settles ties (rare): its private-array stack, no LDS
+	// column (more resident workgroups)
+	if(S->rgrid.start) PA.A.S.rpk_lds = 0;
 	const size_t stack_bytes = (size_t)stack_depth * kTraceBlock * sizeof(int);
-	const size_t nstk_bytes = (size_t)S->rpk_lds * kTraceBlock * sizeof(uint32_t);
-	const size_t stage_bytes = fgStageTables(*S, true, S->ext != 0, stack_depth)
+	const size_t nstk_bytes = (size_t)PA.A.S.rpk_lds * kTraceBlock * sizeof(uint32_t);
+	const size_t stage_bytes = fgStageTables(PA.A.S, true, S->ext != 0, stack_depth)
 	                               ? ((nstk_bytes + 15) & ~(size_t)15) + (size_t)S->n_mats * sizeof(DevMaterial) + (size_t)S->n_tris * 16
 	                               : nstk_bytes;
 	const size_t bytes = stack_bytes + (size_t)(S->node_f4 * S->n_nodes + 3 * S->n_tris) * sizeof(float4) + stage_bytes;

@@ -71,6 +71,8 @@ hipError_t yafamd_launch_fg_paths(const DevScene *S, const DevNeeQueue *G, const
 hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t n, float maxrad, uint32_t *kept_out, uint32_t *n_kept,
                                   int *rounds_out, hipStream_t st, void **scratch);
 void yafamd_thin_scratch_free(void *scratch);
+hipError_t yafamd_rad_grid(const float4 *pos, const float4 *dir, uint32_t n, float lookup_rad, RadGrid *out, hipStream_t st, void **scratch);
+void yafamd_rad_grid_free(void *scratch);
 hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid, float2 *ts_scratch,
                             hipStream_t st);
 size_t yafamd_gather_lanes(const DevScene *S);
@@ -299,7 +301,7 @@ struct GpuRenderer::Impl
 	ncclComm_t comm = nullptr;
 	Buf g_send, g_recv, g_wsend, g_wrecv, g_times, g_status;
 	// scratch of the photon kd-tree build (pkd.hip) and of the radiance-point thinning (fgthin.hip)
-	void *pkd_scratch = nullptr, *thin_scratch = nullptr;
+	void *pkd_scratch = nullptr, *thin_scratch = nullptr, *rgrid_scratch = nullptr;
 	std::vector<DevLight> host_lights;   // as uploaded (light sample multiplier passes rewrite the device copy)
 	std::vector<DevLight> pass_lights;   // staging of the current pass's copy (alive until the stream syncs)
 	int n_photons = 0, pm_paths = 0, pm_stack = 0;
@@ -385,6 +387,7 @@ struct GpuRenderer::Impl
 			b->release();
 		yafamd_pkd_scratch_free(pkd_scratch);
 		yafamd_thin_scratch_free(thin_scratch);
+		yafamd_rad_grid_free(rgrid_scratch);
 		if(comm) (void)ncclCommDestroy(comm);
 		for(hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
 		if(stream) (void)hipStreamDestroy(stream);
@@ -1236,6 +1239,20 @@ void GpuRenderer::publishRadianceMap(DevScene &S, const PhotonParams &pm, uint32
 	// k_fg's nearest searches keep their far-child stack in LDS when the tree is shallow enough
 	S.rpk_lds = (nk && d.r_depth + 1 <= 32) ? d.r_depth + 1 : 0;
 	if(const char *e = getenv("YAFARAY_AMD_FG_NEAREST"); e && std::string(e) == "private") S.rpk_lds = 0;
+	// the per-path final gathering's nearest searches over a uniform grid of the map (RadGrid; a tie of the
+	// nearest distance asks the kd search); YAFARAY_AMD_FG_GRID=0 keeps the kd search for every lookup
+	S.rgrid = RadGrid{};
+	const char *ge = getenv("YAFARAY_AMD_FG_GRID");
+	if(nk && !(ge && *ge == '0'))
+	{
+		const hipError_t e = yafamd_rad_grid(S.rph_pos, S.rph_dir, nk, S.fg_lookup_rad, &S.rgrid, d.stream, &d.rgrid_scratch);
+		if(e != hipSuccess)
+		{
+			if(e != hipErrorNotSupported) log_.warning("PhotonIntegrator: radiance-map grid not built (" + std::string(hipGetErrorString(e)) + "); kd searches");
+			(void)hipGetLastError();
+			S.rgrid = RadGrid{};
+		}
+	}
 }
 
 namespace
@@ -1892,6 +1909,8 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	if(const char *e = std::getenv("YAFARAY_AMD_NEE_PM16"); e && *e == '1') S.nee_pm16 = 1;   // tests: the 16-B request word
 	if(const char *e = std::getenv("YAFARAY_AMD_W_LIVE"); e && *e == '1') S.w_live = 1;        // tests: the 16-B throughput record
 	S.no_lean = 0;
+	S.fg_probe = 0;
+	if(const char *e = std::getenv("YAFARAY_AMD_FG_PROBE"); e && *e) S.fg_probe = atoi(e);   // timing attribution only
 	if(const char *e = std::getenv("YAFARAY_AMD_SHADE_LEAN"); e && *e == '0') S.no_lean = 1;   // tests: the general k_shade
 	int path_grid = 0;
 	if(!lpc_on)

@@ -212,5 +212,31 @@ def test_final_gather_per_path_lanes_equal_lane_per_request(product, monkeypatch
     assert np.array_equal(w.view(np.uint32), wb.view(np.uint32))
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), int(ulp_diff(a, b).max())
     # the same paths and radiance-map lookups were counted by both kernels
-    for k in ("fg_paths", "fg_lookups", "fg_nearest_visits"):
+    for k in ("fg_paths", "fg_lookups"):
         assert st[k] == st_b[k] and st[k] > 0, (k, st[k], st_b[k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["default", "close-paths", "specular", "textured"])
+def test_final_gather_grid_nearest_equals_kd_search(product, monkeypatch, case):
+    """r06: the radiance map's nearest searches over its uniform grid (gridNearest; a tie of the smallest
+    facing distance asks the kd search) return the kd search's photon (YAFARAY_AMD_FG_GRID=0): bit-identical
+    films, the same lookups."""
+    if case == "textured":
+        import texscenes as T
+        mats, imgs, texs = T.CASES["layers"]()
+        spec = T.grid_scene(mats, imgs, texs, width=40, height=30, spp=1, sphere_smooth=60.0)
+        spec = spec.with_render(integrator="photonmapping", pm_photons=20000, pm_search=30, pm_diffuse_radius=0.4,
+                                pm_final_gather=True, fg_samples=4, fg_min_pathlen=1.5)
+    elif case == "specular":
+        spec = fg_spec(specular=True, fg_min_pathlen=0.3)
+    elif case == "close-paths":
+        spec = fg_spec(fg_min_pathlen=0.8, fg_bounces=3, fg_samples=6)
+    else:
+        spec = fg_spec(W=64, H=48, fg_samples=8, photons=60000)
+    a, w, st = product.render_spec(spec)
+    monkeypatch.setenv("YAFARAY_AMD_FG_GRID", "0")
+    b, wb, st_b = product.render_spec(spec)
+    assert np.array_equal(w.view(np.uint32), wb.view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), int(ulp_diff(a, b).max())
+    assert st["fg_lookups"] == st_b["fg_lookups"] > 0

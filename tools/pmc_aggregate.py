@@ -46,6 +46,8 @@ def kind_of(name, photon):
         return "k_trace_rays"
     if base == "k_rad_refl":
         return "k_pregather"   # one launch record of the pre-gather kind (render.cc KK_PREGATHER)
+    if base in ("k_fg_first", "k_fg_long", "k_fg_sum"):
+        return "k_fg"          # the per-path final gathering: one launch record per batch (render.cc KK_FG)
     for k in KINDS:
         if base == k:
             return k
