@@ -651,3 +651,68 @@ extern "C" hipError_t yafamd_build_bvh_gpu(const float *verts_dev, const int *tr
 	*tris_out = trisb.release();
 	return hipSuccess;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Ray binning for the BVH8 refill loop (r06, YAFARAY_AMD_RAY_BIN=1): the closest rays of
+// every queue segment ordered by (direction octant, Morton code of the origin in the scene bounds), so that the
+// waves traversing at the same time read the same part of the tree.  One 32-bit key per queue slot: the
+// segment in the high 10 bits (the sort then keeps each segment's slots inside the segment), octant (3 bits),
+// a 19-bit Morton code (6 / 6 / 7 bits of x / y / z); empty slots after the segment's rays and "no ray" entries
+// sort to the segment's end.  k_trace's refill loop traces entry a0 + j's ray at perm[a0 + j] and writes the hit
+// there: every ray's query is unchanged, so hits are identical.
+// ---------------------------------------------------------------------------------------------
+#include "devscene.h"
+
+namespace
+{
+__device__ __forceinline__ uint32_t spreadBits(uint32_t v)   // bit i -> bit 3 i (v < 2^7)
+{
+	uint32_t r = 0;
+#pragma unroll
+	for(int i = 0; i < 7; ++i) r |= ((v >> i) & 1u) << (3 * i);
+	return r;
+}
+
+__global__ void __launch_bounds__(256) k_ray_keys(yafamd::DevQueues Q, const uint32_t *n_active, uint32_t n_seg, uint32_t cap_a, float3 lo,
+                                                  float3 inv_ext, uint32_t *keys, uint32_t *iota)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if(i >= n_seg * cap_a) return;
+	const uint32_t s = i / cap_a, j = i - s * cap_a;
+	uint32_t k = 0x3fffffu;   // empty slot: the segment's end
+	if(j < n_active[s])
+	{
+		const float dx = Q.ray_d[3 * (size_t)i], dy = Q.ray_d[3 * (size_t)i + 1], dz = Q.ray_d[3 * (size_t)i + 2];
+		if(dx != dx) k = 0x3ffffeu;   // no ray this iteration
+		else
+		{
+			const float ox = Q.ray_o[3 * (size_t)i], oy = Q.ray_o[3 * (size_t)i + 1], oz = Q.ray_o[3 * (size_t)i + 2];
+			const uint32_t oct = (dx < 0.f ? 1u : 0u) | (dy < 0.f ? 2u : 0u) | (dz < 0.f ? 4u : 0u);
+			auto q = [](float v, float l, float inv, uint32_t m) {
+				const float t = (v - l) * inv;
+				const int c = (int)(t * (float)(m + 1u));
+				return (uint32_t)(c < 0 ? 0 : (c > (int)m ? (int)m : c));
+			};
+			const uint32_t mx = q(ox, lo.x, inv_ext.x, 63u), my = q(oy, lo.y, inv_ext.y, 63u), mz = q(oz, lo.z, inv_ext.z, 127u);
+			const uint32_t morton = (spreadBits(mx) | (spreadBits(my) << 1) | (spreadBits(mz) << 2)) & 0x7ffffu;
+			k = (oct << 19) | morton;
+		}
+	}
+	keys[i] = (s << 22) | k;
+	iota[i] = i;
+}
+} // namespace
+
+// scratch: keys_in / keys_out / iota / perm (n_seg * cap_a words each) + the sort's temporary storage
+extern "C" hipError_t yafamd_ray_bin(const yafamd::DevQueues *Q, const yafamd::DevCounters *cnt, uint32_t n_seg, uint32_t cap_a, const float *lo,
+                                     const float *hi, uint32_t *keys_in, uint32_t *keys_out, uint32_t *iota, uint32_t *perm, void *tmp,
+                                     size_t *tmp_bytes, hipStream_t st)
+{
+	const size_t n = (size_t)n_seg * cap_a;
+	if(n_seg > 1024u || n > 0x7fffffffu) return hipErrorInvalidValue;
+	if(!tmp) return hipcub::DeviceRadixSort::SortPairs(nullptr, *tmp_bytes, keys_in, keys_out, iota, perm, (int)n, 0, 32, st);
+	const float3 l = make_float3(lo[0], lo[1], lo[2]);
+	const float3 ie = make_float3(1.f / fmaxf(hi[0] - lo[0], 1e-20f), 1.f / fmaxf(hi[1] - lo[1], 1e-20f), 1.f / fmaxf(hi[2] - lo[2], 1e-20f));
+	hipLaunchKernelGGL(k_ray_keys, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, *Q, cnt->n_active, n_seg, cap_a, l, ie, keys_in, iota);
+	return hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, keys_in, keys_out, iota, perm, (int)n, 0, 32, st);
+}

@@ -398,6 +398,8 @@ struct DevQueues
 	float2 *ts_hit;        // [s_depth * shadow rays] transparent shadows: (t, prim bits) of each transparent surface crossed
 	int *ts_n;             // [shadow rays] number of entries in ts_hit (0 when occluded or clear)
 	float4 *sattr;         // [2 * entries] k_surface output for the hit: (N, diffuse_refl), (diffuse colour, -)
+	const uint32_t *perm;  // ray binning (r06, BVH8 refill loop): closest entry a0 + j traces the ray of entry perm[a0 + j]
+	                       // (its segment's rays ordered by direction octant + origin Morton code); null: identity
 };
 
 // Next-event-estimation requests written by k_shade, consumed by k_nee in the same iteration, and

@@ -1183,6 +1183,8 @@ __device__ void traceRefill8(const TraceCtx &C, const DevQueues &Q, const DevPat
 				if(cur < n_a)
 				{
 					float tw;
+					// (ray binning: the entry's ray and hit live at the permuted queue address)
+					if(Q.perm) cur = Q.perm[a0 + cur] - a0;
 					if(!loadQRay(Q, a0 + cur, o, d, tmin, tw)) continue;
 					tmax = (tw >= 0.f) ? tw : inf;
 					any = false;

@@ -73,6 +73,8 @@ hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t
 void yafamd_thin_scratch_free(void *scratch);
 hipError_t yafamd_rad_grid(const float4 *pos, const float4 *dir, uint32_t n, float lookup_rad, RadGrid *out, hipStream_t st, void **scratch);
 void yafamd_rad_grid_free(void *scratch);
+hipError_t yafamd_ray_bin(const DevQueues *Q, const DevCounters *cnt, uint32_t n_seg, uint32_t cap_a, const float *lo, const float *hi,
+                          uint32_t *keys_in, uint32_t *keys_out, uint32_t *iota, uint32_t *perm, void *tmp, size_t *tmp_bytes, hipStream_t st);
 hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid, float2 *ts_scratch,
                             hipStream_t st);
 size_t yafamd_gather_lanes(const DevScene *S);
@@ -260,6 +262,8 @@ struct GpuRenderer::Impl
 	int trace_grid_bvh4 = 0;   // the grid of the BVH4 k_trace when a BVH8 exists (transparent shadows)
 	Buf pre_stats;             // k_pregather's counters (one DevStats)
 	Buf fg_terms, fg_longs, fg_long_terms, fg_long_count;   // the per-path final gathering's batch buffers (FgBatch)
+	Buf bin_keys, bin_keys2, bin_iota, bin_perm, bin_tmp;   // ray binning (YAFARAY_AMD_RAY_BIN)
+	float scene_lo[3] = {0.f, 0.f, 0.f}, scene_hi[3] = {0.f, 0.f, 0.f};
 	bool pre_stats_valid = false;
 	// surface attributes, textures and shader-node programs (texeval.h)
 	Buf prim_attr, shader_nodes, textures, texels;
@@ -379,7 +383,7 @@ struct GpuRenderer::Impl
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
 		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &walk_spill, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris, &pre_stats, &fg_terms, &fg_longs,
-		              &fg_long_terms, &fg_long_count}) b->release();
+		              &fg_long_terms, &fg_long_count, &bin_keys, &bin_keys2, &bin_iota, &bin_perm, &bin_tmp}) b->release();
 		for(int m = 0; m < 3; ++m)
 			for(Buf *b : {&kd_pos[m], &kd_dir[m], &kd_colb[m]}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
@@ -526,6 +530,14 @@ bool GpuRenderer::upload(HostScene &hs)
 	if(hs.gpu_build)
 	{
 		// device build: PLOC + BVH4 collapse (bvhgpu.hip); only the mesh crosses PCIe
+		// (the scene bounds: ray binning quantises ray origins in them)
+		for(int a = 0; a < 3; ++a) { d.scene_lo[a] = 3.4e38f; d.scene_hi[a] = -3.4e38f; }
+		for(size_t k = 0; k + 2 < hs.verts.size(); k += 3)
+			for(int a = 0; a < 3; ++a)
+			{
+				d.scene_lo[a] = std::min(d.scene_lo[a], hs.verts[k + (size_t)a]);
+				d.scene_hi[a] = std::max(d.scene_hi[a], hs.verts[k + (size_t)a]);
+			}
 		Buf v, t;
 		if(!allocCopy(log_, v, hs.verts.data(), hs.verts.size())) return false;
 		if(!allocCopy(log_, t, hs.tris.data(), hs.tris.size())) return false;
@@ -1850,6 +1862,18 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	// room for every path to bounce (no overflow); a batch is seg_cap request positions of every segment,
 	// within 6 GB
 	const bool fg_paths = yafamd_fg_paths_eligible(&S) != 0;
+	// ray binning for the BVH8 refill loop (opt-in experiment, YAFARAY_AMD_RAY_BIN=1): sort keys and the permutation
+	bool ray_bin = false;
+	if(const char *e = std::getenv("YAFARAY_AMD_RAY_BIN"); e && *e == '1' && S.nodes8 && !S.scene_in_lds && !S.tr_shad && R <= 1024)
+	{
+		const size_t n = (size_t)R * S.cap_a;
+		size_t tb = 0;
+		HIPCHECK(yafamd_ray_bin(nullptr, nullptr, (uint32_t)R, S.cap_a, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &tb, d.stream));
+		if(!ensure(log_, d.bin_keys, n * 4) || !ensure(log_, d.bin_keys2, n * 4) || !ensure(log_, d.bin_iota, n * 4) || !ensure(log_, d.bin_perm, n * 4) ||
+		   !ensure(log_, d.bin_tmp, tb))
+			return false;
+		ray_bin = true;
+	}
 	FgBatch fgb{};
 	auto fgPrepare = [&]() -> bool {
 		const int ns = S.fg_pass_samples > 0 ? S.fg_pass_samples : std::max(1, S.fg_samples);
@@ -1954,6 +1978,15 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// (camera rays with the default clip planes all have (0, unbounded): k_camera writes no ray_tt)
 			if(it != 0 || (S.cur_level == 0 && !S.cam.ray_tt)) qc.ray_tt = nullptr;
 			qc.tmin_dflt = it == 0 ? 0.f : S.ray_min_dist;
+			qc.perm = nullptr;
+			if(ray_bin && it >= 1 && !count_run)
+			{
+				// the bounce rays ordered by direction octant + origin (camera rays are coherent already)
+				size_t tb = d.bin_tmp.bytes;
+				HIPCHECK(yafamd_ray_bin(&qc, &cnt[cur], S.n_seg, S.cap_a, d.scene_lo, d.scene_hi, (uint32_t *)d.bin_keys.p, (uint32_t *)d.bin_keys2.p,
+				                        (uint32_t *)d.bin_iota.p, (uint32_t *)d.bin_perm.p, d.bin_tmp.p, &tb, d.stream));
+				qc.perm = (const uint32_t *)d.bin_perm.p;
+			}
 			PROF(KK_TRACE, yafamd_launch_trace(&S, &qc, &cnt[cur], &d.P[cur], run_stats, d.lds_stack, (int *)d.spill.p,
 			                                    S.tr_shad ? d.trace_grid_bvh4 : d.trace_grid, d.stream));
 			// material-shade dispatch for textured / smooth scenes: surface attributes + shader nodes

@@ -147,6 +147,22 @@ def test_bvh8_refill_equals_bvh4(product, n_tris, monkeypatch):
     assert sa["closest_rays"] == sb["closest_rays"] and sa["shadow_rays"] == sb["shadow_rays"]
 
 
+@pytest.mark.gpu
+def test_ray_binning_equals_unbinned(product, monkeypatch):
+    """r06: ray binning (YAFARAY_AMD_RAY_BIN=1: each queue segment's bounce rays traced in (octant, origin Morton)
+    order through a permutation, hits written back to the rays' own queue addresses) gives the unbinned film
+    bit for bit on the BVH8 refill path (device build, scene in global memory, several chunks)."""
+    use_bvh(monkeypatch, "bvh8-global")
+    spec = scenes.cornell_sphere(n=40, width=48, height=36, spp=4, bounces=6, rr=True)
+    a, wa, sa = product.render_spec(spec, chunk_slots=1500)
+    monkeypatch.setenv("YAFARAY_AMD_RAY_BIN", "1")
+    b, wb, sb = product.render_spec(spec, chunk_slots=1500)
+    assert sa["scene_in_lds"] == 0 and sa["bvh_width"] == 8
+    assert np.array_equal(wa, wb)
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+    assert sa["closest_rays"] == sb["closest_rays"] and sa["shadow_rays"] == sb["shadow_rays"]
+
+
 @pytest.mark.parametrize("offset", [(1000.0, -500.0, 250.0), (0.0, 0.0, 0.0)])
 def test_bvh8_far_from_origin_and_thin_geometry(product, monkeypatch, offset):
     """r05: the quantised BVH8's byte planes are rounded outwards over the node origin; geometry far from
