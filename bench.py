@@ -337,6 +337,8 @@ def main():
     flush_ms = None
     if world <= 1 and a.flush_steps > 0:
         yi.L.yafaray_amd_setProfileKernels(yi.h, 0)
+        # one untimed flushed frame first: the host film (page-locked, reused across frames) is allocated there
+        yi.render(flush=lambda: None)
         sync()
         t0 = time.perf_counter()
         for _ in range(a.flush_steps):
