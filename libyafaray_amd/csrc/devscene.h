@@ -324,7 +324,21 @@ struct DevScene
 	// render visits before it (render.cc lpcBases: an exclusive scan in tile order) and each call takes
 	// the next value; 0: pickLight
 	uint32_t *lpc;
-	int lpc_mode;
+	int lpc_mode;          // 3: deferred pick (r06) — every addition to a path colour becomes a record (below), resolved after the pass
+	// deferred light pick (lpc_mode 3, kernels.hip k_dfr_*): one 80-B record per active entry slot of every
+	// iteration (dfr_seg_off: this iteration's first slot of every segment; a record = hit point + primitive,
+	// wo + the sample's previous record, throughput or term + kind, emission + the call's ordinal, the pixel's
+	// sampling offset + sample index + counter index + light), dfr_last: per camera sample of the pass its last
+	// record (+1, bit 31: diffuse first hit; all ones: not finalized)
+	uint32_t *dfr_kind;    // per slot: 0 none, 1 light estimate, 2 known term | has emission << 2 | the call's ordinal << 3
+	float4 *dfr_pp;        // hit point, primitive (kind 1)
+	float4 *dfr_wo;        // wo, the picked light (k_dfr_nee)
+	float4 *dfr_a;         // the vertex throughput (kind 1) or the term (kind 2), the camera sample's counter index
+	float4 *dfr_emit;      // emission added to the estimate (kind 1 with has emission)
+	uint2 *dfr_pix;        // the pixel's sampling offset, sample index (kind 1)
+	uint32_t *dfr_last;
+	const uint32_t *dfr_seg_off;
+	uint32_t dfr_cap;
 	int nee_pm16;          // 1: NEE requests keep the 16-B pixel / mode word (YAFARAY_AMD_NEE_PM16=1; else 8 B where it fits)
 	int w_live;            // 1: the integrator's sample weight w must persist across vertices (DevPaths::thr.w); 0: thr is a 12-B record
 	int no_lean;           // 1: the general k_shade / k_nee instantiations even where a lean one applies (YAFARAY_AMD_SHADE_LEAN=0: tests, A/B)

@@ -2876,7 +2876,11 @@ __device__ void spawnSpecular(const DevScene &S, const DevMaterial &m, const Sur
 // LEAN: the plain path tracer (PathIntegrator, one path per sample, no AO / photon maps / caustic map /
 // gather queue) with those scene switches fixed at compile time, so the other integrators' state
 // (first-hit records, gather requests, AO sums) costs no registers (launch_shade picks it)
-template<bool SMALL, bool EXT, bool FUSED = false, bool LEAN = false>
+// DEFER (lpc_mode 3, r06): estimateOneDirectLight's light pick in the one-thread order without a count run —
+// every addition to the path colour (the pending light estimate with its throughput and emission, or a term known
+// at once) is written as a record chained per sample instead of being added; k_dfr_* pick the lights once the
+// pass's counter bases are known, estimate them, and fold the records in order (the same additions)
+template<bool SMALL, bool EXT, bool FUSED = false, bool LEAN = false, bool DEFER = false>
 __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_WAVES : YAF_SHADE_MIN_WAVES)) k_shade(ShadeArgs A)
 {
 	extern __shared__ uint4 shade_smem[];
@@ -3080,6 +3084,11 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_
 			}
 		}
 		bool nee_v0 = false, nee_one = false, sample_next = false, end_sub = false, finalize = false, start_sub = false;
+		// DEFER: this vertex's record — 1: a light estimate to pick and estimate later (dfr_a = its throughput),
+		// 2: a term known now (dfr_a)
+		int dfr_kind = 0;
+		C3 dfr_a = c3(0.f), dfr_emit = c3(0.f);
+		uint32_t dfr_n = 0, dfr_has_emit = 0;
 		C3 emit_pend = c3(0.f);
 		C3 pend_thr = c3(0.f);
 		if(live)
@@ -3189,7 +3198,8 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_
 							// lcol = 0 (+ emission): nothing to trace, connect now
 							C3 lcol = c3(0.f);
 							if(flags & F_PEND_EMIT) lcol = lcol + emit_pend;
-							pcol = pcol + lcol * thr;
+							if(DEFER) { dfr_kind = 2; dfr_a = lcol * thr; }
+							else pcol = pcol + lcol * thr;
 							flags &= ~F_PEND_EMIT;
 						}
 						++depth;
@@ -3208,6 +3218,17 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_
 			const uint32_t n = *c;
 			*c = n + 1u;
 			if(S.lpc_mode == 1) nee_one = false;   // count run: the call is counted, nothing is estimated
+			else if(DEFER && S.lpc_mode == 3)
+			{
+				// the call's ordinal in its sample; the estimate, its emission and throughput go to the record
+				dfr_kind = 1;
+				dfr_n = n;
+				dfr_a = pend_thr;
+				dfr_has_emit = (flags & F_PEND_EMIT) ? 1u : 0u;
+				if(dfr_has_emit) dfr_emit = emit_pend;
+				flags &= ~F_PEND_EMIT;
+				nee_one = false;
+			}
 			else lnum = lightOfCounter(S, n);
 		}
 		else if(nee_one)
@@ -3217,6 +3238,31 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_
 			lnum = pickLight(S, offset, sample_idx, (uint32_t)depth + subpath * (uint32_t)S.bounces, n_paths * (uint32_t)(S.bounces + 1));
 		}
 		if(S.lpc_mode == 1) nee_v0 = false;   // count run: no estimateAllDirectLight either
+		if(DEFER && live && dfr_kind == 0)
+		{
+			// no addition at this vertex: the slot stays empty (its kind word)
+			const uint32_t slot = A.S.dfr_seg_off[seg] + (i - a0);
+			if(slot < S.dfr_cap) S.dfr_kind[slot] = 0u;
+		}
+		if(DEFER && dfr_kind != 0)
+		{
+			// the record at this entry's slot of the iteration, chained to the sample's previous one (whose
+			// index + 1 rides in the path colour's red bits: the colour itself is only summed at the end)
+			const uint32_t slot = A.S.dfr_seg_off[seg] + (i - a0);
+			if(slot < S.dfr_cap)
+			{
+				const uint32_t q = (uint32_t)(((size_t)sc.y * (size_t)S.width + (size_t)sc.x) * (size_t)S.spp + (size_t)sc.s);
+				S.dfr_kind[slot] = (uint32_t)dfr_kind | (dfr_has_emit << 2) | (dfr_n << 3);
+				S.dfr_a[slot] = f4(dfr_a, __uint_as_float(q));
+				if(dfr_kind == 1)
+				{
+					S.dfr_pp[slot] = f4(sp.p, __int_as_float(hit_prim));
+					S.dfr_wo[slot] = f4(wo, 0.f);
+					S.dfr_pix[slot] = make_uint2(offset, sample_idx);
+					if(dfr_has_emit) S.dfr_emit[slot] = f4(dfr_emit, 0.f);
+				}
+			}
+		}
 		if(nee_one) flags = (flags & ((1u << F_LNUM_SHIFT) - 1u)) | (lnum << F_LNUM_SHIFT) | F_PEND_ONE;
 		if(nee_v0) flags |= F_PEND_V0;
 		const bool pending = (flags & (F_PEND_V0 | F_PEND_ONE)) != 0;
@@ -3304,7 +3350,14 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_SHADE_LEAN_
 			if(ao_after_caustic && S.do_ao) { g_extra = ao_extra; g_mode |= G_EXTRA; }
 			if(is_path) { g_extra = pcol / (float)n_paths; g_mode |= G_EXTRA; }   // path_tracer.cc:274-278
 		}
-		if(live && finalize && !want_gather)
+		if(DEFER && live && finalize && !want_gather)
+		{
+			// the first-vertex estimate alone; k_dfr_fold adds the paths' colour (col + pcol / n, + 0)
+			loadCol();
+			writeSampleAt(A, sc, col, alpha);
+			S.dfr_last[((size_t)sc.y * (size_t)S.width + (size_t)sc.x) * (size_t)S.spp + (size_t)sc.s] = (is_path && (flags & F_V0_DIFFUSE)) ? 1u : 0u;
+		}
+		else if(live && finalize && !want_gather)
 		{
 			loadCol();
 			// path_tracer.cc:274-278 / direct_light.cc:129-131
@@ -3979,6 +4032,263 @@ __global__ void __launch_bounds__(kShadeBlock, EXT ? 1 : (LEAN ? YAF_NEE_LEAN_WA
 			atomicAdd(&S.stats[seg].tri_tests, (unsigned long long)tests);
 		}
 	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deferred light pick (lpc_mode 3, r06; integrator_montecarlo.cc:70-78 with the one-thread counter
+// integrator_tiled.cc:48): the path pass (k_shade<.., DEFER>) counts every sample's estimateOneDirectLight
+// calls and writes one record per addition to a path colour; once the counter bases are known (lpcBases),
+//   k_dfr_segoff   (before every k_shade of the path pass) this iteration's first record slot per segment;
+//   k_dfr_nee      a batch of records: the light of call n of a sample is lightOfCounter(base + n), sampled as
+//                  k_nee samples it (contributions at slot * K, shadow rays to the segment's queue);
+//   k_trace        the batch's shadow rays;
+//   k_dfr_accum    per iteration range of the batch: lcol = estimate * n_lights (+ emission), term = lcol *
+//                  throughput (k_shade's connection), pcol = pcol + term per sample — iteration by iteration, so
+//                  every sample's additions in the one-pass render's order;
+//   k_dfr_fold     per sample: the first-vertex estimate + pcol / n (k_shade's finalize): the film is bit for bit
+//                  the count-run render's.
+// ---------------------------------------------------------------------------------------------
+struct DfrArgs
+{
+	DevScene S;
+	uint32_t *idx;         // per batch segment: its light-estimate records grouped by light (k_dfr_part), cap_a slots each
+	uint32_t *n_rec;       // per batch segment: their count
+	DevPaths P;            // contributions / occlusion bytes of the batch (slot - r0) * K
+	DevQueues Q;           // the batch's shadow rays (segment s: slots r0 + s * cap_a ..)
+	DevCounters cnt;       // n_active = 0, n_shadow per segment
+	uint32_t r0, total;    // batch start, records of the pass
+	uint32_t *dfr_total;   // running slot count of the path pass (k_dfr_segoff)
+	uint32_t *overflow;
+	uint32_t n_ctr;        // camera samples of the pass (k_dfr_fold)
+	float4 *samples;
+};
+
+// this iteration's record slots: one per active entry, segments in order, after the earlier iterations'
+__global__ void __launch_bounds__(1024) k_dfr_segoff(const uint32_t *n_active, uint32_t n_seg, uint32_t *seg_off, uint32_t *dfr_total, uint32_t cap,
+                                                   uint32_t *overflow, uint32_t *it_start)
+{
+	__shared__ uint32_t part[1024];
+	const uint32_t t = threadIdx.x;
+	const uint32_t per = (n_seg + 1023u) / 1024u;
+	uint32_t sum = 0;
+	for(uint32_t k = 0; k < per; ++k)
+	{
+		const uint32_t s = t * per + k;
+		if(s < n_seg) sum += n_active[s];
+	}
+	part[t] = sum;
+	__syncthreads();
+	for(uint32_t off = 1; off < 1024u; off <<= 1)
+	{
+		const uint32_t v = t >= off ? part[t - off] : 0u;
+		__syncthreads();
+		part[t] += v;
+		__syncthreads();
+	}
+	const uint32_t base = *dfr_total;
+	uint32_t run = base + part[t] - sum;
+	for(uint32_t k = 0; k < per; ++k)
+	{
+		const uint32_t s = t * per + k;
+		if(s < n_seg)
+		{
+			seg_off[s] = run;
+			run += n_active[s];
+		}
+	}
+	__syncthreads();
+	if(t == 1023u)
+	{
+		// the iteration's first slot (k_dfr_accum runs the iterations in order); it_start[0] counts them
+		const uint32_t k = it_start[0];
+		if(k < 4095u) it_start[1u + k] = base;
+		it_start[0] = k + 1u;
+		const uint64_t end = (uint64_t)base + part[1023];
+		*dfr_total = end > 0xffffffffull ? 0xffffffffu : (uint32_t)end;
+		if(end > cap) *overflow = 1u;
+	}
+}
+
+// one batch segment's light-estimate records grouped by their light (a counting sort in LDS; the order inside a
+// light is irrelevant — every record is estimated on its own): k_dfr_nee's waves then sample one light with all
+// lanes instead of one pass per light over a mixed wave (lane utilisation 0.37 unsorted)
+constexpr int kDfrMaxLights = 16;
+// Wave-aggregated LDS counters: one atomic per distinct light in the wave (per-lane atomics on two or three
+// addresses serialise); returns this lane's position within its light (valid where `rec`).
+__device__ __forceinline__ uint32_t waveAppendKeyed(bool rec, uint32_t key, uint32_t *ctr)
+{
+	uint64_t pending = __ballot(rec);
+	uint32_t pos = 0;
+	while(pending)
+	{
+		const int leader = __ffsll((unsigned long long)pending) - 1;
+		const uint32_t k = (uint32_t)__shfl((int)key, leader);
+		const bool mine = rec && key == k;
+		const uint64_t m = __ballot(mine);
+		uint32_t base = 0;
+		if(laneId() == leader) base = atomicAdd(&ctr[k], (uint32_t)__popcll(m));
+		base = (uint32_t)__shfl((int)base, leader);
+		if(mine) pos = base + (uint32_t)__popcll(m & ((1ull << laneId()) - 1ull));
+		pending &= ~m;
+	}
+	return pos;
+}
+
+__global__ void __launch_bounds__(1024) k_dfr_part(DfrArgs A)
+{
+	const DevScene &S = A.S;
+	const uint32_t seg = blockIdx.x;
+	const uint32_t first = A.r0 + seg * S.cap_a;
+	const uint32_t n = first < A.total ? min(S.cap_a, A.total - first) : 0u;
+	__shared__ uint32_t cnt[kDfrMaxLights];
+	if(threadIdx.x < kDfrMaxLights) cnt[threadIdx.x] = 0u;
+	__syncthreads();
+	auto lightOf = [&](uint32_t jj, bool &rec) -> uint32_t {
+		rec = false;
+		if(jj >= n) return 0u;
+		const uint32_t slot = first + jj;
+		const uint32_t kind = S.dfr_kind[slot];
+		rec = (kind & 3u) == 1u;
+		return rec ? lightOfCounter(S, S.lpc[__float_as_uint(S.dfr_a[slot].w)] + (kind >> 3)) : 0u;
+	};
+	for(uint32_t base_j = 0; base_j < n; base_j += blockDim.x)
+	{
+		bool rec;
+		const uint32_t l = lightOf(base_j + threadIdx.x, rec);
+		waveAppendKeyed(rec, l, cnt);
+	}
+	__syncthreads();
+	if(threadIdx.x == 0)
+	{
+		uint32_t run = 0;
+		for(int l = 0; l < kDfrMaxLights; ++l)
+		{
+			const uint32_t c = cnt[l];
+			cnt[l] = run;
+			run += c;
+		}
+		A.n_rec[seg] = run;
+	}
+	__syncthreads();
+	for(uint32_t base_j = 0; base_j < n; base_j += blockDim.x)
+	{
+		bool rec;
+		const uint32_t l = lightOf(base_j + threadIdx.x, rec);
+		const uint32_t pos = waveAppendKeyed(rec, l, cnt);
+		if(rec) A.idx[(size_t)seg * S.cap_a + pos] = first + base_j + threadIdx.x;
+	}
+}
+
+// LEAN: no meshlight in the scene (neeLight's NOMESH: no private arrays), k_nee's occupancy
+template<bool SMALL, bool LEAN>
+__global__ void __launch_bounds__(kShadeBlock, LEAN ? YAF_NEE_LEAN_WAVES : YAF_NEE_MIN_WAVES) k_dfr_nee(DfrArgs A)
+{
+	extern __shared__ uint4 shade_smem[];
+	const DevScene S_ = stageTables<SMALL>(A.S, shade_smem);
+	const DevScene &S = S_;
+	const uint32_t seg = blockIdx.x;
+	__shared__ uint32_t s_count;
+	if(threadIdx.x == 0) s_count = 0;
+	__syncthreads();
+	ShadeOut out;
+	out.sh_count = &s_count;
+	out.sh_base = seg * S.cap_s;
+	out.Qn = A.Q;
+	out.idx_in_o = true;
+	// the segment's light-estimate records, grouped by light (k_dfr_part)
+	const uint32_t n = A.n_rec[seg];
+	const int K = S.nee_k;
+	for(uint32_t base_j = 0; base_j < n; base_j += blockDim.x)
+	{
+		const uint32_t jj = base_j + threadIdx.x;
+		bool live = jj < n;
+		const uint32_t slot = live ? A.idx[(size_t)seg * S.cap_a + jj] : A.r0;
+		uint32_t kind = 0;
+		float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+		uint2 pix = make_uint2(0u, 0u);
+		if(live)
+		{
+			kind = S.dfr_kind[slot];
+			live = (kind & 3u) == 1u;
+		}
+		if(live)
+		{
+			r0 = S.dfr_pp[slot];
+			r1 = S.dfr_wo[slot];
+			r2 = S.dfr_a[slot];
+			pix = S.dfr_pix[slot];
+		}
+		Surf sp;
+		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
+		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
+		uint32_t lnum = 0;
+		if(live)
+		{
+			sp = surfFromPrim(S, xyz(r0), __float_as_int(r0.w));
+			lnum = lightOfCounter(S, S.lpc[__float_as_uint(r2.w)] + (kind >> 3));   // (k_dfr_accum picks it again)
+		}
+		const V3 wo = xyz(r1);
+		const int e0 = (int)(slot - A.r0) * K;   // (k_dfr_accum reads them by slot)
+		for(int l = 0; l < S.n_lights; ++l)
+		{
+			const bool mine = live && lnum == (uint32_t)l;
+			if(!__any(mine)) continue;
+			neeLight<false, ShadeOut, NeeHbm, LEAN>(S, S.lights[l], S.mats[sp.mat], sp, wo, (uint32_t)l, pix.y, pix.x, mine,
+			                                  e0, neeHbm(A.P), A.P.occ, out, nullptr);
+		}
+	}
+	__syncthreads();
+	if(threadIdx.x == 0)
+	{
+		A.cnt.n_shadow[seg] = s_count;
+		A.cnt.n_active[seg] = 0u;
+	}
+}
+
+// the terms of slots [r0, total) of one iteration (a sample has at most one record per iteration, and the
+// iterations' ranges are processed in order): a light estimate becomes lcol = estimate * n_lights (+ emission),
+// term = lcol * throughput (k_shade's connection, its contributions at (slot - batch) * K of this batch), a known
+// term is taken as it is, and pcol = pcol + term per sample (the additions of the one-pass render, in order)
+__global__ void __launch_bounds__(256) k_dfr_accum(DfrArgs A, float *pcol, uint32_t batch0)
+{
+	const DevScene &S = A.S;
+	const uint32_t slot = A.r0 + blockIdx.x * blockDim.x + threadIdx.x;
+	if(slot >= A.total) return;
+	const uint32_t kind = S.dfr_kind[slot];
+	if((kind & 3u) == 0u) return;
+	const float4 a = S.dfr_a[slot];
+	C3 term = rgb(a);
+	if((kind & 3u) == 1u)
+	{
+		const uint32_t lnum = lightOfCounter(S, S.lpc[__float_as_uint(a.w)] + (kind >> 3));   // k_dfr_nee's pick
+		const int kb = (int)(slot - batch0) * S.nee_k;
+		auto ge = [&](int k) { return f4(neeGet(neeHbm(A.P), k), 1.f); };
+		auto go = [&](int k) { return A.P.occ[k] != 0; };
+		// path_tracer.cc:201-207 / :244-266 as k_shade connects it
+		C3 lcol = neeSumT(S.lights[lnum], kb, ge, go) * (float)S.n_lights;
+		if(kind & 4u) lcol = lcol + rgb(S.dfr_emit[slot]);
+		term = lcol * term;
+	}
+	const uint32_t q = __float_as_uint(a.w);
+	float *pc = pcol + 3u * (size_t)q;
+	pc[0] = pc[0] + term.r;
+	pc[1] = pc[1] + term.g;
+	pc[2] = pc[2] + term.b;
+}
+
+// per camera sample of the pass: the first-vertex estimate + the paths' colour (k_shade's finalize)
+__global__ void __launch_bounds__(256) k_dfr_fold(DfrArgs A, const float *pcol)
+{
+	const DevScene &S = A.S;
+	const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+	if(q >= A.n_ctr) return;
+	const uint32_t v = S.dfr_last[q];
+	if(v == 0xffffffffu) return;   // not finalized in this pass
+	const float4 c4 = A.samples[q];
+	C3 col = rgb(c4);
+	if(v & 1u) col = col + C3{pcol[3u * (size_t)q], pcol[3u * (size_t)q + 1u], pcol[3u * (size_t)q + 2u]} / (float)max(1, S.path_samples);
+	col = col + c3(0.f);   // recursiveRaytrace: no specular / glossy component (k_shade's finalize)
+	A.samples[q] = f4(col, c4.w);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -7002,6 +7312,18 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	A.n_jobs = n_jobs;
 	A.chunk_base = chunk_base;
 	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
+	if(S->lpc_mode == 3)
+	{
+		// the deferred light pick's path pass (yafamd_dfr_eligible scenes only)
+		if(S->ext || S->tree || S->gather_on) return hipErrorInvalidValue;
+		const bool lean = S->integrator == INT_PATH && S->path_samples <= 1 && !S->do_ao && !S->caus_map && !S->show_map && S->n_photons == 0 &&
+		                  !S->has_attr && !S->no_lean;
+		if(lean) { if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, false, true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		           else hipLaunchKernelGGL((k_shade<false, false, false, true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A); }
+		else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		else hipLaunchKernelGGL((k_shade<false, false, false, false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+		return hipGetLastError();
+	}
 	if(S->ext)
 	{
 		if(S->small_tables) hipLaunchKernelGGL((k_shade<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
@@ -7020,6 +7342,70 @@ hipError_t yafamd_launch_shade(const DevScene *S, const DevPaths *Pc, const DevP
 	}
 	else if(S->small_tables) hipLaunchKernelGGL((k_shade<true, false, kShadeFused>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
 	else hipLaunchKernelGGL((k_shade<false, false, kShadeFused>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	return hipGetLastError();
+}
+
+// the deferred light pick serves this scene: the plain path tracer (compact records, no recursion tree, photon
+// estimates, surface attributes or transparent shadows); YAFARAY_AMD_LIGHT_PICK=count keeps the count run
+int yafamd_dfr_eligible(const DevScene *S)
+{
+	if(S->n_lights > kDfrMaxLights) return 0;
+	if(S->integrator != INT_PATH || S->ext || S->tree || S->gather_on || S->tr_shad || S->has_attr || S->caus_map || S->do_ao) return 0;
+	const char *e = getenv("YAFARAY_AMD_LIGHT_PICK");
+	return (e && std::string(e) == "count") ? 0 : 1;
+}
+
+hipError_t yafamd_dfr_segoff(const DevCounters *cnt, uint32_t n_seg, uint32_t *seg_off, uint32_t *dfr_total, uint32_t cap, uint32_t *overflow,
+                             uint32_t *it_start, hipStream_t st)
+{
+	hipLaunchKernelGGL(k_dfr_segoff, dim3(1), dim3(1024), 0, st, cnt->n_active, n_seg, seg_off, dfr_total, cap, overflow, it_start);
+	return hipGetLastError();
+}
+
+// one batch of records [r0, r0 + n_seg * cap_a): light pick + estimate (shadow rays to Q), the caller traces them, then connect
+hipError_t yafamd_dfr_nee(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt, uint32_t r0, uint32_t total, uint32_t *idx,
+                         uint32_t *n_rec, hipStream_t st)
+{
+	if(S->n_lights > kDfrMaxLights) return hipErrorInvalidValue;
+	DfrArgs A{};
+	A.S = *S;
+	A.P = *P;
+	A.Q = *Q;
+	A.cnt = *cnt;
+	A.r0 = r0;
+	A.total = total;
+	A.idx = idx;
+	A.n_rec = n_rec;
+	hipLaunchKernelGGL(k_dfr_part, dim3(S->n_seg), dim3(1024), 0, st, A);
+	const size_t lds = shadeLdsBytes(*S, S->small_tables != 0);
+	const bool lean = !S->has_mesh_light;
+	if(S->small_tables) { if(lean) hipLaunchKernelGGL((k_dfr_nee<true, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	                      else hipLaunchKernelGGL((k_dfr_nee<true, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A); }
+	else if(lean) hipLaunchKernelGGL((k_dfr_nee<false, true>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	else hipLaunchKernelGGL((k_dfr_nee<false, false>), dim3(S->n_seg), dim3(kShadeBlock), lds, st, A);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_dfr_accum(const DevScene *S, const DevPaths *P, uint32_t r0, uint32_t r1, uint32_t batch0, float *pcol, hipStream_t st)
+{
+	if(r1 <= r0) return hipSuccess;
+	DfrArgs A{};
+	A.S = *S;
+	A.P = *P;
+	A.r0 = r0;
+	A.total = r1;
+	hipLaunchKernelGGL(k_dfr_accum, dim3((r1 - r0 + 255) / 256), dim3(256), 0, st, A, pcol, batch0);
+	return hipGetLastError();
+}
+
+hipError_t yafamd_dfr_fold(const DevScene *S, float4 *samples, uint32_t n_ctr, const float *pcol, hipStream_t st)
+{
+	if(n_ctr == 0) return hipSuccess;
+	DfrArgs A{};
+	A.S = *S;
+	A.samples = samples;
+	A.n_ctr = n_ctr;
+	hipLaunchKernelGGL(k_dfr_fold, dim3((n_ctr + 255) / 256), dim3(256), 0, st, A, pcol);
 	return hipGetLastError();
 }
 

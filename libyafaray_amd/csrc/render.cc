@@ -73,6 +73,13 @@ hipError_t yafamd_thin_rad_points(const float4 *pos, const float4 *nrm, uint32_t
 void yafamd_thin_scratch_free(void *scratch);
 hipError_t yafamd_rad_grid(const float4 *pos, const float4 *dir, uint32_t n, float lookup_rad, RadGrid *out, hipStream_t st, void **scratch);
 void yafamd_rad_grid_free(void *scratch);
+int yafamd_dfr_eligible(const DevScene *S);
+hipError_t yafamd_dfr_segoff(const DevCounters *cnt, uint32_t n_seg, uint32_t *seg_off, uint32_t *dfr_total, uint32_t cap, uint32_t *overflow,
+                             uint32_t *it_start, hipStream_t st);
+hipError_t yafamd_dfr_accum(const DevScene *S, const DevPaths *P, uint32_t r0, uint32_t r1, uint32_t batch0, float *pcol, hipStream_t st);
+hipError_t yafamd_dfr_nee(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt, uint32_t r0, uint32_t total, uint32_t *idx,
+                         uint32_t *n_rec, hipStream_t st);
+hipError_t yafamd_dfr_fold(const DevScene *S, float4 *samples, uint32_t n_ctr, const float *pcol, hipStream_t st);
 hipError_t yafamd_ray_bin(const DevQueues *Q, const DevCounters *cnt, uint32_t n_seg, uint32_t cap_a, const float *lo, const float *hi,
                           uint32_t *keys_in, uint32_t *keys_out, uint32_t *iota, uint32_t *perm, void *tmp, size_t *tmp_bytes, hipStream_t st);
 hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid, float2 *ts_scratch,
@@ -263,6 +270,9 @@ struct GpuRenderer::Impl
 	Buf pre_stats;             // k_pregather's counters (one DevStats)
 	Buf fg_terms, fg_longs, fg_long_terms, fg_long_count;   // the per-path final gathering's batch buffers (FgBatch)
 	Buf bin_keys, bin_keys2, bin_iota, bin_perm, bin_tmp;   // ray binning (YAFARAY_AMD_RAY_BIN)
+	Buf dfr_kind, dfr_pp, dfr_wo, dfr_a, dfr_emit, dfr_pix;   // deferred light pick (lpc_mode 3): the records (DevScene dfr_*)
+	Buf dfr_last, dfr_segoff, dfr_misc, dfr_its, dfr_pcol;     // per-sample flags, slots, iteration starts, per-sample path colours
+	Buf dfr_idx, dfr_nrec;                                     // a batch's records grouped by light (k_dfr_part)
 	float scene_lo[3] = {0.f, 0.f, 0.f}, scene_hi[3] = {0.f, 0.f, 0.f};
 	bool pre_stats_valid = false;
 	// surface attributes, textures and shader-node programs (texeval.h)
@@ -383,7 +393,9 @@ struct GpuRenderer::Impl
 		for(Buf &b : chunk_bufs) b.release();
 		for(Buf *b : {&g_send, &g_recv, &g_wsend, &g_wrecv, &g_times, &g_status}) b->release();
 		for(Buf *b : {&fg_ts, &g_log, &g_log_n, &walk_spill, &path_next, &lpc, &lpc_seg, &lpc_stats, &mesh_tris, &mesh_cdf, &mesh_nodes, &mesh_btris, &pre_stats, &fg_terms, &fg_longs,
-		              &fg_long_terms, &fg_long_count, &bin_keys, &bin_keys2, &bin_iota, &bin_perm, &bin_tmp}) b->release();
+		              &fg_long_terms, &fg_long_count, &bin_keys, &bin_keys2, &bin_iota, &bin_perm, &bin_tmp, &dfr_kind, &dfr_pp,
+		              &dfr_wo, &dfr_a, &dfr_emit, &dfr_pix, &dfr_last, &dfr_segoff, &dfr_misc, &dfr_its, &dfr_pcol,
+		              &dfr_idx, &dfr_nrec}) b->release();
 		for(int m = 0; m < 3; ++m)
 			for(Buf *b : {&kd_pos[m], &kd_dir[m], &kd_colb[m]}) b->release();
 		for(Buf *b : {&rad_a, &rad_b, &rad_c, &rad_flag, &radc_a, &radc_b, &radc_c, &rad_kept, &rph_pos, &rph_dir, &rph_colb, &rpk_nodes, &seg_pos,
@@ -1994,6 +2006,10 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			// transparent shadows: filter colours of the transparent surfaces the shadow rays crossed
 			if(S.tr_shad && !count_run) PROF(KK_TSHADOW, yafamd_launch_tshadow(&S, &qc, &cnt[cur], &d.P[cur], d.stream));
 			if(S.has_attr) PROF(KK_SURFACE, yafamd_launch_surface(&S, &qc, &cnt[cur], d.stream));
+			// the deferred light pick's record slots of this iteration (one per active entry)
+			if(S.lpc_mode == 3)
+				HIPCHECK(yafamd_dfr_segoff(&cnt[cur], S.n_seg, (uint32_t *)d.dfr_segoff.p, (uint32_t *)d.dfr_misc.p, S.dfr_cap,
+				                           (uint32_t *)d.dfr_misc.p + 1, (uint32_t *)d.dfr_its.p, d.stream));
 			PROF(KK_SHADE, yafamd_launch_shade(&S, &d.P[cur], &d.P[cur ^ 1], &qc, &d.Q[cur ^ 1], &d.N, &d.G, &cnt[cur], &cnt[cur ^ 1],
 			                             (float4 *)d.samples.p, (const DevJob *)d.jobs.p, n_jobs, base, d.stream));
 
@@ -2148,6 +2164,87 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				log_.warning("Integrator: the one-thread light-pick counters (" + std::to_string(n_ctr * 4 >> 20) +
 				             " MB) exceed the memory budget; this pass picks lights by sample hash");
 				return runSamples(n_total);
+			}
+		}
+		// the deferred pick (r06): the pass once with every addition to a path colour kept as a record, the
+		// lights picked from the counters' bases afterwards, the records folded in order — no count run.  A
+		// group render (collective bases) and scenes it does not serve keep the count run; so does a pass whose
+		// records overflow their budget (a third of the free memory), rendered again below
+		if(!group_render && yafamd_dfr_eligible(&S))
+		{
+			size_t free_b = 0, total_b = 0;
+			(void)hipMemGetInfo(&free_b, &total_b);
+			const size_t want = n_ctr * (size_t)(S.bounces + 2) * (size_t)std::max(1, S.path_samples);
+			size_t cap = std::min<size_t>(want, (free_b / 3) / 76);
+			cap = std::min<size_t>(cap, 0x7ffffff0u);
+			if(const char *e = std::getenv("YAFARAY_AMD_DFR_CAP"); e && atoi(e) > 0) cap = std::min<size_t>(cap, (size_t)atoi(e));   // tests: the overflow
+			bool ok_mem = cap > 0 && ensure(log_, d.dfr_kind, cap * 4) && ensure(log_, d.dfr_pp, cap * 16) && ensure(log_, d.dfr_wo, cap * 16) &&
+			              ensure(log_, d.dfr_a, cap * 16) && ensure(log_, d.dfr_emit, cap * 16) && ensure(log_, d.dfr_pix, cap * 8) &&
+			              ensure(log_, d.dfr_last, n_ctr * 4) &&
+			              ensure(log_, d.dfr_segoff, (size_t)S.n_seg * 4) && ensure(log_, d.dfr_misc, 16) && ensure(log_, d.dfr_its, 4096 * 4) &&
+			              ensure(log_, d.dfr_pcol, n_ctr * 12) && ensure(log_, d.dfr_idx, (size_t)S.n_seg * S.cap_a * 4) &&
+			              ensure(log_, d.dfr_nrec, (size_t)S.n_seg * 4);
+			if(ok_mem)
+			{
+				HIPCHECK(hipMemsetAsync(d.lpc.p, 0, n_ctr * 4, d.stream));
+				HIPCHECK(hipMemsetAsync(d.dfr_last.p, 0xff, n_ctr * 4, d.stream));
+				HIPCHECK(hipMemsetAsync(d.dfr_misc.p, 0, 16, d.stream));
+				HIPCHECK(hipMemsetAsync(d.dfr_its.p, 0, 4, d.stream));
+				HIPCHECK(hipMemsetAsync(d.dfr_pcol.p, 0, n_ctr * 12, d.stream));
+				S.lpc = (uint32_t *)d.lpc.p;
+				S.dfr_kind = (uint32_t *)d.dfr_kind.p;
+				S.dfr_pp = (float4 *)d.dfr_pp.p;
+				S.dfr_wo = (float4 *)d.dfr_wo.p;
+				S.dfr_a = (float4 *)d.dfr_a.p;
+				S.dfr_emit = (float4 *)d.dfr_emit.p;
+				S.dfr_pix = (uint2 *)d.dfr_pix.p;
+				S.dfr_last = (uint32_t *)d.dfr_last.p;
+				S.dfr_seg_off = (const uint32_t *)d.dfr_segoff.p;
+				S.dfr_cap = (uint32_t)cap;
+				S.lpc_mode = 3;
+				const bool ok = runSamples(n_total);
+				S.lpc_mode = 0;
+				if(!ok) return false;
+				uint32_t misc[2] = {0u, 0u};
+				std::vector<uint32_t> its(4096, 0u);
+				HIPCHECK(hipMemcpyAsync(misc, d.dfr_misc.p, 8, hipMemcpyDeviceToHost, d.stream));
+				HIPCHECK(hipMemcpyAsync(its.data(), d.dfr_its.p, its.size() * 4, hipMemcpyDeviceToHost, d.stream));
+				HIPCHECK(hipStreamSynchronize(d.stream));
+				if(its[0] > 4095u) misc[1] = 1u;   // more iterations than recorded starts: the count run serves
+				if(!misc[1])
+				{
+					bool cut = done < n_total;
+					if(!lpcBases(rp, pass_spp, jy0, jy1, group_render, cut)) return false;
+					if(cut)
+					{
+						done = 0;   // canceled before the pass rendered anything
+						return true;
+					}
+					const uint32_t total_slots = misc[0];
+					const uint32_t batch = S.n_seg * S.cap_a;
+					for(uint32_t r0 = 0; r0 < total_slots; r0 += batch)
+					{
+						PROF(KK_DFR, yafamd_dfr_nee(&S, &d.P[0], &d.Q[0], &cnt[0], r0, total_slots, (uint32_t *)d.dfr_idx.p, (uint32_t *)d.dfr_nrec.p,
+						                            d.stream));
+						DevQueues qs = d.Q[0];
+						qs.ray_tt = nullptr;
+						qs.perm = nullptr;
+						qs.tmin_dflt = S.ray_min_dist;
+						PROF(KK_TRACE, yafamd_launch_trace(&S, &qs, &cnt[0], &d.P[0], run_stats, d.lds_stack, (int *)d.spill.p, d.trace_grid, d.stream));
+						// every sample's terms of this batch, iteration range by iteration range (one record per sample and
+						// iteration; the ranges increase with the slots, so the additions keep the one-pass order)
+						const uint32_t r1 = std::min<uint64_t>((uint64_t)r0 + batch, total_slots);
+						for(uint32_t k = 0; k < its[0]; ++k)
+						{
+							const uint32_t a = std::max(its[1 + k], r0), b = std::min((k + 1 < its[0]) ? its[2 + k] : total_slots, r1);
+							if(b > a) PROF(KK_DFR, yafamd_dfr_accum(&S, &d.P[0], a, b, r0, (float *)d.dfr_pcol.p, d.stream));
+						}
+					}
+					PROF(KK_DFR, yafamd_dfr_fold(&S, (float4 *)d.samples.p, (uint32_t)n_ctr, (const float *)d.dfr_pcol.p, d.stream));
+					return true;
+				}
+				log_.info("Integrator: the deferred light pick's records exceed their budget (" + std::to_string(cap) +
+				          " slots); the pass renders again with a count run");
 			}
 		}
 		HIPCHECK(hipMemsetAsync(d.lpc.p, 0, n_ctr * 4, d.stream));

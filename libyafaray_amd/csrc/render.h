@@ -91,13 +91,13 @@ struct AaParams
 enum KernelKind : int
 {
 	KK_CAMERA = 0, KK_TRACE, KK_SURFACE, KK_TSHADOW, KK_SHADE, KK_NEE, KK_GATHER, KK_SPAWN, KK_COMBINE, KK_FILM, KK_AA,
-	KK_PHOTON_EMIT, KK_PHOTON_BOUNCE, KK_PHOTON_COMPACT, KK_PHOTON_TREE, KK_FG, KK_PREGATHER, KK_GATHER_WALK, KK_PATH, KK_COUNT
+	KK_PHOTON_EMIT, KK_PHOTON_BOUNCE, KK_PHOTON_COMPACT, KK_PHOTON_TREE, KK_FG, KK_PREGATHER, KK_GATHER_WALK, KK_PATH, KK_DFR, KK_COUNT
 };
 inline const char *kernelKindName(int k)
 {
 	static const char *n[KK_COUNT] = {"k_camera", "k_trace", "k_surface", "k_tshadow", "k_shade", "k_nee", "k_gather", "k_spawn",
 	                                  "k_combine", "k_film", "aa_next_pass", "k_photon_emit", "k_photon_bounce", "photon_compact",
-	                                  "pkd_build", "k_fg", "k_pregather", "k_gather_walk", "k_path"};
+	                                  "pkd_build", "k_fg", "k_pregather", "k_gather_walk", "k_path", "k_dfr"};
 	return (k >= 0 && k < KK_COUNT) ? n[k] : "";
 }
 struct KernelTimes

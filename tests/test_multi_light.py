@@ -154,3 +154,27 @@ def test_nee_request_word_packing(product, oracle_built, case, monkeypatch):
     o, wo, _ = oracle_built.OracleScene(spec, threads=1).render()
     assert np.array_equal(wa, wo)
     assert _ulp(a, o).max() <= 4
+
+
+@pytest.mark.parametrize("case", ["2-lights", "3-lights-paths2", "3-lights-adaptive", "rr-on", "overflow"])
+def test_deferred_light_pick_equals_count_run(product, oracle_built, case, monkeypatch):
+    """r06: the one-thread light pick without a count run (lpc_mode 3: every addition to a path colour kept
+    as a record, the lights picked from the counter bases after the pass, the records folded in order) renders
+    the count run's image bit for bit (YAFARAY_AMD_LIGHT_PICK=count), RR on and off, several chunks; a pass
+    whose records overflow their budget (YAFARAY_AMD_DFR_CAP) renders again with the count run."""
+    if case == "rr-on":
+        spec = with_lights(scenes.cornell(96, 72, spp=8, bounces=8, rr=True), 3)
+    elif case == "overflow":
+        spec = EXACT["2-lights"]()
+        monkeypatch.setenv("YAFARAY_AMD_DFR_CAP", "5000")
+    else:
+        spec = EXACT[case]()
+    a, wa, sa = product.render_spec(spec, chunk_slots=4096)
+    monkeypatch.delenv("YAFARAY_AMD_DFR_CAP", raising=False)
+    monkeypatch.setenv("YAFARAY_AMD_LIGHT_PICK", "count")
+    b, wb, sb = product.render_spec(spec, chunk_slots=4096)
+    assert np.array_equal(wa, wb)
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32)), int(_ulp(a, b).max())
+    if case != "rr-on":
+        o, wo, _ = oracle_built.OracleScene(spec, threads=1).render()
+        assert _ulp(a, o).max() <= 4
