@@ -330,7 +330,7 @@ struct DevScene
 	// wo + the sample's previous record, throughput or term + kind, emission + the call's ordinal, the pixel's
 	// sampling offset + sample index + counter index + light), dfr_last: per camera sample of the pass its last
 	// record (+1, bit 31: diffuse first hit; all ones: not finalized)
-	uint32_t *dfr_kind;    // per slot: 0 none, 1 light estimate, 2 known term | has emission << 2 | the call's ordinal << 3
+	uint32_t *dfr_kind;    // per slot: 0 none, 1 light estimate, 2 known term | has emission << 2 | the call's ordinal << 3 (k_dfr_part replaces it with the picked light)
 	float4 *dfr_pp;        // hit point, primitive (kind 1)
 	float4 *dfr_wo;        // wo, the picked light (k_dfr_nee)
 	float4 *dfr_a;         // the vertex throughput (kind 1) or the term (kind 2), the camera sample's counter index

@@ -4143,18 +4143,25 @@ __global__ void __launch_bounds__(1024) k_dfr_part(DfrArgs A)
 	__shared__ uint32_t cnt[kDfrMaxLights];
 	if(threadIdx.x < kDfrMaxLights) cnt[threadIdx.x] = 0u;
 	__syncthreads();
-	auto lightOf = [&](uint32_t jj, bool &rec) -> uint32_t {
-		rec = false;
-		if(jj >= n) return 0u;
-		const uint32_t slot = first + jj;
-		const uint32_t kind = S.dfr_kind[slot];
-		rec = (kind & 3u) == 1u;
-		return rec ? lightOfCounter(S, S.lpc[__float_as_uint(S.dfr_a[slot].w)] + (kind >> 3)) : 0u;
-	};
+	// pass 1: each record's light (its sample's counter base + the call's ordinal) replaces the spent ordinal in
+	// the kind word (k_dfr_nee / k_dfr_accum read it there); counts per light
 	for(uint32_t base_j = 0; base_j < n; base_j += blockDim.x)
 	{
-		bool rec;
-		const uint32_t l = lightOf(base_j + threadIdx.x, rec);
+		const uint32_t jj = base_j + threadIdx.x;
+		bool rec = false;
+		uint32_t l = 0;
+		if(jj < n)
+		{
+			const uint32_t slot = first + jj;
+			const uint32_t kind = S.dfr_kind[slot];
+			const uint32_t q = __float_as_uint(S.dfr_a[slot].w);   // (loaded with the kind; a hole's is not used)
+			rec = (kind & 3u) == 1u;
+			if(rec)
+			{
+				l = lightOfCounter(S, S.lpc[q] + (kind >> 3));
+				S.dfr_kind[slot] = (kind & 7u) | (l << 3);
+			}
+		}
 		waveAppendKeyed(rec, l, cnt);
 	}
 	__syncthreads();
@@ -4170,12 +4177,14 @@ __global__ void __launch_bounds__(1024) k_dfr_part(DfrArgs A)
 		A.n_rec[seg] = run;
 	}
 	__syncthreads();
+	// pass 2: the slots grouped by light (the order inside a light is irrelevant)
 	for(uint32_t base_j = 0; base_j < n; base_j += blockDim.x)
 	{
-		bool rec;
-		const uint32_t l = lightOf(base_j + threadIdx.x, rec);
-		const uint32_t pos = waveAppendKeyed(rec, l, cnt);
-		if(rec) A.idx[(size_t)seg * S.cap_a + pos] = first + base_j + threadIdx.x;
+		const uint32_t jj = base_j + threadIdx.x;
+		const uint32_t kind = jj < n ? S.dfr_kind[first + jj] : 0u;
+		const bool rec = (kind & 3u) == 1u;
+		const uint32_t pos = waveAppendKeyed(rec, kind >> 3, cnt);
+		if(rec) A.idx[(size_t)seg * S.cap_a + pos] = first + jj;
 	}
 }
 
@@ -4195,37 +4204,30 @@ __global__ void __launch_bounds__(kShadeBlock, LEAN ? YAF_NEE_LEAN_WAVES : YAF_N
 	out.sh_base = seg * S.cap_s;
 	out.Qn = A.Q;
 	out.idx_in_o = true;
-	// the segment's light-estimate records, grouped by light (k_dfr_part)
+	// the segment's light-estimate records, grouped by light (k_dfr_part; every listed slot is a light estimate).
+	// The loop is latency bound (4 waves per SIMD, one record per lane and trip): the next trip's slot is
+	// fetched before this trip's estimate, and a record's arrays are loaded together
 	const uint32_t n = A.n_rec[seg];
 	const int K = S.nee_k;
+	const uint32_t *list = A.idx + (size_t)seg * S.cap_a;
+	uint32_t slot_next = threadIdx.x < n ? list[threadIdx.x] : A.r0;
 	for(uint32_t base_j = 0; base_j < n; base_j += blockDim.x)
 	{
 		const uint32_t jj = base_j + threadIdx.x;
-		bool live = jj < n;
-		const uint32_t slot = live ? A.idx[(size_t)seg * S.cap_a + jj] : A.r0;
-		uint32_t kind = 0;
-		float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
-		uint2 pix = make_uint2(0u, 0u);
-		if(live)
-		{
-			kind = S.dfr_kind[slot];
-			live = (kind & 3u) == 1u;
-		}
-		if(live)
-		{
-			r0 = S.dfr_pp[slot];
-			r1 = S.dfr_wo[slot];
-			r2 = S.dfr_a[slot];
-			pix = S.dfr_pix[slot];
-		}
+		const bool live = jj < n;
+		const uint32_t slot = slot_next;
+		const uint32_t kind = S.dfr_kind[slot];
+		const float4 r0 = S.dfr_pp[slot], r1 = S.dfr_wo[slot], r2 = S.dfr_a[slot];
+		const uint2 pix = S.dfr_pix[slot];
+		slot_next = jj + blockDim.x < n ? list[jj + blockDim.x] : A.r0;
 		Surf sp;
 		sp.p = v3(0.f, 0.f, 0.f); sp.n = sp.ng = sp.nu = sp.nv = sp.p; sp.mat = 0; sp.flags = 0;
 		sp.dcol = c3(0.f); sp.drefl = 1.f; sp.sigma = 0.f;
 		uint32_t lnum = 0;
 		if(live)
 		{
+			lnum = kind >> 3;   // k_dfr_part's pick
 			sp = surfFromPrim(S, xyz(r0), __float_as_int(r0.w));
-			lnum = lightOfCounter(S, S.lpc[__float_as_uint(r2.w)] + (kind >> 3));   // (k_dfr_accum picks it again)
 		}
 		const V3 wo = xyz(r1);
 		const int e0 = (int)(slot - A.r0) * K;   // (k_dfr_accum reads them by slot)
@@ -4260,7 +4262,7 @@ __global__ void __launch_bounds__(256) k_dfr_accum(DfrArgs A, float *pcol, uint3
 	C3 term = rgb(a);
 	if((kind & 3u) == 1u)
 	{
-		const uint32_t lnum = lightOfCounter(S, S.lpc[__float_as_uint(a.w)] + (kind >> 3));   // k_dfr_nee's pick
+		const uint32_t lnum = kind >> 3;   // k_dfr_part's pick
 		const int kb = (int)(slot - batch0) * S.nee_k;
 		auto ge = [&](int k) { return f4(neeGet(neeHbm(A.P), k), 1.f); };
 		auto go = [&](int k) { return A.P.occ[k] != 0; };
