@@ -67,6 +67,8 @@ typedef struct
 	uint64_t fg_nearest_visits; /* final gathering: radiance-map kd nodes those searches fetched (1.6) */
 	uint64_t pregather_visits;  /* final gathering: diffuse-map kd nodes the radiance-map pre-gather fetched (1.6) */
 	uint64_t pregather_photons; /* final gathering: photons summed by the pre-gather (1.6) */
+	uint64_t pkd_split_level;   /* device / render group: the level at which the members split the last point kd-tree
+	                               build (each built the subtrees below it it owns; 0 = every member built the whole tree) (1.6) */
 } yafaray_amd_stats_t;
 
 /* Bytes of the LIBYAFARAY_AMD_1.0 struct (its fields end at photon_tree_seconds): yafaray_amd_getStats
@@ -170,6 +172,19 @@ YAFARAY_C_API_EXPORT int yafaray_amd_unpackBands(const float *recv, int width, i
  * interior: right child << 2 and .x the split position bits, .y / .z the parent's plane; leaf:
  * photon index << 2 and .xyz its position bits), *depth = deepest level (root 0).  Current device. */
 YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_buildPhotonTree(const float *xyz, int n, unsigned int *nodes, int *depth);
+/* (LIBYAFARAY_AMD_1.6) The distributed build of a device / render group (what a group render runs for its
+ * photon maps): member `member` of `members` builds the levels above *split_level = ceil(log2 members)
+ * (0: too few photons to split — the whole tree) and the level-D subtrees it owns, with the map's records
+ * in kd order (leaves index kd_pos, n x 4 floats); the other members' subtrees and the parent planes
+ * (.y / .z of interior nodes) are left zero — a group exchanges the ranges yafaray_amd_photonTreeSegments
+ * gives and writes the planes.  *ms = the build's device time (second of two builds).  Current device. */
+YAFARAY_C_API_EXPORT yafaray_bool_t yafaray_amd_buildPhotonTreeMember(const float *xyz, int n, int member, int members, unsigned int *nodes,
+                                                                      float *kd_pos, int *depth, int *split_level, double *ms);
+/* (LIBYAFARAY_AMD_1.6) The level-`level` subtrees of a tree over n photons, (node, start, end) each in
+ * segments[3 << level] (nodes [node, node + 2 (end - start) - 1), kd-order records [start, end)), and the
+ * consecutive ones member `member` of `members` owns: [*s0, *s1). */
+YAFARAY_C_API_EXPORT void yafaray_amd_photonTreeSegments(unsigned int n, int level, int member, int members, unsigned int *segments,
+                                                         unsigned int *s0, unsigned int *s1);
 YAFARAY_C_API_EXPORT void yafaray_amd_setChunkSlots(yafaray_Interface_t *interface, int slots);
 YAFARAY_C_API_EXPORT void yafaray_amd_setProfileKernels(yafaray_Interface_t *interface, yafaray_bool_t enable);
 /* (LIBYAFARAY_AMD_1.2) Per-visit BVH node / triangle counters in the traversal kernels (default on).

@@ -46,7 +46,7 @@ class Stats(C.Structure):
                 ("gather_accepts", C.c_uint64), ("gather_overflows", C.c_uint64),
                 ("photon_paths_traced", C.c_uint64), ("photon_slots", C.c_uint64),
                 ("fg_paths", C.c_uint64), ("fg_lookups", C.c_uint64), ("fg_nearest_visits", C.c_uint64),
-                ("pregather_visits", C.c_uint64), ("pregather_photons", C.c_uint64)]
+                ("pregather_visits", C.c_uint64), ("pregather_photons", C.c_uint64), ("pkd_split_level", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -149,6 +149,10 @@ def lib():
             "yafaray_amd_packBand": (i, [C.POINTER(C.c_float), i, i, i, C.POINTER(C.c_int), i, i, C.POINTER(C.c_float)]),
             "yafaray_amd_unpackBands": (i, [C.POINTER(C.c_float), i, i, i, C.POINTER(C.c_int), i, i, C.POINTER(C.c_float)]),
             "yafaray_amd_buildPhotonTree": (b, [C.POINTER(C.c_float), i, C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
+            "yafaray_amd_buildPhotonTreeMember": (b, [C.POINTER(C.c_float), i, i, i, C.POINTER(C.c_uint32), C.POINTER(C.c_float),
+                                                      C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
+            "yafaray_amd_photonTreeSegments": (None, [C.c_uint, i, i, i, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                                      C.POINTER(C.c_uint32)]),
             "yafaray_amd_setChunkSlots": (None, [vp, i]),
             "yafaray_amd_setProfileKernels": (None, [vp, b]),
             "yafaray_amd_setTraceStats": (None, [vp, b]),
@@ -390,6 +394,33 @@ def build_photon_tree(xyz):
     if not ok:
         raise RuntimeError("yafaray_amd_buildPhotonTree failed")
     return nodes, depth.value
+
+
+def build_photon_tree_member(xyz, member, members):
+    """A group member's share of the distributed point kd-tree build (yafaray_amd_buildPhotonTreeMember):
+    (nodes (2n - 1, 4) uint32, kd-order positions (n, 4) float32, depth, split level, device ms)."""
+    import numpy as np
+    xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+    n = int(xyz.shape[0])
+    nodes = np.zeros((2 * n - 1, 4), np.uint32)
+    kd = np.zeros((n, 4), np.float32)
+    depth, level, ms = C.c_int(0), C.c_int(0), C.c_double(0)
+    ok = lib().yafaray_amd_buildPhotonTreeMember(xyz.ctypes.data_as(C.POINTER(C.c_float)), n, member, members,
+                                                 nodes.ctypes.data_as(C.POINTER(C.c_uint32)), kd.ctypes.data_as(C.POINTER(C.c_float)),
+                                                 C.byref(depth), C.byref(level), C.byref(ms))
+    if not ok:
+        raise RuntimeError("yafaray_amd_buildPhotonTreeMember failed")
+    return nodes, kd, depth.value, level.value, ms.value
+
+
+def photon_tree_segments(n, level, member=0, members=1):
+    """The level-`level` subtrees of a tree over n photons ((2^level, 3) uint32: node, start, end) and the
+    owned range [s0, s1) of member `member` (yafaray_amd_photonTreeSegments)."""
+    import numpy as np
+    seg = np.zeros((1 << level, 3), np.uint32)
+    s0, s1 = C.c_uint32(0), C.c_uint32(0)
+    lib().yafaray_amd_photonTreeSegments(n, level, member, members, seg.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(s0), C.byref(s1))
+    return seg, (s0.value, s1.value)
 
 
 def rebalance_bands(bounds, times, cap_rows=0):

@@ -718,6 +718,62 @@ yafaray_bool_t yafaray_amd_buildPhotonTree(const float *xyz, int n, unsigned int
 	return ok ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
 }
 
+// (1.6) a device / render group member's share of the distributed build (pkd.hip yafamd_build_pkd_kd_member):
+// the whole top above the split level and the member's own subtrees, nodes and kd-order positions out
+// (the other members' ranges zero); built twice, *ms = the second build's device time
+extern "C" hipError_t yafamd_build_pkd_kd_member(const float4 *pos_dev, const float4 *dir_dev, const float *colb_dev, uint32_t n, uint4 *nodes_dev,
+                                                 float4 *kpos, float4 *kdir, float *kcolb, int *depth_out, hipStream_t st, void **scratch, int member,
+                                                 int members, int *split_level);
+extern "C" void yafamd_pkd_top_segments(uint32_t n, int level, uint32_t *out);
+extern "C" void yafamd_pkd_owned_segments(int level, int member, int members, uint32_t *s0, uint32_t *s1);
+yafaray_bool_t yafaray_amd_buildPhotonTreeMember(const float *xyz, int n, int member, int members, unsigned int *nodes, float *kd_pos, int *depth,
+                                                 int *split_level, double *ms)
+{
+	if(!xyz || !nodes || !kd_pos || !depth || !split_level || n < 1 || members < 1 || member < 0 || member >= members) return YAFARAY_BOOL_FALSE;
+	std::vector<float4> pos((size_t)n);
+	for(int i = 0; i < n; ++i) pos[(size_t)i] = make_float4(xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1], xyz[3 * (size_t)i + 2], 0.f);
+	const size_t nn = 2 * (size_t)n - 1;
+	float4 *pos_dev = nullptr, *dir_dev = nullptr, *kpos = nullptr, *kdir = nullptr;
+	float *colb = nullptr, *kcolb = nullptr;
+	uint4 *nodes_dev = nullptr;
+	hipStream_t st = nullptr;
+	hipEvent_t e0 = nullptr, e1 = nullptr;
+	void *scratch = nullptr;
+	bool ok = hipStreamCreate(&st) == hipSuccess && hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+	          hipMalloc(&pos_dev, (size_t)n * 16) == hipSuccess && hipMalloc(&dir_dev, (size_t)n * 16) == hipSuccess &&
+	          hipMalloc(&colb, (size_t)n * 4) == hipSuccess && hipMalloc(&kpos, (size_t)n * 16) == hipSuccess &&
+	          hipMalloc(&kdir, (size_t)n * 16) == hipSuccess && hipMalloc(&kcolb, (size_t)n * 4) == hipSuccess &&
+	          hipMalloc(&nodes_dev, nn * 16) == hipSuccess && hipMemcpyAsync(pos_dev, pos.data(), (size_t)n * 16, hipMemcpyHostToDevice, st) == hipSuccess &&
+	          hipMemsetAsync(dir_dev, 0, (size_t)n * 16, st) == hipSuccess && hipMemsetAsync(colb, 0, (size_t)n * 4, st) == hipSuccess;
+	for(int pass = 0; pass < 2 && ok; ++pass)
+	{
+		ok = hipMemsetAsync(nodes_dev, 0, nn * 16, st) == hipSuccess && hipMemsetAsync(kpos, 0, (size_t)n * 16, st) == hipSuccess &&
+		     hipEventRecord(e0, st) == hipSuccess &&
+		     yafamd_build_pkd_kd_member(pos_dev, dir_dev, colb, (uint32_t)n, nodes_dev, kpos, kdir, kcolb, depth, st, &scratch, member, members,
+		                                split_level) == hipSuccess &&
+		     hipEventRecord(e1, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+	}
+	float t = 0.f;
+	ok = ok && hipEventElapsedTime(&t, e0, e1) == hipSuccess && hipMemcpy(nodes, nodes_dev, nn * 16, hipMemcpyDeviceToHost) == hipSuccess &&
+	     hipMemcpy(kd_pos, kpos, (size_t)n * 16, hipMemcpyDeviceToHost) == hipSuccess;
+	if(ms) *ms = t;
+	if(scratch) yafamd_pkd_scratch_free(scratch);
+	for(void *p : {(void *)pos_dev, (void *)dir_dev, (void *)colb, (void *)kpos, (void *)kdir, (void *)kcolb, (void *)nodes_dev})
+		if(p) (void)hipFree(p);
+	if(e0) (void)hipEventDestroy(e0);
+	if(e1) (void)hipEventDestroy(e1);
+	if(st) (void)hipStreamDestroy(st);
+	return ok ? YAFARAY_BOOL_TRUE : YAFARAY_BOOL_FALSE;
+}
+
+// (1.6) the level-D subtrees of a tree over n photons (node, start, end each: 3 << level values) and the
+// ones member r of `members` owns ([s0, s1))
+void yafaray_amd_photonTreeSegments(unsigned int n, int level, int member, int members, unsigned int *segments, unsigned int *s0, unsigned int *s1)
+{
+	if(segments) yafamd_pkd_top_segments(n, level, segments);
+	if(s0 && s1 && members >= 1) yafamd_pkd_owned_segments(level, member, members, s0, s1);
+}
+
 int yafaray_amd_packBand(const float *film, int width, int height, int channels, const int *bounds, int world, int rank, float *send)
 {
 	if(!bounds || world < 1) return 0;

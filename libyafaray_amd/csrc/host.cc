@@ -295,6 +295,7 @@ bool Scene::renderDeviceGroup(RenderParams &rp)
 		st.fg_nearest_visits += o.fg_nearest_visits;
 		st.pregather_visits += o.pregather_visits;
 		st.pregather_photons += o.pregather_photons;
+		st.pkd_split_level = std::max(st.pkd_split_level, o.pkd_split_level);
 		st.trace_kernel_ms += o.trace_kernel_ms;
 		st.shade_kernel_ms += o.shade_kernel_ms;
 		st.nee_kernel_ms += o.nee_kernel_ms;

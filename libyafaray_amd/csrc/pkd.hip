@@ -29,6 +29,7 @@
 // (k_gather_walk); the reference's tree is unaffected.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <string>
@@ -105,11 +106,84 @@ __global__ void __launch_bounds__(256) k_parent_planes(uint4 *nodes, uint32_t n_
 	if(i == 0u) { nodes[0].y = 0u; nodes[0].z = 3u; }
 }
 
-static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch, const KdPayload &kp);
+static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch, const KdPayload &kp,
+                           int member = 0, int members = 1, int *split_level = nullptr);
 
 extern "C" hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch)
 {
 	return buildPkd(pos_dev, n, nodes_dev, depth_out, st, scratch, KdPayload{});
+}
+
+// The level at which a group of `members` splits the build: D = ceil(log2 members), when the top phase runs
+// at least D levels (every node of the levels < D holds more than kSub photons); 0 = not split.
+extern "C" int yafamd_pkd_split_level(uint32_t n, int members)
+{
+	if(members <= 1) return 0;
+	int D = 0;
+	while((1 << D) < members) ++D;
+	uint32_t max_m = n;
+	for(int l = 0; l < D; ++l)
+	{
+		if(max_m <= (uint32_t)kSub) return 0;
+		max_m = (max_m + 1) / 2;
+	}
+	return D;
+}
+
+// The level-D segments of a tree over n photons, in order (node, start, end each): level d's nodes are the
+// recursive halving of [0, n) at (start + end) / 2, a node's left child is node + 1 and its right child
+// node + 2 (mid - start) (the depth-first layout).  A subtree of m photons occupies nodes [node, node + 2m - 1)
+// and list (kd-order record) positions [start, end).
+extern "C" void yafamd_pkd_top_segments(uint32_t n, int level, uint32_t *out /* 3 << level */)
+{
+	std::vector<uint32_t> cur{0u, 0u, n}, nxt;
+	for(int l = 0; l < level; ++l)
+	{
+		nxt.clear();
+		for(size_t k = 0; k < cur.size(); k += 3)
+		{
+			const uint32_t node = cur[k], a = cur[k + 1], b = cur[k + 2], mid = (a + b) / 2;
+			nxt.insert(nxt.end(), {node + 1u, a, mid, node + 2u * (mid - a), mid, b});
+		}
+		cur.swap(nxt);
+	}
+	std::copy(cur.begin(), cur.end(), out);
+}
+
+// the level-D segments member r of `members` finishes: [s0, s1), consecutive
+extern "C" void yafamd_pkd_owned_segments(int level, int member, int members, uint32_t *s0, uint32_t *s1)
+{
+	*s0 = (uint32_t)(((uint64_t)member << level) / (uint64_t)members);
+	*s1 = (uint32_t)(((uint64_t)(member + 1) << level) / (uint64_t)members);
+}
+
+// the interior nodes' parent planes (k_parent_planes) — after a group's member builds were exchanged
+extern "C" hipError_t yafamd_pkd_parent_planes(uint4 *nodes_dev, uint32_t n, hipStream_t st)
+{
+	if(n == 0) return hipSuccess;
+	hipLaunchKernelGGL(k_parent_planes, dim3((2 * n - 1 + 255) / 256), dim3(256), 0, st, nodes_dev, 2 * n - 1);
+	return hipGetLastError();
+}
+
+// A group member's share of the build (the distributed point kd-tree): the same sorts and top
+// levels < D as the whole build (every member writes the same ancestor nodes), then only the level-D
+// subtrees this member owns (yafamd_pkd_owned_segments) — their nodes and kd-order records; the other
+// members' subtrees are left unwritten and the parent planes are not written (the caller exchanges the
+// ranges yafamd_pkd_top_segments gives, then runs yafamd_pkd_parent_planes).  *split_level = D, or 0 when
+// the tree is too small to split (then this was the whole build, parent planes included).
+extern "C" hipError_t yafamd_build_pkd_kd_member(const float4 *pos_dev, const float4 *dir_dev, const float *colb_dev, uint32_t n, uint4 *nodes_dev,
+                                                 float4 *kpos, float4 *kdir, float *kcolb, int *depth_out, hipStream_t st, void **scratch, int member,
+                                                 int members, int *split_level)
+{
+	if(n && (!dir_dev || !colb_dev || !kpos || !kdir || !kcolb)) return hipErrorInvalidValue;
+	if(members < 1 || member < 0 || member >= members || !split_level) return hipErrorInvalidValue;
+	KdPayload kp;
+	kp.dir = dir_dev;
+	kp.colb = colb_dev;
+	kp.kpos = kpos;
+	kp.kdir = kdir;
+	kp.kcolb = kcolb;
+	return buildPkd(pos_dev, n, nodes_dev, depth_out, st, scratch, kp, member, members, split_level);
 }
 
 // The same build, and the map's records copied into kd (leaf) order by the subtree pass: leaves
@@ -127,9 +201,17 @@ extern "C" hipError_t yafamd_build_pkd_kd(const float4 *pos_dev, const float4 *d
 	return buildPkd(pos_dev, n, nodes_dev, depth_out, st, scratch, kp);
 }
 
-static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch, const KdPayload &kp)
+static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, int *depth_out, hipStream_t st, void **scratch, const KdPayload &kp,
+                           int member, int members, int *split_level)
 {
+	if(split_level) *split_level = 0;
 	if(n == 0) return hipSuccess;
+	// fused partitions (default) or the scan + partition passes per list (YAFARAY_AMD_PKD_PARTITION=scan;
+	// a member build then builds the whole tree)
+	const char *pe = getenv("YAFARAY_AMD_PKD_PARTITION");
+	const bool fused = !(pe && std::string(pe) == "scan");
+	const int D = fused ? yafamd_pkd_split_level(n, members) : 0;
+	if(split_level) *split_level = D;
 	if(!scratch) return hipErrorInvalidValue;
 	if(!*scratch) *scratch = new PkdScratch;
 	PkdScratch &S = *static_cast<PkdScratch *>(*scratch);
@@ -168,9 +250,6 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 		PKCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, in, S.scan.as<uint32_t>(), (int)n, st));
 	}
 	PKCHECK(S.scan_tmp.ensure(scan_bytes));
-	// fused partitions (default) or the scan + partition passes per list (YAFARAY_AMD_PKD_PARTITION=scan)
-	const char *pe = getenv("YAFARAY_AMD_PKD_PARTITION");
-	const bool fused = !(pe && std::string(pe) == "scan");
 	if(!fused) PKCHECK(hipMemsetAsync(S.seg_of.p, 0, (size_t)n * 4, st));   // the scan passes' per-entry segments
 	const uint32_t n_tiles = (n + kPartTile - 1) / kPartTile;
 	size_t left_scan_bytes = 0;
@@ -185,12 +264,32 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 		PKCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, left_scan_bytes, S.seg_nl.as<uint32_t>(), S.seg_left.as<uint32_t>(), (int)n, st));
 		PKCHECK(S.scan_tmp.ensure(std::max(scan_bytes, left_scan_bytes)));
 	}
-	// top phase: level d has 2^d nodes of floor / ceil(n / 2^d) photons
+	// top phase: level d has 2^d nodes of floor / ceil(n / 2^d) photons.  A member build (D > 0) narrows
+	// to its consecutive level-D segments [s0, s1) once level D is reached: their entries [lo, hi) are
+	// partitioned, and seg_base maps a level's global segment number to the local list
 	uint32_t n_seg = 1;
 	int cur = 0, level = 0;
 	uint32_t max_m = n;
+	uint32_t lo = 0, hi = n, s0 = 0;
+	bool narrowed = false;
+	auto narrow = [&]() -> hipError_t {
+		uint32_t s1 = 0;
+		yafamd_pkd_owned_segments(D, member, members, &s0, &s1);
+		std::vector<uint32_t> top((size_t)3 << D);
+		yafamd_pkd_top_segments(n, D, top.data());
+		lo = top[3 * (size_t)s0 + 1];
+		hi = top[3 * (size_t)(s1 - 1) + 2];
+		// the owned segments at the front of the other list (their bounds came from the levels above)
+		PKCHECK(hipMemcpyAsync(S.segs[cur ^ 1].p, S.segs[cur].as<Seg>() + s0, (size_t)(s1 - s0) * sizeof(Seg), hipMemcpyDeviceToDevice, st));
+		cur ^= 1;
+		n_seg = s1 - s0;
+		narrowed = true;
+		return hipSuccess;
+	};
 	while(max_m > (uint32_t)kSub)
 	{
+		if(D > 0 && level == D) PKCHECK(narrow());
+		const uint32_t seg_base = D > 0 && level >= D ? s0 << (level - D) : 0u;
 		const uint32_t Gs = (n_seg + B - 1) / B;
 		hipLaunchKernelGGL(k_level_split, dim3(Gs), dim3(B), 0, st, S.segs[cur].as<Seg>(), n_seg, n, S.rec[0].as<uint4>(), S.rec[1].as<uint4>(),
 		                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, S.splits.as<Split>(), S.segs[cur ^ 1].as<Seg>(),
@@ -211,12 +310,16 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 			P.splits = S.splits.as<Split>();
 			P.seg_left = S.seg_left.as<uint32_t>();
 			P.n = n;
-			P.n_tiles = n_tiles;
+			P.n_tiles = (hi - lo + kPartTile - 1) / kPartTile;
+			P.lo = lo;
+			P.hi = hi;
+			P.seg_base = seg_base;
+			P.n_seg = n_seg;
 			P.epoch = (uint32_t)level + 1u;
 			P.ticket = S.part_misc.as<uint32_t>();
 			P.err = S.part_misc.as<uint32_t>() + 1;
 			P.status = S.status.as<uint64_t>();
-			hipLaunchKernelGGL(k_level_partition, dim3(3 * n_tiles), dim3(kPartThreads), 0, st, P);
+			hipLaunchKernelGGL(k_level_partition, dim3(3 * P.n_tiles), dim3(kPartThreads), 0, st, P);
 			for(int a = 0; a < 3; ++a)
 			{
 				std::swap(S.rec[a].p, outs[a]->p);
@@ -245,6 +348,7 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 		cur ^= 1;
 		++level;
 	}
+	if(D > 0 && !narrowed) PKCHECK(narrow());   // the top phase ended at level D
 	// bottom phase: one workgroup per subtree
 	// the deepest level: the largest subtree (ceil(n / 2^level) photons) halves (its larger half
 	// rounding up) until single photons — the device build computes it here instead of one atomicMax per
@@ -257,7 +361,7 @@ static hipError_t buildPkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev, 
 	const uint32_t sub_threads = std::min<uint32_t>((uint32_t)kSubThreads, (std::max<uint32_t>(max_m, 1u) + 63u) & ~63u);
 	hipLaunchKernelGGL(k_subtrees, dim3(n_seg), dim3(sub_threads), 0, st, S.segs[cur].as<Seg>(), S.rec[0].as<uint4>(), S.rec[1].as<uint4>(),
 	                   S.rec[2].as<uint4>(), pos_dev, nodes_dev, n, level, dev_max_level, kp);
-	hipLaunchKernelGGL(k_parent_planes, dim3((2 * n - 1 + 255) / 256), dim3(256), 0, st, nodes_dev, 2 * n - 1);
+	if(D == 0) hipLaunchKernelGGL(k_parent_planes, dim3((2 * n - 1 + 255) / 256), dim3(256), 0, st, nodes_dev, 2 * n - 1);
 	int depth = level;
 	for(uint32_t m = max_m; m > 1u; m = (m + 1u) / 2u) ++depth;
 	uint32_t part_err = 0;

@@ -295,6 +295,10 @@ struct PartArgs
 	const Split *splits;
 	const uint32_t *seg_left;
 	uint32_t n, n_tiles, epoch;
+	// the entries [lo, hi) partitioned: the whole list, or the owned subtrees of a group member's build
+	// (consecutive level-D segments); segs / splits / seg_left hold n_seg segments, the first being global
+	// segment seg_base of this level
+	uint32_t lo, hi, seg_base, n_seg;
 	uint32_t *ticket;
 	uint64_t *status;    // 3 x n_tiles: (tag << 32) | count; tag 2 epoch = tile count, 2 epoch + 1 = inclusive prefix
 	uint32_t *err;       // set when a look-back gave up (spin limit): the build reports an error
@@ -334,12 +338,12 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 	const uint4 *in = A.in[list];
 	uint4 *out = A.out[list];
 	uint64_t *st = A.status + (size_t)list * A.n_tiles;
-	const uint32_t base = tile * kPartTile;
+	const uint32_t base = A.lo + tile * kPartTile;
 	// the tile's segments: the first by descent, the starts of it and its successors from the segment
 	// list (no per-entry segment array: 16 B per photon and level less traffic)
-	if(t == 0) s_seg0 = segOfPos(base, A.n, A.level);
+	if(t == 0) s_seg0 = segOfPos(base, A.n, A.level) - A.seg_base;
 	__syncthreads();
-	const uint32_t seg0 = s_seg0, n_seg = 1u << A.level;
+	const uint32_t seg0 = s_seg0, n_seg = A.n_seg;
 #if YAF_PART_PRELOAD
 	// the tile's splits staged with the segment starts, and every record loaded before the first flag is
 	// computed: the eight 16-B loads of a thread are in flight together (computing each flag right after
@@ -356,7 +360,7 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 	for(int i = 0; i < kPartItems; ++i)
 	{
 		const uint32_t e = base + (uint32_t)i * kPartThreads + t;
-		r[i] = e < A.n ? in[e] : make_uint4(0u, 0u, 0u, 0u);
+		r[i] = e < A.hi ? in[e] : make_uint4(0u, 0u, 0u, 0u);
 	}
 	__syncthreads();
 #else
@@ -374,7 +378,7 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 #if !YAF_PART_PRELOAD
 		r[i] = make_uint4(0u, 0u, 0u, 0u);
 #endif
-		if(e < A.n)
+		if(e < A.hi)
 		{
 #if !YAF_PART_PRELOAD
 			r[i] = in[e];
@@ -471,7 +475,7 @@ __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
 	for(int i = 0; i < kPartItems; ++i)
 	{
 		const uint32_t e = base + (uint32_t)i * kPartThreads + t;
-		if(e >= A.n) continue;
+		if(e >= A.hi) continue;
 		const uint32_t s = so[i];
 #if YAF_PART_PRELOAD
 		const uint32_t start = s_start[s - seg0], split_el = s_split[s - seg0].split_el;

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -91,6 +92,12 @@ hipError_t yafamd_build_pkd(const float4 *pos_dev, uint32_t n, uint4 *nodes_dev,
 hipError_t yafamd_build_pkd_kd(const float4 *pos_dev, const float4 *dir_dev, const float *colb_dev, uint32_t n, uint4 *nodes_dev, float4 *kpos,
                                float4 *kdir, float *kcolb, int *depth_out, hipStream_t st, void **scratch);
 void yafamd_pkd_scratch_free(void *scratch);
+hipError_t yafamd_build_pkd_kd_member(const float4 *pos_dev, const float4 *dir_dev, const float *colb_dev, uint32_t n, uint4 *nodes_dev, float4 *kpos,
+                                      float4 *kdir, float *kcolb, int *depth_out, hipStream_t st, void **scratch, int member, int members,
+                                      int *split_level);
+void yafamd_pkd_top_segments(uint32_t n, int level, uint32_t *out);
+void yafamd_pkd_owned_segments(int level, int member, int members, uint32_t *s0, uint32_t *s1);
+hipError_t yafamd_pkd_parent_planes(uint4 *nodes_dev, uint32_t n, hipStream_t st);
 hipError_t yafamd_launch_done_flags(const DevScene *S, const DevJob *jobs, int n_jobs, uint32_t n_pix, uint32_t done_pix, uint8_t *flags,
                                     hipStream_t st);
 hipError_t yafamd_lpc_seg(const uint32_t *lpc, int W, int spp, int ts, int y0, int y1, uint32_t *seg, hipStream_t st);
@@ -985,7 +992,7 @@ bool GpuRenderer::shootMap(RenderParams &rp, const PhotonSet &L, uint32_t N, int
 	// point kd-tree of the map, built on the GPU node for node like the reference's (pkd.hip)
 	if(!ensure(log_, nodes, (2 * (size_t)n - 1) * sizeof(uint4))) return false;
 	int depth = 0;
-	if(!buildMapTree(which, pos.p, dir.p, colb.p, n, nodes.p, depth)) return false;
+	if(!buildMapTree(which, pos.p, dir.p, colb.p, n, nodes.p, depth, group_render)) return false;
 	depth_out = depth;
 	stats_.photon_tree_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
 	return true;
@@ -1145,12 +1152,54 @@ bool GpuRenderer::groupConcat(int kind, const std::vector<uint32_t> &counts)
 // (leaf) order (kd_pos / kd_dir / kd_colb) and the leaves index those copies, so a k-NN lookup's
 // photons are read from neighbouring lines; YAFARAY_AMD_PKD_ORDER=photon keeps photon-order leaves
 // (measurement switch; the estimates are identical either way).
-bool GpuRenderer::buildMapTree(int which, const void *pos, const void *dir, const void *colb, uint32_t n, void *nodes, int &depth)
+//
+// group_split (a device / render group's photon maps, every member holding the whole map): the build is
+// distributed — member r sorts and runs the top levels above level D = ceil(log2 members) like everyone,
+// then only its own level-D subtrees (pkd.hip yafamd_build_pkd_kd_member), and the members exchange those
+// subtrees' node and record ranges (exchangeTree).  YAFARAY_AMD_PKD_SPLIT=0: every member builds the tree.
+bool GpuRenderer::buildMapTree(int which, const void *pos, const void *dir, const void *colb, uint32_t n, void *nodes, int &depth, bool group_split)
 {
 	Impl &d = *d_;
 	const char *oe = std::getenv("YAFARAY_AMD_PKD_ORDER");
 	const bool kd = !(oe && std::string(oe) == "photon");
 	d.kd_on[which] = false;
+	int members = 1, me = 0;
+	if(group_split && peers_ && peers_->size() > 1)
+	{
+		members = peers_->size();
+		me = peer_rank_;
+	}
+	else if(group_split && d.comm && group_world_ > 1)
+	{
+		members = group_world_;
+		me = group_rank_;
+	}
+	if(const char *se = std::getenv("YAFARAY_AMD_PKD_SPLIT"); se && *se == '0') members = 1;
+	if(kd && n && members > 1)
+	{
+		// every member reaches the status agreement below, whatever failed before it
+		bool ok = ensure(log_, d.kd_pos[which], (size_t)n * 16) && ensure(log_, d.kd_dir[which], (size_t)n * 16) &&
+		          ensure(log_, d.kd_colb[which], (size_t)n * 4);
+		int D = 0;
+		if(ok)
+		{
+			const int e0 = d.profBegin();
+			const hipError_t e = yafamd_build_pkd_kd_member((const float4 *)pos, (const float4 *)dir, (const float *)colb, n, (uint4 *)nodes,
+			                                                (float4 *)d.kd_pos[which].p, (float4 *)d.kd_dir[which].p, (float *)d.kd_colb[which].p,
+			                                                &depth, d.stream, &d.pkd_scratch, me, members, &D);
+			d.profEnd(KK_PHOTON_TREE, e0);
+			ok = e == hipSuccess && hipStreamSynchronize(d.stream) == hipSuccess;
+			if(!ok) log_.error(std::string("GPU: point kd-tree build failed (") + hipGetErrorString(e) + ")");
+		}
+		if(groupStatus(ok ? 0 : 2) >= 2)
+		{
+			if(ok) log_.error("GPU group: a member failed; render abandoned");
+			return false;
+		}
+		d.kd_on[which] = true;
+		stats_.pkd_split_level = std::max<uint64_t>(stats_.pkd_split_level, (uint64_t)D);
+		return D == 0 || exchangeTree(which, n, nodes, D, members);
+	}
 	if(kd && n)
 	{
 		if(!ensure(log_, d.kd_pos[which], (size_t)n * 16) || !ensure(log_, d.kd_dir[which], (size_t)n * 16) ||
@@ -1162,6 +1211,71 @@ bool GpuRenderer::buildMapTree(int which, const void *pos, const void *dir, cons
 		d.kd_on[which] = true;
 	}
 	else if(n) PROF(KK_PHOTON_TREE, yafamd_build_pkd((const float4 *)pos, n, (uint4 *)nodes, &depth, d.stream, &d.pkd_scratch));
+	HIPCHECK(hipStreamSynchronize(d.stream));
+	return true;
+}
+
+// The distributed build's exchange: every member receives the node range [node, node + 2m - 1) and the
+// kd-order record range [start, end) of every level-D subtree another member built (the ancestors above
+// level D every member built itself), then writes the parent planes over the whole tree.
+bool GpuRenderer::exchangeTree(int which, uint32_t n, void *nodes, int D, int members)
+{
+	Impl &d = *d_;
+	std::vector<uint32_t> top((size_t)3 << D);
+	yafamd_pkd_top_segments(n, D, top.data());
+	std::vector<int> owner((size_t)1 << D, 0);
+	for(int r = 0; r < members; ++r)
+	{
+		uint32_t s0 = 0, s1 = 0;
+		yafamd_pkd_owned_segments(D, r, members, &s0, &s1);
+		for(uint32_t s = s0; s < s1; ++s) owner[s] = r;
+	}
+	auto nodesOf = [which](Impl &m) -> Buf & { return which == 0 ? m.pk_nodes : which == 1 ? m.cpk_nodes : m.rpk_nodes; };
+	struct Range { size_t off, bytes; };
+	auto ranges = [&](uint32_t s) {
+		const uint32_t node = top[3 * (size_t)s], a = top[3 * (size_t)s + 1], b = top[3 * (size_t)s + 2];
+		return std::array<Range, 4>{Range{(size_t)node * 16, (2 * (size_t)(b - a) - 1) * 16}, Range{(size_t)a * 16, (size_t)(b - a) * 16},
+		                            Range{(size_t)a * 16, (size_t)(b - a) * 16}, Range{(size_t)a * 4, (size_t)(b - a) * 4}};
+	};
+	const int e0 = d.profBegin();
+	if(peers_ && peers_->size() > 1)
+	{
+		peers_->arrive(0);   // every member's subtrees are built (each synchronised its stream)
+		bool ok = true;
+		for(uint32_t s = 0; s < owner.size() && ok; ++s)
+		{
+			if(owner[s] == peer_rank_) continue;
+			GpuRenderer *src = peers_->member(owner[s]);
+			Impl &sd = *src->d_;
+			void *dst_p[4] = {nodes, d.kd_pos[which].p, d.kd_dir[which].p, d.kd_colb[which].p};
+			const void *src_p[4] = {nodesOf(sd).p, sd.kd_pos[which].p, sd.kd_dir[which].p, sd.kd_colb[which].p};
+			const auto rg = ranges(s);
+			for(int k = 0; k < 4 && ok; ++k)
+				ok = hipMemcpyPeerAsync((char *)dst_p[k] + rg[k].off, device_, (const char *)src_p[k] + rg[k].off, src->device_, rg[k].bytes, d.stream) ==
+				     hipSuccess;
+		}
+		ok = ok && hipStreamSynchronize(d.stream) == hipSuccess;
+		if(!ok) log_.error("GPU group: point kd-tree copy between members failed");
+		peers_->arrive(0);   // nobody rebuilds before everyone copied
+		if(!ok) return false;
+	}
+	else
+	{
+		void *bufs[4] = {nodes, d.kd_pos[which].p, d.kd_dir[which].p, d.kd_colb[which].p};
+		NCCLCHECK(ncclGroupStart());
+		for(uint32_t s = 0; s < owner.size(); ++s)
+		{
+			const auto rg = ranges(s);
+			for(int k = 0; k < 4; ++k)
+			{
+				char *p = (char *)bufs[k] + rg[k].off;
+				NCCLCHECK(ncclBroadcast(p, p, rg[k].bytes, ncclChar, owner[s], d.comm, d.stream));
+			}
+		}
+		NCCLCHECK(ncclGroupEnd());
+	}
+	HIPCHECK(yafamd_pkd_parent_planes((uint4 *)nodes, n, d.stream));
+	d.profEnd(KK_PHOTON_TREE, e0);
 	HIPCHECK(hipStreamSynchronize(d.stream));
 	return true;
 }
@@ -1387,6 +1501,7 @@ bool GpuRenderer::buildPhotonMap(RenderParams &rp)
 	S.c_radius2 = pm.caustic_radius * pm.caustic_radius;   // integrator_montecarlo.cc:629
 	S.gather_on = 0;
 	stats_.photon_shoot_seconds = stats_.photon_tree_seconds = 0.0;
+	stats_.pkd_split_level = 0;
 	const auto t0 = std::chrono::steady_clock::now();
 	// integrator_photon_mapping.cc:437 / integrator_montecarlo.cc:604 (threads_photons <= 0 counts as one)
 	const uint32_t T = (uint32_t)std::max(1, pm.threads);

@@ -199,7 +199,8 @@ class GpuRenderer
 		// diffuse, 1 caustic, 2 radiance map
 		bool loadMap(RenderParams &rp, int which, const std::string &file);
 		bool saveMap(RenderParams &rp, int which, const std::string &file);
-		bool buildMapTree(int which, const void *pos, const void *dir, const void *colb, uint32_t n, void *nodes, int &depth);
+		bool buildMapTree(int which, const void *pos, const void *dir, const void *colb, uint32_t n, void *nodes, int &depth, bool group_split = false);
+		bool exchangeTree(int which, uint32_t n, void *nodes, int D, int members);
 		const void *mapView(int which, int field, const void *photon_order) const;
 		void publishRadianceMap(DevScene &S, const PhotonParams &pm, uint32_t nk);
 

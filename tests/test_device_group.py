@@ -259,12 +259,13 @@ SHARDED_PHOTONS = {
 }
 
 
-@pytest.mark.parametrize("members", [2, 3])
+@pytest.mark.parametrize("members", [2, 3, 8])
 @pytest.mark.parametrize("case", list(SHARDED_PHOTONS))
 def test_device_group_sharded_photon_maps_match_oracle(product, oracle_built, case, members):
     """Photon shooting split across the members (contiguous photon-id ranges, the reference threads'
-    split, integrator_photon_mapping.cc:118-127, 437-441), the maps concatenated in member order:
-    the same maps (counts) and film as the oracle's one-thread shooting."""
+    split, integrator_photon_mapping.cc:118-127, 437-441), the maps concatenated in member order and
+    their point kd-trees built distributed (r06): the same maps (counts) and film as the oracle's
+    one-thread shooting."""
     spec = SHARDED_PHOTONS[case]()
     rgba, w, st = product.render_spec(spec, members=members)
     o = oracle_built.OracleScene(spec, threads=8)
@@ -276,3 +277,15 @@ def test_device_group_sharded_photon_maps_match_oracle(product, oracle_built, ca
         assert st["caustic_photons"] == len(o.photon_map("caustic")[0]) > 0
     if spec.render.integrator == "photonmapping":
         assert st["photons"] == len(o.photon_map("diffuse")[0])
+    # the maps' point kd-trees were built distributed: each member its own subtrees below level
+    # ceil(log2 members), exchanged (pkd.hip yafamd_build_pkd_kd_member, render.cc exchangeTree)
+    def split_level(n):
+        d = int(np.ceil(np.log2(members)))
+        for _ in range(d):
+            if n <= 256:
+                return 0
+            n = (n + 1) // 2
+        return d
+    assert st["pkd_split_level"] == max(split_level(st["photons"]), split_level(st["caustic_photons"]))
+    if st["photons"] > 2048:
+        assert st["pkd_split_level"] > 0

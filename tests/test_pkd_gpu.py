@@ -89,3 +89,65 @@ def test_photon_tree_fused_partition_equals_scan_passes(product, monkeypatch):
     scan, d2 = Y.build_photon_tree(pos)
     assert d1 == d2
     assert np.array_equal(fused, scan)
+
+
+def split_level(n, members):
+    """pkd.hip yafamd_pkd_split_level: ceil(log2 members) when every node above that level holds > 256 photons."""
+    d = int(np.ceil(np.log2(members)))
+    for _ in range(d):
+        if n <= 256:
+            return 0
+        n = (n + 1) // 2
+    return d
+
+
+def parent_planes(nodes):
+    """pkd.hip k_parent_planes restated: every interior child gets its parent's plane (.y split, .z axis)."""
+    out = nodes.copy()
+    n_nodes = len(out)
+    inner = np.flatnonzero((out[:, 3] & 3) != 3)
+    for i in inner:
+        for c in (i + 1, int(out[i, 3]) >> 2):
+            if c < n_nodes and (out[c, 3] & 3) != 3:
+                out[c, 1] = out[i, 0]
+                out[c, 2] = out[i, 3] & 3
+    out[0, 1], out[0, 2] = 0, 3
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [300, 3000, 70000])
+@pytest.mark.parametrize("members", [2, 3, 5, 8])
+def test_distributed_photon_tree_equals_whole_build(product, n, members):
+    """The distributed build of device / render groups (pkd.hip yafamd_build_pkd_kd_member): every
+    member's own level-D subtrees (node and kd-order record ranges from yafaray_amd_photonTreeSegments)
+    merged over member 0's top, with the parent planes written afterwards, equal the one-member build
+    node for node and record for record."""
+    pos = positions(n, 300 + n + members)
+    want, want_kd, wdepth, lvl1, _ = Y.build_photon_tree_member(pos, 0, 1)
+    assert lvl1 == 0
+    merged, merged_kd = None, np.zeros_like(want_kd)
+    for r in range(members):
+        nodes, kd, depth, level, _ = Y.build_photon_tree_member(pos, r, members)
+        assert depth == wdepth
+        assert level == split_level(n, members)
+        seg, (s0, s1) = Y.photon_tree_segments(n, level, r, members)
+        if level == 0:
+            merged = nodes.copy()
+            merged_kd = kd.copy()
+            continue
+        assert s1 > s0
+        if merged is None:
+            merged = nodes.copy()
+        for node, a, b in seg[s0:s1]:
+            merged[node:node + 2 * (b - a) - 1] = nodes[node:node + 2 * (b - a) - 1]
+            merged_kd[a:b] = kd[a:b]
+    if split_level(n, members):
+        merged = parent_planes(merged)
+    bad = np.flatnonzero((merged != want).any(axis=1))
+    assert bad.size == 0, f"{bad.size} nodes differ, first {bad[0]}: {merged[bad[0]]} vs {want[bad[0]]}"
+    assert np.array_equal(merged_kd, want_kd)
+    # the whole build's tree is the reference's (test_photon_tree_matches_reference_build, photon-order leaves)
+    ref, _ = ref_tree(pos)
+    inner = (want[:, 3] & 3) != 3
+    assert np.array_equal(interior_core(want)[inner], ref[inner])

@@ -153,18 +153,42 @@ static int refBuild(const std::vector<float4> &pos, std::vector<uint32_t> idx, u
 	return std::max(a, b);
 }
 
-static bool run(uint32_t n, uint32_t seed, bool fused)
+// pkd.hip yafamd_pkd_split_level / yafamd_pkd_top_segments, restated for the member builds
+static int splitLevel(uint32_t n, int members)
 {
-	std::mt19937 rng(seed);
-	std::uniform_real_distribution<float> U(-2.f, 2.f);
-	std::vector<float4> pos(n);
-	for(uint32_t i = 0; i < n; ++i)
+	if(members <= 1) return 0;
+	int D = 0;
+	while((1 << D) < members) ++D;
+	uint32_t m = n;
+	for(int l = 0; l < D; ++l)
 	{
-		pos[i] = {U(rng), U(rng), U(rng), 0.f};
-		if(n > 10 && i % 7 == 0) pos[i].y = 0.5f;
-		if(n > 10 && i % 11 == 0) pos[i].x = -0.f;
-		if(n > 10 && i % 13 == 0) pos[i] = pos[0];
+		if(m <= (uint32_t)kSub) return 0;
+		m = (m + 1) / 2;
 	}
+	return D;
+}
+static std::vector<uint32_t> topSegments(uint32_t n, int level)
+{
+	std::vector<uint32_t> cur{0u, 0u, n}, nxt;
+	for(int l = 0; l < level; ++l)
+	{
+		nxt.clear();
+		for(size_t k = 0; k < cur.size(); k += 3)
+		{
+			const uint32_t node = cur[k], a = cur[k + 1], b = cur[k + 2], mid = (a + b) / 2;
+			nxt.insert(nxt.end(), {node + 1u, a, mid, node + 2u * (mid - a), mid, b});
+		}
+		cur.swap(nxt);
+	}
+	return cur;
+}
+
+// pkd.hip's build driver over the emulated kernels: the whole tree (members 1) or member `member`'s share;
+// returns the number of top levels (-1: a look-back gave up)
+static int build(const std::vector<float4> &pos, uint32_t n, bool fused, int member, int members, std::vector<uint4> &nodes, int &max_level,
+                 uint32_t &max_m_out)
+{
+	max_level = 0;
 	const uint32_t B = 256, G = (n + B - 1) / B;
 	std::vector<uint32_t> kx(n), ky(n), kz(n), iota(n);
 	std::vector<uint4> kxyz(n);
@@ -183,14 +207,31 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 	std::vector<Seg> segs[2] = {std::vector<Seg>(n), std::vector<Seg>(n)};
 	std::vector<Split> splits(n);
 	std::vector<uint32_t> seg_of(n, 0), scan(n + 1), seg_nl(n), seg_left(n);
-	std::vector<uint4> nodes(2 * n - 1, make_uint4(0xdead, 0xdead, 0xdead, 0xdead));
+	nodes.assign(2 * n - 1, make_uint4(0xdead, 0xdead, 0xdead, 0xdead));
 	launch(n_part, 256, [&] { k_bound(pos.data(), n, partial.data()); });
 	launch(1, 256, [&] { k_root(partial.data(), n_part, n, segs[0].data()); });
-	int max_level = 0;
 	uint32_t n_seg = 1, max_m = n;
 	int cur = 0, level = 0;
+	// a member build (pkd.hip yafamd_build_pkd_kd_member): the levels < D whole, then only the owned level-D
+	// segments [s0, s1), whose entries are [lo, hi)
+	const int D = splitLevel(n, members);
+	uint32_t lo = 0, hi = n, s0 = 0;
+	bool narrowed = false;
+	auto narrow = [&] {
+		const uint32_t s1 = (uint32_t)(((uint64_t)(member + 1) << D) / (uint64_t)members);
+		s0 = (uint32_t)(((uint64_t)member << D) / (uint64_t)members);
+		const std::vector<uint32_t> top = topSegments(n, D);
+		lo = top[3 * (size_t)s0 + 1];
+		hi = top[3 * (size_t)(s1 - 1) + 2];
+		std::copy(segs[cur].begin() + s0, segs[cur].begin() + s1, segs[cur ^ 1].begin());
+		cur ^= 1;
+		n_seg = s1 - s0;
+		narrowed = true;
+	};
 	while(max_m > (uint32_t)kSub)
 	{
+		if(D > 0 && level == D) narrow();
+		const uint32_t seg_base = D > 0 && level >= D ? s0 << (level - D) : 0u;
 		launchFlat((n_seg + B - 1) / B, B, [&] {
 			k_level_split(segs[cur].data(), n_seg, n, rec[0].data(), rec[1].data(), rec[2].data(), pos.data(), nodes.data(), splits.data(),
 			              segs[cur ^ 1].data(), seg_nl.data());
@@ -202,7 +243,7 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 			// finds its predecessor's inclusive prefix)
 			uint32_t acc = 0;
 			for(uint32_t k = 0; k < n_seg; ++k) { seg_left[k] = acc; acc += seg_nl[k]; }
-			const uint32_t n_tiles = (n + kPartTile - 1) / kPartTile;
+			const uint32_t n_tiles = (hi - lo + kPartTile - 1) / kPartTile;
 			std::vector<uint64_t> status(3 * n_tiles, 0);
 			uint32_t misc[2] = {0, 0};
 			std::vector<uint4> outs[3] = {std::vector<uint4>(n), std::vector<uint4>(n), std::vector<uint4>(n)};
@@ -214,12 +255,16 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 			P.seg_left = seg_left.data();
 			P.n = n;
 			P.n_tiles = n_tiles;
+			P.lo = lo;
+			P.hi = hi;
+			P.seg_base = seg_base;
+			P.n_seg = n_seg;
 			P.epoch = (uint32_t)level + 1u;
 			P.ticket = &misc[0];
 			P.err = &misc[1];
 			P.status = status.data();
 			launch(3 * n_tiles, kPartThreads, [&] { k_level_partition(P); });
-			if(misc[1]) { std::printf("look-back gave up\n"); return false; }
+			if(misc[1]) { std::printf("look-back gave up\n"); return -1; }
 			for(int a = 0; a < 3; ++a) std::swap(rec[a], outs[a]);
 			n_seg *= 2;
 			max_m = (max_m + 1) / 2;
@@ -241,9 +286,31 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 		cur ^= 1;
 		++level;
 	}
+	if(D > 0 && !narrowed) narrow();
 	launch(n_seg, std::min<uint32_t>((uint32_t)kSubThreads, (std::max<uint32_t>(max_m, 1u) + 63u) & ~63u), [&] {
 		k_subtrees(segs[cur].data(), rec[0].data(), rec[1].data(), rec[2].data(), pos.data(), nodes.data(), n, level, &max_level);
 	});
+	max_m_out = max_m;
+	return level;
+}
+
+static bool run(uint32_t n, uint32_t seed, bool fused)
+{
+	std::mt19937 rng(seed);
+	std::uniform_real_distribution<float> U(-2.f, 2.f);
+	std::vector<float4> pos(n);
+	for(uint32_t i = 0; i < n; ++i)
+	{
+		pos[i] = {U(rng), U(rng), U(rng), 0.f};
+		if(n > 10 && i % 7 == 0) pos[i].y = 0.5f;
+		if(n > 10 && i % 11 == 0) pos[i].x = -0.f;
+		if(n > 10 && i % 13 == 0) pos[i] = pos[0];
+	}
+	std::vector<uint4> nodes;
+	int max_level = 0;
+	uint32_t max_m = 0;
+	const int level = build(pos, n, fused, 0, 1, nodes, max_level, max_m);
+	if(level < 0) return false;
 	std::vector<uint4> want(2 * n - 1);
 	float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
 	for(const float4 &p : pos)
@@ -265,8 +332,36 @@ static bool run(uint32_t n, uint32_t seed, bool fused)
 	int calc = level;
 	for(uint32_t m = max_m; m > 1u; m = (m + 1u) / 2u) ++calc;
 	if(calc != max_level) std::printf("arithmetic depth %d != %d\n", calc, max_level);
-	const bool ok = bad == 0 && g_pkd_err == 0 && depth == max_level && calc == max_level;
+	bool ok = bad == 0 && g_pkd_err == 0 && depth == max_level && calc == max_level;
 	g_pkd_err = 0;
+	// the distributed build: every member's share, its owned level-D subtrees' node ranges merged over member
+	// 0's array (the ancestors every member writes), node for node the whole build
+	for(int members : {2, 3, 5, 8})
+	{
+		if(!fused) break;
+		const int D = splitLevel(n, members);
+		if(D == 0) continue;
+		const std::vector<uint32_t> top = topSegments(n, D);
+		std::vector<uint4> merged;
+		for(int r = 0; r < members && ok; ++r)
+		{
+			std::vector<uint4> part;
+			int ml = 0;
+			uint32_t mm = 0;
+			ok = build(pos, n, true, r, members, part, ml, mm) == level && g_pkd_err == 0;
+			if(r == 0) merged = part;
+			const uint32_t s0 = (uint32_t)(((uint64_t)r << D) / (uint64_t)members), s1 = (uint32_t)(((uint64_t)(r + 1) << D) / (uint64_t)members);
+			for(uint32_t sg = s0; sg < s1; ++sg)
+			{
+				const uint32_t node = top[3 * sg], m = top[3 * sg + 2] - top[3 * sg + 1];
+				std::copy(part.begin() + node, part.begin() + node + 2 * m - 1, merged.begin() + node);
+			}
+		}
+		size_t mb = 0;
+		for(size_t i = 0; i < want.size() && ok; ++i) mb += std::memcmp(&want[i], &merged[i], 16) != 0;
+		std::printf("  members=%d split_level=%d mismatching_nodes=%zu\n", members, D, mb);
+		ok = ok && mb == 0;
+	}
 	return ok;
 }
 
