@@ -95,7 +95,10 @@ def pmc_config(a, W, H):
     """Key of profiles/pmc_<key>.json (tools/pmc_all.sh): one workload, one kernel source."""
     return f"{a.scene}-{W}x{H}x{a.spp}-b{a.bounces}-rr{int(not a.no_rr)}-chunk{a.chunk}" + (
         f"-ph{a.photons}" if a.scene == "photon" else "") + (f"-fg{a.fg}" if a.scene == "photon" and a.fg else "") + (
-        f"-l{a.lights}" if getattr(a, "lights", 1) > 1 else "")
+        f"-l{a.lights}" if getattr(a, "lights", 1) > 1 else "") + (
+        # a member renders a band: its launches are a fraction of the one-GPU launches the PMC file measured
+        f"-g{a.gpus}" if getattr(a, "gpus", 1) > 1 else "") + (
+        f"-m{a.members_per_gpu}" if getattr(a, "members_per_gpu", 1) > 1 else "")
 
 
 def kernels_src_sha1():
@@ -465,6 +468,9 @@ def kernel_table(a, s, kt, pmc):
                 e["traffic_bytes"] = int(p["hbm_bytes_per_launch"] * v["launches"])
             e["traffic_gbs"] = round(e["traffic_bytes"] / (v["ms"] * 1e-3) / 1e9, 1)
             e["traffic_frac"] = round(e["traffic_gbs"] / HBM_PEAK_GBS, 4)
+            if p.get("hbm_bytes_per_launch") and "write_bytes_per_launch" in p:
+                # a write-only stream (k_camera) runs above the guide's 6.29 TB/s, which is a float4 copy
+                e["traffic_write_frac"] = round(p["write_bytes_per_launch"] / p["hbm_bytes_per_launch"], 4)
             if "valu_lane_util" in p:
                 e["valu_lane_util"] = p["valu_lane_util"]
             if "sq_insts_valu_per_launch" in p and v["launches"] and kind in SINGLE_KERNEL_KINDS:

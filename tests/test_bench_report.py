@@ -113,7 +113,10 @@ def _physical(line):
     for k, e in (line.get("kernels") or {}).items():
         if e.get("frac") is not None and e["frac"] > 1.0:
             bad.append((k, "frac", e["frac"]))
-        if e.get("traffic_gbs") is not None and e["traffic_gbs"] > ACHIEVABLE_GBS:
+        # the guide's 6.29 TB/s is a float4 copy (reads + writes); a kernel whose PMC traffic is >= 99 %
+        # writes (k_camera: 32 B per sample streamed out, 6.2-6.4 TB/s) is bounded by the 8 TB/s peak only
+        limit = bench.HBM_PEAK_GBS if (e.get("traffic_write_frac") or 0) >= 0.99 else ACHIEVABLE_GBS
+        if e.get("traffic_gbs") is not None and e["traffic_gbs"] > limit:
             bad.append((k, "traffic_gbs", e["traffic_gbs"]))
     roof = line.get("roofline") or {}
     if roof.get("frac") is not None and roof["frac"] > 1.0:
