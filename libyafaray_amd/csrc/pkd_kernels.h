@@ -281,6 +281,9 @@ __global__ void k_seg_of(uint32_t *seg_of, uint32_t n, const Split *splits)
 #ifndef YAF_SUB_FAST
 #define YAF_SUB_FAST 1
 #endif
+#ifndef YAF_SUB_2BUF
+#define YAF_SUB_2BUF 0
+#endif
 constexpr int kPartItems = YAF_PART_ITEMS;
 constexpr uint32_t kPartThreads = 256;
 constexpr uint32_t kPartTile = kPartThreads * kPartItems;
@@ -325,7 +328,11 @@ __device__ __forceinline__ uint32_t segOfPos(uint32_t e, uint32_t n, uint32_t le
 // kPartTile / kSub + 1 of them
 constexpr uint32_t kPartSegs = kPartTile / (uint32_t)kSub + 2u;
 
+#if defined(YAF_PART_WAVES) && !defined(PKD_EMU)
+__global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(YAF_PART_WAVES))) k_level_partition(PartArgs A)
+#else
 __global__ void __launch_bounds__(kPartThreads) k_level_partition(PartArgs A)
+#endif
 {
 	__shared__ uint32_t s_id, s_first, s_acc, s_seg0;
 	__shared__ uint32_t s_wsum[kPartItems][kPartThreads / 64];
@@ -536,9 +543,21 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
                                                         uint4 *nodes, uint32_t n, int base_level, int *max_level, KdPayload kp = KdPayload{})
 {
 	constexpr uint16_t kNone = 0xffffu;
-	__shared__ uint4 buf[2][3][kSub];
+	// one copy of the three lists: an entry is read into registers (phase 2) before any entry is scattered
+	// (phase 3, after two barriers), and the next level reads after the closing barrier — 40 KB of LDS instead
+	// of 52 KB, four workgroups per CU instead of three (YAF_SUB_2BUF=1: the double buffer)
+#if YAF_SUB_2BUF
+	__shared__ uint4 buf2[2][3][kSub];
+#define PK_BUF(c) buf2[(c)]
+#else
+	__shared__ uint4 buf1[3][kSub];
+#define PK_BUF(c) buf1
+#endif
 	__shared__ uint32_t scan[3][kSub];         // exclusive count of left-going entries before e, per list
-	__shared__ LSeg lsegs[2][kSub];
+	// the level's segments: read by their threads in phase 1 (kept in registers to phase 3) and written as the
+	// next level's in phase 3, so one copy (+ the starts the entries read in phase 3) suffices
+	__shared__ LSeg lsegs[kSub];
+	__shared__ uint32_t lseg_start[kSub];
 	__shared__ Split lsplit[kSub];
 	__shared__ uint32_t cb[kSub];              // first child segment of splitting segment s
 	__shared__ uint16_t seg_of[kSub];          // segment of entry position e (kNone once a leaf)
@@ -555,9 +574,9 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 	const bool act = t < m;
 	if(act)
 	{
-		buf[0][0][t] = gx[g.start + t];
-		buf[0][1][t] = gy[g.start + t];
-		buf[0][2][t] = gz[g.start + t];
+		PK_BUF(0)[0][t] = gx[g.start + t];
+		PK_BUF(0)[1][t] = gy[g.start + t];
+		PK_BUF(0)[2][t] = gz[g.start + t];
 	}
 	seg_of[t] = act ? 0 : kNone;
 	if(t == 0)
@@ -567,18 +586,21 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 		l.start = 0;
 		l.end = m;
 		for(int k = 0; k < 3; ++k) { l.lo[k] = g.lo[k]; l.hi[k] = g.hi[k]; }
-		lsegs[0][0] = l;
+		lsegs[0] = l;
 	}
 	__syncthreads();
-	int cur = 0, cs = 0, level = base_level;
+	int cur = 0, level = base_level;
 	uint32_t ns = 1;
 	for(;;)
 	{
 		// (1) segment t: a leaf (one photon, pkdtree.h:29-33) or a split at the median of its largest axis
 		bool split = false;
+		LSeg myseg;
 		if(t < ns)
 		{
-			const LSeg l = lsegs[cs][t];
+			const LSeg l = lsegs[t];
+			myseg = l;
+			lseg_start[t] = l.start;
 			if(l.end - l.start == 1)
 			{
 #if YAF_SUB_FAST
@@ -586,7 +608,7 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 				// gathers then overlap with every other leaf's instead of stalling the level they finish in
 				leaf_node[l.start] = l.node;
 #else
-				uint32_t idx = buf[cur][0][l.start].w;
+				uint32_t idx = PK_BUF(cur)[0][l.start].w;
 				PK_GUARD(idx < n, idx);
 				const float4 ph = pos[idx];
 				uint32_t nd = l.node;
@@ -609,7 +631,7 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 				const int axis = largestAxis(l.lo, l.hi);
 				uint32_t se = (l.start + l.end) / 2;
 				PK_GUARD(se > l.start && l.end <= m, se);
-				uint4 med = buf[cur][axis][se];
+				uint4 med = PK_BUF(cur)[axis][se];
 				PK_GUARD(med.w < n, med.w);
 #if YAF_SUB_FAST
 				// the split position from the median's key (no dependent load per level; a zero key may be -0)
@@ -659,7 +681,7 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 		bool f[3];
 		for(int a = 0; a < 3; ++a)
 		{
-			r[a] = act ? buf[cur][a][t] : make_uint4(0u, 0u, 0u, 0u);
+			r[a] = act ? PK_BUF(cur)[a][t] : make_uint4(0u, 0u, 0u, 0u);
 			f[a] = part && leftOf(r[a], sp.axis, sp.med_key, sp.med_idx);
 			const uint64_t b = __ballot(f[a]);
 			pre[a] = lanePrefix(b);
@@ -680,23 +702,23 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 			uint16_t nso = kNone;
 			if(part)
 			{
-				const uint32_t start = lsegs[cs][so].start;
+				const uint32_t start = lseg_start[so];
 				for(int a = 0; a < 3; ++a)
 				{
 					const uint32_t left_before = pre[a] - scan[a][start];
 					uint32_t np = f[a] ? start + left_before : sp.split_el + ((t - start) - left_before);
 					PK_GUARD(np < m, np);
-					buf[cur ^ 1][a][np] = r[a];
+					PK_BUF(cur ^ 1)[a][np] = r[a];
 				}
 				nso = (uint16_t)(cb[so] + (t < sp.split_el ? 0u : 1u));
 			}
 			else
-				for(int a = 0; a < 3; ++a) buf[cur ^ 1][a][t] = r[a];
+				for(int a = 0; a < 3; ++a) PK_BUF(cur ^ 1)[a][t] = r[a];
 			seg_of[t] = nso;
 		}
 		if(split)
 		{
-			const LSeg l = lsegs[cs][t];
+			const LSeg l = myseg;
 			const Split ls = lsplit[t];
 #if YAF_SUB_FAST
 			const float split_pos = ls.med_key != kZeroKey ? keyCoord(ls.med_key) : coordOf(pos[ls.med_idx], (int)ls.axis);
@@ -716,12 +738,11 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 				lo.hi[k] = (k == (int)ls.axis) ? split_pos : l.hi[k];
 				hi.lo[k] = (k == (int)ls.axis) ? split_pos : l.lo[k];
 			}
-			lsegs[cs ^ 1][c0] = lo;
-			lsegs[cs ^ 1][c0 + 1] = hi;
+			lsegs[c0] = lo;
+			lsegs[c0 + 1] = hi;
 		}
 		ns = 2u * n_split;
 		cur ^= 1;
-		cs ^= 1;
 		++level;
 		__syncthreads();
 	}
@@ -730,7 +751,7 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 	// position of the lists, which leaves never move
 	if(act)
 	{
-		uint32_t idx = buf[cur][0][t].w;
+		uint32_t idx = PK_BUF(cur)[0][t].w;
 		PK_GUARD(idx < n, idx);
 		const float4 ph = pos[idx];
 		uint32_t nd = leaf_node[t];
@@ -748,5 +769,6 @@ __global__ void __launch_bounds__(kSubThreads) k_subtrees(const Seg *segs, const
 	}
 #endif
 }
+#undef PK_BUF
 
 } // namespace yafamd_pkd
