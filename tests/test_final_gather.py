@@ -240,3 +240,28 @@ def test_final_gather_grid_nearest_equals_kd_search(product, monkeypatch, case):
     assert np.array_equal(w.view(np.uint32), wb.view(np.uint32))
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), int(ulp_diff(a, b).max())
     assert st["fg_lookups"] == st_b["fg_lookups"] > 0
+
+
+@pytest.mark.gpu
+def test_final_gather_lds_scene_near_cap_with_deep_radiance_map(product, oracle_built, monkeypatch):
+    """an LDS-resident scene near the 48 KB cap with a deep radiance map.  k_fg stages its
+    primitive / material tables only while stack + scene + nearest-search column + tables fit 64 KB
+    (fgStageTables, the same decision in the kernel and the launch), so the render runs and matches the
+    oracle — with one lane per gather path and with one lane per request alike."""
+    # a 426-triangle sphere in the box: 37 KB of BVH4 nodes + triangles, 24 stack levels (n = 15 leaves LDS)
+    s = scenes.cornell_sphere(n=14, width=40, height=30, spp=1, integrator="photonmapping")
+    spec = dataclasses.replace(s, render=dataclasses.replace(
+        s.render, pm_photons=3_000_000, pm_search=50, pm_diffuse_radius=0.035, pm_bounces=5, pm_caustics=False,
+        pm_final_gather=True, fg_samples=4))
+    a, w, st = product.render_spec(spec)
+    assert st["scene_in_lds"] == 1
+    assert (8 * st["bvh_nodes"] + 3 * len(spec.tris)) * 16 >= 36 * 1024, st["bvh_nodes"]   # near the 48 KB cap
+    assert st["radiance_photons"] > 1 << 15, st["radiance_photons"]   # kd depth >= 16: a 17-level nearest-search column
+    o = oracle_built.OracleScene(spec, threads=8)
+    orgba, ow, _ = o.render()
+    assert np.array_equal(w.view(np.uint32), ow.view(np.uint32))
+    u = ulp_diff(a, orgba)
+    assert u.max() <= ULP_TOL, f"{(u > ULP_TOL).sum()} values > {ULP_TOL} ULP"
+    monkeypatch.setenv("YAFARAY_AMD_FG", "lane")
+    b, wb, _ = product.render_spec(spec)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
