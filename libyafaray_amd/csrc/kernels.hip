@@ -4251,7 +4251,7 @@ __global__ void __launch_bounds__(kShadeBlock, LEAN ? YAF_NEE_LEAN_WAVES : YAF_N
 // iterations' ranges are processed in order): a light estimate becomes lcol = estimate * n_lights (+ emission),
 // term = lcol * throughput (k_shade's connection, its contributions at (slot - batch) * K of this batch), a known
 // term is taken as it is, and pcol = pcol + term per sample (the additions of the one-pass render, in order)
-__global__ void __launch_bounds__(256) k_dfr_accum(DfrArgs A, float *pcol, uint32_t batch0)
+__global__ void __launch_bounds__(256) k_dfr_accum(DfrArgs A, float4 *pcol, uint32_t batch0)
 {
 	const DevScene &S = A.S;
 	const uint32_t slot = A.r0 + blockIdx.x * blockDim.x + threadIdx.x;
@@ -4271,15 +4271,15 @@ __global__ void __launch_bounds__(256) k_dfr_accum(DfrArgs A, float *pcol, uint3
 		if(kind & 4u) lcol = lcol + rgb(S.dfr_emit[slot]);
 		term = lcol * term;
 	}
+	// the sample's colour as one aligned 16-B record: one load and one store (three 4-B read-modify-writes
+	// of a 12-B record before)
 	const uint32_t q = __float_as_uint(a.w);
-	float *pc = pcol + 3u * (size_t)q;
-	pc[0] = pc[0] + term.r;
-	pc[1] = pc[1] + term.g;
-	pc[2] = pc[2] + term.b;
+	const float4 pc = pcol[q];
+	pcol[q] = make_float4(pc.x + term.r, pc.y + term.g, pc.z + term.b, 0.f);
 }
 
 // per camera sample of the pass: the first-vertex estimate + the paths' colour (k_shade's finalize)
-__global__ void __launch_bounds__(256) k_dfr_fold(DfrArgs A, const float *pcol)
+__global__ void __launch_bounds__(256) k_dfr_fold(DfrArgs A, const float4 *pcol)
 {
 	const DevScene &S = A.S;
 	const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -4288,7 +4288,7 @@ __global__ void __launch_bounds__(256) k_dfr_fold(DfrArgs A, const float *pcol)
 	if(v == 0xffffffffu) return;   // not finalized in this pass
 	const float4 c4 = A.samples[q];
 	C3 col = rgb(c4);
-	if(v & 1u) col = col + C3{pcol[3u * (size_t)q], pcol[3u * (size_t)q + 1u], pcol[3u * (size_t)q + 2u]} / (float)max(1, S.path_samples);
+	if(v & 1u) col = col + rgb(pcol[q]) / (float)max(1, S.path_samples);
 	col = col + c3(0.f);   // recursiveRaytrace: no specular / glossy component (k_shade's finalize)
 	A.samples[q] = f4(col, c4.w);
 }
@@ -7388,7 +7388,7 @@ hipError_t yafamd_dfr_nee(const DevScene *S, const DevPaths *P, const DevQueues 
 	return hipGetLastError();
 }
 
-hipError_t yafamd_dfr_accum(const DevScene *S, const DevPaths *P, uint32_t r0, uint32_t r1, uint32_t batch0, float *pcol, hipStream_t st)
+hipError_t yafamd_dfr_accum(const DevScene *S, const DevPaths *P, uint32_t r0, uint32_t r1, uint32_t batch0, float4 *pcol, hipStream_t st)
 {
 	if(r1 <= r0) return hipSuccess;
 	DfrArgs A{};
@@ -7400,7 +7400,7 @@ hipError_t yafamd_dfr_accum(const DevScene *S, const DevPaths *P, uint32_t r0, u
 	return hipGetLastError();
 }
 
-hipError_t yafamd_dfr_fold(const DevScene *S, float4 *samples, uint32_t n_ctr, const float *pcol, hipStream_t st)
+hipError_t yafamd_dfr_fold(const DevScene *S, float4 *samples, uint32_t n_ctr, const float4 *pcol, hipStream_t st)
 {
 	if(n_ctr == 0) return hipSuccess;
 	DfrArgs A{};

@@ -77,10 +77,10 @@ void yafamd_rad_grid_free(void *scratch);
 int yafamd_dfr_eligible(const DevScene *S);
 hipError_t yafamd_dfr_segoff(const DevCounters *cnt, uint32_t n_seg, uint32_t *seg_off, uint32_t *dfr_total, uint32_t cap, uint32_t *overflow,
                              uint32_t *it_start, hipStream_t st);
-hipError_t yafamd_dfr_accum(const DevScene *S, const DevPaths *P, uint32_t r0, uint32_t r1, uint32_t batch0, float *pcol, hipStream_t st);
+hipError_t yafamd_dfr_accum(const DevScene *S, const DevPaths *P, uint32_t r0, uint32_t r1, uint32_t batch0, float4 *pcol, hipStream_t st);
 hipError_t yafamd_dfr_nee(const DevScene *S, const DevPaths *P, const DevQueues *Q, const DevCounters *cnt, uint32_t r0, uint32_t total, uint32_t *idx,
                          uint32_t *n_rec, hipStream_t st);
-hipError_t yafamd_dfr_fold(const DevScene *S, float4 *samples, uint32_t n_ctr, const float *pcol, hipStream_t st);
+hipError_t yafamd_dfr_fold(const DevScene *S, float4 *samples, uint32_t n_ctr, const float4 *pcol, hipStream_t st);
 hipError_t yafamd_ray_bin(const DevQueues *Q, const DevCounters *cnt, uint32_t n_seg, uint32_t cap_a, const float *lo, const float *hi,
                           uint32_t *keys_in, uint32_t *keys_out, uint32_t *iota, uint32_t *perm, void *tmp, size_t *tmp_bytes, hipStream_t st);
 hipError_t yafamd_launch_fg(const DevScene *S, const DevNeeQueue *G, const DevCounters *cnt_next, int stack_depth, int *spill, int grid, float2 *ts_scratch,
@@ -2297,7 +2297,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 			              ensure(log_, d.dfr_a, cap * 16) && ensure(log_, d.dfr_emit, cap * 16) && ensure(log_, d.dfr_pix, cap * 8) &&
 			              ensure(log_, d.dfr_last, n_ctr * 4) &&
 			              ensure(log_, d.dfr_segoff, (size_t)S.n_seg * 4) && ensure(log_, d.dfr_misc, 16) && ensure(log_, d.dfr_its, 4096 * 4) &&
-			              ensure(log_, d.dfr_pcol, n_ctr * 12) && ensure(log_, d.dfr_idx, (size_t)S.n_seg * S.cap_a * 4) &&
+			              ensure(log_, d.dfr_pcol, n_ctr * 16) && ensure(log_, d.dfr_idx, (size_t)S.n_seg * S.cap_a * 4) &&
 			              ensure(log_, d.dfr_nrec, (size_t)S.n_seg * 4);
 			if(ok_mem)
 			{
@@ -2305,7 +2305,7 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 				HIPCHECK(hipMemsetAsync(d.dfr_last.p, 0xff, n_ctr * 4, d.stream));
 				HIPCHECK(hipMemsetAsync(d.dfr_misc.p, 0, 16, d.stream));
 				HIPCHECK(hipMemsetAsync(d.dfr_its.p, 0, 4, d.stream));
-				HIPCHECK(hipMemsetAsync(d.dfr_pcol.p, 0, n_ctr * 12, d.stream));
+				HIPCHECK(hipMemsetAsync(d.dfr_pcol.p, 0, n_ctr * 16, d.stream));
 				S.lpc = (uint32_t *)d.lpc.p;
 				S.dfr_kind = (uint32_t *)d.dfr_kind.p;
 				S.dfr_pp = (float4 *)d.dfr_pp.p;
@@ -2352,10 +2352,10 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 						for(uint32_t k = 0; k < its[0]; ++k)
 						{
 							const uint32_t a = std::max(its[1 + k], r0), b = std::min((k + 1 < its[0]) ? its[2 + k] : total_slots, r1);
-							if(b > a) PROF(KK_DFR, yafamd_dfr_accum(&S, &d.P[0], a, b, r0, (float *)d.dfr_pcol.p, d.stream));
+							if(b > a) PROF(KK_DFR, yafamd_dfr_accum(&S, &d.P[0], a, b, r0, (float4 *)d.dfr_pcol.p, d.stream));
 						}
 					}
-					PROF(KK_DFR, yafamd_dfr_fold(&S, (float4 *)d.samples.p, (uint32_t)n_ctr, (const float *)d.dfr_pcol.p, d.stream));
+					PROF(KK_DFR, yafamd_dfr_fold(&S, (float4 *)d.samples.p, (uint32_t)n_ctr, (const float4 *)d.dfr_pcol.p, d.stream));
 					return true;
 				}
 				log_.info("Integrator: the deferred light pick's records exceed their budget (" + std::to_string(cap) +
