@@ -254,23 +254,22 @@ class Interface:
 
     # --- render ---
     def render(self, progress=None, put_pixel=None, flush_area=None, flush=None, highlight_area=None):
+        # every callback is (re)registered, a missing one as NULL (an empty CFUNCTYPE instance): the library
+        # keeps the pointers between renders, and the previous render's ctypes thunks are released below
+        # (self._keep) — a render without a callback after one with it called a freed thunk
         cbs = []
-        if highlight_area is not None:
-            cb = FlushAreaCb(lambda v, aid, x0, y0, x1, y1, d: highlight_area(aid, x0, y0, x1, y1))
-            self.L.yafaray_setRenderHighlightAreaCallback(self.h, cb, None)
-            cbs.append(cb)
-        if put_pixel is not None:
-            cb = PutPixelCb(lambda v, l, x, y, r, g, b, a, d: put_pixel(x, y, r, g, b, a))
-            self.L.yafaray_setRenderPutPixelCallback(self.h, cb, None)
-            cbs.append(cb)
-        if flush_area is not None:
-            cb = FlushAreaCb(lambda v, aid, x0, y0, x1, y1, d: flush_area(aid, x0, y0, x1, y1))
-            self.L.yafaray_setRenderFlushAreaCallback(self.h, cb, None)
-            cbs.append(cb)
-        if flush is not None:
-            cb = FlushCb(lambda v, d: flush())
-            self.L.yafaray_setRenderFlushCallback(self.h, cb, None)
-            cbs.append(cb)
+        cb = FlushAreaCb(lambda v, aid, x0, y0, x1, y1, d: highlight_area(aid, x0, y0, x1, y1)) if highlight_area is not None else FlushAreaCb()
+        self.L.yafaray_setRenderHighlightAreaCallback(self.h, cb, None)
+        cbs.append(cb)
+        cb = PutPixelCb(lambda v, l, x, y, r, g, b, a, d: put_pixel(x, y, r, g, b, a)) if put_pixel is not None else PutPixelCb()
+        self.L.yafaray_setRenderPutPixelCallback(self.h, cb, None)
+        cbs.append(cb)
+        cb = FlushAreaCb(lambda v, aid, x0, y0, x1, y1, d: flush_area(aid, x0, y0, x1, y1)) if flush_area is not None else FlushAreaCb()
+        self.L.yafaray_setRenderFlushAreaCallback(self.h, cb, None)
+        cbs.append(cb)
+        cb = FlushCb(lambda v, d: flush()) if flush is not None else FlushCb()
+        self.L.yafaray_setRenderFlushCallback(self.h, cb, None)
+        cbs.append(cb)
         pcb = ProgressCb(lambda t, dn, tag, d: progress(t, dn) if progress else None)
         cbs.append(pcb)
         self._keep = cbs
