@@ -1794,6 +1794,13 @@ bool GpuRenderer::render(RenderParams &rp, volatile bool *canceled)
 	}
 	// ---- chunk buffers ----
 	size_t M = (size_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)rp.chunk_slots, std::max<uint64_t>(total, 1)));
+	// a group member's band moves from frame to frame (rebalanceBands): the chunk buffers hold twice an equal
+	// share, so a band that grows does not re-allocate them (GBs, hipFree + hipMalloc) between timed frames
+	if(rp.shard_world > 1)
+	{
+		const uint64_t share2 = 2 * (((uint64_t)W * H * spp + rp.shard_world - 1) / rp.shard_world);
+		M = std::max<size_t>(M, (size_t)std::min<uint64_t>((uint64_t)rp.chunk_slots, share2));
+	}
 	if(S.tree)
 	{
 		// the recursion tree of a chunk holds up to 2^(raydepth + 1) - 2 spawned nodes per sample
